@@ -1,0 +1,632 @@
+"""Wire codecs: turn one bucket of gradients into a collective payload and back.
+
+Every codec reproduces the reference's *result* — the mean over ranks of each rank's compressed
+dense vector (``CIFAR10/core.py:217-225``) — while changing what travels on the wire (SURVEY.md
+§2.4 "MI355X-native equivalent"):
+
+=================  ==============  ===========================================================
+codec              collective      payload per rank
+=================  ==============  ===========================================================
+DenseCodec         all_reduce      the fp32 bucket itself (method ``none``; DP-3 equivalent)
+TopkCodec          all_gather      (int32 index, fp32 value) pairs, cap_s = m_s + tie slack
+ThresholdCodec     all_gather      pairs, capacity agreed by an all-reduce(MAX) of counts
+RandkCodec         all_reduce      index-free values: shared-seed Philox masks (DP-4 equivalent)
+TernGradCodec      all_gather      one fp32 scale per layer + 2-bit codes
+QSGDCodec          all_gather      one fp32 norm per layer + int8 / 8+1 / int16-bit levels
+DenseWrap(inner)   all_reduce      reference wire format: dense compressed vector (parity mode)
+=================  ==============  ===========================================================
+
+GPU tensors run the HIP kernels (``csrc/compress.hip``); CPU tensors run the torch code below,
+which mirrors the kernels (same Philox streams, same packing, same rank-ordered sums) so the gloo
+tests exercise the same semantics.
+
+Error feedback (``error_feedback=True``) generalises the reference's Random-K-only residual
+(``IMAGENET/training/sparsified_ddp.py:409-413``) to every method: ``g' = g + e`` before
+compression, ``e <- g' - C(g')`` after it, where ``C(g')`` is this rank's decoded contribution.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import reference as ref
+from .plan import GROUP, SMALL_MAX, SegPlan, hdr_words
+from ..ops._ext import ops_for
+from ..utils import philox
+
+SENT = 0x7FFFFFFF
+KM_TOPK, KM_RANDK, KM_THRESH = 0, 1, 2
+OUT_PAIRS, OUT_VALIDX = 0, 1
+Q_TERN, Q_QS8, Q_QS9, Q_QS16 = 0, 1, 2, 3
+
+
+def _ws_tensor(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def tie_slack(m: int) -> int:
+    return max(1, -(-m // 64))
+
+
+class Codec:
+    collective = "all_reduce"
+    name = "codec"
+
+    def __init__(self, plan: SegPlan, world: int, rank: int, seed: int = 0,
+                 error_feedback: bool = False):
+        self.plan = plan
+        self.world = int(world)
+        self.rank = int(rank)
+        self.seed = int(seed) & ((1 << 63) - 1)
+        self.error_feedback = error_feedback
+        self.last_payload_bytes = 0
+
+    def compress(self, grad: torch.Tensor, ef: Optional[torch.Tensor], step: int) -> torch.Tensor:
+        raise NotImplementedError
+
+    def recv_buffer(self, send: torch.Tensor) -> Optional[torch.Tensor]:
+        if self.collective == "all_gather":
+            return torch.empty(send.numel() * self.world, dtype=send.dtype, device=send.device)
+        return None
+
+    def decompress(self, send: torch.Tensor, recv: Optional[torch.Tensor], grad: torch.Tensor,
+                   world: Optional[int] = None) -> None:
+        raise NotImplementedError
+
+    # -- helpers
+    def _segs(self, t: torch.Tensor):
+        for s in range(self.plan.S):
+            o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
+            yield s, t[o:o + n]
+
+
+# ================================================================================= dense
+class DenseCodec(Codec):
+    """No compression: bucketed in-place all-reduce, then ``/ world_size`` (core.py:318-319)."""
+    name = "dense"
+
+    def compress(self, grad, ef, step):
+        self.last_payload_bytes = grad.numel() * grad.element_size()
+        return grad
+
+    def decompress(self, send, recv, grad, world=None):
+        grad.div_(float(world or self.world))
+
+
+# ================================================================================= Top-K
+class TopkCodec(Codec):
+    """Exact reference Top-K selection (``kthvalue`` threshold, ``>=`` keeps ties) → sparse pairs."""
+    collective = "all_gather"
+    name = "topk"
+    km = KM_TOPK
+
+    def __init__(self, plan, world, rank, K: float, seed=0, error_feedback=False):
+        super().__init__(plan, world, rank, seed, error_feedback)
+        self.K = float(K)
+        self.keep = np.asarray([ref.topk_keep_count(int(n), self.K) for n in plan.sizes],
+                               dtype=np.int64)
+        self.cap = self.keep + np.asarray([tie_slack(int(m)) for m in self.keep], dtype=np.int64)
+        self.cap = np.minimum(self.cap, plan.sizes)
+        self.cap_off = np.concatenate([[0], np.cumsum(self.cap)]).astype(np.int64)
+        self.cap_total = int(self.cap_off[-1])
+        self._ws = {}
+        self._send = {}
+
+    def _dev_tables(self, device):
+        t = self.plan.select_tables(device)
+        t["keep"] = self.plan.dev(device, f"keep{self.K}", lambda: torch.from_numpy(
+            self.keep.astype(np.int32)))
+        t["cap_off"] = self.plan.dev(device, f"capoff{self.K}{self.km}", lambda: torch.from_numpy(
+            self.cap_off))
+        return t
+
+    def _workspace(self, device, lib):
+        k = str(device)
+        if k not in self._ws:
+            small, large = self.plan.split(SMALL_MAX)
+            nb = lib.workspace_bytes(len(small), len(large), self.plan.n_tasks(SMALL_MAX))
+            self._ws[k] = _ws_tensor(nb, device)
+        return self._ws[k]
+
+    def send_buffer(self, device):
+        k = str(device)
+        if k not in self._send:
+            self._send[k] = torch.empty(2 * max(self.cap_total, 1), dtype=torch.int32,
+                                        device=device)
+        return self._send[k]
+
+    def compress(self, grad, ef, step):
+        lib = ops_for(grad)
+        out = self.send_buffer(grad.device)
+        self.last_payload_bytes = out.numel() * 4
+        if lib is not None:
+            t = self._dev_tables(grad.device)
+            lib.select_compress(grad, ef, t["seg_off"], t["seg_n"], t["keep"], t["cap_off"],
+                                t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
+                                self._workspace(grad.device, lib), self.km, OUT_PAIRS, out, None,
+                                None, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed)
+            return out
+        self._compress_cpu(grad, ef, step, out)
+        return out
+
+    def _select_cpu(self, s, x, step):
+        """Return (indices selected in index order) with the kernel's exact semantics."""
+        n, m, cap = x.numel(), int(self.keep[s]), int(self.cap[s])
+        if self.km == KM_TOPK:
+            keys = x.abs()
+            t = keys.float().kthvalue(n - m + 1).values if m < n else keys.min()
+            gt = keys > t
+            eq = keys == t
+            quota = 0 if float(t) == 0.0 else min(int(eq.sum()), cap - int(gt.sum()))
+        else:
+            kn = philox.randk_keys(n, self.plan.gid_base + s, int(step) & 0xFFFFFFFF, self.seed)
+            keys = torch.from_numpy(kn.astype(np.int64))
+            t = keys.kthvalue(n - m + 1).values if m < n else keys.min()
+            gt = keys > t
+            eq = keys == t
+            quota = m - int(gt.sum())
+        sel = gt | (eq & (torch.cumsum(eq.to(torch.int64), 0) <= quota))
+        return torch.nonzero(sel, as_tuple=False).flatten()
+
+    def _compress_cpu(self, grad, ef, step, out):
+        pairs = out.view(-1, 2)
+        pairs[:, 0] = SENT
+        pairs[:, 1] = 0
+        for s, x in self._segs(grad):
+            if ef is not None:
+                o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
+                x.add_(ef[o:o + n])
+            idx = self._select_cpu(s, x, step)
+            c0 = int(self.cap_off[s])
+            k = idx.numel()
+            pairs[c0:c0 + k, 0] = idx.to(torch.int32)
+            pairs[c0:c0 + k, 1] = x[idx].float().view(torch.int32)
+            if ef is not None:
+                e = ef[o:o + n]
+                e.copy_(x)
+                e[idx] = 0
+
+    def decompress(self, send, recv, grad, world=None):
+        world = world or self.world
+        gathered = send if recv is None else recv
+        lib = ops_for(grad)
+        if lib is not None:
+            t = self.plan.common(grad.device)
+            t["cap_off"] = self._dev_tables(grad.device)["cap_off"]
+            lib.unpack_pairs(gathered, world, grad, t["seg_off"], t["seg_n"], t["cap_off"],
+                             self.plan.utasks(grad.device))
+            return
+        self.unpack_pairs_cpu(gathered, world, grad, self.cap_off)
+
+    def unpack_pairs_cpu(self, gathered, world, grad, cap_off):
+        cap_total = gathered.numel() // 2 // world
+        P = gathered.view(world, cap_total, 2)
+        for s, x in self._segs(grad):
+            acc = torch.zeros_like(x, dtype=torch.float32)
+            c0, c1 = int(cap_off[s]), int(cap_off[s + 1])
+            for r in range(world):
+                seg = P[r, c0:c1]
+                keep = seg[:, 0] != SENT
+                idx = seg[keep, 0].long()
+                val = seg[keep, 1].view(torch.float32)
+                acc.index_add_(0, idx, val)
+            x.copy_(acc / float(world))
+
+
+class RandkSparseCodec(TopkCodec):
+    """Random-K with explicit indices (masks need not be rank-coherent)."""
+    name = "randk-sparse"
+    km = KM_RANDK
+
+    def __init__(self, plan, world, rank, K, seed=0, error_feedback=False):
+        Codec.__init__(self, plan, world, rank, seed, error_feedback)
+        self.K = float(K)
+        self.keep = np.asarray([ref.randomk_keep_count(int(n), self.K) for n in plan.sizes],
+                               dtype=np.int64)
+        self.keep = np.maximum(self.keep, 1)
+        self.cap = self.keep.copy()
+        self.cap_off = np.concatenate([[0], np.cumsum(self.cap)]).astype(np.int64)
+        self.cap_total = int(self.cap_off[-1])
+        self._ws = {}
+        self._send = {}
+
+
+# ================================================================================= Random-K
+class RandkCodec(RandkSparseCodec):
+    """Index-free Random-K: identical Philox masks on every rank (shared seed), so only the
+    ``k_s = ceil(n_s K)`` selected VALUES are all-reduced — the wire format of the reference's
+    ``RandomKSparsifiedDDP`` (``sparsified_ddp.py:164, 410-412``) without ``randperm``."""
+    collective = "all_reduce"
+    name = "randk"
+
+    def __init__(self, plan, world, rank, K, seed=0, error_feedback=False):
+        super().__init__(plan, world, rank, K, seed, error_feedback)
+        self._idx = {}
+        self._slot_seg = {}
+
+    def send_buffer(self, device):
+        k = str(device)
+        if k not in self._send:
+            self._send[k] = torch.empty(max(self.cap_total, 1), dtype=torch.float32, device=device)
+            self._idx[k] = torch.empty(max(self.cap_total, 1), dtype=torch.int32, device=device)
+        return self._send[k]
+
+    def compress(self, grad, ef, step):
+        lib = ops_for(grad)
+        vals = self.send_buffer(grad.device)
+        idx = self._idx[str(grad.device)]
+        self.last_payload_bytes = vals.numel() * 4
+        if lib is not None:
+            t = self._dev_tables(grad.device)
+            lib.select_compress(grad, ef, t["seg_off"], t["seg_n"], t["keep"], t["cap_off"],
+                                t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
+                                self._workspace(grad.device, lib), KM_RANDK, OUT_VALIDX, None,
+                                vals, idx, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed)
+            return vals
+        for s, x in self._segs(grad):
+            o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
+            xe = x + ef[o:o + n] if ef is not None else x
+            sel = self._select_cpu(s, xe, step)
+            c0 = int(self.cap_off[s])
+            vals[c0:c0 + sel.numel()] = xe[sel]
+            idx[c0:c0 + sel.numel()] = sel.to(torch.int32)
+            if ef is not None:
+                e = ef[o:o + n]
+                e.copy_(xe)
+                e[sel] = 0
+        return vals
+
+    def decompress(self, send, recv, grad, world=None):
+        world = world or self.world
+        lib = ops_for(grad)
+        idx = self._idx[str(grad.device)]
+        grad.zero_()
+        if lib is not None:
+            slot_seg = self.plan.dev(grad.device, f"slotseg{self.K}", lambda: torch.from_numpy(
+                np.repeat(np.arange(self.plan.S, dtype=np.int32), self.cap)))
+            lib.unpack_validx(send, idx, slot_seg, world, grad, self.plan.common(grad.device)
+                              ["seg_off"])
+            return
+        for s, x in self._segs(grad):
+            c0, c1 = int(self.cap_off[s]), int(self.cap_off[s + 1])
+            x[idx[c0:c1].long()] = send[c0:c1] / float(world)
+
+
+# ================================================================================= thresholds
+class ThresholdCodec(TopkCodec):
+    """``Thresholdv`` (|g| >= V) and ``AdaptiveThreshold`` (|2g| >= max|g|): variable counts,
+    so ranks first agree on per-layer capacities with an all-reduce(MAX) of the counts."""
+    name = "threshold"
+    km = KM_THRESH
+
+    def __init__(self, plan, world, rank, V=None, adaptive=False, seed=0, error_feedback=False,
+                 count_exchange=None):
+        Codec.__init__(self, plan, world, rank, seed, error_feedback)
+        self.V = float(V or 0.0)
+        self.adaptive = bool(adaptive)
+        self.count_exchange = count_exchange   # callable(int tensor) -> int tensor (MAX over ranks)
+        self._ws = {}
+        self._send = {}
+        self.cap_off = None
+
+    def compress(self, grad, ef, step):
+        lib = ops_for(grad)
+        dev = grad.device
+        if lib is not None:
+            t = self.plan.all_large_tables(dev)
+            k = str(dev)
+            if k not in self._ws:
+                nb = lib.workspace_bytes(0, self.plan.S, int(t["tasks"].shape[0]))
+                self._ws[k] = _ws_tensor(nb, dev)
+            counts = torch.empty(self.plan.S, dtype=torch.int32, device=dev)
+            lib.thresh_count(grad, ef, t["seg_off"], t["seg_n"], t["segs"], t["tasks"],
+                             t["task_lo"], self._ws[k], self.V, int(self.adaptive), counts)
+        else:
+            counts = torch.empty(self.plan.S, dtype=torch.int32)
+            self._sel = []
+            for s, x in self._segs(grad):
+                if ef is not None:
+                    o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
+                    x.add_(ef[o:o + n])
+                a = x.abs()
+                if self.adaptive:
+                    keep = (x * 2).abs() >= a.max() if x.numel() else a > 0
+                else:
+                    keep = a >= self.V
+                keep &= x != 0
+                idx = torch.nonzero(keep, as_tuple=False).flatten()
+                self._sel.append(idx)
+                counts[s] = idx.numel()
+        caps = counts.to(torch.int64)
+        if self.count_exchange is not None and self.world > 1:
+            caps = self.count_exchange(caps)
+        caps_h = caps.cpu().numpy().astype(np.int64)
+        self.cap_off = np.concatenate([[0], np.cumsum(caps_h)]).astype(np.int64)
+        cap_total = int(self.cap_off[-1])
+        out = torch.empty(2 * max(cap_total, 1), dtype=torch.int32, device=dev)
+        self.last_payload_bytes = out.numel() * 4
+        if lib is not None:
+            t = self.plan.all_large_tables(dev)
+            self._cap_off_dev = torch.from_numpy(self.cap_off).to(dev)
+            lib.thresh_write(grad, ef, t["seg_off"], t["seg_n"], self._cap_off_dev, t["segs"],
+                             t["tasks"], t["task_lo"], self._ws[str(dev)], out)
+            return out
+        pairs = out.view(-1, 2)
+        pairs[:, 0] = SENT
+        pairs[:, 1] = 0
+        for s, x in self._segs(grad):
+            idx = self._sel[s]
+            c0 = int(self.cap_off[s])
+            pairs[c0:c0 + idx.numel(), 0] = idx.to(torch.int32)
+            pairs[c0:c0 + idx.numel(), 1] = x[idx].float().view(torch.int32)
+            if ef is not None:
+                o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
+                e = ef[o:o + n]
+                e.copy_(x)
+                e[idx] = 0
+        return out
+
+    def decompress(self, send, recv, grad, world=None):
+        world = world or self.world
+        gathered = send if recv is None else recv
+        lib = ops_for(grad)
+        if lib is not None:
+            t = self.plan.common(grad.device)
+            lib.unpack_pairs(gathered, world, grad, t["seg_off"], t["seg_n"], self._cap_off_dev,
+                             self.plan.utasks(grad.device))
+            return
+        self.unpack_pairs_cpu(gathered, world, grad, self.cap_off)
+
+
+# ================================================================================= quantisers
+class _QuantCodec(Codec):
+    collective = "all_gather"
+    q = Q_TERN
+    tag = philox.TAG_TERNGRAD
+    qstates = 1
+
+    def __init__(self, plan, world, rank, seed=0, error_feedback=False):
+        super().__init__(plan, world, rank, seed, error_feedback)
+        self.G = plan.groups()
+        self.rec_off = plan.rec_off()
+        self.Gtot = int(self.rec_off[-1])
+        R = {Q_TERN: 2, Q_QS8: 8, Q_QS9: 9, Q_QS16: 16}[self.q]
+        self.hdr = hdr_words(plan.S)
+        self.words = (self.hdr + self.Gtot * R + 3) // 4 * 4
+        self._ws = {}
+        self._send = {}
+
+    def send_buffer(self, device):
+        k = str(device)
+        if k not in self._send:
+            self._send[k] = torch.zeros(self.words, dtype=torch.int32, device=device)
+        return self._send[k]
+
+    def compress(self, grad, ef, step):
+        lib = ops_for(grad)
+        out = self.send_buffer(grad.device)
+        self.last_payload_bytes = out.numel() * 4
+        tag = self.tag | (self.rank & 0xFFFFFF)
+        if lib is not None:
+            t = self.plan.all_large_tables(grad.device)
+            k = str(grad.device)
+            if k not in self._ws:
+                nb = lib.workspace_bytes(0, self.plan.S, int(t["tasks"].shape[0]))
+                self._ws[k] = _ws_tensor(nb, grad.device)
+            lib.quantize(grad, ef, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], t["task_lo"],
+                         t["rec_off"], self._ws[k], out, self.q, self.qstates, self.plan.gid_base,
+                         int(step) & 0xFFFFFFFF, tag, self.seed)
+            return out
+        self._quant_cpu(grad, ef, step, out, tag)
+        return out
+
+    # ---- CPU mirror of k_partial/k_finalize/k_quant
+    def _scale(self, x: torch.Tensor) -> float:
+        raise NotImplementedError
+
+    def _levels(self, x, sc, u):
+        raise NotImplementedError
+
+    def _quant_cpu(self, grad, ef, step, out, tag):
+        words = out.numpy().view(np.uint32)
+        hdr = words[:self.hdr]
+        rec = words[self.hdr:]
+        for s, x in self._segs(grad):
+            o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
+            if ef is not None:
+                x.add_(ef[o:o + n])
+            sc = self._scale(x)
+            hdr[s] = np.float32(sc).view(np.uint32)
+            G = int(self.G[s])
+            xv = np.zeros(G * GROUP, dtype=np.float32)
+            xv[:n] = x.detach().float().numpy()
+            u = philox.uniforms(G * GROUP, self.plan.gid_base + s, int(step) & 0xFFFFFFFF, tag,
+                                self.seed)
+            lv, dq = self._levels(xv, np.float32(sc), u)
+            self._pack(rec, int(self.rec_off[s]), G, lv)
+            if ef is not None:
+                ef[o:o + n].copy_(torch.from_numpy(xv[:n] - dq[:n]))
+
+    def _pack(self, rec, r0, G, lv):
+        raise NotImplementedError
+
+    def _unpack(self, rec, r0, G):
+        raise NotImplementedError
+
+    def decompress(self, send, recv, grad, world=None):
+        world = world or self.world
+        gathered = send if recv is None else recv
+        lib = ops_for(grad)
+        if lib is not None:
+            t = self.plan.all_large_tables(grad.device)
+            lib.dequantize(gathered, world, grad, t["seg_off"], t["seg_n"], t["segs"], t["tasks"],
+                           t["task_lo"], t["rec_off"], self.q, self.qstates)
+            return
+        W = gathered.numpy().view(np.uint32).reshape(world, -1)
+        for s, x in self._segs(grad):
+            n = x.numel()
+            G = int(self.G[s])
+            acc = np.zeros(G * GROUP, dtype=np.float32)
+            for r in range(world):
+                sc = W[r, s].view(np.float32)
+                lv = self._unpack(W[r, self.hdr:], int(self.rec_off[s]), G)
+                acc += self._deq(lv, np.float32(sc))
+            x.copy_(torch.from_numpy(acc[:n] / np.float32(world)))
+
+
+class TernGradCodec(_QuantCodec):
+    """TernGrad (core.py:200-206): s = max|g|, b ~ Bernoulli(|g|/s), out = sign(g)·s·b."""
+    name = "terngrad"
+    q = Q_TERN
+    tag = philox.TAG_TERNGRAD
+
+    def _scale(self, x):
+        return float(x.abs().max()) if x.numel() else 0.0
+
+    def _levels(self, xv, sc, u):
+        if sc > 0:
+            prob = np.abs(xv) / sc
+            b = u < prob
+        else:
+            b = np.zeros_like(xv, dtype=bool)
+        code = np.where(b & (xv > 0), 1, np.where(b & (xv < 0), 2, 0)).astype(np.uint32)
+        dq = np.where(code == 1, sc, np.where(code == 2, -sc, np.float32(0))).astype(np.float32)
+        return code, dq
+
+    def _deq(self, code, sc):
+        return np.where(code == 1, sc, np.where(code == 2, -sc, np.float32(0))).astype(np.float32)
+
+    def _pack(self, rec, r0, G, code):
+        c = code.reshape(G, 2, 16).astype(np.uint32)
+        sh = (2 * np.arange(16, dtype=np.uint32))[None, None, :]
+        w = np.bitwise_or.reduce(c << sh, axis=2)
+        rec[r0 * 2:(r0 + G) * 2] = w.reshape(-1)
+
+    def _unpack(self, rec, r0, G):
+        w = rec[r0 * 2:(r0 + G) * 2].reshape(G, 2, 1)
+        sh = (2 * np.arange(16, dtype=np.uint32))[None, None, :]
+        return ((w >> sh) & np.uint32(3)).reshape(-1)
+
+
+class QSGDCodec(_QuantCodec):
+    """Random dithering / QSGD (core.py:207-213) with ``qstates`` levels:
+    l = floor(|g|/‖g‖·s + u), out = sign(g)·‖g‖·l/s. Packing: s<=127 → int8, s<=255 → uint8 level
+    + sign bit (9 bits/elem), else int16."""
+    name = "qsgd"
+    tag = philox.TAG_QSGD
+
+    def __init__(self, plan, world, rank, qstates=255, seed=0, error_feedback=False):
+        self.qstates = int(qstates)
+        if self.qstates < 1 or self.qstates > 32767:
+            raise ValueError("qstates must be in [1, 32767]")
+        self.q = Q_QS8 if self.qstates <= 127 else (Q_QS9 if self.qstates <= 255 else Q_QS16)
+        super().__init__(plan, world, rank, seed, error_feedback)
+
+    def _scale(self, x):
+        return float(torch.norm(x.float())) if x.numel() else 0.0
+
+    def _levels(self, xv, sc, u):
+        qs = np.float32(self.qstates)
+        if sc > 0:
+            lvl = np.floor(np.abs(xv) / sc * qs + u).astype(np.int64)
+            lvl = np.minimum(lvl, self.qstates)
+        else:
+            lvl = np.zeros(xv.shape, dtype=np.int64)
+        sg = np.sign(xv).astype(np.float32)
+        dq = (sg * sc * (lvl.astype(np.float32) / qs)).astype(np.float32)
+        signed = np.where(xv < 0, -lvl, lvl)
+        return signed, dq
+
+    def _deq(self, signed, sc):
+        qs = np.float32(self.qstates)
+        mag = np.abs(signed).astype(np.float32)
+        return (np.sign(signed).astype(np.float32) * sc * (mag / qs)).astype(np.float32)
+
+    def _pack(self, rec, r0, G, lv):
+        if self.q == Q_QS8:
+            b = (lv.astype(np.int64) & 0xFF).astype(np.uint8)
+            rec[r0 * 8:(r0 + G) * 8] = b.view(np.uint32)
+        elif self.q == Q_QS9:
+            mag = np.abs(lv).astype(np.uint8)
+            rec[r0 * 8:(r0 + G) * 8] = mag.view(np.uint32)
+            sb = (lv < 0).reshape(G, 32).astype(np.uint32)
+            rec[self.Gtot * 8 + r0:self.Gtot * 8 + r0 + G] = np.bitwise_or.reduce(
+                sb << np.arange(32, dtype=np.uint32)[None, :], axis=1)
+        else:
+            h = (lv.astype(np.int64) & 0xFFFF).astype(np.uint16)
+            rec[r0 * 16:(r0 + G) * 16] = h.view(np.uint32)
+
+    def _unpack(self, rec, r0, G):
+        if self.q == Q_QS8:
+            return rec[r0 * 8:(r0 + G) * 8].copy().view(np.int8).astype(np.int64)
+        if self.q == Q_QS9:
+            mag = rec[r0 * 8:(r0 + G) * 8].copy().view(np.uint8).astype(np.int64)
+            sw = rec[self.Gtot * 8 + r0:self.Gtot * 8 + r0 + G]
+            neg = ((sw[:, None] >> np.arange(32, dtype=np.uint32)[None, :]) & 1).reshape(-1)
+            return np.where(neg == 1, -mag, mag)
+        return rec[r0 * 16:(r0 + G) * 16].copy().view(np.int16).astype(np.int64)
+
+
+# ================================================================================= parity mode
+class DenseWrap(Codec):
+    """Reference wire format: every rank all-reduces its *dense* compressed vector
+    (``core.py:217-225``). Implemented as the inner codec's compress → local decode (world=1) →
+    all-reduce → ``/ world_size``."""
+    collective = "all_reduce"
+
+    def __init__(self, inner: Codec):
+        super().__init__(inner.plan, inner.world, inner.rank, inner.seed, inner.error_feedback)
+        self.inner = inner
+        self.name = f"dense({inner.name})"
+
+    def compress(self, grad, ef, step):
+        payload = self.inner.compress(grad, ef, step)
+        if isinstance(self.inner, DenseCodec):
+            return grad
+        self.inner.decompress(payload, None, grad, world=1)
+        self.last_payload_bytes = grad.numel() * grad.element_size()
+        return grad
+
+    def decompress(self, send, recv, grad, world=None):
+        grad.div_(float(world or self.world))
+
+
+# ================================================================================= factory
+def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qstates=None,
+               seed: int = 0, error_feedback: bool = False, wire: str = "auto",
+               count_exchange=None) -> Codec:
+    """Build the codec for ``method`` honouring the reference's falsy-parameter guards
+    (``core.py:178-215``: ``Topk`` without K, ``Thresholdv`` without V... mean no compression)."""
+    method = ref.canonical_method(method)
+    if method == "Topk" and K:
+        if K >= 1.0:
+            c = DenseCodec(plan, world, rank, seed)
+        else:
+            c = TopkCodec(plan, world, rank, K, seed, error_feedback)
+    elif method == "Randomk" and K:
+        if wire in ("sparse",):
+            c = RandkSparseCodec(plan, world, rank, K, seed, error_feedback)
+        else:
+            c = RandkCodec(plan, world, rank, K, seed, error_feedback)
+    elif method == "Thresholdv" and V:
+        c = ThresholdCodec(plan, world, rank, V=V, seed=seed, error_feedback=error_feedback,
+                           count_exchange=count_exchange)
+    elif method == "AdaptiveThreshold":
+        c = ThresholdCodec(plan, world, rank, adaptive=True, seed=seed,
+                           error_feedback=error_feedback, count_exchange=count_exchange)
+    elif method == "TernGrad":
+        c = TernGradCodec(plan, world, rank, seed, error_feedback)
+    elif method == "RandomDithering" and qstates:
+        c = QSGDCodec(plan, world, rank, qstates, seed, error_feedback)
+    else:
+        c = DenseCodec(plan, world, rank, seed)
+    if wire == "dense" and not isinstance(c, DenseCodec):
+        return DenseWrap(c)
+    if wire == "auto" and isinstance(c, TopkCodec) and not isinstance(c, ThresholdCodec):
+        # pairs cost 8 B per kept element on every rank: dense all-reduce wins above ~1/world
+        if c.cap_total * max(world, 2) > plan.numel:
+            return DenseWrap(c)
+    return c

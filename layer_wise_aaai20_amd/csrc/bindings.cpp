@@ -1,0 +1,338 @@
+// torch op bindings for the layer_wise_aaai20_amd HIP kernels (namespace torch.ops.lwaaai).
+//
+// Registered through the dispatcher for the CUDA key (= HIP on ROCm builds of PyTorch); there is
+// deliberately NO CPU kernel here: CPU tensors use the pure-torch implementation in
+// layer_wise_aaai20_amd/ops, and a GPU tensor reaching an op without this library loaded fails
+// loudly in ops/_ext.py.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <torch/library.h>
+
+#include "lw_kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+template <typename T>
+inline T* ptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+template <typename T>
+inline T* optr(const c10::optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_dtype(const Tensor& t, at::ScalarType st, const char* name) {
+  TORCH_CHECK(t.scalar_type() == st, name, " has dtype ", t.scalar_type(), ", expected ", st);
+}
+void check_aligned16(const void* p, const char* name) {
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(p) & 15u) == 0, name, " must be 16-byte aligned");
+}
+
+// Scratch layout shared by all selection ops (one workspace tensor per bucket plan, reused).
+struct Carve {
+  int64_t off = 0;
+  template <typename T>
+  int64_t take(int64_t n) {
+    const int64_t o = off;
+    off += ((int64_t)sizeof(T) * std::max<int64_t>(n, 1) + 255) / 256 * 256;
+    return o;
+  }
+};
+struct WsLayout {
+  int64_t hist, st_small, st_large, cnt, pre, partial, segmax, total;
+};
+WsLayout layout(int64_t n_small, int64_t n_large, int64_t n_tasks) {
+  Carve c;
+  WsLayout w;
+  w.hist = c.take<uint32_t>(n_large * 4096);
+  w.st_small = c.take<lw::SelState>(n_small);
+  w.st_large = c.take<lw::SelState>(n_large);
+  w.cnt = c.take<uint2>(n_tasks);
+  w.pre = c.take<uint2>(n_tasks);
+  w.partial = c.take<float2>(n_tasks);
+  w.segmax = c.take<float>(n_large);
+  w.total = c.off;
+  return w;
+}
+
+int64_t workspace_bytes(int64_t n_small, int64_t n_large, int64_t n_tasks) {
+  return layout(n_small, n_large, n_tasks).total;
+}
+
+lw::SelectArgs make_select_args(const Tensor& g, const c10::optional<Tensor>& ef,
+                                const Tensor& seg_off, const Tensor& seg_n, const Tensor& keep,
+                                const Tensor& cap_off, const Tensor& small_segs,
+                                const Tensor& large_segs, const Tensor& tasks,
+                                const Tensor& task_lo, const Tensor& ws) {
+  check_cuda(g, "g");
+  check_dtype(g, at::kFloat, "g");
+  check_aligned16(g.data_ptr(), "g");
+  check_dtype(seg_off, at::kLong, "seg_off");
+  check_dtype(cap_off, at::kLong, "cap_off");
+  check_dtype(seg_n, at::kInt, "seg_n");
+  check_dtype(keep, at::kInt, "keep");
+  check_dtype(tasks, at::kInt, "tasks");
+  if (ef.has_value() && ef->defined()) {
+    check_cuda(*ef, "ef");
+    check_dtype(*ef, at::kFloat, "ef");
+    TORCH_CHECK(ef->numel() >= g.numel(), "ef smaller than g");
+    check_aligned16(ef->data_ptr(), "ef");
+  }
+  lw::SelectArgs a{};
+  a.g = ptr<float>(g);
+  a.ef = optr<float>(ef);
+  a.seg_off = ptr<int64_t>(seg_off);
+  a.seg_n = ptr<int32_t>(seg_n);
+  a.keep = ptr<int32_t>(keep);
+  a.cap_off = ptr<int64_t>(cap_off);
+  a.small_segs = ptr<int32_t>(small_segs);
+  a.large_segs = ptr<int32_t>(large_segs);
+  a.tasks = ptr<int2>(tasks);
+  a.task_lo = ptr<int32_t>(task_lo);
+  a.n_small = (int)small_segs.numel();
+  a.n_large = (int)large_segs.numel();
+  a.n_tasks = (int)(tasks.numel() / 2);
+  const WsLayout L = layout(a.n_small, a.n_large, a.n_tasks);
+  TORCH_CHECK(ws.numel() >= L.total, "workspace too small: ", ws.numel(), " < ", L.total);
+  uint8_t* base = ptr<uint8_t>(ws);
+  a.hist = reinterpret_cast<uint32_t*>(base + L.hist);
+  a.st_small = reinterpret_cast<lw::SelState*>(base + L.st_small);
+  a.st_large = reinterpret_cast<lw::SelState*>(base + L.st_large);
+  a.cnt = reinterpret_cast<uint2*>(base + L.cnt);
+  a.pre = reinterpret_cast<uint2*>(base + L.pre);
+  return a;
+}
+
+void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
+                     Tensor keep, Tensor cap_off, Tensor small_segs, Tensor large_segs,
+                     Tensor tasks, Tensor task_lo, Tensor ws, int64_t km, int64_t out,
+                     c10::optional<Tensor> pairs, c10::optional<Tensor> vals,
+                     c10::optional<Tensor> idx, int64_t gid_base, int64_t step, int64_t seed) {
+  const c10::hip::HIPGuard guard(g.device());
+  lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, keep, cap_off, small_segs, large_segs,
+                                      tasks, task_lo, ws);
+  a.pairs = optr<int2>(pairs);
+  a.vals = optr<float>(vals);
+  a.idx_out = optr<int32_t>(idx);
+  TORCH_CHECK(out == lw::OUT_PAIRS ? a.pairs != nullptr : (a.vals && a.idx_out),
+              "missing output buffers");
+  a.gid_base = (uint32_t)gid_base;
+  a.step = (uint32_t)step;
+  a.seed0 = (uint32_t)(seed & 0xffffffff);
+  a.seed1 = (uint32_t)((uint64_t)seed >> 32);
+  lw::select_compress(a, (int)km, (int)out, a.ef != nullptr, cur_stream());
+}
+
+void thresh_count(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
+                  Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor ws, double V,
+                  int64_t adaptive, Tensor counts_out) {
+  const c10::hip::HIPGuard guard(g.device());
+  Tensor empty_i = at::empty({0}, seg_n.options());
+  Tensor empty_l = at::empty({1}, seg_off.options());
+  lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, seg_n, empty_l.expand({2}).contiguous(),
+                                      empty_i, large_segs, tasks, task_lo, ws);
+  check_dtype(counts_out, at::kInt, "counts_out");
+  const WsLayout L = layout(a.n_small, a.n_large, a.n_tasks);
+  uint8_t* base = ptr<uint8_t>(ws);
+  lw::thresh_count(a, (float)V, (int)adaptive, a.ef != nullptr,
+                   reinterpret_cast<float*>(base + L.segmax),
+                   reinterpret_cast<float2*>(base + L.partial), ptr<int32_t>(counts_out),
+                   cur_stream());
+}
+
+void thresh_write(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
+                  Tensor cap_off, Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor ws,
+                  Tensor pairs) {
+  const c10::hip::HIPGuard guard(g.device());
+  Tensor empty_i = at::empty({0}, seg_n.options());
+  lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, seg_n, cap_off, empty_i, large_segs,
+                                      tasks, task_lo, ws);
+  check_cuda(pairs, "pairs");
+  a.pairs = ptr<int2>(pairs);
+  lw::thresh_write(a, a.ef != nullptr, cur_stream());
+}
+
+void unpack_pairs(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor seg_n,
+                  Tensor cap_off, Tensor utasks) {
+  const c10::hip::HIPGuard guard(g.device());
+  check_cuda(gathered, "gathered");
+  check_cuda(g, "g");
+  check_aligned16(g.data_ptr(), "g");
+  TORCH_CHECK(world >= 1 && world <= lw::kMaxWorld, "world size out of range");
+  const int64_t cap_total = gathered.numel() / 2 / world;
+  lw::unpack_pairs(ptr<int2>(gathered), cap_total, (int)world, ptr<float>(g), ptr<int64_t>(seg_off),
+                   ptr<int32_t>(seg_n), ptr<int64_t>(cap_off), ptr<int2>(utasks),
+                   (int)(utasks.numel() / 2), cur_stream());
+}
+
+void unpack_validx(Tensor vals, Tensor idx, Tensor slot_seg, int64_t world, Tensor g,
+                   Tensor seg_off) {
+  const c10::hip::HIPGuard guard(g.device());
+  check_cuda(vals, "vals");
+  check_cuda(g, "g");
+  lw::unpack_validx(ptr<float>(vals), ptr<int32_t>(idx), ptr<int32_t>(slot_seg), vals.numel(),
+                    (int)world, ptr<float>(g), ptr<int64_t>(seg_off), cur_stream());
+}
+
+lw::QuantArgs make_quant_args(const Tensor& g, const c10::optional<Tensor>& ef,
+                              const Tensor& seg_off, const Tensor& seg_n, const Tensor& segs,
+                              const Tensor& tasks, const Tensor& task_lo, const Tensor& rec_off,
+                              int64_t qstates) {
+  check_cuda(g, "g");
+  check_dtype(g, at::kFloat, "g");
+  check_aligned16(g.data_ptr(), "g");
+  lw::QuantArgs a{};
+  a.g = ptr<float>(g);
+  a.ef = optr<float>(ef);
+  a.seg_off = ptr<int64_t>(seg_off);
+  a.seg_n = ptr<int32_t>(seg_n);
+  a.segs = ptr<int32_t>(segs);
+  a.tasks = ptr<int2>(tasks);
+  a.task_lo = ptr<int32_t>(task_lo);
+  a.rec_off = ptr<int64_t>(rec_off);
+  a.nseg = (int)segs.numel();
+  a.n_tasks = (int)(tasks.numel() / 2);
+  a.qstates = (int)qstates;
+  return a;
+}
+
+void quantize(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, Tensor segs,
+              Tensor tasks, Tensor task_lo, Tensor rec_off, Tensor ws, Tensor payload, int64_t q,
+              int64_t qstates, int64_t gid_base, int64_t step, int64_t tag, int64_t seed) {
+  const c10::hip::HIPGuard guard(g.device());
+  lw::QuantArgs a = make_quant_args(g, ef, seg_off, seg_n, segs, tasks, task_lo, rec_off, qstates);
+  check_cuda(payload, "payload");
+  check_aligned16(payload.data_ptr(), "payload");
+  const WsLayout L = layout(0, a.nseg, a.n_tasks);
+  TORCH_CHECK(ws.numel() >= L.total, "workspace too small");
+  uint8_t* base = ptr<uint8_t>(ws);
+  a.scale = reinterpret_cast<float*>(base + L.segmax);
+  a.payload = ptr<uint32_t>(payload);
+  a.gid_base = (uint32_t)gid_base;
+  a.step = (uint32_t)step;
+  a.tag = (uint32_t)tag;
+  a.seed0 = (uint32_t)(seed & 0xffffffff);
+  a.seed1 = (uint32_t)((uint64_t)seed >> 32);
+  lw::seg_reduce(a, a.ef != nullptr, q == lw::Q_TERN ? 0 : 1, a.scale,
+                 reinterpret_cast<float2*>(base + L.partial), cur_stream());
+  // after seg_reduce the EF add is already folded into g (g' = g + e)
+  lw::quantize(a, (int)q, a.ef != nullptr, cur_stream());
+}
+
+void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor seg_n,
+                Tensor segs, Tensor tasks, Tensor task_lo, Tensor rec_off, int64_t q,
+                int64_t qstates) {
+  const c10::hip::HIPGuard guard(g.device());
+  lw::QuantArgs a = make_quant_args(g, c10::nullopt, seg_off, seg_n, segs, tasks, task_lo, rec_off,
+                                    qstates);
+  check_cuda(gathered, "gathered");
+  check_aligned16(gathered.data_ptr(), "gathered");
+  const int64_t wpr = gathered.numel() / world;
+  TORCH_CHECK(wpr % 4 == 0, "payload words per rank must be a multiple of 4");
+  lw::dequantize(a, (int)q, ptr<uint32_t>(gathered), wpr, (int)world, cur_stream());
+}
+
+void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tensor segs,
+              Tensor tasks, Tensor seg_wd, double lr, double momentum, double dampening,
+              int64_t nesterov, int64_t first_step, double grad_scale) {
+  const c10::hip::HIPGuard guard(p.device());
+  check_cuda(p, "p");
+  check_cuda(g, "g");
+  check_aligned16(p.data_ptr(), "p");
+  check_aligned16(g.data_ptr(), "g");
+  lw::SgdArgs a{};
+  a.p = ptr<float>(p);
+  a.g = ptr<float>(g);
+  a.buf = buf.numel() ? ptr<float>(buf) : nullptr;
+  if (momentum != 0.0) {
+    TORCH_CHECK(buf.numel() >= p.numel(), "momentum buffer too small");
+    check_aligned16(buf.data_ptr(), "buf");
+  }
+  a.seg_off = ptr<int64_t>(seg_off);
+  a.seg_n = ptr<int32_t>(seg_n);
+  a.segs = ptr<int32_t>(segs);
+  a.tasks = ptr<int2>(tasks);
+  a.seg_wd = ptr<float>(seg_wd);
+  a.n_tasks = (int)(tasks.numel() / 2);
+  a.lr = (float)lr;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.grad_scale = (float)grad_scale;
+  a.nesterov = (int)nesterov;
+  a.first_step = (int)first_step;
+  lw::sgd_step(a, cur_stream());
+}
+
+void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<double> stdv) {
+  const c10::hip::HIPGuard guard(in.device());
+  check_cuda(in, "in");
+  check_dtype(in, at::kByte, "in");
+  TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "mean/std need 3 channels");
+  TORCH_CHECK(out.numel() == in.numel(), "out/in size mismatch");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat,
+              "out must be bf16 or fp32");
+  // `out` is an NCHW tensor in channels_last memory == the NHWC byte order of `in`
+  TORCH_CHECK(out.dim() == 4 && out.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "out must be a channels_last NCHW tensor");
+  check_aligned16(in.data_ptr(), "in");
+  check_aligned16(out.data_ptr(), "out");
+  const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
+  const float s[3] = {(float)stdv[0], (float)stdv[1], (float)stdv[2]};
+  lw::normalize_u8(ptr<uint8_t>(in), out.data_ptr(), in.numel(), m, s,
+                   out.scalar_type() == at::kBFloat16, cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(lwaaai, m) {
+  m.def("workspace_bytes(int n_small, int n_large, int n_tasks) -> int", &workspace_bytes);
+  m.def(
+      "select_compress(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor keep, "
+      "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
+      "Tensor(c!) ws, int km, int out, Tensor(d!)? pairs, Tensor(e!)? vals, Tensor(f!)? idx, "
+      "int gid_base, int step, int seed) -> ()");
+  m.def(
+      "thresh_count(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor large_segs, "
+      "Tensor tasks, Tensor task_lo, Tensor(c!) ws, float V, int adaptive, Tensor(d!) counts_out) "
+      "-> ()");
+  m.def(
+      "thresh_write(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor cap_off, "
+      "Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor(c!) ws, Tensor(d!) pairs) -> ()");
+  m.def(
+      "unpack_pairs(Tensor gathered, int world, Tensor(a!) g, Tensor seg_off, Tensor seg_n, "
+      "Tensor cap_off, Tensor utasks) -> ()");
+  m.def(
+      "unpack_validx(Tensor vals, Tensor idx, Tensor slot_seg, int world, Tensor(a!) g, "
+      "Tensor seg_off) -> ()");
+  m.def(
+      "quantize(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor segs, "
+      "Tensor tasks, Tensor task_lo, Tensor rec_off, Tensor(c!) ws, Tensor(d!) payload, int q, "
+      "int qstates, int gid_base, int step, int tag, int seed) -> ()");
+  m.def(
+      "dequantize(Tensor gathered, int world, Tensor(a!) g, Tensor seg_off, Tensor seg_n, "
+      "Tensor segs, Tensor tasks, Tensor task_lo, Tensor rec_off, int q, int qstates) -> ()");
+  m.def(
+      "sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor seg_off, Tensor seg_n, "
+      "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
+      "int nesterov, int first_step, float grad_scale) -> ()");
+  m.def("normalize_u8(Tensor input, Tensor(a!) out, float[] mean, float[] std) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
+  m.impl("select_compress", &select_compress);
+  m.impl("thresh_count", &thresh_count);
+  m.impl("thresh_write", &thresh_write);
+  m.impl("unpack_pairs", &unpack_pairs);
+  m.impl("unpack_validx", &unpack_validx);
+  m.impl("quantize", &quantize);
+  m.impl("dequantize", &dequantize);
+  m.impl("sgd_step", &sgd_step);
+  m.impl("normalize_u8", &normalize_u8);
+}

@@ -1,0 +1,112 @@
+"""Build the in-tree HIP extension ``layer_wise_aaai20_amd/_lwaaai_C.so`` for gfx950.
+
+Every ``*.hip`` / ``*.cpp`` under ``csrc/`` is compiled with ``hipcc --offload-arch=gfx950 -c`` and
+the objects are linked with the host C++ linker against the HIP runtime *bundled with PyTorch*
+(``torch/lib/libamdhip64.so``, soname ``libamdhip64.so.7``) so that exactly one HIP runtime is
+loaded in the process. No hipify step, no CUDA sources, no JIT cache: the ``.so`` lands next to the
+package and travels with the repo snapshot.
+
+Usage: ``python -m layer_wise_aaai20_amd.csrc.build [--force] [-j N]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+OUT = os.path.join(PKG, "_lwaaai_C.so")
+BUILD = os.path.join(HERE, "build")
+ARCH = os.environ.get("LWAAAI_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    return "hipcc"
+
+
+def _torch_paths():
+    import torch
+    root = os.path.dirname(torch.__file__)
+    inc = [os.path.join(root, "include"), os.path.join(root, "include", "torch", "csrc", "api",
+                                                       "include")]
+    lib = os.path.join(root, "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def sources():
+    return sorted(os.path.join(HERE, f) for f in os.listdir(HERE)
+                  if f.endswith((".hip", ".cpp")))
+
+
+def _digest(paths) -> str:
+    h = hashlib.sha256()
+    for p in sorted(paths):
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    h.update(ARCH.encode())
+    return h.hexdigest()[:16]
+
+
+def _compile(src, inc, abi):
+    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
+           f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM", "-D__HIP_PLATFORM_AMD__=1",
+           "-Wno-unused-result", "-Wno-deprecated-declarations", f"-I{HERE}"]
+    if src.endswith(".cpp"):
+        cmd += [f"-I{p}" for p in inc] + [f"-I{sysconfig.get_paths()['include']}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
+    srcs = sources()
+    headers = [os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith(".h")]
+    stamp = os.path.join(BUILD, "stamp")
+    dig = _digest(srcs + headers + [os.path.abspath(__file__)])
+    if not force and os.path.exists(OUT) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == dig:
+                if verbose:
+                    print(f"[lwaaai] up to date: {OUT}")
+                return OUT
+    os.makedirs(BUILD, exist_ok=True)
+    inc, lib, abi = _torch_paths()
+    jobs = jobs or min(8, len(srcs), os.cpu_count() or 4)
+    if verbose:
+        print(f"[lwaaai] compiling {len(srcs)} sources for {ARCH} with {jobs} jobs")
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, inc, abi), srcs))
+    tmp = OUT + ".tmp"
+    cmd = ["g++", "-shared", "-o", tmp] + objs + [
+        f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+        "-l:libamdhip64.so", f"-Wl,-rpath,{lib}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, OUT)
+    with open(stamp, "w") as f:
+        f.write(dig)
+    if verbose:
+        print(f"[lwaaai] built {OUT}")
+    return OUT
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=0)
+    args = ap.parse_args()
+    build(args.force, args.j)
+    sys.exit(0)

@@ -1,0 +1,1025 @@
+// Gradient-compression kernels for gfx950 (MI355X, CDNA4, wave64).
+//
+// One launch (or one fixed chain of launches) handles ALL segments (= layers) of a communication
+// bucket: the reference runs its compressor once per parameter tensor with torch ops
+// (CIFAR10/core.py:175-215, IMAGENET/training/train_imagenet_nv.py:255-295; SURVEY.md §2.5
+// N1-N9). Kernels here:
+//
+//   Top-K / Random-K (exact selection):
+//     k_small_select   one workgroup per segment of <= 4096 elements: registers + LDS radix select
+//                      + order-preserving compaction, EF fused.
+//     k_hist<PASS>     multi-block 11/10/10-bit radix histogram passes for large segments
+//                      (pass 0 fuses the error-feedback add g' = g + e).
+//     k_select<PASS>   one workgroup per large segment: picks the digit holding the m-th largest key.
+//     k_count, k_scan  per-block (gt, eq) counts and their per-segment exclusive scan.
+//     k_write          order-preserving compaction into (index, value) pairs or index-free values,
+//                      EF residual e = g' with the sent positions zeroed.
+//   Threshold-v / adaptive threshold: k_partial + k_finalize (abs-max), k_thresh_state, then the
+//                      same count / scan / write chain with "keep every key >= t".
+//   TernGrad / QSGD:   k_partial + k_finalize (abs-max or L2 norm), k_quant (Philox dither, bit
+//                      packing, EF), k_dequant (rank-ordered dequantise-and-average).
+//   Unpack:            k_unpack_pairs (rank-ordered LDS accumulation of every rank's pairs for a
+//                      4096-element chunk: deterministic and bit-identical on all ranks),
+//                      k_unpack_validx (index-free Random-K).
+//
+// Selection keys are 31-bit: |x| bit patterns for Top-K/threshold (monotone in |x|), Philox hashes
+// forced odd for Random-K (so padding/invalid keys of 0 never win).
+#include "common.h"
+#include "lw_kernels.h"
+
+namespace lw {
+
+constexpr int NT = 256;
+constexpr int EPB = kLargeEPB;       // elements per block in the multi-block passes (8192)
+constexpr int EPT = EPB / NT;        // 32 contiguous elements per thread in k_write / k_quant
+constexpr int SEPT = kSmallMax / NT; // 16 per thread in k_small_select
+constexpr uint32_t SENT = 0x7fffffffu;
+constexpr int HIST_WORDS = 4096;     // 2048 + 1024 + 1024 bins per large segment
+
+__device__ __forceinline__ uint32_t abs_key(float x) { return __float_as_uint(x) & 0x7fffffffu; }
+
+__device__ __forceinline__ uint32_t randk_key(uint32_t i, uint32_t gid, uint32_t step, uint32_t s0,
+                                              uint32_t s1) {
+  const u4 r = philox4x32_10(u4{i >> 2, gid, step, 1u << 24}, s0, s1);
+  return (pick(r, i & 3) >> 1) | 1u;
+}
+
+// group of 4 keys starting at a multiple of 4
+__device__ __forceinline__ void randk_key4(uint32_t i0, uint32_t gid, uint32_t step, uint32_t s0,
+                                           uint32_t s1, uint32_t k[4]) {
+  const u4 r = philox4x32_10(u4{i0 >> 2, gid, step, 1u << 24}, s0, s1);
+  k[0] = (r.x >> 1) | 1u; k[1] = (r.y >> 1) | 1u; k[2] = (r.z >> 1) | 1u; k[3] = (r.w >> 1) | 1u;
+}
+
+template <int PASS> struct PassCfg;
+template <> struct PassCfg<0> { static constexpr int BITS = 11, SHIFT = 20, HOFF = 0; };
+template <> struct PassCfg<1> { static constexpr int BITS = 10, SHIFT = 10, HOFF = 2048; };
+template <> struct PassCfg<2> { static constexpr int BITS = 10, SHIFT = 0, HOFF = 3072; };
+
+// Find the digit d holding the m-th largest key of histogram h (NB bins) and the rank of that key
+// within bin d. Block-wide; all threads return the same values.
+template <int NB>
+__device__ __forceinline__ void select_digit(const uint32_t* h, uint32_t m, uint32_t& d_out,
+                                             uint32_t& m_out, uint32_t* arr /*NT*/,
+                                             uint32_t* scr /*4*/, uint32_t* res /*2*/) {
+  constexpr int BPT = NB / NT;
+  const int j = threadIdx.x;
+  uint32_t loc[BPT];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int b = 0; b < BPT; ++b) { loc[b] = h[j * BPT + b]; sum += loc[b]; }
+  if (j == 0) { res[0] = 0; res[1] = m; }
+  arr[NT - 1 - j] = sum;
+  __syncthreads();
+  uint32_t tot;
+  const uint32_t e = block_excl_scan<NT>(arr[j], scr, tot);
+  arr[j] = e;
+  __syncthreads();
+  const uint32_t above = arr[NT - 1 - j];   // keys in bins above this thread's range
+  if (above < m && m <= above + sum) {
+    uint32_t cum = above;
+#pragma unroll
+    for (int b = BPT - 1; b >= 0; --b) {
+      if (cum + loc[b] >= m) { res[0] = j * BPT + b; res[1] = m - cum; break; }
+      cum += loc[b];
+    }
+  }
+  __syncthreads();
+  d_out = res[0];
+  m_out = res[1];
+  __syncthreads();
+}
+
+// Final per-segment decision shared by the small and large paths.
+__device__ __forceinline__ void finish_state(SelState& s, int km, uint32_t keep, uint32_t m_rem,
+                                             uint32_t eq_total, uint32_t cap) {
+  s.cnt_gt = keep - m_rem;
+  if (km == KM_RANDK) {
+    s.quota = m_rem;                       // exactly `keep` elements, ties broken by index
+  } else {
+    // Top-K keeps every tie (core.py:182 `|g| < thr` zeroed) up to the payload capacity;
+    // zero-valued ties carry nothing and are never sent.
+    const uint32_t room = cap > s.cnt_gt ? cap - s.cnt_gt : 0u;
+    s.quota = s.tkey == 0 ? 0u : min(eq_total, room);
+  }
+  s.total = s.cnt_gt + s.quota;
+  s.cap = cap;
+}
+
+// ------------------------------------------------------------------------------------------
+// Small segments: whole selection + compaction in one workgroup.
+// ------------------------------------------------------------------------------------------
+template <int KM, int OUT, bool EF>
+__global__ __launch_bounds__(NT) void k_small_select(
+    float* __restrict__ g, float* __restrict__ ef, const int64_t* __restrict__ seg_off,
+    const int32_t* __restrict__ seg_n, const int32_t* __restrict__ keep,
+    const int64_t* __restrict__ cap_off, const int32_t* __restrict__ small_segs,
+    int2* __restrict__ pairs, float* __restrict__ vals, int32_t* __restrict__ idx_out,
+    SelState* __restrict__ st_small, uint32_t gid_base, uint32_t step, uint32_t s0, uint32_t s1) {
+  __shared__ uint32_t h[2048];
+  __shared__ uint32_t arr[NT];
+  __shared__ uint32_t scr[NT / WAVE];
+  __shared__ uint32_t res[2];
+  const int s = small_segs[blockIdx.x];
+  const int n = seg_n[s];
+  const int64_t off = seg_off[s];
+  const uint32_t m = (uint32_t)keep[s];
+  const int64_t c0 = cap_off[s];
+  const uint32_t cap = (uint32_t)(cap_off[s + 1] - c0);
+  float* gp = g + off;
+  float* ep = EF ? ef + off : nullptr;
+  const int base = threadIdx.x * SEPT;
+
+  float v[SEPT];
+  uint32_t key[SEPT];
+#pragma unroll
+  for (int k = 0; k < SEPT; ++k) {
+    const int i = base + k;
+    float x = 0.f;
+    if (i < n) {
+      x = gp[i];
+      if (EF) x += ep[i];
+    }
+    v[k] = x;
+  }
+  if (KM == KM_TOPK) {
+#pragma unroll
+    for (int k = 0; k < SEPT; ++k) key[k] = (base + k < n) ? abs_key(v[k]) : 0u;
+  } else {
+#pragma unroll
+    for (int k = 0; k < SEPT; k += 4) {
+      uint32_t q[4];
+      randk_key4(base + k, gid_base + s, step, s0, s1, q);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) key[k + t] = (base + k + t < n) ? q[t] : 0u;
+    }
+  }
+
+  // three radix passes over the register-resident keys
+  uint32_t prefix = 0, mr = m;
+  uint32_t eq_total = 0;
+#pragma unroll
+  for (int pass = 0; pass < 3; ++pass) {
+    const int bits = pass == 0 ? 11 : 10;
+    const int shift = pass == 0 ? 20 : (pass == 1 ? 10 : 0);
+    const int nb = 1 << bits;
+    for (int b = threadIdx.x; b < nb; b += NT) h[b] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SEPT; ++k) {
+      if (base + k < n && (key[k] >> (shift + bits)) == prefix)
+        atomicAdd(&h[(key[k] >> shift) & (nb - 1)], 1u);
+    }
+    __syncthreads();
+    uint32_t d, mn;
+    if (pass == 0) select_digit<2048>(h, mr, d, mn, arr, scr, res);
+    else select_digit<1024>(h, mr, d, mn, arr, scr, res);
+    if (pass == 2) eq_total = h[d];
+    __syncthreads();
+    prefix = (prefix << bits) | d;
+    mr = mn;
+  }
+  SelState S;
+  S.tkey = prefix;
+  finish_state(S, KM, m, mr, eq_total, cap);
+  if (threadIdx.x == 0) st_small[blockIdx.x] = S;
+
+  // order-preserving compaction: (gt, eq) counts packed in one word (<= 4096 each)
+  uint32_t cg = 0, ce = 0;
+#pragma unroll
+  for (int k = 0; k < SEPT; ++k) {
+    if (base + k < n) { cg += key[k] > S.tkey; ce += key[k] == S.tkey; }
+  }
+  uint32_t tot;
+  const uint32_t pre = block_excl_scan<NT>(cg | (ce << 16), scr, tot);
+  uint32_t gb = pre & 0xffffu, eb = pre >> 16;
+#pragma unroll
+  for (int k = 0; k < SEPT; ++k) {
+    const int i = base + k;
+    if (i >= n) break;
+    bool sel = false;
+    uint32_t pos = 0;
+    if (key[k] > S.tkey) { sel = true; pos = gb + min(eb, S.quota); ++gb; }
+    else if (key[k] == S.tkey) { if (eb < S.quota) { sel = true; pos = gb + eb; } ++eb; }
+    if (sel) {
+      if (OUT == OUT_PAIRS) pairs[c0 + pos] = make_int2(i, __float_as_int(v[k]));
+      else { vals[c0 + pos] = v[k]; idx_out[c0 + pos] = i; }
+    }
+    if (EF) ep[i] = sel ? 0.f : v[k];
+  }
+  if (OUT == OUT_PAIRS)
+    for (uint32_t p = S.total + threadIdx.x; p < cap; p += NT) pairs[c0 + p] = make_int2(SENT, 0);
+}
+
+// ------------------------------------------------------------------------------------------
+// Large segments: multi-block radix select.
+// Coalesced layout for histogram/count passes: element = begin + j*NT*4 + tid*4 + {0..3}.
+// ------------------------------------------------------------------------------------------
+template <int KM, bool EFADD>
+__device__ __forceinline__ void load4_keys(float* gp, const float* ep, int i0, int end, uint32_t gid,
+                                           uint32_t step, uint32_t s0, uint32_t s1, uint32_t k[4],
+                                           bool valid[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) valid[t] = i0 + t < end;
+  if (KM == KM_RANDK) {
+    randk_key4(i0, gid, step, s0, s1, k);
+    return;
+  }
+  float4 v;
+  if (i0 + 3 < end) {
+    v = *reinterpret_cast<const float4*>(gp + i0);
+    if (EFADD) {
+      const float4 e = *reinterpret_cast<const float4*>(ep + i0);
+      v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
+      *reinterpret_cast<float4*>(gp + i0) = v;
+    }
+  } else {
+    float t4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (valid[t]) {
+        float x = gp[i0 + t];
+        if (EFADD) { x += ep[i0 + t]; gp[i0 + t] = x; }
+        t4[t] = x;
+      }
+    v = make_float4(t4[0], t4[1], t4[2], t4[3]);
+  }
+  k[0] = abs_key(v.x); k[1] = abs_key(v.y); k[2] = abs_key(v.z); k[3] = abs_key(v.w);
+}
+
+template <int KM, int PASS, bool EFADD>
+__global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float* __restrict__ ef,
+                                             const int64_t* __restrict__ seg_off,
+                                             const int32_t* __restrict__ seg_n,
+                                             const int32_t* __restrict__ large_segs,
+                                             const int2* __restrict__ tasks,
+                                             const SelState* __restrict__ st,
+                                             uint32_t* __restrict__ hist_all, uint32_t gid_base,
+                                             uint32_t step, uint32_t s0, uint32_t s1) {
+  using C = PassCfg<PASS>;
+  constexpr int NB = 1 << C::BITS;
+  __shared__ uint32_t h[NB];
+  const int2 t = tasks[blockIdx.x];
+  const int li = t.x, begin = t.y;
+  const int s = large_segs[li];
+  const int n = seg_n[s];
+  const int64_t off = seg_off[s];
+  for (int b = threadIdx.x; b < NB; b += NT) h[b] = 0;
+  const uint32_t prefix = PASS > 0 ? st[li].prefix : 0u;
+  __syncthreads();
+  float* gp = g + off;
+  const float* ep = EFADD ? ef + off : nullptr;
+  const int end = min(begin + EPB, n);
+#pragma unroll 2
+  for (int j = 0; j < EPB / (NT * 4); ++j) {
+    const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
+    if (i0 >= end) break;
+    uint32_t k[4];
+    bool valid[4];
+    load4_keys<KM, EFADD>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (valid[q] && (k[q] >> (C::SHIFT + C::BITS)) == prefix)
+        atomicAdd(&h[(k[q] >> C::SHIFT) & (NB - 1)], 1u);
+  }
+  __syncthreads();
+  uint32_t* gh = hist_all + (size_t)li * HIST_WORDS + C::HOFF;
+  for (int b = threadIdx.x; b < NB; b += NT) {
+    const uint32_t c = h[b];
+    if (c) atomicAdd(gh + b, c);
+  }
+}
+
+template <int KM, int PASS>
+__global__ __launch_bounds__(NT) void k_select(const uint32_t* __restrict__ hist_all,
+                                               SelState* __restrict__ st,
+                                               const int32_t* __restrict__ large_segs,
+                                               const int32_t* __restrict__ keep,
+                                               const int64_t* __restrict__ cap_off) {
+  using C = PassCfg<PASS>;
+  constexpr int NB = 1 << C::BITS;
+  __shared__ uint32_t arr[NT];
+  __shared__ uint32_t scr[NT / WAVE];
+  __shared__ uint32_t res[2];
+  const int li = blockIdx.x;
+  const int s = large_segs[li];
+  const uint32_t* h = hist_all + (size_t)li * HIST_WORDS + C::HOFF;
+  const uint32_t m = PASS == 0 ? (uint32_t)keep[s] : st[li].m;
+  const uint32_t prefix = PASS == 0 ? 0u : st[li].prefix;
+  uint32_t d, mn;
+  select_digit<NB>(h, m, d, mn, arr, scr, res);
+  if (threadIdx.x == 0) {
+    SelState S = st[li];
+    S.prefix = (prefix << C::BITS) | d;
+    S.m = mn;
+    if (PASS == 2) {
+      S.tkey = S.prefix;
+      finish_state(S, KM, (uint32_t)keep[s], mn, h[d], (uint32_t)(cap_off[s + 1] - cap_off[s]));
+    }
+    st[li] = S;
+  }
+}
+
+// Threshold methods: t = key(V) (Thresholdv) or key(max|g|/2) (AdaptiveThreshold); keep all ties.
+__global__ void k_thresh_state(SelState* __restrict__ st, const float* __restrict__ segmax,
+                               int nseg, float V, int adaptive) {
+  const int li = blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= nseg) return;
+  const float thr = adaptive ? segmax[li] * 0.5f : V;
+  SelState S{};
+  S.tkey = abs_key(thr);
+  S.cnt_gt = 0;
+  S.quota = S.tkey == 0 ? 0u : 0xffffffffu;
+  st[li] = S;
+}
+
+template <int KM, bool EFADD>
+__global__ __launch_bounds__(NT) void k_count(float* __restrict__ g, const float* __restrict__ ef,
+                                              const int64_t* __restrict__ seg_off,
+                                              const int32_t* __restrict__ seg_n,
+                                              const int32_t* __restrict__ large_segs,
+                                              const int2* __restrict__ tasks,
+                                              const SelState* __restrict__ st,
+                                              uint2* __restrict__ cnt, uint32_t gid_base,
+                                              uint32_t step, uint32_t s0, uint32_t s1) {
+  __shared__ uint32_t scr[NT / WAVE];
+  const int2 t = tasks[blockIdx.x];
+  const int li = t.x, begin = t.y;
+  const int s = large_segs[li];
+  const int n = seg_n[s];
+  const int64_t off = seg_off[s];
+  const uint32_t tk = st[li].tkey;
+  float* gp = g + off;
+  const float* ep = EFADD ? ef + off : nullptr;
+  const int end = min(begin + EPB, n);
+  uint32_t cg = 0, ce = 0;
+#pragma unroll 2
+  for (int j = 0; j < EPB / (NT * 4); ++j) {
+    const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
+    if (i0 >= end) break;
+    uint32_t k[4];
+    bool valid[4];
+    load4_keys<KM, EFADD>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (valid[q]) { cg += k[q] > tk; ce += k[q] == tk; }
+  }
+  uint32_t tg, te;
+  block_excl_scan<NT>(cg, scr, tg);
+  block_excl_scan<NT>(ce, scr, te);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = make_uint2(tg, te);
+}
+
+// One workgroup per large segment: exclusive scan of the per-block (gt, eq) counts.
+template <int KM>
+__global__ __launch_bounds__(NT) void k_scan(const uint2* __restrict__ cnt, uint2* __restrict__ pre,
+                                             const int32_t* __restrict__ task_lo,
+                                             SelState* __restrict__ st,
+                                             int32_t* __restrict__ count_out) {
+  __shared__ uint32_t scr[NT / WAVE];
+  const int li = blockIdx.x;
+  const int lo = task_lo[li], hi = task_lo[li + 1];
+  uint32_t carry_g = 0, carry_e = 0;
+  for (int b = lo; b < hi; b += NT) {
+    const int i = b + threadIdx.x;
+    const uint2 c = i < hi ? cnt[i] : make_uint2(0, 0);
+    uint32_t tg, te;
+    const uint32_t eg = block_excl_scan<NT>(c.x, scr, tg);
+    const uint32_t ee = block_excl_scan<NT>(c.y, scr, te);
+    if (i < hi) pre[i] = make_uint2(carry_g + eg, carry_e + ee);
+    carry_g += tg;
+    carry_e += te;
+  }
+  if (threadIdx.x == 0) {
+    SelState S = st[li];
+    if (KM == KM_THRESH) {
+      S.cnt_gt = carry_g;
+      S.quota = S.tkey == 0 ? 0u : carry_e;
+      S.total = S.cnt_gt + S.quota;
+      st[li] = S;
+    }
+    if (count_out) count_out[li] = (int32_t)S.total;
+  }
+}
+
+// Per-segment capacity for the threshold path is only known after the count exchange.
+__global__ void k_set_caps(SelState* __restrict__ st, const int64_t* __restrict__ cap_off,
+                           const int32_t* __restrict__ large_segs, int nseg) {
+  const int li = blockIdx.x * blockDim.x + threadIdx.x;
+  if (li >= nseg) return;
+  const int s = large_segs[li];
+  SelState S = st[li];
+  S.cap = (uint32_t)(cap_off[s + 1] - cap_off[s]);
+  if (S.total > S.cap) {                  // cannot happen: cap = max over ranks of total
+    S.quota = S.cap > S.cnt_gt ? min(S.quota, S.cap - S.cnt_gt) : 0u;
+    S.total = min(S.cnt_gt, S.cap) + S.quota;
+  }
+  st[li] = S;
+}
+
+__global__ __launch_bounds__(NT) void k_fill_tail(int2* __restrict__ pairs,
+                                                  const int64_t* __restrict__ cap_off,
+                                                  const int32_t* __restrict__ large_segs,
+                                                  const SelState* __restrict__ st) {
+  const int li = blockIdx.x;
+  const int s = large_segs[li];
+  const int64_t c0 = cap_off[s];
+  const uint32_t cap = (uint32_t)(cap_off[s + 1] - c0);
+  for (uint32_t p = st[li].total + threadIdx.x; p < cap; p += NT) pairs[c0 + p] = make_int2(SENT, 0);
+}
+
+// Order-preserving compaction. Thread owns EPT contiguous elements.
+template <int KM, int OUT, bool EF>
+__global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __restrict__ ef,
+                                              const int64_t* __restrict__ seg_off,
+                                              const int32_t* __restrict__ seg_n,
+                                              const int32_t* __restrict__ large_segs,
+                                              const int2* __restrict__ tasks,
+                                              const SelState* __restrict__ st,
+                                              const uint2* __restrict__ pre,
+                                              const int64_t* __restrict__ cap_off,
+                                              int2* __restrict__ pairs, float* __restrict__ vals,
+                                              int32_t* __restrict__ idx_out, uint32_t gid_base,
+                                              uint32_t step, uint32_t s0, uint32_t s1) {
+  __shared__ uint32_t scr[NT / WAVE];
+  const int2 t = tasks[blockIdx.x];
+  const int li = t.x, begin = t.y;
+  const int s = large_segs[li];
+  const int n = seg_n[s];
+  const int64_t off = seg_off[s];
+  const SelState S = st[li];
+  const uint2 bp = pre[blockIdx.x];
+  const int64_t c0 = cap_off[s];
+  float* gp = g + off;
+  float* ep = EF ? ef + off : nullptr;
+  const int i_base = begin + threadIdx.x * EPT;
+  const int end = min(begin + EPB, n);
+  // RANDK never touched g in the histogram passes, so its EF add happens here.
+  constexpr bool ADD_EF_HERE = EF && (KM == KM_RANDK);
+
+  float v[EPT];
+  uint32_t key[EPT];
+  if (i_base + EPT <= end) {
+#pragma unroll
+    for (int q = 0; q < EPT / 4; ++q) {
+      float4 x = *reinterpret_cast<const float4*>(gp + i_base + 4 * q);
+      if (ADD_EF_HERE) {
+        const float4 e = *reinterpret_cast<const float4*>(ep + i_base + 4 * q);
+        x.x += e.x; x.y += e.y; x.z += e.z; x.w += e.w;
+      }
+      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      const int i = i_base + k;
+      float x = 0.f;
+      if (i < end) { x = gp[i]; if (ADD_EF_HERE) x += ep[i]; }
+      v[k] = x;
+    }
+  }
+  if (KM == KM_RANDK) {
+#pragma unroll
+    for (int k = 0; k < EPT; k += 4) {
+      uint32_t q[4];
+      randk_key4(i_base + k, gid_base + s, step, s0, s1, q);
+      key[k] = q[0]; key[k + 1] = q[1]; key[k + 2] = q[2]; key[k + 3] = q[3];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) key[k] = abs_key(v[k]);
+  }
+  uint32_t cg = 0, ce = 0;
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const bool ok = i_base + k < end;
+    cg += ok && key[k] > S.tkey;
+    ce += ok && key[k] == S.tkey;
+  }
+  uint32_t tot;
+  const uint32_t p = block_excl_scan<NT>(cg | (ce << 16), scr, tot);
+  uint32_t gb = bp.x + (p & 0xffffu), eb = bp.y + (p >> 16);
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int i = i_base + k;
+    if (i >= end) break;
+    bool sel = false;
+    uint32_t pos = 0;
+    if (key[k] > S.tkey) { pos = gb + min(eb, S.quota); sel = pos < S.cap; ++gb; }
+    else if (key[k] == S.tkey) { if (eb < S.quota) { sel = true; pos = gb + eb; } ++eb; }
+    if (sel) {
+      if (OUT == OUT_PAIRS) pairs[c0 + pos] = make_int2(i, __float_as_int(v[k]));
+      else { vals[c0 + pos] = v[k]; idx_out[c0 + pos] = i; }
+    }
+    if (EF) ep[i] = sel ? 0.f : v[k];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-segment abs-max / sum-of-squares (two-level, fixed reduction order => deterministic)
+// ------------------------------------------------------------------------------------------
+template <bool EFADD>
+__global__ __launch_bounds__(NT) void k_partial(float* __restrict__ g, const float* __restrict__ ef,
+                                                const int64_t* __restrict__ seg_off,
+                                                const int32_t* __restrict__ seg_n,
+                                                const int32_t* __restrict__ large_segs,
+                                                const int2* __restrict__ tasks,
+                                                float2* __restrict__ partial) {
+  __shared__ float scr[NT / WAVE];
+  const int2 t = tasks[blockIdx.x];
+  const int li = t.x, begin = t.y;
+  const int s = large_segs[li];
+  const int n = seg_n[s];
+  const int64_t off = seg_off[s];
+  float* gp = g + off;
+  const float* ep = EFADD ? ef + off : nullptr;
+  const int end = min(begin + EPB, n);
+  float mx = 0.f, ss = 0.f;
+  for (int j = 0; j < EPB / (NT * 4); ++j) {
+    const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
+    if (i0 >= end) break;
+    float4 v;
+    if (i0 + 3 < end) {
+      v = *reinterpret_cast<const float4*>(gp + i0);
+      if (EFADD) {
+        const float4 e = *reinterpret_cast<const float4*>(ep + i0);
+        v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
+        *reinterpret_cast<float4*>(gp + i0) = v;
+      }
+    } else {
+      float t4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < 4; ++q)
+        if (i0 + q < end) {
+          float x = gp[i0 + q];
+          if (EFADD) { x += ep[i0 + q]; gp[i0 + q] = x; }
+          t4[q] = x;
+        }
+      v = make_float4(t4[0], t4[1], t4[2], t4[3]);
+    }
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  mx = block_max<NT>(mx, scr);
+  ss = block_sum<NT>(ss, scr);
+  if (threadIdx.x == 0) partial[blockIdx.x] = make_float2(mx, ss);
+}
+
+// out[li] = max (what=0) or sqrt(sum sq) (what=1)
+__global__ __launch_bounds__(NT) void k_finalize(const float2* __restrict__ partial,
+                                                 const int32_t* __restrict__ task_lo,
+                                                 float* __restrict__ out, int what) {
+  __shared__ float scr[NT / WAVE];
+  const int li = blockIdx.x;
+  const int lo = task_lo[li], hi = task_lo[li + 1];
+  float mx = 0.f, ss = 0.f;
+  for (int i = lo + threadIdx.x; i < hi; i += NT) {
+    const float2 p = partial[i];
+    mx = fmaxf(mx, p.x);
+    ss += p.y;
+  }
+  mx = block_max<NT>(mx, scr);
+  ss = block_sum<NT>(ss, scr);
+  if (threadIdx.x == 0) out[li] = what == 0 ? mx : sqrtf(ss);
+}
+
+// ------------------------------------------------------------------------------------------
+// Quantisers. Payload (int32 words, per rank): [nseg header floats][records], segment li's
+// group records at hdr + rec_off[li]*R words (a group = 32 consecutive elements).
+//   Q_TERN : 2-bit codes {0, +1, -1}: R = 2
+//   Q_QS8  : signed int8 level, qstates <= 127: R = 8
+//   Q_QS9  : uint8 level + sign bitmap, qstates <= 255: 8 level words at rec*8 and the sign
+//            word at the segment's sign block (levels block: G*8 words, then G sign words)
+//   Q_QS16 : signed int16 level, qstates <= 32767: R = 16
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void rng32(float u[EPT], uint32_t i_base, uint32_t gid, uint32_t step,
+                                      uint32_t tag, uint32_t s0, uint32_t s1) {
+#pragma unroll
+  for (int k = 0; k < EPT; k += 4) {
+    const u4 r = philox4x32_10(u4{(i_base + k) >> 2, gid, step, tag}, s0, s1);
+    u[k] = u01(r.x); u[k + 1] = u01(r.y); u[k + 2] = u01(r.z); u[k + 3] = u01(r.w);
+  }
+}
+
+template <int Q, bool EF>
+__global__ __launch_bounds__(NT) void k_quant(
+    const float* __restrict__ g, float* __restrict__ ef, const int64_t* __restrict__ seg_off,
+    const int32_t* __restrict__ seg_n, const int32_t* __restrict__ large_segs,
+    const int2* __restrict__ tasks, const int64_t* __restrict__ rec_off,
+    const float* __restrict__ scale, uint32_t* __restrict__ payload, int nseg, int qstates,
+    uint32_t gid_base, uint32_t step, uint32_t tag, uint32_t s0, uint32_t s1) {
+  const int2 t = tasks[blockIdx.x];
+  const int li = t.x, begin = t.y;
+  const int s = large_segs[li];
+  const int n = seg_n[s];
+  const int64_t off = seg_off[s];
+  const float sc = scale[li];
+  if (t.y == 0 && threadIdx.x == 0) payload[li] = __float_as_uint(sc);
+  const int i_base = begin + threadIdx.x * EPT;
+  if (i_base >= n) return;
+  const int end = min(begin + EPB, n);
+  const float* gp = g + off;
+  float* ep = EF ? ef + off : nullptr;
+  float v[EPT];
+  if (i_base + EPT <= end) {
+#pragma unroll
+    for (int q = 0; q < EPT / 4; ++q) {
+      const float4 x = *reinterpret_cast<const float4*>(gp + i_base + 4 * q);
+      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) v[k] = (i_base + k < end) ? gp[i_base + k] : 0.f;
+  }
+  float u[EPT];
+  rng32(u, (uint32_t)i_base, gid_base + s, step, tag, s0, s1);
+  const int64_t grp = rec_off[li] + i_base / EPT;   // group index within payload records
+  uint32_t* rec = payload + hdr_words(nseg);
+  float dq[EPT];
+  if (Q == Q_TERN) {
+    uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      uint32_t c = 0;
+      if (sc > 0.f) {
+        const float prob = fabsf(v[k]) / sc;
+        if (u[k] < prob) c = v[k] > 0.f ? 1u : (v[k] < 0.f ? 2u : 0u);
+      }
+      dq[k] = c == 1u ? sc : (c == 2u ? -sc : 0.f);
+      if (k < 16) w0 |= c << (2 * k); else w1 |= c << (2 * (k - 16));
+    }
+    *reinterpret_cast<uint2*>(rec + grp * 2) = make_uint2(w0, w1);
+  } else {
+    const float qs = (float)qstates;
+    int lv[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      int l = 0;
+      if (sc > 0.f) {
+        l = (int)floorf(fabsf(v[k]) / sc * qs + u[k]);
+        l = min(l, qstates);
+      }
+      const float sg = v[k] > 0.f ? 1.f : (v[k] < 0.f ? -1.f : 0.f);
+      dq[k] = sg * sc * ((float)l / qs);
+      lv[k] = v[k] < 0.f ? -l : l;
+    }
+    if (Q == Q_QS8) {
+      uint32_t w[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        w[q] = (uint32_t)(lv[4 * q] & 0xff) | ((uint32_t)(lv[4 * q + 1] & 0xff) << 8) |
+               ((uint32_t)(lv[4 * q + 2] & 0xff) << 16) | ((uint32_t)(lv[4 * q + 3] & 0xff) << 24);
+      uint4* o = reinterpret_cast<uint4*>(rec + grp * 8);
+      o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    } else if (Q == Q_QS9) {
+      const int64_t Gtot = rec_off[nseg];     // all level words first, then all sign words
+      uint32_t w[8], sgn = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        w[q] = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int l = lv[4 * q + r];
+          w[q] |= (uint32_t)(l < 0 ? -l : l) << (8 * r);
+          sgn |= (l < 0 ? 1u : 0u) << (4 * q + r);
+        }
+      }
+      uint4* o = reinterpret_cast<uint4*>(rec + grp * 8);
+      o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+      rec[Gtot * 8 + grp] = sgn;
+    } else {  // Q_QS16
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        w[q] = (uint32_t)(lv[2 * q] & 0xffff) | ((uint32_t)(lv[2 * q + 1] & 0xffff) << 16);
+      uint4* o = reinterpret_cast<uint4*>(rec + grp * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
+  }
+  if (EF) {
+#pragma unroll
+    for (int k = 0; k < EPT; ++k)
+      if (i_base + k < end) ep[i_base + k] = v[k] - dq[k];
+  }
+}
+
+// Dequantise every rank's payload for this thread's 32-element group, summing in rank order, then
+// divide by the world size (core.py:221-223 `compress_grad /= float(world_size)`).
+template <int Q>
+__global__ __launch_bounds__(NT) void k_dequant(const uint32_t* __restrict__ gathered,
+                                                int64_t words_per_rank, int ws,
+                                                float* __restrict__ g,
+                                                const int64_t* __restrict__ seg_off,
+                                                const int32_t* __restrict__ seg_n,
+                                                const int32_t* __restrict__ large_segs,
+                                                const int2* __restrict__ tasks,
+                                                const int64_t* __restrict__ rec_off, int nseg,
+                                                int qstates) {
+  const int2 t = tasks[blockIdx.x];
+  const int li = t.x, begin = t.y;
+  const int s = large_segs[li];
+  const int n = seg_n[s];
+  const int64_t off = seg_off[s];
+  const int i_base = begin + threadIdx.x * EPT;
+  if (i_base >= n) return;
+  const int end = min(begin + EPB, n);
+  const int64_t grp = rec_off[li] + i_base / EPT;
+  const int64_t Gtot = rec_off[nseg];
+  float acc[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) acc[k] = 0.f;
+  for (int r = 0; r < ws; ++r) {
+    const uint32_t* P = gathered + (int64_t)r * words_per_rank;
+    const float sc = __uint_as_float(P[li]);
+    const uint32_t* rec = P + hdr_words(nseg);
+    if (Q == Q_TERN) {
+      const uint2 w = *reinterpret_cast<const uint2*>(rec + grp * 2);
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const uint32_t c = ((k < 16 ? w.x : w.y) >> (2 * (k & 15))) & 3u;
+        acc[k] += c == 1u ? sc : (c == 2u ? -sc : 0.f);
+      }
+    } else if (Q == Q_QS8) {
+      const uint4* o = reinterpret_cast<const uint4*>(rec + grp * 8);
+      const uint4 a = o[0], b = o[1];
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int l = (int)(int8_t)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
+        const float sg = l > 0 ? 1.f : (l < 0 ? -1.f : 0.f);
+        acc[k] += sg * sc * ((float)(l < 0 ? -l : l) / (float)qstates);
+      }
+    } else if (Q == Q_QS9) {
+      const uint4* o = reinterpret_cast<const uint4*>(rec + grp * 8);
+      const uint4 a = o[0], b = o[1];
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const uint32_t sgn = rec[Gtot * 8 + grp];
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int l = (int)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
+        const float sg = l == 0 ? 0.f : (((sgn >> k) & 1u) ? -1.f : 1.f);
+        acc[k] += sg * sc * ((float)l / (float)qstates);
+      }
+    } else {
+      const uint4* o = reinterpret_cast<const uint4*>(rec + grp * 16);
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 x = o[q];
+        w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
+      }
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int l = (int)(int16_t)((w[k >> 1] >> (16 * (k & 1))) & 0xffff);
+        const float sg = l > 0 ? 1.f : (l < 0 ? -1.f : 0.f);
+        acc[k] += sg * sc * ((float)(l < 0 ? -l : l) / (float)qstates);
+      }
+    }
+  }
+  float* gp = g + off;
+  const float fws = (float)ws;
+  if (i_base + EPT <= end) {
+#pragma unroll
+    for (int q = 0; q < EPT / 4; ++q)
+      *reinterpret_cast<float4*>(gp + i_base + 4 * q) =
+          make_float4(acc[4 * q] / fws, acc[4 * q + 1] / fws, acc[4 * q + 2] / fws,
+                      acc[4 * q + 3] / fws);
+  } else {
+    for (int k = 0; k < EPT; ++k)
+      if (i_base + k < end) gp[i_base + k] = acc[k] / fws;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Unpack of all-gathered (index, value) pairs: deterministic rank-ordered sum, / world_size.
+// ------------------------------------------------------------------------------------------
+// First position in a[0..len) whose .x >= x (a sorted by .x): 64-ary search by one wave.
+__device__ __forceinline__ int wave_lower_bound(const int2* __restrict__ a, int len, int x) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  int lo = 0, hi = len;
+  while (hi - lo > WAVE) {
+    const int step = (hi - lo + WAVE - 1) / WAVE;
+    const int p = lo + lane * step;
+    const bool pred = (p < hi) && (a[p].x < x);
+    const int c = __popcll(__ballot(pred));
+    if (c == 0) { hi = lo; }
+    else {
+      const int plast = lo + (c - 1) * step;
+      const int pnext = lo + c * step;
+      lo = plast + 1;
+      hi = min(pnext, hi);
+    }
+  }
+  const int p = lo + lane;
+  const bool pred = (p < hi) && (a[p].x < x);
+  return lo + __popcll(__ballot(pred));
+}
+
+constexpr int UCH = kUnpackChunk;   // 4096 elements per workgroup
+
+__global__ __launch_bounds__(NT) void k_unpack_pairs(const int2* __restrict__ gathered,
+                                                     int64_t cap_total, int ws,
+                                                     float* __restrict__ g,
+                                                     const int64_t* __restrict__ seg_off,
+                                                     const int32_t* __restrict__ seg_n,
+                                                     const int64_t* __restrict__ cap_off,
+                                                     const int2* __restrict__ utasks) {
+  __shared__ float acc[UCH];
+  __shared__ int lo_s[kMaxWorld], hi_s[kMaxWorld];
+  const int2 t = utasks[blockIdx.x];
+  const int s = t.x, cb = t.y;
+  const int n = seg_n[s];
+  const int ce = min(cb + UCH, n);
+  const int64_t c0 = cap_off[s];
+  const int cap = (int)(cap_off[s + 1] - c0);
+  for (int j = threadIdx.x; j < UCH; j += NT) acc[j] = 0.f;
+  const int w = threadIdx.x / WAVE;
+  for (int r = w; r < ws; r += NT / WAVE) {
+    const int2* a = gathered + (int64_t)r * cap_total + c0;
+    const int l = wave_lower_bound(a, cap, cb);
+    const int h = wave_lower_bound(a, cap, ce);
+    if ((threadIdx.x & (WAVE - 1)) == 0) { lo_s[r] = l; hi_s[r] = h; }
+  }
+  __syncthreads();
+  for (int r = 0; r < ws; ++r) {
+    const int2* a = gathered + (int64_t)r * cap_total + c0;
+    for (int j = lo_s[r] + threadIdx.x; j < hi_s[r]; j += NT) {
+      const int2 p = a[j];
+      acc[p.x - cb] += __int_as_float(p.y);
+    }
+    __syncthreads();
+  }
+  float* gp = g + seg_off[s] + cb;
+  const float fws = (float)ws;
+  const int len = ce - cb;
+  if (len == UCH) {
+    for (int j = threadIdx.x * 4; j < UCH; j += NT * 4)
+      *reinterpret_cast<float4*>(gp + j) =
+          make_float4(acc[j] / fws, acc[j + 1] / fws, acc[j + 2] / fws, acc[j + 3] / fws);
+  } else {
+    for (int j = threadIdx.x; j < len; j += NT) gp[j] = acc[j] / fws;
+  }
+}
+
+// Index-free Random-K: every rank selected the same indices; values were all-reduced (summed).
+__global__ __launch_bounds__(NT) void k_unpack_validx(const float* __restrict__ vals,
+                                                      const int32_t* __restrict__ idx,
+                                                      const int32_t* __restrict__ slot_seg,
+                                                      int64_t nslots, int ws,
+                                                      float* __restrict__ g,
+                                                      const int64_t* __restrict__ seg_off) {
+  const int64_t j = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (j >= nslots) return;
+  const int s = slot_seg[j];
+  g[seg_off[s] + idx[j]] = vals[j] / (float)ws;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host launchers
+// ------------------------------------------------------------------------------------------
+#define LW_LAUNCH(kern, grid, stream, ...) \
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, stream, __VA_ARGS__)
+
+template <int KM, int OUT, bool EF>
+static void select_compress_t(const SelectArgs& a, hipStream_t st) {
+  if (a.n_small > 0)
+    LW_LAUNCH((k_small_select<KM, OUT, EF>), a.n_small, st, a.g, a.ef, a.seg_off, a.seg_n, a.keep,
+              a.cap_off, a.small_segs, a.pairs, a.vals, a.idx_out, a.st_small, a.gid_base, a.step,
+              a.seed0, a.seed1);
+  if (a.n_large == 0) return;
+  (void)hipMemsetAsync(a.hist, 0, sizeof(uint32_t) * HIST_WORDS * (size_t)a.n_large, st);
+  LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+            a.large_segs, a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1);
+  LW_LAUNCH((k_select<KM, 0>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);
+  LW_LAUNCH((k_hist<KM, 1, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
+            a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1);
+  LW_LAUNCH((k_select<KM, 1>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);
+  LW_LAUNCH((k_hist<KM, 2, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
+            a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1);
+  LW_LAUNCH((k_select<KM, 2>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);
+  LW_LAUNCH((k_count<KM, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
+            a.tasks, a.st_large, a.cnt, a.gid_base, a.step, a.seed0, a.seed1);
+  LW_LAUNCH((k_scan<KM>), a.n_large, st, a.cnt, a.pre, a.task_lo, a.st_large, (int32_t*)nullptr);
+  if (OUT == OUT_PAIRS)
+    LW_LAUNCH(k_fill_tail, a.n_large, st, a.pairs, a.cap_off, a.large_segs, a.st_large);
+  LW_LAUNCH((k_write<KM, OUT, EF>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
+            a.tasks, a.st_large, a.pre, a.cap_off, a.pairs, a.vals, a.idx_out, a.gid_base, a.step,
+            a.seed0, a.seed1);
+}
+
+void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st) {
+  if (km == KM_TOPK && out == OUT_PAIRS) {
+    ef ? select_compress_t<KM_TOPK, OUT_PAIRS, true>(a, st)
+       : select_compress_t<KM_TOPK, OUT_PAIRS, false>(a, st);
+  } else if (km == KM_RANDK && out == OUT_VALIDX) {
+    ef ? select_compress_t<KM_RANDK, OUT_VALIDX, true>(a, st)
+       : select_compress_t<KM_RANDK, OUT_VALIDX, false>(a, st);
+  } else if (km == KM_RANDK && out == OUT_PAIRS) {
+    ef ? select_compress_t<KM_RANDK, OUT_PAIRS, true>(a, st)
+       : select_compress_t<KM_RANDK, OUT_PAIRS, false>(a, st);
+  } else {
+    ef ? select_compress_t<KM_TOPK, OUT_VALIDX, true>(a, st)
+       : select_compress_t<KM_TOPK, OUT_VALIDX, false>(a, st);
+  }
+}
+
+void thresh_count(const SelectArgs& a, float V, int adaptive, bool ef, float* segmax,
+                  float2* partial, int32_t* count_out, hipStream_t st) {
+  if (adaptive) {
+    if (ef) LW_LAUNCH((k_partial<true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs, a.tasks, partial);
+    else LW_LAUNCH((k_partial<false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs, a.tasks, partial);
+    LW_LAUNCH(k_finalize, a.n_large, st, partial, a.task_lo, segmax, 0);
+  }
+  hipLaunchKernelGGL(k_thresh_state, dim3((a.n_large + NT - 1) / NT), dim3(NT), 0, st, a.st_large,
+                     (const float*)segmax, a.n_large, V, adaptive);
+  if (ef && !adaptive)
+    LW_LAUNCH((k_count<KM_THRESH, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.large_segs, a.tasks, a.st_large, a.cnt, 0u, 0u, 0u, 0u);
+  else
+    LW_LAUNCH((k_count<KM_THRESH, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.large_segs, a.tasks, a.st_large, a.cnt, 0u, 0u, 0u, 0u);
+  LW_LAUNCH((k_scan<KM_THRESH>), a.n_large, st, a.cnt, a.pre, a.task_lo, a.st_large, count_out);
+}
+
+void thresh_write(const SelectArgs& a, bool ef, hipStream_t st) {
+  hipLaunchKernelGGL(k_set_caps, dim3((a.n_large + NT - 1) / NT), dim3(NT), 0, st, a.st_large,
+                     a.cap_off, a.large_segs, a.n_large);
+  LW_LAUNCH(k_fill_tail, a.n_large, st, a.pairs, a.cap_off, a.large_segs, a.st_large);
+  if (ef)
+    LW_LAUNCH((k_write<KM_THRESH, OUT_PAIRS, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.large_segs, a.tasks, a.st_large, a.pre, a.cap_off, a.pairs, a.vals, a.idx_out, 0u,
+              0u, 0u, 0u);
+  else
+    LW_LAUNCH((k_write<KM_THRESH, OUT_PAIRS, false>), a.n_tasks, st, a.g, a.ef, a.seg_off,
+              a.seg_n, a.large_segs, a.tasks, a.st_large, a.pre, a.cap_off, a.pairs, a.vals,
+              a.idx_out, 0u, 0u, 0u, 0u);
+}
+
+void unpack_pairs(const int2* gathered, int64_t cap_total, int ws, float* g, const int64_t* seg_off,
+                  const int32_t* seg_n, const int64_t* cap_off, const int2* utasks, int n_utasks,
+                  hipStream_t st) {
+  if (n_utasks == 0) return;
+  LW_LAUNCH(k_unpack_pairs, n_utasks, st, gathered, cap_total, ws, g, seg_off, seg_n, cap_off,
+            utasks);
+}
+
+void unpack_validx(const float* vals, const int32_t* idx, const int32_t* slot_seg, int64_t nslots,
+                   int ws, float* g, const int64_t* seg_off, hipStream_t st) {
+  if (nslots == 0) return;
+  LW_LAUNCH(k_unpack_validx, (nslots + NT - 1) / NT, st, vals, idx, slot_seg, nslots, ws, g,
+            seg_off);
+}
+
+void seg_reduce(const QuantArgs& a, bool ef_add, int what, float* out, float2* partial,
+                hipStream_t st) {
+  if (ef_add) LW_LAUNCH((k_partial<true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks, partial);
+  else LW_LAUNCH((k_partial<false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks, partial);
+  LW_LAUNCH(k_finalize, a.nseg, st, partial, a.task_lo, out, what);
+}
+
+template <int Q>
+static void quant_t(const QuantArgs& a, bool ef, hipStream_t st) {
+  if (ef)
+    LW_LAUNCH((k_quant<Q, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks,
+              a.rec_off, a.scale, a.payload, a.nseg, a.qstates, a.gid_base, a.step, a.tag, a.seed0,
+              a.seed1);
+  else
+    LW_LAUNCH((k_quant<Q, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks,
+              a.rec_off, a.scale, a.payload, a.nseg, a.qstates, a.gid_base, a.step, a.tag, a.seed0,
+              a.seed1);
+}
+
+void quantize(const QuantArgs& a, int q, bool ef, hipStream_t st) {
+  switch (q) {
+    case Q_TERN: quant_t<Q_TERN>(a, ef, st); break;
+    case Q_QS8: quant_t<Q_QS8>(a, ef, st); break;
+    case Q_QS9: quant_t<Q_QS9>(a, ef, st); break;
+    default: quant_t<Q_QS16>(a, ef, st); break;
+  }
+}
+
+void dequantize(const QuantArgs& a, int q, const uint32_t* gathered, int64_t words_per_rank, int ws,
+                hipStream_t st) {
+  switch (q) {
+    case Q_TERN:
+      LW_LAUNCH(k_dequant<Q_TERN>, a.n_tasks, st, gathered, words_per_rank, ws, a.g, a.seg_off,
+                a.seg_n, a.segs, a.tasks, a.rec_off, a.nseg, a.qstates);
+      break;
+    case Q_QS8:
+      LW_LAUNCH(k_dequant<Q_QS8>, a.n_tasks, st, gathered, words_per_rank, ws, a.g, a.seg_off,
+                a.seg_n, a.segs, a.tasks, a.rec_off, a.nseg, a.qstates);
+      break;
+    case Q_QS9:
+      LW_LAUNCH(k_dequant<Q_QS9>, a.n_tasks, st, gathered, words_per_rank, ws, a.g, a.seg_off,
+                a.seg_n, a.segs, a.tasks, a.rec_off, a.nseg, a.qstates);
+      break;
+    default:
+      LW_LAUNCH(k_dequant<Q_QS16>, a.n_tasks, st, gathered, words_per_rank, ws, a.g, a.seg_off,
+                a.seg_n, a.segs, a.tasks, a.rec_off, a.nseg, a.qstates);
+      break;
+  }
+}
+
+}  // namespace lw

@@ -1,0 +1,108 @@
+// Host-visible launcher API of the layer_wise_aaai20_amd HIP kernels (gfx950).
+// Kernels take raw device pointers + a hipStream_t so they can be driven from the torch op
+// bindings (bindings.cpp) or from the native C++ runtime alike.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace lw {
+
+constexpr int kLargeEPB = 8192;    // elements per workgroup in multi-block passes
+constexpr int kSmallMax = 4096;    // segments up to this size use the single-workgroup path
+constexpr int kUnpackChunk = 4096; // elements per workgroup in the pair unpack
+constexpr int kMaxWorld = 64;
+
+enum KeyMode { KM_TOPK = 0, KM_RANDK = 1, KM_THRESH = 2 };
+enum OutMode { OUT_PAIRS = 0, OUT_VALIDX = 1 };
+enum QuantMode { Q_TERN = 0, Q_QS8 = 1, Q_QS9 = 2, Q_QS16 = 3 };
+
+__host__ __device__ constexpr int64_t hdr_words(int64_t nseg) { return (nseg + 3) / 4 * 4; }
+
+struct SelState {
+  uint32_t prefix;   // radix digits chosen so far
+  uint32_t m;        // rank of the wanted key inside the current prefix bucket (1-based)
+  uint32_t tkey;     // final threshold key
+  uint32_t quota;    // how many keys == tkey are emitted
+  uint32_t cnt_gt;   // keys > tkey in the segment
+  uint32_t total;    // emitted elements
+  uint32_t cap;      // payload slots of the segment
+  uint32_t pad;
+};
+
+struct SelectArgs {
+  float* g;                    // bucket base (fp32 gradient arena slice)
+  float* ef;                   // error-feedback residual (same layout) or nullptr
+  const int64_t* seg_off;      // [S+1] element offsets within the bucket
+  const int32_t* seg_n;        // [S]   true element counts
+  const int32_t* keep;         // [S]   m_s (Top-K / Random-K)
+  const int64_t* cap_off;      // [S+1] payload slot offsets
+  const int32_t* small_segs;   // [n_small]
+  const int32_t* large_segs;   // [n_large]
+  const int2* tasks;           // [n_tasks] (large index, begin)
+  const int32_t* task_lo;      // [n_large+1]
+  int n_small, n_large, n_tasks;
+  // scratch
+  uint32_t* hist;              // [n_large*4096]
+  SelState* st_small;          // [n_small]
+  SelState* st_large;          // [n_large]
+  uint2* cnt;                  // [n_tasks]
+  uint2* pre;                  // [n_tasks]
+  // outputs
+  int2* pairs;                 // OUT_PAIRS: [cap_total] (index, float bits)
+  float* vals;                 // OUT_VALIDX
+  int32_t* idx_out;            // OUT_VALIDX
+  // rng
+  uint32_t gid_base, step, seed0, seed1;
+};
+
+struct QuantArgs {
+  float* g;
+  float* ef;
+  const int64_t* seg_off;
+  const int32_t* seg_n;
+  const int32_t* segs;         // all segments (large path)
+  const int2* tasks;
+  const int32_t* task_lo;
+  const int64_t* rec_off;      // [S+1] group-record offsets (32 elements per group)
+  int nseg, n_tasks, qstates;
+  float* scale;                // [S] abs-max (TernGrad) or L2 norm (QSGD)
+  uint32_t* payload;           // this rank's send buffer
+  uint32_t gid_base, step, tag, seed0, seed1;
+};
+
+void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st);
+void thresh_count(const SelectArgs& a, float V, int adaptive, bool ef, float* segmax,
+                  float2* partial, int32_t* count_out, hipStream_t st);
+void thresh_write(const SelectArgs& a, bool ef, hipStream_t st);
+void unpack_pairs(const int2* gathered, int64_t cap_total, int ws, float* g, const int64_t* seg_off,
+                  const int32_t* seg_n, const int64_t* cap_off, const int2* utasks, int n_utasks,
+                  hipStream_t st);
+void unpack_validx(const float* vals, const int32_t* idx, const int32_t* slot_seg, int64_t nslots,
+                   int ws, float* g, const int64_t* seg_off, hipStream_t st);
+void seg_reduce(const QuantArgs& a, bool ef_add, int what, float* out, float2* partial,
+                hipStream_t st);
+void quantize(const QuantArgs& a, int q, bool ef, hipStream_t st);
+void dequantize(const QuantArgs& a, int q, const uint32_t* gathered, int64_t words_per_rank, int ws,
+                hipStream_t st);
+
+// optimizer (optim.hip)
+struct SgdArgs {
+  float* p;                    // flat param arena
+  const float* g;              // flat grad arena
+  float* buf;                  // flat momentum arena
+  const int64_t* seg_off;
+  const int32_t* seg_n;
+  const int32_t* segs;
+  const int2* tasks;
+  const float* seg_wd;         // [S] weight decay per segment
+  int n_tasks;
+  float lr, momentum, dampening, grad_scale;
+  int nesterov, first_step;
+};
+void sgd_step(const SgdArgs& a, hipStream_t st);
+
+// model-path elementwise (nn.hip)
+void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
+                  const float stdv[3], bool bf16, hipStream_t st);
+
+}  // namespace lw

@@ -1,0 +1,82 @@
+// Fused elementwise kernels on the model path (gfx950).
+//
+//  k_normalize_u8   uint8 NHWC images -> (x - mean[c]) / std[c] -> bf16/fp32 NHWC, i.e. the
+//                   channels_last layout the convolutions consume. Replaces the reference's
+//                   host-collated uint8 batch + `.cuda().half()` + `sub_/div_` chain
+//                   (IMAGENET/training/dataloader.py:81-93) with one pass:
+//                   16 input bytes per lane (one dwordx4 load), two or four 16-B stores.
+#include "common.h"
+#include "lw_kernels.h"
+#include <hip/hip_bf16.h>
+
+namespace lw {
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // round-to-nearest-even (finite inputs only: normalised pixels)
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void k_normalize_u8(const uint8_t* __restrict__ in,
+                                                      void* __restrict__ out, int64_t nbytes,
+                                                      float m0, float m1, float m2, float r0,
+                                                      float r1, float r2) {
+  const int64_t chunk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t base = chunk * 16;
+  if (base >= nbytes) return;
+  const float mean[3] = {m0, m1, m2};
+  const float rstd[3] = {r0, r1, r2};
+  uint8_t b[16];
+  if (base + 16 <= nbytes) {
+    const uint4 v = *reinterpret_cast<const uint4*>(in + base);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) b[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  } else {
+    for (int k = 0; k < 16; ++k) b[k] = base + k < nbytes ? in[base + k] : 0;
+  }
+  const int c0 = (int)(base % 3);
+  float y[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = (c0 + k) % 3;
+    y[k] = ((float)b[k] - mean[c]) * rstd[c];
+  }
+  if (BF16) {
+    uint16_t* o = reinterpret_cast<uint16_t*>(out) + base;
+    if (base + 16 <= nbytes) {
+      uint32_t p[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) p[k] = (uint32_t)f2bf(y[2 * k]) | ((uint32_t)f2bf(y[2 * k + 1]) << 16);
+      reinterpret_cast<uint4*>(o)[0] = make_uint4(p[0], p[1], p[2], p[3]);
+      reinterpret_cast<uint4*>(o)[1] = make_uint4(p[4], p[5], p[6], p[7]);
+    } else {
+      for (int k = 0; k < 16 && base + k < nbytes; ++k) o[k] = f2bf(y[k]);
+    }
+  } else {
+    float* o = reinterpret_cast<float*>(out) + base;
+    if (base + 16 <= nbytes) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        reinterpret_cast<float4*>(o)[q] = make_float4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]);
+    } else {
+      for (int k = 0; k < 16 && base + k < nbytes; ++k) o[k] = y[k];
+    }
+  }
+}
+
+void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
+                  const float stdv[3], bool bf16, hipStream_t st) {
+  const int64_t chunks = (nbytes + 15) / 16;
+  const dim3 grid((unsigned)((chunks + 255) / 256)), block(256);
+  if (bf16)
+    hipLaunchKernelGGL(k_normalize_u8<true>, grid, block, 0, st, in, out, nbytes, mean[0], mean[1],
+                       mean[2], 1.f / stdv[0], 1.f / stdv[1], 1.f / stdv[2]);
+  else
+    hipLaunchKernelGGL(k_normalize_u8<false>, grid, block, 0, st, in, out, nbytes, mean[0], mean[1],
+                       mean[2], 1.f / stdv[0], 1.f / stdv[1], 1.f / stdv[2]);
+}
+
+}  // namespace lw

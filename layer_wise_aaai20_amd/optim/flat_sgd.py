@@ -1,0 +1,120 @@
+"""Fused SGD over the flat parameter / gradient arenas (one HIP launch per step).
+
+Drop-in for the ``torch.optim.SGD`` the reference builds in both workloads
+(``CIFAR10/torch_backend.py:142-143``, ``IMAGENET/training/train_imagenet_nv.py:188-191``):
+same hyper-parameters, same param-group API (the LR ``Scheduler`` writes ``param_groups[i]['lr']``,
+``--no-bn-wd`` gives BN parameters their own ``weight_decay=0`` group, ``experimental_utils.py``),
+and a ``state_dict`` in torch.optim.SGD's format, so checkpoints stay compatible
+(``train_imagenet_nv.py:663-669``). Internally every momentum buffer is a view into one flat buffer
+laid out like the parameter arena, and the update (grad unscale, weight decay, momentum,
+Nesterov) is one kernel (``csrc/optim.hip``).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+from torch.optim import Optimizer
+
+from ..compress.plan import SegPlan
+from ..parallel.arena import _dense_strided_view
+from ..ops._ext import ops_for
+
+
+class FlatSGD(Optimizer):
+    def __init__(self, params, arena, lr: float = 0.0, momentum: float = 0.0,
+                 dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
+                 grad_scale: float = 1.0):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov)
+        super().__init__(params, defaults)
+        self.arena = arena
+        if arena.param_buf is None:
+            raise ValueError("FlatSGD needs an arena built with flat_params=True")
+        self.grad_scale = grad_scale
+        segs = arena.segments
+        self._seg_of = {id(s.param): s.index for s in segs}
+        for g in self.param_groups:
+            for p in g["params"]:
+                if id(p) not in self._seg_of:
+                    raise ValueError("every optimised parameter must live in the arena")
+        self.plan = SegPlan([s.offset for s in segs], [s.numel for s in segs])
+        self.buf = torch.zeros_like(arena.param_buf)
+        self._first = True
+        self._wd_cache = None
+
+    # torch.optim.SGD-compatible state: momentum_buffer views into the flat buffer
+    def _bind_state(self):
+        for g in self.param_groups:
+            if g["momentum"] == 0:
+                continue
+            for p in g["params"]:
+                s = self.arena.segments[self._seg_of[id(p)]]
+                self.state[p]["momentum_buffer"] = _dense_strided_view(self.buf, s.offset, p)
+
+    def _seg_wd(self, device):
+        key = tuple(float(g["weight_decay"]) for g in self.param_groups)
+        if self._wd_cache is None or self._wd_cache[0] != key:
+            wd = np.zeros(len(self.arena.segments), dtype=np.float32)
+            for g in self.param_groups:
+                for p in g["params"]:
+                    wd[self._seg_of[id(p)]] = g["weight_decay"]
+            self._wd_cache = (key, torch.from_numpy(wd).to(device))
+        return self._wd_cache[1]
+
+    def _uniform(self, k):
+        vals = {g[k] for g in self.param_groups}
+        if len(vals) != 1:
+            raise ValueError(f"FlatSGD needs a single {k} across param groups, got {vals}")
+        return vals.pop()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        lr = float(self._uniform("lr"))
+        mom = float(self._uniform("momentum"))
+        damp = float(self._uniform("dampening"))
+        nest = bool(self._uniform("nesterov"))
+        p, g = self.arena.param_buf, self.arena.grad
+        lib = ops_for(p)
+        wd = self._seg_wd(p.device)
+        if lib is not None:
+            t = self.plan.all_large_tables(p.device)
+            lib.sgd_step(p, g, self.buf, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], wd, lr,
+                         mom, damp, int(nest), int(self._first), float(self.grad_scale))
+        else:
+            wdv = torch.repeat_interleave(
+                wd, torch.from_numpy(np.diff(np.append(self.plan.offsets, self.arena.numel))))
+            d = g * self.grad_scale + wdv * p
+            if mom != 0:
+                if self._first:
+                    self.buf.copy_(d)
+                else:
+                    self.buf.mul_(mom).add_(d, alpha=1 - damp)
+                d = d + mom * self.buf if nest else self.buf
+            p.add_(d, alpha=-lr)
+        if self._first and mom != 0:
+            self._bind_state()
+        self._first = False
+        return loss
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.arena.zero_()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        any_buf = False
+        for g in self.param_groups:
+            for p in g["params"]:
+                st = self.state.get(p, {})
+                b = st.get("momentum_buffer")
+                if b is not None:
+                    s = self.arena.segments[self._seg_of[id(p)]]
+                    _dense_strided_view(self.buf, s.offset, p).copy_(b)
+                    any_buf = True
+        self._first = not any_buf
+        if any_buf:
+            self._bind_state()

@@ -1,0 +1,103 @@
+"""Collective helpers over ``torch.distributed`` (RCCL on GPU via the "nccl" backend, gloo on CPU).
+
+The reference issues one *blocking* collective per parameter tensor (``CIFAR10/core.py:218``,
+``train_imagenet_nv.py:298, 385``). Here every collective is asynchronous on
+the backend's own stream and operates on a whole bucket; the caller keeps the handle and
+``wait()``s it only when the result is consumed, which on RCCL makes the *compute stream* wait on an
+event rather than blocking the host.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+def is_dist() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def world_size(group=None) -> int:
+    return dist.get_world_size(group) if is_dist() else 1
+
+
+def rank(group=None) -> int:
+    return dist.get_rank(group) if is_dist() else 0
+
+
+def env_world_size() -> int:
+    """``dist_utils.env_world_size`` (IMAGENET/training/dist_utils.py:27), defaulting to 1."""
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def env_rank() -> int:
+    return int(os.environ.get("RANK", "0"))
+
+
+class _Done:
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+def all_reduce(t: torch.Tensor, group=None, async_op: bool = True, op=None):
+    if not is_dist() or world_size(group) == 1 and t.device.type == "cpu":
+        return _Done()
+    op = op if op is not None else dist.ReduceOp.SUM
+    return dist.all_reduce(t, op=op, group=group, async_op=async_op) or _Done()
+
+
+def all_gather(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool = True):
+    if not is_dist() or world_size(group) == 1 and inp.device.type == "cpu":
+        out.copy_(inp)
+        return _Done()
+    return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op) or _Done()
+
+
+def all_reduce_max(t: torch.Tensor, group=None) -> torch.Tensor:
+    if is_dist() and world_size(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t
+
+
+def broadcast_coalesced(tensors, src: int = 0, group=None) -> None:
+    """Broadcast a list of tensors from ``src`` as one flat message per dtype (replaces the private
+    ``dist._dist_broadcast_coalesced`` of ``ddp.py:193, 374-377``)."""
+    if not is_dist() or world_size(group) == 1 or not tensors:
+        return
+    by_dtype = {}
+    for t in tensors:
+        by_dtype.setdefault((t.dtype, t.device), []).append(t)
+    for (_, _), ts in by_dtype.items():
+        flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        dist.broadcast(flat, src=src, group=group)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
+
+
+def sum_tensor(tensor: torch.Tensor, group=None) -> torch.Tensor:
+    """``dist_utils.sum_tensor`` (dist_utils.py:23-26)."""
+    rt = tensor.clone()
+    if is_dist():
+        dist.all_reduce(rt, op=dist.ReduceOp.SUM, group=group)
+    return rt
+
+
+def reduce_tensor(tensor: torch.Tensor, group=None) -> torch.Tensor:
+    return sum_tensor(tensor, group) / world_size(group)
+
+
+def barrier(group=None, device=None) -> None:
+    if is_dist():
+        if device is not None and torch.device(device).type == "cuda":
+            dist.barrier(group=group, device_ids=[torch.device(device).index or 0])
+        else:
+            dist.barrier(group=group)

@@ -1,0 +1,134 @@
+"""Data-parallel wrappers built on :class:`GradSyncEngine`.
+
+* :class:`CompressedDDP` — bucketed, backward-overlapped DP with any of the reference compressors
+  in layer-wise or entire-model mode, optional error feedback for every method.
+* :func:`DistributedDataParallel` — the uncompressed bucketed DDP (DP-3, the vendored
+  ``IMAGENET/training/ddp.py:19-489``).
+* :func:`RandomKSparsifiedDDP` — shared-seed Random-K with error feedback and index-free payloads
+  (DP-4, ``IMAGENET/training/sparsified_ddp.py:20-495``).
+
+Start-up: module state (parameters AND buffers) is broadcast from rank 0, as in ``ddp.py:190-194``;
+unlike the reference's CIFAR path every mode starts from identical replicas.
+Buffers (BatchNorm running statistics) are re-broadcast before each training forward when
+``broadcast_buffers`` is set (``ddp.py:361-386``), as one coalesced message.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+
+from . import comm
+from .engine import GradSyncEngine
+
+
+class CompressedDDP(nn.Module):
+    def __init__(self, module: nn.Module, compress: str = "layerwise", method="Topk", K=0.001,
+                 V=1e-3, qstates=255, error_feedback: bool = False, bucket_cap_mb: float = 25.0,
+                 first_bucket_mb: Optional[float] = None, process_group=None,
+                 broadcast_buffers: bool = True, wire: str = "auto", seed: int = 2147483647,
+                 flat_params: bool = True, check_reduction: bool = True, device_ids=None,
+                 output_device=None, dim: int = 0):
+        super().__init__()
+        self.module = module
+        self.process_group = process_group
+        self.broadcast_buffers = broadcast_buffers
+        self.check_reduction = check_reduction
+        self.dim = dim
+        if device_ids is not None and len(device_ids) > 1:
+            raise RuntimeError("one process per GPU: pass at most one device id")
+        # identical replicas and an agreed RNG seed on every rank
+        comm.broadcast_coalesced(list(module.state_dict().values()), 0, process_group)
+        if comm.is_dist() and comm.world_size(process_group) > 1:
+            s = torch.tensor([seed], dtype=torch.int64,
+                             device=next(module.parameters()).device)
+            comm.broadcast_coalesced([s], 0, process_group)
+            seed = int(s.item())
+        self.engine = GradSyncEngine(module.named_parameters(), mode=compress, method=method, K=K,
+                                     V=V, qstates=qstates, error_feedback=error_feedback,
+                                     bucket_cap_mb=bucket_cap_mb,
+                                     first_bucket_mb=first_bucket_mb, wire=wire, seed=seed,
+                                     process_group=process_group, flat_params=flat_params)
+        self._buffers_list = [b for b in module.buffers() if b.is_floating_point() or
+                              b.dtype in (torch.int64, torch.int32)]
+        self._hooks = []
+        self._register_hooks()
+        self._callback_queued = False
+
+    # ------------------------------------------------------------------ hooks
+    def _register_hooks(self) -> None:
+        for seg in self.engine.arena.segments:
+            p = seg.param
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(seg.index)))
+
+    def _make_hook(self, seg_index: int):
+        engine = self.engine
+        arena = engine.arena
+        seg = arena.segments[seg_index]
+
+        def hook(p):
+            v = arena.grad_view(seg)
+            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
+                # someone replaced .grad (e.g. zero_grad(set_to_none=True)): fold it back in
+                if p.grad is not None:
+                    v.copy_(p.grad)
+                p.grad = v
+            if not self._callback_queued:
+                self._callback_queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+            engine.mark_ready(seg_index)
+        return hook
+
+    def _finish(self) -> None:
+        self._callback_queued = False
+        self.engine.finish()
+
+    # ------------------------------------------------------------------ module API
+    def forward(self, *inputs, **kwargs):
+        if not self.training:
+            return self.module(*inputs, **kwargs)
+        if self.check_reduction and self.engine._active:
+            raise RuntimeError("Not all gradients have been reduced from the backward of the "
+                               "previous iteration (ddp.py:312-327 check_reduction).")
+        if self.broadcast_buffers and self._buffers_list:
+            comm.broadcast_coalesced(self._buffers_list, 0, self.process_group)
+        self.engine.begin_step()
+        return self.module(*inputs, **kwargs)
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        """Keep ``.grad`` as arena views: zeroing means clearing the arena."""
+        self.engine.begin_step()
+
+    @property
+    def arena(self):
+        return self.engine.arena
+
+    def sync_stats(self):
+        return self.engine.stats
+
+    def extra_repr(self) -> str:
+        return self.engine.describe()
+
+
+def DistributedDataParallel(module, device_ids=None, output_device=None, dim=0,
+                            broadcast_buffers=True, process_group=None, bucket_cap_mb=25,
+                            check_reduction=False, **kw) -> CompressedDDP:
+    """Uncompressed bucketed DDP (DP-3): reverse-order 25 MB buckets, overlapped all-reduce."""
+    return CompressedDDP(module, compress="none", method="none", bucket_cap_mb=bucket_cap_mb,
+                         process_group=process_group, broadcast_buffers=broadcast_buffers,
+                         check_reduction=check_reduction, device_ids=device_ids, **kw)
+
+
+def RandomKSparsifiedDDP(module, device_ids=None, output_device=None, dim=0,
+                         broadcast_buffers=True, process_group=None, bucket_cap_mb=25,
+                         check_reduction=False, randk=1, seed=2147483647, **kw) -> CompressedDDP:
+    """Shared-seed Random-K with error feedback, index-free payloads (DP-4)."""
+    if randk >= 1:
+        return DistributedDataParallel(module, device_ids, output_device, dim, broadcast_buffers,
+                                       process_group, bucket_cap_mb, check_reduction, **kw)
+    return CompressedDDP(module, compress="layerwise", method="Randomk", K=randk,
+                         error_feedback=True, bucket_cap_mb=bucket_cap_mb, seed=seed,
+                         process_group=process_group, broadcast_buffers=broadcast_buffers,
+                         check_reduction=check_reduction, device_ids=device_ids, wire="indexfree",
+                         **kw)

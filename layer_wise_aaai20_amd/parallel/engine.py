@@ -1,0 +1,185 @@
+"""Gradient synchronisation engine: arena + buckets + codecs + async collectives.
+
+One engine drives both entry styles of the reference:
+
+* **hook-driven, overlapped with backward** — what ``CompressedDDP`` uses. Each parameter's
+  post-accumulate-grad hook marks its segment ready; when every segment of a bucket is ready the
+  bucket is compressed and its collective launched asynchronously, strictly in bucket order so all
+  ranks issue collectives identically (the reference's reverse-order ``next_bucket`` rule,
+  ``ddp.py:434-450``, ``sparsified_ddp.py:424-445``). A callback queued on the autograd engine
+  finishes the step: launch leftovers, wait, decompress.
+* **after backward** — the reference's functional ``layerwise_compressed_comm`` /
+  ``entiremodel_compressed_comm`` / ``all_reduce`` (``CIFAR10/core.py:175-301``,
+  ``train_imagenet_nv.py:382-386``): :meth:`sync_now` launches every bucket, then finishes.
+
+Both end with ``param.grad`` = mean over ranks of each rank's compressed gradient, written into the
+flat arena. No gradient is ever reduced twice.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import comm
+from .arena import Bucket, GradArena, plan_buckets
+from ..compress import reference as ref
+from ..compress.codecs import Codec, DenseCodec, make_codec
+from ..compress.plan import SegPlan
+
+MODES = ("layerwise", "entiremodel", "none")
+MODE_ALIASES = {"enitremodel": "entiremodel", "entire": "entiremodel", "entire-model": "entiremodel",
+                "layer-wise": "layerwise", "layer": "layerwise", None: "none", "": "none",
+                "None": "none"}
+
+
+def canonical_mode(mode) -> str:
+    mode = MODE_ALIASES.get(mode, mode)
+    if mode not in MODES:
+        raise ValueError(f"unknown --compress mode {mode!r}; expected one of {MODES}")
+    return mode
+
+
+@dataclass
+class SyncStats:
+    steps: int = 0
+    payload_bytes: int = 0          # bytes this rank sent last step
+    dense_bytes: int = 0            # fp32 gradient bytes (what an uncompressed all-reduce moves)
+    buckets: int = 0
+    history: List[float] = field(default_factory=list)
+
+    @property
+    def ratio(self) -> float:
+        return self.payload_bytes / max(self.dense_bytes, 1)
+
+
+class GradSyncEngine:
+    def __init__(self, named_params, mode: str = "layerwise", method="none", K=None, V=None,
+                 qstates=None, error_feedback: bool = False, bucket_cap_mb: float = 25.0,
+                 first_bucket_mb: Optional[float] = None, wire: str = "auto",
+                 seed: int = 2147483647, process_group=None, flat_params: bool = False,
+                 world_size: Optional[int] = None):
+        self.mode = canonical_mode(mode)
+        self.method = ref.canonical_method(method) if self.mode != "none" else "none"
+        self.pg = process_group
+        self.world = world_size or comm.world_size(self.pg)
+        self.rank = comm.rank(self.pg)
+        named = list(named_params)
+        align = 1 if self.mode == "entiremodel" else 64
+        self.arena = GradArena(named, flat_params=flat_params, align=align)
+        self.device = self.arena.device
+        cap = int(bucket_cap_mb * 2 ** 20)
+        first = int(first_bucket_mb * 2 ** 20) if first_bucket_mb else None
+        self.buckets: List[Bucket] = plan_buckets(self.arena, self.mode, cap, first)
+        self.seed = int(seed)
+        self.ef = torch.zeros_like(self.arena.grad) if (error_feedback and
+                                                       self.method != "none") else None
+        self.codecs: List[Codec] = []
+        self.plans: List[SegPlan] = []
+        for b in self.buckets:
+            segs = self.arena.segments[b.seg_lo:b.seg_hi]
+            if self.mode == "entiremodel":
+                plan = SegPlan([0], [self.arena.numel], gid_base=0)
+            else:
+                plan = SegPlan([s.offset - b.start for s in segs], [s.numel for s in segs],
+                               gid_base=b.seg_lo)
+            self.plans.append(plan)
+            self.codecs.append(make_codec(self.method, plan, self.world, self.rank, K=K, V=V,
+                                          qstates=qstates, seed=self.seed,
+                                          error_feedback=self.ef is not None, wire=wire,
+                                          count_exchange=self._count_exchange))
+        self.seg_bucket = [0] * len(self.arena.segments)
+        for b in self.buckets:
+            for i in range(b.seg_lo, b.seg_hi):
+                self.seg_bucket[i] = b.index
+        self.step = 0
+        self.stats = SyncStats(dense_bytes=self.arena.numel * 4, buckets=len(self.buckets))
+        self._reset_state()
+        self.all_reduced_last = True
+
+    # ----------------------------------------------------------------- state machine
+    def _reset_state(self):
+        nb = len(self.buckets)
+        self._ready_cnt = [0] * nb
+        self._ready = [False] * nb
+        self._next = 0
+        self._pending = []
+        self._active = False
+        self._payload = 0
+
+    def _count_exchange(self, caps: torch.Tensor) -> torch.Tensor:
+        return comm.all_reduce_max(caps, self.pg)
+
+    def begin_step(self) -> None:
+        """Zero the arena and re-point ``.grad`` at it (called before forward/backward)."""
+        self.arena.zero_()
+        if not self.arena.grads_attached():
+            self.arena.attach_grads()
+        self._reset_state()
+
+    def mark_ready(self, seg_index: int) -> None:
+        self._active = True
+        b = self.seg_bucket[seg_index]
+        self._ready_cnt[b] += 1
+        n = self.buckets[b].seg_hi - self.buckets[b].seg_lo
+        if self._ready_cnt[b] == n:
+            self._ready[b] = True
+            self._launch_in_order()
+
+    def _launch_in_order(self) -> None:
+        while self._next < len(self.buckets) and self._ready[self._next]:
+            self._launch(self._next)
+            self._next += 1
+
+    def _launch(self, bi: int) -> None:
+        b = self.buckets[bi]
+        codec = self.codecs[bi]
+        g = self.arena.grad[b.start:b.end]
+        e = self.ef[b.start:b.end] if self.ef is not None else None
+        send = codec.compress(g, e, self.step)
+        self._payload += codec.last_payload_bytes
+        if codec.collective == "all_reduce":
+            work = comm.all_reduce(send, self.pg)
+            recv = None
+        else:
+            recv = codec.recv_buffer(send)
+            work = comm.all_gather(recv, send, self.pg)
+        self._pending.append((bi, work, send, recv))
+
+    def finish(self) -> None:
+        """Launch buckets that never became ready (unused params keep zero grads), wait for every
+        collective and decode into the arena."""
+        for i in range(self._next, len(self.buckets)):
+            self._ready[i] = True
+        self._launch_in_order()
+        for bi, work, send, recv in self._pending:
+            work.wait()
+            b = self.buckets[bi]
+            self.codecs[bi].decompress(send, recv, self.arena.grad[b.start:b.end])
+        self._pending = []
+        self.step += 1
+        self.stats.steps += 1
+        self.stats.payload_bytes = self._payload
+        self._active = False
+        self.all_reduced_last = True
+
+    def sync_now(self) -> None:
+        """Post-backward path: copy any foreign ``.grad`` into the arena, then sync every bucket."""
+        self.arena.gather_grads()
+        self._reset_state()
+        for i in range(len(self.buckets)):
+            self._ready[i] = True
+        self._launch_in_order()
+        self.finish()
+
+    # ----------------------------------------------------------------- introspection
+    def describe(self) -> str:
+        cs = {}
+        for c in self.codecs:
+            cs[c.name] = cs.get(c.name, 0) + 1
+        return (f"GradSyncEngine(mode={self.mode}, method={self.method}, world={self.world}, "
+                f"buckets={len(self.buckets)}, codecs={cs}, ef={self.ef is not None}, "
+                f"{self.arena})")

@@ -1,0 +1,103 @@
+"""ImageNet training engine (ResNet family): the step used by ``bench.py`` and by the
+reference-compatible entry point ``IMAGENET/training/train_imagenet_nv.py``.
+
+Reference step (``IMAGENET/training/train_imagenet_nv.py:388-441``): LR update → forward →
+cross-entropy → (fp16: ×loss_scale) → backward → per-layer compressed all-reduce → master-weight
+SGD. Here the same step is: fused uint8→bf16 NHWC normalise → bf16-autocast channels_last forward →
+backward with bucketed compression overlapped (CompressedDDP) → one fused SGD launch.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+
+from ..models import resnet as resnet_models
+from ..ops import nn as lwnn
+from ..optim.flat_sgd import FlatSGD
+from ..parallel.ddp import CompressedDDP
+
+IMAGENET_MEAN = (0.485 * 255, 0.456 * 255, 0.406 * 255)
+IMAGENET_STD = (0.229 * 255, 0.224 * 255, 0.225 * 255)
+
+
+def bn_param_groups(model: nn.Module, weight_decay: float, no_bn_wd: bool):
+    """Two groups with BN parameters excluded from weight decay (``experimental_utils.py:5-22``),
+    done on the module itself so the fp32 path keeps every parameter (fixes SURVEY.md D12)."""
+    if not no_bn_wd:
+        return [{"params": [p for p in model.parameters() if p.requires_grad],
+                 "weight_decay": weight_decay}]
+    bn_ids = set()
+    for m in model.modules():
+        if isinstance(m, nn.modules.batchnorm._BatchNorm):
+            bn_ids.update(id(p) for p in m.parameters())
+    bn, rest = [], []
+    for p in model.parameters():
+        if p.requires_grad:
+            (bn if id(p) in bn_ids else rest).append(p)
+    return [{"params": bn, "weight_decay": 0.0}, {"params": rest, "weight_decay": weight_decay}]
+
+
+class ImageNetTrainer:
+    def __init__(self, ddp: CompressedDDP, optimizer, device, dtype=torch.bfloat16,
+                 criterion: Optional[nn.Module] = None, channels_last: bool = True):
+        self.ddp = ddp
+        self.opt = optimizer
+        self.device = device
+        self.dtype = dtype
+        self.channels_last = channels_last
+        self.criterion = criterion or nn.CrossEntropyLoss()
+        self.mean = torch.tensor(IMAGENET_MEAN, device=device, dtype=torch.float32)
+        self.std = torch.tensor(IMAGENET_STD, device=device, dtype=torch.float32)
+        self._last = None
+
+    def normalize(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
+        return lwnn.normalize_nhwc_u8(images_u8_nhwc, self.mean, self.std, self.dtype)
+
+    def forward_loss(self, x, target):
+        with torch.autocast(device_type=self.device.type, dtype=self.dtype,
+                            enabled=self.dtype != torch.float32):
+            out = self.ddp(x)
+            loss = self.criterion(out.float(), target)
+        return out, loss
+
+    def step(self, images_u8_nhwc: torch.Tensor, target: torch.Tensor):
+        x = self.normalize(images_u8_nhwc)
+        out, loss = self.forward_loss(x, target)
+        loss.backward()
+        self.opt.step()
+        self._last = (out.detach(), target, loss.detach())
+        return loss
+
+    def last_top1(self) -> Optional[float]:
+        if self._last is None:
+            return None
+        out, target, _ = self._last
+        return float((out.argmax(1) == target).float().mean().item() * 100.0)
+
+
+def build_model(name: str = "resnet50", bn0: bool = False) -> nn.Module:
+    return getattr(resnet_models, name)(bn0=bn0)
+
+
+def build_trainer(model="resnet50", device=None, compress="layerwise", method="Topk", K=0.001,
+                  V=1e-3, qstates=255, error_feedback=False, bucket_cap_mb=25.0, dtype="bf16",
+                  fused=True, momentum=0.9, weight_decay=1e-4, no_bn_wd=True, lr=0.1,
+                  bn0=True, wire="auto") -> ImageNetTrainer:
+    device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    net = build_model(model, bn0=bn0) if isinstance(model, str) else model
+    if fused:
+        lwnn.fuse_resnet(net)
+    net = net.to(device)
+    if device.type == "cuda":
+        net = net.to(memory_format=torch.channels_last)
+    ddp = CompressedDDP(net, compress=compress, method=method, K=K, V=V, qstates=qstates,
+                        error_feedback=error_feedback, bucket_cap_mb=bucket_cap_mb, wire=wire,
+                        flat_params=True)
+    groups = bn_param_groups(net, weight_decay, no_bn_wd)
+    opt = FlatSGD(groups, ddp.arena, lr=lr, momentum=momentum, nesterov=momentum > 0,
+                  weight_decay=weight_decay)
+    tdtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype] \
+        if isinstance(dtype, str) else dtype
+    return ImageNetTrainer(ddp, opt, device, tdtype)

@@ -1,0 +1,202 @@
+"""HIP kernels vs the CPU (torch/numpy) mirror implementation and vs the reference oracles.
+
+Selection (Top-K, Random-K, thresholds) and TernGrad packing must be bit-identical between the
+GPU kernels and the CPU path; QSGD is compared to tolerance because the L2 norm is summed in a
+different order.
+"""
+import numpy as np
+import pytest
+import torch
+
+from layer_wise_aaai20_amd.compress import codecs
+from layer_wise_aaai20_amd.compress import reference as ref
+from layer_wise_aaai20_amd.compress.plan import SegPlan
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [64, 3, 1000, 4096, 4097, 9408, 65536, 147456, 1000, 2359296 // 4]
+
+
+def make_plan(sizes, align=64):
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += (n + align - 1) // align * align
+    return SegPlan(offs, sizes), o
+
+
+def rand_grad(n, seed=0, scale=1e-2):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, generator=g) * scale
+
+
+@pytest.mark.parametrize("K", [0.001, 0.01, 0.25])
+@pytest.mark.parametrize("ef", [False, True])
+def test_topk_gpu_matches_cpu(K, ef):
+    plan, N = make_plan(SIZES)
+    x = rand_grad(N, 1)
+    e = rand_grad(N, 2, 1e-3) if ef else None
+    cc, cg = codecs.TopkCodec(plan, 1, 0, K), codecs.TopkCodec(plan, 1, 0, K)
+    xc, ec = x.clone(), (e.clone() if ef else None)
+    pc = cc.compress(xc, ec, 0).clone()
+    xg, eg = x.cuda(), (e.cuda() if ef else None)
+    pg = cg.compress(xg, eg, 0).cpu()
+    assert torch.equal(pc, pg)
+    if ef:
+        torch.testing.assert_close(ec, eg.cpu(), rtol=0, atol=0)
+    # decoded == reference oracle on g + e
+    out = torch.zeros(N, device="cuda")
+    cg.decompress(pg.cuda(), None, out, world=1)
+    out = out.cpu()
+    base = x + e if ef else x
+    for s in range(plan.S):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        assert torch.equal(out[o:o + n], ref.topk(base[o:o + n], K)), s
+
+
+def test_topk_ties_and_zeros():
+    plan, N = make_plan([5000, 200, 20000])
+    x = torch.zeros(N)
+    x[:3000] = 1.0          # heavy ties at the threshold
+    x[3000:3010] = 2.0
+    x[5120:5130] = torch.arange(10).float()
+    cc, cg = codecs.TopkCodec(plan, 1, 0, 0.01), codecs.TopkCodec(plan, 1, 0, 0.01)
+    pc = cc.compress(x.clone(), None, 0).clone()
+    pg = cg.compress(x.cuda(), None, 0).cpu()
+    assert torch.equal(pc, pg)
+
+
+@pytest.mark.parametrize("K", [0.001, 0.05])
+@pytest.mark.parametrize("ef", [False, True])
+def test_randk_gpu_matches_cpu(K, ef):
+    plan, N = make_plan(SIZES)
+    x = rand_grad(N, 3)
+    e = rand_grad(N, 4, 1e-3) if ef else None
+    cc = codecs.RandkCodec(plan, 1, 0, K, seed=77)
+    cg = codecs.RandkCodec(plan, 1, 0, K, seed=77)
+    ec = e.clone() if ef else None
+    vc = cc.compress(x.clone(), ec, 9).clone()
+    eg = e.cuda() if ef else None
+    vg = cg.compress(x.cuda(), eg, 9).cpu()
+    assert torch.equal(cc._idx["cpu"], cg._idx["cuda:0"].cpu())
+    assert torch.equal(vc, vg)
+    if ef:
+        assert torch.equal(ec, eg.cpu())
+    out = torch.zeros(N, device="cuda")
+    cg.decompress(vg.cuda(), None, out, world=1)
+    for s in range(plan.S):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        assert int((out[o:o + n] != 0).sum()) <= ref.randomk_keep_count(n, K)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_unpack_pairs_rank_ordered(world):
+    plan, N = make_plan(SIZES)
+    c = codecs.TopkCodec(plan, world, 0, 0.01)
+    payloads = []
+    for r in range(world):
+        payloads.append(codecs.TopkCodec(plan, 1, 0, 0.01).compress(rand_grad(N, 10 + r), None, 0)
+                        .clone())
+    gathered = torch.cat(payloads)
+    oc = torch.zeros(N)
+    c.unpack_pairs_cpu(gathered, world, oc, c.cap_off)
+    og = torch.zeros(N, device="cuda")
+    c.decompress(None, gathered.cuda(), og, world=world)
+    assert torch.equal(oc, og.cpu())
+
+
+def test_terngrad_bitwise():
+    plan, N = make_plan(SIZES)
+    x = rand_grad(N, 5)
+    cc = codecs.TernGradCodec(plan, 1, 3, seed=11)
+    cg = codecs.TernGradCodec(plan, 1, 3, seed=11)
+    pc = cc.compress(x.clone(), None, 2).clone()
+    pg = cg.compress(x.cuda(), None, 2).cpu()
+    assert torch.equal(pc, pg)
+    oc = torch.zeros(N)
+    og = torch.zeros(N, device="cuda")
+    cc.decompress(None, torch.cat([pc, pc]), oc, world=2)
+    cg.decompress(None, torch.cat([pg, pg]).cuda(), og, world=2)
+    torch.testing.assert_close(oc, og.cpu())
+
+
+@pytest.mark.parametrize("qstates", [127, 255, 1000])
+def test_qsgd_close(qstates):
+    plan, N = make_plan(SIZES)
+    x = rand_grad(N, 6)
+    cc = codecs.QSGDCodec(plan, 1, 0, qstates, seed=5)
+    cg = codecs.QSGDCodec(plan, 1, 0, qstates, seed=5)
+    e_c, e_g = torch.zeros(N), torch.zeros(N, device="cuda")
+    pc = cc.compress(x.clone(), e_c, 1).clone()
+    pg = cg.compress(x.cuda(), e_g, 1).cpu()
+    hdr = cc.hdr
+    torch.testing.assert_close(pc[:plan.S].view(torch.float32), pg[:plan.S].view(torch.float32),
+                               rtol=1e-5, atol=0)
+    mism = (pc[hdr:] != pg[hdr:]).float().mean().item()
+    assert mism < 2e-3, mism
+    og = torch.zeros(N, device="cuda")
+    cg.decompress(pg.cuda(), None, og, world=1)
+    # EF identity: decoded + residual == input
+    torch.testing.assert_close(og + e_g, x.cuda(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_threshold_gpu_matches_cpu(adaptive):
+    plan, N = make_plan(SIZES)
+    x = rand_grad(N, 7)
+    kw = dict(adaptive=True) if adaptive else dict(V=0.02)
+    cc = codecs.ThresholdCodec(plan, 1, 0, **kw)
+    cg = codecs.ThresholdCodec(plan, 1, 0, **kw)
+    pc = cc.compress(x.clone(), None, 0).clone()
+    pg = cg.compress(x.cuda(), None, 0).cpu()
+    assert torch.equal(pc, pg)
+
+
+def test_flat_sgd_matches_torch():
+    from layer_wise_aaai20_amd.optim.flat_sgd import FlatSGD
+    from layer_wise_aaai20_amd.parallel.arena import GradArena
+    torch.manual_seed(0)
+    m1 = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8),
+                             torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 10)).cuda()
+    m2 = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8),
+                             torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 10)).cuda()
+    m2.load_state_dict(m1.state_dict())
+    arena = GradArena(list(m2.named_parameters()), flat_params=True)
+    o1 = torch.optim.SGD(m1.parameters(), lr=0.1, momentum=0.9, nesterov=True, weight_decay=1e-3)
+    o2 = FlatSGD(m2.parameters(), arena, lr=0.1, momentum=0.9, nesterov=True, weight_decay=1e-3)
+    x = torch.randn(4, 3, 8, 8, device="cuda")
+    for _ in range(3):
+        o1.zero_grad()
+        m1(x).square().mean().backward()
+        arena.zero_()
+        m2(x).square().mean().backward()
+        o1.step()
+        o2.step()
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p1, p2, rtol=1e-5, atol=1e-6)
+
+
+def test_normalize_u8():
+    from layer_wise_aaai20_amd.ops.nn import normalize_nhwc_u8
+    x = torch.randint(0, 256, (3, 17, 13, 3), dtype=torch.uint8, device="cuda")
+    mean = torch.tensor([120.0, 110.0, 100.0])
+    std = torch.tensor([60.0, 61.0, 62.0])
+    y = normalize_nhwc_u8(x, mean, std, torch.float32)
+    ref_ = (x.permute(0, 3, 1, 2).float().cpu() - mean.view(1, 3, 1, 1)) / std.view(1, 3, 1, 1)
+    torch.testing.assert_close(y.cpu(), ref_, rtol=1e-6, atol=1e-5)
+    yb = normalize_nhwc_u8(x, mean, std, torch.bfloat16)
+    torch.testing.assert_close(yb.float().cpu(), ref_, rtol=1e-2, atol=1e-2)
+    assert yb.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_resnet50_step_topk_gpu():
+    from layer_wise_aaai20_amd.ops import _ext
+    from layer_wise_aaai20_amd.train.imagenet import build_trainer
+    _ext.load()
+    tr = build_trainer("resnet50", device=torch.device("cuda", 0), K=0.001)
+    imgs = torch.randint(0, 256, (16, 64, 64, 3), dtype=torch.uint8, device="cuda")
+    tgt = torch.randint(0, 1000, (16,), device="cuda")
+    losses = [float(tr.step(imgs, tgt)) for _ in range(3)]
+    assert all(np.isfinite(losses))
+    st = tr.ddp.sync_stats()
+    assert st.payload_bytes < st.dense_bytes * 0.01

@@ -5,8 +5,8 @@
 // layer_wise_aaai20_amd/ops, and a GPU tensor reaching an op without this library loaded fails
 // loudly in ops/_ext.py.
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
 #include "lw_kernels.h"
@@ -15,7 +15,10 @@ namespace {
 
 using at::Tensor;
 
-inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+// ROCm builds of PyTorch expose HIP devices as DeviceType::CUDA ("masquerading").
+inline hipStream_t cur_stream() {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+}
 
 template <typename T>
 inline T* ptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
@@ -115,7 +118,7 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
                      Tensor tasks, Tensor task_lo, Tensor ws, int64_t km, int64_t out,
                      c10::optional<Tensor> pairs, c10::optional<Tensor> vals,
                      c10::optional<Tensor> idx, int64_t gid_base, int64_t step, int64_t seed) {
-  const c10::hip::HIPGuard guard(g.device());
+  const c10::DeviceGuard guard(g.device());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, keep, cap_off, small_segs, large_segs,
                                       tasks, task_lo, ws);
   a.pairs = optr<int2>(pairs);
@@ -133,7 +136,7 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
 void thresh_count(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
                   Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor ws, double V,
                   int64_t adaptive, Tensor counts_out) {
-  const c10::hip::HIPGuard guard(g.device());
+  const c10::DeviceGuard guard(g.device());
   Tensor empty_i = at::empty({0}, seg_n.options());
   Tensor empty_l = at::empty({1}, seg_off.options());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, seg_n, empty_l.expand({2}).contiguous(),
@@ -150,7 +153,7 @@ void thresh_count(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg
 void thresh_write(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
                   Tensor cap_off, Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor ws,
                   Tensor pairs) {
-  const c10::hip::HIPGuard guard(g.device());
+  const c10::DeviceGuard guard(g.device());
   Tensor empty_i = at::empty({0}, seg_n.options());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, seg_n, cap_off, empty_i, large_segs,
                                       tasks, task_lo, ws);
@@ -161,7 +164,7 @@ void thresh_write(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg
 
 void unpack_pairs(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor seg_n,
                   Tensor cap_off, Tensor utasks) {
-  const c10::hip::HIPGuard guard(g.device());
+  const c10::DeviceGuard guard(g.device());
   check_cuda(gathered, "gathered");
   check_cuda(g, "g");
   check_aligned16(g.data_ptr(), "g");
@@ -174,7 +177,7 @@ void unpack_pairs(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tens
 
 void unpack_validx(Tensor vals, Tensor idx, Tensor slot_seg, int64_t world, Tensor g,
                    Tensor seg_off) {
-  const c10::hip::HIPGuard guard(g.device());
+  const c10::DeviceGuard guard(g.device());
   check_cuda(vals, "vals");
   check_cuda(g, "g");
   lw::unpack_validx(ptr<float>(vals), ptr<int32_t>(idx), ptr<int32_t>(slot_seg), vals.numel(),
@@ -206,7 +209,7 @@ lw::QuantArgs make_quant_args(const Tensor& g, const c10::optional<Tensor>& ef,
 void quantize(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, Tensor segs,
               Tensor tasks, Tensor task_lo, Tensor rec_off, Tensor ws, Tensor payload, int64_t q,
               int64_t qstates, int64_t gid_base, int64_t step, int64_t tag, int64_t seed) {
-  const c10::hip::HIPGuard guard(g.device());
+  const c10::DeviceGuard guard(g.device());
   lw::QuantArgs a = make_quant_args(g, ef, seg_off, seg_n, segs, tasks, task_lo, rec_off, qstates);
   check_cuda(payload, "payload");
   check_aligned16(payload.data_ptr(), "payload");
@@ -229,7 +232,7 @@ void quantize(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, 
 void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor seg_n,
                 Tensor segs, Tensor tasks, Tensor task_lo, Tensor rec_off, int64_t q,
                 int64_t qstates) {
-  const c10::hip::HIPGuard guard(g.device());
+  const c10::DeviceGuard guard(g.device());
   lw::QuantArgs a = make_quant_args(g, c10::nullopt, seg_off, seg_n, segs, tasks, task_lo, rec_off,
                                     qstates);
   check_cuda(gathered, "gathered");
@@ -242,7 +245,7 @@ void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor
 void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tensor segs,
               Tensor tasks, Tensor seg_wd, double lr, double momentum, double dampening,
               int64_t nesterov, int64_t first_step, double grad_scale) {
-  const c10::hip::HIPGuard guard(p.device());
+  const c10::DeviceGuard guard(p.device());
   check_cuda(p, "p");
   check_cuda(g, "g");
   check_aligned16(p.data_ptr(), "p");
@@ -271,7 +274,7 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tens
 }
 
 void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<double> stdv) {
-  const c10::hip::HIPGuard guard(in.device());
+  const c10::DeviceGuard guard(in.device());
   check_cuda(in, "in");
   check_dtype(in, at::kByte, "in");
   TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "mean/std need 3 channels");

@@ -1,0 +1,244 @@
+"""CIFAR-10 data path: preprocessing, epoch-level random augmentation, batching.
+
+API-compatible with ``CIFAR10/core.py:39-114`` (``normalise``/``pad``/``transpose``, ``Crop``/
+``FlipLR``/``Cutout``, ``Transform``) and ``CIFAR10/torch_backend.py:32-63`` (``cifar10``,
+``Batches``). Additions for MI355X:
+
+* :class:`GPUBatches` keeps the whole (padded, normalised) dataset resident in HBM and applies the
+  per-epoch crop / flip / cutout choices as one batched gather on the device,
+  instead of per-sample numpy work in DataLoader workers.
+* :func:`synthetic_cifar10` — random images / labels of the real shapes (no network here).
+* :func:`cifar10` reads the CIFAR-10 *binary* distribution (``cifar-10-batches-bin``) or an
+  ``.npz``; nothing is unpickled.
+"""
+from __future__ import annotations
+
+import os
+from collections import namedtuple
+from typing import Optional
+
+import numpy as np
+import torch
+
+cifar10_mean = (0.4914, 0.4822, 0.4465)
+cifar10_std = (0.2471, 0.2435, 0.2616)
+
+
+def normalise(x, mean=cifar10_mean, std=cifar10_std):
+    x, mean, std = [np.array(a, np.float32) for a in (x, mean, std)]
+    x -= mean * 255
+    x *= 1.0 / (255 * std)
+    return x
+
+
+def pad(x, border=4):
+    return np.pad(x, [(0, 0), (border, border), (border, border), (0, 0)], mode="reflect")
+
+
+def transpose(x, source="NHWC", target="NCHW"):
+    return x.transpose([source.index(d) for d in target])
+
+
+class Crop(namedtuple("Crop", ("h", "w"))):
+    def __call__(self, x, x0, y0):
+        return x[:, y0:y0 + self.h, x0:x0 + self.w]
+
+    def options(self, x_shape):
+        _, H, W = x_shape
+        return {"x0": range(W + 1 - self.w), "y0": range(H + 1 - self.h)}
+
+    def output_shape(self, x_shape):
+        C, _, _ = x_shape
+        return (C, self.h, self.w)
+
+
+class FlipLR(namedtuple("FlipLR", ())):
+    def __call__(self, x, choice):
+        return x[:, :, ::-1].copy() if choice else x
+
+    def options(self, x_shape):
+        return {"choice": [True, False]}
+
+
+class Cutout(namedtuple("Cutout", ("h", "w"))):
+    def __call__(self, x, x0, y0):
+        x = x.copy()
+        x[:, y0:y0 + self.h, x0:x0 + self.w].fill(0.0)
+        return x
+
+    def options(self, x_shape):
+        _, H, W = x_shape
+        return {"x0": range(W + 1 - self.w), "y0": range(H + 1 - self.h)}
+
+
+class Transform:
+    """Draws every augmentation choice of an epoch with one vectorised ``np.random.choice`` per
+    option, applies them per item (``core.py:92-114``)."""
+
+    def __init__(self, dataset, transforms, rng: Optional[np.random.Generator] = None):
+        self.dataset, self.transforms = dataset, transforms
+        self.choices = None
+        self.rng = rng
+
+    def __len__(self):
+        return len(self.dataset)
+
+    def __getitem__(self, index):
+        data, labels = self.dataset[index]
+        for choices, f in zip(self.choices, self.transforms):
+            data = f(data, **{k: v[index] for k, v in choices.items()})
+        return data, labels
+
+    def set_random_choices(self):
+        self.choices = []
+        x_shape = self.dataset[0][0].shape
+        N = len(self)
+        choose = self.rng.choice if self.rng is not None else np.random.choice
+        for t in self.transforms:
+            opts = t.options(x_shape)
+            x_shape = t.output_shape(x_shape) if hasattr(t, "output_shape") else x_shape
+            self.choices.append({k: choose(v, size=N) for k, v in opts.items()})
+
+
+# ----------------------------------------------------------------------------- datasets
+def _read_cifar_bin(path):
+    raw = np.fromfile(path, dtype=np.uint8).reshape(-1, 3073)
+    labels = raw[:, 0].astype(np.int64)
+    data = raw[:, 1:].reshape(-1, 3, 32, 32).transpose(0, 2, 3, 1).copy()
+    return data, labels
+
+
+def cifar10(root: str, synthetic_fallback: bool = True, n_train=50000, n_test=10000, seed=0):
+    """``{'train': {'data': uint8 NHWC, 'labels'}, 'test': ...}``. Reads ``cifar-10-batches-bin``
+    or ``cifar10.npz`` under ``root``; otherwise synthetic data of the same shape."""
+    root = os.path.expanduser(root)
+    bdir = os.path.join(root, "cifar-10-batches-bin")
+    if os.path.isdir(bdir):
+        tr = [_read_cifar_bin(os.path.join(bdir, f"data_batch_{i}.bin")) for i in range(1, 6)]
+        te = _read_cifar_bin(os.path.join(bdir, "test_batch.bin"))
+        return {"train": {"data": np.concatenate([d for d, _ in tr]),
+                          "labels": np.concatenate([l for _, l in tr])},
+                "test": {"data": te[0], "labels": te[1]}}
+    npz = os.path.join(root, "cifar10.npz")
+    if os.path.exists(npz):
+        z = np.load(npz, allow_pickle=False)
+        return {"train": {"data": z["x_train"], "labels": z["y_train"].astype(np.int64)},
+                "test": {"data": z["x_test"], "labels": z["y_test"].astype(np.int64)}}
+    if not synthetic_fallback:
+        raise FileNotFoundError(f"no CIFAR-10 under {root} (need cifar-10-batches-bin or npz)")
+    return synthetic_cifar10(n_train, n_test, seed)
+
+
+def synthetic_cifar10(n_train=50000, n_test=10000, seed=0):
+    """Random uint8 images with labels that depend on a per-class colour bias, so a model can
+    actually learn something (loss decreases) while shapes match the real dataset."""
+    rng = np.random.default_rng(seed)
+
+    def make(n):
+        labels = rng.integers(0, 10, size=n).astype(np.int64)
+        base = rng.integers(0, 256, size=(n, 32, 32, 3)).astype(np.int16)
+        bias = (np.arange(10)[:, None] * np.array([23, 41, 67])[None, :]) % 96 - 48
+        data = np.clip(base // 2 + 64 + bias[labels][:, None, None, :], 0, 255).astype(np.uint8)
+        return {"data": data, "labels": labels}
+    return {"train": make(n_train), "test": make(n_test)}
+
+
+# ----------------------------------------------------------------------------- batching
+class Batches:
+    """DataLoader wrapper yielding ``{'input', 'target'}`` on ``device`` (torch_backend.py:48-63)."""
+
+    def __init__(self, dataset, batch_size, shuffle, set_random_choices=False, num_workers=0,
+                 drop_last=False, device=None, sampler=None):
+        self.dataset = dataset
+        self.batch_size = batch_size
+        self.set_random_choices = set_random_choices
+        self.device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        self.dataloader = torch.utils.data.DataLoader(
+            dataset, batch_size=batch_size, num_workers=num_workers,
+            pin_memory=self.device.type == "cuda", shuffle=shuffle and sampler is None,
+            drop_last=drop_last, sampler=sampler)
+
+    def __iter__(self):
+        if self.set_random_choices:
+            self.dataset.set_random_choices()
+        return ({"input": torch.as_tensor(x).to(self.device, non_blocking=True).float(),
+                 "target": torch.as_tensor(y).to(self.device, non_blocking=True).long()}
+                for (x, y) in self.dataloader)
+
+    def __len__(self):
+        return len(self.dataloader)
+
+
+class GPUBatches:
+    """Device-resident CIFAR batches with batched crop / flip / cutout.
+
+    ``data``: float NCHW (already normalised, padded by ``pad`` px for the random crop). Every epoch
+    draws (x0, y0, flip, cutout x0/y0) per image exactly like ``Transform.set_random_choices`` and
+    applies them with one gather per batch. With ``shard=(rank, world)`` each rank iterates its own
+    slice of a global permutation (fixes SURVEY.md D16: the reference's CIFAR ranks all walk the
+    full dataset)."""
+
+    def __init__(self, data: torch.Tensor, labels: torch.Tensor, batch_size: int, shuffle: bool,
+                 augment: bool = False, crop: int = 32, cutout: int = 8, drop_last: bool = False,
+                 shard=(0, 1), seed: int = 0, channels_last: bool = False, dtype=torch.float32):
+        self.data = data
+        self.labels = labels
+        self.batch_size = batch_size
+        self.shuffle = shuffle
+        self.augment = augment
+        self.crop = crop
+        self.cutout = cutout
+        self.drop_last = drop_last
+        self.rank, self.world = shard
+        self.epoch = 0
+        self.seed = seed
+        self.channels_last = channels_last
+        self.dtype = dtype
+
+    def _indices(self):
+        n = self.data.shape[0]
+        g = torch.Generator().manual_seed(self.seed + self.epoch)
+        idx = torch.randperm(n, generator=g) if self.shuffle else torch.arange(n)
+        per = n // self.world if self.world > 1 else n
+        return idx[self.rank * per:(self.rank + 1) * per] if self.world > 1 else idx
+
+    def __len__(self):
+        n = len(self._indices())
+        return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
+
+    def __iter__(self):
+        idx = self._indices().to(self.data.device)
+        n = idx.numel()
+        dev = self.data.device
+        g = torch.Generator(device="cpu").manual_seed(10_000 + self.seed + self.epoch)
+        H = self.data.shape[2]
+        if self.augment:
+            span = H - self.crop + 1
+            x0 = torch.randint(0, span, (n,), generator=g).to(dev)
+            y0 = torch.randint(0, span, (n,), generator=g).to(dev)
+            flip = torch.randint(0, 2, (n,), generator=g).to(dev).bool()
+            cspan = self.crop - self.cutout + 1
+            cx = torch.randint(0, cspan, (n,), generator=g).to(dev)
+            cy = torch.randint(0, cspan, (n,), generator=g).to(dev)
+        self.epoch += 1
+        bs = self.batch_size
+        stop = (n // bs) * bs if self.drop_last else n
+        ar = torch.arange(self.crop, device=dev)
+        for s in range(0, stop, bs):
+            b = idx[s:s + bs]
+            x = self.data[b]
+            if self.augment:
+                sl = slice(s, s + b.numel())
+                rows = (y0[sl][:, None] + ar[None, :])                      # [B, crop]
+                cols = (x0[sl][:, None] + ar[None, :])
+                cols = torch.where(flip[sl][:, None], cols.flip(1), cols)
+                x = x.gather(2, rows[:, None, :, None].expand(-1, x.shape[1], -1, H))
+                x = x.gather(3, cols[:, None, None, :].expand(-1, x.shape[1], self.crop, -1))
+                m_r = (ar[None, :] >= cy[sl][:, None]) & (ar[None, :] < cy[sl][:, None] + self.cutout)
+                m_c = (ar[None, :] >= cx[sl][:, None]) & (ar[None, :] < cx[sl][:, None] + self.cutout)
+                mask = (m_r[:, :, None] & m_c[:, None, :])[:, None]
+                x = x.masked_fill(mask, 0.0)
+            x = x.to(self.dtype)
+            if self.channels_last:
+                x = x.contiguous(memory_format=torch.channels_last)
+            yield {"input": x, "target": self.labels[b]}

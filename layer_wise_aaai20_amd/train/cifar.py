@@ -1,0 +1,104 @@
+"""CIFAR-10 training engine with the reference signatures (``CIFAR10/core.py:303-341``).
+
+``run_batches`` → forward → ``loss.sum().backward()`` → gradient sync selected by ``compress``
+(layer-wise / entire-model compression or plain averaging) → ``optimizer_step()`` →
+``model.zero_grad()``. ``train`` optionally initialises the process group (gloo, TCP
+``init_method``, as ``core.py:334``) and runs epochs, emitting the summary dict to loggers.
+
+Differences, all deliberate: the sync goes through :mod:`..parallel.functional` (bucketed, one
+collective per bucket, compressed wire formats), model state is broadcast from rank 0 before the
+first step, and ``world_size`` may be an int or the env-callable of D5.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..parallel import comm
+from ..parallel import functional as F
+from ..parallel.engine import canonical_mode
+from ..utils.logging import StatsLogger, Timer
+from ..models.graph import union
+
+
+def run_batches(model, batches, training, world_size=1, optimizer_step=None, stats=None,
+                compress=None, method=None, K=None, V=None, qstates=None,
+                error_feedback: bool = False, wire: str = "auto", max_batches: Optional[int] = None):
+    stats = stats or StatsLogger(("loss", "correct"))
+    model.train(training)
+    mode = canonical_mode(compress) if compress not in (None, "none") else "none"
+    for i, batch in enumerate(batches):
+        if max_batches is not None and i >= max_batches:
+            break
+        if training:
+            output = model(batch)
+            stats.append(output)
+            output["loss"].sum().backward()
+            if mode == "layerwise":
+                F.layerwise_compressed_comm(model, world_size, method, K, V, qstates,
+                                            error_feedback=error_feedback, wire=wire)
+            elif mode == "entiremodel":
+                F.entiremodel_compressed_comm(model, world_size, method, K, V, qstates,
+                                              error_feedback=error_feedback, wire=wire)
+            else:
+                F.all_reduce(model, world_size)
+            optimizer_step()
+            model.zero_grad(set_to_none=False)   # torch 1.x semantics: keep arena views
+        else:
+            with torch.no_grad():
+                output = model(batch)
+            stats.append(output)
+    return stats
+
+
+def train_epoch(model, train_batches, test_batches, optimizer_step, timer, world_size=1,
+                test_time_in_total=True, compress=None, method=None, K=None, V=None, qstates=None,
+                **kw):
+    train_stats = run_batches(model, train_batches, True, world_size, optimizer_step,
+                              compress=compress, method=method, K=K, V=V, qstates=qstates, **kw)
+    train_time = timer()
+    test_stats = run_batches(model, test_batches, False, world_size)
+    test_time = timer(test_time_in_total)
+    return {
+        "train time": train_time, "train loss": train_stats.mean("loss"),
+        "train acc": train_stats.mean("correct"),
+        "test time": test_time, "test loss": test_stats.mean("loss"),
+        "test acc": test_stats.mean("correct"),
+        "total time": timer.total_time,
+    }
+
+
+def init_distributed(master_address, world_size, rank, backend: Optional[str] = None):
+    """``dist.init_process_group(init_method=master_address, ...)`` (core.py:334). A bare host
+    (the reference default ``127.0.0.1``) is completed to ``tcp://host:29500``."""
+    if comm.is_dist() or int(world_size) <= 1:
+        return
+    addr = master_address or "127.0.0.1"
+    if "://" not in addr:
+        addr = f"tcp://{addr}:29500" if ":" not in addr else f"tcp://{addr}"
+    backend = backend or "gloo"
+    dist.init_process_group(backend=backend, init_method=addr, world_size=int(world_size),
+                            rank=int(rank))
+
+
+def train(model, optimizer, train_batches, test_batches, epochs, master_address=None,
+          world_size=1, rank=0, loggers=(), test_time_in_total=True, timer=None, compress=None,
+          method=None, K=None, V=None, qstates=None, backend: Optional[str] = None, **kw):
+    init_distributed(master_address, world_size, rank, backend)
+    if comm.is_dist() and comm.world_size() > 1:
+        comm.broadcast_coalesced(list(model.state_dict().values()), 0)
+    timer = timer or Timer()
+    summary = {}
+    for epoch in range(epochs):
+        epoch_stats = train_epoch(model, train_batches, test_batches, optimizer.step, timer,
+                                  world_size, test_time_in_total=test_time_in_total,
+                                  compress=compress, method=method, K=K, V=V, qstates=qstates,
+                                  **kw)
+        lr = optimizer.param_values()["lr"] if hasattr(optimizer, "param_values") else \
+            optimizer.param_groups[0]["lr"]
+        summary = union({"epoch": epoch + 1, "lr": lr * train_batches.batch_size}, epoch_stats)
+        for logger in loggers:
+            logger.append(summary)
+    return summary

@@ -1,0 +1,112 @@
+"""CIFAR-10 entry point with the reference CLI (``CIFAR10/dawn.py:8-20, 98-155``).
+
+    python -m CIFAR10.dawn -m tcp://127.0.0.1:2222 -r 0 -w 2 -n Resent9 -c layerwise \
+        --method Topk -K 0.01
+
+Recipe (``dawn.py:105-148``): 24 epochs (40 for Randomk / Thresholdv), batch 512 per rank,
+``PiecewiseLinear([0, 5, E], [0, 0.4, 0])`` evaluated at ``step / len(train_batches)`` and divided
+by the batch size (per-sample LR with a summed loss), SGD with ``wd = 5e-4 · bs`` and Nesterov
+momentum only when ``--momentum > 0``, crop / flip / cutout augmentation redrawn every epoch.
+Writes ``logs.tsv`` (``epoch\\thours\\ttop1Accuracy``) to ``--log_dir``.
+
+Added flags (all optional): ``--epochs``, ``--error_feedback``, ``--wire``, ``--synthetic``,
+``--max_batches`` (debug), ``--dtype``, ``--backend``, ``--shard_data`` (each rank sees 1/W of the
+data instead of the whole set, D16), ``--device``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+from ..data import cifar as D
+from ..models.cifar import build_network
+from ..models.graph import SGD, trainable_params
+from ..utils.logging import PiecewiseLinear, TableLogger, Timer, TSVLogger
+from .cifar import train
+
+
+def get_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="layer-wise / entire-model compressed CIFAR-10")
+    p.add_argument("--data_dir", type=str, default="./data")
+    p.add_argument("--log_dir", type=str, default=".")
+    p.add_argument("--master_address", "-m", type=str, default="127.0.0.1")
+    p.add_argument("--rank", "-r", type=int, default=0)
+    p.add_argument("--world_size", "-w", type=int, default=2)
+    p.add_argument("--network", "-n", type=str, default="resnet9")
+    p.add_argument("--compress", "-c", type=str, default="none")
+    p.add_argument("--method", type=str, default="none")
+    p.add_argument("--ratio", "-K", type=float, default=0.5)
+    p.add_argument("--threshold", "-V", type=float, default=0.001)
+    p.add_argument("--qstates", "-Q", type=int, default=255)
+    p.add_argument("--momentum", type=float, default=0.0)
+    # additions
+    p.add_argument("--epochs", type=int, default=None)
+    p.add_argument("--batch_size", type=int, default=512)
+    p.add_argument("--error_feedback", action="store_true")
+    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "dense", "indexfree"])
+    p.add_argument("--synthetic", action="store_true")
+    p.add_argument("--n_train", type=int, default=50000)
+    p.add_argument("--n_test", type=int, default=10000)
+    p.add_argument("--max_batches", type=int, default=None)
+    p.add_argument("--backend", type=str, default=None)
+    p.add_argument("--shard_data", action="store_true")
+    p.add_argument("--device", type=str, default=None)
+    p.add_argument("--seed", type=int, default=0)
+    return p
+
+
+def main(argv=None):
+    args = get_parser().parse_args(argv)
+    device = torch.device(args.device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    if device.type == "cuda":
+        torch.cuda.set_device(device.index or 0)
+    torch.manual_seed(args.seed)
+    np.random.seed(args.seed + args.rank)
+
+    dataset = D.synthetic_cifar10(args.n_train, args.n_test, args.seed) if args.synthetic else \
+        D.cifar10(args.data_dir, n_train=args.n_train, n_test=args.n_test)
+    epochs = args.epochs or (40 if args.method in ("Randomk", "Thresholdv") else 24)
+    lr_schedule = PiecewiseLinear([0, 5, epochs], [0, 0.4, 0])
+    bs = args.batch_size
+    model = build_network(args.network).to(device)
+
+    timer = Timer(synch=torch.cuda.synchronize if device.type == "cuda" else None)
+    train_x = D.transpose(D.normalise(D.pad(dataset["train"]["data"], 4)))
+    test_x = D.transpose(D.normalise(dataset["test"]["data"]))
+    shard = (args.rank, args.world_size) if args.shard_data else (0, 1)
+    train_batches = D.GPUBatches(torch.from_numpy(np.ascontiguousarray(train_x)).to(device),
+                                 torch.as_tensor(dataset["train"]["labels"]).to(device), bs,
+                                 shuffle=True, augment=True, drop_last=True, shard=shard,
+                                 seed=args.seed)
+    test_batches = D.GPUBatches(torch.from_numpy(np.ascontiguousarray(test_x)).to(device),
+                                torch.as_tensor(dataset["test"]["labels"]).to(device), bs,
+                                shuffle=False)
+    print(f"Finished preprocessing in {timer():.2f} seconds")
+
+    def lr(step):
+        return lr_schedule(step / max(len(train_batches), 1)) / bs
+
+    if args.momentum > 0:
+        opt = SGD(trainable_params(model), lr=lr, momentum=args.momentum, weight_decay=5e-4 * bs,
+                  nesterov=True)
+    else:
+        opt = SGD(trainable_params(model), lr=lr, weight_decay=5e-4 * bs)
+
+    tsv = TSVLogger()
+    train(model, opt, train_batches, test_batches, epochs, args.master_address, args.world_size,
+          args.rank, loggers=(TableLogger(), tsv), timer=timer, test_time_in_total=False,
+          compress=args.compress, method=args.method, K=args.ratio, V=args.threshold,
+          qstates=args.qstates, backend=args.backend, error_feedback=args.error_feedback,
+          wire=args.wire, max_batches=args.max_batches)
+    os.makedirs(os.path.expanduser(args.log_dir), exist_ok=True)
+    with open(os.path.join(os.path.expanduser(args.log_dir), "logs.tsv"), "w") as f:
+        f.write(str(tsv))
+    return tsv
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-fused", action="store_true", help="disable fused HIP nn kernels")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--miopen-find", type=int, default=1,
+                    help="1: let MIOpen benchmark conv solvers once (cudnn.benchmark)")
     return ap.parse_args()
 
 
@@ -61,6 +63,7 @@ def main():
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     torch.cuda.set_device(local)
+    torch.backends.cudnn.benchmark = bool(args.miopen_find)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)

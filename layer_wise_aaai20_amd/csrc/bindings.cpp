@@ -292,6 +292,119 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
                    out.scalar_type() == at::kBFloat16, cur_stream());
 }
 
+// ---------------------------------------------------------------- fused BatchNorm (NHWC)
+void check_nhwc(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.dim() == 4 ? t.is_contiguous(at::MemoryFormat::ChannelsLast) : t.is_contiguous(),
+              name, " must be channels_last (4-D) or contiguous (2-D)");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name,
+              " must be bf16 or fp32");
+  check_aligned16(t.data_ptr(), name);
+}
+
+int64_t channels_of(const Tensor& x) { return x.size(1); }
+
+std::tuple<Tensor, Tensor, Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res,
+                                          c10::optional<Tensor> weight,
+                                          c10::optional<Tensor> bias, c10::optional<Tensor> rmean,
+                                          c10::optional<Tensor> rvar, bool training,
+                                          double momentum, double eps, bool relu) {
+  const c10::DeviceGuard guard(x.device());
+  check_nhwc(x, "x");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "fused BN needs C % 8 == 0, got ", C);
+  if (res.has_value() && res->defined()) {
+    check_nhwc(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type(),
+                "residual must match x");
+  }
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor y = at::empty_like(x);
+  Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32);
+  Tensor scale = at::empty({C}, f32), shift = at::empty({C}, f32);
+  lw::BNArgs a{};
+  a.x = x.data_ptr();
+  a.res = (res.has_value() && res->defined()) ? res->data_ptr() : nullptr;
+  a.y = y.data_ptr();
+  a.M = M;
+  a.C = (int)C;
+  a.bf16 = x.scalar_type() == at::kBFloat16;
+  a.training = training;
+  a.relu = relu;
+  a.eps = (float)eps;
+  a.momentum = (float)momentum;
+  a.gamma = optr<float>(weight);
+  a.beta = optr<float>(bias);
+  Tensor partial;
+  if (training) {
+    a.rmean = optr<float>(rmean);
+    a.rvar = optr<float>(rvar);
+    partial = at::empty({(int64_t)lw::bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+    a.partial = ptr<float>(partial);
+    a.mean = ptr<float>(mean);
+    a.invstd = ptr<float>(invstd);
+    a.scale = ptr<float>(scale);
+    a.shift = ptr<float>(shift);
+  } else {
+    TORCH_CHECK(rmean.has_value() && rvar.has_value(), "eval mode needs running stats");
+    mean.copy_(*rmean);
+    invstd.copy_(at::rsqrt(*rvar + eps));
+    Tensor g = (weight.has_value() && weight->defined()) ? *weight : at::ones({C}, f32);
+    Tensor b = (bias.has_value() && bias->defined()) ? *bias : at::zeros({C}, f32);
+    scale.copy_(g * invstd);
+    shift.copy_(b - mean * scale);
+    a.scale = ptr<float>(scale);
+    a.shift = ptr<float>(shift);
+  }
+  lw::bn_forward(a, cur_stream());
+  return {y, mean, invstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y,
+                                                  c10::optional<Tensor> weight, Tensor mean,
+                                                  Tensor invstd, bool training, bool relu,
+                                                  bool need_dres) {
+  const c10::DeviceGuard guard(x.device());
+  check_nhwc(x, "x");
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.sizes() == x.sizes(), "dy must match x");
+  if (relu) {
+    TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
+    check_nhwc(*y, "y");
+  }
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor dx = at::empty_like(x);
+  Tensor dres = need_dres ? at::empty_like(x) : at::empty({0}, x.options());
+  Tensor dgamma = at::empty({C}, f32), dbeta = at::empty({C}, f32);
+  Tensor coef = at::empty({3 * C}, f32);
+  Tensor partial = at::empty({(int64_t)lw::bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+  lw::BNArgs a{};
+  a.x = x.data_ptr();
+  a.dy = dy.data_ptr();
+  a.y = relu ? y->data_ptr() : nullptr;
+  a.dx = dx.data_ptr();
+  a.dres = need_dres ? dres.data_ptr() : nullptr;
+  a.M = M;
+  a.C = (int)C;
+  a.bf16 = x.scalar_type() == at::kBFloat16;
+  a.training = training;
+  a.relu = relu;
+  a.gamma = optr<float>(weight);
+  a.mean = ptr<float>(mean);
+  a.invstd = ptr<float>(invstd);
+  a.partial = ptr<float>(partial);
+  a.dgamma = ptr<float>(dgamma);
+  a.dbeta = ptr<float>(dbeta);
+  a.A = ptr<float>(coef);
+  a.B = a.A + C;
+  a.Cc = a.A + 2 * C;
+  lw::bn_backward(a, cur_stream());
+  return {dx, dgamma, dbeta, dres};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(lwaaai, m) {
@@ -326,6 +439,13 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
       "int nesterov, int first_step, float grad_scale) -> ()");
   m.def("normalize_u8(Tensor input, Tensor(a!) out, float[] mean, float[] std) -> ()");
+  m.def(
+      "bn_fwd(Tensor x, Tensor? res, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
+      "Tensor(b!)? running_var, bool training, float momentum, float eps, bool relu) "
+      "-> (Tensor, Tensor, Tensor)");
+  m.def(
+      "bn_bwd(Tensor dy, Tensor x, Tensor? y, Tensor? weight, Tensor mean, Tensor invstd, "
+      "bool training, bool relu, bool need_dres) -> (Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
@@ -338,4 +458,6 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("dequantize", &dequantize);
   m.impl("sgd_step", &sgd_step);
   m.impl("normalize_u8", &normalize_u8);
+  m.impl("bn_fwd", &bn_fwd);
+  m.impl("bn_bwd", &bn_bwd);
 }

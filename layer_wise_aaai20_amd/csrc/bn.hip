@@ -1,0 +1,399 @@
+// Fused BatchNorm (+ residual add) (+ ReLU) for NHWC (channels_last) activations on gfx950.
+//
+// The reference's ResNets run cuDNN BatchNorm, then a separate ReLU, then a separate residual add
+// (IMAGENET/training/resnet.py:60-80, CIFAR10/dawn.py:23-35): on MI355X those glue ops were 62 % of
+// a ResNet-50 step (profiles/r1_baseline_summary.txt). Here a BN layer costs two passes forward
+// (per-channel sum/sumsq, then normalise+affine+add+ReLU) and two backward (per-channel reductions
+// of dy' and dy'·x̂ with the ReLU mask folded in, then dx and the residual gradient) — SURVEY.md N16.
+//
+// Data layout: x is [M = N*H*W, C] with C contiguous, C % 8 == 0. Each lane moves 8 channels (one
+// 16-byte bf16 load). Reductions go to per-block partial sums in a fixed order (deterministic), and
+// a finalize kernel folds them in fp64.
+#include "common.h"
+#include "lw_kernels.h"
+
+namespace lw {
+
+constexpr int BNT = 256;
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+template <typename T> struct V8;
+template <> struct V8<uint16_t> {
+  static __device__ __forceinline__ void load(const uint16_t* p, float f[8]) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = __uint_as_float(w[k] << 16);
+      f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store(uint16_t* p, const float f[8]) {
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w[k] = (uint32_t)f2bf_rne(f[2 * k]) | ((uint32_t)f2bf_rne(f[2 * k + 1]) << 16);
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <> struct V8<float> {
+  static __device__ __forceinline__ void load(const float* p, float f[8]) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float f[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// Column reductions over [M, C]. MODE 0 (forward): (Σx, Σx²). MODE 1 (backward):
+// (Σdy', Σdy'·(x-mean)) with dy' = relu ? dy·[y>0] : dy.
+// Thread (g, r): channel group g (8 channels), row lane r of R = BNT/G. 4 rows in flight per lane.
+// partial: [gridDim.x][2C]
+// ------------------------------------------------------------------------------------------
+template <typename T, int MODE, bool RELU>
+__global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, const T* __restrict__ dy,
+                                                   const T* __restrict__ y,
+                                                   const float* __restrict__ mean, int64_t M, int C,
+                                                   int64_t rows_per_block,
+                                                   float* __restrict__ partial) {
+  __shared__ float sa[BNT * 8];
+  __shared__ float sb[BNT * 8];
+  const int G = C / 8;
+  const int R = BNT / G;                    // rows processed per iteration (>= 1)
+  const int g = threadIdx.x % G, r = threadIdx.x / G;
+  const bool active = r < R;
+  float a[8], b[8], mu[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { a[k] = 0.f; b[k] = 0.f; mu[k] = 0.f; }
+  if (MODE == 1 && active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) mu[k] = mean[g * 8 + k];
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(r0 + rows_per_block, M);
+  constexpr int U = 4;
+  if (active) {
+    const T* xp = x + g * 8;
+    const T* dp = dy + g * 8;
+    const T* yp = y + g * 8;
+    int64_t row = r0 + r;
+    for (; row + (U - 1) * R < r1; row += U * R) {
+      float xv[U][8], d[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) V8<T>::load(xp + (row + u * R) * C, xv[u]);
+      if (MODE == 1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) V8<T>::load(dp + (row + u * R) * C, d[u]);
+        if (RELU) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            float yv[8];
+            V8<T>::load(yp + (row + u * R) * C, yv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d[u][k] = yv[k] > 0.f ? d[u][k] : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (MODE == 0) { a[k] += xv[u][k]; b[k] += xv[u][k] * xv[u][k]; }
+          else { a[k] += d[u][k]; b[k] += d[u][k] * (xv[u][k] - mu[k]); }
+        }
+      }
+    }
+    for (; row < r1; row += R) {
+      float xv[8];
+      V8<T>::load(xp + row * C, xv);
+      if (MODE == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { a[k] += xv[k]; b[k] += xv[k] * xv[k]; }
+      } else {
+        float d[8];
+        V8<T>::load(dp + row * C, d);
+        if (RELU) {
+          float yv[8];
+          V8<T>::load(yp + row * C, yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { a[k] += d[k]; b[k] += d[k] * (xv[k] - mu[k]); }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sa[r * C + g * 8 + k] = a[k];
+      sb[r * C + g * 8 + k] = b[k];
+    }
+  }
+  __syncthreads();
+  const int64_t nb = gridDim.x;
+  for (int c = threadIdx.x; c < C; c += BNT) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int q = 0; q < R; ++q) { s1 += sa[q * C + c]; s2 += sb[q * C + c]; }
+    partial[(int64_t)c * nb + blockIdx.x] = s1;                 // channel-major: [2][C][nb]
+    partial[((int64_t)C + c) * nb + blockIdx.x] = s2;
+  }
+}
+
+// Fold the block partials: one wave per channel, lanes stride over blocks (coalesced, fixed
+// order), then a fixed butterfly in fp64. Lane 0 of each wave gets the sums.
+__device__ __forceinline__ bool fold_partials(const float* __restrict__ partial, int nblocks, int C,
+                                              double& s1, double& s2, int& c) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  c = blockIdx.x * 4 + w;
+  if (c >= C) return false;
+  const float* p1 = partial + (int64_t)c * nblocks;
+  const float* p2 = partial + ((int64_t)C + c) * nblocks;
+  float a = 0.f, b = 0.f;
+  for (int blk = lane; blk < nblocks; blk += 64) { a += p1[blk]; b += p2[blk]; }
+  double da = a, db = b;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    da += __shfl_xor(da, o, 64);
+    db += __shfl_xor(db, o, 64);
+  }
+  s1 = da;
+  s2 = db;
+  return lane == 0;
+}
+
+__global__ __launch_bounds__(256) void k_bn_finalize_fwd(
+    const float* __restrict__ partial, int nblocks, int C, int64_t M,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
+  double s, q;
+  int c;
+  if (!fold_partials(partial, nblocks, C, s, q, c)) return;
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  scale[c] = gm * invstd;
+  shift[c] = bt - (float)mean * gm * invstd;
+  if (rmean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unbiased);
+  }
+}
+
+// Thread-constant channel group: the grid-stride step is a multiple of G = C/8 (apply_grid), so
+// a thread always touches the same 8 channels and keeps their coefficients in registers.
+template <typename T, bool RES, bool RELU>
+__global__ __launch_bounds__(BNT) void k_bn_apply(const T* __restrict__ x, const T* __restrict__ res,
+                                                  T* __restrict__ y,
+                                                  const float* __restrict__ scale,
+                                                  const float* __restrict__ shift, int64_t n8,
+                                                  int C) {
+  const int G = C / 8;
+  const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
+  const int64_t step = (int64_t)gridDim.x * BNT;
+  const int c0 = (int)(t0 % G) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sc[k] = scale[c0 + k]; sh[k] = shift[c0 + k]; }
+  int64_t i = t0;
+  for (; i + step < n8; i += 2 * step) {
+    float v[2][8], rr[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      V8<T>::load(x + (i + u * step) * 8, v[u]);
+      if (RES) V8<T>::load(res + (i + u * step) * 8, rr[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float t = v[u][k] * sc[k] + sh[k];
+        if (RES) t += rr[u][k];
+        if (RELU) t = fmaxf(t, 0.f);
+        v[u][k] = t;
+      }
+      V8<T>::store(y + (i + u * step) * 8, v[u]);
+    }
+  }
+  if (i < n8) {
+    float v[8], rr[8];
+    V8<T>::load(x + i * 8, v);
+    if (RES) V8<T>::load(res + i * 8, rr);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = v[k] * sc[k] + sh[k];
+      if (RES) t += rr[k];
+      if (RELU) t = fmaxf(t, 0.f);
+      v[k] = t;
+    }
+    V8<T>::store(y + i * 8, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bn_finalize_bwd(
+    const float* __restrict__ partial, int nblocks, int C, int64_t M,
+    const float* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ A, float* __restrict__ B, float* __restrict__ Cc, int training) {
+  double s1, s2;
+  int c;
+  if (!fold_partials(partial, nblocks, C, s1, s2, c)) return;
+  const double is = invstd[c];
+  const double gm = gamma ? gamma[c] : 1.0;
+  if (dbeta) dbeta[c] = (float)s1;
+  if (dgamma) dgamma[c] = (float)(s2 * is);
+  const double a = gm * is;
+  if (!training) {             // running statistics are constants: dx = gamma*invstd*dy'
+    A[c] = (float)a;
+    B[c] = 0.f;
+    Cc[c] = 0.f;
+    return;
+  }
+  const double bb = -gm * is * is * is * s2 / (double)M;
+  A[c] = (float)a;
+  B[c] = (float)bb;
+  Cc[c] = (float)(-a * s1 / (double)M - bb * (double)mean[c]);
+}
+
+// dx = A*dy' + B*x + C ; dres = dy'
+template <typename T, bool RELU, bool DRES>
+__global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ dy,
+                                                      const T* __restrict__ y,
+                                                      const float* __restrict__ A,
+                                                      const float* __restrict__ B,
+                                                      const float* __restrict__ Cc,
+                                                      T* __restrict__ dx, T* __restrict__ dres,
+                                                      int64_t n8, int C) {
+  const int G = C / 8;
+  const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
+  const int64_t step = (int64_t)gridDim.x * BNT;
+  const int c0 = (int)(t0 % G) * 8;
+  float ca[8], cb[8], cc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { ca[k] = A[c0 + k]; cb[k] = B[c0 + k]; cc[k] = Cc[c0 + k]; }
+  for (int64_t i = t0; i < n8; i += step) {
+    const int64_t off = i * 8;
+    float xv[8], d[8];
+    V8<T>::load(x + off, xv);
+    V8<T>::load(dy + off, d);
+    if (RELU) {
+      float yv[8];
+      V8<T>::load(y + off, yv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
+    }
+    if (DRES) V8<T>::store(dres + off, d);
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = ca[k] * d[k] + cb[k] * xv[k] + cc[k];
+    V8<T>::store(dx + off, o);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblocks) {
+  const int G = C / 8;
+  const int R = BNT / G;
+  const int64_t target = 1024;          // ≈ 4 blocks per CU
+  int64_t rpb = (M + target - 1) / target;
+  rpb = (rpb + R - 1) / R * R;
+  rpb = rpb < R ? R : rpb;
+  rows_per_block = rpb;
+  nblocks = (int)((M + rpb - 1) / rpb);
+}
+
+int bn_reduce_blocks(int64_t M, int C) {
+  int64_t rpb;
+  int nb;
+  reduce_geometry(M, C, rpb, nb);
+  return nb;
+}
+
+// grid with (gridDim * BNT) % G == 0 so every thread keeps one channel group
+static int apply_grid(int64_t n8, int C) {
+  const int G = C / 8;
+  int q = G;                                   // blocks must be a multiple of G / gcd(G, BNT)
+  int a = G, b = BNT;
+  while (b) { const int t = a % b; a = b; b = t; }
+  q = G / a;
+  int64_t g = (n8 + BNT - 1) / BNT;
+  g = g > 4096 ? 4096 : (g < 1 ? 1 : g);
+  g = (g + q - 1) / q * q;
+  return (int)g;
+}
+
+template <typename T>
+static void bn_forward_t(const BNArgs& a, hipStream_t st) {
+  const T* x = static_cast<const T*>(a.x);
+  const T* res = static_cast<const T*>(a.res);
+  T* y = static_cast<T*>(a.y);
+  const int64_t n8 = a.M * a.C / 8;
+  if (a.training) {
+    int64_t rpb;
+    int nb;
+    reduce_geometry(a.M, a.C, rpb, nb);
+    hipLaunchKernelGGL((k_bn_reduce<T, 0, false>), dim3(nb), dim3(BNT), 0, st, x, (const T*)nullptr,
+                       (const T*)nullptr, (const float*)nullptr, a.M, a.C, rpb, a.partial);
+    hipLaunchKernelGGL(k_bn_finalize_fwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
+                       a.C, a.M, a.gamma, a.beta, a.eps, a.momentum, a.rmean, a.rvar, a.mean,
+                       a.invstd, a.scale, a.shift);
+  }
+  const dim3 grid(apply_grid(n8, a.C)), block(BNT);
+  if (res) {
+    if (a.relu) hipLaunchKernelGGL((k_bn_apply<T, true, true>), grid, block, 0, st, x, res, y, a.scale, a.shift, n8, a.C);
+    else hipLaunchKernelGGL((k_bn_apply<T, true, false>), grid, block, 0, st, x, res, y, a.scale, a.shift, n8, a.C);
+  } else {
+    if (a.relu) hipLaunchKernelGGL((k_bn_apply<T, false, true>), grid, block, 0, st, x, res, y, a.scale, a.shift, n8, a.C);
+    else hipLaunchKernelGGL((k_bn_apply<T, false, false>), grid, block, 0, st, x, res, y, a.scale, a.shift, n8, a.C);
+  }
+}
+
+template <typename T>
+static void bn_backward_t(const BNArgs& a, hipStream_t st) {
+  const T* x = static_cast<const T*>(a.x);
+  const T* dy = static_cast<const T*>(a.dy);
+  const T* y = static_cast<const T*>(a.y);
+  T* dx = static_cast<T*>(a.dx);
+  T* dres = static_cast<T*>(a.dres);
+  const int64_t n8 = a.M * a.C / 8;
+  int64_t rpb;
+  int nb;
+  reduce_geometry(a.M, a.C, rpb, nb);
+  if (a.relu)
+    hipLaunchKernelGGL((k_bn_reduce<T, 1, true>), dim3(nb), dim3(BNT), 0, st, x, dy, y, a.mean, a.M, a.C, rpb, a.partial);
+  else
+    hipLaunchKernelGGL((k_bn_reduce<T, 1, false>), dim3(nb), dim3(BNT), 0, st, x, dy, y, a.mean, a.M, a.C, rpb, a.partial);
+  hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
+                     a.C, a.M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
+                     (int)a.training);
+  const dim3 grid(apply_grid(n8, a.C)), block(BNT);
+#define LW_BWD(R, D)                                                                            \
+  hipLaunchKernelGGL((k_bn_bwd_apply<T, R, D>), grid, block, 0, st, x, dy, y, a.A, a.B, a.Cc, dx, \
+                     dres, n8, a.C)
+  if (a.relu) { if (dres) LW_BWD(true, true); else LW_BWD(true, false); }
+  else { if (dres) LW_BWD(false, true); else LW_BWD(false, false); }
+#undef LW_BWD
+}
+
+void bn_forward(const BNArgs& a, hipStream_t st) {
+  if (a.bf16) bn_forward_t<uint16_t>(a, st); else bn_forward_t<float>(a, st);
+}
+void bn_backward(const BNArgs& a, hipStream_t st) {
+  if (a.bf16) bn_backward_t<uint16_t>(a, st); else bn_backward_t<float>(a, st);
+}
+
+}  // namespace lw

@@ -101,6 +101,37 @@ struct SgdArgs {
 };
 void sgd_step(const SgdArgs& a, hipStream_t st);
 
+// fused BatchNorm (+add) (+ReLU), NHWC (bn.hip)
+struct BNArgs {
+  const void* x;        // [M, C] bf16 or fp32
+  const void* res;      // residual (forward) or nullptr
+  void* y;              // forward output; backward: saved output for the ReLU mask (or nullptr)
+  const void* dy;
+  void* dx;
+  void* dres;           // backward: gradient w.r.t. the residual input (or nullptr)
+  int64_t M;
+  int C;
+  bool bf16, training, relu;
+  float eps, momentum;
+  const float* gamma;   // may be nullptr (affine=False)
+  const float* beta;
+  float* rmean;         // running stats (nullptr: not tracked)
+  float* rvar;
+  float* mean;          // [C] batch mean (saved)
+  float* invstd;        // [C]
+  float* scale;         // [C] forward scratch
+  float* shift;         // [C]
+  float* partial;       // [nblocks][2C]
+  float* dgamma;
+  float* dbeta;
+  float* A;             // [C] backward coefficients
+  float* B;
+  float* Cc;
+};
+int bn_reduce_blocks(int64_t M, int C);
+void bn_forward(const BNArgs& a, hipStream_t st);
+void bn_backward(const BNArgs& a, hipStream_t st);
+
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
                   const float stdv[3], bool bf16, hipStream_t st);

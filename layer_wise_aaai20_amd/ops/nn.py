@@ -1,10 +1,15 @@
-"""Model-path ops backed by the HIP kernels of ``csrc/nn.hip`` (GPU) or torch (CPU)."""
+"""Model-path ops backed by the HIP kernels of ``csrc/nn.hip`` and ``csrc/bn.hip`` (GPU) or torch
+(CPU): fused uint8 normalisation, and BatchNorm with the following ReLU and residual add fused in
+(``FusedBatchNorm2d``), plus ``fuse_resnet`` which switches a reference-layout ResNet to them
+without changing a single parameter / buffer name (checkpoints stay compatible).
+"""
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 
-from ._ext import ops_for
+from ._ext import load, ops_for
 
 
 def normalize_nhwc_u8(images: torch.Tensor, mean: torch.Tensor, std: torch.Tensor,
@@ -27,7 +32,129 @@ def normalize_nhwc_u8(images: torch.Tensor, mean: torch.Tensor, std: torch.Tenso
     return x.to(dtype).contiguous(memory_format=torch.channels_last)
 
 
+# ----------------------------------------------------------------------------- fused BN
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    if t.dim() == 4:
+        return t.contiguous(memory_format=torch.channels_last)
+    return t.contiguous()
+
+
+class _FusedBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum,
+                eps, relu):
+        lib = load()
+        x = _nhwc(x)
+        if residual is not None:
+            residual = _nhwc(residual).to(x.dtype)
+        y, mean, invstd = lib.bn_fwd(x, residual, weight, bias, running_mean, running_var,
+                                     bool(training), float(momentum), float(eps), bool(relu))
+        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        ctx.flags = (bool(training), bool(relu), residual is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, mean, invstd = ctx.saved_tensors
+        training, relu, has_res = ctx.flags
+        lib = load()
+        dy = _nhwc(dy).to(x.dtype)
+        dx, dgamma, dbeta, dres = lib.bn_bwd(dy, x, y, weight, mean, invstd, training, relu,
+                                             has_res)
+        need_w = weight is not None and ctx.needs_input_grad[2]
+        need_b = ctx.needs_input_grad[3]
+        return (dx, dres if has_res else None, dgamma if need_w else None,
+                dbeta if need_b else None, None, None, None, None, None, None)
+
+
+def fused_batch_norm(x, weight, bias, running_mean, running_var, training, momentum, eps,
+                     relu=False, residual=None):
+    """BN → (+ residual) → (ReLU). HIP kernels for channels_last GPU tensors with C % 8 == 0,
+    torch ops otherwise (CPU path, odd channel counts)."""
+    use_hip = x.is_cuda and x.dim() in (2, 4) and x.size(1) % 8 == 0 and \
+        x.dtype in (torch.bfloat16, torch.float32)
+    if use_hip:
+        return _FusedBN.apply(x, residual, weight, bias, running_mean, running_var, training,
+                              momentum, eps, relu)
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+class FusedBatchNorm2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` (same parameters, buffers and state_dict keys) whose forward can also
+    apply the residual add and the ReLU that follow it in the reference models."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True,
+                 track_running_stats=True, relu: bool = False, **kw):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats, **kw)
+        self.fuse_relu = relu
+
+    def forward(self, x, residual=None):
+        momentum = 0.0 if self.momentum is None else self.momentum
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(1)
+            if self.momentum is None:
+                momentum = 1.0 / float(self.num_batches_tracked)
+        training = self.training or not self.track_running_stats
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        return fused_batch_norm(x, self.weight, self.bias, rm, rv, training, momentum, self.eps,
+                                relu=self.fuse_relu, residual=residual)
+
+    def extra_repr(self):
+        return super().extra_repr() + (", fused_relu=True" if self.fuse_relu else "")
+
+
+def to_fused_bn(bn: nn.BatchNorm2d, relu: bool = False) -> FusedBatchNorm2d:
+    """Re-class in place: the very same Parameter / buffer objects stay registered."""
+    bn.__class__ = FusedBatchNorm2d
+    bn.fuse_relu = relu
+    return bn
+
+
+# ----------------------------------------------------------------------------- fused ResNet
+def _fused_bottleneck_forward(self, x):
+    identity = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
+    out = self.bn1(self.conv1(x))
+    out = self.bn2(self.conv2(out))
+    return self.bn3(self.conv3(out), identity)
+
+
+def _fused_basic_forward(self, x):
+    identity = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
+    out = self.bn1(self.conv1(x))
+    return self.bn2(self.conv2(out), identity)
+
+
+def _fused_resnet_forward(self, x):
+    x = self.maxpool(self.bn1(self.conv1(x)))
+    x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+    x = torch.flatten(self.avgpool(x), 1)
+    return self.fc(x)
+
+
 def fuse_resnet(model: nn.Module) -> nn.Module:
-    """Hook for swapping BN/ReLU/residual chains for fused HIP kernels (kept as a no-op until the
-    fused kernels beat the library path on MI355X; see profiles/)."""
+    """Switch a ``models.resnet`` network to fused BN(+add)(+ReLU). Parameter/buffer names and
+    values are untouched; only forward changes."""
+    from ..models import resnet as R
+    import types
+    for m in model.modules():
+        if isinstance(m, R.Bottleneck):
+            to_fused_bn(m.bn1, relu=True)
+            to_fused_bn(m.bn2, relu=True)
+            to_fused_bn(m.bn3, relu=True)
+            if m.downsample is not None:
+                to_fused_bn(m.downsample[1], relu=False)
+            m.forward = types.MethodType(_fused_bottleneck_forward, m)
+        elif isinstance(m, R.BasicBlock):
+            to_fused_bn(m.bn1, relu=True)
+            to_fused_bn(m.bn2, relu=True)
+            if m.downsample is not None:
+                to_fused_bn(m.downsample[1], relu=False)
+            m.forward = types.MethodType(_fused_basic_forward, m)
+    if isinstance(model, R.ResNet):
+        to_fused_bn(model.bn1, relu=True)
+        model.forward = types.MethodType(_fused_resnet_forward, model)
     return model

@@ -1,0 +1,78 @@
+"""Fused NHWC BatchNorm(+add)(+ReLU) HIP kernels vs torch's BatchNorm (fp32 reference)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from layer_wise_aaai20_amd.ops.nn import fused_batch_norm, fuse_resnet
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, res, w, b, rm, rv, relu):
+    y = F.batch_norm(x.float(), rm, rv, w, b, True, 0.1, 1e-5)
+    if res is not None:
+        y = y + res.float()
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu,residual", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (4, 256, 7, 7), (2, 2048, 3, 3), (3, 24, 5, 5)])
+def test_fused_bn_matches_torch(dtype, relu, residual, shape):
+    torch.manual_seed(0)
+    C = shape[1]
+    x = (torch.randn(*shape, device="cuda") * 2 + 0.5).to(dtype)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_()
+    res = (torch.randn(*shape, device="cuda").to(dtype).contiguous(
+        memory_format=torch.channels_last).requires_grad_() if residual else None)
+    w = (torch.rand(C, device="cuda") + 0.5).requires_grad_()
+    b = torch.randn(C, device="cuda").requires_grad_()
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    rm2, rv2 = rm.clone(), rv.clone()
+    y = fused_batch_norm(x, w, b, rm, rv, True, 0.1, 1e-5, relu=relu, residual=res)
+    xr = x.detach().float().requires_grad_()
+    resr = res.detach().float().requires_grad_() if residual else None
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    yr = _ref(xr, resr, wr, br, rm2, rv2, relu)
+    tol = dict(rtol=2e-2, atol=3e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(rm, rm2, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(rv, rv2, rtol=1e-4, atol=1e-5)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    gtol = dict(rtol=3e-2, atol=5e-1) if dtype == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(w.grad, wr.grad, **gtol)
+    torch.testing.assert_close(b.grad, br.grad, **gtol)
+    if residual:
+        torch.testing.assert_close(res.grad.float(), resr.grad, **tol)
+
+
+def test_fused_bn_eval_mode():
+    C = 32
+    x = torch.randn(4, C, 6, 6, device="cuda").contiguous(memory_format=torch.channels_last)
+    w, b = torch.rand(C, device="cuda"), torch.randn(C, device="cuda")
+    rm, rv = torch.randn(C, device="cuda"), torch.rand(C, device="cuda") + 0.5
+    y = fused_batch_norm(x, w, b, rm, rv, False, 0.1, 1e-5, relu=True)
+    yr = F.relu(F.batch_norm(x, rm, rv, w, b, False, 0.1, 1e-5))
+    torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-5)
+
+
+def test_fused_resnet18_matches_unfused():
+    from layer_wise_aaai20_amd.models.resnet import resnet18
+    torch.manual_seed(0)
+    a = resnet18().cuda().to(memory_format=torch.channels_last)
+    b = resnet18().cuda().to(memory_format=torch.channels_last)
+    b.load_state_dict(a.state_dict())
+    fuse_resnet(b)
+    assert set(a.state_dict()) == set(b.state_dict())
+    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    ya, yb = a(x), b(x)
+    torch.testing.assert_close(yb, ya, rtol=1e-3, atol=1e-3)
+    ya.square().mean().backward()
+    yb.square().mean().backward()
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pb.grad, pa.grad, rtol=2e-3, atol=2e-4, msg=n)
+    for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
+        torch.testing.assert_close(bb.float(), ba.float(), rtol=1e-4, atol=1e-5, msg=n)

@@ -1,0 +1,12 @@
+"""CIFAR-10 entry point (reference ``CIFAR10/dawn.py``): ``python -m CIFAR10.dawn --help``."""
+import sys
+
+from layer_wise_aaai20_amd.models.cifar import (alexnet, basic_alexnet, basic_resnet9, conv_bn,  # noqa
+                                                conv_bn_stride, losses, residual, resnet9)
+from layer_wise_aaai20_amd.train.cifar_main import get_parser, main  # noqa
+from layer_wise_aaai20_amd.utils.logging import TSVLogger  # noqa
+
+parser = get_parser()
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,13 @@
+"""ImageNet entry point (reference ``IMAGENET/training/train_imagenet_nv.py``)."""
+import sys
+
+from layer_wise_aaai20_amd.parallel.functional import (all_reduce,  # noqa
+                                                       entiremodel_compressed_comm,
+                                                       layerwise_compressed_comm)
+from layer_wise_aaai20_amd.train.imagenet_main import (DataManager, Scheduler, accuracy,  # noqa
+                                                       correct, distributed_predict, get_parser,
+                                                       listify, main, save_checkpoint,
+                                                       to_python_float, train, validate)
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

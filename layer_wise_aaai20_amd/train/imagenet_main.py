@@ -1,0 +1,546 @@
+"""ImageNet ResNet training entry point with the reference CLI
+(``IMAGENET/training/train_imagenet_nv.py:39-253, 388-651``).
+
+    torchrun --nproc-per-node 8 -m IMAGENET.training.train_imagenet_nv /data/imagenet \
+        --logdir runs/x --distributed --init-bn0 --no-bn-wd -c layerwise --method Topk -K 0.001
+
+Kept: every reference flag, the progressive-resizing phase schedule (honoured from ``--phases``,
+D14), LR warm-up ``Scheduler``, ``DataManager`` phase swaps, per-step cross-rank metric reduction,
+sharded distributed evaluation with uneven batches (``distributed_predict``), ``event.log`` /
+TensorBoard tags, checkpoint layout ``{epoch, state_dict, best_top5, optimizer}``, ``--resume``.
+
+Fixed: duplicate ``--momentum`` (D4, one flag, default 0.9), ``world_size`` is the
+process-group size (D5), ``enitremodel`` really runs entire-model compression (D3), no double
+reduction after ``--ddp`` / ``--sparsification`` (D11), fp32 ``--no-bn-wd`` keeps every parameter
+(D12), loader dtype follows the model (D13).
+
+Added: ``--bf16`` (autocast, the MI355X default), ``--overlap`` (CompressedDDP: compression of each
+bucket overlapped with backward), ``--error-feedback``, ``--wire``, ``--arch``, ``--epochs``,
+``--synthetic-size``, ``--extra-ckpt`` (also saves EF residuals / scheduler state).
+"""
+from __future__ import annotations
+
+import argparse
+import ast
+import copy
+import json
+import os
+import shutil
+import sys
+import time
+from datetime import datetime
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from ..data import imagenet as D
+from ..models import resnet as R
+from ..ops import nn as lwnn
+from ..parallel import comm
+from ..parallel import functional as F
+from ..parallel.ddp import CompressedDDP, DistributedDataParallel, RandomKSparsifiedDDP
+from ..utils import fp16 as fp16util
+from ..utils.logging import AverageMeter, FileLogger, NetworkMeter, TensorboardLogger, TimeMeter
+
+from .schedules import NAMES as _SCHED_NAMES, schedule as _schedule
+
+
+def get_parser():
+    p = argparse.ArgumentParser(description="ImageNet training with compressed gradients")
+    p.add_argument("data", metavar="DIR", nargs="?", default="synthetic", help="dataset path")
+    p.add_argument("--phases", type=str, default="one_machine",
+                   help="schedule name, or a JSON / python-literal list of phase dicts")
+    p.add_argument("-j", "--workers", default=0, type=int)
+    p.add_argument("--start-epoch", default=0, type=int)
+    p.add_argument("--momentum", default=0.9, type=float)
+    p.add_argument("--weight-decay", "--wd", default=1e-4, type=float)
+    p.add_argument("--init-bn0", action="store_true")
+    p.add_argument("--print-freq", "-p", default=50, type=int)
+    p.add_argument("--no-bn-wd", action="store_true")
+    p.add_argument("--resume", default="", type=str)
+    p.add_argument("-e", "--evaluate", dest="evaluate", action="store_true")
+    p.add_argument("--fp16", action="store_true")
+    p.add_argument("--bf16", action="store_true")
+    p.add_argument("--loss-scale", type=float, default=1024)
+    p.add_argument("--distributed", action="store_true")
+    p.add_argument("--dist-url", default="env://", type=str)
+    p.add_argument("--dist-backend", default=None, type=str)
+    p.add_argument("--local_rank", "--local-rank", default=None, type=int)
+    p.add_argument("--logdir", default="", type=str)
+    p.add_argument("--name", type=str, default="imagenet")
+    p.add_argument("--short-epoch", action="store_true")
+    p.add_argument("--log_all_workers", type=int, default=0)
+    p.add_argument("--sparsification", action="store_true")
+    p.add_argument("--randk", type=float, default=1)
+    p.add_argument("--ddp", action="store_true")
+    p.add_argument("--seed", type=int, default=2147483647)
+    p.add_argument("--compress", "-c", type=str, default="none")
+    p.add_argument("--method", type=str, default="none")
+    p.add_argument("--ratio", "-K", type=float, default=0.5)
+    p.add_argument("--threshold", "-V", type=float, default=0.001)
+    p.add_argument("--qstates", "-Q", type=int, default=255)
+    # additions
+    p.add_argument("--arch", default="resnet50")
+    p.add_argument("--overlap", action="store_true", help="CompressedDDP (bucketed, overlapped)")
+    p.add_argument("--error-feedback", action="store_true")
+    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "dense", "indexfree"])
+    p.add_argument("--epochs", type=int, default=None, help="stop after this many epochs")
+    p.add_argument("--synthetic-size", type=int, default=None,
+                   help="synthetic train images per phase (default 64 batches)")
+    p.add_argument("--no-fused", action="store_true")
+    p.add_argument("--extra-ckpt", action="store_true")
+    p.add_argument("--device", default=None)
+    return p
+
+
+def parse_phases(spec: str):
+    if spec in _SCHED_NAMES or spec == "smoke":
+        return _schedule(spec)
+    if spec.isdigit():
+        return _schedule(int(spec))
+    try:
+        return json.loads(spec)
+    except json.JSONDecodeError:
+        return ast.literal_eval(spec)
+
+
+def listify(p=None, q=None):
+    """``listify`` of train_imagenet_nv.py:691-699 without ``collections.Iterable`` (D9)."""
+    if p is None:
+        p = []
+    elif not isinstance(p, (list, tuple)):
+        p = [p]
+    p = list(p)
+    n = q if isinstance(q, int) else 1 if q is None else len(q)
+    if len(p) == 1:
+        p = p * n
+    return p
+
+
+def to_python_float(t):
+    if isinstance(t, (float, int)):
+        return t
+    return t.item() if hasattr(t, "item") else t[0]
+
+
+def correct(output, target, topk=(1,)):
+    maxk = min(max(topk), output.size(1))
+    _, pred = output.topk(maxk, 1, True, True)
+    pred = pred.t()
+    ok = pred.eq(target.view(1, -1).expand_as(pred))
+    return [ok[:min(k, maxk)].reshape(-1).float().sum(0, keepdim=True) for k in topk]
+
+
+def accuracy(output, target, topk=(1,)):
+    bs = target.size(0)
+    return [c.mul_(100.0 / bs) for c in correct(output, target, topk)]
+
+
+# ------------------------------------------------------------------------------------ scheduler
+class Scheduler:
+    """Per-iteration piecewise-constant / linear LR from the phase list (train_imagenet_nv.py:602)."""
+
+    def __init__(self, optimizer, phases, log=None, tb=None, momentum=None):
+        self.optimizer = optimizer
+        self.current_lr = None
+        self.phases = [self.format_phase(p) for p in phases]
+        self.tot_epochs = max(max(p["ep"]) for p in self.phases)
+        self.log, self.tb, self.momentum = log, tb, momentum
+
+    @staticmethod
+    def format_phase(phase):
+        phase["ep"] = listify(phase["ep"])
+        phase["lr"] = listify(phase["lr"])
+        if len(phase["lr"]) == 2:
+            assert len(phase["ep"]) == 2, "Linear learning rates must contain end epoch"
+        return phase
+
+    @staticmethod
+    def calc_linear_lr(lr_start, lr_end, epoch_curr, batch_curr, epoch_tot, batch_tot):
+        step_tot = epoch_tot * batch_tot
+        step_curr = epoch_curr * batch_tot + batch_curr
+        return lr_start + step_curr * (lr_end - lr_start) / step_tot
+
+    def linear_phase_lr(self, phase, epoch, batch_curr, batch_tot):
+        lr_start, lr_end = phase["lr"]
+        ep_start, ep_end = phase["ep"]
+        if "epoch_step" in phase:
+            batch_curr = 0
+        return self.calc_linear_lr(lr_start, lr_end, epoch - ep_start, batch_curr,
+                                   ep_end - ep_start, batch_tot)
+
+    def get_current_phase(self, epoch):
+        for phase in reversed(self.phases):
+            if epoch >= phase["ep"][0]:
+                return phase
+        raise Exception("Epoch out of range")
+
+    def get_lr(self, epoch, batch_curr, batch_tot):
+        phase = self.get_current_phase(epoch)
+        if len(phase["lr"]) == 1:
+            return phase["lr"][0]
+        return self.linear_phase_lr(phase, epoch, batch_curr, batch_tot)
+
+    def update_lr(self, epoch, batch_num, batch_tot):
+        lr = self.get_lr(epoch, batch_num, batch_tot)
+        if self.current_lr == lr:
+            return
+        if self.log and (batch_num == 1 or batch_num == batch_tot):
+            self.log.event(f"Changing LR from {self.current_lr} to {lr}")
+        self.current_lr = lr
+        for g in self.optimizer.param_groups:
+            g["lr"] = lr
+        if self.tb:
+            self.tb.log("sizes/lr", lr)
+            self.tb.log("sizes/momentum", self.momentum)
+
+    def state_dict(self):
+        return {"current_lr": self.current_lr}
+
+    def load_state_dict(self, sd):
+        self.current_lr = sd.get("current_lr")
+
+
+# ------------------------------------------------------------------------------------ data phases
+class DataManager:
+    """Pre-builds one loader pair per phase and swaps them at phase epochs
+    (train_imagenet_nv.py:545-598)."""
+
+    def __init__(self, phases, args, device, dtype, log=None, tb=None):
+        self.args, self.device, self.dtype, self.log, self.tb = args, device, dtype, log, tb
+        self.phases = self.preload_phase_data(phases)
+        self.trn_dl = self.val_dl = self.trn_smp = self.val_smp = None
+
+    def set_epoch(self, epoch):
+        cur = self.get_phase(epoch)
+        if cur:
+            self.set_data(cur)
+        if hasattr(self.trn_smp, "set_epoch"):
+            self.trn_smp.set_epoch(epoch)
+        if hasattr(self.val_smp, "set_epoch"):
+            self.val_smp.set_epoch(epoch)
+
+    def get_phase(self, epoch):
+        return next((p for p in self.phases if p["ep"] == epoch), None)
+
+    def set_data(self, phase):
+        if phase.get("keep_dl", False):
+            if self.log:
+                self.log.event(f"Batch size changed: {phase['bs']}")
+            if self.tb:
+                self.tb.log_size(phase["bs"])
+            self.trn_dl.update_batch_size(phase["bs"])
+            return
+        if self.log:
+            self.log.event(f"Dataset changed.\nImage size: {phase['sz']}\nBatch size: "
+                           f"{phase['bs']}\nTrain Directory: {phase['trndir']}\nValidation "
+                           f"Directory: {phase['valdir']}")
+        if self.tb:
+            self.tb.log_size(phase["bs"], phase["sz"])
+        self.trn_dl, self.val_dl, self.trn_smp, self.val_smp = phase["data"]
+        self.phases.remove(phase)
+
+    def preload_phase_data(self, phases):
+        for phase in phases:
+            if not phase.get("keep_dl", False):
+                trndir = phase.get("trndir", "")
+                valdir = phase.get("valdir", trndir)
+                phase["trndir"] = self.args.data + trndir + "/train"
+                phase["valdir"] = self.args.data + valdir + "/validation"
+                phase["data"] = self.preload_data(**phase)
+        return phases
+
+    def preload_data(self, ep, sz, bs, trndir, valdir, **kw):
+        kw.pop("lr", None)
+        val_bs = max(bs, 512) if sz == 128 else (max(bs, 256) if sz == 224 else max(bs, 128))
+        if self.args.short_epoch:
+            val_bs = bs
+        n_train = self.args.synthetic_size or (12 if self.args.short_epoch else 64) * bs
+        return D.get_loaders(trndir, valdir, sz=sz, bs=bs, val_bs=val_bs,
+                             workers=self.args.workers, rect_val=kw.get("rect_val", False),
+                             min_scale=kw.get("min_scale", 0.08),
+                             distributed=self.args.distributed, n_train=n_train,
+                             n_val=(4 if self.args.short_epoch else 8) * val_bs,
+                             device=self.device, dtype=self.dtype)
+
+
+# ------------------------------------------------------------------------------------ run state
+class Run:
+    def __init__(self, args):
+        self.args = args
+        self.world = comm.world_size()
+        self.rank = comm.rank()
+        self.is_master = self.rank == 0
+        self.tb = TensorboardLogger(args.logdir, is_master=self.is_master)
+        self.log = FileLogger(args.logdir, is_master=self.is_master,
+                              is_rank0=(args.local_rank or 0) == 0)
+
+
+def save_checkpoint(run, epoch, model, best_top5, optimizer, is_best=False,
+                    filename="checkpoint.pth.tar", extra=None):
+    """``{'epoch', 'state_dict', 'best_top5', 'optimizer'}`` (+ optional extra keys, which older
+    readers ignore) — train_imagenet_nv.py:663-669."""
+    state = {"epoch": epoch + 1, "state_dict": model.state_dict(), "best_top5": best_top5,
+             "optimizer": optimizer.state_dict()}
+    if extra:
+        state.update(extra)
+    path = os.path.join(run.args.logdir or ".", filename)
+    torch.save(state, path)
+    if is_best and run.args.logdir:
+        shutil.copyfile(path, os.path.join(run.args.logdir, "model_best.pth.tar"))
+    return path
+
+
+def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, master):
+    args = run.args
+    net_meter, timer = NetworkMeter(), TimeMeter()
+    losses, top1, top5 = AverageMeter(), AverageMeter(), AverageMeter()
+    model.train()
+    for i, (inp, target) in enumerate(trn_loader):
+        if args.short_epoch and i > 10:
+            break
+        batch_num = i + 1
+        timer.batch_start()
+        scheduler.update_lr(epoch, batch_num, len(trn_loader))
+        with torch.autocast(device_type=inp.device.type, dtype=torch.bfloat16, enabled=args.bf16):
+            output = model(inp)
+            loss = criterion(output.float(), target)
+        if args.fp16:
+            scaled = loss * args.loss_scale
+            model.zero_grad()
+            scaled.backward()
+            sync(model)
+            model_params, master_params = master
+            fp16util.model_grads_to_master_grads(model_params, master_params)
+            for p in master_params:
+                if p.grad is not None:
+                    p.grad.data.mul_(1.0 / args.loss_scale)
+            optimizer.step()
+            fp16util.master_params_to_model_params(model_params, master_params)
+        else:
+            optimizer.zero_grad()
+            loss.backward()
+            sync(model)
+            optimizer.step()
+        timer.batch_end()
+        corr1, corr5 = correct(output.data, target, topk=(1, 5))
+        metrics = torch.cat([torch.tensor([float(inp.size(0))], device=loss.device),
+                             loss.detach().float().reshape(1), corr1, corr5])
+        if args.distributed:
+            metrics = comm.sum_tensor(metrics)
+        batch_total, reduced_loss, c1, c5 = metrics.cpu().tolist()
+        if args.distributed:
+            reduced_loss /= run.world
+        losses.update(reduced_loss, batch_total)
+        top1.update(c1 * 100.0 / batch_total, batch_total)
+        top5.update(c5 * 100.0 / batch_total, batch_total)
+        should_print = batch_num % args.print_freq == 0 or batch_num == len(trn_loader)
+        if run.is_master and should_print:
+            run.tb.log_memory()
+            run.tb.log_trn_times(timer.batch_time.val, timer.data_time.val, inp.size(0))
+            run.tb.log_trn_loss(losses.val, top1.val, top5.val)
+            recv, sent = net_meter.update_bandwidth()
+            run.tb.log("sizes/batch_total", batch_total)
+            run.tb.log("net/recv_gbit", recv)
+            run.tb.log("net/transmit_gbit", sent)
+            run.log.verbose(
+                f"Epoch: [{epoch}][{batch_num}/{len(trn_loader)}]\tTime {timer.batch_time.val:.3f} "
+                f"({timer.batch_time.avg:.3f})\tLoss {losses.val:.4f} ({losses.avg:.4f})\t"
+                f"Acc@1 {top1.val:.3f} ({top1.avg:.3f})\tAcc@5 {top5.val:.3f} ({top5.avg:.3f})\t"
+                f"Data {timer.data_time.val:.3f} ({timer.data_time.avg:.3f})\t"
+                f"BW {recv:.3f} {sent:.3f}")
+        run.tb.update_step_count(batch_total)
+    return losses.avg, top1.avg, top5.avg
+
+
+def distributed_predict(run, inp, target, model, criterion):
+    """Uneven batches across ranks, a rank may hold none (train_imagenet_nv.py:523-542)."""
+    bs = inp.size(0)
+    dev = target.device
+    loss = torch.zeros((), device=dev)
+    c1 = torch.zeros(1, device=dev)
+    c5 = torch.zeros(1, device=dev)
+    valid = 0.0
+    if bs:
+        with torch.no_grad():
+            output = model(inp)
+            loss = criterion(output.float(), target).detach()
+        valid = 1.0
+        c1, c5 = correct(output, target, topk=(1, 5))
+    metrics = torch.cat([torch.tensor([float(bs), valid], device=dev), loss.reshape(1).float(),
+                         c1, c5])
+    batch_total, valid_batches, reduced_loss, c1, c5 = comm.sum_tensor(metrics).cpu().tolist()
+    reduced_loss = reduced_loss / max(valid_batches, 1)
+    return c1 * 100.0 / max(batch_total, 1), c5 * 100.0 / max(batch_total, 1), reduced_loss, \
+        batch_total
+
+
+def validate(run, val_loader, model, criterion, epoch, start_time):
+    args = run.args
+    timer = TimeMeter()
+    losses, top1, top5 = AverageMeter(), AverageMeter(), AverageMeter()
+    model.eval()
+    t0 = time.time()
+    for i, (inp, target) in enumerate(val_loader):
+        if args.short_epoch and i > 10:
+            break
+        timer.batch_start()
+        if args.distributed:
+            a1, a5, loss, batch_total = distributed_predict(run, inp, target, model, criterion)
+        else:
+            with torch.no_grad():
+                output = model(inp)
+                loss = float(criterion(output.float(), target))
+            batch_total = inp.size(0)
+            a1, a5 = [float(a) for a in accuracy(output, target, topk=(1, 5))]
+        timer.batch_end()
+        losses.update(loss, batch_total)
+        top1.update(a1, batch_total)
+        top5.update(a5, batch_total)
+        if run.is_master and ((i + 1) % args.print_freq == 0 or i + 1 == len(val_loader)):
+            run.log.verbose(f"Test:  [{epoch}][{i + 1}/{len(val_loader)}]\tTime "
+                            f"{timer.batch_time.val:.3f} ({timer.batch_time.avg:.3f})\tLoss "
+                            f"{losses.val:.4f} ({losses.avg:.4f})\tAcc@1 {top1.val:.3f} "
+                            f"({top1.avg:.3f})\tAcc@5 {top5.val:.3f} ({top5.avg:.3f})")
+    run.tb.log_eval(top1.avg, top5.avg, time.time() - t0)
+    run.tb.log("epoch", epoch)
+    return top1.avg, top5.avg
+
+
+def _bn_groups(model, params, wd):
+    """``bnwd_optim_params`` without the D12 generator bug."""
+    from .imagenet import bn_param_groups
+    return bn_param_groups(model, wd, True)
+
+
+def main(argv=None):
+    args = get_parser().parse_args(argv)
+    if args.local_rank is None:
+        args.local_rank = int(os.environ.get("LOCAL_RANK", os.environ.get(
+            "OMPI_COMM_WORLD_LOCAL_RANK", "0")))
+    assert not (args.ddp and args.sparsification), "ddp and sparsification can't coexist"
+    device = torch.device(args.device) if args.device else (
+        torch.device("cuda", args.local_rank) if torch.cuda.is_available() else torch.device("cpu"))
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+        torch.backends.cudnn.benchmark = True
+    if args.distributed and not comm.is_dist():
+        backend = args.dist_backend or ("nccl" if device.type == "cuda" else "gloo")
+        dist.init_process_group(backend=backend, init_method=args.dist_url)
+        assert comm.env_world_size() == dist.get_world_size()
+    run = Run(args)
+    log, tb = run.log, run.tb
+    log.console(str(args))
+    log.console(f"using seed {args.seed}")
+    torch.manual_seed(args.seed)
+    tb.log("sizes/world", run.world)
+
+    model = getattr(R, args.arch)(bn0=args.init_bn0)
+    if not args.no_fused and device.type == "cuda" and not args.fp16:
+        lwnn.fuse_resnet(model)
+    model = model.to(device)
+    if device.type == "cuda":
+        model = model.to(memory_format=torch.channels_last)
+    if args.fp16:
+        model = fp16util.network_to_half(model)
+    base_model = model
+    sync = lambda m: None                                       # noqa: E731
+    if args.ddp:
+        model = DistributedDataParallel(model)
+    elif args.sparsification:
+        model = RandomKSparsifiedDDP(model, randk=args.randk, seed=args.seed)
+    elif args.overlap:
+        model = CompressedDDP(model, compress=args.compress, method=args.method, K=args.ratio,
+                              V=args.threshold, qstates=args.qstates,
+                              error_feedback=args.error_feedback, wire=args.wire,
+                              flat_params=False)
+    else:
+        if comm.is_dist():
+            comm.broadcast_coalesced(list(model.state_dict().values()), 0)
+
+        def sync(m):                                                # noqa: F811
+            F.compressed_comm(m, args.compress, run.world, args.method, args.ratio,
+                              args.threshold, args.qstates, error_feedback=args.error_feedback,
+                              wire=args.wire)
+    best_top5 = 93
+
+    master = None
+    if args.fp16:
+        master = fp16util.prep_param_lists(model)
+        opt_params = _bn_groups(base_model, None, args.weight_decay) if args.no_bn_wd else None
+        if opt_params is not None:   # map model params -> masters
+            idx = {id(p): i for i, p in enumerate(master[0])}
+            opt_params = [{"params": [master[1][idx[id(p)]] for p in g["params"]],
+                           "weight_decay": g["weight_decay"]} for g in opt_params]
+        else:
+            opt_params = master[1]
+    else:
+        opt_params = _bn_groups(base_model, None, args.weight_decay) if args.no_bn_wd else \
+            [p for p in model.parameters() if p.requires_grad]
+    criterion = nn.CrossEntropyLoss().to(device)
+    if args.momentum > 0:
+        optimizer = torch.optim.SGD(opt_params, 0.0, momentum=args.momentum,
+                                    weight_decay=args.weight_decay, nesterov=True)
+    else:
+        optimizer = torch.optim.SGD(opt_params, 0.0, weight_decay=args.weight_decay)
+
+    phases = parse_phases(args.phases)
+    dtype = torch.float16 if args.fp16 else torch.float32
+    dm = DataManager([copy.deepcopy(p) for p in phases if "bs" in p], args, device, dtype,
+                     log, tb)
+    scheduler = Scheduler(optimizer, [copy.deepcopy(p) for p in phases if "lr" in p], log, tb,
+                          args.momentum)
+
+    if args.resume:
+        ckpt = torch.load(args.resume, map_location=device, weights_only=True)
+        model.load_state_dict(ckpt["state_dict"])
+        args.start_epoch = ckpt["epoch"]
+        best_top5 = ckpt["best_top5"]
+        optimizer.load_state_dict(ckpt["optimizer"])
+        if "scheduler" in ckpt:
+            scheduler.load_state_dict(ckpt["scheduler"])
+        log.console(f"resumed from {args.resume} at epoch {args.start_epoch}")
+
+    start_time = datetime.now()
+    if args.evaluate:
+        dm.set_epoch(args.start_epoch)
+        return validate(run, dm.val_dl, model, criterion, 0, start_time)
+
+    if args.distributed:
+        log.console("Syncing machines before training")
+        comm.sum_tensor(torch.tensor([1.0], device=device))
+
+    log.event("~~epoch\thours\ttop1\ttop5\n")
+    end_epoch = scheduler.tot_epochs if args.epochs is None else min(scheduler.tot_epochs,
+                                                                     args.start_epoch + args.epochs)
+    # phases before start_epoch must still be applied (resume mid-schedule)
+    for e in range(0, args.start_epoch):
+        if dm.get_phase(e):
+            dm.set_epoch(e)
+    top1 = top5 = 0.0
+    for epoch in range(args.start_epoch, end_epoch):
+        dm.set_epoch(epoch)
+        train(run, dm.trn_dl, model, criterion, optimizer, scheduler, epoch, sync, master)
+        top1, top5 = validate(run, dm.val_dl, model, criterion, epoch, start_time)
+        hours = (datetime.now() - start_time).total_seconds() / 3600.0
+        log.event(f"~~{epoch}\t{hours:.5f}\t\t{top1:.3f}\t\t{top5:.3f}\n")
+        is_best = top5 > best_top5
+        best_top5 = max(top5, best_top5)
+        if args.local_rank == 0 and run.is_master:
+            extra = {"scheduler": scheduler.state_dict()} if args.extra_ckpt else None
+            if is_best:
+                save_checkpoint(run, epoch, model, best_top5, optimizer, is_best=True,
+                                filename="model_best.pth.tar", extra=extra)
+            phase = dm.get_phase(epoch)
+            if phase:
+                save_checkpoint(run, epoch, model, best_top5, optimizer,
+                                filename=f"sz{phase['bs']}_checkpoint.path.tar", extra=extra)
+            save_checkpoint(run, epoch, model, best_top5, optimizer, filename="checkpoint.pth.tar",
+                            extra=extra)
+    tb.close()
+    return top1, top5
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

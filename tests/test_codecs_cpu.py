@@ -1,0 +1,180 @@
+"""Wire codecs on CPU: decode(encode(g)) reproduces the reference compressors; multi-rank
+payloads average like all_reduce(SUM)/world; error-feedback identities; Philox known answers."""
+import numpy as np
+import pytest
+import torch
+
+from layer_wise_aaai20_amd.compress import codecs
+from layer_wise_aaai20_amd.compress import reference as ref
+from layer_wise_aaai20_amd.compress.plan import SegPlan
+from layer_wise_aaai20_amd.utils import philox
+
+SIZES = [64, 3, 1000, 4097, 9408, 20000]
+
+
+def plan_for(sizes, align=64):
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += (n + align - 1) // align * align
+    return SegPlan(offs, sizes), o
+
+
+def segs(plan, t):
+    for s in range(plan.S):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        yield s, t[o:o + n]
+
+
+def test_philox_known_answers():
+    r = philox.philox4x32_10(0, 0, 0, 0, 0, 0)
+    assert [int(x) for x in r] == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    f = 0xFFFFFFFF
+    r = philox.philox4x32_10(f, f, f, f, f, f)
+    assert [int(x) for x in r] == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    u = philox.uniforms(1000, 1, 2, 3, 4)
+    assert u.min() >= 0 and u.max() < 1 and abs(u.mean() - 0.5) < 0.05
+
+
+@pytest.mark.parametrize("K", [0.001, 0.01, 0.3])
+def test_topk_codec_equals_oracle(K):
+    plan, N = plan_for(SIZES)
+    g = torch.randn(N)
+    c = codecs.TopkCodec(plan, 1, 0, K)
+    send = c.compress(g.clone(), None, 0)
+    out = torch.zeros(N)
+    c.decompress(send, None, out, world=1)
+    for s, x in segs(plan, out):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        assert torch.equal(x, ref.topk(g[o:o + n], K))
+
+
+def test_topk_multi_rank_mean_and_union_support():
+    plan, N = plan_for(SIZES)
+    world = 4
+    gs = [torch.randn(N) for _ in range(world)]
+    payloads = [codecs.TopkCodec(plan, 1, 0, 0.01).compress(g.clone(), None, 0).clone()
+                for g in gs]
+    c = codecs.TopkCodec(plan, world, 0, 0.01)
+    out = torch.zeros(N)
+    c.decompress(None, torch.cat(payloads), out, world=world)
+    for s, x in segs(plan, out):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        exp = ref.mean_over_ranks([ref.topk(g[o:o + n], 0.01) for g in gs])
+        torch.testing.assert_close(x, exp, rtol=1e-6, atol=1e-7)
+
+
+def test_topk_error_feedback_identity():
+    plan, N = plan_for(SIZES)
+    g, e = torch.randn(N), torch.randn(N) * 0.1
+    c = codecs.TopkCodec(plan, 1, 0, 0.05)
+    e2 = e.clone()
+    send = c.compress(g.clone(), e2, 0)
+    out = torch.zeros(N)
+    c.decompress(send, None, out, world=1)
+    for s, x in segs(plan, out):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        torch.testing.assert_close(x + e2[o:o + n], g[o:o + n] + e[o:o + n])
+        assert torch.all((x == 0) | (e2[o:o + n] == 0))      # sent positions leave no residual
+
+
+def test_randk_rank_coherent_and_exact_count():
+    plan, N = plan_for(SIZES)
+    a = codecs.RandkCodec(plan, 2, 0, 0.05, seed=99)
+    b = codecs.RandkCodec(plan, 2, 1, 0.05, seed=99)
+    a.compress(torch.randn(N), None, 7)
+    b.compress(torch.randn(N), None, 7)
+    assert torch.equal(a._idx["cpu"], b._idx["cpu"])        # same mask on every rank
+    c = codecs.RandkCodec(plan, 2, 1, 0.05, seed=99)
+    c.compress(torch.randn(N), None, 8)
+    assert not torch.equal(a._idx["cpu"], c._idx["cpu"])    # fresh mask every step
+    for s in range(plan.S):
+        lo, hi = int(a.cap_off[s]), int(a.cap_off[s + 1])
+        assert hi - lo == ref.randomk_keep_count(int(plan.sizes[s]), 0.05)
+        idx = a._idx["cpu"][lo:hi]
+        assert idx.unique().numel() == idx.numel() and int(idx.max()) < plan.sizes[s]
+
+
+def test_randk_index_free_allreduce_semantics():
+    plan, N = plan_for(SIZES)
+    gs = [torch.randn(N) for _ in range(3)]
+    cs = [codecs.RandkCodec(plan, 3, r, 0.1, seed=5) for r in range(3)]
+    sends = [c.compress(g.clone(), None, 0).clone() for c, g in zip(cs, gs)]
+    summed = sum(sends)
+    out = torch.zeros(N)
+    cs[0].decompress(summed, None, out, world=3)
+    mask = out != 0
+    exp = sum(g * mask for g in gs) / 3
+    torch.testing.assert_close(out, exp, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_threshold_codec_equals_oracle(adaptive):
+    plan, N = plan_for(SIZES)
+    g = torch.randn(N)
+    c = codecs.ThresholdCodec(plan, 1, 0, V=1.5, adaptive=adaptive)
+    out = torch.zeros(N)
+    c.decompress(c.compress(g.clone(), None, 0), None, out, world=1)
+    for s, x in segs(plan, out):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        exp = ref.adaptive_threshold(g[o:o + n]) if adaptive else ref.thresholdv(g[o:o + n], 1.5)
+        assert torch.equal(x, exp)
+
+
+@pytest.mark.parametrize("make", [lambda p: codecs.TernGradCodec(p, 1, 0, seed=3),
+                                  lambda p: codecs.QSGDCodec(p, 1, 0, 255, seed=3),
+                                  lambda p: codecs.QSGDCodec(p, 1, 0, 7, seed=3),
+                                  lambda p: codecs.QSGDCodec(p, 1, 0, 4000, seed=3)])
+def test_quantisers_unbiased_and_ef(make):
+    plan, N = plan_for([1000, 513])
+    g = torch.randn(N)
+    c = make(plan)
+    acc = torch.zeros(N)
+    T = 200
+    for step in range(T):
+        out = torch.zeros(N)
+        c.decompress(c.compress(g.clone(), None, step), None, out, world=1)
+        acc += out
+    for s, x in segs(plan, acc / T):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        err = (x - g[o:o + n]).abs().mean()
+        assert err < 0.35 * g[o:o + n].abs().max(), err
+    e = torch.zeros(N)
+    out = torch.zeros(N)
+    c.decompress(c.compress(g.clone(), e, 0), None, out, world=1)
+    for s, x in segs(plan, out):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        torch.testing.assert_close(x + e[o:o + n], g[o:o + n], rtol=1e-5, atol=1e-6)
+
+
+def test_terngrad_levels():
+    plan, N = plan_for([300])
+    g = torch.randn(N)
+    c = codecs.TernGradCodec(plan, 1, 0, seed=1)
+    out = torch.zeros(N)
+    c.decompress(c.compress(g.clone(), None, 0), None, out, world=1)
+    s = g[:300].abs().max()
+    assert torch.all((out[:300] == 0) | (out[:300].abs() == s))
+
+
+def test_make_codec_factory_and_auto_wire():
+    plan, N = plan_for(SIZES)
+    assert isinstance(codecs.make_codec("none", plan, 2, 0), codecs.DenseCodec)
+    assert isinstance(codecs.make_codec("Topk", plan, 2, 0, K=0.001), codecs.TopkCodec)
+    assert isinstance(codecs.make_codec("Topk", plan, 8, 0, K=0.5), codecs.DenseWrap)
+    assert isinstance(codecs.make_codec("Topk", plan, 2, 0, K=0), codecs.DenseCodec)
+    assert isinstance(codecs.make_codec("Randomk", plan, 2, 0, K=0.1), codecs.RandkCodec)
+    assert isinstance(codecs.make_codec("QSGD", plan, 2, 0, qstates=255), codecs.QSGDCodec)
+    assert isinstance(codecs.make_codec("Topk", plan, 2, 0, K=0.01, wire="dense"),
+                      codecs.DenseWrap)
+
+
+def test_dense_wrap_matches_reference_wire():
+    plan, N = plan_for(SIZES)
+    g = torch.randn(N)
+    c = codecs.make_codec("Topk", plan, 1, 0, K=0.01, wire="dense")
+    x = g.clone()
+    c.decompress(c.compress(x, None, 0), None, x, world=1)
+    for s, y in segs(plan, x):
+        o, n = int(plan.offsets[s]), int(plan.sizes[s])
+        assert torch.equal(y, ref.topk(g[o:o + n], 0.01))

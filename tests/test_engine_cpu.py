@@ -1,0 +1,141 @@
+"""Single-process engine / arena / DDP / optimizer behaviour on CPU."""
+import pytest
+import torch
+from torch import nn
+
+from layer_wise_aaai20_amd.compress import reference as ref
+from layer_wise_aaai20_amd.models import cifar
+from layer_wise_aaai20_amd.optim.flat_sgd import FlatSGD
+from layer_wise_aaai20_amd.parallel import functional as F
+from layer_wise_aaai20_amd.parallel.arena import GradArena, plan_buckets
+from layer_wise_aaai20_amd.parallel.ddp import CompressedDDP
+from layer_wise_aaai20_amd.parallel.engine import GradSyncEngine
+
+
+def small_net():
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Conv2d(3, 8, 3), nn.BatchNorm2d(8), nn.ReLU(), nn.Flatten(),
+                         nn.Linear(8 * 6 * 6, 10))
+
+
+def test_arena_views_and_reverse_order():
+    m = small_net().to(memory_format=torch.channels_last)
+    a = GradArena(list(m.named_parameters()))
+    assert [s.name for s in a.segments][0] == "4.bias"          # reverse registration order
+    m(torch.randn(2, 3, 8, 8)).sum().backward()
+    for s in a.segments:
+        assert s.param.grad.data_ptr() == a.grad.data_ptr() + s.offset * 4
+        assert s.offset % 64 == 0
+    w = m[0].weight
+    assert w.grad.stride() == w.stride()                         # channels_last grad view
+    assert float(a.grad.abs().sum()) > 0
+
+
+def test_bucket_plan_caps_and_entire_model():
+    m = cifar.build_network("resnet9")
+    a = GradArena(list(m.named_parameters()))
+    bs = plan_buckets(a, "layerwise", 4 * 2 ** 20)
+    assert bs[0].start == 0 and bs[-1].end == a.numel
+    assert all(b1.end == b2.start for b1, b2 in zip(bs, bs[1:]))
+    assert len(bs) > 2
+    assert len(plan_buckets(a, "entiremodel", 1)) == 1
+
+
+@pytest.mark.parametrize("mode", ["layerwise", "entiremodel"])
+@pytest.mark.parametrize("method,kw", [("Topk", dict(K=0.01)), ("Thresholdv", dict(V=1e-3)),
+                                       ("AdaptiveThreshold", {}), ("none", {})])
+def test_functional_sync_matches_oracle(mode, method, kw):
+    m = cifar.build_network("resnet9")
+    batch = {"input": torch.randn(4, 3, 32, 32), "target": torch.randint(0, 10, (4,))}
+    m(batch)["loss"].sum().backward()
+    grads = [p.grad.clone() for p in m.parameters()]
+    F.compressed_comm(m, mode, 1, method, kw.get("K"), kw.get("V"), None)
+    if mode == "layerwise":
+        for p, g in zip(m.parameters(), grads):
+            assert torch.equal(p.grad.reshape(-1), ref.compress(g.reshape(-1), method, **kw))
+    else:
+        # entire-model: the compressor sees the concatenation in arena (reverse) order
+        flat = torch.cat([g.reshape(-1) for g in reversed(grads)])
+        exp = ref.compress(flat, method, **kw)
+        got = torch.cat([p.grad.reshape(-1) for p in reversed(list(m.parameters()))])
+        assert torch.equal(got, exp)
+
+
+def test_entire_model_starves_small_layers_layerwise_does_not():
+    m = cifar.build_network("resnet9")
+    m({"input": torch.randn(4, 3, 32, 32), "target": torch.randint(0, 10, (4,))})["loss"] \
+        .sum().backward()
+    F.layerwise_compressed_comm(m, 1, "Topk", 0.001)
+    assert all(int((p.grad != 0).sum()) >= 1 for p in m.parameters())
+
+
+def test_compressed_ddp_hooks_match_functional():
+    torch.manual_seed(1)
+    a = cifar.build_network("resnet9")
+    b = cifar.build_network("resnet9")
+    b.load_state_dict(a.state_dict())
+    batch = {"input": torch.randn(4, 3, 32, 32), "target": torch.randint(0, 10, (4,))}
+    ddp = CompressedDDP(b, compress="layerwise", method="Topk", K=0.01, bucket_cap_mb=2,
+                        flat_params=False)
+    a(batch)["loss"].sum().backward()
+    F.layerwise_compressed_comm(a, 1, "Topk", 0.01)
+    ddp(batch)["loss"].sum().backward()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        assert torch.equal(pa.grad, pb.grad)
+    assert ddp.engine.stats.steps == 1 and len(ddp.engine.buckets) > 1
+
+
+def test_bucket_launch_order_is_strict():
+    m = cifar.build_network("resnet9")
+    eng = GradSyncEngine(m.named_parameters(), "layerwise", "Topk", K=0.01, bucket_cap_mb=1)
+    launched = []
+    eng._launch = lambda bi: launched.append(bi)
+    nb = len(eng.buckets)
+    assert nb >= 3
+    # make the LAST bucket ready first: nothing may launch until bucket 0 is complete
+    for b in reversed(eng.buckets):
+        for s in range(b.seg_lo, b.seg_hi):
+            eng.mark_ready(s)
+        if b.index != 0:
+            assert launched == []
+    assert launched == list(range(nb))
+
+
+def test_check_reduction_detects_unfinished_backward():
+    m = small_net()
+    ddp = CompressedDDP(m, method="Topk", K=0.1, flat_params=False)
+    ddp(torch.randn(2, 3, 8, 8))
+    ddp.engine._active = True
+    with pytest.raises(RuntimeError):
+        ddp(torch.randn(2, 3, 8, 8))
+
+
+def test_flat_sgd_matches_torch_sgd_and_state_dict():
+    ma, mb = small_net(), small_net()
+    mb.load_state_dict(ma.state_dict())
+    arena = GradArena(list(mb.named_parameters()), flat_params=True)
+    bn = [mb[1].weight, mb[1].bias]
+    rest = [p for p in mb.parameters() if all(p is not q for q in bn)]
+    bn_a = [ma[1].weight, ma[1].bias]
+    rest_a = [p for p in ma.parameters() if all(p is not q for q in bn_a)]
+    oa = torch.optim.SGD([{"params": bn_a, "weight_decay": 0}, {"params": rest_a}], lr=0.05,
+                         momentum=0.9, nesterov=True, weight_decay=1e-3)
+    ob = FlatSGD([{"params": bn, "weight_decay": 0}, {"params": rest}], arena, lr=0.05,
+                 momentum=0.9, nesterov=True, weight_decay=1e-3)
+    x = torch.randn(4, 3, 8, 8)
+    for _ in range(4):
+        oa.zero_grad()
+        ma(x).square().mean().backward()
+        arena.zero_()
+        mb(x).square().mean().backward()
+        oa.step()
+        ob.step()
+    for pa, pb in zip(ma.parameters(), mb.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+    sd = ob.state_dict()
+    oc = torch.optim.SGD([{"params": bn_a, "weight_decay": 0}, {"params": rest_a}], lr=0.05,
+                         momentum=0.9, nesterov=True, weight_decay=1e-3)
+    oc.load_state_dict(sd)                       # FlatSGD checkpoints load into torch SGD
+    for k, v in oa.state_dict()["state"].items():
+        torch.testing.assert_close(sd["state"][k]["momentum_buffer"], v["momentum_buffer"],
+                                   rtol=1e-5, atol=1e-6)

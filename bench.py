@@ -103,8 +103,14 @@ def main():
     ms = dt / args.steps * 1e3
     value = world * B * args.steps / dt
     stats = tr.ddp.sync_stats()
+    default = (args.model == "resnet50" and args.compress == "layerwise" and args.method == "Topk"
+               and args.ratio == 0.001)
+    metric = BASELINE_METRIC if default else (
+        f"images/sec/node, {args.model} {args.compress} {args.method}"
+        f"{' K=' + str(args.ratio) if args.method in ('Topk', 'Randomk') else ''}"
+        f"{' +EF' if args.ef else ''}")
     line = {
-        "metric": BASELINE_METRIC,
+        "metric": metric,
         "value": round(value, 2),
         "unit": "images/s",
         "n_gpus": world,

@@ -1,0 +1,87 @@
+#!/usr/bin/env python
+"""CIFAR-10 benchmarks for the BASELINE.json side configs (1 line of JSON per config):
+
+  --config anchor   ResNet-9, no compression (the reference's uncompressed V100 anchor:
+                    ~16.5k img/s fp16, CIFAR10/experiments.ipynb:11222)
+  --config vgg16    VGG-16 layer-wise Top-K k=0.1 % (BASELINE config 2)
+  --config alexnet  AlexNet (graph) entire-model Top-K k=1 % + error feedback (config 3)
+  --config all      every one of the above
+
+Synthetic data (random images with class-dependent colour bias), random init, batch 512 per GPU,
+bf16 autocast. Multi-GPU: ``torchrun --nproc-per-node N bench_cifar.py``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+CONFIGS = {
+    "anchor": dict(network="resnet9", compress="none", method="none"),
+    "vgg16": dict(network="vgg16", compress="layerwise", method="Topk", K=0.001),
+    "alexnet": dict(network="alexnet", compress="entiremodel", method="Topk", K=0.01,
+                    error_feedback=True),
+}
+V100_ANCHOR = 16500.0    # img/s, derived in BASELINE.md
+
+
+def run(name, steps, warmup, world, rank, dev):
+    from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
+    cfg = CONFIGS[name]
+    tr = CifarTrainer(device=dev, n_train=512 * 12, **cfg)
+    for _ in range(warmup):
+        tr.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    value = world * tr.bs * steps / dt
+    st = tr.ddp.sync_stats()
+    return {"metric": f"CIFAR-10 {cfg['network']} {cfg['compress']} {cfg['method']} images/s",
+            "value": round(value, 1), "unit": "images/s", "n_gpus": world, "steps": steps,
+            "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": round(value / V100_ANCHOR, 3) if name == "anchor"
+            else None, "dtype": "bf16", "data": "synthetic",
+            "config": dict(cfg, global_batch=world * tr.bs, parallelism=f"dp{world}",
+                           wire_bytes_per_rank=st.payload_bytes, dense_grad_bytes=st.dense_bytes)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="all", choices=["all"] + list(CONFIGS))
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=8)
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    torch.backends.cudnn.benchmark = True
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    names = list(CONFIGS) if args.config == "all" else [args.config]
+    for n in names:
+        line = run(n, args.steps, args.warmup, world, rank, dev)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -304,7 +304,7 @@ void check_nhwc(const Tensor& t, const char* name) {
 
 int64_t channels_of(const Tensor& x) { return x.size(1); }
 
-std::tuple<Tensor, Tensor, Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res,
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res,
                                           c10::optional<Tensor> weight,
                                           c10::optional<Tensor> bias, c10::optional<Tensor> rmean,
                                           c10::optional<Tensor> rvar, bool training,
@@ -322,7 +322,8 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res,
   auto f32 = x.options().dtype(at::kFloat);
   Tensor y = at::empty_like(x);
   Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32);
-  Tensor scale = at::empty({C}, f32), shift = at::empty({C}, f32);
+  Tensor scale_shift = at::empty({2 * C}, f32);
+  Tensor scale = scale_shift.narrow(0, 0, C), shift = scale_shift.narrow(0, C, C);
   lw::BNArgs a{};
   a.x = x.data_ptr();
   a.res = (res.has_value() && res->defined()) ? res->data_ptr() : nullptr;
@@ -358,18 +359,20 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd(Tensor x, c10::optional<Tensor> res,
     a.shift = ptr<float>(shift);
   }
   lw::bn_forward(a, cur_stream());
-  return {y, mean, invstd};
+  // scale/shift as used by the forward: lets the backward recompute the ReLU mask from x
+  return {y, mean, invstd, scale_shift};
 }
 
 std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y,
                                                   c10::optional<Tensor> weight, Tensor mean,
-                                                  Tensor invstd, bool training, bool relu,
-                                                  bool need_dres) {
+                                                  Tensor invstd, c10::optional<Tensor> scale_shift,
+                                                  bool training, bool relu, bool need_dres) {
   const c10::DeviceGuard guard(x.device());
   check_nhwc(x, "x");
   check_nhwc(dy, "dy");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.sizes() == x.sizes(), "dy must match x");
-  if (relu) {
+  const bool have_ss = scale_shift.has_value() && scale_shift->defined();
+  if (relu && !have_ss) {
     TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
     check_nhwc(*y, "y");
   }
@@ -384,7 +387,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
   lw::BNArgs a{};
   a.x = x.data_ptr();
   a.dy = dy.data_ptr();
-  a.y = relu ? y->data_ptr() : nullptr;
+  a.y = (relu && !have_ss) ? y->data_ptr() : nullptr;
+  if (relu && have_ss) {
+    TORCH_CHECK(scale_shift->numel() == 2 * C, "scale_shift must hold 2*C floats");
+    a.scale = ptr<float>(*scale_shift);
+    a.shift = a.scale + C;
+  }
   a.dx = dx.data_ptr();
   a.dres = need_dres ? dres.data_ptr() : nullptr;
   a.M = M;
@@ -442,10 +450,11 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "bn_fwd(Tensor x, Tensor? res, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
       "Tensor(b!)? running_var, bool training, float momentum, float eps, bool relu) "
-      "-> (Tensor, Tensor, Tensor)");
+      "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "bn_bwd(Tensor dy, Tensor x, Tensor? y, Tensor? weight, Tensor mean, Tensor invstd, "
-      "bool training, bool relu, bool need_dres) -> (Tensor, Tensor, Tensor, Tensor)");
+      "Tensor? scale_shift, bool training, bool relu, bool need_dres) "
+      "-> (Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {

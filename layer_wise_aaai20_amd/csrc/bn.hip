@@ -60,11 +60,15 @@ template <> struct V8<float> {
 // Thread (g, r): channel group g (8 channels), row lane r of R = BNT/G. 4 rows in flight per lane.
 // partial: [gridDim.x][2C]
 // ------------------------------------------------------------------------------------------
-template <typename T, int MODE, bool RELU>
+// RELU: 0 none, 1 mask from the saved output y, 2 mask recomputed from x: x*scale+shift > 0
+// (bit-identical to the forward's test, which evaluated the same fp32 expression).
+template <typename T, int MODE, int RELU>
 __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, const T* __restrict__ dy,
                                                    const T* __restrict__ y,
-                                                   const float* __restrict__ mean, int64_t M, int C,
-                                                   int64_t rows_per_block,
+                                                   const float* __restrict__ mean,
+                                                   const float* __restrict__ fscale,
+                                                   const float* __restrict__ fshift, int64_t M,
+                                                   int C, int64_t rows_per_block,
                                                    float* __restrict__ partial) {
   __shared__ float sa[BNT * 8];
   __shared__ float sb[BNT * 8];
@@ -72,12 +76,16 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
   const int R = BNT / G;                    // rows processed per iteration (>= 1)
   const int g = threadIdx.x % G, r = threadIdx.x / G;
   const bool active = r < R;
-  float a[8], b[8], mu[8];
+  float a[8], b[8], mu[8], fs[8], fh[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { a[k] = 0.f; b[k] = 0.f; mu[k] = 0.f; }
+  for (int k = 0; k < 8; ++k) { a[k] = 0.f; b[k] = 0.f; mu[k] = 0.f; fs[k] = 0.f; fh[k] = 0.f; }
   if (MODE == 1 && active) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) mu[k] = mean[g * 8 + k];
+    if (RELU == 2) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { fs[k] = fscale[g * 8 + k]; fh[k] = fshift[g * 8 + k]; }
+    }
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(r0 + rows_per_block, M);
@@ -94,7 +102,7 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
       if (MODE == 1) {
 #pragma unroll
         for (int u = 0; u < U; ++u) V8<T>::load(dp + (row + u * R) * C, d[u]);
-        if (RELU) {
+        if (RELU == 1) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             float yv[8];
@@ -102,6 +110,12 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
 #pragma unroll
             for (int k = 0; k < 8; ++k) d[u][k] = yv[k] > 0.f ? d[u][k] : 0.f;
           }
+        } else if (RELU == 2) {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              d[u][k] = fmaf(xv[u][k], fs[k], fh[k]) > 0.f ? d[u][k] : 0.f;
         }
       }
 #pragma unroll
@@ -122,11 +136,14 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
       } else {
         float d[8];
         V8<T>::load(dp + row * C, d);
-        if (RELU) {
+        if (RELU == 1) {
           float yv[8];
           V8<T>::load(yp + row * C, yv);
 #pragma unroll
           for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
+        } else if (RELU == 2) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) d[k] = fmaf(xv[k], fs[k], fh[k]) > 0.f ? d[k] : 0.f;
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) { a[k] += d[k]; b[k] += d[k] * (xv[k] - mu[k]); }
@@ -221,7 +238,7 @@ __global__ __launch_bounds__(BNT) void k_bn_apply(const T* __restrict__ x, const
     for (int u = 0; u < 2; ++u) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        float t = v[u][k] * sc[k] + sh[k];
+        float t = fmaf(v[u][k], sc[k], sh[k]);
         if (RES) t += rr[u][k];
         if (RELU) t = fmaxf(t, 0.f);
         v[u][k] = t;
@@ -235,7 +252,7 @@ __global__ __launch_bounds__(BNT) void k_bn_apply(const T* __restrict__ x, const
     if (RES) V8<T>::load(res + i * 8, rr);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float t = v[k] * sc[k] + sh[k];
+      float t = fmaf(v[k], sc[k], sh[k]);
       if (RES) t += rr[k];
       if (RELU) t = fmaxf(t, 0.f);
       v[k] = t;
@@ -270,9 +287,11 @@ __global__ __launch_bounds__(256) void k_bn_finalize_bwd(
 }
 
 // dx = A*dy' + B*x + C ; dres = dy'
-template <typename T, bool RELU, bool DRES>
+template <typename T, int RELU, bool DRES>
 __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ dy,
                                                       const T* __restrict__ y,
+                                                      const float* __restrict__ fscale,
+                                                      const float* __restrict__ fshift,
                                                       const float* __restrict__ A,
                                                       const float* __restrict__ B,
                                                       const float* __restrict__ Cc,
@@ -282,19 +301,26 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, c
   const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
   const int64_t step = (int64_t)gridDim.x * BNT;
   const int c0 = (int)(t0 % G) * 8;
-  float ca[8], cb[8], cc[8];
+  float ca[8], cb[8], cc[8], fs[8], fh[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { ca[k] = A[c0 + k]; cb[k] = B[c0 + k]; cc[k] = Cc[c0 + k]; }
+  for (int k = 0; k < 8; ++k) {
+    ca[k] = A[c0 + k]; cb[k] = B[c0 + k]; cc[k] = Cc[c0 + k];
+    fs[k] = RELU == 2 ? fscale[c0 + k] : 0.f;
+    fh[k] = RELU == 2 ? fshift[c0 + k] : 0.f;
+  }
   for (int64_t i = t0; i < n8; i += step) {
     const int64_t off = i * 8;
     float xv[8], d[8];
     V8<T>::load(x + off, xv);
     V8<T>::load(dy + off, d);
-    if (RELU) {
+    if (RELU == 1) {
       float yv[8];
       V8<T>::load(y + off, yv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
+    } else if (RELU == 2) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = fmaf(xv[k], fs[k], fh[k]) > 0.f ? d[k] : 0.f;
     }
     if (DRES) V8<T>::store(dres + off, d);
     float o[8];
@@ -346,8 +372,9 @@ static void bn_forward_t(const BNArgs& a, hipStream_t st) {
     int64_t rpb;
     int nb;
     reduce_geometry(a.M, a.C, rpb, nb);
-    hipLaunchKernelGGL((k_bn_reduce<T, 0, false>), dim3(nb), dim3(BNT), 0, st, x, (const T*)nullptr,
-                       (const T*)nullptr, (const float*)nullptr, a.M, a.C, rpb, a.partial);
+    hipLaunchKernelGGL((k_bn_reduce<T, 0, 0>), dim3(nb), dim3(BNT), 0, st, x, (const T*)nullptr,
+                       (const T*)nullptr, (const float*)nullptr, (const float*)nullptr,
+                       (const float*)nullptr, a.M, a.C, rpb, a.partial);
     hipLaunchKernelGGL(k_bn_finalize_fwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
                        a.C, a.M, a.gamma, a.beta, a.eps, a.momentum, a.rmean, a.rvar, a.mean,
                        a.invstd, a.scale, a.shift);
@@ -373,19 +400,23 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   int64_t rpb;
   int nb;
   reduce_geometry(a.M, a.C, rpb, nb);
-  if (a.relu)
-    hipLaunchKernelGGL((k_bn_reduce<T, 1, true>), dim3(nb), dim3(BNT), 0, st, x, dy, y, a.mean, a.M, a.C, rpb, a.partial);
-  else
-    hipLaunchKernelGGL((k_bn_reduce<T, 1, false>), dim3(nb), dim3(BNT), 0, st, x, dy, y, a.mean, a.M, a.C, rpb, a.partial);
+  // relu mask: recompute from x when the forward had no residual (saves reading y)
+  const int rmode = !a.relu ? 0 : (a.scale ? 2 : 1);
+#define LW_RED(R)                                                                                \
+  hipLaunchKernelGGL((k_bn_reduce<T, 1, R>), dim3(nb), dim3(BNT), 0, st, x, dy, y, a.mean, a.scale, \
+                     a.shift, a.M, a.C, rpb, a.partial)
+  if (rmode == 0) LW_RED(0); else if (rmode == 1) LW_RED(1); else LW_RED(2);
+#undef LW_RED
   hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
                      a.C, a.M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
                      (int)a.training);
   const dim3 grid(apply_grid(n8, a.C)), block(BNT);
 #define LW_BWD(R, D)                                                                            \
-  hipLaunchKernelGGL((k_bn_bwd_apply<T, R, D>), grid, block, 0, st, x, dy, y, a.A, a.B, a.Cc, dx, \
-                     dres, n8, a.C)
-  if (a.relu) { if (dres) LW_BWD(true, true); else LW_BWD(true, false); }
-  else { if (dres) LW_BWD(false, true); else LW_BWD(false, false); }
+  hipLaunchKernelGGL((k_bn_bwd_apply<T, R, D>), grid, block, 0, st, x, dy, y, a.scale, a.shift,  \
+                     a.A, a.B, a.Cc, dx, dres, n8, a.C)
+  if (rmode == 1) { if (dres) LW_BWD(1, true); else LW_BWD(1, false); }
+  else if (rmode == 2) { if (dres) LW_BWD(2, true); else LW_BWD(2, false); }
+  else { if (dres) LW_BWD(0, true); else LW_BWD(0, false); }
 #undef LW_BWD
 }
 

@@ -47,20 +47,26 @@ class _FusedBN(torch.autograd.Function):
         x = _nhwc(x)
         if residual is not None:
             residual = _nhwc(residual).to(x.dtype)
-        y, mean, invstd = lib.bn_fwd(x, residual, weight, bias, running_mean, running_var,
-                                     bool(training), float(momentum), float(eps), bool(relu))
-        ctx.save_for_backward(x, y if relu else None, weight, mean, invstd)
+        y, mean, invstd, scale_shift = lib.bn_fwd(x, residual, weight, bias, running_mean,
+                                                  running_var, bool(training), float(momentum),
+                                                  float(eps), bool(relu))
+        # ReLU mask in backward: recomputed from x (saved scale/shift) unless a residual was
+        # added before the ReLU, in which case the output y is kept instead.
+        if relu and residual is None:
+            ctx.save_for_backward(x, None, weight, mean, invstd, scale_shift)
+        else:
+            ctx.save_for_backward(x, y if relu else None, weight, mean, invstd, None)
         ctx.flags = (bool(training), bool(relu), residual is not None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, mean, invstd = ctx.saved_tensors
+        x, y, weight, mean, invstd, scale_shift = ctx.saved_tensors
         training, relu, has_res = ctx.flags
         lib = load()
         dy = _nhwc(dy).to(x.dtype)
-        dx, dgamma, dbeta, dres = lib.bn_bwd(dy, x, y, weight, mean, invstd, training, relu,
-                                             has_res)
+        dx, dgamma, dbeta, dres = lib.bn_bwd(dy, x, y, weight, mean, invstd, scale_shift,
+                                             training, relu, has_res)
         need_w = weight is not None and ctx.needs_input_grad[2]
         need_b = ctx.needs_input_grad[3]
         return (dx, dres if has_res else None, dgamma if need_w else None,
@@ -94,7 +100,8 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
     def forward(self, x, residual=None):
         momentum = 0.0 if self.momentum is None else self.momentum
         if self.training and self.track_running_stats and self.num_batches_tracked is not None:
-            self.num_batches_tracked.add_(1)
+            if not getattr(self, "_shared_counter", False) or self.momentum is None:
+                self.num_batches_tracked.add_(1)
             if self.momentum is None:
                 momentum = 1.0 / float(self.num_batches_tracked)
         training = self.training or not self.track_running_stats
@@ -105,6 +112,27 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
 
     def extra_repr(self):
         return super().extra_repr() + (", fused_relu=True" if self.fuse_relu else "")
+
+
+def share_bn_counters(model: nn.Module) -> nn.Module:
+    """Make every BN's ``num_batches_tracked`` a view into one int64 vector, bumped by ONE kernel
+    per training forward (a pre-forward hook) instead of one launch per BN layer. Call after the
+    model is on its final device; buffer names / state_dict are unchanged."""
+    bns = [m for m in model.modules() if isinstance(m, FusedBatchNorm2d)
+           and m.track_running_stats and m.momentum is not None]
+    if not bns:
+        return model
+    flat = torch.stack([m.num_batches_tracked.detach().reshape(()) for m in bns])
+    for i, m in enumerate(bns):
+        m._buffers["num_batches_tracked"] = flat[i]
+        m._shared_counter = True
+
+    def bump(mod, args):
+        if mod.training:
+            flat.add_(1)
+    model._bn_counter = flat
+    model.register_forward_pre_hook(bump)
+    return model
 
 
 def to_fused_bn(bn: nn.BatchNorm2d, relu: bool = False) -> FusedBatchNorm2d:
@@ -158,3 +186,33 @@ def fuse_resnet(model: nn.Module) -> nn.Module:
         to_fused_bn(model.bn1, relu=True)
         model.forward = types.MethodType(_fused_resnet_forward, model)
     return model
+
+
+def fuse_graph_network(net: nn.Module) -> nn.Module:
+    """Fuse ``bn -> relu`` node pairs of a dict-graph :class:`~..models.graph.Network` (ResNet-9,
+    graph AlexNet): the BN becomes a FusedBatchNorm2d(relu=True), the ReLU node an Identity.
+    Only pairs where the ReLU is the BN's sole consumer are fused."""
+    from ..models.graph import Identity
+    graph = getattr(net, "graph", None)
+    if graph is None:
+        return net
+    names = list(graph)
+    consumers = {}
+    for k, (_, ins) in graph.items():
+        for i in ins:
+            consumers.setdefault(i, []).append(k)
+    for k in names:
+        mod, _ = graph[k]
+        if not isinstance(mod, nn.BatchNorm2d) or isinstance(mod, FusedBatchNorm2d):
+            continue
+        users = consumers.get(k, [])
+        if len(users) != 1:
+            continue
+        r = users[0]
+        rmod, rins = graph[r]
+        if isinstance(rmod, nn.ReLU) and rins == [k]:
+            to_fused_bn(mod, relu=True)
+            ident = Identity()
+            graph[r] = (ident, rins)
+            net._modules[r] = ident
+    return net

@@ -1,0 +1,80 @@
+"""GPU-resident CIFAR-10 trainer used by ``bench_cifar.py`` (BASELINE configs 2, 3 and the
+uncompressed ResNet-9 anchor).
+
+Recipe of ``CIFAR10/dawn.py:105-148``: batch 512 per rank, summed cross-entropy with a per-sample
+LR (``PiecewiseLinear([0,5,E],[0,0.4,0]) / bs``), SGD weight decay ``5e-4·bs``, Nesterov momentum
+0.9, crop / flip / cutout augmentation. MI355X path: the dataset lives in HBM and is augmented
+there (``GPUBatches``), bf16 autocast + channels_last, fused BN+ReLU in the graph networks,
+CompressedDDP (compression overlapped with backward) and the fused flat-arena SGD.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..data import cifar as D
+from ..models.cifar import build_network
+from ..ops import nn as lwnn
+from ..optim.flat_sgd import FlatSGD
+from ..parallel.ddp import CompressedDDP
+from ..utils.logging import PiecewiseLinear
+
+
+class CifarTrainer:
+    def __init__(self, network="resnet9", device=None, compress="none", method="none", K=None,
+                 V=None, qstates=None, error_feedback=False, batch_size=512, epochs=24,
+                 momentum=0.9, dtype=torch.bfloat16, bucket_cap_mb=25.0, wire="auto",
+                 n_train=50000, seed=0, fused=True):
+        self.device = torch.device(device or "cuda")
+        self.dtype = dtype
+        self.bs = batch_size
+        net = build_network(network)
+        if fused and self.device.type == "cuda":
+            lwnn.fuse_graph_network(net)
+        net = net.to(self.device)
+        if self.device.type == "cuda":
+            net = net.to(memory_format=torch.channels_last)
+        self.model = net
+        self.ddp = CompressedDDP(net, compress=compress, method=method, K=K, V=V,
+                                 qstates=qstates, error_feedback=error_feedback,
+                                 bucket_cap_mb=bucket_cap_mb, wire=wire, flat_params=True)
+        self.opt = FlatSGD(net.parameters(), self.ddp.arena, lr=0.0, momentum=momentum,
+                           nesterov=momentum > 0, weight_decay=5e-4 * batch_size)
+        ds = D.synthetic_cifar10(n_train, 1000, seed)
+        x = D.transpose(D.normalise(D.pad(ds["train"]["data"], 4)))
+        self.batches = D.GPUBatches(torch.from_numpy(np.ascontiguousarray(x)).to(self.device),
+                                    torch.as_tensor(ds["train"]["labels"]).to(self.device),
+                                    batch_size, shuffle=True, augment=True, drop_last=True,
+                                    seed=seed, channels_last=self.device.type == "cuda",
+                                    dtype=torch.float32)
+        self.sched = PiecewiseLinear([0, 5, epochs], [0, 0.4, 0])
+        self.steps_per_epoch = len(self.batches)
+        self.step_count = 0
+        self._it = None
+        self.last = None
+
+    def next_batch(self):
+        if self._it is None:
+            self._it = iter(self.batches)
+        try:
+            return next(self._it)
+        except StopIteration:
+            self._it = iter(self.batches)
+            return next(self._it)
+
+    def step(self, batch=None):
+        batch = batch or self.next_batch()
+        lr = self.sched(self.step_count / self.steps_per_epoch) / self.bs
+        for g in self.opt.param_groups:
+            g["lr"] = lr
+        with torch.autocast(device_type=self.device.type, dtype=self.dtype,
+                            enabled=self.dtype != torch.float32):
+            out = self.ddp(batch)
+            loss = out["loss"].float().sum()
+        loss.backward()
+        self.opt.step()
+        self.step_count += 1
+        self.last = out
+        return loss

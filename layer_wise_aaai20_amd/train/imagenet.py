@@ -92,6 +92,8 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
     net = net.to(device)
     if device.type == "cuda":
         net = net.to(memory_format=torch.channels_last)
+    if fused:
+        lwnn.share_bn_counters(net)
     ddp = CompressedDDP(net, compress=compress, method=method, K=K, V=V, qstates=qstates,
                         error_feedback=error_feedback, bucket_cap_mb=bucket_cap_mb, wire=wire,
                         flat_params=True)

@@ -1,0 +1,43 @@
+#!/usr/bin/env python
+"""Steady-state per-step breakdown from a rocprofv3 kernel_trace.csv: step boundaries are the
+fused-SGD kernel launches (one per step); only the last N steps are summarised, so MIOpen's
+find-mode search in the warm-up does not pollute the numbers."""
+import csv
+import re
+import sys
+
+sys.path.insert(0, __file__.rsplit("/", 1)[0])
+from prof_summary import CATS  # noqa: E402
+
+
+def main(path, last=5, verbose=False):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    sgd = [i for i, r in enumerate(rows) if "k_sgd" in r["Kernel_Name"]]
+    if len(sgd) < last + 1:
+        raise SystemExit(f"only {len(sgd)} steps in trace")
+    lo, hi = sgd[-last - 1] + 1, sgd[-1] + 1
+    sel = rows[lo:hi]
+    wall = (int(rows[hi - 1]["End_Timestamp"]) - int(rows[lo]["Start_Timestamp"])) / 1e6 / last
+    tot, names, busy = {}, {}, 0.0
+    for r in sel:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        busy += d
+        n = r["Kernel_Name"]
+        cat = next((c for c, p in CATS if re.search(p, n)), "other")
+        tot[cat] = tot.get(cat, 0.0) + d
+        key = n[:100]
+        names.setdefault(cat, {}).setdefault(key, [0.0, 0])
+        names[cat][key][0] += d
+        names[cat][key][1] += 1
+    print(f"steps={last}  wall/step={wall:.3f} ms  kernel-busy/step={busy / last:.3f} ms  "
+          f"kernels/step={len(sel) / last:.0f}")
+    for c, t in sorted(tot.items(), key=lambda x: -x[1]):
+        print(f"  {c:28s} {t / last:8.3f} ms  {100 * t / busy:5.1f}%")
+        if verbose:
+            for k, (t2, n2) in sorted(names[c].items(), key=lambda x: -x[1][0])[:6]:
+                print(f"      {t2 / last:7.3f}  x{n2 // last:<4d} {k}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 5, "-v" in sys.argv)

@@ -413,6 +413,55 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
   return {dx, dgamma, dbeta, dres};
 }
 
+// ---------------------------------------------------------------- MFMA GEMM
+Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b_kcontig,
+            int64_t M, int64_t N, int64_t K, c10::optional<Tensor> bias, bool relu,
+            int64_t splits, bool out_bf16) {
+  const c10::DeviceGuard guard(A.device());
+  TORCH_CHECK(A.is_cuda() && B.is_cuda(), "gemm needs GPU tensors");
+  check_dtype(A, at::kBFloat16, "A");
+  check_dtype(B, at::kBFloat16, "B");
+  TORCH_CHECK(A.is_contiguous() && B.is_contiguous(), "gemm operands must be contiguous");
+  check_aligned16(A.data_ptr(), "A");
+  check_aligned16(B.data_ptr(), "B");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "leading dimensions must be multiples of 8");
+  TORCH_CHECK(K % 8 == 0, "K must be a multiple of 8");
+  TORCH_CHECK(a_kcontig || M % 8 == 0, "M must be a multiple of 8 for an M-contiguous A");
+  TORCH_CHECK(b_kcontig || N % 8 == 0, "N must be a multiple of 8 for an N-contiguous B");
+  TORCH_CHECK(N % 8 == 0 || !out_bf16 || true, "");
+  TORCH_CHECK(A.numel() >= (a_kcontig ? (M - 1) * lda + K : (K - 1) * lda + M), "A too small");
+  TORCH_CHECK(B.numel() >= (b_kcontig ? (N - 1) * ldb + K : (K - 1) * ldb + N), "B too small");
+  Tensor C = at::empty({M, N}, A.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  const int zs = lw::gemm_splits_used((int)K, (int)splits);
+  Tensor partial;
+  lw::GemmArgs g{};
+  g.A = ptr<uint16_t>(A);
+  g.lda = lda;
+  g.a_kcontig = a_kcontig;
+  g.B = ptr<uint16_t>(B);
+  g.ldb = ldb;
+  g.b_kcontig = b_kcontig;
+  g.C = C.data_ptr();
+  g.ldc = N;
+  g.out_bf16 = out_bf16;
+  if (bias.has_value() && bias->defined()) {
+    check_dtype(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == N, "bias size");
+    g.bias = ptr<float>(*bias);
+  }
+  g.relu = relu;
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.splits = (int)splits;
+  if (zs > 1) {
+    partial = at::empty({(int64_t)zs * M * N}, A.options().dtype(at::kFloat));
+    g.partial = ptr<float>(partial);
+  }
+  lw::gemm_bf16(g, cur_stream());
+  return C;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(lwaaai, m) {
@@ -455,6 +504,9 @@ TORCH_LIBRARY(lwaaai, m) {
       "bn_bwd(Tensor dy, Tensor x, Tensor? y, Tensor? weight, Tensor mean, Tensor invstd, "
       "Tensor? scale_shift, bool training, bool relu, bool need_dres) "
       "-> (Tensor, Tensor, Tensor, Tensor)");
+  m.def(
+      "gemm(Tensor A, int lda, bool a_kcontig, Tensor B, int ldb, bool b_kcontig, int M, int N, "
+      "int K, Tensor? bias, bool relu, int splits, bool out_bf16) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
@@ -469,4 +521,5 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("normalize_u8", &normalize_u8);
   m.impl("bn_fwd", &bn_fwd);
   m.impl("bn_bwd", &bn_bwd);
+  m.impl("gemm", &gemm);
 }

@@ -132,6 +132,26 @@ int bn_reduce_blocks(int64_t M, int C);
 void bn_forward(const BNArgs& a, hipStream_t st);
 void bn_backward(const BNArgs& a, hipStream_t st);
 
+// bf16 MFMA GEMM with fused epilogue (gemm.hip)
+struct GemmArgs {
+  const uint16_t* A;  // bf16
+  int64_t lda;
+  bool a_kcontig;     // A(m,k) = A[m*lda+k] (true) or A[k*lda+m] (false)
+  const uint16_t* B;
+  int64_t ldb;
+  bool b_kcontig;     // B(k,n) = B[n*ldb+k] (true) or B[k*ldb+n] (false)
+  void* C;            // [M, ldc] row-major, bf16 or fp32
+  int64_t ldc;
+  bool out_bf16;
+  const float* bias;  // [N] or nullptr
+  int relu;
+  int M, N, K;
+  int splits;         // split-K factor (>1 needs `partial`)
+  float* partial;     // [splits][M][N] fp32
+};
+void gemm_bf16(const GemmArgs& g, hipStream_t st);
+int gemm_splits_used(int K, int splits);
+
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
                   const float stdv[3], bool bf16, hipStream_t st);

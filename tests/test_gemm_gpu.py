@@ -1,0 +1,63 @@
+"""Hand-written MFMA GEMM vs fp32 torch matmul (all four operand layouts, bias/ReLU epilogue,
+split-K, ragged edges) and the MFMALinear layer vs nn.Linear."""
+import pytest
+import torch
+
+from layer_wise_aaai20_amd.ops import gemm as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(A, B):
+    return A.float() @ B.float()
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 32), (256, 384, 512), (200, 136, 72),
+                                   (1000, 64, 2048), (64, 1000, 136), (8, 16, 8)])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_layouts(M, N, K, a_kc, b_kc, splits):
+    torch.manual_seed(0)
+    if not a_kc and M % 8:
+        pytest.skip("M-contiguous A needs M % 8 == 0")
+    if not b_kc and N % 8:
+        pytest.skip("N-contiguous B needs N % 8 == 0")
+    Am = torch.randn(M, K, device="cuda").bfloat16()      # logical A[m][k]
+    Bm = torch.randn(K, N, device="cuda").bfloat16()      # logical B[k][n]
+    A = Am.contiguous() if a_kc else Am.t().contiguous()  # stored [M][K] or [K][M]
+    B = Bm.t().contiguous() if b_kc else Bm.contiguous()  # stored [N][K] or [K][N]
+    lda = K if a_kc else M
+    ldb = K if b_kc else N
+    C = G.gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits, False)
+    torch.testing.assert_close(C, _ref(Am, Bm), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_gemm_bias_relu_bf16_out(relu):
+    M, N, K = 300, 264, 96
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = torch.randn(N, K, device="cuda").bfloat16()
+    b = torch.randn(N, device="cuda")
+    y = G.linear_fwd(x, w, b, relu)
+    r = x.float() @ w.float().t() + b
+    r = torch.relu(r) if relu else r
+    torch.testing.assert_close(y.float(), r, rtol=2e-2, atol=5e-2)
+
+
+def test_mfma_linear_matches_nn_linear():
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(256, 136).cuda()
+    ref = torch.nn.Linear(256, 136).cuda()
+    ref.load_state_dict(lin.state_dict())
+    G.to_mfma_linear(lin, fuse_relu=True)
+    x = torch.randn(64, 256, device="cuda", requires_grad=True)
+    xr = x.detach().clone().requires_grad_()
+    y = lin(x)
+    yr = torch.relu(ref(xr.bfloat16().float()))
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=5e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    torch.testing.assert_close(lin.weight.grad, ref.weight.grad, rtol=3e-2, atol=1e-1)
+    torch.testing.assert_close(lin.bias.grad, ref.bias.grad, rtol=3e-2, atol=1e-1)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)

@@ -1,5 +1,10 @@
 """MFMA GEMM vs hipBLASLt (torch.mm) on the model shapes (bf16, fp32 accumulate)."""
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from layer_wise_aaai20_amd.ops import gemm as G
 

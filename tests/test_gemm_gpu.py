@@ -49,11 +49,13 @@ def test_mfma_linear_matches_nn_linear():
     lin = torch.nn.Linear(256, 136).cuda()
     ref = torch.nn.Linear(256, 136).cuda()
     ref.load_state_dict(lin.state_dict())
-    G.to_mfma_linear(lin, fuse_relu=True)
+    with torch.no_grad():                       # same bf16-rounded operands on both sides
+        ref.weight.copy_(ref.weight.bfloat16().float())
+    G.to_mfma_linear(lin, fuse_relu=False)
     x = torch.randn(64, 256, device="cuda", requires_grad=True)
     xr = x.detach().clone().requires_grad_()
     y = lin(x)
-    yr = torch.relu(ref(xr.bfloat16().float()))
+    yr = ref(xr.bfloat16().float())
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=5e-2)
     g = torch.randn_like(yr)
     y.backward(g.bfloat16())

@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-fused", action="store_true", help="disable fused HIP nn kernels")
     ap.add_argument("--json-out", default="")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend (nccl = RCCL on ROCm)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="debug: every rank on cuda:0 (multi-rank plumbing on a 1-GPU box, gloo)")
     ap.add_argument("--miopen-find", type=int, default=1,
                     help="1: let MIOpen benchmark conv solvers once (cudnn.benchmark)")
     return ap.parse_args()
@@ -62,11 +66,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if args.share_gpu:
+        local = 0
     torch.cuda.set_device(local)
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from layer_wise_aaai20_amd.train.imagenet import build_trainer
 

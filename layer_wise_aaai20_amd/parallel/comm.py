@@ -14,6 +14,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+dist = dist  # re-exported for callers that need ReduceOp / backend queries
+
 
 def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized()

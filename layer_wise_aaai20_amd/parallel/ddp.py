@@ -29,7 +29,7 @@ class CompressedDDP(nn.Module):
                  first_bucket_mb: Optional[float] = None, process_group=None,
                  broadcast_buffers: bool = True, wire: str = "auto", seed: int = 2147483647,
                  flat_params: bool = True, check_reduction: bool = True, device_ids=None,
-                 output_device=None, dim: int = 0):
+                 output_device=None, dim: int = 0, timing: bool = False):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -49,7 +49,8 @@ class CompressedDDP(nn.Module):
                                      V=V, qstates=qstates, error_feedback=error_feedback,
                                      bucket_cap_mb=bucket_cap_mb,
                                      first_bucket_mb=first_bucket_mb, wire=wire, seed=seed,
-                                     process_group=process_group, flat_params=flat_params)
+                                     process_group=process_group, flat_params=flat_params,
+                                     timing=timing)
         self._buffers_list = [b for b in module.buffers() if b.is_floating_point() or
                               b.dtype in (torch.int64, torch.int32)]
         self._hooks = []
@@ -106,6 +107,18 @@ class CompressedDDP(nn.Module):
 
     def sync_stats(self):
         return self.engine.stats
+
+    # checkpoint extras: per-rank error-feedback residuals and the step counter (extra keys that
+    # reference readers ignore; SURVEY.md §5 checkpoint row)
+    def compression_state(self) -> dict:
+        e = self.engine
+        return {"step": e.step, "ef": None if e.ef is None else e.ef.detach().clone()}
+
+    def load_compression_state(self, st: dict) -> None:
+        e = self.engine
+        e.step = int(st.get("step", 0))
+        if st.get("ef") is not None and e.ef is not None:
+            e.ef.copy_(st["ef"])
 
     def extra_repr(self) -> str:
         return self.engine.describe()

@@ -61,7 +61,7 @@ class GradSyncEngine:
                  qstates=None, error_feedback: bool = False, bucket_cap_mb: float = 25.0,
                  first_bucket_mb: Optional[float] = None, wire: str = "auto",
                  seed: int = 2147483647, process_group=None, flat_params: bool = False,
-                 world_size: Optional[int] = None):
+                 world_size: Optional[int] = None, timing: bool = False):
         self.mode = canonical_mode(mode)
         self.method = ref.canonical_method(method) if self.mode != "none" else "none"
         self.pg = process_group
@@ -97,8 +97,35 @@ class GradSyncEngine:
                 self.seg_bucket[i] = b.index
         self.step = 0
         self.stats = SyncStats(dense_bytes=self.arena.numel * 4, buckets=len(self.buckets))
+        self.timing = timing and self.device.type == "cuda"
+        self.timings: List[dict] = []
         self._reset_state()
         self.all_reduced_last = True
+        self.verify_plan()
+
+    # ----------------------------------------------------------------- failure detection
+    def plan_signature(self) -> List[int]:
+        """Layout fingerprint: every rank must build the same buckets / codecs, otherwise the
+        collectives would silently pair mismatched payloads (or hang)."""
+        import zlib
+        desc = repr([(b.start, b.end, c.name, getattr(c, "cap_total", 0))
+                     for b, c in zip(self.buckets, self.codecs)]) + self.mode + self.method
+        return [zlib.crc32(desc.encode()) & 0x7FFFFFFF, self.arena.numel, len(self.buckets)]
+
+    def verify_plan(self) -> None:
+        if not comm.is_dist() or comm.world_size(self.pg) == 1:
+            return
+        mine = torch.tensor(self.plan_signature(), dtype=torch.int64,
+                            device=self.device if comm.dist.get_backend(self.pg) == "nccl"
+                            else "cpu")
+        lo, hi = mine.clone(), mine.clone()
+        comm.dist.all_reduce(lo, op=comm.dist.ReduceOp.MIN, group=self.pg)
+        comm.dist.all_reduce(hi, op=comm.dist.ReduceOp.MAX, group=self.pg)
+        if not torch.equal(lo, hi):
+            raise RuntimeError(
+                f"rank {self.rank}: gradient bucket plans differ across ranks (signature "
+                f"{mine.tolist()} vs min {lo.tolist()} / max {hi.tolist()}): the model, the "
+                f"compression settings or the bucket size are not identical on every rank")
 
     # ----------------------------------------------------------------- state machine
     def _reset_state(self):
@@ -134,12 +161,19 @@ class GradSyncEngine:
             self._launch(self._next)
             self._next += 1
 
+    def _event(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
     def _launch(self, bi: int) -> None:
         b = self.buckets[bi]
         codec = self.codecs[bi]
         g = self.arena.grad[b.start:b.end]
         e = self.ef[b.start:b.end] if self.ef is not None else None
+        t0 = self._event() if self.timing else None
         send = codec.compress(g, e, self.step)
+        t1 = self._event() if self.timing else None
         self._payload += codec.last_payload_bytes
         if codec.collective == "all_reduce":
             work = comm.all_reduce(send, self.pg)
@@ -147,7 +181,7 @@ class GradSyncEngine:
         else:
             recv = codec.recv_buffer(send)
             work = comm.all_gather(recv, send, self.pg)
-        self._pending.append((bi, work, send, recv))
+        self._pending.append((bi, work, send, recv, (t0, t1)))
 
     def finish(self) -> None:
         """Launch buckets that never became ready (unused params keep zero grads), wait for every
@@ -155,11 +189,17 @@ class GradSyncEngine:
         for i in range(self._next, len(self.buckets)):
             self._ready[i] = True
         self._launch_in_order()
-        for bi, work, send, recv in self._pending:
+        rec = []
+        for bi, work, send, recv, (t0, t1) in self._pending:
             work.wait()
+            t2 = self._event() if self.timing else None
             b = self.buckets[bi]
             self.codecs[bi].decompress(send, recv, self.arena.grad[b.start:b.end])
+            if self.timing:
+                rec.append((bi, t0, t1, t2, self._event()))
         self._pending = []
+        if self.timing:
+            self._last_events = rec
         self.step += 1
         self.stats.steps += 1
         self.stats.payload_bytes = self._payload
@@ -174,6 +214,17 @@ class GradSyncEngine:
             self._ready[i] = True
         self._launch_in_order()
         self.finish()
+
+    def read_timings(self) -> List[dict]:
+        """Per-bucket µs of the last step: compress, exchange-wait (compress end → collective
+        visible on the compute stream) and decode. Synchronises; call outside the hot loop."""
+        out = []
+        for bi, t0, t1, t2, t3 in getattr(self, "_last_events", []):
+            t3.synchronize()
+            out.append({"bucket": bi, "compress_us": 1e3 * t0.elapsed_time(t1),
+                        "exchange_us": 1e3 * t1.elapsed_time(t2),
+                        "decode_us": 1e3 * t2.elapsed_time(t3)})
+        return out
 
     # ----------------------------------------------------------------- introspection
     def describe(self) -> str:

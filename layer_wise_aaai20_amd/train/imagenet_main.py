@@ -500,6 +500,8 @@ def main(argv=None):
         optimizer.load_state_dict(ckpt["optimizer"])
         if "scheduler" in ckpt:
             scheduler.load_state_dict(ckpt["scheduler"])
+        if "compression" in ckpt and hasattr(model, "load_compression_state"):
+            model.load_compression_state(ckpt["compression"])
         log.console(f"resumed from {args.resume} at epoch {args.start_epoch}")
 
     start_time = datetime.now()
@@ -528,7 +530,11 @@ def main(argv=None):
         is_best = top5 > best_top5
         best_top5 = max(top5, best_top5)
         if args.local_rank == 0 and run.is_master:
-            extra = {"scheduler": scheduler.state_dict()} if args.extra_ckpt else None
+            extra = None
+            if args.extra_ckpt:
+                extra = {"scheduler": scheduler.state_dict()}
+                if hasattr(model, "compression_state"):
+                    extra["compression"] = model.compression_state()
             if is_best:
                 save_checkpoint(run, epoch, model, best_top5, optimizer, is_best=True,
                                 filename="model_best.pth.tar", extra=extra)

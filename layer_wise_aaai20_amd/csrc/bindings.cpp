@@ -414,9 +414,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
 }
 
 // ---------------------------------------------------------------- MFMA GEMM
-Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b_kcontig,
-            int64_t M, int64_t N, int64_t K, c10::optional<Tensor> bias, bool relu,
-            int64_t splits, bool out_bf16) {
+std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb,
+                                   bool b_kcontig, int64_t M, int64_t N, int64_t K,
+                                   c10::optional<Tensor> bias, bool relu, int64_t splits,
+                                   bool out_bf16, int64_t tile, c10::optional<Tensor> pro_scale,
+                                   c10::optional<Tensor> pro_shift, bool pro_on_a,
+                                   bool want_stats) {
   const c10::DeviceGuard guard(A.device());
   TORCH_CHECK(A.is_cuda() && B.is_cuda(), "gemm needs GPU tensors");
   check_dtype(A, at::kBFloat16, "A");
@@ -424,16 +427,15 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
   TORCH_CHECK(A.is_contiguous() && B.is_contiguous(), "gemm operands must be contiguous");
   check_aligned16(A.data_ptr(), "A");
   check_aligned16(B.data_ptr(), "B");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0, "empty GEMM");
   TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "leading dimensions must be multiples of 8");
   TORCH_CHECK(K % 8 == 0, "K must be a multiple of 8");
   TORCH_CHECK(a_kcontig || M % 8 == 0, "M must be a multiple of 8 for an M-contiguous A");
   TORCH_CHECK(b_kcontig || N % 8 == 0, "N must be a multiple of 8 for an N-contiguous B");
-  TORCH_CHECK(N % 8 == 0 || !out_bf16 || true, "");
   TORCH_CHECK(A.numel() >= (a_kcontig ? (M - 1) * lda + K : (K - 1) * lda + M), "A too small");
   TORCH_CHECK(B.numel() >= (b_kcontig ? (N - 1) * ldb + K : (K - 1) * ldb + N), "B too small");
+  TORCH_CHECK(tile >= 0 && tile <= 6, "tile id");
   Tensor C = at::empty({M, N}, A.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
-  const int zs = lw::gemm_splits_used((int)K, (int)splits);
-  Tensor partial;
   lw::GemmArgs g{};
   g.A = ptr<uint16_t>(A);
   g.lda = lda;
@@ -446,7 +448,7 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
   g.out_bf16 = out_bf16;
   if (bias.has_value() && bias->defined()) {
     check_dtype(*bias, at::kFloat, "bias");
-    TORCH_CHECK(bias->numel() == N, "bias size");
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "bias size");
     g.bias = ptr<float>(*bias);
   }
   g.relu = relu;
@@ -454,12 +456,44 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
   g.N = (int)N;
   g.K = (int)K;
   g.splits = (int)splits;
+  g.tile = (int)tile;
+  const bool pro = pro_scale.has_value() && pro_scale->defined();
+  if (pro) {
+    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined(), "prologue needs scale and shift");
+    const int64_t n = pro_on_a ? K : N;
+    TORCH_CHECK(pro_on_a ? a_kcontig : !b_kcontig,
+                "prologue: per-k on a K-contiguous A or per-n on an N-contiguous B");
+    for (const Tensor* t : {&*pro_scale, &*pro_shift}) {
+      check_dtype(*t, at::kFloat, "prologue");
+      TORCH_CHECK(t->numel() >= n && t->is_contiguous(), "prologue vector size");
+      check_aligned16(t->data_ptr(), "prologue");
+    }
+    g.pro_scale = ptr<float>(*pro_scale);
+    g.pro_shift = ptr<float>(*pro_shift);
+    g.pro_on_a = pro_on_a;
+  }
+  const int zs = lw::gemm_splits_used(g);
+  Tensor partial, stats;
   if (zs > 1) {
     partial = at::empty({(int64_t)zs * M * N}, A.options().dtype(at::kFloat));
     g.partial = ptr<float>(partial);
   }
+  if (want_stats) {
+    TORCH_CHECK(zs == 1, "column statistics need splits == 1");
+    stats = at::empty({2, N, (int64_t)lw::gemm_tiles_m(g)}, A.options().dtype(at::kFloat));
+    g.stats = ptr<float>(stats);
+  } else {
+    stats = at::empty({0}, A.options().dtype(at::kFloat));
+  }
   lw::gemm_bf16(g, cur_stream());
-  return C;
+  return {C, stats};
+}
+
+Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b_kcontig,
+            int64_t M, int64_t N, int64_t K, c10::optional<Tensor> bias, bool relu,
+            int64_t splits, bool out_bf16) {
+  return std::get<0>(gemm_ex(A, lda, a_kcontig, B, ldb, b_kcontig, M, N, K, bias, relu, splits,
+                             out_bf16, 0, c10::nullopt, c10::nullopt, true, false));
 }
 
 }  // namespace
@@ -507,6 +541,10 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "gemm(Tensor A, int lda, bool a_kcontig, Tensor B, int ldb, bool b_kcontig, int M, int N, "
       "int K, Tensor? bias, bool relu, int splits, bool out_bf16) -> Tensor");
+  m.def(
+      "gemm_ex(Tensor A, int lda, bool a_kcontig, Tensor B, int ldb, bool b_kcontig, int M, "
+      "int N, int K, Tensor? bias, bool relu, int splits, bool out_bf16, int tile, "
+      "Tensor? pro_scale, Tensor? pro_shift, bool pro_on_a, bool want_stats) -> (Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
@@ -522,4 +560,5 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("bn_fwd", &bn_fwd);
   m.impl("bn_bwd", &bn_bwd);
   m.impl("gemm", &gemm);
+  m.impl("gemm_ex", &gemm_ex);
 }

@@ -1,6 +1,6 @@
-// bf16 MFMA GEMM for gfx950 with fused epilogues.
+// bf16 MFMA GEMM for gfx950 with fused prologues / epilogues.
 //
-//   C[M,N] = A·B (+ bias[n]) (ReLU)            bf16 or fp32 output, fp32 accumulation
+//   C[M,N] = pro(A)·pro(B) (+ bias[n]) (ReLU)       bf16 or fp32 output, fp32 accumulation
 //
 // A(m,k) is read either K-contiguous (A[m*lda+k], "A row-major") or M-contiguous (A[k*lda+m]);
 // B(k,n) either K-contiguous (B[n*ldb+k], i.e. an nn.Linear / 1x1-conv weight [N][K]) or
@@ -9,10 +9,22 @@
 // K-contiguous tiles are read with ds_read_b128, M/N-contiguous tiles with the gfx950 transposing
 // LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10).
 //
-// Geometry: 128x128 output tile per 256-thread workgroup (4 waves as 2x2, 64x64 per wave),
-// BK = 32, v_mfma_f32_16x16x32_bf16 (4x4 per wave per k-step), register-staged double-buffered
-// LDS, LDS-staged coalesced epilogue. Split-K (grid.z) writes fp32 partial slabs that a second
-// kernel reduces in a fixed order (deterministic) and pushes through the same epilogue.
+// Geometry: 256-thread workgroup = 4 waves as 2x2; the output tile BMxBN is one of 128x128,
+// 256x64 (skinny N: 1x1 convs with 64 output channels) or 64x256 (skinny M); BK = 32 or 64 per
+// LDS stage; v_mfma_f32_16x16x32_bf16; register-staged double-buffered LDS; workgroup → tile map is
+// XCD-aware (the 8 XCDs each get one contiguous run of tiles, so tiles sharing an A row-panel share
+// an L2). The epilogue stages the fp32 tile through LDS in two halves for 16-byte coalesced stores.
+//
+// Fusions (what makes this more than a library GEMM):
+//  * prologue PRO_A: a = relu(a*scale[k] + shift[k]) on K-contiguous A — a BatchNorm-apply+ReLU of
+//    the *input* folded into a 1x1 convolution (the normalised activation is never materialised);
+//  * prologue PRO_B: the same per-n on N-contiguous B — the weight-gradient of that convolution
+//    recomputes the normalised activation on load;
+//  * epilogue EPI_STATS: per-column Σv and Σv² of the bf16-rounded output per M-tile, written in the
+//    channel-major [2][N][tiles_m] layout the BatchNorm finalize kernel folds (bn.hip) — the forward
+//    statistics pass of the *next* BatchNorm disappears;
+//  * split-K (EPI_PARTIAL) writes fp32 slabs that a second kernel reduces in a fixed order
+//    (deterministic) and pushes through the same epilogue.
 #include "common.h"
 #include "lw_kernels.h"
 
@@ -23,14 +35,9 @@ typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int GT = 256;
-constexpr int TM = 128, TN = 128, TK = 32;
-constexpr int KPAD = 8;              // bf16 elements of padding per LDS row
-constexpr int LDK = TK + KPAD;       // K-contiguous tile row (40 el = 80 B)
-constexpr int LDMN = TM + KPAD;      // M/N-contiguous tile row (136 el = 272 B)
-
-template <bool KC> struct TileCfg;
-template <> struct TileCfg<true> { static constexpr int ELEMS = TM * LDK; };
-template <> struct TileCfg<false> { static constexpr int ELEMS = TK * LDMN; };
+constexpr int PAD = 8;                   // bf16 elements of padding per LDS row
+enum { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_STATS = 2 };
+enum { PRO_NONE = 0, PRO_A = 1, PRO_B = 2 };
 
 __device__ __forceinline__ uint16_t bf16_rne(float f) {
   uint32_t u = __float_as_uint(f);
@@ -38,55 +45,107 @@ __device__ __forceinline__ uint16_t bf16_rne(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }
+__device__ __forceinline__ float bf16_round(float f) { return __uint_as_float((uint32_t)bf16_rne(f) << 16); }
 
-// Global -> registers: two 16-byte chunks per thread for a 128x32 (or 32x128) bf16 tile.
-// KC: rows = 128 (m or n), 4 chunks of 8 k each. !KC: rows = 32 (k), 16 chunks of 8 m/n each.
-template <bool KC>
+// R = extent of the tile along m (A) or n (B). KC tiles are stored [R][BK+PAD], the others
+// [BK][R+PAD]; both are moved as 16-byte chunks of 8 contiguous elements.
+template <int R, int BK, bool KC> struct Tile {
+  static constexpr int LD = KC ? BK + PAD : R + PAD;
+  static constexpr int ELEMS = KC ? R * LD : BK * LD;
+  static constexpr int CPR = KC ? BK / 8 : R / 8;     // chunks per stored row
+  static constexpr int PER_T = R * BK / 8 / GT;       // chunks per thread
+  static_assert(R * BK / 8 % GT == 0, "tile must split evenly over the workgroup");
+};
+
+template <int R, int BK, bool KC>
+__device__ __forceinline__ void chunk_pos(int c, int& rr, int& cc) {
+  using T = Tile<R, BK, KC>;
+  rr = c / T::CPR;
+  cc = c % T::CPR;
+}
+
+// Global -> registers. `cont` returns the contiguous-dimension index of each chunk (k for KC,
+// m/n otherwise) for the prologue; `ok` marks chunks inside the matrix (others are zero).
+template <int R, int BK, bool KC>
 __device__ __forceinline__ void load_tile(const uint16_t* __restrict__ P, int64_t ld, int row0,
-                                          int rows_total, int k0, int K, uint4 r[2]) {
+                                          int rows_total, int k0, int kend,
+                                          uint4 (&r)[Tile<R, BK, KC>::PER_T],
+                                          int (&cont)[Tile<R, BK, KC>::PER_T], uint32_t& okmask) {
+  using T = Tile<R, BK, KC>;
+  okmask = 0;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int c = threadIdx.x + h * GT;
-    int rr, cc;     // tile-local row / 8-element chunk
-    bool ok;
+  for (int h = 0; h < T::PER_T; ++h) {
+    int rr, cc;
+    chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
     int64_t off;
+    bool ok;
     if (KC) {
-      rr = c >> 2; cc = c & 3;
       const int gr = row0 + rr, gk = k0 + cc * 8;
-      ok = gr < rows_total && gk < K;
+      ok = gr < rows_total && gk < kend;
       off = (int64_t)gr * ld + gk;
+      cont[h] = gk;
     } else {
-      rr = c >> 4; cc = c & 15;
       const int gk = k0 + rr, gr = row0 + cc * 8;
-      ok = gk < K && gr < rows_total;
+      ok = gk < kend && gr < rows_total;
       off = (int64_t)gk * ld + gr;
+      cont[h] = gr;
     }
     r[h] = ok ? *reinterpret_cast<const uint4*>(P + off) : make_uint4(0, 0, 0, 0);
+    okmask |= (ok ? 1u : 0u) << h;
   }
 }
 
-template <bool KC>
-__device__ __forceinline__ void store_tile(uint16_t* __restrict__ S, const uint4 r[2]) {
+// relu(v*scale[j] + shift[j]) on the 8 bf16 of a chunk, j = cont .. cont+7 (same fp32 expression
+// and rounding as the BatchNorm apply kernel, so fused and unfused paths agree bit for bit).
+__device__ __forceinline__ uint4 affine_relu8(uint4 v, const float* __restrict__ sc,
+                                              const float* __restrict__ sh, int j) {
+  const float4 s0 = *reinterpret_cast<const float4*>(sc + j);
+  const float4 s1 = *reinterpret_cast<const float4*>(sc + j + 4);
+  const float4 h0 = *reinterpret_cast<const float4*>(sh + j);
+  const float4 h1 = *reinterpret_cast<const float4*>(sh + j + 4);
+  const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float t[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int c = threadIdx.x + h * GT;
-    uint16_t* d = KC ? S + (c >> 2) * LDK + (c & 3) * 8 : S + (c >> 4) * LDMN + (c & 15) * 8;
-    *reinterpret_cast<uint4*>(d) = r[h];
+  for (int k = 0; k < 4; ++k) {
+    const float lo = fmaxf(fmaf(__uint_as_float(w[k] << 16), s[2 * k], t[2 * k]), 0.f);
+    const float hi = fmaxf(fmaf(__uint_as_float(w[k] & 0xffff0000u), s[2 * k + 1], t[2 * k + 1]), 0.f);
+    w[k] = (uint32_t)bf16_rne(lo) | ((uint32_t)bf16_rne(hi) << 16);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int R, int BK, bool KC, bool PRO>
+__device__ __forceinline__ void store_tile(uint16_t* __restrict__ S,
+                                           const uint4 (&r)[Tile<R, BK, KC>::PER_T],
+                                           const int (&cont)[Tile<R, BK, KC>::PER_T],
+                                           uint32_t okmask, const float* __restrict__ sc,
+                                           const float* __restrict__ sh) {
+  using T = Tile<R, BK, KC>;
+#pragma unroll
+  for (int h = 0; h < T::PER_T; ++h) {
+    int rr, cc;
+    chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
+    uint4 v = r[h];
+    if (PRO && ((okmask >> h) & 1u)) v = affine_relu8(v, sc, sh, cont[h]);
+    *reinterpret_cast<uint4*>(S + rr * T::LD + cc * 8) = v;
   }
 }
 
-// MFMA operand fragment (8 bf16 along k) for tile row/col `i` (0..127) and k-group g = lane>>4.
-template <bool KC>
-__device__ __forceinline__ bf16x8 load_frag(const uint16_t* S, int i_base) {
+// MFMA operand fragment (8 bf16 along k, k-group g = lane>>4, sub-step s of 32 k) for tile
+// row/col i_base + (lane&15).
+template <int R, int BK, bool KC>
+__device__ __forceinline__ bf16x8 load_frag(const uint16_t* S, int i_base, int s) {
+  using T = Tile<R, BK, KC>;
   const int l = threadIdx.x & 63;
   if (KC) {
-    const uint16_t* p = S + (i_base + (l & 15)) * LDK + 8 * (l >> 4);
+    const uint16_t* p = S + (i_base + (l & 15)) * T::LD + 32 * s + 8 * (l >> 4);
     return *reinterpret_cast<const bf16x8*>(p);
   } else {
     const int g = l >> 4, t = l & 15, q = t >> 2, p4 = t & 3;
     typedef __attribute__((address_space(3))) i16x4 lds_v4;
-    const uint16_t* p0 = S + (8 * g + q) * LDMN + i_base + 4 * p4;
-    const uint16_t* p1 = p0 + 4 * LDMN;
+    const uint16_t* p0 = S + (32 * s + 8 * g + q) * T::LD + i_base + 4 * p4;
+    const uint16_t* p1 = p0 + 4 * T::LD;
     const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0));
     const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p1));
     typedef short i16x8 __attribute__((ext_vector_type(8)));
@@ -95,9 +154,8 @@ __device__ __forceinline__ bf16x8 load_frag(const uint16_t* S, int i_base) {
   }
 }
 
-template <bool OUT_BF16>
-__device__ __forceinline__ void store_out8(void* C, int64_t off, const float v[8]) {
-  if (OUT_BF16) {
+__device__ __forceinline__ void store_out8(void* C, int64_t off, const float v[8], bool bf) {
+  if (bf) {
     uint32_t w[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) w[k] = (uint32_t)bf16_rne(v[2 * k]) | ((uint32_t)bf16_rne(v[2 * k + 1]) << 16);
@@ -109,180 +167,383 @@ __device__ __forceinline__ void store_out8(void* C, int64_t off, const float v[8
   }
 }
 
-// Epilogue on a 128x128 fp32 tile staged in LDS: bias, ReLU, conversion, 16-B coalesced stores.
-template <bool OUT_BF16>
-__device__ __forceinline__ void epilogue_store(const float* Cs, int ldcs, void* C, int64_t ldc,
-                                               int m0, int n0, int M, int N,
-                                               const float* __restrict__ bias, bool relu) {
-  // 128 rows x 16 chunks of 8 columns
-  for (int c = threadIdx.x; c < TM * (TN / 8); c += GT) {
-    const int r = c >> 4, cc = (c & 15) * 8;
-    const int gm = m0 + r, gn = n0 + cc;
-    if (gm >= M || gn >= N) continue;
-    float v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float x = Cs[r * ldcs + cc + k];
-      if (bias) x += (gn + k < N) ? bias[gn + k] : 0.f;
-      if (relu) x = fmaxf(x, 0.f);
-      v[k] = x;
-    }
-    if (gn + 8 <= N) {
-      store_out8<OUT_BF16>(C, (int64_t)gm * ldc + gn, v);
-    } else {
-      for (int k = 0; k < 8 && gn + k < N; ++k) {
-        if (OUT_BF16) static_cast<uint16_t*>(C)[(int64_t)gm * ldc + gn + k] = bf16_rne(v[k]);
-        else static_cast<float*>(C)[(int64_t)gm * ldc + gn + k] = v[k];
-      }
-    }
-  }
+struct GemmK {
+  const uint16_t* A;
+  const uint16_t* B;
+  void* C;
+  float* partial;
+  float* stats;
+  const float* bias;
+  const float* pro_scale;
+  const float* pro_shift;
+  int64_t lda, ldb, ldc;
+  int M, N, K, k_per_split, relu, out_bf16;
+};
+
+// Workgroup id → (m-tile, n-tile): consecutive ids are dealt round-robin to the 8 XCDs, so remap
+// each XCD's share onto one contiguous range of the row-major tile order.
+__device__ __forceinline__ int xcd_remap(int pid, int total) {
+  const int q = total >> 3, rem = total & 7;
+  const int x = pid & 7, idx = pid >> 3;
+  return x * q + (x < rem ? x : rem) + idx;
 }
 
-template <bool AKC, bool BKC, bool OUT_BF16>
-__global__ __launch_bounds__(GT) void k_gemm(const uint16_t* __restrict__ A, int64_t lda,
-                                             const uint16_t* __restrict__ B, int64_t ldb,
-                                             void* __restrict__ C, int64_t ldc,
-                                             float* __restrict__ partial,   // split-K slabs
-                                             const float* __restrict__ bias, int relu, int M,
-                                             int N, int K, int k_per_split) {
-  constexpr int AE = TileCfg<AKC>::ELEMS, BE = TileCfg<BKC>::ELEMS;
-  constexpr int STAGE = AE + BE;
-  constexpr int CS_FLOATS = TM * (TN + 4);
-  constexpr int LDS_BYTES_STAGES = 2 * STAGE * 2;
-  constexpr int LDS_BYTES = LDS_BYTES_STAGES > CS_FLOATS * 4 ? LDS_BYTES_STAGES : CS_FLOATS * 4;
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int PRO>
+__global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
+  using TA = Tile<BM, BK, AKC>;
+  using TB = Tile<BN, BK, BKC>;
+  constexpr int WTM = BM / 2, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
+  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
+  constexpr int LDC = BN + 4;                  // fp32 staging row (≡ 4 dwords mod 64 banks)
+  constexpr int LDH = BN + 16;                 // bf16 staging row (≡ 8 dwords mod 64 banks)
+  constexpr int CS_BYTES = WTM * LDC * 4;
+  constexpr int CH_BYTES = BM * LDH * 2 + 2 * 2 * BN * 4;
+  constexpr int ST_BYTES = 2 * STAGE * 2;
+  constexpr int LDS_BYTES = ST_BYTES > CS_BYTES ? (ST_BYTES > CH_BYTES ? ST_BYTES : CH_BYTES)
+                                                : (CS_BYTES > CH_BYTES ? CS_BYTES : CH_BYTES);
+  static_assert(PRO != PRO_A || AKC, "PRO_A needs a K-contiguous A");
+  static_assert(PRO != PRO_B || !BKC, "PRO_B needs an N-contiguous B");
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
   uint16_t* st = reinterpret_cast<uint16_t*>(lds);
 
-  const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
-  const int kbeg = blockIdx.z * k_per_split;
-  const int kend = min(K, kbeg + k_per_split);
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int pid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = pid / tiles_n, tn = pid - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wr = w >> 1, wc = w & 1;
 
-  f32x4 acc[4][4];
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[2], rb[2];
+  uint4 ra[TA::PER_T], rb[TB::PER_T];
+  int ca[TA::PER_T], cb[TB::PER_T];
+  uint32_t oka = 0, okb = 0;
   int cur = 0;
   if (kbeg < kend) {
-    load_tile<AKC>(A, lda, m0, M, kbeg, kend, ra);
-    load_tile<BKC>(B, ldb, n0, N, kbeg, kend, rb);
-    store_tile<AKC>(st, ra);
-    store_tile<BKC>(st + AE, rb);
+    load_tile<BM, BK, AKC>(p.A, p.lda, m0, p.M, kbeg, kend, ra, ca, oka);
+    load_tile<BN, BK, BKC>(p.B, p.ldb, n0, p.N, kbeg, kend, rb, cb, okb);
+    store_tile<BM, BK, AKC, PRO == PRO_A>(st, ra, ca, oka, p.pro_scale, p.pro_shift);
+    store_tile<BN, BK, BKC, PRO == PRO_B>(st + TA::ELEMS, rb, cb, okb, p.pro_scale, p.pro_shift);
   }
   __syncthreads();
-  for (int k0 = kbeg; k0 < kend; k0 += TK) {
-    const bool more = k0 + TK < kend;
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    const bool more = k0 + BK < kend;
     if (more) {
-      load_tile<AKC>(A, lda, m0, M, k0 + TK, kend, ra);
-      load_tile<BKC>(B, ldb, n0, N, k0 + TK, kend, rb);
+      load_tile<BM, BK, AKC>(p.A, p.lda, m0, p.M, k0 + BK, kend, ra, ca, oka);
+      load_tile<BN, BK, BKC>(p.B, p.ldb, n0, p.N, k0 + BK, kend, rb, cb, okb);
     }
     const uint16_t* As = st + cur * STAGE;
-    const uint16_t* Bs = As + AE;
-    bf16x8 fa[4], fb[4];
+    const uint16_t* Bs = As + TA::ELEMS;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = load_frag<AKC>(As, wr * 64 + i * 16);
+    for (int s = 0; s < BK / 32; ++s) {
+      bf16x8 fa[FM], fb[FN];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = load_frag<BKC>(Bs, wc * 64 + j * 16);
+      for (int i = 0; i < FM; ++i) fa[i] = load_frag<BM, BK, AKC>(As, wr * WTM + i * 16, s);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < FN; ++j) fb[j] = load_frag<BN, BK, BKC>(Bs, wc * WTN + j * 16, s);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
     if (more) {
       uint16_t* nx = st + (cur ^ 1) * STAGE;
-      store_tile<AKC>(nx, ra);
-      store_tile<BKC>(nx + AE, rb);
+      store_tile<BM, BK, AKC, PRO == PRO_A>(nx, ra, ca, oka, p.pro_scale, p.pro_shift);
+      store_tile<BN, BK, BKC, PRO == PRO_B>(nx + TA::ELEMS, rb, cb, okb, p.pro_scale, p.pro_shift);
     }
     __syncthreads();
     cur ^= 1;
   }
 
-  // stage the fp32 tile in LDS (C/D map: col = lane&15, row = 4*(lane>>4) + r)
-  float* Cs = reinterpret_cast<float*>(lds);
-  constexpr int LDC = TN + 4;
+  // ---- epilogue. B is the MFMA's first operand, so each accumulator holds Cᵀ: lane l has
+  // C[m = .. + (l&15)][n = .. + 4*(l>>4) + r], r = 0..3 (four consecutive columns of one row).
+  const int lm = l & 15, ln = 4 * (l >> 4);
+  const bool bf_out = EPI != EPI_PARTIAL && p.out_bf16;
+  uint16_t* Ch = reinterpret_cast<uint16_t*>(lds);                  // bf16 tile [BM][LDH]
+  float* red = reinterpret_cast<float*>(lds + BM * LDH * 2);        // stats [2 wave rows][2][BN]
+  if (EPI != EPI_PARTIAL) {
+    // bias / ReLU / rounding in registers; column statistics; bf16 staging of the whole tile
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < FN; ++j) {
+      const int nl = wc * WTN + j * 16 + ln;
+      const int n = n0 + nl;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+        for (int r = 0; r < 4; ++r) bv[r] = n + r < p.N ? p.bias[n + r] : 0.f;
+      }
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Cs[(wr * 64 + i * 16 + 4 * (l >> 4) + r) * LDC + wc * 64 + j * 16 + (l & 15)] = acc[i][j][r];
-  __syncthreads();
-  if (gridDim.z > 1) {
-    float* P = partial + (int64_t)blockIdx.z * M * N;
-    for (int c = threadIdx.x; c < TM * (TN / 4); c += GT) {
-      const int r = c >> 5, cc = (c & 31) * 4;
+      for (int i = 0; i < FM; ++i) {
+        const int ml = wr * WTM + i * 16 + lm;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float x = acc[i][j][r] + bv[r];
+          if (p.relu) x = fmaxf(x, 0.f);
+          v[r] = x;
+        }
+        if (bf_out) {
+          uint16_t h[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            h[r] = bf16_rne(v[r]);
+            v[r] = __uint_as_float((uint32_t)h[r] << 16);
+          }
+          *reinterpret_cast<uint2*>(Ch + ml * LDH + nl) =
+              make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+        }
+        if (EPI == EPI_STATS && m0 + ml < p.M) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { s1[r] += v[r]; s2[r] += v[r] * v[r]; }
+        }
+      }
+      if (EPI == EPI_STATS) {
+        // the 16 rows held by lanes sharing l>>4, fixed butterfly order
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s1[r] += __shfl_xor(s1[r], o, 64);
+            s2[r] += __shfl_xor(s2[r], o, 64);
+          }
+        }
+        if (lm == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            red[(wr * 2 + 0) * BN + nl + r] = s1[r];
+            red[(wr * 2 + 1) * BN + nl + r] = s2[r];
+          }
+        }
+      }
+    }
+  }
+  if (bf_out) {
+    __syncthreads();
+    const bool vec = (p.ldc & 7) == 0;
+    for (int c = threadIdx.x; c < BM * (BN / 8); c += GT) {
+      const int r = c / (BN / 8), cc = (c % (BN / 8)) * 8;
       const int gm = m0 + r, gn = n0 + cc;
-      if (gm >= M || gn >= N) continue;
-      if (gn + 4 <= N && (N & 3) == 0) {
-        *reinterpret_cast<float4*>(P + (int64_t)gm * N + gn) =
-            make_float4(Cs[r * LDC + cc], Cs[r * LDC + cc + 1], Cs[r * LDC + cc + 2], Cs[r * LDC + cc + 3]);
+      if (gm >= p.M || gn >= p.N) continue;
+      const uint16_t* src = Ch + r * LDH + cc;
+      uint16_t* dst = static_cast<uint16_t*>(p.C) + (int64_t)gm * p.ldc + gn;
+      if (vec && gn + 8 <= p.N) {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
       } else {
-        for (int k = 0; k < 4 && gn + k < N; ++k) P[(int64_t)gm * N + gn + k] = Cs[r * LDC + cc + k];
+        for (int k = 0; k < 8 && gn + k < p.N; ++k) dst[k] = src[k];
+      }
+    }
+  } else {
+    // fp32 output or split-K slab: two halves through an fp32 staging tile
+    float* Cs = reinterpret_cast<float*>(lds);
+    float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)blockIdx.y * p.M * p.N : nullptr;
+    float* dstbase = EPI == EPI_PARTIAL ? P : static_cast<float*>(p.C);
+    const int64_t ld = EPI == EPI_PARTIAL ? p.N : p.ldc;
+    const bool vec = (p.N & 3) == 0 && (ld & 3) == 0;
+    float statsave[2] = {0.f, 0.f};
+    if (EPI == EPI_STATS) {                      // red[] overlaps Cs: park this thread's column
+      __syncthreads();
+      for (int c = threadIdx.x; c < BN; c += GT) {
+        statsave[0] = red[0 * BN + c] + red[2 * BN + c];
+        statsave[1] = red[1 * BN + c] + red[3 * BN + c];
+      }
+    }
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      __syncthreads();
+      if (wr == half) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            *reinterpret_cast<float4*>(Cs + (i * 16 + lm) * LDC + wc * WTN + j * 16 + ln) =
+                make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      }
+      __syncthreads();
+      const int mb = m0 + half * WTM;
+      for (int c = threadIdx.x; c < WTM * (BN / 4); c += GT) {
+        const int r = c / (BN / 4), cc = (c % (BN / 4)) * 4;
+        const int gm = mb + r, gn = n0 + cc;
+        if (gm >= p.M || gn >= p.N) continue;
+        const float* src = Cs + r * LDC + cc;
+        float* dst = dstbase + (int64_t)gm * ld + gn;
+        if (vec && gn + 4 <= p.N) {
+          *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+        } else {
+          for (int k = 0; k < 4 && gn + k < p.N; ++k) dst[k] = src[k];
+        }
+      }
+    }
+    if (EPI == EPI_STATS) {
+      for (int c = threadIdx.x; c < BN; c += GT) {
+        const int n = n0 + c;
+        if (n >= p.N) continue;
+        p.stats[(int64_t)n * tiles_m + tm] = statsave[0];
+        p.stats[((int64_t)p.N + n) * tiles_m + tm] = statsave[1];
       }
     }
     return;
   }
-  epilogue_store<OUT_BF16>(Cs, LDC, C, ldc, m0, n0, M, N, bias, relu != 0);
-}
-
-// Fixed-order reduction of split-K slabs + epilogue.
-template <bool OUT_BF16>
-__global__ __launch_bounds__(GT) void k_splitk_reduce(const float* __restrict__ partial, int splits,
-                                                      void* __restrict__ C, int64_t ldc,
-                                                      const float* __restrict__ bias, int relu,
-                                                      int M, int N) {
-  const int64_t i = ((int64_t)blockIdx.x * GT + threadIdx.x);
-  const int64_t total = (int64_t)M * N;
-  if (i >= total) return;
-  float s = 0.f;
-  for (int z = 0; z < splits; ++z) s += partial[(int64_t)z * total + i];
-  const int n = (int)(i % N);
-  const int m = (int)(i / N);
-  if (bias) s += bias[n];
-  if (relu) s = fmaxf(s, 0.f);
-  if (OUT_BF16) static_cast<uint16_t*>(C)[(int64_t)m * ldc + n] = bf16_rne(s);
-  else static_cast<float*>(C)[(int64_t)m * ldc + n] = s;
-}
-
-void gemm_bf16(const GemmArgs& g, hipStream_t st) {
-  const int splits = g.splits < 1 ? 1 : g.splits;
-  int kps = (g.K + splits - 1) / splits;
-  kps = (kps + TK - 1) / TK * TK;
-  const int zs = (g.K + kps - 1) / kps;
-  dim3 grid((g.N + TN - 1) / TN, (g.M + TM - 1) / TM, zs);
-  dim3 block(GT);
-#define LW_G(AK, BK, OB)                                                                       \
-  hipLaunchKernelGGL((k_gemm<AK, BK, OB>), grid, block, 0, st, g.A, g.lda, g.B, g.ldb, g.C,      \
-                     g.ldc, g.partial, zs > 1 ? nullptr : g.bias, zs > 1 ? 0 : g.relu, g.M, g.N, \
-                     g.K, kps)
-#define LW_G2(OB)                                                                              \
-  if (g.a_kcontig && g.b_kcontig) LW_G(true, true, OB);                                       \
-  else if (g.a_kcontig) LW_G(true, false, OB);                                                \
-  else if (g.b_kcontig) LW_G(false, true, OB);                                                \
-  else LW_G(false, false, OB);
-  if (g.out_bf16) { LW_G2(true) } else { LW_G2(false) }
-#undef LW_G2
-#undef LW_G
-  if (zs > 1) {
-    const int64_t total = (int64_t)g.M * g.N;
-    const dim3 rg((unsigned)((total + GT - 1) / GT));
-    if (g.out_bf16)
-      hipLaunchKernelGGL(k_splitk_reduce<true>, rg, block, 0, st, g.partial, zs, g.C, g.ldc, g.bias, g.relu, g.M, g.N);
-    else
-      hipLaunchKernelGGL(k_splitk_reduce<false>, rg, block, 0, st, g.partial, zs, g.C, g.ldc, g.bias, g.relu, g.M, g.N);
+  if (EPI == EPI_STATS) {
+    for (int c = threadIdx.x; c < BN; c += GT) {
+      const int n = n0 + c;
+      if (n >= p.N) continue;
+      p.stats[(int64_t)n * tiles_m + tm] = red[0 * BN + c] + red[2 * BN + c];      // [2][N][tiles_m]
+      p.stats[((int64_t)p.N + n) * tiles_m + tm] = red[1 * BN + c] + red[3 * BN + c];
+    }
   }
 }
 
-int gemm_splits_used(int K, int splits) {
+// Fixed-order reduction of split-K slabs + epilogue. A workgroup owns OT float4 groups of outputs
+// and ZT split lanes (ZT*OT = 256): lane z sums splits z, z+ZT, ... in order, then the ZT lane sums
+// are added in lane order through LDS — the same order on every run.
+__global__ __launch_bounds__(GT) void k_splitk_reduce(const float* __restrict__ partial, int splits,
+                                                      int zt_log2, void* __restrict__ C,
+                                                      int64_t ldc, const float* __restrict__ bias,
+                                                      int relu, int M, int N, int out_bf16) {
+  __shared__ float4 red[GT];
+  const int ZT = 1 << zt_log2, OT = GT >> zt_log2;
+  const int z = threadIdx.x / OT, o = threadIdx.x % OT;
+  const int64_t total = (int64_t)M * N;
+  const int64_t i0 = ((int64_t)blockIdx.x * OT + o) * 4;
+  const bool vec = (N & 3) == 0 && ldc == N;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i0 < total) {
+    if (vec) {
+#pragma unroll 8
+      for (int zz = z; zz < splits; zz += ZT) {
+        const float4 v = *reinterpret_cast<const float4*>(partial + (int64_t)zz * total + i0);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+    } else {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int zz = z; zz < splits; zz += ZT)
+        for (int k = 0; k < 4 && i0 + k < total; ++k) t[k] += partial[(int64_t)zz * total + i0 + k];
+      s = make_float4(t[0], t[1], t[2], t[3]);
+    }
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (z != 0 || i0 >= total) return;
+  for (int q = 1; q < ZT; ++q) {
+    const float4 v = red[q * OT + o];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  float out[4] = {s.x, s.y, s.z, s.w};
+  for (int k = 0; k < 4 && i0 + k < total; ++k) {
+    const int64_t i = i0 + k;
+    const int n = (int)(i % N);
+    const int64_t m = i / N;
+    float x = out[k];
+    if (bias) x += bias[n];
+    if (relu) x = fmaxf(x, 0.f);
+    if (out_bf16) static_cast<uint16_t*>(C)[m * ldc + n] = bf16_rne(x);
+    else static_cast<float*>(C)[m * ldc + n] = x;
+  }
+}
+
+// ------------------------------------------------------------------------------------------ host
+struct TileShape { int bm, bn, bk; };
+static TileShape tile_shape(int t) {
+  switch (t) {
+    case GEMM_T128x128x64: return {128, 128, 64};
+    case GEMM_T256x64x32: return {256, 64, 32};
+    case GEMM_T64x256x32: return {64, 256, 32};
+    case GEMM_T256x64x64: return {256, 64, 64};
+    case GEMM_T64x64x64: return {64, 64, 64};
+    default: return {128, 128, 32};
+  }
+}
+
+int gemm_pick_tile(const GemmArgs& g) {
+  if (g.tile > 0) return g.tile;
+  if (g.M <= 64 && g.N <= 64) return GEMM_T64x64x64;
+  if (g.N <= 64 && g.M >= 512) return GEMM_T256x64x32;
+  if (g.M <= 64 && g.N >= 512) return GEMM_T64x256x32;
+  return GEMM_T128x128x32;
+}
+
+int gemm_tiles_m(const GemmArgs& g) { return (g.M + tile_shape(gemm_pick_tile(g)).bm - 1) / tile_shape(gemm_pick_tile(g)).bm; }
+
+static int k_per_split(int K, int splits, int bk) {
   splits = splits < 1 ? 1 : splits;
   int kps = (K + splits - 1) / splits;
-  kps = (kps + TK - 1) / TK * TK;
-  return (K + kps - 1) / kps;
+  return (kps + bk - 1) / bk * bk;
+}
+
+int gemm_splits_used(const GemmArgs& g) {
+  const int bk = tile_shape(gemm_pick_tile(g)).bk;
+  const int kps = k_per_split(g.K, g.splits, bk);
+  return (g.K + kps - 1) / kps;
+}
+
+template <int BM, int BN, int BK, int EPI, int PRO>
+static void launch_layout(const GemmArgs& g, const GemmK& k, dim3 grid, hipStream_t st) {
+  const dim3 block(GT);
+  if constexpr (PRO == PRO_A) {
+    if (g.b_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, true, EPI, PRO>), grid, block, 0, st, k);
+    else hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI, PRO>), grid, block, 0, st, k);
+  } else if constexpr (PRO == PRO_B) {
+    if (g.a_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI, PRO>), grid, block, 0, st, k);
+    else hipLaunchKernelGGL((k_gemm<BM, BN, BK, false, false, EPI, PRO>), grid, block, 0, st, k);
+  } else {
+    if (g.a_kcontig && g.b_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, true, EPI, PRO>), grid, block, 0, st, k);
+    else if (g.a_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI, PRO>), grid, block, 0, st, k);
+    else if (g.b_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, false, true, EPI, PRO>), grid, block, 0, st, k);
+    else hipLaunchKernelGGL((k_gemm<BM, BN, BK, false, false, EPI, PRO>), grid, block, 0, st, k);
+  }
+}
+
+template <int BM, int BN, int BK>
+static void launch_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, hipStream_t st) {
+  const int pro = g.pro_scale ? (g.pro_on_a ? PRO_A : PRO_B) : PRO_NONE;
+#define LW_E(E)                                                                                  \
+  if (pro == PRO_A) launch_layout<BM, BN, BK, E, PRO_A>(g, k, grid, st);                         \
+  else if (pro == PRO_B) launch_layout<BM, BN, BK, E, PRO_B>(g, k, grid, st);                    \
+  else launch_layout<BM, BN, BK, E, PRO_NONE>(g, k, grid, st);
+  if (epi == EPI_PARTIAL) { LW_E(EPI_PARTIAL) }
+  else if (epi == EPI_STATS) { LW_E(EPI_STATS) }
+  else { LW_E(EPI_STORE) }
+#undef LW_E
+}
+
+void gemm_bf16(const GemmArgs& g, hipStream_t st) {
+  const int t = gemm_pick_tile(g);
+  const TileShape ts = tile_shape(t);
+  const int kps = k_per_split(g.K, g.splits, ts.bk);
+  const int zs = (g.K + kps - 1) / kps;
+  const int tiles = ((g.M + ts.bm - 1) / ts.bm) * ((g.N + ts.bn - 1) / ts.bn);
+  const int epi = zs > 1 ? EPI_PARTIAL : (g.stats ? EPI_STATS : EPI_STORE);
+  GemmK k{g.A, g.B, g.C, g.partial, g.stats, zs > 1 ? nullptr : g.bias, g.pro_scale, g.pro_shift,
+          g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, zs > 1 ? 0 : g.relu, g.out_bf16 ? 1 : 0};
+  const dim3 grid(tiles, zs);
+  switch (t) {
+    case GEMM_T128x128x64: launch_tile<128, 128, 64>(g, k, epi, grid, st); break;
+    case GEMM_T256x64x32: launch_tile<256, 64, 32>(g, k, epi, grid, st); break;
+    case GEMM_T64x256x32: launch_tile<64, 256, 32>(g, k, epi, grid, st); break;
+    case GEMM_T256x64x64: launch_tile<256, 64, 64>(g, k, epi, grid, st); break;
+    case GEMM_T64x64x64: launch_tile<64, 64, 64>(g, k, epi, grid, st); break;
+    default: launch_tile<128, 128, 32>(g, k, epi, grid, st); break;
+  }
+  if (zs > 1) {
+    const int64_t total = (int64_t)g.M * g.N;
+    int zl = 0;                                  // split lanes: up to 32, no more than splits
+    while (zl < 5 && (2 << zl) <= zs) ++zl;
+    const int64_t groups = (total + 3) / 4, ot = GT >> zl;
+    const dim3 rg((unsigned)((groups + ot - 1) / ot));
+    hipLaunchKernelGGL(k_splitk_reduce, rg, dim3(GT), 0, st, g.partial, zs, zl, g.C, g.ldc, g.bias,
+                       g.relu, g.M, g.N, g.out_bf16 ? 1 : 0);
+  }
 }
 
 }  // namespace lw

@@ -148,9 +148,19 @@ struct GemmArgs {
   int M, N, K;
   int splits;         // split-K factor (>1 needs `partial`)
   float* partial;     // [splits][M][N] fp32
+  int tile;           // GemmTile, 0 = heuristic
+  float* stats;       // optional [2][N][tiles_m] per-column Σv, Σv² (no split-K)
+  const float* pro_scale;  // optional prologue relu(v*scale+shift): per-k of a K-contiguous A
+  const float* pro_shift;  // (pro_on_a) or per-n of an N-contiguous B
+  bool pro_on_a;
 };
+enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_T256x64x32 = 3,
+                GEMM_T64x256x32 = 4, GEMM_T256x64x64 = 5,
+                GEMM_T64x64x64 = 6 };
 void gemm_bf16(const GemmArgs& g, hipStream_t st);
-int gemm_splits_used(int K, int splits);
+int gemm_pick_tile(const GemmArgs& g);
+int gemm_tiles_m(const GemmArgs& g);
+int gemm_splits_used(const GemmArgs& g);
 
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],

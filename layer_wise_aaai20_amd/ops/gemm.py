@@ -20,8 +20,22 @@ def _splits(tiles: int, K: int) -> int:
     return int(max(1, min(want, K // 256 if K >= 512 else 1)))
 
 
+TILES = {"auto": 0, "128x128x32": 1, "128x128x64": 2, "256x64x32": 3, "64x256x32": 4,
+         "256x64x64": 5, "64x64x64": 6}
+
+
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False, splits=1, out_bf16=True):
     return load().gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias, relu, splits, out_bf16)
+
+
+def gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False, splits=1, out_bf16=True,
+            tile="auto", pro_scale=None, pro_shift=None, pro_on_a=True, stats=False):
+    """Full-featured entry: explicit tile, prologue ``relu(v*scale+shift)`` (per-k of a
+    K-contiguous A, or per-n of an N-contiguous B) and per-column output statistics
+    ``[2][N][tiles_m]`` (Σv, Σv² of the stored values per M-tile). Returns ``(C, stats)``."""
+    return load().gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias, relu, splits, out_bf16,
+                          TILES[tile] if isinstance(tile, str) else int(tile), pro_scale,
+                          pro_shift, pro_on_a, stats)
 
 
 def linear_fwd(x2, w, bias=None, relu=False):

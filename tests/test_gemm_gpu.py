@@ -63,3 +63,57 @@ def test_mfma_linear_matches_nn_linear():
     torch.testing.assert_close(lin.weight.grad, ref.weight.grad, rtol=3e-2, atol=1e-1)
     torch.testing.assert_close(lin.bias.grad, ref.bias.grad, rtol=3e-2, atol=1e-1)
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=3e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("tile", ["128x128x32", "128x128x64", "256x64x32", "64x256x32",
+                                  "256x64x64", "64x64x64"])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_tiles(tile, a_kc, b_kc):
+    torch.manual_seed(1)
+    M, N, K = 520, 200, 328
+    Am = torch.randn(M, K, device="cuda").bfloat16()
+    Bm = torch.randn(K, N, device="cuda").bfloat16()
+    A = Am.contiguous() if a_kc else Am.t().contiguous()
+    B = Bm.t().contiguous() if b_kc else Bm.contiguous()
+    for splits in (1, 2):
+        C, _ = G.gemm_ex(A, K if a_kc else M, a_kc, B, K if b_kc else N, b_kc, M, N, K,
+                         splits=splits, out_bf16=False, tile=tile)
+        torch.testing.assert_close(C, _ref(Am, Bm), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("tile", ["128x128x32", "256x64x32", "64x256x32", "64x64x64"])
+def test_gemm_stats_epilogue(tile):
+    """Per-column Σ / Σ² of the bf16 output per M-tile (BatchNorm statistics in the epilogue)."""
+    torch.manual_seed(2)
+    M, N, K = 1000, 136, 96
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = torch.randn(N, K, device="cuda").bfloat16()
+    C, st = G.gemm_ex(x, K, True, w, K, True, M, N, K, tile=tile, stats=True)
+    bm = {"128x128x32": 128, "256x64x32": 256, "64x256x32": 64, "64x64x64": 64}[tile]
+    tiles_m = -(-M // bm)
+    assert st.shape == (2, N, tiles_m)
+    c = C.float()
+    torch.testing.assert_close(st[0].sum(1), c.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[1].sum(1), (c * c).sum(0), rtol=1e-4, atol=1e-1)
+    # per-tile partials
+    torch.testing.assert_close(st[0][:, 0], c[:bm].sum(0), rtol=1e-4, atol=1e-2)
+
+
+def test_gemm_prologue_a_and_b():
+    """relu(v*scale+shift) applied while loading: per-k on a K-contiguous A (forward of a 1x1 conv
+    on a BatchNorm'd input) and per-n on an N-contiguous B (its weight gradient)."""
+    torch.manual_seed(3)
+    M, N, K = 704, 192, 136
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = torch.randn(N, K, device="cuda").bfloat16()
+    sc = torch.rand(K, device="cuda") + 0.5
+    sh = torch.randn(K, device="cuda")
+    a = torch.relu(x.float() * sc + sh).bfloat16().float()
+    y, _ = G.gemm_ex(x, K, True, w, K, True, M, N, K, out_bf16=False, pro_scale=sc, pro_shift=sh,
+                     pro_on_a=True)
+    torch.testing.assert_close(y, a @ w.float().t(), rtol=1e-3, atol=1e-2)
+    # weight gradient: dW[N][K] = dyᵀ · a, B = x (N-contiguous over K channels), prologue per-n
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    dw, _ = G.gemm_ex(dy, N, False, x, K, False, N, K, M, splits=3, out_bf16=False, pro_scale=sc,
+                      pro_shift=sh, pro_on_a=False)
+    torch.testing.assert_close(dw, dy.float().t() @ a, rtol=1e-3, atol=5e-2)

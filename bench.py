@@ -25,8 +25,25 @@ import os
 import sys
 import time
 
-import torch
-import torch.distributed as dist
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _miopen_cache_env() -> None:
+    """Point MIOpen's find-db and compiled-kernel cache at an in-repo directory (unless the user
+    already chose one): the solver search and kernel compilation of a fresh box then run once per
+    image, not once per run (a cold find for ResNet-50 takes minutes)."""
+    base = os.path.join(ROOT, ".miopen")
+    for var, sub in (("MIOPEN_USER_DB_PATH", "db"), ("MIOPEN_CUSTOM_CACHE_DIR", "cache")):
+        if var not in os.environ:
+            path = os.path.join(base, sub)
+            os.makedirs(path, exist_ok=True)
+            os.environ[var] = path
+
+
+_miopen_cache_env()
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 BASELINE_METRIC = ("images/sec/node + top-1 acc, ResNet-50 Top-K k=0.1% layer-wise at "
                    "1/2/4/8 GPUs")
@@ -57,6 +74,30 @@ def parse():
     ap.add_argument("--miopen-find", type=int, default=1,
                     help="1: let MIOpen benchmark conv solvers once (cudnn.benchmark)")
     return ap.parse_args()
+
+
+class _Heartbeat:
+    """Progress on stderr every 20 s while warm-up runs (MIOpen's first solver search can take
+    minutes with no output)."""
+
+    def __init__(self, rank: int, every: float = 20.0):
+        import threading
+        self.rank, self.msg, self.t0 = rank, "warmup 0", time.time()
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, args=(every,), daemon=True)
+        self._th.start()
+
+    def _run(self, every):
+        while not self._stop.wait(every):
+            if self.rank == 0:
+                print(f"[bench] {self.msg} ({time.time() - self.t0:.0f} s)", file=sys.stderr,
+                      flush=True)
+
+    def note(self, msg: str) -> None:
+        self.msg = msg
+
+    def stop(self) -> None:
+        self._stop.set()
 
 
 def main():
@@ -90,8 +131,11 @@ def main():
     images = torch.randint(0, 256, (B, S, S, 3), dtype=torch.uint8, device=dev, generator=g)
     target = torch.randint(0, 1000, (B,), device=dev, generator=g)
 
-    for _ in range(args.warmup):
+    beat = _Heartbeat(rank)
+    for i in range(args.warmup):
         tr.step(images, target)
+        beat.note(f"warmup {i + 1}/{args.warmup}")
+    beat.stop()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -419,7 +419,8 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
                                    c10::optional<Tensor> bias, bool relu, int64_t splits,
                                    bool out_bf16, int64_t tile, c10::optional<Tensor> pro_scale,
                                    c10::optional<Tensor> pro_shift, bool pro_on_a,
-                                   bool want_stats) {
+                                   bool want_stats, c10::optional<Tensor> out,
+                                   c10::optional<Tensor> addend, bool accumulate, int64_t ldc) {
   const c10::DeviceGuard guard(A.device());
   TORCH_CHECK(A.is_cuda() && B.is_cuda(), "gemm needs GPU tensors");
   check_dtype(A, at::kBFloat16, "A");
@@ -435,7 +436,24 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
   TORCH_CHECK(A.numel() >= (a_kcontig ? (M - 1) * lda + K : (K - 1) * lda + M), "A too small");
   TORCH_CHECK(B.numel() >= (b_kcontig ? (N - 1) * ldb + K : (K - 1) * ldb + N), "B too small");
   TORCH_CHECK(tile >= 0 && tile <= 6, "tile id");
-  Tensor C = at::empty({M, N}, A.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  if (ldc <= 0) ldc = N;
+  TORCH_CHECK(ldc >= N, "ldc must be >= N");
+  const auto odt = out_bf16 ? at::kBFloat16 : at::kFloat;
+  Tensor C;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    TORCH_CHECK(C.is_cuda() && C.scalar_type() == odt, "out dtype must match out_bf16");
+    TORCH_CHECK(C.is_contiguous(at::MemoryFormat::ChannelsLast) || C.is_contiguous(),
+                "out must be dense");
+    TORCH_CHECK(C.numel() >= (M - 1) * ldc + N, "out too small for [M, ldc]");
+    TORCH_CHECK(out_bf16 ? ldc % 8 == 0 : ldc % 4 == 0, "ldc alignment");
+    check_aligned16(C.data_ptr(), "out");
+  } else {
+    TORCH_CHECK(!accumulate, "accumulate needs an out tensor");
+    TORCH_CHECK(ldc == N, "ldc != N needs an out tensor");
+    C = at::empty({M, N}, A.options().dtype(odt));
+  }
+  TORCH_CHECK(!accumulate || !out_bf16, "accumulate is for fp32 outputs");
   lw::GemmArgs g{};
   g.A = ptr<uint16_t>(A);
   g.lda = lda;
@@ -444,8 +462,18 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
   g.ldb = ldb;
   g.b_kcontig = b_kcontig;
   g.C = C.data_ptr();
-  g.ldc = N;
+  g.ldc = ldc;
   g.out_bf16 = out_bf16;
+  g.accumulate = accumulate;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(out_bf16, "addend needs a bf16 output");
+    check_dtype(*addend, at::kBFloat16, "addend");
+    TORCH_CHECK(addend->numel() >= (M - 1) * ldc + N, "addend too small for [M, ldc]");
+    TORCH_CHECK(addend->is_contiguous(at::MemoryFormat::ChannelsLast) || addend->is_contiguous(),
+                "addend must be dense");
+    check_aligned16(addend->data_ptr(), "addend");
+    g.addend = ptr<uint16_t>(*addend);
+  }
   if (bias.has_value() && bias->defined()) {
     check_dtype(*bias, at::kFloat, "bias");
     TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "bias size");
@@ -493,7 +521,92 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
             int64_t M, int64_t N, int64_t K, c10::optional<Tensor> bias, bool relu,
             int64_t splits, bool out_bf16) {
   return std::get<0>(gemm_ex(A, lda, a_kcontig, B, ldb, b_kcontig, M, N, K, bias, relu, splits,
-                             out_bf16, 0, c10::nullopt, c10::nullopt, true, false));
+                             out_bf16, 0, c10::nullopt, c10::nullopt, true, false, c10::nullopt,
+                             c10::nullopt, false, 0));
+}
+
+// ---------------------------------------------------------------- BN pieces for fused blocks
+// Batch statistics of x ([M, C] / channels_last), or — with `stats` [2, C, nb] from a GEMM's
+// column-statistics epilogue — only the finalize. Returns (mean, invstd, scale_shift[2C]).
+std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stats,
+                                            c10::optional<Tensor> weight,
+                                            c10::optional<Tensor> bias,
+                                            c10::optional<Tensor> rmean,
+                                            c10::optional<Tensor> rvar, double momentum,
+                                            double eps) {
+  const c10::DeviceGuard guard(x.device());
+  check_nhwc(x, "x");
+  const int64_t C = x.dim() == 4 ? x.size(1) : x.size(-1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn_stats needs C % 8 == 0");
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32);
+  Tensor ss = at::empty({2 * C}, f32);
+  lw::BNArgs a{};
+  a.x = x.data_ptr();
+  a.M = M;
+  a.C = (int)C;
+  a.bf16 = x.scalar_type() == at::kBFloat16;
+  a.training = true;
+  a.eps = (float)eps;
+  a.momentum = (float)momentum;
+  a.gamma = optr<float>(weight);
+  a.beta = optr<float>(bias);
+  a.rmean = optr<float>(rmean);
+  a.rvar = optr<float>(rvar);
+  a.mean = ptr<float>(mean);
+  a.invstd = ptr<float>(invstd);
+  a.scale = ptr<float>(ss);
+  a.shift = a.scale + C;
+  Tensor partial;
+  if (stats.has_value() && stats->defined()) {
+    check_dtype(*stats, at::kFloat, "stats");
+    TORCH_CHECK(stats->dim() == 3 && stats->size(0) == 2 && stats->size(1) == C &&
+                stats->is_contiguous(), "stats must be a contiguous [2, C, nb] tensor");
+    a.partial = ptr<float>(*stats);
+    a.stats_blocks = (int)stats->size(2);
+  } else {
+    partial = at::empty({(int64_t)lw::bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+    a.partial = ptr<float>(partial);
+  }
+  lw::bn_stats(a, cur_stream());
+  return {mean, invstd, ss};
+}
+
+// y = relu?(x*scale+shift [+ res | + res*rscale+rshift])
+Tensor bn_apply(Tensor x, Tensor scale_shift, c10::optional<Tensor> res,
+                c10::optional<Tensor> res_scale_shift, bool relu) {
+  const c10::DeviceGuard guard(x.device());
+  check_nhwc(x, "x");
+  const int64_t C = x.dim() == 4 ? x.size(1) : x.size(-1);
+  TORCH_CHECK(C % 8 == 0, "bn_apply needs C % 8 == 0");
+  check_dtype(scale_shift, at::kFloat, "scale_shift");
+  TORCH_CHECK(scale_shift.numel() == 2 * C && scale_shift.is_contiguous(), "scale_shift size");
+  Tensor y = at::empty_like(x);
+  lw::BNArgs a{};
+  a.x = x.data_ptr();
+  a.y = y.data_ptr();
+  a.M = x.numel() / C;
+  a.C = (int)C;
+  a.bf16 = x.scalar_type() == at::kBFloat16;
+  a.relu = relu;
+  a.scale = ptr<float>(scale_shift);
+  a.shift = a.scale + C;
+  if (res.has_value() && res->defined()) {
+    check_nhwc(*res, "res");
+    TORCH_CHECK(res->numel() == x.numel() && res->scalar_type() == x.scalar_type(),
+                "residual must match x");
+    a.res = res->data_ptr();
+    if (res_scale_shift.has_value() && res_scale_shift->defined()) {
+      check_dtype(*res_scale_shift, at::kFloat, "res_scale_shift");
+      TORCH_CHECK(res_scale_shift->numel() == 2 * C && res_scale_shift->is_contiguous(),
+                  "res_scale_shift size");
+      a.res_scale = ptr<float>(*res_scale_shift);
+      a.res_shift = a.res_scale + C;
+    }
+  }
+  lw::bn_apply(a, cur_stream());
+  return y;
 }
 
 }  // namespace
@@ -544,7 +657,14 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "gemm_ex(Tensor A, int lda, bool a_kcontig, Tensor B, int ldb, bool b_kcontig, int M, "
       "int N, int K, Tensor? bias, bool relu, int splits, bool out_bf16, int tile, "
-      "Tensor? pro_scale, Tensor? pro_shift, bool pro_on_a, bool want_stats) -> (Tensor, Tensor)");
+      "Tensor? pro_scale, Tensor? pro_shift, bool pro_on_a, bool want_stats, "
+      "Tensor(a!)? out=None, Tensor? addend=None, bool accumulate=False, int ldc=0) "
+      "-> (Tensor, Tensor)");
+  m.def(
+      "bn_stats(Tensor x, Tensor? stats, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
+      "Tensor(b!)? running_var, float momentum, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? res, Tensor? res_scale_shift, bool relu) "
+        "-> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
@@ -561,4 +681,6 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("bn_bwd", &bn_bwd);
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);
+  m.impl("bn_stats", &bn_stats);
+  m.impl("bn_apply", &bn_apply);
 }

@@ -213,19 +213,28 @@ __global__ __launch_bounds__(256) void k_bn_finalize_fwd(
 
 // Thread-constant channel group: the grid-stride step is a multiple of G = C/8 (apply_grid), so
 // a thread always touches the same 8 channels and keeps their coefficients in registers.
-template <typename T, bool RES, bool RELU>
+// RES: 0 none, 1 plain residual add, 2 residual through its own BatchNorm affine (the downsample
+// branch of a ResNet block: y = relu(x*scale+shift + r*rscale+rshift), the normalised shortcut is
+// never materialised).
+template <typename T, int RES, bool RELU>
 __global__ __launch_bounds__(BNT) void k_bn_apply(const T* __restrict__ x, const T* __restrict__ res,
                                                   T* __restrict__ y,
                                                   const float* __restrict__ scale,
-                                                  const float* __restrict__ shift, int64_t n8,
+                                                  const float* __restrict__ shift,
+                                                  const float* __restrict__ rscale,
+                                                  const float* __restrict__ rshift, int64_t n8,
                                                   int C) {
   const int G = C / 8;
   const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
   const int64_t step = (int64_t)gridDim.x * BNT;
   const int c0 = (int)(t0 % G) * 8;
-  float sc[8], sh[8];
+  float sc[8], sh[8], rs[8], rh[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { sc[k] = scale[c0 + k]; sh[k] = shift[c0 + k]; }
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = scale[c0 + k]; sh[k] = shift[c0 + k];
+    rs[k] = RES == 2 ? rscale[c0 + k] : 1.f;
+    rh[k] = RES == 2 ? rshift[c0 + k] : 0.f;
+  }
   int64_t i = t0;
   for (; i + step < n8; i += 2 * step) {
     float v[2][8], rr[2][8];
@@ -239,7 +248,8 @@ __global__ __launch_bounds__(BNT) void k_bn_apply(const T* __restrict__ x, const
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float t = fmaf(v[u][k], sc[k], sh[k]);
-        if (RES) t += rr[u][k];
+        if (RES == 1) t += rr[u][k];
+        if (RES == 2) t += fmaf(rr[u][k], rs[k], rh[k]);
         if (RELU) t = fmaxf(t, 0.f);
         v[u][k] = t;
       }
@@ -253,7 +263,8 @@ __global__ __launch_bounds__(BNT) void k_bn_apply(const T* __restrict__ x, const
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float t = fmaf(v[k], sc[k], sh[k]);
-      if (RES) t += rr[k];
+      if (RES == 1) t += rr[k];
+      if (RES == 2) t += fmaf(rr[k], rs[k], rh[k]);
       if (RELU) t = fmaxf(t, 0.f);
       v[k] = t;
     }
@@ -363,30 +374,44 @@ static int apply_grid(int64_t n8, int C) {
 }
 
 template <typename T>
-static void bn_forward_t(const BNArgs& a, hipStream_t st) {
+static void bn_apply_t(const BNArgs& a, hipStream_t st) {
   const T* x = static_cast<const T*>(a.x);
   const T* res = static_cast<const T*>(a.res);
   T* y = static_cast<T*>(a.y);
   const int64_t n8 = a.M * a.C / 8;
-  if (a.training) {
-    int64_t rpb;
-    int nb;
-    reduce_geometry(a.M, a.C, rpb, nb);
-    hipLaunchKernelGGL((k_bn_reduce<T, 0, 0>), dim3(nb), dim3(BNT), 0, st, x, (const T*)nullptr,
-                       (const T*)nullptr, (const float*)nullptr, (const float*)nullptr,
-                       (const float*)nullptr, a.M, a.C, rpb, a.partial);
-    hipLaunchKernelGGL(k_bn_finalize_fwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
-                       a.C, a.M, a.gamma, a.beta, a.eps, a.momentum, a.rmean, a.rvar, a.mean,
-                       a.invstd, a.scale, a.shift);
-  }
   const dim3 grid(apply_grid(n8, a.C)), block(BNT);
-  if (res) {
-    if (a.relu) hipLaunchKernelGGL((k_bn_apply<T, true, true>), grid, block, 0, st, x, res, y, a.scale, a.shift, n8, a.C);
-    else hipLaunchKernelGGL((k_bn_apply<T, true, false>), grid, block, 0, st, x, res, y, a.scale, a.shift, n8, a.C);
-  } else {
-    if (a.relu) hipLaunchKernelGGL((k_bn_apply<T, false, true>), grid, block, 0, st, x, res, y, a.scale, a.shift, n8, a.C);
-    else hipLaunchKernelGGL((k_bn_apply<T, false, false>), grid, block, 0, st, x, res, y, a.scale, a.shift, n8, a.C);
+#define LW_AP(R, L)                                                                              \
+  hipLaunchKernelGGL((k_bn_apply<T, R, L>), grid, block, 0, st, x, res, y, a.scale, a.shift,     \
+                     a.res_scale, a.res_shift, n8, a.C)
+  const int rm = !res ? 0 : (a.res_scale ? 2 : 1);
+  if (rm == 2) { if (a.relu) LW_AP(2, true); else LW_AP(2, false); }
+  else if (rm == 1) { if (a.relu) LW_AP(1, true); else LW_AP(1, false); }
+  else { if (a.relu) LW_AP(0, true); else LW_AP(0, false); }
+#undef LW_AP
+}
+
+// Batch statistics -> mean / invstd / scale / shift (+ running-stat update). With
+// a.stats_blocks > 0 the per-block partial sums are already in a.partial (written by the epilogue
+// of the producing GEMM, gemm.hip EPI_STATS) and only the finalize runs.
+template <typename T>
+static void bn_stats_t(const BNArgs& a, hipStream_t st) {
+  int nb = a.stats_blocks;
+  if (nb <= 0) {
+    int64_t rpb;
+    reduce_geometry(a.M, a.C, rpb, nb);
+    hipLaunchKernelGGL((k_bn_reduce<T, 0, 0>), dim3(nb), dim3(BNT), 0, st, static_cast<const T*>(a.x),
+                       (const T*)nullptr, (const T*)nullptr, (const float*)nullptr,
+                       (const float*)nullptr, (const float*)nullptr, a.M, a.C, rpb, a.partial);
   }
+  hipLaunchKernelGGL(k_bn_finalize_fwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
+                     a.C, a.M, a.gamma, a.beta, a.eps, a.momentum, a.rmean, a.rvar, a.mean,
+                     a.invstd, a.scale, a.shift);
+}
+
+template <typename T>
+static void bn_forward_t(const BNArgs& a, hipStream_t st) {
+  if (a.training) bn_stats_t<T>(a, st);
+  bn_apply_t<T>(a, st);
 }
 
 template <typename T>
@@ -422,6 +447,12 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
 
 void bn_forward(const BNArgs& a, hipStream_t st) {
   if (a.bf16) bn_forward_t<uint16_t>(a, st); else bn_forward_t<float>(a, st);
+}
+void bn_stats(const BNArgs& a, hipStream_t st) {
+  if (a.bf16) bn_stats_t<uint16_t>(a, st); else bn_stats_t<float>(a, st);
+}
+void bn_apply(const BNArgs& a, hipStream_t st) {
+  if (a.bf16) bn_apply_t<uint16_t>(a, st); else bn_apply_t<float>(a, st);
 }
 void bn_backward(const BNArgs& a, hipStream_t st) {
   if (a.bf16) bn_backward_t<uint16_t>(a, st); else bn_backward_t<float>(a, st);

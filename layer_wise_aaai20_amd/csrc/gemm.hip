@@ -47,6 +47,20 @@ __device__ __forceinline__ uint16_t bf16_rne(float f) {
 }
 __device__ __forceinline__ float bf16_round(float f) { return __uint_as_float((uint32_t)bf16_rne(f) << 16); }
 
+// bf16 + bf16 -> bf16 per element (fp32 add, one rounding): the same arithmetic as a separate
+// elementwise add of two bf16 tensors, so fusing the residual-gradient add changes no bits.
+__device__ __forceinline__ uint4 add_bf16x8(uint4 a, uint4 b) {
+  const uint32_t x[4] = {a.x, a.y, a.z, a.w}, y[4] = {b.x, b.y, b.z, b.w};
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float lo = __uint_as_float(x[k] << 16) + __uint_as_float(y[k] << 16);
+    const float hi = __uint_as_float(x[k] & 0xffff0000u) + __uint_as_float(y[k] & 0xffff0000u);
+    w[k] = (uint32_t)bf16_rne(lo) | ((uint32_t)bf16_rne(hi) << 16);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // R = extent of the tile along m (A) or n (B). KC tiles are stored [R][BK+PAD], the others
 // [BK][R+PAD]; both are moved as 16-byte chunks of 8 contiguous elements.
 template <int R, int BK, bool KC> struct Tile {
@@ -176,8 +190,9 @@ struct GemmK {
   const float* bias;
   const float* pro_scale;
   const float* pro_shift;
+  const uint16_t* addend;      // optional bf16 [M][ldc] added to a bf16 output (after rounding)
   int64_t lda, ldb, ldc;
-  int M, N, K, k_per_split, relu, out_bf16;
+  int M, N, K, k_per_split, relu, out_bf16, accumulate;   // accumulate: fp32 C += result
 };
 
 // Workgroup id → (m-tile, n-tile): consecutive ids are dealt round-robin to the 8 XCDs, so remap
@@ -338,9 +353,17 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       const uint16_t* src = Ch + r * LDH + cc;
       uint16_t* dst = static_cast<uint16_t*>(p.C) + (int64_t)gm * p.ldc + gn;
       if (vec && gn + 8 <= p.N) {
-        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+        uint4 v = *reinterpret_cast<const uint4*>(src);
+        if (p.addend) v = add_bf16x8(v, *reinterpret_cast<const uint4*>(p.addend + (int64_t)gm * p.ldc + gn));
+        *reinterpret_cast<uint4*>(dst) = v;
       } else {
-        for (int k = 0; k < 8 && gn + k < p.N; ++k) dst[k] = src[k];
+        for (int k = 0; k < 8 && gn + k < p.N; ++k) {
+          uint16_t h = src[k];
+          if (p.addend)
+            h = bf16_rne(__uint_as_float((uint32_t)h << 16) +
+                         __uint_as_float((uint32_t)p.addend[(int64_t)gm * p.ldc + gn + k] << 16));
+          dst[k] = h;
+        }
       }
     }
   } else {
@@ -377,10 +400,16 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
         if (gm >= p.M || gn >= p.N) continue;
         const float* src = Cs + r * LDC + cc;
         float* dst = dstbase + (int64_t)gm * ld + gn;
+        const bool acc_in = EPI != EPI_PARTIAL && p.accumulate;
         if (vec && gn + 4 <= p.N) {
-          *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+          float4 v = *reinterpret_cast<const float4*>(src);
+          if (acc_in) {
+            const float4 o = *reinterpret_cast<const float4*>(dst);
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *reinterpret_cast<float4*>(dst) = v;
         } else {
-          for (int k = 0; k < 4 && gn + k < p.N; ++k) dst[k] = src[k];
+          for (int k = 0; k < 4 && gn + k < p.N; ++k) dst[k] = acc_in ? dst[k] + src[k] : src[k];
         }
       }
     }
@@ -410,13 +439,15 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
 __global__ __launch_bounds__(GT) void k_splitk_reduce(const float* __restrict__ partial, int splits,
                                                       int zt_log2, void* __restrict__ C,
                                                       int64_t ldc, const float* __restrict__ bias,
-                                                      int relu, int M, int N, int out_bf16) {
+                                                      int relu, int M, int N, int out_bf16,
+                                                      const uint16_t* __restrict__ addend,
+                                                      int accumulate) {
   __shared__ float4 red[GT];
   const int ZT = 1 << zt_log2, OT = GT >> zt_log2;
   const int z = threadIdx.x / OT, o = threadIdx.x % OT;
   const int64_t total = (int64_t)M * N;
   const int64_t i0 = ((int64_t)blockIdx.x * OT + o) * 4;
-  const bool vec = (N & 3) == 0 && ldc == N;
+  const bool vec = (N & 3) == 0;
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i0 < total) {
     if (vec) {
@@ -447,8 +478,15 @@ __global__ __launch_bounds__(GT) void k_splitk_reduce(const float* __restrict__ 
     float x = out[k];
     if (bias) x += bias[n];
     if (relu) x = fmaxf(x, 0.f);
-    if (out_bf16) static_cast<uint16_t*>(C)[m * ldc + n] = bf16_rne(x);
-    else static_cast<float*>(C)[m * ldc + n] = x;
+    if (out_bf16) {
+      uint16_t h = bf16_rne(x);
+      if (addend)
+        h = bf16_rne(__uint_as_float((uint32_t)h << 16) + __uint_as_float((uint32_t)addend[m * ldc + n] << 16));
+      static_cast<uint16_t*>(C)[m * ldc + n] = h;
+    } else {
+      float* c = static_cast<float*>(C) + m * ldc + n;
+      *c = accumulate ? *c + x : x;
+    }
   }
 }
 
@@ -525,7 +563,8 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
   const int tiles = ((g.M + ts.bm - 1) / ts.bm) * ((g.N + ts.bn - 1) / ts.bn);
   const int epi = zs > 1 ? EPI_PARTIAL : (g.stats ? EPI_STATS : EPI_STORE);
   GemmK k{g.A, g.B, g.C, g.partial, g.stats, zs > 1 ? nullptr : g.bias, g.pro_scale, g.pro_shift,
-          g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, zs > 1 ? 0 : g.relu, g.out_bf16 ? 1 : 0};
+          g.addend, g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, zs > 1 ? 0 : g.relu,
+          g.out_bf16 ? 1 : 0, g.accumulate ? 1 : 0};
   const dim3 grid(tiles, zs);
   switch (t) {
     case GEMM_T128x128x64: launch_tile<128, 128, 64>(g, k, epi, grid, st); break;
@@ -542,7 +581,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
     const int64_t groups = (total + 3) / 4, ot = GT >> zl;
     const dim3 rg((unsigned)((groups + ot - 1) / ot));
     hipLaunchKernelGGL(k_splitk_reduce, rg, dim3(GT), 0, st, g.partial, zs, zl, g.C, g.ldc, g.bias,
-                       g.relu, g.M, g.N, g.out_bf16 ? 1 : 0);
+                       g.relu, g.M, g.N, g.out_bf16 ? 1 : 0, g.addend, g.accumulate ? 1 : 0);
   }
 }
 

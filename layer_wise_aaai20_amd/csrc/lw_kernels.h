@@ -127,8 +127,13 @@ struct BNArgs {
   float* A;             // [C] backward coefficients
   float* B;
   float* Cc;
+  const float* res_scale;  // forward: residual through its own BN affine (or nullptr)
+  const float* res_shift;
+  int stats_blocks;        // bn_stats: >0 = partial sums already written by a GEMM epilogue
 };
 int bn_reduce_blocks(int64_t M, int C);
+void bn_stats(const BNArgs& a, hipStream_t st);
+void bn_apply(const BNArgs& a, hipStream_t st);
 void bn_forward(const BNArgs& a, hipStream_t st);
 void bn_backward(const BNArgs& a, hipStream_t st);
 
@@ -153,6 +158,8 @@ struct GemmArgs {
   const float* pro_scale;  // optional prologue relu(v*scale+shift): per-k of a K-contiguous A
   const float* pro_shift;  // (pro_on_a) or per-n of an N-contiguous B
   bool pro_on_a;
+  const uint16_t* addend;  // optional bf16 [M][ldc] added to a bf16 output (dgrad + residual grad)
+  bool accumulate;         // fp32 output: C += result (weight gradients into the zeroed arena)
 };
 enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_T256x64x32 = 3,
                 GEMM_T64x256x32 = 4, GEMM_T256x64x64 = 5,

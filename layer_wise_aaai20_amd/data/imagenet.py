@@ -6,13 +6,17 @@ Counterparts of ``IMAGENET/training/dataloader.py`` (``get_loaders``, ``BatchTra
 No network and no ImageNet copy are available here, so the dataset is synthetic: per-sample uint8
 NHWC images of the phase's size and labels drawn from a fixed seed. Everything downstream (GPU
 normalisation, sharding, uneven last batches, rect-val batch shapes) is the real code path.
-``ImageFolderU8`` can read a real ``<root>/<class>/<image>`` tree when PIL is importable.
+``ImageFolderU8`` reads a real ``<root>/<class>/<image>`` tree with PIL (decode in DataLoader
+workers; uint8 HWC out, normalised on the GPU): ``RandomResizedCropFlip`` for training,
+``ResizeCenterCrop`` / ``CropArTfm`` (rect-val) for validation, aspect ratios cached as JSON.
 """
 from __future__ import annotations
 
+import json
 import math
 import os
-from typing import List, Optional, Sequence
+import random
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -149,6 +153,181 @@ class RectValDataset(Dataset):
         return rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8), label
 
 
+# ----------------------------------------------------------------------------- real folders
+IMG_EXTS = (".jpg", ".jpeg", ".png", ".bmp", ".webp", ".ppm", ".tif", ".tiff")
+
+
+def find_classes(root: str) -> Tuple[List[str], dict]:
+    classes = sorted(d.name for d in os.scandir(root) if d.is_dir())
+    if not classes:
+        raise FileNotFoundError(f"no class sub-directories under {root}")
+    return classes, {c: i for i, c in enumerate(classes)}
+
+
+def make_samples(root: str) -> List[Tuple[str, int]]:
+    classes, idx = find_classes(root)
+    out = []
+    for c in classes:
+        for dirpath, _, files in sorted(os.walk(os.path.join(root, c))):
+            for f in sorted(files):
+                if f.lower().endswith(IMG_EXTS):
+                    out.append((os.path.join(dirpath, f), idx[c]))
+    return out
+
+
+def _rng() -> random.Random:
+    """Per-worker RNG seeded from torch's per-worker seed (numpy is not reseeded by DataLoader)."""
+    seed = torch.initial_seed()
+    r = getattr(_rng, "_r", None)
+    if r is None or getattr(_rng, "_seed", None) != seed:
+        _rng._r, _rng._seed = random.Random(seed), seed
+    return _rng._r
+
+
+class RandomResizedCropFlip:
+    """Inception-style crop: area in ``scale`` of the image, log-uniform aspect ratio in
+    ``ratio``, 10 tries then a centre crop; bilinear resize to ``size``; horizontal flip with
+    p = 0.5 (``dataloader.py:28-31``)."""
+
+    def __init__(self, size: int, scale=(0.08, 1.0), ratio=(3 / 4, 4 / 3), flip: bool = True):
+        self.size, self.scale, self.ratio, self.flip = size, scale, ratio, flip
+
+    def box(self, w: int, h: int, r: random.Random):
+        area = w * h
+        lr = (math.log(self.ratio[0]), math.log(self.ratio[1]))
+        for _ in range(10):
+            target = area * r.uniform(*self.scale)
+            ar = math.exp(r.uniform(*lr))
+            cw, ch = int(round(math.sqrt(target * ar))), int(round(math.sqrt(target / ar)))
+            if 0 < cw <= w and 0 < ch <= h:
+                x0, y0 = r.randint(0, w - cw), r.randint(0, h - ch)
+                return x0, y0, cw, ch
+        in_ar = w / h
+        if in_ar < self.ratio[0]:
+            cw, ch = w, int(round(w / self.ratio[0]))
+        elif in_ar > self.ratio[1]:
+            ch, cw = h, int(round(h * self.ratio[1]))
+        else:
+            cw, ch = w, h
+        return (w - cw) // 2, (h - ch) // 2, cw, ch
+
+    def __call__(self, img, index: int = 0):
+        from PIL import Image
+        r = _rng()
+        x0, y0, cw, ch = self.box(img.width, img.height, r)
+        img = img.resize((self.size, self.size), Image.BILINEAR, box=(x0, y0, x0 + cw, y0 + ch))
+        if self.flip and r.random() < 0.5:
+            img = img.transpose(Image.FLIP_LEFT_RIGHT)
+        return img
+
+
+class ResizeCenterCrop:
+    """Validation: shorter side → ``int(size * 1.14)``, centre crop ``size`` (``dataloader.py:
+    60-74``)."""
+
+    def __init__(self, size: int, resize: Optional[int] = None):
+        self.size, self.resize = size, resize or int(size * 1.14)
+
+    def __call__(self, img, index: int = 0):
+        from PIL import Image
+        w, h = img.size
+        s = self.resize / min(w, h)
+        nw, nh = max(self.size, int(round(w * s))), max(self.size, int(round(h * s)))
+        img = img.resize((nw, nh), Image.BILINEAR)
+        x0, y0 = (nw - self.size) // 2, (nh - self.size) // 2
+        return img.crop((x0, y0, x0 + self.size, y0 + self.size))
+
+
+class CropArTfm:
+    """Rect-val: resize the shorter side to ``size`` and centre-crop to the batch's mean aspect
+    ratio (``crop_size_for_ar``), so a batch shares one (h, w) (``dataloader.py:164-201``)."""
+
+    def __init__(self, idx2ar: dict, size: int):
+        self.idx2ar, self.size = idx2ar, size
+
+    def __call__(self, img, index: int = 0):
+        from PIL import Image
+        th, tw = crop_size_for_ar(self.idx2ar[index], self.size)
+        w, h = img.size
+        s = max(tw / w, th / h)
+        nw, nh = max(tw, int(round(w * s))), max(th, int(round(h * s)))
+        img = img.resize((nw, nh), Image.BILINEAR)
+        x0, y0 = (nw - tw) // 2, (nh - th) // 2
+        return img.crop((x0, y0, x0 + tw, y0 + th))
+
+
+class ImageFolderU8(Dataset):
+    """``<root>/<class>/<image>`` → (uint8 [H, W, 3], class index); decoding and augmentation run
+    in the DataLoader workers, normalisation on the GPU (``BatchTransformDataLoader``)."""
+
+    def __init__(self, root: str, transform: Optional[Callable] = None,
+                 samples: Optional[List[Tuple[str, int]]] = None):
+        self.root = root
+        self.samples = samples if samples is not None else make_samples(root)
+        self.transform = transform
+
+    def __len__(self):
+        return len(self.samples)
+
+    def __getitem__(self, i):
+        from PIL import Image
+        path, label = self.samples[i]
+        with Image.open(path) as im:
+            img = im.convert("RGB")
+        if self.transform is not None:
+            img = self.transform(img, i)
+        return np.asarray(img, dtype=np.uint8), label
+
+
+def sort_ar_folder(valdir: str, cache: Optional[str] = None) -> List[tuple]:
+    """[(w/h, index)] of a real validation folder, sorted; image headers only (no decode). Cached
+    as JSON next to the data (the reference pickles ``sorted_idxar.p``; nothing is unpickled
+    here)."""
+    cache = cache or os.path.join(os.path.dirname(os.path.normpath(valdir)), "sorted_idxar.json")
+    samples = make_samples(valdir)
+    if os.path.exists(cache):
+        with open(cache) as f:
+            data = json.load(f)
+        if len(data) == len(samples):
+            return [(float(a), int(i)) for a, i in data]
+    from PIL import Image
+    ars = []
+    for i, (path, _) in enumerate(samples):
+        with Image.open(path) as im:
+            w, h = im.size
+        ars.append((w / h, i))
+    out = sorted(ars)
+    try:
+        with open(cache, "w") as f:
+            json.dump(out, f)
+    except OSError:
+        pass
+    return out
+
+
+def _folder_loaders(traindir, valdir, sz, bs, val_bs, workers, rect_val, min_scale,
+                    distributed, device, dtype):
+    from ..parallel import comm
+    train_ds = ImageFolderU8(traindir, RandomResizedCropFlip(sz, scale=(min_scale, 1.0)))
+    trn_smp = torch.utils.data.distributed.DistributedSampler(
+        train_ds, num_replicas=comm.world_size(), rank=comm.rank()) if distributed else None
+    trn = DataLoader(train_ds, batch_size=bs, shuffle=trn_smp is None, num_workers=workers,
+                     collate_fn=fast_collate, sampler=trn_smp, pin_memory=True,
+                     persistent_workers=workers > 0)
+    if rect_val:
+        idx_ar = sort_ar_folder(valdir)
+        val_ds = ImageFolderU8(valdir, CropArTfm(map_idx2ar(idx_ar, val_bs), sz))
+        order = [i for _, i in idx_ar]
+    else:
+        val_ds = ImageFolderU8(valdir, ResizeCenterCrop(sz))
+        order = list(range(len(val_ds)))
+    val_smp = DistValSampler(order, val_bs, distributed)
+    val = DataLoader(val_ds, batch_sampler=val_smp, num_workers=workers, collate_fn=fast_collate,
+                     pin_memory=True)
+    return (BatchTransformDataLoader(trn, device, dtype),
+            BatchTransformDataLoader(val, device, dtype), trn_smp, val_smp)
+
+
 def get_loaders(traindir=None, valdir=None, sz=128, bs=256, val_bs=None, workers=0,
                 rect_val=False, min_scale=0.08, distributed=False, n_train=None, n_val=None,
                 device=None, dtype=torch.float32, seed=0, synthetic=True):
@@ -161,8 +340,8 @@ def get_loaders(traindir=None, valdir=None, sz=128, bs=256, val_bs=None, workers
     n_train = n_train or 64 * bs
     n_val = n_val or 8 * val_bs
     if not synthetic:
-        raise NotImplementedError("real ImageNet folders need ImageFolderU8 (PIL) — not available "
-                                  "offline; use synthetic=True")
+        return _folder_loaders(traindir, valdir, sz, bs, val_bs, workers, rect_val, min_scale,
+                               distributed, device, dtype)
     train_ds = SyntheticImageNet(n_train, sz, seed=seed)
     trn_smp = torch.utils.data.distributed.DistributedSampler(
         train_ds, num_replicas=comm.world_size(), rank=comm.rank()) if distributed else None

@@ -1,0 +1,332 @@
+"""Whole-block fused ResNet bottleneck for MI355X training.
+
+The reference runs a bottleneck (``IMAGENET/training/resnet.py:80-118``) as nine separate cuDNN /
+ATen ops — conv, BN, ReLU three times, plus the shortcut add — and autograd adds the two gradient
+branches of the block input with one more elementwise kernel. On MI355X every one of those ops is
+an HBM round trip over a large NHWC activation, and the 1x1 convolutions themselves are
+bandwidth-bound (K = 64..512), so the block is organised around the MFMA GEMM of ``csrc/gemm.hip``
+and its prologue / epilogue fusions instead:
+
+forward (training)::
+
+    c1 = x·W1ᵀ                       GEMM, epilogue writes BN1 column statistics
+    a1 = relu(bn1(c1))               one apply pass (the 3x3 conv needs it materialised)
+    c2 = conv3x3(a1)                 MIOpen (channels_last bf16)
+    bn2 statistics                   one reduce pass
+    c3 = relu(bn2(c2))·W3ᵀ           GEMM, BN2-apply+ReLU in the prologue, BN3 stats in the epilogue
+    [cd = x_s·Wdᵀ                    GEMM + stats (downsample shortcut)]
+    out = relu(bn3(c3) + x | bnd(cd)) one pass (the shortcut BN is applied on the fly)
+
+backward::
+
+    bn3 backward (mask from out)     → dc3, dres
+    dW3 = dc3ᵀ·relu(bn2(c2))         GEMM, BN2-apply recomputed in the prologue, fp32 written
+                                     straight into the gradient arena
+    da2 = dc3·W3                     GEMM
+    bn2 backward (mask from c2)      → dc2
+    conv3x3 backward                 MIOpen
+    bn1 backward (mask from c1)      → dc1
+    dW1 = dc1ᵀ·x                     GEMM into the arena
+    dx  = dc1·W1 + dres              GEMM with the shortcut gradient added in the epilogue
+
+Compared with the per-layer path this removes, per block, the BN1 and BN3 statistics passes, the
+BN2 apply pass and its materialised output, the shortcut-BN apply pass, the gradient add of the
+block input, and the fp32 casts/accumulations of the weight gradients.
+
+Weight / BN-parameter gradients go **directly into the gradient arena** when the parameter is
+owned by a :class:`~..parallel.ddp.CompressedDDP` (which marks it with ``_lw_grad_ready``); the
+bucket engine is then notified exactly as a post-accumulate-grad hook would, so compression and
+communication still overlap the rest of the backward pass. Without an arena the gradients are
+returned through autograd as usual.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from ._ext import load
+
+BF16 = torch.bfloat16
+CL = torch.channels_last
+TILES = (1, 2, 3, 4, 5, 6)          # csrc GemmTile ids (0 = heuristic)
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    """channels_last NCHW → [N*H*W, C] view (no copy)."""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def _nchw(rows: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    return rows.view(n, h, w, rows.shape[1]).permute(0, 3, 1, 2)
+
+
+# ----------------------------------------------------------------------------- GEMM + tuner
+def _splits(tiles: int, K: int) -> int:
+    want = max(1, 512 // max(tiles, 1))
+    return int(max(1, min(want, K // 256 if K >= 512 else 1)))
+
+
+def _tile_dims(t: int) -> Tuple[int, int]:
+    return {1: (128, 128), 2: (128, 128), 3: (256, 64), 4: (64, 256), 5: (256, 64),
+            6: (64, 64)}[t]
+
+
+class GemmTuner:
+    """MIOpen-find-style tile selection for the MFMA GEMM: the first time a problem key is seen,
+    every tile shape is timed with HIP events on scratch outputs and the fastest is kept for the
+    rest of the run. ``LWAAAI_GEMM_TUNE=0`` falls back to the built-in heuristic."""
+
+    def __init__(self):
+        self.best: Dict[tuple, int] = {}
+        self.enabled = os.environ.get("LWAAAI_GEMM_TUNE", "1") != "0"
+
+    def pick(self, key, run) -> int:
+        t = self.best.get(key)
+        if t is not None:
+            return t
+        if not self.enabled or torch.cuda.is_current_stream_capturing():
+            self.best[key] = 0
+            return 0
+        times = []
+        for tile in TILES:
+            run(tile)                                  # compile / warm
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(3):
+                run(tile)
+            e.record()
+            e.synchronize()
+            times.append((s.elapsed_time(e), tile))
+        t = min(times)[1]
+        self.best[key] = t
+        return t
+
+
+TUNER = GemmTuner()
+
+
+def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro=None,
+         pro_on_a=True, out=None, addend=None, accumulate=False, ldc=0, split_k=False):
+    """One MFMA GEMM launch (plus the split-K reduce when ``split_k``); see ``csrc/gemm.hip``."""
+    lib = load()
+    ps, ph = (pro[0], pro[1]) if pro is not None else (None, None)
+
+    def splits_for(tile):
+        if not split_k:
+            return 1
+        bm, bn = _tile_dims(tile if tile else 1)
+        return _splits(-(-M // bm) * -(-N // bn), K)
+
+    key = (M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a, split_k,
+           addend is not None)
+
+    def run(tile):
+        lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile), out_bf16,
+                    tile, ps, ph, pro_on_a, stats, None, None, False, 0)
+    tile = TUNER.pick(key, run)
+    return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile),
+                       out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc)
+
+
+# ----------------------------------------------------------------------------- grad sink
+def _direct(p: torch.Tensor) -> bool:
+    """True when ``p.grad`` is an arena view the engine wants written in place."""
+    return getattr(p, "_lw_grad_ready", None) is not None and p.grad is not None
+
+
+def _wgrad_target(p: torch.Tensor, shape) -> Tuple[torch.Tensor, bool]:
+    """fp32 [rows, cols] destination for a 1x1-conv weight gradient: the arena view (accumulate)
+    or a fresh zero buffer returned through autograd."""
+    if _direct(p):
+        return p.grad.view(shape), True
+    return torch.zeros(shape, dtype=torch.float32, device=p.device), False
+
+
+def _finish_param(p: torch.Tensor, g: Optional[torch.Tensor], direct: bool):
+    """Deliver gradient ``g`` of parameter ``p``: add it into the arena view and notify the
+    engine (``g=None``: already accumulated in place), or return it through autograd."""
+    if direct:
+        if g is not None:
+            p.grad.add_(g.view(p.grad.shape))
+        p._lw_grad_ready(p)
+        return None
+    return g.view_as(p) if g is not None else None
+
+
+def _finish_wgrad(p: torch.Tensor, dst: torch.Tensor, direct: bool):
+    return _finish_param(p, None, True) if direct else dst.view_as(p)
+
+
+def _bn_momentum(bn) -> float:
+    if bn.momentum is None:
+        return 1.0 / float(bn.num_batches_tracked)
+    return float(bn.momentum)
+
+
+def _bump(bn) -> None:
+    if bn.track_running_stats and bn.num_batches_tracked is not None and \
+            not getattr(bn, "_shared_counter", False):
+        bn.num_batches_tracked.add_(1)
+
+
+# ----------------------------------------------------------------------------- the block
+class _BottleneckFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd, mods):
+        lib = load()
+        bn1, bn2, bn3, conv2, bnd, down_stride = mods
+        for bn in (bn1, bn2, bn3) + ((bnd,) if bnd is not None else ()):
+            _bump(bn)                 # before the momentum is read (momentum=None: 1/n)
+        stride = conv2.stride
+        N, Cin, H, W = x.shape
+        x = x.to(BF16).contiguous(memory_format=CL)
+        xr = _rows(x)
+        width = w1.shape[0]
+        cout = w3.shape[0]
+        W1 = w1.detach().reshape(width, Cin).to(BF16)
+        W2 = w2.detach().to(BF16).contiguous(memory_format=CL)
+        W3 = w3.detach().reshape(cout, width).to(BF16)
+        M = xr.shape[0]
+        # conv1 (1x1) + BN1 statistics in the epilogue
+        c1, st1 = gemm(xr, Cin, True, W1, Cin, True, M, width, Cin, stats=True)
+        mean1, inv1, ss1 = lib.bn_stats(c1, st1, g1, b1, bn1.running_mean, bn1.running_var,
+                                        _bn_momentum(bn1), bn1.eps)
+        a1 = lib.bn_apply(c1, ss1, None, None, True)
+        a1n = _nchw(a1, N, H, W)
+        c2n = torch.ops.aten.convolution(a1n, W2, None, list(stride), list(conv2.padding),
+                                         list(conv2.dilation), False, [0, 0], 1)
+        c2n = c2n.contiguous(memory_format=CL)
+        N2, _, H2, W2_ = c2n.shape
+        c2 = _rows(c2n)
+        M2 = c2.shape[0]
+        mean2, inv2, ss2 = lib.bn_stats(c2, None, g2, b2, bn2.running_mean, bn2.running_var,
+                                        _bn_momentum(bn2), bn2.eps)
+        # conv3 (1x1) with BN2-apply+ReLU in the prologue and BN3 statistics in the epilogue
+        c3, st3 = gemm(c2, width, True, W3, width, True, M2, cout, width, stats=True,
+                       pro=(ss2[:width], ss2[width:]), pro_on_a=True)
+        mean3, inv3, ss3 = lib.bn_stats(c3, st3, g3, b3, bn3.running_mean, bn3.running_var,
+                                        _bn_momentum(bn3), bn3.eps)
+        if bnd is not None:
+            s = down_stride
+            xs = x if s == 1 else x[:, :, ::s, ::s].contiguous(memory_format=CL)
+            xsr = _rows(xs)
+            Wd = wd.detach().reshape(cout, Cin).to(BF16)
+            cd, std = gemm(xsr, Cin, True, Wd, Cin, True, M2, cout, Cin, stats=True)
+            meand, invd, ssd = lib.bn_stats(cd, std, gd, bd, bnd.running_mean, bnd.running_var,
+                                            _bn_momentum(bnd), bnd.eps)
+            out = lib.bn_apply(c3, ss3, cd, ssd, True)
+            ctx.save_for_backward(x, c1, a1, c2, c3, out, W1, W2, W3, g1, g2, g3, mean1, inv1,
+                                  ss1, mean2, inv2, ss2, mean3, inv3, xsr, cd, Wd, gd, meand,
+                                  invd)
+            ctx.down_stride = s
+        else:
+            out = lib.bn_apply(c3, ss3, xr, None, True)
+            ctx.save_for_backward(x, c1, a1, c2, c3, out, W1, W2, W3, g1, g2, g3, mean1, inv1,
+                                  ss1, mean2, inv2, ss2, mean3, inv3)
+            ctx.down_stride = 0
+        ctx.geom = (N, Cin, H, W, N2, H2, W2_, width, cout, M, M2)
+        ctx.conv2 = (list(stride), list(conv2.padding), list(conv2.dilation))
+        ctx.params = (w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd)
+        return _nchw(out, N2, H2, W2_)
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = load()
+        saved = ctx.saved_tensors
+        x, c1, a1, c2, c3, out, W1, W2, W3, g1, g2, g3, mean1, inv1, ss1, mean2, inv2, ss2, \
+            mean3, inv3 = saved[:20]
+        N, Cin, H, W, N2, H2, W2_, width, cout, M, M2 = ctx.geom
+        w1, g1p, b1p, w2, g2p, b2p, w3, g3p, b3p, wd, gdp, bdp = ctx.params
+        has_down = ctx.down_stride > 0
+        dr = _rows(dout.to(BF16).contiguous(memory_format=CL))
+        # BN3 (+ shortcut) backward, ReLU mask from the block output
+        dc3, dg3, db3, dres = lib.bn_bwd(dr, c3, out, g3, mean3, inv3, None, True, True, True)
+        grads = {}
+        # conv3: weight gradient with BN2-apply recomputed in the B prologue, into the arena
+        dst3, d3 = _wgrad_target(w3, (cout, width))
+        gemm(dc3, cout, False, c2, width, False, cout, width, M2, out_bf16=False,
+             pro=(ss2[:width], ss2[width:]), pro_on_a=False, out=dst3, accumulate=True,
+             split_k=True)
+        grads["w3"] = _finish_wgrad(w3, dst3, d3)
+        da2, _ = gemm(dc3, cout, True, W3, width, False, M2, width, cout)
+        dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False)
+        # conv2 (3x3) backward on MIOpen
+        a1n = _nchw(a1, N, H, W)
+        dc2n = _nchw(dc2, N2, H2, W2_)
+        stride, padding, dilation = ctx.conv2
+        da1n, dW2, _ = torch.ops.aten.convolution_backward(
+            dc2n, a1n, W2, None, stride, padding, dilation, False, [0, 0], 1,
+            [True, True, False])
+        if _direct(w2):
+            w2.grad.add_(dW2)
+            grads["w2"] = _finish_param(w2, None, True)
+        else:
+            grads["w2"] = dW2.float().contiguous(memory_format=CL)
+        da1 = _rows(da1n.contiguous(memory_format=CL))
+        dc1, dg1, db1, _ = lib.bn_bwd(da1, c1, None, g1, mean1, inv1, ss1, True, True, False)
+        xr = _rows(x)
+        dst1, d1 = _wgrad_target(w1, (width, Cin))
+        gemm(dc1, width, False, xr, Cin, False, width, Cin, M, out_bf16=False, out=dst1,
+             accumulate=True, split_k=True)
+        grads["w1"] = _finish_wgrad(w1, dst1, d1)
+        if has_down:
+            xsr, cd, Wd, gd, meand, invd = saved[20:]
+            s = ctx.down_stride
+            dcd, dgd, dbd, _ = lib.bn_bwd(dres, cd, None, gd, meand, invd, None, True, False,
+                                          False)
+            dstd, dd = _wgrad_target(wd, (cout, Cin))
+            gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2, out_bf16=False, out=dstd,
+                 accumulate=True, split_k=True)
+            grads["wd"] = _finish_wgrad(wd, dstd, dd)
+            dx, _ = gemm(dc1, width, True, W1, Cin, False, M, Cin, width)
+            if s == 1:
+                gemm(dcd, cout, True, Wd, Cin, False, M2, Cin, cout, out=dx, addend=dx)
+            else:
+                dxs, _ = gemm(dcd, cout, True, Wd, Cin, False, M2, Cin, cout)
+                dxv = dx.view(N, H, W, Cin)
+                dxv[:, ::s, ::s, :] += dxs.view(N2, H2, W2_, Cin)
+            grads["gd"] = _finish_param(gdp, dgd, _direct(gdp))
+            grads["bd"] = _finish_param(bdp, dbd, _direct(bdp))
+        else:
+            dx, _ = gemm(dc1, width, True, W1, Cin, False, M, Cin, width, addend=dres)
+        for name, p, g in (("g1", g1p, dg1), ("b1", b1p, db1), ("g2", g2p, dg2),
+                           ("b2", b2p, db2), ("g3", g3p, dg3), ("b3", b3p, db3)):
+            grads[name] = _finish_param(p, g, _direct(p))
+        dxn = _nchw(dx, N, H, W)
+        return (dxn, grads["w1"], grads["g1"], grads["b1"], grads["w2"], grads["g2"], grads["b2"],
+                grads["w3"], grads["g3"], grads["b3"], grads.get("wd"), grads.get("gd"),
+                grads.get("bd"), None)
+
+
+def block_supported(m, x: torch.Tensor) -> bool:
+    """The fused path needs a CUDA bf16-able channels_last input, BN with affine params and
+    running stats, 8-aligned channel counts and a plain 1x1 / 3x3 / 1x1 bottleneck."""
+    if not (x.is_cuda and x.dim() == 4 and m.training):
+        return False
+    bns = [m.bn1, m.bn2, m.bn3] + ([m.downsample[1]] if m.downsample is not None else [])
+    if any(not (b.affine and b.track_running_stats) for b in bns):
+        return False
+    if any(c.groups != 1 for c in (m.conv1, m.conv2, m.conv3)):
+        return False
+    chans = [x.shape[1], m.conv1.out_channels, m.conv3.out_channels]
+    return all(c % 8 == 0 for c in chans)
+
+
+def bottleneck_forward(m, x: torch.Tensor) -> torch.Tensor:
+    """Training forward of a ``models.resnet.Bottleneck`` through :class:`_BottleneckFn`."""
+    down = m.downsample
+    if down is not None:
+        wd, bnd = down[0].weight, down[1]
+        gd, bd, ds = bnd.weight, bnd.bias, down[0].stride[0]
+    else:
+        wd = gd = bd = bnd = None
+        ds = 0
+    mods = (m.bn1, m.bn2, m.bn3, m.conv2, bnd, ds)
+    with torch.autocast("cuda", enabled=False):
+        return _BottleneckFn.apply(x, m.conv1.weight, m.bn1.weight, m.bn1.bias, m.conv2.weight,
+                                   m.bn2.weight, m.bn2.bias, m.conv3.weight, m.bn3.weight,
+                                   m.bn3.bias, wd, gd, bd, mods)

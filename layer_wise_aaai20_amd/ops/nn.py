@@ -150,6 +150,15 @@ def _fused_bottleneck_forward(self, x):
     return self.bn3(self.conv3(out), identity)
 
 
+def _block_bottleneck_forward(self, x):
+    """Training: the whole-block fused path (``ops/block.py``); eval / unsupported shapes: the
+    per-layer fused path."""
+    from . import block
+    if block.block_supported(self, x):
+        return block.bottleneck_forward(self, x)
+    return _fused_bottleneck_forward(self, x)
+
+
 def _fused_basic_forward(self, x):
     identity = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
     out = self.bn1(self.conv1(x))
@@ -163,8 +172,9 @@ def _fused_resnet_forward(self, x):
     return self.fc(x)
 
 
-def fuse_resnet(model: nn.Module) -> nn.Module:
-    """Switch a ``models.resnet`` network to fused BN(+add)(+ReLU). Parameter/buffer names and
+def fuse_resnet(model: nn.Module, block: bool = True) -> nn.Module:
+    """Switch a ``models.resnet`` network to fused BN(+add)(+ReLU) and — with ``block`` — its
+    bottlenecks to the whole-block fused MFMA path (``ops/block.py``). Parameter/buffer names and
     values are untouched; only forward changes."""
     from ..models import resnet as R
     import types
@@ -175,7 +185,8 @@ def fuse_resnet(model: nn.Module) -> nn.Module:
             to_fused_bn(m.bn3, relu=True)
             if m.downsample is not None:
                 to_fused_bn(m.downsample[1], relu=False)
-            m.forward = types.MethodType(_fused_bottleneck_forward, m)
+            fwd = _block_bottleneck_forward if block else _fused_bottleneck_forward
+            m.forward = types.MethodType(fwd, m)
         elif isinstance(m, R.BasicBlock):
             to_fused_bn(m.bn1, relu=True)
             to_fused_bn(m.bn2, relu=True)

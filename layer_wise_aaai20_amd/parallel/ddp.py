@@ -61,7 +61,11 @@ class CompressedDDP(nn.Module):
     def _register_hooks(self) -> None:
         for seg in self.engine.arena.segments:
             p = seg.param
-            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(seg.index)))
+            hook = self._make_hook(seg.index)
+            self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+            # fused ops (ops/block.py) write this parameter's gradient straight into its arena
+            # view and then call the same hook, bypassing AccumulateGrad
+            p._lw_grad_ready = hook
 
     def _make_hook(self, seg_index: int):
         engine = self.engine

@@ -257,12 +257,23 @@ class DataManager:
         if self.args.short_epoch:
             val_bs = bs
         n_train = self.args.synthetic_size or (12 if self.args.short_epoch else 64) * bs
+        synthetic = self.args.data in ("synthetic", "")
+        if not synthetic:
+            # phases may name pre-resized copies (<data>-sz/160); use the full-size tree if absent
+            if not os.path.isdir(trndir):
+                trndir = os.path.join(self.args.data, "train")
+            if not os.path.isdir(valdir):
+                valdir = os.path.join(self.args.data, "validation")
+            for d in (trndir, valdir):
+                if not os.path.isdir(d):
+                    raise FileNotFoundError(f"ImageNet directory {d} not found (pass 'synthetic' "
+                                            "as DIR for the synthetic dataset)")
         return D.get_loaders(trndir, valdir, sz=sz, bs=bs, val_bs=val_bs,
                              workers=self.args.workers, rect_val=kw.get("rect_val", False),
                              min_scale=kw.get("min_scale", 0.08),
                              distributed=self.args.distributed, n_train=n_train,
                              n_val=(4 if self.args.short_epoch else 8) * val_bs,
-                             device=self.device, dtype=self.dtype)
+                             device=self.device, dtype=self.dtype, synthetic=synthetic)
 
 
 # ------------------------------------------------------------------------------------ run state

@@ -7,6 +7,7 @@ import sys
 CATS = [
     ("lwaaai compress/unpack", r"lw::k_(small_select|hist|select|count|scan|write|fill_tail|unpack|thresh|set_caps|partial|finalize|quant|dequant)"),
     ("lwaaai sgd", r"lw::k_sgd"),
+    ("lwaaai gemm", r"lw::k_(gemm|splitk)"),
     ("lwaaai nn", r"lw::k_(normalize|bn|relu|add|pool|ce)"),
     ("conv fwd", r"igemm_fwd|conv_fwd|ConvFwd|grouped_conv_fwd|naive_conv_fwd"),
     ("conv bwd-data", r"igemm_bwd|bwd_data|ConvBwdData"),

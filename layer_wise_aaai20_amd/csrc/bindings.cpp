@@ -508,7 +508,7 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
   }
   if (want_stats) {
     TORCH_CHECK(zs == 1, "column statistics need splits == 1");
-    stats = at::empty({2, N, (int64_t)lw::gemm_tiles_m(g)}, A.options().dtype(at::kFloat));
+    stats = at::empty({(int64_t)lw::gemm_tiles_m(g), 2, N}, A.options().dtype(at::kFloat));
     g.stats = ptr<float>(stats);
   } else {
     stats = at::empty({0}, A.options().dtype(at::kFloat));
@@ -561,16 +561,86 @@ std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stat
   Tensor partial;
   if (stats.has_value() && stats->defined()) {
     check_dtype(*stats, at::kFloat, "stats");
-    TORCH_CHECK(stats->dim() == 3 && stats->size(0) == 2 && stats->size(1) == C &&
-                stats->is_contiguous(), "stats must be a contiguous [2, C, nb] tensor");
-    a.partial = ptr<float>(*stats);
-    a.stats_blocks = (int)stats->size(2);
+    TORCH_CHECK(stats->dim() == 3 && stats->size(1) == 2 && stats->size(2) == C &&
+                stats->is_contiguous(), "stats must be a contiguous [rows, 2, C] tensor");
+    const int64_t R = stats->size(0);
+    partial = at::empty({(R < 256 ? R : 256) * 2 * C}, f32);
+    a.partial = ptr<float>(partial);
+    a.stat_rows = ptr<float>(*stats);
+    a.stats_rows_n = R;
   } else {
     partial = at::empty({(int64_t)lw::bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
     a.partial = ptr<float>(partial);
   }
   lw::bn_stats(a, cur_stream());
   return {mean, invstd, ss};
+}
+
+// fused stem BN-apply + ReLU + max-pool (bn.hip)
+static void stem_geom(const Tensor& x, int64_t k, int64_t s, int64_t p, lw::StemArgs& a) {
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem input must be channels_last 4-D");
+  check_dtype(x, at::kBFloat16, "x");
+  a.N = (int)x.size(0); a.C = (int)x.size(1); a.H = (int)x.size(2); a.W = (int)x.size(3);
+  TORCH_CHECK(a.C % 8 == 0, "stem pool needs C % 8 == 0");
+  TORCH_CHECK(k >= 1 && k * k <= 255 && s >= 1 && p >= 0 && p < k, "pool geometry");
+  a.k = (int)k; a.s = (int)s; a.p = (int)p;
+  a.Ho = (int)((a.H + 2 * p - k) / s + 1);
+  a.Wo = (int)((a.W + 2 * p - k) / s + 1);
+}
+
+std::tuple<Tensor, Tensor> stem_pool_fwd(Tensor x, Tensor scale_shift, int64_t k, int64_t s,
+                                         int64_t p) {
+  const c10::DeviceGuard guard(x.device());
+  lw::StemArgs a{};
+  stem_geom(x, k, s, p, a);
+  check_dtype(scale_shift, at::kFloat, "scale_shift");
+  TORCH_CHECK(scale_shift.numel() == 2 * a.C && scale_shift.is_contiguous(), "scale_shift");
+  Tensor out = at::empty({a.N, a.C, a.Ho, a.Wo},
+                         x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor idx = at::empty({(int64_t)a.N * a.Ho * a.Wo * a.C}, x.options().dtype(at::kByte));
+  a.x = x.data_ptr();
+  a.scale = ptr<float>(scale_shift);
+  a.shift = a.scale + a.C;
+  a.out = out.data_ptr();
+  a.idx = ptr<uint8_t>(idx);
+  lw::stem_pool_fwd(a, cur_stream());
+  return {out, idx};
+}
+
+std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x,
+                                                 Tensor scale_shift, c10::optional<Tensor> weight,
+                                                 Tensor mean, Tensor invstd, int64_t k, int64_t s,
+                                                 int64_t p) {
+  const c10::DeviceGuard guard(x.device());
+  lw::StemArgs a{};
+  stem_geom(x, k, s, p, a);
+  check_dtype(dp, at::kBFloat16, "dp");
+  TORCH_CHECK(dp.is_contiguous(at::MemoryFormat::ChannelsLast) && dp.size(2) == a.Ho &&
+              dp.size(3) == a.Wo && dp.size(1) == a.C && dp.size(0) == a.N, "dp shape/layout");
+  TORCH_CHECK(idx.numel() == dp.numel() && idx.scalar_type() == at::kByte, "idx");
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor dx = at::empty_like(x);
+  Tensor dgamma = at::empty({a.C}, f32), dbeta = at::empty({a.C}, f32);
+  Tensor coef = at::empty({3 * a.C}, f32);
+  Tensor partial = at::empty({(int64_t)lw::bn_reduce_blocks((int64_t)a.N * a.H * a.W, a.C) * 2 * a.C}, f32);
+  a.x = x.data_ptr();
+  a.dp = dp.data_ptr();
+  a.idx = ptr<uint8_t>(idx);
+  a.dx = dx.data_ptr();
+  a.scale = ptr<float>(scale_shift);
+  a.shift = a.scale + a.C;
+  a.gamma = optr<float>(weight);
+  a.mean = ptr<float>(mean);
+  a.invstd = ptr<float>(invstd);
+  a.partial = ptr<float>(partial);
+  a.dgamma = ptr<float>(dgamma);
+  a.dbeta = ptr<float>(dbeta);
+  a.A = ptr<float>(coef);
+  a.B = a.A + a.C;
+  a.Cc = a.A + 2 * a.C;
+  lw::stem_pool_bwd(a, cur_stream());
+  return {dx, dgamma, dbeta};
 }
 
 // y = relu?(x*scale+shift [+ res | + res*rscale+rshift])
@@ -665,6 +735,10 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor(b!)? running_var, float momentum, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? res, Tensor? res_scale_shift, bool relu) "
         "-> Tensor");
+  m.def("stem_pool_fwd(Tensor x, Tensor scale_shift, int k, int s, int p) -> (Tensor, Tensor)");
+  m.def(
+      "stem_pool_bwd(Tensor dp, Tensor idx, Tensor x, Tensor scale_shift, Tensor? weight, "
+      "Tensor mean, Tensor invstd, int k, int s, int p) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
@@ -683,4 +757,6 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("gemm_ex", &gemm_ex);
   m.impl("bn_stats", &bn_stats);
   m.impl("bn_apply", &bn_apply);
+  m.impl("stem_pool_fwd", &stem_pool_fwd);
+  m.impl("stem_pool_bwd", &stem_pool_bwd);
 }

@@ -17,11 +17,9 @@ namespace lw {
 constexpr int BNT = 256;
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+// hardware round-to-nearest-even conversion (v_cvt_pk_bf16_f32), same as gemm.hip
 __device__ __forceinline__ uint16_t f2bf_rne(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
 }
 
 template <typename T> struct V8;
@@ -211,6 +209,28 @@ __global__ __launch_bounds__(256) void k_bn_finalize_fwd(
   }
 }
 
+// Rows [R][W] fp32 → per-block column sums, channel-major partial [W][gridDim.x] (the layout
+// k_bn_finalize_fwd folds). Folds the per-M-tile statistics rows a GEMM epilogue wrote
+// (gemm.hip EPI_STATS, W = 2C: Σv then Σv²); rows are summed in order (deterministic).
+__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ rows, int64_t R, int W,
+                                                int64_t rows_per_block,
+                                                float* __restrict__ partial) {
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(r0 + rows_per_block, R);
+  for (int c = threadIdx.x; c < W; c += 256) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t r = r0;
+    for (; r + 3 < r1; r += 4) {
+      s0 += rows[r * W + c];
+      s1 += rows[(r + 1) * W + c];
+      s2 += rows[(r + 2) * W + c];
+      s3 += rows[(r + 3) * W + c];
+    }
+    for (; r < r1; ++r) s0 += rows[r * W + c];
+    partial[(int64_t)c * gridDim.x + blockIdx.x] = (s0 + s1) + (s2 + s3);
+  }
+}
+
 // Thread-constant channel group: the grid-stride step is a multiple of G = C/8 (apply_grid), so
 // a thread always touches the same 8 channels and keeps their coefficients in registers.
 // RES: 0 none, 1 plain residual add, 2 residual through its own BatchNorm affine (the downsample
@@ -396,7 +416,14 @@ static void bn_apply_t(const BNArgs& a, hipStream_t st) {
 template <typename T>
 static void bn_stats_t(const BNArgs& a, hipStream_t st) {
   int nb = a.stats_blocks;
-  if (nb <= 0) {
+  if (a.stat_rows) {                      // GEMM epilogue rows [R][2C] -> [2C][nb]
+    const int64_t R = a.stats_rows_n;
+    nb = (int)(R < 256 ? R : 256);
+    const int64_t rpb = (R + nb - 1) / nb;
+    nb = (int)((R + rpb - 1) / rpb);
+    hipLaunchKernelGGL(k_colsum, dim3(nb), dim3(256), 0, st, a.stat_rows, R, 2 * a.C, rpb,
+                       a.partial);
+  } else if (nb <= 0) {
     int64_t rpb;
     reduce_geometry(a.M, a.C, rpb, nb);
     hipLaunchKernelGGL((k_bn_reduce<T, 0, 0>), dim3(nb), dim3(BNT), 0, st, static_cast<const T*>(a.x),
@@ -456,6 +483,189 @@ void bn_apply(const BNArgs& a, hipStream_t st) {
 }
 void bn_backward(const BNArgs& a, hipStream_t st) {
   if (a.bf16) bn_backward_t<uint16_t>(a, st); else bn_backward_t<float>(a, st);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused ResNet stem tail: BatchNorm-apply + ReLU + k×k max-pool (stride s, pad p), NHWC bf16.
+// The reference runs conv1 → bn1 → relu → maxpool as separate ops (IMAGENET/training/resnet.py:
+// 130-133); here the normalised 112×112 activation is never written: the forward reads the raw
+// conv output once and writes the pooled map plus a one-byte window slot per output element; the
+// backward routes the pooled gradient straight into the BN backward (reduce + apply), so the
+// un-pooled gradient is never materialised either.
+// ------------------------------------------------------------------------------------------
+struct PoolGeom { int N, H, W, C, Ho, Wo, k, s, p; };
+
+__global__ __launch_bounds__(256) void k_stem_pool_fwd(const uint16_t* __restrict__ x,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       uint16_t* __restrict__ out,
+                                                       uint8_t* __restrict__ idx, PoolGeom g) {
+  const int G = g.C / 8;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)g.N * g.Ho * g.Wo * G;
+  if (t >= total) return;
+  const int cg = (int)(t % G);
+  int64_t q = t / G;
+  const int ow = (int)(q % g.Wo);
+  q /= g.Wo;
+  const int oh = (int)(q % g.Ho);
+  const int n = (int)(q / g.Ho);
+  float sc[8], sh[8], best[8];
+  int bi[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale[cg * 8 + j]; sh[j] = shift[cg * 8 + j];
+    best[j] = -__builtin_huge_valf(); bi[j] = 0;
+  }
+  for (int kh = 0; kh < g.k; ++kh) {
+    const int ih = oh * g.s - g.p + kh;
+    if (ih < 0 || ih >= g.H) continue;
+    for (int kw = 0; kw < g.k; ++kw) {
+      const int iw = ow * g.s - g.p + kw;
+      if (iw < 0 || iw >= g.W) continue;
+      float v[8];
+      V8<uint16_t>::load(x + (((int64_t)n * g.H + ih) * g.W + iw) * g.C + cg * 8, v);
+      const int slot = kh * g.k + kw;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float a = bf2f(f2bf_rne(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f)));
+        if (a > best[j]) { best[j] = a; bi[j] = slot; }      // first max wins (PyTorch order)
+      }
+    }
+  }
+  const int64_t o = t * 8;
+  V8<uint16_t>::store(out + o, best);
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    lo |= (uint32_t)bi[j] << (8 * j);
+    hi |= (uint32_t)bi[j + 4] << (8 * j);
+  }
+  *reinterpret_cast<uint2*>(idx + o) = make_uint2(lo, hi);
+}
+
+// Gradient reaching input element (n, ih, iw, 8 channels) through the pool and the ReLU.
+__device__ __forceinline__ void stem_dz(const uint16_t* __restrict__ dp,
+                                        const uint8_t* __restrict__ idx, const PoolGeom& g, int n,
+                                        int ih, int iw, int cg, const float xv[8],
+                                        const float sc[8], const float sh[8], float dz[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dz[j] = 0.f;
+  const int oh0 = max(0, (ih + g.p - g.k + g.s) / g.s), oh1 = min(g.Ho - 1, (ih + g.p) / g.s);
+  const int ow0 = max(0, (iw + g.p - g.k + g.s) / g.s), ow1 = min(g.Wo - 1, (iw + g.p) / g.s);
+  for (int oh = oh0; oh <= oh1; ++oh) {
+    const int kh = ih - (oh * g.s - g.p);
+    if (kh < 0 || kh >= g.k) continue;
+    for (int ow = ow0; ow <= ow1; ++ow) {
+      const int kw = iw - (ow * g.s - g.p);
+      if (kw < 0 || kw >= g.k) continue;
+      const int slot = kh * g.k + kw;
+      const int64_t o = (((int64_t)n * g.Ho + oh) * g.Wo + ow) * g.C + cg * 8;
+      const uint2 ii = *reinterpret_cast<const uint2*>(idx + o);
+      float d[8];
+      V8<uint16_t>::load(dp + o, d);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int s8 = (int)(((j < 4 ? ii.x : ii.y) >> (8 * (j & 3))) & 0xffu);
+        dz[j] += s8 == slot ? d[j] : 0.f;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dz[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? dz[j] : 0.f;
+}
+
+// MODE 0: per-block channel partials of (Σdz, Σdz·(x-mean)) -> [2][C][nb] (fixed order);
+// MODE 1: dx = A·dz + B·x + C.
+template <int MODE>
+__global__ __launch_bounds__(BNT) void k_stem_pool_bwd(const uint16_t* __restrict__ dp,
+                                                       const uint8_t* __restrict__ idx,
+                                                       const uint16_t* __restrict__ x,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ A,
+                                                       const float* __restrict__ B,
+                                                       const float* __restrict__ Cc,
+                                                       uint16_t* __restrict__ dx,
+                                                       float* __restrict__ partial, PoolGeom g,
+                                                       int64_t rows_per_block) {
+  __shared__ float sa[BNT * 8];
+  __shared__ float sb[BNT * 8];
+  const int G = g.C / 8;
+  const int R = BNT / G;
+  const int cg = threadIdx.x % G, r = threadIdx.x / G;
+  const bool active = r < R;
+  const int64_t M = (int64_t)g.N * g.H * g.W;
+  float sc[8], sh[8], mu[8], ca[8], cb[8], cc[8], a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = active ? cg * 8 + j : 0;
+    sc[j] = scale[c]; sh[j] = shift[c];
+    mu[j] = MODE == 0 ? mean[c] : 0.f;
+    ca[j] = MODE == 1 ? A[c] : 0.f; cb[j] = MODE == 1 ? B[c] : 0.f; cc[j] = MODE == 1 ? Cc[c] : 0.f;
+    a[j] = 0.f; b[j] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(r0 + rows_per_block, M);
+  if (active) {
+    for (int64_t row = r0 + r; row < r1; row += R) {
+      const int iw = (int)(row % g.W);
+      const int64_t q = row / g.W;
+      const int ih = (int)(q % g.H), n = (int)(q / g.H);
+      float xv[8], dz[8];
+      V8<uint16_t>::load(x + row * g.C + cg * 8, xv);
+      stem_dz(dp, idx, g, n, ih, iw, cg, xv, sc, sh, dz);
+      if (MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { a[j] += dz[j]; b[j] += dz[j] * (xv[j] - mu[j]); }
+      } else {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = ca[j] * dz[j] + cb[j] * xv[j] + cc[j];
+        V8<uint16_t>::store(dx + row * g.C + cg * 8, o);
+      }
+    }
+  }
+  if (MODE == 1) return;
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sa[r * g.C + cg * 8 + j] = a[j]; sb[r * g.C + cg * 8 + j] = b[j]; }
+  }
+  __syncthreads();
+  const int64_t nb = gridDim.x;
+  for (int c = threadIdx.x; c < g.C; c += BNT) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int qq = 0; qq < R; ++qq) { s1 += sa[qq * g.C + c]; s2 += sb[qq * g.C + c]; }
+    partial[(int64_t)c * nb + blockIdx.x] = s1;
+    partial[((int64_t)g.C + c) * nb + blockIdx.x] = s2;
+  }
+}
+
+void stem_pool_fwd(const StemArgs& a, hipStream_t st) {
+  const PoolGeom g{a.N, a.H, a.W, a.C, a.Ho, a.Wo, a.k, a.s, a.p};
+  const int64_t total = (int64_t)a.N * a.Ho * a.Wo * (a.C / 8);
+  hipLaunchKernelGGL(k_stem_pool_fwd, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     static_cast<const uint16_t*>(a.x), a.scale, a.shift,
+                     static_cast<uint16_t*>(a.out), a.idx, g);
+}
+
+void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
+  const PoolGeom g{a.N, a.H, a.W, a.C, a.Ho, a.Wo, a.k, a.s, a.p};
+  const int64_t M = (int64_t)a.N * a.H * a.W;
+  int64_t rpb;
+  int nb;
+  reduce_geometry(M, a.C, rpb, nb);
+  const auto* dp = static_cast<const uint16_t*>(a.dp);
+  const auto* x = static_cast<const uint16_t*>(a.x);
+  hipLaunchKernelGGL((k_stem_pool_bwd<0>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
+                     a.shift, a.mean, (const float*)nullptr, (const float*)nullptr,
+                     (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb);
+  hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
+                     a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1);
+  hipLaunchKernelGGL((k_stem_pool_bwd<1>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
+                     a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
+                     (float*)nullptr, g, rpb);
 }
 
 }  // namespace lw

@@ -20,9 +20,9 @@
 //    the *input* folded into a 1x1 convolution (the normalised activation is never materialised);
 //  * prologue PRO_B: the same per-n on N-contiguous B — the weight-gradient of that convolution
 //    recomputes the normalised activation on load;
-//  * epilogue EPI_STATS: per-column Σv and Σv² of the bf16-rounded output per M-tile, written in the
-//    channel-major [2][N][tiles_m] layout the BatchNorm finalize kernel folds (bn.hip) — the forward
-//    statistics pass of the *next* BatchNorm disappears;
+//  * epilogue EPI_STATS: per-column Σv and Σv² of the bf16-rounded output per M-tile, written as
+//    one coalesced [2][N] row per M-tile ([tiles_m][2][N]); bn.hip folds the rows (k_colsum) and
+//    finalizes — the forward statistics pass of the *next* BatchNorm disappears;
 //  * split-K (EPI_PARTIAL) writes fp32 slabs that a second kernel reduces in a fixed order
 //    (deterministic) and pushes through the same epilogue.
 #include "common.h"
@@ -39,11 +39,10 @@ constexpr int PAD = 8;                   // bf16 elements of padding per LDS row
 enum { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_STATS = 2 };
 enum { PRO_NONE = 0, PRO_A = 1, PRO_B = 2 };
 
+// f32 -> bf16, round to nearest even: a plain cast, which hipcc lowers to the gfx950 hardware
+// conversion v_cvt_pk_bf16_f32 (NaN stays NaN), instead of integer bit arithmetic.
 __device__ __forceinline__ uint16_t bf16_rne(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
 }
 __device__ __forceinline__ float bf16_round(float f) { return __uint_as_float((uint32_t)bf16_rne(f) << 16); }
 
@@ -109,21 +108,37 @@ __device__ __forceinline__ void load_tile(const uint16_t* __restrict__ P, int64_
   }
 }
 
-// relu(v*scale[j] + shift[j]) on the 8 bf16 of a chunk, j = cont .. cont+7 (same fp32 expression
-// and rounding as the BatchNorm apply kernel, so fused and unfused paths agree bit for bit).
-__device__ __forceinline__ uint4 affine_relu8(uint4 v, const float* __restrict__ sc,
-                                              const float* __restrict__ sh, int j) {
-  const float4 s0 = *reinterpret_cast<const float4*>(sc + j);
-  const float4 s1 = *reinterpret_cast<const float4*>(sc + j + 4);
-  const float4 h0 = *reinterpret_cast<const float4*>(sh + j);
-  const float4 h1 = *reinterpret_cast<const float4*>(sh + j + 4);
-  const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-  const float t[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+// Prologue coefficients of the 8 channels one thread's chunks cover. Every chunk a thread stages
+// has the same contiguous-dimension offset within the tile (the chunks-per-row count divides the
+// workgroup size), so one set of 8 scale/shift values serves all of them: per K-step for PRO_A
+// (channel = k), once per kernel for PRO_B (channel = n).
+struct Coef8 { float s[8], t[8]; };
+
+__device__ __forceinline__ void load_coef8(Coef8& c, const float* __restrict__ sc,
+                                           const float* __restrict__ sh, int j, int limit) {
+  if (j + 8 <= limit) {
+    const float4 s0 = *reinterpret_cast<const float4*>(sc + j);
+    const float4 s1 = *reinterpret_cast<const float4*>(sc + j + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(sh + j);
+    const float4 h1 = *reinterpret_cast<const float4*>(sh + j + 4);
+    c.s[0] = s0.x; c.s[1] = s0.y; c.s[2] = s0.z; c.s[3] = s0.w;
+    c.s[4] = s1.x; c.s[5] = s1.y; c.s[6] = s1.z; c.s[7] = s1.w;
+    c.t[0] = h0.x; c.t[1] = h0.y; c.t[2] = h0.z; c.t[3] = h0.w;
+    c.t[4] = h1.x; c.t[5] = h1.y; c.t[6] = h1.z; c.t[7] = h1.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { c.s[k] = 0.f; c.t[k] = 0.f; }
+  }
+}
+
+// relu(v*scale + shift) on the 8 bf16 of a chunk (same fp32 expression and rounding as the
+// BatchNorm apply kernel, so fused and unfused paths agree bit for bit).
+__device__ __forceinline__ uint4 affine_relu8(uint4 v, const Coef8& c) {
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float lo = fmaxf(fmaf(__uint_as_float(w[k] << 16), s[2 * k], t[2 * k]), 0.f);
-    const float hi = fmaxf(fmaf(__uint_as_float(w[k] & 0xffff0000u), s[2 * k + 1], t[2 * k + 1]), 0.f);
+    const float lo = fmaxf(fmaf(__uint_as_float(w[k] << 16), c.s[2 * k], c.t[2 * k]), 0.f);
+    const float hi = fmaxf(fmaf(__uint_as_float(w[k] & 0xffff0000u), c.s[2 * k + 1], c.t[2 * k + 1]), 0.f);
     w[k] = (uint32_t)bf16_rne(lo) | ((uint32_t)bf16_rne(hi) << 16);
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
@@ -132,16 +147,15 @@ __device__ __forceinline__ uint4 affine_relu8(uint4 v, const float* __restrict__
 template <int R, int BK, bool KC, bool PRO>
 __device__ __forceinline__ void store_tile(uint16_t* __restrict__ S,
                                            const uint4 (&r)[Tile<R, BK, KC>::PER_T],
-                                           const int (&cont)[Tile<R, BK, KC>::PER_T],
-                                           uint32_t okmask, const float* __restrict__ sc,
-                                           const float* __restrict__ sh) {
+                                           uint32_t okmask, const Coef8& co) {
   using T = Tile<R, BK, KC>;
+  static_assert(GT % T::CPR == 0, "chunk column must be constant per thread");
 #pragma unroll
   for (int h = 0; h < T::PER_T; ++h) {
     int rr, cc;
     chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
     uint4 v = r[h];
-    if (PRO && ((okmask >> h) & 1u)) v = affine_relu8(v, sc, sh, cont[h]);
+    if (PRO && ((okmask >> h) & 1u)) v = affine_relu8(v, co);
     *reinterpret_cast<uint4*>(S + rr * T::LD + cc * 8) = v;
   }
 }
@@ -240,11 +254,16 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   int ca[TA::PER_T], cb[TB::PER_T];
   uint32_t oka = 0, okb = 0;
   int cur = 0;
+  Coef8 coA, coB;
+  if (PRO == PRO_B)        // channel n of this thread's B chunks: fixed for the whole kernel
+    load_coef8(coB, p.pro_scale, p.pro_shift, n0 + (threadIdx.x % TB::CPR) * 8, p.N);
+  const int a_koff = (threadIdx.x % TA::CPR) * 8;      // PRO_A: k offset within a K-step
   if (kbeg < kend) {
     load_tile<BM, BK, AKC>(p.A, p.lda, m0, p.M, kbeg, kend, ra, ca, oka);
     load_tile<BN, BK, BKC>(p.B, p.ldb, n0, p.N, kbeg, kend, rb, cb, okb);
-    store_tile<BM, BK, AKC, PRO == PRO_A>(st, ra, ca, oka, p.pro_scale, p.pro_shift);
-    store_tile<BN, BK, BKC, PRO == PRO_B>(st + TA::ELEMS, rb, cb, okb, p.pro_scale, p.pro_shift);
+    if (PRO == PRO_A) load_coef8(coA, p.pro_scale, p.pro_shift, kbeg + a_koff, kend);
+    store_tile<BM, BK, AKC, PRO == PRO_A>(st, ra, oka, coA);
+    store_tile<BN, BK, BKC, PRO == PRO_B>(st + TA::ELEMS, rb, okb, coB);
   }
   __syncthreads();
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
@@ -252,6 +271,9 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
     if (more) {
       load_tile<BM, BK, AKC>(p.A, p.lda, m0, p.M, k0 + BK, kend, ra, ca, oka);
       load_tile<BN, BK, BKC>(p.B, p.ldb, n0, p.N, k0 + BK, kend, rb, cb, okb);
+      // next stage's prologue coefficients travel with its tile loads (latency hidden by the
+      // MFMAs below; coA is free: the current stage was normalised when it was staged)
+      if (PRO == PRO_A) load_coef8(coA, p.pro_scale, p.pro_shift, k0 + BK + a_koff, kend);
     }
     const uint16_t* As = st + cur * STAGE;
     const uint16_t* Bs = As + TA::ELEMS;
@@ -270,8 +292,8 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
     }
     if (more) {
       uint16_t* nx = st + (cur ^ 1) * STAGE;
-      store_tile<BM, BK, AKC, PRO == PRO_A>(nx, ra, ca, oka, p.pro_scale, p.pro_shift);
-      store_tile<BN, BK, BKC, PRO == PRO_B>(nx + TA::ELEMS, rb, cb, okb, p.pro_scale, p.pro_shift);
+      store_tile<BM, BK, AKC, PRO == PRO_A>(nx, ra, oka, coA);
+      store_tile<BN, BK, BKC, PRO == PRO_B>(nx + TA::ELEMS, rb, okb, coB);
     }
     __syncthreads();
     cur ^= 1;
@@ -318,12 +340,12 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
         }
-        if (EPI == EPI_STATS && m0 + ml < p.M) {
+        if (EPI == EPI_STATS && !bf_out && m0 + ml < p.M) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) { s1[r] += v[r]; s2[r] += v[r] * v[r]; }
         }
       }
-      if (EPI == EPI_STATS) {
+      if (EPI == EPI_STATS && !bf_out) {
         // the 16 rows held by lanes sharing l>>4, fixed butterfly order
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
@@ -343,6 +365,13 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       }
     }
   }
+  // Column statistics come from the staged bf16 tile during the store pass: a thread's chunks
+  // all cover the same 8 columns (GT is a multiple of BN/8), so it sums them in registers and
+  // one LDS fold per tile finishes the job (no cross-lane shuffles in the epilogue).
+  static_assert(GT % (BN / 8) == 0, "store chunks must keep their column per thread");
+  float cs1[8], cs2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { cs1[k] = 0.f; cs2[k] = 0.f; }
   if (bf_out) {
     __syncthreads();
     const bool vec = (p.ldc & 7) == 0;
@@ -351,6 +380,19 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       const int gm = m0 + r, gn = n0 + cc;
       if (gm >= p.M || gn >= p.N) continue;
       const uint16_t* src = Ch + r * LDH + cc;
+      if (EPI == EPI_STATS) {
+        const uint4 q = *reinterpret_cast<const uint4*>(src);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float lo = __uint_as_float(w[k] << 16), hi = __uint_as_float(w[k] & 0xffff0000u);
+          const bool in_lo = gn + 2 * k < p.N, in_hi = gn + 2 * k + 1 < p.N;
+          cs1[2 * k] += in_lo ? lo : 0.f;
+          cs2[2 * k] += in_lo ? lo * lo : 0.f;
+          cs1[2 * k + 1] += in_hi ? hi : 0.f;
+          cs2[2 * k + 1] += in_hi ? hi * hi : 0.f;
+        }
+      }
       uint16_t* dst = static_cast<uint16_t*>(p.C) + (int64_t)gm * p.ldc + gn;
       if (vec && gn + 8 <= p.N) {
         uint4 v = *reinterpret_cast<const uint4*>(src);
@@ -417,18 +459,35 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       for (int c = threadIdx.x; c < BN; c += GT) {
         const int n = n0 + c;
         if (n >= p.N) continue;
-        p.stats[(int64_t)n * tiles_m + tm] = statsave[0];
-        p.stats[((int64_t)p.N + n) * tiles_m + tm] = statsave[1];
+        p.stats[(int64_t)tm * 2 * p.N + n] = statsave[0];
+        p.stats[(int64_t)tm * 2 * p.N + p.N + n] = statsave[1];
       }
     }
     return;
   }
   if (EPI == EPI_STATS) {
+    // fold the per-thread column sums: GT/(BN/8) threads share each 8-column group
+    constexpr int G8 = BN / 8, Q = GT / G8;
+    __syncthreads();                              // the staged tile is no longer read
+    float* fold = reinterpret_cast<float*>(lds);  // [GT][16]
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      fold[threadIdx.x * 16 + k] = cs1[k];
+      fold[threadIdx.x * 16 + 8 + k] = cs2[k];
+    }
+    __syncthreads();
     for (int c = threadIdx.x; c < BN; c += GT) {
       const int n = n0 + c;
       if (n >= p.N) continue;
-      p.stats[(int64_t)n * tiles_m + tm] = red[0 * BN + c] + red[2 * BN + c];      // [2][N][tiles_m]
-      p.stats[((int64_t)p.N + n) * tiles_m + tm] = red[1 * BN + c] + red[3 * BN + c];
+      const int g = c / 8, k = c % 8;
+      float a = 0.f, b = 0.f;
+      for (int q = 0; q < Q; ++q) {               // fixed order: deterministic
+        a += fold[(q * G8 + g) * 16 + k];
+        b += fold[(q * G8 + g) * 16 + 8 + k];
+      }
+      // [tiles_m][2][N]: one coalesced row per M-tile (bn.hip k_colsum folds the rows)
+      p.stats[(int64_t)tm * 2 * p.N + n] = a;
+      p.stats[(int64_t)tm * 2 * p.N + p.N + n] = b;
     }
   }
 }

@@ -129,13 +129,38 @@ struct BNArgs {
   float* Cc;
   const float* res_scale;  // forward: residual through its own BN affine (or nullptr)
   const float* res_shift;
-  int stats_blocks;        // bn_stats: >0 = partial sums already written by a GEMM epilogue
+  int stats_blocks;        // bn_stats: >0 = partial sums already in `partial` ([2C][nb])
+  const float* stat_rows;  // bn_stats: per-M-tile rows [R][2C] from a GEMM epilogue (or nullptr)
+  int64_t stats_rows_n;    // R
 };
 int bn_reduce_blocks(int64_t M, int C);
 void bn_stats(const BNArgs& a, hipStream_t st);
 void bn_apply(const BNArgs& a, hipStream_t st);
 void bn_forward(const BNArgs& a, hipStream_t st);
 void bn_backward(const BNArgs& a, hipStream_t st);
+
+// fused stem: BN-apply + ReLU + max-pool (bn.hip), bf16 NHWC
+struct StemArgs {
+  const void* x;          // conv output [N, H, W, C]
+  const float* scale;     // BN scale/shift (forward coefficients)
+  const float* shift;
+  void* out;              // pooled [N, Ho, Wo, C]
+  uint8_t* idx;           // window slot of the max, per pooled element
+  const void* dp;         // backward: gradient of the pooled output
+  void* dx;               // backward: gradient of the conv output
+  const float* gamma;
+  const float* mean;
+  const float* invstd;
+  float* partial;         // [2][C][nb]
+  float* dgamma;
+  float* dbeta;
+  float* A;
+  float* B;
+  float* Cc;
+  int N, H, W, C, Ho, Wo, k, s, p;
+};
+void stem_pool_fwd(const StemArgs& a, hipStream_t st);
+void stem_pool_bwd(const StemArgs& a, hipStream_t st);
 
 // bf16 MFMA GEMM with fused epilogue (gemm.hip)
 struct GemmArgs {

@@ -32,7 +32,7 @@ def gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False, splits=1
             tile="auto", pro_scale=None, pro_shift=None, pro_on_a=True, stats=False):
     """Full-featured entry: explicit tile, prologue ``relu(v*scale+shift)`` (per-k of a
     K-contiguous A, or per-n of an N-contiguous B) and per-column output statistics
-    ``[2][N][tiles_m]`` (Σv, Σv² of the stored values per M-tile). Returns ``(C, stats)``."""
+    ``[tiles_m][2][N]`` (Σv, Σv² of the stored values per M-tile). Returns ``(C, stats)``."""
     return load().gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias, relu, splits, out_bf16,
                           TILES[tile] if isinstance(tile, str) else int(tile), pro_scale,
                           pro_shift, pro_on_a, stats)

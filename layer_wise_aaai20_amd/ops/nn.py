@@ -165,8 +165,62 @@ def _fused_basic_forward(self, x):
     return self.bn2(self.conv2(out), identity)
 
 
+class _StemPoolFn(torch.autograd.Function):
+    """conv1 output → BN (batch stats) → ReLU → max-pool as one forward kernel after the stats
+    pass, and one reduce + one apply kernel backward (``csrc/bn.hip`` k_stem_pool_*)."""
+
+    @staticmethod
+    def forward(ctx, c, weight, bias, bn, geom):
+        from . import block
+        lib = load()
+        c = c.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        block._bump(bn)
+        mean, invstd, ss = lib.bn_stats(c, None, weight, bias, bn.running_mean, bn.running_var,
+                                        block._bn_momentum(bn), bn.eps)
+        out, idx = lib.stem_pool_fwd(c, ss, *geom)
+        ctx.save_for_backward(c, idx, ss, weight, mean, invstd)
+        ctx.geom = geom
+        ctx.params = (weight, bias)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import block
+        c, idx, ss, weight, mean, invstd = ctx.saved_tensors
+        w, b = ctx.params
+        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dc, dg, db = load().stem_pool_bwd(dout, idx, c, ss, weight, mean, invstd, *ctx.geom)
+        return (dc, block._finish_param(w, dg, block._direct(w)),
+                block._finish_param(b, db, block._direct(b)), None, None)
+
+
+def _pool_geom(pool: nn.MaxPool2d):
+    def one(v):
+        return v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else None)
+    k, s, p, d = one(pool.kernel_size), one(pool.stride or pool.kernel_size), one(pool.padding), \
+        one(pool.dilation)
+    if None in (k, s, p) or d != 1 or pool.ceil_mode or pool.return_indices:
+        return None
+    return (k, s, p)
+
+
+def stem_supported(model, c: torch.Tensor) -> bool:
+    bn = model.bn1
+    return (model.training and c.is_cuda and c.dim() == 4 and c.dtype == torch.bfloat16 and
+            c.size(1) % 8 == 0 and bn.affine and bn.track_running_stats and
+            isinstance(model.maxpool, nn.MaxPool2d) and _pool_geom(model.maxpool) is not None)
+
+
+def stem_bn_relu_pool(c: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2d) -> torch.Tensor:
+    return _StemPoolFn.apply(c, bn.weight, bn.bias, bn, _pool_geom(pool))
+
+
 def _fused_resnet_forward(self, x):
-    x = self.maxpool(self.bn1(self.conv1(x)))
+    c = self.conv1(x)
+    if getattr(self, "_lw_stem_fused", False) and stem_supported(self, c):
+        x = stem_bn_relu_pool(c, self.bn1, self.maxpool)
+    else:
+        x = self.maxpool(self.bn1(c))
     x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
     x = torch.flatten(self.avgpool(x), 1)
     return self.fc(x)
@@ -195,6 +249,7 @@ def fuse_resnet(model: nn.Module, block: bool = True) -> nn.Module:
             m.forward = types.MethodType(_fused_basic_forward, m)
     if isinstance(model, R.ResNet):
         to_fused_bn(model.bn1, relu=True)
+        model._lw_stem_fused = block
         model.forward = types.MethodType(_fused_resnet_forward, model)
     return model
 

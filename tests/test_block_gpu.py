@@ -135,3 +135,30 @@ def test_resnet50_block_vs_layer_path():
     mb, ml = statistics.median(errs["block"]), statistics.median(errs["layer"])
     assert mb <= 1.2 * ml + 0.02, (mb, ml)
     assert errs["block"][-1] < 0.05            # fc.bias: only the softmax output enters
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 32, 32), (2, 64, 15, 17)])
+def test_stem_bn_relu_pool_matches_layers(shape):
+    """Fused BN+ReLU+max-pool stem vs FusedBatchNorm2d(relu) + nn.MaxPool2d."""
+    from layer_wise_aaai20_amd.ops.nn import stem_bn_relu_pool, to_fused_bn
+    torch.manual_seed(3)
+    C = shape[1]
+    bn_a = torch.nn.BatchNorm2d(C).cuda()
+    bn_a.weight.data.uniform_(-1.0, 1.5)          # negative gammas too
+    bn_a.bias.data.normal_(0, 0.3)
+    bn_b = copy.deepcopy(bn_a)
+    to_fused_bn(bn_b, relu=True)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    c = torch.randn(*shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    ca, cb = c.clone().requires_grad_(), c.clone().requires_grad_()
+    ya = stem_bn_relu_pool(ca, bn_a, pool)
+    yb = pool(bn_b(cb))
+    torch.testing.assert_close(ya.float(), yb.float(), rtol=0, atol=0)
+    g = torch.randn_like(yb, dtype=torch.float32).to(torch.bfloat16)
+    ya.backward(g)
+    yb.backward(g)
+    assert _rel(ca.grad, cb.grad) < 2e-2
+    assert _rel(bn_a.weight.grad, bn_b.weight.grad) < 2e-2
+    assert _rel(bn_a.bias.grad, bn_b.bias.grad) < 2e-2
+    torch.testing.assert_close(bn_a.running_mean, bn_b.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn_a.running_var, bn_b.running_var, rtol=1e-3, atol=1e-4)

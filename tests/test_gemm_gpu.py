@@ -91,12 +91,12 @@ def test_gemm_stats_epilogue(tile):
     C, st = G.gemm_ex(x, K, True, w, K, True, M, N, K, tile=tile, stats=True)
     bm = {"128x128x32": 128, "256x64x32": 256, "64x256x32": 64, "64x64x64": 64}[tile]
     tiles_m = -(-M // bm)
-    assert st.shape == (2, N, tiles_m)
+    assert st.shape == (tiles_m, 2, N)
     c = C.float()
-    torch.testing.assert_close(st[0].sum(1), c.sum(0), rtol=1e-4, atol=1e-2)
-    torch.testing.assert_close(st[1].sum(1), (c * c).sum(0), rtol=1e-4, atol=1e-1)
+    torch.testing.assert_close(st[:, 0].sum(0), c.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[:, 1].sum(0), (c * c).sum(0), rtol=1e-4, atol=1e-1)
     # per-tile partials
-    torch.testing.assert_close(st[0][:, 0], c[:bm].sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[0, 0], c[:bm].sum(0), rtol=1e-4, atol=1e-2)
 
 
 def test_gemm_prologue_a_and_b():

@@ -363,16 +363,36 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_fwd(Tensor x, c10::optional<Tensor
   return {y, mean, invstd, scale_shift};
 }
 
+// dgamma/dbeta outputs: fresh tensors, or (dgamma_out/dbeta_out) accumulated into given fp32 [C]
+// views — the gradient arena — so no separate add kernel is needed.
+static Tensor dparam_out(const c10::optional<Tensor>& t, int64_t C, const Tensor& like,
+                         bool& accum) {
+  if (t.has_value() && t->defined()) {
+    check_dtype(*t, at::kFloat, "dparam_out");
+    TORCH_CHECK(t->numel() == C && t->is_contiguous(), "dparam_out must be a contiguous [C]");
+    accum = true;
+    return *t;
+  }
+  return at::empty({C}, like.options().dtype(at::kFloat));
+}
+
 std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y,
                                                   c10::optional<Tensor> weight, Tensor mean,
                                                   Tensor invstd, c10::optional<Tensor> scale_shift,
-                                                  bool training, bool relu, bool need_dres) {
+                                                  bool training, bool relu, bool need_dres,
+                                                  c10::optional<Tensor> bits,
+                                                  c10::optional<Tensor> dgamma_out,
+                                                  c10::optional<Tensor> dbeta_out) {
   const c10::DeviceGuard guard(x.device());
   check_nhwc(x, "x");
   check_nhwc(dy, "dy");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.sizes() == x.sizes(), "dy must match x");
   const bool have_ss = scale_shift.has_value() && scale_shift->defined();
-  if (relu && !have_ss) {
+  const bool have_bits = bits.has_value() && bits->defined();
+  if (have_bits) {
+    TORCH_CHECK(bits->scalar_type() == at::kByte && bits->numel() * 8 == x.numel() &&
+                bits->is_contiguous(), "bits must be a contiguous uint8 [numel/8] bitmap");
+  } else if (relu && !have_ss) {
     TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
     check_nhwc(*y, "y");
   }
@@ -381,14 +401,20 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
   auto f32 = x.options().dtype(at::kFloat);
   Tensor dx = at::empty_like(x);
   Tensor dres = need_dres ? at::empty_like(x) : at::empty({0}, x.options());
-  Tensor dgamma = at::empty({C}, f32), dbeta = at::empty({C}, f32);
+  bool accum = false;
+  Tensor dgamma = dparam_out(dgamma_out, C, x, accum), dbeta = dparam_out(dbeta_out, C, x, accum);
   Tensor coef = at::empty({3 * C}, f32);
   Tensor partial = at::empty({(int64_t)lw::bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
   lw::BNArgs a{};
+  a.accum_dparams = accum;
+  TORCH_CHECK(!accum || ((dgamma_out.has_value() && dgamma_out->defined()) &&
+                         (dbeta_out.has_value() && dbeta_out->defined())),
+              "give both dgamma_out and dbeta_out");
   a.x = x.data_ptr();
   a.dy = dy.data_ptr();
-  a.y = (relu && !have_ss) ? y->data_ptr() : nullptr;
-  if (relu && have_ss) {
+  a.bits = (relu && have_bits) ? ptr<uint8_t>(*bits) : nullptr;
+  a.y = (relu && !have_ss && !have_bits) ? y->data_ptr() : nullptr;
+  if (relu && have_ss && !have_bits) {
     TORCH_CHECK(scale_shift->numel() == 2 * C, "scale_shift must hold 2*C floats");
     a.scale = ptr<float>(*scale_shift);
     a.shift = a.scale + C;
@@ -611,7 +637,8 @@ std::tuple<Tensor, Tensor> stem_pool_fwd(Tensor x, Tensor scale_shift, int64_t k
 std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x,
                                                  Tensor scale_shift, c10::optional<Tensor> weight,
                                                  Tensor mean, Tensor invstd, int64_t k, int64_t s,
-                                                 int64_t p) {
+                                                 int64_t p, c10::optional<Tensor> dgamma_out,
+                                                 c10::optional<Tensor> dbeta_out) {
   const c10::DeviceGuard guard(x.device());
   lw::StemArgs a{};
   stem_geom(x, k, s, p, a);
@@ -621,7 +648,10 @@ std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x
   TORCH_CHECK(idx.numel() == dp.numel() && idx.scalar_type() == at::kByte, "idx");
   auto f32 = x.options().dtype(at::kFloat);
   Tensor dx = at::empty_like(x);
-  Tensor dgamma = at::empty({a.C}, f32), dbeta = at::empty({a.C}, f32);
+  bool accum = false;
+  Tensor dgamma = dparam_out(dgamma_out, a.C, x, accum);
+  Tensor dbeta = dparam_out(dbeta_out, a.C, x, accum);
+  a.accum_dparams = accum;
   Tensor coef = at::empty({3 * a.C}, f32);
   Tensor partial = at::empty({(int64_t)lw::bn_reduce_blocks((int64_t)a.N * a.H * a.W, a.C) * 2 * a.C}, f32);
   a.x = x.data_ptr();
@@ -645,7 +675,8 @@ std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x
 
 // y = relu?(x*scale+shift [+ res | + res*rscale+rshift])
 Tensor bn_apply(Tensor x, Tensor scale_shift, c10::optional<Tensor> res,
-                c10::optional<Tensor> res_scale_shift, bool relu) {
+                c10::optional<Tensor> res_scale_shift, bool relu,
+                c10::optional<Tensor> bits_out) {
   const c10::DeviceGuard guard(x.device());
   check_nhwc(x, "x");
   const int64_t C = x.dim() == 4 ? x.size(1) : x.size(-1);
@@ -662,6 +693,12 @@ Tensor bn_apply(Tensor x, Tensor scale_shift, c10::optional<Tensor> res,
   a.relu = relu;
   a.scale = ptr<float>(scale_shift);
   a.shift = a.scale + C;
+  if (bits_out.has_value() && bits_out->defined()) {
+    TORCH_CHECK(relu, "a ReLU bitmap needs relu=True");
+    TORCH_CHECK(bits_out->scalar_type() == at::kByte && bits_out->numel() * 8 == x.numel() &&
+                bits_out->is_contiguous(), "bits_out must be a contiguous uint8 [numel/8]");
+    a.bits = ptr<uint8_t>(*bits_out);
+  }
   if (res.has_value() && res->defined()) {
     check_nhwc(*res, "res");
     TORCH_CHECK(res->numel() == x.numel() && res->scalar_type() == x.scalar_type(),
@@ -719,7 +756,8 @@ TORCH_LIBRARY(lwaaai, m) {
       "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "bn_bwd(Tensor dy, Tensor x, Tensor? y, Tensor? weight, Tensor mean, Tensor invstd, "
-      "Tensor? scale_shift, bool training, bool relu, bool need_dres) "
+      "Tensor? scale_shift, bool training, bool relu, bool need_dres, Tensor? bits=None, "
+      "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) "
       "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "gemm(Tensor A, int lda, bool a_kcontig, Tensor B, int ldb, bool b_kcontig, int M, int N, "
@@ -733,12 +771,13 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "bn_stats(Tensor x, Tensor? stats, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
       "Tensor(b!)? running_var, float momentum, float eps) -> (Tensor, Tensor, Tensor)");
-  m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? res, Tensor? res_scale_shift, bool relu) "
-        "-> Tensor");
+  m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? res, Tensor? res_scale_shift, bool relu, "
+        "Tensor(a!)? bits_out=None) -> Tensor");
   m.def("stem_pool_fwd(Tensor x, Tensor scale_shift, int k, int s, int p) -> (Tensor, Tensor)");
   m.def(
       "stem_pool_bwd(Tensor dp, Tensor idx, Tensor x, Tensor scale_shift, Tensor? weight, "
-      "Tensor mean, Tensor invstd, int k, int s, int p) -> (Tensor, Tensor, Tensor)");
+      "Tensor mean, Tensor invstd, int k, int s, int p, Tensor(a!)? dgamma_out=None, "
+      "Tensor(b!)? dbeta_out=None) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {

@@ -59,10 +59,17 @@ template <> struct V8<float> {
 // partial: [gridDim.x][2C]
 // ------------------------------------------------------------------------------------------
 // RELU: 0 none, 1 mask from the saved output y, 2 mask recomputed from x: x*scale+shift > 0
-// (bit-identical to the forward's test, which evaluated the same fp32 expression).
+// (bit-identical to the forward's test, which evaluated the same fp32 expression), 3 mask from
+// the 1-bit-per-element ReLU bitmap the forward apply wrote (1/16 of the bytes of y).
+__device__ __forceinline__ void mask_bits(float d[8], uint32_t bits) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) d[k] = ((bits >> k) & 1u) ? d[k] : 0.f;
+}
+
 template <typename T, int MODE, int RELU>
 __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, const T* __restrict__ dy,
                                                    const T* __restrict__ y,
+                                                   const uint8_t* __restrict__ bits,
                                                    const float* __restrict__ mean,
                                                    const float* __restrict__ fscale,
                                                    const float* __restrict__ fshift, int64_t M,
@@ -114,6 +121,9 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
 #pragma unroll
             for (int k = 0; k < 8; ++k)
               d[u][k] = fmaf(xv[u][k], fs[k], fh[k]) > 0.f ? d[u][k] : 0.f;
+        } else if (RELU == 3) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) mask_bits(d[u], bits[(row + u * R) * G + g]);
         }
       }
 #pragma unroll
@@ -142,6 +152,8 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
         } else if (RELU == 2) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) d[k] = fmaf(xv[k], fs[k], fh[k]) > 0.f ? d[k] : 0.f;
+        } else if (RELU == 3) {
+          mask_bits(d, bits[row * G + g]);
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) { a[k] += d[k]; b[k] += d[k] * (xv[k] - mu[k]); }
@@ -233,6 +245,15 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ rows, 
 
 // Thread-constant channel group: the grid-stride step is a multiple of G = C/8 (apply_grid), so
 // a thread always touches the same 8 channels and keeps their coefficients in registers.
+// ReLU bitmap of 8 outputs: bit k set iff the STORED (bf16-rounded) value is > 0, i.e. exactly
+// the test the backward would apply to the saved output.
+__device__ __forceinline__ uint8_t relu_bits(const float v[8]) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b |= (bf2f(f2bf_rne(v[k])) > 0.f ? 1u : 0u) << k;
+  return (uint8_t)b;
+}
+
 // RES: 0 none, 1 plain residual add, 2 residual through its own BatchNorm affine (the downsample
 // branch of a ResNet block: y = relu(x*scale+shift + r*rscale+rshift), the normalised shortcut is
 // never materialised).
@@ -242,7 +263,8 @@ __global__ __launch_bounds__(BNT) void k_bn_apply(const T* __restrict__ x, const
                                                   const float* __restrict__ scale,
                                                   const float* __restrict__ shift,
                                                   const float* __restrict__ rscale,
-                                                  const float* __restrict__ rshift, int64_t n8,
+                                                  const float* __restrict__ rshift,
+                                                  uint8_t* __restrict__ bits_out, int64_t n8,
                                                   int C) {
   const int G = C / 8;
   const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
@@ -274,6 +296,7 @@ __global__ __launch_bounds__(BNT) void k_bn_apply(const T* __restrict__ x, const
         v[u][k] = t;
       }
       V8<T>::store(y + (i + u * step) * 8, v[u]);
+      if (RELU && bits_out) bits_out[i + u * step] = relu_bits(v[u]);
     }
   }
   if (i < n8) {
@@ -289,6 +312,7 @@ __global__ __launch_bounds__(BNT) void k_bn_apply(const T* __restrict__ x, const
       v[k] = t;
     }
     V8<T>::store(y + i * 8, v);
+    if (RELU && bits_out) bits_out[i] = relu_bits(v);
   }
 }
 
@@ -296,14 +320,15 @@ __global__ __launch_bounds__(256) void k_bn_finalize_bwd(
     const float* __restrict__ partial, int nblocks, int C, int64_t M,
     const float* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    float* __restrict__ A, float* __restrict__ B, float* __restrict__ Cc, int training) {
+    float* __restrict__ A, float* __restrict__ B, float* __restrict__ Cc, int training,
+    int accum) {
   double s1, s2;
   int c;
   if (!fold_partials(partial, nblocks, C, s1, s2, c)) return;
   const double is = invstd[c];
   const double gm = gamma ? gamma[c] : 1.0;
-  if (dbeta) dbeta[c] = (float)s1;
-  if (dgamma) dgamma[c] = (float)(s2 * is);
+  if (dbeta) dbeta[c] = accum ? dbeta[c] + (float)s1 : (float)s1;
+  if (dgamma) dgamma[c] = accum ? dgamma[c] + (float)(s2 * is) : (float)(s2 * is);
   const double a = gm * is;
   if (!training) {             // running statistics are constants: dx = gamma*invstd*dy'
     A[c] = (float)a;
@@ -321,6 +346,7 @@ __global__ __launch_bounds__(256) void k_bn_finalize_bwd(
 template <typename T, int RELU, bool DRES>
 __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, const T* __restrict__ dy,
                                                       const T* __restrict__ y,
+                                                      const uint8_t* __restrict__ bits,
                                                       const float* __restrict__ fscale,
                                                       const float* __restrict__ fshift,
                                                       const float* __restrict__ A,
@@ -352,6 +378,8 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, c
     } else if (RELU == 2) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) d[k] = fmaf(xv[k], fs[k], fh[k]) > 0.f ? d[k] : 0.f;
+    } else if (RELU == 3) {
+      mask_bits(d, bits[i]);
     }
     if (DRES) V8<T>::store(dres + off, d);
     float o[8];
@@ -402,7 +430,7 @@ static void bn_apply_t(const BNArgs& a, hipStream_t st) {
   const dim3 grid(apply_grid(n8, a.C)), block(BNT);
 #define LW_AP(R, L)                                                                              \
   hipLaunchKernelGGL((k_bn_apply<T, R, L>), grid, block, 0, st, x, res, y, a.scale, a.shift,     \
-                     a.res_scale, a.res_shift, n8, a.C)
+                     a.res_scale, a.res_shift, a.bits, n8, a.C)
   const int rm = !res ? 0 : (a.res_scale ? 2 : 1);
   if (rm == 2) { if (a.relu) LW_AP(2, true); else LW_AP(2, false); }
   else if (rm == 1) { if (a.relu) LW_AP(1, true); else LW_AP(1, false); }
@@ -427,7 +455,8 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
     int64_t rpb;
     reduce_geometry(a.M, a.C, rpb, nb);
     hipLaunchKernelGGL((k_bn_reduce<T, 0, 0>), dim3(nb), dim3(BNT), 0, st, static_cast<const T*>(a.x),
-                       (const T*)nullptr, (const T*)nullptr, (const float*)nullptr,
+                       (const T*)nullptr, (const T*)nullptr, (const uint8_t*)nullptr,
+                       (const float*)nullptr,
                        (const float*)nullptr, (const float*)nullptr, a.M, a.C, rpb, a.partial);
   }
   hipLaunchKernelGGL(k_bn_finalize_fwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
@@ -453,20 +482,22 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   int nb;
   reduce_geometry(a.M, a.C, rpb, nb);
   // relu mask: recompute from x when the forward had no residual (saves reading y)
-  const int rmode = !a.relu ? 0 : (a.scale ? 2 : 1);
+  const int rmode = !a.relu ? 0 : (a.bits ? 3 : (a.scale ? 2 : 1));
 #define LW_RED(R)                                                                                \
-  hipLaunchKernelGGL((k_bn_reduce<T, 1, R>), dim3(nb), dim3(BNT), 0, st, x, dy, y, a.mean, a.scale, \
-                     a.shift, a.M, a.C, rpb, a.partial)
-  if (rmode == 0) LW_RED(0); else if (rmode == 1) LW_RED(1); else LW_RED(2);
+  hipLaunchKernelGGL((k_bn_reduce<T, 1, R>), dim3(nb), dim3(BNT), 0, st, x, dy, y, a.bits, a.mean, \
+                     a.scale, a.shift, a.M, a.C, rpb, a.partial)
+  if (rmode == 0) LW_RED(0); else if (rmode == 1) LW_RED(1); else if (rmode == 2) LW_RED(2);
+  else LW_RED(3);
 #undef LW_RED
   hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
                      a.C, a.M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
-                     (int)a.training);
+                     (int)a.training, (int)a.accum_dparams);
   const dim3 grid(apply_grid(n8, a.C)), block(BNT);
 #define LW_BWD(R, D)                                                                            \
-  hipLaunchKernelGGL((k_bn_bwd_apply<T, R, D>), grid, block, 0, st, x, dy, y, a.scale, a.shift,  \
-                     a.A, a.B, a.Cc, dx, dres, n8, a.C)
-  if (rmode == 1) { if (dres) LW_BWD(1, true); else LW_BWD(1, false); }
+  hipLaunchKernelGGL((k_bn_bwd_apply<T, R, D>), grid, block, 0, st, x, dy, y, a.bits, a.scale,  \
+                     a.shift, a.A, a.B, a.Cc, dx, dres, n8, a.C)
+  if (rmode == 3) { if (dres) LW_BWD(3, true); else LW_BWD(3, false); }
+  else if (rmode == 1) { if (dres) LW_BWD(1, true); else LW_BWD(1, false); }
   else if (rmode == 2) { if (dres) LW_BWD(2, true); else LW_BWD(2, false); }
   else { if (dres) LW_BWD(0, true); else LW_BWD(0, false); }
 #undef LW_BWD
@@ -662,7 +693,8 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
                      a.shift, a.mean, (const float*)nullptr, (const float*)nullptr,
                      (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb);
   hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
-                     a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1);
+                     a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
+                     (int)a.accum_dparams);
   hipLaunchKernelGGL((k_stem_pool_bwd<1>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                      a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
                      (float*)nullptr, g, rpb);

@@ -132,6 +132,9 @@ struct BNArgs {
   int stats_blocks;        // bn_stats: >0 = partial sums already in `partial` ([2C][nb])
   const float* stat_rows;  // bn_stats: per-M-tile rows [R][2C] from a GEMM epilogue (or nullptr)
   int64_t stats_rows_n;    // R
+  uint8_t* bits;           // ReLU bitmap, 1 bit/element: written by the forward apply, read back
+                           // by the backward instead of the saved output (or nullptr)
+  bool accum_dparams;      // backward: dgamma/dbeta += (into the gradient arena) instead of =
 };
 int bn_reduce_blocks(int64_t M, int C);
 void bn_stats(const BNArgs& a, hipStream_t st);
@@ -158,6 +161,7 @@ struct StemArgs {
   float* B;
   float* Cc;
   int N, H, W, C, Ho, Wo, k, s, p;
+  bool accum_dparams;
 };
 void stem_pool_fwd(const StemArgs& a, hipStream_t st);
 void stem_pool_bwd(const StemArgs& a, hipStream_t st);

@@ -157,6 +157,22 @@ def _finish_param(p: torch.Tensor, g: Optional[torch.Tensor], direct: bool):
     return g.view_as(p) if g is not None else None
 
 
+def _bn_grad_outs(g: torch.Tensor, b: torch.Tensor):
+    """Arena views the BN backward kernel accumulates dgamma/dbeta into (no add kernels), or
+    (None, None) when the parameters are not arena-managed."""
+    if _direct(g) and _direct(b):
+        return g.grad.view(-1), b.grad.view(-1)
+    return None, None
+
+
+def _finish_bn(g: torch.Tensor, b: torch.Tensor, dg, db, outs):
+    if outs[0] is not None:          # already accumulated in place by the kernel
+        g._lw_grad_ready(g)
+        b._lw_grad_ready(b)
+        return None, None
+    return _finish_param(g, dg, _direct(g)), _finish_param(b, db, _direct(b))
+
+
 def _finish_wgrad(p: torch.Tensor, dst: torch.Tensor, direct: bool):
     return _finish_param(p, None, True) if direct else dst.view_as(p)
 
@@ -218,14 +234,16 @@ class _BottleneckFn(torch.autograd.Function):
             cd, std = gemm(xsr, Cin, True, Wd, Cin, True, M2, cout, Cin, stats=True)
             meand, invd, ssd = lib.bn_stats(cd, std, gd, bd, bnd.running_mean, bnd.running_var,
                                             _bn_momentum(bnd), bnd.eps)
-            out = lib.bn_apply(c3, ss3, cd, ssd, True)
-            ctx.save_for_backward(x, c1, a1, c2, c3, out, W1, W2, W3, g1, g2, g3, mean1, inv1,
+            bits3 = torch.empty(M2 * cout // 8, dtype=torch.uint8, device=x.device)
+            out = lib.bn_apply(c3, ss3, cd, ssd, True, bits3)
+            ctx.save_for_backward(x, c1, a1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1,
                                   ss1, mean2, inv2, ss2, mean3, inv3, xsr, cd, Wd, gd, meand,
                                   invd)
             ctx.down_stride = s
         else:
-            out = lib.bn_apply(c3, ss3, xr, None, True)
-            ctx.save_for_backward(x, c1, a1, c2, c3, out, W1, W2, W3, g1, g2, g3, mean1, inv1,
+            bits3 = torch.empty(M2 * cout // 8, dtype=torch.uint8, device=x.device)
+            out = lib.bn_apply(c3, ss3, xr, None, True, bits3)
+            ctx.save_for_backward(x, c1, a1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1,
                                   ss1, mean2, inv2, ss2, mean3, inv3)
             ctx.down_stride = 0
         ctx.geom = (N, Cin, H, W, N2, H2, W2_, width, cout, M, M2)
@@ -237,15 +255,18 @@ class _BottleneckFn(torch.autograd.Function):
     def backward(ctx, dout):
         lib = load()
         saved = ctx.saved_tensors
-        x, c1, a1, c2, c3, out, W1, W2, W3, g1, g2, g3, mean1, inv1, ss1, mean2, inv2, ss2, \
+        x, c1, a1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1, ss1, mean2, inv2, ss2, \
             mean3, inv3 = saved[:20]
         N, Cin, H, W, N2, H2, W2_, width, cout, M, M2 = ctx.geom
         w1, g1p, b1p, w2, g2p, b2p, w3, g3p, b3p, wd, gdp, bdp = ctx.params
         has_down = ctx.down_stride > 0
         dr = _rows(dout.to(BF16).contiguous(memory_format=CL))
-        # BN3 (+ shortcut) backward, ReLU mask from the block output
-        dc3, dg3, db3, dres = lib.bn_bwd(dr, c3, out, g3, mean3, inv3, None, True, True, True)
+        # BN3 (+ shortcut) backward, ReLU mask from the forward's 1-bit bitmap
+        o3 = _bn_grad_outs(g3p, b3p)
+        dc3, dg3, db3, dres = lib.bn_bwd(dr, c3, None, g3, mean3, inv3, None, True, True, True,
+                                         bits3, o3[0], o3[1])
         grads = {}
+        grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
         # conv3: weight gradient with BN2-apply recomputed in the B prologue, into the arena
         dst3, d3 = _wgrad_target(w3, (cout, width))
         gemm(dc3, cout, False, c2, width, False, cout, width, M2, out_bf16=False,
@@ -253,7 +274,10 @@ class _BottleneckFn(torch.autograd.Function):
              split_k=True)
         grads["w3"] = _finish_wgrad(w3, dst3, d3)
         da2, _ = gemm(dc3, cout, True, W3, width, False, M2, width, cout)
-        dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False)
+        o2 = _bn_grad_outs(g2p, b2p)
+        dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False,
+                                      None, o2[0], o2[1])
+        grads["g2"], grads["b2"] = _finish_bn(g2p, b2p, dg2, db2, o2)
         # conv2 (3x3) backward on MIOpen
         a1n = _nchw(a1, N, H, W)
         dc2n = _nchw(dc2, N2, H2, W2_)
@@ -267,7 +291,10 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             grads["w2"] = dW2.float().contiguous(memory_format=CL)
         da1 = _rows(da1n.contiguous(memory_format=CL))
-        dc1, dg1, db1, _ = lib.bn_bwd(da1, c1, None, g1, mean1, inv1, ss1, True, True, False)
+        o1 = _bn_grad_outs(g1p, b1p)
+        dc1, dg1, db1, _ = lib.bn_bwd(da1, c1, None, g1, mean1, inv1, ss1, True, True, False,
+                                      None, o1[0], o1[1])
+        grads["g1"], grads["b1"] = _finish_bn(g1p, b1p, dg1, db1, o1)
         xr = _rows(x)
         dst1, d1 = _wgrad_target(w1, (width, Cin))
         gemm(dc1, width, False, xr, Cin, False, width, Cin, M, out_bf16=False, out=dst1,
@@ -276,8 +303,10 @@ class _BottleneckFn(torch.autograd.Function):
         if has_down:
             xsr, cd, Wd, gd, meand, invd = saved[20:]
             s = ctx.down_stride
+            od = _bn_grad_outs(gdp, bdp)
             dcd, dgd, dbd, _ = lib.bn_bwd(dres, cd, None, gd, meand, invd, None, True, False,
-                                          False)
+                                          False, None, od[0], od[1])
+            grads["gd"], grads["bd"] = _finish_bn(gdp, bdp, dgd, dbd, od)
             dstd, dd = _wgrad_target(wd, (cout, Cin))
             gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2, out_bf16=False, out=dstd,
                  accumulate=True, split_k=True)
@@ -289,13 +318,8 @@ class _BottleneckFn(torch.autograd.Function):
                 dxs, _ = gemm(dcd, cout, True, Wd, Cin, False, M2, Cin, cout)
                 dxv = dx.view(N, H, W, Cin)
                 dxv[:, ::s, ::s, :] += dxs.view(N2, H2, W2_, Cin)
-            grads["gd"] = _finish_param(gdp, dgd, _direct(gdp))
-            grads["bd"] = _finish_param(bdp, dbd, _direct(bdp))
         else:
             dx, _ = gemm(dc1, width, True, W1, Cin, False, M, Cin, width, addend=dres)
-        for name, p, g in (("g1", g1p, dg1), ("b1", b1p, db1), ("g2", g2p, dg2),
-                           ("b2", b2p, db2), ("g3", g3p, dg3), ("b3", b3p, db3)):
-            grads[name] = _finish_param(p, g, _direct(p))
         dxn = _nchw(dx, N, H, W)
         return (dxn, grads["w1"], grads["g1"], grads["b1"], grads["w2"], grads["g2"], grads["b2"],
                 grads["w3"], grads["g3"], grads["b3"], grads.get("wd"), grads.get("gd"),

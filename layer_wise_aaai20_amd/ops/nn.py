@@ -189,9 +189,11 @@ class _StemPoolFn(torch.autograd.Function):
         c, idx, ss, weight, mean, invstd = ctx.saved_tensors
         w, b = ctx.params
         dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-        dc, dg, db = load().stem_pool_bwd(dout, idx, c, ss, weight, mean, invstd, *ctx.geom)
-        return (dc, block._finish_param(w, dg, block._direct(w)),
-                block._finish_param(b, db, block._direct(b)), None, None)
+        outs = block._bn_grad_outs(w, b)
+        dc, dg, db = load().stem_pool_bwd(dout, idx, c, ss, weight, mean, invstd, *ctx.geom,
+                                          outs[0], outs[1])
+        gw, gb = block._finish_bn(w, b, dg, db, outs)
+        return dc, gw, gb, None, None
 
 
 def _pool_geom(pool: nn.MaxPool2d):

@@ -549,6 +549,242 @@ __global__ __launch_bounds__(GT) void k_splitk_reduce(const float* __restrict__ 
   }
 }
 
+
+// ==========================================================================================
+// Streaming GEMM for the large-M / small-K problems of a ResNet bottleneck (the 1x1 convolutions
+// of the first two stages: M = N·H·W up to 802816 rows, K = 64..256): HBM-bound, and with one
+// output tile per workgroup the tiled kernel above stalls on a full memory latency per tile at
+// two workgroups per CU. Here a workgroup is persistent over a strided set of 128-row tiles:
+//   * the whole B panel [BN][K] is staged into LDS once and stays resident;
+//   * A fragments go straight from HBM into registers in MFMA layout (each lane one 16-byte load
+//     per 16x32 fragment: 16 rows x 32 k, full 64-byte row segments) — no LDS round trip — and
+//     the NEXT tile's fragments are loaded while the current one runs its MFMAs and epilogue;
+//   * the optional BatchNorm-apply+ReLU prologue runs on the A fragments in registers, its
+//     per-k coefficients held in LDS;
+//   * the epilogue stages the bf16 tile through LDS for 16-byte coalesced stores, adds an
+//     optional bf16 addend, and accumulates per-column Σ/Σ² in registers across all of the
+//     workgroup's tiles (one statistics row per workgroup, folded by bn.hip k_colsum).
+// B is [N][K] (K-contiguous: forward x·Wᵀ) or [K][N] (N-contiguous: data gradient dy·W).
+// ==========================================================================================
+constexpr int SBM = 128;                        // rows per workgroup tile (4 waves x 32)
+
+template <int K, int BN, bool BKC, bool STATS, bool PRO, bool ADD>
+__global__ __launch_bounds__(GT) void k_gemm_stream(const GemmK p) {
+  constexpr int LDB = K + 8;                    // B panel row (bf16), 16-B aligned, bank spread
+  constexpr int LDO = BN + 8;                   // staged output row (bf16)
+  constexpr int KS = K / 32;                    // MFMA k-steps
+  constexpr int FN = BN / 16;
+  constexpr int B_BYTES = BN * LDB * 2;
+  constexpr int C_BYTES = PRO ? 2 * K * 4 : 0;
+  constexpr int O_BYTES = SBM * LDO * 2;
+  constexpr int F_BYTES = GT * 16 * 4;          // stats fold
+  constexpr int TAIL = O_BYTES > F_BYTES ? O_BYTES : F_BYTES;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[B_BYTES + C_BYTES + TAIL];
+  uint16_t* Bs = reinterpret_cast<uint16_t*>(lds);
+  float* coef = reinterpret_cast<float*>(lds + B_BYTES);            // [scale K][shift K]
+  uint16_t* Os = reinterpret_cast<uint16_t*>(lds + B_BYTES + C_BYTES);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int n0 = blockIdx.y * BN;
+
+  // ---- stage the B panel (and prologue coefficients) once
+  if (BKC) {
+    for (int c = threadIdx.x; c < BN * (K / 8); c += GT) {
+      const int n = c / (K / 8), k8 = (c % (K / 8)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n0 + n < p.N) v = *reinterpret_cast<const uint4*>(p.B + (int64_t)(n0 + n) * p.ldb + k8);
+      *reinterpret_cast<uint4*>(Bs + n * LDB + k8) = v;
+    }
+  } else {
+    for (int c = threadIdx.x; c < K * (BN / 8); c += GT) {
+      const int k = c / (BN / 8), n8 = (c % (BN / 8)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n0 + n8 < p.N) v = *reinterpret_cast<const uint4*>(p.B + (int64_t)k * p.ldb + n0 + n8);
+      const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        Bs[(n8 + 2 * j) * LDB + k] = (uint16_t)(q[j] & 0xffffu);
+        Bs[(n8 + 2 * j + 1) * LDB + k] = (uint16_t)(q[j] >> 16);
+      }
+    }
+  }
+  if (PRO) {
+    for (int k = threadIdx.x; k < K; k += GT) {
+      coef[k] = p.pro_scale[k];
+      coef[K + k] = p.pro_shift[k];
+    }
+  }
+  __syncthreads();
+
+  const int tiles_m = (p.M + SBM - 1) / SBM;
+  // A fragments of one tile: [i = 16-row half][s = k-step], 8 bf16 each
+  uint4 a_cur[2][KS], a_nxt[2][KS];
+  auto load_a = [&](uint4 (&dst)[2][KS], int tm) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = tm * SBM + w * 32 + i * 16 + (l & 15);
+      const uint16_t* src = p.A + (int64_t)m * p.lda + 8 * (l >> 4);
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        dst[i][s] = m < p.M ? *reinterpret_cast<const uint4*>(src + 32 * s) : make_uint4(0, 0, 0, 0);
+    }
+  };
+
+  float cs1[8], cs2[8];                         // this thread's 8 columns: Σv, Σv²
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { cs1[k] = 0.f; cs2[k] = 0.f; }
+  const int ccol = (threadIdx.x % (BN / 8)) * 8;  // fixed output column group of this thread
+  static_assert(GT % (BN / 8) == 0, "column group must be fixed per thread");
+
+  int tm = blockIdx.x;
+  if (tm < tiles_m) load_a(a_cur, tm);
+  for (; tm < tiles_m; tm += gridDim.x) {
+    const int tn = tm + gridDim.x;
+    if (tn < tiles_m) load_a(a_nxt, tn);         // next tile in flight during this one
+    if (PRO) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int kb = 32 * s + 8 * (l >> 4);
+        Coef8 co;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { co.s[j] = coef[kb + j]; co.t[j] = coef[K + kb + j]; }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int m = tm * SBM + w * 32 + i * 16 + (l & 15);
+          if (m < p.M) a_cur[i][s] = affine_relu8(a_cur[i][s], co);
+        }
+      }
+    }
+    f32x4 acc[2][FN];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 fa0 = __builtin_bit_cast(bf16x8, a_cur[0][s]);
+      const bf16x8 fa1 = __builtin_bit_cast(bf16x8, a_cur[1][s]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(
+            Bs + (16 * j + (l & 15)) * LDB + 32 * s + 8 * (l >> 4));
+        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa0, acc[0][j], 0, 0, 0);
+        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa1, acc[1][j], 0, 0, 0);
+      }
+    }
+    // ---- epilogue: Cᵀ fragments -> bf16 -> LDS tile -> 16-byte stores
+    __syncthreads();                             // previous tile's readback finished
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = w * 32 + i * 16 + (l & 15);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = 16 * j + 4 * (l >> 4);
+        const uint32_t lo = (uint32_t)bf16_rne(acc[i][j][0]) | ((uint32_t)bf16_rne(acc[i][j][1]) << 16);
+        const uint32_t hi = (uint32_t)bf16_rne(acc[i][j][2]) | ((uint32_t)bf16_rne(acc[i][j][3]) << 16);
+        *reinterpret_cast<uint2*>(Os + r * LDO + c) = make_uint2(lo, hi);
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < SBM * (BN / 8); c += GT) {
+      const int r = c / (BN / 8);
+      const int gm = tm * SBM + r, gn = n0 + ccol;
+      if (gm >= p.M || gn >= p.N) continue;
+      uint4 v = *reinterpret_cast<const uint4*>(Os + r * LDO + ccol);
+      if (STATS) {
+        const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float lo = __uint_as_float(q[k] << 16), hi = __uint_as_float(q[k] & 0xffff0000u);
+          cs1[2 * k] += lo; cs2[2 * k] += lo * lo;
+          cs1[2 * k + 1] += hi; cs2[2 * k + 1] += hi * hi;
+        }
+      }
+      uint16_t* dst = static_cast<uint16_t*>(p.C) + (int64_t)gm * p.ldc + gn;
+      if (ADD) v = add_bf16x8(v, *reinterpret_cast<const uint4*>(p.addend + (int64_t)gm * p.ldc + gn));
+      *reinterpret_cast<uint4*>(dst) = v;
+    }
+    if (tn < tiles_m) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) a_cur[i][s] = a_nxt[i][s];
+    }
+  }
+  if (STATS) {
+    constexpr int G8 = BN / 8, Q = GT / G8;
+    __syncthreads();
+    float* fold = reinterpret_cast<float*>(lds + B_BYTES + C_BYTES);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      fold[threadIdx.x * 16 + k] = cs1[k];
+      fold[threadIdx.x * 16 + 8 + k] = cs2[k];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < BN; c += GT) {
+      const int n = n0 + c;
+      if (n >= p.N) continue;
+      const int g = c / 8, k = c % 8;
+      float a = 0.f, b = 0.f;
+      for (int q = 0; q < Q; ++q) {
+        a += fold[(q * G8 + g) * 16 + k];
+        b += fold[(q * G8 + g) * 16 + 8 + k];
+      }
+      p.stats[(int64_t)blockIdx.x * 2 * p.N + n] = a;        // [gridDim.x][2][N]
+      p.stats[(int64_t)blockIdx.x * 2 * p.N + p.N + n] = b;
+    }
+  }
+}
+
+static int stream_bn(int tile) { return tile == GEMM_S64 ? 64 : (tile == GEMM_S128 ? 128 : 256); }
+
+bool gemm_stream_ok(const GemmArgs& g) {
+  if (g.tile < GEMM_S64 || g.tile > GEMM_S256) return false;
+  const int bn = stream_bn(g.tile);
+  const bool kok = g.K == 64 || g.K == 128 || (g.K == 256 && bn <= 128);
+  return kok && g.a_kcontig && g.out_bf16 && !g.bias && !g.relu && g.splits <= 1 &&
+         !g.accumulate && (g.N % 8) == 0 && (g.ldc % 8) == 0 && (!g.pro_scale || g.pro_on_a) &&
+         !(g.pro_scale && !g.b_kcontig) && !(g.addend && g.stats);
+}
+
+int gemm_stream_grid_m(const GemmArgs& g) {
+  const int panels = (g.N + stream_bn(g.tile) - 1) / stream_bn(g.tile);
+  const int tiles = (g.M + SBM - 1) / SBM;
+  const int bn = stream_bn(g.tile);               // resident workgroups per CU (LDS-bound)
+  int want = 256 * (bn == 64 ? 4 : (bn == 128 ? 2 : 1)) / panels;
+  want = want < 1 ? 1 : want;
+  return tiles < want ? tiles : want;
+}
+
+template <int K, int BN>
+static void stream_launch(const GemmArgs& g, const GemmK& k, hipStream_t st) {
+  const dim3 grid(gemm_stream_grid_m(g), (g.N + BN - 1) / BN), block(GT);
+  const bool stats = g.stats != nullptr, pro = g.pro_scale != nullptr, add = g.addend != nullptr;
+  if (g.b_kcontig) {
+    if (stats && pro) hipLaunchKernelGGL((k_gemm_stream<K, BN, true, true, true, false>), grid, block, 0, st, k);
+    else if (stats) hipLaunchKernelGGL((k_gemm_stream<K, BN, true, true, false, false>), grid, block, 0, st, k);
+    else if (add) hipLaunchKernelGGL((k_gemm_stream<K, BN, true, false, false, true>), grid, block, 0, st, k);
+    else hipLaunchKernelGGL((k_gemm_stream<K, BN, true, false, false, false>), grid, block, 0, st, k);
+  } else {
+    if (stats) hipLaunchKernelGGL((k_gemm_stream<K, BN, false, true, false, false>), grid, block, 0, st, k);
+    else if (add) hipLaunchKernelGGL((k_gemm_stream<K, BN, false, false, false, true>), grid, block, 0, st, k);
+    else hipLaunchKernelGGL((k_gemm_stream<K, BN, false, false, false, false>), grid, block, 0, st, k);
+  }
+}
+
+static void gemm_stream(const GemmArgs& g, hipStream_t st) {
+  GemmK k{g.A, g.B, g.C, nullptr, g.stats, nullptr, g.pro_scale, g.pro_shift, g.addend, g.lda,
+          g.ldb, g.ldc, g.M, g.N, g.K, g.K, 0, 1, 0};
+  const int bn = stream_bn(g.tile);
+#define LW_SK(KK)                                                                               \
+  if (bn == 64) stream_launch<KK, 64>(g, k, st);                                                \
+  else if (bn == 128) stream_launch<KK, 128>(g, k, st);                                         \
+  else stream_launch<KK, 256>(g, k, st);
+  if (g.K == 64) { LW_SK(64) }
+  else if (g.K == 128) { LW_SK(128) }
+  else { if (bn == 64) stream_launch<256, 64>(g, k, st); else stream_launch<256, 128>(g, k, st); }
+#undef LW_SK
+}
+
 // ------------------------------------------------------------------------------------------ host
 struct TileShape { int bm, bn, bk; };
 static TileShape tile_shape(int t) {
@@ -570,7 +806,10 @@ int gemm_pick_tile(const GemmArgs& g) {
   return GEMM_T128x128x32;
 }
 
-int gemm_tiles_m(const GemmArgs& g) { return (g.M + tile_shape(gemm_pick_tile(g)).bm - 1) / tile_shape(gemm_pick_tile(g)).bm; }
+int gemm_tiles_m(const GemmArgs& g) {
+  if (g.tile >= GEMM_S64) return gemm_stream_grid_m(g);   // one statistics row per workgroup
+  return (g.M + tile_shape(gemm_pick_tile(g)).bm - 1) / tile_shape(gemm_pick_tile(g)).bm;
+}
 
 static int k_per_split(int K, int splits, int bk) {
   splits = splits < 1 ? 1 : splits;
@@ -579,6 +818,7 @@ static int k_per_split(int K, int splits, int bk) {
 }
 
 int gemm_splits_used(const GemmArgs& g) {
+  if (g.tile >= GEMM_S64) return 1;
   const int bk = tile_shape(gemm_pick_tile(g)).bk;
   const int kps = k_per_split(g.K, g.splits, bk);
   return (g.K + kps - 1) / kps;
@@ -615,6 +855,10 @@ static void launch_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, h
 }
 
 void gemm_bf16(const GemmArgs& g, hipStream_t st) {
+  if (g.tile >= GEMM_S64) {
+    gemm_stream(g, st);
+    return;
+  }
   const int t = gemm_pick_tile(g);
   const TileShape ts = tile_shape(t);
   const int kps = k_per_split(g.K, g.splits, ts.bk);

@@ -192,11 +192,15 @@ struct GemmArgs {
 };
 enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_T256x64x32 = 3,
                 GEMM_T64x256x32 = 4, GEMM_T256x64x64 = 5,
-                GEMM_T64x64x64 = 6 };
+                GEMM_T64x64x64 = 6,
+                // streaming kernel (persistent, B panel resident in LDS, A straight to registers),
+                // output-panel width 64 / 128 / 256; K must be 64, 128 or 256
+                GEMM_S64 = 11, GEMM_S128 = 12, GEMM_S256 = 13 };
 void gemm_bf16(const GemmArgs& g, hipStream_t st);
 int gemm_pick_tile(const GemmArgs& g);
 int gemm_tiles_m(const GemmArgs& g);
 int gemm_splits_used(const GemmArgs& g);
+bool gemm_stream_ok(const GemmArgs& g);
 
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],

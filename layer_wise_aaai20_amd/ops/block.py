@@ -52,6 +52,7 @@ from ._ext import load
 BF16 = torch.bfloat16
 CL = torch.channels_last
 TILES = (1, 2, 3, 4, 5, 6)          # csrc GemmTile ids (0 = heuristic)
+STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -84,7 +85,7 @@ class GemmTuner:
         self.best: Dict[tuple, int] = {}
         self.enabled = os.environ.get("LWAAAI_GEMM_TUNE", "1") != "0"
 
-    def pick(self, key, run) -> int:
+    def pick(self, key, run, candidates=TILES) -> int:
         t = self.best.get(key)
         if t is not None:
             return t
@@ -92,7 +93,7 @@ class GemmTuner:
             self.best[key] = 0
             return 0
         times = []
-        for tile in TILES:
+        for tile in candidates:
             run(tile)                                  # compile / warm
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -107,6 +108,18 @@ class GemmTuner:
 
 
 TUNER = GemmTuner()
+
+
+def stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro, pro_on_a, add, split_k,
+                 accumulate) -> tuple:
+    """Streaming-kernel candidates for a problem (``csrc/gemm.hip`` k_gemm_stream): large M,
+    K in {64, 128, 256}, K-contiguous A, bf16 output; the prologue only with a K-contiguous B."""
+    if not (a_kc and out_bf16 and not split_k and not accumulate and M >= 16384 and
+            K in (64, 128, 256) and N % 8 == 0 and not (stats and add)):
+        return ()
+    if pro and (not pro_on_a or not b_kc):
+        return ()
+    return tuple(t for t in STREAM if not (K == 256 and t == 13))
 
 
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro=None,
@@ -126,8 +139,11 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
 
     def run(tile):
         lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile), out_bf16,
-                    tile, ps, ph, pro_on_a, stats, None, None, False, 0)
-    tile = TUNER.pick(key, run)
+                    tile, ps, ph, pro_on_a, stats, None, addend if tile in STREAM else None,
+                    False, 0)
+    tile = TUNER.pick(key, run, TILES + stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats,
+                                                     pro is not None, pro_on_a,
+                                                     addend is not None, split_k, accumulate))
     return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile),
                        out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc)
 

@@ -33,9 +33,14 @@ for M, N, K in ((802816, 256, 64), (200704, 512, 128), (802816, 64, 256)):
     for name, b, ldb, bkc in (("Bkc", W, K, True), ("Bnc", Wt, N, False)):
         for stats in (False, True):
             for pro in (False, True):
-                r = {t: timeit(lambda: lib.gemm_ex(A, K, True, b, ldb, bkc, M, N, K, None, False,
-                                                   1, True, t, sc if pro else None,
-                                                   sh if pro else None, True, stats, None, None,
-                                                   False, 0)) for t in (1, 2, 3, 4, 5, 6)}
+                r = {}
+                for t in (1, 2, 3, 4, 5, 6, 11, 12, 13):
+                    try:
+                        r[t] = timeit(lambda: lib.gemm_ex(A, K, True, b, ldb, bkc, M, N, K, None,
+                                                          False, 1, True, t, sc if pro else None,
+                                                          sh if pro else None, True, stats, None,
+                                                          None, False, 0))
+                    except RuntimeError:
+                        pass
                 print(f"  {name} stats={int(stats)} pro={int(pro)}: " +
                       " ".join(f"{t}:{v:.0f}" for t, v in r.items()), flush=True)

@@ -446,7 +446,8 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
                                    bool out_bf16, int64_t tile, c10::optional<Tensor> pro_scale,
                                    c10::optional<Tensor> pro_shift, bool pro_on_a,
                                    bool want_stats, c10::optional<Tensor> out,
-                                   c10::optional<Tensor> addend, bool accumulate, int64_t ldc) {
+                                   c10::optional<Tensor> addend, bool accumulate, int64_t ldc,
+                                   c10::optional<Tensor> addend_bits) {
   const c10::DeviceGuard guard(A.device());
   TORCH_CHECK(A.is_cuda() && B.is_cuda(), "gemm needs GPU tensors");
   check_dtype(A, at::kBFloat16, "A");
@@ -499,6 +500,12 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
                 "addend must be dense");
     check_aligned16(addend->data_ptr(), "addend");
     g.addend = ptr<uint16_t>(*addend);
+    if (addend_bits.has_value() && addend_bits->defined()) {
+      TORCH_CHECK(ldc == N && addend_bits->scalar_type() == at::kByte &&
+                  addend_bits->numel() * 8 >= M * N && N % 8 == 0,
+                  "addend_bits: uint8 bitmap of the [M, N] addend (ldc == N, N % 8 == 0)");
+      g.add_bits = ptr<uint8_t>(*addend_bits);
+    }
   }
   if (bias.has_value() && bias->defined()) {
     check_dtype(*bias, at::kFloat, "bias");
@@ -551,7 +558,7 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
             int64_t splits, bool out_bf16) {
   return std::get<0>(gemm_ex(A, lda, a_kcontig, B, ldb, b_kcontig, M, N, K, bias, relu, splits,
                              out_bf16, 0, c10::nullopt, c10::nullopt, true, false, c10::nullopt,
-                             c10::nullopt, false, 0));
+                             c10::nullopt, false, 0, c10::nullopt));
 }
 
 // ---------------------------------------------------------------- BN pieces for fused blocks
@@ -769,7 +776,8 @@ TORCH_LIBRARY(lwaaai, m) {
       "gemm_ex(Tensor A, int lda, bool a_kcontig, Tensor B, int ldb, bool b_kcontig, int M, "
       "int N, int K, Tensor? bias, bool relu, int splits, bool out_bf16, int tile, "
       "Tensor? pro_scale, Tensor? pro_shift, bool pro_on_a, bool want_stats, "
-      "Tensor(a!)? out=None, Tensor? addend=None, bool accumulate=False, int ldc=0) "
+      "Tensor(a!)? out=None, Tensor? addend=None, bool accumulate=False, int ldc=0, "
+      "Tensor? addend_bits=None) "
       "-> (Tensor, Tensor)");
   m.def(
       "bn_stats(Tensor x, Tensor? stats, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "

@@ -60,6 +60,28 @@ __device__ __forceinline__ uint4 add_bf16x8(uint4 a, uint4 b) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// 8 addend values of a chunk, zeroed where the ReLU bitmap (bits of the chunk's first element,
+// chunk-aligned) is clear.
+__device__ __forceinline__ uint4 masked_addend8(const uint16_t* __restrict__ add,
+                                                const uint8_t* __restrict__ bits, int64_t e) {
+  uint4 a = *reinterpret_cast<const uint4*>(add + e);
+  if (bits) {
+    const uint32_t b = bits[e >> 3];
+    const uint32_t m0 = ((b & 1u) ? 0xffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u);
+    const uint32_t m1 = ((b & 4u) ? 0xffffu : 0u) | ((b & 8u) ? 0xffff0000u : 0u);
+    const uint32_t m2 = ((b & 16u) ? 0xffffu : 0u) | ((b & 32u) ? 0xffff0000u : 0u);
+    const uint32_t m3 = ((b & 64u) ? 0xffffu : 0u) | ((b & 128u) ? 0xffff0000u : 0u);
+    a = make_uint4(a.x & m0, a.y & m1, a.z & m2, a.w & m3);
+  }
+  return a;
+}
+
+__device__ __forceinline__ float masked_addend1(const uint16_t* __restrict__ add,
+                                                const uint8_t* __restrict__ bits, int64_t e) {
+  if (bits && !((bits[e >> 3] >> (e & 7)) & 1u)) return 0.f;
+  return __uint_as_float((uint32_t)add[e] << 16);
+}
+
 // R = extent of the tile along m (A) or n (B). KC tiles are stored [R][BK+PAD], the others
 // [BK][R+PAD]; both are moved as 16-byte chunks of 8 contiguous elements.
 template <int R, int BK, bool KC> struct Tile {
@@ -205,6 +227,8 @@ struct GemmK {
   const float* pro_scale;
   const float* pro_shift;
   const uint16_t* addend;      // optional bf16 [M][ldc] added to a bf16 output (after rounding)
+  const uint8_t* add_bits;     // optional ReLU bitmap of the addend (1 bit/element, ldc == N):
+                               // the addend enters as addend·[bit] (a BN+ReLU backward's dres)
   int64_t lda, ldb, ldc;
   int M, N, K, k_per_split, relu, out_bf16, accumulate;   // accumulate: fp32 C += result
 };
@@ -396,14 +420,14 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       uint16_t* dst = static_cast<uint16_t*>(p.C) + (int64_t)gm * p.ldc + gn;
       if (vec && gn + 8 <= p.N) {
         uint4 v = *reinterpret_cast<const uint4*>(src);
-        if (p.addend) v = add_bf16x8(v, *reinterpret_cast<const uint4*>(p.addend + (int64_t)gm * p.ldc + gn));
+        if (p.addend) v = add_bf16x8(v, masked_addend8(p.addend, p.add_bits, (int64_t)gm * p.ldc + gn));
         *reinterpret_cast<uint4*>(dst) = v;
       } else {
         for (int k = 0; k < 8 && gn + k < p.N; ++k) {
           uint16_t h = src[k];
           if (p.addend)
             h = bf16_rne(__uint_as_float((uint32_t)h << 16) +
-                         __uint_as_float((uint32_t)p.addend[(int64_t)gm * p.ldc + gn + k] << 16));
+                         masked_addend1(p.addend, p.add_bits, (int64_t)gm * p.ldc + gn + k));
           dst[k] = h;
         }
       }
@@ -500,6 +524,7 @@ __global__ __launch_bounds__(GT) void k_splitk_reduce(const float* __restrict__ 
                                                       int64_t ldc, const float* __restrict__ bias,
                                                       int relu, int M, int N, int out_bf16,
                                                       const uint16_t* __restrict__ addend,
+                                                      const uint8_t* __restrict__ add_bits,
                                                       int accumulate) {
   __shared__ float4 red[GT];
   const int ZT = 1 << zt_log2, OT = GT >> zt_log2;
@@ -540,7 +565,7 @@ __global__ __launch_bounds__(GT) void k_splitk_reduce(const float* __restrict__ 
     if (out_bf16) {
       uint16_t h = bf16_rne(x);
       if (addend)
-        h = bf16_rne(__uint_as_float((uint32_t)h << 16) + __uint_as_float((uint32_t)addend[m * ldc + n] << 16));
+        h = bf16_rne(__uint_as_float((uint32_t)h << 16) + masked_addend1(addend, add_bits, m * ldc + n));
       static_cast<uint16_t*>(C)[m * ldc + n] = h;
     } else {
       float* c = static_cast<float*>(C) + m * ldc + n;
@@ -700,7 +725,7 @@ __global__ __launch_bounds__(GT) void k_gemm_stream(const GemmK p) {
         }
       }
       uint16_t* dst = static_cast<uint16_t*>(p.C) + (int64_t)gm * p.ldc + gn;
-      if (ADD) v = add_bf16x8(v, *reinterpret_cast<const uint4*>(p.addend + (int64_t)gm * p.ldc + gn));
+      if (ADD) v = add_bf16x8(v, masked_addend8(p.addend, p.add_bits, (int64_t)gm * p.ldc + gn));
       *reinterpret_cast<uint4*>(dst) = v;
     }
     if (tn < tiles_m) {
@@ -772,7 +797,7 @@ static void stream_launch(const GemmArgs& g, const GemmK& k, hipStream_t st) {
 }
 
 static void gemm_stream(const GemmArgs& g, hipStream_t st) {
-  GemmK k{g.A, g.B, g.C, nullptr, g.stats, nullptr, g.pro_scale, g.pro_shift, g.addend, g.lda,
+  GemmK k{g.A, g.B, g.C, nullptr, g.stats, nullptr, g.pro_scale, g.pro_shift, g.addend, g.add_bits, g.lda,
           g.ldb, g.ldc, g.M, g.N, g.K, g.K, 0, 1, 0};
   const int bn = stream_bn(g.tile);
 #define LW_SK(KK)                                                                               \
@@ -866,7 +891,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
   const int tiles = ((g.M + ts.bm - 1) / ts.bm) * ((g.N + ts.bn - 1) / ts.bn);
   const int epi = zs > 1 ? EPI_PARTIAL : (g.stats ? EPI_STATS : EPI_STORE);
   GemmK k{g.A, g.B, g.C, g.partial, g.stats, zs > 1 ? nullptr : g.bias, g.pro_scale, g.pro_shift,
-          g.addend, g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, zs > 1 ? 0 : g.relu,
+          g.addend, g.add_bits, g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, zs > 1 ? 0 : g.relu,
           g.out_bf16 ? 1 : 0, g.accumulate ? 1 : 0};
   const dim3 grid(tiles, zs);
   switch (t) {
@@ -884,7 +909,8 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
     const int64_t groups = (total + 3) / 4, ot = GT >> zl;
     const dim3 rg((unsigned)((groups + ot - 1) / ot));
     hipLaunchKernelGGL(k_splitk_reduce, rg, dim3(GT), 0, st, g.partial, zs, zl, g.C, g.ldc, g.bias,
-                       g.relu, g.M, g.N, g.out_bf16 ? 1 : 0, g.addend, g.accumulate ? 1 : 0);
+                       g.relu, g.M, g.N, g.out_bf16 ? 1 : 0, g.addend, g.add_bits,
+                       g.accumulate ? 1 : 0);
   }
 }
 

@@ -188,6 +188,7 @@ struct GemmArgs {
   const float* pro_shift;  // (pro_on_a) or per-n of an N-contiguous B
   bool pro_on_a;
   const uint16_t* addend;  // optional bf16 [M][ldc] added to a bf16 output (dgrad + residual grad)
+  const uint8_t* add_bits; // optional ReLU bitmap masking the addend (ldc == N)
   bool accumulate;         // fp32 output: C += result (weight gradients into the zeroed arena)
 };
 enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_T256x64x32 = 3,

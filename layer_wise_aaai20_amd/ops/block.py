@@ -19,7 +19,8 @@ forward (training)::
 
 backward::
 
-    bn3 backward (mask from out)     → dc3, dres
+    bn3 backward (ReLU bitmap)       → dc3   (the shortcut gradient dres = dy·[out>0] is
+                                             never written)
     dW3 = dc3ᵀ·relu(bn2(c2))         GEMM, BN2-apply recomputed in the prologue, fp32 written
                                      straight into the gradient arena
     da2 = dc3·W3                     GEMM
@@ -27,7 +28,7 @@ backward::
     conv3x3 backward                 MIOpen
     bn1 backward (mask from c1)      → dc1
     dW1 = dc1ᵀ·x                     GEMM into the arena
-    dx  = dc1·W1 + dres              GEMM with the shortcut gradient added in the epilogue
+    dx  = dc1·W1 + dy·[out>0]        GEMM; the masked shortcut gradient is added in the epilogue
 
 Compared with the per-layer path this removes, per block, the BN1 and BN3 statistics passes, the
 BN2 apply pass and its materialised output, the shortcut-BN apply pass, the gradient add of the
@@ -123,7 +124,8 @@ def stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro, pro_on_a, add, split
 
 
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro=None,
-         pro_on_a=True, out=None, addend=None, accumulate=False, ldc=0, split_k=False):
+         pro_on_a=True, out=None, addend=None, accumulate=False, ldc=0, split_k=False,
+         addend_bits=None):
     """One MFMA GEMM launch (plus the split-K reduce when ``split_k``); see ``csrc/gemm.hip``."""
     lib = load()
     ps, ph = (pro[0], pro[1]) if pro is not None else (None, None)
@@ -140,12 +142,13 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
     def run(tile):
         lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile), out_bf16,
                     tile, ps, ph, pro_on_a, stats, None, addend if tile in STREAM else None,
-                    False, 0)
+                    False, 0, addend_bits if tile in STREAM else None)
     tile = TUNER.pick(key, run, TILES + stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats,
                                                      pro is not None, pro_on_a,
                                                      addend is not None, split_k, accumulate))
     return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile),
-                       out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc)
+                       out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc,
+                       addend_bits)
 
 
 # ----------------------------------------------------------------------------- grad sink
@@ -193,6 +196,14 @@ def _finish_wgrad(p: torch.Tensor, dst: torch.Tensor, direct: bool):
     return _finish_param(p, None, True) if direct else dst.view_as(p)
 
 
+def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
+    """bf16 copy of a weight: the view into the arena's per-forward bf16 mirror when it is
+    current (``GradArena.refresh_bf16``), else a cast."""
+    f = getattr(w, "_lw_bf16_of", None)
+    v = f() if f is not None else None
+    return v if v is not None else w.detach().to(BF16)
+
+
 def _bn_momentum(bn) -> float:
     if bn.momentum is None:
         return 1.0 / float(bn.num_batches_tracked)
@@ -219,9 +230,9 @@ class _BottleneckFn(torch.autograd.Function):
         xr = _rows(x)
         width = w1.shape[0]
         cout = w3.shape[0]
-        W1 = w1.detach().reshape(width, Cin).to(BF16)
-        W2 = w2.detach().to(BF16).contiguous(memory_format=CL)
-        W3 = w3.detach().reshape(cout, width).to(BF16)
+        W1 = _bf16_weight(w1).reshape(width, Cin)
+        W2 = _bf16_weight(w2).contiguous(memory_format=CL)
+        W3 = _bf16_weight(w3).reshape(cout, width)
         M = xr.shape[0]
         # conv1 (1x1) + BN1 statistics in the epilogue
         c1, st1 = gemm(xr, Cin, True, W1, Cin, True, M, width, Cin, stats=True)
@@ -246,7 +257,7 @@ class _BottleneckFn(torch.autograd.Function):
             s = down_stride
             xs = x if s == 1 else x[:, :, ::s, ::s].contiguous(memory_format=CL)
             xsr = _rows(xs)
-            Wd = wd.detach().reshape(cout, Cin).to(BF16)
+            Wd = _bf16_weight(wd).reshape(cout, Cin)
             cd, std = gemm(xsr, Cin, True, Wd, Cin, True, M2, cout, Cin, stats=True)
             meand, invd, ssd = lib.bn_stats(cd, std, gd, bd, bnd.running_mean, bnd.running_var,
                                             _bn_momentum(bnd), bnd.eps)
@@ -279,8 +290,10 @@ class _BottleneckFn(torch.autograd.Function):
         dr = _rows(dout.to(BF16).contiguous(memory_format=CL))
         # BN3 (+ shortcut) backward, ReLU mask from the forward's 1-bit bitmap
         o3 = _bn_grad_outs(g3p, b3p)
-        dc3, dg3, db3, dres = lib.bn_bwd(dr, c3, None, g3, mean3, inv3, None, True, True, True,
-                                         bits3, o3[0], o3[1])
+        # (the shortcut gradient dy·[out>0] is never materialised: its consumers read dy and
+        # the bitmap — the dx GEMM as a masked addend, the shortcut BN through its ReLU mode)
+        dc3, dg3, db3, _ = lib.bn_bwd(dr, c3, None, g3, mean3, inv3, None, True, True, False,
+                                      bits3, o3[0], o3[1])
         grads = {}
         grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
         # conv3: weight gradient with BN2-apply recomputed in the B prologue, into the arena
@@ -320,8 +333,8 @@ class _BottleneckFn(torch.autograd.Function):
             xsr, cd, Wd, gd, meand, invd = saved[20:]
             s = ctx.down_stride
             od = _bn_grad_outs(gdp, bdp)
-            dcd, dgd, dbd, _ = lib.bn_bwd(dres, cd, None, gd, meand, invd, None, True, False,
-                                          False, None, od[0], od[1])
+            dcd, dgd, dbd, _ = lib.bn_bwd(dr, cd, None, gd, meand, invd, None, True, True,
+                                          False, bits3, od[0], od[1])
             grads["gd"], grads["bd"] = _finish_bn(gdp, bdp, dgd, dbd, od)
             dstd, dd = _wgrad_target(wd, (cout, Cin))
             gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2, out_bf16=False, out=dstd,
@@ -335,7 +348,8 @@ class _BottleneckFn(torch.autograd.Function):
                 dxv = dx.view(N, H, W, Cin)
                 dxv[:, ::s, ::s, :] += dxs.view(N2, H2, W2_, Cin)
         else:
-            dx, _ = gemm(dc1, width, True, W1, Cin, False, M, Cin, width, addend=dres)
+            dx, _ = gemm(dc1, width, True, W1, Cin, False, M, Cin, width, addend=dr,
+                         addend_bits=bits3)
         dxn = _nchw(dx, N, H, W)
         return (dxn, grads["w1"], grads["g1"], grads["b1"], grads["w2"], grads["g2"], grads["b2"],
                 grads["w3"], grads["g3"], grads["b3"], grads.get("wd"), grads.get("gd"),

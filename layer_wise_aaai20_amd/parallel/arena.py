@@ -125,6 +125,28 @@ class GradArena:
             v.copy_(s.param.data)
             s.param.data = v
 
+    # ------------------------------------------------------------------ bf16 weight mirror
+    def refresh_bf16(self) -> None:
+        """One cast of the whole flat fp32 parameter buffer into a bf16 mirror (instead of one
+        cast kernel per layer per forward). ``bf16_of(p)`` hands out views of it while the
+        parameters are unchanged since the refresh — tracked by version counters: the flat
+        buffer's (the fused optimizer writes through it) and each parameter's own (in-place
+        updates such as ``load_state_dict``), so a stale mirror is never used."""
+        if self.param_buf is None:
+            return
+        if getattr(self, "param_bf16", None) is None:
+            self.param_bf16 = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+            for s in self.segments:
+                view = _dense_strided_view(self.param_bf16, s.offset, s.param.data)
+                s.param._lw_bf16_of = (lambda v=view, s=s: v if self.bf16_valid(s) else None)
+        self.param_bf16.copy_(self.param_buf)
+        self._bf16_version = self.param_buf._version
+        self._bf16_pver = [s.param._version for s in self.segments]
+
+    def bf16_valid(self, seg: Segment) -> bool:
+        return (getattr(self, "_bf16_version", None) == self.param_buf._version and
+                self._bf16_pver[seg.index] == seg.param._version)
+
     def layer_sizes(self) -> List[int]:
         return [s.numel for s in self.segments]
 

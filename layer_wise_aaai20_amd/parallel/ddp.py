@@ -29,9 +29,11 @@ class CompressedDDP(nn.Module):
                  first_bucket_mb: Optional[float] = None, process_group=None,
                  broadcast_buffers: bool = True, wire: str = "auto", seed: int = 2147483647,
                  flat_params: bool = True, check_reduction: bool = True, device_ids=None,
-                 output_device=None, dim: int = 0, timing: bool = False):
+                 output_device=None, dim: int = 0, timing: bool = False,
+                 bf16_weights: bool = True):
         super().__init__()
         self.module = module
+        self.bf16_weights = bf16_weights and flat_params
         self.process_group = process_group
         self.broadcast_buffers = broadcast_buffers
         self.check_reduction = check_reduction
@@ -99,6 +101,8 @@ class CompressedDDP(nn.Module):
         if self.broadcast_buffers and self._buffers_list:
             comm.broadcast_coalesced(self._buffers_list, 0, self.process_group)
         self.engine.begin_step()
+        if self.bf16_weights and self.engine.arena.device.type == "cuda":
+            self.engine.arena.refresh_bf16()
         return self.module(*inputs, **kwargs)
 
     def zero_grad(self, set_to_none: bool = True) -> None:

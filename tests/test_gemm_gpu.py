@@ -150,3 +150,24 @@ def test_stream_gemm_matches_tiled(K, tile):
     D, _ = lib.gemm_ex(x, K, True, wt, N, False, M, N, K, None, False, 1, True, tile, None, None,
                        True, False, None, add, False, 0)
     torch.testing.assert_close(D, ref2, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 6, 11, 12])
+def test_gemm_masked_addend(tile):
+    """dx = dy·W + dres·[bit]: the ReLU-masked shortcut gradient enters through the epilogue."""
+    lib = G.load()
+    torch.manual_seed(6)
+    M, N, K = 2048, 256, 64
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    wt = torch.randn(K, N, device="cuda").bfloat16()
+    add = torch.randn(M, N, device="cuda").bfloat16()
+    keep = torch.rand(M, N, device="cuda") > 0.4
+    bits = (keep.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda",
+                                                             dtype=torch.uint8)).sum(1)
+    bits = bits.to(torch.uint8)
+    base = lib.gemm_ex(a, K, True, wt, N, False, M, N, K, None, False, 1, True, 1, None, None,
+                       True, False)[0]
+    ref = (base.float() + (add.float() * keep)).bfloat16()
+    D = lib.gemm_ex(a, K, True, wt, N, False, M, N, K, None, False, 1, True, tile, None, None,
+                    True, False, None, add, False, 0, bits)[0]
+    torch.testing.assert_close(D, ref, rtol=0, atol=0)

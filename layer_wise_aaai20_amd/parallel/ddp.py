@@ -33,7 +33,9 @@ class CompressedDDP(nn.Module):
                  bf16_weights: bool = True):
         super().__init__()
         self.module = module
-        self.bf16_weights = bf16_weights and flat_params
+        import os
+        self.bf16_weights = (bf16_weights and flat_params and
+                             os.environ.get("LWAAAI_BF16_MIRROR", "1") != "0")
         self.process_group = process_group
         self.broadcast_buffers = broadcast_buffers
         self.check_reduction = check_reduction

@@ -35,7 +35,7 @@ def main(path, last=5, verbose=False):
     for c, t in sorted(tot.items(), key=lambda x: -x[1]):
         print(f"  {c:28s} {t / last:8.3f} ms  {100 * t / busy:5.1f}%")
         if verbose:
-            for k, (t2, n2) in sorted(names[c].items(), key=lambda x: -x[1][0])[:6]:
+            for k, (t2, n2) in sorted(names[c].items(), key=lambda x: -x[1][0])[:int(__import__("os").environ.get("TOPK", "14"))]:
                 print(f"      {t2 / last:7.3f}  x{n2 // last:<4d} {k}")
 
 

@@ -75,6 +75,9 @@ def broadcast_coalesced(tensors, src: int = 0, group=None) -> None:
     for t in tensors:
         by_dtype.setdefault((t.dtype, t.device), []).append(t)
     for (_, _), ts in by_dtype.items():
+        if len(ts) == 1 and ts[0].is_contiguous():      # already flat: in place, no copies
+            dist.broadcast(ts[0].detach(), src=src, group=group)
+            continue
         flat = torch.cat([t.detach().reshape(-1) for t in ts])
         dist.broadcast(flat, src=src, group=group)
         off = 0

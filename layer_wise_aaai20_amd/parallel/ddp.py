@@ -55,11 +55,41 @@ class CompressedDDP(nn.Module):
                                      first_bucket_mb=first_bucket_mb, wire=wire, seed=seed,
                                      process_group=process_group, flat_params=flat_params,
                                      timing=timing)
-        self._buffers_list = [b for b in module.buffers() if b.is_floating_point() or
-                              b.dtype in (torch.int64, torch.int32)]
+        self._buffers_list = self._flatten_buffers(module) if broadcast_buffers else []
         self._hooks = []
         self._register_hooks()
         self._callback_queued = False
+
+    @staticmethod
+    def _flatten_buffers(module: nn.Module):
+        """Re-point every floating-point buffer (BN running statistics) at a view of one flat
+        tensor per (dtype, device), so the per-forward buffer broadcast (``ddp.py:361-386``) is a
+        single in-place collective with no gather/scatter copies. Integer buffers already shared
+        through a flat base (``share_bn_counters``) are broadcast via that base."""
+        groups, ints, seen = {}, [], set()
+        for mod in module.modules():
+            for name, b in mod._buffers.items():
+                if b is None:
+                    continue
+                if b.is_floating_point():
+                    groups.setdefault((b.dtype, b.device), []).append((mod, name, b))
+                elif b.dtype in (torch.int64, torch.int32):
+                    base = b._base if b._base is not None else b
+                    if id(base) not in seen:
+                        seen.add(id(base))
+                        ints.append(base)
+        flats = []
+        for (dtype, dev), items in groups.items():
+            flat = torch.empty(sum(b.numel() for _, _, b in items), dtype=dtype, device=dev)
+            off = 0
+            for mod, name, b in items:
+                n = b.numel()
+                v = flat[off:off + n].view_as(b)
+                v.copy_(b)
+                mod._buffers[name] = v
+                off += n
+            flats.append(flat)
+        return flats + ints
 
     # ------------------------------------------------------------------ hooks
     def _register_hooks(self) -> None:

@@ -17,6 +17,7 @@ flat arena. No gradient is ever reduced twice.
 """
 from __future__ import annotations
 
+import contextlib
 import time
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
@@ -61,7 +62,8 @@ class GradSyncEngine:
                  qstates=None, error_feedback: bool = False, bucket_cap_mb: float = 25.0,
                  first_bucket_mb: Optional[float] = None, wire: str = "auto",
                  seed: int = 2147483647, process_group=None, flat_params: bool = False,
-                 world_size: Optional[int] = None, timing: bool = False):
+                 world_size: Optional[int] = None, timing: bool = False,
+                 overlap_compress: bool = True):
         self.mode = canonical_mode(mode)
         self.method = ref.canonical_method(method) if self.mode != "none" else "none"
         self.pg = process_group
@@ -99,6 +101,11 @@ class GradSyncEngine:
         self.stats = SyncStats(dense_bytes=self.arena.numel * 4, buckets=len(self.buckets))
         self.timing = timing and self.device.type == "cuda"
         self.timings: List[dict] = []
+        # compression + collective launch run on a side HIP stream, ordered after the bucket's
+        # last gradient by an event, so they overlap the rest of the backward pass; the compute
+        # stream waits on a second event only when it decodes in finish()
+        self._side = (torch.cuda.Stream(device=self.device)
+                      if overlap_compress and self.device.type == "cuda" else None)
         self._reset_state()
         self.all_reduced_last = True
         self.verify_plan()
@@ -171,17 +178,27 @@ class GradSyncEngine:
         codec = self.codecs[bi]
         g = self.arena.grad[b.start:b.end]
         e = self.ef[b.start:b.end] if self.ef is not None else None
-        t0 = self._event() if self.timing else None
-        send = codec.compress(g, e, self.step)
-        t1 = self._event() if self.timing else None
-        self._payload += codec.last_payload_bytes
-        if codec.collective == "all_reduce":
-            work = comm.all_reduce(send, self.pg)
-            recv = None
-        else:
-            recv = codec.recv_buffer(send)
-            work = comm.all_gather(recv, send, self.pg)
-        self._pending.append((bi, work, send, recv, (t0, t1)))
+        side = self._side
+        if side is not None:
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(self.device))
+            side.wait_event(ready)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            t0 = self._event() if self.timing else None
+            send = codec.compress(g, e, self.step)
+            t1 = self._event() if self.timing else None
+            self._payload += codec.last_payload_bytes
+            if codec.collective == "all_reduce":
+                work = comm.all_reduce(send, self.pg)
+                recv = None
+            else:
+                recv = codec.recv_buffer(send)
+                work = comm.all_gather(recv, send, self.pg)
+            done = None
+            if side is not None:
+                done = torch.cuda.Event()
+                done.record(side)
+        self._pending.append((bi, work, send, recv, (t0, t1), done))
 
     def finish(self) -> None:
         """Launch buckets that never became ready (unused params keep zero grads), wait for every
@@ -190,8 +207,14 @@ class GradSyncEngine:
             self._ready[i] = True
         self._launch_in_order()
         rec = []
-        for bi, work, send, recv, (t0, t1) in self._pending:
+        for bi, work, send, recv, (t0, t1), done in self._pending:
             work.wait()
+            if done is not None:                 # decode on the compute stream after the side
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(done)
+                for t in (send, recv):           # allocated on the side stream, used here
+                    if t is not None:
+                        t.record_stream(cur)
             t2 = self._event() if self.timing else None
             b = self.buckets[bi]
             self.codecs[bi].decompress(send, recv, self.arena.grad[b.start:b.end])

@@ -315,7 +315,9 @@ class _BottleneckFn(torch.autograd.Function):
             dc2n, a1n, W2, None, stride, padding, dilation, False, [0, 0], 1,
             [True, True, False])
         if _direct(w2):
-            w2.grad.add_(dW2)
+            # the arena was zeroed at the start of the step and this is the weight's only
+            # contribution: a bf16→fp32 cast-copy instead of a mixed-dtype accumulate
+            w2.grad.copy_(dW2)
             grads["w2"] = _finish_param(w2, None, True)
         else:
             grads["w2"] = dW2.float().contiguous(memory_format=CL)

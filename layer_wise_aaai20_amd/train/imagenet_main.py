@@ -105,6 +105,19 @@ def parse_phases(spec: str):
         return ast.literal_eval(spec)
 
 
+def adapt_state_dict(sd: dict, model) -> dict:
+    """Checkpoints written under a DP wrapper carry a ``module.`` key prefix
+    (``train_imagenet_nv.py:663-669``); add or strip it so a checkpoint loads into a wrapped or a
+    bare model alike (e.g. ``--evaluate`` without ``--distributed``)."""
+    want = next(iter(model.state_dict()), "")
+    have = next(iter(sd), "")
+    if want.startswith("module.") and not have.startswith("module."):
+        return {"module." + k: v for k, v in sd.items()}
+    if have.startswith("module.") and not want.startswith("module."):
+        return {k[len("module."):]: v for k, v in sd.items()}
+    return sd
+
+
 def listify(p=None, q=None):
     """``listify`` of train_imagenet_nv.py:691-699 without ``collections.Iterable`` (D9)."""
     if p is None:
@@ -505,10 +518,11 @@ def main(argv=None):
 
     if args.resume:
         ckpt = torch.load(args.resume, map_location=device, weights_only=True)
-        model.load_state_dict(ckpt["state_dict"])
+        model.load_state_dict(adapt_state_dict(ckpt["state_dict"], model))
         args.start_epoch = ckpt["epoch"]
         best_top5 = ckpt["best_top5"]
-        optimizer.load_state_dict(ckpt["optimizer"])
+        if not args.evaluate:            # eval-only needs the weights, not the optimizer state
+            optimizer.load_state_dict(ckpt["optimizer"])
         if "scheduler" in ckpt:
             scheduler.load_state_dict(ckpt["scheduler"])
         if "compression" in ckpt and hasattr(model, "load_compression_state"):

@@ -90,3 +90,15 @@ def test_train_modes_run(tmp_path, compress, method):
     T.main(["synthetic", "--phases", "smoke", "--short-epoch", "--arch", "resnet18",
             "--logdir", str(tmp_path), "-c", compress, "--method", method, "-K", "0.01",
             "--epochs", "1", "--device", "cpu", "--print-freq", "100"])
+
+
+def test_adapt_state_dict_prefix():
+    import torch
+    from layer_wise_aaai20_amd.train.imagenet_main import adapt_state_dict
+    m = torch.nn.Linear(2, 2)
+    wrapped = torch.nn.Module()
+    wrapped.module = torch.nn.Linear(2, 2)
+    sd_wrapped = wrapped.state_dict()
+    assert set(adapt_state_dict(sd_wrapped, m)) == set(m.state_dict())
+    assert set(adapt_state_dict(m.state_dict(), wrapped)) == set(sd_wrapped)
+    m.load_state_dict(adapt_state_dict(sd_wrapped, m))

@@ -11,6 +11,7 @@
 // a finalize kernel folds them in fp64.
 #include "common.h"
 #include "lw_kernels.h"
+#include <cstdlib>
 
 namespace lw {
 
@@ -66,7 +67,7 @@ __device__ __forceinline__ void mask_bits(float d[8], uint32_t bits) {
   for (int k = 0; k < 8; ++k) d[k] = ((bits >> k) & 1u) ? d[k] : 0.f;
 }
 
-template <typename T, int MODE, int RELU>
+template <typename T, int MODE, int RELU, int U>
 __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, const T* __restrict__ dy,
                                                    const T* __restrict__ y,
                                                    const uint8_t* __restrict__ bits,
@@ -94,7 +95,6 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(r0 + rows_per_block, M);
-  constexpr int U = 4;
   if (active) {
     const T* xp = x + g * 8;
     const T* dp = dy + g * 8;
@@ -390,10 +390,20 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, c
 }
 
 // ------------------------------------------------------------------------------------------
+// Tuning knobs (read once): rows unrolled per thread in the reduce loop, and the reduce grid size.
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+static int reduce_unroll() {
+  static const int u = env_int("LWAAAI_BN_UNROLL", 4);
+  return u;
+}
+
 static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblocks) {
   const int G = C / 8;
   const int R = BNT / G;
-  const int64_t target = 1024;          // ≈ 4 blocks per CU
+  static const int64_t target = env_int("LWAAAI_BN_BLOCKS", 1024);   // ≈ 4 blocks per CU
   int64_t rpb = (M + target - 1) / target;
   rpb = (rpb + R - 1) / R * R;
   rpb = rpb < R ? R : rpb;
@@ -454,7 +464,8 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
   } else if (nb <= 0) {
     int64_t rpb;
     reduce_geometry(a.M, a.C, rpb, nb);
-    hipLaunchKernelGGL((k_bn_reduce<T, 0, 0>), dim3(nb), dim3(BNT), 0, st, static_cast<const T*>(a.x),
+    auto kern = reduce_unroll() == 8 ? k_bn_reduce<T, 0, 0, 8> : k_bn_reduce<T, 0, 0, 4>;
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(BNT), 0, st, static_cast<const T*>(a.x),
                        (const T*)nullptr, (const T*)nullptr, (const uint8_t*)nullptr,
                        (const float*)nullptr,
                        (const float*)nullptr, (const float*)nullptr, a.M, a.C, rpb, a.partial);
@@ -484,7 +495,8 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   // relu mask: recompute from x when the forward had no residual (saves reading y)
   const int rmode = !a.relu ? 0 : (a.bits ? 3 : (a.scale ? 2 : 1));
 #define LW_RED(R)                                                                                \
-  hipLaunchKernelGGL((k_bn_reduce<T, 1, R>), dim3(nb), dim3(BNT), 0, st, x, dy, y, a.bits, a.mean, \
+  hipLaunchKernelGGL((reduce_unroll() == 8 ? k_bn_reduce<T, 1, R, 8> : k_bn_reduce<T, 1, R, 4>), \
+                     dim3(nb), dim3(BNT), 0, st, x, dy, y, a.bits, a.mean, \
                      a.scale, a.shift, a.M, a.C, rpb, a.partial)
   if (rmode == 0) LW_RED(0); else if (rmode == 1) LW_RED(1); else if (rmode == 2) LW_RED(2);
   else LW_RED(3);

@@ -123,6 +123,24 @@ def stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro, pro_on_a, add, split
     return tuple(t for t in STREAM if not (K == 256 and t == 13))
 
 
+BLAS = -1                           # tuner candidate: the vendor library (hipBLASLt)
+
+
+def _mat(P, ld, kc, rows, K):
+    """Logical [rows, K] matrix over a packed operand: K-contiguous ``P[r*ld + k]`` or
+    row-contiguous ``P[k*ld + r]`` (a transposed view, no copy)."""
+    if kc:
+        return P.view(-1)[: (rows - 1) * ld + K].as_strided((rows, K), (ld, 1))
+    return P.view(-1)[: (K - 1) * ld + rows].as_strided((rows, K), (1, ld))
+
+
+def blas_ok(out_bf16, stats, pro, add, accumulate, split_k, out, ldc, N) -> bool:
+    """Plain problems only (no fused prologue / epilogue): there the library GEMM is a fair
+    candidate for the tuner to time against the hand-written kernels."""
+    return (out_bf16 and not stats and not pro and not add and not accumulate and not split_k
+            and out is None and ldc in (0, N))
+
+
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro=None,
          pro_on_a=True, out=None, addend=None, accumulate=False, ldc=0, split_k=False,
          addend_bits=None):
@@ -139,13 +157,24 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
     key = (M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a, split_k,
            addend is not None)
 
+    def blas():
+        # B(k, n): [N][ldb] K-contiguous -> Bᵀ view, or [K][ldb] N-contiguous
+        Bm = _mat(B, ldb, b_kc, N, K).t()
+        return torch.mm(_mat(A, lda, a_kc, M, K), Bm), torch.empty(0, device=A.device)
+
     def run(tile):
+        if tile == BLAS:
+            return blas()
         lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile), out_bf16,
-                    tile, ps, ph, pro_on_a, stats, None, addend if tile in STREAM else None,
-                    False, 0, addend_bits if tile in STREAM else None)
-    tile = TUNER.pick(key, run, TILES + stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats,
-                                                     pro is not None, pro_on_a,
-                                                     addend is not None, split_k, accumulate))
+                    tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits)
+    cands = TILES + stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a,
+                                 addend is not None, split_k, accumulate)
+    if blas_ok(out_bf16, stats, pro is not None, addend is not None, accumulate, split_k, out,
+               ldc, N) and A.dtype == torch.bfloat16:
+        cands = cands + (BLAS,)
+    tile = TUNER.pick(key, run, cands)
+    if tile == BLAS:
+        return blas()
     return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile),
                        out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc,
                        addend_bits)

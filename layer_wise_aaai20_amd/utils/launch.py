@@ -71,6 +71,50 @@ def format_env(**kw) -> str:
     return " ".join(f"{k}={v}" for k, v in kw.items())
 
 
+def format_env_export(**kw) -> str:
+    """``export K=V`` chain for shell command prefixes (``util.format_env_export``)."""
+    return "; ".join(f"export {k}={v}" for k, v in kw.items())
+
+
+def get_nccl_params(num_tasks: int, num_gpus: int, simple: bool = False) -> str:
+    """Collective tuning environment as one ``K=V ...`` string (``train.py:159-187``); RCCL reads
+    the same variable names."""
+    return format_env(**ring_env(num_tasks, num_gpus, simple))
+
+
+def setup_mpi(hosts: Sequence[str], slots: int, path: str = "hosts.slots",
+              env: Optional[Dict[str, str]] = None) -> str:
+    """Write an MPI hostfile (one ``host slots=N`` line per node, ``util.setup_mpi``) and return the
+    ``mpirun`` prefix that exports the rank variables the worker reads (``train.py:412-416``).
+    Passwordless ssh between the nodes is assumed to be configured by the cluster (the reference's
+    key exchange is AWS-specific)."""
+    with open(path, "w") as f:
+        for h in hosts:
+            f.write(f"{h} slots={slots}\n")
+    exports = " ".join(f"-x {k}={v}" for k, v in (env or {}).items())
+    n = len(hosts) * slots
+    return (f"mpirun -n {n} -N {slots} --hostfile {path} --bind-to none {exports} "
+            "-x MASTER_ADDR -x MASTER_PORT").strip()
+
+
+def run_parallel(fns: Sequence, max_workers: Optional[int] = None) -> list:
+    """Run callables concurrently and return their results in order (``util.run_parallel``)."""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=max_workers or max(1, len(fns))) as ex:
+        return list(ex.map(lambda f: f(), fns))
+
+
+def mount_imagenet(path: str, required=("train", "validation")) -> str:
+    """Check that an ImageNet-layout tree is present on this node (the reference attached and
+    mounted an EBS volume per task, ``train.py:227-287``; MI355X nodes read local NVMe / shared
+    storage — stage it with ``IMAGENET/tools/replicate_imagenet.py``)."""
+    missing = [d for d in required if not os.path.isdir(os.path.join(path, d))]
+    if missing:
+        raise FileNotFoundError(f"{path} lacks {missing}; stage the dataset first "
+                                "(IMAGENET/tools/replicate_imagenet.py)")
+    return path
+
+
 # ----------------------------------------------------------------------------- ring orders
 def build_ring_order(machine_order: Sequence[int], gpu_order: Sequence[int]) -> str:
     gpus = list(gpu_order)

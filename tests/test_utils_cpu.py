@@ -137,3 +137,19 @@ def test_extension_builds_for_gfx950():
     from layer_wise_aaai20_amd.ops import _ext
     ops = _ext.load(build_if_missing=False)
     assert ops.workspace_bytes(1, 1, 1) > 0
+
+
+def test_launch_env_and_mpi_helpers(tmp_path):
+    from layer_wise_aaai20_amd.utils import launch as L
+    assert L.format_env_export(A=1, B="x") == "export A=1; export B=x"
+    assert "NCCL_RINGS=" in L.get_nccl_params(2, 8)
+    cmd = L.setup_mpi(["h1", "h2"], 8, path=str(tmp_path / "hosts.slots"), env={"K": "v"})
+    assert (tmp_path / "hosts.slots").read_text() == "h1 slots=8\nh2 slots=8\n"
+    assert cmd.startswith("mpirun -n 16 -N 8") and "-x K=v" in cmd
+    assert L.run_parallel([lambda: 1, lambda: 2]) == [1, 2]
+    (tmp_path / "d" / "train").mkdir(parents=True)
+    (tmp_path / "d" / "validation").mkdir()
+    assert L.mount_imagenet(str(tmp_path / "d")) == str(tmp_path / "d")
+    import pytest
+    with pytest.raises(FileNotFoundError):
+        L.mount_imagenet(str(tmp_path))

@@ -623,6 +623,9 @@ static void stem_geom(const Tensor& x, int64_t k, int64_t s, int64_t p, lw::Stem
   a.k = (int)k; a.s = (int)s; a.p = (int)p;
   a.Ho = (int)((a.H + 2 * p - k) / s + 1);
   a.Wo = (int)((a.W + 2 * p - k) / s + 1);
+  // the kernels decompose flat pixel / output indices in 32-bit arithmetic
+  TORCH_CHECK((int64_t)a.N * a.H * a.W < (1LL << 31) &&
+              (int64_t)a.N * a.Ho * a.Wo * (a.C / 8) < (1LL << 31), "stem pool: tensor too large");
 }
 
 std::tuple<Tensor, Tensor> stem_pool_fwd(Tensor x, Tensor scale_shift, int64_t k, int64_t s,

@@ -9,6 +9,8 @@
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
+#include <algorithm>
+
 #include "lw_kernels.h"
 
 namespace {
@@ -561,6 +563,160 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
                              c10::nullopt, false, 0, c10::nullopt));
 }
 
+// ---------------------------------------------------------------- implicit-GEMM convolution
+// G: the gathered NHWC bf16 tensor; Op: the other GEMM operand — the packed weights (row-gather
+// modes 1/2: [N][K] for the forward, b_kcontig, or per-class [K_c][N] slabs for the data
+// gradient) or dY [pixels][M] (weight-gradient modes 3/4). geom = [Nb, Hin, Win, C, sh, sw, dh,
+// dw, Hout, Wout, osy, osx, nclass, then per class TR, TS, oh, ow, Hg, Wg, py, px, K, b_off].
+// Every index the kernels can form is checked here against the tensors' sizes.
+std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vector<int64_t> geom,
+                                   int64_t N, int64_t tile, int64_t splits, bool out_bf16,
+                                   c10::optional<Tensor> pro_scale, c10::optional<Tensor> pro_shift,
+                                   bool want_stats, c10::optional<Tensor> out, bool accumulate,
+                                   int64_t ldc, bool b_kcontig, int64_t ldb) {
+  const c10::DeviceGuard guard(G.device());
+  TORCH_CHECK(G.is_cuda() && Op.is_cuda(), "conv needs GPU tensors");
+  check_dtype(G, at::kBFloat16, "gathered tensor");
+  check_dtype(Op, at::kBFloat16, "operand");
+  TORCH_CHECK(G.is_contiguous() || G.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "gathered tensor must be dense NHWC");
+  TORCH_CHECK(Op.is_contiguous() || Op.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "operand must be dense (dY channels_last)");
+  TORCH_CHECK(mode >= lw::CV_A && mode <= lw::CV_B4, "conv mode");
+  TORCH_CHECK(lw::conv_tile_ok((int)mode, (int)tile), "tile ", tile, " not built for conv mode ",
+              mode);
+  TORCH_CHECK(geom.size() >= 13, "geom too short");
+  const int64_t Nb = geom[0];
+  lw::ConvGeomHost h{};
+  h.Hin = (int)geom[1]; h.Win = (int)geom[2]; h.C = (int)geom[3];
+  h.sh = (int)geom[4]; h.sw = (int)geom[5]; h.dh = (int)geom[6]; h.dw = (int)geom[7];
+  h.Hout = (int)geom[8]; h.Wout = (int)geom[9]; h.osy = (int)geom[10]; h.osx = (int)geom[11];
+  h.nclass = (int)geom[12];
+  TORCH_CHECK(h.nclass >= 1 && h.nclass <= 4 && geom.size() == 13 + 10 * (size_t)h.nclass,
+              "geom: 1..4 classes of 10 ints");
+  TORCH_CHECK(std::abs(h.dh) == 1 && std::abs(h.dw) == 1 && h.sh >= 1 && h.sw >= 1 &&
+              h.osy >= 1 && h.osx >= 1, "geom: strides / directions");
+  const bool ga = mode == lw::CV_A || mode == lw::CV_A4;
+  const bool c4 = mode == lw::CV_A4 || mode == lw::CV_B4;
+  TORCH_CHECK(c4 ? h.C == 4 : (h.C > 0 && h.C % 8 == 0),
+              c4 ? "4-channel mode needs C == 4" : "conv needs C % 8 == 0");
+  TORCH_CHECK(G.numel() >= Nb * h.Hin * h.Win * h.C, "gathered tensor smaller than geom");
+  TORCH_CHECK(Nb * h.Hin * h.Win < (1LL << 31), "gathered tensor too large");
+  check_aligned16(G.data_ptr(), "gathered tensor");
+  check_aligned16(Op.data_ptr(), "operand");
+  int64_t Mmax = 0;
+  for (int i = 0; i < h.nclass; ++i) {
+    const int64_t* c = &geom[13 + 10 * i];
+    h.TR[i] = (int)c[0]; h.TS[i] = (int)c[1]; h.oh[i] = (int)c[2]; h.ow[i] = (int)c[3];
+    h.Hg[i] = (int)c[4]; h.Wg[i] = (int)c[5]; h.py[i] = (int)c[6]; h.px[i] = (int)c[7];
+    h.K[i] = (int)c[8]; h.b_off[i] = c[9];
+    TORCH_CHECK(h.TR[i] >= 0 && h.TS[i] >= 1 && h.Hg[i] >= 1 && h.Wg[i] >= 1, "class geometry");
+    TORCH_CHECK(!c4 || h.TS[i] % 2 == 0, "4-channel mode needs an even tap count along w");
+    TORCH_CHECK((int64_t)h.K[i] == (int64_t)h.TR[i] * h.TS[i] * h.C || (!ga),
+                "class K must be taps * C");
+    const int64_t Mc = Nb * h.Hg[i] * h.Wg[i];
+    TORCH_CHECK(Mc < (1LL << 24), "pixel count beyond the fp32 fast divide");
+    h.M[i] = (int)Mc;
+    Mmax = std::max(Mmax, Mc);
+    if (h.osy > 1 || h.osx > 1 || h.nclass > 1) {
+      TORCH_CHECK((int64_t)(h.Hg[i] - 1) * h.osy + h.py[i] < h.Hout &&
+                  (int64_t)(h.Wg[i] - 1) * h.osx + h.px[i] < h.Wout && h.py[i] >= 0 &&
+                  h.px[i] >= 0, "class output map outside the output grid");
+    }
+  }
+  TORCH_CHECK(N > 0 && N % 8 == 0, "conv GEMM N must be a positive multiple of 8");
+  lw::GemmArgs g{};
+  g.tile = (int)tile;
+  g.out_bf16 = out_bf16;
+  g.accumulate = accumulate;
+  g.N = (int)N;
+  Tensor C;
+  if (ga) {
+    TORCH_CHECK(out_bf16 && !accumulate, "row-gather convs write bf16");
+    TORCH_CHECK(h.nclass == 1 || !b_kcontig, "parity classes are a data-gradient feature");
+    for (int i = 0; i < h.nclass; ++i) {
+      const int64_t need = b_kcontig ? h.b_off[i] + (N - 1) * ldb + h.K[i]
+                                     : h.b_off[i] + (int64_t)(h.K[i] - 1) * ldb + N;
+      TORCH_CHECK(h.K[i] == 0 || Op.numel() >= need, "weight operand too small for class ", i);
+      TORCH_CHECK(h.b_off[i] % 8 == 0, "class weight offset alignment");
+    }
+    TORCH_CHECK(ldb % 8 == 0 && ldb >= (b_kcontig ? h.K[0] : N), "ldb");
+    g.M = (int)Mmax;
+    g.K = *std::max_element(h.K, h.K + h.nclass);   // one K range per workgroup: the largest
+    g.A = ptr<uint16_t>(G);
+    g.lda = h.C;
+    g.a_kcontig = true;
+    g.B = ptr<uint16_t>(Op);
+    g.ldb = ldb;
+    g.b_kcontig = b_kcontig;
+    g.splits = 1;
+    if (h.nclass == 1 && h.osy == 1 && h.osx == 1)
+      TORCH_CHECK(h.M[0] <= Nb * h.Hout * h.Wout, "rows beyond the output grid");
+  } else {
+    TORCH_CHECK(h.nclass == 1, "weight gradients take one class");
+    TORCH_CHECK(!out_bf16, "weight gradients are fp32");
+    TORCH_CHECK(N == (int64_t)h.TR[0] * h.TS[0] * h.C, "wgrad N must be taps * C");
+    g.M = (int)(ldb);                          // ldb carries Co (= M) for the weight gradient
+    TORCH_CHECK(g.M > 0 && g.M % 8 == 0, "wgrad: Co must be a multiple of 8");
+    g.K = h.M[0];                              // reduction over the output pixels
+    TORCH_CHECK(Op.numel() >= (int64_t)g.K * g.M, "dY smaller than pixels x Co");
+    g.A = ptr<uint16_t>(Op);
+    g.lda = g.M;
+    g.a_kcontig = false;
+    g.B = ptr<uint16_t>(G);
+    g.ldb = 0;
+    g.b_kcontig = false;
+    g.splits = (int)std::max<int64_t>(splits, 1);
+  }
+  if (ldc <= 0) ldc = N;
+  TORCH_CHECK(ldc >= N && (out_bf16 ? ldc % 8 == 0 : ldc % 4 == 0), "ldc");
+  const int64_t out_rows = ga ? Nb * h.Hout * h.Wout : g.M;
+  const auto odt = out_bf16 ? at::kBFloat16 : at::kFloat;
+  if (out.has_value() && out->defined()) {
+    C = *out;
+    TORCH_CHECK(C.is_cuda() && C.scalar_type() == odt, "out dtype");
+    TORCH_CHECK(C.is_contiguous() || C.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "out must be dense");
+    TORCH_CHECK(C.numel() >= (out_rows - 1) * ldc + N, "out too small");
+    check_aligned16(C.data_ptr(), "out");
+  } else {
+    TORCH_CHECK(!accumulate, "accumulate needs an out tensor");
+    C = at::empty({out_rows, ldc}, G.options().dtype(odt));
+    if (ga && (h.nclass > 1 || h.osy > 1 || h.osx > 1)) C.zero_();   // pixels no class covers
+  }
+  g.C = C.data_ptr();
+  g.ldc = ldc;
+  if (pro_scale.has_value() && pro_scale->defined()) {
+    TORCH_CHECK(!c4 && (ga ? b_kcontig : true), "BN prologue: forward or weight gradient, C % 8");
+    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined(), "prologue needs scale and shift");
+    for (const Tensor* t : {&*pro_scale, &*pro_shift}) {
+      check_dtype(*t, at::kFloat, "prologue");
+      TORCH_CHECK(t->numel() >= h.C && t->is_contiguous(), "prologue vector size");
+      check_aligned16(t->data_ptr(), "prologue");
+    }
+    g.pro_scale = ptr<float>(*pro_scale);
+    g.pro_shift = ptr<float>(*pro_shift);
+    g.pro_on_a = ga;
+  }
+  const int zs = ga ? 1 : lw::conv_splits_used(g);
+  Tensor partial, stats;
+  if (zs > 1) {
+    partial = at::empty({(int64_t)zs * g.M * N}, G.options().dtype(at::kFloat));
+    g.partial = ptr<float>(partial);
+  }
+  if (want_stats) {
+    TORCH_CHECK(ga && b_kcontig && h.nclass == 1, "column statistics: forward convs only");
+    int bm, bn, bk;
+    lw::gemm_tile_shape(g.tile, bm, bn, bk);
+    stats = at::empty({(g.M + bm - 1) / bm, 2, N}, G.options().dtype(at::kFloat));
+    g.stats = ptr<float>(stats);
+  } else {
+    stats = at::empty({0}, G.options().dtype(at::kFloat));
+  }
+  lw::conv_gemm(g, h, (int)mode, cur_stream());
+  return {C, stats};
+}
+
 // ---------------------------------------------------------------- BN pieces for fused blocks
 // Batch statistics of x ([M, C] / channels_last), or — with `stats` [2, C, nb] from a GEMM's
 // column-statistics epilogue — only the finalize. Returns (mean, invstd, scale_shift[2C]).
@@ -783,6 +939,10 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor? addend_bits=None) "
       "-> (Tensor, Tensor)");
   m.def(
+      "conv_ex(Tensor G, Tensor Op, int mode, int[] geom, int N, int tile, int splits, "
+      "bool out_bf16, Tensor? pro_scale, Tensor? pro_shift, bool want_stats, Tensor(a!)? out, "
+      "bool accumulate, int ldc, bool b_kcontig, int ldb) -> (Tensor, Tensor)");
+  m.def(
       "bn_stats(Tensor x, Tensor? stats, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
       "Tensor(b!)? running_var, float momentum, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? res, Tensor? res_scale_shift, bool relu, "
@@ -808,6 +968,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("bn_bwd", &bn_bwd);
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);
+  m.impl("conv_ex", &conv_ex);
   m.impl("bn_stats", &bn_stats);
   m.impl("bn_apply", &bn_apply);
   m.impl("stem_pool_fwd", &stem_pool_fwd);

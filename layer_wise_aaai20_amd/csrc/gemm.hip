@@ -26,495 +26,10 @@
 //  * split-K (EPI_PARTIAL) writes fp32 slabs that a second kernel reduces in a fixed order
 //    (deterministic) and pushes through the same epilogue.
 #include "common.h"
-#include "lw_kernels.h"
+#include "gemm_core.h"
 
 namespace lw {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short i16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int GT = 256;
-constexpr int PAD = 8;                   // bf16 elements of padding per LDS row
-enum { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_STATS = 2 };
-enum { PRO_NONE = 0, PRO_A = 1, PRO_B = 2 };
-
-// f32 -> bf16, round to nearest even: a plain cast, which hipcc lowers to the gfx950 hardware
-// conversion v_cvt_pk_bf16_f32 (NaN stays NaN), instead of integer bit arithmetic.
-__device__ __forceinline__ uint16_t bf16_rne(float f) {
-  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
-}
-__device__ __forceinline__ float bf16_round(float f) { return __uint_as_float((uint32_t)bf16_rne(f) << 16); }
-
-// bf16 + bf16 -> bf16 per element (fp32 add, one rounding): the same arithmetic as a separate
-// elementwise add of two bf16 tensors, so fusing the residual-gradient add changes no bits.
-__device__ __forceinline__ uint4 add_bf16x8(uint4 a, uint4 b) {
-  const uint32_t x[4] = {a.x, a.y, a.z, a.w}, y[4] = {b.x, b.y, b.z, b.w};
-  uint32_t w[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float lo = __uint_as_float(x[k] << 16) + __uint_as_float(y[k] << 16);
-    const float hi = __uint_as_float(x[k] & 0xffff0000u) + __uint_as_float(y[k] & 0xffff0000u);
-    w[k] = (uint32_t)bf16_rne(lo) | ((uint32_t)bf16_rne(hi) << 16);
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// 8 addend values of a chunk, zeroed where the ReLU bitmap (bits of the chunk's first element,
-// chunk-aligned) is clear.
-__device__ __forceinline__ uint4 masked_addend8(const uint16_t* __restrict__ add,
-                                                const uint8_t* __restrict__ bits, int64_t e) {
-  uint4 a = *reinterpret_cast<const uint4*>(add + e);
-  if (bits) {
-    const uint32_t b = bits[e >> 3];
-    const uint32_t m0 = ((b & 1u) ? 0xffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u);
-    const uint32_t m1 = ((b & 4u) ? 0xffffu : 0u) | ((b & 8u) ? 0xffff0000u : 0u);
-    const uint32_t m2 = ((b & 16u) ? 0xffffu : 0u) | ((b & 32u) ? 0xffff0000u : 0u);
-    const uint32_t m3 = ((b & 64u) ? 0xffffu : 0u) | ((b & 128u) ? 0xffff0000u : 0u);
-    a = make_uint4(a.x & m0, a.y & m1, a.z & m2, a.w & m3);
-  }
-  return a;
-}
-
-__device__ __forceinline__ float masked_addend1(const uint16_t* __restrict__ add,
-                                                const uint8_t* __restrict__ bits, int64_t e) {
-  if (bits && !((bits[e >> 3] >> (e & 7)) & 1u)) return 0.f;
-  return __uint_as_float((uint32_t)add[e] << 16);
-}
-
-// R = extent of the tile along m (A) or n (B). KC tiles are stored [R][BK+PAD], the others
-// [BK][R+PAD]; both are moved as 16-byte chunks of 8 contiguous elements.
-template <int R, int BK, bool KC> struct Tile {
-  static constexpr int LD = KC ? BK + PAD : R + PAD;
-  static constexpr int ELEMS = KC ? R * LD : BK * LD;
-  static constexpr int CPR = KC ? BK / 8 : R / 8;     // chunks per stored row
-  static constexpr int PER_T = R * BK / 8 / GT;       // chunks per thread
-  static_assert(R * BK / 8 % GT == 0, "tile must split evenly over the workgroup");
-};
-
-template <int R, int BK, bool KC>
-__device__ __forceinline__ void chunk_pos(int c, int& rr, int& cc) {
-  using T = Tile<R, BK, KC>;
-  rr = c / T::CPR;
-  cc = c % T::CPR;
-}
-
-// Global -> registers. `cont` returns the contiguous-dimension index of each chunk (k for KC,
-// m/n otherwise) for the prologue; `ok` marks chunks inside the matrix (others are zero).
-template <int R, int BK, bool KC>
-__device__ __forceinline__ void load_tile(const uint16_t* __restrict__ P, int64_t ld, int row0,
-                                          int rows_total, int k0, int kend,
-                                          uint4 (&r)[Tile<R, BK, KC>::PER_T],
-                                          int (&cont)[Tile<R, BK, KC>::PER_T], uint32_t& okmask) {
-  using T = Tile<R, BK, KC>;
-  okmask = 0;
-#pragma unroll
-  for (int h = 0; h < T::PER_T; ++h) {
-    int rr, cc;
-    chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
-    int64_t off;
-    bool ok;
-    if (KC) {
-      const int gr = row0 + rr, gk = k0 + cc * 8;
-      ok = gr < rows_total && gk < kend;
-      off = (int64_t)gr * ld + gk;
-      cont[h] = gk;
-    } else {
-      const int gk = k0 + rr, gr = row0 + cc * 8;
-      ok = gk < kend && gr < rows_total;
-      off = (int64_t)gk * ld + gr;
-      cont[h] = gr;
-    }
-    r[h] = ok ? *reinterpret_cast<const uint4*>(P + off) : make_uint4(0, 0, 0, 0);
-    okmask |= (ok ? 1u : 0u) << h;
-  }
-}
-
-// Prologue coefficients of the 8 channels one thread's chunks cover. Every chunk a thread stages
-// has the same contiguous-dimension offset within the tile (the chunks-per-row count divides the
-// workgroup size), so one set of 8 scale/shift values serves all of them: per K-step for PRO_A
-// (channel = k), once per kernel for PRO_B (channel = n).
-struct Coef8 { float s[8], t[8]; };
-
-__device__ __forceinline__ void load_coef8(Coef8& c, const float* __restrict__ sc,
-                                           const float* __restrict__ sh, int j, int limit) {
-  if (j + 8 <= limit) {
-    const float4 s0 = *reinterpret_cast<const float4*>(sc + j);
-    const float4 s1 = *reinterpret_cast<const float4*>(sc + j + 4);
-    const float4 h0 = *reinterpret_cast<const float4*>(sh + j);
-    const float4 h1 = *reinterpret_cast<const float4*>(sh + j + 4);
-    c.s[0] = s0.x; c.s[1] = s0.y; c.s[2] = s0.z; c.s[3] = s0.w;
-    c.s[4] = s1.x; c.s[5] = s1.y; c.s[6] = s1.z; c.s[7] = s1.w;
-    c.t[0] = h0.x; c.t[1] = h0.y; c.t[2] = h0.z; c.t[3] = h0.w;
-    c.t[4] = h1.x; c.t[5] = h1.y; c.t[6] = h1.z; c.t[7] = h1.w;
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { c.s[k] = 0.f; c.t[k] = 0.f; }
-  }
-}
-
-// relu(v*scale + shift) on the 8 bf16 of a chunk (same fp32 expression and rounding as the
-// BatchNorm apply kernel, so fused and unfused paths agree bit for bit).
-__device__ __forceinline__ uint4 affine_relu8(uint4 v, const Coef8& c) {
-  uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float lo = fmaxf(fmaf(__uint_as_float(w[k] << 16), c.s[2 * k], c.t[2 * k]), 0.f);
-    const float hi = fmaxf(fmaf(__uint_as_float(w[k] & 0xffff0000u), c.s[2 * k + 1], c.t[2 * k + 1]), 0.f);
-    w[k] = (uint32_t)bf16_rne(lo) | ((uint32_t)bf16_rne(hi) << 16);
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-template <int R, int BK, bool KC, bool PRO>
-__device__ __forceinline__ void store_tile(uint16_t* __restrict__ S,
-                                           const uint4 (&r)[Tile<R, BK, KC>::PER_T],
-                                           uint32_t okmask, const Coef8& co) {
-  using T = Tile<R, BK, KC>;
-  static_assert(GT % T::CPR == 0, "chunk column must be constant per thread");
-#pragma unroll
-  for (int h = 0; h < T::PER_T; ++h) {
-    int rr, cc;
-    chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
-    uint4 v = r[h];
-    if (PRO && ((okmask >> h) & 1u)) v = affine_relu8(v, co);
-    *reinterpret_cast<uint4*>(S + rr * T::LD + cc * 8) = v;
-  }
-}
-
-// MFMA operand fragment (8 bf16 along k, k-group g = lane>>4, sub-step s of 32 k) for tile
-// row/col i_base + (lane&15).
-template <int R, int BK, bool KC>
-__device__ __forceinline__ bf16x8 load_frag(const uint16_t* S, int i_base, int s) {
-  using T = Tile<R, BK, KC>;
-  const int l = threadIdx.x & 63;
-  if (KC) {
-    const uint16_t* p = S + (i_base + (l & 15)) * T::LD + 32 * s + 8 * (l >> 4);
-    return *reinterpret_cast<const bf16x8*>(p);
-  } else {
-    const int g = l >> 4, t = l & 15, q = t >> 2, p4 = t & 3;
-    typedef __attribute__((address_space(3))) i16x4 lds_v4;
-    const uint16_t* p0 = S + (32 * s + 8 * g + q) * T::LD + i_base + 4 * p4;
-    const uint16_t* p1 = p0 + 4 * T::LD;
-    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0));
-    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p1));
-    typedef short i16x8 __attribute__((ext_vector_type(8)));
-    const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  }
-}
-
-__device__ __forceinline__ void store_out8(void* C, int64_t off, const float v[8], bool bf) {
-  if (bf) {
-    uint32_t w[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = (uint32_t)bf16_rne(v[2 * k]) | ((uint32_t)bf16_rne(v[2 * k + 1]) << 16);
-    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(C) + off) = make_uint4(w[0], w[1], w[2], w[3]);
-  } else {
-    float* c = static_cast<float*>(C) + off;
-    reinterpret_cast<float4*>(c)[0] = make_float4(v[0], v[1], v[2], v[3]);
-    reinterpret_cast<float4*>(c)[1] = make_float4(v[4], v[5], v[6], v[7]);
-  }
-}
-
-struct GemmK {
-  const uint16_t* A;
-  const uint16_t* B;
-  void* C;
-  float* partial;
-  float* stats;
-  const float* bias;
-  const float* pro_scale;
-  const float* pro_shift;
-  const uint16_t* addend;      // optional bf16 [M][ldc] added to a bf16 output (after rounding)
-  const uint8_t* add_bits;     // optional ReLU bitmap of the addend (1 bit/element, ldc == N):
-                               // the addend enters as addend·[bit] (a BN+ReLU backward's dres)
-  int64_t lda, ldb, ldc;
-  int M, N, K, k_per_split, relu, out_bf16, accumulate;   // accumulate: fp32 C += result
-};
-
-// Workgroup id → (m-tile, n-tile): consecutive ids are dealt round-robin to the 8 XCDs, so remap
-// each XCD's share onto one contiguous range of the row-major tile order.
-__device__ __forceinline__ int xcd_remap(int pid, int total) {
-  const int q = total >> 3, rem = total & 7;
-  const int x = pid & 7, idx = pid >> 3;
-  return x * q + (x < rem ? x : rem) + idx;
-}
-
-template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int PRO>
-__global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
-  using TA = Tile<BM, BK, AKC>;
-  using TB = Tile<BN, BK, BKC>;
-  constexpr int WTM = BM / 2, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
-  constexpr int STAGE = TA::ELEMS + TB::ELEMS;
-  constexpr int LDC = BN + 4;                  // fp32 staging row (≡ 4 dwords mod 64 banks)
-  constexpr int LDH = BN + 16;                 // bf16 staging row (≡ 8 dwords mod 64 banks)
-  constexpr int CS_BYTES = WTM * LDC * 4;
-  constexpr int CH_BYTES = BM * LDH * 2 + 2 * 2 * BN * 4;
-  constexpr int ST_BYTES = 2 * STAGE * 2;
-  constexpr int LDS_BYTES = ST_BYTES > CS_BYTES ? (ST_BYTES > CH_BYTES ? ST_BYTES : CH_BYTES)
-                                                : (CS_BYTES > CH_BYTES ? CS_BYTES : CH_BYTES);
-  static_assert(PRO != PRO_A || AKC, "PRO_A needs a K-contiguous A");
-  static_assert(PRO != PRO_B || !BKC, "PRO_B needs an N-contiguous B");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
-  uint16_t* st = reinterpret_cast<uint16_t*>(lds);
-
-  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int pid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = pid / tiles_n, tn = pid - tm * tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * p.k_per_split;
-  const int kend = min(p.K, kbeg + p.k_per_split);
-  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-  const int wr = w >> 1, wc = w & 1;
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  uint4 ra[TA::PER_T], rb[TB::PER_T];
-  int ca[TA::PER_T], cb[TB::PER_T];
-  uint32_t oka = 0, okb = 0;
-  int cur = 0;
-  Coef8 coA, coB;
-  if (PRO == PRO_B)        // channel n of this thread's B chunks: fixed for the whole kernel
-    load_coef8(coB, p.pro_scale, p.pro_shift, n0 + (threadIdx.x % TB::CPR) * 8, p.N);
-  const int a_koff = (threadIdx.x % TA::CPR) * 8;      // PRO_A: k offset within a K-step
-  if (kbeg < kend) {
-    load_tile<BM, BK, AKC>(p.A, p.lda, m0, p.M, kbeg, kend, ra, ca, oka);
-    load_tile<BN, BK, BKC>(p.B, p.ldb, n0, p.N, kbeg, kend, rb, cb, okb);
-    if (PRO == PRO_A) load_coef8(coA, p.pro_scale, p.pro_shift, kbeg + a_koff, kend);
-    store_tile<BM, BK, AKC, PRO == PRO_A>(st, ra, oka, coA);
-    store_tile<BN, BK, BKC, PRO == PRO_B>(st + TA::ELEMS, rb, okb, coB);
-  }
-  __syncthreads();
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    const bool more = k0 + BK < kend;
-    if (more) {
-      load_tile<BM, BK, AKC>(p.A, p.lda, m0, p.M, k0 + BK, kend, ra, ca, oka);
-      load_tile<BN, BK, BKC>(p.B, p.ldb, n0, p.N, k0 + BK, kend, rb, cb, okb);
-      // next stage's prologue coefficients travel with its tile loads (latency hidden by the
-      // MFMAs below; coA is free: the current stage was normalised when it was staged)
-      if (PRO == PRO_A) load_coef8(coA, p.pro_scale, p.pro_shift, k0 + BK + a_koff, kend);
-    }
-    const uint16_t* As = st + cur * STAGE;
-    const uint16_t* Bs = As + TA::ELEMS;
-#pragma unroll
-    for (int s = 0; s < BK / 32; ++s) {
-      bf16x8 fa[FM], fb[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) fa[i] = load_frag<BM, BK, AKC>(As, wr * WTM + i * 16, s);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = load_frag<BN, BK, BKC>(Bs, wc * WTN + j * 16, s);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
-      uint16_t* nx = st + (cur ^ 1) * STAGE;
-      store_tile<BM, BK, AKC, PRO == PRO_A>(nx, ra, oka, coA);
-      store_tile<BN, BK, BKC, PRO == PRO_B>(nx + TA::ELEMS, rb, okb, coB);
-    }
-    __syncthreads();
-    cur ^= 1;
-  }
-
-  // ---- epilogue. B is the MFMA's first operand, so each accumulator holds Cᵀ: lane l has
-  // C[m = .. + (l&15)][n = .. + 4*(l>>4) + r], r = 0..3 (four consecutive columns of one row).
-  const int lm = l & 15, ln = 4 * (l >> 4);
-  const bool bf_out = EPI != EPI_PARTIAL && p.out_bf16;
-  uint16_t* Ch = reinterpret_cast<uint16_t*>(lds);                  // bf16 tile [BM][LDH]
-  float* red = reinterpret_cast<float*>(lds + BM * LDH * 2);        // stats [2 wave rows][2][BN]
-  if (EPI != EPI_PARTIAL) {
-    // bias / ReLU / rounding in registers; column statistics; bf16 staging of the whole tile
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int nl = wc * WTN + j * 16 + ln;
-      const int n = n0 + nl;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bv[r] = n + r < p.N ? p.bias[n + r] : 0.f;
-      }
-      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int ml = wr * WTM + i * 16 + lm;
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x = acc[i][j][r] + bv[r];
-          if (p.relu) x = fmaxf(x, 0.f);
-          v[r] = x;
-        }
-        if (bf_out) {
-          uint16_t h[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            h[r] = bf16_rne(v[r]);
-            v[r] = __uint_as_float((uint32_t)h[r] << 16);
-          }
-          *reinterpret_cast<uint2*>(Ch + ml * LDH + nl) =
-              make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
-        }
-        if (EPI == EPI_STATS && !bf_out && m0 + ml < p.M) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) { s1[r] += v[r]; s2[r] += v[r] * v[r]; }
-        }
-      }
-      if (EPI == EPI_STATS && !bf_out) {
-        // the 16 rows held by lanes sharing l>>4, fixed butterfly order
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s1[r] += __shfl_xor(s1[r], o, 64);
-            s2[r] += __shfl_xor(s2[r], o, 64);
-          }
-        }
-        if (lm == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            red[(wr * 2 + 0) * BN + nl + r] = s1[r];
-            red[(wr * 2 + 1) * BN + nl + r] = s2[r];
-          }
-        }
-      }
-    }
-  }
-  // Column statistics come from the staged bf16 tile during the store pass: a thread's chunks
-  // all cover the same 8 columns (GT is a multiple of BN/8), so it sums them in registers and
-  // one LDS fold per tile finishes the job (no cross-lane shuffles in the epilogue).
-  static_assert(GT % (BN / 8) == 0, "store chunks must keep their column per thread");
-  float cs1[8], cs2[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { cs1[k] = 0.f; cs2[k] = 0.f; }
-  if (bf_out) {
-    __syncthreads();
-    const bool vec = (p.ldc & 7) == 0;
-    for (int c = threadIdx.x; c < BM * (BN / 8); c += GT) {
-      const int r = c / (BN / 8), cc = (c % (BN / 8)) * 8;
-      const int gm = m0 + r, gn = n0 + cc;
-      if (gm >= p.M || gn >= p.N) continue;
-      const uint16_t* src = Ch + r * LDH + cc;
-      if (EPI == EPI_STATS) {
-        const uint4 q = *reinterpret_cast<const uint4*>(src);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float lo = __uint_as_float(w[k] << 16), hi = __uint_as_float(w[k] & 0xffff0000u);
-          const bool in_lo = gn + 2 * k < p.N, in_hi = gn + 2 * k + 1 < p.N;
-          cs1[2 * k] += in_lo ? lo : 0.f;
-          cs2[2 * k] += in_lo ? lo * lo : 0.f;
-          cs1[2 * k + 1] += in_hi ? hi : 0.f;
-          cs2[2 * k + 1] += in_hi ? hi * hi : 0.f;
-        }
-      }
-      uint16_t* dst = static_cast<uint16_t*>(p.C) + (int64_t)gm * p.ldc + gn;
-      if (vec && gn + 8 <= p.N) {
-        uint4 v = *reinterpret_cast<const uint4*>(src);
-        if (p.addend) v = add_bf16x8(v, masked_addend8(p.addend, p.add_bits, (int64_t)gm * p.ldc + gn));
-        *reinterpret_cast<uint4*>(dst) = v;
-      } else {
-        for (int k = 0; k < 8 && gn + k < p.N; ++k) {
-          uint16_t h = src[k];
-          if (p.addend)
-            h = bf16_rne(__uint_as_float((uint32_t)h << 16) +
-                         masked_addend1(p.addend, p.add_bits, (int64_t)gm * p.ldc + gn + k));
-          dst[k] = h;
-        }
-      }
-    }
-  } else {
-    // fp32 output or split-K slab: two halves through an fp32 staging tile
-    float* Cs = reinterpret_cast<float*>(lds);
-    float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)blockIdx.y * p.M * p.N : nullptr;
-    float* dstbase = EPI == EPI_PARTIAL ? P : static_cast<float*>(p.C);
-    const int64_t ld = EPI == EPI_PARTIAL ? p.N : p.ldc;
-    const bool vec = (p.N & 3) == 0 && (ld & 3) == 0;
-    float statsave[2] = {0.f, 0.f};
-    if (EPI == EPI_STATS) {                      // red[] overlaps Cs: park this thread's column
-      __syncthreads();
-      for (int c = threadIdx.x; c < BN; c += GT) {
-        statsave[0] = red[0 * BN + c] + red[2 * BN + c];
-        statsave[1] = red[1 * BN + c] + red[3 * BN + c];
-      }
-    }
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      __syncthreads();
-      if (wr == half) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            *reinterpret_cast<float4*>(Cs + (i * 16 + lm) * LDC + wc * WTN + j * 16 + ln) =
-                make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      }
-      __syncthreads();
-      const int mb = m0 + half * WTM;
-      for (int c = threadIdx.x; c < WTM * (BN / 4); c += GT) {
-        const int r = c / (BN / 4), cc = (c % (BN / 4)) * 4;
-        const int gm = mb + r, gn = n0 + cc;
-        if (gm >= p.M || gn >= p.N) continue;
-        const float* src = Cs + r * LDC + cc;
-        float* dst = dstbase + (int64_t)gm * ld + gn;
-        const bool acc_in = EPI != EPI_PARTIAL && p.accumulate;
-        if (vec && gn + 4 <= p.N) {
-          float4 v = *reinterpret_cast<const float4*>(src);
-          if (acc_in) {
-            const float4 o = *reinterpret_cast<const float4*>(dst);
-            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
-          }
-          *reinterpret_cast<float4*>(dst) = v;
-        } else {
-          for (int k = 0; k < 4 && gn + k < p.N; ++k) dst[k] = acc_in ? dst[k] + src[k] : src[k];
-        }
-      }
-    }
-    if (EPI == EPI_STATS) {
-      for (int c = threadIdx.x; c < BN; c += GT) {
-        const int n = n0 + c;
-        if (n >= p.N) continue;
-        p.stats[(int64_t)tm * 2 * p.N + n] = statsave[0];
-        p.stats[(int64_t)tm * 2 * p.N + p.N + n] = statsave[1];
-      }
-    }
-    return;
-  }
-  if (EPI == EPI_STATS) {
-    // fold the per-thread column sums: GT/(BN/8) threads share each 8-column group
-    constexpr int G8 = BN / 8, Q = GT / G8;
-    __syncthreads();                              // the staged tile is no longer read
-    float* fold = reinterpret_cast<float*>(lds);  // [GT][16]
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      fold[threadIdx.x * 16 + k] = cs1[k];
-      fold[threadIdx.x * 16 + 8 + k] = cs2[k];
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < BN; c += GT) {
-      const int n = n0 + c;
-      if (n >= p.N) continue;
-      const int g = c / 8, k = c % 8;
-      float a = 0.f, b = 0.f;
-      for (int q = 0; q < Q; ++q) {               // fixed order: deterministic
-        a += fold[(q * G8 + g) * 16 + k];
-        b += fold[(q * G8 + g) * 16 + 8 + k];
-      }
-      // [tiles_m][2][N]: one coalesced row per M-tile (bn.hip k_colsum folds the rows)
-      p.stats[(int64_t)tm * 2 * p.N + n] = a;
-      p.stats[(int64_t)tm * 2 * p.N + p.N + n] = b;
-    }
-  }
-}
 
 // Fixed-order reduction of split-K slabs + epilogue. A workgroup owns OT float4 groups of outputs
 // and ZT split lanes (ZT*OT = 256): lane z sums splits z, z+ZT, ... in order, then the ZT lane sums
@@ -879,6 +394,24 @@ static void launch_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, h
 #undef LW_E
 }
 
+void splitk_reduce(const GemmArgs& g, int zs, hipStream_t st) {
+  const int64_t total = (int64_t)g.M * g.N;
+  int zl = 0;                                    // split lanes: up to 32, no more than splits
+  while (zl < 5 && (2 << zl) <= zs) ++zl;
+  const int64_t groups = (total + 3) / 4, ot = GT >> zl;
+  const dim3 rg((unsigned)((groups + ot - 1) / ot));
+  hipLaunchKernelGGL(k_splitk_reduce, rg, dim3(GT), 0, st, g.partial, zs, zl, g.C, g.ldc, g.bias,
+                     g.relu, g.M, g.N, g.out_bf16 ? 1 : 0, g.addend, g.add_bits,
+                     g.accumulate ? 1 : 0);
+}
+
+void gemm_tile_shape(int t, int& bm, int& bn, int& bk) {
+  const TileShape ts = tile_shape(t);
+  bm = ts.bm; bn = ts.bn; bk = ts.bk;
+}
+
+int gemm_k_per_split(int K, int splits, int bk) { return k_per_split(K, splits, bk); }
+
 void gemm_bf16(const GemmArgs& g, hipStream_t st) {
   if (g.tile >= GEMM_S64) {
     gemm_stream(g, st);
@@ -902,16 +435,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
     case GEMM_T64x64x64: launch_tile<64, 64, 64>(g, k, epi, grid, st); break;
     default: launch_tile<128, 128, 32>(g, k, epi, grid, st); break;
   }
-  if (zs > 1) {
-    const int64_t total = (int64_t)g.M * g.N;
-    int zl = 0;                                  // split lanes: up to 32, no more than splits
-    while (zl < 5 && (2 << zl) <= zs) ++zl;
-    const int64_t groups = (total + 3) / 4, ot = GT >> zl;
-    const dim3 rg((unsigned)((groups + ot - 1) / ot));
-    hipLaunchKernelGGL(k_splitk_reduce, rg, dim3(GT), 0, st, g.partial, zs, zl, g.C, g.ldc, g.bias,
-                       g.relu, g.M, g.N, g.out_bf16 ? 1 : 0, g.addend, g.add_bits,
-                       g.accumulate ? 1 : 0);
-  }
+  if (zs > 1) splitk_reduce(g, zs, st);
 }
 
 }  // namespace lw

@@ -202,6 +202,27 @@ int gemm_pick_tile(const GemmArgs& g);
 int gemm_tiles_m(const GemmArgs& g);
 int gemm_splits_used(const GemmArgs& g);
 bool gemm_stream_ok(const GemmArgs& g);
+void splitk_reduce(const GemmArgs& g, int splits, hipStream_t st);   // fixed-order slab reduce
+void gemm_tile_shape(int tile, int& bm, int& bn, int& bk);
+int gemm_k_per_split(int K, int splits, int bk);
+
+// implicit-GEMM convolution, NHWC bf16 (conv.hip). The GEMM view of each pass:
+//   forward  y[pix][co]  = Σ_(tap,ci) X[gather(pix, tap)][ci] · W[co][tap][ci]      A-gather
+//   dgrad    dx[pix][ci] = Σ_(tap,co) dY[gather(pix, tap)][co] · Wt[tap][co][ci]    A-gather,
+//            per stride-parity class (stride 2: 4 classes, each a stride-1 problem)
+//   wgrad    dW[co][tap][ci] = Σ_pix dY[pix][co] · X[gather(pix, tap)][ci]        B-gather
+// `g` carries the plain GEMM part (operands, output, epilogue, prologue, split-K), `cv` the
+// gather geometry; `mode` is CV_A / CV_A4 / CV_B / CV_B4 of gemm_core.h.
+// gather modes: row (A) gather C % 8 / C == 4, column (B) gather C % 8 / C == 4
+enum ConvMode { CV_NONE = 0, CV_A = 1, CV_A4 = 2, CV_B = 3, CV_B4 = 4 };
+struct ConvGeomHost {
+  int Hin, Win, C, sh, sw, dh, dw, Hout, Wout, osy, osx, nclass;
+  int TR[4], TS[4], oh[4], ow[4], Hg[4], Wg[4], py[4], px[4], M[4], K[4];
+  int64_t b_off[4];
+};
+void conv_gemm(const GemmArgs& g, const ConvGeomHost& cv, int mode, hipStream_t st);
+int conv_splits_used(const GemmArgs& g);
+bool conv_tile_ok(int mode, int tile);
 
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],

@@ -1,0 +1,338 @@
+"""Hand-written MFMA implicit-GEMM convolutions (``csrc/conv.hip``) and the layer built on them.
+
+Every convolution of the reference models — the ResNet-50 3x3 bottleneck convs and 7x7 stem
+(``IMAGENET/training/resnet.py:18-21,63-64,100``), the ResNet-9 / AlexNet / VGG-16 CIFAR convs
+(``CIFAR10/dawn.py:23-33``, ``CIFAR10/alexnet.py:15-25``, ``CIFAR10/vgg16.py:76``) — runs its
+forward, data gradient and weight gradient here, on the same MFMA GEMM core as the 1x1 convs and
+Linear layers, with NHWC bf16 activations and fp32 accumulation:
+
+  * forward: ``y = im2col(x)·Wᵀ`` with the window gathered while staging (no im2col buffer); an
+    optional BatchNorm-apply+ReLU of the input in the staging prologue and the next BN's column
+    statistics in the epilogue;
+  * data gradient: the transposed conv as a gather over dY with the taps walked backwards; a
+    stride-2 conv runs as its 4 output-parity classes, each a dense stride-1 GEMM over the taps
+    that reach it;
+  * weight gradient: split-K over the output pixels with fp32 written (or accumulated) straight
+    into the gradient arena view of a channels_last weight ([Co][R][S][C] = the GEMM output).
+
+A 3-channel input (the image) runs as a 4-channel one whose chunks are two adjacent taps.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ._ext import load
+
+BF16 = torch.bfloat16
+CL = torch.channels_last
+CV_A, CV_A4, CV_B, CV_B4 = 1, 2, 3, 4
+ROW_TILES = (1, 2, 3, 5, 6)          # forward / dgrad (csrc GemmTile ids)
+COL_TILES = (1, 2, 4, 6)             # weight gradient
+_TILE_DIMS = {1: (128, 128, 32), 2: (128, 128, 64), 3: (256, 64, 32), 4: (64, 256, 32),
+              5: (256, 64, 64), 6: (64, 64, 64)}
+
+
+def _pair(v) -> Tuple[int, int]:
+    return (v, v) if isinstance(v, int) else (int(v[0]), int(v[1]))
+
+
+def out_size(h: int, k: int, s: int, p: int) -> int:
+    return (h + 2 * p - k) // s + 1
+
+
+def supported(cin: int, cout: int, groups: int = 1, dilation=(1, 1)) -> bool:
+    return groups == 1 and tuple(_pair(dilation)) == (1, 1) and cout % 8 == 0 and \
+        (cin % 8 == 0 or cin in (3, 4))
+
+
+# ----------------------------------------------------------------------------- tile tuner
+class ConvTuner:
+    """First sight of a problem key: time every candidate (tile, or (tile, splits)) with HIP
+    events on scratch outputs and keep the fastest — MIOpen-find-style, but over our own
+    kernels only. ``LWAAAI_CONV_TUNE=0`` keeps the heuristic choice."""
+
+    def __init__(self):
+        self.best = {}
+        self.enabled = os.environ.get("LWAAAI_CONV_TUNE", "1") != "0"
+
+    def pick(self, key, run, candidates, default):
+        c = self.best.get(key)
+        if c is not None:
+            return c
+        if not self.enabled or len(candidates) == 1 or torch.cuda.is_current_stream_capturing():
+            self.best[key] = default
+            return default
+        times = []
+        for cand in candidates:
+            run(cand)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(3):
+                run(cand)
+            e.record()
+            e.synchronize()
+            times.append((s.elapsed_time(e), cand))
+        c = min(times, key=lambda t: t[0])[1]
+        self.best[key] = c
+        return c
+
+
+TUNER = ConvTuner()
+
+
+def _row_default(M: int, N: int) -> int:
+    if N <= 64:
+        return 3 if M >= 4096 else 6
+    return 2 if M * N >= (1 << 20) else 6
+
+
+# ----------------------------------------------------------------------------- weight packing
+def _c4_input(x: torch.Tensor) -> torch.Tensor:
+    """[N, 3, H, W] → bf16 channels_last [N, 4, H, W] with a zero 4th channel."""
+    x = x.to(BF16)
+    if x.shape[1] == 4:
+        return x.contiguous(memory_format=CL)
+    out = torch.zeros((x.shape[0], x.shape[2], x.shape[3], 4), dtype=BF16,
+                      device=x.device).permute(0, 3, 1, 2)
+    out[:, :3].copy_(x)
+    return out
+
+
+def pack_fwd_weight(w: torch.Tensor) -> Tuple[torch.Tensor, int, int]:
+    """Weight [Co, C, R, S] → bf16 GEMM operand [Co][K] (K-contiguous). For C in (3, 4) the taps
+    along w are padded to an even count and the channels to 4. Returns (operand, K, TS)."""
+    co, c, r, s = w.shape
+    wb = w.to(BF16)
+    if c % 8 == 0:
+        return wb.permute(0, 2, 3, 1).contiguous().view(co, -1), r * s * c, s
+    ts = s + (s & 1)
+    p = torch.zeros((co, r, ts, 4), dtype=BF16, device=w.device)
+    p[:, :, :s, :c].copy_(wb.permute(0, 2, 3, 1))
+    return p.view(co, -1), r * ts * 4, ts
+
+
+def _dgrad_classes(H, W, R, S, sh, sw, ph, pw):
+    """Output-parity classes of the data gradient: (ch, cw, r0, s0, TR, TS, Hg, Wg, oh, ow)."""
+    out = []
+    for ch in range(sh):
+        r0 = (ch + ph) % sh
+        TR = len(range(r0, R, sh))
+        Hg = len(range(ch, H, sh))
+        for cw in range(sw):
+            s0 = (cw + pw) % sw
+            TS = len(range(s0, S, sw))
+            Wg = len(range(cw, W, sw))
+            if TR == 0 or TS == 0 or Hg == 0 or Wg == 0:
+                continue                     # no tap reaches these pixels: gradient stays 0
+            out.append((ch, cw, r0, s0, TR, TS, Hg, Wg, (ch + ph - r0) // sh, (cw + pw - s0) // sw))
+    return out
+
+
+def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int) -> Tuple[torch.Tensor, List[int]]:
+    """Per-class slabs Wt_c[jr][js][co][ci] = w[co, ci, r0 + sh*jr, s0 + sw*js], concatenated."""
+    co, c, R, S = w.shape
+    wt = w.to(BF16).permute(2, 3, 0, 1)                      # [R, S, Co, C]
+    if len(classes) == 1 and classes[0][4] == R and classes[0][5] == S:
+        return wt.contiguous().view(-1), [0]
+    parts, offs, off = [], [], 0
+    for (ch, cw, r0, s0, TR, TS, *_r) in classes:
+        p = wt[r0::sh][:TR][:, s0::sw][:, :TS].reshape(-1)
+        parts.append(p)
+        offs.append(off)
+        off += p.numel()
+    return torch.cat(parts), offs
+
+
+# ----------------------------------------------------------------------------- the three passes
+def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=False,
+             wpack=None):
+    """y = conv2d(x, w) as bf16 channels_last [N, Co, Ho, Wo]; optionally the input BN-apply+ReLU
+    ``pro = (scale, shift)`` (fp32 [C]) and the per-M-tile column statistics of y."""
+    lib = load()
+    sh, sw = _pair(stride)
+    ph, pw = _pair(padding)
+    co, c, R, S = w.shape
+    c4 = c % 8 != 0
+    xin = _c4_input(x) if c4 else x.to(BF16).contiguous(memory_format=CL)
+    Nb, _, H, W = xin.shape
+    Ho, Wo = out_size(H, R, sh, ph), out_size(W, S, sw, pw)
+    op, K, TS = wpack if wpack is not None else pack_fwd_weight(w)
+    C = xin.shape[1]
+    geom = [Nb, H, W, C, sh, sw, 1, 1, Ho, Wo, 1, 1, 1,
+            R, TS, -ph, -pw, Ho, Wo, 0, 0, K, 0]
+    mode = CV_A4 if c4 else CV_A
+    ps, pt = (pro[0], pro[1]) if pro is not None else (None, None)
+    M = Nb * Ho * Wo
+
+    def run(tile):
+        return lib.conv_ex(xin, op, mode, geom, co, tile, 1, True, ps, pt, stats, None, False, 0,
+                           True, K)
+    key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats)
+    tile = TUNER.pick(key, run, ROW_TILES, _row_default(M, co))
+    y, st = run(tile)
+    return y.view(Nb, Ho, Wo, co).permute(0, 3, 1, 2), st
+
+
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=None):
+    """dx [N, C, H, W] (bf16 channels_last) of conv2d(x, w) given dy [N, Co, Ho, Wo]."""
+    lib = load()
+    sh, sw = _pair(stride)
+    ph, pw = _pair(padding)
+    co, c, R, S = w.shape
+    H, W = x_hw
+    dyc = dy.to(BF16).contiguous(memory_format=CL)
+    Nb, _, Ho, Wo = dyc.shape
+    classes = _dgrad_classes(H, W, R, S, sh, sw, ph, pw)
+    if not classes:
+        return torch.zeros((Nb, c, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+    wt, offs = wpack if wpack is not None else pack_dgrad_weight(w, classes, sh, sw)
+    geom = [Nb, Ho, Wo, co, 1, 1, -1, -1, H, W, sh, sw, len(classes)]
+    for (ch, cw, r0, s0, TR, TS, Hg, Wg, oh, ow), off in zip(classes, offs):
+        geom += [TR, TS, oh, ow, Hg, Wg, ch, cw, TR * TS * co, off]
+    M = max(Nb * cl[6] * cl[7] for cl in classes)
+
+    def run(tile):
+        return lib.conv_ex(dyc, wt, CV_A, geom, c, tile, 1, True, None, None, False, None,
+                           False, 0, False, c)
+    key = ("d", tuple(dyc.shape), tuple(w.shape), H, W, sh, sw, ph, pw)
+    tile = TUNER.pick(key, run, ROW_TILES, _row_default(M, c))
+    dx, _ = run(tile)
+    return dx.view(Nb, H, W, c).permute(0, 3, 1, 2)
+
+
+def _wgrad_splits(tiles: int, pixels: int, bk: int) -> int:
+    want = max(1, (2 * 256) // max(tiles, 1))
+    return int(max(1, min(want, pixels // (bk * 8))))
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, pro=None,
+               out: Optional[torch.Tensor] = None):
+    """dW of conv2d(x, w): fp32 [Co][R][S'][C'] GEMM output. With ``out`` (a dense fp32 view of
+    the weight's gradient in [Co][R][S][C] memory order, C % 8 == 0) the result is accumulated
+    into it in place and ``out`` is returned; otherwise a fresh [Co, C, R, S] tensor (channels_last
+    memory) is returned."""
+    lib = load()
+    sh, sw = _pair(stride)
+    ph, pw = _pair(padding)
+    co, c, R, S = w_shape
+    c4 = c % 8 != 0
+    xin = _c4_input(x) if c4 else x.to(BF16).contiguous(memory_format=CL)
+    dyc = dy.to(BF16).contiguous(memory_format=CL)
+    Nb, C, H, W = xin.shape
+    _, _, Ho, Wo = dyc.shape
+    TS = S + (S & 1) if c4 else S
+    N = R * TS * C
+    pix = Nb * Ho * Wo
+    geom = [Nb, H, W, C, sh, sw, 1, 1, Ho, Wo, 1, 1, 1, R, TS, -ph, -pw, Ho, Wo, 0, 0, 0, 0]
+    mode = CV_B4 if c4 else CV_B
+    ps, pt = (pro[0], pro[1]) if pro is not None else (None, None)
+
+    def cands():
+        cs = []
+        for t in COL_TILES:
+            bm, bn, bk = _TILE_DIMS[t]
+            tiles = -(-co // bm) * -(-N // bn)
+            s0 = _wgrad_splits(tiles, pix, bk)
+            for s in sorted({max(1, s0 // 2), s0, s0 * 2}):
+                cs.append((t, s))
+        return cs
+
+    def run(cand, dst=None, acc=False):
+        t, s = cand
+        return lib.conv_ex(xin, dyc, mode, geom, N, t, s, False, ps, pt, False, dst, acc, 0,
+                           False, co)
+    key = ("w", tuple(xin.shape), tuple(dyc.shape), tuple(w_shape), sh, sw, ph, pw,
+           pro is not None)
+    bm, bn, bk = _TILE_DIMS[1]
+    default = (1, _wgrad_splits(-(-co // bm) * -(-N // bn), pix, bk))
+    cand = TUNER.pick(key, run, cands(), default)
+    direct = out is not None and not c4
+    if direct:
+        run(cand, out, True)
+        return out
+    g, _ = run(cand)
+    g = g.view(co, R, TS, C)[:, :, :S, :c]
+    return g.permute(0, 3, 1, 2)
+
+
+# ----------------------------------------------------------------------------- autograd layer
+def _arena_view(p: torch.Tensor):
+    """The parameter's fp32 gradient-arena view when the engine wants it written in place and
+    its memory order is [Co][R][S][C] (channels_last), else None."""
+    if getattr(p, "_lw_grad_ready", None) is None or p.grad is None:
+        return None
+    g = p.grad
+    if g.dtype != torch.float32 or not g.is_contiguous(memory_format=CL):
+        return None
+    return g
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding):
+        from .block import _bf16_weight
+        wb = _bf16_weight(weight)
+        y, _ = conv_fwd(x, wb, stride, padding)
+        xs = x.to(BF16).contiguous(memory_format=CL) if x.shape[1] % 8 == 0 else x
+        ctx.save_for_backward(xs, wb)
+        ctx.geom = (stride, padding, tuple(x.shape[2:]), x.dtype)
+        ctx.weight = weight
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, wb = ctx.saved_tensors
+        stride, padding, hw, xdtype = ctx.geom
+        w = ctx.weight
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad(dy, wb, hw, stride, padding).to(xdtype)
+        if ctx.needs_input_grad[1]:
+            dst = _arena_view(w)
+            if dst is not None and w.shape[1] % 8 == 0:
+                conv_wgrad(dy, xs, tuple(w.shape), stride, padding, out=dst)
+                w._lw_grad_ready(w)
+            else:
+                dw = conv_wgrad(dy, xs, tuple(w.shape), stride, padding).to(w.dtype)
+                dw = dw.contiguous(memory_format=CL) if w.is_contiguous(memory_format=CL) \
+                    else dw.contiguous()
+        return dx, dw, None, None
+
+
+def mfma_conv2d(x, weight, bias=None, stride=1, padding=0):
+    y = _ConvFn.apply(x, weight, _pair(stride), _pair(padding))
+    if bias is not None:
+        y = y + bias.to(y.dtype).view(1, -1, 1, 1)
+    return y
+
+
+class MFMAConv2d(nn.Conv2d):
+    """nn.Conv2d (same parameters / state_dict) on the MFMA implicit-GEMM kernels for CUDA
+    inputs; CPU tensors and unsupported configurations keep the torch path."""
+
+    def forward(self, x):
+        if x.is_cuda and isinstance(self.padding, tuple) and self.padding_mode == "zeros" and \
+                supported(self.in_channels, self.out_channels, self.groups, self.dilation):
+            return mfma_conv2d(x, self.weight, self.bias, self.stride, self.padding)
+        return super().forward(x)
+
+
+def to_mfma_conv(m: nn.Conv2d) -> nn.Conv2d:
+    if type(m) is nn.Conv2d:
+        m.__class__ = MFMAConv2d
+    return m
+
+
+def fuse_convs(model: nn.Module) -> nn.Module:
+    """Switch every plain nn.Conv2d of ``model`` to :class:`MFMAConv2d` (in place; parameter and
+    buffer names are unchanged, so checkpoints stay compatible)."""
+    for m in model.modules():
+        if type(m) is nn.Conv2d:
+            to_mfma_conv(m)
+    return model

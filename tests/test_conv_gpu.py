@@ -1,0 +1,138 @@
+"""Hand-written MFMA implicit-GEMM convolutions (csrc/conv.hip) vs a plain fp32 torch reference:
+forward / data gradient / weight gradient for every 3x3 / 7x7 / 5x5 shape of the reference models
+(ResNet-50 bottlenecks and stem, ResNet-9, VGG-16, AlexNet; batch reduced), the fused BN-apply+ReLU
+prologues, the column-statistics epilogue and in-place accumulation into a channels_last arena."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from layer_wise_aaai20_amd.ops import conv as CV
+
+pytestmark = pytest.mark.gpu
+CL = torch.channels_last
+
+# (N, Cin, Cout, H, k, stride, pad): ResNet-50 @224 3x3 (batch 4), stem, CIFAR nets
+SHAPES = [
+    (4, 64, 64, 56, 3, 1, 1), (4, 128, 128, 56, 3, 2, 1), (4, 128, 128, 28, 3, 1, 1),
+    (4, 256, 256, 28, 3, 2, 1), (4, 256, 256, 14, 3, 1, 1), (4, 512, 512, 14, 3, 2, 1),
+    (4, 512, 512, 7, 3, 1, 1),
+    (2, 3, 64, 224, 7, 2, 3),                                   # ResNet-50 stem
+    (8, 3, 64, 32, 3, 1, 1), (8, 64, 128, 32, 3, 1, 1), (8, 128, 256, 16, 3, 1, 1),
+    (8, 256, 512, 8, 3, 1, 1), (8, 512, 512, 2, 3, 1, 1),        # ResNet-9 / VGG-16
+    (8, 64, 192, 8, 5, 1, 2), (8, 3, 64, 32, 11, 4, 5),          # AlexNet-style 5x5 / 11x11
+    (3, 24, 40, 13, 3, 2, 0), (3, 16, 24, 9, 1, 2, 0),           # odd sizes, no padding
+]
+
+
+def _inputs(N, C, Co, H, k, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(N, C, H, H, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(Co, C, k, k, device="cuda", generator=g) / (C * k * k) ** 0.5).bfloat16()
+    return x.contiguous(memory_format=CL), w.contiguous(memory_format=CL)
+
+
+def _close(a, b, tol):
+    err = (a.float() - b.float()).abs().max().item()
+    scale = b.float().abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err:.3e} vs scale {scale:.3e}"
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_conv_fwd(shape):
+    N, C, Co, H, k, s, p = shape
+    x, w = _inputs(N, C, Co, H, k)
+    y, _ = CV.conv_fwd(x, w, s, p)
+    ref = F.conv2d(x.float(), w.float(), stride=s, padding=p)
+    assert y.shape == ref.shape
+    _close(y, ref, 1e-2)
+
+
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] % 8 == 0],
+                         ids=[str(s) for s in SHAPES if s[1] % 8 == 0])
+def test_conv_dgrad(shape):
+    N, C, Co, H, k, s, p = shape
+    x, w = _inputs(N, C, Co, H, k, 1)
+    xf = x.float().requires_grad_()
+    ref = F.conv2d(xf, w.float(), stride=s, padding=p)
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    dx = CV.conv_dgrad(dy.contiguous(memory_format=CL), w, (H, H), s, p)
+    assert dx.shape == x.shape
+    _close(dx, xf.grad, 1e-2)
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
+def test_conv_wgrad(shape):
+    N, C, Co, H, k, s, p = shape
+    x, w = _inputs(N, C, Co, H, k, 2)
+    wf = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wf, stride=s, padding=p)
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    dw = CV.conv_wgrad(dy.contiguous(memory_format=CL), x, tuple(w.shape), s, p)
+    assert dw.shape == w.shape
+    _close(dw, wf.grad, 2e-3)
+
+
+def test_wgrad_accumulates_into_channels_last_arena_view():
+    N, C, Co, H, k, s, p = 4, 64, 128, 28, 3, 2, 1
+    x, w = _inputs(N, C, Co, H, k, 3)
+    wf = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wf, stride=s, padding=p)
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    arena = torch.full((Co * C * k * k + 64,), 0.5, device="cuda")
+    view = arena[32:32 + Co * C * k * k].as_strided(w.shape, (C * k * k, 1, k * C, C))
+    assert view.is_contiguous(memory_format=CL)
+    CV.conv_wgrad(dy.contiguous(memory_format=CL), x, tuple(w.shape), s, p, out=view)
+    _close(view - 0.5, wf.grad, 2e-3)
+    assert torch.all(arena[:32] == 0.5) and torch.all(arena[32 + Co * C * k * k:] == 0.5)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 64, 56, 3, 1, 1), (4, 128, 128, 56, 3, 2, 1),
+                                   (4, 256, 256, 14, 3, 1, 1)])
+def test_bn_prologue_and_stats_epilogue(shape):
+    """conv(relu(x*scale+shift)) with the affine in the staging prologue (padding stays zero),
+    column statistics of the bf16 output, and the weight gradient with the same prologue."""
+    N, C, Co, H, k, s, p = shape
+    x, w = _inputs(N, C, Co, H, k, 4)
+    scale = torch.rand(C, device="cuda") + 0.5
+    shift = torch.randn(C, device="cuda") * 0.5
+    a = torch.relu(x.float() * scale.view(1, -1, 1, 1) + shift.view(1, -1, 1, 1)).bfloat16()
+    y, st = CV.conv_fwd(x, w, s, p, pro=(scale, shift), stats=True)
+    ref = F.conv2d(a.float(), w.float(), stride=s, padding=p)
+    _close(y, ref, 1e-2)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, Co)
+    tot = st.sum(0)
+    torch.testing.assert_close(tot[0], yf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(tot[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+    wf = w.float().requires_grad_()
+    r2 = F.conv2d(a.float(), wf, stride=s, padding=p)
+    dy = torch.randn_like(r2).bfloat16()
+    r2.backward(dy.float())
+    dw = CV.conv_wgrad(dy.contiguous(memory_format=CL), x, tuple(w.shape), s, p,
+                       pro=(scale, shift))
+    _close(dw, wf.grad, 2e-3)
+
+
+def test_mfma_conv2d_module_matches_torch():
+    torch.manual_seed(0)
+    ref = torch.nn.Conv2d(64, 128, 3, stride=2, padding=1, bias=True).cuda()
+    m = torch.nn.Conv2d(64, 128, 3, stride=2, padding=1, bias=True).cuda()
+    m.load_state_dict(ref.state_dict())
+    with torch.no_grad():
+        ref.weight.copy_(ref.weight.bfloat16().float())
+    CV.to_mfma_conv(m)
+    m = m.to(memory_format=CL)
+    x = torch.randn(4, 64, 20, 20, device="cuda").bfloat16().float()
+    xa = x.clone().requires_grad_()
+    xb = x.clone().requires_grad_()
+    y = m(xa)
+    yr = ref(xb)
+    _close(y, yr, 1e-2)
+    g = torch.randn_like(yr)
+    y.float().backward(g)
+    yr.backward(g.bfloat16().float())
+    _close(xa.grad, xb.grad, 2e-2)
+    _close(m.weight.grad, ref.weight.grad, 5e-3)
+    _close(m.bias.grad, ref.bias.grad, 5e-3)

@@ -280,7 +280,6 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
   check_cuda(in, "in");
   check_dtype(in, at::kByte, "in");
   TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "mean/std need 3 channels");
-  TORCH_CHECK(out.numel() == in.numel(), "out/in size mismatch");
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat,
               "out must be bf16 or fp32");
   // `out` is an NCHW tensor in channels_last memory == the NHWC byte order of `in`
@@ -290,6 +289,13 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
   check_aligned16(out.data_ptr(), "out");
   const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
   const float s[3] = {(float)stdv[0], (float)stdv[1], (float)stdv[2]};
+  if (out.size(1) == 4) {                    // 4-channel (zero-padded) bf16 stem input
+    TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.numel() / 4 * 3 == in.numel() &&
+                out.numel() % 4 == 0, "4-channel out: bf16 with in.numel()/3 pixels");
+    lw::normalize_u8_c4(ptr<uint8_t>(in), ptr<uint16_t>(out), in.numel() / 3, m, s, cur_stream());
+    return;
+  }
+  TORCH_CHECK(out.numel() == in.numel(), "out/in size mismatch");
   lw::normalize_u8(ptr<uint8_t>(in), out.data_ptr(), in.numel(), m, s,
                    out.scalar_type() == at::kBFloat16, cur_stream());
 }

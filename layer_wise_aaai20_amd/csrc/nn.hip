@@ -67,6 +67,57 @@ __global__ __launch_bounds__(256) void k_normalize_u8(const uint8_t* __restrict_
   }
 }
 
+// 3-channel uint8 pixels -> 4-channel bf16 pixels (4th channel 0): the input layout of the
+// implicit-GEMM stem convolution (ops/conv.py, C == 4 mode: one 8-byte load per tap). A thread
+// converts 16 pixels: three 16-byte loads, eight 16-byte stores.
+__global__ __launch_bounds__(256) void k_normalize_u8_c4(const uint8_t* __restrict__ in,
+                                                         uint16_t* __restrict__ out, int64_t npix,
+                                                         float m0, float m1, float m2, float r0,
+                                                         float r1, float r2) {
+  const int64_t p0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+  if (p0 >= npix) return;
+  const float mean[3] = {m0, m1, m2};
+  const float rstd[3] = {r0, r1, r2};
+  uint8_t b[48];
+  if (p0 + 16 <= npix) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4*>(in + p0 * 3 + 16 * q);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 16; ++k) b[16 * q + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
+  } else {
+    for (int k = 0; k < 48; ++k) b[k] = p0 * 3 + k < npix * 3 ? in[p0 * 3 + k] : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {            // pixels 2q, 2q+1
+    uint32_t w[4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int px = 2 * q + h;
+      const float y0 = ((float)b[3 * px] - mean[0]) * rstd[0];
+      const float y1 = ((float)b[3 * px + 1] - mean[1]) * rstd[1];
+      const float y2 = ((float)b[3 * px + 2] - mean[2]) * rstd[2];
+      w[2 * h] = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
+      w[2 * h + 1] = (uint32_t)f2bf(y2);
+    }
+    if (p0 + 2 * q + 2 <= npix) {
+      reinterpret_cast<uint4*>(out + (p0 + 2 * q) * 4)[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    } else if (p0 + 2 * q < npix) {
+      reinterpret_cast<uint2*>(out + (p0 + 2 * q) * 4)[0] = make_uint2(w[0], w[1]);
+    }
+  }
+}
+
+void normalize_u8_c4(const uint8_t* in, uint16_t* out, int64_t npix, const float mean[3],
+                     const float stdv[3], hipStream_t st) {
+  const int64_t thr = (npix + 15) / 16;
+  const dim3 grid((unsigned)((thr + 255) / 256)), block(256);
+  hipLaunchKernelGGL(k_normalize_u8_c4, grid, block, 0, st, in, out, npix, mean[0], mean[1],
+                     mean[2], 1.f / stdv[0], 1.f / stdv[1], 1.f / stdv[2]);
+}
+
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
                   const float stdv[3], bool bf16, hipStream_t st) {
   const int64_t chunks = (nbytes + 15) / 16;

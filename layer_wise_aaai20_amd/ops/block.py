@@ -10,9 +10,8 @@ and its prologue / epilogue fusions instead:
 forward (training)::
 
     c1 = x·W1ᵀ                       GEMM, epilogue writes BN1 column statistics
-    a1 = relu(bn1(c1))               one apply pass (the 3x3 conv needs it materialised)
-    c2 = conv3x3(a1)                 MIOpen (channels_last bf16)
-    bn2 statistics                   one reduce pass
+    c2 = conv3x3(relu(bn1(c1)))      implicit GEMM (ops/conv.py): BN1-apply+ReLU in the staging
+                                     prologue (a1 is never materialised), BN2 stats in the epilogue
     c3 = relu(bn2(c2))·W3ᵀ           GEMM, BN2-apply+ReLU in the prologue, BN3 stats in the epilogue
     [cd = x_s·Wdᵀ                    GEMM + stats (downsample shortcut)]
     out = relu(bn3(c3) + x | bnd(cd)) one pass (the shortcut BN is applied on the fly)
@@ -25,14 +24,17 @@ backward::
                                      straight into the gradient arena
     da2 = dc3·W3                     GEMM
     bn2 backward (mask from c2)      → dc2
-    conv3x3 backward                 MIOpen
+    dW2 = dc2ᵀ ⋆ relu(bn1(c1))       implicit-GEMM weight gradient, BN1-apply recomputed in the
+                                     prologue, split-K, fp32 accumulated into the arena
+    da1 = conv3x3ᵀ(dc2)              implicit-GEMM data gradient (stride 2: 4 parity classes)
     bn1 backward (mask from c1)      → dc1
     dW1 = dc1ᵀ·x                     GEMM into the arena
     dx  = dc1·W1 + dy·[out>0]        GEMM; the masked shortcut gradient is added in the epilogue
 
-Compared with the per-layer path this removes, per block, the BN1 and BN3 statistics passes, the
-BN2 apply pass and its materialised output, the shortcut-BN apply pass, the gradient add of the
-block input, and the fp32 casts/accumulations of the weight gradients.
+Compared with the per-layer path this removes, per block, the BN1/BN2/BN3 statistics passes, the
+BN1 and BN2 apply passes and their materialised outputs, the shortcut-BN apply pass, the gradient
+add of the block input, and the fp32 casts/accumulations of the weight gradients. Every GEMM and
+convolution of the block is a hand-written MFMA kernel (no vendor library on this path).
 
 Weight / BN-parameter gradients go **directly into the gradient arena** when the parameter is
 owned by a :class:`~..parallel.ddp.CompressedDDP` (which marks it with ``_lw_grad_ready``); the
@@ -49,6 +51,7 @@ import torch
 import torch.nn.functional as F
 
 from ._ext import load
+from .conv import conv_dgrad, conv_fwd, conv_wgrad
 
 BF16 = torch.bfloat16
 CL = torch.channels_last
@@ -123,24 +126,6 @@ def stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro, pro_on_a, add, split
     return tuple(t for t in STREAM if not (K == 256 and t == 13))
 
 
-BLAS = -1                           # tuner candidate: the vendor library (hipBLASLt)
-
-
-def _mat(P, ld, kc, rows, K):
-    """Logical [rows, K] matrix over a packed operand: K-contiguous ``P[r*ld + k]`` or
-    row-contiguous ``P[k*ld + r]`` (a transposed view, no copy)."""
-    if kc:
-        return P.view(-1)[: (rows - 1) * ld + K].as_strided((rows, K), (ld, 1))
-    return P.view(-1)[: (K - 1) * ld + rows].as_strided((rows, K), (1, ld))
-
-
-def blas_ok(out_bf16, stats, pro, add, accumulate, split_k, out, ldc, N) -> bool:
-    """Plain problems only (no fused prologue / epilogue): there the library GEMM is a fair
-    candidate for the tuner to time against the hand-written kernels."""
-    return (out_bf16 and not stats and not pro and not add and not accumulate and not split_k
-            and out is None and ldc in (0, N))
-
-
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro=None,
          pro_on_a=True, out=None, addend=None, accumulate=False, ldc=0, split_k=False,
          addend_bits=None):
@@ -157,24 +142,12 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
     key = (M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a, split_k,
            addend is not None)
 
-    def blas():
-        # B(k, n): [N][ldb] K-contiguous -> Bᵀ view, or [K][ldb] N-contiguous
-        Bm = _mat(B, ldb, b_kc, N, K).t()
-        return torch.mm(_mat(A, lda, a_kc, M, K), Bm), torch.empty(0, device=A.device)
-
     def run(tile):
-        if tile == BLAS:
-            return blas()
         lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile), out_bf16,
                     tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits)
     cands = TILES + stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a,
                                  addend is not None, split_k, accumulate)
-    if blas_ok(out_bf16, stats, pro is not None, addend is not None, accumulate, split_k, out,
-               ldc, N) and A.dtype == torch.bfloat16:
-        cands = cands + (BLAS,)
     tile = TUNER.pick(key, run, cands)
-    if tile == BLAS:
-        return blas()
     return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile),
                        out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc,
                        addend_bits)
@@ -267,15 +240,14 @@ class _BottleneckFn(torch.autograd.Function):
         c1, st1 = gemm(xr, Cin, True, W1, Cin, True, M, width, Cin, stats=True)
         mean1, inv1, ss1 = lib.bn_stats(c1, st1, g1, b1, bn1.running_mean, bn1.running_var,
                                         _bn_momentum(bn1), bn1.eps)
-        a1 = lib.bn_apply(c1, ss1, None, None, True)
-        a1n = _nchw(a1, N, H, W)
-        c2n = torch.ops.aten.convolution(a1n, W2, None, list(stride), list(conv2.padding),
-                                         list(conv2.dilation), False, [0, 0], 1)
-        c2n = c2n.contiguous(memory_format=CL)
+        # conv2 (3x3, implicit GEMM): relu(bn1(c1)) is applied while the window is staged
+        # (a1 never exists in memory) and the epilogue emits BN2's column statistics
+        c2n, st2 = conv_fwd(_nchw(c1, N, H, W), W2, stride, conv2.padding,
+                            pro=(ss1[:width], ss1[width:]), stats=True)
         N2, _, H2, W2_ = c2n.shape
         c2 = _rows(c2n)
         M2 = c2.shape[0]
-        mean2, inv2, ss2 = lib.bn_stats(c2, None, g2, b2, bn2.running_mean, bn2.running_var,
+        mean2, inv2, ss2 = lib.bn_stats(c2, st2, g2, b2, bn2.running_mean, bn2.running_var,
                                         _bn_momentum(bn2), bn2.eps)
         # conv3 (1x1) with BN2-apply+ReLU in the prologue and BN3 statistics in the epilogue
         c3, st3 = gemm(c2, width, True, W3, width, True, M2, cout, width, stats=True,
@@ -292,14 +264,14 @@ class _BottleneckFn(torch.autograd.Function):
                                             _bn_momentum(bnd), bnd.eps)
             bits3 = torch.empty(M2 * cout // 8, dtype=torch.uint8, device=x.device)
             out = lib.bn_apply(c3, ss3, cd, ssd, True, bits3)
-            ctx.save_for_backward(x, c1, a1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1,
+            ctx.save_for_backward(x, c1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1,
                                   ss1, mean2, inv2, ss2, mean3, inv3, xsr, cd, Wd, gd, meand,
                                   invd)
             ctx.down_stride = s
         else:
             bits3 = torch.empty(M2 * cout // 8, dtype=torch.uint8, device=x.device)
             out = lib.bn_apply(c3, ss3, xr, None, True, bits3)
-            ctx.save_for_backward(x, c1, a1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1,
+            ctx.save_for_backward(x, c1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1,
                                   ss1, mean2, inv2, ss2, mean3, inv3)
             ctx.down_stride = 0
         ctx.geom = (N, Cin, H, W, N2, H2, W2_, width, cout, M, M2)
@@ -311,8 +283,8 @@ class _BottleneckFn(torch.autograd.Function):
     def backward(ctx, dout):
         lib = load()
         saved = ctx.saved_tensors
-        x, c1, a1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1, ss1, mean2, inv2, ss2, \
-            mean3, inv3 = saved[:20]
+        x, c1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1, ss1, mean2, inv2, ss2, \
+            mean3, inv3 = saved[:19]
         N, Cin, H, W, N2, H2, W2_, width, cout, M, M2 = ctx.geom
         w1, g1p, b1p, w2, g2p, b2p, w3, g3p, b3p, wd, gdp, bdp = ctx.params
         has_down = ctx.down_stride > 0
@@ -336,21 +308,19 @@ class _BottleneckFn(torch.autograd.Function):
         dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False,
                                       None, o2[0], o2[1])
         grads["g2"], grads["b2"] = _finish_bn(g2p, b2p, dg2, db2, o2)
-        # conv2 (3x3) backward on MIOpen
-        a1n = _nchw(a1, N, H, W)
-        dc2n = _nchw(dc2, N2, H2, W2_)
+        # conv2 (3x3) backward on the implicit GEMM: the weight gradient recomputes
+        # relu(bn1(c1)) in its staging prologue and accumulates fp32 straight into the arena
         stride, padding, dilation = ctx.conv2
-        da1n, dW2, _ = torch.ops.aten.convolution_backward(
-            dc2n, a1n, W2, None, stride, padding, dilation, False, [0, 0], 1,
-            [True, True, False])
-        if _direct(w2):
-            # the arena was zeroed at the start of the step and this is the weight's only
-            # contribution: a bf16→fp32 cast-copy instead of a mixed-dtype accumulate
-            w2.grad.copy_(dW2)
+        dc2n = _nchw(dc2, N2, H2, W2_)
+        c1n = _nchw(c1, N, H, W)
+        pro1 = (ss1[:width], ss1[width:])
+        if _direct(w2) and w2.grad.is_contiguous(memory_format=CL):
+            conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1, out=w2.grad)
             grads["w2"] = _finish_param(w2, None, True)
         else:
-            grads["w2"] = dW2.float().contiguous(memory_format=CL)
-        da1 = _rows(da1n.contiguous(memory_format=CL))
+            dW2 = conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1)
+            grads["w2"] = _finish_param(w2, dW2.contiguous(memory_format=CL), _direct(w2))
+        da1 = _rows(conv_dgrad(dc2n, W2, (H, W), stride, padding))
         o1 = _bn_grad_outs(g1p, b1p)
         dc1, dg1, db1, _ = lib.bn_bwd(da1, c1, None, g1, mean1, inv1, ss1, True, True, False,
                                       None, o1[0], o1[1])
@@ -361,7 +331,7 @@ class _BottleneckFn(torch.autograd.Function):
              accumulate=True, split_k=True)
         grads["w1"] = _finish_wgrad(w1, dst1, d1)
         if has_down:
-            xsr, cd, Wd, gd, meand, invd = saved[20:]
+            xsr, cd, Wd, gd, meand, invd = saved[19:]
             s = ctx.down_stride
             od = _bn_grad_outs(gdp, bdp)
             dcd, dgd, dbd, _ = lib.bn_bwd(dr, cd, None, gd, meand, invd, None, True, True,

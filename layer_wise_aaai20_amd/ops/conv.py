@@ -306,7 +306,10 @@ class _ConvFn(torch.autograd.Function):
 
 
 def mfma_conv2d(x, weight, bias=None, stride=1, padding=0):
+    """bf16 MFMA convolution; outside autocast an fp32 input gets an fp32 output back."""
     y = _ConvFn.apply(x, weight, _pair(stride), _pair(padding))
+    if x.dtype == torch.float32 and not torch.is_autocast_enabled():
+        y = y.float()
     if bias is not None:
         y = y + bias.to(y.dtype).view(1, -1, 1, 1)
     return y

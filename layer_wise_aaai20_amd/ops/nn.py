@@ -13,14 +13,21 @@ from ._ext import load, ops_for
 
 
 def normalize_nhwc_u8(images: torch.Tensor, mean: torch.Tensor, std: torch.Tensor,
-                      dtype=torch.bfloat16) -> torch.Tensor:
+                      dtype=torch.bfloat16, pad4: bool = False) -> torch.Tensor:
     """uint8 [N, H, W, C] → ``(x - mean) / std`` as an NCHW tensor in channels_last memory.
 
     One fused pass on the GPU; the reference does collate → ``.cuda()`` →
-    ``.half()`` → ``sub_`` → ``div_`` (``IMAGENET/training/dataloader.py:81-93``)."""
+    ``.half()`` → ``sub_`` → ``div_`` (``IMAGENET/training/dataloader.py:81-93``). ``pad4``
+    (GPU, bf16, 3 channels): write 4 channels with a zero 4th — the input layout of the
+    implicit-GEMM stem convolution (``ops/conv.py``)."""
     assert images.dtype == torch.uint8 and images.dim() == 4
     N, H, W, C = images.shape
     lib = ops_for(images)
+    if lib is not None and pad4 and C == 3 and dtype == torch.bfloat16 and images.is_contiguous():
+        out = torch.empty((N, H, W, 4), dtype=dtype, device=images.device).permute(0, 3, 1, 2)
+        lib.normalize_u8(images, out, [float(m) for m in mean.tolist()],
+                         [float(s) for s in std.tolist()])
+        return out
     if lib is not None and images.is_contiguous():
         out = torch.empty((N, C, H, W), dtype=dtype, device=images.device,
                           memory_format=torch.channels_last)
@@ -196,6 +203,73 @@ class _StemPoolFn(torch.autograd.Function):
         return dc, gw, gb, None, None
 
 
+class _StemConvPoolFn(torch.autograd.Function):
+    """The whole ResNet stem — 7x7/2 conv, BN (batch stats), ReLU, 3x3/2 max-pool — as the
+    implicit-GEMM conv (4-channel image chunks, BN statistics in its epilogue) + one fused
+    BN-apply/ReLU/pool kernel; backward: the fused pool/BN backward + the implicit-GEMM weight
+    gradient (the image needs no gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, conv, bn, geom):
+        from . import block
+        from .conv import conv_fwd
+        lib = load()
+        c, st = conv_fwd(x, block._bf16_weight(w), conv.stride, conv.padding, stats=True)
+        block._bump(bn)
+        mean, invstd, ss = lib.bn_stats(c, st, gamma, beta, bn.running_mean, bn.running_var,
+                                        block._bn_momentum(bn), bn.eps)
+        out, idx = lib.stem_pool_fwd(c, ss, *geom)
+        ctx.save_for_backward(x, c, idx, ss, gamma, mean, invstd)
+        ctx.geom = geom
+        ctx.conv = (tuple(conv.stride), tuple(conv.padding))
+        ctx.params = (w, gamma, beta)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from . import block
+        from .conv import conv_dgrad, conv_wgrad
+        x, c, idx, ss, gamma, mean, invstd = ctx.saved_tensors
+        w, g, b = ctx.params
+        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        outs = block._bn_grad_outs(g, b)
+        dc, dg, db = load().stem_pool_bwd(dout, idx, c, ss, gamma, mean, invstd, *ctx.geom,
+                                          outs[0], outs[1])
+        gg, gb = block._finish_bn(g, b, dg, db, outs)
+        stride, padding = ctx.conv
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if x.shape[1] % 8 == 0:
+                dx = conv_dgrad(dc, block._bf16_weight(w), tuple(x.shape[2:]), stride, padding)
+            else:   # an image that requires grad (saliency maps): not a training path
+                dx = torch.ops.aten.convolution_backward(
+                    dc.float(), x[:, :w.shape[1]].float(), w.float(), None, list(stride),
+                    list(padding), [1, 1], False, [0, 0], 1, [True, False, False])[0]
+                if x.shape[1] != w.shape[1]:
+                    dx = torch.cat([dx, torch.zeros_like(dx[:, :x.shape[1] - w.shape[1]])], 1)
+                dx = dx.to(x.dtype)
+        gw = None
+        if ctx.needs_input_grad[1]:
+            dw = conv_wgrad(dc, x, tuple(w.shape), stride, padding)
+            gw = block._finish_param(w, dw, block._direct(w))
+        return dx, gw, gg, gb, None, None, None
+
+
+def stem_conv_supported(model, x: torch.Tensor) -> bool:
+    from .conv import supported
+    conv, bn = model.conv1, model.bn1
+    return (model.training and x.is_cuda and x.dim() == 4 and x.shape[1] in (3, 4) and
+            conv.in_channels == 3 and conv.bias is None and conv.padding_mode == "zeros" and
+            isinstance(conv.padding, tuple) and supported(3, conv.out_channels, conv.groups,
+                                                          conv.dilation) and
+            bn.affine and bn.track_running_stats and isinstance(model.maxpool, nn.MaxPool2d) and
+            _pool_geom(model.maxpool) is not None)
+
+
+def stem_conv_bn_relu_pool(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, pool: nn.MaxPool2d):
+    return _StemConvPoolFn.apply(x, conv.weight, bn.weight, bn.bias, conv, bn, _pool_geom(pool))
+
+
 def _pool_geom(pool: nn.MaxPool2d):
     def one(v):
         return v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else None)
@@ -218,17 +292,20 @@ def stem_bn_relu_pool(c: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2d) -
 
 
 def _fused_resnet_forward(self, x):
-    c = self.conv1(x)
-    if getattr(self, "_lw_stem_fused", False) and stem_supported(self, c):
-        x = stem_bn_relu_pool(c, self.bn1, self.maxpool)
+    if getattr(self, "_lw_stem_c4", False) and stem_conv_supported(self, x):
+        x = stem_conv_bn_relu_pool(x, self.conv1, self.bn1, self.maxpool)
     else:
-        x = self.maxpool(self.bn1(c))
+        c = self.conv1(x)
+        if getattr(self, "_lw_stem_fused", False) and stem_supported(self, c):
+            x = stem_bn_relu_pool(c, self.bn1, self.maxpool)
+        else:
+            x = self.maxpool(self.bn1(c))
     x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
     x = torch.flatten(self.avgpool(x), 1)
     return self.fc(x)
 
 
-def fuse_resnet(model: nn.Module, block: bool = True) -> nn.Module:
+def fuse_resnet(model: nn.Module, block: bool = True, mfma: bool = True) -> nn.Module:
     """Switch a ``models.resnet`` network to fused BN(+add)(+ReLU) and — with ``block`` — its
     bottlenecks to the whole-block fused MFMA path (``ops/block.py``). Parameter/buffer names and
     values are untouched; only forward changes."""
@@ -252,7 +329,16 @@ def fuse_resnet(model: nn.Module, block: bool = True) -> nn.Module:
     if isinstance(model, R.ResNet):
         to_fused_bn(model.bn1, relu=True)
         model._lw_stem_fused = block
+        model._lw_stem_c4 = block and mfma     # stem = implicit-GEMM conv on a 4-channel image
         model.forward = types.MethodType(_fused_resnet_forward, model)
+    # every remaining conv (stem, eval-mode / BasicBlock paths) and the classifier on the
+    # hand-written MFMA kernels (bf16 operands, fp32 accumulation); mfma=False keeps torch's
+    # convs / Linear (fp32 parity checks of the BN fusion alone)
+    if mfma:
+        from .conv import fuse_convs
+        from .gemm import fuse_linears
+        fuse_convs(model)
+        fuse_linears(model)
     return model
 
 

@@ -53,7 +53,9 @@ class ImageNetTrainer:
         self._last = None
 
     def normalize(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
-        return lwnn.normalize_nhwc_u8(images_u8_nhwc, self.mean, self.std, self.dtype)
+        # a fused ResNet takes the image as 4 bf16 channels (the implicit-GEMM stem's layout)
+        pad4 = bool(getattr(self.ddp.module, "_lw_stem_c4", False))
+        return lwnn.normalize_nhwc_u8(images_u8_nhwc, self.mean, self.std, self.dtype, pad4=pad4)
 
     def forward_loss(self, x, target):
         with torch.autocast(device_type=self.device.type, dtype=self.dtype,

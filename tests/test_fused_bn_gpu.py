@@ -65,7 +65,7 @@ def test_fused_resnet18_matches_unfused():
     a = resnet18().cuda().to(memory_format=torch.channels_last)
     b = resnet18().cuda().to(memory_format=torch.channels_last)
     b.load_state_dict(a.state_dict())
-    fuse_resnet(b)
+    fuse_resnet(b, mfma=False)             # BN fusion only: fp32 parity
     assert set(a.state_dict()) == set(b.state_dict())
     x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
     ya, yb = a(x), b(x)
@@ -76,3 +76,32 @@ def test_fused_resnet18_matches_unfused():
         torch.testing.assert_close(pb.grad, pa.grad, rtol=2e-3, atol=2e-4, msg=n)
     for (n, ba), bb in zip(a.named_buffers(), b.buffers()):
         torch.testing.assert_close(bb.float(), ba.float(), rtol=1e-4, atol=1e-5, msg=n)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_fused_resnet18_mfma_convs_close_to_torch():
+    """Fused BN + every conv / the fc on the MFMA kernels (bf16 operands) vs the same model in
+    fp32: the error is of the same size as torch's own bf16-autocast error."""
+    from layer_wise_aaai20_amd.models.resnet import resnet18
+    torch.manual_seed(0)
+    r = resnet18().cuda().to(memory_format=torch.channels_last)      # fp32 reference
+    a = resnet18().cuda().to(memory_format=torch.channels_last)      # torch, bf16 autocast
+    b = resnet18().cuda().to(memory_format=torch.channels_last)      # fused, MFMA kernels
+    a.load_state_dict(r.state_dict())
+    b.load_state_dict(r.state_dict())
+    fuse_resnet(b)
+    x = torch.randn(8, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    yr = r(x)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ya, yb = a(x), b(x)
+    ea, eb = _rel(ya, yr), _rel(yb, yr)
+    assert eb < 2 * ea + 1e-2, (ea, eb)
+    yr.square().mean().backward()
+    ya.float().square().mean().backward()
+    yb.float().square().mean().backward()
+    for (n, pr), pa, pb in zip(r.named_parameters(), a.parameters(), b.parameters()):
+        ga, gb = _rel(pa.grad, pr.grad), _rel(pb.grad, pr.grad)
+        assert gb < 2 * ga + 2e-2, (n, ga, gb)

@@ -489,7 +489,11 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
     C = at::empty({M, N}, A.options().dtype(odt));
   }
   TORCH_CHECK(!accumulate || !out_bf16, "accumulate is for fp32 outputs");
+  TORCH_CHECK(A.numel() * 2 < (1LL << 31) && B.numel() * 2 < (1LL << 31),
+              "gemm operands must be < 2 GiB (32-bit buffer offsets)");
   lw::GemmArgs g{};
+  g.a_bytes = (uint32_t)(A.numel() * 2);
+  g.b_bytes = (uint32_t)(B.numel() * 2);
   g.A = ptr<uint16_t>(A);
   g.lda = lda;
   g.a_kcontig = a_kcontig;
@@ -631,6 +635,8 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
     }
   }
   TORCH_CHECK(N > 0 && N % 8 == 0, "conv GEMM N must be a positive multiple of 8");
+  TORCH_CHECK(G.numel() * 2 < (1LL << 31) && Op.numel() * 2 < (1LL << 31),
+              "conv operands must be < 2 GiB (32-bit buffer offsets)");
   lw::GemmArgs g{};
   g.tile = (int)tile;
   g.out_bf16 = out_bf16;
@@ -650,6 +656,8 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
     g.M = (int)Mmax;
     g.K = *std::max_element(h.K, h.K + h.nclass);   // one K range per workgroup: the largest
     g.A = ptr<uint16_t>(G);
+    g.a_bytes = (uint32_t)(G.numel() * 2);
+    g.b_bytes = (uint32_t)(Op.numel() * 2);
     g.lda = h.C;
     g.a_kcontig = true;
     g.B = ptr<uint16_t>(Op);
@@ -667,6 +675,8 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
     g.K = h.M[0];                              // reduction over the output pixels
     TORCH_CHECK(Op.numel() >= (int64_t)g.K * g.M, "dY smaller than pixels x Co");
     g.A = ptr<uint16_t>(Op);
+    g.a_bytes = (uint32_t)(Op.numel() * 2);
+    g.b_bytes = (uint32_t)(G.numel() * 2);
     g.lda = g.M;
     g.a_kcontig = false;
     g.B = ptr<uint16_t>(G);
@@ -693,7 +703,7 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
   g.C = C.data_ptr();
   g.ldc = ldc;
   if (pro_scale.has_value() && pro_scale->defined()) {
-    TORCH_CHECK(!c4 && (ga ? b_kcontig : true), "BN prologue: forward or weight gradient, C % 8");
+    TORCH_CHECK(ga && b_kcontig && !c4, "BN prologue: forward convs with C % 8 == 0 only");
     TORCH_CHECK(pro_shift.has_value() && pro_shift->defined(), "prologue needs scale and shift");
     for (const Tensor* t : {&*pro_scale, &*pro_shift}) {
       check_dtype(*t, at::kFloat, "prologue");

@@ -19,8 +19,7 @@
 //             back to their pixels by the epilogue's row map.
 //   wgrad     dW[co][(r, s, ci)] = Σ_pix dy[pix][co] · im2col(x)[pix][(r, s, ci)]; the reduction
 //             over N·Ho·Wo pixels is split over workgroups (fixed-order slab reduce) and the fp32
-//             result is accumulated straight into the gradient arena; the input's BN-apply+ReLU
-//             is recomputed in the staging prologue.
+//             result is accumulated straight into the gradient arena.
 //   C == 4    (a 3-channel image padded to 4): the 16-byte chunk is two horizontally adjacent
 //             taps of one pixel pair, so the stem conv runs on the same kernel.
 #include "gemm_core.h"
@@ -61,14 +60,9 @@ static void conv_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, hip
   } else if constexpr (CVM == CV_A4) {
     if (epi == EPI_STATS) LW_LAUNCH(true, true, EPI_STATS, PRO_NONE, CV_A4);
     else LW_LAUNCH(true, true, EPI_STORE, PRO_NONE, CV_A4);
-  } else if constexpr (CVM == CV_B) {
-    if (epi == EPI_PARTIAL) {
-      if (pro) LW_LAUNCH(false, false, EPI_PARTIAL, PRO_B, CV_B);
-      else LW_LAUNCH(false, false, EPI_PARTIAL, PRO_NONE, CV_B);
-    } else {
-      if (pro) LW_LAUNCH(false, false, EPI_STORE, PRO_B, CV_B);
-      else LW_LAUNCH(false, false, EPI_STORE, PRO_NONE, CV_B);
-    }
+  } else if constexpr (CVM == CV_B) {            // (no prologue: the caller materialises)
+    if (epi == EPI_PARTIAL) LW_LAUNCH(false, false, EPI_PARTIAL, PRO_NONE, CV_B);
+    else LW_LAUNCH(false, false, EPI_STORE, PRO_NONE, CV_B);
   } else {
     if (epi == EPI_PARTIAL) LW_LAUNCH(false, false, EPI_PARTIAL, PRO_NONE, CV_B4);
     else LW_LAUNCH(false, false, EPI_STORE, PRO_NONE, CV_B4);
@@ -123,6 +117,8 @@ void conv_gemm(const GemmArgs& g, const ConvGeomHost& cvh, int mode, hipStream_t
   GemmK k{g.A, g.B, g.C, g.partial, g.stats, nullptr, g.pro_scale, g.pro_shift, nullptr, nullptr,
           g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, 0, g.out_bf16 ? 1 : 0, g.accumulate ? 1 : 0};
   k.cv = to_device(cvh);
+  k.a_bytes = g.a_bytes;
+  k.b_bytes = g.b_bytes;
   const dim3 grid(tiles, zs, cvh.nclass);
   switch (mode) {
     case CV_A: conv_dispatch<CV_A>(g, k, epi, grid, st); break;

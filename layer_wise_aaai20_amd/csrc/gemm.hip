@@ -426,6 +426,8 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
   GemmK k{g.A, g.B, g.C, g.partial, g.stats, zs > 1 ? nullptr : g.bias, g.pro_scale, g.pro_shift,
           g.addend, g.add_bits, g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, zs > 1 ? 0 : g.relu,
           g.out_bf16 ? 1 : 0, g.accumulate ? 1 : 0};
+  k.a_bytes = g.a_bytes;
+  k.b_bytes = g.b_bytes;
   const dim3 grid(tiles, zs);
   switch (t) {
     case GEMM_T128x128x64: launch_tile<128, 128, 64>(g, k, epi, grid, st); break;

@@ -59,16 +59,29 @@ __device__ __forceinline__ float masked_addend1(const uint16_t* __restrict__ add
   return __uint_as_float((uint32_t)add[e] << 16);
 }
 
-// R = extent of the tile along m (A) or n (B). KC tiles are stored [R][BK+PAD], the others
-// [BK][R+PAD]; both are moved as 16-byte chunks of 8 contiguous elements.
+// R = extent of the tile along m (A) or n (B). K-contiguous (KC) tiles are stored [R][BK]: at
+// BK = 64 unpadded with the 16-byte chunks of row r XOR-swizzled by (r & 7) (conflict-free
+// ds_read_b128 fragment reads and ds_write_b128 row stores, cdna_hip_programming.md T2), at
+// BK = 32 padded to BK + 8. The M/N-contiguous tiles are stored [BK][R+PAD] and read with the
+// transposing ds_read_b64_tr_b16. Both are moved as 16-byte chunks of 8 contiguous elements.
 template <int R, int BK, bool KC> struct Tile {
-  static constexpr int LD = KC ? BK + PAD : R + PAD;
+  static constexpr bool SWZ = KC && BK == 64;
+  static constexpr int LD = KC ? (SWZ ? BK : BK + PAD) : R + PAD;
   static constexpr int ELEMS = KC ? R * LD : BK * LD;
   static constexpr int CPR = KC ? BK / 8 : R / 8;     // chunks per stored row
   static constexpr int PER_T = R * BK / 8 / GT;       // chunks per thread
   static_assert(R * BK / 8 % GT == 0, "tile must split evenly over the workgroup");
 };
 
+// element offset of chunk c of stored row r
+template <int R, int BK, bool KC>
+__device__ __forceinline__ int tile_off(int r, int c) {
+  using T = Tile<R, BK, KC>;
+  return r * T::LD + (T::SWZ ? (c ^ (r & 7)) : c) * 8;
+}
+
+// Chunk i of the workgroup (thread t stages chunks t + h*GT): stored row rr, chunk column cc.
+// GT is a multiple of CPR, so a thread's chunks all share one column.
 template <int R, int BK, bool KC>
 __device__ __forceinline__ void chunk_pos(int c, int& rr, int& cc) {
   using T = Tile<R, BK, KC>;
@@ -76,36 +89,63 @@ __device__ __forceinline__ void chunk_pos(int c, int& rr, int& cc) {
   cc = c % T::CPR;
 }
 
-// Global -> registers. `cont` returns the contiguous-dimension index of each chunk (k for KC,
-// m/n otherwise) for the prologue; `ok` marks chunks inside the matrix (others are zero).
-template <int R, int BK, bool KC>
-__device__ __forceinline__ void load_tile(const uint16_t* __restrict__ P, int64_t ld, int row0,
-                                          int rows_total, int k0, int kend,
-                                          uint4 (&r)[Tile<R, BK, KC>::PER_T],
-                                          int (&cont)[Tile<R, BK, KC>::PER_T], uint32_t& okmask) {
-  using T = Tile<R, BK, KC>;
-  okmask = 0;
-#pragma unroll
-  for (int h = 0; h < T::PER_T; ++h) {
-    int rr, cc;
-    chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
-    int64_t off;
-    bool ok;
-    if (KC) {
-      const int gr = row0 + rr, gk = k0 + cc * 8;
-      ok = gr < rows_total && gk < kend;
-      off = (int64_t)gr * ld + gk;
-      cont[h] = gk;
-    } else {
-      const int gk = k0 + rr, gr = row0 + cc * 8;
-      ok = gk < kend && gr < rows_total;
-      off = (int64_t)gk * ld + gr;
-      cont[h] = gr;
-    }
-    r[h] = ok ? *reinterpret_cast<const uint4*>(P + off) : make_uint4(0, 0, 0, 0);
-    okmask |= (ok ? 1u : 0u) << h;
-  }
+// ---- global loads: raw buffer loads. A chunk that must read as zero (outside the matrix, the K
+// tail, the convolution padding) gets an offset past the buffer's end, and the hardware's range
+// check returns zeros: no branches, no selects on the data.
+constexpr uint32_t OOB = 0x80000000u;      // every operand is < 2 GiB (checked on the host)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
+
+__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+}
+__device__ __forceinline__ uint2 bload8(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0));
+}
+
+// Plain operand tile: byte offset of each of this thread's chunks at k = 0 (OOB outside the
+// matrix); a K-step adds k*2 (KC) or k*ld*2 (M/N-contiguous) and masks the K tail.
+template <int R, int BK, bool KC>
+struct PlainLoader {
+  static constexpr int PT = Tile<R, BK, KC>::PER_T;
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t voff[PT];
+  int kpos[PT];       // k of each chunk within the step (KC: the chunk column, else its row)
+  uint32_t ld2;
+
+  __device__ __forceinline__ void init(const uint16_t* P, uint32_t bytes, int64_t ld, int row0,
+                                       int rows) {
+    rs = make_rsrc(P, bytes);
+    ld2 = (uint32_t)(ld * 2);
+#pragma unroll
+    for (int h = 0; h < PT; ++h) {
+      int rr, cc;
+      chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
+      if (KC) {
+        const int gr = row0 + rr;
+        voff[h] = gr < rows ? (uint32_t)(((int64_t)gr * ld + cc * 8) * 2) : OOB;
+        kpos[h] = cc * 8;
+      } else {
+        const int gc = row0 + cc * 8;
+        voff[h] = gc < rows ? (uint32_t)((int64_t)rr * ld * 2 + gc * 2) : OOB;
+        kpos[h] = rr;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(uint4 (&r)[PT], uint32_t (&okmask), int k, int kend) const {
+    const uint32_t kb = KC ? (uint32_t)k * 2u : (uint32_t)k * ld2;
+    okmask = 0;
+#pragma unroll
+    for (int h = 0; h < PT; ++h) {
+      const bool ok = voff[h] != OOB && k + kpos[h] < kend;
+      r[h] = bload16(rs, ok ? voff[h] + kb : OOB);
+      okmask |= (ok ? 1u : 0u) << h;
+    }
+  }
+};
 
 // Prologue coefficients of the 8 channels one thread's chunks cover. Every chunk a thread stages
 // has the same contiguous-dimension offset within the tile (the chunks-per-row count divides the
@@ -155,7 +195,7 @@ __device__ __forceinline__ void store_tile(uint16_t* __restrict__ S,
     chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
     uint4 v = r[h];
     if (PRO && ((okmask >> h) & 1u)) v = affine_relu8(v, co);
-    *reinterpret_cast<uint4*>(S + rr * T::LD + cc * 8) = v;
+    *reinterpret_cast<uint4*>(S + tile_off<R, BK, KC>(rr, cc)) = v;
   }
 }
 
@@ -166,7 +206,7 @@ __device__ __forceinline__ bf16x8 load_frag(const uint16_t* S, int i_base, int s
   using T = Tile<R, BK, KC>;
   const int l = threadIdx.x & 63;
   if (KC) {
-    const uint16_t* p = S + (i_base + (l & 15)) * T::LD + 32 * s + 8 * (l >> 4);
+    const uint16_t* p = S + tile_off<R, BK, KC>(i_base + (l & 15), 4 * s + (l >> 4));
     return *reinterpret_cast<const bf16x8*>(p);
   } else {
     const int g = l >> 4, t = l & 15, q = t >> 2, p4 = t & 3;
@@ -236,10 +276,11 @@ struct GemmK {
   int64_t lda, ldb, ldc;
   int M, N, K, k_per_split, relu, out_bf16, accumulate;   // accumulate: fp32 C += result
   ConvGeom cv;                 // CV_* kernels only
+  uint32_t a_bytes, b_bytes;   // operand extents for the buffer loads' range check
 };
 
 // q = a / d, r = a % d for 0 <= a < 2^24 via the fp32 reciprocal (one correction step each way:
-// the estimate is off by at most one) — the per-chunk pixel decode of the gathers.
+// the estimate is off by at most one) — the per-thread pixel decode of the B gather.
 __device__ __forceinline__ int fdivmod(int a, int d, float inv, int& r) {
   int q = (int)((float)a * inv);
   r = a - q * d;
@@ -248,19 +289,30 @@ __device__ __forceinline__ int fdivmod(int a, int d, float inv, int& r) {
   return q;
 }
 
-// ---- A-gather (im2col rows): per-thread row state, fixed for the whole K loop
+// ---- A-gather (im2col rows), K-contiguous tile. Per thread and chunk, fixed for the K loop:
+// the byte offset of the chunk's pixel at tap (0, 0) and channel cc*8, and the pixel's window
+// origin (hb, wb; rows past the class's M get an origin that fails every bounds test).
+// Per K-step with C % BK == 0 the whole step lies in one tap: tap and first channel are uniform
+// (scalar unit), and a chunk costs an add, two bounds tests and a select. Otherwise (C == 4, the
+// image; or C < BK) every chunk decodes its own tap.
 template <int R, int BK>
 struct RowGather {
   static constexpr int PT = Tile<R, BK, true>::PER_T;
-  int base[PT];   // b*Hin*Win, or -1 for rows past the class's M
+  __amdgpu_buffer_rsrc_t rs;
+  int rowoff[PT];       // bytes; may be negative (window origin in the padding)
   int hb[PT], wb[PT];
+  int kc;               // this thread's k offset within a step (cc*8)
+  int ci0, js, jr;      // fast path: tap and first channel of the next K-step (uniform)
 };
 
 template <int R, int BK>
-__device__ __forceinline__ void row_gather_init(RowGather<R, BK>& g, const ConvGeom& cv,
+__device__ __forceinline__ void row_gather_init(RowGather<R, BK>& g, const uint16_t* X,
+                                                uint32_t bytes, const ConvGeom& cv,
                                                 const ConvClass& cc, int m0) {
   using T = Tile<R, BK, true>;
+  g.rs = make_rsrc(X, bytes);
   const int hw = cc.Hg * cc.Wg;
+  g.kc = (threadIdx.x % T::CPR) * 8;
 #pragma unroll
   for (int h = 0; h < T::PER_T; ++h) {
     int rr, c8;
@@ -270,110 +322,169 @@ __device__ __forceinline__ void row_gather_init(RowGather<R, BK>& g, const ConvG
     const int mm = in ? m : 0;                   // (branch-free: see load_coef8)
     const int b = mm / hw, rem = mm - b * hw;
     const int y = rem / cc.Wg, x = rem - y * cc.Wg;
-    g.base[h] = in ? b * cv.Hin * cv.Win : -1;
-    g.hb[h] = y * cv.sh + cc.oh;
-    g.wb[h] = x * cv.sw + cc.ow;
+    const int h0 = y * cv.sh + cc.oh, w0 = x * cv.sw + cc.ow;
+    g.hb[h] = in ? h0 : -(1 << 28);
+    g.wb[h] = w0;
+    g.rowoff[h] = (((b * cv.Hin + h0) * cv.Win + w0) * cv.C + g.kc) * 2;
   }
 }
 
-// K-contiguous A tile of an im2col matrix: chunk = 8 consecutive channels of one pixel and tap
-// (C % 8 == 0), or — C4 — two horizontally adjacent taps of a 4-channel pixel (TS even). `ci`
-// returns the first channel of each chunk for the BN prologue.
+// fast path: position the uniform tap walk at K-step k (divisions once per kernel)
+template <int R, int BK>
+__device__ __forceinline__ void row_gather_seek(RowGather<R, BK>& g, const ConvGeom& cv,
+                                                const ConvClass& cc, int k) {
+  const int t = k / cv.C;
+  g.ci0 = k - t * cv.C;
+  g.jr = t / cc.TS;
+  g.js = t - g.jr * cc.TS;
+}
+
 template <int R, int BK, bool C4>
-__device__ __forceinline__ void load_tile_gather_a(const uint16_t* __restrict__ X, const ConvGeom& cv,
-                                                   const ConvClass& cc, const RowGather<R, BK>& g,
-                                                   int k0, int kend,
+__device__ __forceinline__ void load_tile_gather_a(const ConvGeom& cv, const ConvClass& cc,
+                                                   RowGather<R, BK>& g, int k, int kend,
                                                    uint4 (&r)[Tile<R, BK, true>::PER_T],
                                                    int& ci_out, uint32_t& okmask) {
   using T = Tile<R, BK, true>;
-  const int kk = k0 + (threadIdx.x % T::CPR) * 8;   // same for all of this thread's chunks
+  okmask = 0;
+  const bool kin = k + g.kc < kend;
+  if (!C4 && cv.C % BK == 0) {
+    // the whole K-step lies in one tap: uniform tap / channel arithmetic, walked incrementally
+    // (the K-steps are fetched in order; row_gather_seek positioned the walk at the first)
+    const int ho = cv.dh * g.jr, wo = cv.dw * g.js;
+    const int delta = ((ho * cv.Win + wo) * cv.C + g.ci0) * 2;
+    ci_out = g.ci0 + g.kc;
+    g.ci0 += BK;
+    if (g.ci0 >= cv.C) {
+      g.ci0 = 0;
+      if (++g.js == cc.TS) { g.js = 0; ++g.jr; }
+    }
+#pragma unroll
+    for (int h = 0; h < T::PER_T; ++h) {
+      const bool ok = kin && (unsigned)(g.hb[h] + ho) < (unsigned)cv.Hin &&
+                      (unsigned)(g.wb[h] + wo) < (unsigned)cv.Win;
+      r[h] = bload16(g.rs, ok ? (uint32_t)(g.rowoff[h] + delta) : OOB);
+      okmask |= (ok ? 1u : 0u) << h;
+    }
+    return;
+  }
+  // per-thread tap decode (the chunk's k is k + kc)
+  const int kk = k + g.kc;
   int t, ci;
   if (C4) { t = kk >> 2; ci = 0; }
   else { t = kk / cv.C; ci = kk - t * cv.C; }
   const int jr = t / cc.TS, js = t - jr * cc.TS;
-  const int hoff = cv.dh * jr, woff = cv.dw * js;
-  const bool kin = kk < kend;
+  const int ho = cv.dh * jr, wo = cv.dw * js;
+  // rowoff holds channel kc: rebase it on (tap, ci)
+  const int delta = ((ho * cv.Win + wo) * cv.C + ci - g.kc) * 2;
   ci_out = ci;
-  okmask = 0;
 #pragma unroll
   for (int h = 0; h < T::PER_T; ++h) {
-    const int hi = g.hb[h] + hoff, wi = g.wb[h] + woff;
-    const bool row_ok = kin && g.base[h] >= 0 && (unsigned)hi < (unsigned)cv.Hin;
+    const int hi = g.hb[h] + ho, wi = g.wb[h] + wo;
+    const bool row_ok = kin && (unsigned)hi < (unsigned)cv.Hin;
+    const uint32_t off = (uint32_t)(g.rowoff[h] + delta);
     if (C4) {
-      // pixels wi and wi + dw, 4 channels (8 bytes) each
-      const int wi2 = wi + cv.dw;
+      // pixels wi and wi + dw of a 4-channel (8-byte) image
       const bool ok0 = row_ok && (unsigned)wi < (unsigned)cv.Win;
-      const bool ok1 = row_ok && (unsigned)wi2 < (unsigned)cv.Win;
-      const int64_t rowpix = (int64_t)g.base[h] + (int64_t)hi * cv.Win;
-      const uint2 a = ok0 ? *reinterpret_cast<const uint2*>(X + (rowpix + wi) * 4) : make_uint2(0, 0);
-      const uint2 b = ok1 ? *reinterpret_cast<const uint2*>(X + (rowpix + wi2) * 4) : make_uint2(0, 0);
+      const bool ok1 = row_ok && (unsigned)(wi + cv.dw) < (unsigned)cv.Win;
+      const uint2 a = bload8(g.rs, ok0 ? off : OOB);
+      const uint2 b = bload8(g.rs, ok1 ? off + cv.dw * 8 : OOB);
       r[h] = make_uint4(a.x, a.y, b.x, b.y);
       okmask |= (ok0 || ok1 ? 1u : 0u) << h;
     } else {
       const bool ok = row_ok && (unsigned)wi < (unsigned)cv.Win;
-      const int64_t off = ((int64_t)g.base[h] + (int64_t)hi * cv.Win + wi) * cv.C + ci;
-      r[h] = ok ? *reinterpret_cast<const uint4*>(X + off) : make_uint4(0, 0, 0, 0);
+      r[h] = bload16(g.rs, ok ? off : OOB);
       okmask |= (ok ? 1u : 0u) << h;
     }
   }
 }
 
-// ---- B-gather (weight gradient): N-contiguous B tile whose rows are pixels of the output grid
-// and whose chunks are (tap, 8 channels) — or C4: (tap pair, 4 channels) — of the input.
+// ---- B-gather (weight gradient): N-contiguous tile whose rows are output pixels and whose
+// chunks are (tap, 8 channels) — or C4: (tap pair, 4 channels) — of the input. Here a thread
+// stages PER_T chunks of ONE row (row-major chunk order instead of chunk_pos), so the pixel
+// decode is done once per thread per K-step.
+template <int R, int BK>
 struct ColGather {
-  int hoff, woff, ci;   // tap offsets (origin included) and first channel of this thread's chunk
-  bool ok;
+  static constexpr int PT = Tile<R, BK, false>::PER_T;
+  static constexpr int TPR = Tile<R, BK, false>::CPR / PT;   // threads per stored row
+  static_assert(Tile<R, BK, false>::CPR % PT == 0, "row-major B gather split");
+  __amdgpu_buffer_rsrc_t rs;
+  int tapoff[PT];       // bytes: (hoff*Win + woff)*C*2 + ci*2
+  int hoff[PT], woff[PT];
+  uint32_t nok;         // chunk h inside N
+  int rr;               // this thread's row within the K-step
+  int hw;
+  float inv_hw, inv_w;
 };
 
 template <int R, int BK, bool C4>
-__device__ __forceinline__ void col_gather_init(ColGather& g, const ConvGeom& cv, const ConvClass& cc,
-                                                int n0, int N) {
-  using T = Tile<R, BK, false>;
-  const int nn = n0 + (threadIdx.x % T::CPR) * 8;
-  int t, ci;
-  if (C4) { t = nn >> 2; ci = 0; }
-  else { t = nn / cv.C; ci = nn - t * cv.C; }
-  const int jr = t / cc.TS, js = t - jr * cc.TS;
-  g.hoff = cc.oh + cv.dh * jr;
-  g.woff = cc.ow + cv.dw * js;
-  g.ci = ci;
-  g.ok = nn < N;
+__device__ __forceinline__ void col_gather_init(ColGather<R, BK>& g, const uint16_t* X,
+                                                uint32_t bytes, const ConvGeom& cv,
+                                                const ConvClass& cc, int n0, int N) {
+  using G = ColGather<R, BK>;
+  g.rs = make_rsrc(X, bytes);
+  g.rr = threadIdx.x / G::TPR;
+  g.hw = cc.Hg * cc.Wg;
+  g.inv_hw = 1.f / (float)g.hw;
+  g.inv_w = 1.f / (float)cc.Wg;
+  g.nok = 0;
+#pragma unroll
+  for (int h = 0; h < G::PT; ++h) {
+    const int nn = n0 + ((threadIdx.x % G::TPR) * G::PT + h) * 8;
+    int t, ci;
+    if (C4) { t = nn >> 2; ci = 0; }
+    else { t = nn / cv.C; ci = nn - t * cv.C; }
+    const int jr = t / cc.TS, js = t - jr * cc.TS;
+    g.hoff[h] = cc.oh + cv.dh * jr;
+    g.woff[h] = cc.ow + cv.dw * js;
+    g.tapoff[h] = ((g.hoff[h] * cv.Win + g.woff[h]) * cv.C + ci) * 2;
+    g.nok |= (nn < N ? 1u : 0u) << h;
+  }
 }
 
 template <int R, int BK, bool C4>
-__device__ __forceinline__ void load_tile_gather_b(const uint16_t* __restrict__ X, const ConvGeom& cv,
-                                                   const ConvClass& cc, const ColGather& g,
-                                                   int hw, float inv_hw, float inv_w, int k0,
-                                                   int kend, uint4 (&r)[Tile<R, BK, false>::PER_T],
+__device__ __forceinline__ void load_tile_gather_b(const ConvGeom& cv, const ColGather<R, BK>& g,
+                                                   int k, int kend,
+                                                   uint4 (&r)[Tile<R, BK, false>::PER_T],
                                                    uint32_t& okmask) {
-  using T = Tile<R, BK, false>;
+  using G = ColGather<R, BK>;
+  const int pix = k + g.rr;
+  int rem, x;
+  const int b = fdivmod(pix, g.hw, g.inv_hw, rem);
+  const int y = fdivmod(rem, cv.cls[0].Wg, g.inv_w, x);
+  const int yb = y * cv.sh, xb = x * cv.sw;
+  const int base = ((b * cv.Hin + yb) * cv.Win + xb) * cv.C * 2;
+  const bool pok = pix < kend;
   okmask = 0;
 #pragma unroll
-  for (int h = 0; h < T::PER_T; ++h) {
-    int rr, c8;
-    chunk_pos<R, BK, false>(threadIdx.x + h * GT, rr, c8);
-    const int pix = k0 + rr;
-    int rem, x;
-    const int b = fdivmod(pix, hw, inv_hw, rem);
-    const int y = fdivmod(rem, cc.Wg, inv_w, x);
-    const int hi = y * cv.sh + g.hoff, wi = x * cv.sw + g.woff;
-    const bool row_ok = g.ok && pix < kend && (unsigned)hi < (unsigned)cv.Hin;
-    const int64_t rowpix = (int64_t)b * cv.Hin * cv.Win + (int64_t)hi * cv.Win;
+  for (int h = 0; h < G::PT; ++h) {
+    const int hi = yb + g.hoff[h], wi = xb + g.woff[h];
+    const bool row_ok = pok && ((g.nok >> h) & 1u) && (unsigned)hi < (unsigned)cv.Hin;
+    const uint32_t off = (uint32_t)(base + g.tapoff[h]);
     if (C4) {
-      const int wi2 = wi + cv.dw;
       const bool ok0 = row_ok && (unsigned)wi < (unsigned)cv.Win;
-      const bool ok1 = row_ok && (unsigned)wi2 < (unsigned)cv.Win;
-      const uint2 a = ok0 ? *reinterpret_cast<const uint2*>(X + (rowpix + wi) * 4) : make_uint2(0, 0);
-      const uint2 c = ok1 ? *reinterpret_cast<const uint2*>(X + (rowpix + wi2) * 4) : make_uint2(0, 0);
+      const bool ok1 = row_ok && (unsigned)(wi + cv.dw) < (unsigned)cv.Win;
+      const uint2 a = bload8(g.rs, ok0 ? off : OOB);
+      const uint2 c = bload8(g.rs, ok1 ? off + cv.dw * 8 : OOB);
       r[h] = make_uint4(a.x, a.y, c.x, c.y);
       okmask |= (ok0 || ok1 ? 1u : 0u) << h;
     } else {
       const bool ok = row_ok && (unsigned)wi < (unsigned)cv.Win;
-      r[h] = ok ? *reinterpret_cast<const uint4*>(X + (rowpix + wi) * cv.C + g.ci)
-                : make_uint4(0, 0, 0, 0);
+      r[h] = bload16(g.rs, ok ? off : OOB);
       okmask |= (ok ? 1u : 0u) << h;
     }
   }
+}
+
+// store of a B-gather tile (row-major chunk order, see ColGather)
+template <int R, int BK>
+__device__ __forceinline__ void store_tile_rows(uint16_t* __restrict__ S,
+                                                const uint4 (&r)[Tile<R, BK, false>::PER_T]) {
+  using T = Tile<R, BK, false>;
+  using G = ColGather<R, BK>;
+  const int rr = threadIdx.x / G::TPR, c0 = (threadIdx.x % G::TPR) * G::PT;
+#pragma unroll
+  for (int h = 0; h < G::PT; ++h)
+    *reinterpret_cast<uint4*>(S + rr * T::LD + (c0 + h) * 8) = r[h];
 }
 
 // Workgroup id → (m-tile, n-tile): consecutive ids are dealt round-robin to the 8 XCDs, so remap
@@ -431,48 +542,48 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[TA::PER_T], rb[TB::PER_T];
-  int ca[TA::PER_T], cb[TB::PER_T];
-  uint32_t oka = 0, okb = 0;
-  int cur = 0;
-  Coef8 coA, coB;
+  // One register staging set: the next K-step's global loads are issued before this step's
+  // MFMAs and written to the other LDS buffer after them. (A second set — loads two steps
+  // ahead — measured no faster: the loop is bound by the L2→CU operand traffic of the tile,
+  // not by load latency; profiles/r2_conv_fusion_variants.log.)
+  struct Regs {
+    uint4 a[TA::PER_T], b[TB::PER_T];
+    uint32_t oka, okb;
+    Coef8 coA;
+  };
+  Regs R0;
+  Coef8 coB;
   RowGather<BM, BK> rg;
-  ColGather colg;
-  int g_hw = 1;
-  float g_inv_hw = 1.f, g_inv_w = 1.f;
-  if constexpr (GA) row_gather_init<BM, BK>(rg, p.cv, ccl, m0);
-  if constexpr (GB) {
-    col_gather_init<BN, BK, G4>(colg, p.cv, ccl, n0, p.N);
-    g_hw = ccl.Hg * ccl.Wg;
-    g_inv_hw = 1.f / (float)g_hw;
-    g_inv_w = 1.f / (float)ccl.Wg;
+  ColGather<BN, BK> cg;
+  PlainLoader<BM, BK, AKC> la;
+  PlainLoader<BN, BK, BKC> lb;
+  if constexpr (GA) {
+    row_gather_init<BM, BK>(rg, p.A, p.a_bytes, p.cv, ccl, m0);
+    if (!G4 && p.cv.C % BK == 0) row_gather_seek<BM, BK>(rg, p.cv, ccl, kbeg);
+  } else {
+    la.init(p.A, p.a_bytes, p.lda, m0, p.M);
   }
+  if constexpr (GB) col_gather_init<BN, BK, G4>(cg, p.B, p.b_bytes, p.cv, ccl, n0, p.N);
+  else lb.init(Bp, p.b_bytes - (uint32_t)((Bp - p.B) * 2), p.ldb, n0, p.N);
+  static_assert(!GB || PRO != PRO_B, "B-gather prologue: materialise the input instead");
   if (PRO == PRO_B)        // channel n of this thread's B chunks: fixed for the whole kernel
-    load_coef8(coB, p.pro_scale, p.pro_shift,
-               GB ? colg.ci : n0 + (threadIdx.x % TB::CPR) * 8, GB ? p.cv.C : p.N);
+    load_coef8(coB, p.pro_scale, p.pro_shift, n0 + (threadIdx.x % TB::CPR) * 8, p.N);
   const int a_koff = (threadIdx.x % TA::CPR) * 8;      // PRO_A: k offset within a K-step
   // global -> registers for the K-step at k (and, PRO_A, its prologue coefficients)
-  auto fetch = [&](int k) {
+  auto fetch = [&](int k, Regs& r) {
     int a_ch = k + a_koff;
-    if constexpr (GA) load_tile_gather_a<BM, BK, G4>(p.A, p.cv, ccl, rg, k, kend, ra, a_ch, oka);
-    else load_tile<BM, BK, AKC>(p.A, p.lda, m0, p.M, k, kend, ra, ca, oka);
-    if constexpr (GB)
-      load_tile_gather_b<BN, BK, G4>(Bp, p.cv, ccl, colg, g_hw, g_inv_hw, g_inv_w, k, kend, rb, okb);
-    else load_tile<BN, BK, BKC>(Bp, p.ldb, n0, p.N, k, kend, rb, cb, okb);
-    if (PRO == PRO_A) load_coef8(coA, p.pro_scale, p.pro_shift, a_ch, GA ? p.cv.C : kend);
+    if constexpr (GA) load_tile_gather_a<BM, BK, G4>(p.cv, ccl, rg, k, kend, r.a, a_ch, r.oka);
+    else la.load(r.a, r.oka, k, kend);
+    if constexpr (GB) load_tile_gather_b<BN, BK, G4>(p.cv, cg, k, kend, r.b, r.okb);
+    else lb.load(r.b, r.okb, k, kend);
+    if (PRO == PRO_A) load_coef8(r.coA, p.pro_scale, p.pro_shift, a_ch, GA ? p.cv.C : kend);
   };
-  if (kbeg < kend) {
-    fetch(kbeg);
-    store_tile<BM, BK, AKC, PRO == PRO_A>(st, ra, oka, coA);
-    store_tile<BN, BK, BKC, PRO == PRO_B>(st + TA::ELEMS, rb, okb, coB);
-  }
-  __syncthreads();
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
-    const bool more = k0 + BK < kend;
-    // next stage's tiles (and prologue coefficients) travel during the MFMAs below; coA is
-    // free: the current stage was normalised when it was staged
-    if (more) fetch(k0 + BK);
-    const uint16_t* As = st + cur * STAGE;
+  auto stage = [&](uint16_t* dst, const Regs& r) {
+    store_tile<BM, BK, AKC, PRO == PRO_A>(dst, r.a, r.oka, r.coA);
+    if constexpr (GB) store_tile_rows<BN, BK>(dst + TA::ELEMS, r.b);
+    else store_tile<BN, BK, BKC, PRO == PRO_B>(dst + TA::ELEMS, r.b, r.okb, coB);
+  };
+  auto compute = [&](const uint16_t* As) {
     const uint16_t* Bs = As + TA::ELEMS;
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
@@ -487,11 +598,19 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      uint16_t* nx = st + (cur ^ 1) * STAGE;
-      store_tile<BM, BK, AKC, PRO == PRO_A>(nx, ra, oka, coA);
-      store_tile<BN, BK, BKC, PRO == PRO_B>(nx + TA::ELEMS, rb, okb, coB);
-    }
+  };
+  const int nsteps = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nsteps > 0) {
+    fetch(kbeg, R0);
+    stage(st, R0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int i = 0; i < nsteps; ++i) {
+    const bool more = i + 1 < nsteps;
+    if (more) fetch(kbeg + (i + 1) * BK, R0);
+    compute(st + cur * STAGE);
+    if (more) stage(st + (cur ^ 1) * STAGE, R0);
     __syncthreads();
     cur ^= 1;
   }

@@ -190,6 +190,7 @@ struct GemmArgs {
   const uint16_t* addend;  // optional bf16 [M][ldc] added to a bf16 output (dgrad + residual grad)
   const uint8_t* add_bits; // optional ReLU bitmap masking the addend (ldc == N)
   bool accumulate;         // fp32 output: C += result (weight gradients into the zeroed arena)
+  uint32_t a_bytes, b_bytes;  // operand extents (< 2 GiB): the buffer loads' range check
 };
 enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_T256x64x32 = 3,
                 GEMM_T64x256x32 = 4, GEMM_T256x64x64 = 5,

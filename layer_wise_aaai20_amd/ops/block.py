@@ -55,6 +55,10 @@ from .conv import conv_dgrad, conv_fwd, conv_wgrad
 
 BF16 = torch.bfloat16
 CL = torch.channels_last
+# materialise relu(bn1(c1)) / relu(bn2(c2)) with one apply pass instead of re-normalising in the
+# consumers' staging prologues (see _BottleneckFn.forward)
+MAT_A1 = os.environ.get("LWAAAI_MAT_A1", "1") != "0"
+MAT_A2 = os.environ.get("LWAAAI_MAT_A2", "1") != "0"
 TILES = (1, 2, 3, 4, 5, 6)          # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
 
@@ -240,18 +244,26 @@ class _BottleneckFn(torch.autograd.Function):
         c1, st1 = gemm(xr, Cin, True, W1, Cin, True, M, width, Cin, stats=True)
         mean1, inv1, ss1 = lib.bn_stats(c1, st1, g1, b1, bn1.running_mean, bn1.running_var,
                                         _bn_momentum(bn1), bn1.eps)
-        # conv2 (3x3, implicit GEMM): relu(bn1(c1)) is applied while the window is staged
-        # (a1 never exists in memory) and the epilogue emits BN2's column statistics
-        c2n, st2 = conv_fwd(_nchw(c1, N, H, W), W2, stride, conv2.padding,
-                            pro=(ss1[:width], ss1[width:]), stats=True)
+        # conv2 (3x3, implicit GEMM) on a1 = relu(bn1(c1)), BN2's column statistics in its
+        # epilogue. a1 is materialised by one apply pass (MAT_A1): staging-time BN-apply would
+        # redo the affine for each of the 9 taps of every element (measured 1.6x slower conv);
+        # with MAT_A1=0 the prologue form is used instead.
+        pro1 = (ss1[:width], ss1[width:])
+        a1 = lib.bn_apply(c1, ss1, None, None, True) if MAT_A1 else None
+        c2n, st2 = conv_fwd(_nchw(a1 if MAT_A1 else c1, N, H, W), W2, stride, conv2.padding,
+                            pro=None if MAT_A1 else pro1, stats=True)
         N2, _, H2, W2_ = c2n.shape
         c2 = _rows(c2n)
         M2 = c2.shape[0]
         mean2, inv2, ss2 = lib.bn_stats(c2, st2, g2, b2, bn2.running_mean, bn2.running_var,
                                         _bn_momentum(bn2), bn2.eps)
-        # conv3 (1x1) with BN2-apply+ReLU in the prologue and BN3 statistics in the epilogue
-        c3, st3 = gemm(c2, width, True, W3, width, True, M2, cout, width, stats=True,
-                       pro=(ss2[:width], ss2[width:]), pro_on_a=True)
+        # conv3 (1x1): BN2-apply+ReLU in the prologue (each A row-panel is re-normalised once
+        # per output-column tile) or on a2 materialised by one apply pass (MAT_A2); BN3
+        # statistics in the epilogue
+        pro2 = (ss2[:width], ss2[width:])
+        a2 = lib.bn_apply(c2, ss2, None, None, True) if MAT_A2 else None
+        c3, st3 = gemm(a2 if MAT_A2 else c2, width, True, W3, width, True, M2, cout, width,
+                       stats=True, pro=None if MAT_A2 else pro2, pro_on_a=True)
         mean3, inv3, ss3 = lib.bn_stats(c3, st3, g3, b3, bn3.running_mean, bn3.running_var,
                                         _bn_momentum(bn3), bn3.eps)
         if bnd is not None:
@@ -265,14 +277,14 @@ class _BottleneckFn(torch.autograd.Function):
             bits3 = torch.empty(M2 * cout // 8, dtype=torch.uint8, device=x.device)
             out = lib.bn_apply(c3, ss3, cd, ssd, True, bits3)
             ctx.save_for_backward(x, c1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1,
-                                  ss1, mean2, inv2, ss2, mean3, inv3, xsr, cd, Wd, gd, meand,
-                                  invd)
+                                  ss1, mean2, inv2, ss2, mean3, inv3, a1, a2, xsr, cd, Wd, gd,
+                                  meand, invd)
             ctx.down_stride = s
         else:
             bits3 = torch.empty(M2 * cout // 8, dtype=torch.uint8, device=x.device)
             out = lib.bn_apply(c3, ss3, xr, None, True, bits3)
             ctx.save_for_backward(x, c1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1,
-                                  ss1, mean2, inv2, ss2, mean3, inv3)
+                                  ss1, mean2, inv2, ss2, mean3, inv3, a1, a2)
             ctx.down_stride = 0
         ctx.geom = (N, Cin, H, W, N2, H2, W2_, width, cout, M, M2)
         ctx.conv2 = (list(stride), list(conv2.padding), list(conv2.dilation))
@@ -284,7 +296,7 @@ class _BottleneckFn(torch.autograd.Function):
         lib = load()
         saved = ctx.saved_tensors
         x, c1, c2, c3, bits3, W1, W2, W3, g1, g2, g3, mean1, inv1, ss1, mean2, inv2, ss2, \
-            mean3, inv3 = saved[:19]
+            mean3, inv3, a1, a2 = saved[:21]
         N, Cin, H, W, N2, H2, W2_, width, cout, M, M2 = ctx.geom
         w1, g1p, b1p, w2, g2p, b2p, w3, g3p, b3p, wd, gdp, bdp = ctx.params
         has_down = ctx.down_stride > 0
@@ -297,23 +309,25 @@ class _BottleneckFn(torch.autograd.Function):
                                       bits3, o3[0], o3[1])
         grads = {}
         grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
-        # conv3: weight gradient with BN2-apply recomputed in the B prologue, into the arena
+        # conv3: weight gradient on a2 (or with BN2-apply recomputed in the B prologue), fp32
+        # accumulated into the arena
         dst3, d3 = _wgrad_target(w3, (cout, width))
-        gemm(dc3, cout, False, c2, width, False, cout, width, M2, out_bf16=False,
-             pro=(ss2[:width], ss2[width:]), pro_on_a=False, out=dst3, accumulate=True,
-             split_k=True)
+        gemm(dc3, cout, False, c2 if a2 is None else a2, width, False, cout, width, M2,
+             out_bf16=False, pro=(ss2[:width], ss2[width:]) if a2 is None else None,
+             pro_on_a=False, out=dst3, accumulate=True, split_k=True)
         grads["w3"] = _finish_wgrad(w3, dst3, d3)
         da2, _ = gemm(dc3, cout, True, W3, width, False, M2, width, cout)
         o2 = _bn_grad_outs(g2p, b2p)
         dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False,
                                       None, o2[0], o2[1])
         grads["g2"], grads["b2"] = _finish_bn(g2p, b2p, dg2, db2, o2)
-        # conv2 (3x3) backward on the implicit GEMM: the weight gradient recomputes
-        # relu(bn1(c1)) in its staging prologue and accumulates fp32 straight into the arena
+        # conv2 (3x3) backward on the implicit GEMM: the weight gradient reads a1 (or
+        # recomputes relu(bn1(c1)) in its staging prologue) and accumulates fp32 straight into
+        # the arena
         stride, padding, dilation = ctx.conv2
         dc2n = _nchw(dc2, N2, H2, W2_)
-        c1n = _nchw(c1, N, H, W)
-        pro1 = (ss1[:width], ss1[width:])
+        c1n = _nchw(c1 if a1 is None else a1, N, H, W)
+        pro1 = (ss1[:width], ss1[width:]) if a1 is None else None
         if _direct(w2) and w2.grad.is_contiguous(memory_format=CL):
             conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1, out=w2.grad)
             grads["w2"] = _finish_param(w2, None, True)
@@ -331,7 +345,7 @@ class _BottleneckFn(torch.autograd.Function):
              accumulate=True, split_k=True)
         grads["w1"] = _finish_wgrad(w1, dst1, d1)
         if has_down:
-            xsr, cd, Wd, gd, meand, invd = saved[19:]
+            xsr, cd, Wd, gd, meand, invd = saved[21:]
             s = ctx.down_stride
             od = _bn_grad_outs(gdp, bdp)
             dcd, dgd, dbd, _ = lib.bn_bwd(dr, cd, None, gd, meand, invd, None, True, True,

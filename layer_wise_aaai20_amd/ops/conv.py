@@ -222,6 +222,12 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, pro=
     ph, pw = _pair(padding)
     co, c, R, S = w_shape
     c4 = c % 8 != 0
+    if pro is not None:
+        # the input's BN-apply+ReLU, materialised once (a B-gather prologue would redo it for
+        # every tap and output-channel tile)
+        xa = x.to(BF16).contiguous(memory_format=CL)
+        x = lib.bn_apply(xa, torch.cat([pro[0][:c], pro[1][:c]]).contiguous(), None, None, True)
+        pro = None
     xin = _c4_input(x) if c4 else x.to(BF16).contiguous(memory_format=CL)
     dyc = dy.to(BF16).contiguous(memory_format=CL)
     Nb, C, H, W = xin.shape

@@ -625,8 +625,15 @@ def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qst
         c = DenseCodec(plan, world, rank, seed)
     if wire == "dense" and not isinstance(c, DenseCodec):
         return DenseWrap(c)
-    if wire == "auto" and isinstance(c, TopkCodec) and not isinstance(c, ThresholdCodec):
+    if wire == "auto" and isinstance(c, ThresholdCodec):
+        # data-dependent counts: the sparse wire needs the per-step count exchange and a host
+        # read of the agreed capacity (a sync in the middle of backward); the reference's dense
+        # wire (compressed vector, all-reduce) is exact and sync-free — `wire="sparse"` opts in
+        return DenseWrap(c)
+    if wire == "auto" and isinstance(c, TopkCodec) and c.collective == "all_gather" and \
+            not isinstance(c, ThresholdCodec):
         # pairs cost 8 B per kept element on every rank: dense all-reduce wins above ~1/world
+        # (index-free Random-K sends only its values, one all-reduce: never worth densifying)
         if c.cap_total * max(world, 2) > plan.numel:
             return DenseWrap(c)
     return c

@@ -29,6 +29,16 @@ inline T* optr(const c10::optional<Tensor>& t) {
   return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
 }
 
+// Every binding checks its launches: a bad launch configuration (or a failed async memset before
+// it) raises here, at the op that caused it, instead of surfacing later or not at all.
+// BN kernels keep one 8-channel group per thread of a 256-thread block (bn.hip)
+constexpr int64_t kMaxBnC = 8 * 256;
+
+void launched(const char* op) {
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, "HIP launch failed in lwaaai.", op, ": ", hipGetErrorString(e));
+}
+
 void check_cuda(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
@@ -133,6 +143,7 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
   a.seed0 = (uint32_t)(seed & 0xffffffff);
   a.seed1 = (uint32_t)((uint64_t)seed >> 32);
   lw::select_compress(a, (int)km, (int)out, a.ef != nullptr, cur_stream());
+  launched("select_compress");
 }
 
 void thresh_count(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
@@ -150,6 +161,7 @@ void thresh_count(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg
                    reinterpret_cast<float*>(base + L.segmax),
                    reinterpret_cast<float2*>(base + L.partial), ptr<int32_t>(counts_out),
                    cur_stream());
+  launched("thresh_count");
 }
 
 void thresh_write(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
@@ -162,6 +174,7 @@ void thresh_write(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg
   check_cuda(pairs, "pairs");
   a.pairs = ptr<int2>(pairs);
   lw::thresh_write(a, a.ef != nullptr, cur_stream());
+  launched("thresh_write");
 }
 
 void unpack_pairs(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor seg_n,
@@ -175,6 +188,7 @@ void unpack_pairs(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tens
   lw::unpack_pairs(ptr<int2>(gathered), cap_total, (int)world, ptr<float>(g), ptr<int64_t>(seg_off),
                    ptr<int32_t>(seg_n), ptr<int64_t>(cap_off), ptr<int2>(utasks),
                    (int)(utasks.numel() / 2), cur_stream());
+  launched("unpack_pairs");
 }
 
 void unpack_validx(Tensor vals, Tensor idx, Tensor slot_seg, int64_t world, Tensor g,
@@ -184,6 +198,7 @@ void unpack_validx(Tensor vals, Tensor idx, Tensor slot_seg, int64_t world, Tens
   check_cuda(g, "g");
   lw::unpack_validx(ptr<float>(vals), ptr<int32_t>(idx), ptr<int32_t>(slot_seg), vals.numel(),
                     (int)world, ptr<float>(g), ptr<int64_t>(seg_off), cur_stream());
+  launched("unpack_validx");
 }
 
 lw::QuantArgs make_quant_args(const Tensor& g, const c10::optional<Tensor>& ef,
@@ -227,8 +242,10 @@ void quantize(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, 
   a.seed1 = (uint32_t)((uint64_t)seed >> 32);
   lw::seg_reduce(a, a.ef != nullptr, q == lw::Q_TERN ? 0 : 1, a.scale,
                  reinterpret_cast<float2*>(base + L.partial), cur_stream());
+  launched("seg_reduce");
   // after seg_reduce the EF add is already folded into g (g' = g + e)
   lw::quantize(a, (int)q, a.ef != nullptr, cur_stream());
+  launched("quantize");
 }
 
 void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor seg_n,
@@ -242,6 +259,7 @@ void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor
   const int64_t wpr = gathered.numel() / world;
   TORCH_CHECK(wpr % 4 == 0, "payload words per rank must be a multiple of 4");
   lw::dequantize(a, (int)q, ptr<uint32_t>(gathered), wpr, (int)world, cur_stream());
+  launched("dequantize");
 }
 
 void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tensor segs,
@@ -273,6 +291,7 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tens
   a.nesterov = (int)nesterov;
   a.first_step = (int)first_step;
   lw::sgd_step(a, cur_stream());
+  launched("sgd_step");
 }
 
 void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<double> stdv) {
@@ -293,11 +312,13 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
     TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.numel() / 4 * 3 == in.numel() &&
                 out.numel() % 4 == 0, "4-channel out: bf16 with in.numel()/3 pixels");
     lw::normalize_u8_c4(ptr<uint8_t>(in), ptr<uint16_t>(out), in.numel() / 3, m, s, cur_stream());
+    launched("normalize_u8_c4");
     return;
   }
   TORCH_CHECK(out.numel() == in.numel(), "out/in size mismatch");
   lw::normalize_u8(ptr<uint8_t>(in), out.data_ptr(), in.numel(), m, s,
                    out.scalar_type() == at::kBFloat16, cur_stream());
+  launched("normalize_u8");
 }
 
 // ---------------------------------------------------------------- fused BatchNorm (NHWC)
@@ -321,7 +342,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_fwd(Tensor x, c10::optional<Tensor
   check_nhwc(x, "x");
   const int64_t C = channels_of(x);
   const int64_t M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0, "fused BN needs C % 8 == 0, got ", C);
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxBnC, "fused BN needs C % 8 == 0 and C <= ", kMaxBnC, ", got ", C);
   if (res.has_value() && res->defined()) {
     check_nhwc(*res, "res");
     TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == x.scalar_type(),
@@ -367,6 +388,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_fwd(Tensor x, c10::optional<Tensor
     a.shift = ptr<float>(shift);
   }
   lw::bn_forward(a, cur_stream());
+  launched("bn_forward");
   // scale/shift as used by the forward: lets the backward recompute the ReLU mask from x
   return {y, mean, invstd, scale_shift};
 }
@@ -444,6 +466,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
   a.B = a.A + C;
   a.Cc = a.A + 2 * C;
   lw::bn_backward(a, cur_stream());
+  launched("bn_backward");
   return {dx, dgamma, dbeta, dres};
 }
 
@@ -562,6 +585,7 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
     stats = at::empty({0}, A.options().dtype(at::kFloat));
   }
   lw::gemm_bf16(g, cur_stream());
+  launched("gemm_bf16");
   return {C, stats};
 }
 
@@ -730,6 +754,7 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
     stats = at::empty({0}, G.options().dtype(at::kFloat));
   }
   lw::conv_gemm(g, h, (int)mode, cur_stream());
+  launched("conv_gemm");
   return {C, stats};
 }
 
@@ -746,7 +771,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stat
   check_nhwc(x, "x");
   const int64_t C = x.dim() == 4 ? x.size(1) : x.size(-1);
   const int64_t M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0, "bn_stats needs C % 8 == 0");
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxBnC, "bn_stats needs C % 8 == 0 and C <= ", kMaxBnC);
   auto f32 = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({C}, f32), invstd = at::empty({C}, f32);
   Tensor ss = at::empty({2 * C}, f32);
@@ -781,6 +806,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stat
     a.partial = ptr<float>(partial);
   }
   lw::bn_stats(a, cur_stream());
+  launched("bn_stats");
   return {mean, invstd, ss};
 }
 
@@ -790,8 +816,9 @@ static void stem_geom(const Tensor& x, int64_t k, int64_t s, int64_t p, lw::Stem
               "stem input must be channels_last 4-D");
   check_dtype(x, at::kBFloat16, "x");
   a.N = (int)x.size(0); a.C = (int)x.size(1); a.H = (int)x.size(2); a.W = (int)x.size(3);
-  TORCH_CHECK(a.C % 8 == 0, "stem pool needs C % 8 == 0");
-  TORCH_CHECK(k >= 1 && k * k <= 255 && s >= 1 && p >= 0 && p < k, "pool geometry");
+  TORCH_CHECK(a.C % 8 == 0 && a.C <= kMaxBnC, "stem pool needs C % 8 == 0 and C <= ", kMaxBnC);
+  // PyTorch semantics: padding at most half the window (no window lies entirely in padding)
+  TORCH_CHECK(k >= 1 && k * k <= 255 && s >= 1 && p >= 0 && 2 * p <= k, "pool geometry");
   a.k = (int)k; a.s = (int)s; a.p = (int)p;
   a.Ho = (int)((a.H + 2 * p - k) / s + 1);
   a.Wo = (int)((a.W + 2 * p - k) / s + 1);
@@ -816,6 +843,7 @@ std::tuple<Tensor, Tensor> stem_pool_fwd(Tensor x, Tensor scale_shift, int64_t k
   a.out = out.data_ptr();
   a.idx = ptr<uint8_t>(idx);
   lw::stem_pool_fwd(a, cur_stream());
+  launched("stem_pool_fwd");
   return {out, idx};
 }
 
@@ -855,6 +883,7 @@ std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x
   a.B = a.A + a.C;
   a.Cc = a.A + 2 * a.C;
   lw::stem_pool_bwd(a, cur_stream());
+  launched("stem_pool_bwd");
   return {dx, dgamma, dbeta};
 }
 
@@ -865,7 +894,7 @@ Tensor bn_apply(Tensor x, Tensor scale_shift, c10::optional<Tensor> res,
   const c10::DeviceGuard guard(x.device());
   check_nhwc(x, "x");
   const int64_t C = x.dim() == 4 ? x.size(1) : x.size(-1);
-  TORCH_CHECK(C % 8 == 0, "bn_apply needs C % 8 == 0");
+  TORCH_CHECK(C % 8 == 0 && C <= kMaxBnC, "bn_apply needs C % 8 == 0 and C <= ", kMaxBnC);
   check_dtype(scale_shift, at::kFloat, "scale_shift");
   TORCH_CHECK(scale_shift.numel() == 2 * C && scale_shift.is_contiguous(), "scale_shift size");
   Tensor y = at::empty_like(x);
@@ -898,13 +927,22 @@ Tensor bn_apply(Tensor x, Tensor scale_shift, c10::optional<Tensor> res,
     }
   }
   lw::bn_apply(a, cur_stream());
+  launched("bn_apply");
   return y;
+}
+
+// test hook: a deliberately invalid launch (block of 2048 threads) must raise in launched()
+void selftest_bad_launch(Tensor any) {
+  const c10::DeviceGuard guard(any.device());
+  lw::launch_invalid_config_for_test(cur_stream());
+  launched("selftest_bad_launch");
 }
 
 }  // namespace
 
 TORCH_LIBRARY(lwaaai, m) {
   m.def("workspace_bytes(int n_small, int n_large, int n_tasks) -> int", &workspace_bytes);
+  m.def("selftest_bad_launch(Tensor any) -> ()");
   m.def(
       "select_compress(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor keep, "
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
@@ -971,6 +1009,7 @@ TORCH_LIBRARY(lwaaai, m) {
 }
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
+  m.impl("selftest_bad_launch", &selftest_bad_launch);
   m.impl("select_compress", &select_compress);
   m.impl("thresh_count", &thresh_count);
   m.impl("thresh_write", &thresh_write);

@@ -889,7 +889,9 @@ static void select_compress_t(const SelectArgs& a, hipStream_t st) {
               a.cap_off, a.small_segs, a.pairs, a.vals, a.idx_out, a.st_small, a.gid_base, a.step,
               a.seed0, a.seed1);
   if (a.n_large == 0) return;
-  (void)hipMemsetAsync(a.hist, 0, sizeof(uint32_t) * HIST_WORDS * (size_t)a.n_large, st);
+  // a failed memset stops here; the binding's launch check reports it (hipGetLastError)
+  if (hipMemsetAsync(a.hist, 0, sizeof(uint32_t) * HIST_WORDS * (size_t)a.n_large, st) != hipSuccess)
+    return;
   LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
             a.large_segs, a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1);
   LW_LAUNCH((k_select<KM, 0>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);

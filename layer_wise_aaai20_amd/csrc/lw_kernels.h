@@ -228,6 +228,7 @@ bool conv_tile_ok(int mode, int tile);
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
                   const float stdv[3], bool bf16, hipStream_t st);
+void launch_invalid_config_for_test(hipStream_t st);
 void normalize_u8_c4(const uint8_t* in, uint16_t* out, int64_t npix, const float mean[3],
                      const float stdv[3], hipStream_t st);
 

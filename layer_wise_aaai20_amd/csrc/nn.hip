@@ -118,6 +118,13 @@ void normalize_u8_c4(const uint8_t* in, uint16_t* out, int64_t npix, const float
                      mean[2], 1.f / stdv[0], 1.f / stdv[1], 1.f / stdv[2]);
 }
 
+__global__ void k_noop() {}
+
+// for the launch-check test: 2048 threads per block exceeds the 1024 limit
+void launch_invalid_config_for_test(hipStream_t st) {
+  hipLaunchKernelGGL(k_noop, dim3(1), dim3(2048), 0, st);
+}
+
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
                   const float stdv[3], bool bf16, hipStream_t st) {
   const int64_t chunks = (nbytes + 15) / 16;

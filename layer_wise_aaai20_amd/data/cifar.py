@@ -108,9 +108,11 @@ def _read_cifar_bin(path):
     return data, labels
 
 
-def cifar10(root: str, synthetic_fallback: bool = True, n_train=50000, n_test=10000, seed=0):
+def cifar10(root: str, synthetic_fallback: bool = False, n_train=50000, n_test=10000, seed=0):
     """``{'train': {'data': uint8 NHWC, 'labels'}, 'test': ...}``. Reads ``cifar-10-batches-bin``
-    or ``cifar10.npz`` under ``root``; otherwise synthetic data of the same shape."""
+    or ``cifar10.npz`` under ``root``. A missing dataset raises (accuracy logged for made-up
+    images would be meaningless) unless ``synthetic_fallback`` asks for synthetic data of the same
+    shape (the CLIs' explicit ``--synthetic`` flag)."""
     root = os.path.expanduser(root)
     bdir = os.path.join(root, "cifar-10-batches-bin")
     if os.path.isdir(bdir):
@@ -125,7 +127,11 @@ def cifar10(root: str, synthetic_fallback: bool = True, n_train=50000, n_test=10
         return {"train": {"data": z["x_train"], "labels": z["y_train"].astype(np.int64)},
                 "test": {"data": z["x_test"], "labels": z["y_test"].astype(np.int64)}}
     if not synthetic_fallback:
-        raise FileNotFoundError(f"no CIFAR-10 under {root} (need cifar-10-batches-bin or npz)")
+        raise FileNotFoundError(
+            f"no CIFAR-10 under {root} (need cifar-10-batches-bin/ or cifar10.npz); pass "
+            "--synthetic to train on synthetic data of the same shape")
+    import warnings
+    warnings.warn(f"no CIFAR-10 under {root}: using SYNTHETIC data", stacklevel=2)
     return synthetic_cifar10(n_train, n_test, seed)
 
 

@@ -131,10 +131,12 @@ def map_idx2ar(idx_ar_sorted, batch_size):
 
 
 def crop_size_for_ar(ar: float, size: int):
-    """``CropArTfm``: target (h, w) for an aspect ratio, the short side = size, multiples of 8."""
+    """``CropArTfm`` (``dataloader.py:164-175``): target (h, w) for an aspect ratio ar = w / h,
+    the short side = ``size``, the long side truncated to a multiple of 8. A tall image (ar < 1)
+    gets a tall crop (h > w), a wide one a wide crop."""
     if ar < 1:
-        return size, int(round(size / ar / 8)) * 8
-    return int(round(size * ar / 8)) * 8, size
+        return int(size / ar) // 8 * 8, size
+    return size, int(size * ar) // 8 * 8
 
 
 class RectValDataset(Dataset):

@@ -11,6 +11,8 @@ from torch import nn
 
 from ._ext import load, ops_for
 
+MAX_BN_C = 2048          # csrc/bn.hip: one 8-channel group per thread of a 256-thread block
+
 
 def normalize_nhwc_u8(images: torch.Tensor, mean: torch.Tensor, std: torch.Tensor,
                       dtype=torch.bfloat16, pad4: bool = False) -> torch.Tensor:
@@ -85,7 +87,7 @@ def fused_batch_norm(x, weight, bias, running_mean, running_var, training, momen
     """BN → (+ residual) → (ReLU). HIP kernels for channels_last GPU tensors with C % 8 == 0,
     torch ops otherwise (CPU path, odd channel counts)."""
     use_hip = x.is_cuda and x.dim() in (2, 4) and x.size(1) % 8 == 0 and \
-        x.dtype in (torch.bfloat16, torch.float32)
+        x.size(1) <= MAX_BN_C and x.dtype in (torch.bfloat16, torch.float32)
     if use_hip:
         return _FusedBN.apply(x, residual, weight, bias, running_mean, running_var, training,
                               momentum, eps, relu)
@@ -263,7 +265,11 @@ def stem_conv_supported(model, x: torch.Tensor) -> bool:
             isinstance(conv.padding, tuple) and supported(3, conv.out_channels, conv.groups,
                                                           conv.dilation) and
             bn.affine and bn.track_running_stats and isinstance(model.maxpool, nn.MaxPool2d) and
-            _pool_geom(model.maxpool) is not None)
+            _pool_geom(model.maxpool) is not None and
+            _stem_fits(x.shape[0], conv.out_channels,
+                       (x.shape[2] + 2 * conv.padding[0] - conv.kernel_size[0]) // conv.stride[0] + 1,
+                       (x.shape[3] + 2 * conv.padding[1] - conv.kernel_size[1]) // conv.stride[1] + 1,
+                       _pool_geom(model.maxpool)))
 
 
 def stem_conv_bn_relu_pool(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, pool: nn.MaxPool2d):
@@ -275,16 +281,25 @@ def _pool_geom(pool: nn.MaxPool2d):
         return v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else None)
     k, s, p, d = one(pool.kernel_size), one(pool.stride or pool.kernel_size), one(pool.padding), \
         one(pool.dilation)
-    if None in (k, s, p) or d != 1 or pool.ceil_mode or pool.return_indices:
+    if None in (k, s, p) or d != 1 or pool.ceil_mode or pool.return_indices or 2 * p > k:
         return None
     return (k, s, p)
 
 
+def _stem_fits(n: int, c: int, h: int, w: int, geom) -> bool:
+    """The stem kernels index pixels / outputs in 32-bit arithmetic (bindings.cpp stem_geom):
+    larger inputs take the unfused path instead of raising."""
+    k, s, p = geom
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    return n * h * w < 2 ** 31 and n * ho * wo * (c // 8) < 2 ** 31
+
+
 def stem_supported(model, c: torch.Tensor) -> bool:
     bn = model.bn1
+    geom = _pool_geom(model.maxpool) if isinstance(model.maxpool, nn.MaxPool2d) else None
     return (model.training and c.is_cuda and c.dim() == 4 and c.dtype == torch.bfloat16 and
-            c.size(1) % 8 == 0 and bn.affine and bn.track_running_stats and
-            isinstance(model.maxpool, nn.MaxPool2d) and _pool_geom(model.maxpool) is not None)
+            c.size(1) % 8 == 0 and c.size(1) <= MAX_BN_C and bn.affine and
+            bn.track_running_stats and geom is not None and _stem_fits(*c.shape, geom))
 
 
 def stem_bn_relu_pool(c: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2d) -> torch.Tensor:

@@ -17,6 +17,7 @@ from __future__ import annotations
 from typing import Optional
 
 import torch
+import torch.distributed as dist
 from torch import nn
 
 from . import comm
@@ -151,14 +152,38 @@ class CompressedDDP(nn.Module):
     # checkpoint extras: per-rank error-feedback residuals and the step counter (extra keys that
     # reference readers ignore; SURVEY.md §5 checkpoint row)
     def compression_state(self) -> dict:
+        """Collective (call on every rank): the step counter and EVERY rank's error-feedback
+        residual, ``ef_per_rank[r]`` = rank r's buffer (each rank's residual is its own
+        compression error, so restoring rank 0's everywhere would bias the resumed run)."""
         e = self.engine
-        return {"step": e.step, "ef": None if e.ef is None else e.ef.detach().clone()}
+        st = {"step": e.step, "world": e.world, "ef_per_rank": None}
+        if e.ef is not None:
+            ef = e.ef.detach()
+            if e.world > 1 and dist.is_available() and dist.is_initialized():
+                parts = [torch.empty_like(ef) for _ in range(e.world)]
+                dist.all_gather(parts, ef.contiguous(), group=e.pg)
+                st["ef_per_rank"] = torch.stack(parts).cpu()
+            else:
+                st["ef_per_rank"] = ef.clone()[None].cpu()
+        return st
 
     def load_compression_state(self, st: dict) -> None:
+        """Each rank restores its own residual; a checkpoint from a different world size (or
+        one without residuals) restarts error feedback from zero, with a warning."""
         e = self.engine
         e.step = int(st.get("step", 0))
-        if st.get("ef") is not None and e.ef is not None:
+        if e.ef is None:
+            return
+        per = st.get("ef_per_rank")
+        if per is not None and per.shape[0] == e.world and per.shape[1] == e.ef.numel():
+            e.ef.copy_(per[e.rank].to(e.ef.device))
+        elif st.get("ef") is not None and e.world == 1:          # single-rank legacy layout
             e.ef.copy_(st["ef"])
+        else:
+            import warnings
+            warnings.warn("checkpoint has no error-feedback residuals for this world size: "
+                          "restarting them from zero")
+            e.ef.zero_()
 
     def extra_repr(self) -> str:
         return self.engine.describe()

@@ -312,7 +312,10 @@ def save_checkpoint(run, epoch, model, best_top5, optimizer, is_best=False,
     path = os.path.join(run.args.logdir or ".", filename)
     torch.save(state, path)
     if is_best and run.args.logdir:
-        shutil.copyfile(path, os.path.join(run.args.logdir, "model_best.pth.tar"))
+        dst = os.path.join(run.args.logdir, "model_best.pth.tar")
+        # the best checkpoint may already be written under that name (no self-copy)
+        if not (os.path.exists(dst) and os.path.samefile(path, dst)):
+            shutil.copyfile(path, dst)
     return path
 
 
@@ -554,12 +557,16 @@ def main(argv=None):
         log.event(f"~~{epoch}\t{hours:.5f}\t\t{top1:.3f}\t\t{top5:.3f}\n")
         is_best = top5 > best_top5
         best_top5 = max(top5, best_top5)
+        # every rank takes part: the error-feedback residuals are per rank (a collective
+        # gathers them to the checkpoint writer)
+        comp = model.compression_state() if args.extra_ckpt and \
+            hasattr(model, "compression_state") else None
         if args.local_rank == 0 and run.is_master:
             extra = None
             if args.extra_ckpt:
                 extra = {"scheduler": scheduler.state_dict()}
-                if hasattr(model, "compression_state"):
-                    extra["compression"] = model.compression_state()
+                if comp is not None:
+                    extra["compression"] = comp
             if is_best:
                 save_checkpoint(run, epoch, model, best_top5, optimizer, is_best=True,
                                 filename="model_best.pth.tar", extra=extra)

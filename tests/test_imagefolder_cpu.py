@@ -44,6 +44,25 @@ def test_rect_val_batches_share_shape(tree):
         assert len(shapes) == 1
         h, w, _ = shapes.pop()
         assert min(h, w) == 32
+        ar = np.mean([a for a, _ in chunk])        # ar = w / h
+        assert (h > w) == (ar < 1) or h == w, (ar, h, w)
+
+
+def test_crop_size_for_ar_orientation():
+    """Tall images (ar = w/h < 1) get tall crops, like dataloader.py:164-175."""
+    assert D.crop_size_for_ar(0.5, 128) == (256, 128)
+    assert D.crop_size_for_ar(0.75, 224) == (296, 224)
+    assert D.crop_size_for_ar(4 / 3, 224) == (224, 296)
+    assert D.crop_size_for_ar(1.0, 224) == (224, 224)
+
+
+def test_cifar10_missing_dataset_raises(tmp_path):
+    from layer_wise_aaai20_amd.data import cifar as C
+    with pytest.raises(FileNotFoundError):
+        C.cifar10(str(tmp_path))
+    with pytest.warns(UserWarning):
+        d = C.cifar10(str(tmp_path), synthetic_fallback=True, n_train=16, n_test=8)
+    assert d["train"]["data"].shape == (16, 32, 32, 3)
 
 
 def test_get_loaders_real_folders(tree):

@@ -202,3 +202,13 @@ def test_resnet50_step_topk_gpu():
     assert all(np.isfinite(losses))
     st = tr.ddp.sync_stats()
     assert st.payload_bytes < st.dense_bytes * 0.01
+
+
+def test_invalid_launch_raises():
+    """Every binding checks hipGetLastError after its launches: a rejected launch configuration
+    surfaces as a RuntimeError at the op that caused it."""
+    from layer_wise_aaai20_amd.ops._ext import load
+    with pytest.raises(RuntimeError, match="launch failed"):
+        load().selftest_bad_launch(torch.empty(1, device="cuda"))
+    torch.cuda.synchronize()            # not sticky: the device keeps working
+    assert torch.ones(4, device="cuda").sum().item() == 4

@@ -380,6 +380,35 @@ class ThresholdCodec(TopkCodec):
             return
         self.unpack_pairs_cpu(gathered, world, grad, self.cap_off)
 
+    def compress_dense(self, grad, ef):
+        """In place: ``grad`` becomes the dense compressed vector (EF folded in, residual to
+        ``ef``) — the reference wire's input, with no counts and no host round trip."""
+        lib = ops_for(grad)
+        if lib is not None:
+            t = self.plan.all_large_tables(grad.device)
+            k = str(grad.device)
+            if k not in self._ws:
+                nb = lib.workspace_bytes(0, self.plan.S, int(t["tasks"].shape[0]))
+                self._ws[k] = _ws_tensor(nb, grad.device)
+            lib.thresh_dense(grad, ef, t["seg_off"], t["seg_n"], t["segs"], t["tasks"],
+                             t["task_lo"], self._ws[k], self.V, int(self.adaptive))
+            return
+        for s, x in self._segs(grad):
+            o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
+            if ef is not None:
+                x.add_(ef[o:o + n])
+            a = x.abs()
+            if self.adaptive:
+                keep = (x * 2).abs() >= a.max() if x.numel() else a > 0
+            else:
+                keep = a >= self.V
+            keep &= x != 0
+            if ef is not None:
+                e = ef[o:o + n]
+                e.copy_(x)
+                e[keep] = 0
+            x[~keep] = 0
+
 
 # ================================================================================= quantisers
 class _QuantCodec(Codec):
@@ -583,6 +612,10 @@ class DenseWrap(Codec):
         self.name = f"dense({inner.name})"
 
     def compress(self, grad, ef, step):
+        if isinstance(self.inner, ThresholdCodec):
+            self.inner.compress_dense(grad, ef)
+            self.last_payload_bytes = grad.numel() * grad.element_size()
+            return grad
         payload = self.inner.compress(grad, ef, step)
         if isinstance(self.inner, DenseCodec):
             return grad

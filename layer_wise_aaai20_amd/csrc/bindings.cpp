@@ -164,6 +164,22 @@ void thresh_count(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg
   launched("thresh_count");
 }
 
+void thresh_dense(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
+                  Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor ws, double V,
+                  int64_t adaptive) {
+  const c10::DeviceGuard guard(g.device());
+  Tensor empty_i = at::empty({0}, seg_n.options());
+  Tensor empty_l = at::empty({1}, seg_off.options());
+  lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, seg_n, empty_l.expand({2}).contiguous(),
+                                      empty_i, large_segs, tasks, task_lo, ws);
+  const WsLayout L = layout(a.n_small, a.n_large, a.n_tasks);
+  uint8_t* base = ptr<uint8_t>(ws);
+  lw::thresh_dense(a, (float)V, (int)adaptive, a.ef != nullptr,
+                   reinterpret_cast<float*>(base + L.segmax),
+                   reinterpret_cast<float2*>(base + L.partial), cur_stream());
+  launched("thresh_dense");
+}
+
 void thresh_write(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
                   Tensor cap_off, Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor ws,
                   Tensor pairs) {
@@ -953,6 +969,9 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor tasks, Tensor task_lo, Tensor(c!) ws, float V, int adaptive, Tensor(d!) counts_out) "
       "-> ()");
   m.def(
+      "thresh_dense(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor large_segs, "
+      "Tensor tasks, Tensor task_lo, Tensor(c!) ws, float V, int adaptive) -> ()");
+  m.def(
       "thresh_write(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor cap_off, "
       "Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor(c!) ws, Tensor(d!) pairs) -> ()");
   m.def(
@@ -1013,6 +1032,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("select_compress", &select_compress);
   m.impl("thresh_count", &thresh_count);
   m.impl("thresh_write", &thresh_write);
+  m.impl("thresh_dense", &thresh_dense);
   m.impl("unpack_pairs", &unpack_pairs);
   m.impl("unpack_validx", &unpack_validx);
   m.impl("quantize", &quantize);

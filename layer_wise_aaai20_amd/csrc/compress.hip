@@ -402,6 +402,36 @@ __global__ __launch_bounds__(NT) void k_scan(const uint2* __restrict__ cnt, uint
   }
 }
 
+// Threshold methods on the reference's dense wire: the bucket is overwritten in place with its
+// compressed dense vector (kept entries, zeros elsewhere) and the residual goes to EF — no counts,
+// no payload sizing, so no host round trip in the middle of backward. EFADD: g += ef first (not
+// yet folded in by k_partial); EFW: write the residual.
+template <bool EFADD, bool EFW>
+__global__ __launch_bounds__(NT) void k_thresh_dense(float* __restrict__ g, float* __restrict__ ef,
+                                                     const int64_t* __restrict__ seg_off,
+                                                     const int32_t* __restrict__ seg_n,
+                                                     const int32_t* __restrict__ large_segs,
+                                                     const int2* __restrict__ tasks,
+                                                     const SelState* __restrict__ st) {
+  const int2 t = tasks[blockIdx.x];
+  const int li = t.x, begin = t.y;
+  const int s = large_segs[li];
+  const int n = seg_n[s];
+  const int64_t off = seg_off[s];
+  const uint32_t tk = st[li].tkey;
+  const int end = min(begin + EPB, n);
+  float* gp = g + off;
+  float* ep = EFW ? ef + off : nullptr;
+  for (int i = begin + threadIdx.x; i < end; i += NT) {
+    float x = gp[i];
+    if (EFADD) x += ep[i];
+    const uint32_t k = abs_key(x);
+    const bool keep = tk != 0 ? k >= tk : k > 0;
+    gp[i] = keep ? x : 0.f;
+    if (EFW) ep[i] = keep ? 0.f : x;
+  }
+}
+
 // Per-segment capacity for the threshold path is only known after the count exchange.
 __global__ void k_set_caps(SelState* __restrict__ st, const int64_t* __restrict__ cap_off,
                            const int32_t* __restrict__ large_segs, int nseg) {
@@ -943,6 +973,26 @@ void thresh_count(const SelectArgs& a, float V, int adaptive, bool ef, float* se
     LW_LAUNCH((k_count<KM_THRESH, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
               a.large_segs, a.tasks, a.st_large, a.cnt, 0u, 0u, 0u, 0u);
   LW_LAUNCH((k_scan<KM_THRESH>), a.n_large, st, a.cnt, a.pre, a.task_lo, a.st_large, count_out);
+}
+
+void thresh_dense(const SelectArgs& a, float V, int adaptive, bool ef, float* segmax,
+                  float2* partial, hipStream_t st) {
+  if (adaptive) {
+    if (ef) LW_LAUNCH((k_partial<true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs, a.tasks, partial);
+    else LW_LAUNCH((k_partial<false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs, a.tasks, partial);
+    LW_LAUNCH(k_finalize, a.n_large, st, partial, a.task_lo, segmax, 0);
+  }
+  hipLaunchKernelGGL(k_thresh_state, dim3((a.n_large + NT - 1) / NT), dim3(NT), 0, st, a.st_large,
+                     (const float*)segmax, a.n_large, V, adaptive);
+  if (ef && !adaptive)
+    LW_LAUNCH((k_thresh_dense<true, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.large_segs, a.tasks, a.st_large);
+  else if (ef)   // k_partial<true> already folded the residual into g
+    LW_LAUNCH((k_thresh_dense<false, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.large_segs, a.tasks, a.st_large);
+  else
+    LW_LAUNCH((k_thresh_dense<false, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.large_segs, a.tasks, a.st_large);
 }
 
 void thresh_write(const SelectArgs& a, bool ef, hipStream_t st) {

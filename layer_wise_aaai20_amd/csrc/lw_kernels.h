@@ -74,6 +74,8 @@ void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t 
 void thresh_count(const SelectArgs& a, float V, int adaptive, bool ef, float* segmax,
                   float2* partial, int32_t* count_out, hipStream_t st);
 void thresh_write(const SelectArgs& a, bool ef, hipStream_t st);
+void thresh_dense(const SelectArgs& a, float V, int adaptive, bool ef, float* segmax,
+                  float2* partial, hipStream_t st);
 void unpack_pairs(const int2* gathered, int64_t cap_total, int ws, float* g, const int64_t* seg_off,
                   const int32_t* seg_n, const int64_t* cap_off, const int2* utasks, int n_utasks,
                   hipStream_t st);

@@ -82,7 +82,8 @@ class BatchTransformDataLoader:
             if imgs.numel() == 0:
                 yield torch.empty((0, 3, 1, 1), device=self.device, dtype=self.dtype), target
                 continue
-            yield normalize_nhwc_u8(imgs.contiguous(), self.mean, self.std, self.dtype), target
+            yield normalize_nhwc_u8(imgs.contiguous(), self.mean, self.std, self.dtype,
+                                    pad4=getattr(self, "pad4", False)), target
 
 
 class DistValSampler(Sampler):
@@ -330,9 +331,56 @@ def _folder_loaders(traindir, valdir, sz, bs, val_bs, workers, rect_val, min_sca
             BatchTransformDataLoader(val, device, dtype), trn_smp, val_smp)
 
 
+class GPUSyntheticLoader:
+    """Synthetic training batches generated on the GPU (uint8 noise plus a per-class colour
+    offset, so the model has a signal to learn) and normalised by the same fused kernel as real
+    batches: the training loop of the CLI runs at the model's speed instead of the speed of a
+    host-side numpy generator. Each rank draws its own shard of an epoch (``n // world`` items),
+    deterministically from (seed, epoch, batch, rank)."""
+
+    def __init__(self, n, size, bs, device, dtype=torch.float32, seed=0, distributed=False,
+                 pad4=False, num_classes=1000):
+        from ..parallel import comm
+        self.n, self.size, self.bs, self.dtype, self.seed = n, size, bs, dtype, seed
+        self.device = torch.device(device)
+        self.world = comm.world_size() if distributed else 1
+        self.rank = comm.rank() if distributed else 0
+        self.pad4, self.num_classes, self.epoch = pad4, num_classes, 0
+        self.mean = torch.tensor(IMAGENET_MEAN, dtype=torch.float32)
+        self.std = torch.tensor(IMAGENET_STD, dtype=torch.float32)
+        g = torch.Generator(device=self.device).manual_seed(seed + 17)
+        self.bias = torch.randint(0, 128, (num_classes, 3), dtype=torch.int16, device=self.device,
+                                  generator=g)
+        self.sampler = self
+
+    def set_epoch(self, epoch):
+        self.epoch = int(epoch)
+
+    def update_batch_size(self, bs):
+        self.bs = bs
+
+    def __len__(self):
+        return max(1, -(-(self.n // self.world) // self.bs))
+
+    def __iter__(self):
+        from ..ops.nn import normalize_nhwc_u8
+        per = self.n // self.world
+        for b in range(len(self)):
+            nb = min(self.bs, per - b * self.bs)
+            g = torch.Generator(device=self.device).manual_seed(
+                (self.seed * 1_000_003 + self.epoch * 10_007 + b) * 8191 + self.rank)
+            t = torch.randint(0, self.num_classes, (nb,), device=self.device, generator=g)
+            x = torch.randint(0, 128, (nb, self.size, self.size, 3), dtype=torch.int16,
+                              device=self.device, generator=g)
+            x = (x + self.bias[t].view(nb, 1, 1, 3)).to(torch.uint8)
+            yield normalize_nhwc_u8(x, self.mean, self.std, self.dtype,
+                                    pad4=self.pad4 and self.dtype == torch.bfloat16), t
+
+
 def get_loaders(traindir=None, valdir=None, sz=128, bs=256, val_bs=None, workers=0,
                 rect_val=False, min_scale=0.08, distributed=False, n_train=None, n_val=None,
-                device=None, dtype=torch.float32, seed=0, synthetic=True):
+                device=None, dtype=torch.float32, seed=0, synthetic=True, gpu_synthetic=False,
+                pad4=False):
     """Train / val loaders + samplers for one phase (``dataloader.py:26-57``).
 
     Synthetic sizes default to a small ImageNet stand-in (``n_train = 64 * bs``, ``n_val = 8 *
@@ -344,11 +392,15 @@ def get_loaders(traindir=None, valdir=None, sz=128, bs=256, val_bs=None, workers
     if not synthetic:
         return _folder_loaders(traindir, valdir, sz, bs, val_bs, workers, rect_val, min_scale,
                                distributed, device, dtype)
-    train_ds = SyntheticImageNet(n_train, sz, seed=seed)
-    trn_smp = torch.utils.data.distributed.DistributedSampler(
-        train_ds, num_replicas=comm.world_size(), rank=comm.rank()) if distributed else None
-    trn = DataLoader(train_ds, batch_size=bs, shuffle=trn_smp is None, num_workers=workers,
-                     collate_fn=fast_collate, sampler=trn_smp, drop_last=False)
+    if gpu_synthetic:
+        trn = GPUSyntheticLoader(n_train, sz, bs, device, dtype, seed, distributed, pad4)
+        trn_smp = trn
+    else:
+        train_ds = SyntheticImageNet(n_train, sz, seed=seed)
+        trn_smp = torch.utils.data.distributed.DistributedSampler(
+            train_ds, num_replicas=comm.world_size(), rank=comm.rank()) if distributed else None
+        trn = DataLoader(train_ds, batch_size=bs, shuffle=trn_smp is None, num_workers=workers,
+                         collate_fn=fast_collate, sampler=trn_smp, drop_last=False)
     val_base = SyntheticImageNet(n_val, sz, seed=seed + 1)
     if rect_val:
         idx_ar = sort_ar(n_val, seed)
@@ -360,5 +412,7 @@ def get_loaders(traindir=None, valdir=None, sz=128, bs=256, val_bs=None, workers
         order = list(range(n_val))
     val_smp = DistValSampler(order, val_bs, distributed)
     val = DataLoader(val_ds, batch_sampler=val_smp, num_workers=workers, collate_fn=fast_collate)
-    return (BatchTransformDataLoader(trn, device, dtype), BatchTransformDataLoader(val, device, dtype),
-            trn_smp, val_smp)
+    trn_dl = trn if gpu_synthetic else BatchTransformDataLoader(trn, device, dtype)
+    val_dl = BatchTransformDataLoader(val, device, dtype)
+    val_dl.pad4 = pad4
+    return trn_dl, val_dl, trn_smp, val_smp

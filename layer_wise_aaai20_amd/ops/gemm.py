@@ -62,34 +62,67 @@ def linear_wgrad(dy2, x2):
     return gemm(dy2, N, False, x2, K, False, N, K, M, None, False, _splits(tiles, M), False)
 
 
+def _pad_rows(w: torch.Tensor, n: int) -> torch.Tensor:
+    """[N, K] → [n, K] with zero rows (the GEMM's N and its 16-byte stores need N % 8 == 0)."""
+    if w.shape[0] == n:
+        return w
+    out = torch.zeros((n, w.shape[1]), dtype=w.dtype, device=w.device)
+    out[:w.shape[0]].copy_(w)
+    return out
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, relu):
+        from .block import _bf16_weight
         shp = x.shape
+        N, K = weight.shape
+        Np = N + (-N) % 8                       # e.g. a 10-way classifier runs as 16 columns
         x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
-        w = weight.to(torch.bfloat16).contiguous()
-        y = linear_fwd(x2, w, bias.float() if bias is not None else None, relu)
+        w = _pad_rows(_bf16_weight(weight).contiguous(), Np)
+        b = None
+        if bias is not None:
+            b = bias.float() if Np == N else torch.cat([bias.float(),
+                                                        bias.new_zeros(Np - N).float()])
+        y = linear_fwd(x2, w, b, relu)
+        if Np != N:
+            y = y[:, :N]
         ctx.save_for_backward(x2, w, y if relu else None)
-        ctx.relu, ctx.has_bias, ctx.shape = relu, bias is not None, shp
-        ctx.wdtype = weight.dtype
-        return y.reshape(*shp[:-1], w.shape[0])
+        ctx.relu, ctx.has_bias, ctx.shape, ctx.N, ctx.Np = relu, bias is not None, shp, N, Np
+        ctx.weight = weight
+        return y.reshape(*shp[:-1], N)
 
     @staticmethod
     def backward(ctx, dy):
         x2, w, y = ctx.saved_tensors
-        dy2 = dy.reshape(-1, w.shape[0]).to(torch.bfloat16)
+        N, Np = ctx.N, ctx.Np
+        dy2 = dy.reshape(-1, N).to(torch.bfloat16)
         if ctx.relu:
             dy2 = dy2 * (y > 0)
+        if Np != N:
+            dy2 = torch.cat([dy2, dy2.new_zeros(dy2.shape[0], Np - N)], 1)
         dy2 = dy2.contiguous()
         dx = linear_dgrad(dy2, w).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
-        dw = linear_wgrad(dy2, x2).to(ctx.wdtype) if ctx.needs_input_grad[1] else None
-        db = dy2.float().sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        dw = None
+        p = ctx.weight
+        if ctx.needs_input_grad[1]:
+            g = p.grad if getattr(p, "_lw_grad_ready", None) is not None else None
+            if g is not None and Np == N and g.dtype == torch.float32 and g.is_contiguous():
+                # fp32 weight gradient accumulated straight into the gradient arena (split-K)
+                M, K = x2.shape
+                tiles = -(-N // 128) * -(-K // 128)
+                load().gemm_ex(dy2, N, False, x2, K, False, N, K, M, None, False,
+                               _splits(tiles, M), False, 0, None, None, True, False, g, None,
+                               True, 0, None)
+                p._lw_grad_ready(p)
+            else:
+                dw = linear_wgrad(dy2, x2)[:N].to(p.dtype)
+        db = dy2[:, :N].float().sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return dx, dw, db, None
 
 
 def _gemm_ok(x, weight):
-    K, N = weight.shape[1], weight.shape[0]
-    return x.is_cuda and K % 8 == 0 and N % 8 == 0
+    return x.is_cuda and weight.shape[1] % 8 == 0
 
 
 def mfma_linear(x, weight, bias=None, relu=False):

@@ -25,17 +25,28 @@ from ..models.graph import union
 
 def run_batches(model, batches, training, world_size=1, optimizer_step=None, stats=None,
                 compress=None, method=None, K=None, V=None, qstates=None,
-                error_feedback: bool = False, wire: str = "auto", max_batches: Optional[int] = None):
+                error_feedback: bool = False, wire: str = "auto", max_batches: Optional[int] = None,
+                autocast=None):
+    """``autocast``: compute dtype of the forward (the MI355X path: bf16). A model wrapped in
+    :class:`~..parallel.ddp.CompressedDDP` synchronises its gradients from backward hooks and
+    zeroes its gradient arena at the next forward, so no post-backward sync / zero_grad here."""
     stats = stats or StatsLogger(("loss", "correct"))
     model.train(training)
     mode = canonical_mode(compress) if compress not in (None, "none") else "none"
+    hooked = getattr(model, "engine", None) is not None
+    dev_type = next(model.parameters()).device.type
     for i, batch in enumerate(batches):
         if max_batches is not None and i >= max_batches:
             break
         if training:
-            output = model(batch)
+            with torch.autocast(device_type=dev_type, dtype=autocast or torch.float32,
+                                enabled=autocast is not None):
+                output = model(batch)
             stats.append(output)
-            output["loss"].sum().backward()
+            output["loss"].float().sum().backward()
+            if hooked:
+                optimizer_step()
+                continue
             if mode == "layerwise":
                 F.layerwise_compressed_comm(model, world_size, method, K, V, qstates,
                                             error_feedback=error_feedback, wire=wire)
@@ -47,7 +58,9 @@ def run_batches(model, batches, training, world_size=1, optimizer_step=None, sta
             optimizer_step()
             model.zero_grad(set_to_none=False)   # torch 1.x semantics: keep arena views
         else:
-            with torch.no_grad():
+            with torch.no_grad(), torch.autocast(device_type=dev_type,
+                                                 dtype=autocast or torch.float32,
+                                                 enabled=autocast is not None):
                 output = model(batch)
             stats.append(output)
     return stats
@@ -59,7 +72,8 @@ def train_epoch(model, train_batches, test_batches, optimizer_step, timer, world
     train_stats = run_batches(model, train_batches, True, world_size, optimizer_step,
                               compress=compress, method=method, K=K, V=V, qstates=qstates, **kw)
     train_time = timer()
-    test_stats = run_batches(model, test_batches, False, world_size)
+    test_stats = run_batches(model, test_batches, False, world_size,
+                             autocast=kw.get("autocast"))
     test_time = timer(test_time_in_total)
     return {
         "train time": train_time, "train loss": train_stats.mean("loss"),

@@ -32,7 +32,11 @@ class CifarTrainer:
         self.bs = batch_size
         net = build_network(network)
         if fused and self.device.type == "cuda":
+            from ..ops.conv import fuse_convs
+            from ..ops.gemm import fuse_linears
             lwnn.fuse_graph_network(net)
+            fuse_convs(net)          # every conv / Linear on the MFMA kernels
+            fuse_linears(net)
         net = net.to(self.device)
         if self.device.type == "cuda":
             net = net.to(memory_format=torch.channels_last)

@@ -56,6 +56,8 @@ def get_parser() -> argparse.ArgumentParser:
     p.add_argument("--shard_data", action="store_true")
     p.add_argument("--device", type=str, default=None)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--no_fused", action="store_true",
+                   help="the reference's structure: torch layers, post-backward sync, torch SGD")
     return p
 
 
@@ -72,7 +74,21 @@ def main(argv=None):
     epochs = args.epochs or (40 if args.method in ("Randomk", "Thresholdv") else 24)
     lr_schedule = PiecewiseLinear([0, 5, epochs], [0, 0.4, 0])
     bs = args.batch_size
-    model = build_network(args.network).to(device)
+    model = build_network(args.network)
+    # MI355X path (default on a GPU): fused BN+ReLU, every conv / Linear on the MFMA kernels,
+    # bf16 autocast + channels_last, CompressedDDP (compression overlapped with backward) and
+    # the fused flat-arena SGD; --no_fused keeps the reference's structure.
+    fast = device.type == "cuda" and not args.no_fused
+    if fast:
+        from ..ops import nn as lwnn
+        from ..ops.conv import fuse_convs
+        from ..ops.gemm import fuse_linears
+        lwnn.fuse_graph_network(model)
+        fuse_convs(model)
+        fuse_linears(model)
+    model = model.to(device)
+    if fast:
+        model = model.to(memory_format=torch.channels_last)
 
     timer = Timer(synch=torch.cuda.synchronize if device.type == "cuda" else None)
     train_x = D.transpose(D.normalise(D.pad(dataset["train"]["data"], 4)))
@@ -81,27 +97,43 @@ def main(argv=None):
     train_batches = D.GPUBatches(torch.from_numpy(np.ascontiguousarray(train_x)).to(device),
                                  torch.as_tensor(dataset["train"]["labels"]).to(device), bs,
                                  shuffle=True, augment=True, drop_last=True, shard=shard,
-                                 seed=args.seed)
+                                 seed=args.seed, channels_last=fast)
     test_batches = D.GPUBatches(torch.from_numpy(np.ascontiguousarray(test_x)).to(device),
                                 torch.as_tensor(dataset["test"]["labels"]).to(device), bs,
-                                shuffle=False)
+                                shuffle=False, channels_last=fast)
     print(f"Finished preprocessing in {timer():.2f} seconds")
 
     def lr(step):
         return lr_schedule(step / max(len(train_batches), 1)) / bs
 
+    net = model
+    optimizer_cls = torch.optim.SGD
+    if fast:
+        from ..optim.flat_sgd import FlatSGD
+        from ..parallel.ddp import CompressedDDP
+        from .cifar import init_distributed
+        init_distributed(args.master_address, args.world_size, args.rank, args.backend)
+        model = CompressedDDP(net, compress=args.compress, method=args.method, K=args.ratio,
+                              V=args.threshold, qstates=args.qstates,
+                              error_feedback=args.error_feedback, wire=args.wire,
+                              flat_params=True)
+        arena = model.arena
+
+        def optimizer_cls(weights, **kw):               # noqa: F811
+            return FlatSGD(weights, arena, **kw)
     if args.momentum > 0:
-        opt = SGD(trainable_params(model), lr=lr, momentum=args.momentum, weight_decay=5e-4 * bs,
-                  nesterov=True)
+        opt = SGD(trainable_params(net), lr=lr, momentum=args.momentum, weight_decay=5e-4 * bs,
+                  nesterov=True, optimizer=optimizer_cls)
     else:
-        opt = SGD(trainable_params(model), lr=lr, weight_decay=5e-4 * bs)
+        opt = SGD(trainable_params(net), lr=lr, weight_decay=5e-4 * bs, optimizer=optimizer_cls)
 
     tsv = TSVLogger()
     train(model, opt, train_batches, test_batches, epochs, args.master_address, args.world_size,
           args.rank, loggers=(TableLogger(), tsv), timer=timer, test_time_in_total=False,
-          compress=args.compress, method=args.method, K=args.ratio, V=args.threshold,
-          qstates=args.qstates, backend=args.backend, error_feedback=args.error_feedback,
-          wire=args.wire, max_batches=args.max_batches)
+          compress="none" if fast else args.compress, method=args.method, K=args.ratio,
+          V=args.threshold, qstates=args.qstates, backend=args.backend,
+          error_feedback=args.error_feedback, wire=args.wire, max_batches=args.max_batches,
+          autocast=torch.bfloat16 if fast else None)
     os.makedirs(os.path.expanduser(args.log_dir), exist_ok=True)
     with open(os.path.join(os.path.expanduser(args.log_dir), "logs.tsv"), "w") as f:
         f.write(str(tsv))

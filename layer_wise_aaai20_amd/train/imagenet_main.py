@@ -88,7 +88,8 @@ def get_parser():
     p.add_argument("--epochs", type=int, default=None, help="stop after this many epochs")
     p.add_argument("--synthetic-size", type=int, default=None,
                    help="synthetic train images per phase (default 64 batches)")
-    p.add_argument("--no-fused", action="store_true")
+    p.add_argument("--no-fused", action="store_true",
+                   help="torch convs / BN, post-backward sync, torch SGD (the reference's path)")
     p.add_argument("--extra-ckpt", action="store_true")
     p.add_argument("--device", default=None)
     return p
@@ -286,7 +287,9 @@ class DataManager:
                              min_scale=kw.get("min_scale", 0.08),
                              distributed=self.args.distributed, n_train=n_train,
                              n_val=(4 if self.args.short_epoch else 8) * val_bs,
-                             device=self.device, dtype=self.dtype, synthetic=synthetic)
+                             device=self.device, dtype=self.dtype, synthetic=synthetic,
+                             gpu_synthetic=synthetic and self.device.type == "cuda",
+                             pad4=getattr(self.args, "pad4", False))
 
 
 # ------------------------------------------------------------------------------------ run state
@@ -296,6 +299,7 @@ class Run:
         self.world = comm.world_size()
         self.rank = comm.rank()
         self.is_master = self.rank == 0
+        self.fast = False          # set by main(): the fused / CompressedDDP / FlatSGD path
         self.tb = TensorboardLogger(args.logdir, is_master=self.is_master)
         self.log = FileLogger(args.logdir, is_master=self.is_master,
                               is_rank0=(args.local_rank or 0) == 0)
@@ -324,16 +328,28 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
     net_meter, timer = NetworkMeter(), TimeMeter()
     losses, top1, top5 = AverageMeter(), AverageMeter(), AverageMeter()
     model.train()
+    fast = run.fast
+    eng = getattr(model, "engine", None)
+    acc = None                 # fast path: metrics summed on the device, read at print time
     for i, (inp, target) in enumerate(trn_loader):
         if args.short_epoch and i > 10:
             break
         batch_num = i + 1
         timer.batch_start()
         scheduler.update_lr(epoch, batch_num, len(trn_loader))
-        with torch.autocast(device_type=inp.device.type, dtype=torch.bfloat16, enabled=args.bf16):
+        should_print = batch_num % args.print_freq == 0 or batch_num == len(trn_loader)
+        if eng is not None:
+            eng.timing = should_print and run.is_master
+        with torch.autocast(device_type=inp.device.type, dtype=torch.bfloat16,
+                            enabled=args.bf16 or fast):
             output = model(inp)
             loss = criterion(output.float(), target)
-        if args.fp16:
+        if fast:
+            # CompressedDDP: buckets compressed + exchanged during backward, the arena zeroed by
+            # the next forward (no zero_grad); FlatSGD unscales a loss-scaled gradient itself
+            (loss * args.loss_scale if args.fp16 else loss).backward()
+            optimizer.step()
+        elif args.fp16:
             scaled = loss * args.loss_scale
             model.zero_grad()
             scaled.backward()
@@ -350,19 +366,28 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
             loss.backward()
             sync(model)
             optimizer.step()
-        timer.batch_end()
         corr1, corr5 = correct(output.data, target, topk=(1, 5))
         metrics = torch.cat([torch.tensor([float(inp.size(0))], device=loss.device),
-                             loss.detach().float().reshape(1), corr1, corr5])
+                             loss.detach().float().reshape(1) * inp.size(0), corr1, corr5])
         if args.distributed:
             metrics = comm.sum_tensor(metrics)
-        batch_total, reduced_loss, c1, c5 = metrics.cpu().tolist()
-        if args.distributed:
-            reduced_loss /= run.world
-        losses.update(reduced_loss, batch_total)
+        if fast:
+            # no host sync per step (the reference reads the metrics every step): accumulate on
+            # the device, read once per print interval
+            acc = metrics.clone() if acc is None else acc.add_(metrics)
+            timer.batch_end()
+            if not should_print:
+                run.tb.update_step_count(inp.size(0) * run.world)
+                continue
+            batch_total, loss_sum, c1, c5 = acc.cpu().tolist()
+            acc = None
+            timer.batch_time.val = timer.batch_time.avg   # the interval's mean step time
+        else:
+            timer.batch_end()
+            batch_total, loss_sum, c1, c5 = metrics.cpu().tolist()
+        losses.update(loss_sum / batch_total, batch_total)
         top1.update(c1 * 100.0 / batch_total, batch_total)
         top5.update(c5 * 100.0 / batch_total, batch_total)
-        should_print = batch_num % args.print_freq == 0 or batch_num == len(trn_loader)
         if run.is_master and should_print:
             run.tb.log_memory()
             run.tb.log_trn_times(timer.batch_time.val, timer.data_time.val, inp.size(0))
@@ -371,13 +396,17 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
             run.tb.log("sizes/batch_total", batch_total)
             run.tb.log("net/recv_gbit", recv)
             run.tb.log("net/transmit_gbit", sent)
+            if eng is not None:
+                run.tb.log_comm(eng.stats, eng.read_timings() if eng.timing else None)
             run.log.verbose(
                 f"Epoch: [{epoch}][{batch_num}/{len(trn_loader)}]\tTime {timer.batch_time.val:.3f} "
                 f"({timer.batch_time.avg:.3f})\tLoss {losses.val:.4f} ({losses.avg:.4f})\t"
                 f"Acc@1 {top1.val:.3f} ({top1.avg:.3f})\tAcc@5 {top5.val:.3f} ({top5.avg:.3f})\t"
                 f"Data {timer.data_time.val:.3f} ({timer.data_time.avg:.3f})\t"
                 f"BW {recv:.3f} {sent:.3f}")
-        run.tb.update_step_count(batch_total)
+        run.tb.update_step_count(batch_total if not fast else inp.size(0) * run.world)
+    if eng is not None:
+        eng.timing = False
     return losses.avg, top1.avg, top5.avg
 
 
@@ -464,16 +493,32 @@ def main(argv=None):
     tb.log("sizes/world", run.world)
 
     model = getattr(R, args.arch)(bn0=args.init_bn0)
-    if not args.no_fused and device.type == "cuda" and not args.fp16:
+    # the MI355X path (default on a GPU): fused ResNet on the MFMA kernels, flat parameter /
+    # gradient arenas, compression overlapped with backward (CompressedDDP), one fused SGD launch
+    # (FlatSGD; --fp16 keeps its static loss scale, unscaled inside the SGD kernel). --no-fused
+    # selects the reference's structure (torch layers, post-backward sync, torch SGD).
+    run.fast = fast = device.type == "cuda" and not args.no_fused
+    if fast:
         lwnn.fuse_resnet(model)
     model = model.to(device)
     if device.type == "cuda":
         model = model.to(memory_format=torch.channels_last)
-    if args.fp16:
+    if args.fp16 and not fast:
         model = fp16util.network_to_half(model)
     base_model = model
     sync = lambda m: None                                       # noqa: E731
-    if args.ddp:
+    if fast:
+        if args.ddp:
+            model = DistributedDataParallel(model, flat_params=True)
+        elif args.sparsification:
+            model = RandomKSparsifiedDDP(model, randk=args.randk, seed=args.seed,
+                                         flat_params=True)
+        else:
+            model = CompressedDDP(model, compress=args.compress, method=args.method,
+                                  K=args.ratio, V=args.threshold, qstates=args.qstates,
+                                  error_feedback=args.error_feedback, wire=args.wire,
+                                  flat_params=True)
+    elif args.ddp:
         model = DistributedDataParallel(model)
     elif args.sparsification:
         model = RandomKSparsifiedDDP(model, randk=args.randk, seed=args.seed)
@@ -493,7 +538,15 @@ def main(argv=None):
     best_top5 = 93
 
     master = None
-    if args.fp16:
+    if fast:
+        from ..optim.flat_sgd import FlatSGD
+        groups = _bn_groups(base_model, None, args.weight_decay) if args.no_bn_wd else \
+            [{"params": [p for p in base_model.parameters() if p.requires_grad],
+              "weight_decay": args.weight_decay}]
+        optimizer = FlatSGD(groups, model.arena, lr=0.0, momentum=args.momentum,
+                            nesterov=args.momentum > 0, weight_decay=args.weight_decay,
+                            grad_scale=1.0 / args.loss_scale if args.fp16 else 1.0)
+    elif args.fp16:
         master = fp16util.prep_param_lists(model)
         opt_params = _bn_groups(base_model, None, args.weight_decay) if args.no_bn_wd else None
         if opt_params is not None:   # map model params -> masters
@@ -506,14 +559,17 @@ def main(argv=None):
         opt_params = _bn_groups(base_model, None, args.weight_decay) if args.no_bn_wd else \
             [p for p in model.parameters() if p.requires_grad]
     criterion = nn.CrossEntropyLoss().to(device)
-    if args.momentum > 0:
+    if fast:
+        pass
+    elif args.momentum > 0:
         optimizer = torch.optim.SGD(opt_params, 0.0, momentum=args.momentum,
                                     weight_decay=args.weight_decay, nesterov=True)
     else:
         optimizer = torch.optim.SGD(opt_params, 0.0, weight_decay=args.weight_decay)
 
     phases = parse_phases(args.phases)
-    dtype = torch.float16 if args.fp16 else torch.float32
+    dtype = torch.bfloat16 if fast else (torch.float16 if args.fp16 else torch.float32)
+    args.pad4 = fast and bool(getattr(base_model, "_lw_stem_c4", False))
     dm = DataManager([copy.deepcopy(p) for p in phases if "bs" in p], args, device, dtype,
                      log, tb)
     scheduler = Scheduler(optimizer, [copy.deepcopy(p) for p in phases if "lr" in p], log, tb,
@@ -530,6 +586,9 @@ def main(argv=None):
             scheduler.load_state_dict(ckpt["scheduler"])
         if "compression" in ckpt and hasattr(model, "load_compression_state"):
             model.load_compression_state(ckpt["compression"])
+            ef = getattr(model.engine, "ef", None)
+            if ef is not None:
+                log.console(f"EF residual restored: |e|={float(ef.norm()):.6e}")
         log.console(f"resumed from {args.resume} at epoch {args.start_epoch}")
 
     start_time = datetime.now()
@@ -567,6 +626,9 @@ def main(argv=None):
                 extra = {"scheduler": scheduler.state_dict()}
                 if comp is not None:
                     extra["compression"] = comp
+                    if comp.get("ef_per_rank") is not None:
+                        log.console("EF residual saved: |e|="
+                                    f"{float(comp['ef_per_rank'][run.rank].norm()):.6e}")
             if is_best:
                 save_checkpoint(run, epoch, model, best_top5, optimizer, is_best=True,
                                 filename="model_best.pth.tar", extra=extra)

@@ -228,9 +228,22 @@ class TensorboardLogger:
             self.log("sizes/image", sz)
 
     def log_trn_loss(self, loss, top1, top5):
-        self.log("losses/xent", loss)
-        self.log("loss/top1", top1)
-        self.log("loss/top5", top5)
+        self.log("losses/xent", loss)          # reference tags (logger.py:50-53)
+        self.log("losses/train_1", top1)
+        self.log("losses/train_5", top5)
+
+    def log_comm(self, stats, bucket_us=None):
+        """Compression telemetry (SURVEY.md §5 metrics row): bytes this rank put on the wire last
+        step, their ratio to the dense fp32 gradient, and per-bucket compress / exchange / decode
+        µs when the engine timed the step."""
+        self.log("comm/payload_bytes", stats.payload_bytes)
+        self.log("comm/dense_bytes", stats.dense_bytes)
+        self.log("comm/ratio", stats.ratio)
+        for b in bucket_us or []:
+            i = b["bucket"]
+            self.log(f"comm/bucket{i}_compress_us", b["compress_us"])
+            self.log(f"comm/bucket{i}_exchange_us", b["exchange_us"])
+            self.log(f"comm/bucket{i}_decode_us", b["decode_us"])
 
     def log_eval(self, top1, top5, time_):
         self.log("losses/test_1", top1)

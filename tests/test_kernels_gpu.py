@@ -212,3 +212,25 @@ def test_invalid_launch_raises():
         load().selftest_bad_launch(torch.empty(1, device="cuda"))
     torch.cuda.synchronize()            # not sticky: the device keeps working
     assert torch.ones(4, device="cuda").sum().item() == 4
+
+
+@pytest.mark.parametrize("adaptive", [False, True])
+@pytest.mark.parametrize("with_ef", [False, True])
+def test_threshold_dense_in_place_matches_cpu(adaptive, with_ef):
+    """Threshold methods on the dense wire: the GPU kernel (k_thresh_dense) and the CPU mirror
+    produce the same compressed vector and residual."""
+    torch.manual_seed(0)
+    sizes = [5000, 64, 20000, 9000]
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).tolist()
+    plan = SegPlan(offs, sizes)
+    g = torch.randn(sum(sizes)) * 0.01
+    ef = torch.randn(sum(sizes)) * 0.001 if with_ef else None
+    c = codecs.ThresholdCodec(plan, 1, 0, V=0.005, adaptive=adaptive)
+    gc, ec = g.clone(), (ef.clone() if with_ef else None)
+    c.compress_dense(gc, ec)
+    gg, eg = g.cuda(), (ef.cuda() if with_ef else None)
+    c.compress_dense(gg, eg)
+    assert torch.equal(gg.cpu(), gc)
+    if with_ef:
+        assert torch.equal(eg.cpu(), ec)
+    assert 0 < int((gc != 0).sum()) < gc.numel()

@@ -214,7 +214,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (random uint8 224x224 images, random labels; random-init weights)",
+        "data": "synthetic (class-conditional random uint8 224x224 images, pool of 4 batches; random-init weights)",
         "top1_heldout_synthetic": round(top1, 3),
         "top1_note": (f"held-out batches of the class-conditional synthetic distribution after "
                       f"{args.warmup + args.steps + 1} training steps (chance = 0.1%)"),

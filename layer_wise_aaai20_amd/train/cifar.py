@@ -113,6 +113,10 @@ def train(model, optimizer, train_batches, test_batches, epochs, master_address=
         lr = optimizer.param_values()["lr"] if hasattr(optimizer, "param_values") else \
             optimizer.param_groups[0]["lr"]
         summary = union({"epoch": epoch + 1, "lr": lr * train_batches.batch_size}, epoch_stats)
+        eng = getattr(model, "engine", None)
+        if eng is not None:              # compression telemetry: wire bytes of the last step
+            summary = union(summary, {"comm MB": eng.stats.payload_bytes / 1e6,
+                                      "comm ratio": eng.stats.ratio})
         for logger in loggers:
             logger.append(summary)
     return summary

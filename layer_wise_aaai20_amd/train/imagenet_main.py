@@ -331,6 +331,7 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
     fast = run.fast
     eng = getattr(model, "engine", None)
     acc = None                 # fast path: metrics summed on the device, read at print time
+    t_mark, n_mark = time.perf_counter(), 0
     for i, (inp, target) in enumerate(trn_loader):
         if args.short_epoch and i > 10:
             break
@@ -375,13 +376,17 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
             # no host sync per step (the reference reads the metrics every step): accumulate on
             # the device, read once per print interval
             acc = metrics.clone() if acc is None else acc.add_(metrics)
-            timer.batch_end()
+            timer.start = time.time()            # (data time only; step time per interval)
             if not should_print:
                 run.tb.update_step_count(inp.size(0) * run.world)
                 continue
-            batch_total, loss_sum, c1, c5 = acc.cpu().tolist()
+            batch_total, loss_sum, c1, c5 = acc.cpu().tolist()   # (waits for the GPU)
             acc = None
-            timer.batch_time.val = timer.batch_time.avg   # the interval's mean step time
+            # the interval's mean step time, GPU-complete (host time per step is not: the host
+            # runs ahead of the device between syncs)
+            now = time.perf_counter()
+            timer.batch_time.update((now - t_mark) / (batch_num - n_mark), batch_num - n_mark)
+            t_mark, n_mark = now, batch_num
         else:
             timer.batch_end()
             batch_total, loss_sum, c1, c5 = metrics.cpu().tolist()
@@ -588,7 +593,7 @@ def main(argv=None):
             model.load_compression_state(ckpt["compression"])
             ef = getattr(model.engine, "ef", None)
             if ef is not None:
-                log.console(f"EF residual restored: |e|={float(ef.norm()):.6e}")
+                log.console(f"EF residual restored: |e|={float(ef.double().norm()):.9e}")
         log.console(f"resumed from {args.resume} at epoch {args.start_epoch}")
 
     start_time = datetime.now()
@@ -628,7 +633,7 @@ def main(argv=None):
                     extra["compression"] = comp
                     if comp.get("ef_per_rank") is not None:
                         log.console("EF residual saved: |e|="
-                                    f"{float(comp['ef_per_rank'][run.rank].norm()):.6e}")
+                                    f"{float(comp['ef_per_rank'][run.rank].double().norm()):.9e}")
             if is_best:
                 save_checkpoint(run, epoch, model, best_top5, optimizer, is_best=True,
                                 filename="model_best.pth.tar", extra=extra)

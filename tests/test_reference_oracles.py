@@ -54,12 +54,13 @@ def test_terngrad_values_and_zero_guard():
 
 
 def test_qsgd_unbiased_and_zero_guard():
-    g = torch.randn(256)
+    g = torch.randn(256, generator=torch.Generator().manual_seed(2))
     gen = torch.Generator().manual_seed(3)
     acc = torch.zeros(256)
     for _ in range(400):
         acc += ref.random_dithering(g, 4, gen)
-    torch.testing.assert_close(acc / 400, g, rtol=0, atol=0.25)
+    # level spacing ||g||/s ~ 4 -> per-sample std <= 2, std of the 400-mean <= 0.1: 5 sigma
+    torch.testing.assert_close(acc / 400, g, rtol=0, atol=0.5)
     assert torch.equal(ref.random_dithering(torch.zeros(4), 255), torch.zeros(4))
 
 

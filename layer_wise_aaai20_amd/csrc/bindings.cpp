@@ -337,6 +337,41 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
   launched("normalize_u8");
 }
 
+// global average pool (nn.hip): x channels_last bf16 [N, C, H, W] -> [N, C] bf16
+Tensor gap_fwd(Tensor x) {
+  const c10::DeviceGuard guard(x.device());
+  TORCH_CHECK(x.is_cuda(), "x must be a GPU tensor");
+  check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "x must be a channels_last NCHW tensor");
+  const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
+  TORCH_CHECK(C % 8 == 0 && N * C < (1LL << 31) && N * HW * C < (1LL << 34), "gap_fwd: C % 8 == 0");
+  check_aligned16(x.data_ptr(), "x");
+  Tensor y = at::empty({N, C}, x.options());
+  lw::gap_fwd(ptr<uint16_t>(x), ptr<uint16_t>(y), (int)N, (int)HW, (int)C, cur_stream());
+  launched("gap_fwd");
+  return y;
+}
+
+// dy [N, C] bf16/fp32 -> channels_last bf16 [N, C, H, W] filled with dy / (H*W)
+Tensor gap_bwd(Tensor dy, int64_t H, int64_t W) {
+  const c10::DeviceGuard guard(dy.device());
+  check_cuda(dy, "dy");
+  TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous(), "dy must be a contiguous [N, C] tensor");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kFloat,
+              "dy must be bf16 or fp32");
+  const int64_t N = dy.size(0), C = dy.size(1);
+  TORCH_CHECK(C % 8 == 0 && H > 0 && W > 0 && N * H * W * (C / 8) < (1LL << 31),
+              "gap_bwd: C % 8 == 0 and N*H*W*C/8 < 2^31");
+  check_aligned16(dy.data_ptr(), "dy");
+  Tensor dx = at::empty({N, C, H, W}, dy.options().dtype(at::kBFloat16),
+                        at::MemoryFormat::ChannelsLast);
+  lw::gap_bwd(dy.data_ptr(), dy.scalar_type() == at::kFloat, ptr<uint16_t>(dx), (int)N,
+              (int)(H * W), (int)C, cur_stream());
+  launched("gap_bwd");
+  return dx;
+}
+
 // ---------------------------------------------------------------- fused BatchNorm (NHWC)
 void check_nhwc(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -813,7 +848,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stat
     TORCH_CHECK(stats->dim() == 3 && stats->size(1) == 2 && stats->size(2) == C &&
                 stats->is_contiguous(), "stats must be a contiguous [rows, 2, C] tensor");
     const int64_t R = stats->size(0);
-    partial = at::empty({(R < 256 ? R : 256) * 2 * C}, f32);
+    partial = at::empty({(int64_t)lw::colsum_blocks(R) * 2 * C}, f32);
     a.partial = ptr<float>(partial);
     a.stat_rows = ptr<float>(*stats);
     a.stats_rows_n = R;
@@ -992,6 +1027,8 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
       "int nesterov, int first_step, float grad_scale) -> ()");
   m.def("normalize_u8(Tensor input, Tensor(a!) out, float[] mean, float[] std) -> ()");
+  m.def("gap_fwd(Tensor x) -> Tensor");
+  m.def("gap_bwd(Tensor dy, int H, int W) -> Tensor");
   m.def(
       "bn_fwd(Tensor x, Tensor? res, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
       "Tensor(b!)? running_var, bool training, float momentum, float eps, bool relu) "
@@ -1039,6 +1076,8 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("dequantize", &dequantize);
   m.impl("sgd_step", &sgd_step);
   m.impl("normalize_u8", &normalize_u8);
+  m.impl("gap_fwd", &gap_fwd);
+  m.impl("gap_bwd", &gap_bwd);
   m.impl("bn_fwd", &bn_fwd);
   m.impl("bn_bwd", &bn_bwd);
   m.impl("gemm", &gemm);

@@ -25,6 +25,19 @@ __device__ __forceinline__ uint16_t f2bf_rne(float f) {
 
 template <typename T> struct V8;
 template <> struct V8<uint16_t> {
+  // raw 16-byte form, so a loop can have the next rows' loads in flight while it converts and
+  // accumulates the current ones
+  typedef uint4 Raw;
+  static __device__ __forceinline__ Raw ld(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+  static __device__ __forceinline__ Raw zero() { return make_uint4(0u, 0u, 0u, 0u); }
+  static __device__ __forceinline__ void cvt(const Raw& v, float f[8]) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = __uint_as_float(w[k] << 16);
+      f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
   static __device__ __forceinline__ void load(const uint16_t* p, float f[8]) {
     const uint4 v = *reinterpret_cast<const uint4*>(p);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -43,6 +56,17 @@ template <> struct V8<uint16_t> {
   }
 };
 template <> struct V8<float> {
+  struct Raw { float4 a, b; };
+  static __device__ __forceinline__ Raw ld(const float* p) {
+    return Raw{reinterpret_cast<const float4*>(p)[0], reinterpret_cast<const float4*>(p)[1]};
+  }
+  static __device__ __forceinline__ Raw zero() {
+    return Raw{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+  }
+  static __device__ __forceinline__ void cvt(const Raw& v, float f[8]) {
+    f[0] = v.a.x; f[1] = v.a.y; f[2] = v.a.z; f[3] = v.a.w;
+    f[4] = v.b.x; f[5] = v.b.y; f[6] = v.b.z; f[7] = v.b.w;
+  }
   static __device__ __forceinline__ void load(const float* p, float f[8]) {
     const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
     f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
@@ -78,100 +102,101 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
                                                    float* __restrict__ partial) {
   __shared__ float sa[BNT * 8];
   __shared__ float sb[BNT * 8];
-  const int G = C / 8;
+  // blockIdx.y selects a slice of Cb channels (reduce_geometry): a block reads Cb-wide row
+  // segments, so it writes 2*Cb partial sums instead of 2*C scattered ones (at C = 2048 the
+  // whole-row form spent most of its time on 4096 strided partial stores per block)
+  const int Cb = C / (int)gridDim.y, c_off = (int)blockIdx.y * Cb;
+  const int G = Cb / 8, GC = C / 8;
   const int R = BNT / G;                    // rows processed per iteration (>= 1)
   const int g = threadIdx.x % G, r = threadIdx.x / G;
+  const int gc = c_off / 8 + g;             // this thread's channel group within the full row
   const bool active = r < R;
   float a[8], b[8], mu[8], fs[8], fh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { a[k] = 0.f; b[k] = 0.f; mu[k] = 0.f; fs[k] = 0.f; fh[k] = 0.f; }
   if (MODE == 1 && active) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) mu[k] = mean[g * 8 + k];
+    for (int k = 0; k < 8; ++k) mu[k] = mean[gc * 8 + k];
     if (RELU == 2) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { fs[k] = fscale[g * 8 + k]; fh[k] = fshift[g * 8 + k]; }
+      for (int k = 0; k < 8; ++k) { fs[k] = fscale[gc * 8 + k]; fh[k] = fshift[gc * 8 + k]; }
     }
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(r0 + rows_per_block, M);
   if (active) {
-    const T* xp = x + g * 8;
-    const T* dp = dy + g * 8;
-    const T* yp = y + g * 8;
-    int64_t row = r0 + r;
-    for (; row + (U - 1) * R < r1; row += U * R) {
-      float xv[U][8], d[U][8];
-#pragma unroll
-      for (int u = 0; u < U; ++u) V8<T>::load(xp + (row + u * R) * C, xv[u]);
-      if (MODE == 1) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) V8<T>::load(dp + (row + u * R) * C, d[u]);
-        if (RELU == 1) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            float yv[8];
-            V8<T>::load(yp + (row + u * R) * C, yv);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) d[u][k] = yv[k] > 0.f ? d[u][k] : 0.f;
-          }
-        } else if (RELU == 2) {
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              d[u][k] = fmaf(xv[u][k], fs[k], fh[k]) > 0.f ? d[u][k] : 0.f;
-        } else if (RELU == 3) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) mask_bits(d[u], bits[(row + u * R) * G + g]);
-        }
-      }
+    using V = V8<T>;
+    typedef typename V::Raw Raw;
+    const T* xp = x + gc * 8;
+    const T* dp = dy + gc * 8;
+    const T* yp = y + gc * 8;
+    // Software-pipelined: the U rows of the next iteration are loaded (raw, predicated: rows past
+    // r1 read as zero and add nothing) before the current U rows are converted and accumulated.
+    Raw cx[U], cd[U], cy[U];
+    uint32_t cb[U];
+    auto fetch = [&](int64_t row0, Raw (&fx)[U], Raw (&fd)[U], Raw (&fy)[U], uint32_t (&fb)[U]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          if (MODE == 0) { a[k] += xv[u][k]; b[k] += xv[u][k] * xv[u][k]; }
-          else { a[k] += d[u][k]; b[k] += d[u][k] * (xv[u][k] - mu[k]); }
+        const int64_t rw = row0 + u * R;
+        const bool in = rw < r1;
+        fx[u] = in ? V::ld(xp + rw * C) : V::zero();
+        if (MODE == 1) {
+          fd[u] = in ? V::ld(dp + rw * C) : V::zero();
+          if (RELU == 1) fy[u] = in ? V::ld(yp + rw * C) : V::zero();
+          if (RELU == 3) fb[u] = in ? (uint32_t)bits[rw * GC + gc] : 0u;
         }
       }
-    }
-    for (; row < r1; row += R) {
-      float xv[8];
-      V8<T>::load(xp + row * C, xv);
-      if (MODE == 0) {
+    };
+    int64_t row = r0 + r;
+    fetch(row, cx, cd, cy, cb);
+    for (; row < r1; row += U * R) {
+      Raw nx[U], nd[U], ny[U];
+      uint32_t nb8[U];
+      const bool more = row + U * R < r1;
+      if (more) fetch(row + U * R, nx, nd, ny, nb8);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) { a[k] += xv[k]; b[k] += xv[k] * xv[k]; }
-      } else {
-        float d[8];
-        V8<T>::load(dp + row * C, d);
-        if (RELU == 1) {
-          float yv[8];
-          V8<T>::load(yp + row * C, yv);
+      for (int u = 0; u < U; ++u) {
+        float xv[8];
+        V::cvt(cx[u], xv);
+        if (MODE == 0) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
-        } else if (RELU == 2) {
+          for (int k = 0; k < 8; ++k) { a[k] += xv[k]; b[k] += xv[k] * xv[k]; }
+        } else {
+          float d[8];
+          V::cvt(cd[u], d);
+          if (RELU == 1) {
+            float yv[8];
+            V::cvt(cy[u], yv);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) d[k] = fmaf(xv[k], fs[k], fh[k]) > 0.f ? d[k] : 0.f;
-        } else if (RELU == 3) {
-          mask_bits(d, bits[row * G + g]);
+            for (int k = 0; k < 8; ++k) d[k] = yv[k] > 0.f ? d[k] : 0.f;
+          } else if (RELU == 2) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d[k] = fmaf(xv[k], fs[k], fh[k]) > 0.f ? d[k] : 0.f;
+          } else if (RELU == 3) {
+            mask_bits(d, cb[u]);
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { a[k] += d[k]; b[k] += d[k] * (xv[k] - mu[k]); }
         }
+      }
+      if (more) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) { a[k] += d[k]; b[k] += d[k] * (xv[k] - mu[k]); }
+        for (int u = 0; u < U; ++u) { cx[u] = nx[u]; cd[u] = nd[u]; cy[u] = ny[u]; cb[u] = nb8[u]; }
       }
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      sa[r * C + g * 8 + k] = a[k];
-      sb[r * C + g * 8 + k] = b[k];
+      sa[r * Cb + g * 8 + k] = a[k];
+      sb[r * Cb + g * 8 + k] = b[k];
     }
   }
   __syncthreads();
   const int64_t nb = gridDim.x;
-  for (int c = threadIdx.x; c < C; c += BNT) {
+  for (int c = threadIdx.x; c < Cb; c += BNT) {
     float s1 = 0.f, s2 = 0.f;
-    for (int q = 0; q < R; ++q) { s1 += sa[q * C + c]; s2 += sb[q * C + c]; }
-    partial[(int64_t)c * nb + blockIdx.x] = s1;                 // channel-major: [2][C][nb]
-    partial[((int64_t)C + c) * nb + blockIdx.x] = s2;
+    for (int q = 0; q < R; ++q) { s1 += sa[q * Cb + c]; s2 += sb[q * Cb + c]; }
+    partial[(int64_t)(c_off + c) * nb + blockIdx.x] = s1;       // channel-major: [2][C][nb]
+    partial[((int64_t)C + c_off + c) * nb + blockIdx.x] = s2;
   }
 }
 
@@ -185,7 +210,19 @@ __device__ __forceinline__ bool fold_partials(const float* __restrict__ partial,
   const float* p1 = partial + (int64_t)c * nblocks;
   const float* p2 = partial + ((int64_t)C + c) * nblocks;
   float a = 0.f, b = 0.f;
-  for (int blk = lane; blk < nblocks; blk += 64) { a += p1[blk]; b += p2[blk]; }
+  // 16 strided loads per lane issued together, then added in block order (a plain strided loop
+  // waited for each load in turn: ~8 µs of HBM latency per launch)
+  for (int base = 0; base < nblocks; base += 16 * 64) {
+    float va[16], vb[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int blk = base + u * 64 + lane;
+      va[u] = blk < nblocks ? p1[blk] : 0.f;
+      vb[u] = blk < nblocks ? p2[blk] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) { a += va[u]; b += vb[u]; }
+  }
   double da = a, db = b;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -400,15 +437,29 @@ static int reduce_unroll() {
   return u;
 }
 
+// Reduce grid: (row blocks) x (channel slices of Cb = 128 channels when C is a multiple of 128,
+// else the whole row). About LWAAAI_BN_BLOCKS workgroups in total; nblocks (row blocks) is the
+// number of partial sums per channel the finalize folds.
+static int reduce_slices(int C) { return (C > 128 && C % 128 == 0) ? C / 128 : 1; }
+
 static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblocks) {
-  const int G = C / 8;
+  const int nsl = reduce_slices(C);
+  const int G = C / nsl / 8;
   const int R = BNT / G;
   static const int64_t target = env_int("LWAAAI_BN_BLOCKS", 1024);   // ≈ 4 blocks per CU
-  int64_t rpb = (M + target - 1) / target;
+  const int64_t rb = (target + nsl - 1) / nsl;
+  int64_t rpb = (M + rb - 1) / rb;
   rpb = (rpb + R - 1) / R * R;
   rpb = rpb < R ? R : rpb;
   rows_per_block = rpb;
   nblocks = (int)((M + rpb - 1) / rpb);
+}
+
+// GEMM statistics rows folded per block: a few rows each, so every block's loads are in flight at
+// once (the finalize then folds up to 1024 partials per channel with unrolled loads)
+int colsum_blocks(int64_t rows) {
+  static const int cap = env_int("LWAAAI_COLSUM_BLOCKS", 1024);
+  return (int)(rows < cap ? rows : cap);
 }
 
 int bn_reduce_blocks(int64_t M, int C) {
@@ -456,7 +507,7 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
   int nb = a.stats_blocks;
   if (a.stat_rows) {                      // GEMM epilogue rows [R][2C] -> [2C][nb]
     const int64_t R = a.stats_rows_n;
-    nb = (int)(R < 256 ? R : 256);
+    nb = colsum_blocks(R);
     const int64_t rpb = (R + nb - 1) / nb;
     nb = (int)((R + rpb - 1) / rpb);
     hipLaunchKernelGGL(k_colsum, dim3(nb), dim3(256), 0, st, a.stat_rows, R, 2 * a.C, rpb,
@@ -465,7 +516,7 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
     int64_t rpb;
     reduce_geometry(a.M, a.C, rpb, nb);
     auto kern = reduce_unroll() == 8 ? k_bn_reduce<T, 0, 0, 8> : k_bn_reduce<T, 0, 0, 4>;
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(BNT), 0, st, static_cast<const T*>(a.x),
+    hipLaunchKernelGGL(kern, dim3(nb, reduce_slices(a.C)), dim3(BNT), 0, st, static_cast<const T*>(a.x),
                        (const T*)nullptr, (const T*)nullptr, (const uint8_t*)nullptr,
                        (const float*)nullptr,
                        (const float*)nullptr, (const float*)nullptr, a.M, a.C, rpb, a.partial);
@@ -496,7 +547,7 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   const int rmode = !a.relu ? 0 : (a.bits ? 3 : (a.scale ? 2 : 1));
 #define LW_RED(R)                                                                                \
   hipLaunchKernelGGL((reduce_unroll() == 8 ? k_bn_reduce<T, 1, R, 8> : k_bn_reduce<T, 1, R, 4>), \
-                     dim3(nb), dim3(BNT), 0, st, x, dy, y, a.bits, a.mean, \
+                     dim3(nb, reduce_slices(a.C)), dim3(BNT), 0, st, x, dy, y, a.bits, a.mean, \
                      a.scale, a.shift, a.M, a.C, rpb, a.partial)
   if (rmode == 0) LW_RED(0); else if (rmode == 1) LW_RED(1); else if (rmode == 2) LW_RED(2);
   else LW_RED(3);

@@ -139,6 +139,7 @@ struct BNArgs {
   bool accum_dparams;      // backward: dgamma/dbeta += (into the gradient arena) instead of =
 };
 int bn_reduce_blocks(int64_t M, int C);
+int colsum_blocks(int64_t rows);     // blocks folding R GEMM-epilogue statistics rows
 void bn_stats(const BNArgs& a, hipStream_t st);
 void bn_apply(const BNArgs& a, hipStream_t st);
 void bn_forward(const BNArgs& a, hipStream_t st);
@@ -231,6 +232,10 @@ bool conv_tile_ok(int mode, int tile);
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
                   const float stdv[3], bool bf16, hipStream_t st);
 void launch_invalid_config_for_test(hipStream_t st);
+// global average pool of NHWC bf16 [N, HW, C] (C % 8 == 0): forward to [N, C] bf16, backward
+// from [N, C] bf16/fp32 to the channels_last [N, HW, C] bf16 gradient (nn.hip)
+void gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
+void gap_bwd(const void* dy, bool dy_f32, uint16_t* dx, int N, int HW, int C, hipStream_t st);
 void normalize_u8_c4(const uint8_t* in, uint16_t* out, int64_t npix, const float mean[3],
                      const float stdv[3], hipStream_t st);
 

@@ -18,6 +18,11 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// round to nearest even, NaN-preserving (the gfx950 hardware conversion)
+__device__ __forceinline__ uint16_t bf16_cast(float f) {
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
+}
+
 template <bool BF16>
 __global__ __launch_bounds__(256) void k_normalize_u8(const uint8_t* __restrict__ in,
                                                       void* __restrict__ out, int64_t nbytes,
@@ -135,6 +140,80 @@ void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean
   else
     hipLaunchKernelGGL(k_normalize_u8<false>, grid, block, 0, st, in, out, nbytes, mean[0], mean[1],
                        mean[2], 1.f / stdv[0], 1.f / stdv[1], 1.f / stdv[2]);
+}
+
+// ---- global average pool over NHWC bf16 (the ResNet head, IMAGENET/training/resnet.py:141-142:
+// AdaptiveAvgPool2d(1) + flatten). Forward: y[n, c] = mean over the HW pixels, fp32 accumulation,
+// one thread per (n, 8 channels). Backward: dx[n, p, c] = dy[n, c] / HW written straight into the
+// channels_last gradient the last bottleneck consumes (torch's backward materialised an expanded
+// NCHW tensor and then copied it to channels_last: ~100 µs per step at 256 x 2048 x 7 x 7).
+__global__ __launch_bounds__(256) void k_gap_fwd(const uint16_t* __restrict__ x,
+                                                 uint16_t* __restrict__ y, int N, int HW, int C,
+                                                 float inv_hw) {
+  const int G = C / 8;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * G) return;
+  const int n = t / G, g = t - n * G;
+  const uint16_t* p = x + (int64_t)n * HW * C + g * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < HW; ++i) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p + (int64_t)i * C);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[2 * k] += __uint_as_float(w[k] << 16);
+      acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    o[k] = (uint32_t)bf16_cast(acc[2 * k] * inv_hw) | ((uint32_t)bf16_cast(acc[2 * k + 1] * inv_hw) << 16);
+  *reinterpret_cast<uint4*>(y + (int64_t)n * C + g * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// dy: [N, C] bf16 (DY_F32 = false) or fp32
+template <bool DY_F32>
+__global__ __launch_bounds__(256) void k_gap_bwd(const void* __restrict__ dy,
+                                                 uint16_t* __restrict__ dx, int N, int HW, int C,
+                                                 float inv_hw) {
+  const int G = C / 8;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * HW * G) return;
+  const int g = (int)(t % G);
+  const int n = (int)(t / ((int64_t)HW * G));
+  float d[8];
+  if (DY_F32) {
+    const float* q = static_cast<const float*>(dy) + (int64_t)n * C + g * 8;
+    const float4 a = reinterpret_cast<const float4*>(q)[0], b = reinterpret_cast<const float4*>(q)[1];
+    d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+  } else {
+    const uint4 v = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(dy) + (int64_t)n * C + g * 8);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      d[2 * k] = __uint_as_float(w[k] << 16);
+      d[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  }
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    o[k] = (uint32_t)bf16_cast(d[2 * k] * inv_hw) | ((uint32_t)bf16_cast(d[2 * k + 1] * inv_hw) << 16);
+  *reinterpret_cast<uint4*>(dx + t * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+void gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st) {
+  const int thr = N * (C / 8);
+  hipLaunchKernelGGL(k_gap_fwd, dim3((thr + 255) / 256), dim3(256), 0, st, x, y, N, HW, C,
+                     1.f / (float)HW);
+}
+
+void gap_bwd(const void* dy, bool dy_f32, uint16_t* dx, int N, int HW, int C, hipStream_t st) {
+  const int64_t thr = (int64_t)N * HW * (C / 8);
+  const dim3 grid((unsigned)((thr + 255) / 256)), block(256);
+  if (dy_f32) hipLaunchKernelGGL(k_gap_bwd<true>, grid, block, 0, st, dy, dx, N, HW, C, 1.f / (float)HW);
+  else hipLaunchKernelGGL(k_gap_bwd<false>, grid, block, 0, st, dy, dx, N, HW, C, 1.f / (float)HW);
 }
 
 }  // namespace lw

@@ -306,6 +306,30 @@ def stem_bn_relu_pool(c: torch.Tensor, bn: nn.BatchNorm2d, pool: nn.MaxPool2d) -
     return _StemPoolFn.apply(c, bn.weight, bn.bias, bn, _pool_geom(pool))
 
 
+class _GlobalAvgPoolFn(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1) + flatten on a channels_last bf16 map (``csrc/nn.hip`` k_gap_*): the
+    backward writes ``dy / HW`` straight into the channels_last gradient of the last block."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[2], x.shape[3])
+        return load().gap_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return load().gap_bwd(dy.contiguous(), *ctx.hw)
+
+
+def global_avg_pool(x: torch.Tensor, pool: nn.Module) -> torch.Tensor:
+    """``flatten(pool(x), 1)`` for ``AdaptiveAvgPool2d(1)``: the HIP kernels on a CUDA
+    channels_last bf16 input with C % 8 == 0, torch otherwise."""
+    if (isinstance(pool, nn.AdaptiveAvgPool2d) and pool.output_size in (1, (1, 1)) and x.is_cuda
+            and x.dim() == 4 and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last)):
+        return _GlobalAvgPoolFn.apply(x)
+    return torch.flatten(pool(x), 1)
+
+
 def _fused_resnet_forward(self, x):
     if getattr(self, "_lw_stem_c4", False) and stem_conv_supported(self, x):
         x = stem_conv_bn_relu_pool(x, self.conv1, self.bn1, self.maxpool)
@@ -316,8 +340,7 @@ def _fused_resnet_forward(self, x):
         else:
             x = self.maxpool(self.bn1(c))
     x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-    x = torch.flatten(self.avgpool(x), 1)
-    return self.fc(x)
+    return self.fc(global_avg_pool(x, self.avgpool))
 
 
 def fuse_resnet(model: nn.Module, block: bool = True, mfma: bool = True) -> nn.Module:

@@ -11,5 +11,5 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/prof/$TAG -o run --ou
 KT=$(find /tmp/prof/$TAG -name '*kernel_trace.csv' | head -1)
 ST=$(find /tmp/prof/$TAG -name '*kernel_stats.csv' | head -1)
 cp "$ST" gpurun_out/${TAG}_kernel_stats.csv
-python scripts/trace_steps.py "$KT" 5 -v > gpurun_out/${TAG}_steps.txt
+SEQ=gpurun_out/${TAG}_seq.txt python scripts/trace_steps.py "$KT" 5 -v > gpurun_out/${TAG}_steps.txt
 cat gpurun_out/${TAG}_steps.txt

@@ -37,6 +37,14 @@ def main(path, last=5, verbose=False):
         if verbose:
             for k, (t2, n2) in sorted(names[c].items(), key=lambda x: -x[1][0])[:int(__import__("os").environ.get("TOPK", "14"))]:
                 print(f"      {t2 / last:7.3f}  x{n2 // last:<4d} {k}")
+    seq = __import__("os").environ.get("SEQ")
+    if seq:                       # the last step's kernels in launch order (what precedes a copy)
+        one = rows[sgd[-2] + 1:sgd[-1] + 1]
+        with open(seq, "w") as f:
+            for r in one:
+                d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                grid = r.get("Grid_Size", r.get("Grid_Size_X", ""))
+                f.write(f"{d:9.1f} us  grid={grid:>8}  {r['Kernel_Name'][:110]}\n")
 
 
 if __name__ == "__main__":

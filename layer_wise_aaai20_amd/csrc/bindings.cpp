@@ -658,7 +658,8 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
                                    int64_t N, int64_t tile, int64_t splits, bool out_bf16,
                                    c10::optional<Tensor> pro_scale, c10::optional<Tensor> pro_shift,
                                    bool want_stats, c10::optional<Tensor> out, bool accumulate,
-                                   int64_t ldc, bool b_kcontig, int64_t ldb) {
+                                   int64_t ldc, bool b_kcontig, int64_t ldb,
+                                   c10::optional<Tensor> addend) {
   const c10::DeviceGuard guard(G.device());
   TORCH_CHECK(G.is_cuda() && Op.is_cuda(), "conv needs GPU tensors");
   check_dtype(G, at::kBFloat16, "gathered tensor");
@@ -773,7 +774,17 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
   } else {
     TORCH_CHECK(!accumulate, "accumulate needs an out tensor");
     C = at::empty({out_rows, ldc}, G.options().dtype(odt));
-    if (ga && (h.nclass > 1 || h.osy > 1 || h.osx > 1)) C.zero_();   // pixels no class covers
+    if (ga && (h.nclass > 1 || h.osy > 1 || h.osx > 1)) {
+      // the parity classes are disjoint pixel sets: zero only when some pixel has no class
+      int64_t covered = 0;
+      bool disjoint = true;
+      for (int i = 0; i < h.nclass; ++i) {
+        covered += (int64_t)h.Hg[i] * h.Wg[i];
+        disjoint = disjoint && h.py[i] < h.osy && h.px[i] < h.osx;
+        for (int j = 0; j < i; ++j) disjoint = disjoint && (h.py[j] != h.py[i] || h.px[j] != h.px[i]);
+      }
+      if (!disjoint || covered != (int64_t)h.Hout * h.Wout) C.zero_();
+    }
   }
   g.C = C.data_ptr();
   g.ldc = ldc;
@@ -788,6 +799,16 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
     g.pro_scale = ptr<float>(*pro_scale);
     g.pro_shift = ptr<float>(*pro_shift);
     g.pro_on_a = ga;
+  }
+  if (addend.has_value() && addend->defined()) {
+    // bf16 [out_rows][ldc] added after rounding, indexed by output row (may alias `out`)
+    TORCH_CHECK(ga && out_bf16 && !accumulate, "conv addend: bf16 row-gather (fwd/dgrad) output");
+    check_dtype(*addend, at::kBFloat16, "addend");
+    TORCH_CHECK(addend->is_cuda() && (addend->is_contiguous() ||
+                addend->is_contiguous(at::MemoryFormat::ChannelsLast)), "addend must be dense");
+    TORCH_CHECK(addend->numel() >= (out_rows - 1) * ldc + N, "addend too small");
+    check_aligned16(addend->data_ptr(), "addend");
+    g.addend = ptr<uint16_t>(*addend);
   }
   const int zs = ga ? 1 : lw::conv_splits_used(g);
   Tensor partial, stats;
@@ -1051,7 +1072,7 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "conv_ex(Tensor G, Tensor Op, int mode, int[] geom, int N, int tile, int splits, "
       "bool out_bf16, Tensor? pro_scale, Tensor? pro_shift, bool want_stats, Tensor(a!)? out, "
-      "bool accumulate, int ldc, bool b_kcontig, int ldb) -> (Tensor, Tensor)");
+      "bool accumulate, int ldc, bool b_kcontig, int ldb, Tensor? addend=None) -> (Tensor, Tensor)");
   m.def(
       "bn_stats(Tensor x, Tensor? stats, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
       "Tensor(b!)? running_var, float momentum, float eps) -> (Tensor, Tensor, Tensor)");

@@ -740,6 +740,120 @@ __global__ __launch_bounds__(BNT) void k_stem_pool_bwd(const uint16_t* __restric
   }
 }
 
+// 3x3 / stride 2 / pad 1 pool with H == 2*Ho, W == 2*Wo (the ResNet stem): thread (g, r) takes
+// the 2x2 input block (2y..2y+1, 2x..2x+1) of output-grid point (y, x) — exactly the pixels
+// windows (y|y+1, x|x+1) cover — so every load is issued up front (4 windows' gradients and
+// argmax slots, 4 input pixels) with no data-dependent loop, and each window is read by the 4
+// blocks that share it (L2 hits) instead of each input pixel walking its windows serially.
+// Input row 2y+a is reached by window row y at kh = 1 + a and, for a = 1, by row y+1 at kh = 0.
+template <int MODE>
+__global__ __launch_bounds__(BNT) void k_stem_pool_bwd_s2(const uint16_t* __restrict__ dp,
+                                                          const uint8_t* __restrict__ idx,
+                                                          const uint16_t* __restrict__ x,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ A,
+                                                          const float* __restrict__ B,
+                                                          const float* __restrict__ Cc,
+                                                          uint16_t* __restrict__ dx,
+                                                          float* __restrict__ partial, PoolGeom g,
+                                                          int64_t rows_per_block) {
+  __shared__ float sa[BNT * 8];
+  __shared__ float sb[BNT * 8];
+  const int G = g.C / 8;
+  const int R = BNT / G;
+  const int cg = threadIdx.x % G, r = threadIdx.x / G;
+  const bool active = r < R;
+  const int64_t P = (int64_t)g.N * g.Ho * g.Wo;          // output-grid points = 2x2 blocks
+  float sc[8], sh[8], mu[8], ca[8], cb[8], cc[8], a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = active ? cg * 8 + j : 0;
+    sc[j] = scale[c]; sh[j] = shift[c];
+    mu[j] = MODE == 0 ? mean[c] : 0.f;
+    ca[j] = MODE == 1 ? A[c] : 0.f; cb[j] = MODE == 1 ? B[c] : 0.f; cc[j] = MODE == 1 ? Cc[c] : 0.f;
+    a[j] = 0.f; b[j] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(r0 + rows_per_block, P);
+  if (active) {
+    for (int64_t pt = r0 + r; pt < r1; pt += R) {
+      const uint32_t p32 = (uint32_t)pt;                   // P < 2^31 (binding check)
+      const int xo = (int)(p32 % (uint32_t)g.Wo);
+      const uint32_t q = p32 / (uint32_t)g.Wo;
+      const int yo = (int)(q % (uint32_t)g.Ho), n = (int)(q / (uint32_t)g.Ho);
+      // windows (yo + u, xo + v), u, v in {0, 1}; missing ones (past the grid) contribute 0
+      float d[2][2][8];
+      uint2 s8[2][2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const bool in = yo + u < g.Ho && xo + v < g.Wo;
+          const int64_t o = (((int64_t)n * g.Ho + yo + u) * g.Wo + xo + v) * g.C + cg * 8;
+          if (in) {
+            V8<uint16_t>::load(dp + o, d[u][v]);
+            s8[u][v] = *reinterpret_cast<const uint2*>(idx + o);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[u][v][j] = 0.f;
+            s8[u][v] = make_uint2(0xffffffffu, 0xffffffffu);   // slot 255 matches nothing
+          }
+        }
+      float xv[2][2][8];
+#pragma unroll
+      for (int ay = 0; ay < 2; ++ay)
+#pragma unroll
+        for (int bx = 0; bx < 2; ++bx)
+          V8<uint16_t>::load(x + (((int64_t)n * g.H + 2 * yo + ay) * g.W + 2 * xo + bx) * g.C + cg * 8,
+                             xv[ay][bx]);
+#pragma unroll
+      for (int ay = 0; ay < 2; ++ay)
+#pragma unroll
+        for (int bx = 0; bx < 2; ++bx) {
+          float dz[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float acc = 0.f;
+#pragma unroll
+            for (int u = 0; u <= ay; ++u)            // window row yo+u reaches row 2yo+ay at kh
+#pragma unroll
+              for (int v = 0; v <= bx; ++v) {
+                const int kh = 1 + ay - 2 * u, kw = 1 + bx - 2 * v;
+                const uint32_t w = j < 4 ? s8[u][v].x : s8[u][v].y;
+                const int slot = (int)((w >> (8 * (j & 3))) & 0xffu);
+                acc += slot == kh * 3 + kw ? d[u][v][j] : 0.f;
+              }
+            dz[j] = fmaf(xv[ay][bx][j], sc[j], sh[j]) > 0.f ? acc : 0.f;
+          }
+          if (MODE == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { a[j] += dz[j]; b[j] += dz[j] * (xv[ay][bx][j] - mu[j]); }
+          } else {
+            float o[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = ca[j] * dz[j] + cb[j] * xv[ay][bx][j] + cc[j];
+            V8<uint16_t>::store(dx + (((int64_t)n * g.H + 2 * yo + ay) * g.W + 2 * xo + bx) * g.C + cg * 8, o);
+          }
+        }
+    }
+  }
+  if (MODE == 1) return;
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sa[r * g.C + cg * 8 + j] = a[j]; sb[r * g.C + cg * 8 + j] = b[j]; }
+  }
+  __syncthreads();
+  const int64_t nb = gridDim.x;
+  for (int c = threadIdx.x; c < g.C; c += BNT) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int qq = 0; qq < R; ++qq) { s1 += sa[qq * g.C + c]; s2 += sb[qq * g.C + c]; }
+    partial[(int64_t)c * nb + blockIdx.x] = s1;
+    partial[((int64_t)g.C + c) * nb + blockIdx.x] = s2;
+  }
+}
+
 void stem_pool_fwd(const StemArgs& a, hipStream_t st) {
   const PoolGeom g{a.N, a.H, a.W, a.C, a.Ho, a.Wo, a.k, a.s, a.p};
   const int64_t total = (int64_t)a.N * a.Ho * a.Wo * (a.C / 8);
@@ -756,6 +870,23 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
   reduce_geometry(M, a.C, rpb, nb);
   const auto* dp = static_cast<const uint16_t*>(a.dp);
   const auto* x = static_cast<const uint16_t*>(a.x);
+  if (a.k == 3 && a.s == 2 && a.p == 1 && a.H == 2 * a.Ho && a.W == 2 * a.Wo) {
+    // 2x2-block form over the output grid (same partial layout: nb blocks of the grid points)
+    const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
+    int64_t rpb2;
+    int nb2;
+    reduce_geometry(P, a.C, rpb2, nb2);
+    hipLaunchKernelGGL((k_stem_pool_bwd_s2<0>), dim3(nb2), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
+                       a.shift, a.mean, (const float*)nullptr, (const float*)nullptr,
+                       (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb2);
+    hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb2,
+                       a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
+                       (int)a.accum_dparams);
+    hipLaunchKernelGGL((k_stem_pool_bwd_s2<1>), dim3(nb2), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
+                       a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
+                       (float*)nullptr, g, rpb2);
+    return;
+  }
   hipLaunchKernelGGL((k_stem_pool_bwd<0>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                      a.shift, a.mean, (const float*)nullptr, (const float*)nullptr,
                      (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb);

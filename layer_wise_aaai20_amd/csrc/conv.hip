@@ -114,7 +114,7 @@ void conv_gemm(const GemmArgs& g, const ConvGeomHost& cvh, int mode, hipStream_t
   const int zs = (g.K + kps - 1) / kps;
   const int tiles = ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn);
   const int epi = zs > 1 ? EPI_PARTIAL : (g.stats ? EPI_STATS : EPI_STORE);
-  GemmK k{g.A, g.B, g.C, g.partial, g.stats, nullptr, g.pro_scale, g.pro_shift, nullptr, nullptr,
+  GemmK k{g.A, g.B, g.C, g.partial, g.stats, nullptr, g.pro_scale, g.pro_shift, g.addend, nullptr,
           g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, 0, g.out_bf16 ? 1 : 0, g.accumulate ? 1 : 0};
   k.cv = to_device(cvh);
   k.a_bytes = g.a_bytes;

@@ -716,16 +716,19 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
         orow = ((int64_t)b * p.cv.Hout + y * p.cv.osy + ccl.py) * p.cv.Wout + x * p.cv.osx + ccl.px;
       }
       uint16_t* dst = static_cast<uint16_t*>(p.C) + orow * p.ldc + gn;
+      // the addend is aligned with the OUTPUT rows (a parity class adds into its own pixels,
+      // e.g. a strided shortcut's data gradient accumulated into the block's dx in place)
+      const int64_t aoff = orow * p.ldc + gn;
       if (vec && gn + 8 <= p.N) {
         uint4 v = *reinterpret_cast<const uint4*>(src);
-        if (p.addend) v = add_bf16x8(v, masked_addend8(p.addend, p.add_bits, (int64_t)gm * p.ldc + gn));
+        if (p.addend) v = add_bf16x8(v, masked_addend8(p.addend, p.add_bits, aoff));
         *reinterpret_cast<uint4*>(dst) = v;
       } else {
         for (int k = 0; k < 8 && gn + k < p.N; ++k) {
           uint16_t h = src[k];
           if (p.addend)
             h = bf16_rne(__uint_as_float((uint32_t)h << 16) +
-                         masked_addend1(p.addend, p.add_bits, (int64_t)gm * p.ldc + gn + k));
+                         masked_addend1(p.addend, p.add_bits, aoff + k));
           dst[k] = h;
         }
       }

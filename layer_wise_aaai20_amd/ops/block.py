@@ -268,10 +268,16 @@ class _BottleneckFn(torch.autograd.Function):
                                         _bn_momentum(bn3), bn3.eps)
         if bnd is not None:
             s = down_stride
-            xs = x if s == 1 else x[:, :, ::s, ::s].contiguous(memory_format=CL)
-            xsr = _rows(xs)
             Wd = _bf16_weight(wd).reshape(cout, Cin)
-            cd, std = gemm(xsr, Cin, True, Wd, Cin, True, M2, cout, Cin, stats=True)
+            if s == 1:
+                xsr = xr
+                cd, std = gemm(xsr, Cin, True, Wd, Cin, True, M2, cout, Cin, stats=True)
+            else:
+                # strided 1x1 shortcut as an implicit-GEMM conv gathering every s-th pixel of x
+                # (the subsampled input is never materialised)
+                xsr = None
+                cdn, std = conv_fwd(x, Wd.view(cout, Cin, 1, 1), s, 0, stats=True)
+                cd = _rows(cdn)
             meand, invd, ssd = lib.bn_stats(cd, std, gd, bd, bnd.running_mean, bnd.running_var,
                                             _bn_momentum(bnd), bnd.eps)
             bits3 = torch.empty(M2 * cout // 8, dtype=torch.uint8, device=x.device)
@@ -352,16 +358,21 @@ class _BottleneckFn(torch.autograd.Function):
                                           False, bits3, od[0], od[1])
             grads["gd"], grads["bd"] = _finish_bn(gdp, bdp, dgd, dbd, od)
             dstd, dd = _wgrad_target(wd, (cout, Cin))
-            gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2, out_bf16=False, out=dstd,
-                 accumulate=True, split_k=True)
+            if s == 1:
+                gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2, out_bf16=False, out=dstd,
+                     accumulate=True, split_k=True)
+            else:                     # strided pixel gather of x in the weight-gradient conv
+                conv_wgrad(_nchw(dcd, N2, H2, W2_), x, (cout, Cin, 1, 1), s, 0,
+                           out=dstd.view(cout, Cin, 1, 1))
             grads["wd"] = _finish_wgrad(wd, dstd, dd)
             dx, _ = gemm(dc1, width, True, W1, Cin, False, M, Cin, width)
             if s == 1:
                 gemm(dcd, cout, True, Wd, Cin, False, M2, Cin, cout, out=dx, addend=dx)
             else:
-                dxs, _ = gemm(dcd, cout, True, Wd, Cin, False, M2, Cin, cout)
-                dxv = dx.view(N, H, W, Cin)
-                dxv[:, ::s, ::s, :] += dxs.view(N2, H2, W2_, Cin)
+                # the shortcut's data gradient lands on every s-th pixel of dx: a 1-class
+                # strided data-gradient conv adding into dx in place (no scatter pass)
+                conv_dgrad(_nchw(dcd, N2, H2, W2_), Wd.view(cout, Cin, 1, 1), (H, W), s, 0,
+                           out=dx, addend=dx)
         else:
             dx, _ = gemm(dc1, width, True, W1, Cin, False, M, Cin, width, addend=dr,
                          addend_bits=bits3)

@@ -179,8 +179,14 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
     return y.view(Nb, Ho, Wo, co).permute(0, 3, 1, 2), st
 
 
-def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=None):
-    """dx [N, C, H, W] (bf16 channels_last) of conv2d(x, w) given dy [N, Co, Ho, Wo]."""
+def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=None,
+               out: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None):
+    """dx [N, C, H, W] (bf16 channels_last) of conv2d(x, w) given dy [N, Co, Ho, Wo].
+
+    ``out`` (bf16 [N*H*W, C] rows) receives the result — only the pixels some tap reaches are
+    written — and ``addend`` (same layout, may be ``out`` itself) is added to them after rounding:
+    ``conv_dgrad(dy, w, hw, 2, 0, out=dx, addend=dx)`` accumulates a strided 1x1 shortcut's data
+    gradient into dx in place."""
     lib = load()
     sh, sw = _pair(stride)
     ph, pw = _pair(padding)
@@ -190,6 +196,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
     Nb, _, Ho, Wo = dyc.shape
     classes = _dgrad_classes(H, W, R, S, sh, sw, ph, pw)
     if not classes:
+        if out is not None:
+            return _nchw_rows(out, Nb, H, W)
         return torch.zeros((Nb, c, H, W), dtype=BF16, device=dy.device, memory_format=CL)
     wt, offs = wpack if wpack is not None else pack_dgrad_weight(w, classes, sh, sw)
     geom = [Nb, Ho, Wo, co, 1, 1, -1, -1, H, W, sh, sw, len(classes)]
@@ -197,13 +205,17 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
         geom += [TR, TS, oh, ow, Hg, Wg, ch, cw, TR * TS * co, off]
     M = max(Nb * cl[6] * cl[7] for cl in classes)
 
-    def run(tile):
-        return lib.conv_ex(dyc, wt, CV_A, geom, c, tile, 1, True, None, None, False, None,
-                           False, 0, False, c)
-    key = ("d", tuple(dyc.shape), tuple(w.shape), H, W, sh, sw, ph, pw)
-    tile = TUNER.pick(key, run, ROW_TILES, _row_default(M, c))
-    dx, _ = run(tile)
-    return dx.view(Nb, H, W, c).permute(0, 3, 1, 2)
+    def run(tile, dst=None, add=None):
+        return lib.conv_ex(dyc, wt, CV_A, geom, c, tile, 1, True, None, None, False, dst,
+                           False, 0, False, c, add)
+    key = ("d", tuple(dyc.shape), tuple(w.shape), H, W, sh, sw, ph, pw, addend is not None)
+    tile = TUNER.pick(key, run, ROW_TILES, _row_default(M, c))   # (timed on scratch outputs)
+    dx, _ = run(tile, out, addend)
+    return _nchw_rows(dx, Nb, H, W)
+
+
+def _nchw_rows(rows: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    return rows.view(n, h, w, rows.shape[-1]).permute(0, 3, 1, 2)
 
 
 def _wgrad_splits(tiles: int, pixels: int, bk: int) -> int:

@@ -137,7 +137,7 @@ def test_resnet50_block_vs_layer_path():
     assert errs["block"][-1] < 0.05            # fc.bias: only the softmax output enters
 
 
-@pytest.mark.parametrize("shape", [(4, 64, 32, 32), (2, 64, 15, 17)])
+@pytest.mark.parametrize("shape", [(4, 64, 32, 32), (2, 64, 15, 17), (2, 64, 112, 112), (3, 128, 28, 28)])
 def test_stem_bn_relu_pool_matches_layers(shape):
     """Fused BN+ReLU+max-pool stem vs FusedBatchNorm2d(relu) + nn.MaxPool2d."""
     from layer_wise_aaai20_amd.ops.nn import stem_bn_relu_pool, to_fused_bn

@@ -106,6 +106,8 @@ class GradSyncEngine:
         # stream waits on a second event only when it decodes in finish()
         self._side = (torch.cuda.Stream(device=self.device)
                       if overlap_compress and self.device.type == "cuda" else None)
+        self._stream_waitable = (comm.is_dist() and comm.world_size(self.pg) > 1 and
+                                 comm.dist.get_backend(self.pg) == "nccl")
         self._reset_state()
         self.all_reduced_last = True
         self.verify_plan()
@@ -194,11 +196,17 @@ class GradSyncEngine:
             else:
                 recv = codec.recv_buffer(send)
                 work = comm.all_gather(recv, send, self.pg)
+            tx = None
+            if side is not None and self._stream_waitable:
+                # RCCL: wait() only orders the side stream after the collective (no host block),
+                # so the exchange itself can be timed and `done` covers compress + exchange
+                work.wait()
+                tx = self._event() if self.timing else None
             done = None
             if side is not None:
                 done = torch.cuda.Event()
                 done.record(side)
-        self._pending.append((bi, work, send, recv, (t0, t1), done))
+        self._pending.append((bi, work, send, recv, (t0, t1, tx), done))
 
     def finish(self) -> None:
         """Launch buckets that never became ready (unused params keep zero grads), wait for every
@@ -207,7 +215,7 @@ class GradSyncEngine:
             self._ready[i] = True
         self._launch_in_order()
         rec = []
-        for bi, work, send, recv, (t0, t1), done in self._pending:
+        for bi, work, send, recv, (t0, t1, tx), done in self._pending:
             work.wait()
             if done is not None:                 # decode on the compute stream after the side
                 cur = torch.cuda.current_stream(self.device)
@@ -219,7 +227,7 @@ class GradSyncEngine:
             b = self.buckets[bi]
             self.codecs[bi].decompress(send, recv, self.arena.grad[b.start:b.end])
             if self.timing:
-                rec.append((bi, t0, t1, t2, self._event()))
+                rec.append((bi, t0, t1, tx, t2, self._event()))
         self._pending = []
         if self.timing:
             self._last_events = rec
@@ -239,13 +247,19 @@ class GradSyncEngine:
         self.finish()
 
     def read_timings(self) -> List[dict]:
-        """Per-bucket µs of the last step: compress, exchange-wait (compress end → collective
-        visible on the compute stream) and decode. Synchronises; call outside the hot loop."""
+        """Per-bucket µs of the last step (HIP events): ``compress_us`` (select + pack on the side
+        stream), ``exchange_us`` (compress end → collective complete; RCCL, whose wait() is
+        stream-ordered: includes queueing behind earlier buckets' collectives), ``idle_us``
+        (exchange done → the compute stream decodes it, i.e. the rest of the backward pass the
+        exchange was hidden behind) and ``decode_us``. Without a stream-waitable backend (gloo,
+        world 1) ``exchange_us`` is None and ``idle_us`` spans compress end → decode.
+        Synchronises; call outside the hot loop."""
         out = []
-        for bi, t0, t1, t2, t3 in getattr(self, "_last_events", []):
+        for bi, t0, t1, tx, t2, t3 in getattr(self, "_last_events", []):
             t3.synchronize()
             out.append({"bucket": bi, "compress_us": 1e3 * t0.elapsed_time(t1),
-                        "exchange_us": 1e3 * t1.elapsed_time(t2),
+                        "exchange_us": 1e3 * t1.elapsed_time(tx) if tx is not None else None,
+                        "idle_us": 1e3 * (tx if tx is not None else t1).elapsed_time(t2),
                         "decode_us": 1e3 * t2.elapsed_time(t3)})
         return out
 

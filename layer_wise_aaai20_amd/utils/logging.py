@@ -241,9 +241,9 @@ class TensorboardLogger:
         self.log("comm/ratio", stats.ratio)
         for b in bucket_us or []:
             i = b["bucket"]
-            self.log(f"comm/bucket{i}_compress_us", b["compress_us"])
-            self.log(f"comm/bucket{i}_exchange_us", b["exchange_us"])
-            self.log(f"comm/bucket{i}_decode_us", b["decode_us"])
+            for k in ("compress_us", "exchange_us", "idle_us", "decode_us"):
+                if b.get(k) is not None:
+                    self.log(f"comm/bucket{i}_{k}", b[k])
 
     def log_eval(self, top1, top5, time_):
         self.log("losses/test_1", top1)

@@ -463,7 +463,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
                                                   bool training, bool relu, bool need_dres,
                                                   c10::optional<Tensor> bits,
                                                   c10::optional<Tensor> dgamma_out,
-                                                  c10::optional<Tensor> dbeta_out) {
+                                                  c10::optional<Tensor> dbeta_out,
+                                                  c10::optional<Tensor> stats_rows) {
   const c10::DeviceGuard guard(x.device());
   check_nhwc(x, "x");
   check_nhwc(dy, "dy");
@@ -485,9 +486,23 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
   bool accum = false;
   Tensor dgamma = dparam_out(dgamma_out, C, x, accum), dbeta = dparam_out(dbeta_out, C, x, accum);
   Tensor coef = at::empty({3 * C}, f32);
-  Tensor partial = at::empty({(int64_t)lw::bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
+  const bool have_rows = stats_rows.has_value() && stats_rows->defined();
+  int64_t nb = lw::bn_reduce_blocks(M, (int)C);
+  if (have_rows) {
+    // (Σdy', Σdy'·(x−mean)) per M-tile from the producing GEMM's EPI_BSTATS epilogue
+    check_dtype(*stats_rows, at::kFloat, "stats_rows");
+    TORCH_CHECK(stats_rows->is_cuda() && stats_rows->dim() == 3 && stats_rows->size(1) == 2 &&
+                stats_rows->size(2) == C && stats_rows->is_contiguous(),
+                "stats_rows must be a contiguous [rows, 2, C] fp32 tensor");
+    nb = std::max<int64_t>(nb, lw::colsum_blocks(stats_rows->size(0)));
+  }
+  Tensor partial = at::empty({nb * 2 * C}, f32);
   lw::BNArgs a{};
   a.accum_dparams = accum;
+  if (have_rows) {
+    a.stat_rows = ptr<float>(*stats_rows);
+    a.stats_rows_n = stats_rows->size(0);
+  }
   TORCH_CHECK(!accum || ((dgamma_out.has_value() && dgamma_out->defined()) &&
                          (dbeta_out.has_value() && dbeta_out->defined())),
               "give both dgamma_out and dbeta_out");
@@ -522,6 +537,38 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
 }
 
 // ---------------------------------------------------------------- MFMA GEMM
+// EPI_BSTATS operands (see lw_kernels.h GemmArgs): the BN input x laid out like the output rows
+// ([out_rows][N], ldc == N), its batch mean, and the ReLU mask source — the BN output's bitmap or
+// the BN's scale/shift (mask = x*scale+shift > 0).
+static void set_bstats(lw::GemmArgs& g, const c10::optional<Tensor>& bx,
+                       const c10::optional<Tensor>& bmean, const c10::optional<Tensor>& bss,
+                       const c10::optional<Tensor>& bbits, int64_t out_rows, int64_t N,
+                       int64_t ldc, bool out_bf16) {
+  if (!(bx.has_value() && bx->defined())) return;
+  TORCH_CHECK(out_bf16 && ldc == N && N % 8 == 0,
+              "backward statistics need a bf16 output with ldc == N and N % 8 == 0");
+  check_dtype(*bx, at::kBFloat16, "bst_x");
+  TORCH_CHECK(bx->is_cuda() && (bx->is_contiguous() ||
+              bx->is_contiguous(at::MemoryFormat::ChannelsLast)) && bx->numel() >= out_rows * N,
+              "bst_x must be a dense [rows, N] bf16 tensor");
+  check_aligned16(bx->data_ptr(), "bst_x");
+  TORCH_CHECK(bmean.has_value() && bmean->defined() && bmean->numel() >= N, "bst_mean [N]");
+  check_dtype(*bmean, at::kFloat, "bst_mean");
+  g.bst_x = ptr<uint16_t>(*bx);
+  g.bst_mean = ptr<float>(*bmean);
+  if (bbits.has_value() && bbits->defined()) {
+    TORCH_CHECK(bbits->scalar_type() == at::kByte && bbits->numel() * 8 >= out_rows * N,
+                "bst_bits: uint8 bitmap of the [rows, N] BN output");
+    g.bst_bits = ptr<uint8_t>(*bbits);
+  } else {
+    TORCH_CHECK(bss.has_value() && bss->defined() && bss->numel() == 2 * N && bss->is_contiguous(),
+                "bst_scale_shift: the BN's [2N] scale/shift (mask = x*scale+shift > 0)");
+    check_dtype(*bss, at::kFloat, "bst_scale_shift");
+    g.bst_scale = ptr<float>(*bss);
+    g.bst_shift = g.bst_scale + N;
+  }
+}
+
 std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb,
                                    bool b_kcontig, int64_t M, int64_t N, int64_t K,
                                    c10::optional<Tensor> bias, bool relu, int64_t splits,
@@ -529,7 +576,10 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
                                    c10::optional<Tensor> pro_shift, bool pro_on_a,
                                    bool want_stats, c10::optional<Tensor> out,
                                    c10::optional<Tensor> addend, bool accumulate, int64_t ldc,
-                                   c10::optional<Tensor> addend_bits) {
+                                   c10::optional<Tensor> addend_bits,
+                                   c10::optional<Tensor> bst_x, c10::optional<Tensor> bst_mean,
+                                   c10::optional<Tensor> bst_scale_shift,
+                                   c10::optional<Tensor> bst_bits) {
   const c10::DeviceGuard guard(A.device());
   TORCH_CHECK(A.is_cuda() && B.is_cuda(), "gemm needs GPU tensors");
   check_dtype(A, at::kBFloat16, "A");
@@ -628,6 +678,12 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
     partial = at::empty({(int64_t)zs * M * N}, A.options().dtype(at::kFloat));
     g.partial = ptr<float>(partial);
   }
+  set_bstats(g, bst_x, bst_mean, bst_scale_shift, bst_bits, M, N, ldc, out_bf16);
+  if (g.bst_x) {
+    TORCH_CHECK(want_stats && a_kcontig && !b_kcontig && !pro && tile < 11,
+                "backward statistics: a tiled data-gradient GEMM (K-contiguous A, N-contiguous "
+                "B, no prologue) with want_stats");
+  }
   if (want_stats) {
     TORCH_CHECK(zs == 1, "column statistics need splits == 1");
     stats = at::empty({(int64_t)lw::gemm_tiles_m(g), 2, N}, A.options().dtype(at::kFloat));
@@ -645,7 +701,8 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
             int64_t splits, bool out_bf16) {
   return std::get<0>(gemm_ex(A, lda, a_kcontig, B, ldb, b_kcontig, M, N, K, bias, relu, splits,
                              out_bf16, 0, c10::nullopt, c10::nullopt, true, false, c10::nullopt,
-                             c10::nullopt, false, 0, c10::nullopt));
+                             c10::nullopt, false, 0, c10::nullopt, c10::nullopt, c10::nullopt,
+                             c10::nullopt, c10::nullopt));
 }
 
 // ---------------------------------------------------------------- implicit-GEMM convolution
@@ -659,7 +716,10 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
                                    c10::optional<Tensor> pro_scale, c10::optional<Tensor> pro_shift,
                                    bool want_stats, c10::optional<Tensor> out, bool accumulate,
                                    int64_t ldc, bool b_kcontig, int64_t ldb,
-                                   c10::optional<Tensor> addend) {
+                                   c10::optional<Tensor> addend, c10::optional<Tensor> bst_x,
+                                   c10::optional<Tensor> bst_mean,
+                                   c10::optional<Tensor> bst_scale_shift,
+                                   c10::optional<Tensor> bst_bits) {
   const c10::DeviceGuard guard(G.device());
   TORCH_CHECK(G.is_cuda() && Op.is_cuda(), "conv needs GPU tensors");
   check_dtype(G, at::kBFloat16, "gathered tensor");
@@ -816,13 +876,26 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
     partial = at::empty({(int64_t)zs * g.M * N}, G.options().dtype(at::kFloat));
     g.partial = ptr<float>(partial);
   }
-  if (want_stats) {
+  set_bstats(g, bst_x, bst_mean, bst_scale_shift, bst_bits, out_rows, N, ldc, out_bf16);
+  if (want_stats && g.bst_x) {
+    // data-gradient conv that also does the reduce pass of the BN its output feeds: one stats
+    // row per (parity class, M-tile); rows of tiles a smaller class skips stay zero
+    TORCH_CHECK(ga && !b_kcontig && !c4 && g.pro_scale == nullptr && zs == 1,
+                "backward statistics: data-gradient convs only");
+    int bm, bn, bk;
+    lw::gemm_tile_shape(g.tile, bm, bn, bk);
+    stats = at::zeros({(int64_t)h.nclass * ((g.M + bm - 1) / bm), 2, N},
+                      G.options().dtype(at::kFloat));
+    g.stats = ptr<float>(stats);
+  } else if (want_stats) {
+    TORCH_CHECK(!g.bst_x, "backward statistics need want_stats");
     TORCH_CHECK(ga && b_kcontig && h.nclass == 1, "column statistics: forward convs only");
     int bm, bn, bk;
     lw::gemm_tile_shape(g.tile, bm, bn, bk);
     stats = at::empty({(g.M + bm - 1) / bm, 2, N}, G.options().dtype(at::kFloat));
     g.stats = ptr<float>(stats);
   } else {
+    TORCH_CHECK(!g.bst_x, "backward statistics need want_stats");
     stats = at::empty({0}, G.options().dtype(at::kFloat));
   }
   lw::conv_gemm(g, h, (int)mode, cur_stream());
@@ -1057,7 +1130,7 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "bn_bwd(Tensor dy, Tensor x, Tensor? y, Tensor? weight, Tensor mean, Tensor invstd, "
       "Tensor? scale_shift, bool training, bool relu, bool need_dres, Tensor? bits=None, "
-      "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None) "
+      "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? stats_rows=None) "
       "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
       "gemm(Tensor A, int lda, bool a_kcontig, Tensor B, int ldb, bool b_kcontig, int M, int N, "
@@ -1067,12 +1140,15 @@ TORCH_LIBRARY(lwaaai, m) {
       "int N, int K, Tensor? bias, bool relu, int splits, bool out_bf16, int tile, "
       "Tensor? pro_scale, Tensor? pro_shift, bool pro_on_a, bool want_stats, "
       "Tensor(a!)? out=None, Tensor? addend=None, bool accumulate=False, int ldc=0, "
-      "Tensor? addend_bits=None) "
+      "Tensor? addend_bits=None, Tensor? bst_x=None, Tensor? bst_mean=None, "
+      "Tensor? bst_scale_shift=None, Tensor? bst_bits=None) "
       "-> (Tensor, Tensor)");
   m.def(
       "conv_ex(Tensor G, Tensor Op, int mode, int[] geom, int N, int tile, int splits, "
       "bool out_bf16, Tensor? pro_scale, Tensor? pro_shift, bool want_stats, Tensor(a!)? out, "
-      "bool accumulate, int ldc, bool b_kcontig, int ldb, Tensor? addend=None) -> (Tensor, Tensor)");
+      "bool accumulate, int ldc, bool b_kcontig, int ldb, Tensor? addend=None, "
+      "Tensor? bst_x=None, Tensor? bst_mean=None, Tensor? bst_scale_shift=None, "
+      "Tensor? bst_bits=None) -> (Tensor, Tensor)");
   m.def(
       "bn_stats(Tensor x, Tensor? stats, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
       "Tensor(b!)? running_var, float momentum, float eps) -> (Tensor, Tensor, Tensor)");

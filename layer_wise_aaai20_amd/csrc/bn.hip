@@ -545,13 +545,24 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   reduce_geometry(a.M, a.C, rpb, nb);
   // relu mask: recompute from x when the forward had no residual (saves reading y)
   const int rmode = !a.relu ? 0 : (a.bits ? 3 : (a.scale ? 2 : 1));
+  if (a.stat_rows) {
+    // the GEMM that produced dy already reduced (Σdy', Σdy'·(x−mean)) per M-tile
+    // (gemm_core.h EPI_BSTATS): only fold its rows
+    const int64_t R = a.stats_rows_n;
+    nb = colsum_blocks(R);
+    const int64_t rows_pb = (R + nb - 1) / nb;
+    nb = (int)((R + rows_pb - 1) / rows_pb);
+    hipLaunchKernelGGL(k_colsum, dim3(nb), dim3(256), 0, st, a.stat_rows, R, 2 * a.C, rows_pb,
+                       a.partial);
+  } else {
 #define LW_RED(R)                                                                                \
   hipLaunchKernelGGL((reduce_unroll() == 8 ? k_bn_reduce<T, 1, R, 8> : k_bn_reduce<T, 1, R, 4>), \
                      dim3(nb, reduce_slices(a.C)), dim3(BNT), 0, st, x, dy, y, a.bits, a.mean, \
                      a.scale, a.shift, a.M, a.C, rpb, a.partial)
-  if (rmode == 0) LW_RED(0); else if (rmode == 1) LW_RED(1); else if (rmode == 2) LW_RED(2);
-  else LW_RED(3);
+    if (rmode == 0) LW_RED(0); else if (rmode == 1) LW_RED(1); else if (rmode == 2) LW_RED(2);
+    else LW_RED(3);
 #undef LW_RED
+  }
   hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
                      a.C, a.M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
                      (int)a.training, (int)a.accum_dparams);

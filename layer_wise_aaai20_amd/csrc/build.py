@@ -20,8 +20,12 @@ import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
-OUT = os.path.join(PKG, "_lwaaai_C.so")
-BUILD = os.path.join(HERE, "build")
+# experiment builds: LWAAAI_SO names another output (loaded by ops/_ext.py from the same
+# variable), LWAAAI_HIPCC_FLAGS adds compile flags (e.g. -DLW_GLDS=0), objects go to their own dir
+OUT = os.environ.get("LWAAAI_SO") or os.path.join(PKG, "_lwaaai_C.so")
+EXTRA = os.environ.get("LWAAAI_HIPCC_FLAGS", "").split()
+BUILD = os.path.join(HERE, "build" + ("" if not os.environ.get("LWAAAI_SO") else
+                                      "_" + os.path.basename(OUT).replace(".so", "")))
 ARCH = os.environ.get("LWAAAI_ARCH", "gfx950")
 
 
@@ -54,6 +58,7 @@ def _digest(paths) -> str:
             h.update(p.encode())
             h.update(f.read())
     h.update(ARCH.encode())
+    h.update(" ".join(EXTRA).encode())
     return h.hexdigest()[:16]
 
 
@@ -61,7 +66,7 @@ def _compile(src, inc, abi):
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM", "-D__HIP_PLATFORM_AMD__=1",
-           "-Wno-unused-result", "-Wno-deprecated-declarations", f"-I{HERE}"]
+           "-Wno-unused-result", "-Wno-deprecated-declarations", f"-I{HERE}"] + EXTRA
     if src.endswith(".cpp"):
         cmd += [f"-I{p}" for p in inc] + [f"-I{sysconfig.get_paths()['include']}"]
     r = subprocess.run(cmd, capture_output=True, text=True)

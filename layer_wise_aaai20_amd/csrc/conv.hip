@@ -49,7 +49,8 @@ static void conv_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, hip
   const bool pro = g.pro_scale != nullptr;
   if constexpr (CVM == CV_A) {
     if (!g.b_kcontig) {                                   // data gradient: Wt is [K][C]
-      LW_LAUNCH(true, false, EPI_STORE, PRO_NONE, CV_A);
+      if (epi == EPI_BSTATS) LW_LAUNCH(true, false, EPI_BSTATS, PRO_NONE, CV_A);
+      else LW_LAUNCH(true, false, EPI_STORE, PRO_NONE, CV_A);
     } else if (epi == EPI_STATS) {
       if (pro) LW_LAUNCH(true, true, EPI_STATS, PRO_A, CV_A);
       else LW_LAUNCH(true, true, EPI_STATS, PRO_NONE, CV_A);
@@ -113,12 +114,18 @@ void conv_gemm(const GemmArgs& g, const ConvGeomHost& cvh, int mode, hipStream_t
   const int kps = gemm_k_per_split(g.K, g.splits, bk);
   const int zs = (g.K + kps - 1) / kps;
   const int tiles = ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn);
-  const int epi = zs > 1 ? EPI_PARTIAL : (g.stats ? EPI_STATS : EPI_STORE);
+  const int epi = zs > 1 ? EPI_PARTIAL
+                          : (g.stats ? (g.bst_x ? EPI_BSTATS : EPI_STATS) : EPI_STORE);
   GemmK k{g.A, g.B, g.C, g.partial, g.stats, nullptr, g.pro_scale, g.pro_shift, g.addend, nullptr,
           g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, 0, g.out_bf16 ? 1 : 0, g.accumulate ? 1 : 0};
   k.cv = to_device(cvh);
   k.a_bytes = g.a_bytes;
   k.b_bytes = g.b_bytes;
+  k.bst_x = g.bst_x;
+  k.bst_mean = g.bst_mean;
+  k.bst_scale = g.bst_scale;
+  k.bst_shift = g.bst_shift;
+  k.bst_bits = g.bst_bits;
   const dim3 grid(tiles, zs, cvh.nclass);
   switch (mode) {
     case CV_A: conv_dispatch<CV_A>(g, k, epi, grid, st); break;

@@ -390,6 +390,12 @@ static void launch_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, h
   else launch_layout<BM, BN, BK, E, PRO_NONE>(g, k, grid, st);
   if (epi == EPI_PARTIAL) { LW_E(EPI_PARTIAL) }
   else if (epi == EPI_STATS) { LW_E(EPI_STATS) }
+  else if (epi == EPI_BSTATS) {
+    // a data-gradient GEMM (dy·W: K-contiguous dy, N-contiguous W) that also does the reduce
+    // pass of the BatchNorm its output feeds (the host checks the layout and no prologue)
+    hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI_BSTATS, PRO_NONE>), grid, dim3(GT), 0,
+                       st, k);
+  }
   else { LW_E(EPI_STORE) }
 #undef LW_E
 }
@@ -422,12 +428,18 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
   const int kps = k_per_split(g.K, g.splits, ts.bk);
   const int zs = (g.K + kps - 1) / kps;
   const int tiles = ((g.M + ts.bm - 1) / ts.bm) * ((g.N + ts.bn - 1) / ts.bn);
-  const int epi = zs > 1 ? EPI_PARTIAL : (g.stats ? EPI_STATS : EPI_STORE);
+  const int epi = zs > 1 ? EPI_PARTIAL
+                          : (g.stats ? (g.bst_x ? EPI_BSTATS : EPI_STATS) : EPI_STORE);
   GemmK k{g.A, g.B, g.C, g.partial, g.stats, zs > 1 ? nullptr : g.bias, g.pro_scale, g.pro_shift,
           g.addend, g.add_bits, g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, zs > 1 ? 0 : g.relu,
           g.out_bf16 ? 1 : 0, g.accumulate ? 1 : 0};
   k.a_bytes = g.a_bytes;
   k.b_bytes = g.b_bytes;
+  k.bst_x = g.bst_x;
+  k.bst_mean = g.bst_mean;
+  k.bst_scale = g.bst_scale;
+  k.bst_shift = g.bst_shift;
+  k.bst_bits = g.bst_bits;
   const dim3 grid(tiles, zs);
   switch (t) {
     case GEMM_T128x128x64: launch_tile<128, 128, 64>(g, k, epi, grid, st); break;

@@ -13,7 +13,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int GT = 256;
 constexpr int PAD = 8;                   // bf16 elements of padding per LDS row
-enum { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_STATS = 2 };
+enum { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_STATS = 2, EPI_BSTATS = 3 };
 enum { PRO_NONE = 0, PRO_A = 1, PRO_B = 2 };
 
 // f32 -> bf16, round to nearest even: a plain cast, which hipcc lowers to the gfx950 hardware
@@ -105,6 +105,34 @@ __device__ __forceinline__ uint2 bload8(__amdgpu_buffer_rsrc_t r, uint32_t voff)
   return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0));
 }
 
+// LDS-DMA staging (buffer_load_dwordx4 ... lds): 16 bytes per lane straight from memory into LDS
+// at the wave-uniform base `wave_dst` + 16 * lane, no VGPRs and no ds_write. A range-checked
+// (OOB) source writes zeros (scripts/probes/glds_oob_probe.hip, run on MI355X), so the
+// convolution padding / matrix edges work exactly as with the register loads.
+#ifndef LW_GLDS
+#define LW_GLDS 1
+#endif
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint16_t* wave_dst, uint32_t voff) {
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr)wave_dst, 16, voff, 0, 0, 0);
+}
+
+// A K-contiguous BK = 64 tile filled by LDS-DMA: every wave-instruction writes 1 KiB = 8 whole
+// 128-byte rows in lane order, so the XOR swizzle moves to the SOURCE: the lane that lands in
+// stored chunk slot cc of row rr fetches logical chunk cc ^ (rr & 7). A thread's rows all share
+// rr & 7 (they differ by multiples of GT / 8 rows), so one per-thread chunk column serves all.
+template <int R, int BK, bool KC, bool DMA>
+__device__ __forceinline__ int src_chunk(int cc, int rr) {
+  return (DMA && Tile<R, BK, KC>::SWZ) ? (cc ^ (rr & 7)) : cc;
+}
+
+// LDS element offset of the first row of wave-instruction h of this thread's wave
+template <int R, int BK, bool KC>
+__device__ __forceinline__ int dma_wave_off(int h) {
+  using T = Tile<R, BK, KC>;
+  return (((int)(threadIdx.x & ~63u) + h * GT) / T::CPR) * T::LD;
+}
+
 // Plain operand tile: byte offset of each of this thread's chunks at k = 0 (OOB outside the
 // matrix); a K-step adds k*2 (KC) or k*ld*2 (M/N-contiguous) and masks the K tail.
 template <int R, int BK, bool KC>
@@ -115,6 +143,7 @@ struct PlainLoader {
   int kpos[PT];       // k of each chunk within the step (KC: the chunk column, else its row)
   uint32_t ld2;
 
+  template <bool DMA = false>
   __device__ __forceinline__ void init(const uint16_t* P, uint32_t bytes, int64_t ld, int row0,
                                        int rows) {
     rs = make_rsrc(P, bytes);
@@ -123,6 +152,7 @@ struct PlainLoader {
     for (int h = 0; h < PT; ++h) {
       int rr, cc;
       chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
+      cc = src_chunk<R, BK, KC, DMA>(cc, rr);
       if (KC) {
         const int gr = row0 + rr;
         voff[h] = gr < rows ? (uint32_t)(((int64_t)gr * ld + cc * 8) * 2) : OOB;
@@ -143,6 +173,16 @@ struct PlainLoader {
       const bool ok = voff[h] != OOB && k + kpos[h] < kend;
       r[h] = bload16(rs, ok ? voff[h] + kb : OOB);
       okmask |= (ok ? 1u : 0u) << h;
+    }
+  }
+
+  // the same chunks by LDS-DMA into tile S (init<true>)
+  __device__ __forceinline__ void dma(uint16_t* S, int k, int kend) const {
+    const uint32_t kb = KC ? (uint32_t)k * 2u : (uint32_t)k * ld2;
+#pragma unroll
+    for (int h = 0; h < PT; ++h) {
+      const bool ok = voff[h] != OOB && k + kpos[h] < kend;
+      glds16(rs, S + dma_wave_off<R, BK, KC>(h), ok ? voff[h] + kb : OOB);
     }
   }
 };
@@ -277,6 +317,12 @@ struct GemmK {
   int M, N, K, k_per_split, relu, out_bf16, accumulate;   // accumulate: fp32 C += result
   ConvGeom cv;                 // CV_* kernels only
   uint32_t a_bytes, b_bytes;   // operand extents for the buffer loads' range check
+  // EPI_BSTATS (lw_kernels.h GemmArgs): x of the BN whose backward reduction the epilogue does
+  const uint16_t* bst_x;
+  const float* bst_mean;
+  const float* bst_scale;
+  const float* bst_shift;
+  const uint8_t* bst_bits;
 };
 
 // q = a / d, r = a % d for 0 <= a < 2^24 via the fp32 reciprocal (one correction step each way:
@@ -305,14 +351,14 @@ struct RowGather {
   int ci0, js, jr;      // fast path: tap and first channel of the next K-step (uniform)
 };
 
-template <int R, int BK>
+template <int R, int BK, bool DMA = false>
 __device__ __forceinline__ void row_gather_init(RowGather<R, BK>& g, const uint16_t* X,
                                                 uint32_t bytes, const ConvGeom& cv,
                                                 const ConvClass& cc, int m0) {
   using T = Tile<R, BK, true>;
   g.rs = make_rsrc(X, bytes);
   const int hw = cc.Hg * cc.Wg;
-  g.kc = (threadIdx.x % T::CPR) * 8;
+  g.kc = src_chunk<R, BK, true, DMA>((int)(threadIdx.x % T::CPR), (int)(threadIdx.x / T::CPR)) * 8;
 #pragma unroll
   for (int h = 0; h < T::PER_T; ++h) {
     int rr, c8;
@@ -339,12 +385,14 @@ __device__ __forceinline__ void row_gather_seek(RowGather<R, BK>& g, const ConvG
   g.js = t - g.jr * cc.TS;
 }
 
-template <int R, int BK, bool C4>
+template <int R, int BK, bool C4, bool DMA = false>
 __device__ __forceinline__ void load_tile_gather_a(const ConvGeom& cv, const ConvClass& cc,
                                                    RowGather<R, BK>& g, int k, int kend,
                                                    uint4 (&r)[Tile<R, BK, true>::PER_T],
-                                                   int& ci_out, uint32_t& okmask) {
+                                                   int& ci_out, uint32_t& okmask,
+                                                   uint16_t* S = nullptr) {
   using T = Tile<R, BK, true>;
+  static_assert(!(DMA && C4), "4-channel gathers stage through registers");
   okmask = 0;
   const bool kin = k + g.kc < kend;
   if (!C4 && cv.C % BK == 0) {
@@ -362,7 +410,9 @@ __device__ __forceinline__ void load_tile_gather_a(const ConvGeom& cv, const Con
     for (int h = 0; h < T::PER_T; ++h) {
       const bool ok = kin && (unsigned)(g.hb[h] + ho) < (unsigned)cv.Hin &&
                       (unsigned)(g.wb[h] + wo) < (unsigned)cv.Win;
-      r[h] = bload16(g.rs, ok ? (uint32_t)(g.rowoff[h] + delta) : OOB);
+      const uint32_t off = ok ? (uint32_t)(g.rowoff[h] + delta) : OOB;
+      if constexpr (DMA) glds16(g.rs, S + dma_wave_off<R, BK, true>(h), off);
+      else r[h] = bload16(g.rs, off);
       okmask |= (ok ? 1u : 0u) << h;
     }
     return;
@@ -392,7 +442,8 @@ __device__ __forceinline__ void load_tile_gather_a(const ConvGeom& cv, const Con
       okmask |= (ok0 || ok1 ? 1u : 0u) << h;
     } else {
       const bool ok = row_ok && (unsigned)wi < (unsigned)cv.Win;
-      r[h] = bload16(g.rs, ok ? off : OOB);
+      if constexpr (DMA) glds16(g.rs, S + dma_wave_off<R, BK, true>(h), ok ? off : OOB);
+      else r[h] = bload16(g.rs, ok ? off : OOB);
       okmask |= (ok ? 1u : 0u) << h;
     }
   }
@@ -535,6 +586,9 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   const int Mrow = GA ? ccl.M : p.M;             // valid GEMM rows of this workgroup
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wr = w >> 1, wc = w & 1;
+  // both operands K-contiguous BK = 64 swizzled tiles, no prologue: stage by LDS-DMA
+  constexpr bool GL = LW_GLDS && AKC && BKC && BK == 64 && PRO == PRO_NONE &&
+                      (CV == CV_NONE || CV == CV_A);
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -558,13 +612,13 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   PlainLoader<BM, BK, AKC> la;
   PlainLoader<BN, BK, BKC> lb;
   if constexpr (GA) {
-    row_gather_init<BM, BK>(rg, p.A, p.a_bytes, p.cv, ccl, m0);
+    row_gather_init<BM, BK, GL>(rg, p.A, p.a_bytes, p.cv, ccl, m0);
     if (!G4 && p.cv.C % BK == 0) row_gather_seek<BM, BK>(rg, p.cv, ccl, kbeg);
   } else {
-    la.init(p.A, p.a_bytes, p.lda, m0, p.M);
+    la.template init<GL>(p.A, p.a_bytes, p.lda, m0, p.M);
   }
   if constexpr (GB) col_gather_init<BN, BK, G4>(cg, p.B, p.b_bytes, p.cv, ccl, n0, p.N);
-  else lb.init(Bp, p.b_bytes - (uint32_t)((Bp - p.B) * 2), p.ldb, n0, p.N);
+  else lb.template init<GL>(Bp, p.b_bytes - (uint32_t)((Bp - p.B) * 2), p.ldb, n0, p.N);
   static_assert(!GB || PRO != PRO_B, "B-gather prologue: materialise the input instead");
   if (PRO == PRO_B)        // channel n of this thread's B chunks: fixed for the whole kernel
     load_coef8(coB, p.pro_scale, p.pro_shift, n0 + (threadIdx.x % TB::CPR) * 8, p.N);
@@ -600,25 +654,52 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
     }
   };
   const int nsteps = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
-  if (nsteps > 0) {
-    fetch(kbeg, R0);
-    stage(st, R0);
-  }
-  __syncthreads();
-  int cur = 0;
-  for (int i = 0; i < nsteps; ++i) {
-    const bool more = i + 1 < nsteps;
-    if (more) fetch(kbeg + (i + 1) * BK, R0);
-    compute(st + cur * STAGE);
-    if (more) stage(st + (cur ^ 1) * STAGE, R0);
+  if constexpr (GL) {
+    // K-step i+1 is DMA'd into the other buffer while step i computes; the barrier at the end of
+    // each step (its vmcnt(0) drains this wave's DMA) publishes it and retires the reads of the
+    // buffer the next DMA overwrites.
+    auto issue = [&](int k, uint16_t* dst) {
+      if constexpr (GA) {
+        uint4 unused[TA::PER_T];
+        uint32_t okm;
+        int ch;
+        load_tile_gather_a<BM, BK, false, true>(p.cv, ccl, rg, k, kend, unused, ch, okm, dst);
+      } else {
+        la.dma(dst, k, kend);
+      }
+      lb.dma(dst + TA::ELEMS, k, kend);
+    };
+    if (nsteps > 0) issue(kbeg, st);
     __syncthreads();
-    cur ^= 1;
+    int cur = 0;
+    for (int i = 0; i < nsteps; ++i) {
+      if (i + 1 < nsteps) issue(kbeg + (i + 1) * BK, st + (cur ^ 1) * STAGE);
+      compute(st + cur * STAGE);
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    if (nsteps > 0) {
+      fetch(kbeg, R0);
+      stage(st, R0);
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int i = 0; i < nsteps; ++i) {
+      const bool more = i + 1 < nsteps;
+      if (more) fetch(kbeg + (i + 1) * BK, R0);
+      compute(st + cur * STAGE);
+      if (more) stage(st + (cur ^ 1) * STAGE, R0);
+      __syncthreads();
+      cur ^= 1;
+    }
   }
 
   // ---- epilogue. B is the MFMA's first operand, so each accumulator holds Cᵀ: lane l has
   // C[m = .. + (l&15)][n = .. + 4*(l>>4) + r], r = 0..3 (four consecutive columns of one row).
   const int lm = l & 15, ln = 4 * (l >> 4);
   const bool bf_out = EPI != EPI_PARTIAL && p.out_bf16;
+  static_assert(EPI != EPI_BSTATS || GA || CV == CV_NONE, "backward statistics: row outputs only");
   uint16_t* Ch = reinterpret_cast<uint16_t*>(lds);                  // bf16 tile [BM][LDH]
   float* red = reinterpret_cast<float*>(lds + BM * LDH * 2);        // stats [2 wave rows][2][BN]
   if (EPI != EPI_PARTIAL) {
@@ -688,13 +769,40 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   float cs1[8], cs2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { cs1[k] = 0.f; cs2[k] = 0.f; }
+  // EPI_BSTATS: this thread's 8 columns' mean (and mask affine) — fixed for the whole tile
+  float bmu[8], bsc[8], bsh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { bmu[k] = 0.f; bsc[k] = 0.f; bsh[k] = 0.f; }
+  if constexpr (EPI == EPI_BSTATS) {
+    const int gn0 = n0 + (threadIdx.x % (BN / 8)) * 8;
+    if (gn0 + 8 <= p.N) {           // (the host guarantees N % 8 == 0)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        bmu[k] = p.bst_mean[gn0 + k];
+        bsc[k] = p.bst_bits ? 0.f : p.bst_scale[gn0 + k];
+        bsh[k] = p.bst_bits ? 0.f : p.bst_shift[gn0 + k];
+      }
+    }
+  }
   if (bf_out) {
-    __syncthreads();
+    constexpr int NCH = BM * (BN / 8) / GT;          // store chunks per thread
+    static_assert(BM * (BN / 8) % GT == 0, "store chunks must split evenly");
     const bool vec = (p.ldc & 7) == 0;
-    for (int c = threadIdx.x; c < BM * (BN / 8); c += GT) {
+    // output row of a tile row (a parity class scatters its rows to its pixels)
+    auto orow_of = [&](int gm) -> int64_t {
+      if (GA && (p.cv.osy > 1 || p.cv.osx > 1)) {
+        const int hw = ccl.Hg * ccl.Wg, b = gm / hw, rem = gm - b * hw;
+        const int y = rem / ccl.Wg, x = rem - y * ccl.Wg;
+        return ((int64_t)b * p.cv.Hout + y * p.cv.osy + ccl.py) * p.cv.Wout + x * p.cv.osx + ccl.px;
+      }
+      return gm;
+    };
+    // One chunk of the store pass: stats of the staged tile, addend, store, EPI_BSTATS sums.
+    // `pa` / `px` / `pxb` are the chunk's prefetched addend, BN input and ReLU-bitmap byte.
+    auto store_chunk = [&](int c, const uint4& pa, const uint4& px, uint32_t pxb, bool pref) {
       const int r = c / (BN / 8), cc = (c % (BN / 8)) * 8;
       const int gm = m0 + r, gn = n0 + cc;
-      if (gm >= Mrow || gn >= p.N) continue;
+      if (gm >= Mrow || gn >= p.N) return;
       const uint16_t* src = Ch + r * LDH + cc;
       if (EPI == EPI_STATS) {
         const uint4 q = *reinterpret_cast<const uint4*>(src);
@@ -709,20 +817,29 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
           cs2[2 * k + 1] += in_hi ? hi * hi : 0.f;
         }
       }
-      int64_t orow = gm;
-      if (GA && (p.cv.osy > 1 || p.cv.osx > 1)) {   // parity class -> its pixels of the output
-        const int hw = ccl.Hg * ccl.Wg, b = gm / hw, rem = gm - b * hw;
-        const int y = rem / ccl.Wg, x = rem - y * ccl.Wg;
-        orow = ((int64_t)b * p.cv.Hout + y * p.cv.osy + ccl.py) * p.cv.Wout + x * p.cv.osx + ccl.px;
-      }
+      const int64_t orow = orow_of(gm);
       uint16_t* dst = static_cast<uint16_t*>(p.C) + orow * p.ldc + gn;
       // the addend is aligned with the OUTPUT rows (a parity class adds into its own pixels,
       // e.g. a strided shortcut's data gradient accumulated into the block's dx in place)
       const int64_t aoff = orow * p.ldc + gn;
       if (vec && gn + 8 <= p.N) {
         uint4 v = *reinterpret_cast<const uint4*>(src);
-        if (p.addend) v = add_bf16x8(v, masked_addend8(p.addend, p.add_bits, aoff));
+        if (p.addend) v = add_bf16x8(v, pref ? pa : masked_addend8(p.addend, p.add_bits, aoff));
         *reinterpret_cast<uint4*>(dst) = v;
+        if constexpr (EPI == EPI_BSTATS) {
+          // the stored gradient (bf16, as the BN backward would read it), masked by the ReLU of
+          // that BN's output, against its input x at the same element
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w}, xw[4] = {px.x, px.y, px.z, px.w};
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float d = k & 1 ? __uint_as_float(w[k >> 1] & 0xffff0000u) : __uint_as_float(w[k >> 1] << 16);
+            const float xv = k & 1 ? __uint_as_float(xw[k >> 1] & 0xffff0000u) : __uint_as_float(xw[k >> 1] << 16);
+            const bool m = p.bst_bits ? ((pxb >> k) & 1u) != 0u : fmaf(xv, bsc[k], bsh[k]) > 0.f;
+            const float dm = m ? d : 0.f;
+            cs1[k] += dm;
+            cs2[k] += dm * (xv - bmu[k]);
+          }
+        }
       } else {
         for (int k = 0; k < 8 && gn + k < p.N; ++k) {
           uint16_t h = src[k];
@@ -732,6 +849,39 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
           dst[k] = h;
         }
       }
+    };
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (EPI == EPI_BSTATS) {
+      // The memory operands of the chunks (addend, BN input x, ReLU bitmap) are loaded four
+      // chunks at a time before those chunks are processed — the first group before the
+      // barrier — so their latency overlaps instead of stalling every chunk in turn.
+      constexpr int PG = NCH < 4 ? NCH : 4;
+      static_assert(NCH % PG == 0, "prefetch groups");
+      uint4 pa[PG], px[PG];
+      uint32_t pxb[PG];
+      auto prefetch = [&](int g) {
+#pragma unroll
+        for (int j = 0; j < PG; ++j) {
+          const int c = threadIdx.x + (g * PG + j) * GT;
+          const int gm = m0 + c / (BN / 8), gn = n0 + (c % (BN / 8)) * 8;
+          const bool ok = vec && gm < Mrow && gn + 8 <= p.N;
+          const int64_t aoff = ok ? orow_of(gm) * p.ldc + gn : 0;
+          pa[j] = (ok && p.addend) ? masked_addend8(p.addend, p.add_bits, aoff) : z4;
+          px[j] = ok ? *reinterpret_cast<const uint4*>(p.bst_x + aoff) : z4;
+          pxb[j] = (ok && p.bst_bits) ? (uint32_t)p.bst_bits[aoff >> 3] : 0u;
+        }
+      };
+      prefetch(0);
+      __syncthreads();
+#pragma unroll
+      for (int g = 0; g < NCH / PG; ++g) {
+        if (g > 0) prefetch(g);
+#pragma unroll
+        for (int j = 0; j < PG; ++j) store_chunk(threadIdx.x + (g * PG + j) * GT, pa[j], px[j], pxb[j], true);
+      }
+    } else {
+      __syncthreads();
+      for (int c = threadIdx.x; c < BM * (BN / 8); c += GT) store_chunk(c, z4, z4, 0u, false);
     }
   } else {
     // fp32 output or split-K slab: two halves through an fp32 staging tile
@@ -790,9 +940,11 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
     }
     return;
   }
-  if (EPI == EPI_STATS) {
+  if (EPI == EPI_STATS || EPI == EPI_BSTATS) {
     // fold the per-thread column sums: GT/(BN/8) threads share each 8-column group
     constexpr int G8 = BN / 8, Q = GT / G8;
+    // statistics row: the M-tile (+ the parity class: classes stack their tiles_m rows)
+    const int srow = tm + (GA ? zc * tiles_m : 0);
     __syncthreads();                              // the staged tile is no longer read
     float* fold = reinterpret_cast<float*>(lds);  // [GT][16]
 #pragma unroll
@@ -811,8 +963,8 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
         b += fold[(q * G8 + g) * 16 + 8 + k];
       }
       // [tiles_m][2][N]: one coalesced row per M-tile (bn.hip k_colsum folds the rows)
-      p.stats[(int64_t)tm * 2 * p.N + n] = a;
-      p.stats[(int64_t)tm * 2 * p.N + p.N + n] = b;
+      p.stats[(int64_t)srow * 2 * p.N + n] = a;
+      p.stats[(int64_t)srow * 2 * p.N + p.N + n] = b;
     }
   }
 }

@@ -133,7 +133,8 @@ struct BNArgs {
   const float* res_shift;
   int stats_blocks;        // bn_stats: >0 = partial sums already in `partial` ([2C][nb])
   const float* stat_rows;  // bn_stats: per-M-tile rows [R][2C] from a GEMM epilogue (or nullptr)
-  int64_t stats_rows_n;    // R
+  int64_t stats_rows_n;    // R (bn_stats; bn_backward: precomputed (Σdy', Σdy'(x−mean)) rows from
+                           // a GEMM's EPI_BSTATS epilogue replace the reduce pass)
   uint8_t* bits;           // ReLU bitmap, 1 bit/element: written by the forward apply, read back
                            // by the backward instead of the saved output (or nullptr)
   bool accum_dparams;      // backward: dgamma/dbeta += (into the gradient arena) instead of =
@@ -194,6 +195,15 @@ struct GemmArgs {
   const uint8_t* add_bits; // optional ReLU bitmap masking the addend (ldc == N)
   bool accumulate;         // fp32 output: C += result (weight gradients into the zeroed arena)
   uint32_t a_bytes, b_bytes;  // operand extents (< 2 GiB): the buffer loads' range check
+  // backward BatchNorm statistics of the bf16 output (EPI_BSTATS, with `stats`): the output is the
+  // gradient dy reaching a BN+ReLU whose input was bst_x ([rows][ldc], ldc == N); per M-tile row
+  // (Σ dy', Σ dy'·(x − mean)) with dy' = dy·mask, mask from bst_bits (ReLU bitmap of the BN's
+  // output) or x*scale+shift > 0 (bst_scale/bst_shift) — the reduce pass of that BN's backward
+  const uint16_t* bst_x;
+  const float* bst_mean;
+  const float* bst_scale;
+  const float* bst_shift;
+  const uint8_t* bst_bits;
 };
 enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_T256x64x32 = 3,
                 GEMM_T64x256x32 = 4, GEMM_T256x64x64 = 5,

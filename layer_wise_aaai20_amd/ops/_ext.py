@@ -13,7 +13,7 @@ import threading
 import torch
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO_PATH = os.path.join(_PKG, "_lwaaai_C.so")
+SO_PATH = os.environ.get("LWAAAI_SO") or os.path.join(_PKG, "_lwaaai_C.so")
 _lock = threading.Lock()
 _loaded = False
 

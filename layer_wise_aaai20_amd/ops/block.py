@@ -59,6 +59,12 @@ CL = torch.channels_last
 # consumers' staging prologues (see _BottleneckFn.forward)
 MAT_A1 = os.environ.get("LWAAAI_MAT_A1", "1") != "0"
 MAT_A2 = os.environ.get("LWAAAI_MAT_A2", "1") != "0"
+# BN1 / BN2 backward reductions in the epilogues of the data-gradient GEMM / conv producing their
+# input gradient (csrc gemm_core.h EPI_BSTATS) instead of a separate pass over dy and x. Off by
+# default: it saves the reduce passes (-1.6 ms of BN kernels) but the extra epilogue operands raise
+# those GEMMs' registers and serialise their memory phases (+2.4 ms): 9,770 vs 10,297 img/s
+# (profiles/r2_bstats_ab.log). LWAAAI_BSTATS=1 / LWAAAI_CROSS_BN3=1 turn the two parts on.
+BSTATS = os.environ.get("LWAAAI_BSTATS", "0") == "1"
 TILES = (1, 2, 3, 4, 5, 6)          # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
 
@@ -132,10 +138,16 @@ def stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro, pro_on_a, add, split
 
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro=None,
          pro_on_a=True, out=None, addend=None, accumulate=False, ldc=0, split_k=False,
-         addend_bits=None):
-    """One MFMA GEMM launch (plus the split-K reduce when ``split_k``); see ``csrc/gemm.hip``."""
+         addend_bits=None, bst=None):
+    """One MFMA GEMM launch (plus the split-K reduce when ``split_k``); see ``csrc/gemm.hip``.
+
+    ``bst = (x, mean, scale_shift, bits)``: the output is the gradient reaching a BN+ReLU whose
+    input was ``x``; with ``stats=True`` the epilogue also writes that BN backward's per-M-tile
+    (Σdy', Σdy'·(x−mean)) rows (mask from ``bits`` or x*scale+shift > 0), which
+    ``bn_bwd(..., stats_rows=)`` folds instead of running its reduce pass."""
     lib = load()
     ps, ph = (pro[0], pro[1]) if pro is not None else (None, None)
+    bx, bm, bss, bb = bst if bst is not None else (None, None, None, None)
 
     def splits_for(tile):
         if not split_k:
@@ -144,17 +156,41 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
         return _splits(-(-M // bm) * -(-N // bn), K)
 
     key = (M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a, split_k,
-           addend is not None)
+           addend is not None, bst is not None)
 
     def run(tile):
         lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile), out_bf16,
-                    tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits)
-    cands = TILES + stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a,
-                                 addend is not None, split_k, accumulate)
+                    tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits,
+                    bx, bm, bss, bb)
+    cands = TILES + (() if bst is not None else
+                     stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a,
+                                  addend is not None, split_k, accumulate))
     tile = TUNER.pick(key, run, cands)
     return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile),
                        out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc,
-                       addend_bits)
+                       addend_bits, bx, bm, bss, bb)
+
+
+# ----------------------------------------------------------------------------- cross-block BN3
+# The gradient reaching block i's output, dout_i, is the dx written by block i+1's last GEMM. When
+# block i+1 has an identity shortcut, that GEMM's epilogue also reduces block i's BN3 backward
+# statistics (Σ dout·[out>0], Σ dout·[out>0]·(c3 − mean3)), so block i skips its reduce pass over
+# dout and c3. Forward hands block i's (output, c3, mean3, ReLU bitmap) to the next block through
+# _FWD_SLOT; backward hands the statistics rows back through _BWD_SLOT, keyed by the gradient
+# tensor and checked against block i's own c3, so a mismatch just falls back to the reduce pass.
+_FWD_SLOT = [None]
+_BWD_SLOT = [None]
+CROSS_BN3 = os.environ.get("LWAAAI_CROSS_BN3", "0") == "1"
+
+
+def _take_prev(x: torch.Tensor):
+    prev, _FWD_SLOT[0] = _FWD_SLOT[0], None
+    if prev is None or not CROSS_BN3:
+        return None
+    out_ptr, shape, c3, mean3, bits3 = prev
+    if x.data_ptr() != out_ptr or tuple(x.shape) != shape:
+        return None
+    return c3, mean3, bits3
 
 
 # ----------------------------------------------------------------------------- grad sink
@@ -230,6 +266,8 @@ class _BottleneckFn(torch.autograd.Function):
         bn1, bn2, bn3, conv2, bnd, down_stride = mods
         for bn in (bn1, bn2, bn3) + ((bnd,) if bnd is not None else ()):
             _bump(bn)                 # before the momentum is read (momentum=None: 1/n)
+        # the previous block's BN3 state, when x is its output (identity shortcut only)
+        ctx.prev = _take_prev(x) if bnd is None else None
         stride = conv2.stride
         N, Cin, H, W = x.shape
         x = x.to(BF16).contiguous(memory_format=CL)
@@ -295,6 +333,7 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.geom = (N, Cin, H, W, N2, H2, W2_, width, cout, M, M2)
         ctx.conv2 = (list(stride), list(conv2.padding), list(conv2.dilation))
         ctx.params = (w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd)
+        _FWD_SLOT[0] = (out.data_ptr(), (N2, cout, H2, W2_), c3, mean3, bits3)
         return _nchw(out, N2, H2, W2_)
 
     @staticmethod
@@ -311,8 +350,12 @@ class _BottleneckFn(torch.autograd.Function):
         o3 = _bn_grad_outs(g3p, b3p)
         # (the shortcut gradient dy·[out>0] is never materialised: its consumers read dy and
         # the bitmap — the dx GEMM as a masked addend, the shortcut BN through its ReLU mode)
+        rows3 = None
+        slot, _BWD_SLOT[0] = _BWD_SLOT[0], None
+        if slot is not None and slot[0] == dr.data_ptr() and slot[2] == c3.data_ptr():
+            rows3 = slot[1]             # reduced by the next block's dx GEMM epilogue
         dc3, dg3, db3, _ = lib.bn_bwd(dr, c3, None, g3, mean3, inv3, None, True, True, False,
-                                      bits3, o3[0], o3[1])
+                                      bits3, o3[0], o3[1], rows3)
         grads = {}
         grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
         # conv3: weight gradient on a2 (or with BN2-apply recomputed in the B prologue), fp32
@@ -322,10 +365,12 @@ class _BottleneckFn(torch.autograd.Function):
              out_bf16=False, pro=(ss2[:width], ss2[width:]) if a2 is None else None,
              pro_on_a=False, out=dst3, accumulate=True, split_k=True)
         grads["w3"] = _finish_wgrad(w3, dst3, d3)
-        da2, _ = gemm(dc3, cout, True, W3, width, False, M2, width, cout)
+        # da2 = dc3·W3, its epilogue doing BN2's backward reduction (mask from c2 via ss2)
+        da2, rows2 = gemm(dc3, cout, True, W3, width, False, M2, width, cout, stats=BSTATS,
+                          bst=(c2, mean2, ss2, None) if BSTATS else None)
         o2 = _bn_grad_outs(g2p, b2p)
         dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False,
-                                      None, o2[0], o2[1])
+                                      None, o2[0], o2[1], rows2 if BSTATS else None)
         grads["g2"], grads["b2"] = _finish_bn(g2p, b2p, dg2, db2, o2)
         # conv2 (3x3) backward on the implicit GEMM: the weight gradient reads a1 (or
         # recomputes relu(bn1(c1)) in its staging prologue) and accumulates fp32 straight into
@@ -340,10 +385,15 @@ class _BottleneckFn(torch.autograd.Function):
         else:
             dW2 = conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1)
             grads["w2"] = _finish_param(w2, dW2.contiguous(memory_format=CL), _direct(w2))
-        da1 = _rows(conv_dgrad(dc2n, W2, (H, W), stride, padding))
+        # da1 = conv3x3ᵀ(dc2), its epilogue doing BN1's backward reduction
+        if BSTATS:
+            da1n, rows1 = conv_dgrad(dc2n, W2, (H, W), stride, padding, bst=(c1, mean1, ss1, None))
+        else:
+            da1n, rows1 = conv_dgrad(dc2n, W2, (H, W), stride, padding), None
+        da1 = _rows(da1n)
         o1 = _bn_grad_outs(g1p, b1p)
         dc1, dg1, db1, _ = lib.bn_bwd(da1, c1, None, g1, mean1, inv1, ss1, True, True, False,
-                                      None, o1[0], o1[1])
+                                      None, o1[0], o1[1], rows1)
         grads["g1"], grads["b1"] = _finish_bn(g1p, b1p, dg1, db1, o1)
         xr = _rows(x)
         dst1, d1 = _wgrad_target(w1, (width, Cin))
@@ -374,8 +424,14 @@ class _BottleneckFn(torch.autograd.Function):
                 conv_dgrad(_nchw(dcd, N2, H2, W2_), Wd.view(cout, Cin, 1, 1), (H, W), s, 0,
                            out=dx, addend=dx)
         else:
-            dx, _ = gemm(dc1, width, True, W1, Cin, False, M, Cin, width, addend=dr,
-                         addend_bits=bits3)
+            prev = ctx.prev           # the previous block's (c3, mean3, bits3): reduce its BN3
+            dx, rows_prev = gemm(dc1, width, True, W1, Cin, False, M, Cin, width, addend=dr,
+                                 addend_bits=bits3, stats=prev is not None,
+                                 bst=(prev[0], prev[1], None, prev[2]) if prev is not None
+                                 else None)
+            if prev is not None:
+                _BWD_SLOT[0] = (dx.data_ptr(), rows_prev, prev[0].data_ptr())
+        ctx.prev = None
         dxn = _nchw(dx, N, H, W)
         return (dxn, grads["w1"], grads["g1"], grads["b1"], grads["w2"], grads["g2"], grads["b2"],
                 grads["w3"], grads["g3"], grads["b3"], grads.get("wd"), grads.get("gd"),

@@ -180,13 +180,18 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=None,
-               out: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None):
+               out: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None,
+               bst=None):
     """dx [N, C, H, W] (bf16 channels_last) of conv2d(x, w) given dy [N, Co, Ho, Wo].
 
     ``out`` (bf16 [N*H*W, C] rows) receives the result — only the pixels some tap reaches are
     written — and ``addend`` (same layout, may be ``out`` itself) is added to them after rounding:
     ``conv_dgrad(dy, w, hw, 2, 0, out=dx, addend=dx)`` accumulates a strided 1x1 shortcut's data
-    gradient into dx in place."""
+    gradient into dx in place.
+
+    ``bst = (x, mean, scale_shift, bits)`` (see ``ops/block.py gemm``): also return the per-tile
+    backward statistics of the BN+ReLU whose input was ``x`` (rows per parity class), i.e.
+    ``(dx, stats_rows)``."""
     lib = load()
     sh, sw = _pair(stride)
     ph, pw = _pair(padding)
@@ -196,6 +201,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
     Nb, _, Ho, Wo = dyc.shape
     classes = _dgrad_classes(H, W, R, S, sh, sw, ph, pw)
     if not classes:
+        assert bst is None, "backward statistics of an all-zero gradient"
         if out is not None:
             return _nchw_rows(out, Nb, H, W)
         return torch.zeros((Nb, c, H, W), dtype=BF16, device=dy.device, memory_format=CL)
@@ -205,12 +211,17 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
         geom += [TR, TS, oh, ow, Hg, Wg, ch, cw, TR * TS * co, off]
     M = max(Nb * cl[6] * cl[7] for cl in classes)
 
+    bx, bm, bss, bb = bst if bst is not None else (None, None, None, None)
+
     def run(tile, dst=None, add=None):
-        return lib.conv_ex(dyc, wt, CV_A, geom, c, tile, 1, True, None, None, False, dst,
-                           False, 0, False, c, add)
-    key = ("d", tuple(dyc.shape), tuple(w.shape), H, W, sh, sw, ph, pw, addend is not None)
+        return lib.conv_ex(dyc, wt, CV_A, geom, c, tile, 1, True, None, None, bst is not None,
+                           dst, False, 0, False, c, add, bx, bm, bss, bb)
+    key = ("d", tuple(dyc.shape), tuple(w.shape), H, W, sh, sw, ph, pw, addend is not None,
+           bst is not None)
     tile = TUNER.pick(key, run, ROW_TILES, _row_default(M, c))   # (timed on scratch outputs)
-    dx, _ = run(tile, out, addend)
+    dx, st = run(tile, out, addend)
+    if bst is not None:
+        return _nchw_rows(dx, Nb, H, W), st
     return _nchw_rows(dx, Nb, H, W)
 
 

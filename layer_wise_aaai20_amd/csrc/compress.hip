@@ -200,7 +200,7 @@ __global__ __launch_bounds__(NT) void k_small_select(
     bool sel = false;
     uint32_t pos = 0;
     if (key[k] > S.tkey) { sel = true; pos = gb + min(eb, S.quota); ++gb; }
-    else if (key[k] == S.tkey) { if (eb < S.quota) { sel = true; pos = gb + eb; } ++eb; }
+    else if (key[k] == S.tkey) { if (eb < S.quota) { pos = gb + eb; sel = pos < S.cap; } ++eb; }
     if (sel) {
       if (OUT == OUT_PAIRS) pairs[c0 + pos] = make_int2(i, __float_as_int(v[k]));
       else { vals[c0 + pos] = v[k]; idx_out[c0 + pos] = i; }
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
     bool sel = false;
     uint32_t pos = 0;
     if (key[k] > S.tkey) { pos = gb + min(eb, S.quota); sel = pos < S.cap; ++gb; }
-    else if (key[k] == S.tkey) { if (eb < S.quota) { sel = true; pos = gb + eb; } ++eb; }
+    else if (key[k] == S.tkey) { if (eb < S.quota) { pos = gb + eb; sel = pos < S.cap; } ++eb; }
     if (sel) {
       if (OUT == OUT_PAIRS) pairs[c0 + pos] = make_int2(i, __float_as_int(v[k]));
       else { vals[c0 + pos] = v[k]; idx_out[c0 + pos] = i; }

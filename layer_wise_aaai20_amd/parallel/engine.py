@@ -104,8 +104,12 @@ class GradSyncEngine:
         # compression + collective launch run on a side HIP stream, ordered after the bucket's
         # last gradient by an event, so they overlap the rest of the backward pass; the compute
         # stream waits on a second event only when it decodes in finish()
+        import os
+        overlap_compress = overlap_compress and os.environ.get("LWAAAI_OVERLAP", "1") != "0"
         self._side = (torch.cuda.Stream(device=self.device)
                       if overlap_compress and self.device.type == "cuda" else None)
+        self._retired = []            # (fence event, events held until it completes)
+        self._check = os.environ.get("LWAAAI_ENGINE_CHECK", "0") == "1"
         self._stream_waitable = (comm.is_dist() and comm.world_size(self.pg) > 1 and
                                  comm.dist.get_backend(self.pg) == "nccl")
         self._reset_state()
@@ -138,6 +142,7 @@ class GradSyncEngine:
 
     # ----------------------------------------------------------------- state machine
     def _reset_state(self):
+        self._marked = bytearray(len(self.arena.segments))
         nb = len(self.buckets)
         self._ready_cnt = [0] * nb
         self._ready = [False] * nb
@@ -157,6 +162,17 @@ class GradSyncEngine:
         self._reset_state()
 
     def mark_ready(self, seg_index: int) -> None:
+        """A segment's gradient is complete in the arena. Idempotent within a step: a parameter
+        whose gradient a fused op wrote straight into the arena is announced by that op, and
+        autograd then runs its post-accumulate-grad hook as well (PyTorch calls those hooks even
+        when the Function returned no gradient for the input) — counted twice, the bucket would
+        launch before its other segments were written (profiles/r2_vgg_fault.md)."""
+        if self._marked[seg_index]:
+            return
+        self._marked[seg_index] = 1
+        if self._check and self.seg_bucket[seg_index] < self._next:
+            raise RuntimeError(f"segment {self.arena.segments[seg_index].name} marked ready "
+                               f"after its bucket {self.seg_bucket[seg_index]} was launched")
         self._active = True
         b = self.seg_bucket[seg_index]
         self._ready_cnt[b] += 1
@@ -181,7 +197,11 @@ class GradSyncEngine:
         g = self.arena.grad[b.start:b.end]
         e = self.ef[b.start:b.end] if self.ef is not None else None
         side = self._side
+        ready = None
         if side is not None:
+            # the event must outlive the side stream's wait on it: it stays in _pending until
+            # finish() (a HIP event destroyed while a queued wait still references it faulted
+            # the VGG-16 run: hipErrorIllegalAddress, profiles/r2_vgg_fault.md)
             ready = torch.cuda.Event()
             ready.record(torch.cuda.current_stream(self.device))
             side.wait_event(ready)
@@ -206,7 +226,7 @@ class GradSyncEngine:
             if side is not None:
                 done = torch.cuda.Event()
                 done.record(side)
-        self._pending.append((bi, work, send, recv, (t0, t1, tx), done))
+        self._pending.append((bi, work, send, recv, (t0, t1, tx), done, ready))
 
     def finish(self) -> None:
         """Launch buckets that never became ready (unused params keep zero grads), wait for every
@@ -215,7 +235,9 @@ class GradSyncEngine:
             self._ready[i] = True
         self._launch_in_order()
         rec = []
-        for bi, work, send, recv, (t0, t1, tx), done in self._pending:
+        hold = []                                # events some stream still waits on (see below)
+        for bi, work, send, recv, (t0, t1, tx), done, ready in self._pending:
+            hold += [e for e in (ready, done) if e is not None]
             work.wait()
             if done is not None:                 # decode on the compute stream after the side
                 cur = torch.cuda.current_stream(self.device)
@@ -229,6 +251,15 @@ class GradSyncEngine:
             if self.timing:
                 rec.append((bi, t0, t1, tx, t2, self._event()))
         self._pending = []
+        if hold:
+            # Keep the cross-stream events alive until a fence on the compute stream, recorded
+            # after every wait on them, has completed: destroying a HIP event while a queued
+            # stream wait still references it is what faulted the VGG-16 run
+            # (hipErrorIllegalAddress; profiles/r2_vgg_fault.md).
+            fence = torch.cuda.Event()
+            fence.record(torch.cuda.current_stream(self.device))
+            self._retired = [(f, h) for f, h in self._retired if not f.query()]
+            self._retired.append((fence, hold))
         if self.timing:
             self._last_events = rec
         self.step += 1

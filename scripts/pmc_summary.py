@@ -1,0 +1,19 @@
+#!/usr/bin/env python
+"""Sum a rocprofv3 counter_collection.csv per kernel name (last 2 steps' worth of dispatches are
+what a short bench run mostly contains; warm-up dispatches are included) and print one row per
+kernel, largest SQ_WAVE_CYCLES / FETCH_SIZE first."""
+import collections
+import csv
+import sys
+
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+disp = collections.defaultdict(set)
+for r in csv.DictReader(open(sys.argv[1])):
+    k = r["Kernel_Name"][:90]
+    agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+    disp[k].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
+names = sorted({n for d in agg.values() for n in d})
+key = "SQ_WAVE_CYCLES" if "SQ_WAVE_CYCLES" in names else names[0]
+print("kernel".ljust(92), "disp", " ".join(n[:16].rjust(16) for n in names))
+for k, d in sorted(agg.items(), key=lambda kv: -kv[1].get(key, 0))[:60]:
+    print(k.ljust(92), str(len(disp[k])).rjust(4), " ".join(f"{d.get(n, 0):16.0f}" for n in names))

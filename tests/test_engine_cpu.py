@@ -139,3 +139,73 @@ def test_flat_sgd_matches_torch_sgd_and_state_dict():
     for k, v in oa.state_dict()["state"].items():
         torch.testing.assert_close(sd["state"][k]["momentum_buffer"], v["momentum_buffer"],
                                    rtol=1e-5, atol=1e-6)
+
+
+class _DirectLinear(torch.autograd.Function):
+    """Like the fused MFMA ops (ops/block.py, ops/gemm.py): the weight gradient is written straight
+    into its arena view, the op announces it with ``_lw_grad_ready`` and returns None for it —
+    after which PyTorch still runs the weight's post-accumulate-grad hook."""
+
+    @staticmethod
+    def forward(ctx, x, w, written):
+        ctx.save_for_backward(x, w)
+        ctx.written = written
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        p = ctx.w_param
+        if getattr(p, "_lw_grad_ready", None) is not None and p.grad is not None:
+            p.grad.add_(dy.t() @ x)
+            ctx.written.add(id(p))
+            p._lw_grad_ready(p)
+            return dy @ w, None, None
+        return dy @ w, dy.t() @ x, None
+
+
+class _DirectNet(nn.Module):
+    def __init__(self, written):
+        super().__init__()
+        self.written = written
+        self.l1, self.l2, self.l3 = (nn.Linear(16, 16, bias=False) for _ in range(3))
+
+    def forward(self, x):
+        for m in (self.l1, self.l2, self.l3):
+            x = torch.relu(_DirectLinear.apply(x, m.weight, self.written))
+        return x
+
+
+def test_direct_arena_gradients_count_once_per_step():
+    """A bucket is launched only once every one of its segments is complete, even though a
+    directly-written parameter is announced twice (by the op, then by autograd's hook)."""
+    written = set()
+    net = _DirectNet(written)
+    ddp = CompressedDDP(net, compress="layerwise", method="Topk", K=0.5, bucket_cap_mb=1.0,
+                        flat_params=True)
+    params = {id(m.weight): m.weight for m in (net.l1, net.l2, net.l3)}
+    launched = []
+    real = ddp.engine._launch
+
+    def launch(bi):
+        b = ddp.engine.buckets[bi]
+        segs = ddp.engine.arena.segments[b.seg_lo:b.seg_hi]
+        launched.append(all(id(s.param) in written for s in segs))
+        real(bi)
+    ddp.engine._launch = launch
+    # route each Function call to its weight
+    apply = _DirectLinear.apply
+
+    def apply_with_param(x, w, wr):
+        out = apply(x, w, wr)
+        out.grad_fn.w_param = params[id(w)]
+        return out
+    _DirectLinear.apply = staticmethod(apply_with_param)
+    try:
+        for _ in range(2):
+            written.clear()
+            launched.clear()
+            ddp(torch.randn(4, 16)).sum().backward()
+            assert launched and all(launched), launched
+    finally:
+        _DirectLinear.apply = staticmethod(apply)

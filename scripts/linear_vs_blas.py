@@ -6,10 +6,14 @@ BLAS path from the models cost nothing. Prints one row per (shape, pass): µs ou
 
 Shapes: ResNet-50 fc (IMAGENET/training/resnet.py:110, batch 256), CIFAR AlexNet classic and
 VGG-16 classifiers (CIFAR10/alexnet.py:29-37, CIFAR10/vgg16.py:23-31, batch 512)."""
-import torch
-import torch.nn.functional as F
+import os
+import sys
 
-from layer_wise_aaai20_amd.ops import gemm as G
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from layer_wise_aaai20_amd.ops import gemm as G  # noqa: E402
 
 SHAPES = [("resnet50.fc", 256, 2048, 1000), ("alexnet.fc1", 512, 1024, 4096),
           ("alexnet.fc2", 512, 4096, 4096), ("alexnet.fc3", 512, 4096, 10),

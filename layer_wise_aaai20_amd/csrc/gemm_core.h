@@ -349,6 +349,7 @@ struct RowGather {
   int hb[PT], wb[PT];
   int kc;               // this thread's k offset within a step (cc*8)
   int ci0, js, jr;      // fast path: tap and first channel of the next K-step (uniform)
+  int c4_drow, c4_js;   // 4-channel image: the thread's tap relative to the step's first row
 };
 
 template <int R, int BK, bool DMA = false>
@@ -359,6 +360,10 @@ __device__ __forceinline__ void row_gather_init(RowGather<R, BK>& g, const uint1
   g.rs = make_rsrc(X, bytes);
   const int hw = cc.Hg * cc.Wg;
   g.kc = src_chunk<R, BK, true, DMA>((int)(threadIdx.x % T::CPR), (int)(threadIdx.x / T::CPR)) * 8;
+  // 4-channel gather with BK a multiple of a whole filter row (4*TS elements): a K-step covers
+  // whole rows, so the thread's tap offset within them is fixed (no per-chunk division)
+  g.c4_drow = (g.kc >> 2) / cc.TS;
+  g.c4_js = (g.kc >> 2) - g.c4_drow * cc.TS;
 #pragma unroll
   for (int h = 0; h < T::PER_T; ++h) {
     int rr, c8;
@@ -419,10 +424,17 @@ __device__ __forceinline__ void load_tile_gather_a(const ConvGeom& cv, const Con
   }
   // per-thread tap decode (the chunk's k is k + kc)
   const int kk = k + g.kc;
-  int t, ci;
-  if (C4) { t = kk >> 2; ci = 0; }
-  else { t = kk / cv.C; ci = kk - t * cv.C; }
-  const int jr = t / cc.TS, js = t - jr * cc.TS;
+  int t, ci, jr, js;
+  if (C4 && BK % (4 * cc.TS) == 0) {      // whole filter rows per step: uniform row, fixed tap
+    ci = 0;
+    jr = k / (4 * cc.TS) + g.c4_drow;
+    js = g.c4_js;
+  } else {
+    if (C4) { t = kk >> 2; ci = 0; }
+    else { t = kk / cv.C; ci = kk - t * cv.C; }
+    jr = t / cc.TS;
+    js = t - jr * cc.TS;
+  }
   const int ho = cv.dh * jr, wo = cv.dw * js;
   // rowoff holds channel kc: rebase it on (tap, ci)
   const int delta = ((ho * cv.Win + wo) * cv.C + ci - g.kc) * 2;

@@ -48,7 +48,10 @@ def _ws_tensor(nbytes: int, device) -> torch.Tensor:
 
 
 def tie_slack(m: int) -> int:
-    return max(1, -(-m // 64))
+    """Extra payload slots per layer for Top-K values tied at the threshold (the reference keeps
+    every element >= the k-th largest, so a tie can make it send more than k): 1/64 of k, and at
+    least 16 — small layers (a 1000-way classifier bias keeps k = 1) can tie many ways."""
+    return max(16, -(-m // 64))
 
 
 class Codec:

@@ -38,12 +38,12 @@ def gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False, splits=1
                           pro_shift, pro_on_a, stats)
 
 
-def linear_fwd(x2, w, bias=None, relu=False):
-    """x2 [M,K] bf16, w [N,K] bf16 -> [M,N] bf16 = relu?(x2·wᵀ + bias)."""
+def linear_fwd(x2, w, bias=None, relu=False, out_fp32=False):
+    """x2 [M,K] bf16, w [N,K] bf16 -> [M,N] bf16 (or fp32) = relu?(x2·wᵀ + bias)."""
     M, K = x2.shape
     N = w.shape[0]
     tiles = -(-M // 128) * -(-N // 128)
-    return gemm(x2, K, True, w, K, True, M, N, K, bias, relu, _splits(tiles, K), True)
+    return gemm(x2, K, True, w, K, True, M, N, K, bias, relu, _splits(tiles, K), not out_fp32)
 
 
 def linear_dgrad(dy2, w):
@@ -73,7 +73,7 @@ def _pad_rows(w: torch.Tensor, n: int) -> torch.Tensor:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, relu):
+    def forward(ctx, x, weight, bias, relu, out_fp32=False):
         from .block import _bf16_weight
         shp = x.shape
         N, K = weight.shape
@@ -84,7 +84,7 @@ class _LinearFn(torch.autograd.Function):
         if bias is not None:
             b = bias.float() if Np == N else torch.cat([bias.float(),
                                                         bias.new_zeros(Np - N).float()])
-        y = linear_fwd(x2, w, b, relu)
+        y = linear_fwd(x2, w, b, relu, out_fp32)
         if Np != N:
             y = y[:, :N]
         ctx.save_for_backward(x2, w, y if relu else None)
@@ -96,9 +96,13 @@ class _LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w, y = ctx.saved_tensors
         N, Np = ctx.N, ctx.Np
-        dy2 = dy.reshape(-1, N).to(torch.bfloat16)
+        dyf = dy.reshape(-1, N)
         if ctx.relu:
-            dy2 = dy2 * (y > 0)
+            dyf = dyf * (y > 0)
+        # the bias gradient from dy as it arrives (fp32 for an fp32-output classifier: a bf16 dy
+        # makes many logits' bias gradients exactly equal — Top-K ties at the threshold)
+        db = dyf.float().sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        dy2 = dyf.to(torch.bfloat16)
         if Np != N:
             dy2 = torch.cat([dy2, dy2.new_zeros(dy2.shape[0], Np - N)], 1)
         dy2 = dy2.contiguous()
@@ -117,17 +121,16 @@ class _LinearFn(torch.autograd.Function):
                 p._lw_grad_ready(p)
             else:
                 dw = linear_wgrad(dy2, x2)[:N].to(p.dtype)
-        db = dy2[:, :N].float().sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def _gemm_ok(x, weight):
     return x.is_cuda and weight.shape[1] % 8 == 0
 
 
-def mfma_linear(x, weight, bias=None, relu=False):
+def mfma_linear(x, weight, bias=None, relu=False, out_fp32=False):
     if _gemm_ok(x, weight):
-        return _LinearFn.apply(x, weight, bias, relu)
+        return _LinearFn.apply(x, weight, bias, relu, out_fp32)
     y = F.linear(x, weight, bias)
     return F.relu(y) if relu else y
 
@@ -136,17 +139,21 @@ class MFMALinear(nn.Linear):
     """nn.Linear on the hand-written MFMA GEMM; ``fuse_relu`` applies the following ReLU in the
     epilogue (VGG / AlexNet classifiers)."""
 
-    def __init__(self, in_features, out_features, bias=True, fuse_relu=False, **kw):
+    def __init__(self, in_features, out_features, bias=True, fuse_relu=False, out_fp32=False,
+                 **kw):
         super().__init__(in_features, out_features, bias, **kw)
         self.fuse_relu = fuse_relu
+        self.out_fp32 = out_fp32
 
     def forward(self, x):
-        return mfma_linear(x, self.weight, self.bias, self.fuse_relu)
+        return mfma_linear(x, self.weight, self.bias, self.fuse_relu,
+                           getattr(self, "out_fp32", False))
 
 
-def to_mfma_linear(m: nn.Linear, fuse_relu=False) -> MFMALinear:
+def to_mfma_linear(m: nn.Linear, fuse_relu=False, out_fp32=False) -> MFMALinear:
     m.__class__ = MFMALinear
     m.fuse_relu = fuse_relu
+    m.out_fp32 = out_fp32
     return m
 
 
@@ -165,4 +172,9 @@ def fuse_linears(model: nn.Module) -> nn.Module:
     for mod in model.modules():
         if type(mod) is nn.Linear:
             to_mfma_linear(mod)
+    # the model's last Linear (the classifier) produces fp32 logits: the loss reads them in fp32
+    # anyway, and its gradient — the classifier bias gradient — stays fp32
+    last = [m for m in model.modules() if isinstance(m, MFMALinear)]
+    if last and not last[-1].fuse_relu:
+        last[-1].out_fp32 = True
     return model

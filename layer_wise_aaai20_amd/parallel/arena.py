@@ -169,28 +169,43 @@ class Bucket:
 
 
 def plan_buckets(arena: GradArena, mode: str, cap_bytes: int,
-                 first_bucket_bytes: Optional[int] = None) -> List[Bucket]:
+                 first_bucket_bytes: Optional[int] = None,
+                 last_bucket_bytes: Optional[int] = None) -> List[Bucket]:
     """Contiguous buckets over the arena.
 
     ``mode == 'entiremodel'`` → one bucket, one segment spanning everything (the compressor sees the
     concatenated model, ``core.py:227-236``).  ``layerwise``/``none`` → consecutive segments are
     grouped until ``cap_bytes`` (of fp32 gradient) is reached; a bucket never splits a segment. A
     smaller first bucket lets communication start earlier in backward (the last layers' grads come
-    first).
+    first). A smaller LAST bucket shortens the tail: the first layers' gradients are the last to be
+    computed, so that bucket's compression and exchange cannot overlap any backward work — its
+    size is what the step waits for after the backward pass.
     """
     segs = arena.segments
     if mode == "entiremodel":
         return [Bucket(0, 0, len(segs), 0, arena.numel)]
     esize = arena.grad.element_size()
+    # tail: whole segments from the end until last_bucket_bytes (never all of them)
+    tail = len(segs)
+    if last_bucket_bytes:
+        acc = 0
+        while tail > 1 and acc < last_bucket_bytes:
+            tail -= 1
+            acc += segs[tail].numel * esize
+        if tail == 0:
+            tail = len(segs)
     buckets: List[Bucket] = []
     lo = 0
     acc = 0
     cap = first_bucket_bytes if first_bucket_bytes else cap_bytes
-    for i, s in enumerate(segs):
-        acc += s.numel * esize
-        if acc >= cap and i + 1 < len(segs):
+    for i in range(tail):
+        acc += segs[i].numel * esize
+        if acc >= cap and i + 1 < tail:
             buckets.append(Bucket(len(buckets), lo, i + 1, segs[lo].offset,
                                   segs[i + 1].offset))
             lo, acc, cap = i + 1, 0, cap_bytes
-    buckets.append(Bucket(len(buckets), lo, len(segs), segs[lo].offset, arena.numel))
+    end = segs[tail].offset if tail < len(segs) else arena.numel
+    buckets.append(Bucket(len(buckets), lo, tail, segs[lo].offset, end))
+    if tail < len(segs):
+        buckets.append(Bucket(len(buckets), tail, len(segs), segs[tail].offset, arena.numel))
     return buckets

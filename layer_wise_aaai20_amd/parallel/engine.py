@@ -18,6 +18,7 @@ flat arena. No gradient is ever reduced twice.
 from __future__ import annotations
 
 import contextlib
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
@@ -60,7 +61,8 @@ class SyncStats:
 class GradSyncEngine:
     def __init__(self, named_params, mode: str = "layerwise", method="none", K=None, V=None,
                  qstates=None, error_feedback: bool = False, bucket_cap_mb: float = 25.0,
-                 first_bucket_mb: Optional[float] = None, wire: str = "auto",
+                 first_bucket_mb: Optional[float] = None, last_bucket_mb: Optional[float] = 4.0,
+                 wire: str = "auto",
                  seed: int = 2147483647, process_group=None, flat_params: bool = False,
                  world_size: Optional[int] = None, timing: bool = False,
                  overlap_compress: bool = True):
@@ -75,7 +77,10 @@ class GradSyncEngine:
         self.device = self.arena.device
         cap = int(bucket_cap_mb * 2 ** 20)
         first = int(first_bucket_mb * 2 ** 20) if first_bucket_mb else None
-        self.buckets: List[Bucket] = plan_buckets(self.arena, self.mode, cap, first)
+        last_bucket_mb = float(os.environ.get("LWAAAI_LAST_BUCKET_MB", last_bucket_mb or 0))
+        last = int(last_bucket_mb * 2 ** 20) if last_bucket_mb else None
+        self.buckets: List[Bucket] = plan_buckets(self.arena, self.mode, cap, first,
+                                                  last if last and last < cap else None)
         self.seed = int(seed)
         self.ef = torch.zeros_like(self.arena.grad) if (error_feedback and
                                                        self.method != "none") else None

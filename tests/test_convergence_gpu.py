@@ -9,9 +9,10 @@ is unpinned (no CIFAR-10 here).
 
 Error feedback needs a contractive compressor (||C(v) - v||² < ||v||²). QSGD with s levels on an
 n-element vector has relative variance up to sqrt(n)/s: ≈ 20 for s = 127 over the whole
-6.6 M-parameter ResNet-9, so with EF the residual grows geometrically (the loss reached 1e14 in
-200 steps on MI355X). Entire-model QSGD therefore runs with 16-bit codes (s = 32767, variance
-≈ 0.08); layer-wise keeps s = 127 (per-layer n is smaller and the gradients heavy-tailed)."""
+6.6 M-parameter ResNet-9 and ≈ 12 for its largest layer, so with EF the residual grows
+geometrically (entire-model: the loss reached 1e14 in 200 steps on MI355X; layer-wise: held-out
+accuracy 25 %). QSGD therefore runs with 16-bit codes here (s = 32767, variance ≈ 0.08); the 8/9-bit
+codes are checked bit for bit against the CPU mirror in tests/test_kernels_gpu.py."""
 import pytest
 import torch
 
@@ -19,13 +20,7 @@ pytestmark = pytest.mark.gpu
 
 METHODS = [("none", {}), ("Topk", {"K": 0.01}), ("Randomk", {"K": 0.05}),
            ("Thresholdv", {"V": 1e-3}), ("AdaptiveThreshold", {}), ("TernGrad", {}),
-           ("RandomDithering", {"qstates": 127})]
-
-
-def entire_model_kw(method, mode, kw):
-    if method == "RandomDithering" and mode == "entiremodel":
-        return {"qstates": 32767}
-    return kw
+           ("RandomDithering", {"qstates": 32767})]
 
 
 @pytest.mark.parametrize("mode", ["layerwise", "entiremodel"])
@@ -36,7 +31,7 @@ def test_resnet9_learns_with_compression(method, kw, mode):
     torch.manual_seed(0)
     tr = CifarTrainer("resnet9", compress=mode if method != "none" else "none", method=method,
                       error_feedback=method != "none", batch_size=128, epochs=2,
-                      n_train=12800, seed=0, **entire_model_kw(method, mode, kw))
+                      n_train=12800, seed=0, **kw)
     from layer_wise_aaai20_amd.utils.logging import PiecewiseLinear
     steps = 200
     tr.steps_per_epoch = 1                           # schedule in steps: warm-up 40, decay to 0

@@ -109,7 +109,6 @@ class GradSyncEngine:
         # compression + collective launch run on a side HIP stream, ordered after the bucket's
         # last gradient by an event, so they overlap the rest of the backward pass; the compute
         # stream waits on a second event only when it decodes in finish()
-        import os
         overlap_compress = overlap_compress and os.environ.get("LWAAAI_OVERLAP", "1") != "0"
         self._side = (torch.cuda.Stream(device=self.device)
                       if overlap_compress and self.device.type == "cuda" else None)

@@ -550,12 +550,51 @@ __device__ __forceinline__ void store_tile_rows(uint16_t* __restrict__ S,
     *reinterpret_cast<uint4*>(S + rr * T::LD + (c0 + h) * 8) = r[h];
 }
 
+// LDS-DMA ring depth: bytes in flight per CU, not K-steps, hide the L2/Infinity-Cache latency
+// (Little's law: ~64 KB in flight caps a 128x128 tile at ~40 % of the MFMA rate). LW_NSTAGE
+// overrides for experiments.
+#ifndef LW_NSTAGE
+#define LW_NSTAGE 2
+#endif
+__host__ __device__ constexpr int dma_stages(int bm, int bn) {
+  return (bm + bn) * 64 * 2 * LW_NSTAGE <= 160 * 1024 - 8192 ? LW_NSTAGE : 2;
+}
+
+// Wait until at most `ahead` K-steps (PER DMAs each) of this wave are still in flight, then
+// barrier. Inline asm with a memory clobber: a __syncthreads() would drain every DMA (vmcnt(0)).
+template <int N>
+__device__ __forceinline__ void vm_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+template <int NS, int PER>
+__device__ __forceinline__ void dma_wait_barrier(int ahead) {
+  static_assert((NS - 2) * PER <= 63, "vmcnt is 6 bits");
+  if (NS >= 4 && ahead >= 2) vm_wait_barrier<(NS >= 4 ? 2 * PER : 0)>();
+  else if (NS >= 3 && ahead >= 1) vm_wait_barrier<(NS >= 3 ? PER : 0)>();
+  else vm_wait_barrier<0>();
+}
+
 // Workgroup id → (m-tile, n-tile): consecutive ids are dealt round-robin to the 8 XCDs, so remap
 // each XCD's share onto one contiguous range of the row-major tile order.
 __device__ __forceinline__ int xcd_remap(int pid, int total) {
   const int q = total >> 3, rem = total & 7;
   const int x = pid & 7, idx = pid >> 3;
   return x * q + (x < rem ? x : rem) + idx;
+}
+
+// Tile order within an XCD's contiguous range: groups of GROUP_M tile rows, column-major inside
+// a group, so the ~64 workgroups an XCD holds at once cover a GROUP_M x (64 / GROUP_M) block of
+// tiles and share GROUP_M A row-panels and as many B column-panels in its L2 — instead of one A
+// panel and 64 B panels (row-major). Skinny-M problems (tiles_m <= GROUP_M, e.g. a classifier at
+// batch 512) become column-major: each XCD streams its own slice of the large weight operand.
+constexpr int GROUP_M = 8;
+__device__ __forceinline__ void tile_of(int pid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int per_group = GROUP_M * tiles_n;
+  const int g = pid / per_group, first = g * GROUP_M;
+  const int rows = min(tiles_m - first, GROUP_M);
+  const int r = pid - g * per_group;
+  tm = first + r % rows;
+  tn = r / rows;
 }
 
 template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int PRO, int CV = CV_NONE>
@@ -568,7 +607,11 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   constexpr int LDH = BN + 16;                 // bf16 staging row (≡ 8 dwords mod 64 banks)
   constexpr int CS_BYTES = WTM * LDC * 4;
   constexpr int CH_BYTES = BM * LDH * 2 + 2 * 2 * BN * 4;
-  constexpr int ST_BYTES = 2 * STAGE * 2;
+  // both operands K-contiguous BK = 64 swizzled tiles, no prologue: stage by LDS-DMA
+  constexpr bool GL = LW_GLDS && AKC && BKC && BK == 64 && PRO == PRO_NONE &&
+                      (CV == CV_NONE || CV == CV_A);
+  constexpr int NS = GL ? dma_stages(BM, BN) : 2;    // LDS stages (ring)
+  constexpr int ST_BYTES = NS * STAGE * 2;
   constexpr int LDS_BYTES = ST_BYTES > CS_BYTES ? (ST_BYTES > CH_BYTES ? ST_BYTES : CH_BYTES)
                                                 : (CS_BYTES > CH_BYTES ? CS_BYTES : CH_BYTES);
   constexpr bool GA = CV == CV_A || CV == CV_A4, GB = CV == CV_B || CV == CV_B4;
@@ -582,8 +625,8 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   uint16_t* st = reinterpret_cast<uint16_t*>(lds);
 
   const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
-  const int pid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = pid / tiles_n, tn = pid - tm * tiles_n;
+  int tm, tn;
+  tile_of(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   // the class record by constant index (a runtime index into the by-value kernel argument
   // would copy the whole array to scratch)
@@ -598,9 +641,6 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   const int Mrow = GA ? ccl.M : p.M;             // valid GEMM rows of this workgroup
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wr = w >> 1, wc = w & 1;
-  // both operands K-contiguous BK = 64 swizzled tiles, no prologue: stage by LDS-DMA
-  constexpr bool GL = LW_GLDS && AKC && BKC && BK == 64 && PRO == PRO_NONE &&
-                      (CV == CV_NONE || CV == CV_A);
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -681,14 +721,21 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       }
       lb.dma(dst + TA::ELEMS, k, kend);
     };
-    if (nsteps > 0) issue(kbeg, st);
-    __syncthreads();
-    int cur = 0;
+    // NS-stage ring: K-steps i+1 .. i+NS-1 are in flight while step i computes. Before the
+    // barrier that publishes step i+1, a wave waits only for that step's DMAs (the newer ones
+    // stay outstanding: loads complete in order, PER per step and thread).
+    constexpr int PER = TA::PER_T + TB::PER_T;
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nsteps) issue(kbeg + s * BK, st + s * STAGE);
+    dma_wait_barrier<NS, PER>(min(NS - 2, nsteps - 1));
+    int cur = 0, nxt = NS - 1;
     for (int i = 0; i < nsteps; ++i) {
-      if (i + 1 < nsteps) issue(kbeg + (i + 1) * BK, st + (cur ^ 1) * STAGE);
+      if (i + NS - 1 < nsteps) issue(kbeg + (i + NS - 1) * BK, st + nxt * STAGE);
       compute(st + cur * STAGE);
-      __syncthreads();
-      cur ^= 1;
+      dma_wait_barrier<NS, PER>(min(NS - 2, nsteps - 2 - i));
+      cur = cur + 1 == NS ? 0 : cur + 1;
+      nxt = nxt + 1 == NS ? 0 : nxt + 1;
     }
   } else {
     if (nsteps > 0) {

@@ -8,6 +8,8 @@ M/N-contiguous operands through the gfx950 transposing LDS read.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -38,28 +40,87 @@ def gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False, splits=1
                           pro_shift, pro_on_a, stats)
 
 
+class LinearTuner:
+    """First sight of a Linear GEMM problem: time every (tile, split-K) candidate with HIP events
+    on scratch outputs and keep the fastest (``LWAAAI_GEMM_TUNE=0``: the 128x128 heuristic). The
+    classifier GEMMs are skinny in M (batch 256-512) and span K = 1k-25k, so the right tile and
+    split count differ per layer and pass (``profiles/r2_linear_vs_blas*.log``)."""
+
+    TILES = (1, 2, 3, 4, 5, 6)
+    SPLITS = (1, 2, 4, 8, 16)
+
+    def __init__(self):
+        self.best = {}
+        self.enabled = os.environ.get("LWAAAI_GEMM_TUNE", "1") != "0"
+
+    def pick(self, key, tiles_of, K, run):
+        c = self.best.get(key)
+        if c is not None:
+            return c
+        default = (0, _splits(tiles_of(128, 128), K))
+        if not self.enabled or torch.cuda.is_current_stream_capturing():
+            self.best[key] = default
+            return default
+        times = []
+        for t in self.TILES:
+            for sp in self.SPLITS:
+                if sp > 1 and K // sp < 256:
+                    continue
+                run(t, sp)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(3):
+                    run(t, sp)
+                e.record()
+                e.synchronize()
+                times.append((s.elapsed_time(e), (t, sp)))
+        c = min(times, key=lambda v: v[0])[1]
+        self.best[key] = c
+        return c
+
+
+TUNER = LinearTuner()
+
+
+def _tiles(M: int, N: int):
+    return lambda bm, bn: -(-M // bm) * -(-N // bn)
+
+
+def _gemm_tuned(kind, A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False,
+                out_bf16=True, out=None, accumulate=False):
+    """One Linear GEMM on the tuned (tile, splits); ``out``/``accumulate``: fp32 C += result
+    (the tuner times on scratch outputs, never on ``out``)."""
+    lib = load()
+
+    def run(t, sp, dst=None, acc=False):
+        return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias, relu, sp, out_bf16, t, None,
+                           None, True, False, dst, None, acc, 0, None)[0]
+    key = (kind, M, N, K, bias is not None, relu, out_bf16)
+    t, sp = TUNER.pick(key, _tiles(M, N), K, run)
+    return run(t, sp, out, accumulate)
+
+
 def linear_fwd(x2, w, bias=None, relu=False, out_fp32=False):
     """x2 [M,K] bf16, w [N,K] bf16 -> [M,N] bf16 (or fp32) = relu?(x2·wᵀ + bias)."""
     M, K = x2.shape
     N = w.shape[0]
-    tiles = -(-M // 128) * -(-N // 128)
-    return gemm(x2, K, True, w, K, True, M, N, K, bias, relu, _splits(tiles, K), not out_fp32)
+    return _gemm_tuned("fwd", x2, K, True, w, K, True, M, N, K, bias, relu, not out_fp32)
 
 
 def linear_dgrad(dy2, w):
     """dy2 [M,N], w [N,K] -> dx [M,K] bf16 = dy2·w."""
     M, N = dy2.shape
     K = w.shape[1]
-    tiles = -(-M // 128) * -(-K // 128)
-    return gemm(dy2, N, True, w, K, False, M, K, N, None, False, _splits(tiles, N), True)
+    return _gemm_tuned("dgrad", dy2, N, True, w, K, False, M, K, N)
 
 
-def linear_wgrad(dy2, x2):
-    """dy2 [M,N], x2 [M,K] -> dW [N,K] fp32 = dy2ᵀ·x2 (reduction over the batch, split-K)."""
+def linear_wgrad(dy2, x2, out=None):
+    """dy2 [M,N], x2 [M,K] -> dW [N,K] fp32 = dy2ᵀ·x2 (reduction over the batch, split-K);
+    ``out``: accumulate into that fp32 [N,K] buffer (the gradient arena) instead."""
     M, N = dy2.shape
     K = x2.shape[1]
-    tiles = -(-N // 128) * -(-K // 128)
-    return gemm(dy2, N, False, x2, K, False, N, K, M, None, False, _splits(tiles, M), False)
+    return _gemm_tuned("wgrad", dy2, N, False, x2, K, False, N, K, M, out_bf16=False, out=out,
+                       accumulate=out is not None)
 
 
 def _pad_rows(w: torch.Tensor, n: int) -> torch.Tensor:
@@ -113,11 +174,7 @@ class _LinearFn(torch.autograd.Function):
             g = p.grad if getattr(p, "_lw_grad_ready", None) is not None else None
             if g is not None and Np == N and g.dtype == torch.float32 and g.is_contiguous():
                 # fp32 weight gradient accumulated straight into the gradient arena (split-K)
-                M, K = x2.shape
-                tiles = -(-N // 128) * -(-K // 128)
-                load().gemm_ex(dy2, N, False, x2, K, False, N, K, M, None, False,
-                               _splits(tiles, M), False, 0, None, None, True, False, g, None,
-                               True, 0, None)
+                linear_wgrad(dy2, x2, out=g)
                 p._lw_grad_ready(p)
             else:
                 dw = linear_wgrad(dy2, x2)[:N].to(p.dtype)

@@ -353,6 +353,66 @@ Tensor gap_fwd(Tensor x) {
   return y;
 }
 
+// fused cross-entropy (nn.hip): logits fp32 [B, C] contiguous, target int64 [B] ->
+// (loss rows [B], correct [B, 2] (top-1, top-5), grad [B, C] = (softmax - onehot)·gscale or empty)
+std::tuple<Tensor, Tensor, Tensor> xent(Tensor logits, Tensor target, double gscale,
+                                        int64_t ignore_index, bool want_grad) {
+  const c10::DeviceGuard guard(logits.device());
+  TORCH_CHECK(logits.is_cuda(), "logits must be a GPU tensor");
+  check_dtype(logits, at::kFloat, "logits");
+  check_cuda(target, "target");
+  check_dtype(target, at::kLong, "target");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "logits must be contiguous [B, C]");
+  const int64_t B = logits.size(0), C = logits.size(1);
+  TORCH_CHECK(target.dim() == 1 && target.size(0) == B && target.is_contiguous(), "target [B]");
+  TORCH_CHECK(B < (1LL << 30) && C > 0 && B * C < (1LL << 40), "xent: size");
+  Tensor loss = at::empty({B}, logits.options());
+  Tensor corr = at::empty({B, 2}, logits.options());
+  Tensor grad = want_grad ? at::empty({B, C}, logits.options()) : at::empty({0}, logits.options());
+  if (B > 0)
+    lw::xent(ptr<float>(logits), ptr<int64_t>(target), (int)B, (int)C, (float)gscale,
+             (int)ignore_index, ptr<float>(loss), ptr<float>(corr),
+             want_grad ? ptr<float>(grad) : nullptr, cur_stream());
+  launched("xent");
+  return {loss, corr, grad};
+}
+
+// bias + ReLU epilogue backward (nn.hip): dy, y bf16 rows [M, C] (channels_last NCHW or 2-D) ->
+// (dy·[y > 0] (or dy itself without y), db fp32 [C]; accumulated into db_out when given)
+std::tuple<Tensor, Tensor> relu_bias_bwd(Tensor dy, c10::optional<Tensor> y,
+                                         c10::optional<Tensor> db_out) {
+  const c10::DeviceGuard guard(dy.device());
+  TORCH_CHECK(dy.is_cuda(), "dy must be a GPU tensor");
+  check_dtype(dy, at::kBFloat16, "dy");
+  const bool cl = dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(cl || (dy.dim() == 2 && dy.is_contiguous()), "dy: channels_last NCHW or [M, C]");
+  const int64_t C = dy.size(1), M = dy.numel() / std::max<int64_t>(C, 1);
+  TORCH_CHECK(C % 8 == 0 && C > 0 && C <= 2048 && M < (1LL << 40), "relu_bias_bwd: C % 8, <= 2048");
+  check_aligned16(dy.data_ptr(), "dy");
+  const bool relu = y.has_value() && y->defined();
+  if (relu) {
+    check_dtype(*y, at::kBFloat16, "y");
+    TORCH_CHECK(y->sizes() == dy.sizes() && y->strides() == dy.strides(), "y must match dy");
+    check_aligned16(y->data_ptr(), "y");
+  }
+  Tensor dym = relu ? at::empty_like(dy) : dy;
+  Tensor db;
+  const bool acc = db_out.has_value() && db_out->defined();
+  if (acc) {
+    db = *db_out;
+    check_dtype(db, at::kFloat, "db_out");
+    TORCH_CHECK(db.numel() == C && db.is_contiguous(), "db_out [C]");
+  } else {
+    db = at::empty({C}, dy.options().dtype(at::kFloat));
+  }
+  Tensor partial = at::empty({(int64_t)lw::relu_bias_bwd_blocks(M) * C}, db.options());
+  lw::relu_bias_bwd(ptr<uint16_t>(dy), relu ? ptr<uint16_t>(*y) : nullptr,
+                    relu ? ptr<uint16_t>(dym) : nullptr, ptr<float>(partial), ptr<float>(db), M,
+                    (int)C, acc, cur_stream());
+  launched("relu_bias_bwd");
+  return {dym, db};
+}
+
 // dy [N, C] bf16/fp32 -> channels_last bf16 [N, C, H, W] filled with dy / (H*W)
 Tensor gap_bwd(Tensor dy, int64_t H, int64_t W) {
   const c10::DeviceGuard guard(dy.device());
@@ -719,7 +779,8 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
                                    c10::optional<Tensor> addend, c10::optional<Tensor> bst_x,
                                    c10::optional<Tensor> bst_mean,
                                    c10::optional<Tensor> bst_scale_shift,
-                                   c10::optional<Tensor> bst_bits) {
+                                   c10::optional<Tensor> bst_bits, c10::optional<Tensor> bias,
+                                   bool relu) {
   const c10::DeviceGuard guard(G.device());
   TORCH_CHECK(G.is_cuda() && Op.is_cuda(), "conv needs GPU tensors");
   check_dtype(G, at::kBFloat16, "gathered tensor");
@@ -898,6 +959,14 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
     TORCH_CHECK(!g.bst_x, "backward statistics need want_stats");
     stats = at::empty({0}, G.options().dtype(at::kFloat));
   }
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(ga && out_bf16 && !g.bst_x, "conv bias epilogue: forward convs only");
+    check_dtype(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->is_cuda() && bias->numel() >= N && bias->is_contiguous(), "bias [N] fp32");
+    g.bias = ptr<float>(*bias);
+  }
+  TORCH_CHECK(!relu || (ga && out_bf16 && !g.bst_x), "conv ReLU epilogue: forward convs only");
+  g.relu = relu;
   lw::conv_gemm(g, h, (int)mode, cur_stream());
   launched("conv_gemm");
   return {C, stats};
@@ -990,6 +1059,47 @@ std::tuple<Tensor, Tensor> stem_pool_fwd(Tensor x, Tensor scale_shift, int64_t k
   lw::stem_pool_fwd(a, cur_stream());
   launched("stem_pool_fwd");
   return {out, idx};
+}
+
+// max-pool of a post-ReLU bf16 map (no BN): [scale 1][shift 0][A 1][B 0][C 0] constant vectors
+static Tensor relu_pool_consts(const Tensor& x, int64_t C) {
+  Tensor c = at::zeros({5 * C}, x.options().dtype(at::kFloat));
+  c.narrow(0, 0, C).fill_(1.0);
+  c.narrow(0, 2 * C, C).fill_(1.0);
+  return c;
+}
+
+std::tuple<Tensor, Tensor> relu_pool_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
+  const c10::DeviceGuard guard(x.device());
+  lw::StemArgs a{};
+  stem_geom(x, k, s, p, a);
+  Tensor c = relu_pool_consts(x, a.C);
+  return stem_pool_fwd(x, c.narrow(0, 0, 2 * a.C), k, s, p);
+}
+
+Tensor relu_pool_bwd(Tensor dp, Tensor idx, Tensor x, int64_t k, int64_t s, int64_t p) {
+  const c10::DeviceGuard guard(x.device());
+  lw::StemArgs a{};
+  stem_geom(x, k, s, p, a);
+  check_dtype(dp, at::kBFloat16, "dp");
+  TORCH_CHECK(dp.is_contiguous(at::MemoryFormat::ChannelsLast) && dp.size(2) == a.Ho &&
+              dp.size(3) == a.Wo && dp.size(1) == a.C && dp.size(0) == a.N, "dp shape/layout");
+  TORCH_CHECK(idx.numel() == dp.numel() && idx.scalar_type() == at::kByte, "idx");
+  Tensor c = relu_pool_consts(x, a.C);
+  Tensor dx = at::empty_like(x);
+  a.x = x.data_ptr();
+  a.dp = dp.data_ptr();
+  a.idx = ptr<uint8_t>(idx);
+  a.dx = dx.data_ptr();
+  a.scale = ptr<float>(c);
+  a.shift = a.scale + a.C;
+  a.mean = a.shift;                 // unused by the apply pass
+  a.A = ptr<float>(c) + 2 * a.C;
+  a.B = ptr<float>(c) + 3 * a.C;
+  a.Cc = ptr<float>(c) + 4 * a.C;
+  lw::relu_pool_bwd(a, cur_stream());
+  launched("relu_pool_bwd");
+  return dx;
 }
 
 std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x,
@@ -1122,6 +1232,9 @@ TORCH_LIBRARY(lwaaai, m) {
       "int nesterov, int first_step, float grad_scale) -> ()");
   m.def("normalize_u8(Tensor input, Tensor(a!) out, float[] mean, float[] std) -> ()");
   m.def("gap_fwd(Tensor x) -> Tensor");
+  m.def("relu_bias_bwd(Tensor dy, Tensor? y, Tensor(a!)? db_out) -> (Tensor, Tensor)");
+  m.def("xent(Tensor logits, Tensor target, float gscale, int ignore_index, bool want_grad) "
+        "-> (Tensor, Tensor, Tensor)");
   m.def("gap_bwd(Tensor dy, int H, int W) -> Tensor");
   m.def(
       "bn_fwd(Tensor x, Tensor? res, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
@@ -1148,13 +1261,15 @@ TORCH_LIBRARY(lwaaai, m) {
       "bool out_bf16, Tensor? pro_scale, Tensor? pro_shift, bool want_stats, Tensor(a!)? out, "
       "bool accumulate, int ldc, bool b_kcontig, int ldb, Tensor? addend=None, "
       "Tensor? bst_x=None, Tensor? bst_mean=None, Tensor? bst_scale_shift=None, "
-      "Tensor? bst_bits=None) -> (Tensor, Tensor)");
+      "Tensor? bst_bits=None, Tensor? bias=None, bool relu=False) -> (Tensor, Tensor)");
   m.def(
       "bn_stats(Tensor x, Tensor? stats, Tensor? weight, Tensor? bias, Tensor(a!)? running_mean, "
       "Tensor(b!)? running_var, float momentum, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("bn_apply(Tensor x, Tensor scale_shift, Tensor? res, Tensor? res_scale_shift, bool relu, "
         "Tensor(a!)? bits_out=None) -> Tensor");
   m.def("stem_pool_fwd(Tensor x, Tensor scale_shift, int k, int s, int p) -> (Tensor, Tensor)");
+  m.def("relu_pool_fwd(Tensor x, int k, int s, int p) -> (Tensor, Tensor)");
+  m.def("relu_pool_bwd(Tensor dp, Tensor idx, Tensor x, int k, int s, int p) -> Tensor");
   m.def(
       "stem_pool_bwd(Tensor dp, Tensor idx, Tensor x, Tensor scale_shift, Tensor? weight, "
       "Tensor mean, Tensor invstd, int k, int s, int p, Tensor(a!)? dgamma_out=None, "
@@ -1174,6 +1289,8 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("sgd_step", &sgd_step);
   m.impl("normalize_u8", &normalize_u8);
   m.impl("gap_fwd", &gap_fwd);
+  m.impl("relu_bias_bwd", &relu_bias_bwd);
+  m.impl("xent", &xent);
   m.impl("gap_bwd", &gap_bwd);
   m.impl("bn_fwd", &bn_fwd);
   m.impl("bn_bwd", &bn_bwd);
@@ -1183,5 +1300,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("bn_stats", &bn_stats);
   m.impl("bn_apply", &bn_apply);
   m.impl("stem_pool_fwd", &stem_pool_fwd);
+  m.impl("relu_pool_fwd", &relu_pool_fwd);
+  m.impl("relu_pool_bwd", &relu_pool_bwd);
   m.impl("stem_pool_bwd", &stem_pool_bwd);
 }

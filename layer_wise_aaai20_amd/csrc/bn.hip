@@ -873,6 +873,34 @@ void stem_pool_fwd(const StemArgs& a, hipStream_t st) {
                      static_cast<uint16_t*>(a.out), a.idx, g);
 }
 
+// Max-pool of a post-ReLU map without a BatchNorm (VGG / AlexNet conv+ReLU -> MaxPool2d): the
+// forward is k_stem_pool_fwd with scale 1 / shift 0 (relu(v) == v there), the backward only the
+// apply pass with (A, B, C) = (1, 0, 0): dx = the routed pooled gradient masked by [x > 0], i.e.
+// the max-pool AND the preceding ReLU backward in one kernel. a.A / a.B / a.Cc / a.scale / a.shift
+// must hold those constants (the binding fills them).
+void relu_pool_bwd(const StemArgs& a, hipStream_t st) {
+  const PoolGeom g{a.N, a.H, a.W, a.C, a.Ho, a.Wo, a.k, a.s, a.p};
+  const auto* dp = static_cast<const uint16_t*>(a.dp);
+  const auto* x = static_cast<const uint16_t*>(a.x);
+  if (a.k == 3 && a.s == 2 && a.p == 1 && a.H == 2 * a.Ho && a.W == 2 * a.Wo) {
+    const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
+    int64_t rpb;
+    int nb;
+    reduce_geometry(P, a.C, rpb, nb);
+    hipLaunchKernelGGL((k_stem_pool_bwd_s2<1>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
+                       a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
+                       (float*)nullptr, g, rpb);
+    return;
+  }
+  const int64_t M = (int64_t)a.N * a.H * a.W;
+  int64_t rpb;
+  int nb;
+  reduce_geometry(M, a.C, rpb, nb);
+  hipLaunchKernelGGL((k_stem_pool_bwd<1>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
+                     a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
+                     (float*)nullptr, g, rpb);
+}
+
 void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
   const PoolGeom g{a.N, a.H, a.W, a.C, a.Ho, a.Wo, a.k, a.s, a.p};
   const int64_t M = (int64_t)a.N * a.H * a.W;

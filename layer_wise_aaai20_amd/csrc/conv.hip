@@ -116,8 +116,9 @@ void conv_gemm(const GemmArgs& g, const ConvGeomHost& cvh, int mode, hipStream_t
   const int tiles = ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn);
   const int epi = zs > 1 ? EPI_PARTIAL
                           : (g.stats ? (g.bst_x ? EPI_BSTATS : EPI_STATS) : EPI_STORE);
-  GemmK k{g.A, g.B, g.C, g.partial, g.stats, nullptr, g.pro_scale, g.pro_shift, g.addend, nullptr,
-          g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, 0, g.out_bf16 ? 1 : 0, g.accumulate ? 1 : 0};
+  GemmK k{g.A, g.B, g.C, g.partial, g.stats, zs > 1 ? nullptr : g.bias, g.pro_scale, g.pro_shift,
+          g.addend, nullptr, g.lda, g.ldb, g.ldc, g.M, g.N, g.K, kps, zs > 1 ? 0 : (g.relu ? 1 : 0),
+          g.out_bf16 ? 1 : 0, g.accumulate ? 1 : 0};
   k.cv = to_device(cvh);
   k.a_bytes = g.a_bytes;
   k.b_bytes = g.b_bytes;

@@ -169,6 +169,7 @@ struct StemArgs {
 };
 void stem_pool_fwd(const StemArgs& a, hipStream_t st);
 void stem_pool_bwd(const StemArgs& a, hipStream_t st);
+void relu_pool_bwd(const StemArgs& a, hipStream_t st);   // pool + ReLU backward, no BN
 
 // bf16 MFMA GEMM with fused epilogue (gemm.hip)
 struct GemmArgs {
@@ -246,6 +247,16 @@ void launch_invalid_config_for_test(hipStream_t st);
 // from [N, C] bf16/fp32 to the channels_last [N, HW, C] bf16 gradient (nn.hip)
 void gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
 void gap_bwd(const void* dy, bool dy_f32, uint16_t* dx, int N, int HW, int C, hipStream_t st);
+// fused softmax cross-entropy (nn.hip): per-row loss, top-1/top-5 correctness [B][2] and, when
+// `grad` is non-null, the logit gradient (softmax - onehot)·gscale (0 for ignored targets)
+void xent(const float* logits, const int64_t* target, int B, int C, float gscale,
+          int ignore_index, float* loss, float* corr, float* grad, hipStream_t st);
+// backward of a fused bias + ReLU epilogue (nn.hip): dym = dy·[y > 0] (y null: no ReLU, dym
+// unused) and db (+)= Σ_rows dym; rows [M][C] bf16, C % 8 == 0, C <= 2048; partial holds
+// relu_bias_bwd_blocks(M) * C floats
+int relu_bias_bwd_blocks(int64_t M);
+void relu_bias_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dym, float* partial,
+                   float* db, int64_t M, int C, bool accumulate, hipStream_t st);
 void normalize_u8_c4(const uint8_t* in, uint16_t* out, int64_t npix, const float mean[3],
                      const float stdv[3], hipStream_t st);
 

@@ -217,3 +217,195 @@ void gap_bwd(const void* dy, bool dy_f32, uint16_t* dx, int N, int HW, int C, hi
 }
 
 }  // namespace lw
+
+namespace lw {
+
+// ---- fused softmax cross-entropy + top-1/top-5 correctness + logit gradient.
+// The reference computes the loss (nn.CrossEntropyLoss: log_softmax + nll), its backward
+// (softmax - onehot), and the accuracy (output.topk(5) + eq, IMAGENET/training/
+// train_imagenet_nv.py:679-689) as separate passes over the [B, C] logits. Here one wave owns one
+// row: a max pass, a Σexp pass with the target logit and its rank (# logits strictly greater —
+// top-k correct iff rank < k), then the gradient row (softmax - onehot)·gscale, all from the fp32
+// logits held in registers (C <= 64*XR) or re-read from L2 (larger C). Deterministic: fixed
+// butterfly order per row.
+constexpr int XR = 32;                 // register-resident elements per lane (C <= 2048)
+
+__device__ __forceinline__ float xent_wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float xent_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void k_xent(const float* __restrict__ logits,
+                                              const int64_t* __restrict__ target, int B, int C,
+                                              float gscale, int ignore_index,
+                                              float* __restrict__ loss, float* __restrict__ corr,
+                                              float* __restrict__ grad) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+  if (row >= B) return;
+  const float* x = logits + (int64_t)row * C;
+  const int64_t t64 = target[row];
+  const bool ign = t64 == ignore_index;
+  const int t = (ign || t64 < 0 || t64 >= C) ? -1 : (int)t64;
+  const bool reg = C <= 64 * XR;
+  float v[XR];
+  float m = -__builtin_huge_valf();
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int c = l + 64 * i;
+    v[i] = (reg && c < C) ? x[c] : -__builtin_huge_valf();
+    m = fmaxf(m, v[i]);
+  }
+  if (!reg)
+    for (int c = l; c < C; c += 64) m = fmaxf(m, x[c]);
+  m = xent_wave_max(m);
+  const float xt = t >= 0 ? x[t] : 0.f;
+  float s = 0.f, gt = 0.f;
+  if (reg) {
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int c = l + 64 * i;
+      if (c < C) {
+        s += __expf(v[i] - m);
+        gt += v[i] > xt ? 1.f : 0.f;
+      }
+    }
+  } else {
+    for (int c = l; c < C; c += 64) {
+      const float a = x[c];
+      s += __expf(a - m);
+      gt += a > xt ? 1.f : 0.f;
+    }
+  }
+  s = xent_wave_sum(s);
+  gt = xent_wave_sum(gt);
+  if (l == 0) {
+    loss[row] = t >= 0 ? (__logf(s) + m - xt) : 0.f;
+    corr[2 * row] = (t >= 0 && gt < 1.f) ? 1.f : 0.f;
+    corr[2 * row + 1] = (t >= 0 && gt < 5.f) ? 1.f : 0.f;
+  }
+  if (!grad) return;
+  float* g = grad + (int64_t)row * C;
+  const float inv = 1.f / s;
+  const float gs = t >= 0 ? gscale : 0.f;
+  if (reg) {
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int c = l + 64 * i;
+      if (c < C) g[c] = (__expf(v[i] - m) * inv - (c == t ? 1.f : 0.f)) * gs;
+    }
+  } else {
+    for (int c = l; c < C; c += 64) g[c] = (__expf(x[c] - m) * inv - (c == t ? 1.f : 0.f)) * gs;
+  }
+}
+
+void xent(const float* logits, const int64_t* target, int B, int C, float gscale,
+          int ignore_index, float* loss, float* corr, float* grad, hipStream_t st) {
+  hipLaunchKernelGGL(k_xent, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, logits, target, B,
+                     C, gscale, ignore_index, loss, corr, grad);
+}
+
+}  // namespace lw
+
+namespace lw {
+
+// ---- backward of a conv/linear epilogue's bias + ReLU (VGG / AlexNet conv -> ReLU,
+// CIFAR10/vgg16.py:76, CIFAR10/alexnet.py:15-25): dym = dy·[y > 0] (bf16 NHWC rows [M][C]) and the
+// bias gradient Σ_rows dym, in one pass over dy / y (torch: threshold_backward + a reduce kernel).
+// Thread (r, cg) owns 8 channels; per-block column sums fold through LDS in row order into
+// partial[block][C]; k_fold_rows adds the blocks in order (deterministic).
+template <bool RELU>
+__global__ __launch_bounds__(256) void k_relu_bias_bwd(const uint16_t* __restrict__ dy,
+                                                       const uint16_t* __restrict__ y,
+                                                       uint16_t* __restrict__ dym,
+                                                       float* __restrict__ partial, int64_t M,
+                                                       int C, int64_t rows_per_block) {
+  __shared__ float sa[256 * 8];
+  const int G = C / 8, R = 256 / G;
+  const int cg = threadIdx.x % G, r = threadIdx.x / G;
+  const bool active = r < R;
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(r0 + rows_per_block, M);
+  if (active) {
+    for (int64_t row = r0 + r; row < r1; row += R) {
+      const int64_t o = row * C + cg * 8;
+      uint4 d = *reinterpret_cast<const uint4*>(dy + o);
+      if (RELU) {
+        const uint4 v = *reinterpret_cast<const uint4*>(y + o);
+        const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+        uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // bf16 > 0: sign bit clear and not +0
+          const uint32_t lo = ((vw[k] & 0x8000u) == 0u && (vw[k] & 0x7fffu) != 0u) ? 0xffffu : 0u;
+          const uint32_t hi = ((vw[k] & 0x80000000u) == 0u && (vw[k] & 0x7fff0000u) != 0u)
+                                  ? 0xffff0000u : 0u;
+          dw[k] &= lo | hi;
+        }
+        d = make_uint4(dw[0], dw[1], dw[2], dw[3]);
+        *reinterpret_cast<uint4*>(dym + o) = d;
+      }
+      const uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[2 * k] += __uint_as_float(w[k] << 16);
+        a[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sa[r * C + cg * 8 + j] = a[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int q = 0; q < R; ++q) s += sa[q * C + c];
+    partial[(int64_t)blockIdx.x * C + c] = s;
+  }
+}
+
+// partial [nb][C] -> out[C]: a block folds 64 consecutive channels with 4 row lanes (coalesced
+// 256-byte row segments), the lanes added in lane order (deterministic)
+__global__ __launch_bounds__(256) void k_fold_rows(const float* __restrict__ partial, int nb,
+                                                   int C, float* __restrict__ out, int accumulate) {
+  __shared__ float red[256];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < C)
+    for (int b = q; b < nb; b += 4) s += partial[(int64_t)b * C + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (q != 0 || c >= C) return;
+  s = ((red[cl] + red[64 + cl]) + red[128 + cl]) + red[192 + cl];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+int relu_bias_bwd_blocks(int64_t M) {
+  const int64_t nb = (M + 511) / 512;
+  return (int)(nb < 512 ? (nb < 1 ? 1 : nb) : 512);
+}
+
+void relu_bias_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dym, float* partial,
+                   float* db, int64_t M, int C, bool accumulate, hipStream_t st) {
+  const int nb = relu_bias_bwd_blocks(M);
+  const int64_t rpb = (M + nb - 1) / nb;
+  if (y)
+    hipLaunchKernelGGL(k_relu_bias_bwd<true>, dim3(nb), dim3(256), 0, st, dy, y, dym, partial, M,
+                       C, rpb);
+  else
+    hipLaunchKernelGGL(k_relu_bias_bwd<false>, dim3(nb), dim3(256), 0, st, dy, y, dym, partial, M,
+                       C, rpb);
+  if (db)
+    hipLaunchKernelGGL(k_fold_rows, dim3((C + 63) / 64), dim3(256), 0, st, partial, nb, C, db,
+                       accumulate ? 1 : 0);
+}
+
+}  // namespace lw

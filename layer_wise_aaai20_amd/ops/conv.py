@@ -151,9 +151,10 @@ def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int) -> Tuple[torch
 
 # ----------------------------------------------------------------------------- the three passes
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=False,
-             wpack=None):
+             wpack=None, bias=None, relu=False):
     """y = conv2d(x, w) as bf16 channels_last [N, Co, Ho, Wo]; optionally the input BN-apply+ReLU
-    ``pro = (scale, shift)`` (fp32 [C]) and the per-M-tile column statistics of y."""
+    ``pro = (scale, shift)`` (fp32 [C]), the per-M-tile column statistics of y, and an fp32
+    ``bias`` [Co] / ReLU applied in the epilogue before the bf16 rounding."""
     lib = load()
     sh, sw = _pair(stride)
     ph, pw = _pair(padding)
@@ -170,10 +171,13 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
     ps, pt = (pro[0], pro[1]) if pro is not None else (None, None)
     M = Nb * Ho * Wo
 
+    bf = bias.float().contiguous() if bias is not None else None
+
     def run(tile):
         return lib.conv_ex(xin, op, mode, geom, co, tile, 1, True, ps, pt, stats, None, False, 0,
-                           True, K)
-    key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats)
+                           True, K, bias=bf, relu=bool(relu))
+    key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats,
+           bias is not None, bool(relu))
     tile = TUNER.pick(key, run, ROW_TILES, _row_default(M, co))
     y, st = run(tile)
     return y.view(Nb, Ho, Wo, co).permute(0, 3, 1, 2), st
@@ -303,23 +307,38 @@ def _arena_view(p: torch.Tensor):
 
 
 class _ConvFn(torch.autograd.Function):
+    """conv2d (+ bias) (+ ReLU) on the implicit-GEMM kernels. Bias and ReLU run in the forward
+    epilogue; backward masks dy by the saved output and reduces the bias gradient in one pass
+    (``csrc/nn.hip`` k_relu_bias_bwd) before the data / weight gradient convs."""
+
     @staticmethod
-    def forward(ctx, x, weight, stride, padding):
+    def forward(ctx, x, weight, bias, stride, padding, relu):
         from .block import _bf16_weight
         wb = _bf16_weight(weight)
-        y, _ = conv_fwd(x, wb, stride, padding)
+        y, _ = conv_fwd(x, wb, stride, padding, bias=bias, relu=relu)
         xs = x.to(BF16).contiguous(memory_format=CL) if x.shape[1] % 8 == 0 else x
-        ctx.save_for_backward(xs, wb)
+        ctx.save_for_backward(xs, wb, y if relu else None)
         ctx.geom = (stride, padding, tuple(x.shape[2:]), x.dtype)
         ctx.weight = weight
+        ctx.bias = bias
+        ctx.relu = relu
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xs, wb = ctx.saved_tensors
+        xs, wb, y = ctx.saved_tensors
         stride, padding, hw, xdtype = ctx.geom
-        w = ctx.weight
-        dx = dw = None
+        w, b = ctx.weight, ctx.bias
+        dx = dw = db = None
+        dy = dy.to(BF16).contiguous(memory_format=CL)
+        if ctx.relu or (b is not None and ctx.needs_input_grad[2]):
+            if dy.shape[1] % 8 == 0 and dy.shape[1] <= 2048:
+                dy, db = load().relu_bias_bwd(dy, y if ctx.relu else None, None)
+            else:
+                if ctx.relu:
+                    dy = dy * (y > 0)
+                db = dy.float().sum((0, 2, 3))
+            db = db.to(b.dtype) if b is not None and ctx.needs_input_grad[2] else None
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad(dy, wb, hw, stride, padding).to(xdtype)
         if ctx.needs_input_grad[1]:
@@ -331,16 +350,15 @@ class _ConvFn(torch.autograd.Function):
                 dw = conv_wgrad(dy, xs, tuple(w.shape), stride, padding).to(w.dtype)
                 dw = dw.contiguous(memory_format=CL) if w.is_contiguous(memory_format=CL) \
                     else dw.contiguous()
-        return dx, dw, None, None
+        return dx, dw, db, None, None, None
 
 
-def mfma_conv2d(x, weight, bias=None, stride=1, padding=0):
-    """bf16 MFMA convolution; outside autocast an fp32 input gets an fp32 output back."""
-    y = _ConvFn.apply(x, weight, _pair(stride), _pair(padding))
+def mfma_conv2d(x, weight, bias=None, stride=1, padding=0, relu=False):
+    """bf16 MFMA convolution (+ bias, + ReLU in the epilogue); outside autocast an fp32 input
+    gets an fp32 output back."""
+    y = _ConvFn.apply(x, weight, bias, _pair(stride), _pair(padding), bool(relu))
     if x.dtype == torch.float32 and not torch.is_autocast_enabled():
         y = y.float()
-    if bias is not None:
-        y = y + bias.to(y.dtype).view(1, -1, 1, 1)
     return y
 
 
@@ -351,8 +369,10 @@ class MFMAConv2d(nn.Conv2d):
     def forward(self, x):
         if x.is_cuda and isinstance(self.padding, tuple) and self.padding_mode == "zeros" and \
                 supported(self.in_channels, self.out_channels, self.groups, self.dilation):
-            return mfma_conv2d(x, self.weight, self.bias, self.stride, self.padding)
-        return super().forward(x)
+            return mfma_conv2d(x, self.weight, self.bias, self.stride, self.padding,
+                               getattr(self, "fuse_relu", False))
+        y = super().forward(x)
+        return F.relu(y) if getattr(self, "fuse_relu", False) else y
 
 
 def to_mfma_conv(m: nn.Conv2d) -> nn.Conv2d:
@@ -361,9 +381,25 @@ def to_mfma_conv(m: nn.Conv2d) -> nn.Conv2d:
     return m
 
 
-def fuse_convs(model: nn.Module) -> nn.Module:
+def fuse_convs(model: nn.Module, relu: bool = True) -> nn.Module:
     """Switch every plain nn.Conv2d of ``model`` to :class:`MFMAConv2d` (in place; parameter and
-    buffer names are unchanged, so checkpoints stay compatible)."""
+    buffer names are unchanged, so checkpoints stay compatible). With ``relu``, a Conv2d directly
+    followed by a ReLU inside an nn.Sequential (VGG / AlexNet features) gets the ReLU in its
+    epilogue and the ReLU module becomes an Identity."""
+    if relu:
+        for mod in model.modules():
+            if isinstance(mod, nn.Sequential):
+                kids = list(mod._modules.items())
+                for i, (name, child) in enumerate(kids):
+                    if type(child) is nn.Conv2d and i + 1 < len(kids) and \
+                            isinstance(kids[i + 1][1], nn.ReLU):
+                        to_mfma_conv(child)
+                        child.fuse_relu = True
+                        mod._modules[kids[i + 1][0]] = nn.Identity()
+                        # a max-pool right after the ReLU: the ReLU-aware pool kernels
+                        if i + 2 < len(kids) and type(kids[i + 2][1]) is nn.MaxPool2d:
+                            from .nn import ReluMaxPool2d
+                            kids[i + 2][1].__class__ = ReluMaxPool2d
     for m in model.modules():
         if type(m) is nn.Conv2d:
             to_mfma_conv(m)

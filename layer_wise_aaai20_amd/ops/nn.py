@@ -120,7 +120,26 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
                                 relu=self.fuse_relu, residual=residual)
 
     def extra_repr(self):
-        return super().extra_repr() + (", fused_relu=True" if self.fuse_relu else "")
+        return super().extra_repr() + (", fused_relu=True" if self.fuse_relu else "") + \
+            (f", fused_pool={self.fuse_pool}" if getattr(self, "fuse_pool", None) else "")
+
+
+class FusedBNReluPool2d(FusedBatchNorm2d):
+    """BN → ReLU → max-pool of a CIFAR graph net (``CIFAR10/dawn.py:23-33``: conv_bn then
+    ``MaxPool2d(2)``) as ONE forward kernel after the statistics pass and one reduce + one apply
+    kernel backward — the ``csrc/bn.hip`` k_stem_pool_* kernels, whose window slot byte routes the
+    pooled gradient straight into the BN backward (neither the normalised activation nor the
+    un-pooled gradient is ever written). Same parameters / buffers / state_dict as the BN; eval
+    mode and unsupported inputs run BN+ReLU then ``F.max_pool2d``."""
+
+    def forward(self, x, residual=None):
+        k, s, p = self.fuse_pool
+        if (residual is None and self.training and self.track_running_stats and x.is_cuda and
+                x.dim() == 4 and x.dtype == torch.bfloat16 and x.size(1) % 8 == 0 and
+                x.size(1) <= MAX_BN_C and self.affine and _stem_fits(*x.shape, self.fuse_pool)):
+            return _StemPoolFn.apply(x, self.weight, self.bias, self, self.fuse_pool)
+        y = super().forward(x, residual)
+        return F.max_pool2d(y, k, s, p)
 
 
 def share_bn_counters(model: nn.Module) -> nn.Module:
@@ -276,6 +295,38 @@ def stem_conv_bn_relu_pool(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, pool: nn.MaxP
     return _StemConvPoolFn.apply(x, conv.weight, bn.weight, bn.bias, conv, bn, _pool_geom(pool))
 
 
+class _ReluPoolFn(torch.autograd.Function):
+    """Max-pool of a post-ReLU map (``csrc/bn.hip`` k_stem_pool_fwd with an identity affine, and
+    the apply pass of its backward): the backward routes the pooled gradient to the window's max
+    AND applies the preceding ReLU's mask in the same kernel."""
+
+    @staticmethod
+    def forward(ctx, x, geom):
+        out, idx = load().relu_pool_fwd(x, *geom)
+        ctx.save_for_backward(x, idx)
+        ctx.geom = geom
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, idx = ctx.saved_tensors
+        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        return load().relu_pool_bwd(dout, idx, x, *ctx.geom), None
+
+
+class ReluMaxPool2d(nn.MaxPool2d):
+    """``nn.MaxPool2d`` placed after a ReLU (``fuse_convs`` installs it behind a conv whose ReLU
+    runs in the epilogue): HIP kernels on CUDA bf16 channels_last maps, torch otherwise."""
+
+    def forward(self, x):
+        geom = _pool_geom(self)
+        if (geom is not None and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and
+                x.size(1) % 8 == 0 and x.size(1) <= MAX_BN_C and
+                x.is_contiguous(memory_format=torch.channels_last) and _stem_fits(*x.shape, geom)):
+            return _ReluPoolFn.apply(x, geom)
+        return super().forward(x)
+
+
 def _pool_geom(pool: nn.MaxPool2d):
     def one(v):
         return v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else None)
@@ -380,14 +431,18 @@ def fuse_resnet(model: nn.Module, block: bool = True, mfma: bool = True) -> nn.M
     return model
 
 
-def fuse_graph_network(net: nn.Module) -> nn.Module:
+def fuse_graph_network(net: nn.Module, pool: bool = True) -> nn.Module:
     """Fuse ``bn -> relu`` node pairs of a dict-graph :class:`~..models.graph.Network` (ResNet-9,
     graph AlexNet): the BN becomes a FusedBatchNorm2d(relu=True), the ReLU node an Identity.
-    Only pairs where the ReLU is the BN's sole consumer are fused."""
+    Only pairs where the ReLU is the BN's sole consumer are fused; with ``pool``, a max-pool that
+    is the ReLU's sole consumer is folded in too (:class:`FusedBNReluPool2d`)."""
     from ..models.graph import Identity
     graph = getattr(net, "graph", None)
     if graph is None:
         return net
+    for mod, _ in graph.values():          # the loss node on the fused cross-entropy kernel
+        if type(mod) is nn.CrossEntropyLoss:
+            mod.__class__ = FusedCrossEntropyLoss
     names = list(graph)
     consumers = {}
     for k, (_, ins) in graph.items():
@@ -407,4 +462,83 @@ def fuse_graph_network(net: nn.Module) -> nn.Module:
             ident = Identity()
             graph[r] = (ident, rins)
             net._modules[r] = ident
+            # BN+ReLU whose only consumer is a max-pool: the pool joins the BN kernel pair
+            pu = consumers.get(r, [])
+            if pool and len(pu) == 1:
+                pmod, pins = graph[pu[0]]
+                geom = _pool_geom(pmod) if isinstance(pmod, nn.MaxPool2d) else None
+                if geom is not None and pins == [r]:
+                    mod.__class__ = FusedBNReluPool2d
+                    mod.fuse_pool = geom
+                    pid = Identity()
+                    graph[pu[0]] = (pid, pins)
+                    net._modules[pu[0]] = pid
     return net
+
+
+# ----------------------------------------------------------------------------- fused loss
+class _XentFn(torch.autograd.Function):
+    """Softmax cross-entropy + top-1/top-5 correctness in one HIP kernel (``csrc/nn.hip`` k_xent):
+    the forward already writes the unscaled logit gradient (softmax - onehot); backward only
+    scales it by the incoming gradient / the valid-target count (device tensors: no host sync)."""
+
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index, reduction):
+        lg = logits.detach().float().contiguous()
+        rows, corr, grad = load().xent(lg, target.contiguous(), 1.0, int(ignore_index),
+                                       bool(logits.requires_grad))
+        ctx.reduction = reduction
+        ctx.dtype = logits.dtype
+        if reduction == "mean":
+            n = (target != ignore_index).sum().clamp_min(1).to(torch.float32)
+            loss = rows.sum() / n
+        elif reduction == "sum":
+            n = None
+            loss = rows.sum()
+        else:
+            n = None
+            loss = rows
+        ctx.save_for_backward(grad, n)
+        ctx.mark_non_differentiable(corr)
+        return loss, corr
+
+    @staticmethod
+    def backward(ctx, gl, _gc):
+        grad, n = ctx.saved_tensors
+        if ctx.reduction == "none":
+            g = grad * gl.view(-1, 1)
+        elif ctx.reduction == "mean":
+            g = grad * (gl / n)
+        else:
+            g = grad * gl
+        return g.to(ctx.dtype), None, None, None
+
+
+def fused_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100,
+                        reduction: str = "mean"):
+    """(loss, correct[B, 2]) — correct[:, 0] / [:, 1]: the target is the top-1 / within the
+    top-5 logits (strictly-greater rank < k). GPU fp32/bf16 [B, C] logits with int64 targets;
+    torch ops elsewhere."""
+    if logits.is_cuda and logits.dim() == 2 and target.dim() == 1 and \
+            target.dtype == torch.int64 and reduction in ("mean", "sum", "none"):
+        return _XentFn.apply(logits, target, ignore_index, reduction)
+    loss = F.cross_entropy(logits.float(), target, ignore_index=ignore_index, reduction=reduction)
+    k = min(5, logits.shape[1])
+    top = logits.topk(k, 1).indices
+    ok = top.eq(target.view(-1, 1))
+    corr = torch.stack([ok[:, 0].float(), ok.any(1).float()], 1)
+    return loss, corr
+
+
+class FusedCrossEntropyLoss(nn.CrossEntropyLoss):
+    """``nn.CrossEntropyLoss`` on the fused kernel (no class weights / label smoothing); the
+    per-sample top-1/top-5 correctness of the last call is kept in ``last_correct`` ([B, 2]) so a
+    training loop needs no separate ``topk`` pass."""
+
+    def forward(self, input, target):
+        if self.weight is None and self.label_smoothing == 0.0:
+            loss, corr = fused_cross_entropy(input, target, self.ignore_index, self.reduction)
+            self.last_correct = corr
+            return loss
+        self.last_correct = None
+        return super().forward(input, target)

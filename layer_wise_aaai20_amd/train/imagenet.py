@@ -47,7 +47,7 @@ class ImageNetTrainer:
         self.device = device
         self.dtype = dtype
         self.channels_last = channels_last
-        self.criterion = criterion or nn.CrossEntropyLoss()
+        self.criterion = criterion or lwnn.FusedCrossEntropyLoss()
         self.mean = torch.tensor(IMAGENET_MEAN, device=device, dtype=torch.float32)
         self.std = torch.tensor(IMAGENET_STD, device=device, dtype=torch.float32)
         self._last = None

@@ -367,7 +367,12 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
             loss.backward()
             sync(model)
             optimizer.step()
-        corr1, corr5 = correct(output.data, target, topk=(1, 5))
+        last = getattr(criterion, "last_correct", None)
+        if last is not None:          # top-1/top-5 from the fused loss kernel (no topk pass)
+            cs = last.sum(0)
+            corr1, corr5 = cs[0:1], cs[1:2]
+        else:
+            corr1, corr5 = correct(output.data, target, topk=(1, 5))
         metrics = torch.cat([torch.tensor([float(inp.size(0))], device=loss.device),
                              loss.detach().float().reshape(1) * inp.size(0), corr1, corr5])
         if args.distributed:
@@ -563,7 +568,7 @@ def main(argv=None):
     else:
         opt_params = _bn_groups(base_model, None, args.weight_decay) if args.no_bn_wd else \
             [p for p in model.parameters() if p.requires_grad]
-    criterion = nn.CrossEntropyLoss().to(device)
+    criterion = lwnn.FusedCrossEntropyLoss().to(device)
     if fast:
         pass
     elif args.momentum > 0:

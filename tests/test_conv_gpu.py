@@ -136,3 +136,69 @@ def test_mfma_conv2d_module_matches_torch():
     _close(xa.grad, xb.grad, 2e-2)
     _close(m.weight.grad, ref.weight.grad, 5e-3)
     _close(m.bias.grad, ref.bias.grad, 5e-3)
+
+
+@pytest.mark.parametrize("cin,cout,hw,relu", [(64, 128, 16, True), (128, 64, 8, True),
+                                              (3, 64, 32, True), (256, 256, 4, False)])
+def test_conv_bias_relu_epilogue_matches_torch(cin, cout, hw, relu):
+    """Conv2d + bias + ReLU with bias and ReLU in the MFMA epilogue and the fused
+    mask / bias-gradient backward kernel (the VGG / AlexNet features pattern)."""
+    torch.manual_seed(cin + cout)
+    ref = torch.nn.Conv2d(cin, cout, 3, padding=1, bias=True).cuda()
+    m = torch.nn.Conv2d(cin, cout, 3, padding=1, bias=True).cuda()
+    with torch.no_grad():
+        ref.bias.normal_(0, 0.5)
+        ref.weight.copy_(ref.weight.bfloat16().float())
+    m.load_state_dict(ref.state_dict())
+    CV.to_mfma_conv(m)
+    m.fuse_relu = relu
+    x = torch.randn(8, cin, hw, hw, device="cuda").bfloat16().float()
+    xa = x.clone().requires_grad_(cin % 8 == 0)     # (an image input needs no gradient)
+    xb = x.clone().requires_grad_(cin % 8 == 0)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(xa)
+    yr = ref(xb)
+    yr = F.relu(yr) if relu else yr
+    _close(y.float(), yr, 1e-2)
+    g = torch.randn_like(yr).bfloat16().float()
+    y.float().backward(g)
+    # the reference masks with the bf16-rounded output the fused backward sees
+    yr.backward(g * (y.detach().float() > 0).float() if relu else g)
+    _close(m.weight.grad, ref.weight.grad, 5e-3)
+    _close(m.bias.grad, ref.bias.grad, 5e-3)
+    if cin % 8 == 0:
+        _close(xa.grad, xb.grad, 2e-2)
+
+
+def test_fuse_convs_folds_sequential_relu():
+    from layer_wise_aaai20_amd.models.cifar import vgg16
+    net = CV.fuse_convs(vgg16())
+    convs = [m for m in net.modules() if isinstance(m, CV.MFMAConv2d)]
+    assert len(convs) == 13 and all(getattr(c, "fuse_relu", False) for c in convs)
+    assert not any(isinstance(m, torch.nn.ReLU) for m in net.features.modules())
+    from layer_wise_aaai20_amd.ops.nn import ReluMaxPool2d
+    assert sum(isinstance(m, ReluMaxPool2d) for m in net.features.modules()) == 5
+
+
+@pytest.mark.parametrize("shape,k,s,p", [((16, 64, 32, 32), 2, 2, 0), ((8, 512, 2, 2), 2, 2, 0),
+                                         ((4, 64, 56, 56), 3, 2, 1)])
+def test_relu_pool_matches_torch(shape, k, s, p):
+    """ReluMaxPool2d (pool + the preceding ReLU's backward mask in one kernel) vs torch."""
+    from layer_wise_aaai20_amd.ops.nn import ReluMaxPool2d
+    torch.manual_seed(shape[1])
+    a = F.relu(torch.randn(*shape, device="cuda")).bfloat16().contiguous(memory_format=CL)
+    pool = torch.nn.MaxPool2d(k, s, p)
+    pool.__class__ = ReluMaxPool2d
+    xa = a.clone().requires_grad_()
+    y = pool(xa)
+    xr = a.float().requires_grad_()
+    yr = F.max_pool2d(xr, k, s, p)
+    torch.testing.assert_close(y.float(), yr)
+    g = torch.randn_like(yr).bfloat16()
+    y.backward(g)
+    yr.backward(g.float())
+    # torch routes a window of zeros to its first zero; the fused kernel also applies the ReLU
+    # mask (x > 0), so compare on the pixels that are positive
+    m = a.float() > 0
+    torch.testing.assert_close(xa.grad.float() * m, xr.grad * m, atol=1e-2, rtol=1e-2)
+    assert float(xa.grad.float()[~m].abs().max()) == 0.0

@@ -105,3 +105,58 @@ def test_fused_resnet18_mfma_convs_close_to_torch():
     for (n, pr), pa, pb in zip(r.named_parameters(), a.parameters(), b.parameters()):
         ga, gb = _rel(pa.grad, pr.grad), _rel(pb.grad, pr.grad)
         assert gb < 2 * ga + 2e-2, (n, ga, gb)
+
+
+@pytest.mark.parametrize("shape,k", [((16, 128, 32, 32), 2), ((8, 256, 16, 16), 2),
+                                     ((8, 512, 8, 8), 2), ((4, 64, 16, 16), 4)])
+def test_bn_relu_pool_matches_torch(shape, k):
+    """FusedBNReluPool2d (the CIFAR conv_bn -> MaxPool2d fusion) vs fp32 torch BN+ReLU+pool:
+    output, input gradient, gamma/beta gradients and running statistics."""
+    from layer_wise_aaai20_amd.ops.nn import FusedBNReluPool2d, to_fused_bn
+    torch.manual_seed(1)
+    C = shape[1]
+    x = (torch.randn(*shape, device="cuda") * 1.5 + 0.3).bfloat16()
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_()
+    bn = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_()
+    ref = torch.nn.BatchNorm2d(C).cuda()
+    ref.load_state_dict(bn.state_dict())
+    to_fused_bn(bn, relu=True)
+    bn.__class__ = FusedBNReluPool2d
+    bn.fuse_pool = (k, k, 0)
+    y = bn(x)
+    xr = x.detach().float().requires_grad_()
+    a = F.relu(ref(xr))
+    # the fused kernel pools the bf16-rounded activation: round straight-through so that window
+    # ties (and their first-max routing) match
+    a = a + (a.detach().bfloat16().float() - a.detach())
+    yr = F.max_pool2d(a, k)
+    assert y.shape == yr.shape and y.dtype == torch.bfloat16
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    dy = torch.randn_like(yr).bfloat16()
+    y.backward(dy)
+    yr.backward(dy.float())
+    # a window whose two maxima differ only past bf16 precision in the two BN paths routes its
+    # gradient to a different pixel: allow a handful of such pixels, all others must match
+    err = (x.grad.float() - xr.grad).abs()
+    bad = err > 5e-2 + 5e-2 * xr.grad.abs()
+    assert bad.float().mean().item() < 2e-4, f"{int(bad.sum())} mismatched gradient elements"
+    for a_, b_ in ((bn.weight.grad, ref.weight.grad), (bn.bias.grad, ref.bias.grad)):
+        # (a misrouted tie moves one pixel's gradient between two pixels of a channel's sums)
+        assert (a_ - b_).abs().max().item() <= 2e-2 * b_.abs().max().item() + 1e-3
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-2, rtol=1e-2)
+
+
+def test_graph_fusion_folds_pools():
+    """fuse_graph_network folds every conv_bn -> MaxPool2d of ResNet-9 into the BN (and leaves
+    the final 4x4 pool after the residual add alone)."""
+    from layer_wise_aaai20_amd.models.cifar import resnet9
+    from layer_wise_aaai20_amd.models.graph import Network
+    from layer_wise_aaai20_amd.ops.nn import FusedBNReluPool2d, fuse_graph_network
+    net = fuse_graph_network(Network(resnet9()))
+    fused = [n for n, m in net.named_modules() if isinstance(m, FusedBNReluPool2d)]
+    assert sorted(fused) == ["layer1_bn", "layer2_bn", "layer3_bn"]
+    assert isinstance(net.pool, torch.nn.MaxPool2d)

@@ -73,6 +73,10 @@ def parse():
                     help="process-group backend (nccl = RCCL on ROCm)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="debug: every rank on cuda:0 (multi-rank plumbing on a 1-GPU box, gloo)")
+    ap.add_argument("--graph", default="on", choices=["on", "off"],
+                    help="on: after 3 eager warm-up steps capture the whole step (fwd, bwd, "
+                         "overlapped compression + collectives, SGD) as one HIP graph and "
+                         "replay it (train/imagenet.py ImageNetTrainer)")
     ap.add_argument("--miopen-find", type=int, default=1,
                     help="1: let MIOpen benchmark conv solvers once (cudnn.benchmark)")
     return ap.parse_args()
@@ -147,7 +151,7 @@ def main():
                        K=args.ratio, V=args.threshold, qstates=args.qstates,
                        error_feedback=args.ef, bucket_cap_mb=args.bucket_mb, dtype=args.dtype,
                        fused=not args.no_fused, momentum=0.9, weight_decay=1e-4, no_bn_wd=True,
-                       lr=0.1)
+                       lr=0.1, graph=args.graph == "on")
     B, S = args.batch, args.image_size
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -185,6 +189,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms = dt / args.steps * 1e3
+    graphed = tr.graph_replays >= args.steps
     # ---- outside the timed region: per-bucket compress / exchange / decode µs of one step,
     # and top-1 on held-out batches of the same synthetic distribution
     eng = tr.ddp.engine
@@ -218,6 +223,7 @@ def main():
         "top1_heldout_synthetic": round(top1, 3),
         "top1_note": (f"held-out batches of the class-conditional synthetic distribution after "
                       f"{args.warmup + args.steps + 1} training steps (chance = 0.1%)"),
+        "hip_graph": graphed,
         "comm": {"backend": dist.get_backend() if world > 1 else "none (1 rank)",
                  "world_size": dist.get_world_size() if world > 1 else 1,
                  "bucket_us": [{k: (round(v, 1) if isinstance(v, float) else v)

@@ -57,6 +57,10 @@ def tie_slack(m: int) -> int:
 class Codec:
     collective = "all_reduce"
     name = "codec"
+    # True when compress/decompress issue no host synchronisation and depend on nothing that
+    # changes from step to step on the host (e.g. a Philox step counter passed as a kernel
+    # argument): the whole training step can then be captured once as a HIP graph and replayed
+    graph_safe = False
 
     def __init__(self, plan: SegPlan, world: int, rank: int, seed: int = 0,
                  error_feedback: bool = False):
@@ -90,6 +94,7 @@ class Codec:
 class DenseCodec(Codec):
     """No compression: bucketed in-place all-reduce, then ``/ world_size`` (core.py:318-319)."""
     name = "dense"
+    graph_safe = True
 
     def compress(self, grad, ef, step):
         self.last_payload_bytes = grad.numel() * grad.element_size()
@@ -105,6 +110,10 @@ class TopkCodec(Codec):
     collective = "all_gather"
     name = "topk"
     km = KM_TOPK
+
+    @property
+    def graph_safe(self) -> bool:          # exact Top-K ignores the step; Random-K keys use it
+        return self.km == KM_TOPK and type(self) is TopkCodec
 
     def __init__(self, plan, world, rank, K: float, seed=0, error_feedback=False):
         super().__init__(plan, world, rank, seed, error_feedback)
@@ -613,6 +622,12 @@ class DenseWrap(Codec):
         super().__init__(inner.plan, inner.world, inner.rank, inner.seed, inner.error_feedback)
         self.inner = inner
         self.name = f"dense({inner.name})"
+
+    @property
+    def graph_safe(self) -> bool:
+        # the threshold methods' dense path is sync-free and step-invariant
+        # (tests/test_sync_free_gpu.py)
+        return isinstance(self.inner, ThresholdCodec) or bool(self.inner.graph_safe)
 
     def compress(self, grad, ef, step):
         if isinstance(self.inner, ThresholdCodec):

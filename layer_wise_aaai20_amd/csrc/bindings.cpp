@@ -280,7 +280,8 @@ void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor
 
 void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tensor segs,
               Tensor tasks, Tensor seg_wd, double lr, double momentum, double dampening,
-              int64_t nesterov, int64_t first_step, double grad_scale) {
+              int64_t nesterov, int64_t first_step, double grad_scale,
+              c10::optional<Tensor> hyper) {
   const c10::DeviceGuard guard(p.device());
   check_cuda(p, "p");
   check_cuda(g, "g");
@@ -306,6 +307,12 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tens
   a.grad_scale = (float)grad_scale;
   a.nesterov = (int)nesterov;
   a.first_step = (int)first_step;
+  if (hyper.has_value() && hyper->defined()) {
+    check_cuda(*hyper, "hyper");
+    TORCH_CHECK(hyper->scalar_type() == at::kFloat && hyper->numel() >= 2 &&
+                    hyper->is_contiguous(), "hyper must be a contiguous float32 [lr, grad_scale]");
+    a.hyper = hyper->data_ptr<float>();
+  }
   lw::sgd_step(a, cur_stream());
   launched("sgd_step");
 }
@@ -1229,7 +1236,7 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
-      "int nesterov, int first_step, float grad_scale) -> ()");
+      "int nesterov, int first_step, float grad_scale, Tensor? hyper=None) -> ()");
   m.def("normalize_u8(Tensor input, Tensor(a!) out, float[] mean, float[] std) -> ()");
   m.def("gap_fwd(Tensor x) -> Tensor");
   m.def("relu_bias_bwd(Tensor dy, Tensor? y, Tensor(a!)? db_out) -> (Tensor, Tensor)");

@@ -100,6 +100,7 @@ struct SgdArgs {
   int n_tasks;
   float lr, momentum, dampening, grad_scale;
   int nesterov, first_step;
+  const float* hyper;          // optional device [lr, grad_scale] (overrides the scalars)
 };
 void sgd_step(const SgdArgs& a, hipStream_t st);
 

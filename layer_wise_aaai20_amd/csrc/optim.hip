@@ -20,7 +20,14 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
                                              const int32_t* __restrict__ segs,
                                              const int2* __restrict__ tasks,
                                              const float* __restrict__ seg_wd, float lr,
-                                             float momentum, float dampening, float grad_scale) {
+                                             float momentum, float dampening, float grad_scale,
+                                             const float* __restrict__ hyper) {
+  // graph-captured steps read (lr, grad_scale) from device memory, so a replayed HIP graph
+  // follows the LR schedule / loss scale without being re-captured
+  if (hyper != nullptr) {
+    lr = hyper[0];
+    grad_scale = hyper[1];
+  }
   const int2 t = tasks[blockIdx.x];
   const int s = segs[t.x];
   const int n = seg_n[s];
@@ -75,7 +82,8 @@ void sgd_step(const SgdArgs& a, hipStream_t st) {
   const dim3 grid(a.n_tasks), block(SNT);
 #define LW_SGD(M, N, F)                                                                        \
   hipLaunchKernelGGL((k_sgd<M, N, F>), grid, block, 0, st, a.p, a.g, a.buf, a.seg_off, a.seg_n, \
-                     a.segs, a.tasks, a.seg_wd, a.lr, a.momentum, a.dampening, a.grad_scale)
+                     a.segs, a.tasks, a.seg_wd, a.lr, a.momentum, a.dampening, a.grad_scale, \
+                     a.hyper)
   if (!mom) LW_SGD(false, false, false);
   else if (a.nesterov) { if (a.first_step) LW_SGD(true, true, true); else LW_SGD(true, true, false); }
   else { if (a.first_step) LW_SGD(true, false, true); else LW_SGD(true, false, false); }

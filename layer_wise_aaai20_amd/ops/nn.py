@@ -14,28 +14,31 @@ from ._ext import load, ops_for
 MAX_BN_C = 2048          # csrc/bn.hip: one 8-channel group per thread of a 256-thread block
 
 
-def normalize_nhwc_u8(images: torch.Tensor, mean: torch.Tensor, std: torch.Tensor,
-                      dtype=torch.bfloat16, pad4: bool = False) -> torch.Tensor:
+def normalize_nhwc_u8(images: torch.Tensor, mean, std, dtype=torch.bfloat16,
+                      pad4: bool = False) -> torch.Tensor:
     """uint8 [N, H, W, C] → ``(x - mean) / std`` as an NCHW tensor in channels_last memory.
 
     One fused pass on the GPU; the reference does collate → ``.cuda()`` →
     ``.half()`` → ``sub_`` → ``div_`` (``IMAGENET/training/dataloader.py:81-93``). ``pad4``
     (GPU, bf16, 3 channels): write 4 channels with a zero 4th — the input layout of the
-    implicit-GEMM stem convolution (``ops/conv.py``)."""
+    implicit-GEMM stem convolution (``ops/conv.py``). ``mean`` / ``std`` are per-channel
+    sequences of floats (preferred: no device read) or tensors."""
     assert images.dtype == torch.uint8 and images.dim() == 4
     N, H, W, C = images.shape
     lib = ops_for(images)
+    mh = [float(m) for m in (mean.tolist() if torch.is_tensor(mean) else mean)]
+    sh = [float(v) for v in (std.tolist() if torch.is_tensor(std) else std)]
     if lib is not None and pad4 and C == 3 and dtype == torch.bfloat16 and images.is_contiguous():
         out = torch.empty((N, H, W, 4), dtype=dtype, device=images.device).permute(0, 3, 1, 2)
-        lib.normalize_u8(images, out, [float(m) for m in mean.tolist()],
-                         [float(s) for s in std.tolist()])
+        lib.normalize_u8(images, out, mh, sh)
         return out
     if lib is not None and images.is_contiguous():
         out = torch.empty((N, C, H, W), dtype=dtype, device=images.device,
                           memory_format=torch.channels_last)
-        lib.normalize_u8(images, out, [float(m) for m in mean.tolist()],
-                         [float(s) for s in std.tolist()])
+        lib.normalize_u8(images, out, mh, sh)
         return out
+    mean = torch.as_tensor(mh, dtype=torch.float32)
+    std = torch.as_tensor(sh, dtype=torch.float32)
     x = images.permute(0, 3, 1, 2).float()
     x = (x - mean.view(1, -1, 1, 1).to(x.device)) / std.view(1, -1, 1, 1).to(x.device)
     return x.to(dtype).contiguous(memory_format=torch.channels_last)

@@ -45,6 +45,11 @@ class FlatSGD(Optimizer):
         self.buf = torch.zeros_like(arena.param_buf)
         self._first = True
         self._wd_cache = None
+        # graph mode (train/imagenet.py GraphedStep): lr / grad_scale live in a device tensor the
+        # kernel reads, written by load_hyper() outside the captured graph before each replay
+        self.device_hyper = False
+        self._hyper = None
+        self._hyper_host = None
 
     # torch.optim.SGD-compatible state: momentum_buffer views into the flat buffer
     def _bind_state(self):
@@ -71,6 +76,25 @@ class FlatSGD(Optimizer):
             raise ValueError(f"FlatSGD needs a single {k} across param groups, got {vals}")
         return vals.pop()
 
+    def load_hyper(self) -> None:
+        """Write the current (lr, grad_scale) into the device tensor a captured step reads (two
+        stream-ordered fills, only when they changed; call outside graph capture)."""
+        vals = (float(self._uniform("lr")), float(self.grad_scale))
+        if self._hyper is None:
+            self._hyper = torch.empty(2, dtype=torch.float32, device=self.arena.param_buf.device)
+            self._hyper_host = None
+        if vals != self._hyper_host:
+            self._hyper[0].fill_(vals[0])
+            self._hyper[1].fill_(vals[1])
+            self._hyper_host = vals
+
+    def graph_signature(self) -> tuple:
+        """Everything a captured SGD launch bakes in as kernel arguments (lr and grad_scale are
+        read from device memory instead): a change means the step must be re-captured."""
+        return (float(self._uniform("momentum")), float(self._uniform("dampening")),
+                bool(self._uniform("nesterov")), self._first,
+                tuple(float(g["weight_decay"]) for g in self.param_groups))
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
@@ -81,10 +105,13 @@ class FlatSGD(Optimizer):
         p, g = self.arena.param_buf, self.arena.grad
         lib = ops_for(p)
         wd = self._seg_wd(p.device)
+        if self.device_hyper and not torch.cuda.is_current_stream_capturing():
+            self.load_hyper()
         if lib is not None:
             t = self.plan.all_large_tables(p.device)
             lib.sgd_step(p, g, self.buf, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], wd, lr,
-                         mom, damp, int(nest), int(self._first), float(self.grad_scale))
+                         mom, damp, int(nest), int(self._first), float(self.grad_scale),
+                         self._hyper if self.device_hyper else None)
         else:
             wdv = torch.repeat_interleave(
                 wd, torch.from_numpy(np.diff(np.append(self.plan.offsets, self.arena.numel))))

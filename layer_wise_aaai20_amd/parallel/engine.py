@@ -255,7 +255,9 @@ class GradSyncEngine:
             if self.timing:
                 rec.append((bi, t0, t1, tx, t2, self._event()))
         self._pending = []
-        if hold:
+        if hold and not torch.cuda.is_current_stream_capturing():
+            # (under HIP-graph capture the event record / wait pairs become graph edges: there is
+            # nothing to keep alive, and an event query would invalidate the capture)
             # Keep the cross-stream events alive until a fence on the compute stream, recorded
             # after every wait on them, has completed: destroying a HIP event while a queued
             # stream wait still references it is what faulted the VGG-16 run
@@ -280,6 +282,12 @@ class GradSyncEngine:
             self._ready[i] = True
         self._launch_in_order()
         self.finish()
+
+    def graph_safe(self) -> bool:
+        """Whether a whole step through this engine can be captured as one HIP graph and
+        replayed: every codec is sync-free and step-invariant, and per-bucket timing is off."""
+        return (self.device.type == "cuda" and not self.timing and
+                all(bool(c.graph_safe) for c in self.codecs))
 
     def read_timings(self) -> List[dict]:
         """Per-bucket µs of the last step (HIP events): ``compress_us`` (select + pack on the side

@@ -29,10 +29,10 @@ CONFIGS = {
 V100_ANCHOR = 16500.0    # img/s, derived in BASELINE.md
 
 
-def run(name, steps, warmup, world, rank, dev):
+def run(name, steps, warmup, world, rank, dev, graph=True):
     from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
     cfg = CONFIGS[name]
-    tr = CifarTrainer(device=dev, n_train=512 * 12, **cfg)
+    tr = CifarTrainer(device=dev, n_train=512 * 12, graph=graph, **cfg)
     for _ in range(warmup):
         tr.step()
     torch.cuda.synchronize()
@@ -56,6 +56,7 @@ def run(name, steps, warmup, world, rank, dev):
             "warmup": warmup, "ms_per_step": round(dt / steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": round(value / V100_ANCHOR, 3) if name == "anchor"
             else None, "dtype": "bf16", "data": "synthetic",
+            "hip_graph": tr.graphed.replays >= steps,
             "config": dict(cfg, global_batch=world * tr.bs, parallelism=f"dp{world}",
                            wire_bytes_per_rank=st.payload_bytes, dense_grad_bytes=st.dense_bytes)}
 
@@ -65,6 +66,8 @@ def main():
     ap.add_argument("--config", default="all", choices=["all"] + list(CONFIGS))
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--graph", default="on", choices=["on", "off"],
+                    help="capture the whole step as one HIP graph after 3 eager steps")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -76,7 +79,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     names = list(CONFIGS) if args.config == "all" else [args.config]
     for n in names:
-        line = run(n, args.steps, args.warmup, world, rank, dev)
+        line = run(n, args.steps, args.warmup, world, rank, dev, args.graph == "on")
         if rank == 0:
             print(json.dumps(line), flush=True)
     if world > 1:

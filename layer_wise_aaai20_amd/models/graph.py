@@ -123,7 +123,10 @@ class Network(nn.Module):
         cache = dict(inputs)
         for name, (_, ins) in self.graph.items():
             cache[name] = self._modules[name](*[cache[i] for i in ins])
-        self.cache = cache
+        # (the reference keeps the live dict, torch_backend.py:69-80; a detached view keeps the
+        # outputs inspectable without holding the previous step's autograd graph — and its
+        # AccumulateGrad nodes — alive into the next step, which breaks HIP-graph capture)
+        self.cache = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in cache.items()}
         return cache
 
 

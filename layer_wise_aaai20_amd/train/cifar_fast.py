@@ -20,13 +20,14 @@ from ..ops import nn as lwnn
 from ..optim.flat_sgd import FlatSGD
 from ..parallel.ddp import CompressedDDP
 from ..utils.logging import PiecewiseLinear
+from .graphs import StepGraph
 
 
 class CifarTrainer:
     def __init__(self, network="resnet9", device=None, compress="none", method="none", K=None,
                  V=None, qstates=None, error_feedback=False, batch_size=512, epochs=24,
                  momentum=0.9, dtype=torch.bfloat16, bucket_cap_mb=25.0, wire="auto",
-                 n_train=50000, seed=0, fused=True):
+                 n_train=50000, seed=0, fused=True, graph=None):
         self.device = torch.device(device or "cuda")
         self.dtype = dtype
         self.bs = batch_size
@@ -58,6 +59,9 @@ class CifarTrainer:
         self.step_count = 0
         self._it = None
         self.last = None
+        # whole step as one HIP graph after 3 eager steps (train/graphs.py): at 1.5-6 ms per
+        # step the per-kernel host launch cost is a large share of an eager CIFAR step
+        self.graphed = StepGraph(self._eager, self.ddp.engine, self.opt, self.device, 3, graph)
 
     def next_batch(self):
         if self._it is None:
@@ -68,17 +72,22 @@ class CifarTrainer:
             self._it = iter(self.batches)
             return next(self._it)
 
+    def _eager(self, x, target):
+        with torch.autocast(device_type=self.device.type, dtype=self.dtype,
+                            enabled=self.dtype != torch.float32, cache_enabled=False):
+            out = self.ddp({"input": x, "target": target})
+            loss = out["loss"].float().sum()
+        loss.backward()
+        self.opt.step()
+        return {k: (v.detach() if torch.is_tensor(v) else v) for k, v in out.items()}, \
+            loss.detach()
+
     def step(self, batch=None):
         batch = batch or self.next_batch()
         lr = self.sched(self.step_count / self.steps_per_epoch) / self.bs
         for g in self.opt.param_groups:
             g["lr"] = lr
-        with torch.autocast(device_type=self.device.type, dtype=self.dtype,
-                            enabled=self.dtype != torch.float32):
-            out = self.ddp(batch)
-            loss = out["loss"].float().sum()
-        loss.backward()
-        self.opt.step()
+        out, loss = self.graphed(batch["input"], batch["target"])
         self.step_count += 1
         self.last = out
         return loss

@@ -8,7 +8,6 @@ backward with bucketed compression overlapped (CompressedDDP) → one fused SGD 
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -18,6 +17,7 @@ from ..models import resnet as resnet_models
 from ..ops import nn as lwnn
 from ..optim.flat_sgd import FlatSGD
 from ..parallel.ddp import CompressedDDP
+from .graphs import StepGraph
 
 IMAGENET_MEAN = (0.485 * 255, 0.456 * 255, 0.406 * 255)
 IMAGENET_STD = (0.229 * 255, 0.224 * 255, 0.225 * 255)
@@ -44,18 +44,11 @@ class ImageNetTrainer:
     """One training step = normalise → forward → loss → backward (+ overlapped compressed
     gradient exchange) → fused SGD.
 
-    **HIP-graph mode** (``graph=True``, the default on a GPU when every codec is graph-safe): the
-    step issues ~650 kernels, and on a host whose Python launch rate is below the GPU's kernel rate
-    the GPU idles between them (measured: 27.6 ms wall for 24.6 ms of kernels,
-    ``profiles/r2_head3_step_breakdown.txt``). After ``graph_warmup`` eager steps (GEMM tile tuner
-    populated, RCCL communicators and the allocator warm), the whole step — forward, backward with
-    its side-stream compression and collectives, decode, SGD — is captured once with
-    ``torch.cuda.graph`` and each later step is two input copies plus one graph replay. The
-    learning rate and loss scale are read by the SGD kernel from device memory
-    (:meth:`FlatSGD.load_hyper`), so the reference's per-iteration LR schedule needs no
-    re-capture; anything else the capture bakes in (momentum, weight decay, input shapes) triggers
-    a re-capture when it changes. Codecs whose kernels take a host step counter (Random-K, the
-    quantisers) or synchronise (sparse threshold wire) keep the eager path."""
+    **HIP-graph mode** (``graph=True``, the default on a GPU when every codec is graph-safe): after
+    ``graph_warmup`` eager steps the whole step is captured once and replayed
+    (:class:`~.graphs.StepGraph`): ~650 kernel launches become two input copies and one replay,
+    so the host's launch rate no longer sets the step time. The LR schedule reaches the captured
+    SGD kernel through device memory (:meth:`FlatSGD.load_hyper`)."""
 
     def __init__(self, ddp: CompressedDDP, optimizer, device, dtype=torch.bfloat16,
                  criterion: Optional[nn.Module] = None, channels_last: bool = True,
@@ -69,13 +62,11 @@ class ImageNetTrainer:
         self.mean = torch.tensor(IMAGENET_MEAN, device=device, dtype=torch.float32)
         self.std = torch.tensor(IMAGENET_STD, device=device, dtype=torch.float32)
         self._last = None
-        if graph is None:
-            graph = os.environ.get("LWAAAI_GRAPH", "1") != "0"
-        self.graph = bool(graph) and device.type == "cuda" and hasattr(optimizer, "load_hyper")
-        self.graph_warmup = int(graph_warmup)
-        self._g = None                 # (CUDAGraph, static inputs/outputs, signature)
-        self._eager_done = 0
-        self.graph_replays = 0
+        self.graphed = StepGraph(self._eager, ddp.engine, optimizer, device, graph_warmup, graph)
+
+    @property
+    def graph_replays(self) -> int:
+        return self.graphed.replays
 
     def normalize(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
         # a fused ResNet takes the image as 4 bf16 channels (the implicit-GEMM stem's layout)
@@ -97,58 +88,12 @@ class ImageNetTrainer:
         out, loss = self.forward_loss(x, target)
         loss.backward()
         self.opt.step()
-        return out.detach(), loss.detach()
-
-    def graph_active(self) -> bool:
-        return (self.graph and self.ddp.training and self.ddp.engine.graph_safe())
+        return out.detach(), target, loss.detach()
 
     def step(self, images_u8_nhwc: torch.Tensor, target: torch.Tensor):
-        if not self.graph_active():
-            out, loss = self._eager(images_u8_nhwc, target)
-            self._last = (out, target, loss)
-            return loss
-        sig = (tuple(images_u8_nhwc.shape), images_u8_nhwc.dtype, tuple(target.shape),
-               self.opt.graph_signature())
-        if self._g is None or self._g[-1] != sig:
-            if self._eager_done < self.graph_warmup:
-                self._eager_done += 1
-                out, loss = self._eager(images_u8_nhwc, target)
-                self._last = (out, target, loss)
-                return loss
-            try:
-                self._capture(images_u8_nhwc, target, sig)
-            except RuntimeError as e:          # capture unsupported here: stay eager
-                self.graph = False
-                self._g = None
-                torch.cuda.synchronize(self.device)
-                self.ddp.engine._reset_state()
-                print(f"[lwaaai] HIP-graph capture failed, running eagerly: {e}", flush=True)
-                out, loss = self._eager(images_u8_nhwc, target)
-                self._last = (out, target, loss)
-                return loss
-        graph, xin, tin, out, loss, _ = self._g
-        xin.copy_(images_u8_nhwc, non_blocking=True)
-        tin.copy_(target, non_blocking=True)
-        self.opt.load_hyper()
-        graph.replay()
-        self.graph_replays += 1
-        self._last = (out, tin, loss)
-        return loss
-
-    def _capture(self, images_u8_nhwc, target, sig) -> None:
-        self._g = None
-        xin = images_u8_nhwc.clone()
-        tin = target.clone()
-        self.opt.device_hyper = True
-        self.opt.load_hyper()
-        torch.cuda.synchronize(self.device)
-        graph = torch.cuda.CUDAGraph()
-        # thread_local: RCCL's watchdog thread queries events while this thread captures
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-            out, loss = self._eager(xin, tin)
-        torch.cuda.synchronize(self.device)
-        # the capture recorded the step without running it: the caller's replay performs it
-        self._g = (graph, xin, tin, out, loss, sig)
+        run = self.graphed if self.ddp.training else self._eager
+        self._last = run(images_u8_nhwc, target)
+        return self._last[2]
 
     def last_top1(self) -> Optional[float]:
         if self._last is None:

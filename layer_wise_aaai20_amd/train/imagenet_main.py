@@ -43,6 +43,7 @@ from ..parallel.ddp import CompressedDDP, DistributedDataParallel, RandomKSparsi
 from ..utils import fp16 as fp16util
 from ..utils.logging import AverageMeter, FileLogger, NetworkMeter, TensorboardLogger, TimeMeter
 
+from .graphs import StepGraph
 from .schedules import NAMES as _SCHED_NAMES, schedule as _schedule
 
 
@@ -62,6 +63,9 @@ def get_parser():
     p.add_argument("-e", "--evaluate", dest="evaluate", action="store_true")
     p.add_argument("--fp16", action="store_true")
     p.add_argument("--bf16", action="store_true")
+    p.add_argument("--no-graph", action="store_true",
+                   help="fused path: launch every kernel from Python instead of replaying the "
+                        "captured HIP graph of the step")
     p.add_argument("--loss-scale", type=float, default=1024)
     p.add_argument("--distributed", action="store_true")
     p.add_argument("--dist-url", default="env://", type=str)
@@ -323,6 +327,30 @@ def save_checkpoint(run, epoch, model, best_top5, optimizer, is_best=False,
     return path
 
 
+def _fast_step(run, model, criterion, optimizer, eng):
+    """The fused-path step closure (forward, loss, backward with overlapped compression, FlatSGD)
+    wrapped in a :class:`~.graphs.StepGraph`, built once per run."""
+    sg = getattr(run, "step_graph", None)
+    if sg is not None:
+        return sg
+    args = run.args
+
+    def body(inp, target):
+        with torch.autocast(device_type=inp.device.type, dtype=torch.bfloat16,
+                            cache_enabled=False):
+            output = model(inp)
+            loss = criterion(output.float(), target)
+        (loss * args.loss_scale if args.fp16 else loss).backward()
+        optimizer.step()
+        last = getattr(criterion, "last_correct", None)
+        return output.detach(), loss.detach(), last
+
+    dev = next(model.parameters()).device
+    run.step_graph = StepGraph(body, eng, optimizer, dev,
+                               enabled=not getattr(args, "no_graph", False))
+    return run.step_graph
+
+
 def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, master):
     args = run.args
     net_meter, timer = NetworkMeter(), TimeMeter()
@@ -341,15 +369,19 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
         should_print = batch_num % args.print_freq == 0 or batch_num == len(trn_loader)
         if eng is not None:
             eng.timing = should_print and run.is_master
-        with torch.autocast(device_type=inp.device.type, dtype=torch.bfloat16,
-                            enabled=args.bf16 or fast):
-            output = model(inp)
-            loss = criterion(output.float(), target)
         if fast:
             # CompressedDDP: buckets compressed + exchanged during backward, the arena zeroed by
-            # the next forward (no zero_grad); FlatSGD unscales a loss-scaled gradient itself
-            (loss * args.loss_scale if args.fp16 else loss).backward()
-            optimizer.step()
+            # the next forward (no zero_grad); FlatSGD unscales a loss-scaled gradient itself.
+            # The whole step runs as one replayed HIP graph once warm (train/graphs.py).
+            output, loss, last = _fast_step(run, model, criterion, optimizer, eng)(inp, target)
+        else:
+            with torch.autocast(device_type=inp.device.type, dtype=torch.bfloat16,
+                                enabled=args.bf16):
+                output = model(inp)
+                loss = criterion(output.float(), target)
+            last = None
+        if fast:
+            pass
         elif args.fp16:
             scaled = loss * args.loss_scale
             model.zero_grad()
@@ -367,7 +399,8 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
             loss.backward()
             sync(model)
             optimizer.step()
-        last = getattr(criterion, "last_correct", None)
+        if not fast:
+            last = getattr(criterion, "last_correct", None)
         if last is not None:          # top-1/top-5 from the fused loss kernel (no topk pass)
             cs = last.sum(0)
             corr1, corr5 = cs[0:1], cs[1:2]
@@ -621,6 +654,10 @@ def main(argv=None):
     for epoch in range(args.start_epoch, end_epoch):
         dm.set_epoch(epoch)
         train(run, dm.trn_dl, model, criterion, optimizer, scheduler, epoch, sync, master)
+        sg = getattr(run, "step_graph", None)
+        if sg is not None:
+            log.event(f"HIP-graph step replays so far: {sg.replays} "
+                      f"({'active' if sg.active() else 'eager'})")
         top1, top5 = validate(run, dm.val_dl, model, criterion, epoch, start_time)
         hours = (datetime.now() - start_time).total_seconds() / 3600.0
         log.event(f"~~{epoch}\t{hours:.5f}\t\t{top1:.3f}\t\t{top5:.3f}\n")

@@ -92,3 +92,25 @@ def test_graph_capture_with_rccl_collectives():
                        timeout=100, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "replays 3 backend nccl" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("network,compress,method,K",
+                         [("resnet9", "none", "none", None), ("alexnet", "entiremodel", "Topk", 0.01),
+                          ("vgg16", "layerwise", "Topk", 0.001)])
+def test_cifar_graph_step_matches_eager(network, compress, method, K):
+    from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
+    runs = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        tr = CifarTrainer(network, compress=compress, method=method, K=K,
+                          error_feedback=compress == "entiremodel", n_train=4096, graph=graph)
+        losses = [float(tr.step()) for _ in range(6)]
+        torch.cuda.synchronize()
+        runs[graph] = (torch.cat([p.detach().float().reshape(-1) for p in tr.model.parameters()]),
+                       losses, tr.graphed.replays)
+    pe, le, _ = runs[False]
+    pg, lg, replays = runs[True]
+    assert replays == 3
+    for a, b in zip(le, lg):
+        assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (le, lg)
+    assert (pe - pg).abs().max().item() <= 2e-3 * pe.abs().max().item()

@@ -286,6 +286,9 @@ class GradSyncEngine:
     def graph_safe(self) -> bool:
         """Whether a whole step through this engine can be captured as one HIP graph and
         replayed: every codec is sync-free and step-invariant, and per-bucket timing is off."""
+        if comm.is_dist() and comm.world_size(self.pg) > 1 and \
+                comm.dist.get_backend(self.pg) != "nccl":
+            return False                  # gloo collectives run on the host: not capturable
         return (self.device.type == "cuda" and not self.timing and
                 all(bool(c.graph_safe) for c in self.codecs))
 

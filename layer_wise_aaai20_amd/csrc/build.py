@@ -96,7 +96,7 @@ def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
     tmp = OUT + ".tmp"
     cmd = ["g++", "-shared", "-o", tmp] + objs + [
         f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-        "-l:libamdhip64.so", f"-Wl,-rpath,{lib}", "-Wl,-z,defs"]   # unresolved symbols fail here
+        "-l:libamdhip64.so", "-lrccl", f"-Wl,-rpath,{lib}", "-Wl,-z,defs"]   # unresolved symbols fail here
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -60,16 +60,92 @@ def all_gather(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool 
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op) or _Done()
 
 
+class NativeRccl:
+    """Direct RCCL communicator (``csrc/rccl.cpp``) for the stream-ordered, graph-capturable
+    bucket collectives: calls are enqueued on the caller's current HIP stream and return
+    :class:`_Done` (nothing to wait for on the host; later work on that stream is ordered after
+    them). Built collectively over an initialised ``nccl`` process group: rank 0's unique id is
+    broadcast through it, then every rank joins with ``ncclCommInitRank``."""
+
+    def __init__(self, group=None, device=None):
+        from ..ops._ext import load
+        self.lib = load()
+        self.world = world_size(group)
+        self.rank = rank(group)
+        dev = torch.device(device) if device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        uid = self.lib.rccl_unique_id() if self.rank == 0 else \
+            torch.zeros(128, dtype=torch.uint8)
+        if self.world > 1:
+            t = uid.to(dev)
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast(t, src=src, group=group)
+            uid = t.cpu()
+        self.handle = int(self.lib.rccl_init(uid, self.world, self.rank, dev.index or 0))
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
+        self.lib.rccl_all_gather(self.handle, inp, out)
+        return _Done()
+
+    def all_reduce(self, t: torch.Tensor, op: str = "sum"):
+        self.lib.rccl_all_reduce(self.handle, t, {"sum": 0, "max": 1, "min": 2}[op])
+        return _Done()
+
+    def broadcast(self, t: torch.Tensor, src: int = 0):
+        self.lib.rccl_broadcast(self.handle, t, src)
+        return _Done()
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.rccl_destroy(self.handle)
+            self.handle = 0
+
+
+_NATIVE = {}
+
+
+def native_rccl(group=None, device=None) -> Optional[NativeRccl]:
+    """The process group's native RCCL communicator (created on first use; a collective call, so
+    every rank must reach it), or None when the group is not ``nccl`` / ``LWAAAI_NATIVE_RCCL=0``."""
+    if not is_dist() or dist.get_backend(group) != "nccl" or \
+            os.environ.get("LWAAAI_NATIVE_RCCL", "1") == "0":
+        return None
+    key = id(group) if group is not None else None
+    if key not in _NATIVE:
+        _NATIVE[key] = NativeRccl(group, device)
+    return _NATIVE[key]
+
+
 def all_reduce_max(t: torch.Tensor, group=None) -> torch.Tensor:
     if is_dist() and world_size(group) > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return t
 
 
-def broadcast_coalesced(tensors, src: int = 0, group=None) -> None:
+def broadcast_coalesced(tensors, src: int = 0, group=None, native: Optional[NativeRccl] = None
+                        ) -> None:
     """Broadcast a list of tensors from ``src`` as one flat message per dtype (replaces the private
-    ``dist._dist_broadcast_coalesced`` of ``ddp.py:193, 374-377``)."""
+    ``dist._dist_broadcast_coalesced`` of ``ddp.py:193, 374-377``). ``native``: send GPU tensors
+    through that RCCL communicator (stream-ordered, graph-capturable) instead of c10d."""
     if not is_dist() or world_size(group) == 1 or not tensors:
+        return
+    if native is not None and all(t.is_cuda for t in tensors):
+        by_dtype = {}
+        for t in tensors:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        for ts in by_dtype.values():
+            if len(ts) == 1 and ts[0].is_contiguous():
+                native.broadcast(ts[0].detach(), src)
+                continue
+            flat = torch.cat([t.detach().reshape(-1) for t in ts])
+            native.broadcast(flat, src)
+            off = 0
+            with torch.no_grad():
+                for t in ts:
+                    n = t.numel()
+                    t.copy_(flat[off:off + n].view_as(t))
+                    off += n
         return
     by_dtype = {}
     for t in tensors:

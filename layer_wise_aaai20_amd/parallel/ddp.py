@@ -132,7 +132,8 @@ class CompressedDDP(nn.Module):
             raise RuntimeError("Not all gradients have been reduced from the backward of the "
                                "previous iteration (ddp.py:312-327 check_reduction).")
         if self.broadcast_buffers and self._buffers_list:
-            comm.broadcast_coalesced(self._buffers_list, 0, self.process_group)
+            comm.broadcast_coalesced(self._buffers_list, 0, self.process_group,
+                                     native=self.engine._native)
         self.engine.begin_step()
         if self.bf16_weights and self.engine.arena.device.type == "cuda":
             self.engine.arena.refresh_bf16()

@@ -114,8 +114,14 @@ class GradSyncEngine:
                       if overlap_compress and self.device.type == "cuda" else None)
         self._retired = []            # (fence event, events held until it completes)
         self._check = os.environ.get("LWAAAI_ENGINE_CHECK", "0") == "1"
-        self._stream_waitable = (comm.is_dist() and comm.world_size(self.pg) > 1 and
-                                 comm.dist.get_backend(self.pg) == "nccl")
+        # bucket collectives on a native RCCL communicator (csrc/rccl.cpp) when the group is
+        # nccl: stream-ordered calls without c10d Work objects, so a captured step never puts
+        # events on the ProcessGroup watchdog's list (see graph_safe)
+        self._native = (comm.native_rccl(self.pg, self.device)
+                        if self.device.type == "cuda" else None)
+        self._stream_waitable = self._native is not None or (
+            comm.is_dist() and comm.world_size(self.pg) > 1 and
+            comm.dist.get_backend(self.pg) == "nccl")
         self._reset_state()
         self.all_reduced_last = True
         self.verify_plan()
@@ -215,11 +221,13 @@ class GradSyncEngine:
             t1 = self._event() if self.timing else None
             self._payload += codec.last_payload_bytes
             if codec.collective == "all_reduce":
-                work = comm.all_reduce(send, self.pg)
+                work = (self._native.all_reduce(send) if self._native is not None
+                        else comm.all_reduce(send, self.pg))
                 recv = None
             else:
                 recv = codec.recv_buffer(send)
-                work = comm.all_gather(recv, send, self.pg)
+                work = (self._native.all_gather(recv, send) if self._native is not None
+                        else comm.all_gather(recv, send, self.pg))
             tx = None
             if side is not None and self._stream_waitable:
                 # RCCL: wait() only orders the side stream after the collective (no host block),
@@ -286,9 +294,11 @@ class GradSyncEngine:
     def graph_safe(self) -> bool:
         """Whether a whole step through this engine can be captured as one HIP graph and
         replayed: every codec is sync-free and step-invariant, and per-bucket timing is off."""
-        if comm.is_dist() and comm.world_size(self.pg) > 1 and \
-                comm.dist.get_backend(self.pg) != "nccl":
-            return False                  # gloo collectives run on the host: not capturable
+        if comm.is_dist() and self._native is None:
+            # gloo collectives run on the host; c10d RCCL calls leave Work events for the
+            # ProcessGroup watchdog, which may query one recorded inside the capture and abort
+            # (hipErrorCapturedEvent): capture only with the native communicator
+            return False
         return (self.device.type == "cuda" and not self.timing and
                 all(bool(c.graph_safe) for c in self.codecs))
 

@@ -66,8 +66,10 @@ def test_graph_mode_falls_back_for_step_dependent_codecs():
 
 
 def test_graph_capture_with_rccl_collectives():
-    """World-1 RCCL process group: the bucket all-gathers really go through RCCL and are captured
-    into the graph (the multi-GPU path's capture mechanics, on one GPU)."""
+    """World-1 RCCL process group: the bucket all-gathers really go through RCCL — on the native
+    communicator (csrc/rccl.cpp), not c10d, whose watchdog can trip over events recorded inside
+    the capture (profiles/r2_rccl_capture_race.log) — and are captured into the graph (the
+    multi-GPU path's capture mechanics, on one GPU)."""
     script = textwrap.dedent("""
         import sys, torch, torch.distributed as dist
         sys.path.insert(0, %r)
@@ -85,6 +87,19 @@ def test_graph_capture_with_rccl_collectives():
             loss = tr.step(x, t)
         torch.cuda.synchronize()
         assert torch.isfinite(loss).item()
+        eng = tr.ddp.engine
+        assert eng._native is not None and eng._native.world == 1
+        # the native communicator's collectives on their own
+        x = torch.arange(6, dtype=torch.float32, device="cuda")
+        eng._native.all_reduce(x)
+        y = torch.empty(6, dtype=torch.float32, device="cuda")
+        eng._native.all_gather(y, x)
+        eng._native.broadcast(x, 0)
+        m = torch.tensor([3, 7], dtype=torch.int32, device="cuda")
+        eng._native.all_reduce(m, "max")
+        torch.cuda.synchronize()
+        assert torch.equal(x, torch.arange(6, dtype=torch.float32, device="cuda"))
+        assert torch.equal(y, x) and m.tolist() == [3, 7]
         print("replays", tr.graph_replays, "backend", dist.get_backend(), flush=True)
         dist.destroy_process_group()
     """ % ROOT)

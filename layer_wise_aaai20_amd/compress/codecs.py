@@ -61,6 +61,9 @@ class Codec:
     # changes from step to step on the host (e.g. a Philox step counter passed as a kernel
     # argument): the whole training step can then be captured once as a HIP graph and replayed
     graph_safe = False
+    # device step counter (GradSyncEngine._dstep) the Philox-keyed kernels read instead of the
+    # host `step` argument, so a replayed HIP graph draws fresh random keys every step
+    step_t = None
 
     def __init__(self, plan: SegPlan, world: int, rank: int, seed: int = 0,
                  error_feedback: bool = False):
@@ -111,9 +114,8 @@ class TopkCodec(Codec):
     name = "topk"
     km = KM_TOPK
 
-    @property
-    def graph_safe(self) -> bool:          # exact Top-K ignores the step; Random-K keys use it
-        return self.km == KM_TOPK and type(self) is TopkCodec
+    # exact Top-K ignores the step; Random-K reads it from the device counter (step_t)
+    graph_safe = True
 
     def __init__(self, plan, world, rank, K: float, seed=0, error_feedback=False):
         super().__init__(plan, world, rank, seed, error_feedback)
@@ -159,7 +161,8 @@ class TopkCodec(Codec):
             lib.select_compress(grad, ef, t["seg_off"], t["seg_n"], t["keep"], t["cap_off"],
                                 t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
                                 self._workspace(grad.device, lib), self.km, OUT_PAIRS, out, None,
-                                None, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed)
+                                None, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
+                                self.step_t)
             return out
         self._compress_cpu(grad, ef, step, out)
         return out
@@ -232,6 +235,11 @@ class RandkSparseCodec(TopkCodec):
     """Random-K with explicit indices (masks need not be rank-coherent)."""
     name = "randk-sparse"
     km = KM_RANDK
+    # Kept eager: with the device step counter the layer-wise Random-K step replays bit-exactly,
+    # but the entire-model (single 6.6 M-element segment) + EF replay diverged from the eager
+    # step from the second replay on (duplicate slots: scripts/probes/graph_vs_eager_probe.py,
+    # profiles/r2_randk_graph_divergence.log) — not captured until that is understood.
+    graph_safe = False
 
     def __init__(self, plan, world, rank, K, seed=0, error_feedback=False):
         Codec.__init__(self, plan, world, rank, seed, error_feedback)
@@ -276,7 +284,8 @@ class RandkCodec(RandkSparseCodec):
             lib.select_compress(grad, ef, t["seg_off"], t["seg_n"], t["keep"], t["cap_off"],
                                 t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
                                 self._workspace(grad.device, lib), KM_RANDK, OUT_VALIDX, None,
-                                vals, idx, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed)
+                                vals, idx, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
+                                self.step_t)
             return vals
         for s, x in self._segs(grad):
             o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
@@ -313,6 +322,7 @@ class ThresholdCodec(TopkCodec):
     so ranks first agree on per-layer capacities with an all-reduce(MAX) of the counts."""
     name = "threshold"
     km = KM_THRESH
+    graph_safe = False          # the sparse wire reads the agreed capacity on the host
 
     def __init__(self, plan, world, rank, V=None, adaptive=False, seed=0, error_feedback=False,
                  count_exchange=None):
@@ -425,6 +435,7 @@ class ThresholdCodec(TopkCodec):
 # ================================================================================= quantisers
 class _QuantCodec(Codec):
     collective = "all_gather"
+    graph_safe = True           # stochastic rounding keyed by the device step counter (step_t)
     q = Q_TERN
     tag = philox.TAG_TERNGRAD
     qstates = 1
@@ -459,7 +470,7 @@ class _QuantCodec(Codec):
                 self._ws[k] = _ws_tensor(nb, grad.device)
             lib.quantize(grad, ef, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], t["task_lo"],
                          t["rec_off"], self._ws[k], out, self.q, self.qstates, self.plan.gid_base,
-                         int(step) & 0xFFFFFFFF, tag, self.seed)
+                         int(step) & 0xFFFFFFFF, tag, self.seed, self.step_t)
             return out
         self._quant_cpu(grad, ef, step, out, tag)
         return out

@@ -81,6 +81,15 @@ int64_t workspace_bytes(int64_t n_small, int64_t n_large, int64_t n_tasks) {
   return layout(n_small, n_large, n_tasks).total;
 }
 
+// optional device step counter (int32/int64 scalar; the kernels read its low 32 bits)
+const uint32_t* step_ptr(const c10::optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_cuda(*t, "step_t");
+  TORCH_CHECK((t->scalar_type() == at::kInt || t->scalar_type() == at::kLong) && t->numel() >= 1,
+              "step_t must be an int32/int64 GPU scalar");
+  return reinterpret_cast<const uint32_t*>(t->data_ptr());
+}
+
 lw::SelectArgs make_select_args(const Tensor& g, const c10::optional<Tensor>& ef,
                                 const Tensor& seg_off, const Tensor& seg_n, const Tensor& keep,
                                 const Tensor& cap_off, const Tensor& small_segs,
@@ -129,7 +138,8 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
                      Tensor keep, Tensor cap_off, Tensor small_segs, Tensor large_segs,
                      Tensor tasks, Tensor task_lo, Tensor ws, int64_t km, int64_t out,
                      c10::optional<Tensor> pairs, c10::optional<Tensor> vals,
-                     c10::optional<Tensor> idx, int64_t gid_base, int64_t step, int64_t seed) {
+                     c10::optional<Tensor> idx, int64_t gid_base, int64_t step, int64_t seed,
+                     c10::optional<Tensor> step_t) {
   const c10::DeviceGuard guard(g.device());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, keep, cap_off, small_segs, large_segs,
                                       tasks, task_lo, ws);
@@ -140,6 +150,7 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
               "missing output buffers");
   a.gid_base = (uint32_t)gid_base;
   a.step = (uint32_t)step;
+  a.step_ptr = step_ptr(step_t);
   a.seed0 = (uint32_t)(seed & 0xffffffff);
   a.seed1 = (uint32_t)((uint64_t)seed >> 32);
   lw::select_compress(a, (int)km, (int)out, a.ef != nullptr, cur_stream());
@@ -241,7 +252,8 @@ lw::QuantArgs make_quant_args(const Tensor& g, const c10::optional<Tensor>& ef,
 
 void quantize(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, Tensor segs,
               Tensor tasks, Tensor task_lo, Tensor rec_off, Tensor ws, Tensor payload, int64_t q,
-              int64_t qstates, int64_t gid_base, int64_t step, int64_t tag, int64_t seed) {
+              int64_t qstates, int64_t gid_base, int64_t step, int64_t tag, int64_t seed,
+              c10::optional<Tensor> step_t) {
   const c10::DeviceGuard guard(g.device());
   lw::QuantArgs a = make_quant_args(g, ef, seg_off, seg_n, segs, tasks, task_lo, rec_off, qstates);
   check_cuda(payload, "payload");
@@ -253,6 +265,7 @@ void quantize(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, 
   a.payload = ptr<uint32_t>(payload);
   a.gid_base = (uint32_t)gid_base;
   a.step = (uint32_t)step;
+  a.step_ptr = step_ptr(step_t);
   a.tag = (uint32_t)tag;
   a.seed0 = (uint32_t)(seed & 0xffffffff);
   a.seed1 = (uint32_t)((uint64_t)seed >> 32);
@@ -1209,7 +1222,7 @@ TORCH_LIBRARY(lwaaai, m) {
       "select_compress(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor keep, "
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
       "Tensor(c!) ws, int km, int out, Tensor(d!)? pairs, Tensor(e!)? vals, Tensor(f!)? idx, "
-      "int gid_base, int step, int seed) -> ()");
+      "int gid_base, int step, int seed, Tensor? step_t=None) -> ()");
   m.def(
       "thresh_count(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor large_segs, "
       "Tensor tasks, Tensor task_lo, Tensor(c!) ws, float V, int adaptive, Tensor(d!) counts_out) "
@@ -1229,7 +1242,7 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "quantize(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor segs, "
       "Tensor tasks, Tensor task_lo, Tensor rec_off, Tensor(c!) ws, Tensor(d!) payload, int q, "
-      "int qstates, int gid_base, int step, int tag, int seed) -> ()");
+      "int qstates, int gid_base, int step, int tag, int seed, Tensor? step_t=None) -> ()");
   m.def(
       "dequantize(Tensor gathered, int world, Tensor(a!) g, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor task_lo, Tensor rec_off, int q, int qstates) -> ()");

@@ -115,7 +115,9 @@ __global__ __launch_bounds__(NT) void k_small_select(
     const int32_t* __restrict__ seg_n, const int32_t* __restrict__ keep,
     const int64_t* __restrict__ cap_off, const int32_t* __restrict__ small_segs,
     int2* __restrict__ pairs, float* __restrict__ vals, int32_t* __restrict__ idx_out,
-    SelState* __restrict__ st_small, uint32_t gid_base, uint32_t step, uint32_t s0, uint32_t s1) {
+    SelState* __restrict__ st_small, uint32_t gid_base, uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp) {
+  // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
+  const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t h[2048];
   __shared__ uint32_t arr[NT];
   __shared__ uint32_t scr[NT / WAVE];
@@ -255,7 +257,9 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
                                              const int2* __restrict__ tasks,
                                              const SelState* __restrict__ st,
                                              uint32_t* __restrict__ hist_all, uint32_t gid_base,
-                                             uint32_t step, uint32_t s0, uint32_t s1) {
+                                             uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp) {
+  // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
+  const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   using C = PassCfg<PASS>;
   constexpr int NB = 1 << C::BITS;
   __shared__ uint32_t h[NB];
@@ -341,7 +345,9 @@ __global__ __launch_bounds__(NT) void k_count(float* __restrict__ g, const float
                                               const int2* __restrict__ tasks,
                                               const SelState* __restrict__ st,
                                               uint2* __restrict__ cnt, uint32_t gid_base,
-                                              uint32_t step, uint32_t s0, uint32_t s1) {
+                                              uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp) {
+  // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
+  const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t scr[NT / WAVE];
   const int2 t = tasks[blockIdx.x];
   const int li = t.x, begin = t.y;
@@ -470,7 +476,9 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
                                               const int64_t* __restrict__ cap_off,
                                               int2* __restrict__ pairs, float* __restrict__ vals,
                                               int32_t* __restrict__ idx_out, uint32_t gid_base,
-                                              uint32_t step, uint32_t s0, uint32_t s1) {
+                                              uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp) {
+  // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
+  const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t scr[NT / WAVE];
   const int2 t = tasks[blockIdx.x];
   const int li = t.x, begin = t.y;
@@ -636,7 +644,9 @@ __global__ __launch_bounds__(NT) void k_quant(
     const int32_t* __restrict__ seg_n, const int32_t* __restrict__ large_segs,
     const int2* __restrict__ tasks, const int64_t* __restrict__ rec_off,
     const float* __restrict__ scale, uint32_t* __restrict__ payload, int nseg, int qstates,
-    uint32_t gid_base, uint32_t step, uint32_t tag, uint32_t s0, uint32_t s1) {
+    uint32_t gid_base, uint32_t step_arg, uint32_t tag, uint32_t s0, uint32_t s1,
+    const uint32_t* __restrict__ stepp) {
+  const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   const int2 t = tasks[blockIdx.x];
   const int li = t.x, begin = t.y;
   const int s = large_segs[li];
@@ -917,28 +927,28 @@ static void select_compress_t(const SelectArgs& a, hipStream_t st) {
   if (a.n_small > 0)
     LW_LAUNCH((k_small_select<KM, OUT, EF>), a.n_small, st, a.g, a.ef, a.seg_off, a.seg_n, a.keep,
               a.cap_off, a.small_segs, a.pairs, a.vals, a.idx_out, a.st_small, a.gid_base, a.step,
-              a.seed0, a.seed1);
+              a.seed0, a.seed1, a.step_ptr);
   if (a.n_large == 0) return;
   // a failed memset stops here; the binding's launch check reports it (hipGetLastError)
   if (hipMemsetAsync(a.hist, 0, sizeof(uint32_t) * HIST_WORDS * (size_t)a.n_large, st) != hipSuccess)
     return;
   LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
-            a.large_segs, a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1);
+            a.large_segs, a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
   LW_LAUNCH((k_select<KM, 0>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);
   LW_LAUNCH((k_hist<KM, 1, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
-            a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1);
+            a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
   LW_LAUNCH((k_select<KM, 1>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);
   LW_LAUNCH((k_hist<KM, 2, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
-            a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1);
+            a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
   LW_LAUNCH((k_select<KM, 2>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);
   LW_LAUNCH((k_count<KM, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
-            a.tasks, a.st_large, a.cnt, a.gid_base, a.step, a.seed0, a.seed1);
+            a.tasks, a.st_large, a.cnt, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
   LW_LAUNCH((k_scan<KM>), a.n_large, st, a.cnt, a.pre, a.task_lo, a.st_large, (int32_t*)nullptr);
   if (OUT == OUT_PAIRS)
     LW_LAUNCH(k_fill_tail, a.n_large, st, a.pairs, a.cap_off, a.large_segs, a.st_large);
   LW_LAUNCH((k_write<KM, OUT, EF>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
             a.tasks, a.st_large, a.pre, a.cap_off, a.pairs, a.vals, a.idx_out, a.gid_base, a.step,
-            a.seed0, a.seed1);
+            a.seed0, a.seed1, a.step_ptr);
 }
 
 void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st) {
@@ -968,10 +978,10 @@ void thresh_count(const SelectArgs& a, float V, int adaptive, bool ef, float* se
                      (const float*)segmax, a.n_large, V, adaptive);
   if (ef && !adaptive)
     LW_LAUNCH((k_count<KM_THRESH, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
-              a.large_segs, a.tasks, a.st_large, a.cnt, 0u, 0u, 0u, 0u);
+              a.large_segs, a.tasks, a.st_large, a.cnt, 0u,  0u, 0u, 0u, (const uint32_t*)nullptr);
   else
     LW_LAUNCH((k_count<KM_THRESH, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
-              a.large_segs, a.tasks, a.st_large, a.cnt, 0u, 0u, 0u, 0u);
+              a.large_segs, a.tasks, a.st_large, a.cnt, 0u,  0u, 0u, 0u, (const uint32_t*)nullptr);
   LW_LAUNCH((k_scan<KM_THRESH>), a.n_large, st, a.cnt, a.pre, a.task_lo, a.st_large, count_out);
 }
 
@@ -1002,11 +1012,11 @@ void thresh_write(const SelectArgs& a, bool ef, hipStream_t st) {
   if (ef)
     LW_LAUNCH((k_write<KM_THRESH, OUT_PAIRS, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
               a.large_segs, a.tasks, a.st_large, a.pre, a.cap_off, a.pairs, a.vals, a.idx_out, 0u,
-              0u, 0u, 0u);
+               0u, 0u, 0u, (const uint32_t*)nullptr);
   else
     LW_LAUNCH((k_write<KM_THRESH, OUT_PAIRS, false>), a.n_tasks, st, a.g, a.ef, a.seg_off,
               a.seg_n, a.large_segs, a.tasks, a.st_large, a.pre, a.cap_off, a.pairs, a.vals,
-              a.idx_out, 0u, 0u, 0u, 0u);
+              a.idx_out, 0u,  0u, 0u, 0u, (const uint32_t*)nullptr);
 }
 
 void unpack_pairs(const int2* gathered, int64_t cap_total, int ws, float* g, const int64_t* seg_off,
@@ -1036,11 +1046,11 @@ static void quant_t(const QuantArgs& a, bool ef, hipStream_t st) {
   if (ef)
     LW_LAUNCH((k_quant<Q, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks,
               a.rec_off, a.scale, a.payload, a.nseg, a.qstates, a.gid_base, a.step, a.tag, a.seed0,
-              a.seed1);
+              a.seed1, a.step_ptr);
   else
     LW_LAUNCH((k_quant<Q, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks,
               a.rec_off, a.scale, a.payload, a.nseg, a.qstates, a.gid_base, a.step, a.tag, a.seed0,
-              a.seed1);
+              a.seed1, a.step_ptr);
 }
 
 void quantize(const QuantArgs& a, int q, bool ef, hipStream_t st) {

@@ -53,6 +53,7 @@ struct SelectArgs {
   int32_t* idx_out;            // OUT_VALIDX
   // rng
   uint32_t gid_base, step, seed0, seed1;
+  const uint32_t* step_ptr;    // optional device step counter (overrides `step`; HIP graphs)
 };
 
 struct QuantArgs {
@@ -68,6 +69,7 @@ struct QuantArgs {
   float* scale;                // [S] abs-max (TernGrad) or L2 norm (QSGD)
   uint32_t* payload;           // this rank's send buffer
   uint32_t gid_base, step, tag, seed0, seed1;
+  const uint32_t* step_ptr;    // optional device step counter (overrides `step`; HIP graphs)
 };
 
 void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st);

@@ -172,7 +172,7 @@ class CompressedDDP(nn.Module):
         """Each rank restores its own residual; a checkpoint from a different world size (or
         one without residuals) restarts error feedback from zero, with a warning."""
         e = self.engine
-        e.step = int(st.get("step", 0))
+        e.set_step(int(st.get("step", 0)))
         if e.ef is None:
             return
         per = st.get("ef_per_rank")

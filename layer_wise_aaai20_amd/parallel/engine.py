@@ -29,7 +29,7 @@ import torch.distributed as dist
 from . import comm
 from .arena import Bucket, GradArena, plan_buckets
 from ..compress import reference as ref
-from ..compress.codecs import Codec, DenseCodec, make_codec
+from ..compress.codecs import Codec, DenseCodec, DenseWrap, make_codec
 from ..compress.plan import SegPlan
 
 MODES = ("layerwise", "entiremodel", "none")
@@ -98,6 +98,14 @@ class GradSyncEngine:
                                           qstates=qstates, seed=self.seed,
                                           error_feedback=self.ef is not None, wire=wire,
                                           count_exchange=self._count_exchange))
+        # device mirror of self.step for the Philox-keyed kernels (Random-K, TernGrad, QSGD):
+        # advanced by finish() on the GPU, so a replayed HIP graph of the step advances it too
+        self._dstep = (torch.zeros(1, dtype=torch.int64, device=self.device)
+                       if self.device.type == "cuda" else None)
+        for c in self.codecs:
+            c.step_t = self._dstep
+            if isinstance(c, DenseWrap):
+                c.inner.step_t = self._dstep
         self.seg_bucket = [0] * len(self.arena.segments)
         for b in self.buckets:
             for i in range(b.seg_lo, b.seg_hi):
@@ -263,6 +271,8 @@ class GradSyncEngine:
             if self.timing:
                 rec.append((bi, t0, t1, tx, t2, self._event()))
         self._pending = []
+        if self._dstep is not None:
+            self._dstep.add_(1)
         if hold and not torch.cuda.is_current_stream_capturing():
             # (under HIP-graph capture the event record / wait pairs become graph edges: there is
             # nothing to keep alive, and an event query would invalidate the capture)
@@ -290,6 +300,12 @@ class GradSyncEngine:
             self._ready[i] = True
         self._launch_in_order()
         self.finish()
+
+    def set_step(self, step: int) -> None:
+        """Set the step counter (host and device), e.g. when a checkpoint is restored."""
+        self.step = int(step)
+        if self._dstep is not None:
+            self._dstep.fill_(self.step)
 
     def graph_safe(self) -> bool:
         """Whether a whole step through this engine can be captured as one HIP graph and

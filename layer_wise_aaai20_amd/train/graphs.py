@@ -13,9 +13,11 @@ RCCL communicators and the caching allocator settle), then captures it once with
 collectives, decode, fused SGD — and afterwards every call is: copy the inputs into the captured
 buffers, write the learning rate / loss scale into the device tensor the SGD kernel reads
 (``FlatSGD.load_hyper``), replay. Anything else a capture bakes in is part of the signature
-(input shapes/dtypes, ``FlatSGD.graph_signature``); a change re-captures. Steps the capture cannot
-represent — codecs that take a host step counter (Random-K keys, stochastic quantisers) or
-synchronise — stay eager (``GradSyncEngine.graph_safe``).
+(input shapes/dtypes, ``FlatSGD.graph_signature``); a change re-captures. The Philox-keyed codecs
+(Random-K, TernGrad, QSGD) read the step counter from device memory (``GradSyncEngine._dstep``,
+advanced inside the graph), so every replay draws fresh keys. Steps the capture cannot represent
+— the threshold methods' sparse wire (a host read of the agreed capacity), gloo collectives,
+c10d RCCL calls — stay eager (``GradSyncEngine.graph_safe``).
 """
 from __future__ import annotations
 
@@ -75,6 +77,9 @@ class StepGraph:
         self.opt.load_hyper()
         graph.replay()
         self.replays += 1
+        # host mirror of what the replayed finish() did on the device (engine._dstep += 1)
+        self.engine.step += 1
+        self.engine.stats.steps += 1
         return static_out
 
     def _capture(self, inputs, sig) -> None:
@@ -83,10 +88,15 @@ class StepGraph:
         self.opt.device_hyper = True
         self.opt.load_hyper()
         torch.cuda.synchronize(self.device)
+        host_step = (self.engine.step, self.engine.stats.steps)
         graph = torch.cuda.CUDAGraph()
-        # thread_local: RCCL's watchdog thread queries events while this thread captures
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-            static_out = self.fn(*static_in)
-        torch.cuda.synchronize(self.device)
+        try:
+            # thread_local: RCCL's watchdog thread queries events while this thread captures
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                static_out = self.fn(*static_in)
+            torch.cuda.synchronize(self.device)
+        finally:
+            # the capture ran the step's Python (finish() counted a step) but no kernel
+            self.engine.step, self.engine.stats.steps = host_step
         # the capture recorded the step without running it: the caller's replay performs it
         self._g = (graph, static_in, static_out, sig)

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _trainer(graph, method="Topk", compress="layerwise"):
     torch.manual_seed(0)
     return build_trainer("resnet50", device="cuda", compress=compress, method=method, K=0.01,
-                         graph=graph)
+                         qstates=255, graph=graph)
 
 
 def _batches(n, b=8, s=64):
@@ -32,7 +32,9 @@ def _params(tr):
     return torch.cat([p.detach().float().reshape(-1) for p in tr.ddp.module.parameters()])
 
 
-@pytest.mark.parametrize("method,compress", [("Topk", "layerwise"), ("none", "none")])
+@pytest.mark.parametrize("method,compress", [("Topk", "layerwise"), ("none", "none"),
+                                             ("RandomDithering", "entiremodel"),
+                                             ("TernGrad", "layerwise")])
 def test_graph_step_matches_eager(method, compress):
     data = _batches(7)
     lrs = [0.1, 0.1, 0.1, 0.1, 0.05, 0.02, 0.2]     # LR changes after the capture
@@ -57,12 +59,35 @@ def test_graph_step_matches_eager(method, compress):
     assert err <= 2e-3 * scale, err
 
 
-def test_graph_mode_falls_back_for_step_dependent_codecs():
+def test_graph_mode_falls_back_for_host_synchronising_codecs():
+    torch.manual_seed(0)
+    tr = build_trainer("resnet50", device="cuda", compress="layerwise", method="Thresholdv",
+                       V=1e-3, wire="sparse", graph=True)
+    for x, t in _batches(5):
+        tr.step(x, t)
+    torch.cuda.synchronize()
+    assert tr.graph_replays == 0           # the sparse wire reads the agreed capacity on the host
+
+
+def test_graph_replays_advance_the_device_step():
+    """QSGD's stochastic rounding is keyed by the device step counter, advanced inside the graph;
+    the host mirror tracks it (a counter frozen at capture time would repeat one rounding pattern
+    — the parameter comparison with the eager run in test_graph_step_matches_eager would fail)."""
+    tr = _trainer(True, "RandomDithering", "entiremodel")
+    eng = tr.ddp.engine
+    for x, t in _batches(7):
+        tr.step(x, t)
+    torch.cuda.synchronize()
+    assert tr.graph_replays == 4
+    assert int(eng._dstep.item()) == eng.step == 7
+
+
+def test_random_k_stays_eager():
     tr = _trainer(True, "Randomk")
     for x, t in _batches(5):
         tr.step(x, t)
     torch.cuda.synchronize()
-    assert tr.graph_replays == 0                 # Random-K keys depend on the host step counter
+    assert tr.graph_replays == 0
 
 
 def test_graph_capture_with_rccl_collectives():

@@ -8,6 +8,9 @@ import torch  # noqa: E402
 from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer  # noqa: E402
 
 net, mode, method = sys.argv[1:4]
+if "force" in sys.argv[4:]:                 # capture even the codecs kept eager (investigation)
+    from layer_wise_aaai20_amd.compress import codecs as C
+    C.RandkSparseCodec.graph_safe = True
 runs = {}
 for graph in (False, True):
     torch.manual_seed(0)

@@ -52,11 +52,10 @@ def test_graph_step_matches_eager(method, compress):
     pg, lg, replays = runs[True]
     assert replays == 4                       # 3 eager warm-up steps, then capture + replays
     assert torch.isfinite(pg).all()
-    for a, b in zip(le, lg):
-        assert abs(a - b) <= 2e-2 * max(1.0, abs(a)), (le, lg)
-    err = (pe - pg).abs().max().item()
-    scale = pe.abs().max().item()
-    assert err <= 2e-3 * scale, err
+    # every kernel of the step is deterministic (fixed-order reductions, no atomics on the
+    # gradient path): the replayed step is bit-identical to the eager one
+    assert le == lg, (le, lg)
+    assert torch.equal(pe, pg), (pe - pg).abs().max().item()
 
 
 def test_graph_mode_falls_back_for_host_synchronising_codecs():

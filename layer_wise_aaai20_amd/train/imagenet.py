@@ -109,7 +109,7 @@ def build_model(name: str = "resnet50", bn0: bool = False) -> nn.Module:
 def build_trainer(model="resnet50", device=None, compress="layerwise", method="Topk", K=0.001,
                   V=1e-3, qstates=255, error_feedback=False, bucket_cap_mb=25.0, dtype="bf16",
                   fused=True, momentum=0.9, weight_decay=1e-4, no_bn_wd=True, lr=0.1,
-                  bn0=True, wire="auto", graph=None) -> ImageNetTrainer:
+                  bn0=True, wire="auto", graph=None, graph_warmup: int = 3) -> ImageNetTrainer:
     device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     net = build_model(model, bn0=bn0) if isinstance(model, str) else model
     if fused:
@@ -127,4 +127,4 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
                   weight_decay=weight_decay)
     tdtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype] \
         if isinstance(dtype, str) else dtype
-    return ImageNetTrainer(ddp, opt, device, tdtype, graph=graph)
+    return ImageNetTrainer(ddp, opt, device, tdtype, graph=graph, graph_warmup=graph_warmup)

@@ -151,10 +151,10 @@ def main():
                        K=args.ratio, V=args.threshold, qstates=args.qstates,
                        error_feedback=args.ef, bucket_cap_mb=args.bucket_mb, dtype=args.dtype,
                        fused=not args.no_fused, momentum=0.9, weight_decay=1e-4, no_bn_wd=True,
-                       lr=0.1, graph=args.graph == "on" and args.warmup > 0,
-                       # capture inside the untimed warm-up whatever W is: eager steps (tile tuner,
-                       # allocator, RCCL warm) then capture + at least one replay before timing
-                       graph_warmup=max(0, min(3, args.warmup - 2)))
+                       lr=0.1, graph=args.graph == "on" and args.warmup >= 2,
+                       # capture inside the untimed warm-up: at least one eager step (tile tuner,
+                       # lazily built device tables, allocator, RCCL warm), then capture + replay
+                       graph_warmup=max(1, min(3, args.warmup - 1)))
     B, S = args.batch, args.image_size
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)

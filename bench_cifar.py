@@ -32,8 +32,8 @@ V100_ANCHOR = 16500.0    # img/s, derived in BASELINE.md
 def run(name, steps, warmup, world, rank, dev, graph=True):
     from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
     cfg = CONFIGS[name]
-    tr = CifarTrainer(device=dev, n_train=512 * 12, graph=graph and warmup > 0, **cfg)
-    tr.graphed.warmup = max(0, min(3, warmup - 2))    # capture inside the untimed warm-up
+    tr = CifarTrainer(device=dev, n_train=512 * 12, graph=graph and warmup >= 2, **cfg)
+    tr.graphed.warmup = max(1, min(3, warmup - 1))    # capture inside the untimed warm-up
     for _ in range(warmup):
         tr.step()
     torch.cuda.synchronize()

@@ -103,7 +103,9 @@ class GemmTuner:
         t = self.best.get(key)
         if t is not None:
             return t
-        if not self.enabled or torch.cuda.is_current_stream_capturing():
+        if torch.cuda.is_current_stream_capturing():
+            return 0                  # no timing inside a graph capture; tune on the next eager call
+        if not self.enabled:
             self.best[key] = 0
             return 0
         times = []

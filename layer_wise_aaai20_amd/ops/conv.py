@@ -65,7 +65,9 @@ class ConvTuner:
         c = self.best.get(key)
         if c is not None:
             return c
-        if not self.enabled or len(candidates) == 1 or torch.cuda.is_current_stream_capturing():
+        if torch.cuda.is_current_stream_capturing():
+            return default            # no timing inside a graph capture; tune on the next eager call
+        if not self.enabled or len(candidates) == 1:
             self.best[key] = default
             return default
         times = []

@@ -58,7 +58,9 @@ class LinearTuner:
         if c is not None:
             return c
         default = (0, _splits(tiles_of(128, 128), K))
-        if not self.enabled or torch.cuda.is_current_stream_capturing():
+        if torch.cuda.is_current_stream_capturing():
+            return default            # no timing inside a graph capture; tune on the next eager call
+        if not self.enabled:
             self.best[key] = default
             return default
         times = []

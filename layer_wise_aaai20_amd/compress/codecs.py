@@ -235,10 +235,11 @@ class RandkSparseCodec(TopkCodec):
     """Random-K with explicit indices (masks need not be rank-coherent)."""
     name = "randk-sparse"
     km = KM_RANDK
-    # Kept eager: with the device step counter the layer-wise Random-K step replays bit-exactly,
-    # but the entire-model (single 6.6 M-element segment) + EF replay diverged from the eager
-    # step from the second replay on (duplicate slots: scripts/probes/graph_vs_eager_probe.py,
-    # profiles/r2_randk_graph_divergence.log) — not captured until that is understood.
+    # Kept eager: the entire-model (single 6.6 M-element segment) + EF replay diverges from the
+    # eager step from the second replay on, deterministically, whether the graph compresses on a
+    # side stream or inline, while eager side-stream and eager inline runs agree bit for bit
+    # (scripts/probes/graph_vs_eager_probe.py, profiles/r2_randk_graph_divergence.log). Layer-wise
+    # Random-K replays exactly; not captured until the entire-model case is understood.
     graph_safe = False
 
     def __init__(self, plan, world, rank, K, seed=0, error_feedback=False):

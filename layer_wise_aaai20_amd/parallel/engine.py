@@ -120,6 +120,7 @@ class GradSyncEngine:
         overlap_compress = overlap_compress and os.environ.get("LWAAAI_OVERLAP", "1") != "0"
         self._side = (torch.cuda.Stream(device=self.device)
                       if overlap_compress and self.device.type == "cuda" else None)
+        self._graph_overlap = os.environ.get("LWAAAI_GRAPH_OVERLAP", "0") == "1"
         self._retired = []            # (fence event, events held until it completes)
         self._check = os.environ.get("LWAAAI_ENGINE_CHECK", "0") == "1"
         # bucket collectives on a native RCCL communicator (csrc/rccl.cpp) when the group is
@@ -215,6 +216,12 @@ class GradSyncEngine:
         g = self.arena.grad[b.start:b.end]
         e = self.ef[b.start:b.end] if self.ef is not None else None
         side = self._side
+        if side is not None and not self._graph_overlap and \
+                torch.cuda.is_current_stream_capturing():
+            # inside a captured step the side-stream branch costs more than it hides (ResNet-50,
+            # 1 GPU: 24.67 ms/step with it, 24.17 ms without; profiles/r2_graph_overlap_ab.log):
+            # the bucket is compressed and exchanged inline on the compute stream
+            side = None
         ready = None
         if side is not None:
             # the event must outlive the side stream's wait on it: it stays in _pending until

@@ -12,10 +12,13 @@ if "force" in sys.argv[4:]:                 # capture even the codecs kept eager
     from layer_wise_aaai20_amd.compress import codecs as C
     C.RandkSparseCodec.graph_safe = True
 runs = {}
+ab = "overlap-ab" in sys.argv[4:]     # eager with the side stream vs eager inline instead
 for graph in (False, True):
+    if ab:
+        os.environ["LWAAAI_OVERLAP"] = "0" if graph else "1"
     torch.manual_seed(0)
     tr = CifarTrainer(net, compress=mode, method=method, K=0.05, error_feedback=True,
-                      batch_size=128, n_train=2560, graph=graph)
+                      batch_size=128, n_train=2560, graph=graph and not ab)
     hist = []
     for i in range(8):
         loss = float(tr.step())

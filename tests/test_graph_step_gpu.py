@@ -16,10 +16,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _trainer(graph, method="Topk", compress="layerwise"):
+def _trainer(graph, method="Topk", compress="layerwise", ef=False):
     torch.manual_seed(0)
     return build_trainer("resnet50", device="cuda", compress=compress, method=method, K=0.01,
-                         qstates=255, graph=graph)
+                         qstates=255, error_feedback=ef, graph=graph)
 
 
 def _batches(n, b=8, s=64):
@@ -32,15 +32,17 @@ def _params(tr):
     return torch.cat([p.detach().float().reshape(-1) for p in tr.ddp.module.parameters()])
 
 
-@pytest.mark.parametrize("method,compress", [("Topk", "layerwise"), ("none", "none"),
-                                             ("RandomDithering", "entiremodel"),
-                                             ("TernGrad", "layerwise")])
-def test_graph_step_matches_eager(method, compress):
+@pytest.mark.parametrize("method,compress,ef", [("Topk", "layerwise", False),
+                                                ("none", "none", False),
+                                                ("Topk", "entiremodel", True),
+                                                ("RandomDithering", "entiremodel", False),
+                                                ("TernGrad", "layerwise", True)])
+def test_graph_step_matches_eager(method, compress, ef):
     data = _batches(7)
     lrs = [0.1, 0.1, 0.1, 0.1, 0.05, 0.02, 0.2]     # LR changes after the capture
     runs = {}
     for graph in (False, True):
-        tr = _trainer(graph, method, compress)
+        tr = _trainer(graph, method, compress, ef)
         losses = []
         for (x, t), lr in zip(data, lrs):
             for grp in tr.opt.param_groups:

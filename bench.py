@@ -205,7 +205,7 @@ def main():
     value = world * B * args.steps / dt
     stats = tr.ddp.sync_stats()
     default = (args.model == "resnet50" and args.compress == "layerwise" and args.method == "Topk"
-               and args.ratio == 0.001)
+               and args.ratio == 0.001 and not args.ef)
     metric = BASELINE_METRIC if default else (
         f"images/sec/node, {args.model} {args.compress} {args.method}"
         f"{' K=' + str(args.ratio) if args.method in ('Topk', 'Randomk') else ''}"

@@ -330,6 +330,32 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tens
   launched("sgd_step");
 }
 
+void cifar_augment(Tensor data, Tensor idx, Tensor prm, int64_t offset, int64_t crop,
+                   int64_t cutout, Tensor out) {
+  const c10::DeviceGuard guard(data.device());
+  check_cuda(data, "data");
+  check_cuda(idx, "idx");
+  check_cuda(prm, "prm");
+  check_dtype(data, at::kFloat, "data");
+  check_dtype(idx, at::kLong, "idx");
+  check_dtype(prm, at::kInt, "prm");
+  TORCH_CHECK(data.dim() == 4 && prm.dim() == 2 && prm.size(1) == 5, "cifar_augment: shapes");
+  const int64_t B = idx.numel(), C = data.size(1), Hp = data.size(2), Wp = data.size(3);
+  TORCH_CHECK(crop >= 1 && crop <= Hp && crop <= Wp && cutout >= 0 && cutout <= crop,
+              "cifar_augment: crop / cutout out of range");
+  TORCH_CHECK(offset >= 0 && offset + B <= prm.size(0), "cifar_augment: choice rows out of range");
+  TORCH_CHECK(out.is_cuda() && out.dim() == 4 && out.size(0) == B && out.size(1) == C &&
+                  out.size(2) == crop && out.size(3) == crop &&
+                  out.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "cifar_augment: out must be a channels_last [B, C, crop, crop] GPU tensor");
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16,
+              "cifar_augment: out must be float32 or bfloat16");
+  lw::cifar_augment(ptr<float>(data), ptr<int64_t>(idx), ptr<int32_t>(prm), out.data_ptr(),
+                    (int)B, (int)C, (int)Hp, (int)Wp, (int)crop, (int)cutout, offset,
+                    out.scalar_type() == at::kBFloat16, cur_stream());
+  launched("cifar_augment");
+}
+
 void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<double> stdv) {
   const c10::DeviceGuard guard(in.device());
   check_cuda(in, "in");
@@ -1251,6 +1277,8 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
       "int nesterov, int first_step, float grad_scale, Tensor? hyper=None) -> ()");
   m.def("normalize_u8(Tensor input, Tensor(a!) out, float[] mean, float[] std) -> ()");
+  m.def("cifar_augment(Tensor data, Tensor idx, Tensor prm, int offset, int crop, int cutout, "
+        "Tensor(a!) out) -> ()");
   m.def("gap_fwd(Tensor x) -> Tensor");
   m.def("relu_bias_bwd(Tensor dy, Tensor? y, Tensor(a!)? db_out) -> (Tensor, Tensor)");
   m.def("xent(Tensor logits, Tensor target, float gscale, int ignore_index, bool want_grad) "
@@ -1308,6 +1336,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("dequantize", &dequantize);
   m.impl("sgd_step", &sgd_step);
   m.impl("normalize_u8", &normalize_u8);
+  m.impl("cifar_augment", &cifar_augment);
   m.impl("gap_fwd", &gap_fwd);
   m.impl("relu_bias_bwd", &relu_bias_bwd);
   m.impl("xent", &xent);

@@ -200,6 +200,14 @@ class GPUBatches:
         self.seed = seed
         self.channels_last = channels_last
         self.dtype = dtype
+        # GPU: crop / flip / cutout + NHWC layout + dtype cast in one HIP kernel per batch
+        # (csrc/augment.hip); False keeps the torch gather path (the reference-shaped fallback)
+        self.use_kernel = True
+
+    def _kernel_ok(self) -> bool:
+        return (self.use_kernel and self.augment and self.data.is_cuda and self.channels_last and
+                self.data.dtype == torch.float32 and self.data.dim() == 4 and
+                self.data.is_contiguous() and self.dtype in (torch.float32, torch.bfloat16))
 
     def _indices(self):
         n = self.data.shape[0]
@@ -227,11 +235,22 @@ class GPUBatches:
             cx = torch.randint(0, cspan, (n,), generator=g).to(dev)
             cy = torch.randint(0, cspan, (n,), generator=g).to(dev)
         self.epoch += 1
+        kern = self._kernel_ok()
+        if kern:
+            from ..ops._ext import load
+            lib = load()
+            prm = torch.stack([x0, y0, flip.to(x0.dtype), cx, cy], 1).to(torch.int32).contiguous()
         bs = self.batch_size
         stop = (n // bs) * bs if self.drop_last else n
         ar = torch.arange(self.crop, device=dev)
         for s in range(0, stop, bs):
             b = idx[s:s + bs]
+            if kern:
+                x = torch.empty((b.numel(), self.data.shape[1], self.crop, self.crop),
+                                dtype=self.dtype, device=dev, memory_format=torch.channels_last)
+                lib.cifar_augment(self.data, b.contiguous(), prm, s, self.crop, self.cutout, x)
+                yield {"input": x, "target": self.labels[b]}
+                continue
             x = self.data[b]
             if self.augment:
                 sl = slice(s, s + b.numel())

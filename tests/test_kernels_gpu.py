@@ -234,3 +234,25 @@ def test_threshold_dense_in_place_matches_cpu(adaptive, with_ef):
     if with_ef:
         assert torch.equal(eg.cpu(), ec)
     assert 0 < int((gc != 0).sum()) < gc.numel()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cifar_augment_kernel_matches_torch_gathers(dtype):
+    """csrc/augment.hip (random crop + flip + cutout into a channels_last batch) against the
+    torch gather path of GPUBatches with the same per-epoch choices."""
+    from layer_wise_aaai20_amd.data.cifar import GPUBatches
+    torch.manual_seed(0)
+    data = torch.randn(300, 3, 40, 40, device="cuda")
+    labels = torch.randint(0, 10, (300,), device="cuda")
+    outs = []
+    for kern in (True, False):
+        gb = GPUBatches(data, labels, 64, shuffle=True, augment=True, seed=5,
+                        channels_last=True, dtype=dtype)
+        gb.use_kernel = kern
+        assert gb._kernel_ok() == kern
+        outs.append([(b["input"], b["target"]) for b in gb])
+    assert len(outs[0]) == len(outs[1]) == 5
+    for (xk, tk), (xt, tt) in zip(*outs):
+        assert xk.is_contiguous(memory_format=torch.channels_last) and xk.dtype == dtype
+        assert torch.equal(tk, tt)
+        assert torch.equal(xk, xt)

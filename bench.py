@@ -63,7 +63,10 @@ def parse():
     ap.add_argument("--threshold", "-V", type=float, default=0.001)
     ap.add_argument("--qstates", "-Q", type=int, default=255)
     ap.add_argument("--ef", action="store_true", help="error feedback")
-    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    # 50 MB: 3 buckets for ResNet-50's 97.5 MiB fp32 arena. Inside a captured step each bucket is
+    # compressed + exchanged inline, so fewer buckets = fewer launches / collectives: 24.29 ms
+    # vs 24.47-24.50 ms at the reference's 25 MB (profiles/r2_bucket_mb_graph.log)
+    ap.add_argument("--bucket-mb", type=float, default=50.0)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-fused", action="store_true", help="disable fused HIP nn kernels")
     ap.add_argument("--json-out", default="")

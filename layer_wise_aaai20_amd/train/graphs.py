@@ -22,6 +22,7 @@ c10d RCCL calls — stay eager (``GradSyncEngine.graph_safe``).
 from __future__ import annotations
 
 import os
+import time
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -46,6 +47,16 @@ class StepGraph:
         self.replays = 0
         self._eager_done = 0
         self._g = None        # (graph, static inputs, static outputs, signature)
+        # find-style choice on one rank: the last eager warm-up steps and the first replays are
+        # timed and the graph is dropped if it is not faster (a GPU-bound step whose side-stream
+        # overlap outweighs the saved launches, e.g. VGG-16: 5.96 ms eager vs 6.08 ms graph).
+        # Multi-rank jobs keep the graph (one decision for every rank, no extra collective).
+        self.auto = os.environ.get("LWAAAI_GRAPH_AUTO", "1") != "0"
+        self.decided = False
+        self._eager_ms = []
+        self._t0 = 0.0
+        self._replay_t0 = None
+        self._timed_replays = 0
 
     def active(self) -> bool:
         return self.enabled and self.engine.graph_safe()
@@ -61,7 +72,14 @@ class StepGraph:
         if self._g is None or self._g[-1] != sig:
             if self._eager_done < self.warmup:
                 self._eager_done += 1
-                return self.fn(*inputs)
+                # steady-state eager rate: the last two warm-up steps timed back to back
+                deciding = self.warmup >= 3 and self._deciding()
+                if deciding and self._eager_done == self.warmup - 1:
+                    self._t0 = self._sync_time()
+                out = self.fn(*inputs)
+                if deciding and self._eager_done == self.warmup:
+                    self._eager_ms = [(self._sync_time() - self._t0) / 2]
+                return out
             try:
                 self._capture(inputs, sig)
             except RuntimeError as e:          # capture unsupported here: stay eager
@@ -72,15 +90,37 @@ class StepGraph:
                 print(f"[lwaaai] HIP-graph capture failed, running eagerly: {e}", flush=True)
                 return self.fn(*inputs)
         graph, static_in, static_out, _ = self._g
+        timing = self._deciding() and bool(self._eager_ms)
+        if timing and self._replay_t0 is None:
+            self._replay_t0 = self._sync_time()       # first two replays timed back to back
         for dst, src in zip(static_in, inputs):
             dst.copy_(src, non_blocking=True)
         self.opt.load_hyper()
         graph.replay()
         self.replays += 1
+        if timing:
+            self._timed_replays += 1
+            if self._timed_replays == 2:
+                graph_ms = (self._sync_time() - self._replay_t0) / 2
+                self.decided = True
+                if graph_ms > self._eager_ms[0]:
+                    # not faster than launching from Python on this host: stay eager
+                    self.enabled = False
+                    self._g = None
+                    print(f"[lwaaai] HIP-graph step {graph_ms:.2f} ms vs eager "
+                          f"{self._eager_ms[0]:.2f} ms: staying eager", flush=True)
         # host mirror of what the replayed finish() did on the device (engine._dstep += 1)
         self.engine.step += 1
         self.engine.stats.steps += 1
         return static_out
+
+    def _deciding(self) -> bool:
+        return self.auto and not self.decided and getattr(self.engine, "world", 1) == 1
+
+    def _sync_time(self) -> float:
+        """Milliseconds on the host clock after the device has drained."""
+        torch.cuda.synchronize(self.device)
+        return time.perf_counter() * 1e3
 
     def _capture(self, inputs, sig) -> None:
         self._g = None

@@ -13,6 +13,13 @@ import torch
 from layer_wise_aaai20_amd.train.imagenet import build_trainer
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _always_graph(monkeypatch):
+    # these tests compare the replayed step with the eager one: keep the graph even where the
+    # find-style timing (train/graphs.py StepGraph.auto) would fall back to eager
+    monkeypatch.setenv("LWAAAI_GRAPH_AUTO", "0")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 

@@ -67,7 +67,7 @@ def main():
     ap.add_argument("--config", default="all", choices=["all"] + list(CONFIGS))
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--graph", default="on", choices=["on", "off"],
+    ap.add_argument("--graph", default="off", choices=["on", "off"],
                     help="capture the whole step as one HIP graph after 3 eager steps")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))

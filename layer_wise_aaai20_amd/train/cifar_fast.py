@@ -9,6 +9,7 @@ CompressedDDP (compression overlapped with backward) and the fused flat-arena SG
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -61,6 +62,8 @@ class CifarTrainer:
         self.last = None
         # whole step as one HIP graph after 3 eager steps (train/graphs.py): at 1.5-6 ms per
         # step the per-kernel host launch cost is a large share of an eager CIFAR step
+        if graph is None:          # opt-in for the CIFAR trainer (see README: graph coverage)
+            graph = os.environ.get("LWAAAI_CIFAR_GRAPH", "0") == "1"
         self.graphed = StepGraph(self._eager, self.ddp.engine, self.opt, self.device, 3, graph)
 
     def next_batch(self):

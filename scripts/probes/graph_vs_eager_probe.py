@@ -20,7 +20,7 @@ for graph in (False, True):
     tr = CifarTrainer(net, compress=mode, method=method, K=0.05, error_feedback=True,
                       batch_size=128, n_train=2560, graph=graph and not ab)
     hist = []
-    for i in range(8):
+    for i in range(int(os.environ.get("PROBE_STEPS", "8"))):
         loss = float(tr.step())
         torch.cuda.synchronize()
         eng = tr.ddp.engine

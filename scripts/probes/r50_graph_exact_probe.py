@@ -9,7 +9,7 @@ from layer_wise_aaai20_amd.train.imagenet import build_trainer  # noqa: E402
 method, mode = sys.argv[1], sys.argv[2]
 g = torch.Generator(device="cuda").manual_seed(3)
 data = [(torch.randint(0, 256, (16, 96, 96, 3), dtype=torch.uint8, device="cuda", generator=g),
-         torch.randint(0, 1000, (16,), device="cuda", generator=g)) for _ in range(8)]
+         torch.randint(0, 1000, (16,), device="cuda", generator=g)) for _ in range(int(os.environ.get("PROBE_STEPS", "8")))]
 runs = {}
 for graph in (False, True):
     torch.manual_seed(0)

@@ -20,6 +20,7 @@ def _always_graph(monkeypatch):
     # these tests compare the replayed step with the eager one: keep the graph even where the
     # find-style timing (train/graphs.py StepGraph.auto) would fall back to eager
     monkeypatch.setenv("LWAAAI_GRAPH_AUTO", "0")
+    monkeypatch.setenv("LWAAAI_GRAPH_ENTIRE", "1")      # the exactness tests cover entire-model
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 

@@ -11,8 +11,11 @@ from layer_wise_aaai20_amd.utils.logging import PiecewiseLinear  # noqa: E402
 method, mode = sys.argv[1], sys.argv[2]
 torch.manual_seed(0)
 tr = CifarTrainer("resnet9", compress=mode, method=method, error_feedback=True, batch_size=128,
-                  epochs=2, n_train=12800, seed=0, K=0.01)
+                  epochs=2, n_train=12800, seed=0, K=0.01,
+                  graph=os.environ.get("PROBE_GRAPH", "1") == "1")
 tr.steps_per_epoch = 1
+if os.environ.get("PROBE_TORCH_AUG") == "1":
+    tr.batches.use_kernel = False
 tr.sched = PiecewiseLinear([0, 40, 200], [0, 0.4, 0])
 ls = []
 sync_each = os.environ.get("PROBE_SYNC") == "1"

@@ -19,9 +19,19 @@ if os.environ.get("PROBE_TORCH_AUG") == "1":
 tr.sched = PiecewiseLinear([0, 40, 200], [0, 0.4, 0])
 ls = []
 sync_each = os.environ.get("PROBE_SYNC") == "1"
+keep = [] if os.environ.get("PROBE_KEEP") == "1" else None    # never free the batch tensors
 for i in range(40):
     if sync_each:
         torch.cuda.synchronize()
-    ls.append(float(tr.step()) / tr.bs)
+    if keep is not None:
+        b = tr.next_batch()
+        if os.environ.get("PROBE_SYNC_AFTER_BATCH") == "1":
+            torch.cuda.synchronize()
+        if os.environ.get("PROBE_PRINT_STREAM") == "1" and i < 6:
+            print("stream", torch.cuda.current_stream(), flush=True)
+        keep.append(b)
+        ls.append(float(tr.step(b)) / tr.bs)
+    else:
+        ls.append(float(tr.step()) / tr.bs)
 print("graph", tr.graphed.enabled, "replays", tr.graphed.replays, "decided", tr.graphed.decided)
 print(" ".join(f"{v:.2f}" for v in ls))

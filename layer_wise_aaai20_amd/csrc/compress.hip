@@ -922,6 +922,19 @@ __global__ __launch_bounds__(NT) void k_unpack_validx(const float* __restrict__ 
 #define LW_LAUNCH(kern, grid, stream, ...) \
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), 0, stream, __VA_ARGS__)
 
+// Histogram reset as a kernel of our own, NOT hipMemsetAsync: inside a replayed HIP graph the
+// runtime's memset node (the __amd_rocclr_fillBufferAligned blit) was seen to fill this buffer with
+// a non-zero periodic pattern after a few replays (bin sums 2:1:1 across the 2048/1024/1024-bin
+// pass regions, i.e. a repeated garbage word pattern, on top of which k_hist added its counts),
+// which made the radix select pick a threshold no key reached: nothing was sent and the error
+// feedback kept the whole gradient (scripts/probes/replay_bisect.py,
+// profiles/r3_graph_divergence_root_cause.md). Stream-ordered kernels only, here and everywhere
+// else on the captured path.
+__global__ __launch_bounds__(NT) void k_zero_words(uint32_t* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
+    p[i] = 0u;
+}
+
 template <int KM, int OUT, bool EF>
 static void select_compress_t(const SelectArgs& a, hipStream_t st) {
   if (a.n_small > 0)
@@ -929,9 +942,11 @@ static void select_compress_t(const SelectArgs& a, hipStream_t st) {
               a.cap_off, a.small_segs, a.pairs, a.vals, a.idx_out, a.st_small, a.gid_base, a.step,
               a.seed0, a.seed1, a.step_ptr);
   if (a.n_large == 0) return;
-  // a failed memset stops here; the binding's launch check reports it (hipGetLastError)
-  if (hipMemsetAsync(a.hist, 0, sizeof(uint32_t) * HIST_WORDS * (size_t)a.n_large, st) != hipSuccess)
-    return;
+  {
+    const int64_t words = (int64_t)HIST_WORDS * a.n_large;
+    const int64_t nb = (words + NT - 1) / NT;
+    LW_LAUNCH(k_zero_words, (int)(nb < 1024 ? nb : 1024), st, a.hist, words);
+  }
   LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
             a.large_segs, a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
   LW_LAUNCH((k_select<KM, 0>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);

@@ -152,18 +152,23 @@ class CompressedDDP(nn.Module):
 
     # checkpoint extras: per-rank error-feedback residuals and the step counter (extra keys that
     # reference readers ignore; SURVEY.md §5 checkpoint row)
-    def compression_state(self) -> dict:
+    def compression_state(self, dst: int = 0) -> dict:
         """Collective (call on every rank): the step counter and EVERY rank's error-feedback
         residual, ``ef_per_rank[r]`` = rank r's buffer (each rank's residual is its own
-        compression error, so restoring rank 0's everywhere would bias the resumed run)."""
+        compression error, so restoring rank 0's everywhere would bias the resumed run).
+        The residuals are gathered to the checkpoint writer ``dst`` only (group rank); on every
+        other rank ``ef_per_rank`` is None, so no rank but the writer holds world x |arena|."""
         e = self.engine
         st = {"step": e.step, "world": e.world, "ef_per_rank": None}
         if e.ef is not None:
-            ef = e.ef.detach()
+            ef = e.ef.detach().contiguous()
             if e.world > 1 and dist.is_available() and dist.is_initialized():
-                parts = [torch.empty_like(ef) for _ in range(e.world)]
-                dist.all_gather(parts, ef.contiguous(), group=e.pg)
-                st["ef_per_rank"] = torch.stack(parts).cpu()
+                mine = e.rank == dst
+                parts = [torch.empty_like(ef) for _ in range(e.world)] if mine else None
+                gdst = dist.get_global_rank(e.pg, dst) if e.pg is not None else dst
+                dist.gather(ef, parts, dst=gdst, group=e.pg)
+                if mine:
+                    st["ef_per_rank"] = torch.stack([p.cpu() for p in parts])
             else:
                 st["ef_per_rank"] = ef.clone()[None].cpu()
         return st

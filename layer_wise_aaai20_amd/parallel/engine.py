@@ -84,6 +84,9 @@ class GradSyncEngine:
         self.seed = int(seed)
         self.ef = torch.zeros_like(self.arena.grad) if (error_feedback and
                                                        self.method != "none") else None
+        # what a peer needs to build this engine's codecs for another rank (loopback tests)
+        self.codec_kw = dict(K=K, V=V, qstates=qstates, seed=self.seed,
+                             error_feedback=self.ef is not None, wire=wire)
         self.codecs: List[Codec] = []
         self.plans: List[SegPlan] = []
         for b in self.buckets:
@@ -94,10 +97,9 @@ class GradSyncEngine:
                 plan = SegPlan([s.offset - b.start for s in segs], [s.numel for s in segs],
                                gid_base=b.seg_lo)
             self.plans.append(plan)
-            self.codecs.append(make_codec(self.method, plan, self.world, self.rank, K=K, V=V,
-                                          qstates=qstates, seed=self.seed,
-                                          error_feedback=self.ef is not None, wire=wire,
-                                          count_exchange=self._count_exchange))
+            self.codecs.append(make_codec(self.method, plan, self.world, self.rank,
+                                          count_exchange=self._count_exchange,
+                                          **self.codec_kw))
         # device mirror of self.step for the Philox-keyed kernels (Random-K, TernGrad, QSGD):
         # advanced by finish() on the GPU, so a replayed HIP graph of the step advances it too
         self._dstep = (torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -158,6 +160,17 @@ class GradSyncEngine:
                 f"rank {self.rank}: gradient bucket plans differ across ranks (signature "
                 f"{mine.tolist()} vs min {lo.tolist()} / max {hi.tolist()}): the model, the "
                 f"compression settings or the bucket size are not identical on every rank")
+
+    def use_communicator(self, native) -> None:
+        """Route the bucket collectives through ``native`` (a :class:`~.comm.NativeRccl`-like
+        object: stream-ordered ``all_gather(out, inp)`` / ``all_reduce(t)`` / ``broadcast``),
+        e.g. the single-GPU :class:`~.loopback.LoopbackRccl` that stands in for a world of W
+        ranks. Its world size must be the one the codecs were built for."""
+        w = getattr(native, "world", self.world)
+        if w != self.world:
+            raise ValueError(f"communicator world {w} != engine world {self.world}")
+        self._native = native
+        self._stream_waitable = True
 
     # ----------------------------------------------------------------- state machine
     def _reset_state(self):

@@ -7,23 +7,31 @@ ResNet-50: 27.6 ms wall for 24.6 ms of kernels on one box, ``profiles/r2_head3_s
 The reference has no counterpart (it launches per-op CUDA kernels and per-tensor NCCL calls from
 Python, ``IMAGENET/training/train_imagenet_nv.py:388-441``, ``CIFAR10/core.py:175-301``).
 
-:class:`StepGraph` runs a step closure eagerly for ``warmup`` calls (GEMM tile tuner, workspaces,
-RCCL communicators and the caching allocator settle), then captures it once with
-``torch.cuda.graph`` — forward, backward with the side-stream compression and the bucket
-collectives, decode, fused SGD — and afterwards every call is: copy the inputs into the captured
-buffers, write the learning rate / loss scale into the device tensor the SGD kernel reads
-(``FlatSGD.load_hyper``), replay. Anything else a capture bakes in is part of the signature
-(input shapes/dtypes, ``FlatSGD.graph_signature``); a change re-captures. The Philox-keyed codecs
-(Random-K, TernGrad, QSGD) read the step counter from device memory (``GradSyncEngine._dstep``,
-advanced inside the graph), so every replay draws fresh keys. Steps the capture cannot represent
-— the threshold methods' sparse wire (a host read of the agreed capacity), gloo collectives,
-c10d RCCL calls — stay eager (``GradSyncEngine.graph_safe``).
+:class:`StepGraph` keeps one captured graph per step *signature* (input shapes / dtypes / strides
+plus everything the optimizer bakes into its launch, ``FlatSGD.graph_signature``). A signature is
+run eagerly for ``warmup`` calls (GEMM tile tuner, workspaces, RCCL communicators and the caching
+allocator settle for exactly these shapes), then captured once with ``torch.cuda.graph`` — forward,
+backward with the bucket compression and collectives, decode, fused SGD — and every later call with
+that signature is: copy the inputs into the captured buffers, write the learning rate / loss scale
+into the device tensor the SGD kernel reads (``FlatSGD.load_hyper``), replay. An epoch's odd-sized
+last batch therefore never evicts the full-size graph; it stays eager until it has been seen
+``warmup`` times. The Philox-keyed codecs (Random-K, TernGrad, QSGD) read the step counter from
+device memory (``GradSyncEngine._dstep``, advanced inside the graph), so every replay draws fresh
+keys. Steps the capture cannot represent — gloo collectives, per-bucket timing — stay eager
+(``GradSyncEngine.graph_safe``).
+
+Graph-vs-eager choice (``auto``, MIOpen-find style): once per run, after the first capture, the
+first replay (which pays the one-time graph upload) is discarded, ``timed`` replays are timed back
+to back and compared with the last ``timed`` eager warm-up steps; the graph is dropped when it is
+not faster. At world > 1 every rank measures and the sums are all-reduced, so all ranks take the
+same decision (a rank replaying while another runs eagerly would still pair its collectives
+correctly, but the step would then be as slow as the slowest mode).
 """
 from __future__ import annotations
 
 import os
 import time
-from typing import Callable, Optional, Sequence
+from typing import Callable, Dict, Optional, Sequence
 
 import torch
 
@@ -33,8 +41,10 @@ def graphs_enabled(default: bool = True) -> bool:
 
 
 class StepGraph:
+    MAX_GRAPHS = 4            # distinct captured signatures kept (LRU beyond that)
+
     def __init__(self, fn: Callable, engine, optimizer, device, warmup: int = 3,
-                 enabled: Optional[bool] = None):
+                 enabled: Optional[bool] = None, auto: Optional[bool] = None, timed: int = 5):
         self.fn = fn
         self.engine = engine
         self.opt = optimizer
@@ -45,19 +55,20 @@ class StepGraph:
         self.enabled = (bool(enabled) and self.device.type == "cuda" and
                         hasattr(optimizer, "load_hyper"))
         self.replays = 0
-        self._eager_done = 0
-        self._g = None        # (graph, static inputs, static outputs, signature)
-        # find-style choice on one rank: the last eager warm-up steps and the first replays are
-        # timed and the graph is dropped if it is not faster (a GPU-bound step whose side-stream
-        # overlap outweighs the saved launches, e.g. VGG-16: 5.96 ms eager vs 6.08 ms graph).
-        # Multi-rank jobs keep the graph (one decision for every rank, no extra collective).
-        self.auto = os.environ.get("LWAAAI_GRAPH_AUTO", "1") != "0"
-        self.decided = False
-        self._eager_ms = []
-        self._t0 = 0.0
-        self._replay_t0 = None
-        self._timed_replays = 0
+        self.captures = 0
+        self._graphs: Dict[tuple, tuple] = {}     # signature -> (graph, static_in, static_out)
+        self._seen: Dict[tuple, int] = {}         # signature -> eager calls so far
+        if auto is None:
+            auto = os.environ.get("LWAAAI_GRAPH_AUTO", "1") != "0"
+        self.auto = bool(auto)
+        self.timed = max(1, int(timed))
+        self.decided = not self.auto
+        self._eager_t = []        # host ms of consecutive eager steps (device drained)
+        self._replay_t = []
+        self._t_last = None
+        self.choice = None        # (graph ms, eager ms) of the decision, for the logs
 
+    # ------------------------------------------------------------------ policy
     def active(self) -> bool:
         return self.enabled and self.engine.graph_safe()
 
@@ -65,71 +76,102 @@ class StepGraph:
         return (tuple((tuple(t.shape), t.dtype, t.stride()) for t in inputs),
                 self.opt.graph_signature())
 
+    @property
+    def _g(self):
+        """The most recently used captured graph (compatibility with older callers/tests)."""
+        return next(reversed(self._graphs.values())) if self._graphs else None
+
     def __call__(self, *inputs: torch.Tensor):
         if not self.active():
             return self.fn(*inputs)
         sig = self._signature(inputs)
-        if self._g is None or self._g[-1] != sig:
-            if self._eager_done < self.warmup:
-                self._eager_done += 1
-                # steady-state eager rate: the last two warm-up steps timed back to back
-                deciding = self.warmup >= 3 and self._deciding()
-                if deciding and self._eager_done == self.warmup - 1:
-                    self._t0 = self._sync_time()
-                out = self.fn(*inputs)
-                if deciding and self._eager_done == self.warmup:
-                    self._eager_ms = [(self._sync_time() - self._t0) / 2]
-                return out
+        g = self._graphs.get(sig)
+        if g is None:
+            n = self._seen.get(sig, 0)
+            if n < self.warmup:
+                self._seen[sig] = n + 1
+                return self._eager_timed(inputs, n)
             try:
-                self._capture(inputs, sig)
+                g = self._capture(inputs, sig)
             except RuntimeError as e:          # capture unsupported here: stay eager
                 self.enabled = False
-                self._g = None
+                self._graphs.clear()
                 torch.cuda.synchronize(self.device)
                 self.engine._reset_state()
                 print(f"[lwaaai] HIP-graph capture failed, running eagerly: {e}", flush=True)
                 return self.fn(*inputs)
-        graph, static_in, static_out, _ = self._g
-        timing = self._deciding() and bool(self._eager_ms)
-        if timing and self._replay_t0 is None:
-            self._replay_t0 = self._sync_time()       # first two replays timed back to back
+        else:
+            self._graphs[sig] = self._graphs.pop(sig)      # LRU order
+        return self._replay(g, inputs)
+
+    def _eager_timed(self, inputs, n: int):
+        deciding = not self.decided
+        if deciding and n >= 1:                 # (the first call of a signature tunes tiles)
+            self._mark()
+        out = self.fn(*inputs)
+        if deciding and n >= 1:
+            self._eager_t.append(self._lap())
+            self._eager_t = self._eager_t[-self.timed:]
+        return out
+
+    def _replay(self, g, inputs):
+        graph, static_in, static_out = g
+        deciding = not self.decided
+        if deciding:
+            self._mark()
         for dst, src in zip(static_in, inputs):
             dst.copy_(src, non_blocking=True)
         self.opt.load_hyper()
         graph.replay()
         self.replays += 1
-        if timing:
-            self._timed_replays += 1
-            if self._timed_replays == 2:
-                graph_ms = (self._sync_time() - self._replay_t0) / 2
-                self.decided = True
-                if graph_ms > self._eager_ms[0]:
-                    # not faster than launching from Python on this host: stay eager
-                    self.enabled = False
-                    self._g = None
-                    print(f"[lwaaai] HIP-graph step {graph_ms:.2f} ms vs eager "
-                          f"{self._eager_ms[0]:.2f} ms: staying eager", flush=True)
         # host mirror of what the replayed finish() did on the device (engine._dstep += 1)
         self.engine.step += 1
         self.engine.stats.steps += 1
+        if deciding:
+            self._replay_t.append(self._lap())
+            if len(self._replay_t) > self.timed:          # [0] paid the graph upload
+                self._decide()
         return static_out
 
-    def _deciding(self) -> bool:
-        return self.auto and not self.decided and getattr(self.engine, "world", 1) == 1
-
-    def _sync_time(self) -> float:
-        """Milliseconds on the host clock after the device has drained."""
+    def _mark(self) -> None:
         torch.cuda.synchronize(self.device)
-        return time.perf_counter() * 1e3
+        self._t_last = time.perf_counter()
 
-    def _capture(self, inputs, sig) -> None:
-        self._g = None
+    def _lap(self) -> float:
+        torch.cuda.synchronize(self.device)
+        return (time.perf_counter() - self._t_last) * 1e3
+
+    def _decide(self) -> None:
+        self.decided = True
+        graph_ms = sum(self._replay_t[1:]) / len(self._replay_t[1:])
+        eager_ms = sum(self._eager_t) / len(self._eager_t) if self._eager_t else float("inf")
+        world = getattr(self.engine, "world", 1)
+        if world > 1:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                backend = dist.get_backend(getattr(self.engine, "pg", None))
+                dev = self.device if backend == "nccl" else torch.device("cpu")
+                t = torch.tensor([graph_ms, eager_ms], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, group=getattr(self.engine, "pg", None))
+                graph_ms, eager_ms = (float(v) / world for v in t.tolist())
+        self.choice = (graph_ms, eager_ms)
+        if graph_ms > eager_ms:
+            # not faster than launching from Python on this host: stay eager
+            self.enabled = False
+            self._graphs.clear()
+            print(f"[lwaaai] HIP-graph step {graph_ms:.2f} ms vs eager {eager_ms:.2f} ms: "
+                  f"staying eager", flush=True)
+
+    # ------------------------------------------------------------------ capture
+    def _capture(self, inputs, sig) -> tuple:
         static_in = [t.clone() for t in inputs]
         self.opt.device_hyper = True
         self.opt.load_hyper()
         torch.cuda.synchronize(self.device)
         host_step = (self.engine.step, self.engine.stats.steps)
         graph = torch.cuda.CUDAGraph()
+        # (each signature keeps its own private memory pool: graphs sharing a pool would alias
+        # each other's step temporaries; 288 GB of HBM affords a few copies of the activations)
         try:
             # thread_local: RCCL's watchdog thread queries events while this thread captures
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
@@ -138,5 +180,9 @@ class StepGraph:
         finally:
             # the capture ran the step's Python (finish() counted a step) but no kernel
             self.engine.step, self.engine.stats.steps = host_step
-        # the capture recorded the step without running it: the caller's replay performs it
-        self._g = (graph, static_in, static_out, sig)
+        while len(self._graphs) >= self.MAX_GRAPHS:
+            self._graphs.pop(next(iter(self._graphs)))
+        g = (graph, static_in, static_out)
+        self._graphs[sig] = g
+        self.captures += 1
+        return g

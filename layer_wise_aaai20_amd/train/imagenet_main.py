@@ -367,13 +367,18 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
         timer.batch_start()
         scheduler.update_lr(epoch, batch_num, len(trn_loader))
         should_print = batch_num % args.print_freq == 0 or batch_num == len(trn_loader)
+        step_fn = _fast_step(run, model, criterion, optimizer, eng) if fast else None
         if eng is not None:
-            eng.timing = should_print and run.is_master
+            # per-bucket HIP-event timing makes a step eager; the same decision on every rank
+            # (a rank running eagerly while the others replay would still pair its collectives,
+            # but the logged numbers would describe a different step than the one timed), and
+            # none while the step graph is on (the logged interval time is the replayed step's)
+            eng.timing = should_print and (step_fn is None or not step_fn.enabled)
         if fast:
             # CompressedDDP: buckets compressed + exchanged during backward, the arena zeroed by
             # the next forward (no zero_grad); FlatSGD unscales a loss-scaled gradient itself.
             # The whole step runs as one replayed HIP graph once warm (train/graphs.py).
-            output, loss, last = _fast_step(run, model, criterion, optimizer, eng)(inp, target)
+            output, loss, last = step_fn(inp, target)
         else:
             with torch.autocast(device_type=inp.device.type, dtype=torch.bfloat16,
                                 enabled=args.bf16):

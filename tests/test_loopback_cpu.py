@@ -1,0 +1,85 @@
+"""The loopback communicator (``parallel/loopback.py``) on CPU: one engine at a simulated world of
+4 ranks whose 3 peers compress stored gradients with codecs built for their own ranks. Checks the
+multi-rank result the real collectives must produce (``tests/test_dist_world8.py`` invariants):
+one collective per bucket in bucket order, and the decoded arena equals the mean over ranks of what
+each rank sent — ``g_r + e_r(before) - e_r(after)`` with error feedback, the reference compressor's
+mean (``CIFAR10/core.py:175-225``) without."""
+import pytest
+import torch
+
+from layer_wise_aaai20_amd.compress import reference as ref
+from layer_wise_aaai20_amd.parallel.engine import GradSyncEngine
+from layer_wise_aaai20_amd.parallel.loopback import attach_loopback
+
+W = 4
+METHODS = [("none", {}), ("Topk", {"K": 0.05}), ("Randomk", {"K": 0.1}),
+           ("Thresholdv", {"V": 0.5}), ("AdaptiveThreshold", {}), ("TernGrad", {}),
+           ("RandomDithering", {"qstates": 127}), ("RandomDithering", {"qstates": 255})]
+
+
+def _params():
+    torch.manual_seed(0)
+    shapes = [(16, 3, 3, 3), (16,), (32, 16, 3, 3), (32,), (10, 32), (10,)]
+    return [(f"p{i}", torch.nn.Parameter(torch.randn(s))) for i, s in enumerate(shapes)]
+
+
+def _grads(eng, seed):
+    g = torch.Generator().manual_seed(seed)
+    out = torch.zeros(eng.arena.numel)
+    for s in eng.arena.segments:
+        out[s.offset:s.offset + s.numel] = torch.randn(s.numel, generator=g)
+    return out
+
+
+@pytest.mark.parametrize("mode", ["layerwise", "entiremodel"])
+@pytest.mark.parametrize("ef", [False, True])
+@pytest.mark.parametrize("method,kw", METHODS,
+                         ids=[f"{m}{kw.get('qstates', '')}" for m, kw in METHODS])
+def test_loopback_world4(method, kw, mode, ef):
+    if method == "none" and ef:
+        pytest.skip("no residual without compression")
+    eng = GradSyncEngine(_params(), mode=mode, method=method, error_feedback=ef,
+                         bucket_cap_mb=0.01, world_size=W, **kw)
+    if mode == "layerwise":
+        assert len(eng.buckets) > 1
+    peers = [_grads(eng, 100 + r) for r in range(1, W)]
+    lb = attach_loopback(eng, peers)
+    g0 = _grads(eng, 100)
+    for step in range(3):                                # residuals evolve over steps
+        eng.arena.grad.copy_(g0)
+        e_old = [eng.ef.clone() if ef else None] + \
+            [e.clone() if e is not None else None for e in lb.sim.ef]
+        lb.calls.clear()
+        eng.sync_now()
+        got = eng.arena.grad.clone()
+        kinds = {c[0] for c in lb.calls}
+        assert [c[1] for c in lb.calls] == list(range(len(eng.buckets)))
+        assert len(kinds) == 1
+        raw = [g0] + peers
+        if ef:
+            e_new = [eng.ef] + lb.sim.ef
+            sent = sum(raw[r] + e_old[r] - e_new[r] for r in range(W)) / W
+            torch.testing.assert_close(got, sent, rtol=1e-5, atol=1e-6)
+            assert float(eng.ef.abs().sum()) > 0 or method == "none"
+        elif method in ("none", "Topk", "Thresholdv", "AdaptiveThreshold"):
+            exp = torch.zeros_like(got)
+            for r in range(W):
+                if mode == "entiremodel":
+                    exp += ref.compress(raw[r], method, **kw)
+                else:
+                    for s in eng.arena.segments:
+                        sl = slice(s.offset, s.offset + s.numel)
+                        exp[sl] += ref.compress(raw[r][sl], method, **kw)
+            torch.testing.assert_close(got, exp / W, rtol=1e-5, atol=1e-6)
+        elif method == "Randomk":
+            nz = got != 0                                # shared-seed support: the rank mean there
+            mean = sum(raw) / W
+            torch.testing.assert_close(got[nz], mean[nz], rtol=1e-5, atol=1e-6)
+        else:                                            # unbiased quantisers: finite, bounded
+            assert torch.isfinite(got).all()
+
+
+def test_loopback_rejects_world_mismatch():
+    eng = GradSyncEngine(_params(), mode="layerwise", method="Topk", K=0.1, world_size=2)
+    with pytest.raises(ValueError):
+        attach_loopback(eng, [_grads(eng, 1), _grads(eng, 2)])

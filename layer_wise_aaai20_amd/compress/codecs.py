@@ -235,12 +235,10 @@ class RandkSparseCodec(TopkCodec):
     """Random-K with explicit indices (masks need not be rank-coherent)."""
     name = "randk-sparse"
     km = KM_RANDK
-    # Kept eager: the entire-model (single 6.6 M-element segment) + EF replay diverges from the
-    # eager step from the second replay on, deterministically, whether the graph compresses on a
-    # side stream or inline, while eager side-stream and eager inline runs agree bit for bit
-    # (scripts/probes/graph_vs_eager_probe.py, profiles/r2_randk_graph_divergence.log). Layer-wise
-    # Random-K replays exactly; not captured until the entire-model case is understood.
-    graph_safe = False
+    # Philox masks keyed by the device step counter (step_t): replays draw fresh masks. (Its
+    # round-2 replay divergence was the runtime memset node that reset the radix histogram,
+    # profiles/r3_graph_divergence_root_cause.md; graph == eager bit for bit since.)
+    graph_safe = True
 
     def __init__(self, plan, world, rank, K, seed=0, error_feedback=False):
         Codec.__init__(self, plan, world, rank, seed, error_feedback)

@@ -335,11 +335,6 @@ class GradSyncEngine:
             # ProcessGroup watchdog, which may query one recorded inside the capture and abort
             # (hipErrorCapturedEvent): capture only with the native communicator
             return False
-        if self.mode == "entiremodel" and os.environ.get("LWAAAI_GRAPH_ENTIRE", "0") != "1":
-            # entire-model steps (one bucket over the whole arena) replayed inexactly in long
-            # CIFAR runs (profiles/r2_randk_graph_divergence.log, r2_graph_entire_race.log):
-            # kept eager until understood; LWAAAI_GRAPH_ENTIRE=1 captures them anyway
-            return False
         return (self.device.type == "cuda" and not self.timing and
                 all(bool(c.graph_safe) for c in self.codecs))
 

@@ -57,7 +57,7 @@ class StepGraph:
         self.replays = 0
         self.captures = 0
         self._graphs: Dict[tuple, tuple] = {}     # signature -> (graph, static_in, static_out)
-        self._seen: Dict[tuple, int] = {}         # signature -> eager calls so far
+        self._seen: Dict[tuple, int] = {}         # input signature -> eager calls so far
         if auto is None:
             auto = os.environ.get("LWAAAI_GRAPH_AUTO", "1") != "0"
         self.auto = bool(auto)
@@ -87,9 +87,11 @@ class StepGraph:
         sig = self._signature(inputs)
         g = self._graphs.get(sig)
         if g is None:
-            n = self._seen.get(sig, 0)
+            # warm-up is counted per input shape (what the tuners / allocator settle on); the
+            # optimizer part of the signature (e.g. SGD's first-step flag) does not restart it
+            n = self._seen.get(sig[0], 0)
             if n < self.warmup:
-                self._seen[sig] = n + 1
+                self._seen[sig[0]] = n + 1
                 return self._eager_timed(inputs, n)
             try:
                 g = self._capture(inputs, sig)

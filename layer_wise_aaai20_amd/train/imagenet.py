@@ -109,7 +109,10 @@ def build_model(name: str = "resnet50", bn0: bool = False) -> nn.Module:
 def build_trainer(model="resnet50", device=None, compress="layerwise", method="Topk", K=0.001,
                   V=1e-3, qstates=255, error_feedback=False, bucket_cap_mb=25.0, dtype="bf16",
                   fused=True, momentum=0.9, weight_decay=1e-4, no_bn_wd=True, lr=0.1,
-                  bn0=True, wire="auto", graph=None, graph_warmup: int = 3) -> ImageNetTrainer:
+                  bn0=True, wire="auto", graph=None, graph_warmup: int = 3,
+                  world_size=None) -> ImageNetTrainer:
+    """``world_size``: build the codecs for that many ranks without a process group (a simulated
+    world driven by ``parallel/loopback.py``); default: the process group's size."""
     device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     net = build_model(model, bn0=bn0) if isinstance(model, str) else model
     if fused:
@@ -121,7 +124,7 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
         lwnn.share_bn_counters(net)
     ddp = CompressedDDP(net, compress=compress, method=method, K=K, V=V, qstates=qstates,
                         error_feedback=error_feedback, bucket_cap_mb=bucket_cap_mb, wire=wire,
-                        flat_params=True)
+                        flat_params=True, world_size=world_size)
     groups = bn_param_groups(net, weight_decay, no_bn_wd)
     opt = FlatSGD(groups, ddp.arena, lr=lr, momentum=momentum, nesterov=momentum > 0,
                   weight_decay=weight_decay)

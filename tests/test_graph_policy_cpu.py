@@ -20,7 +20,7 @@ def test_codec_graph_flags():
     assert mk("none").graph_safe
     assert mk("TernGrad").graph_safe
     assert mk("RandomDithering", qstates=255).graph_safe
-    assert not mk("Randomk", K=0.05).graph_safe                      # kept eager
+    assert mk("Randomk", K=0.05).graph_safe           # device step counter keys masks
     assert not mk("Thresholdv", V=1e-3, wire="sparse").graph_safe   # host read of capacity
     assert mk("Thresholdv", V=1e-3).graph_safe                      # default dense wire
     assert mk("Topk", K=0.5, wire="dense").graph_safe

@@ -157,7 +157,10 @@ def main():
                        lr=0.1, graph=args.graph == "on" and args.warmup >= 2,
                        # capture inside the untimed warm-up: at least one eager step (tile tuner,
                        # lazily built device tables, allocator, RCCL warm), then capture + replay
-                       graph_warmup=max(1, min(3, args.warmup - 1)))
+                       graph_warmup=max(1, min(3, args.warmup - 1)),
+                       # no graph-vs-eager timing decision: it would spill syncs into the timed
+                       # steps (the captured ResNet-50 step is the faster one: 24.3 vs 27.2 ms)
+                       graph_auto=False)
     B, S = args.batch, args.image_size
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)

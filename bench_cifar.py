@@ -29,11 +29,17 @@ CONFIGS = {
 V100_ANCHOR = 16500.0    # img/s, derived in BASELINE.md
 
 
-def run(name, steps, warmup, world, rank, dev, graph=True):
+def run(name, steps, warmup, world, rank, dev, graph="auto"):
     from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
     cfg = CONFIGS[name]
-    tr = CifarTrainer(device=dev, n_train=512 * 12, graph=graph and warmup >= 2, **cfg)
-    tr.graphed.warmup = max(1, min(3, warmup - 1))    # capture inside the untimed warm-up
+    tr = CifarTrainer(device=dev, n_train=512 * 12, graph=graph != "off" and warmup >= 2, **cfg)
+    sg = tr.graphed
+    sg.warmup = max(1, min(3, warmup - 1))    # capture inside the untimed warm-up
+    # auto: the graph-vs-eager choice (train/graphs.py) finishes inside the warm-up: the
+    # replays after the discarded upload replay that fit before the timed steps are timed
+    sg.timed = max(1, warmup - sg.warmup - 1)
+    sg.auto = graph == "auto" and warmup - sg.warmup >= 3
+    sg.decided = not sg.auto
     for _ in range(warmup):
         tr.step()
     torch.cuda.synchronize()
@@ -58,6 +64,9 @@ def run(name, steps, warmup, world, rank, dev, graph=True):
             "scaling": "weak", "vs_baseline": round(value / V100_ANCHOR, 3) if name == "anchor"
             else None, "dtype": "bf16", "data": "synthetic",
             "hip_graph": tr.graphed.replays >= steps,
+            "graph_choice_ms": (None if tr.graphed.choice is None else
+                                {"graph": round(tr.graphed.choice[0], 3),
+                                 "eager": round(tr.graphed.choice[1], 3)}),
             "config": dict(cfg, global_batch=world * tr.bs, parallelism=f"dp{world}",
                            wire_bytes_per_rank=st.payload_bytes, dense_grad_bytes=st.dense_bytes)}
 
@@ -67,8 +76,10 @@ def main():
     ap.add_argument("--config", default="all", choices=["all"] + list(CONFIGS))
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--graph", default="off", choices=["on", "off"],
-                    help="capture the whole step as one HIP graph after 3 eager steps")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="on: capture the whole step as one HIP graph after the eager warm-up "
+                         "steps; auto: also time graph vs eager in the warm-up and keep the "
+                         "faster (train/graphs.py)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -80,7 +91,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     names = list(CONFIGS) if args.config == "all" else [args.config]
     for n in names:
-        line = run(n, args.steps, args.warmup, world, rank, dev, args.graph == "on")
+        line = run(n, args.steps, args.warmup, world, rank, dev, args.graph)
         if rank == 0:
             print(json.dumps(line), flush=True)
     if world > 1:

@@ -1239,11 +1239,19 @@ void selftest_bad_launch(Tensor any) {
   launched("selftest_bad_launch");
 }
 
+// test hook: keep the current stream busy for `ms` milliseconds (bounded, always drains)
+void selftest_spin(Tensor any, double ms) {
+  const c10::DeviceGuard guard(any.device());
+  lw::spin_for_test(ms, cur_stream());
+  launched("selftest_spin");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(lwaaai, m) {
   m.def("workspace_bytes(int n_small, int n_large, int n_tasks) -> int", &workspace_bytes);
   m.def("selftest_bad_launch(Tensor any) -> ()");
+  m.def("selftest_spin(Tensor any, float ms) -> ()");
   m.def(
       "select_compress(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor keep, "
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
@@ -1326,6 +1334,7 @@ TORCH_LIBRARY(lwaaai, m) {
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("selftest_bad_launch", &selftest_bad_launch);
+  m.impl("selftest_spin", &selftest_spin);
   m.impl("select_compress", &select_compress);
   m.impl("thresh_count", &thresh_count);
   m.impl("thresh_write", &thresh_write);

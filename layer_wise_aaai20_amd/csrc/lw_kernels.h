@@ -246,6 +246,8 @@ bool conv_tile_ok(int mode, int tile);
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
                   const float stdv[3], bool bf16, hipStream_t st);
 void launch_invalid_config_for_test(hipStream_t st);
+// bounded busy kernel (<= 30 s) for the communicator-watchdog test (nn.hip)
+void spin_for_test(double ms, hipStream_t st);
 // global average pool of NHWC bf16 [N, HW, C] (C % 8 == 0): forward to [N, C] bf16, backward
 // from [N, C] bf16/fp32 to the channels_last [N, HW, C] bf16 gradient (nn.hip)
 void gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);

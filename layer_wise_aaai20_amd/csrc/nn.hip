@@ -130,6 +130,23 @@ void launch_invalid_config_for_test(hipStream_t st) {
   hipLaunchKernelGGL(k_noop, dim3(1), dim3(2048), 0, st);
 }
 
+// for the communicator-watchdog test: one wave that keeps the stream busy for a bounded time (the
+// constant-rate wall clock bounds it, so the grid always drains), standing in for a collective
+// whose peer never arrives
+__global__ void k_spin_for(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
+void spin_for_test(double ms, hipStream_t st) {
+  int dev = 0, khz = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+    khz = 100000;
+  const double capped = ms < 0 ? 0 : (ms > 30000 ? 30000 : ms);
+  hipLaunchKernelGGL(k_spin_for, dim3(1), dim3(64), 0, st, (uint64_t)(capped * khz));
+}
+
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],
                   const float stdv[3], bool bf16, hipStream_t st) {
   const int64_t chunks = (nbytes + 15) / 16;

@@ -16,7 +16,14 @@
 #include <rccl/rccl.h>
 #include <torch/library.h>
 
+#include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unistd.h>
 
 namespace {
 
@@ -109,9 +116,150 @@ void rccl_broadcast(int64_t h, Tensor t, int64_t root) {
         "ncclBroadcast");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Watchdog. c10d's ProcessGroup watchdog never sees these collectives (they bypass c10d), so a rank
+// that stops participating — a crashed peer, a rank whose control flow diverged, a mismatched
+// bucket plan at run time — would leave every other rank blocked inside an RCCL kernel forever,
+// silently, inside a replayed graph. One host thread per communicator:
+//   * polls ncclCommGetAsyncError (RCCL's own error reporting: peer loss, IB/xGMI errors);
+//   * enforces a deadline on the last step "mark": an event recorded on the compute stream after
+//     each step (outside any graph capture: an event recorded inside a capture must not be
+//     queried). If it has not completed `timeout` seconds after it was recorded, the step is
+//     declared hung.
+// On failure: action 0 (training) prints the reason, aborts the communicator (which makes the
+// blocked RCCL kernels return) and ends the process with exit code 86 — the launcher sees a
+// non-zero exit instead of a hang; action 1 (tests) only records the failure for check().
+// Reference failure handling: train_imagenet_nv.py:161-163 (world-size assert), :704-716 (top-level
+// catch and log).
+struct Watchdog {
+  ncclComm_t comm = nullptr;
+  int device = 0;
+  double timeout_s = 600.0;
+  int action = 0;
+  std::mutex mu;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+  std::chrono::steady_clock::time_point t_mark;
+  std::atomic<int> fired{0};
+  std::atomic<bool> stop{false};
+  std::string why;
+  std::thread th;
+
+  void fail(const std::string& msg) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (fired.load()) return;
+      why = msg;
+      fired.store(1);
+    }
+    std::fprintf(stderr, "[lwaaai] communicator watchdog: %s\n", msg.c_str());
+    std::fflush(stderr);
+    if (action == 0) {
+      if (comm != nullptr) ncclCommAbort(comm);
+      std::fprintf(stderr, "[lwaaai] communicator aborted; exiting with code 86\n");
+      std::fflush(stderr);
+      _exit(86);
+    }
+  }
+
+  void loop() {
+    (void)hipSetDevice(device);
+    const auto period = std::chrono::milliseconds(
+        (int)std::max(10.0, std::min(500.0, timeout_s * 1000.0 / 20.0)));
+    while (!stop.load() && !fired.load()) {
+      std::this_thread::sleep_for(period);
+      if (comm != nullptr) {
+        ncclResult_t r = ncclSuccess;
+        if (ncclCommGetAsyncError(comm, &r) == ncclSuccess && r != ncclSuccess &&
+            r != ncclInProgress) {
+          fail(std::string("RCCL asynchronous error: ") + ncclGetErrorString(r));
+          break;
+        }
+      }
+      std::unique_lock<std::mutex> g(mu);
+      if (!pending) continue;
+      const hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) {
+        pending = false;
+      } else if (q == hipErrorNotReady) {
+        const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() -
+                                                            t_mark).count();
+        if (waited > timeout_s) {
+          g.unlock();
+          fail("training step not complete " + std::to_string(waited) + " s after it was " +
+               "enqueued (deadline " + std::to_string(timeout_s) + " s): a peer rank is not " +
+               "taking part in the collectives");
+          break;
+        }
+      } else {
+        g.unlock();
+        fail(std::string("device error while waiting for the step: ") + hipGetErrorString(q));
+        break;
+      }
+    }
+  }
+};
+
+int64_t rccl_watch_start(int64_t h, double timeout_s, int64_t action, int64_t device) {
+  auto* w = new Watchdog();
+  w->comm = h != 0 ? comm_of(h) : nullptr;
+  w->device = (int)device;
+  w->timeout_s = timeout_s;
+  w->action = (int)action;
+  const c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  TORCH_CHECK(hipEventCreateWithFlags(&w->ev, hipEventDisableTiming) == hipSuccess,
+              "watchdog: hipEventCreate failed");
+  w->th = std::thread([w] { w->loop(); });
+  return reinterpret_cast<int64_t>(w);
+}
+
+Watchdog* watch_of(int64_t wh) {
+  TORCH_CHECK(wh != 0, "watchdog not started");
+  return reinterpret_cast<Watchdog*>(wh);
+}
+
+// Record the step's completion event on the current stream (skipped while capturing).
+void rccl_watch_mark(int64_t wh) {
+  Watchdog* w = watch_of(wh);
+  hipStream_t st = cur_stream();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return;
+  std::lock_guard<std::mutex> g(w->mu);
+  if (w->pending) {
+    // keep the older deadline running until that step completes
+    if (hipEventQuery(w->ev) != hipSuccess) return;
+    w->pending = false;
+  }
+  TORCH_CHECK(hipEventRecord(w->ev, st) == hipSuccess, "watchdog: hipEventRecord failed");
+  w->t_mark = std::chrono::steady_clock::now();
+  w->pending = true;
+}
+
+// "" while healthy, else the failure reason (action 1 watchdogs).
+std::string rccl_watch_status(int64_t wh) {
+  Watchdog* w = watch_of(wh);
+  if (!w->fired.load()) return std::string();
+  std::lock_guard<std::mutex> g(w->mu);
+  return w->why;
+}
+
+void rccl_watch_stop(int64_t wh) {
+  if (wh == 0) return;
+  Watchdog* w = watch_of(wh);
+  w->stop.store(true);
+  if (w->th.joinable()) w->th.join();
+  if (w->ev != nullptr) (void)hipEventDestroy(w->ev);
+  delete w;
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(lwaaai, m) {
+  m.def("rccl_watch_start(int comm, float timeout_s, int action, int device) -> int",
+        &rccl_watch_start);
+  m.def("rccl_watch_mark(int watch) -> ()", &rccl_watch_mark);
+  m.def("rccl_watch_status(int watch) -> str", &rccl_watch_status);
+  m.def("rccl_watch_stop(int watch) -> ()", &rccl_watch_stop);
   m.def("rccl_unique_id() -> Tensor", &rccl_unique_id);
   m.def("rccl_init(Tensor uid, int world, int rank, int device) -> int", &rccl_init);
   m.def("rccl_destroy(int comm) -> ()", &rccl_destroy);

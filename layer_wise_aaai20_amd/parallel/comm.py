@@ -96,10 +96,73 @@ class NativeRccl:
         self.lib.rccl_broadcast(self.handle, t, src)
         return _Done()
 
+    def start_watchdog(self, timeout_s: float, action: int = 0) -> "Watchdog":
+        """Deadline + asynchronous-error watchdog on this communicator (``csrc/rccl.cpp``)."""
+        self.watch = Watchdog(self.handle, self.device, timeout_s, action)
+        return self.watch
+
     def close(self) -> None:
+        w = getattr(self, "watch", None)
+        if w is not None:
+            w.close()
+            self.watch = None
         if self.handle:
             self.lib.rccl_destroy(self.handle)
             self.handle = 0
+
+
+class Watchdog:
+    """Host thread that fails a run loudly instead of letting it hang (``csrc/rccl.cpp``).
+
+    The native RCCL calls bypass c10d and therefore its ProcessGroup watchdog. This one:
+
+    * polls ``ncclCommGetAsyncError``;
+    * checks that the step completion event recorded by :meth:`mark` (once per step, outside
+      graph capture) completes within ``timeout_s``.
+
+    When either check fails:
+
+    * ``action=0`` (training): abort the communicator and exit the process with code 86;
+    * ``action=1`` (tests): record the reason; :meth:`check` raises it.
+
+    ``comm_handle=0`` watches the step deadline only."""
+
+    def __init__(self, comm_handle: int, device, timeout_s: float, action: int = 0):
+        from ..ops._ext import load
+        self.lib = load()
+        dev = torch.device(device)
+        self.handle = int(self.lib.rccl_watch_start(int(comm_handle), float(timeout_s),
+                                                    int(action), dev.index or 0))
+        self.timeout_s = float(timeout_s)
+
+    def mark(self) -> None:
+        if self.handle:
+            self.lib.rccl_watch_mark(self.handle)
+
+    def status(self) -> str:
+        return str(self.lib.rccl_watch_status(self.handle)) if self.handle else ""
+
+    def check(self) -> None:
+        why = self.status()
+        if why:
+            raise RuntimeError(f"communicator watchdog: {why}")
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.rccl_watch_stop(self.handle)
+            self.handle = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_timeout() -> float:
+    """Seconds a step may take before the watchdog declares the job hung
+    (``LWAAAI_COMM_TIMEOUT``, default 600, like c10d's default; 0 disables it)."""
+    return float(os.environ.get("LWAAAI_COMM_TIMEOUT", "600"))
 
 
 _NATIVE = {}

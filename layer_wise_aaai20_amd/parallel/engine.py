@@ -122,7 +122,12 @@ class GradSyncEngine:
         overlap_compress = overlap_compress and os.environ.get("LWAAAI_OVERLAP", "1") != "0"
         self._side = (torch.cuda.Stream(device=self.device)
                       if overlap_compress and self.device.type == "cuda" else None)
-        self._graph_overlap = os.environ.get("LWAAAI_GRAPH_OVERLAP", "0") == "1"
+        # inside a captured step: at world 1 the exchange is a no-op and the side-stream branch
+        # only costs (24.67 vs 24.17 ms/step, profiles/r2_graph_overlap_ab.log), so buckets are
+        # compressed inline; at world > 1 each bucket's compression AND its RCCL collective run on
+        # the side branch, overlapped with the rest of backward
+        self._graph_overlap = os.environ.get(
+            "LWAAAI_GRAPH_OVERLAP", "1" if self.world > 1 else "0") == "1"
         self._retired = []            # (fence event, events held until it completes)
         self._check = os.environ.get("LWAAAI_ENGINE_CHECK", "0") == "1"
         # bucket collectives on a native RCCL communicator (csrc/rccl.cpp) when the group is
@@ -133,6 +138,12 @@ class GradSyncEngine:
         self._stream_waitable = self._native is not None or (
             comm.is_dist() and comm.world_size(self.pg) > 1 and
             comm.dist.get_backend(self.pg) == "nccl")
+        # a rank that stops taking part would leave the others blocked inside RCCL forever: the
+        # watchdog (csrc/rccl.cpp) turns that into an abort + non-zero exit after the deadline
+        self._watch = None
+        if self._native is not None and self.world > 1 and comm.comm_timeout() > 0:
+            self._watch = (getattr(self._native, "watch", None) or
+                           self._native.start_watchdog(comm.comm_timeout()))
         self._reset_state()
         self.all_reduced_last = True
         self.verify_plan()
@@ -293,6 +304,8 @@ class GradSyncEngine:
         self._pending = []
         if self._dstep is not None:
             self._dstep.add_(1)
+        if not torch.cuda.is_available() or not torch.cuda.is_current_stream_capturing():
+            self.heartbeat()
         if hold and not torch.cuda.is_current_stream_capturing():
             # (under HIP-graph capture the event record / wait pairs become graph edges: there is
             # nothing to keep alive, and an event query would invalidate the capture)
@@ -311,6 +324,12 @@ class GradSyncEngine:
         self.stats.payload_bytes = self._payload
         self._active = False
         self.all_reduced_last = True
+
+    def heartbeat(self) -> None:
+        """Mark the end of a step for the communicator watchdog (no-op without one; never
+        inside a graph capture — a replayed step is marked by StepGraph after the replay)."""
+        if self._watch is not None:
+            self._watch.mark()
 
     def sync_now(self) -> None:
         """Post-backward path: copy any foreign ``.grad`` into the arena, then sync every bucket."""

@@ -126,6 +126,9 @@ class StepGraph:
         self.opt.load_hyper()
         graph.replay()
         self.replays += 1
+        hb = getattr(self.engine, "heartbeat", None)
+        if hb is not None:
+            hb()                     # communicator watchdog deadline for this step
         # host mirror of what the replayed finish() did on the device (engine._dstep += 1)
         self.engine.step += 1
         self.engine.stats.steps += 1

@@ -52,7 +52,8 @@ class ImageNetTrainer:
 
     def __init__(self, ddp: CompressedDDP, optimizer, device, dtype=torch.bfloat16,
                  criterion: Optional[nn.Module] = None, channels_last: bool = True,
-                 graph: Optional[bool] = None, graph_warmup: int = 3):
+                 graph: Optional[bool] = None, graph_warmup: int = 3,
+                 graph_auto: Optional[bool] = None):
         self.ddp = ddp
         self.opt = optimizer
         self.device = device
@@ -62,7 +63,8 @@ class ImageNetTrainer:
         self.mean = torch.tensor(IMAGENET_MEAN, device=device, dtype=torch.float32)
         self.std = torch.tensor(IMAGENET_STD, device=device, dtype=torch.float32)
         self._last = None
-        self.graphed = StepGraph(self._eager, ddp.engine, optimizer, device, graph_warmup, graph)
+        self.graphed = StepGraph(self._eager, ddp.engine, optimizer, device, graph_warmup, graph,
+                                 auto=graph_auto)
 
     @property
     def graph_replays(self) -> int:
@@ -110,7 +112,7 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
                   V=1e-3, qstates=255, error_feedback=False, bucket_cap_mb=25.0, dtype="bf16",
                   fused=True, momentum=0.9, weight_decay=1e-4, no_bn_wd=True, lr=0.1,
                   bn0=True, wire="auto", graph=None, graph_warmup: int = 3,
-                  world_size=None) -> ImageNetTrainer:
+                  world_size=None, graph_auto=None) -> ImageNetTrainer:
     """``world_size``: build the codecs for that many ranks without a process group (a simulated
     world driven by ``parallel/loopback.py``); default: the process group's size."""
     device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -130,4 +132,5 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
                   weight_decay=weight_decay)
     tdtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype] \
         if isinstance(dtype, str) else dtype
-    return ImageNetTrainer(ddp, opt, device, tdtype, graph=graph, graph_warmup=graph_warmup)
+    return ImageNetTrainer(ddp, opt, device, tdtype, graph=graph, graph_warmup=graph_warmup,
+                           graph_auto=graph_auto)

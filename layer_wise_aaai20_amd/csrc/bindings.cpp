@@ -294,7 +294,7 @@ void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor
 void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tensor segs,
               Tensor tasks, Tensor seg_wd, double lr, double momentum, double dampening,
               int64_t nesterov, int64_t first_step, double grad_scale,
-              c10::optional<Tensor> hyper) {
+              c10::optional<Tensor> hyper, c10::optional<Tensor> pb) {
   const c10::DeviceGuard guard(p.device());
   check_cuda(p, "p");
   check_cuda(g, "g");
@@ -325,6 +325,13 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tens
     TORCH_CHECK(hyper->scalar_type() == at::kFloat && hyper->numel() >= 2 &&
                     hyper->is_contiguous(), "hyper must be a contiguous float32 [lr, grad_scale]");
     a.hyper = hyper->data_ptr<float>();
+  }
+  if (pb.has_value() && pb->defined()) {
+    check_cuda(*pb, "pb");
+    TORCH_CHECK(pb->scalar_type() == at::kBFloat16 && pb->numel() == p.numel(),
+                "pb must be a bf16 tensor with p's layout");
+    check_aligned16(pb->data_ptr(), "pb");
+    a.pb = reinterpret_cast<uint16_t*>(pb->data_ptr());
   }
   lw::sgd_step(a, cur_stream());
   launched("sgd_step");
@@ -1283,7 +1290,8 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
-      "int nesterov, int first_step, float grad_scale, Tensor? hyper=None) -> ()");
+      "int nesterov, int first_step, float grad_scale, Tensor? hyper=None, "
+      "Tensor(c!)? pb=None) -> ()");
   m.def("normalize_u8(Tensor input, Tensor(a!) out, float[] mean, float[] std) -> ()");
   m.def("cifar_augment(Tensor data, Tensor idx, Tensor prm, int offset, int crop, int cutout, "
         "Tensor(a!) out) -> ()");

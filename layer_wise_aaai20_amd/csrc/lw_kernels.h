@@ -103,6 +103,7 @@ struct SgdArgs {
   float lr, momentum, dampening, grad_scale;
   int nesterov, first_step;
   const float* hyper;          // optional device [lr, grad_scale] (overrides the scalars)
+  uint16_t* pb;                // optional bf16 mirror of p (same layout), written in the same pass
 };
 void sgd_step(const SgdArgs& a, hipStream_t st);
 

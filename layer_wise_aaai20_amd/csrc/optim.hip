@@ -2,8 +2,9 @@
 // flat parameter, gradient and momentum arenas: ONE launch updates the whole model.
 // Semantics are those of torch.optim.SGD, which the reference uses for both workloads
 // (CIFAR10/torch_backend.py:120-143, IMAGENET/training/train_imagenet_nv.py:188-191), with the
-// fp16 master-gradient unscale of train_imagenet_nv.py:424-426 folded in as `grad_scale`
-// (SURVEY.md N12/N13).
+// fp16 master-gradient unscale of train_imagenet_nv.py:424-426 folded in as `grad_scale`, and the
+// master -> model copy of fp16util.py:103-138 (master_params_to_model_params) folded in as the
+// bf16 mirror write `pb`: the next forward reads the mirror with no cast pass.
 #include "common.h"
 #include "lw_kernels.h"
 
@@ -11,6 +12,10 @@ namespace lw {
 
 constexpr int SNT = 256;
 constexpr int SEPB = kLargeEPB;
+
+__device__ __forceinline__ uint16_t to_bf16(float f) {
+  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));   // RNE, as torch's cast
+}
 
 template <bool MOM, bool NEST, bool FIRST>
 __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float* __restrict__ g,
@@ -21,7 +26,8 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
                                              const int2* __restrict__ tasks,
                                              const float* __restrict__ seg_wd, float lr,
                                              float momentum, float dampening, float grad_scale,
-                                             const float* __restrict__ hyper) {
+                                             const float* __restrict__ hyper,
+                                             uint16_t* __restrict__ pb) {
   // graph-captured steps read (lr, grad_scale) from device memory, so a replayed HIP graph
   // follows the LR schedule / loss scale without being re-captured
   if (hyper != nullptr) {
@@ -59,6 +65,10 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
       }
       *reinterpret_cast<float4*>(p + off + i0) = make_float4(x[0], x[1], x[2], x[3]);
       if (MOM) *reinterpret_cast<float4*>(buf + off + i0) = make_float4(b[0], b[1], b[2], b[3]);
+      if (pb != nullptr)
+        *reinterpret_cast<uint2*>(pb + off + i0) =
+            make_uint2((uint32_t)to_bf16(x[0]) | ((uint32_t)to_bf16(x[1]) << 16),
+                       (uint32_t)to_bf16(x[2]) | ((uint32_t)to_bf16(x[3]) << 16));
     } else {
       for (int k = 0; k < 4 && i0 + k < end; ++k) {
         const int64_t i = off + i0 + k;
@@ -71,6 +81,7 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
           dp = NEST ? dp + momentum * bv : bv;
         }
         p[i] = x - lr * dp;
+        if (pb != nullptr) pb[i] = to_bf16(p[i]);
       }
     }
   }
@@ -83,7 +94,7 @@ void sgd_step(const SgdArgs& a, hipStream_t st) {
 #define LW_SGD(M, N, F)                                                                        \
   hipLaunchKernelGGL((k_sgd<M, N, F>), grid, block, 0, st, a.p, a.g, a.buf, a.seg_off, a.seg_n, \
                      a.segs, a.tasks, a.seg_wd, a.lr, a.momentum, a.dampening, a.grad_scale, \
-                     a.hyper)
+                     a.hyper, a.pb)
   if (!mom) LW_SGD(false, false, false);
   else if (a.nesterov) { if (a.first_step) LW_SGD(true, true, true); else LW_SGD(true, true, false); }
   else { if (a.first_step) LW_SGD(true, false, true); else LW_SGD(true, false, false); }

@@ -109,9 +109,14 @@ class FlatSGD(Optimizer):
             self.load_hyper()
         if lib is not None:
             t = self.plan.all_large_tables(p.device)
+            # the bf16 weight mirror the next forward reads is written by the same kernel
+            # (master -> model copy of fp16util.py:103-138 fused: no separate cast pass)
+            pb = getattr(self.arena, "param_bf16", None)
             lib.sgd_step(p, g, self.buf, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], wd, lr,
                          mom, damp, int(nest), int(self._first), float(self.grad_scale),
-                         self._hyper if self.device_hyper else None)
+                         self._hyper if self.device_hyper else None, pb)
+            if pb is not None:
+                self.arena.mark_bf16_fresh()
         else:
             wdv = torch.repeat_interleave(
                 wd, torch.from_numpy(np.diff(np.append(self.plan.offsets, self.arena.numel))))

@@ -139,9 +139,22 @@ class GradArena:
             for s in self.segments:
                 view = _dense_strided_view(self.param_bf16, s.offset, s.param.data)
                 s.param._lw_bf16_of = (lambda v=view, s=s: v if self.bf16_valid(s) else None)
+        if getattr(self, "_bf16_by_sgd", False) and self._bf16_current():
+            return                 # the fused SGD kernel already wrote it (FlatSGD)
         self.param_bf16.copy_(self.param_buf)
+        self._bf16_by_sgd = False
         self._bf16_version = self.param_buf._version
         self._bf16_pver = [s.param._version for s in self.segments]
+
+    def mark_bf16_fresh(self) -> None:
+        """The optimizer kernel has just written the mirror along with the fp32 parameters."""
+        self._bf16_by_sgd = True
+        self._bf16_version = self.param_buf._version
+        self._bf16_pver = [s.param._version for s in self.segments]
+
+    def _bf16_current(self) -> bool:
+        return (getattr(self, "_bf16_version", None) == self.param_buf._version and
+                self._bf16_pver == [s.param._version for s in self.segments])
 
     def bf16_valid(self, seg: Segment) -> bool:
         return (getattr(self, "_bf16_version", None) == self.param_buf._version and

@@ -84,6 +84,19 @@ class GradSyncEngine:
         self.seed = int(seed)
         self.ef = torch.zeros_like(self.arena.grad) if (error_feedback and
                                                        self.method != "none") else None
+        if self.method == "RandomDithering" and self.ef is not None and qstates and \
+                int(qstates) <= 255:
+            # EF needs a contractive compressor (||C(v) - v|| < ||v||); QSGD with s levels on n
+            # elements has relative variance up to sqrt(n)/s — ~20 on ResNet-9 at s = 127 —
+            # so the residual grows geometrically (loss 1e14 within 200 steps on MI355X,
+            # tests/test_convergence_gpu.py)
+            import warnings
+            msg = (f"QSGD (RandomDithering) with qstates={qstates} and error feedback is not "
+                   f"contractive on large tensors: the residual can diverge; use qstates >= "
+                   f"~4096 (16-bit codes) with --error_feedback, or drop error feedback")
+            warnings.warn(msg, stacklevel=2)
+            if self.rank == 0:
+                print(f"[lwaaai] warning: {msg}", flush=True)
         # what a peer needs to build this engine's codecs for another rank (loopback tests)
         self.codec_kw = dict(K=K, V=V, qstates=qstates, seed=self.seed,
                              error_feedback=self.ef is not None, wire=wire)

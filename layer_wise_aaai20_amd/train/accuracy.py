@@ -1,0 +1,79 @@
+"""Short-run held-out accuracy on the learnable synthetic ImageNet task: the "top-1" half of the
+headline metric ("images/sec/node + top-1 acc, ResNet-50 Top-K k=0.1% layer-wise").
+
+The task is the bench's class-conditional synthetic distribution: uint8 noise plus a per-class
+colour offset, 1000 classes. The model is a random-init ResNet-50 trained through the full MI355X
+path (fused MFMA convolutions, CompressedDDP compression inline in the HIP-graph step, FlatSGD).
+
+* Schedule: the linear LR warm-up of the reference's first phase
+  (``IMAGENET/training/train_imagenet_nv.py:204-218``, peak ``2.0 · bs/512``), 128 px.
+* Evaluation: top-1 / top-5 on held-out batches of the same distribution, summed over ranks as
+  ``distributed_predict`` does (``train_imagenet_nv.py:523-542``).
+
+Chance is 0.1 % top-1. Parity with real ImageNet is unpinned (no dataset on this machine).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .imagenet import build_trainer
+
+
+def class_conditional_batches(batch: int, size: int, device, seed_bias: int = 7):
+    """``make_batch(generator) -> (uint8 NHWC images, int64 labels)`` of the bench's task."""
+    dev = torch.device(device)
+    bias = torch.randint(0, 128, (1000, 3), dtype=torch.int16, device=dev,
+                         generator=torch.Generator(device=dev).manual_seed(seed_bias))
+
+    def make_batch(gen):
+        t = torch.randint(0, 1000, (batch,), device=dev, generator=gen)
+        x = torch.randint(0, 128, (batch, size, size, 3), dtype=torch.int16, device=dev,
+                          generator=gen)
+        return (x + bias[t].view(batch, 1, 1, 3)).to(torch.uint8), t
+    return make_batch
+
+
+def short_run_top1(device, steps: int = 300, size: int = 128, batch: int = 256,
+                   peak_lr_512: float = 2.0, warmup: int = 100, eval_batches: int = 8,
+                   rank: int = 0, world: int = 1, seed: int = 0,
+                   **method_kw) -> dict:
+    """Train a fresh ResNet-50 for ``steps`` steps with the given compression settings
+    (``compress=``, ``method=``, ``K=``, ``error_feedback=`` ...) and return held-out accuracy."""
+    dev = torch.device(device)
+    torch.manual_seed(seed)
+    tr = build_trainer("resnet50", device=dev, momentum=0.9, weight_decay=1e-4, no_bn_wd=True,
+                       lr=0.0, bucket_cap_mb=50.0, graph_auto=False, **method_kw)
+    make_batch = class_conditional_batches(batch, size, dev)
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    peak = peak_lr_512 * batch * world / 512
+    losses = []
+    for i in range(steps):
+        for grp in tr.opt.param_groups:
+            grp["lr"] = peak * min(1.0, (i + 1) / warmup)
+        losses.append(tr.step(*make_batch(g)))
+    model = tr.ddp.module
+    model.eval()
+    counts = torch.zeros(3, dtype=torch.float64, device=dev)
+    eg = torch.Generator(device=dev).manual_seed(99 + rank)
+    with torch.no_grad():
+        for _ in range(eval_batches):
+            x, t = make_batch(eg)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = model(tr.normalize(x)).float()
+            top5 = out.topk(5, 1).indices
+            counts[0] += (top5[:, 0] == t).sum()
+            counts[1] += (top5 == t[:, None]).any(1).sum()
+            counts[2] += t.numel()
+    model.train()
+    if world > 1 and dist.is_available() and dist.is_initialized():
+        dist.all_reduce(counts)
+    c1, c5, n = counts.tolist()
+    first = sum(float(v) for v in losses[:20]) / max(1, min(20, len(losses)))
+    last = sum(float(v) for v in losses[-20:]) / max(1, min(20, len(losses)))
+    return {"top1": round(100.0 * c1 / n, 3), "top5": round(100.0 * c5 / n, 3),
+            "steps": steps, "image_size": size, "per_gpu_batch": batch,
+            "loss_first20": round(first, 4), "loss_last20": round(last, 4),
+            "graph_replays": tr.graph_replays}

@@ -23,21 +23,64 @@ from ..utils.logging import StatsLogger, Timer
 from ..models.graph import union
 
 
+def _graphed_step(model, optimizer_step, autocast, dev_type, graph):
+    """The hooked (CompressedDDP + FlatSGD) training step as a :class:`~.graphs.StepGraph`
+    (forward, summed-loss backward with the bucket compression, fused SGD): built once per model.
+    The step-number-dependent LR is pushed into the param groups outside the graph and reaches
+    the captured SGD kernel through device memory (``FlatSGD.load_hyper``)."""
+    opt = getattr(optimizer_step, "__self__", None)           # TorchOptimiser.step
+    inner = getattr(opt, "_opt", None)
+    if not graph or dev_type != "cuda" or not hasattr(inner, "load_hyper"):
+        return None
+    sg = getattr(model, "_lw_step_graph", None)
+    if sg is None:
+        from .graphs import StepGraph
+
+        def body(x, target):
+            with torch.autocast(device_type=dev_type, dtype=autocast or torch.float32,
+                                enabled=autocast is not None):
+                out = model({"input": x, "target": target})
+            out["loss"].float().sum().backward()
+            inner.step()
+            return {"loss": out["loss"].detach(), "correct": out["correct"].detach()}
+
+        sg = StepGraph(body, model.engine, inner, next(model.parameters()).device)
+        model._lw_step_graph = sg
+    return opt, sg
+
+
 def run_batches(model, batches, training, world_size=1, optimizer_step=None, stats=None,
                 compress=None, method=None, K=None, V=None, qstates=None,
                 error_feedback: bool = False, wire: str = "auto", max_batches: Optional[int] = None,
-                autocast=None):
+                autocast=None, graph: Optional[bool] = None):
     """``autocast``: compute dtype of the forward (the MI355X path: bf16). A model wrapped in
     :class:`~..parallel.ddp.CompressedDDP` synchronises its gradients from backward hooks and
-    zeroes its gradient arena at the next forward, so no post-backward sync / zero_grad here."""
+    zeroes its gradient arena at the next forward, so no post-backward sync / zero_grad here;
+    its whole step is replayed as one HIP graph once warm (``graph``, default on:
+    ``LWAAAI_CIFAR_GRAPH=0`` keeps it eager)."""
     stats = stats or StatsLogger(("loss", "correct"))
     model.train(training)
     mode = canonical_mode(compress) if compress not in (None, "none") else "none"
     hooked = getattr(model, "engine", None) is not None
     dev_type = next(model.parameters()).device.type
+    if graph is None:
+        import os
+        graph = os.environ.get("LWAAAI_CIFAR_GRAPH", "1") == "1"
+    gs = _graphed_step(model, optimizer_step, autocast, dev_type, graph) \
+        if training and hooked else None
     for i, batch in enumerate(batches):
         if max_batches is not None and i >= max_batches:
             break
+        if training and gs is not None:
+            opt, sg = gs
+            opt.step_number += 1                  # TorchOptimiser.step's LR update, host side
+            vals = opt.param_values()
+            for g in opt.param_groups:
+                g.update(**vals)
+            out = sg(batch["input"], batch["target"])
+            # a replay rewrites the same output buffers: keep this step's values
+            stats.append({k: v.clone() for k, v in out.items()} if sg.replays else out)
+            continue
         if training:
             with torch.autocast(device_type=dev_type, dtype=autocast or torch.float32,
                                 enabled=autocast is not None):
@@ -84,17 +127,32 @@ def train_epoch(model, train_batches, test_batches, optimizer_step, timer, world
     }
 
 
+def default_backend() -> str:
+    """RCCL ("nccl") when the ranks train on GPUs — the bucket collectives then go through the
+    native, graph-capturable RCCL communicator (csrc/rccl.cpp) — gloo for CPU plumbing. (The
+    reference hard-codes gloo, core.py:334, which stages every GPU tensor through the host.)"""
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
 def init_distributed(master_address, world_size, rank, backend: Optional[str] = None):
     """``dist.init_process_group(init_method=master_address, ...)`` (core.py:334). A bare host
-    (the reference default ``127.0.0.1``) is completed to ``tcp://host:29500``."""
-    if comm.is_dist() or int(world_size) <= 1:
+    (the reference default ``127.0.0.1``) is completed to ``tcp://host:29500``. On a GPU the
+    group is created even for one rank, as the reference does, so the single-rank run takes
+    the same (RCCL) path as a multi-rank one."""
+    backend = backend or default_backend()
+    if comm.is_dist() or (int(world_size) <= 1 and backend != "nccl"):
         return
     addr = master_address or "127.0.0.1"
     if "://" not in addr:
         addr = f"tcp://{addr}:29500" if ":" not in addr else f"tcp://{addr}"
-    backend = backend or "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(torch.cuda.current_device())
+    kw = {"device_id": torch.device("cuda", torch.cuda.current_device())} \
+        if backend == "nccl" else {}
     dist.init_process_group(backend=backend, init_method=addr, world_size=int(world_size),
-                            rank=int(rank))
+                            rank=int(rank), **kw)
+    print(f"process group: backend={dist.get_backend()} world={dist.get_world_size()} "
+          f"rank={dist.get_rank()}", flush=True)
 
 
 def train(model, optimizer, train_batches, test_batches, epochs, master_address=None,

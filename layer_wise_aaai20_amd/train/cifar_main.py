@@ -108,6 +108,8 @@ def main(argv=None):
 
     net = model
     optimizer_cls = torch.optim.SGD
+    from ..parallel import comm as _comm
+    owns_pg = not _comm.is_dist()            # this CLI created the process group (and ends it)
     if fast:
         from ..optim.flat_sgd import FlatSGD
         from ..parallel.ddp import CompressedDDP
@@ -134,9 +136,17 @@ def main(argv=None):
           V=args.threshold, qstates=args.qstates, backend=args.backend,
           error_feedback=args.error_feedback, wire=args.wire, max_batches=args.max_batches,
           autocast=torch.bfloat16 if fast else None)
+    sg = getattr(model, "_lw_step_graph", None)
+    if sg is not None:
+        print(f"HIP-graph step: {sg.replays} replays, {sg.captures} capture(s), "
+              f"{'active' if sg.enabled else 'eager'}", flush=True)
     os.makedirs(os.path.expanduser(args.log_dir), exist_ok=True)
     with open(os.path.join(os.path.expanduser(args.log_dir), "logs.tsv"), "w") as f:
         f.write(str(tsv))
+    from ..parallel import comm
+    if comm.is_dist() and owns_pg:
+        comm.dist.barrier()
+        comm.dist.destroy_process_group()
     return tsv
 
 

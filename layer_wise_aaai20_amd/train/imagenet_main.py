@@ -546,6 +546,15 @@ def main(argv=None):
     # (FlatSGD; --fp16 keeps its static loss scale, unscaled inside the SGD kernel). --no-fused
     # selects the reference's structure (torch layers, post-backward sync, torch SGD).
     run.fast = fast = device.type == "cuda" and not args.no_fused
+    if fast and args.fp16:
+        # The MFMA kernels of the fast path compute in bf16 (same 16-bit class, no loss scale
+        # needed). --fp16 asks for the reference's numerics: fp16 model with fp32 BatchNorm,
+        # fp32 master weights and the static loss scale (train_imagenet_nv.py:410-428,
+        # fp16util.py:21-138), so it runs the reference-structure path — never silently bf16.
+        log.console("--fp16: running the reference fp16 path (fp16 model + fp32 BN, fp32 master "
+                    f"weights, static loss scale {args.loss_scale}); the fused MFMA path is bf16 "
+                    "(drop --fp16 to use it)")
+        run.fast = fast = False
     if fast:
         lwnn.fuse_resnet(model)
     model = model.to(device)

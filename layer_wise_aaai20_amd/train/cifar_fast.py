@@ -28,7 +28,8 @@ class CifarTrainer:
     def __init__(self, network="resnet9", device=None, compress="none", method="none", K=None,
                  V=None, qstates=None, error_feedback=False, batch_size=512, epochs=24,
                  momentum=0.9, dtype=torch.bfloat16, bucket_cap_mb=25.0, wire="auto",
-                 n_train=50000, seed=0, fused=True, graph=None):
+                 n_train=50000, seed=0, fused=True, graph=None, n_test=1000,
+                 task="textures", amp=None):
         self.device = torch.device(device or "cuda")
         self.dtype = dtype
         self.bs = batch_size
@@ -48,8 +49,13 @@ class CifarTrainer:
                                  bucket_cap_mb=bucket_cap_mb, wire=wire, flat_params=True)
         self.opt = FlatSGD(net.parameters(), self.ddp.arena, lr=0.0, momentum=momentum,
                            nesterov=momentum > 0, weight_decay=5e-4 * batch_size)
-        ds = D.synthetic_cifar10(n_train, 1000, seed)
+        ds = D.synthetic_cifar10(n_train, n_test, seed, task=task, amp=amp)
         x = D.transpose(D.normalise(D.pad(ds["train"]["data"], 4)))
+        tx = D.transpose(D.normalise(ds["test"]["data"]))
+        self.test_batches = D.GPUBatches(
+            torch.from_numpy(np.ascontiguousarray(tx)).to(self.device),
+            torch.as_tensor(ds["test"]["labels"]).to(self.device), batch_size, shuffle=False,
+            channels_last=self.device.type == "cuda", dtype=torch.float32)
         self.batches = D.GPUBatches(torch.from_numpy(np.ascontiguousarray(x)).to(self.device),
                                     torch.as_tensor(ds["train"]["labels"]).to(self.device),
                                     batch_size, shuffle=True, augment=True, drop_last=True,
@@ -94,3 +100,17 @@ class CifarTrainer:
         self.step_count += 1
         self.last = out
         return loss
+
+    @torch.no_grad()
+    def evaluate(self) -> float:
+        """Held-out accuracy on the synthetic test split (eval-mode BatchNorm)."""
+        self.model.eval()
+        correct = total = 0
+        for b in self.test_batches:
+            with torch.autocast(device_type=self.device.type, dtype=self.dtype,
+                                enabled=self.dtype != torch.float32):
+                out = self.model({"input": b["input"], "target": b["target"]})
+            correct += int(out["correct"].float().sum())
+            total += int(b["target"].numel())
+        self.model.train()
+        return correct / max(total, 1)

@@ -31,7 +31,7 @@ def test_resnet9_learns_with_compression(method, kw, mode):
     torch.manual_seed(0)
     tr = CifarTrainer("resnet9", compress=mode if method != "none" else "none", method=method,
                       error_feedback=method != "none", batch_size=128, epochs=2,
-                      n_train=12800, seed=0, **kw)
+                      n_train=12800, seed=0, task="colour", **kw)
     from layer_wise_aaai20_amd.utils.logging import PiecewiseLinear
     steps = 200
     tr.steps_per_epoch = 1                           # schedule in steps: warm-up 40, decay to 0
@@ -43,7 +43,7 @@ def test_resnet9_learns_with_compression(method, kw, mode):
     assert all(l == l for l in losses), "NaN loss"
     assert last < first * 0.8, (first, last)
     # held-out accuracy on fresh samples of the same synthetic distribution
-    ds = D.synthetic_cifar10(16, 2048, seed=1)["test"]
+    ds = D.synthetic_cifar10(16, 2048, seed=1, task="colour")["test"]
     x = torch.from_numpy(D.transpose(D.normalise(ds["data"]))).cuda()
     x = x.contiguous(memory_format=torch.channels_last)
     y = torch.as_tensor(ds["labels"]).cuda()

@@ -189,6 +189,7 @@ def main():
     bucket_us = eng.read_timings()
     eng.timing = False
     stats = tr.ddp.sync_stats()
+    overflow = eng.read_overflow()
     acc = None
     if args.acc_steps > 0:
         del tr                            # (free the 224 px trainer's graph pool first)
@@ -243,6 +244,7 @@ def main():
             "ratio": args.ratio,
             "error_feedback": args.ef,
             "wire_bytes_per_rank": stats.payload_bytes,
+            "selection_overflow": overflow,
             "dense_grad_bytes": stats.dense_bytes,
             "buckets": stats.buckets,
         },

@@ -27,6 +27,7 @@ compression, ``e <- g' - C(g')`` after it, where ``C(g')`` is this rank's decode
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import numpy as np
@@ -64,6 +65,10 @@ class Codec:
     # device step counter (GradSyncEngine._dstep) the Philox-keyed kernels read instead of the
     # host `step` argument, so a replayed HIP graph draws fresh random keys every step
     step_t = None
+    # device int32 counter of elements the reference rule selects that the payload could not
+    # carry (Top-K ties beyond the slack, threshold hits beyond a fixed sparse capacity); they
+    # stay in the error-feedback residual (GradSyncEngine.read_overflow)
+    overflow = None
 
     def __init__(self, plan: SegPlan, world: int, rank: int, seed: int = 0,
                  error_feedback: bool = False):
@@ -162,7 +167,7 @@ class TopkCodec(Codec):
                                 t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
                                 self._workspace(grad.device, lib), self.km, OUT_PAIRS, out, None,
                                 None, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
-                                self.step_t)
+                                self.step_t, self.overflow)
             return out
         self._compress_cpu(grad, ef, step, out)
         return out
@@ -317,14 +322,23 @@ class RandkCodec(RandkSparseCodec):
 
 # ================================================================================= thresholds
 class ThresholdCodec(TopkCodec):
-    """``Thresholdv`` (|g| >= V) and ``AdaptiveThreshold`` (|2g| >= max|g|): variable counts,
-    so ranks first agree on per-layer capacities with an all-reduce(MAX) of the counts."""
+    """``Thresholdv`` (|g| >= V) and ``AdaptiveThreshold`` (|2g| >= max|g|) on a sparse wire.
+
+    The number of hits is data-dependent, so the payload capacity is either:
+
+    * **fixed** (``max_density``, the default sparse wire): each segment carries at most
+      ``max(16, ceil(density · n))`` pairs. It is sync-free and graph-capturable. Hits beyond the
+      capacity — the first in index order travel, strictly-above-threshold hits first — stay in
+      the error-feedback residual and are counted on the device (``GradSyncEngine.read_overflow``).
+    * **agreed per step** (``max_density=None``, ``wire="sparse-exact"``): the ranks take an
+      all-reduce(MAX) of the counts. This is exact for any density, but the capacity is read on
+      the host in the middle of backward, so that step stays eager.
+    """
     name = "threshold"
     km = KM_THRESH
-    graph_safe = False          # the sparse wire reads the agreed capacity on the host
 
     def __init__(self, plan, world, rank, V=None, adaptive=False, seed=0, error_feedback=False,
-                 count_exchange=None):
+                 count_exchange=None, max_density=None):
         Codec.__init__(self, plan, world, rank, seed, error_feedback)
         self.V = float(V or 0.0)
         self.adaptive = bool(adaptive)
@@ -332,10 +346,21 @@ class ThresholdCodec(TopkCodec):
         self._ws = {}
         self._send = {}
         self.cap_off = None
+        self.max_density = None if max_density is None else float(max_density)
+        if self.max_density is not None:
+            sizes = np.asarray(plan.sizes, dtype=np.int64)
+            cap = np.minimum(sizes, np.maximum(16, np.ceil(sizes * self.max_density))).astype(
+                np.int64)
+            self.cap = cap
+            self.cap_off = np.concatenate([[0], np.cumsum(cap)]).astype(np.int64)
+            self.cap_total = int(self.cap_off[-1])
 
-    def compress(self, grad, ef, step):
-        lib = ops_for(grad)
-        dev = grad.device
+    @property
+    def graph_safe(self) -> bool:
+        return self.max_density is not None
+
+    def _counts(self, grad, ef, lib, dev):
+        """Threshold state + per-segment hit counts (device), or the CPU selection."""
         if lib is not None:
             t = self.plan.all_large_tables(dev)
             k = str(dev)
@@ -345,35 +370,52 @@ class ThresholdCodec(TopkCodec):
             counts = torch.empty(self.plan.S, dtype=torch.int32, device=dev)
             lib.thresh_count(grad, ef, t["seg_off"], t["seg_n"], t["segs"], t["tasks"],
                              t["task_lo"], self._ws[k], self.V, int(self.adaptive), counts)
+            return counts
+        counts = torch.empty(self.plan.S, dtype=torch.int32)
+        self._sel = []
+        for s, x in self._segs(grad):
+            if ef is not None:
+                o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
+                x.add_(ef[o:o + n])
+            a = x.abs()
+            thr = float(a.max()) * 0.5 if self.adaptive and x.numel() else self.V
+            gt = (a > thr) & (x != 0)
+            eq = (a == thr) & (x != 0) if thr != 0.0 else torch.zeros_like(gt)
+            gi = torch.nonzero(gt, as_tuple=False).flatten()
+            ei = torch.nonzero(eq, as_tuple=False).flatten()
+            if self.max_density is not None:          # the kernels' capacity rule (k_set_caps)
+                cap = int(self.cap[s])
+                gi = gi[:cap]
+                ei = ei[:max(0, cap - gi.numel())]
+            idx = torch.sort(torch.cat([gi, ei])).values
+            self._sel.append(idx)
+            counts[s] = idx.numel()
+        return counts
+
+    def compress(self, grad, ef, step):
+        lib = ops_for(grad)
+        dev = grad.device
+        counts = self._counts(grad, ef, lib, dev)
+        if self.max_density is not None:
+            out = self.send_buffer(dev)
+            if lib is not None:
+                self._cap_off_dev = self.plan.dev(dev, f"thrcap{self.max_density}",
+                                                  lambda: torch.from_numpy(self.cap_off))
         else:
-            counts = torch.empty(self.plan.S, dtype=torch.int32)
-            self._sel = []
-            for s, x in self._segs(grad):
-                if ef is not None:
-                    o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
-                    x.add_(ef[o:o + n])
-                a = x.abs()
-                if self.adaptive:
-                    keep = (x * 2).abs() >= a.max() if x.numel() else a > 0
-                else:
-                    keep = a >= self.V
-                keep &= x != 0
-                idx = torch.nonzero(keep, as_tuple=False).flatten()
-                self._sel.append(idx)
-                counts[s] = idx.numel()
-        caps = counts.to(torch.int64)
-        if self.count_exchange is not None and self.world > 1:
-            caps = self.count_exchange(caps)
-        caps_h = caps.cpu().numpy().astype(np.int64)
-        self.cap_off = np.concatenate([[0], np.cumsum(caps_h)]).astype(np.int64)
-        cap_total = int(self.cap_off[-1])
-        out = torch.empty(2 * max(cap_total, 1), dtype=torch.int32, device=dev)
+            caps = counts.to(torch.int64)
+            if self.count_exchange is not None and self.world > 1:
+                caps = self.count_exchange(caps)
+            caps_h = caps.cpu().numpy().astype(np.int64)
+            self.cap_off = np.concatenate([[0], np.cumsum(caps_h)]).astype(np.int64)
+            cap_total = int(self.cap_off[-1])
+            out = torch.empty(2 * max(cap_total, 1), dtype=torch.int32, device=dev)
+            if lib is not None:
+                self._cap_off_dev = torch.from_numpy(self.cap_off).to(dev)
         self.last_payload_bytes = out.numel() * 4
         if lib is not None:
             t = self.plan.all_large_tables(dev)
-            self._cap_off_dev = torch.from_numpy(self.cap_off).to(dev)
             lib.thresh_write(grad, ef, t["seg_off"], t["seg_n"], self._cap_off_dev, t["segs"],
-                             t["tasks"], t["task_lo"], self._ws[str(dev)], out)
+                             t["tasks"], t["task_lo"], self._ws[str(dev)], out, self.overflow)
             return out
         pairs = out.view(-1, 2)
         pairs[:, 0] = SENT
@@ -658,7 +700,7 @@ class DenseWrap(Codec):
 # ================================================================================= factory
 def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qstates=None,
                seed: int = 0, error_feedback: bool = False, wire: str = "auto",
-               count_exchange=None) -> Codec:
+               count_exchange=None, max_density=None) -> Codec:
     """Build the codec for ``method`` honouring the reference's falsy-parameter guards
     (``core.py:178-215``: ``Topk`` without K, ``Thresholdv`` without V... mean no compression)."""
     method = ref.canonical_method(method)
@@ -672,12 +714,15 @@ def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qst
             c = RandkSparseCodec(plan, world, rank, K, seed, error_feedback)
         else:
             c = RandkCodec(plan, world, rank, K, seed, error_feedback)
-    elif method == "Thresholdv" and V:
-        c = ThresholdCodec(plan, world, rank, V=V, seed=seed, error_feedback=error_feedback,
-                           count_exchange=count_exchange)
-    elif method == "AdaptiveThreshold":
-        c = ThresholdCodec(plan, world, rank, adaptive=True, seed=seed,
-                           error_feedback=error_feedback, count_exchange=count_exchange)
+    elif method in ("Thresholdv", "AdaptiveThreshold") and (V or method == "AdaptiveThreshold"):
+        # sparse wire capacity: fixed (graph-capturable) unless "sparse-exact" asks for the
+        # per-step count exchange
+        dens = None if wire == "sparse-exact" else float(
+            max_density if max_density is not None else
+            os.environ.get("LWAAAI_THRESH_DENSITY", "0.05"))
+        c = ThresholdCodec(plan, world, rank, V=V, adaptive=method == "AdaptiveThreshold",
+                           seed=seed, error_feedback=error_feedback,
+                           count_exchange=count_exchange, max_density=dens)
     elif method == "TernGrad":
         c = TernGradCodec(plan, world, rank, seed, error_feedback)
     elif method == "RandomDithering" and qstates:

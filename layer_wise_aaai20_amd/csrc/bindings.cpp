@@ -90,6 +90,15 @@ const uint32_t* step_ptr(const c10::optional<Tensor>& t) {
   return reinterpret_cast<const uint32_t*>(t->data_ptr());
 }
 
+// optional device overflow counter (int32 scalar, incremented with atomics)
+unsigned int* overflow_ptr(const c10::optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_cuda(*t, "overflow");
+  TORCH_CHECK(t->scalar_type() == at::kInt && t->numel() >= 1,
+              "overflow must be an int32 GPU tensor");
+  return reinterpret_cast<unsigned int*>(t->data_ptr());
+}
+
 lw::SelectArgs make_select_args(const Tensor& g, const c10::optional<Tensor>& ef,
                                 const Tensor& seg_off, const Tensor& seg_n, const Tensor& keep,
                                 const Tensor& cap_off, const Tensor& small_segs,
@@ -139,7 +148,7 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
                      Tensor tasks, Tensor task_lo, Tensor ws, int64_t km, int64_t out,
                      c10::optional<Tensor> pairs, c10::optional<Tensor> vals,
                      c10::optional<Tensor> idx, int64_t gid_base, int64_t step, int64_t seed,
-                     c10::optional<Tensor> step_t) {
+                     c10::optional<Tensor> step_t, c10::optional<Tensor> overflow) {
   const c10::DeviceGuard guard(g.device());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, keep, cap_off, small_segs, large_segs,
                                       tasks, task_lo, ws);
@@ -151,6 +160,7 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
   a.gid_base = (uint32_t)gid_base;
   a.step = (uint32_t)step;
   a.step_ptr = step_ptr(step_t);
+  a.overflow = overflow_ptr(overflow);
   a.seed0 = (uint32_t)(seed & 0xffffffff);
   a.seed1 = (uint32_t)((uint64_t)seed >> 32);
   lw::select_compress(a, (int)km, (int)out, a.ef != nullptr, cur_stream());
@@ -193,13 +203,14 @@ void thresh_dense(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg
 
 void thresh_write(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
                   Tensor cap_off, Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor ws,
-                  Tensor pairs) {
+                  Tensor pairs, c10::optional<Tensor> overflow) {
   const c10::DeviceGuard guard(g.device());
   Tensor empty_i = at::empty({0}, seg_n.options());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, seg_n, cap_off, empty_i, large_segs,
                                       tasks, task_lo, ws);
   check_cuda(pairs, "pairs");
   a.pairs = ptr<int2>(pairs);
+  a.overflow = overflow_ptr(overflow);
   lw::thresh_write(a, a.ef != nullptr, cur_stream());
   launched("thresh_write");
 }
@@ -1263,7 +1274,7 @@ TORCH_LIBRARY(lwaaai, m) {
       "select_compress(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor keep, "
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
       "Tensor(c!) ws, int km, int out, Tensor(d!)? pairs, Tensor(e!)? vals, Tensor(f!)? idx, "
-      "int gid_base, int step, int seed, Tensor? step_t=None) -> ()");
+      "int gid_base, int step, int seed, Tensor? step_t=None, Tensor(g!)? overflow=None) -> ()");
   m.def(
       "thresh_count(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor large_segs, "
       "Tensor tasks, Tensor task_lo, Tensor(c!) ws, float V, int adaptive, Tensor(d!) counts_out) "
@@ -1273,7 +1284,8 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor tasks, Tensor task_lo, Tensor(c!) ws, float V, int adaptive) -> ()");
   m.def(
       "thresh_write(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor cap_off, "
-      "Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor(c!) ws, Tensor(d!) pairs) -> ()");
+      "Tensor large_segs, Tensor tasks, Tensor task_lo, Tensor(c!) ws, Tensor(d!) pairs, "
+      "Tensor(e!)? overflow=None) -> ()");
   m.def(
       "unpack_pairs(Tensor gathered, int world, Tensor(a!) g, Tensor seg_off, Tensor seg_n, "
       "Tensor cap_off, Tensor utasks) -> ()");

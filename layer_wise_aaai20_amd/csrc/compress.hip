@@ -115,7 +115,8 @@ __global__ __launch_bounds__(NT) void k_small_select(
     const int32_t* __restrict__ seg_n, const int32_t* __restrict__ keep,
     const int64_t* __restrict__ cap_off, const int32_t* __restrict__ small_segs,
     int2* __restrict__ pairs, float* __restrict__ vals, int32_t* __restrict__ idx_out,
-    SelState* __restrict__ st_small, uint32_t gid_base, uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp) {
+    SelState* __restrict__ st_small, uint32_t gid_base, uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp,
+    unsigned int* __restrict__ overflow) {
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t h[2048];
@@ -184,7 +185,12 @@ __global__ __launch_bounds__(NT) void k_small_select(
   SelState S;
   S.tkey = prefix;
   finish_state(S, KM, m, mr, eq_total, cap);
-  if (threadIdx.x == 0) st_small[blockIdx.x] = S;
+  if (threadIdx.x == 0) {
+    st_small[blockIdx.x] = S;
+    // ties the reference's `>=` rule keeps but the payload slack could not hold (left in EF)
+    if (KM == KM_TOPK && overflow != nullptr && S.tkey != 0 && eq_total > S.quota)
+      atomicAdd(overflow, eq_total - S.quota);
+  }
 
   // order-preserving compaction: (gt, eq) counts packed in one word (<= 4096 each)
   uint32_t cg = 0, ce = 0;
@@ -299,7 +305,8 @@ __global__ __launch_bounds__(NT) void k_select(const uint32_t* __restrict__ hist
                                                SelState* __restrict__ st,
                                                const int32_t* __restrict__ large_segs,
                                                const int32_t* __restrict__ keep,
-                                               const int64_t* __restrict__ cap_off) {
+                                               const int64_t* __restrict__ cap_off,
+                                               unsigned int* __restrict__ overflow) {
   using C = PassCfg<PASS>;
   constexpr int NB = 1 << C::BITS;
   __shared__ uint32_t arr[NT];
@@ -319,6 +326,8 @@ __global__ __launch_bounds__(NT) void k_select(const uint32_t* __restrict__ hist
     if (PASS == 2) {
       S.tkey = S.prefix;
       finish_state(S, KM, (uint32_t)keep[s], mn, h[d], (uint32_t)(cap_off[s + 1] - cap_off[s]));
+      if (KM == KM_TOPK && overflow != nullptr && S.tkey != 0 && h[d] > S.quota)
+        atomicAdd(overflow, h[d] - S.quota);
     }
     st[li] = S;
   }
@@ -440,13 +449,18 @@ __global__ __launch_bounds__(NT) void k_thresh_dense(float* __restrict__ g, floa
 
 // Per-segment capacity for the threshold path is only known after the count exchange.
 __global__ void k_set_caps(SelState* __restrict__ st, const int64_t* __restrict__ cap_off,
-                           const int32_t* __restrict__ large_segs, int nseg) {
+                           const int32_t* __restrict__ large_segs, int nseg,
+                           unsigned int* __restrict__ overflow) {
   const int li = blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= nseg) return;
   const int s = large_segs[li];
   SelState S = st[li];
   S.cap = (uint32_t)(cap_off[s + 1] - cap_off[s]);
-  if (S.total > S.cap) {                  // cannot happen: cap = max over ranks of total
+  if (S.total > S.cap) {
+    // a fixed-capacity sparse wire: the first `cap` hits (index order) travel, the rest stay in
+    // the error-feedback residual (or are dropped without EF) and are counted; with capacities
+    // from the count exchange this cannot happen (cap = max over ranks of total)
+    if (overflow != nullptr) atomicAdd(overflow, S.total - S.cap);
     S.quota = S.cap > S.cnt_gt ? min(S.quota, S.cap - S.cnt_gt) : 0u;
     S.total = min(S.cnt_gt, S.cap) + S.quota;
   }
@@ -940,7 +954,7 @@ static void select_compress_t(const SelectArgs& a, hipStream_t st) {
   if (a.n_small > 0)
     LW_LAUNCH((k_small_select<KM, OUT, EF>), a.n_small, st, a.g, a.ef, a.seg_off, a.seg_n, a.keep,
               a.cap_off, a.small_segs, a.pairs, a.vals, a.idx_out, a.st_small, a.gid_base, a.step,
-              a.seed0, a.seed1, a.step_ptr);
+              a.seed0, a.seed1, a.step_ptr, a.overflow);
   if (a.n_large == 0) return;
   {
     const int64_t words = (int64_t)HIST_WORDS * a.n_large;
@@ -949,13 +963,16 @@ static void select_compress_t(const SelectArgs& a, hipStream_t st) {
   }
   LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
             a.large_segs, a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
-  LW_LAUNCH((k_select<KM, 0>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);
+  LW_LAUNCH((k_select<KM, 0>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off,
+            a.overflow);
   LW_LAUNCH((k_hist<KM, 1, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
             a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
-  LW_LAUNCH((k_select<KM, 1>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);
+  LW_LAUNCH((k_select<KM, 1>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off,
+            a.overflow);
   LW_LAUNCH((k_hist<KM, 2, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
             a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
-  LW_LAUNCH((k_select<KM, 2>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off);
+  LW_LAUNCH((k_select<KM, 2>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off,
+            a.overflow);
   LW_LAUNCH((k_count<KM, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
             a.tasks, a.st_large, a.cnt, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
   LW_LAUNCH((k_scan<KM>), a.n_large, st, a.cnt, a.pre, a.task_lo, a.st_large, (int32_t*)nullptr);
@@ -1022,7 +1039,7 @@ void thresh_dense(const SelectArgs& a, float V, int adaptive, bool ef, float* se
 
 void thresh_write(const SelectArgs& a, bool ef, hipStream_t st) {
   hipLaunchKernelGGL(k_set_caps, dim3((a.n_large + NT - 1) / NT), dim3(NT), 0, st, a.st_large,
-                     a.cap_off, a.large_segs, a.n_large);
+                     a.cap_off, a.large_segs, a.n_large, a.overflow);
   LW_LAUNCH(k_fill_tail, a.n_large, st, a.pairs, a.cap_off, a.large_segs, a.st_large);
   if (ef)
     LW_LAUNCH((k_write<KM_THRESH, OUT_PAIRS, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,

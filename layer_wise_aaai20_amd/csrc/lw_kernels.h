@@ -54,6 +54,9 @@ struct SelectArgs {
   // rng
   uint32_t gid_base, step, seed0, seed1;
   const uint32_t* step_ptr;    // optional device step counter (overrides `step`; HIP graphs)
+  // optional device counter: elements the reference rule would send that did not fit the
+  // payload (Top-K ties beyond the tie slack; threshold hits beyond a fixed sparse capacity)
+  unsigned int* overflow;
 };
 
 struct QuantArgs {

@@ -51,6 +51,7 @@ class SyncStats:
     payload_bytes: int = 0          # bytes this rank sent last step
     dense_bytes: int = 0            # fp32 gradient bytes (what an uncompressed all-reduce moves)
     buckets: int = 0
+    overflow: int = 0               # last read_overflow(): selected elements the payload dropped
     history: List[float] = field(default_factory=list)
 
     @property
@@ -117,10 +118,16 @@ class GradSyncEngine:
         # advanced by finish() on the GPU, so a replayed HIP graph of the step advances it too
         self._dstep = (torch.zeros(1, dtype=torch.int64, device=self.device)
                        if self.device.type == "cuda" else None)
+        # device count of elements the reference rule selected but the payload could not carry
+        # (Top-K ties beyond the slack, threshold hits beyond a fixed capacity; read_overflow)
+        self._overflow = (torch.zeros(1, dtype=torch.int32, device=self.device)
+                          if self.device.type == "cuda" else None)
         for c in self.codecs:
             c.step_t = self._dstep
+            c.overflow = self._overflow
             if isinstance(c, DenseWrap):
                 c.inner.step_t = self._dstep
+                c.inner.overflow = self._overflow
         self.seg_bucket = [0] * len(self.arena.segments)
         for b in self.buckets:
             for i in range(b.seg_lo, b.seg_hi):
@@ -337,6 +344,16 @@ class GradSyncEngine:
         self.stats.payload_bytes = self._payload
         self._active = False
         self.all_reduced_last = True
+
+    def read_overflow(self) -> int:
+        """Cumulative count of elements the compression rule selected that did not fit the
+        payload (they stayed in the error-feedback residual, or were dropped without EF): Top-K
+        ties beyond ``tie_slack``, threshold hits beyond the fixed sparse capacity. Synchronises;
+        call at logging time. Also kept in ``stats.overflow``."""
+        if self._overflow is None:
+            return 0
+        self.stats.overflow = int(self._overflow.item()) & 0xFFFFFFFF
+        return self.stats.overflow
 
     def heartbeat(self) -> None:
         """Mark the end of a step for the communicator watchdog (no-op without one; never

@@ -88,7 +88,7 @@ def get_parser():
     p.add_argument("--arch", default="resnet50")
     p.add_argument("--overlap", action="store_true", help="CompressedDDP (bucketed, overlapped)")
     p.add_argument("--error-feedback", action="store_true")
-    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "dense", "indexfree"])
+    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "dense", "indexfree"])
     p.add_argument("--epochs", type=int, default=None, help="stop after this many epochs")
     p.add_argument("--synthetic-size", type=int, default=None,
                    help="synthetic train images per phase (default 64 batches)")
@@ -445,6 +445,7 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
             run.tb.log("net/recv_gbit", recv)
             run.tb.log("net/transmit_gbit", sent)
             if eng is not None:
+                eng.read_overflow()
                 run.tb.log_comm(eng.stats, eng.read_timings() if eng.timing else None)
             run.log.verbose(
                 f"Epoch: [{epoch}][{batch_num}/{len(trn_loader)}]\tTime {timer.batch_time.val:.3f} "

@@ -239,6 +239,7 @@ class TensorboardLogger:
         self.log("comm/payload_bytes", stats.payload_bytes)
         self.log("comm/dense_bytes", stats.dense_bytes)
         self.log("comm/ratio", stats.ratio)
+        self.log("comm/overflow", getattr(stats, "overflow", 0))
         for b in bucket_us or []:
             i = b["bucket"]
             for k in ("compress_us", "exchange_us", "idle_us", "decode_us"):

@@ -69,14 +69,21 @@ def test_graph_step_matches_eager(method, compress, ef):
     assert torch.equal(pe, pg), (pe - pg).abs().max().item()
 
 
-def test_graph_mode_falls_back_for_host_synchronising_codecs():
-    torch.manual_seed(0)
-    tr = build_trainer("resnet50", device="cuda", compress="layerwise", method="Thresholdv",
-                       V=1e-3, wire="sparse", graph=True)
-    for x, t in _batches(5):
-        tr.step(x, t)
-    torch.cuda.synchronize()
-    assert tr.graph_replays == 0           # the sparse wire reads the agreed capacity on the host
+@pytest.mark.parametrize("wire,replays", [("sparse", 4), ("sparse-exact", 0)])
+def test_threshold_sparse_wire_in_graph(wire, replays):
+    """The fixed-capacity sparse threshold wire is sync-free: captured and bit-equal to eager.
+    The count-exchange variant reads the agreed capacity on the host, so it stays eager."""
+    runs = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        tr = build_trainer("resnet50", device="cuda", compress="layerwise", method="Thresholdv",
+                           V=1e-3, wire=wire, error_feedback=True, graph=graph)
+        losses = [float(tr.step(x, t)) for x, t in _batches(7)]
+        torch.cuda.synchronize()
+        runs[graph] = (_params(tr), losses, tr.graph_replays)
+    assert runs[True][2] == replays
+    assert runs[False][1] == runs[True][1]
+    assert torch.equal(runs[False][0], runs[True][0])
 
 
 def test_graph_replays_advance_the_device_step():

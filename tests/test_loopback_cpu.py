@@ -83,3 +83,30 @@ def test_loopback_rejects_world_mismatch():
     eng = GradSyncEngine(_params(), mode="layerwise", method="Topk", K=0.1, world_size=2)
     with pytest.raises(ValueError):
         attach_loopback(eng, [_grads(eng, 1), _grads(eng, 2)])
+
+
+@pytest.mark.parametrize("method,kw", [("Thresholdv", {"V": 0.5}), ("AdaptiveThreshold", {})])
+@pytest.mark.parametrize("density", [1.0, 0.02])
+def test_fixed_capacity_threshold_wire(method, kw, density, monkeypatch):
+    """The graph-capturable sparse threshold wire (fixed per-segment capacity): with room for
+    every hit it equals the exact dense-wire result; with too little room the hits that do not
+    fit stay in the error-feedback residual, so decoded == mean_r(what each rank sent)."""
+    monkeypatch.setenv("LWAAAI_THRESH_DENSITY", str(density))
+    res = {}
+    for wire in ("dense", "sparse"):
+        eng = GradSyncEngine(_params(), mode="layerwise", method=method, error_feedback=True,
+                             bucket_cap_mb=0.01, world_size=W, wire=wire, **kw)
+        if wire == "sparse":
+            assert all(c.graph_safe and c.name == "threshold" for c in eng.codecs)
+        peers = [_grads(eng, 100 + r) for r in range(1, W)]
+        lb = attach_loopback(eng, peers)
+        g0 = _grads(eng, 100)
+        eng.arena.grad.copy_(g0)
+        e_old = [eng.ef.clone()] + [e.clone() for e in lb.sim.ef]
+        eng.sync_now()
+        e_new = [eng.ef] + lb.sim.ef
+        sent = sum(([g0] + peers)[r] + e_old[r] - e_new[r] for r in range(W)) / W
+        torch.testing.assert_close(eng.arena.grad, sent, rtol=1e-5, atol=1e-6)
+        res[wire] = eng.arena.grad.clone()
+    if density == 1.0:
+        torch.testing.assert_close(res["sparse"], res["dense"], rtol=1e-6, atol=1e-7)

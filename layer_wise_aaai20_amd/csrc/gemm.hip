@@ -30,6 +30,7 @@
 
 namespace lw {
 
+void gemm_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st);   // gemm_big.hip
 
 // Fixed-order reduction of split-K slabs + epilogue. A workgroup owns OT float4 groups of outputs
 // and ZT split lanes (ZT*OT = 256): lane z sums splits z, z+ZT, ... in order, then the ZT lane sums
@@ -275,6 +276,7 @@ __global__ __launch_bounds__(GT) void k_gemm_stream(const GemmK p) {
   }
 }
 
+static bool is_stream_tile(int t) { return t >= GEMM_S64 && t <= GEMM_S256; }
 static int stream_bn(int tile) { return tile == GEMM_S64 ? 64 : (tile == GEMM_S128 ? 128 : 256); }
 
 bool gemm_stream_ok(const GemmArgs& g) {
@@ -334,11 +336,13 @@ static TileShape tile_shape(int t) {
     case GEMM_T64x256x32: return {64, 256, 32};
     case GEMM_T256x64x64: return {256, 64, 64};
     case GEMM_T64x64x64: return {64, 64, 64};
+    case GEMM_B256: return {256, 256, 64};
     default: return {128, 128, 32};
   }
 }
 
 int gemm_pick_tile(const GemmArgs& g) {
+  if (g.tile == GEMM_B256 && !gemm_big_ok(g)) return GEMM_T128x128x64;
   if (g.tile > 0) return g.tile;
   if (g.M <= 64 && g.N <= 64) return GEMM_T64x64x64;
   if (g.N <= 64 && g.M >= 512) return GEMM_T256x64x32;
@@ -347,7 +351,7 @@ int gemm_pick_tile(const GemmArgs& g) {
 }
 
 int gemm_tiles_m(const GemmArgs& g) {
-  if (g.tile >= GEMM_S64) return gemm_stream_grid_m(g);   // one statistics row per workgroup
+  if (is_stream_tile(g.tile)) return gemm_stream_grid_m(g);   // one statistics row per workgroup
   return (g.M + tile_shape(gemm_pick_tile(g)).bm - 1) / tile_shape(gemm_pick_tile(g)).bm;
 }
 
@@ -358,7 +362,7 @@ static int k_per_split(int K, int splits, int bk) {
 }
 
 int gemm_splits_used(const GemmArgs& g) {
-  if (g.tile >= GEMM_S64) return 1;
+  if (is_stream_tile(g.tile)) return 1;
   const int bk = tile_shape(gemm_pick_tile(g)).bk;
   const int kps = k_per_split(g.K, g.splits, bk);
   return (g.K + kps - 1) / kps;
@@ -419,7 +423,7 @@ void gemm_tile_shape(int t, int& bm, int& bn, int& bk) {
 int gemm_k_per_split(int K, int splits, int bk) { return k_per_split(K, splits, bk); }
 
 void gemm_bf16(const GemmArgs& g, hipStream_t st) {
-  if (g.tile >= GEMM_S64) {
+  if (is_stream_tile(g.tile)) {
     gemm_stream(g, st);
     return;
   }
@@ -441,6 +445,11 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
   k.bst_shift = g.bst_shift;
   k.bst_bits = g.bst_bits;
   const dim3 grid(tiles, zs);
+  if (t == GEMM_B256) {
+    gemm_big(g, k, zs, st);
+    if (zs > 1) splitk_reduce(g, zs, st);
+    return;
+  }
   switch (t) {
     case GEMM_T128x128x64: launch_tile<128, 128, 64>(g, k, epi, grid, st); break;
     case GEMM_T256x64x32: launch_tile<256, 64, 32>(g, k, epi, grid, st); break;

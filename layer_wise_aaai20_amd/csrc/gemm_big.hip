@@ -1,0 +1,246 @@
+// Large-tile bf16 MFMA GEMM for gfx950: 256x256 output tile per 512-thread workgroup (8 waves as
+// 2 (M) x 4 (N), each wave 128x64), BK = 64, both operands K-contiguous (A [M][K], B [N][K]:
+// x·Wᵀ of a Linear / 1x1 convolution, and the square benchmark shapes).
+//
+// Why a second GEMM structure: the 128x128 / 4-wave tiles of gemm_core.h cross a workgroup barrier
+// with vmcnt(0) once per K-step, which caps them near 900 TFLOP/s on large problems
+// (profiles/r2_gemm_tile_experiments.txt: 8192^3 at 0.84-1.05 PF vs hipBLASLt 1.45-1.57). Here the
+// LDS-DMA prefetch stays in flight across the barriers (cdna_hip_programming.md §5 "256² 8-phase
+// template"):
+//   * LDS = 2 buffers x 4 half-tiles of 16 KB (A rows of quadrant row 0 / 1, B cols of quadrant
+//     col 0 / 1), filled by buffer_load ... lds (16 B per lane, XOR-swizzled on the SOURCE address
+//     so the lane-linear LDS image is bank-conflict free for ds_read_b128);
+//   * each K-tile is computed in 4 phases, one 64x32 C-quadrant per wave per phase
+//     (16 x v_mfma_f32_16x16x32_bf16). A phase is  R: ds_reads + one half-tile DMA + counted waits
+//     | barrier | M: the MFMA cluster (s_setprio 1) | barrier;
+//   * the two wave rows run staggered by one barrier (row 1 takes an extra barrier up front), so on
+//     every SIMD one wave reads LDS / issues DMA while its partner runs MFMAs;
+//   * a half-tile is refilled for a later K-tile one phase after its last read (the reads are
+//     retired by lgkmcnt(0) before the barrier that ends R, so with the stagger both rows are past
+//     them), and five half-tiles stay in flight: every load gets 6-7 phases to land;
+//   * one `s_waitcnt vmcnt(10)` (5 half-tiles x 2 loads) at the end of R in P0, P1, P3 retires the
+//     data read in the next phase; raw s_barrier only (a __syncthreads() would drain every DMA).
+// Issue order in K-tile c (buffer c&1; halves A0/A1 = A rows of quadrant row 0/1, B0/B1 = B cols):
+//   P0: read A0,B0 -> Q00   DMA (c+1).A1 -> buffer (c+1)&1   vmcnt: (c).B1 landed
+//   P1: read B1    -> Q01   DMA (c+2).A0 -> buffer c&1       vmcnt: (c).A1 landed
+//   P2: read A1    -> Q11   DMA (c+2).B0 -> buffer c&1
+//   P3: (registers)-> Q10   DMA (c+2).B1 -> buffer c&1       vmcnt: (c+1).A0,B0 landed
+// Epilogues: bf16 / fp32 store with bias + ReLU, or an fp32 split-K slab (reduced by
+// k_splitk_reduce in gemm.hip, fixed order).
+#include "common.h"
+#include "gemm_core.h"
+
+namespace lw {
+
+constexpr int BGT = 512;                     // threads
+constexpr int BBM = 256, BBN = 256, BBK = 64;
+constexpr int BHALF = 128 * BBK;             // bf16 elements per half-tile (16 KB)
+
+// element offset of 16-byte chunk c of stored row r in a half-tile (128-byte rows, XOR swizzle)
+__device__ __forceinline__ int big_off(int r, int c) { return r * BBK + ((c ^ (r & 7)) << 3); }
+
+template <int EPI>
+__global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 4 * BHALF];   // 128 KB, one array
+  const int tiles_n = (p.N + BBN - 1) / BBN, tiles_m = (p.M + BBM - 1) / BBM;
+  int tm, tn;
+  tile_of(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BBM, n0 = tn * BBN;
+  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int T = kbeg < kend ? (kend - kbeg + BBK - 1) / BBK : 0;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  const int wm = w >> 2, wn = w & 3;   // wave-uniform (scalar): the stagger branch is a real branch
+
+  // ---- per-thread DMA sources: half h (0,1: A quad rows; 2,3: B quad cols), instruction hh
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, p.a_bytes), rb = make_rsrc(p.B, p.b_bytes);
+  uint32_t voff[4][2];
+  int kch[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int q = threadIdx.x + hh * BGT;           // chunk of the half-tile this lane lands in
+    const int lr = q >> 3, cc = q & 7;
+    const int gc = cc ^ (lr & 7);                   // logical chunk fetched (swizzle at the source)
+    kch[hh] = gc * 8;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa) {
+      const int row = m0 + (lr >> 6) * 128 + qa * 64 + (lr & 63);
+      voff[qa][hh] = row < p.M ? (uint32_t)(((int64_t)row * p.lda + kbeg + gc * 8) * 2) : OOB;
+    }
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int col = n0 + (lr >> 5) * 64 + qb * 32 + (lr & 31);
+      voff[2 + qb][hh] = col < p.N ? (uint32_t)(((int64_t)col * p.ldb + kbeg + gc * 8) * 2) : OOB;
+    }
+  }
+  auto dma = [&](int kt, int buf, int h) {
+    uint16_t* base = lds + (buf * 4 + h) * BHALF;
+    const __amdgpu_buffer_rsrc_t r = h < 2 ? ra : rb;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const bool ok = kt < T && voff[h][hh] != OOB && kbeg + kt * BBK + kch[hh] < kend;
+      glds16(r, base + (w * 64 + hh * BGT) * 8, ok ? voff[h][hh] + (uint32_t)(kt * BBK * 2) : OOB);
+    }
+  };
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa0[4][2], fa1[4][2], fb0[2][2], fb1[2][2];
+  auto read_a = [&](bf16x8 (&f)[4][2], const uint16_t* h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        f[i][s] = *reinterpret_cast<const bf16x8*>(
+            h + big_off(wm * 64 + i * 16 + (l & 15), 4 * s + (l >> 4)));
+  };
+  auto read_b = [&](bf16x8 (&f)[2][2], const uint16_t* h) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        f[j][s] = *reinterpret_cast<const bf16x8*>(
+            h + big_off(wn * 32 + j * 16 + (l & 15), 4 * s + (l >> 4)));
+  };
+  auto mfma_q = [&](f32x4 (&c)[4][2], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], c[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  auto vmc10 = [] { asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); };
+  auto bar = [] { __builtin_amdgcn_s_barrier(); };
+
+  // prologue, in the steady-state issue order: (0,A0) (0,B0) (0,B1) (0,A1) (1,A0) (1,B0) (1,B1);
+  // vmcnt(10) retires the first two (the 5 half-tiles issued after them stay in flight)
+  dma(0, 0, 0); dma(0, 0, 2); dma(0, 0, 3); dma(0, 0, 1);
+  dma(1, 1, 0); dma(1, 1, 2); dma(1, 1, 3);
+  vmc10();
+  if (wm == 1) bar();                 // the stagger: wave row 1 runs one barrier behind row 0
+  bar();
+  for (int c = 0; c < T; ++c) {
+    const int b = c & 1, nb = b ^ 1;
+    const uint16_t* H = lds + b * 4 * BHALF;
+    // P0: Q00
+    read_a(fa0, H);
+    read_b(fb0, H + 2 * BHALF);
+    dma(c + 1, nb, 1);                // (c+1).A1 -> buffer nb (its last reader: P2 of c-1)
+    vmc10();                          // retires (c).B1, read in P1
+    lgkm0();
+    bar();
+    mfma_q(acc[0][0], fa0, fb0);
+    bar();
+    // P1: Q01
+    read_b(fb1, H + 3 * BHALF);
+    dma(c + 2, b, 0);                 // (c+2).A0 -> buffer b (read in P0, retired before its barrier)
+    vmc10();                          // retires (c).A1, read in P2
+    lgkm0();
+    bar();
+    mfma_q(acc[0][1], fa0, fb1);
+    bar();
+    // P2: Q11
+    read_a(fa1, H + BHALF);
+    dma(c + 2, b, 2);                 // (c+2).B0 (read in P0)
+    lgkm0();
+    bar();
+    mfma_q(acc[1][1], fa1, fb1);
+    bar();
+    // P3: Q10 from registers
+    dma(c + 2, b, 3);                 // (c+2).B1 (read in P1)
+    vmc10();                          // retires (c+1).A0 and (c+1).B0, read in P0 of c+1
+    bar();
+    mfma_q(acc[1][0], fa1, fb0);
+    bar();
+  }
+  // no LDS-DMA may land after the workgroup has released its LDS; row 0 takes the barrier row 1
+  // took up front, so both rows have passed the same number when they leave
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wm == 0) bar();
+
+  // ---- epilogue, straight from the accumulators. B was the MFMA's first operand, so lane l holds
+  // C[m = .. + (l & 15)][n = .. + 4 * (l >> 4) + r], r = 0..3.
+  const bool vec4 = (EPI == EPI_PARTIAL ? (p.N & 3) == 0 : (p.ldc & 3) == 0);
+  float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)blockIdx.y * p.M * p.N : nullptr;
+#pragma unroll
+  for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn * 64 + qb * 32 + j * 16 + 4 * (l >> 4);
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (EPI == EPI_STORE && p.bias) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bv[r] = n + r < p.N ? p.bias[n + r] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + wm * 128 + qa * 64 + i * 16 + (l & 15);
+          if (m >= p.M) continue;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = acc[qa][qb][i][j][r];
+            if (EPI == EPI_STORE) {
+              x += bv[r];
+              if (p.relu) x = fmaxf(x, 0.f);
+            }
+            v[r] = x;
+          }
+          if (EPI == EPI_PARTIAL) {
+            float* d = P + (int64_t)m * p.N + n;
+            if (vec4 && n + 3 < p.N) *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+            else for (int r = 0; r < 4 && n + r < p.N; ++r) d[r] = v[r];
+          } else if (p.out_bf16) {
+            uint16_t* d = static_cast<uint16_t*>(p.C) + (int64_t)m * p.ldc + n;
+            if (vec4 && n + 3 < p.N) {
+              *reinterpret_cast<uint2*>(d) =
+                  make_uint2((uint32_t)bf16_rne(v[0]) | ((uint32_t)bf16_rne(v[1]) << 16),
+                             (uint32_t)bf16_rne(v[2]) | ((uint32_t)bf16_rne(v[3]) << 16));
+            } else {
+              for (int r = 0; r < 4 && n + r < p.N; ++r) d[r] = bf16_rne(v[r]);
+            }
+          } else {
+            float* d = static_cast<float*>(p.C) + (int64_t)m * p.ldc + n;
+            if (vec4 && n + 3 < p.N) {
+              float4 o = make_float4(v[0], v[1], v[2], v[3]);
+              if (p.accumulate) {
+                const float4 q = *reinterpret_cast<const float4*>(d);
+                o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+              }
+              *reinterpret_cast<float4*>(d) = o;
+            } else {
+              for (int r = 0; r < 4 && n + r < p.N; ++r) d[r] = p.accumulate ? d[r] + v[r] : v[r];
+            }
+          }
+        }
+      }
+}
+
+bool gemm_big_ok(const GemmArgs& g) {
+  return g.a_kcontig && g.b_kcontig && g.pro_scale == nullptr && g.stats == nullptr &&
+         g.addend == nullptr && (g.K % 8) == 0 && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
+}
+
+void gemm_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st) {
+  const int tiles = ((g.M + BBM - 1) / BBM) * ((g.N + BBN - 1) / BBN);
+  const dim3 grid(tiles, zs), block(BGT);
+  if (zs > 1) hipLaunchKernelGGL((k_gemm_big<EPI_PARTIAL>), grid, block, 0, st, k);
+  else hipLaunchKernelGGL((k_gemm_big<EPI_STORE>), grid, block, 0, st, k);
+}
+
+}  // namespace lw

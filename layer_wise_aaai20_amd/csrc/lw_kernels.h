@@ -218,12 +218,16 @@ enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_
                 GEMM_T64x64x64 = 6,
                 // streaming kernel (persistent, B panel resident in LDS, A straight to registers),
                 // output-panel width 64 / 128 / 256; K must be 64, 128 or 256
-                GEMM_S64 = 11, GEMM_S128 = 12, GEMM_S256 = 13 };
+                GEMM_S64 = 11, GEMM_S128 = 12, GEMM_S256 = 13,
+                // 256x256x64 tile, 8 waves, LDS-DMA kept in flight across barriers (gemm_big.hip);
+                // K-contiguous A and B, no prologue / statistics / addend
+                GEMM_B256 = 21 };
 void gemm_bf16(const GemmArgs& g, hipStream_t st);
 int gemm_pick_tile(const GemmArgs& g);
 int gemm_tiles_m(const GemmArgs& g);
 int gemm_splits_used(const GemmArgs& g);
 bool gemm_stream_ok(const GemmArgs& g);
+bool gemm_big_ok(const GemmArgs& g);
 void splitk_reduce(const GemmArgs& g, int splits, hipStream_t st);   // fixed-order slab reduce
 void gemm_tile_shape(int tile, int& bm, int& bn, int& bk);
 int gemm_k_per_split(int K, int splits, int bk);

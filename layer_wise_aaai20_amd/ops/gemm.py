@@ -23,7 +23,7 @@ def _splits(tiles: int, K: int) -> int:
 
 
 TILES = {"auto": 0, "128x128x32": 1, "128x128x64": 2, "256x64x32": 3, "64x256x32": 4,
-         "256x64x64": 5, "64x64x64": 6}
+         "256x64x64": 5, "64x64x64": 6, "256x256x64": 21}
 
 
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False, splits=1, out_bf16=True):

@@ -1,0 +1,71 @@
+#!/usr/bin/env python
+"""Forward-layout (A [M][K], B [N][K]) GEMM throughput: the 256x256x64 8-wave LDS-DMA kernel
+(tile 21, csrc/gemm_big.hip) vs the 128x128x64 4-wave tile (tile 2) vs hipBLASLt (torch.mm), each
+of ours at its best split-K count. Prints one JSON line per shape (TFLOP/s)."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from layer_wise_aaai20_amd.ops import gemm as G  # noqa: E402
+
+SHAPES = [("sq8192", 8192, 8192, 8192), ("sq4096", 4096, 4096, 4096),
+          ("sq16384x8192", 16384, 16384, 8192),
+          ("vgg fc0 b512", 512, 4096, 25088), ("vgg fc1 b512", 512, 4096, 4096),
+          ("r50 l1 c3", 200704, 256, 64), ("r50 l2 c3", 100352, 512, 128),
+          ("r50 l3 c3", 50176, 1024, 256), ("r50 l4 c3", 12544, 2048, 512),
+          ("r50 l3 c1", 50176, 256, 1024), ("r50 l4 c1", 12544, 512, 2048),
+          ("r50 l2 c1", 100352, 128, 512)]
+SPLITS = (1, 2, 4, 8)
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    only = os.environ.get("ONLY")
+    torch.manual_seed(0)
+    for name, M, N, K in SHAPES:
+        if only and only not in name:
+            continue
+        fl = 2.0 * M * N * K
+        iters = max(3, min(50, int(2e13 / fl)))
+        a = torch.randn(M, K, device="cuda").bfloat16()
+        w = torch.randn(N, K, device="cuda").bfloat16()
+        row = {"shape": name, "M": M, "N": N, "K": K}
+        ref = None
+        for t in (2, 21):
+            best = None
+            for sp in SPLITS:
+                if sp > 1 and K // sp < 256:
+                    continue
+                ms = timeit(lambda: G.gemm_ex(a, K, True, w, K, True, M, N, K, splits=sp, tile=t),
+                            iters)
+                if best is None or ms < best[0]:
+                    best = (ms, sp)
+            row[f"t{t}_tflops"] = round(fl / best[0] / 1e9, 1)
+            row[f"t{t}_splits"] = best[1]
+            c, _ = G.gemm_ex(a, K, True, w, K, True, M, N, K, splits=1, tile=t)
+            if ref is None:
+                ref = c
+            else:
+                row["t21_eq_t2"] = bool(torch.equal(c, ref))
+        row["blas_tflops"] = round(fl / timeit(lambda: torch.mm(a, w.t()), iters) / 1e9, 1)
+        print(json.dumps(row), flush=True)
+        del a, w, ref
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -243,3 +243,40 @@ def test_conv_dgrad_backward_bn_stats_epilogue(stride):
     s = st.sum(0)
     torch.testing.assert_close(s[0], d.sum(0), atol=1e-2, rtol=1e-3)
     torch.testing.assert_close(s[1], (d * (xr.float() - mean)).sum(0), atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 512, 512), (520, 264, 328), (1000, 136, 72),
+                                   (256, 1024, 2048), (64, 40, 8)])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_big_tile(M, N, K, splits):
+    """256x256x64 / 8-wave LDS-DMA kernel (csrc/gemm_big.hip, tile 21): fp32 and bf16 outputs,
+    bias + ReLU, ragged M/N/K edges, split-K, and fp32 accumulate into an existing C."""
+    lib = _lib()
+    torch.manual_seed(7)
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    B = torch.randn(N, K, device="cuda").bfloat16()
+    ref = A.float() @ B.float().t()
+    C, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, splits=splits, out_bf16=False,
+                     tile="256x256x64")
+    torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
+    bias = torch.randn(N, device="cuda")
+    Y, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, bias=bias, relu=True, splits=splits,
+                     tile="256x256x64")
+    torch.testing.assert_close(Y.float(), torch.relu(ref + bias), rtol=2e-2, atol=5e-2)
+    base = torch.randn(M, N, device="cuda")
+    out = base.clone()
+    lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, splits, False, 21, None, None, True,
+                False, out, None, True, 0, None)
+    torch.testing.assert_close(out, base + ref, rtol=1e-3, atol=1e-2)
+
+
+def test_gemm_big_tile_bitwise_vs_128():
+    """Same per-element k order as the 128x128x64 tile (k ascending in 32-wide MFMA steps):
+    the outputs agree exactly."""
+    torch.manual_seed(8)
+    M, N, K = 768, 512, 640
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    B = torch.randn(N, K, device="cuda").bfloat16()
+    c1, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, out_bf16=False, tile="256x256x64")
+    c2, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, out_bf16=False, tile="128x128x64")
+    torch.testing.assert_close(c1, c2, rtol=0, atol=0)

@@ -718,10 +718,8 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
   TORCH_CHECK(b_kcontig || N % 8 == 0, "N must be a multiple of 8 for an N-contiguous B");
   TORCH_CHECK(A.numel() >= (a_kcontig ? (M - 1) * lda + K : (K - 1) * lda + M), "A too small");
   TORCH_CHECK(B.numel() >= (b_kcontig ? (N - 1) * ldb + K : (K - 1) * ldb + N), "B too small");
-  TORCH_CHECK((tile >= 0 && tile <= 6) || (tile >= 11 && tile <= 13) || tile == 21, "tile id");
-  // the 256x256 kernel has no statistics epilogue: the 128x128x64 tile (same BK, so the same
-  // split-K slabs) runs those, and the stats rows below are sized for it
-  if (tile == 21 && want_stats) tile = 2;
+  TORCH_CHECK((tile >= 0 && tile <= 6) || (tile >= 11 && tile <= 13) || tile == 21 || tile == 22,
+              "tile id");
   if (ldc <= 0) ldc = N;
   TORCH_CHECK(ldc >= N, "ldc must be >= N");
   const auto odt = out_bf16 ? at::kBFloat16 : at::kFloat;

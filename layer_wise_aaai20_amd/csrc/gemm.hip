@@ -337,12 +337,13 @@ static TileShape tile_shape(int t) {
     case GEMM_T256x64x64: return {256, 64, 64};
     case GEMM_T64x64x64: return {64, 64, 64};
     case GEMM_B256: return {256, 256, 64};
+    case GEMM_B256x128: return {256, 128, 64};
     default: return {128, 128, 32};
   }
 }
 
 int gemm_pick_tile(const GemmArgs& g) {
-  if (g.tile == GEMM_B256 && !gemm_big_ok(g)) return GEMM_T128x128x64;
+  if ((g.tile == GEMM_B256 || g.tile == GEMM_B256x128) && !gemm_big_ok(g)) return GEMM_T128x128x64;
   if (g.tile > 0) return g.tile;
   if (g.M <= 64 && g.N <= 64) return GEMM_T64x64x64;
   if (g.N <= 64 && g.M >= 512) return GEMM_T256x64x32;
@@ -445,7 +446,7 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
   k.bst_shift = g.bst_shift;
   k.bst_bits = g.bst_bits;
   const dim3 grid(tiles, zs);
-  if (t == GEMM_B256) {
+  if (t == GEMM_B256 || t == GEMM_B256x128) {
     gemm_big(g, k, zs, st);
     if (zs > 1) splitk_reduce(g, zs, st);
     return;

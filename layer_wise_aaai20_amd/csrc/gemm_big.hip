@@ -33,57 +33,89 @@
 namespace lw {
 
 constexpr int BGT = 512;                     // threads
-constexpr int BBM = 256, BBN = 256, BBK = 64;
-constexpr int BHALF = 128 * BBK;             // bf16 elements per half-tile (16 KB)
+constexpr int BBM = 256, BBK = 64;
+constexpr int AHALF = 128 * BBK;             // bf16 elements per A half-tile (16 KB)
 
 // element offset of 16-byte chunk c of stored row r in a half-tile (128-byte rows, XOR swizzle)
 __device__ __forceinline__ int big_off(int r, int c) { return r * BBK + ((c ^ (r & 7)) << 3); }
 
-template <int EPI>
+template <int N>
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// BN = 256 (wave tile 128x64) or 128 (wave tile 128x32); waves 2 (M) x 4 (N)
+template <int BN, int EPI>
 __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 4 * BHALF];   // 128 KB, one array
-  const int tiles_n = (p.N + BBN - 1) / BBN, tiles_m = (p.M + BBM - 1) / BBM;
+  constexpr int BHALF = (BN / 2) * BBK;        // bf16 elements per B half-tile
+  constexpr int BUF = 2 * AHALF + 2 * BHALF;   // one K-tile: A0 A1 B0 B1
+  constexpr int NB = BN / 128;                 // DMA instructions per B half (A: 2)
+  constexpr int QN = BN / 8;                   // columns of a wave's B quadrant
+  constexpr int FQ = QN / 16;                  // 16-wide MFMA blocks per B quadrant
+  // counted waits (loads issued after the half-tile the next phase reads; see the schedule)
+  constexpr int VM_P01 = 3 * 2 + 2 * NB, VM_P3 = 2 * 2 + 3 * NB;
+  static_assert(BN == 256 || BN == 128, "tile width");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];   // one array (rule 4a)
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BBM - 1) / BBM;
   int tm, tn;
   tile_of(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * BBM, n0 = tn * BBN;
+  const int m0 = tm * BBM, n0 = tn * BN;
   const int kbeg = blockIdx.y * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int T = kbeg < kend ? (kend - kbeg + BBK - 1) / BBK : 0;
+  const int klen = kend - kbeg;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
   const int wm = w >> 2, wn = w & 3;   // wave-uniform (scalar): the stagger branch is a real branch
 
-  // ---- per-thread DMA sources: half h (0,1: A quad rows; 2,3: B quad cols), instruction hh
+  // ---- per-thread DMA sources: A half qa (rows), instruction hh; B half qb (cols), instruction hb.
+  // A row-chunk out of range → OOB (the buffer load returns zeros); the offset stays OOB when a
+  // K-step is added (every operand is < 2 GiB)
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, p.a_bytes), rb = make_rsrc(p.B, p.b_bytes);
-  uint32_t voff[4][2];
-  int kch[2];
+  uint32_t va[2][2], vb[2][NB];
+  int ka[2], kb[NB];
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     const int q = threadIdx.x + hh * BGT;           // chunk of the half-tile this lane lands in
     const int lr = q >> 3, cc = q & 7;
     const int gc = cc ^ (lr & 7);                   // logical chunk fetched (swizzle at the source)
-    kch[hh] = gc * 8;
+    ka[hh] = gc * 8;
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa) {
       const int row = m0 + (lr >> 6) * 128 + qa * 64 + (lr & 63);
-      voff[qa][hh] = row < p.M ? (uint32_t)(((int64_t)row * p.lda + kbeg + gc * 8) * 2) : OOB;
-    }
-#pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const int col = n0 + (lr >> 5) * 64 + qb * 32 + (lr & 31);
-      voff[2 + qb][hh] = col < p.N ? (uint32_t)(((int64_t)col * p.ldb + kbeg + gc * 8) * 2) : OOB;
+      va[qa][hh] = row < p.M ? (uint32_t)(((int64_t)row * p.lda + kbeg + gc * 8) * 2) : OOB;
     }
   }
-  auto dma = [&](int kt, int buf, int h) {
-    uint16_t* base = lds + (buf * 4 + h) * BHALF;
-    const __amdgpu_buffer_rsrc_t r = h < 2 ? ra : rb;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const bool ok = kt < T && voff[h][hh] != OOB && kbeg + kt * BBK + kch[hh] < kend;
-      glds16(r, base + (w * 64 + hh * BGT) * 8, ok ? voff[h][hh] + (uint32_t)(kt * BBK * 2) : OOB);
+  for (int hb = 0; hb < NB; ++hb) {
+    const int q = threadIdx.x + hb * BGT;
+    const int lr = q >> 3, cc = q & 7;
+    const int gc = cc ^ (lr & 7);
+    kb[hb] = gc * 8;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int col = n0 + (lr / QN) * (BN / 4) + qb * QN + (lr % QN);
+      vb[qb][hb] = col < p.N ? (uint32_t)(((int64_t)col * p.ldb + kbeg + gc * 8) * 2) : OOB;
+    }
+  }
+  // half h of K-tile kt into buffer buf: 0/1 = A quadrant row 0/1, 2/3 = B quadrant col 0/1.
+  // Chunks past the K range are zero-filled (split-K slices and ragged K); K-tiles past the last
+  // are never read, so their chunks only need to stay inside the operands.
+  auto dma = [&](int kt, int buf, int h) {
+    const uint32_t kofs = (uint32_t)(kt * BBK * 2);
+    if (h < 2) {
+      uint16_t* base = lds + buf * BUF + h * AHALF;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        glds16(ra, base + (w * 64 + hh * BGT) * 8,
+               kt * BBK + ka[hh] < klen ? va[h][hh] + kofs : OOB);
+    } else {
+      uint16_t* base = lds + buf * BUF + 2 * AHALF + (h - 2) * BHALF;
+#pragma unroll
+      for (int hb = 0; hb < NB; ++hb)
+        glds16(rb, base + (w * 64 + hb * BGT) * 8,
+               kt * BBK + kb[hb] < klen ? vb[h - 2][hb] + kofs : OOB);
     }
   };
 
-  f32x4 acc[2][2][4][2];
+  f32x4 acc[2][2][4][FQ];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -91,9 +123,9 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < FQ; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 fa0[4][2], fa1[4][2], fb0[2][2], fb1[2][2];
+  bf16x8 fa0[4][2], fa1[4][2], fb0[FQ][2], fb1[FQ][2];
   auto read_a = [&](bf16x8 (&f)[4][2], const uint16_t* h) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -102,58 +134,57 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
         f[i][s] = *reinterpret_cast<const bf16x8*>(
             h + big_off(wm * 64 + i * 16 + (l & 15), 4 * s + (l >> 4)));
   };
-  auto read_b = [&](bf16x8 (&f)[2][2], const uint16_t* h) {
+  auto read_b = [&](bf16x8 (&f)[FQ][2], const uint16_t* h) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FQ; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
         f[j][s] = *reinterpret_cast<const bf16x8*>(
-            h + big_off(wn * 32 + j * 16 + (l & 15), 4 * s + (l >> 4)));
+            h + big_off(wn * QN + j * 16 + (l & 15), 4 * s + (l >> 4)));
   };
-  auto mfma_q = [&](f32x4 (&c)[4][2], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
+  auto mfma_q = [&](f32x4 (&c)[4][FQ], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[FQ][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FQ; ++j)
           c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], c[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
   auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
-  auto vmc10 = [] { asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); };
   auto bar = [] { __builtin_amdgcn_s_barrier(); };
 
   // prologue, in the steady-state issue order: (0,A0) (0,B0) (0,B1) (0,A1) (1,A0) (1,B0) (1,B1);
-  // vmcnt(10) retires the first two (the 5 half-tiles issued after them stay in flight)
+  // the wait retires the first two (the 5 half-tiles issued after them stay in flight)
   dma(0, 0, 0); dma(0, 0, 2); dma(0, 0, 3); dma(0, 0, 1);
   dma(1, 1, 0); dma(1, 1, 2); dma(1, 1, 3);
-  vmc10();
+  vm_wait<VM_P3>();
   if (wm == 1) bar();                 // the stagger: wave row 1 runs one barrier behind row 0
   bar();
   for (int c = 0; c < T; ++c) {
     const int b = c & 1, nb = b ^ 1;
-    const uint16_t* H = lds + b * 4 * BHALF;
+    const uint16_t* H = lds + b * BUF;
     // P0: Q00
     read_a(fa0, H);
-    read_b(fb0, H + 2 * BHALF);
+    read_b(fb0, H + 2 * AHALF);
     dma(c + 1, nb, 1);                // (c+1).A1 -> buffer nb (its last reader: P2 of c-1)
-    vmc10();                          // retires (c).B1, read in P1
+    vm_wait<VM_P01>();                // retires (c).B1, read in P1
     lgkm0();
     bar();
     mfma_q(acc[0][0], fa0, fb0);
     bar();
     // P1: Q01
-    read_b(fb1, H + 3 * BHALF);
+    read_b(fb1, H + 2 * AHALF + BHALF);
     dma(c + 2, b, 0);                 // (c+2).A0 -> buffer b (read in P0, retired before its barrier)
-    vmc10();                          // retires (c).A1, read in P2
+    vm_wait<VM_P01>();                // retires (c).A1, read in P2
     lgkm0();
     bar();
     mfma_q(acc[0][1], fa0, fb1);
     bar();
     // P2: Q11
-    read_a(fa1, H + BHALF);
+    read_a(fa1, H + AHALF);
     dma(c + 2, b, 2);                 // (c+2).B0 (read in P0)
     lgkm0();
     bar();
@@ -161,7 +192,7 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
     bar();
     // P3: Q10 from registers
     dma(c + 2, b, 3);                 // (c+2).B1 (read in P1)
-    vmc10();                          // retires (c+1).A0 and (c+1).B0, read in P0 of c+1
+    vm_wait<VM_P3>();                 // retires (c+1).A0 and (c+1).B0, read in P0 of c+1
     bar();
     mfma_q(acc[1][0], fa1, fb0);
     bar();
@@ -170,49 +201,61 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   // took up front, so both rows have passed the same number when they leave
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wm == 0) bar();
+  // the statistics fold reuses the LDS: wait until row 1 has drained its DMAs as well
+  if constexpr (EPI == EPI_STATS) bar();
 
   // ---- epilogue, straight from the accumulators. B was the MFMA's first operand, so lane l holds
   // C[m = .. + (l & 15)][n = .. + 4 * (l >> 4) + r], r = 0..3.
   const bool vec4 = (EPI == EPI_PARTIAL ? (p.N & 3) == 0 : (p.ldc & 3) == 0);
   float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)blockIdx.y * p.M * p.N : nullptr;
+  // EPI_STATS: Σv / Σv² of the stored (bf16-rounded) outputs per column over the tile's rows,
+  // folded across the 16 row-lanes by a fixed butterfly and across the two wave rows in LDS
+  float* red = reinterpret_cast<float*>(lds);                     // [2 wave rows][2][BN]
 #pragma unroll
-  for (int qa = 0; qa < 2; ++qa)
+  for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
+    for (int j = 0; j < FQ; ++j) {
+      const int nl = wn * (BN / 4) + qb * QN + j * 16 + 4 * (l >> 4);
+      const int n = n0 + nl;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (EPI != EPI_PARTIAL && p.bias) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn * 64 + qb * 32 + j * 16 + 4 * (l >> 4);
-        float bv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (EPI == EPI_STORE && p.bias) {
+        for (int r = 0; r < 4; ++r) bv[r] = n + r < p.N ? p.bias[n + r] : 0.f;
+      }
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) bv[r] = n + r < p.N ? p.bias[n + r] : 0.f;
-        }
+      for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int m = m0 + wm * 128 + qa * 64 + i * 16 + (l & 15);
-          if (m >= p.M) continue;
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             float x = acc[qa][qb][i][j][r];
-            if (EPI == EPI_STORE) {
+            if (EPI != EPI_PARTIAL) {
               x += bv[r];
               if (p.relu) x = fmaxf(x, 0.f);
             }
             v[r] = x;
           }
+          if (m >= p.M) continue;
           if (EPI == EPI_PARTIAL) {
             float* d = P + (int64_t)m * p.N + n;
             if (vec4 && n + 3 < p.N) *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
             else for (int r = 0; r < 4 && n + r < p.N; ++r) d[r] = v[r];
           } else if (p.out_bf16) {
+            uint16_t h[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              h[r] = bf16_rne(v[r]);
+              v[r] = __uint_as_float((uint32_t)h[r] << 16);
+            }
             uint16_t* d = static_cast<uint16_t*>(p.C) + (int64_t)m * p.ldc + n;
             if (vec4 && n + 3 < p.N) {
               *reinterpret_cast<uint2*>(d) =
-                  make_uint2((uint32_t)bf16_rne(v[0]) | ((uint32_t)bf16_rne(v[1]) << 16),
-                             (uint32_t)bf16_rne(v[2]) | ((uint32_t)bf16_rne(v[3]) << 16));
+                  make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
             } else {
-              for (int r = 0; r < 4 && n + r < p.N; ++r) d[r] = bf16_rne(v[r]);
+              for (int r = 0; r < 4 && n + r < p.N; ++r) d[r] = h[r];
             }
           } else {
             float* d = static_cast<float*>(p.C) + (int64_t)m * p.ldc + n;
@@ -227,20 +270,55 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
               for (int r = 0; r < 4 && n + r < p.N; ++r) d[r] = p.accumulate ? d[r] + v[r] : v[r];
             }
           }
+          if (EPI == EPI_STATS) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { s1[r] += v[r]; s2[r] += v[r] * v[r]; }
+          }
+        }
+      if (EPI == EPI_STATS) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s1[r] += __shfl_xor(s1[r], o, 64);
+            s2[r] += __shfl_xor(s2[r], o, 64);
+          }
+        }
+        if ((l & 15) == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            red[(wm * 2 + 0) * BN + nl + r] = s1[r];
+            red[(wm * 2 + 1) * BN + nl + r] = s2[r];
+          }
         }
       }
+    }
+  if constexpr (EPI == EPI_STATS) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < BN; c += BGT) {
+      const int n = n0 + c;
+      if (n >= p.N) continue;
+      p.stats[(int64_t)tm * 2 * p.N + n] = red[0 * BN + c] + red[2 * BN + c];
+      p.stats[(int64_t)tm * 2 * p.N + p.N + n] = red[1 * BN + c] + red[3 * BN + c];
+    }
+  }
 }
 
 bool gemm_big_ok(const GemmArgs& g) {
-  return g.a_kcontig && g.b_kcontig && g.pro_scale == nullptr && g.stats == nullptr &&
-         g.addend == nullptr && (g.K % 8) == 0 && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
+  return g.a_kcontig && g.b_kcontig && g.pro_scale == nullptr && g.addend == nullptr &&
+         g.bst_x == nullptr && (g.K % 8) == 0 && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
 }
 
 void gemm_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st) {
-  const int tiles = ((g.M + BBM - 1) / BBM) * ((g.N + BBN - 1) / BBN);
+  const int bn = g.tile == GEMM_B256 ? 256 : 128;
+  const int tiles = ((g.M + BBM - 1) / BBM) * ((g.N + bn - 1) / bn);
   const dim3 grid(tiles, zs), block(BGT);
-  if (zs > 1) hipLaunchKernelGGL((k_gemm_big<EPI_PARTIAL>), grid, block, 0, st, k);
-  else hipLaunchKernelGGL((k_gemm_big<EPI_STORE>), grid, block, 0, st, k);
+#define LW_BIG(BNV)                                                                              \
+  if (zs > 1) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_PARTIAL>), grid, block, 0, st, k);         \
+  else if (g.stats) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STATS>), grid, block, 0, st, k);     \
+  else hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STORE>), grid, block, 0, st, k);
+  if (bn == 256) { LW_BIG(256) } else { LW_BIG(128) }
+#undef LW_BIG
 }
 
 }  // namespace lw

@@ -796,12 +796,14 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
         }
-        if (EPI == EPI_STATS && !bf_out && m0 + ml < Mrow) {
+        // column statistics of the stored values (bf16-rounded when the output is bf16), from
+        // the accumulators: a per-lane sum over the FM row blocks, then a 16-lane butterfly
+        if (EPI == EPI_STATS && m0 + ml < Mrow) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) { s1[r] += v[r]; s2[r] += v[r] * v[r]; }
         }
       }
-      if (EPI == EPI_STATS && !bf_out) {
+      if (EPI == EPI_STATS) {
         // the 16 rows held by lanes sharing l>>4, fixed butterfly order
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
@@ -821,9 +823,10 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       }
     }
   }
-  // Column statistics come from the staged bf16 tile during the store pass: a thread's chunks
-  // all cover the same 8 columns (GT is a multiple of BN/8), so it sums them in registers and
-  // one LDS fold per tile finishes the job (no cross-lane shuffles in the epilogue).
+  // EPI_BSTATS sums come from the stored chunks during the store pass: a thread's chunks all
+  // cover the same 8 columns (GT is a multiple of BN/8), so it sums them in registers and one
+  // LDS fold per tile finishes the job. (EPI_STATS folds in registers above: summing the staged
+  // tile here cost 35-58 % of a K <= 256 forward GEMM, profiles/r3/gemm_big_v3_stats.jsonl.)
   static_assert(GT % (BN / 8) == 0, "store chunks must keep their column per thread");
   float cs1[8], cs2[8];
 #pragma unroll
@@ -863,19 +866,6 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       const int gm = m0 + r, gn = n0 + cc;
       if (gm >= Mrow || gn >= p.N) return;
       const uint16_t* src = Ch + r * LDH + cc;
-      if (EPI == EPI_STATS) {
-        const uint4 q = *reinterpret_cast<const uint4*>(src);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float lo = __uint_as_float(w[k] << 16), hi = __uint_as_float(w[k] & 0xffff0000u);
-          const bool in_lo = gn + 2 * k < p.N, in_hi = gn + 2 * k + 1 < p.N;
-          cs1[2 * k] += in_lo ? lo : 0.f;
-          cs2[2 * k] += in_lo ? lo * lo : 0.f;
-          cs1[2 * k + 1] += in_hi ? hi : 0.f;
-          cs2[2 * k + 1] += in_hi ? hi * hi : 0.f;
-        }
-      }
       const int64_t orow = orow_of(gm);
       uint16_t* dst = static_cast<uint16_t*>(p.C) + orow * p.ldc + gn;
       // the addend is aligned with the OUTPUT rows (a parity class adds into its own pixels,
@@ -999,7 +989,17 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
     }
     return;
   }
-  if (EPI == EPI_STATS || EPI == EPI_BSTATS) {
+  if (EPI == EPI_STATS) {
+    // the two wave rows' column sums (red[], written before the store pass's barrier)
+    for (int c = threadIdx.x; c < BN; c += GT) {
+      const int n = n0 + c;
+      if (n >= p.N) continue;
+      const int srow = tm + (GA ? zc * tiles_m : 0);
+      p.stats[(int64_t)srow * 2 * p.N + n] = red[0 * BN + c] + red[2 * BN + c];
+      p.stats[(int64_t)srow * 2 * p.N + p.N + n] = red[1 * BN + c] + red[3 * BN + c];
+    }
+  }
+  if (EPI == EPI_BSTATS) {
     // fold the per-thread column sums: GT/(BN/8) threads share each 8-column group
     constexpr int G8 = BN / 8, Q = GT / G8;
     // statistics row: the M-tile (+ the parity class: classes stack their tiles_m rows)

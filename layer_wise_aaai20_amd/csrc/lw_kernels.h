@@ -221,7 +221,7 @@ enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_
                 GEMM_S64 = 11, GEMM_S128 = 12, GEMM_S256 = 13,
                 // 256x256x64 tile, 8 waves, LDS-DMA kept in flight across barriers (gemm_big.hip);
                 // K-contiguous A and B, no prologue / statistics / addend
-                GEMM_B256 = 21 };
+                GEMM_B256 = 21, GEMM_B256x128 = 22 };
 void gemm_bf16(const GemmArgs& g, hipStream_t st);
 int gemm_pick_tile(const GemmArgs& g);
 int gemm_tiles_m(const GemmArgs& g);

@@ -67,6 +67,7 @@ MAT_A2 = os.environ.get("LWAAAI_MAT_A2", "1") != "0"
 BSTATS = os.environ.get("LWAAAI_BSTATS", "0") == "1"
 TILES = (1, 2, 3, 4, 5, 6)          # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
+BIG = (21, 22)                      # 256x256 / 256x128 8-wave LDS-DMA kernel (csrc/gemm_big.hip)
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -87,7 +88,7 @@ def _splits(tiles: int, K: int) -> int:
 
 def _tile_dims(t: int) -> Tuple[int, int]:
     return {1: (128, 128), 2: (128, 128), 3: (256, 64), 4: (64, 256), 5: (256, 64),
-            6: (64, 64)}[t]
+            6: (64, 64), 21: (256, 256), 22: (256, 128)}[t]
 
 
 class GemmTuner:
@@ -164,9 +165,12 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
         lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile), out_bf16,
                     tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits,
                     bx, bm, bss, bb)
-    cands = TILES + (() if bst is not None else
-                     stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a,
-                                  addend is not None, split_k, accumulate))
+    # the big tiles take both operands K-contiguous, no prologue / addend / backward statistics
+    big = BIG if (a_kc and b_kc and pro is None and addend is None and bst is None
+                  and K % 8 == 0) else ()
+    cands = TILES + big + (() if bst is not None else
+                           stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None,
+                                        pro_on_a, addend is not None, split_k, accumulate))
     tile = TUNER.pick(key, run, cands)
     return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile),
                        out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc,

@@ -23,7 +23,7 @@ def _splits(tiles: int, K: int) -> int:
 
 
 TILES = {"auto": 0, "128x128x32": 1, "128x128x64": 2, "256x64x32": 3, "64x256x32": 4,
-         "256x64x64": 5, "64x64x64": 6, "256x256x64": 21}
+         "256x64x64": 5, "64x64x64": 6, "256x256x64": 21, "256x128x64": 22}
 
 
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False, splits=1, out_bf16=True):
@@ -47,13 +47,14 @@ class LinearTuner:
     split count differ per layer and pass (``profiles/r2_linear_vs_blas*.log``)."""
 
     TILES = (1, 2, 3, 4, 5, 6)
+    BIG = (21, 22)                    # 8-wave LDS-DMA tiles: both operands K-contiguous only
     SPLITS = (1, 2, 4, 8, 16)
 
     def __init__(self):
         self.best = {}
         self.enabled = os.environ.get("LWAAAI_GEMM_TUNE", "1") != "0"
 
-    def pick(self, key, tiles_of, K, run):
+    def pick(self, key, tiles_of, K, run, big=False):
         c = self.best.get(key)
         if c is not None:
             return c
@@ -64,7 +65,7 @@ class LinearTuner:
             self.best[key] = default
             return default
         times = []
-        for t in self.TILES:
+        for t in self.TILES + (self.BIG if big else ()):
             for sp in self.SPLITS:
                 if sp > 1 and K // sp < 256:
                     continue
@@ -98,7 +99,7 @@ def _gemm_tuned(kind, A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False
         return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias, relu, sp, out_bf16, t, None,
                            None, True, False, dst, None, acc, 0, None)[0]
     key = (kind, M, N, K, bias is not None, relu, out_bf16)
-    t, sp = TUNER.pick(key, _tiles(M, N), K, run)
+    t, sp = TUNER.pick(key, _tiles(M, N), K, run, big=a_kc and b_kc and K % 8 == 0)
     return run(t, sp, out, accumulate)
 
 

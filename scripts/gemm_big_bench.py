@@ -14,22 +14,32 @@ from layer_wise_aaai20_amd.ops import gemm as G  # noqa: E402
 SHAPES = [("sq8192", 8192, 8192, 8192), ("sq4096", 4096, 4096, 4096),
           ("sq16384x8192", 16384, 16384, 8192),
           ("vgg fc0 b512", 512, 4096, 25088), ("vgg fc1 b512", 512, 4096, 4096),
-          ("r50 l1 c3", 200704, 256, 64), ("r50 l2 c3", 100352, 512, 128),
-          ("r50 l3 c3", 50176, 1024, 256), ("r50 l4 c3", 12544, 2048, 512),
-          ("r50 l3 c1", 50176, 256, 1024), ("r50 l4 c1", 12544, 512, 2048),
-          ("r50 l2 c1", 100352, 128, 512)]
+          # ResNet-50 at batch 256: 1x1 forward convs (M = pixels, N = out, K = in channels);
+          # the c1 shapes are also the data-gradient GEMMs of the c3 convs with Wᵀ as B
+          ("r50 l1 c1", 802816, 64, 256), ("r50 l1 c3", 802816, 256, 64),
+          ("r50 l2 c1", 200704, 128, 512), ("r50 l2 c3", 200704, 512, 128),
+          ("r50 l3 c1", 50176, 256, 1024), ("r50 l3 c3", 50176, 1024, 256),
+          ("r50 l4 c1", 12544, 512, 2048), ("r50 l4 c3", 12544, 2048, 512)]
 SPLITS = (1, 2, 4, 8)
 
 
 def timeit(fn, iters):
+    """Device time per call: the calls are captured into one HIP graph and replayed, so host
+    launch overhead (allocations, binding) does not hide small kernels."""
     fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(iters):
-        fn()
+    g.replay()
     e.record()
     e.synchronize()
+    del g
     return s.elapsed_time(e) / iters
 
 
@@ -45,7 +55,7 @@ def main():
         w = torch.randn(N, K, device="cuda").bfloat16()
         row = {"shape": name, "M": M, "N": N, "K": K}
         ref = None
-        for t in (2, 21):
+        for t in (2, 21, 22):
             best = None
             for sp in SPLITS:
                 if sp > 1 and K // sp < 256:
@@ -56,11 +66,25 @@ def main():
                     best = (ms, sp)
             row[f"t{t}_tflops"] = round(fl / best[0] / 1e9, 1)
             row[f"t{t}_splits"] = best[1]
+            if name.startswith("r50"):      # conv forward: BN statistics in the epilogue
+                ms = timeit(lambda: G.gemm_ex(a, K, True, w, K, True, M, N, K, tile=t, stats=True),
+                            iters)
+                row[f"t{t}_stats_tflops"] = round(fl / ms / 1e9, 1)
             c, _ = G.gemm_ex(a, K, True, w, K, True, M, N, K, splits=1, tile=t)
             if ref is None:
                 ref = c
             else:
-                row["t21_eq_t2"] = bool(torch.equal(c, ref))
+                row[f"t{t}_eq_t2"] = bool(torch.equal(c, ref))
+        if name.startswith("r50"):
+            # data-gradient layout: B = W as stored for the forward ([K][N] here, N-contiguous)
+            wt = w.t().contiguous()
+            ms = timeit(lambda: G.gemm_ex(a, K, True, wt, N, False, M, N, K, tile=2), iters)
+            row["t2_nkc_tflops"] = round(fl / ms / 1e9, 1)
+            if K in (64, 128, 256):       # streaming kernel (B panel resident in LDS)
+                best = min(timeit(lambda: G.gemm_ex(a, K, True, w, K, True, M, N, K, tile=t,
+                                                    stats=True), iters)
+                           for t in (11, 12, 13) if not (K == 256 and t == 13))
+                row["stream_stats_tflops"] = round(fl / best / 1e9, 1)
         row["blas_tflops"] = round(fl / timeit(lambda: torch.mm(a, w.t()), iters) / 1e9, 1)
         print(json.dumps(row), flush=True)
         del a, w, ref

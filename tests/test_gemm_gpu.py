@@ -86,7 +86,8 @@ def test_gemm_tiles(tile, a_kc, b_kc):
         torch.testing.assert_close(C, _ref(Am, Bm), rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("tile", ["128x128x32", "256x64x32", "64x256x32", "64x64x64"])
+@pytest.mark.parametrize("tile", ["128x128x32", "256x64x32", "64x256x32", "64x64x64",
+                                  "256x256x64", "256x128x64"])
 def test_gemm_stats_epilogue(tile):
     """Per-column Σ / Σ² of the bf16 output per M-tile (BatchNorm statistics in the epilogue)."""
     torch.manual_seed(2)
@@ -94,7 +95,8 @@ def test_gemm_stats_epilogue(tile):
     x = torch.randn(M, K, device="cuda").bfloat16()
     w = torch.randn(N, K, device="cuda").bfloat16()
     C, st = G.gemm_ex(x, K, True, w, K, True, M, N, K, tile=tile, stats=True)
-    bm = {"128x128x32": 128, "256x64x32": 256, "64x256x32": 64, "64x64x64": 64}[tile]
+    bm = {"128x128x32": 128, "256x64x32": 256, "64x256x32": 64, "64x64x64": 64,
+          "256x256x64": 256, "256x128x64": 256}[tile]
     tiles_m = -(-M // bm)
     assert st.shape == (tiles_m, 2, N)
     c = C.float()
@@ -248,7 +250,8 @@ def test_conv_dgrad_backward_bn_stats_epilogue(stride):
 @pytest.mark.parametrize("M,N,K", [(512, 512, 512), (520, 264, 328), (1000, 136, 72),
                                    (256, 1024, 2048), (64, 40, 8)])
 @pytest.mark.parametrize("splits", [1, 3])
-def test_gemm_big_tile(M, N, K, splits):
+@pytest.mark.parametrize("tile", ["256x256x64", "256x128x64"])
+def test_gemm_big_tile(M, N, K, splits, tile):
     """256x256x64 / 8-wave LDS-DMA kernel (csrc/gemm_big.hip, tile 21): fp32 and bf16 outputs,
     bias + ReLU, ragged M/N/K edges, split-K, and fp32 accumulate into an existing C."""
     lib = _lib()
@@ -257,26 +260,27 @@ def test_gemm_big_tile(M, N, K, splits):
     B = torch.randn(N, K, device="cuda").bfloat16()
     ref = A.float() @ B.float().t()
     C, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, splits=splits, out_bf16=False,
-                     tile="256x256x64")
+                     tile=tile)
     torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
     bias = torch.randn(N, device="cuda")
     Y, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, bias=bias, relu=True, splits=splits,
-                     tile="256x256x64")
+                     tile=tile)
     torch.testing.assert_close(Y.float(), torch.relu(ref + bias), rtol=2e-2, atol=5e-2)
     base = torch.randn(M, N, device="cuda")
     out = base.clone()
-    lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, splits, False, 21, None, None, True,
-                False, out, None, True, 0, None)
+    lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, splits, False, G.TILES[tile], None,
+                None, True, False, out, None, True, 0, None)
     torch.testing.assert_close(out, base + ref, rtol=1e-3, atol=1e-2)
 
 
-def test_gemm_big_tile_bitwise_vs_128():
+@pytest.mark.parametrize("tile", ["256x256x64", "256x128x64"])
+def test_gemm_big_tile_bitwise_vs_128(tile):
     """Same per-element k order as the 128x128x64 tile (k ascending in 32-wide MFMA steps):
     the outputs agree exactly."""
     torch.manual_seed(8)
     M, N, K = 768, 512, 640
     A = torch.randn(M, K, device="cuda").bfloat16()
     B = torch.randn(N, K, device="cuda").bfloat16()
-    c1, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, out_bf16=False, tile="256x256x64")
+    c1, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, out_bf16=False, tile=tile)
     c2, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, out_bf16=False, tile="128x128x64")
     torch.testing.assert_close(c1, c2, rtol=0, atol=0)

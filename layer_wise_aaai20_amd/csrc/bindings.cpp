@@ -907,14 +907,14 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
   Tensor C;
   if (ga) {
     TORCH_CHECK(out_bf16 && !accumulate, "row-gather convs write bf16");
-    TORCH_CHECK(h.nclass == 1 || !b_kcontig, "parity classes are a data-gradient feature");
     for (int i = 0; i < h.nclass; ++i) {
       const int64_t need = b_kcontig ? h.b_off[i] + (N - 1) * ldb + h.K[i]
                                      : h.b_off[i] + (int64_t)(h.K[i] - 1) * ldb + N;
       TORCH_CHECK(h.K[i] == 0 || Op.numel() >= need, "weight operand too small for class ", i);
       TORCH_CHECK(h.b_off[i] % 8 == 0, "class weight offset alignment");
     }
-    TORCH_CHECK(ldb % 8 == 0 && ldb >= (b_kcontig ? h.K[0] : N), "ldb");
+    TORCH_CHECK(ldb % 8 == 0 && ldb >= (b_kcontig ? *std::max_element(h.K, h.K + h.nclass) : N),
+                "ldb");
     g.M = (int)Mmax;
     g.K = *std::max_element(h.K, h.K + h.nclass);   // one K range per workgroup: the largest
     g.A = ptr<uint16_t>(G);

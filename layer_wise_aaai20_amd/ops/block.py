@@ -52,6 +52,7 @@ import torch.nn.functional as F
 
 from ._ext import load
 from .conv import conv_dgrad, conv_fwd, conv_wgrad
+from .tuning import Tuner
 
 BF16 = torch.bfloat16
 CL = torch.channels_last
@@ -91,37 +92,17 @@ def _tile_dims(t: int) -> Tuple[int, int]:
             6: (64, 64), 21: (256, 256), 22: (256, 128)}[t]
 
 
-class GemmTuner:
+class GemmTuner(Tuner):
     """MIOpen-find-style tile selection for the MFMA GEMM: the first time a problem key is seen,
     every tile shape is timed with HIP events on scratch outputs and the fastest is kept for the
-    rest of the run. ``LWAAAI_GEMM_TUNE=0`` falls back to the built-in heuristic."""
+    rest of the run. ``LWAAAI_GEMM_TUNE=0`` falls back to the built-in heuristic;
+    ``LWAAAI_TUNE_FILE`` pins the choices (``ops/tuning.py``)."""
 
     def __init__(self):
-        self.best: Dict[tuple, int] = {}
-        self.enabled = os.environ.get("LWAAAI_GEMM_TUNE", "1") != "0"
+        super().__init__("gemm", "LWAAAI_GEMM_TUNE")
 
     def pick(self, key, run, candidates=TILES) -> int:
-        t = self.best.get(key)
-        if t is not None:
-            return t
-        if torch.cuda.is_current_stream_capturing():
-            return 0                  # no timing inside a graph capture; tune on the next eager call
-        if not self.enabled:
-            self.best[key] = 0
-            return 0
-        times = []
-        for tile in candidates:
-            run(tile)                                  # compile / warm
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(3):
-                run(tile)
-            e.record()
-            e.synchronize()
-            times.append((s.elapsed_time(e), tile))
-        t = min(times)[1]
-        self.best[key] = t
-        return t
+        return super().pick(key, run, candidates, 0)
 
 
 TUNER = GemmTuner()
@@ -175,6 +156,29 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
     return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile),
                        out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc,
                        addend_bits, bx, bm, bss, bb)
+
+
+LAYOUT_TUNER = Tuner("dgrad-layout", "LWAAAI_GEMM_TUNE")
+
+
+def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
+    """Data-gradient GEMM ``dy[M, K] · W[K, N]`` of a 1x1 convolution (W is the forward weight
+    [out = K][in = N], N-contiguous as a GEMM B operand). Two layouts are timed on first sight:
+    W as stored (the kernel's transposing LDS reads), or Wᵀ copied to [N][K] (a few µs: at most
+    2048x512) so that both operands are K-contiguous and the LDS-DMA staging and the big tiles
+    apply. ``bst`` (backward statistics) needs the stored layout."""
+    def run(layout, **over):
+        args = dict(kw, **over)
+        if layout == "kc":
+            wt = W.t().contiguous()
+            return gemm(dy, ldy, True, wt, K, True, M, N, K, **args)
+        return gemm(dy, ldy, True, W, N, False, M, N, K, **args)
+    if kw.get("bst") is not None:
+        return run("nkc")
+    key = (M, N, K, kw.get("addend") is not None, kw.get("out") is not None)
+    # timed on a scratch output (``out`` may also be the addend: dx += ... in place)
+    layout = LAYOUT_TUNER.pick(key, lambda c: run(c, out=None), ("nkc", "kc"), "nkc")
+    return run(layout)
 
 
 # ----------------------------------------------------------------------------- cross-block BN3
@@ -372,8 +376,8 @@ class _BottleneckFn(torch.autograd.Function):
              pro_on_a=False, out=dst3, accumulate=True, split_k=True)
         grads["w3"] = _finish_wgrad(w3, dst3, d3)
         # da2 = dc3·W3, its epilogue doing BN2's backward reduction (mask from c2 via ss2)
-        da2, rows2 = gemm(dc3, cout, True, W3, width, False, M2, width, cout, stats=BSTATS,
-                          bst=(c2, mean2, ss2, None) if BSTATS else None)
+        da2, rows2 = gemm_dgrad(dc3, cout, W3, M2, width, cout, stats=BSTATS,
+                                bst=(c2, mean2, ss2, None) if BSTATS else None)
         o2 = _bn_grad_outs(g2p, b2p)
         dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False,
                                       None, o2[0], o2[1], rows2 if BSTATS else None)
@@ -421,9 +425,9 @@ class _BottleneckFn(torch.autograd.Function):
                 conv_wgrad(_nchw(dcd, N2, H2, W2_), x, (cout, Cin, 1, 1), s, 0,
                            out=dstd.view(cout, Cin, 1, 1))
             grads["wd"] = _finish_wgrad(wd, dstd, dd)
-            dx, _ = gemm(dc1, width, True, W1, Cin, False, M, Cin, width)
+            dx, _ = gemm_dgrad(dc1, width, W1, M, Cin, width)
             if s == 1:
-                gemm(dcd, cout, True, Wd, Cin, False, M2, Cin, cout, out=dx, addend=dx)
+                gemm_dgrad(dcd, cout, Wd, M2, Cin, cout, out=dx, addend=dx)
             else:
                 # the shortcut's data gradient lands on every s-th pixel of dx: a 1-class
                 # strided data-gradient conv adding into dx in place (no scatter pass)
@@ -431,10 +435,10 @@ class _BottleneckFn(torch.autograd.Function):
                            out=dx, addend=dx)
         else:
             prev = ctx.prev           # the previous block's (c3, mean3, bits3): reduce its BN3
-            dx, rows_prev = gemm(dc1, width, True, W1, Cin, False, M, Cin, width, addend=dr,
-                                 addend_bits=bits3, stats=prev is not None,
-                                 bst=(prev[0], prev[1], None, prev[2]) if prev is not None
-                                 else None)
+            dx, rows_prev = gemm_dgrad(dc1, width, W1, M, Cin, width, addend=dr,
+                                       addend_bits=bits3, stats=prev is not None,
+                                       bst=(prev[0], prev[1], None, prev[2]) if prev is not None
+                                       else None)
             if prev is not None:
                 _BWD_SLOT[0] = (dx.data_ptr(), rows_prev, prev[0].data_ptr())
         ctx.prev = None

@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ._ext import load
+from .tuning import Tuner
 
 BF16 = torch.bfloat16
 CL = torch.channels_last
@@ -52,37 +53,14 @@ def supported(cin: int, cout: int, groups: int = 1, dilation=(1, 1)) -> bool:
 
 
 # ----------------------------------------------------------------------------- tile tuner
-class ConvTuner:
+class ConvTuner(Tuner):
     """First sight of a problem key: time every candidate (tile, or (tile, splits)) with HIP
     events on scratch outputs and keep the fastest — MIOpen-find-style, but over our own
-    kernels only. ``LWAAAI_CONV_TUNE=0`` keeps the heuristic choice."""
+    kernels only. ``LWAAAI_CONV_TUNE=0`` keeps the heuristic choice; ``LWAAAI_TUNE_FILE`` pins
+    the choices (``ops/tuning.py``)."""
 
     def __init__(self):
-        self.best = {}
-        self.enabled = os.environ.get("LWAAAI_CONV_TUNE", "1") != "0"
-
-    def pick(self, key, run, candidates, default):
-        c = self.best.get(key)
-        if c is not None:
-            return c
-        if torch.cuda.is_current_stream_capturing():
-            return default            # no timing inside a graph capture; tune on the next eager call
-        if not self.enabled or len(candidates) == 1:
-            self.best[key] = default
-            return default
-        times = []
-        for cand in candidates:
-            run(cand)
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(3):
-                run(cand)
-            e.record()
-            e.synchronize()
-            times.append((s.elapsed_time(e), cand))
-        c = min(times, key=lambda t: t[0])[1]
-        self.best[key] = c
-        return c
+        super().__init__("conv", "LWAAAI_CONV_TUNE")
 
 
 TUNER = ConvTuner()
@@ -149,6 +127,21 @@ def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int) -> Tuple[torch
         offs.append(off)
         off += p.numel()
     return torch.cat(parts), offs
+
+
+def pack_dgrad_weight_kc(w: torch.Tensor, classes, sh: int, sw: int):
+    """K-contiguous per-class slabs Wk_c[ci][jr][js][co] = w[co, ci, r0 + sh*jr, s0 + sw*js]
+    (the transpose of :func:`pack_dgrad_weight`'s slabs), each row padded to the largest class K
+    so that one row stride serves every class. Returns (packed, offsets, row stride)."""
+    co, c, R, S = w.shape
+    wt = w.to(BF16).permute(1, 2, 3, 0)                      # [C, R, S, Co]
+    kmax = max(TR * TS * co for (_c, _w, _r, _s, TR, TS, *_x) in classes)
+    kmax = -(-kmax // 8) * 8
+    out = torch.zeros((len(classes), c, kmax), dtype=BF16, device=w.device)
+    for i, (ch, cw, r0, s0, TR, TS, *_r) in enumerate(classes):
+        slab = wt[:, r0::sh][:, :TR][:, :, s0::sw][:, :, :TS].reshape(c, TR * TS * co)
+        out[i, :, :slab.shape[1]].copy_(slab)
+    return out.view(-1), [i * c * kmax for i in range(len(classes))], kmax
 
 
 # ----------------------------------------------------------------------------- the three passes
@@ -219,13 +212,29 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
 
     bx, bm, bss, bb = bst if bst is not None else (None, None, None, None)
 
-    def run(tile, dst=None, add=None):
+    kc = []                           # K-contiguous weight pack, built on first use
+
+    def run(cand, dst=None, add=None):
+        layout, tile = cand
+        if layout == "kc":
+            if not kc:
+                kc.append(pack_dgrad_weight_kc(w, classes, sh, sw))
+            wk, koffs, kmax = kc[0]
+            g = list(geom)
+            for i, off in enumerate(koffs):
+                g[13 + 10 * i + 9] = off
+            return lib.conv_ex(dyc, wk, CV_A, g, c, tile, 1, True, None, None, False, dst, False,
+                               0, True, kmax, add)
         return lib.conv_ex(dyc, wt, CV_A, geom, c, tile, 1, True, None, None, bst is not None,
                            dst, False, 0, False, c, add, bx, bm, bss, bb)
     key = ("d", tuple(dyc.shape), tuple(w.shape), H, W, sh, sw, ph, pw, addend is not None,
            bst is not None)
-    tile = TUNER.pick(key, run, ROW_TILES, _row_default(M, c))   # (timed on scratch outputs)
-    dx, st = run(tile, out, addend)
+    # the weight as [K][C] (the kernel's transposing LDS reads) or packed K-contiguous [C][K]
+    # (LDS-DMA staging of both operands); backward statistics need the first
+    cands = [("nkc", t) for t in ROW_TILES] + \
+        ([("kc", t) for t in ROW_TILES] if bst is None else [])
+    cand = TUNER.pick(key, run, cands, ("nkc", _row_default(M, c)))   # (timed on scratch outputs)
+    dx, st = run(cand, out, addend)
     if bst is not None:
         return _nchw_rows(dx, Nb, H, W), st
     return _nchw_rows(dx, Nb, H, W)

@@ -15,6 +15,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ._ext import load
+from .tuning import Tuner
 
 
 def _splits(tiles: int, K: int) -> int:
@@ -40,46 +41,25 @@ def gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False, splits=1
                           pro_shift, pro_on_a, stats)
 
 
-class LinearTuner:
+class LinearTuner(Tuner):
     """First sight of a Linear GEMM problem: time every (tile, split-K) candidate with HIP events
-    on scratch outputs and keep the fastest (``LWAAAI_GEMM_TUNE=0``: the 128x128 heuristic). The
-    classifier GEMMs are skinny in M (batch 256-512) and span K = 1k-25k, so the right tile and
-    split count differ per layer and pass (``profiles/r2_linear_vs_blas*.log``)."""
+    on scratch outputs and keep the fastest (``LWAAAI_GEMM_TUNE=0``: the 128x128 heuristic;
+    ``LWAAAI_TUNE_FILE`` pins the choices, ``ops/tuning.py``). The classifier GEMMs are skinny in
+    M (batch 256-512) and span K = 1k-25k, so the right tile and split count differ per layer and
+    pass (``profiles/r2_linear_vs_blas*.log``)."""
 
     TILES = (1, 2, 3, 4, 5, 6)
     BIG = (21, 22)                    # 8-wave LDS-DMA tiles: both operands K-contiguous only
     SPLITS = (1, 2, 4, 8, 16)
 
     def __init__(self):
-        self.best = {}
-        self.enabled = os.environ.get("LWAAAI_GEMM_TUNE", "1") != "0"
+        super().__init__("linear", "LWAAAI_GEMM_TUNE")
 
     def pick(self, key, tiles_of, K, run, big=False):
-        c = self.best.get(key)
-        if c is not None:
-            return c
         default = (0, _splits(tiles_of(128, 128), K))
-        if torch.cuda.is_current_stream_capturing():
-            return default            # no timing inside a graph capture; tune on the next eager call
-        if not self.enabled:
-            self.best[key] = default
-            return default
-        times = []
-        for t in self.TILES + (self.BIG if big else ()):
-            for sp in self.SPLITS:
-                if sp > 1 and K // sp < 256:
-                    continue
-                run(t, sp)
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s.record()
-                for _ in range(3):
-                    run(t, sp)
-                e.record()
-                e.synchronize()
-                times.append((s.elapsed_time(e), (t, sp)))
-        c = min(times, key=lambda v: v[0])[1]
-        self.best[key] = c
-        return c
+        cands = [(t, sp) for t in self.TILES + (self.BIG if big else ()) for sp in self.SPLITS
+                 if sp == 1 or K // sp >= 256]
+        return super().pick(key, lambda c: run(*c), cands, default)
 
 
 TUNER = LinearTuner()

@@ -61,6 +61,30 @@ def test_conv_dgrad(shape):
     _close(dx, xf.grad, 1e-2)
 
 
+@pytest.mark.parametrize("layout", ["nkc", "kc"])
+@pytest.mark.parametrize("shape", [s for s in SHAPES if s[1] % 8 == 0],
+                         ids=[str(s) for s in SHAPES if s[1] % 8 == 0])
+def test_conv_dgrad_layouts(shape, layout, monkeypatch):
+    """Both weight layouts the dgrad tuner chooses between (the transposing-read [K][C] pack and
+    the K-contiguous [C][K] pack, parity classes padded to one row stride), every tile, with and
+    without an in-place addend."""
+    N, C, Co, H, k, s, p = shape
+    x, w = _inputs(N, C, Co, H, k, 2)
+    xf = x.float().requires_grad_()
+    ref = F.conv2d(xf, w.float(), stride=s, padding=p)
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    for tile in CV.ROW_TILES:
+        monkeypatch.setattr(CV.TUNER, "pick", lambda key, run, cands, default: (layout, tile))
+        dx = CV.conv_dgrad(dy.contiguous(memory_format=CL), w, (H, H), s, p)
+        _close(dx, xf.grad, 1e-2)
+        rows = torch.randn(N * H * H, C, device="cuda").bfloat16()
+        base = rows.clone()
+        CV.conv_dgrad(dy.contiguous(memory_format=CL), w, (H, H), s, p, out=rows, addend=rows)
+        got = rows.view(N, H, H, C).permute(0, 3, 1, 2).float()
+        _close(got, xf.grad + base.view(N, H, H, C).permute(0, 3, 1, 2).float(), 1e-2)
+
+
 @pytest.mark.parametrize("shape", SHAPES, ids=[str(s) for s in SHAPES])
 def test_conv_wgrad(shape):
     N, C, Co, H, k, s, p = shape

@@ -836,6 +836,33 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
 // gradient) or dY [pixels][M] (weight-gradient modes 3/4). geom = [Nb, Hin, Win, C, sh, sw, dh,
 // dw, Hout, Wout, osy, osx, nclass, then per class TR, TS, oh, ow, Hg, Wg, py, px, K, b_off].
 // Every index the kernels can form is checked here against the tensors' sizes.
+// K-contiguous data-gradient weight pack (csrc/conv.hip k_pack_dgrad_kc): w is a bf16
+// channels_last [Co, C, R, S] weight; cls = 4 ints (r0, s0, TR, TS) per parity class.
+Tensor pack_dgrad_kc(Tensor w, std::vector<int64_t> cls, int64_t sh, int64_t sw, int64_t kmax) {
+  const c10::DeviceGuard guard(w.device());
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4, "pack_dgrad_kc: a 4-d GPU weight");
+  check_dtype(w, at::kBFloat16, "weight");
+  TORCH_CHECK(w.is_contiguous(at::MemoryFormat::ChannelsLast) || (w.size(2) == 1 && w.size(3) == 1
+              && w.is_contiguous()), "weight must be channels_last [Co][R][S][C] in memory");
+  const int Co = (int)w.size(0), C = (int)w.size(1), R = (int)w.size(2), S = (int)w.size(3);
+  const int nclass = (int)(cls.size() / 4);
+  TORCH_CHECK(cls.size() % 4 == 0 && nclass >= 1 && nclass <= 4, "cls: 1..4 classes of 4 ints");
+  TORCH_CHECK(kmax % 8 == 0 && sh >= 1 && sw >= 1, "kmax / strides");
+  int r0[4], s0[4], TR[4], TS[4];
+  for (int i = 0; i < nclass; ++i) {
+    r0[i] = (int)cls[4 * i]; s0[i] = (int)cls[4 * i + 1];
+    TR[i] = (int)cls[4 * i + 2]; TS[i] = (int)cls[4 * i + 3];
+    TORCH_CHECK(r0[i] >= 0 && s0[i] >= 0 && TR[i] >= 1 && TS[i] >= 1 &&
+                r0[i] + sh * (TR[i] - 1) < R && s0[i] + sw * (TS[i] - 1) < S &&
+                (int64_t)TR[i] * TS[i] * Co <= kmax, "class taps outside the kernel window");
+  }
+  Tensor out = at::empty({(int64_t)nclass * C * kmax}, w.options());
+  lw::pack_dgrad_kc(ptr<uint16_t>(w), ptr<uint16_t>(out), Co, C, R, S, (int)sh, (int)sw, nclass,
+                    r0, s0, TR, TS, (int)kmax, cur_stream());
+  launched("pack_dgrad_kc");
+  return out;
+}
+
 std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vector<int64_t> geom,
                                    int64_t N, int64_t tile, int64_t splits, bool out_bf16,
                                    c10::optional<Tensor> pro_scale, c10::optional<Tensor> pro_shift,
@@ -1333,6 +1360,7 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor? addend_bits=None, Tensor? bst_x=None, Tensor? bst_mean=None, "
       "Tensor? bst_scale_shift=None, Tensor? bst_bits=None) "
       "-> (Tensor, Tensor)");
+  m.def("pack_dgrad_kc(Tensor w, int[] cls, int sh, int sw, int kmax) -> Tensor");
   m.def(
       "conv_ex(Tensor G, Tensor Op, int mode, int[] geom, int N, int tile, int splits, "
       "bool out_bf16, Tensor? pro_scale, Tensor? pro_shift, bool want_stats, Tensor(a!)? out, "
@@ -1376,6 +1404,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);
   m.impl("conv_ex", &conv_ex);
+  m.impl("pack_dgrad_kc", &pack_dgrad_kc);
   m.impl("bn_stats", &bn_stats);
   m.impl("bn_apply", &bn_apply);
   m.impl("stem_pool_fwd", &stem_pool_fwd);

@@ -26,6 +26,63 @@
 
 namespace lw {
 
+// K-contiguous data-gradient weight pack, one launch: out[i][c][k] for parity class i,
+// k = (jr * TS + js) * Co + o < TR * TS * Co, = w[o][r0 + sh * jr][s0 + sw * js][c] (channels_last
+// [Co][R][S][C] source), zero up to the row stride kmax. Each thread writes 8 consecutive k (one
+// 16-byte store); the gathered reads hit L2 (a weight is at most a few MB). A 1x1 convolution
+// (one class, R = S = 1) is the plain transpose Wᵀ.
+struct PackClasses { int r0[4], s0[4], TR[4], TS[4]; };
+
+__global__ __launch_bounds__(256) void k_pack_dgrad_kc(const uint16_t* __restrict__ w,
+                                                       uint16_t* __restrict__ out, int Co, int C,
+                                                       int R, int S, int sh, int sw, int nclass,
+                                                       PackClasses pc, int kmax) {
+  const int64_t per_row = kmax / 8, per_class = (int64_t)C * per_row;
+  const int64_t total = nclass * per_class;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * 256) {
+    const int i = (int)(t / per_class);
+    const int64_t rem = t - i * per_class;
+    const int c = (int)(rem / per_row);
+    const int k0 = (int)(rem - (int64_t)c * per_row) * 8;
+    const int r0 = i == 0 ? pc.r0[0] : i == 1 ? pc.r0[1] : i == 2 ? pc.r0[2] : pc.r0[3];
+    const int s0 = i == 0 ? pc.s0[0] : i == 1 ? pc.s0[1] : i == 2 ? pc.s0[2] : pc.s0[3];
+    const int TR = i == 0 ? pc.TR[0] : i == 1 ? pc.TR[1] : i == 2 ? pc.TR[2] : pc.TR[3];
+    const int TS = i == 0 ? pc.TS[0] : i == 1 ? pc.TS[1] : i == 2 ? pc.TS[2] : pc.TS[3];
+    const int Kc = TR * TS * Co;
+    uint16_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = k0 + q;
+      uint16_t x = 0;
+      if (k < Kc) {
+        const int tap = k / Co, o = k - tap * Co;
+        const int jr = tap / TS, js = tap - jr * TS;
+        const int r = r0 + sh * jr, sx = s0 + sw * js;
+        x = w[(((int64_t)o * R + r) * S + sx) * C + c];
+      }
+      v[q] = x;
+    }
+    *reinterpret_cast<uint4*>(out + (int64_t)i * C * kmax + (int64_t)c * kmax + k0) =
+        make_uint4((uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+                   (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16));
+  }
+}
+
+void pack_dgrad_kc(const uint16_t* w, uint16_t* out, int Co, int C, int R, int S, int sh, int sw,
+                   int nclass, const int* r0, const int* s0, const int* TR, const int* TS,
+                   int kmax, hipStream_t st) {
+  PackClasses pc{};
+  for (int i = 0; i < nclass; ++i) {
+    pc.r0[i] = r0[i]; pc.s0[i] = s0[i]; pc.TR[i] = TR[i]; pc.TS[i] = TS[i];
+  }
+  const int64_t total = (int64_t)nclass * C * (kmax / 8);
+  int64_t blocks = (total + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 4096 ? 4096 : blocks);
+  hipLaunchKernelGGL(k_pack_dgrad_kc, dim3((unsigned)blocks), dim3(256), 0, st, w, out, Co, C, R,
+                     S, sh, sw, nclass, pc, kmax);
+}
+
 static ConvGeom to_device(const ConvGeomHost& h) {
   ConvGeom c{};
   c.Hin = h.Hin; c.Win = h.Win; c.C = h.C;

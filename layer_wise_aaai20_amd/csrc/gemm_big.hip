@@ -43,6 +43,9 @@ template <int N>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
 // BN = 256 (wave tile 128x64) or 128 (wave tile 128x32); waves 2 (M) x 4 (N)
+// (Tried: reading the next K-tile's B0 fragments in P3 after a wait moved to P2, so the LDS reads
+// spread 8/4/8/4 over the phases instead of 12/4/8/0: 251 VGPRs and 7 % slower at 8192^3,
+// profiles/r3/gemm_big_pf_ab.jsonl.)
 template <int BN, int EPI>
 __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   constexpr int BHALF = (BN / 2) * BBK;        // bf16 elements per B half-tile

@@ -227,6 +227,9 @@ int gemm_pick_tile(const GemmArgs& g);
 int gemm_tiles_m(const GemmArgs& g);
 int gemm_splits_used(const GemmArgs& g);
 bool gemm_stream_ok(const GemmArgs& g);
+void pack_dgrad_kc(const uint16_t* w, uint16_t* out, int Co, int C, int R, int S, int sh, int sw,
+                   int nclass, const int* r0, const int* s0, const int* TR, const int* TS,
+                   int kmax, hipStream_t st);
 bool gemm_big_ok(const GemmArgs& g);
 void splitk_reduce(const GemmArgs& g, int splits, hipStream_t st);   // fixed-order slab reduce
 void gemm_tile_shape(int tile, int& bm, int& bn, int& bk);

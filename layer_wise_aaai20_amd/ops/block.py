@@ -169,9 +169,10 @@ def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
     apply. ``bst`` (backward statistics) needs the stored layout."""
     def run(layout, **over):
         args = dict(kw, **over)
-        if layout == "kc":
-            wt = W.t().contiguous()
-            return gemm(dy, ldy, True, wt, K, True, M, N, K, **args)
+        if layout == "kc":            # Wᵀ by one pack launch, timed with the GEMM
+            kp = -(-K // 8) * 8
+            wt = load().pack_dgrad_kc(W.reshape(K, N, 1, 1), [0, 0, 1, 1], 1, 1, kp)
+            return gemm(dy, ldy, True, wt, kp, True, M, N, K, **args)
         return gemm(dy, ldy, True, W, N, False, M, N, K, **args)
     if kw.get("bst") is not None:
         return run("nkc")

@@ -132,16 +132,17 @@ def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int) -> Tuple[torch
 def pack_dgrad_weight_kc(w: torch.Tensor, classes, sh: int, sw: int):
     """K-contiguous per-class slabs Wk_c[ci][jr][js][co] = w[co, ci, r0 + sh*jr, s0 + sw*js]
     (the transpose of :func:`pack_dgrad_weight`'s slabs), each row padded to the largest class K
-    so that one row stride serves every class. Returns (packed, offsets, row stride)."""
+    so that one row stride serves every class; one launch (``csrc/conv.hip k_pack_dgrad_kc``).
+    Returns (packed, offsets, row stride)."""
     co, c, R, S = w.shape
-    wt = w.to(BF16).permute(1, 2, 3, 0)                      # [C, R, S, Co]
     kmax = max(TR * TS * co for (_c, _w, _r, _s, TR, TS, *_x) in classes)
     kmax = -(-kmax // 8) * 8
-    out = torch.zeros((len(classes), c, kmax), dtype=BF16, device=w.device)
-    for i, (ch, cw, r0, s0, TR, TS, *_r) in enumerate(classes):
-        slab = wt[:, r0::sh][:, :TR][:, :, s0::sw][:, :, :TS].reshape(c, TR * TS * co)
-        out[i, :, :slab.shape[1]].copy_(slab)
-    return out.view(-1), [i * c * kmax for i in range(len(classes))], kmax
+    cls = []
+    for (_c, _w, r0, s0, TR, TS, *_x) in classes:
+        cls += [r0, s0, TR, TS]
+    wb = w.to(BF16).contiguous(memory_format=CL)
+    packed = load().pack_dgrad_kc(wb, cls, sh, sw, kmax)
+    return packed, [i * c * kmax for i in range(len(classes))], kmax
 
 
 # ----------------------------------------------------------------------------- the three passes
@@ -212,14 +213,10 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
 
     bx, bm, bss, bb = bst if bst is not None else (None, None, None, None)
 
-    kc = []                           # K-contiguous weight pack, built on first use
-
     def run(cand, dst=None, add=None):
         layout, tile = cand
-        if layout == "kc":
-            if not kc:
-                kc.append(pack_dgrad_weight_kc(w, classes, sh, sw))
-            wk, koffs, kmax = kc[0]
+        if layout == "kc":            # packed per call: the tuner times the pack with the conv
+            wk, koffs, kmax = pack_dgrad_weight_kc(w, classes, sh, sw)
             g = list(geom)
             for i, off in enumerate(koffs):
                 g[13 + 10 * i + 9] = off

@@ -226,3 +226,21 @@ def test_relu_pool_matches_torch(shape, k, s, p):
     m = a.float() > 0
     torch.testing.assert_close(xa.grad.float() * m, xr.grad * m, atol=1e-2, rtol=1e-2)
     assert float(xa.grad.float()[~m].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("shape", [(64, 32, 3, 1, 1), (48, 24, 3, 2, 1), (40, 16, 1, 2, 0),
+                                   (16, 8, 7, 2, 3), (24, 16, 1, 1, 0)])
+def test_pack_dgrad_kc_matches_torch(shape):
+    """One-launch K-contiguous data-gradient weight pack vs the same slabs built with torch."""
+    co, c, k, s, p = shape
+    H = 11
+    w = torch.randn(co, c, k, k, device="cuda").bfloat16().contiguous(memory_format=CL)
+    classes = CV._dgrad_classes(H, H, k, k, s, s, p, p)
+    packed, offs, kmax = CV.pack_dgrad_weight_kc(w, classes, s, s)
+    wt = w.permute(1, 2, 3, 0)                                   # [C, R, S, Co]
+    ref = torch.zeros(len(classes), c, kmax, dtype=torch.bfloat16, device="cuda")
+    for i, (ch, cw, r0, s0, TR, TS, *_r) in enumerate(classes):
+        slab = wt[:, r0::s][:, :TR][:, :, s0::s][:, :, :TS].reshape(c, TR * TS * co)
+        ref[i, :, :slab.shape[1]] = slab
+    assert offs == [i * c * kmax for i in range(len(classes))]
+    assert torch.equal(packed.view(len(classes), c, kmax), ref)

@@ -39,6 +39,30 @@ constexpr int AHALF = 128 * BBK;             // bf16 elements per A half-tile (1
 // element offset of 16-byte chunk c of stored row r in a half-tile (128-byte rows, XOR swizzle)
 __device__ __forceinline__ int big_off(int r, int c) { return r * BBK + ((c ^ (r & 7)) << 3); }
 
+// MN-contiguous operands (A [K][M], B [K][N]: a weight gradient dYᵀ·X) are staged as [k][column]
+// images of W = 128 or 64 columns and read by ds_read_b64_tr_b16 (the transposing LDS read): a
+// lane reads 8 bytes at row k = 32s + 8g + q (+4) and columns i + 4p (gemm_core.h load_frag). The
+// 16-byte chunk of column c in row k is stored at chunk (c/8) ^ x(k), which puts the 8 rows one
+// 32-lane group reads on 8 disjoint 32-byte windows of the bank row (conflict-free); the DMA
+// swizzles its SOURCE address to match, the LDS image stays lane-linear.
+__device__ __forceinline__ int xw128(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
+__device__ __forceinline__ int xw64(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
+template <int W>
+__device__ __forceinline__ bf16x8 frag_tr(const uint16_t* img, int i_base, int s) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, t = l & 15, q = t >> 2, p4 = t & 3;
+  const int k0 = 32 * s + 8 * g + q;
+  const int c = i_base + 4 * p4;
+  const int x = W == 128 ? xw128(k0) : xw64(k0);       // the same for row k0 + 4
+  const uint16_t* p0 = img + k0 * W + ((((c >> 3) ^ x) << 3) | (c & 7));
+  typedef __attribute__((address_space(3))) i16x4 lds_v4;
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0 + 4 * W));
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
@@ -46,7 +70,7 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :
 // (Tried: reading the next K-tile's B0 fragments in P3 after a wait moved to P2, so the LDS reads
 // spread 8/4/8/4 over the phases instead of 12/4/8/0: 251 VGPRs and 7 % slower at 8192^3,
 // profiles/r3/gemm_big_pf_ab.jsonl.)
-template <int BN, int EPI>
+template <int BN, int EPI, bool MN>
 __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   constexpr int BHALF = (BN / 2) * BBK;        // bf16 elements per B half-tile
   constexpr int BUF = 2 * AHALF + 2 * BHALF;   // one K-tile: A0 A1 B0 B1
@@ -73,43 +97,67 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   // K-step is added (every operand is < 2 GiB)
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, p.a_bytes), rb = make_rsrc(p.B, p.b_bytes);
   uint32_t va[2][2], vb[2][NB];
-  int ka[2], kb[NB];
+  int ka[2], kb[NB];                   // k offset of the lane's chunk within a K-tile
+  constexpr int WB = BN / 2;           // MN: columns of a B half image
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     const int q = threadIdx.x + hh * BGT;           // chunk of the half-tile this lane lands in
-    const int lr = q >> 3, cc = q & 7;
-    const int gc = cc ^ (lr & 7);                   // logical chunk fetched (swizzle at the source)
-    ka[hh] = gc * 8;
+    if constexpr (!MN) {
+      const int lr = q >> 3, cc = q & 7;
+      const int gc = cc ^ (lr & 7);                 // logical chunk fetched (swizzle at the source)
+      ka[hh] = gc * 8;
 #pragma unroll
-    for (int qa = 0; qa < 2; ++qa) {
-      const int row = m0 + (lr >> 6) * 128 + qa * 64 + (lr & 63);
-      va[qa][hh] = row < p.M ? (uint32_t)(((int64_t)row * p.lda + kbeg + gc * 8) * 2) : OOB;
+      for (int qa = 0; qa < 2; ++qa) {
+        const int row = m0 + (lr >> 6) * 128 + qa * 64 + (lr & 63);
+        va[qa][hh] = row < p.M ? (uint32_t)(((int64_t)row * p.lda + kbeg + gc * 8) * 2) : OOB;
+      }
+    } else {
+      const int k = q >> 4, lc = (q & 15) ^ xw128(k);   // [64 k][128 m] image
+      ka[hh] = k;
+#pragma unroll
+      for (int qa = 0; qa < 2; ++qa) {
+        const int m = m0 + (lc >> 3) * 128 + qa * 64 + (lc & 7) * 8;
+        va[qa][hh] = m < p.M ? (uint32_t)(((int64_t)(kbeg + k) * p.lda + m) * 2) : OOB;
+      }
     }
   }
 #pragma unroll
   for (int hb = 0; hb < NB; ++hb) {
     const int q = threadIdx.x + hb * BGT;
-    const int lr = q >> 3, cc = q & 7;
-    const int gc = cc ^ (lr & 7);
-    kb[hb] = gc * 8;
+    if constexpr (!MN) {
+      const int lr = q >> 3, cc = q & 7;
+      const int gc = cc ^ (lr & 7);
+      kb[hb] = gc * 8;
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const int col = n0 + (lr / QN) * (BN / 4) + qb * QN + (lr % QN);
-      vb[qb][hb] = col < p.N ? (uint32_t)(((int64_t)col * p.ldb + kbeg + gc * 8) * 2) : OOB;
+      for (int qb = 0; qb < 2; ++qb) {
+        const int col = n0 + (lr / QN) * (BN / 4) + qb * QN + (lr % QN);
+        vb[qb][hb] = col < p.N ? (uint32_t)(((int64_t)col * p.ldb + kbeg + gc * 8) * 2) : OOB;
+      }
+    } else {
+      const int k = q / (WB / 8);
+      const int lc = (q % (WB / 8)) ^ (WB == 128 ? xw128(k) : xw64(k));
+      kb[hb] = k;
+      const int c = lc * 8;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const int n = n0 + (c / QN) * (BN / 4) + qb * QN + (c % QN);
+        vb[qb][hb] = n < p.N ? (uint32_t)(((int64_t)(kbeg + k) * p.ldb + n) * 2) : OOB;
+      }
     }
   }
   // half h of K-tile kt into buffer buf: 0/1 = A quadrant row 0/1, 2/3 = B quadrant col 0/1.
   // Chunks past the K range are zero-filled (split-K slices and ragged K); K-tiles past the last
   // are never read, so their chunks only need to stay inside the operands.
   auto dma = [&](int kt, int buf, int h) {
-    const uint32_t kofs = (uint32_t)(kt * BBK * 2);
     if (h < 2) {
+      const uint32_t kofs = MN ? (uint32_t)(kt * BBK) * (uint32_t)p.lda * 2u : (uint32_t)(kt * BBK * 2);
       uint16_t* base = lds + buf * BUF + h * AHALF;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
         glds16(ra, base + (w * 64 + hh * BGT) * 8,
                kt * BBK + ka[hh] < klen ? va[h][hh] + kofs : OOB);
     } else {
+      const uint32_t kofs = MN ? (uint32_t)(kt * BBK) * (uint32_t)p.ldb * 2u : (uint32_t)(kt * BBK * 2);
       uint16_t* base = lds + buf * BUF + 2 * AHALF + (h - 2) * BHALF;
 #pragma unroll
       for (int hb = 0; hb < NB; ++hb)
@@ -133,17 +181,21 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        f[i][s] = *reinterpret_cast<const bf16x8*>(
+      for (int s = 0; s < 2; ++s) {
+        if constexpr (MN) f[i][s] = frag_tr<128>(h, wm * 64 + i * 16, s);
+        else f[i][s] = *reinterpret_cast<const bf16x8*>(
             h + big_off(wm * 64 + i * 16 + (l & 15), 4 * s + (l >> 4)));
+      }
   };
   auto read_b = [&](bf16x8 (&f)[FQ][2], const uint16_t* h) {
 #pragma unroll
     for (int j = 0; j < FQ; ++j)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        f[j][s] = *reinterpret_cast<const bf16x8*>(
+      for (int s = 0; s < 2; ++s) {
+        if constexpr (MN) f[j][s] = frag_tr<WB>(h, wn * QN + j * 16, s);
+        else f[j][s] = *reinterpret_cast<const bf16x8*>(
             h + big_off(wn * QN + j * 16 + (l & 15), 4 * s + (l >> 4)));
+      }
   };
   auto mfma_q = [&](f32x4 (&c)[4][FQ], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[FQ][2]) {
     __builtin_amdgcn_s_setprio(1);
@@ -308,19 +360,26 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
 }
 
 bool gemm_big_ok(const GemmArgs& g) {
-  return g.a_kcontig && g.b_kcontig && g.pro_scale == nullptr && g.addend == nullptr &&
-         g.bst_x == nullptr && (g.K % 8) == 0 && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
+  if (g.pro_scale != nullptr || g.addend != nullptr || g.bst_x != nullptr) return false;
+  if (g.a_kcontig && g.b_kcontig) return (g.K % 8) == 0 && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
+  // both MN-contiguous: whole 16-byte column chunks
+  return !g.a_kcontig && !g.b_kcontig && (g.M % 8) == 0 && (g.N % 8) == 0 && (g.lda % 8) == 0 &&
+         (g.ldb % 8) == 0 && g.stats == nullptr;
 }
 
 void gemm_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st) {
   const int bn = g.tile == GEMM_B256 ? 256 : 128;
   const int tiles = ((g.M + BBM - 1) / BBM) * ((g.N + bn - 1) / bn);
   const dim3 grid(tiles, zs), block(BGT);
-#define LW_BIG(BNV)                                                                              \
-  if (zs > 1) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_PARTIAL>), grid, block, 0, st, k);         \
-  else if (g.stats) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STATS>), grid, block, 0, st, k);     \
-  else hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STORE>), grid, block, 0, st, k);
-  if (bn == 256) { LW_BIG(256) } else { LW_BIG(128) }
+#define LW_BIG(BNV, MNV)                                                                         \
+  if (zs > 1) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_PARTIAL, MNV>), grid, block, 0, st, k);    \
+  else if (g.stats) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STATS, MNV>), grid, block, 0, st, k); \
+  else hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STORE, MNV>), grid, block, 0, st, k);
+  if (g.a_kcontig) {
+    if (bn == 256) { LW_BIG(256, false) } else { LW_BIG(128, false) }
+  } else {
+    if (bn == 256) { LW_BIG(256, true) } else { LW_BIG(128, true) }
+  }
 #undef LW_BIG
 }
 

@@ -146,9 +146,11 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
         lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile), out_bf16,
                     tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits,
                     bx, bm, bss, bb)
-    # the big tiles take both operands K-contiguous, no prologue / addend / backward statistics
-    big = BIG if (a_kc and b_kc and pro is None and addend is None and bst is None
-                  and K % 8 == 0) else ()
+    # the big tiles: both operands K-contiguous (forward, transposed-weight dgrad) or both
+    # MN-contiguous (weight gradients); no prologue / addend / backward statistics
+    big = BIG if (pro is None and addend is None and bst is None and
+                  ((a_kc and b_kc and K % 8 == 0) or
+                   (not a_kc and not b_kc and M % 8 == 0 and N % 8 == 0 and not stats))) else ()
     cands = TILES + big + (() if bst is not None else
                            stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None,
                                         pro_on_a, addend is not None, split_k, accumulate))
@@ -247,6 +249,59 @@ def _finish_bn(g: torch.Tensor, b: torch.Tensor, dg, db, outs):
 
 def _finish_wgrad(p: torch.Tensor, dst: torch.Tensor, direct: bool):
     return _finish_param(p, None, True) if direct else dst.view_as(p)
+
+
+# Weight gradients on a side stream: dW of a layer is independent of the data-gradient chain
+# that follows it, so the block's three (four) weight-gradient GEMMs run beside the dgrad GEMMs
+# and the latency-bound BN backward kernels instead of between them (fork/join by stream waits;
+# inside a HIP-graph capture the fork and join become graph edges). LWAAAI_WGRAD_SIDE=0: inline.
+WGRAD_SIDE = os.environ.get("LWAAAI_WGRAD_SIDE", "0") == "1"
+_SIDE: Dict[int, torch.cuda.Stream] = {}
+
+
+class _WgradLane:
+    def __init__(self, device: torch.device):
+        self.on = WGRAD_SIDE and device.type == "cuda"
+        self.main = torch.cuda.current_stream(device) if self.on else None
+        if self.on:
+            idx = device.index if device.index is not None else torch.cuda.current_device()
+            if idx not in _SIDE:
+                _SIDE[idx] = torch.cuda.Stream(device=idx)
+            self.side = _SIDE[idx]
+        self.ready = []
+        self.used = False
+
+    def run(self, fn):
+        """Launch ``fn`` after everything the main stream has queued so far."""
+        if not self.on:
+            return fn()
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            out = fn()
+        self.used = True
+        return out
+
+    def finish(self, thunk) -> None:
+        """Grad-ready notifications wait for the join (the engine records its bucket events on
+        the main stream)."""
+        if self.on:
+            self.ready.append(thunk)
+        else:
+            thunk()
+
+    def join(self) -> None:
+        if self.on and self.used:
+            self.main.wait_stream(self.side)
+        for t in self.ready:
+            t()
+        self.ready = []
+
+
+def _wgrad_done(lane: _WgradLane, p: torch.Tensor, dst: torch.Tensor, direct: bool):
+    if direct:
+        lane.finish(lambda: _finish_param(p, None, True))
+        return None
+    return dst.view_as(p)
 
 
 def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
@@ -371,11 +426,13 @@ class _BottleneckFn(torch.autograd.Function):
         grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
         # conv3: weight gradient on a2 (or with BN2-apply recomputed in the B prologue), fp32
         # accumulated into the arena
+        lane = _WgradLane(dc3.device)
         dst3, d3 = _wgrad_target(w3, (cout, width))
-        gemm(dc3, cout, False, c2 if a2 is None else a2, width, False, cout, width, M2,
-             out_bf16=False, pro=(ss2[:width], ss2[width:]) if a2 is None else None,
-             pro_on_a=False, out=dst3, accumulate=True, split_k=True)
-        grads["w3"] = _finish_wgrad(w3, dst3, d3)
+        lane.run(lambda: gemm(dc3, cout, False, c2 if a2 is None else a2, width, False, cout,
+                              width, M2, out_bf16=False,
+                              pro=(ss2[:width], ss2[width:]) if a2 is None else None,
+                              pro_on_a=False, out=dst3, accumulate=True, split_k=True))
+        grads["w3"] = _wgrad_done(lane, w3, dst3, d3)
         # da2 = dc3·W3, its epilogue doing BN2's backward reduction (mask from c2 via ss2)
         da2, rows2 = gemm_dgrad(dc3, cout, W3, M2, width, cout, stats=BSTATS,
                                 bst=(c2, mean2, ss2, None) if BSTATS else None)
@@ -391,11 +448,18 @@ class _BottleneckFn(torch.autograd.Function):
         c1n = _nchw(c1 if a1 is None else a1, N, H, W)
         pro1 = (ss1[:width], ss1[width:]) if a1 is None else None
         if _direct(w2) and w2.grad.is_contiguous(memory_format=CL):
-            conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1, out=w2.grad)
-            grads["w2"] = _finish_param(w2, None, True)
+            lane.run(lambda: conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1,
+                                        out=w2.grad))
+            lane.finish(lambda: _finish_param(w2, None, True))
+            grads["w2"] = None
         else:
-            dW2 = conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1)
-            grads["w2"] = _finish_param(w2, dW2.contiguous(memory_format=CL), _direct(w2))
+            dW2 = lane.run(lambda: conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding,
+                                              pro=pro1).contiguous(memory_format=CL))
+            if _direct(w2):
+                lane.finish(lambda: _finish_param(w2, dW2, True))
+                grads["w2"] = None
+            else:
+                grads["w2"] = dW2.view_as(w2)
         # da1 = conv3x3ᵀ(dc2), its epilogue doing BN1's backward reduction
         if BSTATS:
             da1n, rows1 = conv_dgrad(dc2n, W2, (H, W), stride, padding, bst=(c1, mean1, ss1, None))
@@ -408,9 +472,9 @@ class _BottleneckFn(torch.autograd.Function):
         grads["g1"], grads["b1"] = _finish_bn(g1p, b1p, dg1, db1, o1)
         xr = _rows(x)
         dst1, d1 = _wgrad_target(w1, (width, Cin))
-        gemm(dc1, width, False, xr, Cin, False, width, Cin, M, out_bf16=False, out=dst1,
-             accumulate=True, split_k=True)
-        grads["w1"] = _finish_wgrad(w1, dst1, d1)
+        lane.run(lambda: gemm(dc1, width, False, xr, Cin, False, width, Cin, M, out_bf16=False,
+                              out=dst1, accumulate=True, split_k=True))
+        grads["w1"] = _wgrad_done(lane, w1, dst1, d1)
         if has_down:
             xsr, cd, Wd, gd, meand, invd = saved[21:]
             s = ctx.down_stride
@@ -420,12 +484,12 @@ class _BottleneckFn(torch.autograd.Function):
             grads["gd"], grads["bd"] = _finish_bn(gdp, bdp, dgd, dbd, od)
             dstd, dd = _wgrad_target(wd, (cout, Cin))
             if s == 1:
-                gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2, out_bf16=False, out=dstd,
-                     accumulate=True, split_k=True)
+                lane.run(lambda: gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2,
+                                      out_bf16=False, out=dstd, accumulate=True, split_k=True))
             else:                     # strided pixel gather of x in the weight-gradient conv
-                conv_wgrad(_nchw(dcd, N2, H2, W2_), x, (cout, Cin, 1, 1), s, 0,
-                           out=dstd.view(cout, Cin, 1, 1))
-            grads["wd"] = _finish_wgrad(wd, dstd, dd)
+                lane.run(lambda: conv_wgrad(_nchw(dcd, N2, H2, W2_), x, (cout, Cin, 1, 1), s, 0,
+                                            out=dstd.view(cout, Cin, 1, 1)))
+            grads["wd"] = _wgrad_done(lane, wd, dstd, dd)
             dx, _ = gemm_dgrad(dc1, width, W1, M, Cin, width)
             if s == 1:
                 gemm_dgrad(dcd, cout, Wd, M2, Cin, cout, out=dx, addend=dx)
@@ -443,6 +507,7 @@ class _BottleneckFn(torch.autograd.Function):
             if prev is not None:
                 _BWD_SLOT[0] = (dx.data_ptr(), rows_prev, prev[0].data_ptr())
         ctx.prev = None
+        lane.join()                   # the weight gradients are done before anything reads them
         dxn = _nchw(dx, N, H, W)
         return (dxn, grads["w1"], grads["g1"], grads["b1"], grads["w2"], grads["g2"], grads["b2"],
                 grads["w3"], grads["g3"], grads["b3"], grads.get("wd"), grads.get("gd"),

@@ -43,6 +43,48 @@ def timeit(fn, iters):
     return s.elapsed_time(e) / iters
 
 
+WGRAD = [("wg l1 c3", 256, 64, 802816), ("wg l2 c3", 512, 128, 200704),
+         ("wg l3 c3", 1024, 256, 50176), ("wg l4 c3", 2048, 512, 12544),
+         ("wg l2 c1", 128, 512, 200704), ("wg l3 c1", 256, 1024, 50176),
+         ("wg l4 c1", 512, 2048, 12544)]
+DIMS = {2: (128, 128), 21: (256, 256), 22: (256, 128)}
+
+
+def wgrad_rows():
+    """Weight-gradient layout (both operands MN-contiguous: dY [pix][Co], X [pix][C]), fp32
+    accumulated into the output as the engine does, each tile at the split counts around the
+    engine's heuristic (ops/block.py _splits)."""
+    for name, M, N, K in WGRAD:
+        fl = 2.0 * M * N * K
+        iters = max(3, min(50, int(2e13 / fl)))
+        dy = torch.randn(K, M, device="cuda").bfloat16()
+        x = torch.randn(K, N, device="cuda").bfloat16()
+        out = torch.zeros(M, N, device="cuda")
+        row = {"shape": name, "M": M, "N": N, "K": K}
+        ref = None
+        for t, (bm, bn) in DIMS.items():
+            tiles = -(-M // bm) * -(-N // bn)
+            s0 = max(1, min(512 // tiles, K // 256))
+            best = None
+            for sp in sorted({max(1, s0 // 2), s0, s0 * 2}):
+                ms = timeit(lambda: G.load().gemm_ex(dy, M, False, x, N, False, M, N, K, None,
+                                                     False, sp, False, t, None, None, True, False,
+                                                     out, None, True, 0, None), iters)
+                if best is None or ms < best[0]:
+                    best = (ms, sp)
+            row[f"t{t}_tflops"] = round(fl / best[0] / 1e9, 1)
+            row[f"t{t}_splits"] = best[1]
+            c, _ = G.gemm_ex(dy, M, False, x, N, False, M, N, K, splits=4, out_bf16=False, tile=t)
+            if ref is None:
+                ref = c
+            else:
+                row[f"t{t}_eq_t2"] = bool(torch.equal(c, ref))
+        row["blas_tflops"] = round(fl / timeit(lambda: torch.mm(dy.t(), x), iters) / 1e9, 1)
+        print(json.dumps(row), flush=True)
+        del dy, x, out, ref
+        torch.cuda.empty_cache()
+
+
 def main():
     only = os.environ.get("ONLY")
     torch.manual_seed(0)
@@ -92,4 +134,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if os.environ.get("WGRAD", "1") == "1":
+        wgrad_rows()
+    if os.environ.get("FWD", "1") == "1":
+        main()

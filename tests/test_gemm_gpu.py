@@ -251,36 +251,44 @@ def test_conv_dgrad_backward_bn_stats_epilogue(stride):
                                    (256, 1024, 2048), (64, 40, 8)])
 @pytest.mark.parametrize("splits", [1, 3])
 @pytest.mark.parametrize("tile", ["256x256x64", "256x128x64"])
-def test_gemm_big_tile(M, N, K, splits, tile):
-    """256x256x64 / 8-wave LDS-DMA kernel (csrc/gemm_big.hip, tile 21): fp32 and bf16 outputs,
-    bias + ReLU, ragged M/N/K edges, split-K, and fp32 accumulate into an existing C."""
+@pytest.mark.parametrize("kc", [True, False], ids=["kc", "mn"])
+def test_gemm_big_tile(M, N, K, splits, tile, kc):
+    """256x256 / 256x128 8-wave LDS-DMA kernel (csrc/gemm_big.hip, tiles 21/22), both operands
+    K-contiguous (x·Wᵀ) or both MN-contiguous (a weight gradient dYᵀ·X, transposing LDS reads):
+    fp32 and bf16 outputs, bias + ReLU, ragged M/N/K edges, split-K, fp32 accumulate."""
     lib = _lib()
     torch.manual_seed(7)
-    A = torch.randn(M, K, device="cuda").bfloat16()
-    B = torch.randn(N, K, device="cuda").bfloat16()
-    ref = A.float() @ B.float().t()
-    C, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, splits=splits, out_bf16=False,
-                     tile=tile)
+    Am = torch.randn(M, K, device="cuda").bfloat16()
+    Bm = torch.randn(N, K, device="cuda").bfloat16()
+    A = Am if kc else Am.t().contiguous()              # [M][K] or [K][M]
+    B = Bm if kc else Bm.t().contiguous()              # [N][K] or [K][N]
+    lda, ldb = (K, K) if kc else (M, N)
+    ref = Am.float() @ Bm.float().t()
+    C, _ = G.gemm_ex(A, lda, kc, B, ldb, kc, M, N, K, splits=splits, out_bf16=False, tile=tile)
     torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
     bias = torch.randn(N, device="cuda")
-    Y, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, bias=bias, relu=True, splits=splits,
+    Y, _ = G.gemm_ex(A, lda, kc, B, ldb, kc, M, N, K, bias=bias, relu=True, splits=splits,
                      tile=tile)
     torch.testing.assert_close(Y.float(), torch.relu(ref + bias), rtol=2e-2, atol=5e-2)
     base = torch.randn(M, N, device="cuda")
     out = base.clone()
-    lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, splits, False, G.TILES[tile], None,
+    lib.gemm_ex(A, lda, kc, B, ldb, kc, M, N, K, None, False, splits, False, G.TILES[tile], None,
                 None, True, False, out, None, True, 0, None)
     torch.testing.assert_close(out, base + ref, rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.parametrize("tile", ["256x256x64", "256x128x64"])
-def test_gemm_big_tile_bitwise_vs_128(tile):
+@pytest.mark.parametrize("kc", [True, False], ids=["kc", "mn"])
+def test_gemm_big_tile_bitwise_vs_128(tile, kc):
     """Same per-element k order as the 128x128x64 tile (k ascending in 32-wide MFMA steps):
     the outputs agree exactly."""
     torch.manual_seed(8)
     M, N, K = 768, 512, 640
-    A = torch.randn(M, K, device="cuda").bfloat16()
-    B = torch.randn(N, K, device="cuda").bfloat16()
-    c1, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, out_bf16=False, tile=tile)
-    c2, _ = G.gemm_ex(A, K, True, B, K, True, M, N, K, out_bf16=False, tile="128x128x64")
+    Am = torch.randn(M, K, device="cuda").bfloat16()
+    Bm = torch.randn(N, K, device="cuda").bfloat16()
+    A = Am if kc else Am.t().contiguous()
+    B = Bm if kc else Bm.t().contiguous()
+    lda, ldb = (K, K) if kc else (M, N)
+    c1, _ = G.gemm_ex(A, lda, kc, B, ldb, kc, M, N, K, out_bf16=False, tile=tile)
+    c2, _ = G.gemm_ex(A, lda, kc, B, ldb, kc, M, N, K, out_bf16=False, tile="128x128x64")
     torch.testing.assert_close(c1, c2, rtol=0, atol=0)

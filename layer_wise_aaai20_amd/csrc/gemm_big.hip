@@ -27,6 +27,11 @@
 //   P3: (registers)-> Q10   DMA (c+2).B1 -> buffer c&1       vmcnt: (c+1).A0,B0 landed
 // Epilogues: bf16 / fp32 store with bias + ReLU, or an fp32 split-K slab (reduced by
 // k_splitk_reduce in gemm.hip, fixed order).
+// GA: the A operand is the im2col row gather of a convolution (conv.hip CV_A, one parity class,
+// C % 64 == 0): a K-tile then lies inside one filter tap, so a lane's DMA source is its pixel's
+// window origin + the tap's (uniform) offset, and a tap falling into the padding becomes an OOB
+// offset (the DMA lands zeros) — the same big-tile schedule runs the 3x3 forward and stride-1
+// data-gradient convolutions with no im2col buffer.
 #include "common.h"
 #include "gemm_core.h"
 
@@ -70,8 +75,9 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :
 // (Tried: reading the next K-tile's B0 fragments in P3 after a wait moved to P2, so the LDS reads
 // spread 8/4/8/4 over the phases instead of 12/4/8/0: 251 VGPRs and 7 % slower at 8192^3,
 // profiles/r3/gemm_big_pf_ab.jsonl.)
-template <int BN, int EPI, bool MN>
+template <int BN, int EPI, bool MN, bool GA = false>
 __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
+  static_assert(!(GA && MN), "the row gather stages a K-contiguous A");
   constexpr int BHALF = (BN / 2) * BBK;        // bf16 elements per B half-tile
   constexpr int BUF = 2 * AHALF + 2 * BHALF;   // one K-tile: A0 A1 B0 B1
   constexpr int NB = BN / 128;                 // DMA instructions per B half (A: 2)
@@ -99,10 +105,34 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   uint32_t va[2][2], vb[2][NB];
   int ka[2], kb[NB];                   // k offset of the lane's chunk within a K-tile
   constexpr int WB = BN / 2;           // MN: columns of a B half image
+  // GA: the pixel's window origin (hb, wb; rows past M fail every bounds test) and the byte offset
+  // of its tap-(0, 0) chunk, per A half qa and instruction hh
+  int ghb[2][2], gwb[2][2], grow[2][2];
+  const int gC = p.cv.C, gHin = p.cv.Hin, gWin = p.cv.Win;
+  const float inv_c = 1.f / (float)gC, inv_ts = 1.f / (float)p.cv.cls[0].TS;
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     const int q = threadIdx.x + hh * BGT;           // chunk of the half-tile this lane lands in
-    if constexpr (!MN) {
+    if constexpr (GA) {
+      const int lr = q >> 3, cc = q & 7;
+      const int gc = cc ^ (lr & 7);
+      ka[hh] = gc * 8;
+      const ConvClass& k0c = p.cv.cls[0];
+      const int hw = k0c.Hg * k0c.Wg;
+#pragma unroll
+      for (int qa = 0; qa < 2; ++qa) {
+        const int row = m0 + (lr >> 6) * 128 + qa * 64 + (lr & 63);
+        const bool in = row < k0c.M;
+        const int mm = in ? row : 0;
+        const int b = mm / hw, rem = mm - b * hw;
+        const int y = rem / k0c.Wg, x = rem - y * k0c.Wg;
+        const int h0 = y * p.cv.sh + k0c.oh, w0 = x * p.cv.sw + k0c.ow;
+        ghb[qa][hh] = in ? h0 : -(1 << 28);
+        gwb[qa][hh] = w0;
+        grow[qa][hh] = (((b * gHin + h0) * gWin + w0) * gC + gc * 8) * 2;
+        va[qa][hh] = 0;
+      }
+    } else if constexpr (!MN) {
       const int lr = q >> 3, cc = q & 7;
       const int gc = cc ^ (lr & 7);                 // logical chunk fetched (swizzle at the source)
       ka[hh] = gc * 8;
@@ -150,8 +180,26 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   // are never read, so their chunks only need to stay inside the operands.
   auto dma = [&](int kt, int buf, int h) {
     if (h < 2) {
-      const uint32_t kofs = MN ? (uint32_t)(kt * BBK) * (uint32_t)p.lda * 2u : (uint32_t)(kt * BBK * 2);
       uint16_t* base = lds + buf * BUF + h * AHALF;
+      if constexpr (GA) {
+        // the K-tile's tap (jr, js) and first channel: uniform, exact float division (< 2^24)
+        const int kk = kbeg + kt * BBK;
+        int ci0;
+        const int t = fdivmod(kk, gC, inv_c, ci0);
+        int js;
+        const int jr = fdivmod(t, p.cv.cls[0].TS, inv_ts, js);
+        const int ho = p.cv.dh * jr, wo = p.cv.dw * js;
+        const int delta = ((ho * gWin + wo) * gC + ci0) * 2;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const bool ok = kt * BBK + ka[hh] < klen &&
+                          (unsigned)(ghb[h][hh] + ho) < (unsigned)gHin &&
+                          (unsigned)(gwb[h][hh] + wo) < (unsigned)gWin;
+          glds16(ra, base + (w * 64 + hh * BGT) * 8, ok ? (uint32_t)(grow[h][hh] + delta) : OOB);
+        }
+        return;
+      }
+      const uint32_t kofs = MN ? (uint32_t)(kt * BBK) * (uint32_t)p.lda * 2u : (uint32_t)(kt * BBK * 2);
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
         glds16(ra, base + (w * 64 + hh * BGT) * 8,
@@ -365,6 +413,26 @@ bool gemm_big_ok(const GemmArgs& g) {
   // both MN-contiguous: whole 16-byte column chunks
   return !g.a_kcontig && !g.b_kcontig && (g.M % 8) == 0 && (g.N % 8) == 0 && (g.lda % 8) == 0 &&
          (g.ldb % 8) == 0 && g.stats == nullptr;
+}
+
+// The big tiles for a row-gather convolution (conv.hip CV_A): one class with the identity row map,
+// whole 64-channel K-tiles, a K-contiguous weight operand, no prologue / addend / backward
+// statistics.
+bool conv_big_ok(const GemmArgs& g, const ConvGeomHost& h) {
+  return h.nclass == 1 && h.osy == 1 && h.osx == 1 && h.C % BBK == 0 && g.b_kcontig &&
+         (g.ldb % 8) == 0 && g.pro_scale == nullptr && g.addend == nullptr && g.bst_x == nullptr &&
+         g.N % 8 == 0;
+}
+
+void conv_big(const GemmArgs& g, const GemmK& k, hipStream_t st) {
+  const int bn = g.tile == GEMM_B256 ? 256 : 128;
+  const int tiles = ((g.M + BBM - 1) / BBM) * ((g.N + bn - 1) / bn);
+  const dim3 grid(tiles, 1), block(BGT);
+#define LW_CBIG(BNV)                                                                                \
+  if (g.stats) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STATS, false, true>), grid, block, 0, st, k); \
+  else hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STORE, false, true>), grid, block, 0, st, k);
+  if (bn == 256) { LW_CBIG(256) } else { LW_CBIG(128) }
+#undef LW_CBIG
 }
 
 void gemm_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st) {

@@ -252,6 +252,9 @@ struct ConvGeomHost {
 void conv_gemm(const GemmArgs& g, const ConvGeomHost& cv, int mode, hipStream_t st);
 int conv_splits_used(const GemmArgs& g);
 bool conv_tile_ok(int mode, int tile);
+// the 256x256 / 256x128 big tiles (GEMM_B256*) on a row-gather conv: one class, identity row
+// map, C % 64 == 0, K-contiguous weight, no prologue / addend / backward statistics
+bool conv_big_ok(const GemmArgs& g, const ConvGeomHost& h);
 
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],

@@ -35,6 +35,10 @@ CL = torch.channels_last
 CV_A, CV_A4, CV_B, CV_B4 = 1, 2, 3, 4
 ROW_TILES = (1, 2, 3, 5, 6)          # forward / dgrad (csrc GemmTile ids)
 COL_TILES = (1, 2, 4, 6)             # weight gradient
+# 256x256 / 256x128 8-wave LDS-DMA tiles (csrc/gemm_big.hip, row gather): one stride-1 class,
+# C % 64 == 0 (a K-tile inside one tap), K-contiguous weight, no prologue / addend / statistics
+# of the backward; LWAAAI_CONV_BIG=0 leaves them out of the tuner's candidates
+BIG_TILES = (21, 22) if os.environ.get("LWAAAI_CONV_BIG", "1") != "0" else ()
 _TILE_DIMS = {1: (128, 128, 32), 2: (128, 128, 64), 3: (256, 64, 32), 4: (64, 256, 32),
               5: (256, 64, 64), 6: (64, 64, 64)}
 
@@ -174,7 +178,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
                            True, K, bias=bf, relu=bool(relu))
     key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats,
            bias is not None, bool(relu))
-    tile = TUNER.pick(key, run, ROW_TILES, _row_default(M, co))
+    big = BIG_TILES if (not c4 and C % 64 == 0 and pro is None and co % 8 == 0) else ()
+    tile = TUNER.pick(key, run, ROW_TILES + big, _row_default(M, co))
     y, st = run(tile)
     return y.view(Nb, Ho, Wo, co).permute(0, 3, 1, 2), st
 
@@ -228,8 +233,10 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
            bst is not None)
     # the weight as [K][C] (the kernel's transposing LDS reads) or packed K-contiguous [C][K]
     # (LDS-DMA staging of both operands); backward statistics need the first
+    big = BIG_TILES if (len(classes) == 1 and sh == 1 and sw == 1 and co % 64 == 0 and
+                        c % 8 == 0 and addend is None and bst is None) else ()
     cands = [("nkc", t) for t in ROW_TILES] + \
-        ([("kc", t) for t in ROW_TILES] if bst is None else [])
+        ([("kc", t) for t in ROW_TILES + big] if bst is None else [])
     cand = TUNER.pick(key, run, cands, ("nkc", _row_default(M, c)))   # (timed on scratch outputs)
     dx, st = run(cand, out, addend)
     if bst is not None:

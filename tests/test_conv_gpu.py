@@ -244,3 +244,72 @@ def test_pack_dgrad_kc_matches_torch(shape):
         ref[i, :, :slab.shape[1]] = slab
     assert offs == [i * c * kmax for i in range(len(classes))]
     assert torch.equal(packed.view(len(classes), c, kmax), ref)
+
+
+BIG_SHAPES = [(4, 64, 64, 56, 3, 1, 1), (4, 128, 128, 56, 3, 2, 1), (4, 128, 128, 28, 3, 1, 1),
+              (4, 256, 256, 14, 3, 1, 1), (4, 512, 512, 7, 3, 1, 1), (3, 64, 136, 9, 3, 1, 0),
+              (2, 192, 64, 11, 5, 1, 2)]
+
+
+@pytest.mark.parametrize("shape", BIG_SHAPES, ids=[str(s) for s in BIG_SHAPES])
+def test_conv_big_tiles(shape, monkeypatch):
+    """The 256x256 / 256x128 8-wave LDS-DMA tiles with the im2col row gather (gemm_big.hip GA):
+    forward (+ column statistics, + bias/ReLU epilogue) and the stride-1 data gradient on the
+    K-contiguous weight pack, against fp32 torch and bit-identical to the 128x128x64 DMA tile
+    (same per-element MFMA accumulation order); row counts off the 256 grid, padding 0 / 1 / 2,
+    N below the tile width."""
+    N, C, Co, H, k, s, p = shape
+    x, w = _inputs(N, C, Co, H, k, 5)
+    ref = F.conv2d(x.float(), w.float(), stride=s, padding=p)
+    pick = CV.TUNER.pick
+    outs = {}
+    bias = torch.randn(Co, device="cuda")
+    for tile in (2, 21, 22):
+        monkeypatch.setattr(CV.TUNER, "pick", lambda key, run, cands, default: tile)
+        y, st = CV.conv_fwd(x, w, s, p, stats=True)
+        _close(y, ref, 1e-2)
+        yf = y.float().permute(0, 2, 3, 1).reshape(-1, Co)
+        tot = st.sum(0)
+        torch.testing.assert_close(tot[0], yf.sum(0), rtol=1e-3, atol=1e-2)
+        torch.testing.assert_close(tot[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+        yb, _ = CV.conv_fwd(x, w, s, p, bias=bias, relu=True)
+        _close(yb, torch.relu(ref + bias.view(1, -1, 1, 1)), 1e-2)
+        outs[tile] = (y, yb)
+    for tile in (21, 22):
+        assert torch.equal(outs[tile][0], outs[2][0]) and torch.equal(outs[tile][1], outs[2][1])
+    if s != 1:
+        return
+    # data gradient of conv(x2: Co -> C channels): the gathered tensor dy has C % 64 == 0 channels
+    x2, w2 = _inputs(N, Co, C, H, k, 6)
+    xf = x2.float().requires_grad_()
+    r2 = F.conv2d(xf, w2.float(), stride=1, padding=p)
+    dy = torch.randn_like(r2).bfloat16().contiguous(memory_format=CL)
+    r2.backward(dy.float())
+    dxs = {}
+    for tile in (2, 21, 22):
+        monkeypatch.setattr(CV.TUNER, "pick", lambda key, run, cands, default: ("kc", tile))
+        dxs[tile] = CV.conv_dgrad(dy, w2, (H, H), 1, p)
+        _close(dxs[tile], xf.grad, 1e-2)
+    assert torch.equal(dxs[21], dxs[2]) and torch.equal(dxs[22], dxs[2])
+    monkeypatch.setattr(CV.TUNER, "pick", pick)
+
+
+def test_conv_big_tiles_are_tuner_candidates(monkeypatch):
+    """The tuner is offered the big tiles exactly where the kernel supports them."""
+    seen = {}
+
+    def spy(key, run, cands, default):
+        seen[key[0]] = tuple(cands)
+        return default
+    monkeypatch.setattr(CV.TUNER, "pick", spy)
+    x, w = _inputs(2, 64, 128, 14, 3, 7)
+    CV.conv_fwd(x, w, 1, 1, stats=True)
+    assert 21 in seen["f"] and 22 in seen["f"]
+    CV.conv_fwd(x, w, 1, 1, pro=(torch.ones(64, device="cuda"), torch.zeros(64, device="cuda")))
+    assert 21 not in seen["f"]
+    dy = torch.randn(2, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=CL)
+    CV.conv_dgrad(dy, w, (14, 14), 1, 1)
+    assert ("kc", 21) in seen["d"] and ("nkc", 21) not in seen["d"]
+    dy2 = torch.randn(2, 128, 7, 7, device="cuda").bfloat16().contiguous(memory_format=CL)
+    CV.conv_dgrad(dy2, w, (14, 14), 2, 1)          # stride 2: parity classes, no big tiles
+    assert all(c[1] not in (21, 22) for c in seen["d"])

@@ -660,6 +660,77 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
   return {dx, dgamma, dbeta, dres};
 }
 
+// Two BN+ReLU backwards that share dy and the forward's ReLU bitmap — a bottleneck's BN3 and its
+// downsample BN, both feeding out = relu(bn3(c3) + bnd(cd)): one reduce pass and one apply pass
+// read dy and the bitmap once for both (bf16, training). Returns (dx, dx2, dgamma, dbeta,
+// dgamma2, dbeta2); the *_out tensors, when given, are accumulated into (arena views).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn_bwd_dual(
+    Tensor dy, Tensor x, Tensor x2, Tensor bits, c10::optional<Tensor> weight, Tensor mean,
+    Tensor invstd, c10::optional<Tensor> weight2, Tensor mean2, Tensor invstd2,
+    c10::optional<Tensor> dgamma_out, c10::optional<Tensor> dbeta_out,
+    c10::optional<Tensor> dgamma2_out, c10::optional<Tensor> dbeta2_out) {
+  const c10::DeviceGuard guard(x.device());
+  check_nhwc(x, "x");
+  check_nhwc(x2, "x2");
+  check_nhwc(dy, "dy");
+  check_dtype(x, at::kBFloat16, "x");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.sizes() == x.sizes() &&
+              x2.scalar_type() == x.scalar_type() && x2.sizes() == x.sizes(),
+              "dy, x and x2 must match");
+  TORCH_CHECK(bits.scalar_type() == at::kByte && bits.numel() * 8 == x.numel() &&
+              bits.is_contiguous(), "bits must be a contiguous uint8 [numel/8] bitmap");
+  const int64_t C = channels_of(x);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(mean.numel() == C && invstd.numel() == C && mean2.numel() == C &&
+              invstd2.numel() == C, "per-channel statistics must hold C floats");
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor dx = at::empty_like(x), dx2 = at::empty_like(x);
+  bool acc1 = false, acc1b = false, acc2 = false, acc2b = false;
+  Tensor dg = dparam_out(dgamma_out, C, x, acc1), db = dparam_out(dbeta_out, C, x, acc1b);
+  Tensor dg2 = dparam_out(dgamma2_out, C, x, acc2), db2 = dparam_out(dbeta2_out, C, x, acc2b);
+  TORCH_CHECK(acc1 == acc1b && acc2 == acc2b, "give both dgamma_out and dbeta_out of a BN");
+  const int64_t nb = lw::bn_reduce_blocks(M, (int)C);
+  Tensor partial = at::empty({2 * nb * 2 * C}, f32);
+  Tensor coef = at::empty({6 * C}, f32);
+  lw::BNArgs a{}, b{};
+  for (lw::BNArgs* p : {&a, &b}) {
+    p->M = M;
+    p->C = (int)C;
+    p->bf16 = true;
+    p->training = true;
+    p->relu = true;
+  }
+  a.x = x.data_ptr();
+  a.dy = dy.data_ptr();
+  a.bits = ptr<uint8_t>(bits);
+  a.dx = dx.data_ptr();
+  a.gamma = optr<float>(weight);
+  a.mean = ptr<float>(mean);
+  a.invstd = ptr<float>(invstd);
+  a.partial = ptr<float>(partial);
+  a.dgamma = ptr<float>(dg);
+  a.dbeta = ptr<float>(db);
+  a.accum_dparams = acc1;
+  a.A = ptr<float>(coef);
+  a.B = a.A + C;
+  a.Cc = a.A + 2 * C;
+  b.x = x2.data_ptr();
+  b.dx = dx2.data_ptr();
+  b.gamma = optr<float>(weight2);
+  b.mean = ptr<float>(mean2);
+  b.invstd = ptr<float>(invstd2);
+  b.partial = a.partial + nb * 2 * C;
+  b.dgamma = ptr<float>(dg2);
+  b.dbeta = ptr<float>(db2);
+  b.accum_dparams = acc2;
+  b.A = a.A + 3 * C;
+  b.B = a.A + 4 * C;
+  b.Cc = a.A + 5 * C;
+  lw::bn_backward_dual(a, b, cur_stream());
+  launched("bn_backward_dual");
+  return {dx, dx2, dg, db, dg2, db2};
+}
+
 // ---------------------------------------------------------------- MFMA GEMM
 // EPI_BSTATS operands (see lw_kernels.h GemmArgs): the BN input x laid out like the output rows
 // ([out_rows][N], ldc == N), its batch mean, and the ReLU mask source — the BN output's bitmap or
@@ -718,7 +789,7 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
   TORCH_CHECK(b_kcontig || N % 8 == 0, "N must be a multiple of 8 for an N-contiguous B");
   TORCH_CHECK(A.numel() >= (a_kcontig ? (M - 1) * lda + K : (K - 1) * lda + M), "A too small");
   TORCH_CHECK(B.numel() >= (b_kcontig ? (N - 1) * ldb + K : (K - 1) * ldb + N), "B too small");
-  TORCH_CHECK((tile >= 0 && tile <= 6) || (tile >= 11 && tile <= 13) || tile == 21 || tile == 22,
+  TORCH_CHECK((tile >= 0 && tile <= 6) || (tile >= 11 && tile <= 13) || (tile >= 21 && tile <= 24),
               "tile id");
   if (ldc <= 0) ldc = N;
   TORCH_CHECK(ldc >= N, "ldc must be >= N");
@@ -1043,8 +1114,7 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
   } else if (want_stats) {
     TORCH_CHECK(!g.bst_x, "backward statistics need want_stats");
     TORCH_CHECK(ga && b_kcontig && h.nclass == 1, "column statistics: forward convs only");
-    int bm, bn, bk;
-    lw::gemm_tile_shape(g.tile, bm, bn, bk);
+    const int bm = lw::stats_rows_bm(g.tile);
     stats = at::empty({(g.M + bm - 1) / bm, 2, N}, G.options().dtype(at::kFloat));
     g.stats = ptr<float>(stats);
   } else {
@@ -1354,6 +1424,11 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? stats_rows=None) "
       "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def(
+      "bn_bwd_dual(Tensor dy, Tensor x, Tensor x2, Tensor bits, Tensor? weight, Tensor mean, "
+      "Tensor invstd, Tensor? weight2, Tensor mean2, Tensor invstd2, "
+      "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor(c!)? dgamma2_out=None, "
+      "Tensor(d!)? dbeta2_out=None) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def(
       "gemm(Tensor A, int lda, bool a_kcontig, Tensor B, int ldb, bool b_kcontig, int M, int N, "
       "int K, Tensor? bias, bool relu, int splits, bool out_bf16) -> Tensor");
   m.def(
@@ -1405,6 +1480,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("gap_bwd", &gap_bwd);
   m.impl("bn_fwd", &bn_fwd);
   m.impl("bn_bwd", &bn_bwd);
+  m.impl("bn_bwd_dual", &bn_bwd_dual);
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);
   m.impl("conv_ex", &conv_ex);

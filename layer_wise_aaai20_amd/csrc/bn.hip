@@ -91,7 +91,10 @@ __device__ __forceinline__ void mask_bits(float d[8], uint32_t bits) {
   for (int k = 0; k < 8; ++k) d[k] = ((bits >> k) & 1u) ? d[k] : 0.f;
 }
 
-template <typename T, int MODE, int RELU, int U>
+// DUAL (MODE 1): a second BN whose input x2 received the same gradient dy and ReLU mask (the
+// downsample shortcut's BN next to BN3 in a bottleneck): Σdy' is shared, Σdy'·(x2−mean2) goes to
+// partial2 ([2][C][nb] like partial) — one pass over dy and the bitmap for both BNs.
+template <typename T, int MODE, int RELU, int U, bool DUAL = false>
 __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, const T* __restrict__ dy,
                                                    const T* __restrict__ y,
                                                    const uint8_t* __restrict__ bits,
@@ -99,9 +102,14 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
                                                    const float* __restrict__ fscale,
                                                    const float* __restrict__ fshift, int64_t M,
                                                    int C, int64_t rows_per_block,
-                                                   float* __restrict__ partial) {
+                                                   float* __restrict__ partial,
+                                                   const T* __restrict__ x2 = nullptr,
+                                                   const float* __restrict__ mean2 = nullptr,
+                                                   float* __restrict__ partial2 = nullptr) {
+  static_assert(!DUAL || MODE == 1, "dual reduce: backward only");
   __shared__ float sa[BNT * 8];
   __shared__ float sb[BNT * 8];
+  __shared__ float sb2[DUAL ? BNT * 8 : 1];
   // blockIdx.y selects a slice of Cb channels (reduce_geometry): a block reads Cb-wide row
   // segments, so it writes 2*Cb partial sums instead of 2*C scattered ones (at C = 2048 the
   // whole-row form spent most of its time on 4096 strided partial stores per block)
@@ -111,12 +119,18 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
   const int g = threadIdx.x % G, r = threadIdx.x / G;
   const int gc = c_off / 8 + g;             // this thread's channel group within the full row
   const bool active = r < R;
-  float a[8], b[8], mu[8], fs[8], fh[8];
+  float a[8], b[8], mu[8], fs[8], fh[8], b2[8], mu2[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { a[k] = 0.f; b[k] = 0.f; mu[k] = 0.f; fs[k] = 0.f; fh[k] = 0.f; }
+  for (int k = 0; k < 8; ++k) {
+    a[k] = 0.f; b[k] = 0.f; mu[k] = 0.f; fs[k] = 0.f; fh[k] = 0.f; b2[k] = 0.f; mu2[k] = 0.f;
+  }
   if (MODE == 1 && active) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) mu[k] = mean[gc * 8 + k];
+    if (DUAL) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mu2[k] = mean2[gc * 8 + k];
+    }
     if (RELU == 2) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) { fs[k] = fscale[gc * 8 + k]; fh[k] = fshift[gc * 8 + k]; }
@@ -130,8 +144,11 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
     const T* xp = x + gc * 8;
     const T* dp = dy + gc * 8;
     const T* yp = y + gc * 8;
+    const T* x2p = DUAL ? x2 + gc * 8 : nullptr;
     // Software-pipelined: the U rows of the next iteration are loaded (raw, predicated: rows past
     // r1 read as zero and add nothing) before the current U rows are converted and accumulated.
+    // (with DUAL, the y slots carry x2: a dual reduce always takes its mask from the bitmap)
+    static_assert(!DUAL || RELU == 3, "dual reduce: bitmap mask");
     Raw cx[U], cd[U], cy[U];
     uint32_t cb[U];
     auto fetch = [&](int64_t row0, Raw (&fx)[U], Raw (&fd)[U], Raw (&fy)[U], uint32_t (&fb)[U]) {
@@ -143,6 +160,7 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
         if (MODE == 1) {
           fd[u] = in ? V::ld(dp + rw * C) : V::zero();
           if (RELU == 1) fy[u] = in ? V::ld(yp + rw * C) : V::zero();
+          if (DUAL) fy[u] = in ? V::ld(x2p + rw * C) : V::zero();
           if (RELU == 3) fb[u] = in ? (uint32_t)bits[rw * GC + gc] : 0u;
         }
       }
@@ -177,6 +195,12 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
           }
 #pragma unroll
           for (int k = 0; k < 8; ++k) { a[k] += d[k]; b[k] += d[k] * (xv[k] - mu[k]); }
+          if (DUAL) {
+            float x2v[8];
+            V::cvt(cy[u], x2v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) b2[k] += d[k] * (x2v[k] - mu2[k]);
+          }
         }
       }
       if (more) {
@@ -188,15 +212,24 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
     for (int k = 0; k < 8; ++k) {
       sa[r * Cb + g * 8 + k] = a[k];
       sb[r * Cb + g * 8 + k] = b[k];
+      if (DUAL) sb2[r * Cb + g * 8 + k] = b2[k];
     }
   }
   __syncthreads();
   const int64_t nb = gridDim.x;
   for (int c = threadIdx.x; c < Cb; c += BNT) {
-    float s1 = 0.f, s2 = 0.f;
-    for (int q = 0; q < R; ++q) { s1 += sa[q * Cb + c]; s2 += sb[q * Cb + c]; }
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (int q = 0; q < R; ++q) {
+      s1 += sa[q * Cb + c];
+      s2 += sb[q * Cb + c];
+      if (DUAL) s3 += sb2[q * Cb + c];
+    }
     partial[(int64_t)(c_off + c) * nb + blockIdx.x] = s1;       // channel-major: [2][C][nb]
     partial[((int64_t)C + c_off + c) * nb + blockIdx.x] = s2;
+    if (DUAL) {
+      partial2[(int64_t)(c_off + c) * nb + blockIdx.x] = s1;
+      partial2[((int64_t)C + c_off + c) * nb + blockIdx.x] = s3;
+    }
   }
 }
 
@@ -426,6 +459,42 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, c
   }
 }
 
+// The two BN backwards of k_bn_reduce DUAL in one pass: dx = A*dy' + B*x + C and
+// dx2 = A2*dy' + B2*x2 + C2 with dy' = dy·bit (dy and the bitmap read once).
+__global__ __launch_bounds__(BNT) void k_bn_bwd_apply_dual(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ x2,
+    const uint16_t* __restrict__ dy, const uint8_t* __restrict__ bits,
+    const float* __restrict__ A, const float* __restrict__ B, const float* __restrict__ Cc,
+    const float* __restrict__ A2, const float* __restrict__ B2, const float* __restrict__ Cc2,
+    uint16_t* __restrict__ dx, uint16_t* __restrict__ dx2, int64_t n8, int C) {
+  const int G = C / 8;
+  const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
+  const int64_t step = (int64_t)gridDim.x * BNT;
+  const int c0 = (int)(t0 % G) * 8;
+  float ca[8], cb[8], cc[8], ca2[8], cb2[8], cc2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    ca[k] = A[c0 + k]; cb[k] = B[c0 + k]; cc[k] = Cc[c0 + k];
+    ca2[k] = A2[c0 + k]; cb2[k] = B2[c0 + k]; cc2[k] = Cc2[c0 + k];
+  }
+  for (int64_t i = t0; i < n8; i += step) {
+    const int64_t off = i * 8;
+    float xv[8], x2v[8], d[8];
+    V8<uint16_t>::load(x + off, xv);
+    V8<uint16_t>::load(x2 + off, x2v);
+    V8<uint16_t>::load(dy + off, d);
+    mask_bits(d, bits[i]);
+    float o[8], o2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      o[k] = ca[k] * d[k] + cb[k] * xv[k] + cc[k];
+      o2[k] = ca2[k] * d[k] + cb2[k] * x2v[k] + cc2[k];
+    }
+    V8<uint16_t>::store(dx + off, o);
+    V8<uint16_t>::store(dx2 + off, o2);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Tuning knobs (read once): rows unrolled per thread in the reduce loop, and the reduce grid size.
 static int env_int(const char* name, int dflt) {
@@ -519,7 +588,8 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(kern, dim3(nb, reduce_slices(a.C)), dim3(BNT), 0, st, static_cast<const T*>(a.x),
                        (const T*)nullptr, (const T*)nullptr, (const uint8_t*)nullptr,
                        (const float*)nullptr,
-                       (const float*)nullptr, (const float*)nullptr, a.M, a.C, rpb, a.partial);
+                       (const float*)nullptr, (const float*)nullptr, a.M, a.C, rpb, a.partial,
+                       (const T*)nullptr, (const float*)nullptr, (float*)nullptr);
   }
   hipLaunchKernelGGL(k_bn_finalize_fwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
                      a.C, a.M, a.gamma, a.beta, a.eps, a.momentum, a.rmean, a.rvar, a.mean,
@@ -558,7 +628,8 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
 #define LW_RED(R)                                                                                \
   hipLaunchKernelGGL((reduce_unroll() == 8 ? k_bn_reduce<T, 1, R, 8> : k_bn_reduce<T, 1, R, 4>), \
                      dim3(nb, reduce_slices(a.C)), dim3(BNT), 0, st, x, dy, y, a.bits, a.mean, \
-                     a.scale, a.shift, a.M, a.C, rpb, a.partial)
+                     a.scale, a.shift, a.M, a.C, rpb, a.partial, (const T*)nullptr,      \
+                     (const float*)nullptr, (float*)nullptr)
     if (rmode == 0) LW_RED(0); else if (rmode == 1) LW_RED(1); else if (rmode == 2) LW_RED(2);
     else LW_RED(3);
 #undef LW_RED
@@ -575,6 +646,31 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   else if (rmode == 2) { if (dres) LW_BWD(2, true); else LW_BWD(2, false); }
   else { if (dres) LW_BWD(0, true); else LW_BWD(0, false); }
 #undef LW_BWD
+}
+
+// Two BatchNorm+ReLU backwards sharing dy and the ReLU bitmap (bf16, training): a = the first BN
+// (x, mean, gamma, ... as in bn_backward), b = the second (its x, mean, invstd, gamma, partial,
+// dgamma/dbeta, coefficients and dx); b.dy / b.bits are ignored.
+void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st) {
+  int64_t rpb;
+  int nb;
+  reduce_geometry(a.M, a.C, rpb, nb);
+  const auto* x = static_cast<const uint16_t*>(a.x);
+  const auto* x2 = static_cast<const uint16_t*>(b.x);
+  const auto* dy = static_cast<const uint16_t*>(a.dy);
+  hipLaunchKernelGGL((reduce_unroll() == 8 ? k_bn_reduce<uint16_t, 1, 3, 8, true>
+                                            : k_bn_reduce<uint16_t, 1, 3, 4, true>),
+                     dim3(nb, reduce_slices(a.C)), dim3(BNT), 0, st, x, dy, (const uint16_t*)nullptr,
+                     a.bits, a.mean, (const float*)nullptr, (const float*)nullptr, a.M, a.C, rpb,
+                     a.partial, x2, b.mean, b.partial);
+  for (const BNArgs* p : {&a, &b})
+    hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((p->C + 3) / 4), dim3(256), 0, st, p->partial, nb,
+                       p->C, p->M, p->gamma, p->mean, p->invstd, p->dgamma, p->dbeta, p->A, p->B,
+                       p->Cc, 1, (int)p->accum_dparams);
+  const int64_t n8 = a.M * a.C / 8;
+  hipLaunchKernelGGL(k_bn_bwd_apply_dual, dim3(apply_grid(n8, a.C)), dim3(BNT), 0, st, x, x2, dy,
+                     a.bits, a.A, a.B, a.Cc, b.A, b.B, b.Cc, static_cast<uint16_t*>(a.dx),
+                     static_cast<uint16_t*>(b.dx), n8, a.C);
 }
 
 void bn_forward(const BNArgs& a, hipStream_t st) {

@@ -152,6 +152,8 @@ void bn_stats(const BNArgs& a, hipStream_t st);
 void bn_apply(const BNArgs& a, hipStream_t st);
 void bn_forward(const BNArgs& a, hipStream_t st);
 void bn_backward(const BNArgs& a, hipStream_t st);
+// two BN+ReLU backwards sharing dy and the ReLU bitmap (a bottleneck's BN3 and downsample BN)
+void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st);
 
 // fused stem: BN-apply + ReLU + max-pool (bn.hip), bf16 NHWC
 struct StemArgs {
@@ -221,7 +223,11 @@ enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_
                 GEMM_S64 = 11, GEMM_S128 = 12, GEMM_S256 = 13,
                 // 256x256x64 tile, 8 waves, LDS-DMA kept in flight across barriers (gemm_big.hip);
                 // K-contiguous A and B, no prologue / statistics / addend
-                GEMM_B256 = 21, GEMM_B256x128 = 22 };
+                GEMM_B256 = 21, GEMM_B256x128 = 22,
+                // the same tiles as a persistent kernel (one workgroup per CU walking tiles, the
+                // next tile's first K-tiles loaded during this tile's epilogue): K-contiguous A/B,
+                // bf16 output (+ statistics rows, + masked addend), K > 64
+                GEMM_P256 = 23, GEMM_P256x128 = 24 };
 void gemm_bf16(const GemmArgs& g, hipStream_t st);
 int gemm_pick_tile(const GemmArgs& g);
 int gemm_tiles_m(const GemmArgs& g);
@@ -231,8 +237,10 @@ void pack_dgrad_kc(const uint16_t* w, uint16_t* out, int Co, int C, int R, int S
                    int nclass, const int* r0, const int* s0, const int* TR, const int* TS,
                    int kmax, hipStream_t st);
 bool gemm_big_ok(const GemmArgs& g);
+bool gemm_bigp_ok(const GemmArgs& g);
 void splitk_reduce(const GemmArgs& g, int splits, hipStream_t st);   // fixed-order slab reduce
 void gemm_tile_shape(int tile, int& bm, int& bn, int& bk);
+int stats_rows_bm(int tile);      // rows of C per column-statistics row of a tile
 int gemm_k_per_split(int K, int splits, int bk);
 
 // implicit-GEMM convolution, NHWC bf16 (conv.hip). The GEMM view of each pass:

@@ -66,6 +66,10 @@ MAT_A2 = os.environ.get("LWAAAI_MAT_A2", "1") != "0"
 # those GEMMs' registers and serialise their memory phases (+2.4 ms): 9,770 vs 10,297 img/s
 # (profiles/r2_bstats_ab.log). LWAAAI_BSTATS=1 / LWAAAI_CROSS_BN3=1 turn the two parts on.
 BSTATS = os.environ.get("LWAAAI_BSTATS", "0") == "1"
+# The downsample block's BN3 and shortcut-BN backwards share dy and the ReLU bitmap: one dual
+# reduce + one dual apply pass (csrc bn.hip k_bn_reduce DUAL / k_bn_bwd_apply_dual) read them once
+# for both. LWAAAI_BN_DUAL=0: two separate BN backwards.
+BN_DUAL = os.environ.get("LWAAAI_BN_DUAL", "1") != "0"
 TILES = (1, 2, 3, 4, 5, 6)          # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
 BIG = (21, 22)                      # 256x256 / 256x128 8-wave LDS-DMA kernel (csrc/gemm_big.hip)
@@ -420,9 +424,18 @@ class _BottleneckFn(torch.autograd.Function):
         slot, _BWD_SLOT[0] = _BWD_SLOT[0], None
         if slot is not None and slot[0] == dr.data_ptr() and slot[2] == c3.data_ptr():
             rows3 = slot[1]             # reduced by the next block's dx GEMM epilogue
-        dc3, dg3, db3, _ = lib.bn_bwd(dr, c3, None, g3, mean3, inv3, None, True, True, False,
-                                      bits3, o3[0], o3[1], rows3)
         grads = {}
+        dual = None
+        if has_down and BN_DUAL and rows3 is None:
+            cd, gd, meand, invd = saved[22], saved[24], saved[25], saved[26]
+            od = _bn_grad_outs(gdp, bdp)
+            dc3, dcd, dg3, db3, dgd, dbd = lib.bn_bwd_dual(dr, c3, cd, bits3, g3, mean3, inv3, gd,
+                                                           meand, invd, o3[0], o3[1], od[0],
+                                                           od[1])
+            dual = (dcd, dgd, dbd, od)
+        else:
+            dc3, dg3, db3, _ = lib.bn_bwd(dr, c3, None, g3, mean3, inv3, None, True, True, False,
+                                          bits3, o3[0], o3[1], rows3)
         grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
         # conv3: weight gradient on a2 (or with BN2-apply recomputed in the B prologue), fp32
         # accumulated into the arena
@@ -478,9 +491,12 @@ class _BottleneckFn(torch.autograd.Function):
         if has_down:
             xsr, cd, Wd, gd, meand, invd = saved[21:]
             s = ctx.down_stride
-            od = _bn_grad_outs(gdp, bdp)
-            dcd, dgd, dbd, _ = lib.bn_bwd(dr, cd, None, gd, meand, invd, None, True, True,
-                                          False, bits3, od[0], od[1])
+            if dual is not None:
+                dcd, dgd, dbd, od = dual
+            else:
+                od = _bn_grad_outs(gdp, bdp)
+                dcd, dgd, dbd, _ = lib.bn_bwd(dr, cd, None, gd, meand, invd, None, True, True,
+                                              False, bits3, od[0], od[1])
             grads["gd"], grads["bd"] = _finish_bn(gdp, bdp, dgd, dbd, od)
             dstd, dd = _wgrad_target(wd, (cout, Cin))
             if s == 1:

@@ -160,3 +160,30 @@ def test_graph_fusion_folds_pools():
     fused = [n for n, m in net.named_modules() if isinstance(m, FusedBNReluPool2d)]
     assert sorted(fused) == ["layer1_bn", "layer2_bn", "layer3_bn"]
     assert isinstance(net.pool, torch.nn.MaxPool2d)
+
+
+@pytest.mark.parametrize("M,C", [(4096, 256), (3136, 512), (784, 2048), (1000, 64)])
+def test_bn_bwd_dual_matches_two_single_passes(M, C):
+    """bn_bwd_dual (BN3 + downsample BN sharing dy and the ReLU bitmap, one reduce and one apply
+    pass) is bit-identical to two bn_bwd calls, including accumulation into dgamma/dbeta views."""
+    from layer_wise_aaai20_amd.ops._ext import load
+    lib = load()
+    g = torch.Generator(device="cuda").manual_seed(M + C)
+    mk = lambda: torch.randn(M, C, device="cuda", generator=g).bfloat16()  # noqa: E731
+    dy, x, x2 = mk(), mk(), mk()
+    bits = torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device="cuda", generator=g)
+    stats = [(torch.rand(C, device="cuda", generator=g) + 0.5,
+              torch.randn(C, device="cuda", generator=g) * 0.1,
+              torch.rand(C, device="cuda", generator=g) + 0.5) for _ in range(2)]
+    (g1, m1, i1), (g2, m2, i2) = stats
+    outs = [torch.randn(C, device="cuda", generator=g) for _ in range(4)]
+    ref_outs = [o.clone() for o in outs]
+    dx_a, dg_a, db_a, _ = lib.bn_bwd(dy, x, None, g1, m1, i1, None, True, True, False, bits,
+                                     ref_outs[0], ref_outs[1])
+    dx_b, dg_b, db_b, _ = lib.bn_bwd(dy, x2, None, g2, m2, i2, None, True, True, False, bits,
+                                     ref_outs[2], ref_outs[3])
+    dx, dx2, dg, db, dg2, db2 = lib.bn_bwd_dual(dy, x, x2, bits, g1, m1, i1, g2, m2, i2, *outs)
+    assert torch.equal(dx, dx_a) and torch.equal(dx2, dx_b)
+    for a, b in zip((dg, db, dg2, db2), ref_outs):
+        assert torch.equal(a, b)
+    assert dg.data_ptr() == outs[0].data_ptr()          # accumulated in place

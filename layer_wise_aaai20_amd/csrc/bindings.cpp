@@ -7,6 +7,8 @@
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
+#include <map>
+#include <mutex>
 #include <torch/library.h>
 
 #include <algorithm>
@@ -1138,7 +1140,56 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
   return {C, stats};
 }
 
+// Direct stem convolution (conv.hip k_stem_conv7): x4 [N, 4, H, W] bf16 channels_last (the image
+// padded to 4 channels), w the packed [64][224] operand of pack_fwd_weight; returns
+// (y [N, 64, Ho, Wo] channels_last, stats [N*Ho/4, 2, 64]).
+std::tuple<Tensor, Tensor> stem_conv7(Tensor x, Tensor w) {
+  const c10::DeviceGuard guard(x.device());
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && x.size(1) == 4 &&
+              x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: [N, 4, H, W] channels_last");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == 64 * 224, "w: packed [64][224]");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t Ho = (H + 6 - 7) / 2 + 1, Wo = (W + 6 - 7) / 2 + 1;
+  TORCH_CHECK(lw::stem_conv7_ok(4, 64, 7, 7, 2, 2, 3, 3, (int)H, (int)W, (int)Ho, (int)Wo),
+              "stem_conv7: unsupported geometry");
+  TORCH_CHECK(N * H * W * 8 < (1LL << 31) && N * Ho * Wo * 128 < (1LL << 40), "stem_conv7 size");
+  check_aligned16(x.data_ptr(), "x");
+  check_aligned16(w.data_ptr(), "w");
+  Tensor y = at::empty({N, 64, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor st = at::empty({N * Ho / 4, 2, 64}, x.options().dtype(at::kFloat));
+  lw::stem_conv7(ptr<uint16_t>(x), ptr<uint16_t>(w), ptr<uint16_t>(y), ptr<float>(st), (int)N,
+                 (int)H, (int)W, (int)Ho, (int)Wo, cur_stream());
+  launched("stem_conv7");
+  return {y, st};
+}
+
 // ---------------------------------------------------------------- BN pieces for fused blocks
+// Arrival tickets of the one-launch colsum + finalize (bn.hip k_colsum_finalize), one per 64-channel
+// slice: zeroed once per device (eagerly: never created inside a graph capture) and re-armed by the
+// kernel's last block. LWAAAI_COLSUM_FUSED=1 turns it on (default: the two-kernel path).
+static unsigned* colsum_tickets(const Tensor& like) {
+  static const bool on = [] {
+    const char* v = getenv("LWAAAI_COLSUM_FUSED");
+    return v && v[0] == '1';
+  }();
+  if (!on) return nullptr;
+  static std::mutex mu;
+  static std::map<int, Tensor> per_dev;
+  std::lock_guard<std::mutex> lock(mu);
+  const int dev = like.device().index();
+  auto it = per_dev.find(dev);
+  if (it == per_dev.end()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(cur_stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
+      return nullptr;
+    Tensor t = at::zeros({kMaxBnC / 64 + 1}, like.options().dtype(at::kInt));
+    it = per_dev.emplace(dev, t).first;
+  }
+  return reinterpret_cast<unsigned*>(it->second.data_ptr());
+}
+
 // Batch statistics of x ([M, C] / channels_last), or — with `stats` [2, C, nb] from a GEMM's
 // column-statistics epilogue — only the finalize. Returns (mean, invstd, scale_shift[2C]).
 std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stats,
@@ -1177,7 +1228,9 @@ std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stat
     TORCH_CHECK(stats->dim() == 3 && stats->size(1) == 2 && stats->size(2) == C &&
                 stats->is_contiguous(), "stats must be a contiguous [rows, 2, C] tensor");
     const int64_t R = stats->size(0);
-    partial = at::empty({(int64_t)lw::colsum_blocks(R) * 2 * C}, f32);
+    a.tickets = colsum_tickets(x);
+    partial = at::empty({(int64_t)(a.tickets ? lw::colsum_fused_blocks(R) : lw::colsum_blocks(R)) *
+                         2 * C}, f32);
     a.partial = ptr<float>(partial);
     a.stat_rows = ptr<float>(*stats);
     a.stats_rows_n = R;
@@ -1423,6 +1476,7 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor? scale_shift, bool training, bool relu, bool need_dres, Tensor? bits=None, "
       "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? stats_rows=None) "
       "-> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("stem_conv7(Tensor x, Tensor w) -> (Tensor, Tensor)");
   m.def(
       "bn_bwd_dual(Tensor dy, Tensor x, Tensor x2, Tensor bits, Tensor? weight, Tensor mean, "
       "Tensor invstd, Tensor? weight2, Tensor mean2, Tensor invstd2, "
@@ -1481,6 +1535,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("bn_fwd", &bn_fwd);
   m.impl("bn_bwd", &bn_bwd);
   m.impl("bn_bwd_dual", &bn_bwd_dual);
+  m.impl("stem_conv7", &stem_conv7);
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);
   m.impl("conv_ex", &conv_ex);

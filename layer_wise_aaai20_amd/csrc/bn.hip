@@ -235,11 +235,17 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
 
 // Fold the block partials: one wave per channel, lanes stride over blocks (coalesced, fixed
 // order), then a fixed butterfly in fp64. Lane 0 of each wave gets the sums.
+__device__ __forceinline__ bool fold_channel(const float* __restrict__ partial, int nblocks, int C,
+                                             int c, double& s1, double& s2);
 __device__ __forceinline__ bool fold_partials(const float* __restrict__ partial, int nblocks, int C,
                                               double& s1, double& s2, int& c) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  c = blockIdx.x * 4 + w;
+  c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return false;
+  return fold_channel(partial, nblocks, C, c, s1, s2);
+}
+__device__ __forceinline__ bool fold_channel(const float* __restrict__ partial, int nblocks, int C,
+                                             int c, double& s1, double& s2) {
+  const int lane = threadIdx.x & 63;
   const float* p1 = partial + (int64_t)c * nblocks;
   const float* p2 = partial + ((int64_t)C + c) * nblocks;
   float a = 0.f, b = 0.f;
@@ -265,6 +271,91 @@ __device__ __forceinline__ bool fold_partials(const float* __restrict__ partial,
   s1 = da;
   s2 = db;
   return lane == 0;
+}
+
+// mean / invstd / scale / shift (+ running statistics) of channel c from its folded sums
+__device__ __forceinline__ void finalize_fwd_channel(int c, double s, double q, int64_t M,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     float momentum, float* __restrict__ rmean,
+                                                     float* __restrict__ rvar,
+                                                     float* __restrict__ mean_out,
+                                                     float* __restrict__ invstd_out,
+                                                     float* __restrict__ scale,
+                                                     float* __restrict__ shift) {
+  const double mean = s / (double)M;
+  double var = q / (double)M - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  scale[c] = gm * invstd;
+  shift[c] = bt - (float)mean * gm * invstd;
+  if (rmean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * unbiased);
+  }
+}
+
+// Column statistics rows of a GEMM / conv epilogue [R][2C] -> the BatchNorm finalize, in ONE
+// launch: block (x, y) sums rows [x*rpb, (x+1)*rpb) of the 2*64 columns of channel slice y
+// (Σv and Σv² of 64 channels) into partial [2C][nb]; the last block of a slice to arrive (an
+// agent-scope release / relaxed ticket / acquire, cdna_hip_programming.md §6 Guideline 16 — no
+// block ever waits) folds the slice's nb partials in the fixed fp64 order of k_bn_finalize_fwd and
+// writes mean / invstd / scale / shift / running statistics, then re-arms the slice's ticket.
+constexpr int CSF_SLICE = 64;
+__global__ __launch_bounds__(256) void k_colsum_finalize(
+    const float* __restrict__ rows, int64_t R, int C, int64_t rows_per_block,
+    float* __restrict__ partial, unsigned* __restrict__ tickets, int64_t M,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
+    float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ mean_out,
+    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
+  __shared__ unsigned sh_last[1];
+  const int nb = gridDim.x;
+  const int c0 = blockIdx.y * CSF_SLICE;
+  const int cs = min(CSF_SLICE, C - c0);
+  const int W = 2 * C;
+  if ((int)threadIdx.x < 2 * cs) {
+    const int col = (int)threadIdx.x < cs ? c0 + (int)threadIdx.x : C + c0 + (int)threadIdx.x - cs;
+    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t r1 = min(r0 + rows_per_block, R);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t r = r0;
+    for (; r + 3 < r1; r += 4) {
+      s0 += rows[r * W + col];
+      s1 += rows[(r + 1) * W + col];
+      s2 += rows[(r + 2) * W + col];
+      s3 += rows[(r + 3) * W + col];
+    }
+    for (; r < r1; ++r) s0 += rows[r * W + col];
+    partial[(int64_t)col * nb + blockIdx.x] = (s0 + s1) + (s2 + s3);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(tickets + blockIdx.y, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    sh_last[0] = prev == (unsigned)(nb - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (sh_last[0] == 0u) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int c = c0 + (int)(threadIdx.x >> 6); c < c0 + cs; c += 4) {
+    double sm, sq;
+    if (fold_channel(partial, nb, C, c, sm, sq))
+      finalize_fwd_channel(c, sm, sq, M, gamma, beta, eps, momentum, rmean, rvar, mean_out,
+                           invstd_out, scale, shift);
+  }
+  if (threadIdx.x == 0)
+    __hip_atomic_store(tickets + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(256) void k_bn_finalize_fwd(
@@ -526,6 +617,13 @@ static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblo
 
 // GEMM statistics rows folded per block: a few rows each, so every block's loads are in flight at
 // once (the finalize then folds up to 1024 partials per channel with unrolled loads)
+// row blocks of the fused colsum + finalize: few enough that the last block's fold of a slice
+// (64 channels x 2 x nb partials) stays short
+int colsum_fused_blocks(int64_t rows) {
+  static const int cap = env_int("LWAAAI_COLSUM_FUSED_BLOCKS", 64);
+  return (int)(rows < cap ? rows : cap);
+}
+
 int colsum_blocks(int64_t rows) {
   static const int cap = env_int("LWAAAI_COLSUM_BLOCKS", 1024);
   return (int)(rows < cap ? rows : cap);
@@ -574,6 +672,17 @@ static void bn_apply_t(const BNArgs& a, hipStream_t st) {
 template <typename T>
 static void bn_stats_t(const BNArgs& a, hipStream_t st) {
   int nb = a.stats_blocks;
+  if (a.stat_rows && a.tickets) {         // rows -> statistics in one launch (k_colsum_finalize)
+    const int64_t R = a.stats_rows_n;
+    int nbf = colsum_fused_blocks(R);
+    const int64_t rpb = (R + nbf - 1) / nbf;
+    nbf = (int)((R + rpb - 1) / rpb);
+    const int slices = (a.C + CSF_SLICE - 1) / CSF_SLICE;
+    hipLaunchKernelGGL(k_colsum_finalize, dim3(nbf, slices), dim3(256), 0, st, a.stat_rows, R,
+                       a.C, rpb, a.partial, a.tickets, a.M, a.gamma, a.beta, a.eps, a.momentum,
+                       a.rmean, a.rvar, a.mean, a.invstd, a.scale, a.shift);
+    return;
+  }
   if (a.stat_rows) {                      // GEMM epilogue rows [R][2C] -> [2C][nb]
     const int64_t R = a.stats_rows_n;
     nb = colsum_blocks(R);

@@ -31,6 +31,7 @@
 namespace lw {
 
 void gemm_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st);   // gemm_big.hip
+void gemm_bigp(const GemmArgs& g, const GemmK& k, hipStream_t st);
 
 // Fixed-order reduction of split-K slabs + epilogue. A workgroup owns OT float4 groups of outputs
 // and ZT split lanes (ZT*OT = 256): lane z sums splits z, z+ZT, ... in order, then the ZT lane sums
@@ -329,6 +330,9 @@ static void gemm_stream(const GemmArgs& g, hipStream_t st) {
 
 // ------------------------------------------------------------------------------------------ host
 struct TileShape { int bm, bn, bk; };
+static bool is_big_tile(int t) {
+  return t == GEMM_B256 || t == GEMM_B256x128 || t == GEMM_P256 || t == GEMM_P256x128;
+}
 static TileShape tile_shape(int t) {
   switch (t) {
     case GEMM_T128x128x64: return {128, 128, 64};
@@ -338,12 +342,22 @@ static TileShape tile_shape(int t) {
     case GEMM_T64x64x64: return {64, 64, 64};
     case GEMM_B256: return {256, 256, 64};
     case GEMM_B256x128: return {256, 128, 64};
+    case GEMM_P256: return {256, 256, 64};
+    case GEMM_P256x128: return {256, 128, 64};
     default: return {128, 128, 32};
   }
 }
 
+// rows of C per column-statistics row: the tile height, but 128 for the big tiles (one row per
+// wave row, gemm_big.hip)
+int stats_rows_bm(int tile) {
+  if (is_big_tile(tile)) return 128;
+  return tile_shape(tile).bm;
+}
+
 int gemm_pick_tile(const GemmArgs& g) {
   if ((g.tile == GEMM_B256 || g.tile == GEMM_B256x128) && !gemm_big_ok(g)) return GEMM_T128x128x64;
+  if ((g.tile == GEMM_P256 || g.tile == GEMM_P256x128) && !gemm_bigp_ok(g)) return GEMM_T128x128x64;
   if (g.tile > 0) return g.tile;
   if (g.M <= 64 && g.N <= 64) return GEMM_T64x64x64;
   if (g.N <= 64 && g.M >= 512) return GEMM_T256x64x32;
@@ -353,7 +367,9 @@ int gemm_pick_tile(const GemmArgs& g) {
 
 int gemm_tiles_m(const GemmArgs& g) {
   if (is_stream_tile(g.tile)) return gemm_stream_grid_m(g);   // one statistics row per workgroup
-  return (g.M + tile_shape(gemm_pick_tile(g)).bm - 1) / tile_shape(gemm_pick_tile(g)).bm;
+  const int t = gemm_pick_tile(g);
+  const int bm = stats_rows_bm(t);
+  return (g.M + bm - 1) / bm;
 }
 
 static int k_per_split(int K, int splits, int bk) {
@@ -364,6 +380,8 @@ static int k_per_split(int K, int splits, int bk) {
 
 int gemm_splits_used(const GemmArgs& g) {
   if (is_stream_tile(g.tile)) return 1;
+  const int pt = gemm_pick_tile(g);
+  if (pt == GEMM_P256 || pt == GEMM_P256x128) return 1;
   const int bk = tile_shape(gemm_pick_tile(g)).bk;
   const int kps = k_per_split(g.K, g.splits, bk);
   return (g.K + kps - 1) / kps;
@@ -430,7 +448,8 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
   }
   const int t = gemm_pick_tile(g);
   const TileShape ts = tile_shape(t);
-  const int kps = k_per_split(g.K, g.splits, ts.bk);
+  const bool persist = t == GEMM_P256 || t == GEMM_P256x128;     // never split
+  const int kps = persist ? g.K : k_per_split(g.K, g.splits, ts.bk);
   const int zs = (g.K + kps - 1) / kps;
   const int tiles = ((g.M + ts.bm - 1) / ts.bm) * ((g.N + ts.bn - 1) / ts.bn);
   const int epi = zs > 1 ? EPI_PARTIAL
@@ -446,6 +465,10 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
   k.bst_shift = g.bst_shift;
   k.bst_bits = g.bst_bits;
   const dim3 grid(tiles, zs);
+  if (persist) {
+    gemm_bigp(g, k, st);
+    return;
+  }
   if (t == GEMM_B256 || t == GEMM_B256x128) {
     gemm_big(g, k, zs, st);
     if (zs > 1) splitk_reduce(g, zs, st);

@@ -304,16 +304,14 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   // took up front, so both rows have passed the same number when they leave
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wm == 0) bar();
-  // the statistics fold reuses the LDS: wait until row 1 has drained its DMAs as well
-  if constexpr (EPI == EPI_STATS) bar();
 
   // ---- epilogue, straight from the accumulators. B was the MFMA's first operand, so lane l holds
   // C[m = .. + (l & 15)][n = .. + 4 * (l >> 4) + r], r = 0..3.
   const bool vec4 = (EPI == EPI_PARTIAL ? (p.N & 3) == 0 : (p.ldc & 3) == 0);
   float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)blockIdx.y * p.M * p.N : nullptr;
-  // EPI_STATS: Σv / Σv² of the stored (bf16-rounded) outputs per column over the tile's rows,
-  // folded across the 16 row-lanes by a fixed butterfly and across the two wave rows in LDS
-  float* red = reinterpret_cast<float*>(lds);                     // [2 wave rows][2][BN]
+  // EPI_STATS: Σv / Σv² of the stored (bf16-rounded) outputs per column over a wave row's 128
+  // rows, folded across the 16 row-lanes in DPP rows; one statistics row per wave row (128 rows of
+  // C: gemm_stats_rows), written straight from the registers — no LDS, no barrier
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
@@ -380,35 +378,276 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
         }
       if (EPI == EPI_STATS) {
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s1[r] += __shfl_xor(s1[r], o, 64);
-            s2[r] += __shfl_xor(s2[r], o, 64);
-          }
+        for (int r = 0; r < 4; ++r) {      // the 16 row-lanes: one DPP row (gemm_core.h sum16)
+          s1[r] = sum16(s1[r]);
+          s2[r] = sum16(s2[r]);
         }
-        if ((l & 15) == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            red[(wm * 2 + 0) * BN + nl + r] = s1[r];
-            red[(wm * 2 + 1) * BN + nl + r] = s2[r];
-          }
+        const int srow = tm * 2 + wm;
+        if ((l & 15) == 0 && srow * 128 < p.M && n < p.N) {
+          float* d = p.stats + (int64_t)srow * 2 * p.N + n;
+          *reinterpret_cast<float4*>(d) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+          *reinterpret_cast<float4*>(d + p.N) = make_float4(s2[0], s2[1], s2[2], s2[3]);
         }
       }
     }
-  if constexpr (EPI == EPI_STATS) {
-    __syncthreads();
-    for (int c = threadIdx.x; c < BN; c += BGT) {
-      const int n = n0 + c;
-      if (n >= p.N) continue;
-      p.stats[(int64_t)tm * 2 * p.N + n] = red[0 * BN + c] + red[2 * BN + c];
-      p.stats[(int64_t)tm * 2 * p.N + p.N + n] = red[1 * BN + c] + red[3 * BN + c];
-    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Persistent form (GEMM_P256 / GEMM_P256x128) for K-contiguous A and B with a bf16 output: one
+// workgroup per CU walks tiles blockIdx.x, +gridDim.x, ... and the K-tile schedule above runs on
+// over the tile boundary: the last two K-tiles of tile j issue the DMAs of K-tiles 0 and 1 of tile
+// j+1, so tile j's epilogue (stores straight from the accumulators, the statistics rows, the
+// masked addend) overlaps the next tile's loads instead of every tile paying a cold pipeline fill
+// and a workgroup launch. This is what the short-K, wide-N 1x1 convolutions of a ResNet need
+// (K = 64..512 is 1-8 K-tiles: the fill and the epilogue were most of a tile's time).
+// The epilogue ends with s_waitcnt vmcnt(0) (its stores and loads are then older than every later
+// counted wait), so the counted waits of the next tile stay exact. The statistics rows are one per
+// wave row, as in k_gemm_big. ADD: C = round(acc) + addend·[bit] (the residual gradient of a
+// bottleneck's dx, gemm_core.h masked_addend), ldc == N.
+template <int BN, bool STATS, bool ADD>
+__global__ __launch_bounds__(BGT) void k_gemm_bigp(const GemmK p) {
+  constexpr int BHALF = (BN / 2) * BBK;
+  constexpr int BUF = 2 * AHALF + 2 * BHALF;
+  constexpr int NB = BN / 128;
+  constexpr int QN = BN / 8;
+  constexpr int FQ = QN / 16;
+  constexpr int VM_P01 = 3 * 2 + 2 * NB, VM_P3 = 2 * 2 + 3 * NB;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BBM - 1) / BBM;
+  const int total = tiles_m * tiles_n;
+  const int T = (p.K + BBK - 1) / BBK;             // >= 2 (host)
+  const int klen = p.K;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
+  const int wm = w >> 2, wn = w & 3;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A, p.a_bytes), rb = make_rsrc(p.B, p.b_bytes);
+  int ka[2], kb[NB];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int q = threadIdx.x + hh * BGT;
+    ka[hh] = ((q & 7) ^ ((q >> 3) & 7)) * 8;
   }
+#pragma unroll
+  for (int hb = 0; hb < NB; ++hb) {
+    const int q = threadIdx.x + hb * BGT;
+    kb[hb] = ((q & 7) ^ ((q >> 3) & 7)) * 8;
+  }
+  // DMA sources of a tile (see k_gemm_big): [0] the tile being computed, [1] the next one
+  auto setup = [&](int t, uint32_t (&va)[2][2], uint32_t (&vb)[2][NB], int& m0, int& n0) {
+    int tm, tn;
+    tile_of(xcd_remap(t, total), tiles_m, tiles_n, tm, tn);
+    m0 = tm * BBM;
+    n0 = tn * BN;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int q = threadIdx.x + hh * BGT, lr = q >> 3;
+#pragma unroll
+      for (int qa = 0; qa < 2; ++qa) {
+        const int row = m0 + (lr >> 6) * 128 + qa * 64 + (lr & 63);
+        va[qa][hh] = row < p.M ? (uint32_t)(((int64_t)row * p.lda + ka[hh]) * 2) : OOB;
+      }
+    }
+#pragma unroll
+    for (int hb = 0; hb < NB; ++hb) {
+      const int q = threadIdx.x + hb * BGT, lr = q >> 3;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const int col = n0 + (lr / QN) * (BN / 4) + qb * QN + (lr % QN);
+        vb[qb][hb] = col < p.N ? (uint32_t)(((int64_t)col * p.ldb + kb[hb]) * 2) : OOB;
+      }
+    }
+  };
+  int t = blockIdx.x;
+  uint32_t va[2][2], vb[2][NB], van[2][2], vbn[2][NB];
+  int m0, n0, m0n = 0, n0n = 0;
+  setup(t, va, vb, m0, n0);
+  bool has_next = t + (int)gridDim.x < total;
+  if (has_next) setup(t + gridDim.x, van, vbn, m0n, n0n);
+  // K-tile kt of the current tile (kt >= T: K-tile kt - T of the next tile, or a zero-filling
+  // OOB DMA past the last tile: the same number of DMA instructions in every phase)
+  auto dma = [&](int kt, int buf, int h) {
+    const bool nx = kt >= T;
+    const int k = nx ? kt - T : kt;
+    const bool live = !nx || has_next;
+    if (h < 2) {
+      uint16_t* base = lds + buf * BUF + h * AHALF;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const uint32_t v = nx ? van[h][hh] : va[h][hh];
+        const bool ok = live && v != OOB && k * BBK + ka[hh] < klen;
+        glds16(ra, base + (w * 64 + hh * BGT) * 8, ok ? v + (uint32_t)(k * BBK * 2) : OOB);
+      }
+    } else {
+      uint16_t* base = lds + buf * BUF + 2 * AHALF + (h - 2) * BHALF;
+#pragma unroll
+      for (int hb = 0; hb < NB; ++hb) {
+        const uint32_t v = nx ? vbn[h - 2][hb] : vb[h - 2][hb];
+        const bool ok = live && v != OOB && k * BBK + kb[hb] < klen;
+        glds16(rb, base + (w * 64 + hb * BGT) * 8, ok ? v + (uint32_t)(k * BBK * 2) : OOB);
+      }
+    }
+  };
+  f32x4 acc[2][2][4][FQ];
+  bf16x8 fa0[4][2], fa1[4][2], fb0[FQ][2], fb1[FQ][2];
+  auto read_a = [&](bf16x8 (&f)[4][2], const uint16_t* h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        f[i][s] = *reinterpret_cast<const bf16x8*>(h + big_off(wm * 64 + i * 16 + (l & 15), 4 * s + (l >> 4)));
+  };
+  auto read_b = [&](bf16x8 (&f)[FQ][2], const uint16_t* h) {
+#pragma unroll
+    for (int j = 0; j < FQ; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        f[j][s] = *reinterpret_cast<const bf16x8*>(h + big_off(wn * QN + j * 16 + (l & 15), 4 * s + (l >> 4)));
+  };
+  auto mfma_q = [&](f32x4 (&c)[4][FQ], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[FQ][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FQ; ++j)
+          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], c[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  auto bar = [] { __builtin_amdgcn_s_barrier(); };
+
+  dma(0, 0, 0); dma(0, 0, 2); dma(0, 0, 3); dma(0, 0, 1);
+  dma(1, 1, 0); dma(1, 1, 2); dma(1, 1, 3);
+  vm_wait<VM_P3>();
+  if (wm == 1) bar();
+  bar();
+  int gb = 0;                          // buffer parity of this tile's K-tile 0
+  for (;;) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < FQ; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < T; ++c) {
+      const int b = (gb + c) & 1, nb = b ^ 1;
+      const uint16_t* H = lds + b * BUF;
+      read_a(fa0, H);
+      read_b(fb0, H + 2 * AHALF);
+      dma(c + 1, nb, 1);
+      vm_wait<VM_P01>();
+      lgkm0();
+      bar();
+      mfma_q(acc[0][0], fa0, fb0);
+      bar();
+      read_b(fb1, H + 2 * AHALF + BHALF);
+      dma(c + 2, b, 0);
+      vm_wait<VM_P01>();
+      lgkm0();
+      bar();
+      mfma_q(acc[0][1], fa0, fb1);
+      bar();
+      read_a(fa1, H + AHALF);
+      dma(c + 2, b, 2);
+      lgkm0();
+      bar();
+      mfma_q(acc[1][1], fa1, fb1);
+      bar();
+      dma(c + 2, b, 3);
+      vm_wait<VM_P3>();
+      bar();
+      mfma_q(acc[1][0], fa1, fb0);
+      bar();
+    }
+    // ---- epilogue of this tile (the next tile's K-tiles 0 and 1 are in flight)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int j = 0; j < FQ; ++j) {
+        const int n = n0 + wn * (BN / 4) + qb * QN + j * 16 + 4 * (l >> 4);
+        float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int m = m0 + wm * 128 + qa * 64 + i * 16 + (l & 15);
+            const bool ok = m < p.M && n < p.N;
+            const int64_t e = (int64_t)m * p.ldc + n;
+            uint16_t h[4];
+            float v[4];
+            if constexpr (ADD) {
+              // addend·[bit] added after rounding, as gemm_core.h add_bf16x8 (one more rounding)
+              uint2 ad = make_uint2(0u, 0u);
+              uint32_t bits = 0xfu;
+              if (ok) {
+                ad = *reinterpret_cast<const uint2*>(p.addend + e);
+                if (p.add_bits) bits = (uint32_t)(p.add_bits[e >> 3] >> (e & 7)) & 0xfu;
+              }
+              const uint32_t aw[2] = {ad.x, ad.y};
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float c0 = bf16_round(acc[qa][qb][i][j][r]);
+                const uint32_t word = aw[r >> 1];
+                const float av = ((bits >> r) & 1u) ? __uint_as_float(r & 1 ? word & 0xffff0000u : word << 16) : 0.f;
+                h[r] = bf16_rne(c0 + av);
+                v[r] = __uint_as_float((uint32_t)h[r] << 16);
+              }
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                h[r] = bf16_rne(acc[qa][qb][i][j][r]);
+                v[r] = __uint_as_float((uint32_t)h[r] << 16);
+              }
+            }
+            if (ok) {
+              *reinterpret_cast<uint2*>(static_cast<uint16_t*>(p.C) + e) =
+                  make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+            }
+            if (STATS && ok) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) { s1[r] += v[r]; s2[r] += v[r] * v[r]; }
+            }
+          }
+        if constexpr (STATS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s1[r] = sum16(s1[r]);
+            s2[r] = sum16(s2[r]);
+          }
+          const int srow = (m0 / 128) + wm;
+          if ((l & 15) == 0 && srow * 128 < p.M && n < p.N) {
+            float* d = p.stats + (int64_t)srow * 2 * p.N + n;
+            *reinterpret_cast<float4*>(d) = make_float4(s1[0], s1[1], s1[2], s1[3]);
+            *reinterpret_cast<float4*>(d + p.N) = make_float4(s2[0], s2[1], s2[2], s2[3]);
+          }
+        }
+      }
+    // every epilogue access is now older than the next counted wait
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!has_next) break;
+    gb = (gb + T) & 1;
+    t += gridDim.x;
+    m0 = m0n; n0 = n0n;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) va[a][hh] = van[a][hh];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int hb = 0; hb < NB; ++hb) vb[a][hb] = vbn[a][hb];
+    has_next = t + (int)gridDim.x < total;
+    if (has_next) setup(t + gridDim.x, van, vbn, m0n, n0n);
+  }
+  if (wm == 0) bar();
 }
 
 bool gemm_big_ok(const GemmArgs& g) {
   if (g.pro_scale != nullptr || g.addend != nullptr || g.bst_x != nullptr) return false;
+  if (g.stats != nullptr && (g.N % 4) != 0) return false;      // float4 statistics rows
   if (g.a_kcontig && g.b_kcontig) return (g.K % 8) == 0 && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
   // both MN-contiguous: whole 16-byte column chunks
   return !g.a_kcontig && !g.b_kcontig && (g.M % 8) == 0 && (g.N % 8) == 0 && (g.lda % 8) == 0 &&
@@ -449,6 +688,43 @@ void gemm_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st) {
     if (bn == 256) { LW_BIG(256, true) } else { LW_BIG(128, true) }
   }
 #undef LW_BIG
+}
+
+// the persistent big tiles: K-contiguous operands, bf16 output without bias / ReLU / accumulate,
+// no prologue / split-K / backward statistics, at least two K-tiles
+bool gemm_bigp_ok(const GemmArgs& g) {
+  if (!(g.a_kcontig && g.b_kcontig && g.out_bf16 && !g.accumulate && g.bias == nullptr &&
+        !g.relu && g.pro_scale == nullptr && g.bst_x == nullptr && g.K > BBK))
+    return false;
+  if ((g.K % 8) != 0 || (g.lda % 8) != 0 || (g.ldb % 8) != 0 || (g.N % 8) != 0 || (g.ldc % 4) != 0)
+    return false;
+  if (g.add_bits != nullptr && g.ldc != g.N) return false;
+  return true;
+}
+
+static int cu_count() {
+  int dev = 0, n = 0;
+  (void)hipGetDevice(&dev);
+  static int cached[64] = {0};
+  if (dev >= 0 && dev < 64 && cached[dev] > 0) return cached[dev];
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    n = 256;
+  if (dev >= 0 && dev < 64) cached[dev] = n;
+  return n;
+}
+
+void gemm_bigp(const GemmArgs& g, const GemmK& k, hipStream_t st) {
+  const int bn = g.tile == GEMM_P256 ? 256 : 128;
+  const int tiles = ((g.M + BBM - 1) / BBM) * ((g.N + bn - 1) / bn);
+  const int grid = tiles < cu_count() ? tiles : cu_count();     // one workgroup per CU (LDS)
+  const bool add = g.addend != nullptr, stats = g.stats != nullptr;
+#define LW_P(BNV)                                                                                  \
+  if (stats && add) hipLaunchKernelGGL((k_gemm_bigp<BNV, true, true>), dim3(grid), dim3(BGT), 0, st, k);  \
+  else if (stats) hipLaunchKernelGGL((k_gemm_bigp<BNV, true, false>), dim3(grid), dim3(BGT), 0, st, k);   \
+  else if (add) hipLaunchKernelGGL((k_gemm_bigp<BNV, false, true>), dim3(grid), dim3(BGT), 0, st, k);     \
+  else hipLaunchKernelGGL((k_gemm_bigp<BNV, false, false>), dim3(grid), dim3(BGT), 0, st, k);
+  if (bn == 256) { LW_P(256) } else { LW_P(128) }
+#undef LW_P
 }
 
 }  // namespace lw

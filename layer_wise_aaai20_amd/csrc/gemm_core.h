@@ -23,6 +23,24 @@ __device__ __forceinline__ uint16_t bf16_rne(float f) {
 }
 __device__ __forceinline__ float bf16_round(float f) { return __uint_as_float((uint32_t)bf16_rne(f) << 16); }
 
+// Sum over the 16 lanes of a DPP row, every lane getting the total: quad_perm [1,0,3,2] and
+// [2,3,0,1] (partners l^1, l^2), row_half_mirror (partner 7-l: holds the other quad's identical
+// sum, so equivalent to l^4) and row_mirror (15-l, equivalent to l^8). Each step is one VALU add
+// with a DPP operand instead of a ds_bpermute round trip through the LDS crossbar, and the adds
+// pair the same values in the same order as a l^1, l^2, l^4, l^8 butterfly (bit-identical).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                               0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum16(float v) {
+  v += dpp_mov<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);     // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);    // row_half_mirror
+  v += dpp_mov<0x140>(v);    // row_mirror
+  return v;
+}
+
 // bf16 + bf16 -> bf16 per element (fp32 add, one rounding): the same arithmetic as a separate
 // elementwise add of two bf16 tensors, so fusing the residual-gradient add changes no bits.
 __device__ __forceinline__ uint4 add_bf16x8(uint4 a, uint4 b) {
@@ -804,14 +822,11 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
         }
       }
       if (EPI == EPI_STATS) {
-        // the 16 rows held by lanes sharing l>>4, fixed butterfly order
+        // the 16 rows held by lanes sharing l>>4 (one DPP row), fixed pairing order
 #pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s1[r] += __shfl_xor(s1[r], o, 64);
-            s2[r] += __shfl_xor(s2[r], o, 64);
-          }
+        for (int r = 0; r < 4; ++r) {
+          s1[r] = sum16(s1[r]);
+          s2[r] = sum16(s2[r]);
         }
         if (lm == 0) {
 #pragma unroll

@@ -145,8 +145,11 @@ struct BNArgs {
   uint8_t* bits;           // ReLU bitmap, 1 bit/element: written by the forward apply, read back
                            // by the backward instead of the saved output (or nullptr)
   bool accum_dparams;      // backward: dgamma/dbeta += (into the gradient arena) instead of =
+  unsigned* tickets = nullptr;  // bn_stats with stat_rows: per-slice arrival tickets (zero, and
+                                // re-armed by the kernel) -> one-launch colsum + finalize
 };
 int bn_reduce_blocks(int64_t M, int C);
+int colsum_fused_blocks(int64_t rows);
 int colsum_blocks(int64_t rows);     // blocks folding R GEMM-epilogue statistics rows
 void bn_stats(const BNArgs& a, hipStream_t st);
 void bn_apply(const BNArgs& a, hipStream_t st);
@@ -263,6 +266,12 @@ bool conv_tile_ok(int mode, int tile);
 // the 256x256 / 256x128 big tiles (GEMM_B256*) on a row-gather conv: one class, identity row
 // map, C % 64 == 0, K-contiguous weight, no prologue / addend / backward statistics
 bool conv_big_ok(const GemmArgs& g, const ConvGeomHost& h);
+// direct 7x7/2 stem convolution from an LDS patch (conv.hip): 4-channel NHWC image, the packed
+// [64][7*8*4] weight, bf16 NHWC output + one column-statistics row per 4 output rows
+bool stem_conv7_ok(int C, int Co, int R, int S, int sh, int sw, int ph, int pw, int H, int W,
+                   int Ho, int Wo);
+void stem_conv7(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
+                int W, int Ho, int Wo, hipStream_t st);
 
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],

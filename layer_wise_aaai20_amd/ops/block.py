@@ -73,6 +73,9 @@ BN_DUAL = os.environ.get("LWAAAI_BN_DUAL", "1") != "0"
 TILES = (1, 2, 3, 4, 5, 6)          # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
 BIG = (21, 22)                      # 256x256 / 256x128 8-wave LDS-DMA kernel (csrc/gemm_big.hip)
+# the same tiles as a persistent kernel (csrc/gemm_big.hip k_gemm_bigp: one workgroup per CU, the
+# next tile's first K-tiles loaded during this tile's epilogue); LWAAAI_GEMM_PERSIST=0 drops them
+PERSIST = (23, 24) if os.environ.get("LWAAAI_GEMM_PERSIST", "0") != "0" else ()
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -93,7 +96,7 @@ def _splits(tiles: int, K: int) -> int:
 
 def _tile_dims(t: int) -> Tuple[int, int]:
     return {1: (128, 128), 2: (128, 128), 3: (256, 64), 4: (64, 256), 5: (256, 64),
-            6: (64, 64), 21: (256, 256), 22: (256, 128)}[t]
+            6: (64, 64), 21: (256, 256), 22: (256, 128), 23: (256, 256), 24: (256, 128)}[t]
 
 
 class GemmTuner(Tuner):
@@ -155,7 +158,10 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
     big = BIG if (pro is None and addend is None and bst is None and
                   ((a_kc and b_kc and K % 8 == 0) or
                    (not a_kc and not b_kc and M % 8 == 0 and N % 8 == 0 and not stats))) else ()
-    cands = TILES + big + (() if bst is not None else
+    persist = PERSIST if (pro is None and bst is None and a_kc and b_kc and out_bf16 and
+                          not accumulate and not split_k and K % 8 == 0 and K > 64 and
+                          N % 8 == 0) else ()
+    cands = TILES + big + persist + (() if bst is not None else
                            stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None,
                                         pro_on_a, addend is not None, split_k, accumulate))
     tile = TUNER.pick(key, run, cands)

@@ -39,6 +39,10 @@ COL_TILES = (1, 2, 4, 6)             # weight gradient
 # C % 64 == 0 (a K-tile inside one tap), K-contiguous weight, no prologue / addend / statistics
 # of the backward; LWAAAI_CONV_BIG=0 leaves them out of the tuner's candidates
 BIG_TILES = (21, 22) if os.environ.get("LWAAAI_CONV_BIG", "1") != "0" else ()
+# the direct 7x7/2 stem convolution from an LDS patch (csrc/conv.hip k_stem_conv7), a tuner
+# candidate of the ResNet stem's forward; LWAAAI_STEM_DIRECT=0 leaves it out
+STEM_DIRECT = 31
+STEM_DIRECT_ON = os.environ.get("LWAAAI_STEM_DIRECT", "0") != "0"
 _TILE_DIMS = {1: (128, 128, 32), 2: (128, 128, 64), 3: (256, 64, 32), 4: (64, 256, 32),
               5: (256, 64, 64), 6: (64, 64, 64)}
 
@@ -174,12 +178,18 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
     bf = bias.float().contiguous() if bias is not None else None
 
     def run(tile):
+        if tile == STEM_DIRECT:
+            return lib.stem_conv7(xin, op)
         return lib.conv_ex(xin, op, mode, geom, co, tile, 1, True, ps, pt, stats, None, False, 0,
                            True, K, bias=bf, relu=bool(relu))
     key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats,
            bias is not None, bool(relu))
     big = BIG_TILES if (not c4 and C % 64 == 0 and pro is None and co % 8 == 0) else ()
-    tile = TUNER.pick(key, run, ROW_TILES + big, _row_default(M, co))
+    direct = (STEM_DIRECT,) if (STEM_DIRECT_ON and c4 and co == 64 and (R, S) == (7, 7) and
+                                (sh, sw) == (2, 2) and (ph, pw) == (3, 3) and pro is None and
+                                bias is None and not relu and Ho % 4 == 0 and
+                                (4 * Wo) % 112 == 0 and 4 * Wo <= 448) else ()
+    tile = TUNER.pick(key, run, ROW_TILES + big + direct, _row_default(M, co))
     y, st = run(tile)
     return y.view(Nb, Ho, Wo, co).permute(0, 3, 1, 2), st
 

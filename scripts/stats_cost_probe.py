@@ -35,7 +35,7 @@ for m, n, k, cnt in [(802816, 64, 256, 2), (802816, 64, 64, 1), (802816, 256, 64
     best = {}
     for stats in (False, True):
         res = {}
-        for t in (2, 5, 21, 22, 12):
+        for t in (2, 5, 21, 22, 23, 24, 12):
             try:
                 res[t] = timeit(lambda: lib.gemm_ex(a, k, True, b, k, True, m, n, k, None, False,
                                                     1, True, t, None, None, True, stats, None,

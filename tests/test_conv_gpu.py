@@ -313,3 +313,25 @@ def test_conv_big_tiles_are_tuner_candidates(monkeypatch):
     dy2 = torch.randn(2, 128, 7, 7, device="cuda").bfloat16().contiguous(memory_format=CL)
     CV.conv_dgrad(dy2, w, (14, 14), 2, 1)          # stride 2: parity classes, no big tiles
     assert all(c[1] not in (21, 22) for c in seen["d"])
+
+
+@pytest.mark.parametrize("N,H", [(2, 224), (3, 112)])
+def test_stem_direct_conv_matches_gemm_path(N, H, monkeypatch):
+    """The direct 7x7/2 stem convolution from an LDS patch (csrc/conv.hip k_stem_conv7) is
+    bit-identical to the implicit-GEMM 4-channel path (same k order, 32-wide MFMA steps) and its
+    statistics rows (one per 4 output rows) fold to the column sums of the stored output."""
+    x, w = _inputs(N, 3, 64, H, 7, 9)
+    ref = F.conv2d(x.float(), w.float(), stride=2, padding=3)
+    outs = {}
+    for tile in (3, 2, CV.STEM_DIRECT):
+        monkeypatch.setattr(CV.TUNER, "pick", lambda key, run, cands, default, t=tile: t)
+        y, st = CV.conv_fwd(x, w, 2, 3, stats=True)
+        _close(y, ref, 1e-2)
+        outs[tile] = (y, st)
+    y, st = outs[CV.STEM_DIRECT]
+    assert torch.equal(y, outs[3][0]) and torch.equal(y, outs[2][0])
+    assert y.is_contiguous(memory_format=CL)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, 64)
+    tot = st.sum(0)
+    torch.testing.assert_close(tot[0], yf.sum(0), rtol=1e-3, atol=1e-1)
+    torch.testing.assert_close(tot[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)

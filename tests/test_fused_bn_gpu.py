@@ -187,3 +187,31 @@ def test_bn_bwd_dual_matches_two_single_passes(M, C):
     for a, b in zip((dg, db, dg2, db2), ref_outs):
         assert torch.equal(a, b)
     assert dg.data_ptr() == outs[0].data_ptr()          # accumulated in place
+
+
+@pytest.mark.parametrize("M,C,R", [(50176, 256, 392), (12544, 2048, 98), (802816, 64, 6272),
+                                   (1000, 136, 8)])
+def test_bn_stats_from_rows_one_launch(M, C, R, monkeypatch):
+    """bn_stats on GEMM-epilogue statistics rows: the one-launch colsum + finalize (per-slice
+    arrival tickets, last block folds) gives the batch mean / invstd / scale-shift and running
+    statistics of the rows, and its tickets re-arm: repeated calls agree bit for bit."""
+    from layer_wise_aaai20_amd.ops._ext import load
+    lib = load()
+    g = torch.Generator(device="cuda").manual_seed(C)
+    rows = torch.randn(R, 2, C, device="cuda", generator=g)
+    rows[:, 1] = rows[:, 1].abs() * 4 + 2
+    x = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+    gamma = torch.rand(C, device="cuda", generator=g) + 0.5
+    beta = torch.randn(C, device="cuda", generator=g)
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    outs = [lib.bn_stats(x, rows, gamma, beta, rm, rv, 0.1, 1e-5) for _ in range(3)]
+    s = rows.double().sum(0)
+    mean = s[0] / M
+    var = (s[1] / M - mean * mean).clamp_min(0)
+    torch.testing.assert_close(outs[0][0].double(), mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(outs[0][1].double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-5)
+    sc = gamma.double() / torch.sqrt(var + 1e-5)
+    torch.testing.assert_close(outs[0][2][:C].double(), sc, rtol=1e-4, atol=1e-5)
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(o, outs[0]))
+    assert torch.isfinite(rm).all() and not torch.equal(rm, torch.zeros_like(rm))

@@ -96,7 +96,7 @@ def test_gemm_stats_epilogue(tile):
     w = torch.randn(N, K, device="cuda").bfloat16()
     C, st = G.gemm_ex(x, K, True, w, K, True, M, N, K, tile=tile, stats=True)
     bm = {"128x128x32": 128, "256x64x32": 256, "64x256x32": 64, "64x64x64": 64,
-          "256x256x64": 256, "256x128x64": 256}[tile]
+          "256x256x64": 128, "256x128x64": 128}[tile]   # big tiles: one row per wave row
     tiles_m = -(-M // bm)
     assert st.shape == (tiles_m, 2, N)
     c = C.float()
@@ -292,3 +292,43 @@ def test_gemm_big_tile_bitwise_vs_128(tile, kc):
     c1, _ = G.gemm_ex(A, lda, kc, B, ldb, kc, M, N, K, out_bf16=False, tile=tile)
     c2, _ = G.gemm_ex(A, lda, kc, B, ldb, kc, M, N, K, out_bf16=False, tile="128x128x64")
     torch.testing.assert_close(c1, c2, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,N,K", [(50176 // 4, 1024, 256), (3000, 264, 136), (70000, 64, 128),
+                                   (1000, 2048, 512), (256 * 300, 256, 72)])
+@pytest.mark.parametrize("tile", [23, 24])
+def test_gemm_persistent_big_tile(M, N, K, tile):
+    """Persistent big tiles (csrc/gemm_big.hip k_gemm_bigp, tiles 23/24: one workgroup per CU
+    walking several tiles, the next tile's K-tiles 0/1 loaded during the epilogue): bf16 output
+    bit-identical to the 128x128x64 tile (plain, + column statistics, + ReLU-masked addend), the
+    statistics rows (one per 128 rows) fold to the column sums; ragged M / N / K, T = 2 K-tiles,
+    more tiles than CUs."""
+    lib = _lib()
+    torch.manual_seed(tile + K)
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    B = torch.randn(N, K, device="cuda").bfloat16()
+    add = torch.randn(M, N, device="cuda").bfloat16()
+    bits = torch.randint(0, 256, (M * N // 8,), dtype=torch.uint8, device="cuda")
+    for stats in (False, True):
+        ref, _ = lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, 1, True, 2, None, None,
+                             True, stats, None, None, False, 0)
+        got, st = lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, 1, True, tile, None,
+                              None, True, stats, None, None, False, 0)
+        assert torch.equal(got, ref)
+        if stats:
+            assert st.shape[0] == -(-M // 128)
+            yf = got.float()
+            s = st.sum(0)
+            torch.testing.assert_close(s[0], yf.sum(0), rtol=1e-3, atol=1e-1)
+            torch.testing.assert_close(s[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+    ref = lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, 1, True, 2, None, None, True,
+                      False, None, add, False, 0, bits)[0]
+    got = lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, 1, True, tile, None, None,
+                      True, False, None, add, False, 0, bits)[0]
+    assert torch.equal(got, ref)
+    dst = add.clone()                                 # in place: out aliases the addend
+    lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, 1, True, tile, None, None, True,
+                False, dst, dst, False, 0, None)
+    ref2 = lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, 1, True, 2, None, None, True,
+                       False, None, add, False, 0, None)[0]
+    assert torch.equal(dst, ref2)

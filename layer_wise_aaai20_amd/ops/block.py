@@ -75,7 +75,7 @@ STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 
 BIG = (21, 22)                      # 256x256 / 256x128 8-wave LDS-DMA kernel (csrc/gemm_big.hip)
 # the same tiles as a persistent kernel (csrc/gemm_big.hip k_gemm_bigp: one workgroup per CU, the
 # next tile's first K-tiles loaded during this tile's epilogue); LWAAAI_GEMM_PERSIST=0 drops them
-PERSIST = (23, 24) if os.environ.get("LWAAAI_GEMM_PERSIST", "0") != "0" else ()
+PERSIST = (23, 24) if os.environ.get("LWAAAI_GEMM_PERSIST", "1") != "0" else ()
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:

@@ -40,9 +40,10 @@ COL_TILES = (1, 2, 4, 6)             # weight gradient
 # of the backward; LWAAAI_CONV_BIG=0 leaves them out of the tuner's candidates
 BIG_TILES = (21, 22) if os.environ.get("LWAAAI_CONV_BIG", "1") != "0" else ()
 # the direct 7x7/2 stem convolution from an LDS patch (csrc/conv.hip k_stem_conv7), a tuner
-# candidate of the ResNet stem's forward; LWAAAI_STEM_DIRECT=0 leaves it out
+# candidate of the ResNet stem's forward (337 vs 392 us at bs 256, profiles/r3s2/);
+# LWAAAI_STEM_DIRECT=0 leaves it out
 STEM_DIRECT = 31
-STEM_DIRECT_ON = os.environ.get("LWAAAI_STEM_DIRECT", "0") != "0"
+STEM_DIRECT_ON = os.environ.get("LWAAAI_STEM_DIRECT", "1") != "0"
 _TILE_DIMS = {1: (128, 128, 32), 2: (128, 128, 64), 3: (256, 64, 32), 4: (64, 256, 32),
               5: (256, 64, 64), 6: (64, 64, 64)}
 
@@ -178,8 +179,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
     bf = bias.float().contiguous() if bias is not None else None
 
     def run(tile):
-        if tile == STEM_DIRECT:
-            return lib.stem_conv7(xin, op)
+        if tile == STEM_DIRECT:               # NHWC output: as the [pixels, Co] GEMM rows
+            ys, sts = lib.stem_conv7(xin, op)
+            return ys.permute(0, 2, 3, 1).reshape(M, co), sts
         return lib.conv_ex(xin, op, mode, geom, co, tile, 1, True, ps, pt, stats, None, False, 0,
                            True, K, bias=bf, relu=bool(relu))
     key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats,

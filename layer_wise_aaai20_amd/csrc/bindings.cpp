@@ -1132,7 +1132,7 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
   TORCH_CHECK(!relu || (ga && out_bf16 && !g.bst_x), "conv ReLU epilogue: forward convs only");
   g.relu = relu;
   if (tile == lw::GEMM_B256 || tile == lw::GEMM_B256x128)
-    TORCH_CHECK(mode == lw::CV_A && lw::conv_big_ok(g, h),
+    TORCH_CHECK((mode == lw::CV_A || mode == lw::CV_B) && lw::conv_big_ok(g, h),
                 "conv big tiles: one-class row gather, C % 64 == 0, K-contiguous weight, no "
                 "prologue / addend / backward statistics");
   lw::conv_gemm(g, h, (int)mode, cur_stream());

@@ -130,10 +130,10 @@ static void conv_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, hip
 
 // Tile families: the row-gather passes (forward / dgrad: M = pixels, large) take the square and
 // skinny-N tiles; the weight-gradient pass (M = Co, N = taps·C) the square and skinny-M ones.
-void conv_big(const GemmArgs& g, const GemmK& k, hipStream_t st);     // gemm_big.hip
+void conv_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st);   // gemm_big.hip
 
 bool conv_tile_ok(int mode, int tile) {
-  if (mode == CV_A && (tile == GEMM_B256 || tile == GEMM_B256x128)) return true;
+  if ((mode == CV_A || mode == CV_B) && (tile == GEMM_B256 || tile == GEMM_B256x128)) return true;
   if (mode == CV_A || mode == CV_A4)
     return tile == GEMM_T128x128x32 || tile == GEMM_T128x128x64 || tile == GEMM_T256x64x32 ||
            tile == GEMM_T256x64x64 || tile == GEMM_T64x64x64;
@@ -188,7 +188,8 @@ void conv_gemm(const GemmArgs& g, const ConvGeomHost& cvh, int mode, hipStream_t
   k.bst_shift = g.bst_shift;
   k.bst_bits = g.bst_bits;
   if (g.tile == GEMM_B256 || g.tile == GEMM_B256x128) {
-    conv_big(g, k, st);              // (bindings.cpp checked conv_big_ok)
+    conv_big(g, k, zs, st);          // (bindings.cpp checked conv_big_ok)
+    if (zs > 1) splitk_reduce(g, zs, st);
     return;
   }
   const dim3 grid(tiles, zs, cvh.nclass);

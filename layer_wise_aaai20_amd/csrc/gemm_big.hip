@@ -75,9 +75,10 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :
 // (Tried: reading the next K-tile's B0 fragments in P3 after a wait moved to P2, so the LDS reads
 // spread 8/4/8/4 over the phases instead of 12/4/8/0: 251 VGPRs and 7 % slower at 8192^3,
 // profiles/r3/gemm_big_pf_ab.jsonl.)
-template <int BN, int EPI, bool MN, bool GA = false>
+template <int BN, int EPI, bool MN, bool GA = false, bool GB = false>
 __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   static_assert(!(GA && MN), "the row gather stages a K-contiguous A");
+  static_assert(!GB || MN, "the column gather (weight gradient) stages an MN-contiguous B");
   constexpr int BHALF = (BN / 2) * BBK;        // bf16 elements per B half-tile
   constexpr int BUF = 2 * AHALF + 2 * BHALF;   // one K-tile: A0 A1 B0 B1
   constexpr int NB = BN / 128;                 // DMA instructions per B half (A: 2)
@@ -110,6 +111,12 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   int ghb[2][2], gwb[2][2], grow[2][2];
   const int gC = p.cv.C, gHin = p.cv.Hin, gWin = p.cv.Win;
   const float inv_c = 1.f / (float)gC, inv_ts = 1.f / (float)p.cv.cls[0].TS;
+  // GB (weight gradient): B rows are output pixels, columns (tap, channel) of the input window:
+  // per B chunk the tap's window offset (bho, bwo; columns past N fail every bounds test) and,
+  // in vb, the byte offset of (tap, channel) relative to the pixel's window origin
+  int bho[2][NB], bwo[2][NB];
+  const int gHw = p.cv.cls[0].Hg * p.cv.cls[0].Wg;
+  const float inv_hw = 1.f / (float)gHw, inv_wg = 1.f / (float)p.cv.cls[0].Wg;
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     const int q = threadIdx.x + hh * BGT;           // chunk of the half-tile this lane lands in
@@ -171,7 +178,20 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         const int n = n0 + (c / QN) * (BN / 4) + qb * QN + (c % QN);
-        vb[qb][hb] = n < p.N ? (uint32_t)(((int64_t)(kbeg + k) * p.ldb + n) * 2) : OOB;
+        if constexpr (GB) {
+          // column n = (tap, channel): the chunk's window offset, fixed for the kernel
+          const int nn = n < p.N ? n : 0;
+          int ci;
+          const int t = fdivmod(nn, gC, inv_c, ci);
+          int js;
+          const int jr = fdivmod(t, p.cv.cls[0].TS, inv_ts, js);
+          const int ho = p.cv.cls[0].oh + p.cv.dh * jr;
+          bwo[qb][hb] = p.cv.cls[0].ow + p.cv.dw * js;
+          vb[qb][hb] = (uint32_t)(((ho * gWin + bwo[qb][hb]) * gC + ci) * 2);
+          bho[qb][hb] = n < p.N ? ho : -(1 << 28);
+        } else {
+          vb[qb][hb] = n < p.N ? (uint32_t)(((int64_t)(kbeg + k) * p.ldb + n) * 2) : OOB;
+        }
       }
     }
   }
@@ -207,6 +227,23 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
     } else {
       const uint32_t kofs = MN ? (uint32_t)(kt * BBK) * (uint32_t)p.ldb * 2u : (uint32_t)(kt * BBK * 2);
       uint16_t* base = lds + buf * BUF + 2 * AHALF + (h - 2) * BHALF;
+      if constexpr (GB) {
+        // the chunk's output pixel (row kt*64 + kb of the K-slice) -> its window origin
+#pragma unroll
+        for (int hb = 0; hb < NB; ++hb) {
+          const int kk = kt * BBK + kb[hb];
+          const int pix = kbeg + (kk < klen ? kk : 0);
+          int rem, x;
+          const int b = fdivmod(pix, gHw, inv_hw, rem);
+          const int y = fdivmod(rem, p.cv.cls[0].Wg, inv_wg, x);
+          const int yb = y * p.cv.sh, xb = x * p.cv.sw;
+          const bool ok = kk < klen && (unsigned)(yb + bho[h - 2][hb]) < (unsigned)gHin &&
+                          (unsigned)(xb + bwo[h - 2][hb]) < (unsigned)gWin;
+          const int pbase = ((b * gHin + yb) * gWin + xb) * gC * 2;
+          glds16(rb, base + (w * 64 + hb * BGT) * 8, ok ? (uint32_t)(pbase + (int)vb[h - 2][hb]) : OOB);
+        }
+        return;
+      }
 #pragma unroll
       for (int hb = 0; hb < NB; ++hb)
         glds16(rb, base + (w * 64 + hb * BGT) * 8,
@@ -658,15 +695,26 @@ bool gemm_big_ok(const GemmArgs& g) {
 // whole 64-channel K-tiles, a K-contiguous weight operand, no prologue / addend / backward
 // statistics.
 bool conv_big_ok(const GemmArgs& g, const ConvGeomHost& h) {
+  if (!g.a_kcontig && !g.b_kcontig)          // weight gradient: B = the im2col column gather
+    return h.nclass == 1 && h.C % 8 == 0 && g.M % 8 == 0 && g.N % 8 == 0 && (g.lda % 8) == 0 &&
+           g.pro_scale == nullptr && g.stats == nullptr && !g.out_bf16;
   return h.nclass == 1 && h.osy == 1 && h.osx == 1 && h.C % BBK == 0 && g.b_kcontig &&
          (g.ldb % 8) == 0 && g.pro_scale == nullptr && g.addend == nullptr && g.bst_x == nullptr &&
          g.N % 8 == 0;
 }
 
-void conv_big(const GemmArgs& g, const GemmK& k, hipStream_t st) {
+void conv_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st) {
   const int bn = g.tile == GEMM_B256 ? 256 : 128;
   const int tiles = ((g.M + BBM - 1) / BBM) * ((g.N + bn - 1) / bn);
-  const dim3 grid(tiles, 1), block(BGT);
+  const dim3 grid(tiles, zs), block(BGT);
+  if (!g.a_kcontig) {                        // weight gradient (fp32 slab or accumulate)
+#define LW_CBIGW(BNV)                                                                              \
+  if (zs > 1) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_PARTIAL, true, false, true>), grid, block, 0, st, k); \
+  else hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STORE, true, false, true>), grid, block, 0, st, k);
+    if (bn == 256) { LW_CBIGW(256) } else { LW_CBIGW(128) }
+#undef LW_CBIGW
+    return;
+  }
 #define LW_CBIG(BNV)                                                                                \
   if (g.stats) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STATS, false, true>), grid, block, 0, st, k); \
   else hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STORE, false, true>), grid, block, 0, st, k);

@@ -45,7 +45,7 @@ BIG_TILES = (21, 22) if os.environ.get("LWAAAI_CONV_BIG", "1") != "0" else ()
 STEM_DIRECT = 31
 STEM_DIRECT_ON = os.environ.get("LWAAAI_STEM_DIRECT", "1") != "0"
 _TILE_DIMS = {1: (128, 128, 32), 2: (128, 128, 64), 3: (256, 64, 32), 4: (64, 256, 32),
-              5: (256, 64, 64), 6: (64, 64, 64)}
+              5: (256, 64, 64), 6: (64, 64, 64), 21: (256, 256, 64), 22: (256, 128, 64)}
 
 
 def _pair(v) -> Tuple[int, int]:
@@ -293,9 +293,12 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, pro=
     mode = CV_B4 if c4 else CV_B
     ps, pt = (pro[0], pro[1]) if pro is not None else (None, None)
 
+    # the big tiles with the im2col column gather (csrc/gemm_big.hip GB): C % 8, Co % 8, no prologue
+    big = BIG_TILES if (not c4 and co % 8 == 0 and pro is None) else ()
+
     def cands():
         cs = []
-        for t in COL_TILES:
+        for t in COL_TILES + big:
             bm, bn, bk = _TILE_DIMS[t]
             tiles = -(-co // bm) * -(-N // bn)
             s0 = _wgrad_splits(tiles, pix, bk)

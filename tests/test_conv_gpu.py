@@ -335,3 +335,28 @@ def test_stem_direct_conv_matches_gemm_path(N, H, monkeypatch):
     tot = st.sum(0)
     torch.testing.assert_close(tot[0], yf.sum(0), rtol=1e-3, atol=1e-1)
     torch.testing.assert_close(tot[1], (yf * yf).sum(0), rtol=1e-3, atol=1e-1)
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 256, 14, 3, 1, 1), (4, 512, 512, 7, 3, 1, 1),
+                                   (4, 128, 256, 28, 3, 2, 1), (3, 64, 136, 9, 3, 1, 0),
+                                   (2, 256, 512, 14, 1, 2, 0)],
+                         ids=lambda s: str(s))
+@pytest.mark.parametrize("tile", [21, 22])
+def test_conv_wgrad_big_tiles(shape, tile, monkeypatch):
+    """Weight gradients on the 8-wave big tiles with the im2col column gather (gemm_big.hip GB):
+    fp32 vs torch for 1 / 2 / 4 split-K slices, padding 0 / 1, stride 1 / 2, N = taps*C off the
+    tile grid, and accumulation into a channels_last arena view."""
+    N, C, Co, H, k, s, p = shape
+    x, w = _inputs(N, C, Co, H, k, 11)
+    wf = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wf, stride=s, padding=p)
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    for sp in (1, 2, 4):
+        monkeypatch.setattr(CV.TUNER, "pick", lambda key, run, cands, default, c=(tile, sp): c)
+        dw = CV.conv_wgrad(dy.contiguous(memory_format=CL), x, tuple(w.shape), s, p)
+        _close(dw, wf.grad, 2e-3)
+    arena = torch.full((Co * C * k * k,), 0.25, device="cuda")
+    view = arena.as_strided(w.shape, (C * k * k, 1, k * C, C))
+    CV.conv_wgrad(dy.contiguous(memory_format=CL), x, tuple(w.shape), s, p, out=view)
+    _close(view - 0.25, wf.grad, 2e-3)

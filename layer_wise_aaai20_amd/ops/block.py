@@ -147,10 +147,14 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
         return _splits(-(-M // bm) * -(-N // bn), K)
 
     key = (M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a, split_k,
-           addend is not None, bst is not None)
+           addend is not None, bst is not None) + (("sk",) if split_k else ())
 
-    def run(tile):
-        lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile), out_bf16,
+    def unpack(c):
+        return c if isinstance(c, tuple) else (c, splits_for(c))
+
+    def run(c):
+        tile, sp = unpack(c)
+        lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, sp, out_bf16,
                     tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits,
                     bx, bm, bss, bb)
     # the big tiles: both operands K-contiguous (forward, transposed-weight dgrad) or both
@@ -164,8 +168,13 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
     cands = TILES + big + persist + (() if bst is not None else
                            stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None,
                                         pro_on_a, addend is not None, split_k, accumulate))
-    tile = TUNER.pick(key, run, cands)
-    return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, splits_for(tile),
+    if split_k:
+        # (tile, split-K) pairs: fewer, longer K-slices write fewer fp32 slabs for the fixed-order
+        # reduce (the weight gradients are HBM-bound; fewer workgroups can still stream them)
+        cands = tuple((t, s) for t in cands
+                      for s in sorted({max(1, splits_for(t) >> q) for q in (0, 1, 2, 3)}))
+    tile, sp = unpack(TUNER.pick(key, run, cands))
+    return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, sp,
                        out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc,
                        addend_bits, bx, bm, bss, bb)
 

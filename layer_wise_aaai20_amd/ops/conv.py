@@ -302,7 +302,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, pro=
             bm, bn, bk = _TILE_DIMS[t]
             tiles = -(-co // bm) * -(-N // bn)
             s0 = _wgrad_splits(tiles, pix, bk)
-            for s in sorted({max(1, s0 // 2), s0, s0 * 2}):
+            for s in sorted({max(1, s0 // 8), max(1, s0 // 4), max(1, s0 // 2), s0, s0 * 2}):
                 cs.append((t, s))
         return cs
 

@@ -1165,6 +1165,30 @@ std::tuple<Tensor, Tensor> stem_conv7(Tensor x, Tensor w) {
   return {y, st};
 }
 
+// Direct 3x3 / stride-1 / pad-1 convolution 64 -> 64 channels (conv.hip k_conv3_direct):
+// x [N, 64, H, W] bf16 channels_last, w the K-contiguous [64][576] operand ((r, s, ci) order);
+// returns (y [N, 64, H, W] channels_last, stats [N*H/8, 2, 64] or an empty tensor).
+std::tuple<Tensor, Tensor> conv3_direct(Tensor x, Tensor w, bool want_stats) {
+  const c10::DeviceGuard guard(x.device());
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 &&
+              x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: [N, 64, H, W] channels_last");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == 64 * 576, "w: [64][576]");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(lw::conv3_direct_ok((int)C, 64, (int)H, (int)W), "conv3_direct: unsupported geometry");
+  TORCH_CHECK(x.numel() * 2 < (1LL << 40), "conv3_direct size");
+  check_aligned16(x.data_ptr(), "x");
+  check_aligned16(w.data_ptr(), "w");
+  Tensor y = at::empty({N, 64, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor st = want_stats ? at::empty({N * H / 8, 2, 64}, x.options().dtype(at::kFloat))
+                         : at::empty({0}, x.options().dtype(at::kFloat));
+  lw::conv3_direct(ptr<uint16_t>(x), ptr<uint16_t>(w), ptr<uint16_t>(y),
+                   want_stats ? ptr<float>(st) : nullptr, (int)N, (int)H, (int)W, cur_stream());
+  launched("conv3_direct");
+  return {y, st};
+}
+
 // ---------------------------------------------------------------- BN pieces for fused blocks
 // Arrival tickets of the one-launch colsum + finalize (bn.hip k_colsum_finalize), one per 64-channel
 // slice: zeroed once per device (eagerly: never created inside a graph capture) and re-armed by the
@@ -1477,6 +1501,7 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? stats_rows=None) "
       "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("stem_conv7(Tensor x, Tensor w) -> (Tensor, Tensor)");
+  m.def("conv3_direct(Tensor x, Tensor w, bool want_stats) -> (Tensor, Tensor)");
   m.def(
       "bn_bwd_dual(Tensor dy, Tensor x, Tensor x2, Tensor bits, Tensor? weight, Tensor mean, "
       "Tensor invstd, Tensor? weight2, Tensor mean2, Tensor invstd2, "
@@ -1536,6 +1561,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("bn_bwd", &bn_bwd);
   m.impl("bn_bwd_dual", &bn_bwd_dual);
   m.impl("stem_conv7", &stem_conv7);
+  m.impl("conv3_direct", &conv3_direct);
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);
   m.impl("conv_ex", &conv_ex);

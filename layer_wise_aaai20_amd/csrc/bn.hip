@@ -606,7 +606,7 @@ static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblo
   const int nsl = reduce_slices(C);
   const int G = C / nsl / 8;
   const int R = BNT / G;
-  static const int64_t target = env_int("LWAAAI_BN_BLOCKS", 1024);   // ≈ 4 blocks per CU
+  static const int64_t target = env_int("LWAAAI_BN_BLOCKS", 512);   // ≈ 4 blocks per CU
   const int64_t rb = (target + nsl - 1) / nsl;
   int64_t rpb = (M + rb - 1) / rb;
   rpb = (rpb + R - 1) / R * R;

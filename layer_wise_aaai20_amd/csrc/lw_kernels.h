@@ -272,6 +272,11 @@ bool stem_conv7_ok(int C, int Co, int R, int S, int sh, int sw, int ph, int pw, 
                    int Ho, int Wo);
 void stem_conv7(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
                 int W, int Ho, int Wo, hipStream_t st);
+// direct 3x3 / stride-1 / pad-1 convolution, 64 -> 64 channels, NHWC, from an LDS patch
+// (conv.hip k_conv3_direct); stats (optional): one column-statistics row per 8 output rows
+bool conv3_direct_ok(int C, int Co, int H, int W);
+void conv3_direct(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
+                  int W, hipStream_t st);
 
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],

@@ -44,6 +44,18 @@ BIG_TILES = (21, 22) if os.environ.get("LWAAAI_CONV_BIG", "1") != "0" else ()
 # LWAAAI_STEM_DIRECT=0 leaves it out
 STEM_DIRECT = 31
 STEM_DIRECT_ON = os.environ.get("LWAAAI_STEM_DIRECT", "1") != "0"
+# the direct 3x3/1 convolution 64 -> 64 channels from an LDS patch (csrc/conv.hip
+# k_conv3_direct), for that forward and its data gradient (flipped, transposed weight). Opt-in
+# (LWAAAI_CONV3_DIRECT=1): at bs 256 it measured 130 us forward / 151 us data gradient against
+# 127 / 117 us for the implicit-GEMM tiles (profiles/r3s2/direct_probe.txt) — its 149 KB of LDS
+# (patch + the whole weight) leave one workgroup per CU, so staging and MFMAs do not overlap
+CONV3_DIRECT = 32
+CONV3_DIRECT_ON = os.environ.get("LWAAAI_CONV3_DIRECT", "0") != "0"
+
+
+def _conv3_direct_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
+    return (CONV3_DIRECT_ON and c == 64 and co == 64 and (R, S) == (3, 3) and (sh, sw) == (1, 1)
+            and (ph, pw) == (1, 1) and H % 8 == 0 and (8 * W) % 112 == 0 and 8 * W <= 448)
 _TILE_DIMS = {1: (128, 128, 32), 2: (128, 128, 64), 3: (256, 64, 32), 4: (64, 256, 32),
               5: (256, 64, 64), 6: (64, 64, 64), 21: (256, 256, 64), 22: (256, 128, 64)}
 
@@ -182,6 +194,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
         if tile == STEM_DIRECT:               # NHWC output: as the [pixels, Co] GEMM rows
             ys, sts = lib.stem_conv7(xin, op)
             return ys.permute(0, 2, 3, 1).reshape(M, co), sts
+        if tile == CONV3_DIRECT:
+            ys, sts = lib.conv3_direct(xin, op, True)
+            return ys.permute(0, 2, 3, 1).reshape(M, co), sts
         return lib.conv_ex(xin, op, mode, geom, co, tile, 1, True, ps, pt, stats, None, False, 0,
                            True, K, bias=bf, relu=bool(relu))
     key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats,
@@ -191,6 +206,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
                                 (sh, sw) == (2, 2) and (ph, pw) == (3, 3) and pro is None and
                                 bias is None and not relu and Ho % 4 == 0 and
                                 (4 * Wo) % 112 == 0 and 4 * Wo <= 448) else ()
+    if (pro is None and bias is None and not relu and not c4 and
+            _conv3_direct_fits(C, co, R, S, sh, sw, ph, pw, H, W)):
+        direct = direct + (CONV3_DIRECT,)
     tile = TUNER.pick(key, run, ROW_TILES + big + direct, _row_default(M, co))
     y, st = run(tile)
     return y.view(Nb, Ho, Wo, co).permute(0, 3, 1, 2), st
@@ -232,6 +250,12 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
 
     def run(cand, dst=None, add=None):
         layout, tile = cand
+        if layout == "direct" and (dst is not None or add is not None):
+            layout, tile = "kc", 2            # the direct kernel writes a fresh tensor only
+        if layout == "direct":        # conv of dy with W'[ci][r][s][co] = w[co][ci][2-r][2-s]
+            wf = w.to(BF16).flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).contiguous()
+            ys, _ = lib.conv3_direct(dyc, wf, False)
+            return ys.permute(0, 2, 3, 1).reshape(-1, c), None
         if layout == "kc":            # packed per call: the tuner times the pack with the conv
             wk, koffs, kmax = pack_dgrad_weight_kc(w, classes, sh, sw)
             g = list(geom)
@@ -249,6 +273,9 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
                         c % 8 == 0 and addend is None and bst is None) else ()
     cands = [("nkc", t) for t in ROW_TILES] + \
         ([("kc", t) for t in ROW_TILES + big] if bst is None else [])
+    if (addend is None and bst is None and out is None and
+            _conv3_direct_fits(co, c, R, S, sh, sw, ph, pw, Ho, Wo) and (H, W) == (Ho, Wo)):
+        cands.append(("direct", CONV3_DIRECT))
     cand = TUNER.pick(key, run, cands, ("nkc", _row_default(M, c)))   # (timed on scratch outputs)
     dx, st = run(cand, out, addend)
     if bst is not None:

@@ -1208,7 +1208,7 @@ static unsigned* colsum_tickets(const Tensor& like) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(cur_stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
       return nullptr;
-    Tensor t = at::zeros({kMaxBnC / 64 + 1}, like.options().dtype(at::kInt));
+    Tensor t = at::zeros({kMaxBnC / 32 + 1}, like.options().dtype(at::kInt));
     it = per_dev.emplace(dev, t).first;
   }
   return reinterpret_cast<unsigned*>(it->second.data_ptr());

@@ -299,39 +299,50 @@ __device__ __forceinline__ void finalize_fwd_channel(int c, double s, double q, 
   }
 }
 
-// Column statistics rows of a GEMM / conv epilogue [R][2C] -> the BatchNorm finalize, in ONE
-// launch: block (x, y) sums rows [x*rpb, (x+1)*rpb) of the 2*64 columns of channel slice y
-// (Σv and Σv² of 64 channels) into partial [2C][nb]; the last block of a slice to arrive (an
+// Column statistics rows of a GEMM / conv epilogue [R][2C] -> the BatchNorm finalize in ONE launch
+// (opt-in, LWAAAI_COLSUM_FUSED=1: measured 0.25 ms per step SLOWER than k_colsum +
+// k_bn_finalize_fwd, profiles/r3s2/colsum_fused_ab.txt). The last block of a slice to arrive (an
 // agent-scope release / relaxed ticket / acquire, cdna_hip_programming.md §6 Guideline 16 — no
-// block ever waits) folds the slice's nb partials in the fixed fp64 order of k_bn_finalize_fwd and
-// writes mean / invstd / scale / shift / running statistics, then re-arms the slice's ticket.
-constexpr int CSF_SLICE = 64;
-__global__ __launch_bounds__(256) void k_colsum_finalize(
+// block ever waits) does the fold and finalize, then re-arms the slice's ticket. Block (x, y) sums rows
+// [x*rpb, (x+1)*rpb) of slice y's 64 columns (Σv and Σv² of 32 channels) with its 256 threads as
+// 4 row phases x 64 columns (fixed order, combined in LDS), and the slice's last-arriving block
+// folds the nb partials with all 256 threads (4 contiguous block ranges x 64 columns, fp64, fixed
+// order) before the finalize. nb ~ 2*sqrt(R) balances the two phases.
+constexpr int CS2_CH = 32;
+__global__ __launch_bounds__(256) void k_colsum_finalize2(
     const float* __restrict__ rows, int64_t R, int C, int64_t rows_per_block,
     float* __restrict__ partial, unsigned* __restrict__ tickets, int64_t M,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ mean_out,
     float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
-  __shared__ unsigned sh_last[1];
+  __shared__ __attribute__((aligned(16))) double sh[4 * 64 + 1];   // one array: partial sums, flag
+  float* shf = reinterpret_cast<float*>(sh);
+  unsigned* sh_last = reinterpret_cast<unsigned*>(sh + 4 * 64);
   const int nb = gridDim.x;
-  const int c0 = blockIdx.y * CSF_SLICE;
-  const int cs = min(CSF_SLICE, C - c0);
+  const int c0 = blockIdx.y * CS2_CH;
+  const int cs = min(CS2_CH, C - c0);
   const int W = 2 * C;
-  if ((int)threadIdx.x < 2 * cs) {
-    const int col = (int)threadIdx.x < cs ? c0 + (int)threadIdx.x : C + c0 + (int)threadIdx.x - cs;
+  const int cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const bool active = cl < 2 * cs;
+  const int col = cl < cs ? c0 + cl : C + c0 + (cl - cs);
+  {
     const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t r1 = min(r0 + rows_per_block, R);
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int64_t r = r0;
-    for (; r + 3 < r1; r += 4) {
-      s0 += rows[r * W + col];
-      s1 += rows[(r + 1) * W + col];
-      s2 += rows[(r + 2) * W + col];
-      s3 += rows[(r + 3) * W + col];
+    float a = 0.f;
+    if (active) {
+      int64_t r = r0 + ph;
+      for (; r + 12 < r1; r += 16) {      // 4 loads in flight, added in row order
+        const float v0 = rows[r * W + col], v1 = rows[(r + 4) * W + col];
+        const float v2 = rows[(r + 8) * W + col], v3 = rows[(r + 12) * W + col];
+        a += v0; a += v1; a += v2; a += v3;
+      }
+      for (; r < r1; r += 4) a += rows[r * W + col];
     }
-    for (; r < r1; ++r) s0 += rows[r * W + col];
-    partial[(int64_t)col * nb + blockIdx.x] = (s0 + s1) + (s2 + s3);
+    shf[ph * 64 + cl] = a;
   }
+  __syncthreads();
+  if (threadIdx.x < 64 && active)
+    partial[(int64_t)col * nb + blockIdx.x] = ((shf[cl] + shf[64 + cl]) + shf[128 + cl]) + shf[192 + cl];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -339,20 +350,40 @@ __global__ __launch_bounds__(256) void k_colsum_finalize(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = __hip_atomic_fetch_add(tickets + blockIdx.y, 1u, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
-    sh_last[0] = prev == (unsigned)(nb - 1) ? 1u : 0u;
+    *sh_last = prev == (unsigned)(nb - 1) ? 1u : 0u;
   }
   __syncthreads();
-  if (sh_last[0] == 0u) return;
+  if (*sh_last == 0u) return;
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  for (int c = c0 + (int)(threadIdx.x >> 6); c < c0 + cs; c += 4) {
-    double sm, sq;
-    if (fold_channel(partial, nb, C, c, sm, sq))
-      finalize_fwd_channel(c, sm, sq, M, gamma, beta, eps, momentum, rmean, rvar, mean_out,
-                           invstd_out, scale, shift);
+  // fold: thread (ph, cl) sums blocks [ph*q, (ph+1)*q) of column col in fp64, 8 loads in flight
+  double d = 0.0;
+  if (active) {
+    const int q = (nb + 3) / 4;
+    const int b0 = ph * q, b1 = min(nb, b0 + q);
+    const float* p = partial + (int64_t)col * nb;
+    int b = b0;
+    for (; b + 7 < b1; b += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[b + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) d += (double)v[u];
+    }
+    for (; b < b1; ++b) d += (double)p[b];
+  }
+  __syncthreads();                        // (shf is reused as the fp64 fold area)
+  sh[ph * 64 + cl] = d;
+  __syncthreads();
+  if (threadIdx.x < cs) {
+    const int c = threadIdx.x;
+    const double s = ((sh[c] + sh[64 + c]) + sh[128 + c]) + sh[192 + c];
+    const double qq = ((sh[cs + c] + sh[64 + cs + c]) + sh[128 + cs + c]) + sh[192 + cs + c];
+    finalize_fwd_channel(c0 + c, s, qq, M, gamma, beta, eps, momentum, rmean, rvar, mean_out,
+                         invstd_out, scale, shift);
   }
   if (threadIdx.x == 0)
     __hip_atomic_store(tickets + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -620,8 +651,11 @@ static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblo
 // row blocks of the fused colsum + finalize: few enough that the last block's fold of a slice
 // (64 channels x 2 x nb partials) stays short
 int colsum_fused_blocks(int64_t rows) {
-  static const int cap = env_int("LWAAAI_COLSUM_FUSED_BLOCKS", 64);
-  return (int)(rows < cap ? rows : cap);
+  // ~2*sqrt(R) row blocks balance the row-sum phase against the last block's fold
+  static const int cap = env_int("LWAAAI_COLSUM_FUSED_BLOCKS", 256);
+  int nb = 2;
+  while ((int64_t)nb * nb < 4 * rows && nb < cap) ++nb;
+  return (int)(rows < nb ? rows : nb);
 }
 
 int colsum_blocks(int64_t rows) {
@@ -672,13 +706,13 @@ static void bn_apply_t(const BNArgs& a, hipStream_t st) {
 template <typename T>
 static void bn_stats_t(const BNArgs& a, hipStream_t st) {
   int nb = a.stats_blocks;
-  if (a.stat_rows && a.tickets) {         // rows -> statistics in one launch (k_colsum_finalize)
+  if (a.stat_rows && a.tickets) {         // rows -> statistics in one launch (k_colsum_finalize2)
     const int64_t R = a.stats_rows_n;
     int nbf = colsum_fused_blocks(R);
     const int64_t rpb = (R + nbf - 1) / nbf;
     nbf = (int)((R + rpb - 1) / rpb);
-    const int slices = (a.C + CSF_SLICE - 1) / CSF_SLICE;
-    hipLaunchKernelGGL(k_colsum_finalize, dim3(nbf, slices), dim3(256), 0, st, a.stat_rows, R,
+    const int slices = (a.C + CS2_CH - 1) / CS2_CH;
+    hipLaunchKernelGGL(k_colsum_finalize2, dim3(nbf, slices), dim3(256), 0, st, a.stat_rows, R,
                        a.C, rpb, a.partial, a.tickets, a.M, a.gamma, a.beta, a.eps, a.momentum,
                        a.rmean, a.rvar, a.mean, a.invstd, a.scale, a.shift);
     return;

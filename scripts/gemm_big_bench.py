@@ -97,10 +97,10 @@ def main():
         w = torch.randn(N, K, device="cuda").bfloat16()
         row = {"shape": name, "M": M, "N": N, "K": K}
         ref = None
-        for t in (2, 21, 22):
+        for t in (2, 21, 22, 23, 24):     # 23 / 24: the persistent big tiles (never split)
             best = None
             for sp in SPLITS:
-                if sp > 1 and K // sp < 256:
+                if sp > 1 and (K // sp < 256 or t in (23, 24)):
                     continue
                 ms = timeit(lambda: G.gemm_ex(a, K, True, w, K, True, M, N, K, splits=sp, tile=t),
                             iters)

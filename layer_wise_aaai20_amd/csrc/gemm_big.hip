@@ -75,10 +75,12 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" :
 // (Tried: reading the next K-tile's B0 fragments in P3 after a wait moved to P2, so the LDS reads
 // spread 8/4/8/4 over the phases instead of 12/4/8/0: 251 VGPRs and 7 % slower at 8192^3,
 // profiles/r3/gemm_big_pf_ab.jsonl.)
-template <int BN, int EPI, bool MN, bool GA = false, bool GB = false>
+// MN: A is MN-contiguous ([K][M]); MNB (default MN): B is ([K][N]). Mixed layouts (K-contiguous
+// A with an N-contiguous B: a data gradient dY·W with W as stored) stage each operand its own way.
+template <int BN, int EPI, bool MN, bool GA = false, bool GB = false, bool MNB = MN>
 __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   static_assert(!(GA && MN), "the row gather stages a K-contiguous A");
-  static_assert(!GB || MN, "the column gather (weight gradient) stages an MN-contiguous B");
+  static_assert(!GB || MNB, "the column gather (weight gradient) stages an MN-contiguous B");
   constexpr int BHALF = (BN / 2) * BBK;        // bf16 elements per B half-tile
   constexpr int BUF = 2 * AHALF + 2 * BHALF;   // one K-tile: A0 A1 B0 B1
   constexpr int NB = BN / 128;                 // DMA instructions per B half (A: 2)
@@ -161,7 +163,7 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
 #pragma unroll
   for (int hb = 0; hb < NB; ++hb) {
     const int q = threadIdx.x + hb * BGT;
-    if constexpr (!MN) {
+    if constexpr (!MNB) {
       const int lr = q >> 3, cc = q & 7;
       const int gc = cc ^ (lr & 7);
       kb[hb] = gc * 8;
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
         glds16(ra, base + (w * 64 + hh * BGT) * 8,
                kt * BBK + ka[hh] < klen ? va[h][hh] + kofs : OOB);
     } else {
-      const uint32_t kofs = MN ? (uint32_t)(kt * BBK) * (uint32_t)p.ldb * 2u : (uint32_t)(kt * BBK * 2);
+      const uint32_t kofs = MNB ? (uint32_t)(kt * BBK) * (uint32_t)p.ldb * 2u : (uint32_t)(kt * BBK * 2);
       uint16_t* base = lds + buf * BUF + 2 * AHALF + (h - 2) * BHALF;
       if constexpr (GB) {
         // the chunk's output pixel (row kt*64 + kb of the K-slice) -> its window origin
@@ -277,7 +279,7 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
     for (int j = 0; j < FQ; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        if constexpr (MN) f[j][s] = frag_tr<WB>(h, wn * QN + j * 16, s);
+        if constexpr (MNB) f[j][s] = frag_tr<WB>(h, wn * QN + j * 16, s);
         else f[j][s] = *reinterpret_cast<const bf16x8*>(
             h + big_off(wn * QN + j * 16 + (l & 15), 4 * s + (l >> 4)));
       }
@@ -686,6 +688,8 @@ bool gemm_big_ok(const GemmArgs& g) {
   if (g.pro_scale != nullptr || g.addend != nullptr || g.bst_x != nullptr) return false;
   if (g.stats != nullptr && (g.N % 4) != 0) return false;      // float4 statistics rows
   if (g.a_kcontig && g.b_kcontig) return (g.K % 8) == 0 && (g.lda % 8) == 0 && (g.ldb % 8) == 0;
+  if (g.a_kcontig && !g.b_kcontig)       // data gradient dY·W, W as stored ([K][N])
+    return (g.K % 8) == 0 && (g.lda % 8) == 0 && (g.N % 8) == 0 && (g.ldb % 8) == 0;
   // both MN-contiguous: whole 16-byte column chunks
   return !g.a_kcontig && !g.b_kcontig && (g.M % 8) == 0 && (g.N % 8) == 0 && (g.lda % 8) == 0 &&
          (g.ldb % 8) == 0 && g.stats == nullptr;
@@ -730,7 +734,14 @@ void gemm_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st) {
   if (zs > 1) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_PARTIAL, MNV>), grid, block, 0, st, k);    \
   else if (g.stats) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STATS, MNV>), grid, block, 0, st, k); \
   else hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STORE, MNV>), grid, block, 0, st, k);
-  if (g.a_kcontig) {
+  if (g.a_kcontig && !g.b_kcontig) {
+#define LW_BIGX(BNV)                                                                                          \
+  if (zs > 1) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_PARTIAL, false, false, false, true>), grid, block, 0, st, k); \
+  else if (g.stats) hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STATS, false, false, false, true>), grid, block, 0, st, k); \
+  else hipLaunchKernelGGL((k_gemm_big<BNV, EPI_STORE, false, false, false, true>), grid, block, 0, st, k);
+    if (bn == 256) { LW_BIGX(256) } else { LW_BIGX(128) }
+#undef LW_BIGX
+  } else if (g.a_kcontig) {
     if (bn == 256) { LW_BIG(256, false) } else { LW_BIG(128, false) }
   } else {
     if (bn == 256) { LW_BIG(256, true) } else { LW_BIG(128, true) }

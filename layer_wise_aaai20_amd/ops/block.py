@@ -157,10 +157,12 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
         lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, sp, out_bf16,
                     tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits,
                     bx, bm, bss, bb)
-    # the big tiles: both operands K-contiguous (forward, transposed-weight dgrad) or both
-    # MN-contiguous (weight gradients); no prologue / addend / backward statistics
+    # the big tiles: both operands K-contiguous (forward, transposed-weight dgrad), a K-contiguous
+    # A with the weight as stored (dgrad), or both MN-contiguous (weight gradients); no prologue /
+    # addend / backward statistics
     big = BIG if (pro is None and addend is None and bst is None and
                   ((a_kc and b_kc and K % 8 == 0) or
+                   (a_kc and not b_kc and K % 8 == 0 and N % 8 == 0 and ldb % 8 == 0) or
                    (not a_kc and not b_kc and M % 8 == 0 and N % 8 == 0 and not stats))) else ()
     persist = PERSIST if (pro is None and bst is None and a_kc and b_kc and out_bf16 and
                           not accumulate and not split_k and K % 8 == 0 and K > 64 and

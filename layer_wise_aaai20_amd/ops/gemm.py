@@ -49,7 +49,7 @@ class LinearTuner(Tuner):
     pass (``profiles/r2_linear_vs_blas*.log``)."""
 
     TILES = (1, 2, 3, 4, 5, 6)
-    BIG = (21, 22)                    # 8-wave LDS-DMA tiles: both operands K- or both MN-contiguous
+    BIG = (21, 22)                    # 8-wave LDS-DMA tiles: K-/K-, K-/N- or M-/N-contiguous operands
     SPLITS = (1, 2, 4, 8, 16)
 
     def __init__(self):
@@ -79,7 +79,8 @@ def _gemm_tuned(kind, A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False
         return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias, relu, sp, out_bf16, t, None,
                            None, True, False, dst, None, acc, 0, None)[0]
     key = (kind, M, N, K, bias is not None, relu, out_bf16)
-    big = (a_kc and b_kc and K % 8 == 0) or (not a_kc and not b_kc and M % 8 == 0 and N % 8 == 0)
+    big = (a_kc and b_kc and K % 8 == 0) or (not a_kc and not b_kc and M % 8 == 0 and N % 8 == 0) \
+        or (a_kc and not b_kc and K % 8 == 0 and N % 8 == 0 and ldb % 8 == 0)
     t, sp = TUNER.pick(key, _tiles(M, N), K, run, big=big)
     return run(t, sp, out, accumulate)
 

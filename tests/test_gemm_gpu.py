@@ -332,3 +332,20 @@ def test_gemm_persistent_big_tile(M, N, K, tile):
     ref2 = lib.gemm_ex(A, K, True, B, K, True, M, N, K, None, False, 1, True, 2, None, None, True,
                        False, None, add, False, 0, None)[0]
     assert torch.equal(dst, ref2)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 25088 // 8, 4096 // 4), (520, 264, 328), (1000, 136, 72)])
+@pytest.mark.parametrize("tile", ["256x256x64", "256x128x64"])
+def test_gemm_big_tile_mixed_layout(M, N, K, tile):
+    """Big tiles with a K-contiguous A and an N-contiguous B (a data gradient dY·W with W as
+    stored): fp32 vs torch with 1 / 3 split-K slices and bit-identical to the 128x128x64 tile."""
+    torch.manual_seed(9)
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    Bkn = torch.randn(K, N, device="cuda").bfloat16()           # [K][N], N-contiguous
+    ref = A.float() @ Bkn.float()
+    for sp in (1, 3):
+        C, _ = G.gemm_ex(A, K, True, Bkn, N, False, M, N, K, splits=sp, out_bf16=False, tile=tile)
+        torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
+    c1, _ = G.gemm_ex(A, K, True, Bkn, N, False, M, N, K, out_bf16=False, tile=tile)
+    c2, _ = G.gemm_ex(A, K, True, Bkn, N, False, M, N, K, out_bf16=False, tile="128x128x64")
+    torch.testing.assert_close(c1, c2, rtol=0, atol=0)

@@ -1,6 +1,7 @@
-// Large-tile bf16 MFMA GEMM for gfx950: 256x256 output tile per 512-thread workgroup (8 waves as
-// 2 (M) x 4 (N), each wave 128x64), BK = 64, both operands K-contiguous (A [M][K], B [N][K]:
-// x·Wᵀ of a Linear / 1x1 convolution, and the square benchmark shapes).
+// Large-tile bf16 MFMA GEMM for gfx950: 256x256 (or 256x128) output tile per 512-thread workgroup
+// (8 waves as 2 (M) x 4 (N), each wave 128x64), BK = 64. Operands K-contiguous (A [M][K], B [N][K]:
+// x·Wᵀ of a Linear / 1x1 convolution, the square benchmark shapes), both M/N-contiguous (weight
+// gradients dYᵀ·X), or a K-contiguous A with an N-contiguous B (data gradients dY·W).
 //
 // Why a second GEMM structure: the 128x128 / 4-wave tiles of gemm_core.h cross a workgroup barrier
 // with vmcnt(0) once per K-step, which caps them near 900 TFLOP/s on large problems
@@ -25,13 +26,14 @@
 //   P1: read B1    -> Q01   DMA (c+2).A0 -> buffer c&1       vmcnt: (c).A1 landed
 //   P2: read A1    -> Q11   DMA (c+2).B0 -> buffer c&1
 //   P3: (registers)-> Q10   DMA (c+2).B1 -> buffer c&1       vmcnt: (c+1).A0,B0 landed
-// Epilogues: bf16 / fp32 store with bias + ReLU, or an fp32 split-K slab (reduced by
-// k_splitk_reduce in gemm.hip, fixed order).
+// Epilogues: bf16 / fp32 store with bias + ReLU (+ column statistics, one row per wave row), or
+// an fp32 split-K slab (reduced by k_splitk_reduce in gemm.hip, fixed order).
 // GA: the A operand is the im2col row gather of a convolution (conv.hip CV_A, one parity class,
 // C % 64 == 0): a K-tile then lies inside one filter tap, so a lane's DMA source is its pixel's
 // window origin + the tap's (uniform) offset, and a tap falling into the padding becomes an OOB
 // offset (the DMA lands zeros) — the same big-tile schedule runs the 3x3 forward and stride-1
-// data-gradient convolutions with no im2col buffer.
+// data-gradient convolutions with no im2col buffer. GB: the B operand of a weight gradient is the
+// im2col column gather (column = (tap, channel), row = output pixel, decoded per K-tile).
 #include "common.h"
 #include "gemm_core.h"
 
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)blockIdx.y * p.M * p.N : nullptr;
   // EPI_STATS: Σv / Σv² of the stored (bf16-rounded) outputs per column over a wave row's 128
   // rows, folded across the 16 row-lanes in DPP rows; one statistics row per wave row (128 rows of
-  // C: gemm_stats_rows), written straight from the registers — no LDS, no barrier
+  // C: gemm.hip stats_rows_bm), written straight from the registers — no LDS, no barrier
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb)
 #pragma unroll

@@ -224,8 +224,9 @@ enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_
                 // streaming kernel (persistent, B panel resident in LDS, A straight to registers),
                 // output-panel width 64 / 128 / 256; K must be 64, 128 or 256
                 GEMM_S64 = 11, GEMM_S128 = 12, GEMM_S256 = 13,
-                // 256x256x64 tile, 8 waves, LDS-DMA kept in flight across barriers (gemm_big.hip);
-                // K-contiguous A and B, no prologue / statistics / addend
+                // 256x256 / 256x128 x64 tiles, 8 waves, LDS-DMA kept in flight across barriers
+                // (gemm_big.hip): K-/K-, K-/N- or M-/N-contiguous operands, column statistics (one
+                // row per 128 rows), split-K slabs; no prologue / addend
                 GEMM_B256 = 21, GEMM_B256x128 = 22,
                 // the same tiles as a persistent kernel (one workgroup per CU walking tiles, the
                 // next tile's first K-tiles loaded during this tile's epilogue): K-contiguous A/B,

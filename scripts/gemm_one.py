@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Run one MFMA GEMM problem repeatedly (for rocprofv3 counter passes on a single kernel).
-usage: gemm_one.py M N K tile [layout fwd|dgrad|wgrad] [iters]"""
+usage: gemm_one.py M N K tile [layout fwd|dgrad|wgrad] [iters] [splits]"""
 import os
 import sys
 
@@ -12,6 +12,7 @@ from layer_wise_aaai20_amd.ops import gemm as G  # noqa: E402
 M, N, K, tile = (int(v) for v in sys.argv[1:5])
 lay = sys.argv[5] if len(sys.argv) > 5 else "fwd"
 iters = int(sys.argv[6]) if len(sys.argv) > 6 else 5
+splits = int(sys.argv[7]) if len(sys.argv) > 7 else 1
 a = torch.randn(M, K, device="cuda").bfloat16()
 w = torch.randn(N, K, device="cuda").bfloat16()
 if lay == "fwd":
@@ -21,7 +22,8 @@ elif lay == "dgrad":
     run = lambda: G.gemm_ex(a, K, True, wt, N, False, M, N, K, tile=tile)  # noqa: E731
 else:
     at, wt = a.t().contiguous(), w.t().contiguous()
-    run = lambda: G.gemm_ex(at, M, False, wt, N, False, M, N, K, tile=tile, out_bf16=False)  # noqa: E731
+    run = lambda: G.gemm_ex(at, M, False, wt, N, False, M, N, K, tile=tile, out_bf16=False,  # noqa: E731
+                            splits=splits)
 for _ in range(iters):
     run()
 torch.cuda.synchronize()

@@ -8,7 +8,16 @@ import sys
 
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
-for r in csv.DictReader(open(sys.argv[1])):
+rows = list(csv.DictReader(open(sys.argv[1])))
+if "--last-step" in sys.argv:
+    # only the dispatches of the last step: after the second-to-last fused-SGD dispatch (the tile
+    # tuners' timing runs of the first eager step are excluded)
+    did = lambda r: int(r.get("Dispatch_Id", r.get("Correlation_Id", "0")) or 0)  # noqa: E731
+    sgd = sorted({did(r) for r in rows if "k_sgd" in r["Kernel_Name"]})
+    if len(sgd) >= 2:
+        lo, hi = sgd[-2], sgd[-1]
+        rows = [r for r in rows if lo < did(r) <= hi]
+for r in rows:
     k = r["Kernel_Name"][:90]
     agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
     disp[k].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))

@@ -94,9 +94,10 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];   // one array (rule 4a)
   const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BBM - 1) / BBM;
   int tm, tn;
-  tile_of(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
+  int split;
+  tile_split_of(tiles_m, tiles_n, tm, tn, split);     // gemm_core.h (split-K slices per XCD)
   const int m0 = tm * BBM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kbeg = split * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int T = kbeg < kend ? (kend - kbeg + BBK - 1) / BBK : 0;
   const int klen = kend - kbeg;
@@ -349,7 +350,7 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
   // ---- epilogue, straight from the accumulators. B was the MFMA's first operand, so lane l holds
   // C[m = .. + (l & 15)][n = .. + 4 * (l >> 4) + r], r = 0..3.
   const bool vec4 = (EPI == EPI_PARTIAL ? (p.N & 3) == 0 : (p.ldc & 3) == 0);
-  float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)blockIdx.y * p.M * p.N : nullptr;
+  float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)split * p.M * p.N : nullptr;
   // EPI_STATS: Σv / Σv² of the stored (bf16-rounded) outputs per column over a wave row's 128
   // rows, folded across the 16 row-lanes in DPP rows; one statistics row per wave row (128 rows of
   // C: gemm.hip stats_rows_bm), written straight from the registers — no LDS, no barrier

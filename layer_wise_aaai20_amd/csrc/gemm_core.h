@@ -615,6 +615,27 @@ __device__ __forceinline__ void tile_of(int pid, int tiles_m, int tiles_n, int& 
   tn = r / rows;
 }
 
+#ifndef LW_SPLIT_XCD
+#define LW_SPLIT_XCD 1           // 0: split = blockIdx.y, tiles remapped within a slice only (A/B)
+#endif
+// (tile, split-K slice) of this workgroup. Workgroups are dealt to the 8 XCDs round-robin in
+// dispatch order (x fastest, then y); remap that order so each XCD gets one contiguous range of the
+// split-major (slice, tile) order: the tiles of one K-slice then sit on the same XCD and share
+// their common operand rows in its L2 (a weight gradient's im2col columns of one pixel range are
+// read by every column tile) instead of each fetching them from HBM. zs == 1: the plain map.
+__device__ __forceinline__ void tile_split_of(int tiles_m, int tiles_n, int& tm, int& tn,
+                                              int& split) {
+  const int tiles = tiles_m * tiles_n;
+  if (gridDim.y == 1 || !LW_SPLIT_XCD) {
+    split = (int)blockIdx.y;
+    tile_of(xcd_remap(blockIdx.x, tiles), tiles_m, tiles_n, tm, tn);
+    return;
+  }
+  const int lin = xcd_remap((int)(blockIdx.y * gridDim.x + blockIdx.x), tiles * (int)gridDim.y);
+  split = lin / tiles;
+  tile_of(lin - split * tiles, tiles_m, tiles_n, tm, tn);
+}
+
 template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int PRO, int CV = CV_NONE>
 __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   using TA = Tile<BM, BK, AKC>;
@@ -644,7 +665,8 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
 
   const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
   int tm, tn;
-  tile_of(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
+  int split;
+  tile_split_of(tiles_m, tiles_n, tm, tn, split);
   const int m0 = tm * BM, n0 = tn * BN;
   // the class record by constant index (a runtime index into the by-value kernel argument
   // would copy the whole array to scratch)
@@ -653,7 +675,7 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
                       : zc == 2 ? p.cv.cls[2] : p.cv.cls[3];
   if (GA && m0 >= ccl.M) return;                // parity class with fewer rows than the grid
   const int Kc = GA ? ccl.K : p.K;
-  const int kbeg = blockIdx.y * p.k_per_split;
+  const int kbeg = split * p.k_per_split;
   const int kend = min(Kc, kbeg + p.k_per_split);
   const uint16_t* Bp = GA ? p.B + ccl.b_off : p.B;
   const int Mrow = GA ? ccl.M : p.M;             // valid GEMM rows of this workgroup
@@ -950,7 +972,7 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   } else {
     // fp32 output or split-K slab: two halves through an fp32 staging tile
     float* Cs = reinterpret_cast<float*>(lds);
-    float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)blockIdx.y * Mrow * p.N : nullptr;
+    float* P = EPI == EPI_PARTIAL ? p.partial + (int64_t)split * Mrow * p.N : nullptr;
     float* dstbase = EPI == EPI_PARTIAL ? P : static_cast<float*>(p.C);
     const int64_t ld = EPI == EPI_PARTIAL ? p.N : p.ldc;
     const bool vec = (p.N & 3) == 0 && (ld & 3) == 0;

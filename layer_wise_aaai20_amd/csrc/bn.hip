@@ -545,11 +545,14 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, c
                                                       const float* __restrict__ B,
                                                       const float* __restrict__ Cc,
                                                       T* __restrict__ dx, T* __restrict__ dres,
-                                                      int64_t n8, int C) {
+                                                      int64_t n8, int C, int rev) {
   const int G = C / 8;
   const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
   const int64_t step = (int64_t)gridDim.x * BNT;
-  const int c0 = (int)(t0 % G) * 8;
+  // rev: walk the rows last to first (element e = n8-1-i; n8 and step are multiples of G, so the
+  // channel group stays fixed per thread): the reduce pass just streamed the same dy / x first to
+  // last, so its most recent lines — the ones still in the 256 MB Infinity Cache — come first
+  const int c0 = (int)((rev ? n8 - 1 - t0 : t0) % G) * 8;
   float ca[8], cb[8], cc[8], fs[8], fh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -557,7 +560,8 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, c
     fs[k] = RELU == 2 ? fscale[c0 + k] : 0.f;
     fh[k] = RELU == 2 ? fshift[c0 + k] : 0.f;
   }
-  for (int64_t i = t0; i < n8; i += step) {
+  for (int64_t i0 = t0; i0 < n8; i0 += step) {
+    const int64_t i = rev ? n8 - 1 - i0 : i0;
     const int64_t off = i * 8;
     float xv[8], d[8];
     V8<T>::load(x + off, xv);
@@ -588,18 +592,19 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply_dual(
     const uint16_t* __restrict__ dy, const uint8_t* __restrict__ bits,
     const float* __restrict__ A, const float* __restrict__ B, const float* __restrict__ Cc,
     const float* __restrict__ A2, const float* __restrict__ B2, const float* __restrict__ Cc2,
-    uint16_t* __restrict__ dx, uint16_t* __restrict__ dx2, int64_t n8, int C) {
+    uint16_t* __restrict__ dx, uint16_t* __restrict__ dx2, int64_t n8, int C, int rev) {
   const int G = C / 8;
   const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
   const int64_t step = (int64_t)gridDim.x * BNT;
-  const int c0 = (int)(t0 % G) * 8;
+  const int c0 = (int)((rev ? n8 - 1 - t0 : t0) % G) * 8;     // (rev: see k_bn_bwd_apply)
   float ca[8], cb[8], cc[8], ca2[8], cb2[8], cc2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     ca[k] = A[c0 + k]; cb[k] = B[c0 + k]; cc[k] = Cc[c0 + k];
     ca2[k] = A2[c0 + k]; cb2[k] = B2[c0 + k]; cc2[k] = Cc2[c0 + k];
   }
-  for (int64_t i = t0; i < n8; i += step) {
+  for (int64_t i0 = t0; i0 < n8; i0 += step) {
+    const int64_t i = rev ? n8 - 1 - i0 : i0;
     const int64_t off = i * 8;
     float xv[8], x2v[8], d[8];
     V8<uint16_t>::load(x + off, xv);
@@ -622,6 +627,11 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply_dual(
 static int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
+}
+// backward apply passes walk the rows last to first with LWAAAI_BN_REVERSE=1 (default: first to last)
+static bool bn_reverse() {
+  static const bool r = env_int("LWAAAI_BN_REVERSE", 0) != 0;
+  return r;
 }
 static int reduce_unroll() {
   static const int u = env_int("LWAAAI_BN_UNROLL", 4);
@@ -783,7 +793,7 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   const dim3 grid(apply_grid(n8, a.C)), block(BNT);
 #define LW_BWD(R, D)                                                                            \
   hipLaunchKernelGGL((k_bn_bwd_apply<T, R, D>), grid, block, 0, st, x, dy, y, a.bits, a.scale,  \
-                     a.shift, a.A, a.B, a.Cc, dx, dres, n8, a.C)
+                     a.shift, a.A, a.B, a.Cc, dx, dres, n8, a.C, bn_reverse() ? 1 : 0)
   if (rmode == 3) { if (dres) LW_BWD(3, true); else LW_BWD(3, false); }
   else if (rmode == 1) { if (dres) LW_BWD(1, true); else LW_BWD(1, false); }
   else if (rmode == 2) { if (dres) LW_BWD(2, true); else LW_BWD(2, false); }
@@ -813,7 +823,7 @@ void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st) {
   const int64_t n8 = a.M * a.C / 8;
   hipLaunchKernelGGL(k_bn_bwd_apply_dual, dim3(apply_grid(n8, a.C)), dim3(BNT), 0, st, x, x2, dy,
                      a.bits, a.A, a.B, a.Cc, b.A, b.B, b.Cc, static_cast<uint16_t*>(a.dx),
-                     static_cast<uint16_t*>(b.dx), n8, a.C);
+                     static_cast<uint16_t*>(b.dx), n8, a.C, bn_reverse() ? 1 : 0);
 }
 
 void bn_forward(const BNArgs& a, hipStream_t st) {

@@ -35,7 +35,12 @@ def test_resnet9_learns_with_compression(method, kw, mode):
     from layer_wise_aaai20_amd.utils.logging import PiecewiseLinear
     steps = 200
     tr.steps_per_epoch = 1                           # schedule in steps: warm-up 40, decay to 0
-    tr.sched = PiecewiseLinear([0, 40, steps], [0, 0.4, 0])
+    # entire-model TernGrad scales the ternary code by max|g| over all 6.6 M parameters, so its
+    # variance dwarfs ||g||²: at the recipe's peak LR it diverges without EF (loss 2.8e26 over 24
+    # epochs, profiles/r3/cifar_method_accuracy_table.jsonl) and can stall with it (loss 1.02 ->
+    # 1.05 on one tuner draw); it trains at a quarter of the peak LR
+    peak = 0.1 if (method, mode) == ("TernGrad", "entiremodel") else 0.4
+    tr.sched = PiecewiseLinear([0, 40, steps], [0, peak, 0])
     losses = []
     for _ in range(steps):
         losses.append(float(tr.step()) / tr.bs)

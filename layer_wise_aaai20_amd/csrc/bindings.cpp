@@ -1142,7 +1142,7 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
 
 // Direct stem convolution (conv.hip k_stem_conv7): x4 [N, 4, H, W] bf16 channels_last (the image
 // padded to 4 channels), w the packed [64][224] operand of pack_fwd_weight; returns
-// (y [N, 64, Ho, Wo] channels_last, stats [N*Ho/4, 2, 64]).
+// (y [N, 64, Ho, Wo] channels_last, stats [workgroups, 2, 64]).
 std::tuple<Tensor, Tensor> stem_conv7(Tensor x, Tensor w) {
   const c10::DeviceGuard guard(x.device());
   check_dtype(x, at::kBFloat16, "x");
@@ -1158,7 +1158,7 @@ std::tuple<Tensor, Tensor> stem_conv7(Tensor x, Tensor w) {
   check_aligned16(x.data_ptr(), "x");
   check_aligned16(w.data_ptr(), "w");
   Tensor y = at::empty({N, 64, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  Tensor st = at::empty({N * Ho / 4, 2, 64}, x.options().dtype(at::kFloat));
+  Tensor st = at::empty({lw::stem_conv7_blocks((int)N, (int)Ho), 2, 64}, x.options().dtype(at::kFloat));
   lw::stem_conv7(ptr<uint16_t>(x), ptr<uint16_t>(w), ptr<uint16_t>(y), ptr<float>(st), (int)N,
                  (int)H, (int)W, (int)Ho, (int)Wo, cur_stream());
   launched("stem_conv7");
@@ -1349,7 +1349,8 @@ std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x
                                                  Tensor scale_shift, c10::optional<Tensor> weight,
                                                  Tensor mean, Tensor invstd, int64_t k, int64_t s,
                                                  int64_t p, c10::optional<Tensor> dgamma_out,
-                                                 c10::optional<Tensor> dbeta_out) {
+                                                 c10::optional<Tensor> dbeta_out,
+                                                 c10::optional<Tensor> pooled) {
   const c10::DeviceGuard guard(x.device());
   lw::StemArgs a{};
   stem_geom(x, k, s, p, a);
@@ -1357,6 +1358,12 @@ std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x
   TORCH_CHECK(dp.is_contiguous(at::MemoryFormat::ChannelsLast) && dp.size(2) == a.Ho &&
               dp.size(3) == a.Wo && dp.size(1) == a.C && dp.size(0) == a.N, "dp shape/layout");
   TORCH_CHECK(idx.numel() == dp.numel() && idx.scalar_type() == at::kByte, "idx");
+  if (pooled.has_value() && pooled->defined()) {
+    check_dtype(*pooled, at::kBFloat16, "pooled");
+    TORCH_CHECK(pooled->sizes() == dp.sizes() &&
+                pooled->is_contiguous(at::MemoryFormat::ChannelsLast), "pooled shape/layout");
+    a.pooled = pooled->data_ptr();
+  }
   auto f32 = x.options().dtype(at::kFloat);
   Tensor dx = at::empty_like(x);
   bool accum = false;
@@ -1536,7 +1543,7 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def(
       "stem_pool_bwd(Tensor dp, Tensor idx, Tensor x, Tensor scale_shift, Tensor? weight, "
       "Tensor mean, Tensor invstd, int k, int s, int p, Tensor(a!)? dgamma_out=None, "
-      "Tensor(b!)? dbeta_out=None) -> (Tensor, Tensor, Tensor)");
+      "Tensor(b!)? dbeta_out=None, Tensor? pooled=None) -> (Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {

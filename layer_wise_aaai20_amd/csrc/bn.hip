@@ -1114,6 +1114,85 @@ __global__ __launch_bounds__(BNT) void k_stem_pool_bwd_s2(const uint16_t* __rest
   }
 }
 
+// Reduce pass of the stem backward from the POOLED side. The routed gradient dz is non-zero only
+// at each window's argmax, where relu(scale·x + shift) is exactly the stored pooled value p, so
+//   Σdz = Σ_{p > 0} d   and   Σdz·(x - mean) = Σ_{p > 0} d·(p - beta) / scale,
+// beta = shift + mean·scale (linear in dz, so overlapping windows need no care). The pass reads
+// the pooled gradient and the pooled map (2 x N·Ho·Wo·C bf16) instead of the 4x larger conv output
+// plus the slot bytes. A channel with scale == 0 (p constant, x not recoverable) reads x at the
+// argmax through the slot byte instead. Partials as k_stem_pool_bwd<0>: [2][C][nb].
+__global__ __launch_bounds__(BNT) void k_stem_pool_reduce_out(const uint16_t* __restrict__ dp,
+                                                              const uint16_t* __restrict__ pooled,
+                                                              const uint8_t* __restrict__ idx,
+                                                              const uint16_t* __restrict__ x,
+                                                              const float* __restrict__ scale,
+                                                              const float* __restrict__ shift,
+                                                              const float* __restrict__ mean,
+                                                              float* __restrict__ partial,
+                                                              PoolGeom g, int64_t rows_per_block) {
+  __shared__ float sa[BNT * 8];
+  __shared__ float sb[BNT * 8];
+  const int G = g.C / 8;
+  const int R = BNT / G;
+  const int cg = threadIdx.x % G, r = threadIdx.x / G;
+  const bool active = r < R;
+  const int64_t P = (int64_t)g.N * g.Ho * g.Wo;
+  float sc[8], rs[8], be[8], mu[8], a[8], b[8];
+  bool degen = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = active ? cg * 8 + j : 0;
+    sc[j] = scale[c]; mu[j] = mean[c];
+    be[j] = fmaf(mu[j], sc[j], shift[c]);
+    rs[j] = sc[j] != 0.f ? 1.f / sc[j] : 0.f;
+    degen |= sc[j] == 0.f;
+    a[j] = 0.f; b[j] = 0.f;
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(r0 + rows_per_block, P);
+  if (active) {
+    for (int64_t pt = r0 + r; pt < r1; pt += R) {
+      const int64_t o = pt * g.C + cg * 8;
+      float d[8], p[8];
+      V8<uint16_t>::load(dp + o, d);
+      V8<uint16_t>::load(pooled + o, p);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dz = p[j] > 0.f ? d[j] : 0.f;
+        a[j] += dz;
+        b[j] += dz * ((p[j] - be[j]) * rs[j]);
+      }
+      if (degen) {                                   // rare: gather x at the argmax
+        const uint32_t p32 = (uint32_t)pt;
+        const int ow = (int)(p32 % (uint32_t)g.Wo);
+        const uint32_t q = p32 / (uint32_t)g.Wo;
+        const int oh = (int)(q % (uint32_t)g.Ho), n = (int)(q / (uint32_t)g.Ho);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (sc[j] != 0.f || !(p[j] > 0.f)) continue;
+          const int slot = idx[o + j];
+          const int ih = oh * g.s - g.p + slot / g.k, iw = ow * g.s - g.p + slot % g.k;
+          const float xv = __uint_as_float((uint32_t)x[(((int64_t)n * g.H + ih) * g.W + iw) * g.C +
+                                                       cg * 8 + j] << 16);
+          b[j] += d[j] * (xv - mu[j]);
+        }
+      }
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { sa[r * g.C + cg * 8 + j] = a[j]; sb[r * g.C + cg * 8 + j] = b[j]; }
+  }
+  __syncthreads();
+  const int64_t nb = gridDim.x;
+  for (int c = threadIdx.x; c < g.C; c += BNT) {
+    float s1 = 0.f, s2 = 0.f;
+    for (int qq = 0; qq < R; ++qq) { s1 += sa[qq * g.C + c]; s2 += sb[qq * g.C + c]; }
+    partial[(int64_t)c * nb + blockIdx.x] = s1;
+    partial[((int64_t)g.C + c) * nb + blockIdx.x] = s2;
+  }
+}
+
 void stem_pool_fwd(const StemArgs& a, hipStream_t st) {
   const PoolGeom g{a.N, a.H, a.W, a.C, a.Ho, a.Wo, a.k, a.s, a.p};
   const int64_t total = (int64_t)a.N * a.Ho * a.Wo * (a.C / 8);
@@ -1158,29 +1237,41 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
   reduce_geometry(M, a.C, rpb, nb);
   const auto* dp = static_cast<const uint16_t*>(a.dp);
   const auto* x = static_cast<const uint16_t*>(a.x);
-  if (a.k == 3 && a.s == 2 && a.p == 1 && a.H == 2 * a.Ho && a.W == 2 * a.Wo) {
-    // 2x2-block form over the output grid (same partial layout: nb blocks of the grid points)
-    const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
-    int64_t rpb2;
-    int nb2;
-    reduce_geometry(P, a.C, rpb2, nb2);
-    hipLaunchKernelGGL((k_stem_pool_bwd_s2<0>), dim3(nb2), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
-                       a.shift, a.mean, (const float*)nullptr, (const float*)nullptr,
-                       (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb2);
+  const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
+  int64_t rpb2;
+  int nb2;
+  reduce_geometry(P, a.C, rpb2, nb2);
+  if (a.pooled) {   // statistics from the pooled side (any geometry); partials over nb2 blocks
+    hipLaunchKernelGGL(k_stem_pool_reduce_out, dim3(nb2), dim3(BNT), 0, st, dp,
+                       static_cast<const uint16_t*>(a.pooled), a.idx, x, a.scale, a.shift, a.mean,
+                       a.partial, g, rpb2);
     hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb2,
                        a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
                        (int)a.accum_dparams);
+  }
+  if (a.k == 3 && a.s == 2 && a.p == 1 && a.H == 2 * a.Ho && a.W == 2 * a.Wo) {
+    // 2x2-block form over the output grid (same partial layout: nb blocks of the grid points)
+    if (!a.pooled) {
+      hipLaunchKernelGGL((k_stem_pool_bwd_s2<0>), dim3(nb2), dim3(BNT), 0, st, dp, a.idx, x,
+                         a.scale, a.shift, a.mean, (const float*)nullptr, (const float*)nullptr,
+                         (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb2);
+      hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial,
+                         nb2, a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
+                         1, (int)a.accum_dparams);
+    }
     hipLaunchKernelGGL((k_stem_pool_bwd_s2<1>), dim3(nb2), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                        a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
                        (float*)nullptr, g, rpb2);
     return;
   }
-  hipLaunchKernelGGL((k_stem_pool_bwd<0>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
-                     a.shift, a.mean, (const float*)nullptr, (const float*)nullptr,
-                     (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb);
-  hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
-                     a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
-                     (int)a.accum_dparams);
+  if (!a.pooled) {
+    hipLaunchKernelGGL((k_stem_pool_bwd<0>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
+                       a.shift, a.mean, (const float*)nullptr, (const float*)nullptr,
+                       (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb);
+    hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
+                       a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
+                       (int)a.accum_dparams);
+  }
   hipLaunchKernelGGL((k_stem_pool_bwd<1>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                      a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
                      (float*)nullptr, g, rpb);

@@ -218,51 +218,77 @@ namespace lw {
 // The k order (r, tap, channel) and the 32-wide MFMA steps are those of the GEMM path's packed
 // weight (pack_fwd_weight), so the outputs are bit-identical to it. Epilogue: bf16 NHWC store and
 // one column-statistics row (Σv, Σv² of the stored values) per workgroup.
-constexpr int STEM_SY = 4;                 // output rows per workgroup
+// A workgroup walks `tpw` consecutive row tiles: the packed weight is staged once, and the next
+// tile's patch is loaded into registers (all its loads in flight at once) while the MFMAs of the
+// current tile run, so the staging latency is paid once per workgroup instead of once per tile
+// (the one-tile-per-workgroup form waited on ~11 serial global round trips per tile).
+constexpr int STEM_SY = 4;                 // output rows per tile
 constexpr int STEM_CO = 64;
 constexpr int STEM_K = 224;                // 7 rows x 8 taps (7 + 1 zero) x 4 channels
 constexpr int STEM_WLD = STEM_K + 8;       // padded LDS weight row (bank spread)
 constexpr int STEM_WAVES = 7;              // 448 threads: 28 pixel blocks of 16 = 4 per wave
 constexpr int STEM_T = STEM_WAVES * 64;
+constexpr int STEM_WOMAX = 112;            // widest output row (224 px images)
+constexpr int STEM_PW = 2 * STEM_WOMAX + 6;  // patch row pitch (pixels): a compile-time stride, so
+                                           // every patch read is one base + immediate offset
+constexpr int STEM_PR = 2 * STEM_SY + 5;   // patch rows
+constexpr int STEM_PMAX = (STEM_PR * STEM_PW + STEM_T - 1) / STEM_T;   // patch pixels per thread
 
-__global__ __launch_bounds__(STEM_T) void k_stem_conv7(const uint16_t* __restrict__ x,
+// OCC: waves per SIMD the register allocation targets (4 = two workgroups per CU at 128 VGPRs,
+// a few spills; 3 = no spills, one workgroup per CU)
+template <int OCC>
+__global__ __launch_bounds__(STEM_T) __attribute__((amdgpu_waves_per_eu(OCC))) void k_stem_conv7(const uint16_t* __restrict__ x,
                                                     const uint16_t* __restrict__ w,
                                                     uint16_t* __restrict__ y,
                                                     float* __restrict__ stats, int H, int W,
-                                                    int Ho, int Wo) {
+                                                    int Ho, int Wo, int tiles, int tpw) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int PW = 2 * Wo + 6;                       // patch columns (pixels), even
-  const int PR = 2 * STEM_SY + 5;                  // patch rows
+  constexpr int PW = STEM_PW, PR = STEM_PR;       // columns past 2 * Wo + 6 are never read
   uint16_t* patch = reinterpret_cast<uint16_t*>(smem);               // [PR][PW][4]
   uint16_t* ws = patch + PR * PW * 4;                                 // [64][STEM_WLD]
   float* red = reinterpret_cast<float*>(ws + STEM_CO * STEM_WLD);     // [waves][2][64]
   const int tiles_y = Ho / STEM_SY;
-  const int img = blockIdx.x / tiles_y, y0 = (blockIdx.x - img * tiles_y) * STEM_SY;
-  // ---- stage the patch (8-byte pixels; rows / columns outside the image are zeros) and weights
-  const int64_t img_off = (int64_t)img * H * W * 4;
-  for (int e = threadIdx.x; e < PR * PW; e += STEM_T) {
-    const int pr = e / PW, pc = e - pr * PW;
-    const int hi = 2 * y0 - 3 + pr, wi = pc - 3;
-    uint2 v = make_uint2(0u, 0u);
-    if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
-      v = *reinterpret_cast<const uint2*>(x + img_off + ((int64_t)hi * W + wi) * 4);
-    *reinterpret_cast<uint2*>(patch + e * 4) = v;
+  const int t0 = blockIdx.x * tpw, t1 = min(t0 + tpw, tiles);
+  // this thread's patch pixels e = tid + i * STEM_T, walked as (row, column) with a carry (kept
+  // out of registers across the tile loop)
+  const int prow0 = threadIdx.x / PW, pcol0 = threadIdx.x - prow0 * PW;
+  const int dq = STEM_T / PW, dr = STEM_T - dq * PW;
+  uint2 pv[STEM_PMAX];
+  auto load_patch = [&](int t) {                   // 8-byte pixels; outside the image: zeros
+    const int img = t / tiles_y, y0 = (t - img * tiles_y) * STEM_SY;
+    const uint16_t* xi = x + (int64_t)img * H * W * 4;
+    int pr = prow0, pc = pcol0;
+#pragma unroll
+    for (int i = 0; i < STEM_PMAX; ++i) {
+      const int hi = 2 * y0 - 3 + pr, wi = pc - 3;
+      pv[i] = make_uint2(0u, 0u);
+      if (pr < PR && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
+        pv[i] = *reinterpret_cast<const uint2*>(xi + ((int64_t)hi * W + wi) * 4);
+      pc += dr; pr += dq;
+      if (pc >= PW) { pc -= PW; ++pr; }
+    }
+  };
+  {
+    constexpr int WPT = STEM_CO * (STEM_K / 8) / STEM_T;      // 4 uint4 per thread
+    static_assert(STEM_CO * (STEM_K / 8) == WPT * STEM_T, "weight staging");
+    uint4 wv[WPT];
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int e = threadIdx.x + i * STEM_T;
+      const int co = e / (STEM_K / 8), kc = e - co * (STEM_K / 8);
+      wv[i] = *reinterpret_cast<const uint4*>(w + co * STEM_K + kc * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int e = threadIdx.x + i * STEM_T;
+      const int co = e / (STEM_K / 8), kc = e - co * (STEM_K / 8);
+      *reinterpret_cast<uint4*>(ws + co * STEM_WLD + kc * 8) = wv[i];
+    }
   }
-  for (int e = threadIdx.x; e < STEM_CO * (STEM_K / 8); e += STEM_T) {
-    const int co = e / (STEM_K / 8), kc = e - co * (STEM_K / 8);
-    *reinterpret_cast<uint4*>(ws + co * STEM_WLD + kc * 8) =
-        *reinterpret_cast<const uint4*>(w + co * STEM_K + kc * 8);
-  }
-  __syncthreads();
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, lr = l & 15;
   const int npix = STEM_SY * Wo;                   // STEM_WAVES * 16 * RB (host)
   const int RB = npix / (STEM_WAVES * 16);         // 16-row blocks per wave
   constexpr int MAXRB = 4;
-  f32x4 acc[MAXRB][4];
-#pragma unroll
-  for (int i = 0; i < MAXRB; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // this lane's pixel of row block i: wave wv takes blocks wv, wv + STEM_WAVES, ...
   int poff[MAXRB];
 #pragma unroll
@@ -271,75 +297,85 @@ __global__ __launch_bounds__(STEM_T) void k_stem_conv7(const uint16_t* __restric
     const int yy = p / Wo, xx = p - yy * Wo;
     poff[i] = ((2 * yy) * PW + 2 * xx + 2 * g) * 4;   // element offset at filter row 0
   }
-  for (int r = 0; r < 7; ++r) {
-    bf16x8 fb[4];
+  // column statistics: each wave folds its tile sums into its own [2][64] LDS row (no races)
+  for (int c = l; c < 2 * STEM_CO; c += 64) red[wv * 2 * STEM_CO + c] = 0.f;
+  for (int t = t0; t < t1; ++t) {
+    load_patch(t);                                 // all loads in flight at once
+    __syncthreads();                               // the previous tile's patch reads are done
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      fb[j] = *reinterpret_cast<const bf16x8*>(ws + (j * 16 + lr) * STEM_WLD + r * 32 + g * 8);
+    for (int i = 0; i < STEM_PMAX; ++i) {
+      const int e = threadIdx.x + i * STEM_T;
+      if (e < PR * PW) *reinterpret_cast<uint2*>(patch + e * 4) = pv[i];
+    }
+    __syncthreads();
+    f32x4 acc[MAXRB][4];
 #pragma unroll
-    for (int i = 0; i < MAXRB; ++i) {
-      if (i < RB) {
-        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(patch + poff[i] + r * PW * 4);
+    for (int i = 0; i < MAXRB; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa, acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 7; ++r) {
+      bf16x8 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(ws + (j * 16 + lr) * STEM_WLD + r * 32 + g * 8);
+#pragma unroll
+      for (int i = 0; i < MAXRB; ++i) {
+        if (i < RB) {
+          const bf16x8 fa = *reinterpret_cast<const bf16x8*>(patch + poff[i] + r * PW * 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa, acc[i][j], 0, 0, 0);
+        }
       }
     }
-  }
-  // ---- epilogue: lane holds C[pixel (l & 15)][channel 4 * (l >> 4) + q] of each 16x16 block
-  float s1[4][4], s2[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) { s1[j][q] = 0.f; s2[j][q] = 0.f; }
-  const int64_t out_base = ((int64_t)img * Ho + y0) * Wo;         // first pixel of the tile
-#pragma unroll
-  for (int i = 0; i < MAXRB; ++i) {
-    if (i >= RB) continue;
-    const int p = (wv + STEM_WAVES * i) * 16 + lr;
+    // ---- epilogue: lane holds C[pixel (l & 15)][channel 4 * (l >> 4) + q] of each 16x16 block
+    const int img = t / tiles_y, y0 = (t - img * tiles_y) * STEM_SY;
+    const int64_t out_base = ((int64_t)img * Ho + y0) * Wo;       // first pixel of the tile
+    // channel block j at a time (its 4 statistics pairs only live across the row blocks)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      uint16_t h[4];
+      float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < MAXRB; ++i) {
+        if (i >= RB) continue;
+        const int p = (wv + STEM_WAVES * i) * 16 + lr;
+        uint16_t h[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          h[q] = bf16_rne(acc[i][j][q]);
+          const float v = __uint_as_float((uint32_t)h[q] << 16);
+          s1[q] += v;
+          s2[q] += v * v;
+        }
+        *reinterpret_cast<uint2*>(y + (out_base + p) * STEM_CO + j * 16 + 4 * g) =
+            make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        h[q] = bf16_rne(acc[i][j][q]);
-        const float v = __uint_as_float((uint32_t)h[q] << 16);
-        s1[j][q] += v;
-        s2[j][q] += v * v;
+        s1[q] = sum16(s1[q]);
+        s2[q] = sum16(s2[q]);
       }
-      *reinterpret_cast<uint2*>(y + (out_base + p) * STEM_CO + j * 16 + 4 * g) =
-          make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
-    }
-  }
+      if (lr == 0) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      s1[j][q] = sum16(s1[j][q]);
-      s2[j][q] = sum16(s2[j][q]);
-    }
-  if (lr == 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        red[(wv * 2 + 0) * STEM_CO + j * 16 + 4 * g + q] = s1[j][q];
-        red[(wv * 2 + 1) * STEM_CO + j * 16 + 4 * g + q] = s2[j][q];
+        for (int q = 0; q < 4; ++q) {
+          red[(wv * 2 + 0) * STEM_CO + j * 16 + 4 * g + q] += s1[q];
+          red[(wv * 2 + 1) * STEM_CO + j * 16 + 4 * g + q] += s2[q];
+        }
       }
+    }
   }
   __syncthreads();
   if (threadIdx.x < 2 * STEM_CO) {
     const int sidx = threadIdx.x / STEM_CO, c = threadIdx.x - sidx * STEM_CO;
-    float t = 0.f;
+    float tsum = 0.f;
 #pragma unroll
-    for (int q = 0; q < STEM_WAVES; ++q) t += red[(q * 2 + sidx) * STEM_CO + c];   // fixed order
-    stats[((int64_t)blockIdx.x * 2 + sidx) * STEM_CO + c] = t;
+    for (int q = 0; q < STEM_WAVES; ++q) tsum += red[(q * 2 + sidx) * STEM_CO + c];   // fixed order
+    stats[((int64_t)blockIdx.x * 2 + sidx) * STEM_CO + c] = tsum;
   }
 }
 
-int stem_conv7_smem(int Wo) {
-  const int PW = 2 * Wo + 6, PR = 2 * STEM_SY + 5;
-  return PR * PW * 4 * 2 + STEM_CO * STEM_WLD * 2 + STEM_WAVES * 2 * STEM_CO * 4;
+int stem_conv7_smem(int) {
+  return STEM_PR * STEM_PW * 4 * 2 + STEM_CO * STEM_WLD * 2 + STEM_WAVES * 2 * STEM_CO * 4;
 }
 
 bool stem_conv7_ok(int C, int Co, int R, int S, int sh, int sw, int ph, int pw, int H, int W,
@@ -347,14 +383,42 @@ bool stem_conv7_ok(int C, int Co, int R, int S, int sh, int sw, int ph, int pw, 
   return C == 4 && Co == STEM_CO && R == 7 && S == 7 && sh == 2 && sw == 2 && ph == 3 && pw == 3 &&
          Ho == (H + 6 - 7) / 2 + 1 && Wo == (W + 6 - 7) / 2 + 1 && Ho % STEM_SY == 0 &&
          (STEM_SY * Wo) % (STEM_WAVES * 16) == 0 && STEM_SY * Wo / (STEM_WAVES * 16) <= 4 &&
-         stem_conv7_smem(Wo) <= 64 * 1024;
+         Wo <= STEM_WOMAX && stem_conv7_smem(Wo) <= 64 * 1024;
+}
+
+// tiles per workgroup: enough workgroups for two resident per CU (the LDS footprint allows two),
+// LWAAAI_STEM_TPW overrides (1 = one tile per workgroup)
+static int stem_tpw(int tiles) {
+  static const int env = [] {
+    const char* e = getenv("LWAAAI_STEM_TPW");
+    return e ? atoi(e) : 0;
+  }();
+  if (env > 0) return env;
+  const int slots = 2 * cu_count();
+  return std::max(1, (tiles + slots - 1) / slots);
+}
+
+int stem_conv7_blocks(int N, int Ho) {
+  const int tiles = N * (Ho / STEM_SY);
+  const int tpw = stem_tpw(tiles);
+  return (tiles + tpw - 1) / tpw;
 }
 
 void stem_conv7(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
                 int W, int Ho, int Wo, hipStream_t st) {
-  const int blocks = N * (Ho / STEM_SY);
-  hipLaunchKernelGGL(k_stem_conv7, dim3(blocks), dim3(STEM_T), stem_conv7_smem(Wo), st, x, w, y, stats,
-                     H, W, Ho, Wo);
+  const int tiles = N * (Ho / STEM_SY);
+  const int tpw = stem_tpw(tiles);
+  const int blocks = (tiles + tpw - 1) / tpw;
+  static const bool occ3 = [] {
+    const char* e = getenv("LWAAAI_STEM_OCC");
+    return e && atoi(e) == 3;
+  }();
+  if (occ3)
+    hipLaunchKernelGGL(k_stem_conv7<3>, dim3(blocks), dim3(STEM_T), stem_conv7_smem(Wo), st, x, w, y,
+                       stats, H, W, Ho, Wo, tiles, tpw);
+  else
+    hipLaunchKernelGGL(k_stem_conv7<4>, dim3(blocks), dim3(STEM_T), stem_conv7_smem(Wo), st, x, w, y,
+                       stats, H, W, Ho, Wo, tiles, tpw);
 }
 
 }  // namespace lw

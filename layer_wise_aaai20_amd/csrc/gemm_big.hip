@@ -764,7 +764,7 @@ bool gemm_bigp_ok(const GemmArgs& g) {
   return true;
 }
 
-static int cu_count() {
+int cu_count() {
   int dev = 0, n = 0;
   (void)hipGetDevice(&dev);
   static int cached[64] = {0};

@@ -176,6 +176,7 @@ struct StemArgs {
   float* A;
   float* B;
   float* Cc;
+  const void* pooled;     // backward: the forward's pooled map (statistics from the pooled side)
   int N, H, W, C, Ho, Wo, k, s, p;
   bool accum_dparams;
 };
@@ -269,6 +270,8 @@ bool conv_tile_ok(int mode, int tile);
 bool conv_big_ok(const GemmArgs& g, const ConvGeomHost& h);
 // direct 7x7/2 stem convolution from an LDS patch (conv.hip): 4-channel NHWC image, the packed
 // [64][7*8*4] weight, bf16 NHWC output + one column-statistics row per 4 output rows
+int cu_count();                       // compute units of the current device (cached)
+int stem_conv7_blocks(int N, int Ho);  // workgroups (= statistics rows) of stem_conv7
 bool stem_conv7_ok(int C, int Co, int R, int S, int sh, int sw, int ph, int pw, int H, int W,
                    int Ho, int Wo);
 void stem_conv7(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,

@@ -5,6 +5,8 @@ without changing a single parameter / buffer name (checkpoints stay compatible).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -196,6 +198,12 @@ def _fused_basic_forward(self, x):
     return self.bn2(self.conv2(out), identity)
 
 
+# The stem backward's BN statistics pass reads the pooled gradient and the pooled map (saved from
+# the forward) instead of the 112x112 conv output and the slot bytes (csrc/bn.hip
+# k_stem_pool_reduce_out); LWAAAI_STEM_POOLED=0 keeps the full-resolution reduce
+STEM_POOLED = os.environ.get("LWAAAI_STEM_POOLED", "1") != "0"
+
+
 class _StemPoolFn(torch.autograd.Function):
     """conv1 output → BN (batch stats) → ReLU → max-pool as one forward kernel after the stats
     pass, and one reduce + one apply kernel backward (``csrc/bn.hip`` k_stem_pool_*)."""
@@ -209,7 +217,7 @@ class _StemPoolFn(torch.autograd.Function):
         mean, invstd, ss = lib.bn_stats(c, None, weight, bias, bn.running_mean, bn.running_var,
                                         block._bn_momentum(bn), bn.eps)
         out, idx = lib.stem_pool_fwd(c, ss, *geom)
-        ctx.save_for_backward(c, idx, ss, weight, mean, invstd)
+        ctx.save_for_backward(c, idx, ss, weight, mean, invstd, out if STEM_POOLED else None)
         ctx.geom = geom
         ctx.params = (weight, bias)
         return out
@@ -217,12 +225,12 @@ class _StemPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         from . import block
-        c, idx, ss, weight, mean, invstd = ctx.saved_tensors
+        c, idx, ss, weight, mean, invstd, pooled = ctx.saved_tensors
         w, b = ctx.params
         dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         outs = block._bn_grad_outs(w, b)
         dc, dg, db = load().stem_pool_bwd(dout, idx, c, ss, weight, mean, invstd, *ctx.geom,
-                                          outs[0], outs[1])
+                                          outs[0], outs[1], pooled)
         gw, gb = block._finish_bn(w, b, dg, db, outs)
         return dc, gw, gb, None, None
 
@@ -243,7 +251,7 @@ class _StemConvPoolFn(torch.autograd.Function):
         mean, invstd, ss = lib.bn_stats(c, st, gamma, beta, bn.running_mean, bn.running_var,
                                         block._bn_momentum(bn), bn.eps)
         out, idx = lib.stem_pool_fwd(c, ss, *geom)
-        ctx.save_for_backward(x, c, idx, ss, gamma, mean, invstd)
+        ctx.save_for_backward(x, c, idx, ss, gamma, mean, invstd, out if STEM_POOLED else None)
         ctx.geom = geom
         ctx.conv = (tuple(conv.stride), tuple(conv.padding))
         ctx.params = (w, gamma, beta)
@@ -253,12 +261,12 @@ class _StemConvPoolFn(torch.autograd.Function):
     def backward(ctx, dout):
         from . import block
         from .conv import conv_dgrad, conv_wgrad
-        x, c, idx, ss, gamma, mean, invstd = ctx.saved_tensors
+        x, c, idx, ss, gamma, mean, invstd, pooled = ctx.saved_tensors
         w, g, b = ctx.params
         dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         outs = block._bn_grad_outs(g, b)
         dc, dg, db = load().stem_pool_bwd(dout, idx, c, ss, gamma, mean, invstd, *ctx.geom,
-                                          outs[0], outs[1])
+                                          outs[0], outs[1], pooled)
         gg, gb = block._finish_bn(g, b, dg, db, outs)
         stride, padding = ctx.conv
         dx = None

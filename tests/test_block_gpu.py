@@ -137,15 +137,23 @@ def test_resnet50_block_vs_layer_path():
     assert errs["block"][-1] < 0.05            # fc.bias: only the softmax output enters
 
 
+@pytest.mark.parametrize("pooled", [True, False])
 @pytest.mark.parametrize("shape", [(4, 64, 32, 32), (2, 64, 15, 17), (2, 64, 112, 112), (3, 128, 28, 28)])
-def test_stem_bn_relu_pool_matches_layers(shape):
-    """Fused BN+ReLU+max-pool stem vs FusedBatchNorm2d(relu) + nn.MaxPool2d."""
+def test_stem_bn_relu_pool_matches_layers(shape, pooled, monkeypatch, zero_gamma=False):
+    """Fused BN+ReLU+max-pool stem vs FusedBatchNorm2d(relu) + nn.MaxPool2d, with the backward's
+    statistics taken from the pooled side (csrc/bn.hip k_stem_pool_reduce_out) or from the
+    full-resolution conv output."""
+    from layer_wise_aaai20_amd.ops import nn as NN
     from layer_wise_aaai20_amd.ops.nn import stem_bn_relu_pool, to_fused_bn
+    monkeypatch.setattr(NN, "STEM_POOLED", pooled)
     torch.manual_seed(3)
     C = shape[1]
     bn_a = torch.nn.BatchNorm2d(C).cuda()
     bn_a.weight.data.uniform_(-1.0, 1.5)          # negative gammas too
     bn_a.bias.data.normal_(0, 0.3)
+    if zero_gamma:                                # scale 0: x is not recoverable from the pooled map
+        bn_a.weight.data[::5] = 0.0
+        bn_a.bias.data[::5] = bn_a.bias.data[::5].abs() + 0.1
     bn_b = copy.deepcopy(bn_a)
     to_fused_bn(bn_b, relu=True)
     pool = torch.nn.MaxPool2d(3, 2, 1)
@@ -162,6 +170,13 @@ def test_stem_bn_relu_pool_matches_layers(shape):
     assert _rel(bn_a.bias.grad, bn_b.bias.grad) < 2e-2
     torch.testing.assert_close(bn_a.running_mean, bn_b.running_mean, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(bn_a.running_var, bn_b.running_var, rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 32, 32), (2, 64, 15, 17)])
+def test_stem_pool_backward_zero_gamma(shape, monkeypatch):
+    """Channels with gamma == 0 (pooled map constant): the pooled-side statistics pass gathers x
+    at the argmax for them instead of inverting the affine."""
+    test_stem_bn_relu_pool_matches_layers(shape, True, monkeypatch, zero_gamma=True)
 
 
 def test_backward_stats_epilogues_match_reduce_pass(monkeypatch):

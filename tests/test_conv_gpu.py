@@ -315,11 +315,13 @@ def test_conv_big_tiles_are_tuner_candidates(monkeypatch):
     assert all(c[1] not in (21, 22) for c in seen["d"])
 
 
-@pytest.mark.parametrize("N,H", [(2, 224), (3, 112)])
+@pytest.mark.parametrize("N,H", [(2, 224), (3, 112), (40, 224)])
 def test_stem_direct_conv_matches_gemm_path(N, H, monkeypatch):
     """The direct 7x7/2 stem convolution from an LDS patch (csrc/conv.hip k_stem_conv7) is
     bit-identical to the implicit-GEMM 4-channel path (same k order, 32-wide MFMA steps) and its
-    statistics rows (one per 4 output rows) fold to the column sums of the stored output."""
+    statistics rows (one per workgroup) fold to the column sums of the stored output. N = 40 at
+    224 px gives more row tiles than two per CU, so workgroups walk several tiles (the last one a
+    partial run)."""
     x, w = _inputs(N, 3, 64, H, 7, 9)
     ref = F.conv2d(x.float(), w.float(), stride=2, padding=3)
     outs = {}

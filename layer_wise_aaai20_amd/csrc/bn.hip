@@ -1150,31 +1150,48 @@ __global__ __launch_bounds__(BNT) void k_stem_pool_reduce_out(const uint16_t* __
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(r0 + rows_per_block, P);
+  constexpr int U = 4;                                // rows per iteration, loads all in flight
   if (active) {
-    for (int64_t pt = r0 + r; pt < r1; pt += R) {
-      const int64_t o = pt * g.C + cg * 8;
-      float d[8], p[8];
-      V8<uint16_t>::load(dp + o, d);
-      V8<uint16_t>::load(pooled + o, p);
+    for (int64_t pt0 = r0 + r; pt0 < r1; pt0 += U * R) {
+      float d[U][8], p[U][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float dz = p[j] > 0.f ? d[j] : 0.f;
-        a[j] += dz;
-        b[j] += dz * ((p[j] - be[j]) * rs[j]);
+      for (int u = 0; u < U; ++u) {
+        const int64_t pt = pt0 + u * R;
+        if (pt < r1) {
+          V8<uint16_t>::load(dp + pt * g.C + cg * 8, d[u]);
+          V8<uint16_t>::load(pooled + pt * g.C + cg * 8, p[u]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { d[u][j] = 0.f; p[u][j] = 0.f; }
+        }
       }
-      if (degen) {                                   // rare: gather x at the argmax
-        const uint32_t p32 = (uint32_t)pt;
-        const int ow = (int)(p32 % (uint32_t)g.Wo);
-        const uint32_t q = p32 / (uint32_t)g.Wo;
-        const int oh = (int)(q % (uint32_t)g.Ho), n = (int)(q / (uint32_t)g.Ho);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          if (sc[j] != 0.f || !(p[j] > 0.f)) continue;
-          const int slot = idx[o + j];
-          const int ih = oh * g.s - g.p + slot / g.k, iw = ow * g.s - g.p + slot % g.k;
-          const float xv = __uint_as_float((uint32_t)x[(((int64_t)n * g.H + ih) * g.W + iw) * g.C +
-                                                       cg * 8 + j] << 16);
-          b[j] += d[j] * (xv - mu[j]);
+          const float dz = p[u][j] > 0.f ? d[u][j] : 0.f;
+          a[j] += dz;
+          b[j] += dz * ((p[u][j] - be[j]) * rs[j]);
+        }
+      if (degen) {                                   // rare: gather x at the argmax
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t pt = pt0 + u * R;
+          if (pt >= r1) continue;
+          const int64_t o = pt * g.C + cg * 8;
+          const uint32_t p32 = (uint32_t)pt;
+          const int ow = (int)(p32 % (uint32_t)g.Wo);
+          const uint32_t q = p32 / (uint32_t)g.Wo;
+          const int oh = (int)(q % (uint32_t)g.Ho), n = (int)(q / (uint32_t)g.Ho);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if (sc[j] != 0.f || !(p[u][j] > 0.f)) continue;
+            const int slot = idx[o + j];
+            const int ih = oh * g.s - g.p + slot / g.k, iw = ow * g.s - g.p + slot % g.k;
+            const float xv = __uint_as_float(
+                (uint32_t)x[(((int64_t)n * g.H + ih) * g.W + iw) * g.C + cg * 8 + j] << 16);
+            b[j] += d[u][j] * (xv - mu[j]);
+          }
         }
       }
     }
@@ -1201,6 +1218,13 @@ void stem_pool_fwd(const StemArgs& a, hipStream_t st) {
                      static_cast<uint16_t*>(a.out), a.idx, g);
 }
 
+// Apply passes: the reduce geometry (~512 blocks walking ~50 rows each). One row per thread
+// (a grid of ~25k blocks) measured slower: stem pool backward +50 us, CIFAR ResNet-9 -15 %
+// (profiles/r3s2/stem_ab.txt).
+static void pool_apply_geometry(int64_t rows, int C, int64_t& rpb, int& nb) {
+  reduce_geometry(rows, C, rpb, nb);
+}
+
 // Max-pool of a post-ReLU map without a BatchNorm (VGG / AlexNet conv+ReLU -> MaxPool2d): the
 // forward is k_stem_pool_fwd with scale 1 / shift 0 (relu(v) == v there), the backward only the
 // apply pass with (A, B, C) = (1, 0, 0): dx = the routed pooled gradient masked by [x > 0], i.e.
@@ -1214,7 +1238,7 @@ void relu_pool_bwd(const StemArgs& a, hipStream_t st) {
     const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
     int64_t rpb;
     int nb;
-    reduce_geometry(P, a.C, rpb, nb);
+    pool_apply_geometry(P, a.C, rpb, nb);
     hipLaunchKernelGGL((k_stem_pool_bwd_s2<1>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                        a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
                        (float*)nullptr, g, rpb);
@@ -1223,7 +1247,7 @@ void relu_pool_bwd(const StemArgs& a, hipStream_t st) {
   const int64_t M = (int64_t)a.N * a.H * a.W;
   int64_t rpb;
   int nb;
-  reduce_geometry(M, a.C, rpb, nb);
+  pool_apply_geometry(M, a.C, rpb, nb);
   hipLaunchKernelGGL((k_stem_pool_bwd<1>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                      a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
                      (float*)nullptr, g, rpb);
@@ -1259,9 +1283,12 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
                          nb2, a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
                          1, (int)a.accum_dparams);
     }
-    hipLaunchKernelGGL((k_stem_pool_bwd_s2<1>), dim3(nb2), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
+    int64_t rpa;
+    int nba;
+    pool_apply_geometry(P, a.C, rpa, nba);
+    hipLaunchKernelGGL((k_stem_pool_bwd_s2<1>), dim3(nba), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                        a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
-                       (float*)nullptr, g, rpb2);
+                       (float*)nullptr, g, rpa);
     return;
   }
   if (!a.pooled) {
@@ -1272,9 +1299,12 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
                        a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
                        (int)a.accum_dparams);
   }
-  hipLaunchKernelGGL((k_stem_pool_bwd<1>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
+  int64_t rpa;
+  int nba;
+  pool_apply_geometry(M, a.C, rpa, nba);
+  hipLaunchKernelGGL((k_stem_pool_bwd<1>), dim3(nba), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                      a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
-                     (float*)nullptr, g, rpb);
+                     (float*)nullptr, g, rpa);
 }
 
 }  // namespace lw

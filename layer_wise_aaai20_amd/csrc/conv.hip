@@ -235,8 +235,9 @@ constexpr int STEM_PR = 2 * STEM_SY + 5;   // patch rows
 constexpr int STEM_PMAX = (STEM_PR * STEM_PW + STEM_T - 1) / STEM_T;   // patch pixels per thread
 
 // OCC: waves per SIMD the register allocation targets (4 = two workgroups per CU at 128 VGPRs,
-// a few spills; 3 = no spills, one workgroup per CU)
-template <int OCC>
+// a few spills; 3 = no spills, one workgroup per CU). PF: the next tile's patch loads are issued
+// before this tile's MFMAs (held in registers across them) instead of at the top of each tile.
+template <int OCC, bool PF>
 __global__ __launch_bounds__(STEM_T) __attribute__((amdgpu_waves_per_eu(OCC))) void k_stem_conv7(const uint16_t* __restrict__ x,
                                                     const uint16_t* __restrict__ w,
                                                     uint16_t* __restrict__ y,
@@ -299,8 +300,9 @@ __global__ __launch_bounds__(STEM_T) __attribute__((amdgpu_waves_per_eu(OCC))) v
   }
   // column statistics: each wave folds its tile sums into its own [2][64] LDS row (no races)
   for (int c = l; c < 2 * STEM_CO; c += 64) red[wv * 2 * STEM_CO + c] = 0.f;
+  if (PF && t0 < t1) load_patch(t0);
   for (int t = t0; t < t1; ++t) {
-    load_patch(t);                                 // all loads in flight at once
+    if (!PF) load_patch(t);                        // all loads in flight at once
     __syncthreads();                               // the previous tile's patch reads are done
 #pragma unroll
     for (int i = 0; i < STEM_PMAX; ++i) {
@@ -308,6 +310,7 @@ __global__ __launch_bounds__(STEM_T) __attribute__((amdgpu_waves_per_eu(OCC))) v
       if (e < PR * PW) *reinterpret_cast<uint2*>(patch + e * 4) = pv[i];
     }
     __syncthreads();
+    if (PF && t + 1 < t1) load_patch(t + 1);       // in flight under this tile's MFMAs
     f32x4 acc[MAXRB][4];
 #pragma unroll
     for (int i = 0; i < MAXRB; ++i)
@@ -409,16 +412,22 @@ void stem_conv7(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats,
   const int tiles = N * (Ho / STEM_SY);
   const int tpw = stem_tpw(tiles);
   const int blocks = (tiles + tpw - 1) / tpw;
-  static const bool occ3 = [] {
-    const char* e = getenv("LWAAAI_STEM_OCC");
-    return e && atoi(e) == 3;
+  static const int var = [] {       // LWAAAI_STEM_OCC=3 / LWAAAI_STEM_PF=1 variants (A/B)
+    const char* o = getenv("LWAAAI_STEM_OCC");
+    const char* f = getenv("LWAAAI_STEM_PF");
+    return (o && atoi(o) == 3 ? 1 : 0) + (f && atoi(f) == 1 ? 2 : 0);
   }();
-  if (occ3)
-    hipLaunchKernelGGL(k_stem_conv7<3>, dim3(blocks), dim3(STEM_T), stem_conv7_smem(Wo), st, x, w, y,
-                       stats, H, W, Ho, Wo, tiles, tpw);
-  else
-    hipLaunchKernelGGL(k_stem_conv7<4>, dim3(blocks), dim3(STEM_T), stem_conv7_smem(Wo), st, x, w, y,
-                       stats, H, W, Ho, Wo, tiles, tpw);
+  const int smem = stem_conv7_smem(Wo);
+  switch (var) {
+    case 1: hipLaunchKernelGGL((k_stem_conv7<3, false>), dim3(blocks), dim3(STEM_T), smem, st, x, w, y,
+                               stats, H, W, Ho, Wo, tiles, tpw); break;
+    case 2: hipLaunchKernelGGL((k_stem_conv7<4, true>), dim3(blocks), dim3(STEM_T), smem, st, x, w, y,
+                               stats, H, W, Ho, Wo, tiles, tpw); break;
+    case 3: hipLaunchKernelGGL((k_stem_conv7<3, true>), dim3(blocks), dim3(STEM_T), smem, st, x, w, y,
+                               stats, H, W, Ho, Wo, tiles, tpw); break;
+    default: hipLaunchKernelGGL((k_stem_conv7<4, false>), dim3(blocks), dim3(STEM_T), smem, st, x, w,
+                                y, stats, H, W, Ho, Wo, tiles, tpw);
+  }
 }
 
 }  // namespace lw

@@ -412,7 +412,10 @@ void stem_conv7(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats,
   const int tiles = N * (Ho / STEM_SY);
   const int tpw = stem_tpw(tiles);
   const int blocks = (tiles + tpw - 1) / tpw;
-  static const int var = [] {       // LWAAAI_STEM_OCC=3 / LWAAAI_STEM_PF=1 variants (A/B)
+  // default: no prefetch at 4 waves/SIMD. LWAAAI_STEM_PF=1 LWAAAI_STEM_OCC=3 (prefetch at 3
+  // waves/SIMD) is faster in isolation (213 vs 251 us, bs 256, profiles/r3s2/stem_ab.txt) but its
+  // one bench run came in lower (11,060-11,126 img/s) and no same-box A/B ran yet: opt-in
+  static const int var = [] {
     const char* o = getenv("LWAAAI_STEM_OCC");
     const char* f = getenv("LWAAAI_STEM_PF");
     return (o && atoi(o) == 3 ? 1 : 0) + (f && atoi(f) == 1 ? 2 : 0);

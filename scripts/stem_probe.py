@@ -29,7 +29,8 @@ def timeit(fn, n=20):
 
 
 lib = load()
-tag = f"tpw={os.environ.get('LWAAAI_STEM_TPW', 'auto')} occ={os.environ.get('LWAAAI_STEM_OCC', '4')}"
+tag = (f"tpw={os.environ.get('LWAAAI_STEM_TPW', 'auto')} occ={os.environ.get('LWAAAI_STEM_OCC', '4')} "
+       f"pf={os.environ.get('LWAAAI_STEM_PF', '0')}")
 xs = torch.randn(256, 4, 224, 224, device=dev).bfloat16().contiguous(memory_format=CL)
 ws = torch.randn(64, 3, 7, 7, device=dev).bfloat16().contiguous(memory_format=CL)
 CV.TUNER.pick = lambda key, run, cands, default: CV.STEM_DIRECT

@@ -9,7 +9,17 @@ from layer_wise_aaai20_amd.models.graph import (SGD, Add, Concat, Correct, Flatt
 from layer_wise_aaai20_amd.utils.viz import cat, to_numpy  # noqa
 
 torch.backends.cudnn.benchmark = True   # MIOpen find mode on ROCm
-device = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
+def _rank_device() -> torch.device:
+    """This rank's GPU (``cuda:LOCAL_RANK``, else ``RANK % device_count``); the reference pins
+    every rank to ``cuda:0`` (``torch_backend.py:8``), which puts a one-node world on one GPU."""
+    if not torch.cuda.is_available():
+        return torch.device("cpu")
+    from layer_wise_aaai20_amd.parallel.comm import env_local_rank, env_rank, rank_device_index
+    return torch.device("cuda", rank_device_index(env_rank(), torch.cuda.device_count(),
+                                                  env_local_rank()))
+
+
+device = _rank_device()
 
 
 def warmup_cudnn(model, batch_size, dev=None):

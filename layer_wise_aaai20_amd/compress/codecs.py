@@ -326,11 +326,11 @@ class ThresholdCodec(TopkCodec):
 
     The number of hits is data-dependent, so the payload capacity is either:
 
-    * **fixed** (``max_density``, the default sparse wire): each segment carries at most
+    * **fixed** (``max_density``, opt-in ``wire="sparse-capped"``): each segment carries at most
       ``max(16, ceil(density · n))`` pairs. It is sync-free and graph-capturable. Hits beyond the
       capacity — the first in index order travel, strictly-above-threshold hits first — stay in
       the error-feedback residual and are counted on the device (``GradSyncEngine.read_overflow``).
-    * **agreed per step** (``max_density=None``, ``wire="sparse-exact"``): the ranks take an
+    * **agreed per step** (``max_density=None``, ``wire="sparse"`` / ``"sparse-exact"``): the ranks take an
       all-reduce(MAX) of the counts. This is exact for any density, but the capacity is read on
       the host in the middle of backward, so that step stays eager.
     """
@@ -715,11 +715,20 @@ def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qst
         else:
             c = RandkCodec(plan, world, rank, K, seed, error_feedback)
     elif method in ("Thresholdv", "AdaptiveThreshold") and (V or method == "AdaptiveThreshold"):
-        # sparse wire capacity: fixed (graph-capturable) unless "sparse-exact" asks for the
-        # per-step count exchange
-        dens = None if wire == "sparse-exact" else float(
-            max_density if max_density is not None else
-            os.environ.get("LWAAAI_THRESH_DENSITY", "0.05"))
+        # sparse wire capacity: agreed per step by the count exchange ("sparse" /
+        # "sparse-exact": exact, like the reference's |g| >= V), or fixed per segment
+        # ("sparse-capped": sync-free and graph-capturable, hits beyond the cap are counted and
+        # stay in the error-feedback residual — dropped without EF)
+        dens = None
+        if wire == "sparse-capped" or max_density is not None:
+            dens = float(max_density if max_density is not None else
+                         os.environ.get("LWAAAI_THRESH_DENSITY", "0.05"))
+            if not error_feedback and rank == 0:
+                import warnings
+                msg = (f"{method} on the capped sparse wire without error feedback: hits beyond "
+                       f"{dens:.1%} of a segment are dropped (counted in comm/overflow); use "
+                       f"wire='sparse' for the exact rule")
+                warnings.warn(msg, stacklevel=2)
         c = ThresholdCodec(plan, world, rank, V=V, adaptive=method == "AdaptiveThreshold",
                            seed=seed, error_feedback=error_feedback,
                            count_exchange=count_exchange, max_density=dens)

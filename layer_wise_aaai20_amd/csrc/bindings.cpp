@@ -92,13 +92,14 @@ const uint32_t* step_ptr(const c10::optional<Tensor>& t) {
   return reinterpret_cast<const uint32_t*>(t->data_ptr());
 }
 
-// optional device overflow counter (int32 scalar, incremented with atomics)
-unsigned int* overflow_ptr(const c10::optional<Tensor>& t) {
+// optional device overflow counter (int64 scalar, incremented with 64-bit atomics: a 32-bit
+// count of capped threshold hits wraps within a few hundred steps)
+unsigned long long* overflow_ptr(const c10::optional<Tensor>& t) {
   if (!t.has_value() || !t->defined()) return nullptr;
   check_cuda(*t, "overflow");
-  TORCH_CHECK(t->scalar_type() == at::kInt && t->numel() >= 1,
-              "overflow must be an int32 GPU tensor");
-  return reinterpret_cast<unsigned int*>(t->data_ptr());
+  TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() >= 1,
+              "overflow must be an int64 GPU tensor");
+  return reinterpret_cast<unsigned long long*>(t->data_ptr());
 }
 
 lw::SelectArgs make_select_args(const Tensor& g, const c10::optional<Tensor>& ef,

@@ -1119,8 +1119,11 @@ __global__ __launch_bounds__(BNT) void k_stem_pool_bwd_s2(const uint16_t* __rest
 //   Σdz = Σ_{p > 0} d   and   Σdz·(x - mean) = Σ_{p > 0} d·(p - beta) / scale,
 // beta = shift + mean·scale (linear in dz, so overlapping windows need no care). The pass reads
 // the pooled gradient and the pooled map (2 x N·Ho·Wo·C bf16) instead of the 4x larger conv output
-// plus the slot bytes. A channel with scale == 0 (p constant, x not recoverable) reads x at the
-// argmax through the slot byte instead. Partials as k_stem_pool_bwd<0>: [2][C][nb].
+// plus the slot bytes. A channel where that inversion is ill-conditioned reads x at the argmax
+// through the slot byte instead: scale == 0 (p constant, x not recoverable), or |beta| large
+// against |scale|·sigma = |gamma| — p's bf16 rounding (~2^-9·|beta|) would then become an error of
+// up to 2^-9·|beta/gamma| standard deviations in every recovered x - mean, a per-channel bias in
+// dgamma. Partials as k_stem_pool_bwd<0>: [2][C][nb].
 __global__ __launch_bounds__(BNT) void k_stem_pool_reduce_out(const uint16_t* __restrict__ dp,
                                                               const uint16_t* __restrict__ pooled,
                                                               const uint8_t* __restrict__ idx,
@@ -1128,6 +1131,7 @@ __global__ __launch_bounds__(BNT) void k_stem_pool_reduce_out(const uint16_t* __
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift,
                                                               const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
                                                               float* __restrict__ partial,
                                                               PoolGeom g, int64_t rows_per_block) {
   __shared__ float sa[BNT * 8];
@@ -1138,14 +1142,17 @@ __global__ __launch_bounds__(BNT) void k_stem_pool_reduce_out(const uint16_t* __
   const bool active = r < R;
   const int64_t P = (int64_t)g.N * g.Ho * g.Wo;
   float sc[8], rs[8], be[8], mu[8], a[8], b[8];
+  bool ill[8];
   bool degen = false;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = active ? cg * 8 + j : 0;
     sc[j] = scale[c]; mu[j] = mean[c];
     be[j] = fmaf(mu[j], sc[j], shift[c]);
-    rs[j] = sc[j] != 0.f ? 1.f / sc[j] : 0.f;
-    degen |= sc[j] == 0.f;
+    // |beta| > 8·|gamma| (gamma = scale / invstd): recover x - mean by gathering x instead
+    ill[j] = sc[j] == 0.f || fabsf(be[j]) * invstd[c] > 8.f * fabsf(sc[j]);
+    rs[j] = ill[j] ? 0.f : 1.f / sc[j];
+    degen |= ill[j];
     a[j] = 0.f; b[j] = 0.f;
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
@@ -1185,7 +1192,7 @@ __global__ __launch_bounds__(BNT) void k_stem_pool_reduce_out(const uint16_t* __
           const int oh = (int)(q % (uint32_t)g.Ho), n = (int)(q / (uint32_t)g.Ho);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            if (sc[j] != 0.f || !(p[u][j] > 0.f)) continue;
+            if (!ill[j] || !(p[u][j] > 0.f)) continue;
             const int slot = idx[o + j];
             const int ih = oh * g.s - g.p + slot / g.k, iw = ow * g.s - g.p + slot % g.k;
             const float xv = __uint_as_float(
@@ -1268,7 +1275,7 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
   if (a.pooled) {   // statistics from the pooled side (any geometry); partials over nb2 blocks
     hipLaunchKernelGGL(k_stem_pool_reduce_out, dim3(nb2), dim3(BNT), 0, st, dp,
                        static_cast<const uint16_t*>(a.pooled), a.idx, x, a.scale, a.shift, a.mean,
-                       a.partial, g, rpb2);
+                       a.invstd, a.partial, g, rpb2);
     hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb2,
                        a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
                        (int)a.accum_dparams);

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(NT) void k_small_select(
     const int64_t* __restrict__ cap_off, const int32_t* __restrict__ small_segs,
     int2* __restrict__ pairs, float* __restrict__ vals, int32_t* __restrict__ idx_out,
     SelState* __restrict__ st_small, uint32_t gid_base, uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp,
-    unsigned int* __restrict__ overflow) {
+    unsigned long long* __restrict__ overflow) {
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t h[2048];
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(NT) void k_small_select(
     st_small[blockIdx.x] = S;
     // ties the reference's `>=` rule keeps but the payload slack could not hold (left in EF)
     if (KM == KM_TOPK && overflow != nullptr && S.tkey != 0 && eq_total > S.quota)
-      atomicAdd(overflow, eq_total - S.quota);
+      atomicAdd(overflow, (unsigned long long)(eq_total - S.quota));
   }
 
   // order-preserving compaction: (gt, eq) counts packed in one word (<= 4096 each)
@@ -306,7 +306,7 @@ __global__ __launch_bounds__(NT) void k_select(const uint32_t* __restrict__ hist
                                                const int32_t* __restrict__ large_segs,
                                                const int32_t* __restrict__ keep,
                                                const int64_t* __restrict__ cap_off,
-                                               unsigned int* __restrict__ overflow) {
+                                               unsigned long long* __restrict__ overflow) {
   using C = PassCfg<PASS>;
   constexpr int NB = 1 << C::BITS;
   __shared__ uint32_t arr[NT];
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(NT) void k_select(const uint32_t* __restrict__ hist
       S.tkey = S.prefix;
       finish_state(S, KM, (uint32_t)keep[s], mn, h[d], (uint32_t)(cap_off[s + 1] - cap_off[s]));
       if (KM == KM_TOPK && overflow != nullptr && S.tkey != 0 && h[d] > S.quota)
-        atomicAdd(overflow, h[d] - S.quota);
+        atomicAdd(overflow, (unsigned long long)(h[d] - S.quota));
     }
     st[li] = S;
   }
@@ -450,7 +450,7 @@ __global__ __launch_bounds__(NT) void k_thresh_dense(float* __restrict__ g, floa
 // Per-segment capacity for the threshold path is only known after the count exchange.
 __global__ void k_set_caps(SelState* __restrict__ st, const int64_t* __restrict__ cap_off,
                            const int32_t* __restrict__ large_segs, int nseg,
-                           unsigned int* __restrict__ overflow) {
+                           unsigned long long* __restrict__ overflow) {
   const int li = blockIdx.x * blockDim.x + threadIdx.x;
   if (li >= nseg) return;
   const int s = large_segs[li];
@@ -460,7 +460,7 @@ __global__ void k_set_caps(SelState* __restrict__ st, const int64_t* __restrict_
     // a fixed-capacity sparse wire: the first `cap` hits (index order) travel, the rest stay in
     // the error-feedback residual (or are dropped without EF) and are counted; with capacities
     // from the count exchange this cannot happen (cap = max over ranks of total)
-    if (overflow != nullptr) atomicAdd(overflow, S.total - S.cap);
+    if (overflow != nullptr) atomicAdd(overflow, (unsigned long long)(S.total - S.cap));
     S.quota = S.cap > S.cnt_gt ? min(S.quota, S.cap - S.cnt_gt) : 0u;
     S.total = min(S.cnt_gt, S.cap) + S.quota;
   }

@@ -56,7 +56,7 @@ struct SelectArgs {
   const uint32_t* step_ptr;    // optional device step counter (overrides `step`; HIP graphs)
   // optional device counter: elements the reference rule would send that did not fit the
   // payload (Top-K ties beyond the tie slack; threshold hits beyond a fixed sparse capacity)
-  unsigned int* overflow;
+  unsigned long long* overflow;
 };
 
 struct QuantArgs {

@@ -5,27 +5,75 @@ time every candidate kernel (tile, or (tile, split-K)) the first time a problem 
 keep the fastest, as MIOpen's find mode does for the reference's cuDNN/MIOpen convolutions
 (``IMAGENET/training/train_imagenet_nv.py:36`` sets ``cudnn.benchmark``). Timing noise can make
 two processes pick different kernels for the same shape, and different kernels round differently.
-``LWAAAI_TUNE_FILE=path`` pins the choices:
+Three mechanisms make the choices reproducible and identical on every rank:
 
-* at import the table is read (JSON: ``{"<tuner>|<key repr>": choice}``) and every entry in it
-  is used instead of timing;
-* a new decision is added to the table and, on rank 0 (``RANK`` unset or 0), written back
-  atomically, so a second run — or every rank of a multi-process run pointed at a file tuned
-  beforehand — makes exactly the same choices.
+* **Shipped gfx950 table** (``ops/tune_gfx950.json``): the choices for the benchmark / recipe
+  shapes, measured on MI355X. It is read at import unless ``LWAAAI_TUNE_FILE`` names another
+  table (``LWAAAI_TUNE_FILE=none`` disables both), so two runs of ``bench.py`` pick the same
+  kernels and train bit-identically.
+* ``LWAAAI_TUNE_FILE=path``: that table is read at import and a new decision is added to it and,
+  on rank 0 (``RANK`` unset or 0), written back atomically.
+* **Cross-rank agreement**: inside :func:`rank_agreement` (the trainers wrap their eager
+  training steps in it, where every rank runs the same shapes in the same order) the candidate
+  times are summed over ranks with one all-reduce before the minimum is taken, so every rank
+  picks the same kernel and the step is not paced by one rank's unlucky choice.
+
+A pinned entry is used only if it is one of the current candidates (a table written with other
+kernel switches, or before a kernel was removed, is stale for that key): otherwise the shape is
+timed as usual and a warning names the stale entry.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
+import warnings
 from typing import Callable, Dict, Sequence
 
 import torch
 
+SHIPPED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tune_gfx950.json")
 _FILE = os.environ.get("LWAAAI_TUNE_FILE", "")
+if _FILE.lower() == "none":
+    _FILE, _READ = "", ""
+else:
+    _READ = _FILE or SHIPPED
 _TABLE: Dict[str, object] = {}
-if _FILE and os.path.exists(_FILE):
-    with open(_FILE) as f:
+if _READ and os.path.exists(_READ):
+    with open(_READ) as f:
         _TABLE = json.load(f)
+
+_AGREE: list = []          # stack of (process group, device) set by rank_agreement()
+
+
+@contextlib.contextmanager
+def rank_agreement(group=None, device=None):
+    """Within this context every new tuning decision is taken on the candidate times summed over
+    the ranks of ``group`` (one all-reduce per decision), so all ranks pick the same kernel. Use
+    it only where every rank reaches the same tuner calls in the same order (a training step)."""
+    import torch.distributed as dist
+    on = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    if on:
+        _AGREE.append((group, device))
+    try:
+        yield
+    finally:
+        if on:
+            _AGREE.pop()
+
+
+def _agree_times(times):
+    if not _AGREE:
+        return times
+    import torch.distributed as dist
+    group, device = _AGREE[-1]
+    dev = torch.device("cpu")
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device(device) if device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([x for x, _ in times], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, group=group)
+    return [(float(v), c) for v, (_, c) in zip(t.tolist(), times)]
 
 
 def _encode(v):
@@ -37,7 +85,7 @@ def _decode(v):
 
 
 def _save() -> None:
-    if not _FILE or os.environ.get("RANK", "0") != "0":
+    if not _FILE or os.environ.get("RANK", "0") != "0":   # (the shipped table is read-only)
         return
     tmp = f"{_FILE}.tmp{os.getpid()}"
     with open(tmp, "w") as f:
@@ -71,8 +119,13 @@ class Tuner:
         pinned = _TABLE.get(self._tkey(key))
         if pinned is not None:
             c = _decode(pinned)
-            self.best[key] = c
-            return c
+            if any(c == _decode(_encode(x)) for x in candidates) or \
+                    (len(candidates) <= 1 and c == default):
+                self.best[key] = c
+                return c
+            warnings.warn(f"stale tuning entry {self._tkey(key)} = {pinned!r}: not among the "
+                          f"current candidates {list(candidates)!r}; timing instead",
+                          stacklevel=2)
         if torch.cuda.is_current_stream_capturing():
             return default            # no timing inside a graph capture; tune on the next eager call
         if not self.enabled or len(candidates) <= 1:
@@ -88,6 +141,7 @@ class Tuner:
             e.record()
             e.synchronize()
             times.append((s.elapsed_time(e), cand))
+        times = _agree_times(times)
         c = min(times, key=lambda t: t[0])[1]
         self.best[key] = c
         if _FILE:

@@ -38,6 +38,56 @@ def env_rank() -> int:
     return int(os.environ.get("RANK", "0"))
 
 
+def env_local_rank() -> Optional[int]:
+    """``LOCAL_RANK`` (torchrun) or ``OMPI_COMM_WORLD_LOCAL_RANK`` (mpirun), None if neither."""
+    for k in ("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK"):
+        if os.environ.get(k, "") != "":
+            return int(os.environ[k])
+    return None
+
+
+def rank_device_index(rank: int, n_devices: int, local_rank: Optional[int] = None) -> int:
+    """The GPU a rank binds to: its launcher-provided local rank when there is one, otherwise
+    ``rank % n_devices`` (one process per GPU on every node). The reference puts every rank on
+    ``cuda:0`` (``CIFAR10/torch_backend.py:8``); the ImageNet script uses ``local_rank``
+    (``train_imagenet_nv.py:160``)."""
+    if n_devices <= 0:
+        raise ValueError("no GPU to bind to")
+    idx = local_rank if local_rank is not None else int(rank)
+    return idx % n_devices
+
+
+def bind_rank_device(rank: int, requested: Optional[str] = None) -> torch.device:
+    """Pick and select this rank's device: ``requested`` verbatim when given (``--device``),
+    otherwise ``cuda:<rank_device_index>`` when a GPU is visible, else the CPU."""
+    if requested:
+        dev = torch.device(requested)
+    elif torch.cuda.is_available():
+        dev = torch.device("cuda", rank_device_index(rank, torch.cuda.device_count(),
+                                                     env_local_rank()))
+    else:
+        dev = torch.device("cpu")
+    if dev.type == "cuda":
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        torch.cuda.set_device(dev)
+    return dev
+
+
+def agree(ok: bool, group=None, device=None) -> bool:
+    """All-rank AND of a local flag (one tiny all-reduce; ``True`` without a process group), so
+    a fallback decision — graph capture, native communicator — is taken by every rank or none."""
+    if not is_dist() or world_size(group) == 1:
+        return bool(ok)
+    dev = torch.device(device) if device is not None and \
+        dist.get_backend(group) == "nccl" else torch.device("cpu")
+    if dist.get_backend(group) == "nccl" and dev.type != "cuda":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
 class _Done:
     def wait(self):
         return True
@@ -60,6 +110,15 @@ def all_gather(out: torch.Tensor, inp: torch.Tensor, group=None, async_op: bool 
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op) or _Done()
 
 
+def _bcast_uid(uid: torch.Tensor, group, dev) -> torch.Tensor:
+    if world_size(group) <= 1:
+        return uid
+    t = uid.to(dev)
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast(t, src=src, group=group)
+    return t.cpu()
+
+
 class NativeRccl:
     """Direct RCCL communicator (``csrc/rccl.cpp``) for the stream-ordered, graph-capturable
     bucket collectives: calls are enqueued on the caller's current HIP stream and return
@@ -67,21 +126,19 @@ class NativeRccl:
     them). Built collectively over an initialised ``nccl`` process group: rank 0's unique id is
     broadcast through it, then every rank joins with ``ncclCommInitRank``."""
 
-    def __init__(self, group=None, device=None):
+    def __init__(self, group=None, device=None, uid: Optional[torch.Tensor] = None):
         from ..ops._ext import load
         self.lib = load()
         self.world = world_size(group)
         self.rank = rank(group)
+        self.handle = 0
         dev = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
         self.device = dev
-        uid = self.lib.rccl_unique_id() if self.rank == 0 else \
-            torch.zeros(128, dtype=torch.uint8)
-        if self.world > 1:
-            t = uid.to(dev)
-            src = dist.get_global_rank(group, 0) if group is not None else 0
-            dist.broadcast(t, src=src, group=group)
-            uid = t.cpu()
+        if uid is None:       # (given: already broadcast by the caller)
+            uid = self.lib.rccl_unique_id() if self.rank == 0 else \
+                torch.zeros(128, dtype=torch.uint8)
+            uid = _bcast_uid(uid, group, dev)
         self.handle = int(self.lib.rccl_init(uid, self.world, self.rank, dev.index or 0))
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
@@ -176,8 +233,55 @@ def native_rccl(group=None, device=None) -> Optional[NativeRccl]:
         return None
     key = id(group) if group is not None else None
     if key not in _NATIVE:
-        _NATIVE[key] = NativeRccl(group, device)
+        _NATIVE[key] = _init_native_agreed(group, device)
     return _NATIVE[key]
+
+
+def _init_native_agreed(group, device) -> Optional[NativeRccl]:
+    """Create the native communicator as one collective decision: every rank first checks that it
+    can (extension loaded, unique id obtained), the ranks agree, and only then do they all enter
+    ``ncclCommInitRank``; a rank whose init then fails makes every rank drop its communicator.
+    On a no, all ranks fall back to the c10d collectives (eager steps at world > 1) instead of
+    some ranks waiting in an init that one of them never joins."""
+    uid = torch.zeros(128, dtype=torch.uint8)
+    try:
+        from ..ops._ext import load
+        lib = load()
+        if rank(group) == 0:
+            uid = lib.rccl_unique_id()
+        ready = True
+    except Exception as e:                     # noqa: BLE001 — reported, then agreed on
+        print(f"[lwaaai] native RCCL unavailable on rank {rank(group)}: {e}", flush=True)
+        ready = False
+    if not agree(ready, group, device):
+        print("[lwaaai] native RCCL disabled (not every rank can create it): c10d collectives",
+              flush=True)
+        return None
+    dev = torch.device(device) if device is not None else \
+        torch.device("cuda", torch.cuda.current_device())
+    uid = _bcast_uid(uid, group, dev)
+    comm, err = None, None
+    try:
+        comm = NativeRccl(group, device, uid=uid)
+        # validate the new communicator with one tiny all-reduce before trusting it
+        probe = torch.ones(1, dtype=torch.float32, device=dev)
+        comm.all_reduce(probe)
+        if int(probe.item()) != comm.world:
+            raise RuntimeError(f"probe all-reduce gave {probe.item()}, expected {comm.world}")
+        if os.environ.get("LWAAAI_FAKE_NATIVE_INIT_FAIL", "") == str(rank(group)):
+            raise RuntimeError("injected native init failure (LWAAAI_FAKE_NATIVE_INIT_FAIL)")
+    except Exception as e:                     # noqa: BLE001
+        err = e
+        if comm is not None:
+            comm.close()
+            comm = None
+    if not agree(comm is not None, group, device):
+        if comm is not None:
+            comm.close()
+        print(f"[lwaaai] native RCCL init failed on some rank ({err or 'peer'}): c10d collectives",
+              flush=True)
+        return None
+    return comm
 
 
 def all_reduce_max(t: torch.Tensor, group=None) -> torch.Tensor:

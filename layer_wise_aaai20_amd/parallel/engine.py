@@ -120,7 +120,7 @@ class GradSyncEngine:
                        if self.device.type == "cuda" else None)
         # device count of elements the reference rule selected but the payload could not carry
         # (Top-K ties beyond the slack, threshold hits beyond a fixed capacity; read_overflow)
-        self._overflow = (torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._overflow = (torch.zeros(1, dtype=torch.int64, device=self.device)
                           if self.device.type == "cuda" else None)
         for c in self.codecs:
             c.step_t = self._dstep
@@ -352,7 +352,7 @@ class GradSyncEngine:
         call at logging time. Also kept in ``stats.overflow``."""
         if self._overflow is None:
             return 0
-        self.stats.overflow = int(self._overflow.item()) & 0xFFFFFFFF
+        self.stats.overflow = int(self._overflow.item())
         return self.stats.overflow
 
     def heartbeat(self) -> None:

@@ -136,15 +136,26 @@ def default_backend() -> str:
 
 def init_distributed(master_address, world_size, rank, backend: Optional[str] = None):
     """``dist.init_process_group(init_method=master_address, ...)`` (core.py:334). A bare host
-    (the reference default ``127.0.0.1``) is completed to ``tcp://host:29500``. On a GPU the
-    group is created even for one rank, as the reference does, so the single-rank run takes
-    the same (RCCL) path as a multi-rank one."""
+    (the reference default ``127.0.0.1``) is completed to ``tcp://host:$MASTER_PORT`` (29500
+    by default). On a GPU the group is created even for one rank, as the reference does, so the
+    single-rank run takes the same (RCCL) path as a multi-rank one; a one-rank group on a bare
+    host takes a free ephemeral port, so concurrent single-GPU runs on one host do not collide."""
     backend = backend or default_backend()
     if comm.is_dist() or (int(world_size) <= 1 and backend != "nccl"):
         return
     addr = master_address or "127.0.0.1"
-    if "://" not in addr:
-        addr = f"tcp://{addr}:29500" if ":" not in addr else f"tcp://{addr}"
+    if "://" not in addr and ":" not in addr:
+        if int(world_size) <= 1:
+            import socket
+            with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+                s.bind((addr, 0))
+                port = s.getsockname()[1]
+        else:
+            import os
+            port = int(os.environ.get("MASTER_PORT", "29500"))
+        addr = f"tcp://{addr}:{port}"
+    elif "://" not in addr:
+        addr = f"tcp://{addr}"
     if backend == "nccl":
         torch.cuda.set_device(torch.cuda.current_device())
     kw = {"device_id": torch.device("cuda", torch.cuda.current_device())} \

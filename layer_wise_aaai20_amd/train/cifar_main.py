@@ -10,8 +10,12 @@ momentum only when ``--momentum > 0``, crop / flip / cutout augmentation redrawn
 Writes ``logs.tsv`` (``epoch\\thours\\ttop1Accuracy``) to ``--log_dir``.
 
 Added flags (all optional): ``--epochs``, ``--error_feedback``, ``--wire``, ``--synthetic``,
-``--max_batches`` (debug), ``--dtype``, ``--backend``, ``--shard_data`` (each rank sees 1/W of the
-data instead of the whole set, D16), ``--device``.
+``--max_batches`` (debug), ``--dtype``, ``--backend``, ``--full_data`` (every rank iterates the whole
+training set, as the reference does — by default each rank sees its 1/W shard, D16), ``--device``.
+
+Device placement: each rank binds to ``cuda:LOCAL_RANK`` (``rank % device_count`` without a
+launcher-provided local rank), so ``-w 8`` on one node puts one rank on each GPU. The reference
+puts every rank on ``cuda:0`` (``CIFAR10/torch_backend.py:8``).
 """
 from __future__ import annotations
 
@@ -47,13 +51,16 @@ def get_parser() -> argparse.ArgumentParser:
     p.add_argument("--epochs", type=int, default=None)
     p.add_argument("--batch_size", type=int, default=512)
     p.add_argument("--error_feedback", action="store_true")
-    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "dense", "indexfree"])
+    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "sparse-capped", "dense", "indexfree"])
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--n_train", type=int, default=50000)
     p.add_argument("--n_test", type=int, default=10000)
     p.add_argument("--max_batches", type=int, default=None)
     p.add_argument("--backend", type=str, default=None)
-    p.add_argument("--shard_data", action="store_true")
+    p.add_argument("--full_data", action="store_true",
+                   help="every rank iterates the full training set (reference behaviour)")
+    p.add_argument("--shard_data", action="store_true",
+                   help="(default; kept for old command lines) each rank sees 1/W of the data")
     p.add_argument("--device", type=str, default=None)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no_fused", action="store_true",
@@ -63,9 +70,8 @@ def get_parser() -> argparse.ArgumentParser:
 
 def main(argv=None):
     args = get_parser().parse_args(argv)
-    device = torch.device(args.device or ("cuda" if torch.cuda.is_available() else "cpu"))
-    if device.type == "cuda":
-        torch.cuda.set_device(device.index or 0)
+    from ..parallel.comm import bind_rank_device
+    device = bind_rank_device(args.rank, args.device)
     torch.manual_seed(args.seed)
     np.random.seed(args.seed + args.rank)
 
@@ -93,7 +99,7 @@ def main(argv=None):
     timer = Timer(synch=torch.cuda.synchronize if device.type == "cuda" else None)
     train_x = D.transpose(D.normalise(D.pad(dataset["train"]["data"], 4)))
     test_x = D.transpose(D.normalise(dataset["test"]["data"]))
-    shard = (args.rank, args.world_size) if args.shard_data else (0, 1)
+    shard = (0, 1) if args.full_data else (args.rank, args.world_size)
     train_batches = D.GPUBatches(torch.from_numpy(np.ascontiguousarray(train_x)).to(device),
                                  torch.as_tensor(dataset["train"]["labels"]).to(device), bs,
                                  shuffle=True, augment=True, drop_last=True, shard=shard,

@@ -81,9 +81,18 @@ class StepGraph:
         """The most recently used captured graph (compatibility with older callers/tests)."""
         return next(reversed(self._graphs.values())) if self._graphs else None
 
+    def _fn(self, *inputs: torch.Tensor):
+        """The eager step. At world > 1 its kernel-tuning decisions are agreed across ranks
+        (``ops/tuning.py`` ``rank_agreement``): every rank then runs the same kernels."""
+        if getattr(self.engine, "world", 1) <= 1:
+            return self.fn(*inputs)
+        from ..ops.tuning import rank_agreement
+        with rank_agreement(getattr(self.engine, "pg", None), self.device):
+            return self.fn(*inputs)
+
     def __call__(self, *inputs: torch.Tensor):
         if not self.active():
-            return self.fn(*inputs)
+            return self._fn(*inputs)
         sig = self._signature(inputs)
         g = self._graphs.get(sig)
         if g is None:
@@ -93,24 +102,43 @@ class StepGraph:
             if n < self.warmup:
                 self._seen[sig[0]] = n + 1
                 return self._eager_timed(inputs, n)
+            err = None
             try:
+                if os.environ.get("LWAAAI_FAKE_CAPTURE_FAIL", "") == str(self._rank()):
+                    raise RuntimeError("injected capture failure (LWAAAI_FAKE_CAPTURE_FAIL)")
                 g = self._capture(inputs, sig)
-            except RuntimeError as e:          # capture unsupported here: stay eager
+            except RuntimeError as e:          # capture unsupported here
+                err = e
+            # one decision for all ranks: a rank replaying while another runs eagerly would
+            # still pair its collectives, but the whole job would then run at the slow mode
+            if not self._agree(err is None):
                 self.enabled = False
                 self._graphs.clear()
                 torch.cuda.synchronize(self.device)
                 self.engine._reset_state()
-                print(f"[lwaaai] HIP-graph capture failed, running eagerly: {e}", flush=True)
-                return self.fn(*inputs)
+                why = err if err is not None else "another rank's capture failed"
+                print(f"[lwaaai] HIP-graph capture failed ({why}): every rank runs eagerly",
+                      flush=True)
+                return self._fn(*inputs)
         else:
             self._graphs[sig] = self._graphs.pop(sig)      # LRU order
         return self._replay(g, inputs)
+
+    def _rank(self) -> int:
+        from ..parallel import comm
+        return comm.rank(getattr(self.engine, "pg", None))
+
+    def _agree(self, ok: bool) -> bool:
+        if getattr(self.engine, "world", 1) <= 1:
+            return ok
+        from ..parallel import comm
+        return comm.agree(ok, getattr(self.engine, "pg", None), self.device)
 
     def _eager_timed(self, inputs, n: int):
         deciding = not self.decided
         if deciding and n >= 1:                 # (the first call of a signature tunes tiles)
             self._mark()
-        out = self.fn(*inputs)
+        out = self._fn(*inputs)
         if deciding and n >= 1:
             self._eager_t.append(self._lap())
             self._eager_t = self._eager_t[-self.timed:]

@@ -88,7 +88,7 @@ def get_parser():
     p.add_argument("--arch", default="resnet50")
     p.add_argument("--overlap", action="store_true", help="CompressedDDP (bucketed, overlapped)")
     p.add_argument("--error-feedback", action="store_true")
-    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "dense", "indexfree"])
+    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "sparse-capped", "dense", "indexfree"])
     p.add_argument("--epochs", type=int, default=None, help="stop after this many epochs")
     p.add_argument("--synthetic-size", type=int, default=None,
                    help="synthetic train images per phase (default 64 batches)")

@@ -1,0 +1,199 @@
+"""Rank bodies for ``tests/test_multigpu_gpu.py``: one process per GPU, RCCL ("nccl") process
+group, the native communicator (``csrc/rccl.cpp``) and captured steps — the world > 1 default
+path. Results travel back as ``(status, value)`` files of plain tensors/lists (our own files)."""
+import os
+import pickle
+import socket
+import tempfile
+import traceback
+
+import torch
+import torch.multiprocessing as mp
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, fn, outdir, args, env):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), **env)
+    if os.environ.get("LWAAAI_TEST_SHARE_GPU") == "1":
+        # rehearsal on a one-GPU box: every rank on cuda:0, each rank declared its own "host" so
+        # RCCL accepts two ranks on one device (it then moves data over its socket transport)
+        os.environ["NCCL_HOSTID"] = f"lwaaai-rank{rank}"
+    res = None
+    try:
+        from layer_wise_aaai20_amd.parallel.comm import bind_rank_device
+        dev = bind_rank_device(rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        res = ("ok", fn(rank, world, dev, *args))
+    except Exception:  # noqa: BLE001
+        res = ("err", traceback.format_exc())
+    finally:
+        with open(os.path.join(outdir, f"r{rank}.pkl"), "wb") as f:
+            pickle.dump(res, f)
+        try:
+            from layer_wise_aaai20_amd.parallel import comm
+            for c in list(comm._NATIVE.values()):
+                if c is not None:
+                    c.close()
+            if dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def run_world(fn, world, args=(), env=None):
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(world, port, fn, d, args, dict(env or {})),
+                           nprocs=world, start_method="spawn", join=True)
+        out = []
+        for r in range(world):
+            with open(os.path.join(d, f"r{r}.pkl"), "rb") as f:
+                status, val = pickle.load(f)         # written by _worker above
+            if status != "ok":
+                raise AssertionError(f"rank {r} failed:\n{val}")
+            out.append(val)
+    return out
+
+
+# ----------------------------------------------------------------------------------- bodies
+def _gather_cpu(t):
+    import torch.distributed as dist
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [p.cpu() for p in parts]
+
+
+def exchange_vs_oracle(rank, world, dev, mode, method, ef, kw, steps=3):
+    """Engine-level: each rank puts a rank-seeded random gradient in its arena and syncs through
+    the native communicator; the decoded arena must equal the CPU oracle mean on every rank."""
+    from layer_wise_aaai20_amd.compress import reference as ref
+    from layer_wise_aaai20_amd.models import resnet as R
+    from layer_wise_aaai20_amd.parallel.engine import GradSyncEngine
+    torch.manual_seed(0)
+    net = R.resnet50().to(dev)
+    eng = GradSyncEngine(list(net.named_parameters()), mode=mode, method=method,
+                         error_feedback=ef, **kw)
+    assert eng._native is not None, "native RCCL communicator not in use"
+    errs = []
+    for step in range(steps):
+        g = torch.Generator(device=dev).manual_seed(1000 * step + rank)
+        local = torch.zeros(eng.arena.numel, device=dev)
+        for s in eng.arena.segments:
+            local[s.offset:s.offset + s.numel] = 1e-2 * torch.randn(s.numel, device=dev,
+                                                                    generator=g)
+        e_old = eng.ef.clone() if ef else None
+        eng.arena.grad.copy_(local)
+        eng.sync_now()
+        torch.cuda.synchronize(dev)
+        got = eng.arena.grad.clone()
+        raws = _gather_cpu(local)
+        if ef:
+            sent_local = local + e_old - eng.ef
+            exp = sum(_gather_cpu(sent_local)) / world
+            errs.append(float((got.cpu() - exp).abs().max()))
+            tol = 1e-5
+        elif method in ("RandomDithering", "TernGrad"):
+            # the CPU mirror of every rank's quantiser (same Philox keys), decoded as the mean
+            from layer_wise_aaai20_amd.compress.codecs import make_codec
+            exp = torch.zeros(eng.arena.numel)
+            for b, plan in zip(eng.buckets, eng.plans):
+                sl = slice(b.start, b.end)
+                cods = [make_codec(method, plan, world, r, **eng.codec_kw) for r in range(world)]
+                sends = [c.compress(raws[r][sl].clone(), None, step)
+                         for r, c in enumerate(cods)]
+                part = torch.zeros(b.end - b.start)
+                cods[0].decompress(sends[0], torch.cat(sends), part)
+                exp[sl] = part
+            diff = (got.cpu() - exp).abs()
+            # a norm summed in another order may flip a rare stochastic level by one step
+            errs.append(float((diff > 1e-6 * exp.abs().max()).float().mean()))
+            tol = 1e-4
+        elif method == "Topk":
+            exp = torch.zeros(eng.arena.numel)
+            for r in range(world):
+                for s in eng.arena.segments:
+                    sl = slice(s.offset, s.offset + s.numel)
+                    exp[sl] += ref.compress(raws[r][sl], "Topk", **{"K": kw["K"]})
+            exp /= world
+            errs.append(float((got.cpu() - exp).abs().max()))
+            tol = 1e-8
+        else:
+            exp = sum(raws) / world
+            errs.append(float((got.cpu() - exp).abs().max()))
+            tol = 1e-7
+        # identical on every rank, bit for bit
+        allg = _gather_cpu(got)
+        assert all(torch.equal(allg[0], a) for a in allg[1:]), "decoded gradients differ"
+    return errs, tol
+
+
+def train_graph_vs_eager(rank, world, dev, compress, method, ef, kw, steps=8):
+    """Trainer-level: the same per-rank batches through an eager trainer and a HIP-graph trainer
+    (collectives captured on the side-stream branches); parameters must be bit-identical across
+    ranks and between the two modes."""
+    os.environ["LWAAAI_GRAPH_AUTO"] = "0"
+    from layer_wise_aaai20_amd.train.imagenet import build_trainer
+    out = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        tr = build_trainer("resnet50", device=dev, compress=compress, method=method,
+                           error_feedback=ef, graph=graph, **kw)
+        assert tr.ddp.engine._native is not None
+        g = torch.Generator(device=dev).manual_seed(77 + rank)
+        losses = []
+        for _ in range(steps):
+            x = torch.randint(0, 256, (8, 64, 64, 3), dtype=torch.uint8, device=dev, generator=g)
+            t = torch.randint(0, 1000, (8,), device=dev, generator=g)
+            losses.append(float(tr.step(x, t)))
+        torch.cuda.synchronize(dev)
+        p = torch.cat([q.detach().float().reshape(-1) for q in tr.ddp.module.parameters()])
+        allp = _gather_cpu(p)
+        out[graph] = (p.cpu(), losses, tr.graph_replays,
+                      all(torch.equal(allp[0], a) for a in allp[1:]))
+        del tr
+        torch.cuda.empty_cache()
+    return out
+
+
+def capture_fallback_collective(rank, world, dev):
+    """LWAAAI_FAKE_CAPTURE_FAIL=1 makes rank 1's capture fail: every rank must then run eagerly
+    (no replays anywhere) and the parameters must still agree."""
+    os.environ["LWAAAI_GRAPH_AUTO"] = "0"
+    from layer_wise_aaai20_amd.train.imagenet import build_trainer
+    torch.manual_seed(0)
+    tr = build_trainer("resnet50", device=dev, compress="layerwise", method="Topk", K=0.01,
+                       graph=True)
+    g = torch.Generator(device=dev).manual_seed(5 + rank)
+    for _ in range(6):
+        x = torch.randint(0, 256, (8, 64, 64, 3), dtype=torch.uint8, device=dev, generator=g)
+        t = torch.randint(0, 1000, (8,), device=dev, generator=g)
+        tr.step(x, t)
+    torch.cuda.synchronize(dev)
+    p = torch.cat([q.detach().float().reshape(-1) for q in tr.ddp.module.parameters()])
+    allp = _gather_cpu(p)
+    return tr.graph_replays, tr.graphed.enabled, all(torch.equal(allp[0], a) for a in allp[1:])
+
+
+def native_init_fallback(rank, world, dev):
+    """LWAAAI_FAKE_NATIVE_INIT_FAIL=1: rank 1 rejects its native communicator; every rank must
+    fall back to c10d (no native communicator anywhere) and still train in agreement."""
+    from layer_wise_aaai20_amd.train.imagenet import build_trainer
+    torch.manual_seed(0)
+    tr = build_trainer("resnet50", device=dev, compress="layerwise", method="Topk", K=0.01)
+    native = tr.ddp.engine._native is not None
+    g = torch.Generator(device=dev).manual_seed(9 + rank)
+    for _ in range(3):
+        x = torch.randint(0, 256, (8, 64, 64, 3), dtype=torch.uint8, device=dev, generator=g)
+        t = torch.randint(0, 1000, (8,), device=dev, generator=g)
+        tr.step(x, t)
+    torch.cuda.synchronize(dev)
+    p = torch.cat([q.detach().float().reshape(-1) for q in tr.ddp.module.parameters()])
+    allp = _gather_cpu(p)
+    return native, all(torch.equal(allp[0], a) for a in allp[1:])

@@ -179,6 +179,45 @@ def test_stem_pool_backward_zero_gamma(shape, monkeypatch):
     test_stem_bn_relu_pool_matches_layers(shape, True, monkeypatch, zero_gamma=True)
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 32, 32), (2, 64, 112, 112)])
+def test_stem_pool_backward_ill_conditioned_channels(shape, monkeypatch):
+    """|gamma| ~ 1e-3 with beta ~ 0.5: recovering x - mean from the bf16 pooled value would put
+    a per-channel bias into dgamma. Per channel, the pooled-side pass must agree with the
+    full-resolution pass (which reads x itself) and with an fp32 torch reference."""
+    from layer_wise_aaai20_amd.ops import nn as NN
+    from layer_wise_aaai20_amd.ops.nn import stem_bn_relu_pool
+    torch.manual_seed(5)
+    C = shape[1]
+    bn0 = torch.nn.BatchNorm2d(C).cuda()
+    bn0.weight.data.uniform_(0.5e-3, 2e-3)
+    bn0.weight.data[1::2] *= -1
+    bn0.weight.data[::4] = torch.empty(C // 4, device="cuda").uniform_(0.5, 1.5)  # well-conditioned
+    bn0.bias.data.uniform_(0.3, 0.7)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    c = torch.randn(*shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    g = torch.randn(shape[0], C, (shape[2] + 1) // 2, (shape[3] + 1) // 2, device="cuda")
+    g = g.to(torch.bfloat16)
+    res = {}
+    for pooled in (True, False):
+        monkeypatch.setattr(NN, "STEM_POOLED", pooled)
+        bn = copy.deepcopy(bn0)
+        ca = c.clone().requires_grad_()
+        stem_bn_relu_pool(ca, bn, pool).backward(g)
+        res[pooled] = (ca.grad.float(), bn.weight.grad.clone(), bn.bias.grad.clone())
+    bnr = copy.deepcopy(bn0).float()
+    cr = c.float().requires_grad_()
+    pool(torch.relu(bnr(cr))).backward(g.float())
+    for (dx, dg, db) in res.values():
+        scale = dg.abs().max()
+        assert ((dg - bnr.weight.grad).abs() < 3e-2 * scale + 1e-3).all(), \
+            (dg - bnr.weight.grad).abs().max()
+        torch.testing.assert_close(db, bnr.bias.grad, rtol=2e-2, atol=2e-2 * db.abs().max())
+        for ch in range(C):                      # every channel's dx, not just the whole tensor
+            assert _rel(dx[:, ch], cr.grad[:, ch]) < 5e-2, ch
+    torch.testing.assert_close(res[True][1], res[False][1], rtol=2e-2,
+                               atol=2e-2 * res[False][1].abs().max())
+
+
 def test_backward_stats_epilogues_match_reduce_pass(monkeypatch):
     """LWAAAI_BSTATS / LWAAAI_CROSS_BN3 (BN backward reductions in the data-gradient GEMM / conv
     epilogues, off by default — slower on MI355X, see profiles/r2_bstats_ab.log): a 3-block

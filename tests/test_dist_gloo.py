@@ -105,7 +105,7 @@ def test_randomk_sparsified_ddp_world2():
         assert torch.equal(a, b) and torch.equal(m0, m1)
 
 
-def _w_cifar_train(rank, world):
+def _w_cifar_train(rank, world, extra=()):
     import os
     import tempfile
     from layer_wise_aaai20_amd.train.cifar_main import main
@@ -113,7 +113,7 @@ def _w_cifar_train(rank, world):
     tsv = main(["-r", str(rank), "-w", str(world), "-n", "Resent9", "-c", "layerwise",
                 "--method", "Topk", "-K", "0.01", "--synthetic", "--n_train", "256",
                 "--n_test", "64", "--batch_size", "64", "--epochs", "2", "--log_dir", d,
-                "--device", "cpu", "--shard_data"])
+                "--device", "cpu"] + list(extra))
     return str(tsv), open(os.path.join(d, "logs.tsv")).read()
 
 
@@ -121,6 +121,44 @@ def test_cifar_entrypoint_world2():
     (t0, f0), (t1, f1) = run_world(_w_cifar_train, 2)
     assert f0.splitlines()[0] == "epoch\thours\ttop1Accuracy"
     assert len(f0.splitlines()) == 3
+
+
+def _w_cifar_batches(rank, world, full):
+    from layer_wise_aaai20_amd.train import cifar_main
+    seen = {}
+    orig = cifar_main.D.GPUBatches
+
+    def spy(*a, **kw):
+        b = orig(*a, **kw)
+        if kw.get("augment"):
+            seen["shard"] = kw.get("shard")
+            seen["n"] = len(b)
+        return b
+    cifar_main.D.GPUBatches = spy
+    try:
+        _w_cifar_train(rank, world, ["--full_data"] if full else [])
+    finally:
+        cifar_main.D.GPUBatches = orig
+    return seen
+
+
+def test_cifar_cli_shards_by_default():
+    """Each rank trains on its own 1/W shard unless --full_data."""
+    s = run_world(_w_cifar_batches, 2, (False,))
+    assert [x["shard"] for x in s] == [(0, 2), (1, 2)]
+    assert s[0]["n"] == s[1]["n"] == 2                  # 256 / 2 ranks / bs 64
+    f = run_world(_w_cifar_batches, 2, (True,))
+    assert [x["shard"] for x in f] == [(0, 1), (0, 1)] and f[0]["n"] == 4
+
+
+def _w_agree(rank, world):
+    from layer_wise_aaai20_amd.parallel import comm
+    return comm.agree(True), comm.agree(rank != 1), comm.agree(False)
+
+
+def test_agree_is_collective_and():
+    for r in run_world(_w_agree, 2):
+        assert r == (True, False, False)
 
 
 def _w_dist_predict(rank, world):

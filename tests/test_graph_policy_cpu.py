@@ -21,9 +21,10 @@ def test_codec_graph_flags():
     assert mk("TernGrad").graph_safe
     assert mk("RandomDithering", qstates=255).graph_safe
     assert mk("Randomk", K=0.05).graph_safe           # device step counter keys masks
-    assert mk("Thresholdv", V=1e-3, wire="sparse").graph_safe       # fixed capacity
-    assert not mk("Thresholdv", V=1e-3, wire="sparse-exact").graph_safe   # host read of capacity
-    assert mk("AdaptiveThreshold", wire="sparse").graph_safe
+    assert mk("Thresholdv", V=1e-3, wire="sparse-capped").graph_safe   # fixed capacity
+    assert not mk("Thresholdv", V=1e-3, wire="sparse").graph_safe   # host read of capacity
+    assert not mk("Thresholdv", V=1e-3, wire="sparse-exact").graph_safe
+    assert mk("AdaptiveThreshold", wire="sparse-capped").graph_safe
     assert mk("Thresholdv", V=1e-3).graph_safe                      # default dense wire
     assert mk("Topk", K=0.5, wire="dense").graph_safe
 

@@ -69,7 +69,7 @@ def test_graph_step_matches_eager(method, compress, ef):
     assert torch.equal(pe, pg), (pe - pg).abs().max().item()
 
 
-@pytest.mark.parametrize("wire,replays", [("sparse", 4), ("sparse-exact", 0)])
+@pytest.mark.parametrize("wire,replays", [("sparse-capped", 4), ("sparse", 0)])
 def test_threshold_sparse_wire_in_graph(wire, replays):
     """The fixed-capacity sparse threshold wire is sync-free: captured and bit-equal to eager.
     The count-exchange variant reads the agreed capacity on the host, so it stays eager."""

@@ -93,10 +93,10 @@ def test_fixed_capacity_threshold_wire(method, kw, density, monkeypatch):
     fit stay in the error-feedback residual, so decoded == mean_r(what each rank sent)."""
     monkeypatch.setenv("LWAAAI_THRESH_DENSITY", str(density))
     res = {}
-    for wire in ("dense", "sparse"):
+    for wire in ("dense", "sparse-capped"):
         eng = GradSyncEngine(_params(), mode="layerwise", method=method, error_feedback=True,
                              bucket_cap_mb=0.01, world_size=W, wire=wire, **kw)
-        if wire == "sparse":
+        if wire == "sparse-capped":
             assert all(c.graph_safe and c.name == "threshold" for c in eng.codecs)
         peers = [_grads(eng, 100 + r) for r in range(1, W)]
         lb = attach_loopback(eng, peers)
@@ -109,4 +109,4 @@ def test_fixed_capacity_threshold_wire(method, kw, density, monkeypatch):
         torch.testing.assert_close(eng.arena.grad, sent, rtol=1e-5, atol=1e-6)
         res[wire] = eng.arena.grad.clone()
     if density == 1.0:
-        torch.testing.assert_close(res["sparse"], res["dense"], rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(res["sparse-capped"], res["dense"], rtol=1e-6, atol=1e-7)

@@ -1,0 +1,88 @@
+"""World > 1 on real GPUs: one process per GPU over RCCL with the native communicator
+(``csrc/rccl.cpp``) and captured steps — the path the 8-GPU benchmark runs. Skipped unless the
+box has at least two GPUs; world 2 and world = device_count (capped at 8).
+
+Checks, per configuration (layer-wise Top-K ± EF, entire-model QSGD-255, dense):
+
+* the decoded gradient equals the CPU oracle — the mean over ranks of what each rank sent —
+  and is bit-identical on every rank;
+* after several training steps the parameters are bit-identical across ranks, and the HIP-graph
+  step equals the eager step bit for bit;
+* the fallbacks are collective: a capture failure or a native-communicator failure on one rank
+  puts every rank on the same (eager / c10d) path.
+
+Reference machinery being replaced: ``IMAGENET/training/train_imagenet_nv.py:160-163``,
+``IMAGENET/training/sparsified_ddp.py:454-494``, ``IMAGENET/training/ddp.py:434-477``."""
+import os
+
+import pytest
+import torch
+
+from mgpu_workers import (capture_fallback_collective, exchange_vs_oracle, native_init_fallback,
+                          run_world, train_graph_vs_eager)
+
+pytestmark = pytest.mark.gpu
+
+
+def _ngpu() -> int:
+    return torch.cuda.device_count() if torch.cuda.is_available() else 0
+
+
+def _share() -> bool:
+    """``LWAAAI_TEST_SHARE_GPU=1``: rehearse world 2 on a one-GPU box (both ranks on cuda:0, RCCL
+    over its socket transport; ``mgpu_workers._worker``)."""
+    return os.environ.get("LWAAAI_TEST_SHARE_GPU") == "1" and _ngpu() >= 1
+
+
+def _worlds():
+    n = min(_ngpu(), 8)
+    return sorted({2, n}) if n >= 2 else [2]
+
+
+need2 = pytest.mark.skipif(_ngpu() < 2 and not _share(),
+                           reason="needs >= 2 GPUs (or LWAAAI_TEST_SHARE_GPU=1)")
+
+CASES = [("layerwise", "Topk", False, {"K": 0.001}),
+         ("layerwise", "Topk", True, {"K": 0.001}),
+         ("entiremodel", "RandomDithering", False, {"qstates": 255}),
+         ("none", "none", False, {})]
+IDS = [f"{c[1]}-{c[0]}-{'ef' if c[2] else 'noef'}" for c in CASES]
+
+
+@need2
+@pytest.mark.parametrize("world", _worlds())
+@pytest.mark.parametrize("mode,method,ef,kw", CASES, ids=IDS)
+def test_native_exchange_matches_oracle(world, mode, method, ef, kw):
+    for errs, tol in run_world(exchange_vs_oracle, world, (mode, method, ef, kw)):
+        assert max(errs) <= tol, errs
+
+
+@need2
+@pytest.mark.parametrize("world", _worlds())
+@pytest.mark.parametrize("mode,method,ef,kw", CASES, ids=IDS)
+def test_training_ranks_agree_and_graph_matches_eager(world, mode, method, ef, kw):
+    kw = dict(kw)
+    if method == "Topk":
+        kw["K"] = 0.01
+    res = run_world(train_graph_vs_eager, world, (mode, method, ef, kw))
+    for r in res:
+        (pe, le, _, same_e), (pg, lg, replays, same_g) = r[False], r[True]
+        assert same_e and same_g, "parameters differ across ranks"
+        assert replays > 0
+        assert le == lg
+        assert torch.equal(pe, pg), (pe - pg).abs().max().item()
+    assert all(torch.equal(res[0][True][0], r[True][0]) for r in res[1:])
+
+
+@need2
+def test_capture_failure_is_a_collective_decision():
+    res = run_world(capture_fallback_collective, 2, env={"LWAAAI_FAKE_CAPTURE_FAIL": "1"})
+    for replays, enabled, same in res:
+        assert replays == 0 and not enabled and same
+
+
+@need2
+def test_native_init_failure_falls_back_everywhere():
+    res = run_world(native_init_fallback, 2, env={"LWAAAI_FAKE_NATIVE_INIT_FAIL": "1"})
+    for native, same in res:
+        assert not native and same

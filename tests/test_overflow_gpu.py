@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 def test_topk_tie_overflow_counted(n):
     plan = SegPlan([0], [n])
     codec = C.TopkCodec(plan, 1, 0, K=0.01, error_feedback=True)
-    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
     codec.overflow = cnt
     g = torch.ones(n, device="cuda")                    # every element ties at the threshold
     ef = torch.zeros(n, device="cuda")
@@ -37,7 +37,7 @@ def test_fixed_capacity_threshold_matches_cpu_mirror(adaptive):
     mk = lambda: C.ThresholdCodec(plan, 1, 0, V=0.5, adaptive=adaptive,          # noqa: E731
                                   error_feedback=True, max_density=0.02)
     gpu, cpu = mk(), mk()
-    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
     gpu.overflow = cnt
     torch.manual_seed(0)
     g = torch.randn(sum(sizes))

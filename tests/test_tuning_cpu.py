@@ -43,7 +43,7 @@ def test_pinned_entries_skip_timing(tuning):
     def run(c):
         raise AssertionError("a pinned choice must not be timed")
     assert T.Tuner("gemm", "X").pick((1, 2, 3), run, (1, 2, 21, 22), 0) == 22
-    assert T.Tuner("linear", "X").pick(("fwd", 8), run, [(1, 1)], (0, 1)) == (21, 4)
+    assert T.Tuner("linear", "X").pick(("fwd", 8), run, [(1, 1), (21, 4)], (0, 1)) == (21, 4)
 
 
 def test_new_decision_is_persisted(tuning):
@@ -67,3 +67,48 @@ def test_disabled_uses_default(monkeypatch):
     monkeypatch.setenv("LWAAAI_X_OFF", "0")
     monkeypatch.setattr(T.torch.cuda, "is_current_stream_capturing", lambda: False)
     assert T.Tuner("q", "LWAAAI_X_OFF").pick(7, lambda c: 1 / 0, (1, 2), 9) == 9
+
+
+def test_stale_pinned_entry_is_timed(tuning):
+    """A pinned choice that is not among the current candidates is ignored (and timed)."""
+    T, _ = tuning
+    cost = {1: 5.0, 2: 1.0}
+
+    def run(c):
+        _FakeEvent.clock[0] += cost[c]
+    with pytest.warns(UserWarning, match="stale tuning entry"):
+        assert T.Tuner("gemm", "X").pick((1, 2, 3), run, (1, 2), 1) == 2
+
+
+def test_shipped_table_default_and_none(monkeypatch):
+    import layer_wise_aaai20_amd.ops.tuning as T
+    monkeypatch.delenv("LWAAAI_TUNE_FILE", raising=False)
+    T = importlib.reload(T)
+    assert T._READ == T.SHIPPED and T._FILE == ""           # read-only: never written back
+    monkeypatch.setenv("LWAAAI_TUNE_FILE", "none")
+    T = importlib.reload(T)
+    assert T.table() == {} and T._FILE == ""
+    monkeypatch.delenv("LWAAAI_TUNE_FILE")
+    importlib.reload(T)
+
+
+def _w_agree_tuner(rank, world):
+    import layer_wise_aaai20_amd.ops.tuning as T
+    T.torch.cuda.Event = _FakeEvent
+    T.torch.cuda.is_current_stream_capturing = lambda: False
+    # rank 0 finds candidate 1 fastest, rank 1 finds 3 fastest; summed, 2 wins
+    cost = [{1: 1.0, 2: 2.0, 3: 9.0}, {1: 9.0, 2: 2.0, 3: 1.0}][rank]
+
+    def run(c):
+        _FakeEvent.clock[0] += cost[c]
+    local = T.Tuner("agree-a", "X").pick(("k",), run, (1, 2, 3), 1)
+    with T.rank_agreement():
+        agreed = T.Tuner("agree-b", "X").pick(("k",), run, (1, 2, 3), 1)
+    return local, agreed
+
+
+def test_rank_agreement_picks_one_kernel_for_all_ranks():
+    from dist_utils import run_world
+    (l0, a0), (l1, a1) = run_world(_w_agree_tuner, 2)
+    assert (l0, l1) == (1, 3)          # timed alone, the ranks disagree
+    assert a0 == a1 == 2               # agreed: the candidate with the lowest summed time

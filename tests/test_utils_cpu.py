@@ -153,3 +153,28 @@ def test_launch_env_and_mpi_helpers(tmp_path):
     import pytest
     with pytest.raises(FileNotFoundError):
         L.mount_imagenet(str(tmp_path))
+
+
+def test_rank_device_mapping():
+    """Rank → GPU binding of the CLIs: LOCAL_RANK when the launcher gives one, else
+    rank % device_count (the reference binds every rank to cuda:0)."""
+    from layer_wise_aaai20_amd.parallel.comm import rank_device_index
+    assert [rank_device_index(r, 8) for r in range(8)] == list(range(8))
+    assert [rank_device_index(r, 8) for r in range(8, 16)] == list(range(8))   # 2 nodes
+    assert rank_device_index(13, 8, local_rank=5) == 5
+    assert [rank_device_index(r, 2) for r in range(4)] == [0, 1, 0, 1]
+    import pytest
+    with pytest.raises(ValueError):
+        rank_device_index(0, 0)
+
+
+def test_env_local_rank(monkeypatch):
+    from layer_wise_aaai20_amd.parallel import comm
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
+    monkeypatch.delenv("OMPI_COMM_WORLD_LOCAL_RANK", raising=False)
+    assert comm.env_local_rank() is None
+    monkeypatch.setenv("OMPI_COMM_WORLD_LOCAL_RANK", "3")
+    assert comm.env_local_rank() == 3
+    monkeypatch.setenv("LOCAL_RANK", "2")
+    assert comm.env_local_rank() == 2
+    assert comm.bind_rank_device(5).type == "cpu"        # no GPU in this container

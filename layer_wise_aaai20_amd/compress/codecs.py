@@ -122,11 +122,16 @@ class TopkCodec(Codec):
     # exact Top-K ignores the step; Random-K reads it from the device counter (step_t)
     graph_safe = True
 
-    def __init__(self, plan, world, rank, K: float, seed=0, error_feedback=False):
+    def __init__(self, plan, world, rank, K: float, seed=0, error_feedback=False,
+                 dense_below: int = 0):
         super().__init__(plan, world, rank, seed, error_feedback)
         self.K = float(K)
         self.keep = np.asarray([ref.topk_keep_count(int(n), self.K) for n in plan.sizes],
                                dtype=np.int64)
+        self.dense_below = int(dense_below or 0)
+        if self.dense_below > 0:     # opt-in deviation: small tensors travel whole (see below)
+            self.keep = np.where(np.asarray(plan.sizes) <= self.dense_below,
+                                 np.asarray(plan.sizes, dtype=np.int64), self.keep)
         self.cap = self.keep + np.asarray([tie_slack(int(m)) for m in self.keep], dtype=np.int64)
         self.cap = np.minimum(self.cap, plan.sizes)
         self.cap_off = np.concatenate([[0], np.cumsum(self.cap)]).astype(np.int64)
@@ -136,9 +141,10 @@ class TopkCodec(Codec):
 
     def _dev_tables(self, device):
         t = self.plan.select_tables(device)
-        t["keep"] = self.plan.dev(device, f"keep{self.K}", lambda: torch.from_numpy(
+        kk = f"{self.K}d{getattr(self, 'dense_below', 0)}"
+        t["keep"] = self.plan.dev(device, f"keep{kk}", lambda: torch.from_numpy(
             self.keep.astype(np.int32)))
-        t["cap_off"] = self.plan.dev(device, f"capoff{self.K}{self.km}", lambda: torch.from_numpy(
+        t["cap_off"] = self.plan.dev(device, f"capoff{kk}{self.km}", lambda: torch.from_numpy(
             self.cap_off))
         return t
 
@@ -245,12 +251,17 @@ class RandkSparseCodec(TopkCodec):
     # profiles/r3_graph_divergence_root_cause.md; graph == eager bit for bit since.)
     graph_safe = True
 
-    def __init__(self, plan, world, rank, K, seed=0, error_feedback=False):
+    def __init__(self, plan, world, rank, K, seed=0, error_feedback=False,
+                 dense_below: int = 0):
         Codec.__init__(self, plan, world, rank, seed, error_feedback)
         self.K = float(K)
         self.keep = np.asarray([ref.randomk_keep_count(int(n), self.K) for n in plan.sizes],
                                dtype=np.int64)
         self.keep = np.maximum(self.keep, 1)
+        self.dense_below = int(dense_below or 0)
+        if self.dense_below > 0:
+            self.keep = np.where(np.asarray(plan.sizes) <= self.dense_below,
+                                 np.asarray(plan.sizes, dtype=np.int64), self.keep)
         self.cap = self.keep.copy()
         self.cap_off = np.concatenate([[0], np.cumsum(self.cap)]).astype(np.int64)
         self.cap_total = int(self.cap_off[-1])
@@ -266,8 +277,8 @@ class RandkCodec(RandkSparseCodec):
     collective = "all_reduce"
     name = "randk"
 
-    def __init__(self, plan, world, rank, K, seed=0, error_feedback=False):
-        super().__init__(plan, world, rank, K, seed, error_feedback)
+    def __init__(self, plan, world, rank, K, seed=0, error_feedback=False, dense_below=0):
+        super().__init__(plan, world, rank, K, seed, error_feedback, dense_below)
         self._idx = {}
         self._slot_seg = {}
 
@@ -310,7 +321,8 @@ class RandkCodec(RandkSparseCodec):
         idx = self._idx[str(grad.device)]
         grad.zero_()
         if lib is not None:
-            slot_seg = self.plan.dev(grad.device, f"slotseg{self.K}", lambda: torch.from_numpy(
+            slot_seg = self.plan.dev(grad.device, f"slotseg{self.K}d{self.dense_below}",
+                                     lambda: torch.from_numpy(
                 np.repeat(np.arange(self.plan.S, dtype=np.int32), self.cap)))
             lib.unpack_validx(send, idx, slot_seg, world, grad, self.plan.common(grad.device)
                               ["seg_off"])
@@ -700,20 +712,26 @@ class DenseWrap(Codec):
 # ================================================================================= factory
 def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qstates=None,
                seed: int = 0, error_feedback: bool = False, wire: str = "auto",
-               count_exchange=None, max_density=None) -> Codec:
+               count_exchange=None, max_density=None, dense_below: int = 0) -> Codec:
     """Build the codec for ``method`` honouring the reference's falsy-parameter guards
-    (``core.py:178-215``: ``Topk`` without K, ``Thresholdv`` without V... mean no compression)."""
+    (``core.py:178-215``: ``Topk`` without K, ``Thresholdv`` without V... mean no compression).
+
+    ``dense_below`` (opt-in deviation, Top-K / Random-K): a tensor of at most that many elements
+    travels whole instead of keeping ``ceil(nK)``. The reference keeps >= 1 element of every
+    layer, so a 64-element BatchNorm tensor at K = 1 % sends 1 element a step; with error
+    feedback the other 63 accumulate ~64 steps of gradient and are released in bursts
+    (``profiles/r4/ef_root_cause.md``)."""
     method = ref.canonical_method(method)
     if method == "Topk" and K:
         if K >= 1.0:
             c = DenseCodec(plan, world, rank, seed)
         else:
-            c = TopkCodec(plan, world, rank, K, seed, error_feedback)
+            c = TopkCodec(plan, world, rank, K, seed, error_feedback, dense_below)
     elif method == "Randomk" and K:
         if wire in ("sparse",):
-            c = RandkSparseCodec(plan, world, rank, K, seed, error_feedback)
+            c = RandkSparseCodec(plan, world, rank, K, seed, error_feedback, dense_below)
         else:
-            c = RandkCodec(plan, world, rank, K, seed, error_feedback)
+            c = RandkCodec(plan, world, rank, K, seed, error_feedback, dense_below)
     elif method in ("Thresholdv", "AdaptiveThreshold") and (V or method == "AdaptiveThreshold"):
         # sparse wire capacity: agreed per step by the count exchange ("sparse" /
         # "sparse-exact": exact, like the reference's |g| >= V), or fixed per segment

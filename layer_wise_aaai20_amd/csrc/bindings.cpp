@@ -1190,6 +1190,33 @@ std::tuple<Tensor, Tensor> conv3_direct(Tensor x, Tensor w, bool want_stats) {
   return {y, st};
 }
 
+// Tap-reuse 3x3 / stride-1 / pad-1 convolution (conv3tap.hip k_conv3_tap): x [N, C, H, W] bf16
+// channels_last, w the K-contiguous [Co][9C] operand ((r, s, ci) order; for a data gradient the
+// flipped, transposed weight); returns (y [N, Co, H, W] channels_last, stats [tiles_m, 2, Co] or
+// an empty tensor).
+std::tuple<Tensor, Tensor> conv3_tap(Tensor x, Tensor w, int64_t Co, bool want_stats) {
+  const c10::DeviceGuard guard(x.device());
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 &&
+              x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: [N, C, H, W] channels_last");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(w.is_contiguous() && w.numel() == Co * 9 * C, "w: [Co][9C] K-contiguous");
+  TORCH_CHECK(lw::conv3_tap_ok((int)C, (int)Co, (int)H, (int)W), "conv3_tap: unsupported geometry");
+  TORCH_CHECK(x.numel() * 2 < (1LL << 31) && w.numel() * 2 < (1LL << 31), "conv3_tap: operand > 2 GiB");
+  check_aligned16(x.data_ptr(), "x");
+  check_aligned16(w.data_ptr(), "w");
+  Tensor y = at::empty({N, Co, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t rows = lw::conv3_tap_tiles_m((int)N, (int)H, (int)W);
+  Tensor st = want_stats ? at::empty({rows, 2, Co}, x.options().dtype(at::kFloat))
+                         : at::empty({0}, x.options().dtype(at::kFloat));
+  lw::conv3_tap(ptr<uint16_t>(x), ptr<uint16_t>(w), ptr<uint16_t>(y),
+                want_stats ? ptr<float>(st) : nullptr, (int)N, (int)H, (int)W, (int)C, (int)Co,
+                cur_stream());
+  launched("conv3_tap");
+  return {y, st};
+}
+
 // ---------------------------------------------------------------- BN pieces for fused blocks
 // Arrival tickets of the one-launch colsum + finalize (bn.hip k_colsum_finalize), one per 64-channel
 // slice: zeroed once per device (eagerly: never created inside a graph capture) and re-armed by the
@@ -1510,6 +1537,7 @@ TORCH_LIBRARY(lwaaai, m) {
       "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("stem_conv7(Tensor x, Tensor w) -> (Tensor, Tensor)");
   m.def("conv3_direct(Tensor x, Tensor w, bool want_stats) -> (Tensor, Tensor)");
+  m.def("conv3_tap(Tensor x, Tensor w, int Co, bool want_stats) -> (Tensor, Tensor)");
   m.def(
       "bn_bwd_dual(Tensor dy, Tensor x, Tensor x2, Tensor bits, Tensor? weight, Tensor mean, "
       "Tensor invstd, Tensor? weight2, Tensor mean2, Tensor invstd2, "
@@ -1570,6 +1598,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("bn_bwd_dual", &bn_bwd_dual);
   m.impl("stem_conv7", &stem_conv7);
   m.impl("conv3_direct", &conv3_direct);
+  m.impl("conv3_tap", &conv3_tap);
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);
   m.impl("conv_ex", &conv_ex);

@@ -278,6 +278,12 @@ void stem_conv7(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats,
                 int W, int Ho, int Wo, hipStream_t st);
 // direct 3x3 / stride-1 / pad-1 convolution, 64 -> 64 channels, NHWC, from an LDS patch
 // (conv.hip k_conv3_direct); stats (optional): one column-statistics row per 8 output rows
+// tap-reuse 3x3 / stride-1 / pad-1 convolution (conv3tap.hip): x NHWC [N*H*W][C] bf16, w the
+// K-contiguous [Co][9C] operand ((r, s, ci) order); stats (optional) [tiles_m][2][Co]
+bool conv3_tap_ok(int C, int Co, int H, int W);
+int conv3_tap_tiles_m(int N, int H, int W);
+void conv3_tap(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
+               int W, int C, int Co, hipStream_t st);
 bool conv3_direct_ok(int C, int Co, int H, int W);
 void conv3_direct(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
                   int W, hipStream_t st);

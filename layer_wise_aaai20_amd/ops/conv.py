@@ -56,6 +56,30 @@ CONV3_DIRECT_ON = os.environ.get("LWAAAI_CONV3_DIRECT", "0") != "0"
 def _conv3_direct_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
     return (CONV3_DIRECT_ON and c == 64 and co == 64 and (R, S) == (3, 3) and (sh, sw) == (1, 1)
             and (ph, pw) == (1, 1) and H % 8 == 0 and (8 * W) % 112 == 0 and 8 * W <= 448)
+# the tap-reuse 3x3/1 convolution (csrc/conv3tap.hip k_conv3_tap): the input patch of a
+# 224-pixel tile is staged once per 32-channel chunk and read by all 9 taps (the implicit GEMM
+# gathers it 9 times), forward and — flipped, transposed weight — data gradient. C % 32 == 0,
+# Co == 64 or Co % 128 == 0, image width dividing 224. LWAAAI_CONV3_TAP=0 leaves it out.
+CONV3_TAP = 33
+CONV3_TAP_ON = os.environ.get("LWAAAI_CONV3_TAP", "1") != "0"
+
+
+def _conv3_tap_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
+    if not (CONV3_TAP_ON and (R, S) == (3, 3) and (sh, sw) == (1, 1) and (ph, pw) == (1, 1)):
+        return False
+    if c % 32 or c < 32 or not (co == 64 or co % 128 == 0) or W < 4 or 224 % W:
+        return False
+    rows = 224 // W
+    return (rows + 2) * (W + 2) * 64 <= 24 * 1024
+
+
+def tap_dgrad_weight(w: torch.Tensor) -> torch.Tensor:
+    """The data gradient of a 3x3/1/1 conv as a forward conv of dy: W'[ci][r][s][co] =
+    w[co][ci][2-r][2-s], K-contiguous [C][9 Co]."""
+    c = w.shape[1]
+    return w.to(BF16).flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).contiguous()
+
+
 _TILE_DIMS = {1: (128, 128, 32), 2: (128, 128, 64), 3: (256, 64, 32), 4: (64, 256, 32),
               5: (256, 64, 64), 6: (64, 64, 64), 21: (256, 256, 64), 22: (256, 128, 64)}
 
@@ -197,6 +221,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
         if tile == CONV3_DIRECT:
             ys, sts = lib.conv3_direct(xin, op, True)
             return ys.permute(0, 2, 3, 1).reshape(M, co), sts
+        if tile == CONV3_TAP:
+            ys, sts = lib.conv3_tap(xin, op, co, bool(stats))
+            return ys.permute(0, 2, 3, 1).reshape(M, co), (sts if stats else None)
         return lib.conv_ex(xin, op, mode, geom, co, tile, 1, True, ps, pt, stats, None, False, 0,
                            True, K, bias=bf, relu=bool(relu))
     key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats,
@@ -209,6 +236,9 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
     if (pro is None and bias is None and not relu and not c4 and
             _conv3_direct_fits(C, co, R, S, sh, sw, ph, pw, H, W)):
         direct = direct + (CONV3_DIRECT,)
+    if (pro is None and bias is None and not relu and not c4 and
+            _conv3_tap_fits(C, co, R, S, sh, sw, ph, pw, H, W)):
+        direct = direct + (CONV3_TAP,)
     tile = TUNER.pick(key, run, ROW_TILES + big + direct, _row_default(M, co))
     y, st = run(tile)
     return y.view(Nb, Ho, Wo, co).permute(0, 3, 1, 2), st
@@ -250,11 +280,13 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
 
     def run(cand, dst=None, add=None):
         layout, tile = cand
-        if layout == "direct" and (dst is not None or add is not None):
-            layout, tile = "kc", 2            # the direct kernel writes a fresh tensor only
+        if layout in ("direct", "tap") and (dst is not None or add is not None):
+            layout, tile = "kc", 2            # the direct kernels write a fresh tensor only
         if layout == "direct":        # conv of dy with W'[ci][r][s][co] = w[co][ci][2-r][2-s]
-            wf = w.to(BF16).flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).contiguous()
-            ys, _ = lib.conv3_direct(dyc, wf, False)
+            ys, _ = lib.conv3_direct(dyc, tap_dgrad_weight(w), False)
+            return ys.permute(0, 2, 3, 1).reshape(-1, c), None
+        if layout == "tap":           # (the flip + transpose pack is timed with the conv)
+            ys, _ = lib.conv3_tap(dyc, tap_dgrad_weight(w), c, False)
             return ys.permute(0, 2, 3, 1).reshape(-1, c), None
         if layout == "kc":            # packed per call: the tuner times the pack with the conv
             wk, koffs, kmax = pack_dgrad_weight_kc(w, classes, sh, sw)
@@ -276,6 +308,9 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
     if (addend is None and bst is None and out is None and
             _conv3_direct_fits(co, c, R, S, sh, sw, ph, pw, Ho, Wo) and (H, W) == (Ho, Wo)):
         cands.append(("direct", CONV3_DIRECT))
+    if (addend is None and bst is None and out is None and
+            _conv3_tap_fits(co, c, R, S, sh, sw, ph, pw, Ho, Wo) and (H, W) == (Ho, Wo)):
+        cands.append(("tap", CONV3_TAP))
     cand = TUNER.pick(key, run, cands, ("nkc", _row_default(M, c)))   # (timed on scratch outputs)
     dx, st = run(cand, out, addend)
     if bst is not None:

@@ -31,7 +31,8 @@ class CompressedDDP(nn.Module):
                  broadcast_buffers: bool = True, wire: str = "auto", seed: int = 2147483647,
                  flat_params: bool = True, check_reduction: bool = True, device_ids=None,
                  output_device=None, dim: int = 0, timing: bool = False,
-                 bf16_weights: bool = True, world_size: Optional[int] = None):
+                 bf16_weights: bool = True, world_size: Optional[int] = None,
+                 dense_below: int = 0, momentum_correction: float = 0.0):
         super().__init__()
         self.module = module
         import os
@@ -55,7 +56,9 @@ class CompressedDDP(nn.Module):
                                      bucket_cap_mb=bucket_cap_mb,
                                      first_bucket_mb=first_bucket_mb, wire=wire, seed=seed,
                                      process_group=process_group, flat_params=flat_params,
-                                     timing=timing, world_size=world_size)
+                                     timing=timing, world_size=world_size,
+                                     dense_below=dense_below,
+                                     momentum_correction=momentum_correction)
         self._buffers_list = self._flatten_buffers(module) if broadcast_buffers else []
         self._hooks = []
         self._register_hooks()

@@ -66,7 +66,8 @@ class GradSyncEngine:
                  wire: str = "auto",
                  seed: int = 2147483647, process_group=None, flat_params: bool = False,
                  world_size: Optional[int] = None, timing: bool = False,
-                 overlap_compress: bool = True):
+                 overlap_compress: bool = True, dense_below: int = 0,
+                 momentum_correction: float = 0.0):
         self.mode = canonical_mode(mode)
         self.method = ref.canonical_method(method) if self.mode != "none" else "none"
         self.pg = process_group
@@ -98,9 +99,21 @@ class GradSyncEngine:
             warnings.warn(msg, stacklevel=2)
             if self.rank == 0:
                 print(f"[lwaaai] warning: {msg}", flush=True)
+        # DGC-style momentum correction (opt-in, Lin et al. 2018; profiles/r4/ef_root_cause.md):
+        # each rank accumulates its velocity u = m·u + g locally and the error-feedback residual
+        # accumulates u instead of g; the coordinates that were sent have their velocity zeroed
+        # (momentum factor masking). The optimizer then runs WITHOUT momentum (the trainers
+        # switch it off). Needs error feedback.
+        self.mc = float(momentum_correction or 0.0)
+        self.mom = None
+        if self.mc > 0:
+            if self.ef is None:
+                raise ValueError("momentum correction needs error_feedback=True")
+            self.mom = torch.zeros_like(self.arena.grad)
         # what a peer needs to build this engine's codecs for another rank (loopback tests)
         self.codec_kw = dict(K=K, V=V, qstates=qstates, seed=self.seed,
-                             error_feedback=self.ef is not None, wire=wire)
+                             error_feedback=self.ef is not None, wire=wire,
+                             dense_below=int(dense_below or 0))
         self.codecs: List[Codec] = []
         self.plans: List[SegPlan] = []
         for b in self.buckets:
@@ -276,7 +289,14 @@ class GradSyncEngine:
             side.wait_event(ready)
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             t0 = self._event() if self.timing else None
+            u = None
+            if self.mom is not None:
+                u = self.mom[b.start:b.end]
+                u.mul_(self.mc).add_(g)                  # local velocity
+                g.copy_(u)                               # the residual accumulates velocity
             send = codec.compress(g, e, self.step)
+            if u is not None:
+                u.mul_(e != 0)                           # momentum factor masking: sent -> 0
             t1 = self._event() if self.timing else None
             self._payload += codec.last_payload_bytes
             if codec.collective == "all_reduce":

@@ -29,7 +29,7 @@ class CifarTrainer:
                  V=None, qstates=None, error_feedback=False, batch_size=512, epochs=24,
                  momentum=0.9, dtype=torch.bfloat16, bucket_cap_mb=25.0, wire="auto",
                  n_train=50000, seed=0, fused=True, graph=None, n_test=1000,
-                 task="textures", amp=None):
+                 task="textures", amp=None, dense_below=0, momentum_correction=False):
         self.device = torch.device(device or "cuda")
         self.dtype = dtype
         self.bs = batch_size
@@ -44,11 +44,16 @@ class CifarTrainer:
         if self.device.type == "cuda":
             net = net.to(memory_format=torch.channels_last)
         self.model = net
+        # momentum_correction (DGC, opt-in): the velocity lives in the compressor's residual and
+        # the optimizer runs without momentum (parallel/engine.py)
+        mc = float(momentum) if momentum_correction else 0.0
         self.ddp = CompressedDDP(net, compress=compress, method=method, K=K, V=V,
                                  qstates=qstates, error_feedback=error_feedback,
-                                 bucket_cap_mb=bucket_cap_mb, wire=wire, flat_params=True)
-        self.opt = FlatSGD(net.parameters(), self.ddp.arena, lr=0.0, momentum=momentum,
-                           nesterov=momentum > 0, weight_decay=5e-4 * batch_size)
+                                 bucket_cap_mb=bucket_cap_mb, wire=wire, flat_params=True,
+                                 dense_below=dense_below, momentum_correction=mc)
+        om = 0.0 if mc > 0 else momentum
+        self.opt = FlatSGD(net.parameters(), self.ddp.arena, lr=0.0, momentum=om,
+                           nesterov=om > 0, weight_decay=5e-4 * batch_size)
         ds = D.synthetic_cifar10(n_train, n_test, seed, task=task, amp=amp)
         x = D.transpose(D.normalise(D.pad(ds["train"]["data"], 4)))
         tx = D.transpose(D.normalise(ds["test"]["data"]))

@@ -63,6 +63,13 @@ def get_parser() -> argparse.ArgumentParser:
                    help="(default; kept for old command lines) each rank sees 1/W of the data")
     p.add_argument("--device", type=str, default=None)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--ef_dense_below", type=int, default=0,
+                   help="(opt-in) Top-K / Random-K: tensors of at most this many elements are "
+                        "sent whole (profiles/r4/ef_root_cause.md)")
+    p.add_argument("--momentum_correction", action="store_true",
+                   help="(opt-in, needs --error_feedback and --momentum) DGC momentum correction "
+                        "+ factor masking: the velocity is accumulated before compression and the "
+                        "optimizer runs without momentum")
     p.add_argument("--no_fused", action="store_true",
                    help="the reference's structure: torch layers, post-backward sync, torch SGD")
     return p
@@ -124,12 +131,14 @@ def main(argv=None):
         model = CompressedDDP(net, compress=args.compress, method=args.method, K=args.ratio,
                               V=args.threshold, qstates=args.qstates,
                               error_feedback=args.error_feedback, wire=args.wire,
-                              flat_params=True)
+                              flat_params=True, dense_below=args.ef_dense_below,
+                              momentum_correction=args.momentum if args.momentum_correction
+                              else 0.0)
         arena = model.arena
 
         def optimizer_cls(weights, **kw):               # noqa: F811
             return FlatSGD(weights, arena, **kw)
-    if args.momentum > 0:
+    if args.momentum > 0 and not (fast and args.momentum_correction):
         opt = SGD(trainable_params(net), lr=lr, momentum=args.momentum, weight_decay=5e-4 * bs,
                   nesterov=True, optimizer=optimizer_cls)
     else:

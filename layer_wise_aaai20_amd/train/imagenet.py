@@ -112,7 +112,8 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
                   V=1e-3, qstates=255, error_feedback=False, bucket_cap_mb=25.0, dtype="bf16",
                   fused=True, momentum=0.9, weight_decay=1e-4, no_bn_wd=True, lr=0.1,
                   bn0=True, wire="auto", graph=None, graph_warmup: int = 3,
-                  world_size=None, graph_auto=None) -> ImageNetTrainer:
+                  world_size=None, graph_auto=None, dense_below=0,
+                  momentum_correction=False) -> ImageNetTrainer:
     """``world_size``: build the codecs for that many ranks without a process group (a simulated
     world driven by ``parallel/loopback.py``); default: the process group's size."""
     device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -124,11 +125,14 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
         net = net.to(memory_format=torch.channels_last)
     if fused:
         lwnn.share_bn_counters(net)
+    mc = float(momentum) if momentum_correction else 0.0     # DGC: velocity in the residual
     ddp = CompressedDDP(net, compress=compress, method=method, K=K, V=V, qstates=qstates,
                         error_feedback=error_feedback, bucket_cap_mb=bucket_cap_mb, wire=wire,
-                        flat_params=True, world_size=world_size)
+                        flat_params=True, world_size=world_size, dense_below=dense_below,
+                        momentum_correction=mc)
     groups = bn_param_groups(net, weight_decay, no_bn_wd)
-    opt = FlatSGD(groups, ddp.arena, lr=lr, momentum=momentum, nesterov=momentum > 0,
+    om = 0.0 if mc > 0 else momentum
+    opt = FlatSGD(groups, ddp.arena, lr=lr, momentum=om, nesterov=om > 0,
                   weight_decay=weight_decay)
     tdtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype] \
         if isinstance(dtype, str) else dtype

@@ -1,0 +1,128 @@
+#!/usr/bin/env python
+"""Error-feedback diagnostics on the CIFAR ResNet-9 dawn recipe (verdict r3 item 5).
+
+For each configuration a ResNet-9 is trained with the 24-epoch recipe (40 for Random-K) on the
+synthetic texture task, and every ``--every`` steps the per-layer ratio ||e|| / ||g|| is
+recorded: the residual left after compression against the raw gradient of that step, per
+parameter tensor. Output: one JSON line per run with the held-out accuracy, the final train loss
+and the trace summarised per layer kind (BatchNorm weight / bias, conv, linear) at a few points.
+
+usage: python scripts/ef_trace.py [--only 0,1,2] [--every 25] [--trace-out FILE.jsonl]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+RUNS = [
+    # (name, method, mode, kw, ef, extra)
+    ("none", "none", "none", {}, False, {}),
+    ("topk1", "Topk", "layerwise", {"K": 0.01}, False, {}),
+    ("topk1+ef", "Topk", "layerwise", {"K": 0.01}, True, {}),
+    ("topk1+ef+dense4k", "Topk", "layerwise", {"K": 0.01}, True, {"dense_below": 4096}),
+    ("topk1+ef+mc", "Topk", "layerwise", {"K": 0.01}, True, {"momentum_correction": True}),
+    ("topk1+ef+mc+dense4k", "Topk", "layerwise", {"K": 0.01}, True,
+     {"momentum_correction": True, "dense_below": 4096}),
+    ("randk1+ef", "Randomk", "layerwise", {"K": 0.01}, True, {}),
+    ("randk1+ef+mc", "Randomk", "layerwise", {"K": 0.01}, True, {"momentum_correction": True}),
+    ("randk1+ef+mc+dense4k", "Randomk", "layerwise", {"K": 0.01}, True,
+     {"momentum_correction": True, "dense_below": 4096}),
+    ("randk10+ef", "Randomk", "layerwise", {"K": 0.1}, True, {}),
+    ("randk10+ef+mc", "Randomk", "layerwise", {"K": 0.1}, True, {"momentum_correction": True}),
+    ("topk0.1+ef", "Topk", "layerwise", {"K": 0.001}, True, {}),
+    ("topk0.1+ef+mc+dense4k", "Topk", "layerwise", {"K": 0.001}, True,
+     {"momentum_correction": True, "dense_below": 4096}),
+]
+
+
+def kind_of(name, numel):
+    if "bn" in name or numel <= 4096 and name.endswith(("weight", "bias")) and "conv" not in name:
+        return "bn_w" if name.endswith("weight") else "bn_b"
+    if "linear" in name or "fc" in name:
+        return "linear"
+    return "conv"
+
+
+def run(cfg, every, trace_f, seed, epochs_override):
+    from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
+    name, method, mode, kw, ef, extra = cfg
+    epochs = epochs_override or (40 if method in ("Randomk", "Thresholdv") else 24)
+    torch.manual_seed(seed)
+    trace = every > 0 and ef
+    tr = CifarTrainer("resnet9", compress=mode, method=method, error_feedback=ef, epochs=epochs,
+                      graph=not trace, seed=seed, **kw, **extra)
+    eng = tr.ddp.engine
+    segs = eng.arena.segments
+    names = {id(p): n for n, p in tr.model.named_parameters()}
+    seg_names = [names.get(id(s.param), f"seg{s.index}") for s in segs]
+    rec = []
+    if trace:
+        # wrap each bucket's compress: ||g|| of the raw gradient before, ||e|| after
+        for b, codec in zip(eng.buckets, eng.codecs):
+            orig = codec.compress
+
+            def wrapped(g, e, step, orig=orig, b=b):
+                on = step % every == 0
+                if on:
+                    gn = [(s.index, g[s.offset - b.start:s.offset - b.start + s.numel].norm())
+                          for s in segs[b.seg_lo:b.seg_hi]]
+                out = orig(g, e, step)
+                if on:
+                    for (si, n), s in zip(gn, segs[b.seg_lo:b.seg_hi]):
+                        en = e[s.offset - b.start:s.offset - b.start + s.numel].norm()
+                        rec.append((step, si, n, en))
+                return out
+            codec.compress = wrapped
+    steps = epochs * tr.steps_per_epoch
+    t0 = time.time()
+    losses = []
+    for _ in range(steps):
+        losses.append(tr.step())
+    torch.cuda.synchronize()
+    wall = time.time() - t0
+    acc = tr.evaluate()
+    last = sum(float(v) for v in losses[-tr.steps_per_epoch:]) / tr.steps_per_epoch / tr.bs
+    out = {"run": name, "method": method, "mode": mode, **kw, "error_feedback": ef, **extra,
+           "epochs": epochs, "seed": seed, "test_acc": round(100 * acc, 2),
+           "final_train_loss": round(last, 4), "train_s": round(wall, 1)}
+    if rec:
+        by = {}
+        for step, si, gn, en in rec:
+            k = kind_of(seg_names[si], segs[si].numel)
+            by.setdefault((step, k), []).append(float(en) / max(float(gn), 1e-30))
+        steps_seen = sorted({s for s, _ in by})
+        pick = [steps_seen[int(f * (len(steps_seen) - 1))] for f in (0.1, 0.25, 0.5, 0.75, 1.0)]
+        out["e_over_g_median"] = {
+            k: {str(s): round(sorted(by[(s, k)])[len(by[(s, k)]) // 2], 2)
+                for s in pick if (s, k) in by}
+            for k in ("bn_w", "bn_b", "conv", "linear")}
+        if trace_f:
+            with open(trace_f, "a") as f:
+                for step, si, gn, en in rec:
+                    f.write(json.dumps({"run": name, "step": step, "layer": seg_names[si],
+                                        "numel": segs[si].numel, "g": float(gn),
+                                        "e": float(en)}) + "\n")
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--every", type=int, default=0, help="trace ||e||/||g|| every N steps")
+    ap.add_argument("--trace-out", default="")
+    ap.add_argument("--seeds", default="0")
+    ap.add_argument("--epochs", type=int, default=0)
+    args = ap.parse_args()
+    idx = [int(i) for i in args.only.split(",")] if args.only else range(len(RUNS))
+    for seed in [int(s) for s in args.seeds.split(",")]:
+        for i in idx:
+            print(json.dumps(run(RUNS[i], args.every, args.trace_out, seed, args.epochs)),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

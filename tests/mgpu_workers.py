@@ -25,12 +25,18 @@ def _worker(rank, world, port, fn, outdir, args, env):
         # rehearsal on a one-GPU box: every rank on cuda:0, each rank declared its own "host" so
         # RCCL accepts two ranks on one device (it then moves data over its socket transport)
         os.environ["NCCL_HOSTID"] = f"lwaaai-rank{rank}"
+    import faulthandler
+    import sys
+    # a rank stuck in a collective prints every thread's stack before the harness gives up on it
+    faulthandler.dump_traceback_later(int(os.environ.get("LWAAAI_TEST_STACK_AFTER", "100")),
+                                      exit=False, file=sys.stderr)
     res = None
     try:
         from layer_wise_aaai20_amd.parallel.comm import bind_rank_device
         dev = bind_rank_device(rank)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
         res = ("ok", fn(rank, world, dev, *args))
+        faulthandler.cancel_dump_traceback_later()
     except Exception:  # noqa: BLE001
         res = ("err", traceback.format_exc())
     finally:
@@ -148,10 +154,11 @@ def train_graph_vs_eager(rank, world, dev, compress, method, ef, kw, steps=8):
         assert tr.ddp.engine._native is not None
         g = torch.Generator(device=dev).manual_seed(77 + rank)
         losses = []
-        for _ in range(steps):
+        for i in range(steps):
             x = torch.randint(0, 256, (8, 64, 64, 3), dtype=torch.uint8, device=dev, generator=g)
             t = torch.randint(0, 1000, (8,), device=dev, generator=g)
             losses.append(float(tr.step(x, t)))
+            print(f"[rank {rank}] graph={graph} step {i} loss {losses[-1]:.4f}", flush=True)
         torch.cuda.synchronize(dev)
         p = torch.cat([q.detach().float().reshape(-1) for q in tr.ddp.module.parameters()])
         allp = _gather_cpu(p)

@@ -393,3 +393,57 @@ def test_conv3_direct_matches_gemm_path(N, H, monkeypatch):
     dx = CV.conv_dgrad(dy, w, (H, H), 1, 1)
     assert dx.shape == x.shape
     _close(dx, xf.grad, 1e-2)
+
+
+# the tap-reuse 3x3/1 kernel (csrc/conv3tap.hip): every stride-1 3x3 shape of ResNet-50 (batch
+# reduced; 28 / 14 / 7 px tiles span images), the CIFAR nets, and both channel tiles (64, 128)
+TAP_SHAPES = [(3, 64, 64, 56), (3, 128, 128, 28), (3, 256, 256, 14), (5, 512, 512, 7),
+              (4, 64, 128, 32), (4, 128, 256, 16), (6, 256, 512, 8), (9, 512, 512, 4),
+              (2, 32, 64, 14), (4, 96, 128, 28)]
+
+
+@pytest.mark.parametrize("shape", TAP_SHAPES, ids=[str(s) for s in TAP_SHAPES])
+def test_conv3_tap_fwd_stats_dgrad(shape):
+    """k_conv3_tap vs fp32 F.conv2d: forward (and its column statistics of the stored bf16
+    values, one row per 224-pixel tile) and the data gradient through the flipped weight."""
+    from layer_wise_aaai20_amd.ops._ext import load
+    N, C, Co, H = shape
+    lib = load()
+    x, w = _inputs(N, C, Co, H, 3, 7)
+    op, K, _ = CV.pack_fwd_weight(w)
+    y, st = lib.conv3_tap(x, op, Co, True)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=CL)
+    _close(y, ref, 1e-2)
+    yb = y.float().permute(0, 2, 3, 1).reshape(-1, Co)
+    assert st.shape[1:] == (2, Co)
+    torch.testing.assert_close(st[:, 0].sum(0), yb.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[:, 1].sum(0), (yb * yb).sum(0), rtol=1e-4, atol=1e-2)
+    # data gradient: dx = conv(dy, W') with W'[ci][r][s][co] = w[co][ci][2-r][2-s]
+    dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
+    xf = x.float().requires_grad_()
+    F.conv2d(xf, w.float(), padding=1).backward(dy.float())
+    dx, _ = lib.conv3_tap(dy, CV.tap_dgrad_weight(w), C, False)
+    _close(dx, xf.grad, 1e-2)
+
+
+def test_conv3_tap_is_a_tuner_candidate(monkeypatch):
+    """Forced through the tuner (conv_fwd / conv_dgrad), the tap kernel gives the GEMM path's
+    results to bf16 rounding."""
+    x, w = _inputs(2, 64, 64, 56, 3, 3)
+    calls = []
+    orig = CV.TUNER.pick
+
+    def pick(key, run, cands, default):
+        c = [c for c in cands if (c == CV.CONV3_TAP or (isinstance(c, tuple) and c[0] == "tap"))]
+        calls.append(bool(c))
+        return c[0] if c else orig(key, run, cands, default)
+    monkeypatch.setattr(CV.TUNER, "pick", pick)
+    y, st = CV.conv_fwd(x, w, 1, 1, stats=True)
+    _close(y, F.conv2d(x.float(), w.float(), padding=1), 1e-2)
+    dy = torch.randn_like(y.float()).bfloat16().contiguous(memory_format=CL)
+    dx = CV.conv_dgrad(dy, w, (56, 56), 1, 1)
+    xf = x.float().requires_grad_()
+    F.conv2d(xf, w.float(), padding=1).backward(dy.float())
+    _close(dx, xf.grad, 1e-2)
+    assert calls == [True, True]

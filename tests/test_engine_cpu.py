@@ -209,3 +209,49 @@ def test_direct_arena_gradients_count_once_per_step():
             assert launched and all(launched), launched
     finally:
         _DirectLinear.apply = staticmethod(apply)
+
+
+def test_dense_below_sends_small_tensors_whole():
+    """``dense_below`` (opt-in EF fix): segments of at most that many elements keep every
+    element; larger ones keep the reference count."""
+    from layer_wise_aaai20_amd.compress.codecs import TopkCodec, RandkCodec
+    from layer_wise_aaai20_amd.compress.plan import SegPlan
+    plan = SegPlan([0, 64], [64, 10000])
+    c = TopkCodec(plan, 1, 0, K=0.01, dense_below=4096)
+    assert c.keep.tolist() == [64, ref.topk_keep_count(10000, 0.01)]
+    g = torch.randn(10064)
+    ef = torch.zeros(10064)
+    send = c.compress(g.clone(), ef, 0)
+    out = torch.zeros(10064)
+    c.decompress(send, None, out)
+    assert torch.equal(out[:64], g[:64])                       # small: all of it
+    assert int((out[64:] != 0).sum()) == c.keep[1]
+    assert float(ef[:64].abs().sum()) == 0.0
+    r = RandkCodec(plan, 1, 0, K=0.01, dense_below=100)
+    assert r.keep.tolist()[0] == 64
+
+
+def test_momentum_correction_accumulates_velocity_and_masks():
+    """DGC momentum correction: u = m·u + g; the residual accumulates u; sent coordinates have
+    their velocity zeroed; decoded + e_new == e_old + u (what was sent is exactly removed)."""
+    torch.manual_seed(0)
+    net = small_net()
+    eng = GradSyncEngine(list(net.named_parameters()), mode="layerwise", method="Topk", K=0.05,
+                         error_feedback=True, momentum_correction=0.9)
+    u_prev = torch.zeros_like(eng.arena.grad)
+    for _ in range(4):
+        g = torch.zeros(eng.arena.numel)
+        for s in eng.arena.segments:
+            g[s.offset:s.offset + s.numel] = torch.randn(s.numel)
+        e_old = eng.ef.clone()
+        eng.arena.grad.copy_(g)
+        eng.sync_now()
+        u_expect = 0.9 * u_prev + g
+        sent = eng.arena.grad                                     # world 1: decoded = sent
+        torch.testing.assert_close(sent + eng.ef, e_old + u_expect, rtol=1e-5, atol=1e-6)
+        # velocity zeroed exactly where something was sent (residual zeroed)
+        torch.testing.assert_close(eng.mom, u_expect * (eng.ef != 0), rtol=0, atol=0)
+        u_prev = eng.mom.clone()
+    with pytest.raises(ValueError):
+        GradSyncEngine(list(net.named_parameters()), mode="layerwise", method="Topk", K=0.05,
+                       error_feedback=False, momentum_correction=0.9)

@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--no-fused", action="store_true", help="disable fused HIP nn kernels")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
-    ap.add_argument("--acc-steps", type=int, default=300,
+    ap.add_argument("--acc-steps", type=int, default=1000,
                     help="after the timed run: train a fresh ResNet-50 with the same compression "
                          "this many steps at 128 px and report its held-out top-1 "
                          "(train/accuracy.py); 0 = not measured")
@@ -110,6 +110,23 @@ class _Heartbeat:
 
     def stop(self) -> None:
         self._stop.set()
+
+
+def _reference_points(steps: int) -> str:
+    """Reference points for the printed top-1, measured at the same step budget over several
+    seeds (profiles/r4/accuracy_reference.json, written by scripts/accuracy_r50.py runs)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r4",
+                        "accuracy_reference.json")
+    try:
+        with open(path) as f:
+            ref = json.load(f)
+    except (OSError, ValueError):
+        return ""
+    if int(ref.get("steps", -1)) != int(steps):
+        return ""
+    parts = [f"{k}: {v['mean']:.1f}% (seeds {', '.join(f'{x:.1f}' for x in v['top1'])})"
+             for k, v in ref.get("methods", {}).items()]
+    return "; reference points at this budget, " + "; ".join(parts) + f" ({path[-39:]})"
 
 
 def main():
@@ -223,10 +240,11 @@ def main():
         "top1": acc["top1"] if acc else None,
         "top1_note": (f"held-out top-1 (%) of a fresh ResNet-50 trained {acc['steps']} steps with "
                       f"the same compression at {acc['image_size']} px, {acc['per_gpu_batch']}/GPU "
-                      f"(linear LR warm-up, graph step) on the class-conditional synthetic task; "
+                      f"(linear LR warm-up, graph step, kernel choices pinned by the shipped "
+                      f"gfx950 tuning table) on the class-conditional synthetic task; "
                       f"chance 0.1%; top-5 {acc['top5']}%; train loss {acc['loss_first20']} -> "
-                      f"{acc['loss_last20']} (train/accuracy.py)" if acc else
-                      "not measured (--acc-steps 0)"),
+                      f"{acc['loss_last20']} (train/accuracy.py)" + _reference_points(acc['steps'])
+                      if acc else "not measured (--acc-steps 0)"),
         "hip_graph": graphed,
         "comm": {"backend": dist.get_backend() if world > 1 else "none (1 rank)",
                  "world_size": dist.get_world_size() if world > 1 else 1,
@@ -255,6 +273,8 @@ def main():
             with open(args.json_out, "w") as f:
                 json.dump(line, f)
     if world > 1:
+        from layer_wise_aaai20_amd.parallel import comm as _comm
+        _comm.shutdown_native()           # local aborts first: no teardown waits on a peer
         dist.destroy_process_group()
 
 

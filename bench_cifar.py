@@ -95,6 +95,8 @@ def main():
         if rank == 0:
             print(json.dumps(line), flush=True)
     if world > 1:
+        from layer_wise_aaai20_amd.parallel import comm as _comm
+        _comm.shutdown_native()           # local aborts first: no teardown waits on a peer
         dist.destroy_process_group()
 
 

@@ -1217,6 +1217,45 @@ std::tuple<Tensor, Tensor> conv3_tap(Tensor x, Tensor w, int64_t Co, bool want_s
   return {y, st};
 }
 
+// Weight gradient of the tap-reuse conv (conv3tap.hip k_conv3_tap_wgrad): dy [N, Co, H, W] and
+// x [N, C, H, W] bf16 channels_last; returns fp32 dW in [Co][3][3][C] memory order (a channels_last
+// [Co, C, 3, 3] tensor), written into / accumulated onto `out` when given.
+Tensor conv3_tap_wgrad(Tensor dy, Tensor x, c10::optional<Tensor> out, bool accumulate) {
+  const c10::DeviceGuard guard(x.device());
+  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(dy, at::kBFloat16, "dy");
+  TORCH_CHECK(x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4 &&
+              x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+              dy.is_contiguous(at::MemoryFormat::ChannelsLast), "x, dy: channels_last 4-D");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), Co = dy.size(1);
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == H && dy.size(3) == W, "dy / x shapes");
+  TORCH_CHECK(lw::conv3_tap_ok((int)C, (int)Co, (int)H, (int)W), "conv3_tap_wgrad: geometry");
+  TORCH_CHECK(x.numel() * 2 < (1LL << 31) && dy.numel() * 2 < (1LL << 31), "operand > 2 GiB");
+  check_aligned16(x.data_ptr(), "x");
+  check_aligned16(dy.data_ptr(), "dy");
+  Tensor o;
+  if (out.has_value() && out->defined()) {
+    o = *out;
+    check_dtype(o, at::kFloat, "out");
+    TORCH_CHECK(o.is_cuda() && o.numel() == Co * 9 * C, "out: Co*9*C floats");
+    TORCH_CHECK(o.is_contiguous() || o.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "out: dense [Co][3][3][C] memory");
+    if (o.dim() == 4) TORCH_CHECK(o.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                                  o.size(1) == C && o.size(2) == 3, "out: channels_last [Co, C, 3, 3]");
+    check_aligned16(o.data_ptr(), "out");
+  } else {
+    o = at::empty({Co, C, 3, 3}, x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+    accumulate = false;
+  }
+  const int splits = lw::conv3_tap_wgrad_splits((int)N, (int)H, (int)W, (int)C, (int)Co);
+  Tensor part = at::empty({(int64_t)splits * Co * 9 * C}, x.options().dtype(at::kFloat));
+  lw::conv3_tap_wgrad(ptr<uint16_t>(dy), ptr<uint16_t>(x), ptr<float>(part),
+                      static_cast<float*>(o.data_ptr()), (int)N, (int)H, (int)W, (int)C, (int)Co,
+                      accumulate ? 1 : 0, cur_stream());
+  launched("conv3_tap_wgrad");
+  return o;
+}
+
 // ---------------------------------------------------------------- BN pieces for fused blocks
 // Arrival tickets of the one-launch colsum + finalize (bn.hip k_colsum_finalize), one per 64-channel
 // slice: zeroed once per device (eagerly: never created inside a graph capture) and re-armed by the
@@ -1538,6 +1577,7 @@ TORCH_LIBRARY(lwaaai, m) {
   m.def("stem_conv7(Tensor x, Tensor w) -> (Tensor, Tensor)");
   m.def("conv3_direct(Tensor x, Tensor w, bool want_stats) -> (Tensor, Tensor)");
   m.def("conv3_tap(Tensor x, Tensor w, int Co, bool want_stats) -> (Tensor, Tensor)");
+  m.def("conv3_tap_wgrad(Tensor dy, Tensor x, Tensor(a!)? out, bool accumulate) -> Tensor");
   m.def(
       "bn_bwd_dual(Tensor dy, Tensor x, Tensor x2, Tensor bits, Tensor? weight, Tensor mean, "
       "Tensor invstd, Tensor? weight2, Tensor mean2, Tensor invstd2, "
@@ -1599,6 +1639,7 @@ TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
   m.impl("stem_conv7", &stem_conv7);
   m.impl("conv3_direct", &conv3_direct);
   m.impl("conv3_tap", &conv3_tap);
+  m.impl("conv3_tap_wgrad", &conv3_tap_wgrad);
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);
   m.impl("conv_ex", &conv_ex);

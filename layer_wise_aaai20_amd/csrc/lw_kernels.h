@@ -284,6 +284,11 @@ bool conv3_tap_ok(int C, int Co, int H, int W);
 int conv3_tap_tiles_m(int N, int H, int W);
 void conv3_tap(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
                int W, int C, int Co, hipStream_t st);
+// its weight gradient: fp32 dW [Co][3][3][C] (= out, accumulated when `accumulate`), `part` a
+// [splits][Co][9][C] fp32 workspace (splits: conv3_tap_wgrad_splits)
+int conv3_tap_wgrad_splits(int N, int H, int W, int C, int Co);
+void conv3_tap_wgrad(const uint16_t* dy, const uint16_t* x, float* part, float* out, int N,
+                     int H, int W, int C, int Co, int accumulate, hipStream_t st);
 bool conv3_direct_ok(int C, int Co, int H, int W);
 void conv3_direct(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
                   int W, hipStream_t st);

@@ -86,6 +86,13 @@ void rccl_destroy(int64_t h) {
   if (h != 0) check(ncclCommDestroy(comm_of(h)), "ncclCommDestroy");
 }
 
+// Local, non-blocking teardown: ncclCommDestroy finalizes the communicator, which waits on the
+// peers (it hung a 2-rank test whose ranks tore down in different orders around c10d's own
+// destroy); ncclCommAbort frees it without any peer involvement.
+void rccl_abort(int64_t h) {
+  if (h != 0) check(ncclCommAbort(comm_of(h)), "ncclCommAbort");
+}
+
 void rccl_all_gather(int64_t h, Tensor send, Tensor recv) {
   check_dev(send, "send");
   check_dev(recv, "recv");
@@ -263,6 +270,7 @@ TORCH_LIBRARY_FRAGMENT(lwaaai, m) {
   m.def("rccl_unique_id() -> Tensor", &rccl_unique_id);
   m.def("rccl_init(Tensor uid, int world, int rank, int device) -> int", &rccl_init);
   m.def("rccl_destroy(int comm) -> ()", &rccl_destroy);
+  m.def("rccl_abort(int comm) -> ()", &rccl_abort);
   m.def("rccl_all_gather(int comm, Tensor send, Tensor(a!) recv) -> ()", &rccl_all_gather);
   m.def("rccl_all_reduce(int comm, Tensor(a!) t, int op) -> ()", &rccl_all_reduce);
   m.def("rccl_broadcast(int comm, Tensor(a!) t, int root) -> ()", &rccl_broadcast);

@@ -70,7 +70,7 @@ def _conv3_tap_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
     if c % 32 or c < 32 or not (co == 64 or co % 128 == 0) or W < 4 or 224 % W:
         return False
     rows = 224 // W
-    return (rows + 2) * (W + 2) * 64 <= 24 * 1024
+    return ((rows + 2) * W + 2) * 64 <= 24 * 1024
 
 
 def tap_dgrad_weight(w: torch.Tensor) -> torch.Tensor:
@@ -370,13 +370,20 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, pro=
 
     def run(cand, dst=None, acc=False):
         t, s = cand
+        if t == "tap":                # fp32 [Co][3][3][C], written into / added onto dst
+            o = lib.conv3_tap_wgrad(dyc, xin, dst, acc)
+            return o.permute(0, 2, 3, 1).reshape(co, -1), None
         return lib.conv_ex(xin, dyc, mode, geom, N, t, s, False, ps, pt, False, dst, acc, 0,
                            False, co)
     key = ("w", tuple(xin.shape), tuple(dyc.shape), tuple(w_shape), sh, sw, ph, pw,
            pro is not None)
     bm, bn, bk = _TILE_DIMS[1]
     default = (1, _wgrad_splits(-(-co // bm) * -(-N // bn), pix, bk))
-    cand = TUNER.pick(key, run, cands(), default)
+    cs = cands()
+    if pro is None and not c4 and (H, W) == (Ho, Wo) and \
+            _conv3_tap_fits(C, co, R, S, sh, sw, ph, pw, H, W):
+        cs.append(("tap", 0))
+    cand = TUNER.pick(key, run, cs, default)
     direct = out is not None and not c4
     if direct:
         run(cand, out, True)

@@ -159,12 +159,14 @@ class NativeRccl:
         return self.watch
 
     def close(self) -> None:
+        """Stop the watchdog and free the communicator locally (``ncclCommAbort``: it involves no
+        peer, so a teardown in any rank order cannot block)."""
         w = getattr(self, "watch", None)
         if w is not None:
             w.close()
             self.watch = None
         if self.handle:
-            self.lib.rccl_destroy(self.handle)
+            self.lib.rccl_abort(self.handle)
             self.handle = 0
 
 
@@ -282,6 +284,15 @@ def _init_native_agreed(group, device) -> Optional[NativeRccl]:
               flush=True)
         return None
     return comm
+
+
+def shutdown_native() -> None:
+    """Close every native communicator (see :meth:`NativeRccl.close`); call before the process
+    group is destroyed or the process exits."""
+    for k in list(_NATIVE):
+        c = _NATIVE.pop(k)
+        if c is not None:
+            c.close()
 
 
 def all_reduce_max(t: torch.Tensor, group=None) -> torch.Tensor:

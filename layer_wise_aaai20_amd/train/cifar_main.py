@@ -161,6 +161,7 @@ def main(argv=None):
     from ..parallel import comm
     if comm.is_dist() and owns_pg:
         comm.dist.barrier()
+        comm.shutdown_native()
         comm.dist.destroy_process_group()
     return tsv
 

@@ -35,7 +35,13 @@ import torch  # noqa: E402
 
 METHODS = {"none": dict(compress="none", method="none"),
            "topk0.1%": dict(compress="layerwise", method="Topk", K=0.001),
-           "topk0.1%+ef": dict(compress="layerwise", method="Topk", K=0.001, error_feedback=True)}
+           "topk0.1%+ef": dict(compress="layerwise", method="Topk", K=0.001, error_feedback=True),
+           # opt-in EF variants (profiles/r4/ef_root_cause.md)
+           "topk0.1%+ef+dense4k": dict(compress="layerwise", method="Topk", K=0.001,
+                                       error_feedback=True, dense_below=4096),
+           "topk0.1%+ef+mc+dense4k": dict(compress="layerwise", method="Topk", K=0.001,
+                                          error_feedback=True, dense_below=4096,
+                                          momentum_correction=True)}
 
 
 def main():
@@ -46,18 +52,21 @@ def main():
     ap.add_argument("--lr", type=float, default=2.0, help="peak LR at batch 512 (phase 0)")
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--eval-batches", type=int, default=8)
-    ap.add_argument("--methods", default=",".join(METHODS))
+    ap.add_argument("--methods", default="none,topk0.1%,topk0.1%+ef")
+    ap.add_argument("--seeds", default="0", help="comma list: model-init seeds")
     args = ap.parse_args()
     from layer_wise_aaai20_amd.train.accuracy import short_run_top1
-    for name in args.methods.split(","):
+    runs = [(seed, name) for seed in [int(v) for v in args.seeds.split(",")]
+            for name in args.methods.split(",")]
+    for seed, name in runs:
         t0 = time.time()
         r = short_run_top1("cuda:0", steps=args.steps, size=args.size, batch=args.batch,
                            peak_lr_512=args.lr, warmup=args.warmup,
-                           eval_batches=args.eval_batches, **METHODS[name])
-        print(json.dumps(dict(method=name, chance_top1=0.1, wall_s=round(time.time() - t0, 1),
+                           eval_batches=args.eval_batches, seed=seed, **METHODS[name])
+        print(json.dumps(dict(method=name, seed=seed, chance_top1=0.1,
+                              wall_s=round(time.time() - t0, 1),
                               data="synthetic class-conditional (bench.py distribution), "
                                    "random init", **r)), flush=True)
-
 
 if __name__ == "__main__":
     main()

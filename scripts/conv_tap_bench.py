@@ -48,10 +48,13 @@ def main():
         wf = CV.tap_dgrad_weight(w)
         t_f = timeit(lambda: lib.conv3_tap(x, op, Co, True))
         t_d = timeit(lambda: lib.conv3_tap(dy, wf, C, False))
+        dw = torch.zeros(Co, C, 3, 3, device="cuda").contiguous(memory_format=CL)
+        t_w = timeit(lambda: lib.conv3_tap_wgrad(dy, x, dw, True))
         CV.CONV3_TAP_ON = False
         try:
             g_f = timeit(lambda: CV.conv_fwd(x, w, 1, 1, wpack=(op, 9 * C, 3), stats=True))
             g_d = timeit(lambda: CV.conv_dgrad(dy, w, (H, H), 1, 1))
+            g_w = timeit(lambda: CV.conv_wgrad(dy, x, tuple(w.shape), 1, 1, out=dw))
         finally:
             CV.CONV3_TAP_ON = True
         name = f"{tag} x({N},{C},{H},{H})->{Co}"
@@ -59,6 +62,8 @@ def main():
               f"{flops / g_f / 1e6:6.0f}", flush=True)
         print(f"{name:28s} {'dgrad':5s} {t_d:8.1f} {flops / t_d / 1e6:6.0f} {g_d:8.1f} "
               f"{flops / g_d / 1e6:6.0f}", flush=True)
+        print(f"{name:28s} {'wgrad':5s} {t_w:8.1f} {flops / t_w / 1e6:6.0f} {g_w:8.1f} "
+              f"{flops / g_w / 1e6:6.0f}", flush=True)
 
 
 if __name__ == "__main__":

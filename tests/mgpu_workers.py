@@ -44,13 +44,14 @@ def _worker(rank, world, port, fn, outdir, args, env):
             pickle.dump(res, f)
         try:
             from layer_wise_aaai20_amd.parallel import comm
-            for c in list(comm._NATIVE.values()):
-                if c is not None:
-                    c.close()
-            if dist.is_initialized():
-                dist.destroy_process_group()
+            comm.shutdown_native()
         except Exception:  # noqa: BLE001
             pass
+        # the result is on disk: leave without c10d's teardown, whose NCCL communicator
+        # finalization waits on the peers
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 def run_world(fn, world, args=(), env=None):
@@ -87,6 +88,15 @@ def exchange_vs_oracle(rank, world, dev, mode, method, ef, kw, steps=3):
     eng = GradSyncEngine(list(net.named_parameters()), mode=mode, method=method,
                          error_feedback=ef, **kw)
     assert eng._native is not None, "native RCCL communicator not in use"
+    sent = {}
+    for bi, codec in enumerate(eng.codecs):          # keep each bucket's payload of the step
+        orig = codec.compress
+
+        def grab(g, e, step, orig=orig, bi=bi):
+            out = orig(g, e, step)
+            sent[bi] = out.detach().clone()
+            return out
+        codec.compress = grab
     errs = []
     for step in range(steps):
         g = torch.Generator(device=dev).manual_seed(1000 * step + rank)
@@ -106,21 +116,19 @@ def exchange_vs_oracle(rank, world, dev, mode, method, ef, kw, steps=3):
             errs.append(float((got.cpu() - exp).abs().max()))
             tol = 1e-5
         elif method in ("RandomDithering", "TernGrad"):
-            # the CPU mirror of every rank's quantiser (same Philox keys), decoded as the mean
+            # every rank's GPU payload, gathered and decoded by the CPU mirror codec: checks the
+            # exchange and the rank-ordered dequantise-and-average (encoding: test_kernels_gpu)
             from layer_wise_aaai20_amd.compress.codecs import make_codec
             exp = torch.zeros(eng.arena.numel)
-            for b, plan in zip(eng.buckets, eng.plans):
+            for bi, (b, plan) in enumerate(zip(eng.buckets, eng.plans)):
                 sl = slice(b.start, b.end)
-                cods = [make_codec(method, plan, world, r, **eng.codec_kw) for r in range(world)]
-                sends = [c.compress(raws[r][sl].clone(), None, step)
-                         for r, c in enumerate(cods)]
+                pays = _gather_cpu(sent[bi].to(dev))
+                cod = make_codec(method, plan, world, rank, **eng.codec_kw)
                 part = torch.zeros(b.end - b.start)
-                cods[0].decompress(sends[0], torch.cat(sends), part)
+                cod.decompress(pays[rank], torch.cat(pays), part)
                 exp[sl] = part
-            diff = (got.cpu() - exp).abs()
-            # a norm summed in another order may flip a rare stochastic level by one step
-            errs.append(float((diff > 1e-6 * exp.abs().max()).float().mean()))
-            tol = 1e-4
+            errs.append(float((got.cpu() - exp).abs().max()))
+            tol = 1e-6 * float(exp.abs().max())
         elif method == "Topk":
             exp = torch.zeros(eng.arena.numel)
             for r in range(world):

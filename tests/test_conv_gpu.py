@@ -419,7 +419,10 @@ def test_conv3_tap_fwd_stats_dgrad(shape):
     assert st.shape[1:] == (2, Co)
     torch.testing.assert_close(st[:, 0].sum(0), yb.sum(0), rtol=1e-4, atol=1e-2)
     torch.testing.assert_close(st[:, 1].sum(0), (yb * yb).sum(0), rtol=1e-4, atol=1e-2)
-    # data gradient: dx = conv(dy, W') with W'[ci][r][s][co] = w[co][ci][2-r][2-s]
+    # data gradient: dx = conv(dy, W') with W'[ci][r][s][co] = w[co][ci][2-r][2-s] (its output
+    # channel tile needs C == 64 or C % 128 == 0)
+    if not (C == 64 or C % 128 == 0):
+        return
     dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
     xf = x.float().requires_grad_()
     F.conv2d(xf, w.float(), padding=1).backward(dy.float())
@@ -447,3 +450,24 @@ def test_conv3_tap_is_a_tuner_candidate(monkeypatch):
     F.conv2d(xf, w.float(), padding=1).backward(dy.float())
     _close(dx, xf.grad, 1e-2)
     assert calls == [True, True]
+
+
+@pytest.mark.parametrize("shape", TAP_SHAPES, ids=[str(s) for s in TAP_SHAPES])
+def test_conv3_tap_wgrad(shape):
+    """k_conv3_tap_wgrad (+ the fixed-order split reduce) vs fp32 torch, fresh and accumulated
+    into a channels_last fp32 arena view."""
+    from layer_wise_aaai20_amd.ops._ext import load
+    N, C, Co, H = shape
+    lib = load()
+    x, w = _inputs(N, C, Co, H, 3, 11)
+    wf = w.float().requires_grad_()
+    ref = F.conv2d(x.float(), wf, padding=1)
+    dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=CL)
+    ref.backward(dy.float())
+    dw = lib.conv3_tap_wgrad(dy, x, None, False)
+    assert dw.shape == (Co, C, 3, 3) and dw.is_contiguous(memory_format=CL)
+    _close(dw, wf.grad, 2e-3)
+    base = torch.randn(Co, C, 3, 3, device="cuda").contiguous(memory_format=CL)
+    out = base.clone()
+    lib.conv3_tap_wgrad(dy, x, out, True)
+    _close(out - base, wf.grad, 2e-3)

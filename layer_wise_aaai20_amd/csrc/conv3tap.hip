@@ -45,8 +45,13 @@ __device__ __forceinline__ void t3_wait_barrier() {
 }
 
 // BN output channels per workgroup (BN / 16 waves: 2 pixel halves x BN / 32 channel groups)
-template <int BN, bool STATS>
-__global__ __launch_bounds__(BN * 4) __attribute__((amdgpu_waves_per_eu(BN == 128 ? 4 : 2)))
+// DEPTH: weight slices in the ring (3: prefetch 2 K-steps ahead; 4: 3 ahead, 80 KB of LDS at
+// BN = 128, still two workgroups per CU)
+// TPB > 1: TPB taps (K-steps) per barrier, ring of 2·TPB weight slices (the next TPB prefetched
+// while the current TPB are computed), one s_waitcnt vmcnt(0) + barrier per TPB steps.
+template <int BN, bool STATS, int DEPTH = T3_NWS, int TPB = 1>
+__global__ __launch_bounds__(BN * 4)
+__attribute__((amdgpu_waves_per_eu(BN == 128 && 2 * T3_PATCH + DEPTH * BN * 64 <= 81920 ? 4 : 2)))
 void k_conv3_tap(const uint16_t* __restrict__ x,
                                                          const uint16_t* __restrict__ w,
                                                          uint16_t* __restrict__ y,
@@ -57,7 +62,8 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
   constexpr int NWAVE = BN / 16;
   constexpr int NPJ = T3_PATCH / (NWAVE * 1024);   // patch DMA instructions per thread
   constexpr int WSL = BN * 64;                     // bytes per weight slice (BN rows x 32 k)
-  constexpr int LDS = 2 * T3_PATCH + T3_NWS * WSL;
+  constexpr int LDS = 2 * T3_PATCH + DEPTH * WSL;
+  constexpr int AH = DEPTH - 1;                    // K-steps of weight prefetch
   constexpr int LDH = BN + 8;                      // bf16 staging row (epilogue)
   static_assert(T3_M * LDH * 2 <= LDS, "epilogue staging fits the ring");
   static_assert(NT * 16 * 4 <= LDS, "statistics fold fits");
@@ -170,12 +176,40 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // ---- prologue: patch of chunk 0, weight slices 0 and 1
+  if constexpr (TPB > 1) {
+    static_assert(DEPTH == 2 * TPB, "ring of two super-steps");
+    issue_patch(0, 0);
+#pragma unroll
+    for (int q = 0; q < TPB; ++q) issue_w(q, q);
+    t3_wait_barrier<0>();
+#pragma unroll 1
+    for (int base = 0; base < S; base += TPB) {
+      const int half = (base / TPB) & 1;             // ring half holding this super-step
+#pragma unroll
+      for (int q = 0; q < TPB; ++q)
+        if (base + TPB + q < S) issue_w(base + TPB + q, (half ^ 1) * TPB + q);
+#pragma unroll
+      for (int q = 0; q < TPB; ++q) {
+        const int s2 = base + q, c2 = s2 / 9;
+        if (s2 < S && s2 - c2 * 9 == 4 && c2 + 1 < NC) issue_patch(c2 + 1, (c2 + 1) & 1);
+      }
+#pragma unroll
+      for (int q = 0; q < TPB; ++q) {
+        const int s2 = base + q;
+        if (s2 < S) {
+          const int c2 = s2 / 9, t2 = s2 - c2 * 9;
+          compute(lds + (c2 & 1) * T3_PATCH, lds + 2 * T3_PATCH + (half * TPB + q) * WSL, t2 / 3,
+                  t2 % 3);
+        }
+      }
+      t3_wait_barrier<0>();
+    }
+  } else {
+  // ---- prologue: patch of chunk 0, weight slices 0 .. AH-1 (S >= 9 > AH)
   issue_patch(0, 0);
-  issue_w(0, 0);
-  if (S > 1) issue_w(1, 1);
-  if (S > 1) t3_wait_barrier<1>();
-  else t3_wait_barrier<0>();
+#pragma unroll
+  for (int q = 0; q < AH; ++q) issue_w(q, q);
+  t3_wait_barrier<AH - 1>();                       // slice 0 and the patch landed
   int slot = 0;
 #pragma unroll 1
   for (int c = 0; c < NC; ++c) {
@@ -184,20 +218,26 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int s = c * 9 + t;
-      const bool w2 = s + 2 < S;
-      if (w2) issue_w(s + 2, slot == 0 ? 2 : slot - 1);        // (s + 2) % 3
+      // slice s + AH goes to the slot read at step s - 1 (retired by that step's barrier)
+      if (s + AH < S) issue_w(s + AH, slot == 0 ? DEPTH - 1 : slot - 1);
       if (t == 4 && next_chunk) issue_patch(c + 1, (c + 1) & 1);
       compute(P, lds + 2 * T3_PATCH + slot * WSL, t / 3, t % 3);
-      // DMAs issued after slice s + 1 may stay in flight (loads retire in order)
-      if ((t == 4 || t == 5) && next_chunk) {
-        if (w2) t3_wait_barrier<NPJ + 1>();
+      // wait for slice s + 1 only: the DMAs issued after it (later slices, and the next
+      // chunk's patch when it was issued within the last AH steps) may stay in flight
+      const int later = (s + 2 < S ? 1 : 0) + (AH >= 3 && s + 3 < S ? 1 : 0);
+      const bool pend = next_chunk && t >= 4 && t < 4 + AH;
+      if (pend) {
+        if (later == 2) t3_wait_barrier<NPJ + 2>();
+        else if (later == 1) t3_wait_barrier<NPJ + 1>();
         else t3_wait_barrier<NPJ>();
       } else {
-        if (w2) t3_wait_barrier<1>();
+        if (later == 2) t3_wait_barrier<2>();
+        else if (later == 1) t3_wait_barrier<1>();
         else t3_wait_barrier<0>();
       }
-      slot = slot == 2 ? 0 : slot + 1;
+      slot = slot == DEPTH - 1 ? 0 : slot + 1;
     }
+  }
   }
 
   // ---- epilogue: bf16 tile staged in LDS, 16-byte stores, column statistics
@@ -284,16 +324,33 @@ void conv3_tap(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, 
   const int tiles = conv3_tap_tiles_m(N, H, W) * (Co / bn);
   const uint32_t xb = (uint32_t)((int64_t)NH * W * C * 2);
   const uint32_t wb = (uint32_t)((int64_t)Co * 9 * C * 2);
-#define LW_T3(BNV, ST)                                                                             \
-  hipLaunchKernelGGL((k_conv3_tap<BNV, ST>), dim3(tiles), dim3(BNV * 4), 0, st, x, w, y, stats,    \
-                     NH, H, W, C, Co, xb, wb)
-  if (bn == 128) {
-    if (stats) LW_T3(128, true);
-    else LW_T3(128, false);
-  } else {
-    if (stats) LW_T3(64, true);
-    else LW_T3(64, false);
+  // LWAAAI_TAP_VAR (A/B): 3 = ring of 3 slices, barrier per tap (default); 4 = ring of 4;
+  // 22 / 33 = 2 / 3 taps per barrier (ring 4 / 6)
+  static const int var = [] {
+    const char* e = getenv("LWAAAI_TAP_VAR");
+    const int v = e ? atoi(e) : 3;
+    return v == 4 || v == 22 || v == 33 ? v : 3;
+  }();
+#define LW_T3(BNV, ST, D, T)                                                                       \
+  hipLaunchKernelGGL((k_conv3_tap<BNV, ST, D, T>), dim3(tiles), dim3(BNV * 4), 0, st, x, w, y,      \
+                     stats, NH, H, W, C, Co, xb, wb)
+#define LW_T3V(D, T)                                                                               \
+  do {                                                                                             \
+    if (bn == 128) {                                                                               \
+      if (stats) LW_T3(128, true, D, T);                                                           \
+      else LW_T3(128, false, D, T);                                                                \
+    } else {                                                                                       \
+      if (stats) LW_T3(64, true, D, T);                                                            \
+      else LW_T3(64, false, D, T);                                                                 \
+    }                                                                                              \
+  } while (0)
+  switch (var) {
+    case 4: LW_T3V(4, 1); break;
+    case 22: LW_T3V(4, 2); break;
+    case 33: LW_T3V(6, 3); break;
+    default: LW_T3V(3, 1);
   }
+#undef LW_T3V
 #undef LW_T3
 }
 

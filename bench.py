@@ -273,9 +273,16 @@ def main():
             with open(args.json_out, "w") as f:
                 json.dump(line, f)
     if world > 1:
+        # the result line is out: a teardown that blocks must not turn a finished run into a
+        # hung one. faulthandler's watchdog is a C thread (it needs no GIL, which a blocked
+        # native call may hold): it ends the process if the clean teardown takes over a minute
+        import faulthandler
+        sys.stdout.flush()
+        faulthandler.dump_traceback_later(60, exit=True)
         from layer_wise_aaai20_amd.parallel import comm as _comm
-        _comm.shutdown_native()           # local aborts first: no teardown waits on a peer
+        _comm.shutdown_native()           # captured graphs released, then local aborts
         dist.destroy_process_group()
+        faulthandler.cancel_dump_traceback_later()
 
 
 if __name__ == "__main__":

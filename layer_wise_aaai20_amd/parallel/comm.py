@@ -288,7 +288,16 @@ def _init_native_agreed(group, device) -> Optional[NativeRccl]:
 
 def shutdown_native() -> None:
     """Close every native communicator (see :meth:`NativeRccl.close`); call before the process
-    group is destroyed or the process exits."""
+    group is destroyed or the process exits. Captured step graphs holding its collectives are
+    released first (``train/graphs.py release_graphs``)."""
+    if not _NATIVE:
+        return
+    import gc
+    from ..train.graphs import release_graphs
+    release_graphs()
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     for k in list(_NATIVE):
         c = _NATIVE.pop(k)
         if c is not None:

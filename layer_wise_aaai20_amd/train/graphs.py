@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import os
 import time
+import weakref
 from typing import Callable, Dict, Optional, Sequence
 
 import torch
@@ -38,6 +39,21 @@ import torch
 
 def graphs_enabled(default: bool = True) -> bool:
     return os.environ.get("LWAAAI_GRAPH", "1" if default else "0") != "0"
+
+
+_LIVE = weakref.WeakSet()      # every StepGraph, for release_graphs()
+
+
+def release_graphs() -> None:
+    """Drop every captured step graph (after draining the device). A communicator whose
+    collectives live on in a captured graph cannot be torn down: ncclCommAbort waited forever on
+    one in a 2-rank run (scripts/mgpu_probe.py), so ``comm.shutdown_native`` calls this first."""
+    live = list(_LIVE)
+    if any(sg._graphs for sg in live) and torch.cuda.is_available():
+        torch.cuda.synchronize()
+    for sg in live:
+        sg._graphs.clear()
+        sg.enabled = False
 
 
 class StepGraph:
@@ -67,6 +83,7 @@ class StepGraph:
         self._replay_t = []
         self._t_last = None
         self.choice = None        # (graph ms, eager ms) of the decision, for the logs
+        _LIVE.add(self)
 
     # ------------------------------------------------------------------ policy
     def active(self) -> bool:

@@ -67,7 +67,8 @@ def parse():
     # compressed + exchanged inline, so fewer buckets = fewer launches / collectives: 24.29 ms
     # vs 24.47-24.50 ms at the reference's 25 MB (profiles/r2_bucket_mb_graph.log)
     ap.add_argument("--bucket-mb", type=float, default=50.0)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="fp16: the fp16 build of the MFMA kernels with a static loss scale 1024")
     ap.add_argument("--no-fused", action="store_true", help="disable fused HIP nn kernels")
     ap.add_argument("--json-out", default="")
     ap.add_argument("--pool", type=int, default=4, help="distinct synthetic batches cycled")
@@ -215,7 +216,7 @@ def main():
         acc = short_run_top1(dev, steps=args.acc_steps, size=128, batch=256, rank=rank,
                              world=world, compress=args.compress, method=args.method,
                              K=args.ratio, V=args.threshold, qstates=args.qstates,
-                             error_feedback=args.ef)
+                             error_feedback=args.ef, dtype=args.dtype)
     value = world * B * args.steps / dt
     default = (args.model == "resnet50" and args.compress == "layerwise" and args.method == "Topk"
                and args.ratio == 0.001 and not args.ef)

@@ -6,6 +6,7 @@
 // choices (x0, y0, flip, cutout corner) are drawn on the host once per epoch.
 #include "common.h"
 #include "lw_kernels.h"
+#include "elem16.h"
 
 namespace lw {
 
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(256) void k_cifar_augment(const float* __restrict__
   const int xs = flip ? crop - 1 - x : x;
   float v = data[((idx[b] * C + c) * Hp + (y0 + y)) * Wp + (x0 + xs)];
   if (cutout > 0 && y >= cy && y < cy + cutout && x >= cx && x < cx + cutout) v = 0.f;
-  if (BF16) static_cast<uint16_t*>(out)[t] = __builtin_bit_cast(uint16_t, static_cast<__bf16>(v));
+  if (BF16) static_cast<uint16_t*>(out)[t] = f2h(v);
   else static_cast<float*>(out)[t] = v;
 }
 

@@ -15,9 +15,24 @@
 
 #include "lw_kernels.h"
 
+// The 16-bit element of the fused path (elem16.h): bf16 in lwaaai, fp16 in the lwaaai16 build of
+// the same sources (csrc/build.py), whose ops register under torch.ops.lwaaai16.
+#ifndef LW_OPS_NS
+#define LW_OPS_NS lwaaai
+#endif
+#ifdef LW_FP16
+#define LW_H16_TYPE at::kHalf
+#else
+#define LW_H16_TYPE at::kBFloat16
+#endif
+// one expansion step so that TORCH_LIBRARY pastes the namespace's value, not the macro name
+#define LW_LIBRARY(ns, m) TORCH_LIBRARY(ns, m)
+#define LW_LIBRARY_IMPL(ns, k, m) TORCH_LIBRARY_IMPL(ns, k, m)
+
 namespace {
 
 using at::Tensor;
+constexpr at::ScalarType kH16 = LW_H16_TYPE;
 
 // ROCm builds of PyTorch expose HIP devices as DeviceType::CUDA ("masquerading").
 inline hipStream_t cur_stream() {
@@ -342,7 +357,7 @@ void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tens
   }
   if (pb.has_value() && pb->defined()) {
     check_cuda(*pb, "pb");
-    TORCH_CHECK(pb->scalar_type() == at::kBFloat16 && pb->numel() == p.numel(),
+    TORCH_CHECK(pb->scalar_type() == kH16 && pb->numel() == p.numel(),
                 "pb must be a bf16 tensor with p's layout");
     check_aligned16(pb->data_ptr(), "pb");
     a.pb = reinterpret_cast<uint16_t*>(pb->data_ptr());
@@ -369,11 +384,11 @@ void cifar_augment(Tensor data, Tensor idx, Tensor prm, int64_t offset, int64_t 
                   out.size(2) == crop && out.size(3) == crop &&
                   out.is_contiguous(at::MemoryFormat::ChannelsLast),
               "cifar_augment: out must be a channels_last [B, C, crop, crop] GPU tensor");
-  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16,
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == kH16,
               "cifar_augment: out must be float32 or bfloat16");
   lw::cifar_augment(ptr<float>(data), ptr<int64_t>(idx), ptr<int32_t>(prm), out.data_ptr(),
                     (int)B, (int)C, (int)Hp, (int)Wp, (int)crop, (int)cutout, offset,
-                    out.scalar_type() == at::kBFloat16, cur_stream());
+                    out.scalar_type() == kH16, cur_stream());
   launched("cifar_augment");
 }
 
@@ -382,7 +397,7 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
   check_cuda(in, "in");
   check_dtype(in, at::kByte, "in");
   TORCH_CHECK(mean.size() == 3 && stdv.size() == 3, "mean/std need 3 channels");
-  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat,
+  TORCH_CHECK(out.scalar_type() == kH16 || out.scalar_type() == at::kFloat,
               "out must be bf16 or fp32");
   // `out` is an NCHW tensor in channels_last memory == the NHWC byte order of `in`
   TORCH_CHECK(out.dim() == 4 && out.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -392,7 +407,7 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
   const float m[3] = {(float)mean[0], (float)mean[1], (float)mean[2]};
   const float s[3] = {(float)stdv[0], (float)stdv[1], (float)stdv[2]};
   if (out.size(1) == 4) {                    // 4-channel (zero-padded) bf16 stem input
-    TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.numel() / 4 * 3 == in.numel() &&
+    TORCH_CHECK(out.scalar_type() == kH16 && out.numel() / 4 * 3 == in.numel() &&
                 out.numel() % 4 == 0, "4-channel out: bf16 with in.numel()/3 pixels");
     lw::normalize_u8_c4(ptr<uint8_t>(in), ptr<uint16_t>(out), in.numel() / 3, m, s, cur_stream());
     launched("normalize_u8_c4");
@@ -400,7 +415,7 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
   }
   TORCH_CHECK(out.numel() == in.numel(), "out/in size mismatch");
   lw::normalize_u8(ptr<uint8_t>(in), out.data_ptr(), in.numel(), m, s,
-                   out.scalar_type() == at::kBFloat16, cur_stream());
+                   out.scalar_type() == kH16, cur_stream());
   launched("normalize_u8");
 }
 
@@ -408,7 +423,7 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
 Tensor gap_fwd(Tensor x) {
   const c10::DeviceGuard guard(x.device());
   TORCH_CHECK(x.is_cuda(), "x must be a GPU tensor");
-  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(x, kH16, "x");
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "x must be a channels_last NCHW tensor");
   const int64_t N = x.size(0), C = x.size(1), HW = x.size(2) * x.size(3);
@@ -450,7 +465,7 @@ std::tuple<Tensor, Tensor> relu_bias_bwd(Tensor dy, c10::optional<Tensor> y,
                                          c10::optional<Tensor> db_out) {
   const c10::DeviceGuard guard(dy.device());
   TORCH_CHECK(dy.is_cuda(), "dy must be a GPU tensor");
-  check_dtype(dy, at::kBFloat16, "dy");
+  check_dtype(dy, kH16, "dy");
   const bool cl = dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(cl || (dy.dim() == 2 && dy.is_contiguous()), "dy: channels_last NCHW or [M, C]");
   const int64_t C = dy.size(1), M = dy.numel() / std::max<int64_t>(C, 1);
@@ -458,7 +473,7 @@ std::tuple<Tensor, Tensor> relu_bias_bwd(Tensor dy, c10::optional<Tensor> y,
   check_aligned16(dy.data_ptr(), "dy");
   const bool relu = y.has_value() && y->defined();
   if (relu) {
-    check_dtype(*y, at::kBFloat16, "y");
+    check_dtype(*y, kH16, "y");
     TORCH_CHECK(y->sizes() == dy.sizes() && y->strides() == dy.strides(), "y must match dy");
     check_aligned16(y->data_ptr(), "y");
   }
@@ -485,13 +500,13 @@ Tensor gap_bwd(Tensor dy, int64_t H, int64_t W) {
   const c10::DeviceGuard guard(dy.device());
   check_cuda(dy, "dy");
   TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous(), "dy must be a contiguous [N, C] tensor");
-  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kFloat,
+  TORCH_CHECK(dy.scalar_type() == kH16 || dy.scalar_type() == at::kFloat,
               "dy must be bf16 or fp32");
   const int64_t N = dy.size(0), C = dy.size(1);
   TORCH_CHECK(C % 8 == 0 && H > 0 && W > 0 && N * H * W * (C / 8) < (1LL << 31),
               "gap_bwd: C % 8 == 0 and N*H*W*C/8 < 2^31");
   check_aligned16(dy.data_ptr(), "dy");
-  Tensor dx = at::empty({N, C, H, W}, dy.options().dtype(at::kBFloat16),
+  Tensor dx = at::empty({N, C, H, W}, dy.options().dtype(kH16),
                         at::MemoryFormat::ChannelsLast);
   lw::gap_bwd(dy.data_ptr(), dy.scalar_type() == at::kFloat, ptr<uint16_t>(dx), (int)N,
               (int)(H * W), (int)C, cur_stream());
@@ -504,7 +519,7 @@ void check_nhwc(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.dim() == 4 ? t.is_contiguous(at::MemoryFormat::ChannelsLast) : t.is_contiguous(),
               name, " must be channels_last (4-D) or contiguous (2-D)");
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name,
+  TORCH_CHECK(t.scalar_type() == kH16 || t.scalar_type() == at::kFloat, name,
               " must be bf16 or fp32");
   check_aligned16(t.data_ptr(), name);
 }
@@ -537,7 +552,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_fwd(Tensor x, c10::optional<Tensor
   a.y = y.data_ptr();
   a.M = M;
   a.C = (int)C;
-  a.bf16 = x.scalar_type() == at::kBFloat16;
+  a.bf16 = x.scalar_type() == kH16;
   a.training = training;
   a.relu = relu;
   a.eps = (float)eps;
@@ -646,7 +661,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_bwd(Tensor dy, Tensor x, c10::opti
   a.dres = need_dres ? dres.data_ptr() : nullptr;
   a.M = M;
   a.C = (int)C;
-  a.bf16 = x.scalar_type() == at::kBFloat16;
+  a.bf16 = x.scalar_type() == kH16;
   a.training = training;
   a.relu = relu;
   a.gamma = optr<float>(weight);
@@ -676,7 +691,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn_bwd_dual(
   check_nhwc(x, "x");
   check_nhwc(x2, "x2");
   check_nhwc(dy, "dy");
-  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(x, kH16, "x");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.sizes() == x.sizes() &&
               x2.scalar_type() == x.scalar_type() && x2.sizes() == x.sizes(),
               "dy, x and x2 must match");
@@ -745,7 +760,7 @@ static void set_bstats(lw::GemmArgs& g, const c10::optional<Tensor>& bx,
   if (!(bx.has_value() && bx->defined())) return;
   TORCH_CHECK(out_bf16 && ldc == N && N % 8 == 0,
               "backward statistics need a bf16 output with ldc == N and N % 8 == 0");
-  check_dtype(*bx, at::kBFloat16, "bst_x");
+  check_dtype(*bx, kH16, "bst_x");
   TORCH_CHECK(bx->is_cuda() && (bx->is_contiguous() ||
               bx->is_contiguous(at::MemoryFormat::ChannelsLast)) && bx->numel() >= out_rows * N,
               "bst_x must be a dense [rows, N] bf16 tensor");
@@ -780,8 +795,8 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
                                    c10::optional<Tensor> bst_bits) {
   const c10::DeviceGuard guard(A.device());
   TORCH_CHECK(A.is_cuda() && B.is_cuda(), "gemm needs GPU tensors");
-  check_dtype(A, at::kBFloat16, "A");
-  check_dtype(B, at::kBFloat16, "B");
+  check_dtype(A, kH16, "A");
+  check_dtype(B, kH16, "B");
   TORCH_CHECK(A.is_contiguous() && B.is_contiguous(), "gemm operands must be contiguous");
   check_aligned16(A.data_ptr(), "A");
   check_aligned16(B.data_ptr(), "B");
@@ -796,7 +811,7 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
               "tile id");
   if (ldc <= 0) ldc = N;
   TORCH_CHECK(ldc >= N, "ldc must be >= N");
-  const auto odt = out_bf16 ? at::kBFloat16 : at::kFloat;
+  const auto odt = out_bf16 ? kH16 : at::kFloat;
   Tensor C;
   if (out.has_value() && out->defined()) {
     C = *out;
@@ -829,7 +844,7 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
   g.accumulate = accumulate;
   if (addend.has_value() && addend->defined()) {
     TORCH_CHECK(out_bf16, "addend needs a bf16 output");
-    check_dtype(*addend, at::kBFloat16, "addend");
+    check_dtype(*addend, kH16, "addend");
     TORCH_CHECK(addend->numel() >= (M - 1) * ldc + N, "addend too small for [M, ldc]");
     TORCH_CHECK(addend->is_contiguous(at::MemoryFormat::ChannelsLast) || addend->is_contiguous(),
                 "addend must be dense");
@@ -915,7 +930,7 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
 Tensor pack_dgrad_kc(Tensor w, std::vector<int64_t> cls, int64_t sh, int64_t sw, int64_t kmax) {
   const c10::DeviceGuard guard(w.device());
   TORCH_CHECK(w.is_cuda() && w.dim() == 4, "pack_dgrad_kc: a 4-d GPU weight");
-  check_dtype(w, at::kBFloat16, "weight");
+  check_dtype(w, kH16, "weight");
   TORCH_CHECK(w.is_contiguous(at::MemoryFormat::ChannelsLast) || (w.size(2) == 1 && w.size(3) == 1
               && w.is_contiguous()), "weight must be channels_last [Co][R][S][C] in memory");
   const int Co = (int)w.size(0), C = (int)w.size(1), R = (int)w.size(2), S = (int)w.size(3);
@@ -949,8 +964,8 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
                                    bool relu) {
   const c10::DeviceGuard guard(G.device());
   TORCH_CHECK(G.is_cuda() && Op.is_cuda(), "conv needs GPU tensors");
-  check_dtype(G, at::kBFloat16, "gathered tensor");
-  check_dtype(Op, at::kBFloat16, "operand");
+  check_dtype(G, kH16, "gathered tensor");
+  check_dtype(Op, kH16, "operand");
   TORCH_CHECK(G.is_contiguous() || G.is_contiguous(at::MemoryFormat::ChannelsLast),
               "gathered tensor must be dense NHWC");
   TORCH_CHECK(Op.is_contiguous() || Op.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -1050,7 +1065,7 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
   if (ldc <= 0) ldc = N;
   TORCH_CHECK(ldc >= N && (out_bf16 ? ldc % 8 == 0 : ldc % 4 == 0), "ldc");
   const int64_t out_rows = ga ? Nb * h.Hout * h.Wout : g.M;
-  const auto odt = out_bf16 ? at::kBFloat16 : at::kFloat;
+  const auto odt = out_bf16 ? kH16 : at::kFloat;
   if (out.has_value() && out->defined()) {
     C = *out;
     TORCH_CHECK(C.is_cuda() && C.scalar_type() == odt, "out dtype");
@@ -1090,7 +1105,7 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
   if (addend.has_value() && addend->defined()) {
     // bf16 [out_rows][ldc] added after rounding, indexed by output row (may alias `out`)
     TORCH_CHECK(ga && out_bf16 && !accumulate, "conv addend: bf16 row-gather (fwd/dgrad) output");
-    check_dtype(*addend, at::kBFloat16, "addend");
+    check_dtype(*addend, kH16, "addend");
     TORCH_CHECK(addend->is_cuda() && (addend->is_contiguous() ||
                 addend->is_contiguous(at::MemoryFormat::ChannelsLast)), "addend must be dense");
     TORCH_CHECK(addend->numel() >= (out_rows - 1) * ldc + N, "addend too small");
@@ -1146,8 +1161,8 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
 // (y [N, 64, Ho, Wo] channels_last, stats [workgroups, 2, 64]).
 std::tuple<Tensor, Tensor> stem_conv7(Tensor x, Tensor w) {
   const c10::DeviceGuard guard(x.device());
-  check_dtype(x, at::kBFloat16, "x");
-  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(x, kH16, "x");
+  check_dtype(w, kH16, "w");
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && x.size(1) == 4 &&
               x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: [N, 4, H, W] channels_last");
   TORCH_CHECK(w.is_contiguous() && w.numel() == 64 * 224, "w: packed [64][224]");
@@ -1171,8 +1186,8 @@ std::tuple<Tensor, Tensor> stem_conv7(Tensor x, Tensor w) {
 // returns (y [N, 64, H, W] channels_last, stats [N*H/8, 2, 64] or an empty tensor).
 std::tuple<Tensor, Tensor> conv3_direct(Tensor x, Tensor w, bool want_stats) {
   const c10::DeviceGuard guard(x.device());
-  check_dtype(x, at::kBFloat16, "x");
-  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(x, kH16, "x");
+  check_dtype(w, kH16, "w");
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 &&
               x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: [N, 64, H, W] channels_last");
   TORCH_CHECK(w.is_contiguous() && w.numel() == 64 * 576, "w: [64][576]");
@@ -1196,8 +1211,8 @@ std::tuple<Tensor, Tensor> conv3_direct(Tensor x, Tensor w, bool want_stats) {
 // an empty tensor).
 std::tuple<Tensor, Tensor> conv3_tap(Tensor x, Tensor w, int64_t Co, bool want_stats) {
   const c10::DeviceGuard guard(x.device());
-  check_dtype(x, at::kBFloat16, "x");
-  check_dtype(w, at::kBFloat16, "w");
+  check_dtype(x, kH16, "x");
+  check_dtype(w, kH16, "w");
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 &&
               x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: [N, C, H, W] channels_last");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -1222,8 +1237,8 @@ std::tuple<Tensor, Tensor> conv3_tap(Tensor x, Tensor w, int64_t Co, bool want_s
 // [Co, C, 3, 3] tensor), written into / accumulated onto `out` when given.
 Tensor conv3_tap_wgrad(Tensor dy, Tensor x, c10::optional<Tensor> out, bool accumulate) {
   const c10::DeviceGuard guard(x.device());
-  check_dtype(x, at::kBFloat16, "x");
-  check_dtype(dy, at::kBFloat16, "dy");
+  check_dtype(x, kH16, "x");
+  check_dtype(dy, kH16, "dy");
   TORCH_CHECK(x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4 &&
               x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
               dy.is_contiguous(at::MemoryFormat::ChannelsLast), "x, dy: channels_last 4-D");
@@ -1301,7 +1316,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stat
   a.x = x.data_ptr();
   a.M = M;
   a.C = (int)C;
-  a.bf16 = x.scalar_type() == at::kBFloat16;
+  a.bf16 = x.scalar_type() == kH16;
   a.training = true;
   a.eps = (float)eps;
   a.momentum = (float)momentum;
@@ -1338,7 +1353,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stat
 static void stem_geom(const Tensor& x, int64_t k, int64_t s, int64_t p, lw::StemArgs& a) {
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "stem input must be channels_last 4-D");
-  check_dtype(x, at::kBFloat16, "x");
+  check_dtype(x, kH16, "x");
   a.N = (int)x.size(0); a.C = (int)x.size(1); a.H = (int)x.size(2); a.W = (int)x.size(3);
   TORCH_CHECK(a.C % 8 == 0 && a.C <= kMaxBnC, "stem pool needs C % 8 == 0 and C <= ", kMaxBnC);
   // PyTorch semantics: padding at most half the window (no window lies entirely in padding)
@@ -1391,7 +1406,7 @@ Tensor relu_pool_bwd(Tensor dp, Tensor idx, Tensor x, int64_t k, int64_t s, int6
   const c10::DeviceGuard guard(x.device());
   lw::StemArgs a{};
   stem_geom(x, k, s, p, a);
-  check_dtype(dp, at::kBFloat16, "dp");
+  check_dtype(dp, kH16, "dp");
   TORCH_CHECK(dp.is_contiguous(at::MemoryFormat::ChannelsLast) && dp.size(2) == a.Ho &&
               dp.size(3) == a.Wo && dp.size(1) == a.C && dp.size(0) == a.N, "dp shape/layout");
   TORCH_CHECK(idx.numel() == dp.numel() && idx.scalar_type() == at::kByte, "idx");
@@ -1421,12 +1436,12 @@ std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x
   const c10::DeviceGuard guard(x.device());
   lw::StemArgs a{};
   stem_geom(x, k, s, p, a);
-  check_dtype(dp, at::kBFloat16, "dp");
+  check_dtype(dp, kH16, "dp");
   TORCH_CHECK(dp.is_contiguous(at::MemoryFormat::ChannelsLast) && dp.size(2) == a.Ho &&
               dp.size(3) == a.Wo && dp.size(1) == a.C && dp.size(0) == a.N, "dp shape/layout");
   TORCH_CHECK(idx.numel() == dp.numel() && idx.scalar_type() == at::kByte, "idx");
   if (pooled.has_value() && pooled->defined()) {
-    check_dtype(*pooled, at::kBFloat16, "pooled");
+    check_dtype(*pooled, kH16, "pooled");
     TORCH_CHECK(pooled->sizes() == dp.sizes() &&
                 pooled->is_contiguous(at::MemoryFormat::ChannelsLast), "pooled shape/layout");
     a.pooled = pooled->data_ptr();
@@ -1475,7 +1490,7 @@ Tensor bn_apply(Tensor x, Tensor scale_shift, c10::optional<Tensor> res,
   a.y = y.data_ptr();
   a.M = x.numel() / C;
   a.C = (int)C;
-  a.bf16 = x.scalar_type() == at::kBFloat16;
+  a.bf16 = x.scalar_type() == kH16;
   a.relu = relu;
   a.scale = ptr<float>(scale_shift);
   a.shift = a.scale + C;
@@ -1519,7 +1534,7 @@ void selftest_spin(Tensor any, double ms) {
 
 }  // namespace
 
-TORCH_LIBRARY(lwaaai, m) {
+LW_LIBRARY(LW_OPS_NS, m) {
   m.def("workspace_bytes(int n_small, int n_large, int n_tasks) -> int", &workspace_bytes);
   m.def("selftest_bad_launch(Tensor any) -> ()");
   m.def("selftest_spin(Tensor any, float ms) -> ()");
@@ -1615,7 +1630,7 @@ TORCH_LIBRARY(lwaaai, m) {
       "Tensor(b!)? dbeta_out=None, Tensor? pooled=None) -> (Tensor, Tensor, Tensor)");
 }
 
-TORCH_LIBRARY_IMPL(lwaaai, CUDA, m) {
+LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("selftest_bad_launch", &selftest_bad_launch);
   m.impl("selftest_spin", &selftest_spin);
   m.impl("select_compress", &select_compress);

@@ -11,17 +11,12 @@
 // a finalize kernel folds them in fp64.
 #include "common.h"
 #include "lw_kernels.h"
+#include "elem16.h"
 #include <cstdlib>
 
 namespace lw {
 
 constexpr int BNT = 256;
-
-__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
-// hardware round-to-nearest-even conversion (v_cvt_pk_bf16_f32), same as gemm.hip
-__device__ __forceinline__ uint16_t f2bf_rne(float f) {
-  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
-}
 
 template <typename T> struct V8;
 template <> struct V8<uint16_t> {
@@ -34,8 +29,8 @@ template <> struct V8<uint16_t> {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      f[2 * k] = __uint_as_float(w[k] << 16);
-      f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+      f[2 * k] = hlo(w[k]);
+      f[2 * k + 1] = hhi(w[k]);
     }
   }
   static __device__ __forceinline__ void load(const uint16_t* p, float f[8]) {
@@ -43,15 +38,15 @@ template <> struct V8<uint16_t> {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      f[2 * k] = __uint_as_float(w[k] << 16);
-      f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+      f[2 * k] = hlo(w[k]);
+      f[2 * k + 1] = hhi(w[k]);
     }
   }
   static __device__ __forceinline__ void store(uint16_t* p, const float f[8]) {
     uint32_t w[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      w[k] = (uint32_t)f2bf_rne(f[2 * k]) | ((uint32_t)f2bf_rne(f[2 * k + 1]) << 16);
+      w[k] = (uint32_t)f2h(f[2 * k]) | ((uint32_t)f2h(f[2 * k + 1]) << 16);
     *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 };
@@ -442,7 +437,7 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ rows, 
 __device__ __forceinline__ uint8_t relu_bits(const float v[8]) {
   uint32_t b = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) b |= (bf2f(f2bf_rne(v[k])) > 0.f ? 1u : 0u) << k;
+  for (int k = 0; k < 8; ++k) b |= (h2f(f2h(v[k])) > 0.f ? 1u : 0u) << k;
   return (uint8_t)b;
 }
 
@@ -885,7 +880,7 @@ __global__ __launch_bounds__(256) void k_stem_pool_fwd(const uint16_t* __restric
       const int slot = kh * g.k + kw;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float a = bf2f(f2bf_rne(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f)));
+        const float a = h2f(f2h(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f)));
         if (a > best[j]) { best[j] = a; bi[j] = slot; }      // first max wins (PyTorch order)
       }
     }
@@ -1195,8 +1190,7 @@ __global__ __launch_bounds__(BNT) void k_stem_pool_reduce_out(const uint16_t* __
             if (!ill[j] || !(p[u][j] > 0.f)) continue;
             const int slot = idx[o + j];
             const int ih = oh * g.s - g.p + slot / g.k, iw = ow * g.s - g.p + slot % g.k;
-            const float xv = __uint_as_float(
-                (uint32_t)x[(((int64_t)n * g.H + ih) * g.W + iw) * g.C + cg * 8 + j] << 16);
+            const float xv = h2f(x[(((int64_t)n * g.H + ih) * g.W + iw) * g.C + cg * 8 + j]);
             b[j] += d[u][j] * (xv - mu[j]);
           }
         }

@@ -51,22 +51,22 @@ def sources():
                   if f.endswith((".hip", ".cpp")))
 
 
-def _digest(paths) -> str:
+def _digest(paths, flags=()) -> str:
     h = hashlib.sha256()
     for p in sorted(paths):
         with open(p, "rb") as f:
             h.update(p.encode())
             h.update(f.read())
     h.update(ARCH.encode())
-    h.update(" ".join(EXTRA).encode())
+    h.update(" ".join(EXTRA + list(flags)).encode())
     return h.hexdigest()[:16]
 
 
-def _compile(src, inc, abi):
-    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+def _compile(src, inc, abi, bdir=BUILD, flags=()):
+    obj = os.path.join(bdir, os.path.basename(src) + ".o")
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM", "-D__HIP_PLATFORM_AMD__=1",
-           "-Wno-unused-result", "-Wno-deprecated-declarations", f"-I{HERE}"] + EXTRA
+           "-Wno-unused-result", "-Wno-deprecated-declarations", f"-I{HERE}"] + EXTRA + list(flags)
     if src.endswith(".cpp"):
         cmd += [f"-I{p}" for p in inc] + [f"-I{sysconfig.get_paths()['include']}"]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -75,37 +75,54 @@ def _compile(src, inc, abi):
     return obj
 
 
-def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> str:
-    srcs = sources()
+# The fp16 build of the same kernels (csrc/elem16.h: fp16 conversions, v_mfma_f32_16x16x32_f16),
+# registered as torch.ops.lwaaai16 and used when the fused path runs the reference's --fp16
+# recipe (ops/_ext.py set_half). The communicator (rccl.cpp) lives only in the main library.
+OUT16 = os.environ.get("LWAAAI_SO16") or os.path.join(PKG, "_lwaaai16_C.so")
+FLAGS16 = ["-DLW_FP16", "-DLW_OPS_NS=lwaaai16"]
+
+
+def _build_one(out, bdir, flags, srcs, force, jobs, verbose):
     headers = [os.path.join(HERE, f) for f in os.listdir(HERE) if f.endswith(".h")]
-    stamp = os.path.join(BUILD, "stamp")
-    dig = _digest(srcs + headers + [os.path.abspath(__file__)])
-    if not force and os.path.exists(OUT) and os.path.exists(stamp):
+    stamp = os.path.join(bdir, "stamp")
+    dig = _digest(srcs + headers + [os.path.abspath(__file__)], flags)
+    if not force and os.path.exists(out) and os.path.exists(stamp):
         with open(stamp) as f:
             if f.read().strip() == dig:
                 if verbose:
-                    print(f"[lwaaai] up to date: {OUT}")
-                return OUT
-    os.makedirs(BUILD, exist_ok=True)
+                    print(f"[lwaaai] up to date: {out}")
+                return out
+    os.makedirs(bdir, exist_ok=True)
     inc, lib, abi = _torch_paths()
     jobs = jobs or min(8, len(srcs), os.cpu_count() or 4)
     if verbose:
-        print(f"[lwaaai] compiling {len(srcs)} sources for {ARCH} with {jobs} jobs")
+        print(f"[lwaaai] compiling {len(srcs)} sources for {ARCH} ({' '.join(flags) or 'bf16'}) "
+              f"with {jobs} jobs")
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, inc, abi), srcs))
-    tmp = OUT + ".tmp"
+        objs = list(ex.map(lambda s: _compile(s, inc, abi, bdir, flags), srcs))
+    tmp = out + ".tmp"
     cmd = ["g++", "-shared", "-o", tmp] + objs + [
         f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
         "-l:libamdhip64.so", "-lrccl", f"-Wl,-rpath,{lib}", "-Wl,-z,defs"]   # unresolved symbols fail here
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, OUT)
+    os.replace(tmp, out)
     with open(stamp, "w") as f:
         f.write(dig)
     if verbose:
-        print(f"[lwaaai] built {OUT}")
-    return OUT
+        print(f"[lwaaai] built {out}")
+    return out
+
+
+def build(force: bool = False, jobs: int = 0, verbose: bool = True, half: bool = True) -> str:
+    """Build the bf16 library (and, with ``half``, its fp16 twin); returns the bf16 one's path."""
+    srcs = sources()
+    main = _build_one(OUT, BUILD, [], srcs, force, jobs, verbose)
+    if half and not os.environ.get("LWAAAI_SO"):
+        _build_one(OUT16, os.path.join(HERE, "build_fp16"), FLAGS16,
+                   [s for s in srcs if not s.endswith("rccl.cpp")], force, jobs, verbose)
+    return main
 
 
 if __name__ == "__main__":

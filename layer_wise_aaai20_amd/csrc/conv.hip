@@ -317,17 +317,17 @@ __global__ __launch_bounds__(STEM_T) __attribute__((amdgpu_waves_per_eu(OCC))) v
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int r = 0; r < 7; ++r) {
-      bf16x8 fb[4];
+      h16x8 fb[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(ws + (j * 16 + lr) * STEM_WLD + r * 32 + g * 8);
+        fb[j] = *reinterpret_cast<const h16x8*>(ws + (j * 16 + lr) * STEM_WLD + r * 32 + g * 8);
 #pragma unroll
       for (int i = 0; i < MAXRB; ++i) {
         if (i < RB) {
-          const bf16x8 fa = *reinterpret_cast<const bf16x8*>(patch + poff[i] + r * PW * 4);
+          const h16x8 fa = *reinterpret_cast<const h16x8*>(patch + poff[i] + r * PW * 4);
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa, acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16(fb[j], fa, acc[i][j]);
         }
       }
     }
@@ -345,8 +345,8 @@ __global__ __launch_bounds__(STEM_T) __attribute__((amdgpu_waves_per_eu(OCC))) v
         uint16_t h[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          h[q] = bf16_rne(acc[i][j][q]);
-          const float v = __uint_as_float((uint32_t)h[q] << 16);
+          h[q] = f2h(acc[i][j][q]);
+          const float v = h2f(h[q]);
           s1[q] += v;
           s2[q] += v * v;
         }
@@ -501,19 +501,19 @@ __global__ __launch_bounds__(D3_T) void k_conv3_direct(const uint16_t* __restric
   for (int ks = 0; ks < D3_K / 32; ++ks) {
     const int t = ks >> 1, r = t / 3, s = t - r * 3;
     const int q = (ks & 1) * 4 + g;                  // this lane's 8-channel chunk
-    bf16x8 fb[4];
+    h16x8 fb[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      fb[j] = *reinterpret_cast<const bf16x8*>(ws + (j * 16 + lr) * D3_WLD + ks * 32 + g * 8);
+      fb[j] = *reinterpret_cast<const h16x8*>(ws + (j * 16 + lr) * D3_WLD + ks * 32 + g * 8);
 #pragma unroll
     for (int i = 0; i < D3_MAXRB; ++i) {
       if (i < RB) {
         const int pc = px[i] + s;
-        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(
+        const h16x8 fa = *reinterpret_cast<const h16x8*>(
             patch + ((py[i] + r) * PW + pc) * D3_C + ((q ^ (pc & 7)) * 8));
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa, acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(fb[j], fa, acc[i][j]);
       }
     }
   }
@@ -533,8 +533,8 @@ __global__ __launch_bounds__(D3_T) void k_conv3_direct(const uint16_t* __restric
       uint16_t h[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        h[c] = bf16_rne(acc[i][j][c]);
-        const float v = __uint_as_float((uint32_t)h[c] << 16);
+        h[c] = f2h(acc[i][j][c]);
+        const float v = h2f(h[c]);
         s1[j][c] += v;
         s2[j][c] += v * v;
       }

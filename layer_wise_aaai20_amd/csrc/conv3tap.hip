@@ -149,9 +149,9 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto compute = [&](const uint8_t* P, const uint8_t* Wt, int r, int s) {
-    bf16x8 fb[2], fa[7];
+    h16x8 fb[2], fa[7];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(Wt + wbyte[j]);
+    for (int j = 0; j < 2; ++j) fb[j] = *reinterpret_cast<const h16x8*>(Wt + wbyte[j]);
     const int toff = r * W + s;
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
@@ -160,11 +160,11 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
       int pb = ppix[i];
       asm volatile("" : "+v"(pb));
       const int p = pb + toff;
-      fa[i] = *reinterpret_cast<const bf16x8*>(P + pplane + p * 16);
+      fa[i] = *reinterpret_cast<const h16x8*>(P + pplane + p * 16);
       if (r != 1 || s != 1) {
         const uint32_t need = (r == 0 ? 1u : r == 2 ? 2u : 0u) | (s == 0 ? 4u : s == 2 ? 8u : 0u);
         const bool ok = ((vmask >> (4 * i)) & need) == need;
-        if (!ok) fa[i] = bf16x8{};
+        if (!ok) fa[i] = h16x8{};
       }
     }
     __builtin_amdgcn_s_setprio(1);
@@ -172,7 +172,7 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
     for (int i = 0; i < 7; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -252,7 +252,7 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
       const int n = wn * 32 + j * 16 + 4 * g;
       uint16_t h[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h[r] = bf16_rne(acc[i][j][r]);
+      for (int r = 0; r < 4; ++r) h[r] = f2h(acc[i][j][r]);
       *reinterpret_cast<uint2*>(Ch + m * LDH + n) =
           make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
     }
@@ -273,7 +273,7 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
       const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float f = k & 1 ? __uint_as_float(u[k >> 1] & 0xffff0000u) : __uint_as_float(u[k >> 1] << 16);
+        const float f = k & 1 ? hhi(u[k >> 1]) : hlo(u[k >> 1]);
         s1[k] += f;
         s2[k] += f * f;
       }
@@ -465,10 +465,10 @@ void k_conv3_tap_wgrad(const uint16_t* __restrict__ dy, const uint16_t* __restri
   auto cat8 = [](i16x4 lo, i16x4 hi) {
     typedef short i16x8 __attribute__((ext_vector_type(8)));
     const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
+    return __builtin_bit_cast(h16x8, v);
   };
   auto compute = [&](const uint8_t* P, const uint8_t* D, int g0, int ks) {
-    bf16x8 fa[2], fb[9];
+    h16x8 fa[2], fb[9];
 #pragma unroll
     for (int i = 0; i < 2; ++i) fa[i] = cat8(tr(D + aoff[i][0]), tr(D + aoff[i][1]));
     // this lane's two rows: pixels m = ks*32 + 8g + q4 (+4) of the tile, patch pixel m + tap
@@ -503,7 +503,7 @@ void k_conv3_tap_wgrad(const uint16_t* __restrict__ dy, const uint16_t* __restri
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 9; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
 

@@ -80,9 +80,9 @@ __global__ __launch_bounds__(GT) void k_splitk_reduce(const float* __restrict__ 
     if (bias) x += bias[n];
     if (relu) x = fmaxf(x, 0.f);
     if (out_bf16) {
-      uint16_t h = bf16_rne(x);
+      uint16_t h = f2h(x);
       if (addend)
-        h = bf16_rne(__uint_as_float((uint32_t)h << 16) + masked_addend1(addend, add_bits, m * ldc + n));
+        h = f2h(h2f(h) + masked_addend1(addend, add_bits, m * ldc + n));
       static_cast<uint16_t*>(C)[m * ldc + n] = h;
     } else {
       float* c = static_cast<float*>(C) + m * ldc + n;
@@ -203,14 +203,14 @@ __global__ __launch_bounds__(GT) void k_gemm_stream(const GemmK p) {
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const bf16x8 fa0 = __builtin_bit_cast(bf16x8, a_cur[0][s]);
-      const bf16x8 fa1 = __builtin_bit_cast(bf16x8, a_cur[1][s]);
+      const h16x8 fa0 = __builtin_bit_cast(h16x8, a_cur[0][s]);
+      const h16x8 fa1 = __builtin_bit_cast(h16x8, a_cur[1][s]);
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const bf16x8 fb = *reinterpret_cast<const bf16x8*>(
+        const h16x8 fb = *reinterpret_cast<const h16x8*>(
             Bs + (16 * j + (l & 15)) * LDB + 32 * s + 8 * (l >> 4));
-        acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa0, acc[0][j], 0, 0, 0);
-        acc[1][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb, fa1, acc[1][j], 0, 0, 0);
+        acc[0][j] = mfma16(fb, fa0, acc[0][j]);
+        acc[1][j] = mfma16(fb, fa1, acc[1][j]);
       }
     }
     // ---- epilogue: Cᵀ fragments -> bf16 -> LDS tile -> 16-byte stores
@@ -221,8 +221,8 @@ __global__ __launch_bounds__(GT) void k_gemm_stream(const GemmK p) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int c = 16 * j + 4 * (l >> 4);
-        const uint32_t lo = (uint32_t)bf16_rne(acc[i][j][0]) | ((uint32_t)bf16_rne(acc[i][j][1]) << 16);
-        const uint32_t hi = (uint32_t)bf16_rne(acc[i][j][2]) | ((uint32_t)bf16_rne(acc[i][j][3]) << 16);
+        const uint32_t lo = (uint32_t)f2h(acc[i][j][0]) | ((uint32_t)f2h(acc[i][j][1]) << 16);
+        const uint32_t hi = (uint32_t)f2h(acc[i][j][2]) | ((uint32_t)f2h(acc[i][j][3]) << 16);
         *reinterpret_cast<uint2*>(Os + r * LDO + c) = make_uint2(lo, hi);
       }
     }
@@ -236,13 +236,13 @@ __global__ __launch_bounds__(GT) void k_gemm_stream(const GemmK p) {
         const uint32_t q[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const float lo = __uint_as_float(q[k] << 16), hi = __uint_as_float(q[k] & 0xffff0000u);
+          const float lo = hlo(q[k]), hi = hhi(q[k]);
           cs1[2 * k] += lo; cs2[2 * k] += lo * lo;
           cs1[2 * k + 1] += hi; cs2[2 * k + 1] += hi * hi;
         }
       }
       uint16_t* dst = static_cast<uint16_t*>(p.C) + (int64_t)gm * p.ldc + gn;
-      if (ADD) v = add_bf16x8(v, masked_addend8(p.addend, p.add_bits, (int64_t)gm * p.ldc + gn));
+      if (ADD) v = add_h16x8(v, masked_addend8(p.addend, p.add_bits, (int64_t)gm * p.ldc + gn));
       *reinterpret_cast<uint4*>(dst) = v;
     }
     if (tn < tiles_m) {

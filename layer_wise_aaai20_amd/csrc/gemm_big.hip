@@ -55,7 +55,7 @@ __device__ __forceinline__ int big_off(int r, int c) { return r * BBK + ((c ^ (r
 __device__ __forceinline__ int xw128(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
 __device__ __forceinline__ int xw64(int k) { return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
 template <int W>
-__device__ __forceinline__ bf16x8 frag_tr(const uint16_t* img, int i_base, int s) {
+__device__ __forceinline__ h16x8 frag_tr(const uint16_t* img, int i_base, int s) {
   const int l = threadIdx.x & 63;
   const int g = l >> 4, t = l & 15, q = t >> 2, p4 = t & 3;
   const int k0 = 32 * s + 8 * g + q;
@@ -67,7 +67,7 @@ __device__ __forceinline__ bf16x8 frag_tr(const uint16_t* img, int i_base, int s
   const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0 + 4 * W));
   typedef short i16x8 __attribute__((ext_vector_type(8)));
   const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
+  return __builtin_bit_cast(h16x8, v);
 }
 
 template <int N>
@@ -266,28 +266,28 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
 #pragma unroll
         for (int j = 0; j < FQ; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 fa0[4][2], fa1[4][2], fb0[FQ][2], fb1[FQ][2];
-  auto read_a = [&](bf16x8 (&f)[4][2], const uint16_t* h) {
+  h16x8 fa0[4][2], fa1[4][2], fb0[FQ][2], fb1[FQ][2];
+  auto read_a = [&](h16x8 (&f)[4][2], const uint16_t* h) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if constexpr (MN) f[i][s] = frag_tr<128>(h, wm * 64 + i * 16, s);
-        else f[i][s] = *reinterpret_cast<const bf16x8*>(
+        else f[i][s] = *reinterpret_cast<const h16x8*>(
             h + big_off(wm * 64 + i * 16 + (l & 15), 4 * s + (l >> 4)));
       }
   };
-  auto read_b = [&](bf16x8 (&f)[FQ][2], const uint16_t* h) {
+  auto read_b = [&](h16x8 (&f)[FQ][2], const uint16_t* h) {
 #pragma unroll
     for (int j = 0; j < FQ; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if constexpr (MNB) f[j][s] = frag_tr<WB>(h, wn * QN + j * 16, s);
-        else f[j][s] = *reinterpret_cast<const bf16x8*>(
+        else f[j][s] = *reinterpret_cast<const h16x8*>(
             h + big_off(wn * QN + j * 16 + (l & 15), 4 * s + (l >> 4)));
       }
   };
-  auto mfma_q = [&](f32x4 (&c)[4][FQ], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[FQ][2]) {
+  auto mfma_q = [&](f32x4 (&c)[4][FQ], const h16x8 (&fa)[4][2], const h16x8 (&fb)[FQ][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < FQ; ++j)
-          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], c[i][j], 0, 0, 0);
+          c[i][j] = mfma16(fb[j][s], fa[i][s], c[i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
   auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
@@ -390,8 +390,8 @@ __global__ __launch_bounds__(BGT) void k_gemm_big(const GemmK p) {
             uint16_t h[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              h[r] = bf16_rne(v[r]);
-              v[r] = __uint_as_float((uint32_t)h[r] << 16);
+              h[r] = f2h(v[r]);
+              v[r] = h2f(h[r]);
             }
             uint16_t* d = static_cast<uint16_t*>(p.C) + (int64_t)m * p.ldc + n;
             if (vec4 && n + 3 < p.N) {
@@ -530,22 +530,22 @@ __global__ __launch_bounds__(BGT) void k_gemm_bigp(const GemmK p) {
     }
   };
   f32x4 acc[2][2][4][FQ];
-  bf16x8 fa0[4][2], fa1[4][2], fb0[FQ][2], fb1[FQ][2];
-  auto read_a = [&](bf16x8 (&f)[4][2], const uint16_t* h) {
+  h16x8 fa0[4][2], fa1[4][2], fb0[FQ][2], fb1[FQ][2];
+  auto read_a = [&](h16x8 (&f)[4][2], const uint16_t* h) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
-        f[i][s] = *reinterpret_cast<const bf16x8*>(h + big_off(wm * 64 + i * 16 + (l & 15), 4 * s + (l >> 4)));
+        f[i][s] = *reinterpret_cast<const h16x8*>(h + big_off(wm * 64 + i * 16 + (l & 15), 4 * s + (l >> 4)));
   };
-  auto read_b = [&](bf16x8 (&f)[FQ][2], const uint16_t* h) {
+  auto read_b = [&](h16x8 (&f)[FQ][2], const uint16_t* h) {
 #pragma unroll
     for (int j = 0; j < FQ; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s)
-        f[j][s] = *reinterpret_cast<const bf16x8*>(h + big_off(wn * QN + j * 16 + (l & 15), 4 * s + (l >> 4)));
+        f[j][s] = *reinterpret_cast<const h16x8*>(h + big_off(wn * QN + j * 16 + (l & 15), 4 * s + (l >> 4)));
   };
-  auto mfma_q = [&](f32x4 (&c)[4][FQ], const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[FQ][2]) {
+  auto mfma_q = [&](f32x4 (&c)[4][FQ], const h16x8 (&fa)[4][2], const h16x8 (&fb)[FQ][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -553,7 +553,7 @@ __global__ __launch_bounds__(BGT) void k_gemm_bigp(const GemmK p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < FQ; ++j)
-          c[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j][s], fa[i][s], c[i][j], 0, 0, 0);
+          c[i][j] = mfma16(fb[j][s], fa[i][s], c[i][j]);
     __builtin_amdgcn_s_setprio(0);
   };
   auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
@@ -621,7 +621,7 @@ __global__ __launch_bounds__(BGT) void k_gemm_bigp(const GemmK p) {
             uint16_t h[4];
             float v[4];
             if constexpr (ADD) {
-              // addend·[bit] added after rounding, as gemm_core.h add_bf16x8 (one more rounding)
+              // addend·[bit] added after rounding, as gemm_core.h add_h16x8 (one more rounding)
               uint2 ad = make_uint2(0u, 0u);
               uint32_t bits = 0xfu;
               if (ok) {
@@ -631,17 +631,17 @@ __global__ __launch_bounds__(BGT) void k_gemm_bigp(const GemmK p) {
               const uint32_t aw[2] = {ad.x, ad.y};
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const float c0 = bf16_round(acc[qa][qb][i][j][r]);
+                const float c0 = h_round(acc[qa][qb][i][j][r]);
                 const uint32_t word = aw[r >> 1];
-                const float av = ((bits >> r) & 1u) ? __uint_as_float(r & 1 ? word & 0xffff0000u : word << 16) : 0.f;
-                h[r] = bf16_rne(c0 + av);
-                v[r] = __uint_as_float((uint32_t)h[r] << 16);
+                const float av = ((bits >> r) & 1u) ? (r & 1 ? hhi(word) : hlo(word)) : 0.f;
+                h[r] = f2h(c0 + av);
+                v[r] = h2f(h[r]);
               }
             } else {
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                h[r] = bf16_rne(acc[qa][qb][i][j][r]);
-                v[r] = __uint_as_float((uint32_t)h[r] << 16);
+                h[r] = f2h(acc[qa][qb][i][j][r]);
+                v[r] = h2f(h[r]);
               }
             }
             if (ok) {

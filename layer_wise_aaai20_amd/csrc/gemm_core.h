@@ -1,27 +1,20 @@
-// bf16 MFMA GEMM core for gfx950, shared by the plain GEMM (gemm.hip) and the implicit-GEMM
-// convolutions (conv.hip): tile staging, MFMA main loop and the fused epilogues.
+// 16-bit MFMA GEMM core for gfx950 (bf16, or fp16 in the lwaaai16 build: elem16.h), shared by the
+// plain GEMM (gemm.hip) and the implicit-GEMM convolutions (conv.hip): tile staging, MFMA main
+// loop and the fused epilogues.
 // See gemm.hip for the design notes.
 #pragma once
 #include "common.h"
 #include "lw_kernels.h"
+#include "elem16.h"
 
 namespace lw {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int GT = 256;
 constexpr int PAD = 8;                   // bf16 elements of padding per LDS row
 enum { EPI_STORE = 0, EPI_PARTIAL = 1, EPI_STATS = 2, EPI_BSTATS = 3 };
 enum { PRO_NONE = 0, PRO_A = 1, PRO_B = 2 };
-
-// f32 -> bf16, round to nearest even: a plain cast, which hipcc lowers to the gfx950 hardware
-// conversion v_cvt_pk_bf16_f32 (NaN stays NaN), instead of integer bit arithmetic.
-__device__ __forceinline__ uint16_t bf16_rne(float f) {
-  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
-}
-__device__ __forceinline__ float bf16_round(float f) { return __uint_as_float((uint32_t)bf16_rne(f) << 16); }
 
 // Sum over the 16 lanes of a DPP row, every lane getting the total: quad_perm [1,0,3,2] and
 // [2,3,0,1] (partners l^1, l^2), row_half_mirror (partner 7-l: holds the other quad's identical
@@ -41,16 +34,16 @@ __device__ __forceinline__ float sum16(float v) {
   return v;
 }
 
-// bf16 + bf16 -> bf16 per element (fp32 add, one rounding): the same arithmetic as a separate
+// 16-bit + 16-bit -> 16-bit per element (fp32 add, one rounding): the same arithmetic as a separate
 // elementwise add of two bf16 tensors, so fusing the residual-gradient add changes no bits.
-__device__ __forceinline__ uint4 add_bf16x8(uint4 a, uint4 b) {
+__device__ __forceinline__ uint4 add_h16x8(uint4 a, uint4 b) {
   const uint32_t x[4] = {a.x, a.y, a.z, a.w}, y[4] = {b.x, b.y, b.z, b.w};
   uint32_t w[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float lo = __uint_as_float(x[k] << 16) + __uint_as_float(y[k] << 16);
-    const float hi = __uint_as_float(x[k] & 0xffff0000u) + __uint_as_float(y[k] & 0xffff0000u);
-    w[k] = (uint32_t)bf16_rne(lo) | ((uint32_t)bf16_rne(hi) << 16);
+    const float lo = hlo(x[k]) + hlo(y[k]);
+    const float hi = hhi(x[k]) + hhi(y[k]);
+    w[k] = (uint32_t)f2h(lo) | ((uint32_t)f2h(hi) << 16);
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
@@ -74,7 +67,7 @@ __device__ __forceinline__ uint4 masked_addend8(const uint16_t* __restrict__ add
 __device__ __forceinline__ float masked_addend1(const uint16_t* __restrict__ add,
                                                 const uint8_t* __restrict__ bits, int64_t e) {
   if (bits && !((bits[e >> 3] >> (e & 7)) & 1u)) return 0.f;
-  return __uint_as_float((uint32_t)add[e] << 16);
+  return h2f(add[e]);
 }
 
 // R = extent of the tile along m (A) or n (B). K-contiguous (KC) tiles are stored [R][BK]: at
@@ -234,9 +227,9 @@ __device__ __forceinline__ uint4 affine_relu8(uint4 v, const Coef8& c) {
   uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float lo = fmaxf(fmaf(__uint_as_float(w[k] << 16), c.s[2 * k], c.t[2 * k]), 0.f);
-    const float hi = fmaxf(fmaf(__uint_as_float(w[k] & 0xffff0000u), c.s[2 * k + 1], c.t[2 * k + 1]), 0.f);
-    w[k] = (uint32_t)bf16_rne(lo) | ((uint32_t)bf16_rne(hi) << 16);
+    const float lo = fmaxf(fmaf(hlo(w[k]), c.s[2 * k], c.t[2 * k]), 0.f);
+    const float hi = fmaxf(fmaf(hhi(w[k]), c.s[2 * k + 1], c.t[2 * k + 1]), 0.f);
+    w[k] = (uint32_t)f2h(lo) | ((uint32_t)f2h(hi) << 16);
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
@@ -260,12 +253,12 @@ __device__ __forceinline__ void store_tile(uint16_t* __restrict__ S,
 // MFMA operand fragment (8 bf16 along k, k-group g = lane>>4, sub-step s of 32 k) for tile
 // row/col i_base + (lane&15).
 template <int R, int BK, bool KC>
-__device__ __forceinline__ bf16x8 load_frag(const uint16_t* S, int i_base, int s) {
+__device__ __forceinline__ h16x8 load_frag(const uint16_t* S, int i_base, int s) {
   using T = Tile<R, BK, KC>;
   const int l = threadIdx.x & 63;
   if (KC) {
     const uint16_t* p = S + tile_off<R, BK, KC>(i_base + (l & 15), 4 * s + (l >> 4));
-    return *reinterpret_cast<const bf16x8*>(p);
+    return *reinterpret_cast<const h16x8*>(p);
   } else {
     const int g = l >> 4, t = l & 15, q = t >> 2, p4 = t & 3;
     typedef __attribute__((address_space(3))) i16x4 lds_v4;
@@ -275,7 +268,7 @@ __device__ __forceinline__ bf16x8 load_frag(const uint16_t* S, int i_base, int s
     const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p1));
     typedef short i16x8 __attribute__((ext_vector_type(8)));
     const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
+    return __builtin_bit_cast(h16x8, v);
   }
 }
 
@@ -283,7 +276,7 @@ __device__ __forceinline__ void store_out8(void* C, int64_t off, const float v[8
   if (bf) {
     uint32_t w[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = (uint32_t)bf16_rne(v[2 * k]) | ((uint32_t)bf16_rne(v[2 * k + 1]) << 16);
+    for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f2h(v[2 * k]) | ((uint32_t)f2h(v[2 * k + 1]) << 16);
     *reinterpret_cast<uint4*>(static_cast<uint16_t*>(C) + off) = make_uint4(w[0], w[1], w[2], w[3]);
   } else {
     float* c = static_cast<float*>(C) + off;
@@ -733,7 +726,7 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
     const uint16_t* Bs = As + TA::ELEMS;
 #pragma unroll
     for (int s = 0; s < BK / 32; ++s) {
-      bf16x8 fa[FM], fb[FN];
+      h16x8 fa[FM], fb[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) fa[i] = load_frag<BM, BK, AKC>(As, wr * WTM + i * 16, s);
 #pragma unroll
@@ -742,7 +735,7 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
     }
   };
   const int nsteps = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
@@ -827,8 +820,8 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
           uint16_t h[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            h[r] = bf16_rne(v[r]);
-            v[r] = __uint_as_float((uint32_t)h[r] << 16);
+            h[r] = f2h(v[r]);
+            v[r] = h2f(h[r]);
           }
           *reinterpret_cast<uint2*>(Ch + ml * LDH + nl) =
               make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
@@ -910,7 +903,7 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       const int64_t aoff = orow * p.ldc + gn;
       if (vec && gn + 8 <= p.N) {
         uint4 v = *reinterpret_cast<const uint4*>(src);
-        if (p.addend) v = add_bf16x8(v, pref ? pa : masked_addend8(p.addend, p.add_bits, aoff));
+        if (p.addend) v = add_h16x8(v, pref ? pa : masked_addend8(p.addend, p.add_bits, aoff));
         *reinterpret_cast<uint4*>(dst) = v;
         if constexpr (EPI == EPI_BSTATS) {
           // the stored gradient (bf16, as the BN backward would read it), masked by the ReLU of
@@ -918,8 +911,8 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
           const uint32_t w[4] = {v.x, v.y, v.z, v.w}, xw[4] = {px.x, px.y, px.z, px.w};
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
-            const float d = k & 1 ? __uint_as_float(w[k >> 1] & 0xffff0000u) : __uint_as_float(w[k >> 1] << 16);
-            const float xv = k & 1 ? __uint_as_float(xw[k >> 1] & 0xffff0000u) : __uint_as_float(xw[k >> 1] << 16);
+            const float d = k & 1 ? hhi(w[k >> 1]) : hlo(w[k >> 1]);
+            const float xv = k & 1 ? hhi(xw[k >> 1]) : hlo(xw[k >> 1]);
             const bool m = p.bst_bits ? ((pxb >> k) & 1u) != 0u : fmaf(xv, bsc[k], bsh[k]) > 0.f;
             const float dm = m ? d : 0.f;
             cs1[k] += dm;
@@ -930,7 +923,7 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
         for (int k = 0; k < 8 && gn + k < p.N; ++k) {
           uint16_t h = src[k];
           if (p.addend)
-            h = bf16_rne(__uint_as_float((uint32_t)h << 16) +
+            h = f2h(h2f(h) +
                          masked_addend1(p.addend, p.add_bits, aoff + k));
           dst[k] = h;
         }

@@ -7,21 +7,9 @@
 //                   16 input bytes per lane (one dwordx4 load), two or four 16-B stores.
 #include "common.h"
 #include "lw_kernels.h"
-#include <hip/hip_bf16.h>
+#include "elem16.h"
 
 namespace lw {
-
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  // round-to-nearest-even (finite inputs only: normalised pixels)
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-
-// round to nearest even, NaN-preserving (the gfx950 hardware conversion)
-__device__ __forceinline__ uint16_t bf16_cast(float f) {
-  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));
-}
 
 template <bool BF16>
 __global__ __launch_bounds__(256) void k_normalize_u8(const uint8_t* __restrict__ in,
@@ -54,11 +42,11 @@ __global__ __launch_bounds__(256) void k_normalize_u8(const uint8_t* __restrict_
     if (base + 16 <= nbytes) {
       uint32_t p[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) p[k] = (uint32_t)f2bf(y[2 * k]) | ((uint32_t)f2bf(y[2 * k + 1]) << 16);
+      for (int k = 0; k < 8; ++k) p[k] = (uint32_t)f2h(y[2 * k]) | ((uint32_t)f2h(y[2 * k + 1]) << 16);
       reinterpret_cast<uint4*>(o)[0] = make_uint4(p[0], p[1], p[2], p[3]);
       reinterpret_cast<uint4*>(o)[1] = make_uint4(p[4], p[5], p[6], p[7]);
     } else {
-      for (int k = 0; k < 16 && base + k < nbytes; ++k) o[k] = f2bf(y[k]);
+      for (int k = 0; k < 16 && base + k < nbytes; ++k) o[k] = f2h(y[k]);
     }
   } else {
     float* o = reinterpret_cast<float*>(out) + base;
@@ -104,8 +92,8 @@ __global__ __launch_bounds__(256) void k_normalize_u8_c4(const uint8_t* __restri
       const float y0 = ((float)b[3 * px] - mean[0]) * rstd[0];
       const float y1 = ((float)b[3 * px + 1] - mean[1]) * rstd[1];
       const float y2 = ((float)b[3 * px + 2] - mean[2]) * rstd[2];
-      w[2 * h] = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
-      w[2 * h + 1] = (uint32_t)f2bf(y2);
+      w[2 * h] = (uint32_t)f2h(y0) | ((uint32_t)f2h(y1) << 16);
+      w[2 * h + 1] = (uint32_t)f2h(y2);
     }
     if (p0 + 2 * q + 2 <= npix) {
       reinterpret_cast<uint4*>(out + (p0 + 2 * q) * 4)[0] = make_uint4(w[0], w[1], w[2], w[3]);
@@ -178,14 +166,14 @@ __global__ __launch_bounds__(256) void k_gap_fwd(const uint16_t* __restrict__ x,
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      acc[2 * k] += __uint_as_float(w[k] << 16);
-      acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+      acc[2 * k] += hlo(w[k]);
+      acc[2 * k + 1] += hhi(w[k]);
     }
   }
   uint32_t o[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
-    o[k] = (uint32_t)bf16_cast(acc[2 * k] * inv_hw) | ((uint32_t)bf16_cast(acc[2 * k + 1] * inv_hw) << 16);
+    o[k] = (uint32_t)f2h(acc[2 * k] * inv_hw) | ((uint32_t)f2h(acc[2 * k + 1] * inv_hw) << 16);
   *reinterpret_cast<uint4*>(y + (int64_t)n * C + g * 8) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
@@ -209,14 +197,14 @@ __global__ __launch_bounds__(256) void k_gap_bwd(const void* __restrict__ dy,
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      d[2 * k] = __uint_as_float(w[k] << 16);
-      d[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+      d[2 * k] = hlo(w[k]);
+      d[2 * k + 1] = hhi(w[k]);
     }
   }
   uint32_t o[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
-    o[k] = (uint32_t)bf16_cast(d[2 * k] * inv_hw) | ((uint32_t)bf16_cast(d[2 * k + 1] * inv_hw) << 16);
+    o[k] = (uint32_t)f2h(d[2 * k] * inv_hw) | ((uint32_t)f2h(d[2 * k + 1] * inv_hw) << 16);
   *reinterpret_cast<uint4*>(dx + t * 8) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
@@ -361,7 +349,7 @@ __global__ __launch_bounds__(256) void k_relu_bias_bwd(const uint16_t* __restric
         uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          // bf16 > 0: sign bit clear and not +0
+          // 16-bit float > 0: sign bit clear and not +0
           const uint32_t lo = ((vw[k] & 0x8000u) == 0u && (vw[k] & 0x7fffu) != 0u) ? 0xffffu : 0u;
           const uint32_t hi = ((vw[k] & 0x80000000u) == 0u && (vw[k] & 0x7fff0000u) != 0u)
                                   ? 0xffff0000u : 0u;
@@ -373,8 +361,8 @@ __global__ __launch_bounds__(256) void k_relu_bias_bwd(const uint16_t* __restric
       const uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        a[2 * k] += __uint_as_float(w[k] << 16);
-        a[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+        a[2 * k] += hlo(w[k]);
+        a[2 * k + 1] += hhi(w[k]);
       }
     }
 #pragma unroll

@@ -7,15 +7,13 @@
 // bf16 mirror write `pb`: the next forward reads the mirror with no cast pass.
 #include "common.h"
 #include "lw_kernels.h"
+#include "elem16.h"
 
 namespace lw {
 
 constexpr int SNT = 256;
 constexpr int SEPB = kLargeEPB;
 
-__device__ __forceinline__ uint16_t to_bf16(float f) {
-  return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f));   // RNE, as torch's cast
-}
 
 template <bool MOM, bool NEST, bool FIRST>
 __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float* __restrict__ g,
@@ -67,8 +65,8 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
       if (MOM) *reinterpret_cast<float4*>(buf + off + i0) = make_float4(b[0], b[1], b[2], b[3]);
       if (pb != nullptr)
         *reinterpret_cast<uint2*>(pb + off + i0) =
-            make_uint2((uint32_t)to_bf16(x[0]) | ((uint32_t)to_bf16(x[1]) << 16),
-                       (uint32_t)to_bf16(x[2]) | ((uint32_t)to_bf16(x[3]) << 16));
+            make_uint2((uint32_t)f2h(x[0]) | ((uint32_t)f2h(x[1]) << 16),
+                       (uint32_t)f2h(x[2]) | ((uint32_t)f2h(x[3]) << 16));
     } else {
       for (int k = 0; k < 4 && i0 + k < end; ++k) {
         const int64_t i = off + i0 + k;
@@ -81,7 +79,7 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
           dp = NEST ? dp + momentum * bv : bv;
         }
         p[i] = x - lr * dp;
-        if (pb != nullptr) pb[i] = to_bf16(p[i]);
+        if (pb != nullptr) pb[i] = f2h(p[i]);
       }
     }
   }

@@ -21,6 +21,8 @@ from typing import Optional
 import numpy as np
 import torch
 
+from ..ops._ext import h16
+
 cifar10_mean = (0.4914, 0.4822, 0.4465)
 cifar10_std = (0.2471, 0.2435, 0.2616)
 
@@ -274,7 +276,7 @@ class GPUBatches:
     def _kernel_ok(self) -> bool:
         return (self.use_kernel and self.augment and self.data.is_cuda and self.channels_last and
                 self.data.dtype == torch.float32 and self.data.dim() == 4 and
-                self.data.is_contiguous() and self.dtype in (torch.float32, torch.bfloat16))
+                self.data.is_contiguous() and self.dtype in (torch.float32, h16()))
 
     def _indices(self):
         n = self.data.shape[0]

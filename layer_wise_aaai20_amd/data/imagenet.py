@@ -20,6 +20,8 @@ from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
+
+from ..ops._ext import h16
 from torch.utils.data import DataLoader, Dataset, Sampler
 
 IMAGENET_MEAN = [0.485 * 255, 0.456 * 255, 0.406 * 255]
@@ -374,7 +376,7 @@ class GPUSyntheticLoader:
                               device=self.device, generator=g)
             x = (x + self.bias[t].view(nb, 1, 1, 3)).to(torch.uint8)
             yield normalize_nhwc_u8(x, self.mean, self.std, self.dtype,
-                                    pad4=self.pad4 and self.dtype == torch.bfloat16), t
+                                    pad4=self.pad4 and self.dtype == h16()), t
 
 
 def get_loaders(traindir=None, valdir=None, sz=128, bs=256, val_bs=None, workers=0,

@@ -14,16 +14,19 @@ import torch
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO_PATH = os.environ.get("LWAAAI_SO") or os.path.join(_PKG, "_lwaaai_C.so")
+# the same kernels built for fp16 (csrc/elem16.h, registered as torch.ops.lwaaai16)
+SO16_PATH = os.environ.get("LWAAAI_SO16") or os.path.join(_PKG, "_lwaaai16_C.so")
 _lock = threading.Lock()
 _loaded = False
+_loaded16 = False
+_HALF = False
 
 
 class ExtensionMissing(RuntimeError):
     pass
 
 
-def load(build_if_missing: bool = True):
-    """Load (building first if needed) and return ``torch.ops.lwaaai``."""
+def _load_main(build_if_missing: bool = True):
     global _loaded
     if _loaded:
         return torch.ops.lwaaai
@@ -41,6 +44,54 @@ def load(build_if_missing: bool = True):
     return torch.ops.lwaaai
 
 
+def _load_half(build_if_missing: bool = True):
+    global _loaded16
+    if _loaded16:
+        return torch.ops.lwaaai16
+    _load_main(build_if_missing)              # the communicator and the shared state live there
+    with _lock:
+        if _loaded16:
+            return torch.ops.lwaaai16
+        if not os.path.exists(SO16_PATH) and build_if_missing:
+            from ..csrc import build as _b
+            _b.build(verbose=False)
+        if not os.path.exists(SO16_PATH):
+            raise ExtensionMissing(
+                f"{SO16_PATH} not found; run `python -m layer_wise_aaai20_amd.csrc.build`")
+        torch.ops.load_library(SO16_PATH)
+        _loaded16 = True
+    return torch.ops.lwaaai16
+
+
+def load(build_if_missing: bool = True):
+    """The kernel ops of the current precision: ``torch.ops.lwaaai`` (bf16 activations), or
+    ``torch.ops.lwaaai16`` (the fp16 build of the same kernels) after ``set_half(True)``."""
+    return _load_half(build_if_missing) if _HALF else _load_main(build_if_missing)
+
+
+def load_main(build_if_missing: bool = True):
+    """``torch.ops.lwaaai`` whatever the precision: the native communicator (csrc/rccl.cpp) is
+    only built there, so its handles stay valid across ``set_half`` switches."""
+    return _load_main(build_if_missing)
+
+
+def set_half(on: bool) -> None:
+    """Run the fused path's 16-bit tensors as fp16 (the reference's ``--fp16`` recipe on the MFMA
+    kernels: v_mfma_f32_16x16x32_f16, fp32 accumulation, static loss scale in the SGD kernel)
+    instead of bf16. Process-wide: set it before building a model."""
+    global _HALF
+    _HALF = bool(on)
+
+
+def half() -> bool:
+    return _HALF
+
+
+def h16() -> torch.dtype:
+    """The 16-bit element type of activations / weight mirrors on the fused path."""
+    return torch.float16 if _HALF else torch.bfloat16
+
+
 def ops_for(t: torch.Tensor):
     """Return torch.ops.lwaaai for GPU tensors (loud failure if unavailable), None for CPU."""
     if t.device.type == "cpu":
@@ -49,4 +100,4 @@ def ops_for(t: torch.Tensor):
 
 
 def is_loaded() -> bool:
-    return _loaded
+    return _loaded or _loaded16

@@ -50,11 +50,10 @@ from typing import Dict, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from ._ext import load
+from ._ext import h16, load
 from .conv import conv_dgrad, conv_fwd, conv_wgrad
 from .tuning import Tuner
 
-BF16 = torch.bfloat16
 CL = torch.channels_last
 # materialise relu(bn1(c1)) / relu(bn2(c2)) with one apply pass instead of re-normalising in the
 # consumers' staging prologues (see _BottleneckFn.forward)
@@ -218,7 +217,7 @@ def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
         return run("nkc")
     plain = (not kw.get("stats") and kw.get("addend_bits") is None and
              kw.get("out_bf16", True) and not kw.get("accumulate") and
-             dy.dtype == torch.bfloat16 and W.dtype == torch.bfloat16)
+             dy.dtype == W.dtype)
     cands = ("nkc", "kc") + (("blas",) if plain and DGRAD_BLAS else ())
     key = (M, N, K, kw.get("addend") is not None, kw.get("out") is not None)
     # timed on a scratch output (``out`` may also be the addend: dx += ... in place)
@@ -351,7 +350,7 @@ def _bf16_weight(w: torch.Tensor) -> torch.Tensor:
     current (``GradArena.refresh_bf16``), else a cast."""
     f = getattr(w, "_lw_bf16_of", None)
     v = f() if f is not None else None
-    return v if v is not None else w.detach().to(BF16)
+    return v if v is not None else w.detach().to(h16())
 
 
 def _bn_momentum(bn) -> float:
@@ -378,7 +377,7 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.prev = _take_prev(x) if bnd is None else None
         stride = conv2.stride
         N, Cin, H, W = x.shape
-        x = x.to(BF16).contiguous(memory_format=CL)
+        x = x.to(h16()).contiguous(memory_format=CL)
         xr = _rows(x)
         width = w1.shape[0]
         cout = w3.shape[0]
@@ -453,7 +452,7 @@ class _BottleneckFn(torch.autograd.Function):
         N, Cin, H, W, N2, H2, W2_, width, cout, M, M2 = ctx.geom
         w1, g1p, b1p, w2, g2p, b2p, w3, g3p, b3p, wd, gdp, bdp = ctx.params
         has_down = ctx.down_stride > 0
-        dr = _rows(dout.to(BF16).contiguous(memory_format=CL))
+        dr = _rows(dout.to(h16()).contiguous(memory_format=CL))
         # BN3 (+ shortcut) backward, ReLU mask from the forward's 1-bit bitmap
         o3 = _bn_grad_outs(g3p, b3p)
         # (the shortcut gradient dy·[out>0] is never materialised: its consumers read dy and

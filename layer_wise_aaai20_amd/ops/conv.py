@@ -27,10 +27,9 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from ._ext import load
+from ._ext import h16, load
 from .tuning import Tuner
 
-BF16 = torch.bfloat16
 CL = torch.channels_last
 CV_A, CV_A4, CV_B, CV_B4 = 1, 2, 3, 4
 ROW_TILES = (1, 2, 3, 5, 6)          # forward / dgrad (csrc GemmTile ids)
@@ -77,7 +76,7 @@ def tap_dgrad_weight(w: torch.Tensor) -> torch.Tensor:
     """The data gradient of a 3x3/1/1 conv as a forward conv of dy: W'[ci][r][s][co] =
     w[co][ci][2-r][2-s], K-contiguous [C][9 Co]."""
     c = w.shape[1]
-    return w.to(BF16).flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).contiguous()
+    return w.to(h16()).flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).contiguous()
 
 
 _TILE_DIMS = {1: (128, 128, 32), 2: (128, 128, 64), 3: (256, 64, 32), 4: (64, 256, 32),
@@ -120,10 +119,10 @@ def _row_default(M: int, N: int) -> int:
 # ----------------------------------------------------------------------------- weight packing
 def _c4_input(x: torch.Tensor) -> torch.Tensor:
     """[N, 3, H, W] → bf16 channels_last [N, 4, H, W] with a zero 4th channel."""
-    x = x.to(BF16)
+    x = x.to(h16())
     if x.shape[1] == 4:
         return x.contiguous(memory_format=CL)
-    out = torch.zeros((x.shape[0], x.shape[2], x.shape[3], 4), dtype=BF16,
+    out = torch.zeros((x.shape[0], x.shape[2], x.shape[3], 4), dtype=h16(),
                       device=x.device).permute(0, 3, 1, 2)
     out[:, :3].copy_(x)
     return out
@@ -133,11 +132,11 @@ def pack_fwd_weight(w: torch.Tensor) -> Tuple[torch.Tensor, int, int]:
     """Weight [Co, C, R, S] → bf16 GEMM operand [Co][K] (K-contiguous). For C in (3, 4) the taps
     along w are padded to an even count and the channels to 4. Returns (operand, K, TS)."""
     co, c, r, s = w.shape
-    wb = w.to(BF16)
+    wb = w.to(h16())
     if c % 8 == 0:
         return wb.permute(0, 2, 3, 1).contiguous().view(co, -1), r * s * c, s
     ts = s + (s & 1)
-    p = torch.zeros((co, r, ts, 4), dtype=BF16, device=w.device)
+    p = torch.zeros((co, r, ts, 4), dtype=h16(), device=w.device)
     p[:, :, :s, :c].copy_(wb.permute(0, 2, 3, 1))
     return p.view(co, -1), r * ts * 4, ts
 
@@ -162,7 +161,7 @@ def _dgrad_classes(H, W, R, S, sh, sw, ph, pw):
 def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int) -> Tuple[torch.Tensor, List[int]]:
     """Per-class slabs Wt_c[jr][js][co][ci] = w[co, ci, r0 + sh*jr, s0 + sw*js], concatenated."""
     co, c, R, S = w.shape
-    wt = w.to(BF16).permute(2, 3, 0, 1)                      # [R, S, Co, C]
+    wt = w.to(h16()).permute(2, 3, 0, 1)                      # [R, S, Co, C]
     if len(classes) == 1 and classes[0][4] == R and classes[0][5] == S:
         return wt.contiguous().view(-1), [0]
     parts, offs, off = [], [], 0
@@ -185,7 +184,7 @@ def pack_dgrad_weight_kc(w: torch.Tensor, classes, sh: int, sw: int):
     cls = []
     for (_c, _w, r0, s0, TR, TS, *_x) in classes:
         cls += [r0, s0, TR, TS]
-    wb = w.to(BF16).contiguous(memory_format=CL)
+    wb = w.to(h16()).contiguous(memory_format=CL)
     packed = load().pack_dgrad_kc(wb, cls, sh, sw, kmax)
     return packed, [i * c * kmax for i in range(len(classes))], kmax
 
@@ -201,7 +200,7 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
     ph, pw = _pair(padding)
     co, c, R, S = w.shape
     c4 = c % 8 != 0
-    xin = _c4_input(x) if c4 else x.to(BF16).contiguous(memory_format=CL)
+    xin = _c4_input(x) if c4 else x.to(h16()).contiguous(memory_format=CL)
     Nb, _, H, W = xin.shape
     Ho, Wo = out_size(H, R, sh, ph), out_size(W, S, sw, pw)
     op, K, TS = wpack if wpack is not None else pack_fwd_weight(w)
@@ -262,14 +261,14 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
     ph, pw = _pair(padding)
     co, c, R, S = w.shape
     H, W = x_hw
-    dyc = dy.to(BF16).contiguous(memory_format=CL)
+    dyc = dy.to(h16()).contiguous(memory_format=CL)
     Nb, _, Ho, Wo = dyc.shape
     classes = _dgrad_classes(H, W, R, S, sh, sw, ph, pw)
     if not classes:
         assert bst is None, "backward statistics of an all-zero gradient"
         if out is not None:
             return _nchw_rows(out, Nb, H, W)
-        return torch.zeros((Nb, c, H, W), dtype=BF16, device=dy.device, memory_format=CL)
+        return torch.zeros((Nb, c, H, W), dtype=h16(), device=dy.device, memory_format=CL)
     wt, offs = wpack if wpack is not None else pack_dgrad_weight(w, classes, sh, sw)
     geom = [Nb, Ho, Wo, co, 1, 1, -1, -1, H, W, sh, sw, len(classes)]
     for (ch, cw, r0, s0, TR, TS, Hg, Wg, oh, ow), off in zip(classes, offs):
@@ -341,11 +340,11 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, pro=
     if pro is not None:
         # the input's BN-apply+ReLU, materialised once (a B-gather prologue would redo it for
         # every tap and output-channel tile)
-        xa = x.to(BF16).contiguous(memory_format=CL)
+        xa = x.to(h16()).contiguous(memory_format=CL)
         x = lib.bn_apply(xa, torch.cat([pro[0][:c], pro[1][:c]]).contiguous(), None, None, True)
         pro = None
-    xin = _c4_input(x) if c4 else x.to(BF16).contiguous(memory_format=CL)
-    dyc = dy.to(BF16).contiguous(memory_format=CL)
+    xin = _c4_input(x) if c4 else x.to(h16()).contiguous(memory_format=CL)
+    dyc = dy.to(h16()).contiguous(memory_format=CL)
     Nb, C, H, W = xin.shape
     _, _, Ho, Wo = dyc.shape
     TS = S + (S & 1) if c4 else S
@@ -415,7 +414,7 @@ class _ConvFn(torch.autograd.Function):
         from .block import _bf16_weight
         wb = _bf16_weight(weight)
         y, _ = conv_fwd(x, wb, stride, padding, bias=bias, relu=relu)
-        xs = x.to(BF16).contiguous(memory_format=CL) if x.shape[1] % 8 == 0 else x
+        xs = x.to(h16()).contiguous(memory_format=CL) if x.shape[1] % 8 == 0 else x
         ctx.save_for_backward(xs, wb, y if relu else None)
         ctx.geom = (stride, padding, tuple(x.shape[2:]), x.dtype)
         ctx.weight = weight
@@ -429,7 +428,7 @@ class _ConvFn(torch.autograd.Function):
         stride, padding, hw, xdtype = ctx.geom
         w, b = ctx.weight, ctx.bias
         dx = dw = db = None
-        dy = dy.to(BF16).contiguous(memory_format=CL)
+        dy = dy.to(h16()).contiguous(memory_format=CL)
         if ctx.relu or (b is not None and ctx.needs_input_grad[2]):
             if dy.shape[1] % 8 == 0 and dy.shape[1] <= 2048:
                 dy, db = load().relu_bias_bwd(dy, y if ctx.relu else None, None)

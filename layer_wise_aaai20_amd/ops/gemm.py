@@ -14,7 +14,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from ._ext import load
+from ._ext import h16, load
 from .tuning import Tuner
 
 
@@ -124,7 +124,7 @@ class _LinearFn(torch.autograd.Function):
         shp = x.shape
         N, K = weight.shape
         Np = N + (-N) % 8                       # e.g. a 10-way classifier runs as 16 columns
-        x2 = x.reshape(-1, shp[-1]).to(torch.bfloat16).contiguous()
+        x2 = x.reshape(-1, shp[-1]).to(h16()).contiguous()
         w = _pad_rows(_bf16_weight(weight).contiguous(), Np)
         b = None
         if bias is not None:
@@ -148,7 +148,7 @@ class _LinearFn(torch.autograd.Function):
         # the bias gradient from dy as it arrives (fp32 for an fp32-output classifier: a bf16 dy
         # makes many logits' bias gradients exactly equal — Top-K ties at the threshold)
         db = dyf.float().sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
-        dy2 = dyf.to(torch.bfloat16)
+        dy2 = dyf.to(h16())
         if Np != N:
             dy2 = torch.cat([dy2, dy2.new_zeros(dy2.shape[0], Np - N)], 1)
         dy2 = dy2.contiguous()

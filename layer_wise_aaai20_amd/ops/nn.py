@@ -11,12 +11,12 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from ._ext import load, ops_for
+from ._ext import h16, load, ops_for
 
 MAX_BN_C = 2048          # csrc/bn.hip: one 8-channel group per thread of a 256-thread block
 
 
-def normalize_nhwc_u8(images: torch.Tensor, mean, std, dtype=torch.bfloat16,
+def normalize_nhwc_u8(images: torch.Tensor, mean, std, dtype=None,
                       pad4: bool = False) -> torch.Tensor:
     """uint8 [N, H, W, C] → ``(x - mean) / std`` as an NCHW tensor in channels_last memory.
 
@@ -26,11 +26,12 @@ def normalize_nhwc_u8(images: torch.Tensor, mean, std, dtype=torch.bfloat16,
     implicit-GEMM stem convolution (``ops/conv.py``). ``mean`` / ``std`` are per-channel
     sequences of floats (preferred: no device read) or tensors."""
     assert images.dtype == torch.uint8 and images.dim() == 4
+    dtype = h16() if dtype is None else dtype
     N, H, W, C = images.shape
     lib = ops_for(images)
     mh = [float(m) for m in (mean.tolist() if torch.is_tensor(mean) else mean)]
     sh = [float(v) for v in (std.tolist() if torch.is_tensor(std) else std)]
-    if lib is not None and pad4 and C == 3 and dtype == torch.bfloat16 and images.is_contiguous():
+    if lib is not None and pad4 and C == 3 and dtype == h16() and images.is_contiguous():
         out = torch.empty((N, H, W, 4), dtype=dtype, device=images.device).permute(0, 3, 1, 2)
         lib.normalize_u8(images, out, mh, sh)
         return out
@@ -92,7 +93,7 @@ def fused_batch_norm(x, weight, bias, running_mean, running_var, training, momen
     """BN → (+ residual) → (ReLU). HIP kernels for channels_last GPU tensors with C % 8 == 0,
     torch ops otherwise (CPU path, odd channel counts)."""
     use_hip = x.is_cuda and x.dim() in (2, 4) and x.size(1) % 8 == 0 and \
-        x.size(1) <= MAX_BN_C and x.dtype in (torch.bfloat16, torch.float32)
+        x.size(1) <= MAX_BN_C and x.dtype in (h16(), torch.float32)
     if use_hip:
         return _FusedBN.apply(x, residual, weight, bias, running_mean, running_var, training,
                               momentum, eps, relu)
@@ -140,7 +141,7 @@ class FusedBNReluPool2d(FusedBatchNorm2d):
     def forward(self, x, residual=None):
         k, s, p = self.fuse_pool
         if (residual is None and self.training and self.track_running_stats and x.is_cuda and
-                x.dim() == 4 and x.dtype == torch.bfloat16 and x.size(1) % 8 == 0 and
+                x.dim() == 4 and x.dtype == h16() and x.size(1) % 8 == 0 and
                 x.size(1) <= MAX_BN_C and self.affine and _stem_fits(*x.shape, self.fuse_pool)):
             return _StemPoolFn.apply(x, self.weight, self.bias, self, self.fuse_pool)
         y = super().forward(x, residual)
@@ -212,7 +213,7 @@ class _StemPoolFn(torch.autograd.Function):
     def forward(ctx, c, weight, bias, bn, geom):
         from . import block
         lib = load()
-        c = c.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        c = c.to(h16()).contiguous(memory_format=torch.channels_last)
         block._bump(bn)
         mean, invstd, ss = lib.bn_stats(c, None, weight, bias, bn.running_mean, bn.running_var,
                                         block._bn_momentum(bn), bn.eps)
@@ -227,7 +228,7 @@ class _StemPoolFn(torch.autograd.Function):
         from . import block
         c, idx, ss, weight, mean, invstd, pooled = ctx.saved_tensors
         w, b = ctx.params
-        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dout = dout.to(h16()).contiguous(memory_format=torch.channels_last)
         outs = block._bn_grad_outs(w, b)
         dc, dg, db = load().stem_pool_bwd(dout, idx, c, ss, weight, mean, invstd, *ctx.geom,
                                           outs[0], outs[1], pooled)
@@ -263,7 +264,7 @@ class _StemConvPoolFn(torch.autograd.Function):
         from .conv import conv_dgrad, conv_wgrad
         x, c, idx, ss, gamma, mean, invstd, pooled = ctx.saved_tensors
         w, g, b = ctx.params
-        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dout = dout.to(h16()).contiguous(memory_format=torch.channels_last)
         outs = block._bn_grad_outs(g, b)
         dc, dg, db = load().stem_pool_bwd(dout, idx, c, ss, gamma, mean, invstd, *ctx.geom,
                                           outs[0], outs[1], pooled)
@@ -321,7 +322,7 @@ class _ReluPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, idx = ctx.saved_tensors
-        dout = dout.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        dout = dout.to(h16()).contiguous(memory_format=torch.channels_last)
         return load().relu_pool_bwd(dout, idx, x, *ctx.geom), None
 
 
@@ -331,7 +332,7 @@ class ReluMaxPool2d(nn.MaxPool2d):
 
     def forward(self, x):
         geom = _pool_geom(self)
-        if (geom is not None and x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and
+        if (geom is not None and x.is_cuda and x.dim() == 4 and x.dtype == h16() and
                 x.size(1) % 8 == 0 and x.size(1) <= MAX_BN_C and
                 x.is_contiguous(memory_format=torch.channels_last) and _stem_fits(*x.shape, geom)):
             return _ReluPoolFn.apply(x, geom)
@@ -359,7 +360,7 @@ def _stem_fits(n: int, c: int, h: int, w: int, geom) -> bool:
 def stem_supported(model, c: torch.Tensor) -> bool:
     bn = model.bn1
     geom = _pool_geom(model.maxpool) if isinstance(model.maxpool, nn.MaxPool2d) else None
-    return (model.training and c.is_cuda and c.dim() == 4 and c.dtype == torch.bfloat16 and
+    return (model.training and c.is_cuda and c.dim() == 4 and c.dtype == h16() and
             c.size(1) % 8 == 0 and c.size(1) <= MAX_BN_C and bn.affine and
             bn.track_running_stats and geom is not None and _stem_fits(*c.shape, geom))
 
@@ -386,7 +387,7 @@ def global_avg_pool(x: torch.Tensor, pool: nn.Module) -> torch.Tensor:
     """``flatten(pool(x), 1)`` for ``AdaptiveAvgPool2d(1)``: the HIP kernels on a CUDA
     channels_last bf16 input with C % 8 == 0, torch otherwise."""
     if (isinstance(pool, nn.AdaptiveAvgPool2d) and pool.output_size in (1, (1, 1)) and x.is_cuda
-            and x.dim() == 4 and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0
+            and x.dim() == 4 and x.dtype == h16() and x.shape[1] % 8 == 0
             and x.is_contiguous(memory_format=torch.channels_last)):
         return _GlobalAvgPoolFn.apply(x)
     return torch.flatten(pool(x), 1)

@@ -23,6 +23,8 @@ from typing import Dict, List, Optional, Sequence
 
 import torch
 
+from ..ops._ext import h16
+
 ALIGN = 64  # elements: keeps every segment 256-B aligned for 16-B vector loads
 
 
@@ -135,7 +137,7 @@ class GradArena:
         if self.param_buf is None:
             return
         if getattr(self, "param_bf16", None) is None:
-            self.param_bf16 = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+            self.param_bf16 = torch.empty(self.numel, dtype=h16(), device=self.device)
             for s in self.segments:
                 view = _dense_strided_view(self.param_bf16, s.offset, s.param.data)
                 s.param._lw_bf16_of = (lambda v=view, s=s: v if self.bf16_valid(s) else None)

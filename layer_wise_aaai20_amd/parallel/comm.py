@@ -127,7 +127,7 @@ class NativeRccl:
     broadcast through it, then every rank joins with ``ncclCommInitRank``."""
 
     def __init__(self, group=None, device=None, uid: Optional[torch.Tensor] = None):
-        from ..ops._ext import load
+        from ..ops._ext import load_main as load
         self.lib = load()
         self.world = world_size(group)
         self.rank = rank(group)
@@ -187,7 +187,7 @@ class Watchdog:
     ``comm_handle=0`` watches the step deadline only."""
 
     def __init__(self, comm_handle: int, device, timeout_s: float, action: int = 0):
-        from ..ops._ext import load
+        from ..ops._ext import load_main as load
         self.lib = load()
         dev = torch.device(device)
         self.handle = int(self.lib.rccl_watch_start(int(comm_handle), float(timeout_s),
@@ -247,7 +247,7 @@ def _init_native_agreed(group, device) -> Optional[NativeRccl]:
     some ranks waiting in an init that one of them never joins."""
     uid = torch.zeros(128, dtype=torch.uint8)
     try:
-        from ..ops._ext import load
+        from ..ops._ext import load_main as load
         lib = load()
         if rank(group) == 0:
             uid = lib.rccl_unique_id()

@@ -61,7 +61,7 @@ def short_run_top1(device, steps: int = 300, size: int = 128, batch: int = 256,
     with torch.no_grad():
         for _ in range(eval_batches):
             x, t = make_batch(eg)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=tr.dtype):
                 out = model(tr.normalize(x)).float()
             top5 = out.topk(5, 1).indices
             counts[0] += (top5[:, 0] == t).sum()

@@ -15,6 +15,7 @@ from torch import nn
 
 from ..models import resnet as resnet_models
 from ..ops import nn as lwnn
+from ..ops._ext import set_half
 from ..optim.flat_sgd import FlatSGD
 from ..parallel.ddp import CompressedDDP
 from .graphs import StepGraph
@@ -53,11 +54,14 @@ class ImageNetTrainer:
     def __init__(self, ddp: CompressedDDP, optimizer, device, dtype=torch.bfloat16,
                  criterion: Optional[nn.Module] = None, channels_last: bool = True,
                  graph: Optional[bool] = None, graph_warmup: int = 3,
-                 graph_auto: Optional[bool] = None):
+                 graph_auto: Optional[bool] = None, loss_scale: float = 1.0):
         self.ddp = ddp
         self.opt = optimizer
         self.device = device
         self.dtype = dtype
+        # static loss scale (fp16: the reference's --loss-scale, train_imagenet_nv.py:412-428);
+        # the optimizer unscales inside its kernel (FlatSGD grad_scale = 1 / loss_scale)
+        self.loss_scale = float(loss_scale)
         self.channels_last = channels_last
         self.criterion = criterion or lwnn.FusedCrossEntropyLoss()
         self.mean = torch.tensor(IMAGENET_MEAN, device=device, dtype=torch.float32)
@@ -88,7 +92,7 @@ class ImageNetTrainer:
     def _eager(self, images_u8_nhwc: torch.Tensor, target: torch.Tensor):
         x = self.normalize(images_u8_nhwc)
         out, loss = self.forward_loss(x, target)
-        loss.backward()
+        (loss * self.loss_scale if self.loss_scale != 1.0 else loss).backward()
         self.opt.step()
         return out.detach(), target, loss.detach()
 
@@ -113,10 +117,21 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
                   fused=True, momentum=0.9, weight_decay=1e-4, no_bn_wd=True, lr=0.1,
                   bn0=True, wire="auto", graph=None, graph_warmup: int = 3,
                   world_size=None, graph_auto=None, dense_below=0,
-                  momentum_correction=False) -> ImageNetTrainer:
+                  momentum_correction=False, loss_scale=None) -> ImageNetTrainer:
     """``world_size``: build the codecs for that many ranks without a process group (a simulated
-    world driven by ``parallel/loopback.py``); default: the process group's size."""
+    world driven by ``parallel/loopback.py``); default: the process group's size.
+
+    ``dtype="fp16"`` with ``fused``: the reference's fp16 recipe on the MFMA kernels — the fp16
+    build of the kernel library (``ops/_ext.py set_half``), fp32 master weights with an fp16
+    mirror written by the SGD kernel, and a static loss scale (default 1024, as the reference's
+    ``--loss-scale``) unscaled inside that kernel."""
     device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    tdtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype] \
+        if isinstance(dtype, str) else dtype
+    if fused and device.type == "cuda":
+        set_half(tdtype == torch.float16)       # before any 16-bit buffer or kernel choice
+    if loss_scale is None:
+        loss_scale = 1024.0 if tdtype == torch.float16 else 1.0
     net = build_model(model, bn0=bn0) if isinstance(model, str) else model
     if fused:
         lwnn.fuse_resnet(net)
@@ -133,8 +148,6 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
     groups = bn_param_groups(net, weight_decay, no_bn_wd)
     om = 0.0 if mc > 0 else momentum
     opt = FlatSGD(groups, ddp.arena, lr=lr, momentum=om, nesterov=om > 0,
-                  weight_decay=weight_decay)
-    tdtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype] \
-        if isinstance(dtype, str) else dtype
+                  weight_decay=weight_decay, grad_scale=1.0 / float(loss_scale))
     return ImageNetTrainer(ddp, opt, device, tdtype, graph=graph, graph_warmup=graph_warmup,
-                           graph_auto=graph_auto)
+                           graph_auto=graph_auto, loss_scale=loss_scale)

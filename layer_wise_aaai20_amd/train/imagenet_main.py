@@ -37,6 +37,7 @@ from torch import nn
 from ..data import imagenet as D
 from ..models import resnet as R
 from ..ops import nn as lwnn
+from ..ops._ext import h16, set_half
 from ..parallel import comm
 from ..parallel import functional as F
 from ..parallel.ddp import CompressedDDP, DistributedDataParallel, RandomKSparsifiedDDP
@@ -336,8 +337,7 @@ def _fast_step(run, model, criterion, optimizer, eng):
     args = run.args
 
     def body(inp, target):
-        with torch.autocast(device_type=inp.device.type, dtype=torch.bfloat16,
-                            cache_enabled=False):
+        with torch.autocast(device_type=inp.device.type, dtype=h16(), cache_enabled=False):
             output = model(inp)
             loss = criterion(output.float(), target)
         (loss * args.loss_scale if args.fp16 else loss).backward()
@@ -547,15 +547,15 @@ def main(argv=None):
     # (FlatSGD; --fp16 keeps its static loss scale, unscaled inside the SGD kernel). --no-fused
     # selects the reference's structure (torch layers, post-backward sync, torch SGD).
     run.fast = fast = device.type == "cuda" and not args.no_fused
-    if fast and args.fp16:
-        # The MFMA kernels of the fast path compute in bf16 (same 16-bit class, no loss scale
-        # needed). --fp16 asks for the reference's numerics: fp16 model with fp32 BatchNorm,
-        # fp32 master weights and the static loss scale (train_imagenet_nv.py:410-428,
-        # fp16util.py:21-138), so it runs the reference-structure path — never silently bf16.
-        log.console("--fp16: running the reference fp16 path (fp16 model + fp32 BN, fp32 master "
-                    f"weights, static loss scale {args.loss_scale}); the fused MFMA path is bf16 "
-                    "(drop --fp16 to use it)")
-        run.fast = fast = False
+    if fast:
+        # --fp16 on the fused path: the fp16 build of the same MFMA kernels
+        # (v_mfma_f32_16x16x32_f16, ops/_ext.py set_half), fp32 master weights with an fp16
+        # mirror written by the SGD kernel, the static loss scale unscaled inside it
+        # (train_imagenet_nv.py:410-428, fp16util.py:21-138). Without --fp16 the fused path
+        # runs bf16 (no loss scale needed).
+        set_half(bool(args.fp16))
+        if args.fp16:
+            log.console(f"--fp16: fused MFMA path in fp16, static loss scale {args.loss_scale}")
     if fast:
         lwnn.fuse_resnet(model)
     model = model.to(device)
@@ -626,7 +626,7 @@ def main(argv=None):
         optimizer = torch.optim.SGD(opt_params, 0.0, weight_decay=args.weight_decay)
 
     phases = parse_phases(args.phases)
-    dtype = torch.bfloat16 if fast else (torch.float16 if args.fp16 else torch.float32)
+    dtype = h16() if fast else (torch.float16 if args.fp16 else torch.float32)
     args.pad4 = fast and bool(getattr(base_model, "_lw_stem_c4", False))
     dm = DataManager([copy.deepcopy(p) for p in phases if "bs" in p], args, device, dtype,
                      log, tb)

@@ -183,7 +183,10 @@ def test_stem_pool_backward_zero_gamma(shape, monkeypatch):
 def test_stem_pool_backward_ill_conditioned_channels(shape, monkeypatch):
     """|gamma| ~ 1e-3 with beta ~ 0.5: recovering x - mean from the bf16 pooled value would put
     a per-channel bias into dgamma. Per channel, the pooled-side pass must agree with the
-    full-resolution pass (which reads x itself) and with an fp32 torch reference."""
+    full-resolution pass (which reads x itself). An fp32 torch reference pins the well-conditioned
+    channels only: on the others bn(x) ~ beta +- 1e-3 rounds to a handful of bf16 values, so the
+    bf16 forward's max-pool argmax (which both backward passes share) and fp32's pick different
+    pixels and no 16-bit implementation can match it."""
     from layer_wise_aaai20_amd.ops import nn as NN
     from layer_wise_aaai20_amd.ops.nn import stem_bn_relu_pool
     torch.manual_seed(5)
@@ -191,7 +194,8 @@ def test_stem_pool_backward_ill_conditioned_channels(shape, monkeypatch):
     bn0 = torch.nn.BatchNorm2d(C).cuda()
     bn0.weight.data.uniform_(0.5e-3, 2e-3)
     bn0.weight.data[1::2] *= -1
-    bn0.weight.data[::4] = torch.empty(C // 4, device="cuda").uniform_(0.5, 1.5)  # well-conditioned
+    good = torch.arange(0, C, 4)
+    bn0.weight.data[good] = torch.empty(len(good), device="cuda").uniform_(0.5, 1.5)
     bn0.bias.data.uniform_(0.3, 0.7)
     pool = torch.nn.MaxPool2d(3, 2, 1)
     c = torch.randn(*shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
@@ -207,15 +211,25 @@ def test_stem_pool_backward_ill_conditioned_channels(shape, monkeypatch):
     bnr = copy.deepcopy(bn0).float()
     cr = c.float().requires_grad_()
     pool(torch.relu(bnr(cr))).backward(g.float())
-    for (dx, dg, db) in res.values():
-        scale = dg.abs().max()
-        assert ((dg - bnr.weight.grad).abs() < 3e-2 * scale + 1e-3).all(), \
-            (dg - bnr.weight.grad).abs().max()
-        torch.testing.assert_close(db, bnr.bias.grad, rtol=2e-2, atol=2e-2 * db.abs().max())
-        for ch in range(C):                      # every channel's dx, not just the whole tensor
-            assert _rel(dx[:, ch], cr.grad[:, ch]) < 5e-2, ch
-    torch.testing.assert_close(res[True][1], res[False][1], rtol=2e-2,
-                               atol=2e-2 * res[False][1].abs().max())
+    (dxp, dgp, dbp), (dxf, dgf, dbf) = res[True], res[False]
+    # pooled-side vs full-resolution: every channel (the ill-conditioned ones included)
+    # (dgamma is a cancelling sum: the two passes' rounding differs by ~1e-3 of its largest
+    # channel; the bias the pooled inversion would add on an ill-conditioned channel is O(1) of it)
+    sc = float(dgf.abs().max())
+    for ch in range(C):
+        assert abs(float(dgp[ch] - dgf[ch])) < 1e-2 * sc, (ch, dgp[ch], dgf[ch])
+        assert _rel(dxp[:, ch], dxf[:, ch]) < 2e-2, ch
+    torch.testing.assert_close(dbp, dbf, rtol=1e-2, atol=1e-2 * dbf.abs().max())
+    # both against fp32 torch on the well-conditioned channels
+    for (_, dg, db) in res.values():
+        ref = bnr.weight.grad[good]
+        assert ((dg[good] - ref).abs() < 3e-2 * ref.abs().max() + 1e-3).all(), \
+            (dg[good] - ref).abs().max()
+        torch.testing.assert_close(db[good], bnr.bias.grad[good], rtol=2e-2,
+                                   atol=2e-2 * db[good].abs().max())
+    # (dx is not compared with fp32 elementwise: bf16 ties in a 3x3 window send a pixel's
+    # gradient to a different argmax than fp32 picks; test_stem_bn_relu_pool_matches_layers
+    # pins dx against the unfused bf16 layers instead)
 
 
 def test_backward_stats_epilogues_match_reduce_pass(monkeypatch):

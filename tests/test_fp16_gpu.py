@@ -1,0 +1,243 @@
+"""The reference's --fp16 recipe on the hand-written MFMA kernels.
+
+``ops/_ext.set_half(True)`` switches the fused path to the fp16 build of the same kernels
+(``_lwaaai16_C.so``, csrc/elem16.h: v_mfma_f32_16x16x32_f16, fp16 conversions). Every check is
+against a plain fp32 PyTorch reference of the same op: GEMM tiles and layouts, the implicit-GEMM
+and tap-reuse convolutions (forward / data gradient / weight gradient), the fused bottleneck, and
+a whole fused ResNet-50 training step with the static loss scale unscaled inside the SGD kernel
+(reference: IMAGENET/training/train_imagenet_nv.py:410-428, fp16util.py:21-138)."""
+import copy
+import statistics
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from layer_wise_aaai20_amd.ops import _ext
+
+pytestmark = pytest.mark.gpu
+CL = torch.channels_last
+
+
+@pytest.fixture(autouse=True)
+def half():
+    _ext.set_half(True)
+    yield
+    _ext.set_half(False)
+
+
+def _close(a, b, tol):
+    err = (a.float() - b.float()).abs().max().item()
+    scale = b.float().abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err:.3e} vs scale {scale:.3e}"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
+def test_half_mode_loads_the_fp16_library():
+    lib = _ext.load()
+    assert lib is torch.ops.lwaaai16
+    assert _ext.h16() == torch.float16
+    assert _ext.load_main() is torch.ops.lwaaai
+    from layer_wise_aaai20_amd.ops import gemm as G
+    a = torch.randn(64, 64, device="cuda").half()
+    c, _ = G.gemm_ex(a, 64, True, a, 64, True, 64, 64, 64, out_bf16=True)
+    assert c.dtype == torch.float16
+    # a bf16 operand reaching the fp16 library fails loudly instead of being misread
+    with pytest.raises(RuntimeError):
+        G.gemm_ex(a.bfloat16(), 64, True, a.bfloat16(), 64, True, 64, 64, 64, out_bf16=True)
+
+
+@pytest.mark.parametrize("tile", ["128x128x32", "128x128x64", "256x64x32", "64x256x32",
+                                  "256x64x64", "64x64x64", "256x256x64", "256x128x64"])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_tiles_fp16(tile, a_kc, b_kc):
+    from layer_wise_aaai20_amd.ops import gemm as G
+    if tile.startswith("256x2") or tile.startswith("256x128"):
+        if not ((a_kc and b_kc) or (a_kc and not b_kc) or (not a_kc and not b_kc)):
+            pytest.skip("big tiles: no M-contiguous A with K-contiguous B")
+    torch.manual_seed(1)
+    M, N, K = 520, 200, 328
+    Am = torch.randn(M, K, device="cuda").half()
+    Bm = torch.randn(K, N, device="cuda").half()
+    A = Am.contiguous() if a_kc else Am.t().contiguous()
+    B = Bm.t().contiguous() if b_kc else Bm.contiguous()
+    ref = Am.float() @ Bm.float()
+    for splits in (1, 2):
+        C, _ = G.gemm_ex(A, K if a_kc else M, a_kc, B, K if b_kc else N, b_kc, M, N, K,
+                         splits=splits, out_bf16=False, tile=tile)
+        torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
+    # 16-bit output: fp16 keeps 3 more mantissa bits than bf16
+    C, _ = G.gemm_ex(A, K if a_kc else M, a_kc, B, K if b_kc else N, b_kc, M, N, K,
+                     out_bf16=True, tile=tile)
+    assert C.dtype == torch.float16
+    _close(C, ref, 2e-3)
+
+
+def test_gemm_stats_epilogue_fp16():
+    from layer_wise_aaai20_amd.ops import gemm as G
+    torch.manual_seed(2)
+    M, N, K = 1000, 136, 96
+    x = torch.randn(M, K, device="cuda").half()
+    w = torch.randn(N, K, device="cuda").half()
+    C, st = G.gemm_ex(x, K, True, w, K, True, M, N, K, tile="128x128x32", stats=True)
+    c = C.float()
+    torch.testing.assert_close(st[:, 0].sum(0), c.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[:, 1].sum(0), (c * c).sum(0), rtol=1e-4, atol=1e-1)
+
+
+# (N, Cin, Cout, H, k, stride, pad): ResNet-50 3x3 (both tap-reuse shapes and strided), stem,
+# CIFAR, odd sizes
+CONV_SHAPES = [(4, 64, 64, 56, 3, 1, 1), (4, 128, 128, 28, 3, 2, 1), (4, 256, 256, 14, 3, 1, 1),
+               (2, 3, 64, 112, 7, 2, 3), (8, 64, 128, 32, 3, 1, 1), (3, 24, 40, 13, 3, 2, 0)]
+
+
+def _conv_inputs(N, C, Co, H, k, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    x = torch.randn(N, C, H, H, device="cuda", generator=g).half()
+    w = (torch.randn(Co, C, k, k, device="cuda", generator=g) / (C * k * k) ** 0.5).half()
+    return x.contiguous(memory_format=CL), w.contiguous(memory_format=CL)
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES, ids=[str(s) for s in CONV_SHAPES])
+def test_conv_fwd_dgrad_wgrad_fp16(shape):
+    from layer_wise_aaai20_amd.ops import conv as CV
+    N, C, Co, H, k, s, p = shape
+    x, w = _conv_inputs(N, C, Co, H, k)
+    xf, wf = x.float().requires_grad_(), w.float().requires_grad_()
+    ref = F.conv2d(xf, wf, stride=s, padding=p)
+    y, _ = CV.conv_fwd(x, w, s, p)
+    assert y.dtype == torch.float16
+    _close(y, ref, 3e-3)
+    dy = torch.randn_like(ref).half().contiguous(memory_format=CL)
+    ref.backward(dy.float())
+    if C % 8 == 0:
+        dx = CV.conv_dgrad(dy, w, (H, H), s, p)
+        assert dx.dtype == torch.float16
+        _close(dx, xf.grad, 3e-3)
+    dw = CV.conv_wgrad(dy, x, tuple(w.shape), s, p)
+    _close(dw, wf.grad, 2e-3)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64, 56), (2, 128, 128, 28), (4, 256, 256, 14)])
+def test_conv3_tap_fp16(shape):
+    """The tap-reuse 3x3 kernels (csrc/conv3tap.hip) in the fp16 build."""
+    from layer_wise_aaai20_amd.ops import conv as CV
+    N, C, Co, H = shape
+    lib = _ext.load()
+    x, w = _conv_inputs(N, C, Co, H, 3, 4)
+    xf, wf = x.float().requires_grad_(), w.float().requires_grad_()
+    ref = F.conv2d(xf, wf, padding=1)
+    op, _, _ = CV.pack_fwd_weight(w)
+    y, _ = lib.conv3_tap(x, op, Co, False)
+    _close(y, ref, 3e-3)
+    dy = torch.randn_like(ref).half().contiguous(memory_format=CL)
+    ref.backward(dy.float())
+    dx, _ = lib.conv3_tap(dy, CV.tap_dgrad_weight(w), C, False)
+    _close(dx, xf.grad, 3e-3)
+    dw = lib.conv3_tap_wgrad(dy, x, None, False)
+    _close(dw, wf.grad, 2e-3)
+
+
+def _bottleneck(inplanes, planes, stride, down):
+    from layer_wise_aaai20_amd.models.resnet import Bottleneck, conv1x1
+    ds = None
+    if down:
+        ds = torch.nn.Sequential(conv1x1(inplanes, planes * 4, stride),
+                                 torch.nn.BatchNorm2d(planes * 4))
+    m = Bottleneck(inplanes, planes, stride, ds)
+    for bn in [m.bn1, m.bn2, m.bn3] + ([ds[1]] if down else []):
+        bn.weight.data.uniform_(0.5, 1.5)
+        bn.bias.data.normal_(0, 0.2)
+    for p in m.parameters():     # fp16-representable weights: both paths see the same values
+        p.data = p.data.half().float()
+    return m
+
+
+@pytest.mark.parametrize("inplanes,planes,stride,down", [(256, 64, 1, False), (256, 128, 2, True)])
+def test_bottleneck_fp16_matches_fp32(inplanes, planes, stride, down):
+    from layer_wise_aaai20_amd.ops import block as blk
+    from layer_wise_aaai20_amd.ops.nn import fuse_resnet
+    torch.manual_seed(0)
+    ref = _bottleneck(inplanes, planes, stride, down).cuda().to(memory_format=CL)
+    m = copy.deepcopy(ref)
+    x = torch.randn(8, inplanes, 14, 14, device="cuda").half().contiguous(memory_format=CL)
+    xf = x.float().requires_grad_()
+    y_ref = ref(xf)
+    g = torch.randn_like(y_ref)
+    y_ref.backward(g)
+    fuse_resnet(m, block=True)
+    xb = x.clone().requires_grad_()
+    assert blk.block_supported(m, xb)
+    with torch.autocast("cuda", dtype=torch.float16):
+        y = m(xb)
+    assert y.dtype == torch.float16
+    y.backward(g.half())
+    assert _rel(y, y_ref) < 5e-3
+    assert _rel(xb.grad, xf.grad) < 0.05
+    for (n, p), r in zip(m.named_parameters(), ref.parameters()):
+        assert _rel(p.grad, r.grad) < 0.08, n
+
+
+def test_resnet50_fp16_fused_grads_match_fp32():
+    """Whole fused ResNet-50 forward + backward in fp16 (loss-scaled) vs the fp32 torch model:
+    same loss, and the per-parameter gradient errors (after unscaling) at the fp16 noise level."""
+    from layer_wise_aaai20_amd.models.resnet import resnet50
+    from layer_wise_aaai20_amd.ops.nn import fuse_resnet, share_bn_counters
+    torch.manual_seed(2)
+    ref = resnet50().cuda()
+    for p in ref.parameters():
+        p.data = p.data.half().float()
+    m = copy.deepcopy(ref)
+    ref = ref.to(memory_format=CL)
+    x = torch.randn(16, 3, 96, 96, device="cuda").half().float().contiguous(memory_format=CL)
+    t = torch.randint(0, 1000, (16,), device="cuda")
+    ref_loss = F.cross_entropy(ref(x), t)
+    ref_loss.backward()
+    fuse_resnet(m, block=True)
+    m.to(memory_format=CL)
+    share_bn_counters(m)
+    scale = 1024.0
+    with torch.autocast("cuda", dtype=torch.float16):
+        out = m(x)
+    loss = F.cross_entropy(out.float(), t)
+    (loss * scale).backward()
+    assert abs(float(loss) - float(ref_loss)) < 1e-2 * abs(float(ref_loss))
+    errs = [_rel(p.grad / scale, q.grad) for p, q in zip(m.parameters(), ref.parameters())]
+    assert all(e == e for e in errs), "non-finite gradient (fp16 overflow)"
+    assert statistics.median(errs) < 0.1, statistics.median(errs)
+    assert errs[-1] < 0.02                     # fc.bias: only the softmax output enters
+
+
+def test_resnet50_fp16_trainer_step_matches_fp32_sgd():
+    """One fused fp16 training step (graph off, no compression): the fp16 weight mirror the SGD
+    kernel writes, the loss scale unscaled in that kernel, against torch SGD on the fp32 model."""
+    from layer_wise_aaai20_amd.train.imagenet import build_trainer
+    torch.manual_seed(3)
+    tr = build_trainer("resnet50", device="cuda", compress="none", method="none", dtype="fp16",
+                       graph=False, lr=0.05, momentum=0.9, weight_decay=1e-4, no_bn_wd=True)
+    assert tr.loss_scale == 1024.0 and _ext.half()
+    net = tr.ddp.module
+    assert tr.ddp.arena.param_bf16.dtype == torch.float16
+    p0 = {n: p.detach().clone() for n, p in net.named_parameters()}
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randint(0, 256, (8, 64, 64, 3), dtype=torch.uint8, device="cuda", generator=g)
+    t = torch.randint(0, 1000, (8,), device="cuda", generator=g)
+    loss = float(tr.step(x, t))
+    assert loss == loss and 3.0 < loss < 12.0
+    moved = [float((p.detach() - p0[n]).norm() / p0[n].norm().clamp_min(1e-12))
+             for n, p in net.named_parameters() if p.dim() > 1]
+    # lr 0.05 on unit-scale gradients: a loss scale left in the update would move the weights
+    # ~1000x further; a missing step would not move them at all
+    assert 0 < statistics.median(moved) < 0.5, statistics.median(moved)
+    # the fp16 mirror the next forward reads equals the fp32 master weights rounded
+    for seg in tr.ddp.arena.segments[:20]:
+        a = tr.ddp.arena.param_buf[seg.offset:seg.offset + seg.numel]
+        b = tr.ddp.arena.param_bf16[seg.offset:seg.offset + seg.numel]
+        torch.testing.assert_close(b, a.half(), rtol=0, atol=0)
+    for _ in range(3):
+        tr.step(x, t)
+    assert float(tr.step(x, t)) < loss        # same batch: the loss goes down

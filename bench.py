@@ -63,6 +63,10 @@ def parse():
     ap.add_argument("--threshold", "-V", type=float, default=0.001)
     ap.add_argument("--qstates", "-Q", type=int, default=255)
     ap.add_argument("--ef", action="store_true", help="error feedback")
+    ap.add_argument("--ef-dense-below", type=int, default=0,
+                    help="opt-in EF variant: tensors of at most this many elements sent densely")
+    ap.add_argument("--momentum-correction", action="store_true",
+                    help="opt-in EF variant: DGC momentum correction (profiles/r4/ef_root_cause.md)")
     # 50 MB: 3 buckets for ResNet-50's 97.5 MiB fp32 arena. Inside a captured step each bucket is
     # compressed + exchanged inline, so fewer buckets = fewer launches / collectives: 24.29 ms
     # vs 24.47-24.50 ms at the reference's 25 MB (profiles/r2_bucket_mb_graph.log)
@@ -153,7 +157,8 @@ def main():
     tr = build_trainer(model=args.model, device=dev, compress=args.compress, method=args.method,
                        K=args.ratio, V=args.threshold, qstates=args.qstates,
                        error_feedback=args.ef, bucket_cap_mb=args.bucket_mb, dtype=args.dtype,
-                       fused=not args.no_fused, momentum=0.9, weight_decay=1e-4, no_bn_wd=True,
+                       dense_below=args.ef_dense_below,
+                       momentum_correction=args.momentum_correction, fused=not args.no_fused, momentum=0.9, weight_decay=1e-4, no_bn_wd=True,
                        lr=0.1, graph=args.graph == "on" and args.warmup >= 2,
                        # capture inside the untimed warm-up: at least one eager step (tile tuner,
                        # lazily built device tables, allocator, RCCL warm), then capture + replay
@@ -216,10 +221,13 @@ def main():
         acc = short_run_top1(dev, steps=args.acc_steps, size=128, batch=256, rank=rank,
                              world=world, compress=args.compress, method=args.method,
                              K=args.ratio, V=args.threshold, qstates=args.qstates,
-                             error_feedback=args.ef, dtype=args.dtype)
+                             error_feedback=args.ef, dtype=args.dtype,
+                             dense_below=args.ef_dense_below,
+                             momentum_correction=args.momentum_correction)
     value = world * B * args.steps / dt
     default = (args.model == "resnet50" and args.compress == "layerwise" and args.method == "Topk"
-               and args.ratio == 0.001 and not args.ef)
+               and args.ratio == 0.001 and not args.ef and args.ef_dense_below == 0
+               and not args.momentum_correction)
     metric = BASELINE_METRIC if default else (
         f"images/sec/node, {args.model} {args.compress} {args.method}"
         f"{' K=' + str(args.ratio) if args.method in ('Topk', 'Randomk') else ''}"
@@ -262,6 +270,8 @@ def main():
             "method": args.method,
             "ratio": args.ratio,
             "error_feedback": args.ef,
+            "ef_dense_below": args.ef_dense_below,
+            "momentum_correction": args.momentum_correction,
             "wire_bytes_per_rank": stats.payload_bytes,
             "selection_overflow": overflow,
             "dense_grad_bytes": stats.dense_bytes,

@@ -29,7 +29,8 @@ class CifarTrainer:
                  V=None, qstates=None, error_feedback=False, batch_size=512, epochs=24,
                  momentum=0.9, dtype=torch.bfloat16, bucket_cap_mb=25.0, wire="auto",
                  n_train=50000, seed=0, fused=True, graph=None, n_test=1000,
-                 task="textures", amp=None, dense_below=0, momentum_correction=False):
+                 task="textures", amp=None, dense_below=0, momentum_correction=False,
+                 lr_scale=1.0):
         self.device = torch.device(device or "cuda")
         self.dtype = dtype
         self.bs = batch_size
@@ -66,7 +67,9 @@ class CifarTrainer:
                                     batch_size, shuffle=True, augment=True, drop_last=True,
                                     seed=seed, channels_last=self.device.type == "cuda",
                                     dtype=torch.float32)
-        self.sched = PiecewiseLinear([0, 5, epochs], [0, 0.4, 0])
+        # lr_scale: the peak LR as a multiple of the dawn recipe's 0.4 (the Random-K + EF
+        # stability sweep, scripts/ef_trace.py)
+        self.sched = PiecewiseLinear([0, 5, epochs], [0, 0.4 * float(lr_scale), 0])
         self.steps_per_epoch = len(self.batches)
         self.step_count = 0
         self._it = None

@@ -89,6 +89,13 @@ def get_parser():
     p.add_argument("--arch", default="resnet50")
     p.add_argument("--overlap", action="store_true", help="CompressedDDP (bucketed, overlapped)")
     p.add_argument("--error-feedback", action="store_true")
+    # opt-in EF variants (fused path; profiles/r4/ef_root_cause.md)
+    p.add_argument("--ef-dense-below", type=int, default=0,
+                   help="send tensors of at most this many elements densely (e.g. 4096: BN "
+                        "parameters and biases)")
+    p.add_argument("--momentum-correction", action="store_true",
+                   help="DGC momentum correction: the velocity lives in the EF residual and the "
+                        "optimizer runs without momentum")
     p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "sparse-capped", "dense", "indexfree"])
     p.add_argument("--epochs", type=int, default=None, help="stop after this many epochs")
     p.add_argument("--synthetic-size", type=int, default=None,
@@ -565,17 +572,20 @@ def main(argv=None):
         model = fp16util.network_to_half(model)
     base_model = model
     sync = lambda m: None                                       # noqa: E731
+    mc = float(args.momentum) if args.momentum_correction else 0.0
     if fast:
         if args.ddp:
             model = DistributedDataParallel(model, flat_params=True)
         elif args.sparsification:
             model = RandomKSparsifiedDDP(model, randk=args.randk, seed=args.seed,
-                                         flat_params=True)
+                                         flat_params=True, dense_below=args.ef_dense_below,
+                                         momentum_correction=mc)
         else:
             model = CompressedDDP(model, compress=args.compress, method=args.method,
                                   K=args.ratio, V=args.threshold, qstates=args.qstates,
                                   error_feedback=args.error_feedback, wire=args.wire,
-                                  flat_params=True)
+                                  flat_params=True, dense_below=args.ef_dense_below,
+                                  momentum_correction=mc)
     elif args.ddp:
         model = DistributedDataParallel(model)
     elif args.sparsification:
@@ -601,8 +611,9 @@ def main(argv=None):
         groups = _bn_groups(base_model, None, args.weight_decay) if args.no_bn_wd else \
             [{"params": [p for p in base_model.parameters() if p.requires_grad],
               "weight_decay": args.weight_decay}]
-        optimizer = FlatSGD(groups, model.arena, lr=0.0, momentum=args.momentum,
-                            nesterov=args.momentum > 0, weight_decay=args.weight_decay,
+        om = 0.0 if mc > 0 else args.momentum        # DGC: the residual holds the velocity
+        optimizer = FlatSGD(groups, model.arena, lr=0.0, momentum=om,
+                            nesterov=om > 0, weight_decay=args.weight_decay,
                             grad_scale=1.0 / args.loss_scale if args.fp16 else 1.0)
     elif args.fp16:
         master = fp16util.prep_param_lists(model)

@@ -41,7 +41,16 @@ METHODS = {"none": dict(compress="none", method="none"),
                                        error_feedback=True, dense_below=4096),
            "topk0.1%+ef+mc+dense4k": dict(compress="layerwise", method="Topk", K=0.001,
                                           error_feedback=True, dense_below=4096,
-                                          momentum_correction=True)}
+                                          momentum_correction=True),
+           "topk0.1%+ef+mc": dict(compress="layerwise", method="Topk", K=0.001,
+                                  error_feedback=True, momentum_correction=True),
+           "topk0.1%+dense4k": dict(compress="layerwise", method="Topk", K=0.001,
+                                    dense_below=4096),
+           "randk1%+ef": dict(compress="layerwise", method="Randomk", K=0.01,
+                              error_feedback=True),
+           "randk1%+ef+mc+dense4k": dict(compress="layerwise", method="Randomk", K=0.01,
+                                         error_feedback=True, dense_below=4096,
+                                         momentum_correction=True)}
 
 
 def main():

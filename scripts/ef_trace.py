@@ -36,6 +36,20 @@ RUNS = [
     ("topk0.1+ef", "Topk", "layerwise", {"K": 0.001}, True, {}),
     ("topk0.1+ef+mc+dense4k", "Topk", "layerwise", {"K": 0.001}, True,
      {"momentum_correction": True, "dense_below": 4096}),
+    # 13-18: Random-K 1 % + EF at a lower peak LR (the residual releases ~1/K = 100 steps of
+    # gradient at once: a stale-gradient stability limit, not a bias)
+    ("randk1+ef lr/4", "Randomk", "layerwise", {"K": 0.01}, True, {"lr_scale": 0.25}),
+    ("randk1+ef lr/10", "Randomk", "layerwise", {"K": 0.01}, True, {"lr_scale": 0.1}),
+    ("randk1+ef+mc lr/4", "Randomk", "layerwise", {"K": 0.01}, True,
+     {"momentum_correction": True, "lr_scale": 0.25}),
+    ("randk1+ef+dense4k lr/4", "Randomk", "layerwise", {"K": 0.01}, True,
+     {"dense_below": 4096, "lr_scale": 0.25}),
+    ("randk10+ef+dense4k", "Randomk", "layerwise", {"K": 0.1}, True, {"dense_below": 4096}),
+    ("randk10+ef+mc+dense4k", "Randomk", "layerwise", {"K": 0.1}, True,
+     {"momentum_correction": True, "dense_below": 4096}),
+    # 19-20: the dense exemption alone at K = 0.1 %, and entire-model Top-K 1 % + EF
+    ("topk0.1+ef+dense4k", "Topk", "layerwise", {"K": 0.001}, True, {"dense_below": 4096}),
+    ("entire topk1+ef", "Topk", "entiremodel", {"K": 0.01}, True, {}),
 ]
 
 

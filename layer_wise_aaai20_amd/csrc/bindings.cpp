@@ -1366,19 +1366,15 @@ static void stem_geom(const Tensor& x, int64_t k, int64_t s, int64_t p, lw::Stem
               (int64_t)a.N * a.Ho * a.Wo * (a.C / 8) < (1LL << 31), "stem pool: tensor too large");
 }
 
-std::tuple<Tensor, Tensor> stem_pool_fwd(Tensor x, Tensor scale_shift, int64_t k, int64_t s,
-                                         int64_t p) {
-  const c10::DeviceGuard guard(x.device());
-  lw::StemArgs a{};
-  stem_geom(x, k, s, p, a);
-  check_dtype(scale_shift, at::kFloat, "scale_shift");
-  TORCH_CHECK(scale_shift.numel() == 2 * a.C && scale_shift.is_contiguous(), "scale_shift");
+// the forward pass on geometry `a` with BN coefficients `scale` / `shift` ([C] each)
+static std::tuple<Tensor, Tensor> pool_fwd_launch(const Tensor& x, lw::StemArgs& a,
+                                                  const float* scale, const float* shift) {
   Tensor out = at::empty({a.N, a.C, a.Ho, a.Wo},
                          x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor idx = at::empty({(int64_t)a.N * a.Ho * a.Wo * a.C}, x.options().dtype(at::kByte));
   a.x = x.data_ptr();
-  a.scale = ptr<float>(scale_shift);
-  a.shift = a.scale + a.C;
+  a.scale = scale;
+  a.shift = shift;
   a.out = out.data_ptr();
   a.idx = ptr<uint8_t>(idx);
   lw::stem_pool_fwd(a, cur_stream());
@@ -1386,20 +1382,30 @@ std::tuple<Tensor, Tensor> stem_pool_fwd(Tensor x, Tensor scale_shift, int64_t k
   return {out, idx};
 }
 
-// max-pool of a post-ReLU bf16 map (no BN): [scale 1][shift 0][A 1][B 0][C 0] constant vectors
-static Tensor relu_pool_consts(const Tensor& x, int64_t C) {
-  Tensor c = at::zeros({5 * C}, x.options().dtype(at::kFloat));
-  c.narrow(0, 0, C).fill_(1.0);
-  c.narrow(0, 2 * C, C).fill_(1.0);
-  return c;
+std::tuple<Tensor, Tensor> stem_pool_fwd(Tensor x, Tensor scale_shift, int64_t k, int64_t s,
+                                         int64_t p) {
+  const c10::DeviceGuard guard(x.device());
+  lw::StemArgs a{};
+  stem_geom(x, k, s, p, a);
+  check_dtype(scale_shift, at::kFloat, "scale_shift");
+  TORCH_CHECK(scale_shift.numel() == 2 * a.C && scale_shift.is_contiguous(), "scale_shift");
+  return pool_fwd_launch(x, a, ptr<float>(scale_shift), ptr<float>(scale_shift) + a.C);
+}
+
+// max-pool of a post-ReLU 16-bit map (no BN): scale / A = 1, shift / B / C = 0, read from the
+// device-resident [ones][zeros] table (bn.hip kPoolIdentity) instead of filled per call
+static const float* pool_ones(int64_t C) {
+  const float* base = lw::pool_identity_consts();
+  TORCH_CHECK(base != nullptr && C <= lw::kPoolIdC, "pool identity constants unavailable");
+  return base + (lw::kPoolIdC - C);           // C ones, then the zeros
 }
 
 std::tuple<Tensor, Tensor> relu_pool_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
   const c10::DeviceGuard guard(x.device());
   lw::StemArgs a{};
   stem_geom(x, k, s, p, a);
-  Tensor c = relu_pool_consts(x, a.C);
-  return stem_pool_fwd(x, c.narrow(0, 0, 2 * a.C), k, s, p);
+  const float* ones = pool_ones(a.C);
+  return pool_fwd_launch(x, a, ones, ones + a.C);
 }
 
 Tensor relu_pool_bwd(Tensor dp, Tensor idx, Tensor x, int64_t k, int64_t s, int64_t p) {
@@ -1410,18 +1416,19 @@ Tensor relu_pool_bwd(Tensor dp, Tensor idx, Tensor x, int64_t k, int64_t s, int6
   TORCH_CHECK(dp.is_contiguous(at::MemoryFormat::ChannelsLast) && dp.size(2) == a.Ho &&
               dp.size(3) == a.Wo && dp.size(1) == a.C && dp.size(0) == a.N, "dp shape/layout");
   TORCH_CHECK(idx.numel() == dp.numel() && idx.scalar_type() == at::kByte, "idx");
-  Tensor c = relu_pool_consts(x, a.C);
+  const float* ones = pool_ones(a.C);
+  const float* zeros = ones + a.C;
   Tensor dx = at::empty_like(x);
   a.x = x.data_ptr();
   a.dp = dp.data_ptr();
   a.idx = ptr<uint8_t>(idx);
   a.dx = dx.data_ptr();
-  a.scale = ptr<float>(c);
-  a.shift = a.scale + a.C;
-  a.mean = a.shift;                 // unused by the apply pass
-  a.A = ptr<float>(c) + 2 * a.C;
-  a.B = ptr<float>(c) + 3 * a.C;
-  a.Cc = ptr<float>(c) + 4 * a.C;
+  a.scale = ones;
+  a.shift = zeros;
+  a.mean = zeros;                   // unused by the apply pass
+  a.A = const_cast<float*>(ones);   // (read-only here: relu_pool_bwd only applies them)
+  a.B = const_cast<float*>(zeros);
+  a.Cc = const_cast<float*>(zeros);
   lw::relu_pool_bwd(a, cur_stream());
   launched("relu_pool_bwd");
   return dx;

@@ -1231,6 +1231,21 @@ static void pool_apply_geometry(int64_t rows, int C, int64_t& rpb, int& nb) {
 // apply pass with (A, B, C) = (1, 0, 0): dx = the routed pooled gradient masked by [x > 0], i.e.
 // the max-pool AND the preceding ReLU backward in one kernel. a.A / a.B / a.Cc / a.scale / a.shift
 // must hold those constants (the binding fills them).
+// [ones][zeros], kPoolIdC each, initialised at module load (no kernel, graph-capture safe)
+struct PoolIdentity { float v[2 * kPoolIdC]; };
+constexpr PoolIdentity make_pool_identity() {
+  PoolIdentity p{};
+  for (int i = 0; i < kPoolIdC; ++i) p.v[i] = 1.f;
+  return p;
+}
+__device__ PoolIdentity kPoolIdentity = make_pool_identity();
+
+const float* pool_identity_consts() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(kPoolIdentity)) != hipSuccess) return nullptr;
+  return static_cast<const float*>(p);
+}
+
 void relu_pool_bwd(const StemArgs& a, hipStream_t st) {
   const PoolGeom g{a.N, a.H, a.W, a.C, a.Ho, a.Wo, a.k, a.s, a.p};
   const auto* dp = static_cast<const uint16_t*>(a.dp);

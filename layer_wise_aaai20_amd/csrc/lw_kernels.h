@@ -183,6 +183,10 @@ struct StemArgs {
 void stem_pool_fwd(const StemArgs& a, hipStream_t st);
 void stem_pool_bwd(const StemArgs& a, hipStream_t st);
 void relu_pool_bwd(const StemArgs& a, hipStream_t st);   // pool + ReLU backward, no BN
+// kPoolIdC ones followed by kPoolIdC zeros in device memory (current device): the identity BN
+// constants of a plain ReLU max-pool, so a pool call needs no per-call fill kernels
+constexpr int kPoolIdC = 2048;
+const float* pool_identity_consts();
 
 // bf16 MFMA GEMM with fused epilogue (gemm.hip)
 struct GemmArgs {

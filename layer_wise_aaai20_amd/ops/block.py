@@ -181,7 +181,7 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
 
 
 LAYOUT_TUNER = Tuner("dgrad-layout", "LWAAAI_GEMM_TUNE")
-DGRAD_BLAS = os.environ.get("LWAAAI_DGRAD_BLAS", "1") != "0"
+DGRAD_BLAS = os.environ.get("LWAAAI_DGRAD_BLAS", "0") == "1"
 
 
 def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
@@ -192,9 +192,10 @@ def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
     apply. ``bst`` (backward statistics) needs the stored layout.
 
     A dgrad with no fused epilogue (no statistics, no masked addend) is a plain library GEMM, so
-    hipBLASLt (``torch.mm``) is a third candidate: it wins some short-K layer-3/4 shapes
-    (``profiles/r3s2/op_roofline_vendor_start.txt``: M50176 N256 K1024 33 vs 49 µs).
-    ``LWAAAI_DGRAD_BLAS=0`` keeps the hand-written kernels only."""
+    hipBLASLt (``torch.mm``) can be a third candidate (``LWAAAI_DGRAD_BLAS=1``): it wins some
+    short-K layer-3/4 shapes (``profiles/r3s2/op_roofline_vendor_start.txt``: M50176 N256 K1024
+    33 vs 49 µs), but the whole step gains only 0.3 % (11,354-11,370 vs 11,327-11,328 img/s on one
+    box, ``profiles/r4/dgrad_blas_ab.txt``), so by default every kernel of the step is ours."""
     def run(layout, **over):
         args = dict(kw, **over)
         if layout == "blas":

@@ -404,6 +404,14 @@ def _arena_view(p: torch.Tensor):
     return g
 
 
+def _bias_arena_view(b: Optional[torch.Tensor]):
+    """The bias's fp32 [C] gradient-arena view when the engine wants it written in place."""
+    if b is None or getattr(b, "_lw_grad_ready", None) is None or b.grad is None:
+        return None
+    g = b.grad
+    return g if g.dtype == torch.float32 and g.is_contiguous() and g.dim() == 1 else None
+
+
 class _ConvFn(torch.autograd.Function):
     """conv2d (+ bias) (+ ReLU) on the implicit-GEMM kernels. Bias and ReLU run in the forward
     epilogue; backward masks dy by the saved output and reduces the bias gradient in one pass
@@ -430,13 +438,20 @@ class _ConvFn(torch.autograd.Function):
         dx = dw = db = None
         dy = dy.to(h16()).contiguous(memory_format=CL)
         if ctx.relu or (b is not None and ctx.needs_input_grad[2]):
+            # an arena-managed bias gets its gradient accumulated in place by the fold kernel
+            # (no AccumulateGrad add kernel, no fresh [C] buffer)
+            db_dst = _bias_arena_view(b) if ctx.needs_input_grad[2] else None
             if dy.shape[1] % 8 == 0 and dy.shape[1] <= 2048:
-                dy, db = load().relu_bias_bwd(dy, y if ctx.relu else None, None)
+                dy, db = load().relu_bias_bwd(dy, y if ctx.relu else None, db_dst)
+                if db_dst is not None:
+                    b._lw_grad_ready(b)
+                    db = None
             else:
                 if ctx.relu:
                     dy = dy * (y > 0)
                 db = dy.float().sum((0, 2, 3))
-            db = db.to(b.dtype) if b is not None and ctx.needs_input_grad[2] else None
+            db = db.to(b.dtype) if db is not None and b is not None and \
+                ctx.needs_input_grad[2] else None
         if ctx.needs_input_grad[0]:
             dx = conv_dgrad(dy, wb, hw, stride, padding).to(xdtype)
         if ctx.needs_input_grad[1]:

@@ -8,8 +8,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -2 gpurun_out/full_smoke.log
 timeout -k 10 600 python bench.py --steps 20 --warmup 8 > gpurun_out/full_bench.log 2>&1 || { tail -20 gpurun_out/full_bench.log; exit 1; }
 tail -1 gpurun_out/full_bench.log
-timeout -k 10 900 bash scripts/prof_step.sh r3s2_final --acc-steps 0 > gpurun_out/full_prof.log 2>&1 || { tail -20 gpurun_out/full_prof.log; exit 1; }
-head -3 gpurun_out/r3s2_final_steps.txt
+timeout -k 10 900 bash scripts/prof_step.sh r4_final --acc-steps 0 > gpurun_out/full_prof.log 2>&1 || { tail -20 gpurun_out/full_prof.log; exit 1; }
+head -3 gpurun_out/r4_final_steps.txt
 timeout -k 10 600 python bench_cifar.py --config all > gpurun_out/full_cifar.log 2>&1 || { tail -20 gpurun_out/full_cifar.log; exit 1; }
 grep -o '"metric": "[^"]*", "value": [0-9.]*' gpurun_out/full_cifar.log
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 4 --warmup 2 --batch 64 --share-gpu --backend gloo --acc-steps 0 > gpurun_out/full_share2.log 2>&1 || { tail -20 gpurun_out/full_share2.log; exit 1; }

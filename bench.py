@@ -119,9 +119,10 @@ class _Heartbeat:
 
 def _reference_points(steps: int) -> str:
     """Reference points for the printed top-1, measured at the same step budget over several
-    seeds (profiles/r4/accuracy_reference.json, written by scripts/accuracy_r50.py runs)."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r4",
-                        "accuracy_reference.json")
+    seeds (layer_wise_aaai20_amd/train/accuracy_reference.json, folded by scripts/acc_reference.py
+    from scripts/accuracy_r50.py runs; the raw runs are in profiles/r4/)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "layer_wise_aaai20_amd",
+                        "train", "accuracy_reference.json")
     try:
         with open(path) as f:
             ref = json.load(f)
@@ -131,7 +132,8 @@ def _reference_points(steps: int) -> str:
         return ""
     parts = [f"{k}: {v['mean']:.1f}% (seeds {', '.join(f'{x:.1f}' for x in v['top1'])})"
              for k, v in ref.get("methods", {}).items()]
-    return "; reference points at this budget, " + "; ".join(parts) + f" ({path[-39:]})"
+    return ("; reference points at this budget, " + "; ".join(parts) +
+            " (layer_wise_aaai20_amd/train/accuracy_reference.json)")
 
 
 def main():

@@ -30,6 +30,10 @@
 namespace lw {
 
 constexpr int NT = 256;
+#ifndef LW_HIST_CP
+#define LW_HIST_CP 4             // interleaved LDS histogram copies in the first radix pass
+#endif
+static_assert((LW_HIST_CP & (LW_HIST_CP - 1)) == 0, "LW_HIST_CP: a power of two");
 constexpr int EPB = kLargeEPB;       // elements per block in the multi-block passes (8192)
 constexpr int EPT = EPB / NT;        // 32 contiguous elements per thread in k_write / k_quant
 constexpr int SEPT = kSmallMax / NT; // 16 per thread in k_small_select
@@ -268,13 +272,18 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   using C = PassCfg<PASS>;
   constexpr int NB = 1 << C::BITS;
-  __shared__ uint32_t h[NB];
+  // Pass 0 counts EVERY key, and gradient magnitudes cluster in a few exponent bins, so many
+  // lanes of one ds_add hit the same word and serialise. CP interleaved copies of the histogram
+  // (copy = lane % CP, bin-major so a bin's copies sit in adjacent banks) split those lanes;
+  // passes 1/2 count only the keys under the selected prefix and keep one copy.
+  constexpr int CP = PASS == 0 ? LW_HIST_CP : 1;
+  __shared__ uint32_t h[NB * CP];
   const int2 t = tasks[blockIdx.x];
   const int li = t.x, begin = t.y;
   const int s = large_segs[li];
   const int n = seg_n[s];
   const int64_t off = seg_off[s];
-  for (int b = threadIdx.x; b < NB; b += NT) h[b] = 0;
+  for (int b = threadIdx.x; b < NB * CP; b += NT) h[b] = 0;
   const uint32_t prefix = PASS > 0 ? st[li].prefix : 0u;
   __syncthreads();
   float* gp = g + off;
@@ -290,12 +299,14 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       if (valid[q] && (k[q] >> (C::SHIFT + C::BITS)) == prefix)
-        atomicAdd(&h[(k[q] >> C::SHIFT) & (NB - 1)], 1u);
+        atomicAdd(&h[((k[q] >> C::SHIFT) & (NB - 1)) * CP + (threadIdx.x & (CP - 1))], 1u);
   }
   __syncthreads();
   uint32_t* gh = hist_all + (size_t)li * HIST_WORDS + C::HOFF;
   for (int b = threadIdx.x; b < NB; b += NT) {
-    const uint32_t c = h[b];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < CP; ++j) c += h[b * CP + j];
     if (c) atomicAdd(gh + b, c);
   }
 }

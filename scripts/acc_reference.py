@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """Fold scripts/accuracy_r50.py output (one JSON line per (seed, method)) into the reference-point
-table bench.py quotes next to its top-1 (profiles/r4/accuracy_reference.json).
+table bench.py quotes next to its top-1 (layer_wise_aaai20_amd/train/accuracy_reference.json: package
+data, so it ships to the GPU box; profiles/ does not).
 usage: python scripts/acc_reference.py RUNS.jsonl [OUT.json]"""
 import json
 import statistics
@@ -9,7 +10,7 @@ import sys
 
 def main():
     src = sys.argv[1]
-    dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r4/accuracy_reference.json"
+    dst = sys.argv[2] if len(sys.argv) > 2 else "layer_wise_aaai20_amd/train/accuracy_reference.json"
     by, steps = {}, None
     for line in open(src):
         d = json.loads(line)

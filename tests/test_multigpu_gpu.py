@@ -1,6 +1,7 @@
 """World > 1 on real GPUs: one process per GPU over RCCL with the native communicator
 (``csrc/rccl.cpp``) and captured steps — the path the 8-GPU benchmark runs. Skipped unless the
-box has at least two GPUs; world 2 and world = device_count (capped at 8).
+box has at least two GPUs: world 2 and world = device_count (capped at 8); on a one-GPU box two
+ranks share the card.
 
 Checks, per configuration (layer-wise Top-K ± EF, entire-model QSGD-255, dense):
 
@@ -29,9 +30,16 @@ def _ngpu() -> int:
 
 
 def _share() -> bool:
-    """``LWAAAI_TEST_SHARE_GPU=1``: rehearse world 2 on a one-GPU box (both ranks on cuda:0, RCCL
-    over its socket transport; ``mgpu_workers._worker``)."""
-    return os.environ.get("LWAAAI_TEST_SHARE_GPU") == "1" and _ngpu() >= 1
+    """World 2 on a one-GPU box (both ranks on cuda:0, RCCL over its socket transport;
+    ``mgpu_workers._worker``): the default when exactly one GPU is visible, so the round's GPU
+    run still puts two real RCCL ranks through the native communicator and captured steps.
+    ``LWAAAI_TEST_SHARE_GPU=0`` skips instead; ``=1`` forces it."""
+    default = "1" if _ngpu() == 1 else "0"
+    return os.environ.get("LWAAAI_TEST_SHARE_GPU", default) == "1" and _ngpu() >= 1
+
+
+if _share():                      # the spawned ranks read it (mgpu_workers._worker)
+    os.environ["LWAAAI_TEST_SHARE_GPU"] = "1"
 
 
 def _worlds():
@@ -40,7 +48,7 @@ def _worlds():
 
 
 need2 = pytest.mark.skipif(_ngpu() < 2 and not _share(),
-                           reason="needs >= 2 GPUs (or LWAAAI_TEST_SHARE_GPU=1)")
+                           reason="needs >= 2 GPUs, or one shared (LWAAAI_TEST_SHARE_GPU=0 set)")
 
 CASES = [("layerwise", "Topk", False, {"K": 0.001}),
          ("layerwise", "Topk", True, {"K": 0.001}),

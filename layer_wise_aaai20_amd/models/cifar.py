@@ -8,6 +8,8 @@ per-layer message list that drives layer-wise compression are 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -151,6 +153,13 @@ def make_layers(cfg, batch_norm: bool = False) -> nn.Sequential:
     return nn.Sequential(*layers)
 
 
+_VGG_FOLD = os.environ.get("LWAAAI_VGG_FOLD", "1") != "0"
+
+
+def _pair_size(s):
+    return (s, s) if isinstance(s, int) else tuple(s)
+
+
 class VGG(nn.Module, _DictLossMixin):
     def __init__(self, features: nn.Module, num_classes: int = 10, init_weights: bool = True):
         super().__init__()
@@ -175,8 +184,20 @@ class VGG(nn.Module, _DictLossMixin):
                     nn.init.zeros_(m.bias)
 
     def forward(self, batch):
-        x = self.avgpool(self.features(batch["input"]))
-        x = self.classifier(torch.flatten(x, 1))
+        x = self.features(batch["input"])
+        fc1 = self.classifier[0]
+        oh, ow = _pair_size(self.avgpool.output_size)
+        if (x.is_cuda and x.shape[-2:] == (1, 1) and hasattr(fc1, "fuse_relu") and
+                fc1.in_features == x.shape[1] * oh * ow and _VGG_FOLD):
+            # 32x32 CIFAR images leave a 1x1 map, which the 7x7 adaptive pool only replicates:
+            # fc1 runs on the folded weight (ops/gemm.py replicated_linear, exactly the same
+            # layer). LWAAAI_VGG_FOLD=0 keeps the pool + full-width GEMMs.
+            from ..ops.gemm import replicated_linear
+            x = replicated_linear(torch.flatten(x, 1), fc1, oh * ow)
+            x = self.classifier[1:](x)
+        else:
+            x = self.avgpool(x)
+            x = self.classifier(torch.flatten(x, 1))
         return self._out(x, batch["target"])
 
 

@@ -166,6 +166,56 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+class _ReplicatedLinearFn(torch.autograd.Function):
+    """``Linear(W)`` applied to an input whose every feature is repeated ``reps`` times, as
+    ``flatten(AdaptiveAvgPool2d((7, 7))(x))`` makes it when ``x`` is 1x1 spatially (CIFAR VGG-16:
+    ``CIFAR10/vgg16.py:10-94``; 512 features repeated 49 times into fc1's 25088 inputs). Exactly
+    the same layer: ``W · rep(x) = (Σ_r W[:, c, r]) · x``, so the forward and data-gradient GEMMs run
+    on the folded ``[O][C]`` weight (49x fewer FLOPs), and the weight gradient — ``dy ⊗ x``, the
+    same for every repeat — is computed once and added to each repeat's slice of the arena."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu, reps):
+        from .block import _bf16_weight
+        O, K = weight.shape
+        C = K // reps
+        wb = _bf16_weight(weight)                                  # [O][C*reps] 16-bit mirror
+        weff = wb.view(O, C, reps).sum(-1, dtype=torch.float32).to(h16()).contiguous()
+        x2 = x.reshape(-1, C).to(h16()).contiguous()
+        b = bias.float() if bias is not None else None
+        y = linear_fwd(x2, weff, b, relu)
+        ctx.save_for_backward(x2, weff, y if relu else None)
+        ctx.weight, ctx.reps, ctx.relu, ctx.has_bias = weight, reps, relu, bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weff, y = ctx.saved_tensors
+        p, reps = ctx.weight, ctx.reps
+        dyf = dy * (y > 0) if ctx.relu else dy
+        db = dyf.float().sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        dy2 = dyf.to(h16()).contiguous()
+        dx = linear_dgrad(dy2, weff) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            g1 = linear_wgrad(dy2, x2)                             # [O][C] fp32
+            O, C = g1.shape
+            g = p.grad if getattr(p, "_lw_grad_ready", None) is not None else None
+            if g is not None and g.dtype == torch.float32 and g.is_contiguous():
+                g.view(O, C, reps).add_(g1.unsqueeze(-1))
+                p._lw_grad_ready(p)
+            else:
+                dw = g1.unsqueeze(-1).expand(O, C, reps).reshape(O, C * reps).to(p.dtype)
+        return dx, dw, db, None, None
+
+
+def replicated_linear(x, lin, reps: int):
+    """``lin(x.repeat_interleave(reps, dim=1))`` for an MFMALinear ``lin`` (see
+    :class:`_ReplicatedLinearFn`); ``x`` is [B, C] with ``C * reps == lin.in_features``."""
+    return _ReplicatedLinearFn.apply(x, lin.weight, lin.bias, bool(getattr(lin, "fuse_relu",
+                                                                           False)), reps)
+
+
 def _gemm_ok(x, weight):
     return x.is_cuda and weight.shape[1] % 8 == 0
 

@@ -349,3 +349,36 @@ def test_gemm_big_tile_mixed_layout(M, N, K, tile):
     c1, _ = G.gemm_ex(A, K, True, Bkn, N, False, M, N, K, out_bf16=False, tile=tile)
     c2, _ = G.gemm_ex(A, K, True, Bkn, N, False, M, N, K, out_bf16=False, tile="128x128x64")
     torch.testing.assert_close(c1, c2, rtol=0, atol=0)
+
+
+def test_vgg_replicated_fc1_matches_pool_and_full_gemm(monkeypatch):
+    """CIFAR VGG-16: the 1x1 feature map through AdaptiveAvgPool2d((7, 7)) is 49 copies of each
+    feature, so fc1 runs on the folded weight (ops/gemm.py replicated_linear). Output, input
+    gradient and fc1's weight / bias gradients match the pool + full-width GEMM path."""
+    import copy
+    from layer_wise_aaai20_amd.models import cifar as CM
+    from layer_wise_aaai20_amd.ops.conv import fuse_convs
+    torch.manual_seed(3)
+    base = CM.vgg16()
+    fuse_convs(base)
+    G.fuse_linears(base)
+    base = base.cuda().to(memory_format=torch.channels_last).eval()       # eval: no dropout
+    x = torch.randn(8, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (8,), device="cuda")
+    res = {}
+    for fold in (True, False):
+        monkeypatch.setattr(CM, "_VGG_FOLD", fold)
+        m = copy.deepcopy(base)
+        xi = x.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = m({"input": xi, "target": t})
+        out["loss"].float().sum().backward()
+        fc1 = m.classifier[0]
+        res[fold] = (out["classifier"].float(), xi.grad.float(), fc1.weight.grad.float(),
+                     fc1.bias.grad.float())
+    for a, b in zip(res[True], res[False]):
+        err = float((a - b).norm() / b.norm().clamp_min(1e-12))
+        assert err < 2e-2, err
+    # the weight gradient is the same for every repeat of a feature
+    g = res[True][2].view(4096, 512, 49)
+    assert torch.equal(g, g[:, :, :1].expand_as(g))

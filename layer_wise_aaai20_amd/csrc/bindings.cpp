@@ -420,6 +420,19 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
 }
 
 // global average pool (nn.hip): x channels_last bf16 [N, C, H, W] -> [N, C] bf16
+// w [..., R] contiguous 16-bit -> [...] = Σ over the last dim (fp32 sum, 16-bit out)
+Tensor sum_repeats(Tensor w, int64_t R) {
+  const c10::DeviceGuard guard(w.device());
+  TORCH_CHECK(w.is_cuda() && w.is_contiguous(), "sum_repeats: contiguous GPU tensor");
+  check_dtype(w, kH16, "w");
+  TORCH_CHECK(R >= 1 && R <= 64 && w.numel() % R == 0, "sum_repeats: 1 <= R <= 64 dividing numel");
+  const int64_t n = w.numel() / R;
+  Tensor out = at::empty({n}, w.options());
+  if (n > 0) lw::sum_repeats(ptr<uint16_t>(w), ptr<uint16_t>(out), n, (int)R, cur_stream());
+  launched("sum_repeats");
+  return out;
+}
+
 Tensor gap_fwd(Tensor x) {
   const c10::DeviceGuard guard(x.device());
   TORCH_CHECK(x.is_cuda(), "x must be a GPU tensor");
@@ -1583,6 +1596,7 @@ LW_LIBRARY(LW_OPS_NS, m) {
   m.def("cifar_augment(Tensor data, Tensor idx, Tensor prm, int offset, int crop, int cutout, "
         "Tensor(a!) out) -> ()");
   m.def("gap_fwd(Tensor x) -> Tensor");
+  m.def("sum_repeats(Tensor w, int R) -> Tensor");
   m.def("relu_bias_bwd(Tensor dy, Tensor? y, Tensor(a!)? db_out) -> (Tensor, Tensor)");
   m.def("xent(Tensor logits, Tensor target, float gscale, int ignore_index, bool want_grad) "
         "-> (Tensor, Tensor, Tensor)");
@@ -1652,6 +1666,7 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("normalize_u8", &normalize_u8);
   m.impl("cifar_augment", &cifar_augment);
   m.impl("gap_fwd", &gap_fwd);
+  m.impl("sum_repeats", &sum_repeats);
   m.impl("relu_bias_bwd", &relu_bias_bwd);
   m.impl("xent", &xent);
   m.impl("gap_bwd", &gap_bwd);

@@ -208,6 +208,31 @@ __global__ __launch_bounds__(256) void k_gap_bwd(const void* __restrict__ dy,
   *reinterpret_cast<uint4*>(dx + t * 8) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// out[i] = Σ_{r<R} w[i*R + r] (16-bit in, fp32 sum in order, 16-bit out): the folded weight of a
+// Linear whose input repeats every feature R times (ops/gemm.py replicated_linear). A block's
+// 256 outputs read one contiguous run of 256*R inputs, staged through LDS by coalesced loads.
+constexpr int kSumRepMax = 64;
+__global__ __launch_bounds__(256) void k_sum_repeats(const uint16_t* __restrict__ w,
+                                                     uint16_t* __restrict__ out, int64_t n, int R) {
+  __shared__ uint16_t s[256 * kSumRepMax];
+  const int64_t o0 = (int64_t)blockIdx.x * 256;
+  const int cnt = (int)min((int64_t)256, n - o0);
+  const uint16_t* src = w + o0 * R;
+  for (int e = threadIdx.x; e < cnt * R; e += 256) s[e] = src[e];
+  __syncthreads();
+  if ((int)threadIdx.x < cnt) {
+    const uint16_t* p = s + threadIdx.x * R;
+    float acc = 0.f;
+    for (int r = 0; r < R; ++r) acc += h2f(p[r]);
+    out[o0 + threadIdx.x] = f2h(acc);
+  }
+}
+
+void sum_repeats(const uint16_t* w, uint16_t* out, int64_t n, int R, hipStream_t st) {
+  hipLaunchKernelGGL(k_sum_repeats, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, out,
+                     n, R);
+}
+
 void gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st) {
   const int thr = N * (C / 8);
   hipLaunchKernelGGL(k_gap_fwd, dim3((thr + 255) / 256), dim3(256), 0, st, x, y, N, HW, C,

@@ -180,7 +180,7 @@ class _ReplicatedLinearFn(torch.autograd.Function):
         O, K = weight.shape
         C = K // reps
         wb = _bf16_weight(weight)                                  # [O][C*reps] 16-bit mirror
-        weff = wb.view(O, C, reps).sum(-1, dtype=torch.float32).to(h16()).contiguous()
+        weff = load().sum_repeats(wb.contiguous(), reps).view(O, C)    # one HBM pass (nn.hip)
         x2 = x.reshape(-1, C).to(h16()).contiguous()
         b = bias.float() if bias is not None else None
         y = linear_fwd(x2, weff, b, relu)

@@ -351,10 +351,47 @@ def test_gemm_big_tile_mixed_layout(M, N, K, tile):
     torch.testing.assert_close(c1, c2, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("n,R", [(1000, 49), (4096 * 512, 49), (77, 1), (300, 64)])
+def test_sum_repeats_matches_torch(n, R):
+    """nn.hip k_sum_repeats (the folded fc1 weight): Σ over the last dim of a 16-bit tensor."""
+    torch.manual_seed(5)
+    w = torch.randn(n, R, device="cuda").bfloat16()
+    got = _lib().sum_repeats(w, R)
+    ref = w.float().sum(-1)
+    assert got.dtype == torch.bfloat16 and got.shape == (n,)
+    torch.testing.assert_close(got.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+def test_replicated_linear_matches_fp32():
+    """ops/gemm.py replicated_linear (the folded fc1 of CIFAR VGG-16) against an fp32 Linear on
+    the explicitly repeated input: output, input / weight / bias gradients."""
+    torch.manual_seed(4)
+    B, C, R, O = 32, 512, 49, 1024
+    lin = G.MFMALinear(C * R, O).cuda()
+    lin.weight.data = lin.weight.data.bfloat16().float()
+    x = torch.randn(B, C, device="cuda").bfloat16().float().requires_grad_()
+    xr = x.detach().clone().requires_grad_()
+    ref = torch.nn.Linear(C * R, O).cuda()
+    ref.load_state_dict(lin.state_dict())
+    y = G.replicated_linear(x, lin, R)
+    yr = ref(xr.unsqueeze(-1).expand(B, C, R).reshape(B, C * R))
+    _close_rel = lambda a, b, tol: float((a.float() - b).norm() / b.norm()) < tol   # noqa: E731
+    assert _close_rel(y, yr, 1e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.to(y.dtype))
+    yr.backward(g)
+    assert _close_rel(x.grad, xr.grad, 1e-2)
+    assert _close_rel(lin.weight.grad, ref.weight.grad, 1e-2)
+    assert _close_rel(lin.bias.grad, ref.bias.grad, 1e-2)
+    # the weight gradient is the same for every repeat of a feature
+    gw = lin.weight.grad.view(O, C, R)
+    assert torch.equal(gw, gw[:, :, :1].expand_as(gw))
+
+
 def test_vgg_replicated_fc1_matches_pool_and_full_gemm(monkeypatch):
-    """CIFAR VGG-16: the 1x1 feature map through AdaptiveAvgPool2d((7, 7)) is 49 copies of each
-    feature, so fc1 runs on the folded weight (ops/gemm.py replicated_linear). Output, input
-    gradient and fc1's weight / bias gradients match the pool + full-width GEMM path."""
+    """CIFAR VGG-16 end to end: with the folded fc1 (1x1 feature map, AdaptiveAvgPool2d((7, 7))
+    replicating it) the loss matches the pool + full-width GEMM path. (Gradients differ by the
+    ReLU-mask flips of near-zero bf16 activations, so they are pinned layer-level above.)"""
     import copy
     from layer_wise_aaai20_amd.models import cifar as CM
     from layer_wise_aaai20_amd.ops.conv import fuse_convs
@@ -365,20 +402,13 @@ def test_vgg_replicated_fc1_matches_pool_and_full_gemm(monkeypatch):
     base = base.cuda().to(memory_format=torch.channels_last).eval()       # eval: no dropout
     x = torch.randn(8, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
     t = torch.randint(0, 10, (8,), device="cuda")
-    res = {}
+    loss = {}
     for fold in (True, False):
         monkeypatch.setattr(CM, "_VGG_FOLD", fold)
         m = copy.deepcopy(base)
-        xi = x.clone().requires_grad_()
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = m({"input": xi, "target": t})
+            out = m({"input": x, "target": t})
+        loss[fold] = float(out["loss"].float().sum())
         out["loss"].float().sum().backward()
-        fc1 = m.classifier[0]
-        res[fold] = (out["classifier"].float(), xi.grad.float(), fc1.weight.grad.float(),
-                     fc1.bias.grad.float())
-    for a, b in zip(res[True], res[False]):
-        err = float((a - b).norm() / b.norm().clamp_min(1e-12))
-        assert err < 2e-2, err
-    # the weight gradient is the same for every repeat of a feature
-    g = res[True][2].view(4096, 512, 49)
-    assert torch.equal(g, g[:, :, :1].expand_as(g))
+        assert m.classifier[0].weight.grad is not None
+    assert abs(loss[True] - loss[False]) < 1e-2 * abs(loss[False]), loss

@@ -414,8 +414,18 @@ __global__ __launch_bounds__(64 * FOLD_LANES) void k_fold_rows(const float* __re
   const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  if (c < C)
-    for (int b = q; b < nb; b += FOLD_LANES) s += partial[(int64_t)b * C + c];
+  if (c < C) {
+    // 8 independent partial sums keep 8 loads in flight per lane (the adds of one chain waited
+    // for each load in turn); combined in a fixed order, so the result stays deterministic
+    float t[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int b = q;
+    for (; b + 7 * FOLD_LANES < nb; b += 8 * FOLD_LANES) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] += partial[(int64_t)(b + u * FOLD_LANES) * C + c];
+    }
+    for (; b < nb; b += FOLD_LANES) t[0] += partial[(int64_t)b * C + c];
+    s = ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+  }
   red[threadIdx.x] = s;
   __syncthreads();
   if (q != 0 || c >= C) return;

@@ -83,7 +83,9 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL on ROCm)")
     ap.add_argument("--share-gpu", action="store_true",
-                    help="debug: every rank on cuda:0 (multi-rank plumbing on a 1-GPU box, gloo)")
+                    help="debug: every rank on cuda:0 (multi-rank rehearsal on a 1-GPU box; with "
+                         "--backend nccl each rank declares its own RCCL host id, so the native "
+                         "communicator, captured collectives and teardown run as on a node)")
     ap.add_argument("--graph", default="on", choices=["on", "off"],
                     help="on: after 3 eager warm-up steps capture the whole step (fwd, bwd, "
                          "overlapped compression + collectives, SGD) as one HIP graph and "
@@ -145,6 +147,10 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if args.share_gpu:
         local = 0
+        if world > 1 and args.backend == "nccl":
+            # RCCL refuses two ranks on one device of one host; distinct host ids make it treat
+            # them as separate nodes (socket transport) — set before anything touches RCCL
+            os.environ["NCCL_HOSTID"] = f"lwaaai-rank{rank}"
     torch.cuda.set_device(local)
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
     dev = torch.device("cuda", local)

@@ -949,13 +949,16 @@ Tensor pack_dgrad_kc(Tensor w, std::vector<int64_t> cls, int64_t sh, int64_t sw,
   const int Co = (int)w.size(0), C = (int)w.size(1), R = (int)w.size(2), S = (int)w.size(3);
   const int nclass = (int)(cls.size() / 4);
   TORCH_CHECK(cls.size() % 4 == 0 && nclass >= 1 && nclass <= 4, "cls: 1..4 classes of 4 ints");
-  TORCH_CHECK(kmax % 8 == 0 && sh >= 1 && sw >= 1, "kmax / strides");
+  // sh / sw = -1 walks the window backwards: the flipped weight of a 3x3/1 data gradient run as
+  // a forward conv (ops/conv.py tap_dgrad_weight: r0 = s0 = 2, stride -1)
+  TORCH_CHECK(kmax % 8 == 0 && (sh >= 1 || sh == -1) && (sw >= 1 || sw == -1), "kmax / strides");
   int r0[4], s0[4], TR[4], TS[4];
   for (int i = 0; i < nclass; ++i) {
     r0[i] = (int)cls[4 * i]; s0[i] = (int)cls[4 * i + 1];
     TR[i] = (int)cls[4 * i + 2]; TS[i] = (int)cls[4 * i + 3];
-    TORCH_CHECK(r0[i] >= 0 && s0[i] >= 0 && TR[i] >= 1 && TS[i] >= 1 &&
-                r0[i] + sh * (TR[i] - 1) < R && s0[i] + sw * (TS[i] - 1) < S &&
+    const int64_t rl = r0[i] + sh * (TR[i] - 1), sl = s0[i] + sw * (TS[i] - 1);
+    TORCH_CHECK(r0[i] >= 0 && s0[i] >= 0 && TR[i] >= 1 && TS[i] >= 1 && r0[i] < R &&
+                s0[i] < S && rl >= 0 && rl < R && sl >= 0 && sl < S &&
                 (int64_t)TR[i] * TS[i] * Co <= kmax, "class taps outside the kernel window");
   }
   Tensor out = at::empty({(int64_t)nclass * C * kmax}, w.options());

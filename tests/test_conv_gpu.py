@@ -471,3 +471,13 @@ def test_conv3_tap_wgrad(shape):
     out = base.clone()
     lib.conv3_tap_wgrad(dy, x, out, True)
     _close(out - base, wf.grad, 2e-3)
+
+
+@pytest.mark.parametrize("co,c", [(64, 64), (128, 128), (512, 512), (64, 32), (256, 128)])
+def test_tap_dgrad_weight_pack_matches_flip(co, c):
+    """tap_dgrad_weight by one pack_dgrad_kc launch walking the 3x3 window backwards equals the
+    flip + transpose it replaces, bit for bit."""
+    w = torch.randn(co, c, 3, 3, device="cuda").bfloat16().contiguous(memory_format=CL)
+    got = CV.tap_dgrad_weight(w)
+    ref = w.flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).contiguous()
+    assert got.shape == ref.shape and torch.equal(got, ref)

@@ -72,12 +72,16 @@ def _conv3_tap_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
     return ((rows + 2) * W + 2) * 64 <= 24 * 1024
 
 
+_TAP_PACK = os.environ.get("LWAAAI_TAP_PACK", "1") != "0"
+
+
 def tap_dgrad_weight(w: torch.Tensor) -> torch.Tensor:
     """The data gradient of a 3x3/1/1 conv as a forward conv of dy: W'[ci][r][s][co] =
     w[co][ci][2-r][2-s], K-contiguous [C][9 Co]."""
     co, c, R, S = w.shape
     wb = w.to(h16())
-    if wb.is_cuda and (R, S) == (3, 3) and co % 8 == 0 and wb.is_contiguous(memory_format=CL):
+    if (_TAP_PACK and wb.is_cuda and (R, S) == (3, 3) and co % 8 == 0 and
+            wb.is_contiguous(memory_format=CL)):
         # one pack kernel walking the window backwards (was flip + two copies, ~15 µs a call)
         return load().pack_dgrad_kc(wb, [2, 2, 3, 3], -1, -1, 9 * co).view(c, 9 * co)
     return wb.flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).contiguous()

@@ -88,6 +88,13 @@ class FlatSGD(Optimizer):
             self._hyper[1].fill_(vals[1])
             self._hyper_host = vals
 
+    def lr_device(self) -> torch.Tensor:
+        """The current LR as a 1-element device tensor (the one a captured step reads; refreshed
+        by load_hyper, which the trainers call before every step)."""
+        if self._hyper is None:
+            self.load_hyper()
+        return self._hyper[:1]
+
     def graph_signature(self) -> tuple:
         """Everything a captured SGD launch bakes in as kernel arguments (lr and grad_scale are
         read from device memory instead): a change means the step must be re-captured."""

@@ -32,7 +32,8 @@ class CompressedDDP(nn.Module):
                  flat_params: bool = True, check_reduction: bool = True, device_ids=None,
                  output_device=None, dim: int = 0, timing: bool = False,
                  bf16_weights: bool = True, world_size: Optional[int] = None,
-                 dense_below: int = 0, momentum_correction: float = 0.0):
+                 dense_below: int = 0, momentum_correction: float = 0.0,
+                 ef_lr_scaled: bool = False):
         super().__init__()
         self.module = module
         import os
@@ -58,7 +59,8 @@ class CompressedDDP(nn.Module):
                                      process_group=process_group, flat_params=flat_params,
                                      timing=timing, world_size=world_size,
                                      dense_below=dense_below,
-                                     momentum_correction=momentum_correction)
+                                     momentum_correction=momentum_correction,
+                                     ef_lr_scaled=ef_lr_scaled)
         self._buffers_list = self._flatten_buffers(module) if broadcast_buffers else []
         self._hooks = []
         self._register_hooks()

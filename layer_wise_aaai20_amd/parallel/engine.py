@@ -67,7 +67,7 @@ class GradSyncEngine:
                  seed: int = 2147483647, process_group=None, flat_params: bool = False,
                  world_size: Optional[int] = None, timing: bool = False,
                  overlap_compress: bool = True, dense_below: int = 0,
-                 momentum_correction: float = 0.0):
+                 momentum_correction: float = 0.0, ef_lr_scaled: bool = False):
         self.mode = canonical_mode(mode)
         self.method = ref.canonical_method(method) if self.mode != "none" else "none"
         self.pg = process_group
@@ -110,6 +110,19 @@ class GradSyncEngine:
             if self.ef is None:
                 raise ValueError("momentum correction needs error_feedback=True")
             self.mom = torch.zeros_like(self.arena.grad)
+        # LR-scaled residuals (opt-in, EF-SGD's "residual in update units"): the residual left at
+        # step t-1 was meant to be applied at lr_{t-1}; before step t adds it to the new gradient
+        # it is rescaled by lr_{t-1} / lr_t, so a warm-up / decay schedule neither amplifies nor
+        # damps the deferred updates. The LR comes from ``lr_source`` (a callable returning the
+        # optimizer's 1-element device LR, FlatSGD.lr_device) and the ratio is computed on the
+        # device in begin_step, so it stays inside a captured step.
+        self.lr_scaled = bool(ef_lr_scaled)
+        self.lr_source = None
+        if self.lr_scaled:
+            if self.ef is None:
+                raise ValueError("LR-scaled residuals need error_feedback=True")
+            self._lr_prev = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._lr_ratio = torch.ones(1, dtype=torch.float32, device=self.device)
         # what a peer needs to build this engine's codecs for another rank (loopback tests)
         self.codec_kw = dict(K=K, V=V, qstates=qstates, seed=self.seed,
                              error_feedback=self.ef is not None, wire=wire,
@@ -235,6 +248,13 @@ class GradSyncEngine:
         self.arena.zero_()
         if not self.arena.grads_attached():
             self.arena.attach_grads()
+        if self.lr_scaled:
+            if self.lr_source is None:
+                raise RuntimeError("ef_lr_scaled: set engine.lr_source to the optimizer's LR")
+            cur = self.lr_source()
+            ok = (self._lr_prev > 0) & (cur > 0)
+            self._lr_ratio.copy_(torch.where(ok, self._lr_prev / torch.where(ok, cur, 1.0), 1.0))
+            self._lr_prev.copy_(cur)
         self._reset_state()
 
     def mark_ready(self, seg_index: int) -> None:
@@ -289,6 +309,8 @@ class GradSyncEngine:
             side.wait_event(ready)
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             t0 = self._event() if self.timing else None
+            if self.lr_scaled:
+                e.mul_(self._lr_ratio)                   # residual re-expressed at this step's LR
             u = None
             if self.mom is not None:
                 u = self.mom[b.start:b.end]

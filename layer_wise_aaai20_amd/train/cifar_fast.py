@@ -30,7 +30,7 @@ class CifarTrainer:
                  momentum=0.9, dtype=torch.bfloat16, bucket_cap_mb=25.0, wire="auto",
                  n_train=50000, seed=0, fused=True, graph=None, n_test=1000,
                  task="textures", amp=None, dense_below=0, momentum_correction=False,
-                 lr_scale=1.0):
+                 lr_scale=1.0, ef_lr_scaled=False):
         self.device = torch.device(device or "cuda")
         self.dtype = dtype
         self.bs = batch_size
@@ -51,10 +51,13 @@ class CifarTrainer:
         self.ddp = CompressedDDP(net, compress=compress, method=method, K=K, V=V,
                                  qstates=qstates, error_feedback=error_feedback,
                                  bucket_cap_mb=bucket_cap_mb, wire=wire, flat_params=True,
-                                 dense_below=dense_below, momentum_correction=mc)
+                                 dense_below=dense_below, momentum_correction=mc,
+                                 ef_lr_scaled=ef_lr_scaled)
         om = 0.0 if mc > 0 else momentum
         self.opt = FlatSGD(net.parameters(), self.ddp.arena, lr=0.0, momentum=om,
                            nesterov=om > 0, weight_decay=5e-4 * batch_size)
+        if ef_lr_scaled:
+            self.ddp.engine.lr_source = self.opt.lr_device
         ds = D.synthetic_cifar10(n_train, n_test, seed, task=task, amp=amp)
         x = D.transpose(D.normalise(D.pad(ds["train"]["data"], 4)))
         tx = D.transpose(D.normalise(ds["test"]["data"]))
@@ -104,6 +107,8 @@ class CifarTrainer:
         lr = self.sched(self.step_count / self.steps_per_epoch) / self.bs
         for g in self.opt.param_groups:
             g["lr"] = lr
+        if self.ddp.engine.lr_scaled:
+            self.opt.load_hyper()             # the residual rescale reads this step's LR
         out, loss = self.graphed(batch["input"], batch["target"])
         self.step_count += 1
         self.last = out

@@ -50,6 +50,12 @@ RUNS = [
     # 19-20: the dense exemption alone at K = 0.1 %, and entire-model Top-K 1 % + EF
     ("topk0.1+ef+dense4k", "Topk", "layerwise", {"K": 0.001}, True, {"dense_below": 4096}),
     ("entire topk1+ef", "Topk", "entiremodel", {"K": 0.01}, True, {}),
+    # 21-24: LR-scaled residuals (EF-SGD's residual in update units: rescaled by lr_{t-1}/lr_t)
+    ("topk1+ef+lrscaled", "Topk", "layerwise", {"K": 0.01}, True, {"ef_lr_scaled": True}),
+    ("topk1+ef+lrscaled+dense4k", "Topk", "layerwise", {"K": 0.01}, True,
+     {"ef_lr_scaled": True, "dense_below": 4096}),
+    ("randk10+ef+lrscaled", "Randomk", "layerwise", {"K": 0.1}, True, {"ef_lr_scaled": True}),
+    ("randk1+ef+lrscaled", "Randomk", "layerwise", {"K": 0.01}, True, {"ef_lr_scaled": True}),
 ]
 
 

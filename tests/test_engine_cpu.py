@@ -255,3 +255,31 @@ def test_momentum_correction_accumulates_velocity_and_masks():
     with pytest.raises(ValueError):
         GradSyncEngine(list(net.named_parameters()), mode="layerwise", method="Topk", K=0.05,
                        error_feedback=False, momentum_correction=0.9)
+
+
+def test_lr_scaled_residual_rescales_by_lr_ratio():
+    """ef_lr_scaled: before step t compresses, the residual left at step t-1 is multiplied by
+    lr_{t-1} / lr_t (1 on the first step and whenever either LR is 0), so sent + e_new equals
+    e_old * ratio + g."""
+    torch.manual_seed(0)
+    net = small_net()
+    eng = GradSyncEngine(list(net.named_parameters()), mode="layerwise", method="Topk", K=0.05,
+                         error_feedback=True, ef_lr_scaled=True)
+    lrs = [0.1, 0.2, 0.2, 0.05, 0.0, 0.3]
+    ratios = [1.0, 0.5, 1.0, 4.0, 1.0, 1.0]
+    box = {}
+    eng.lr_source = lambda: box["lr"]
+    for lr, r in zip(lrs, ratios):
+        box["lr"] = torch.tensor([lr])
+        eng.begin_step()
+        assert abs(float(eng._lr_ratio) - r) < 1e-6, (lr, float(eng._lr_ratio))
+        g = torch.zeros(eng.arena.numel)
+        for s in eng.arena.segments:
+            g[s.offset:s.offset + s.numel] = torch.randn(s.numel)
+        e_old = eng.ef.clone()
+        eng.arena.grad.copy_(g)
+        eng.sync_now()
+        torch.testing.assert_close(eng.arena.grad + eng.ef, e_old * r + g, rtol=1e-5, atol=1e-6)
+    with pytest.raises(ValueError):
+        GradSyncEngine(list(net.named_parameters()), mode="layerwise", method="Topk", K=0.05,
+                       error_feedback=False, ef_lr_scaled=True)

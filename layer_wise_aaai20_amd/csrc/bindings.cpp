@@ -968,6 +968,36 @@ Tensor pack_dgrad_kc(Tensor w, std::vector<int64_t> cls, int64_t sh, int64_t sw,
   return out;
 }
 
+// [K][C] per-class slabs Wt_c[jr][js][co][ci] = w[co, ci, r0 + sh*jr, s0 + sw*js], concatenated
+// (ops/conv.py pack_dgrad_weight): w channels_last bf16/fp16 [Co][C][R][S], C % 8 == 0
+Tensor pack_dgrad_nkc(Tensor w, std::vector<int64_t> cls, int64_t sh, int64_t sw) {
+  const c10::DeviceGuard guard(w.device());
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "pack_dgrad_nkc: a channels_last 4-d GPU weight");
+  check_dtype(w, kH16, "weight");
+  check_aligned16(w.data_ptr(), "weight");
+  const int Co = (int)w.size(0), C = (int)w.size(1), R = (int)w.size(2), S = (int)w.size(3);
+  TORCH_CHECK(C % 8 == 0, "pack_dgrad_nkc: C % 8 == 0");
+  const int nclass = (int)(cls.size() / 4);
+  TORCH_CHECK(cls.size() % 4 == 0 && nclass >= 1 && nclass <= 4 && sh >= 1 && sw >= 1,
+              "cls: 1..4 classes of 4 ints; positive strides");
+  int r0[4], s0[4], TR[4], TS[4];
+  int64_t total = 0;
+  for (int i = 0; i < nclass; ++i) {
+    r0[i] = (int)cls[4 * i]; s0[i] = (int)cls[4 * i + 1];
+    TR[i] = (int)cls[4 * i + 2]; TS[i] = (int)cls[4 * i + 3];
+    TORCH_CHECK(r0[i] >= 0 && s0[i] >= 0 && TR[i] >= 1 && TS[i] >= 1 &&
+                r0[i] + sh * (TR[i] - 1) < R && s0[i] + sw * (TS[i] - 1) < S,
+                "class taps outside the kernel window");
+    total += (int64_t)TR[i] * TS[i] * Co * C;
+  }
+  Tensor out = at::empty({total}, w.options());
+  lw::pack_dgrad_nkc(ptr<uint16_t>(w), ptr<uint16_t>(out), Co, C, R, S, (int)sh, (int)sw, nclass,
+                     r0, s0, TR, TS, cur_stream());
+  launched("pack_dgrad_nkc");
+  return out;
+}
+
 std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vector<int64_t> geom,
                                    int64_t N, int64_t tile, int64_t splits, bool out_bf16,
                                    c10::optional<Tensor> pro_scale, c10::optional<Tensor> pro_shift,
@@ -1600,6 +1630,7 @@ LW_LIBRARY(LW_OPS_NS, m) {
         "Tensor(a!) out) -> ()");
   m.def("gap_fwd(Tensor x) -> Tensor");
   m.def("sum_repeats(Tensor w, int R) -> Tensor");
+  m.def("pack_dgrad_nkc(Tensor w, int[] cls, int sh, int sw) -> Tensor");
   m.def("relu_bias_bwd(Tensor dy, Tensor? y, Tensor(a!)? db_out) -> (Tensor, Tensor)");
   m.def("xent(Tensor logits, Tensor target, float gscale, int ignore_index, bool want_grad) "
         "-> (Tensor, Tensor, Tensor)");
@@ -1670,6 +1701,7 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("cifar_augment", &cifar_augment);
   m.impl("gap_fwd", &gap_fwd);
   m.impl("sum_repeats", &sum_repeats);
+  m.impl("pack_dgrad_nkc", &pack_dgrad_nkc);
   m.impl("relu_bias_bwd", &relu_bias_bwd);
   m.impl("xent", &xent);
   m.impl("gap_bwd", &gap_bwd);

@@ -69,6 +69,51 @@ __global__ __launch_bounds__(256) void k_pack_dgrad_kc(const uint16_t* __restric
   }
 }
 
+// The [K][C] form (the data-gradient GEMM's B operand read with the transposing LDS loads): class
+// i's slab Wt_i[jr][js][co][ci] = w[co][r0 + sh*jr][s0 + sw*js][ci], slabs back to back. Each
+// thread moves 8 consecutive ci (one 16-byte load and store; C % 8 == 0). Replaces a permute +
+// per-class slice copies + concatenation (up to 5 ATen kernels per stride-2 layer).
+__global__ __launch_bounds__(256) void k_pack_dgrad_nkc(const uint16_t* __restrict__ w,
+                                                        uint16_t* __restrict__ out, int Co, int C,
+                                                        int R, int S, int sh, int sw, int nclass,
+                                                        PackClasses pc) {
+  const int C8 = C / 8;
+  int64_t base = 0;
+  for (int i = 0; i < nclass; ++i) {
+    const int r0 = pc.r0[i], s0 = pc.s0[i], TR = pc.TR[i], TS = pc.TS[i];
+    const int64_t n = (int64_t)TR * TS * Co * C8;      // 16-byte chunks of this class
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n;
+         t += (int64_t)gridDim.x * 256) {
+      const int cg = (int)(t % C8);
+      const int64_t row = t / C8;                        // (jr, js, co)
+      const int o = (int)(row % Co);
+      const int tap = (int)(row / Co);
+      const int jr = tap / TS, js = tap - jr * TS;
+      const int r = r0 + sh * jr, sx = s0 + sw * js;
+      const uint4 v = *reinterpret_cast<const uint4*>(w + (((int64_t)o * R + r) * S + sx) * C +
+                                                      cg * 8);
+      *reinterpret_cast<uint4*>(out + base + row * C + cg * 8) = v;
+    }
+    base += (int64_t)TR * TS * Co * C;
+  }
+}
+
+void pack_dgrad_nkc(const uint16_t* w, uint16_t* out, int Co, int C, int R, int S, int sh, int sw,
+                    int nclass, const int* r0, const int* s0, const int* TR, const int* TS,
+                    hipStream_t st) {
+  PackClasses pc{};
+  int64_t most = 1;
+  for (int i = 0; i < nclass; ++i) {
+    pc.r0[i] = r0[i]; pc.s0[i] = s0[i]; pc.TR[i] = TR[i]; pc.TS[i] = TS[i];
+    const int64_t n = (int64_t)TR[i] * TS[i] * Co * (C / 8);
+    most = n > most ? n : most;
+  }
+  int64_t blocks = (most + 255) / 256;
+  blocks = blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(k_pack_dgrad_nkc, dim3((unsigned)blocks), dim3(256), 0, st, w, out, Co, C, R,
+                     S, sh, sw, nclass, pc);
+}
+
 void pack_dgrad_kc(const uint16_t* w, uint16_t* out, int Co, int C, int R, int S, int sh, int sw,
                    int nclass, const int* r0, const int* s0, const int* TR, const int* TS,
                    int kmax, hipStream_t st) {

@@ -242,6 +242,10 @@ int gemm_pick_tile(const GemmArgs& g);
 int gemm_tiles_m(const GemmArgs& g);
 int gemm_splits_used(const GemmArgs& g);
 bool gemm_stream_ok(const GemmArgs& g);
+// [class][jr][js][Co][C] slabs of a channels_last weight (conv.hip k_pack_dgrad_nkc), C % 8 == 0
+void pack_dgrad_nkc(const uint16_t* w, uint16_t* out, int Co, int C, int R, int S, int sh, int sw,
+                    int nclass, const int* r0, const int* s0, const int* TR, const int* TS,
+                    hipStream_t st);
 void pack_dgrad_kc(const uint16_t* w, uint16_t* out, int Co, int C, int R, int S, int sh, int sw,
                    int nclass, const int* r0, const int* s0, const int* TR, const int* TS,
                    int kmax, hipStream_t st);

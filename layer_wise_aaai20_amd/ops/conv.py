@@ -73,6 +73,7 @@ def _conv3_tap_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
 
 
 _TAP_PACK = os.environ.get("LWAAAI_TAP_PACK", "1") != "0"
+_NKC_PACK = os.environ.get("LWAAAI_NKC_PACK", "1") != "0"
 
 
 def tap_dgrad_weight(w: torch.Tensor) -> torch.Tensor:
@@ -167,9 +168,20 @@ def _dgrad_classes(H, W, R, S, sh, sw, ph, pw):
 
 
 def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int) -> Tuple[torch.Tensor, List[int]]:
-    """Per-class slabs Wt_c[jr][js][co][ci] = w[co, ci, r0 + sh*jr, s0 + sw*js], concatenated."""
+    """Per-class slabs Wt_c[jr][js][co][ci] = w[co, ci, r0 + sh*jr, s0 + sw*js], concatenated:
+    one pack launch (``csrc/conv.hip k_pack_dgrad_nkc``) for a channels_last GPU weight, else the
+    permute / slice / cat form (the reference implementation of the same layout)."""
     co, c, R, S = w.shape
-    wt = w.to(h16()).permute(2, 3, 0, 1)                      # [R, S, Co, C]
+    wb = w.to(h16())
+    if (_NKC_PACK and wb.is_cuda and c % 8 == 0 and wb.is_contiguous(memory_format=CL) and
+            wb.data_ptr() % 16 == 0):
+        cls, offs, off = [], [], 0
+        for (_ch, _cw, r0, s0, TR, TS, *_r) in classes:
+            cls += [r0, s0, TR, TS]
+            offs.append(off)
+            off += TR * TS * co * c
+        return load().pack_dgrad_nkc(wb, cls, sh, sw), offs
+    wt = wb.permute(2, 3, 0, 1)                               # [R, S, Co, C]
     if len(classes) == 1 and classes[0][4] == R and classes[0][5] == S:
         return wt.contiguous().view(-1), [0]
     parts, offs, off = [], [], 0

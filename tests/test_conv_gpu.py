@@ -481,3 +481,17 @@ def test_tap_dgrad_weight_pack_matches_flip(co, c):
     got = CV.tap_dgrad_weight(w)
     ref = w.flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).contiguous()
     assert got.shape == ref.shape and torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("shape", [(64, 64, 3, 1, 1), (128, 128, 3, 2, 1), (512, 256, 3, 2, 1),
+                                   (256, 64, 1, 1, 0), (64, 32, 1, 2, 0), (48, 24, 3, 2, 0)])
+def test_pack_dgrad_nkc_matches_slices(shape, monkeypatch):
+    """pack_dgrad_weight's one-launch [K][C] pack equals the permute / slice / cat form."""
+    co, c, k, s, p = shape
+    w = torch.randn(co, c, k, k, device="cuda").bfloat16().contiguous(memory_format=CL)
+    H = 14
+    classes = CV._dgrad_classes(H, H, k, k, s, s, p, p)
+    got, go = CV.pack_dgrad_weight(w, classes, s, s)
+    monkeypatch.setattr(CV, "_NKC_PACK", False)
+    ref, ro = CV.pack_dgrad_weight(w, classes, s, s)
+    assert go == ro and torch.equal(got, ref)

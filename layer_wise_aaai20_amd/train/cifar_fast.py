@@ -44,6 +44,8 @@ class CifarTrainer:
         net = net.to(self.device)
         if self.device.type == "cuda":
             net = net.to(memory_format=torch.channels_last)
+            if fused:
+                lwnn.share_bn_counters(net)   # one counter-bump kernel per step, not one per BN
         self.model = net
         # momentum_correction (DGC, opt-in): the velocity lives in the compressor's residual and
         # the optimizer runs without momentum (parallel/engine.py)

@@ -134,7 +134,7 @@ def _reference_points(steps: int) -> str:
         return ""
     parts = [f"{k}: {v['mean']:.1f}% (seeds {', '.join(f'{x:.1f}' for x in v['top1'])})"
              for k, v in ref.get("methods", {}).items()]
-    return ("; reference points at this budget, " + "; ".join(parts) +
+    return ("; reference points at this budget (bf16, 3 seeds), " + "; ".join(parts) +
             " (layer_wise_aaai20_amd/train/accuracy_reference.json)")
 
 

@@ -86,6 +86,14 @@ def parse():
                     help="debug: every rank on cuda:0 (multi-rank rehearsal on a 1-GPU box; with "
                          "--backend nccl each rank declares its own RCCL host id, so the native "
                          "communicator, captured collectives and teardown run as on a node)")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="time a world of W ranks on this one GPU (train/simworld.py: codecs, "
+                         "decode and captured side-stream branch for W ranks, loopback "
+                         "communicator with replayed peer payloads) and print one JSON line per "
+                         "configuration instead of the benchmark line")
+    ap.add_argument("--sim-all", action="store_true",
+                    help="with --simulate-world: the ResNet-50 BASELINE configs (layer-wise "
+                         "Top-K 0.1 %%, entire-model QSGD 8-bit) instead of the given method")
     ap.add_argument("--graph", default="on", choices=["on", "off"],
                     help="on: after 3 eager warm-up steps capture the whole step (fwd, bwd, "
                          "overlapped compression + collectives, SGD) as one HIP graph and "
@@ -138,8 +146,36 @@ def _reference_points(steps: int) -> str:
             " (layer_wise_aaai20_amd/train/accuracy_reference.json)")
 
 
+def simulate(args) -> None:
+    """--simulate-world W (train/simworld.py): JSON lines, no benchmark line."""
+    from layer_wise_aaai20_amd.train.simworld import simulate_imagenet
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    if args.sim_all:
+        cfgs = [dict(compress="layerwise", method="Topk", K=0.001),
+                dict(compress="entiremodel", method="RandomDithering", qstates=255)]
+    else:
+        cfgs = [dict(compress=args.compress, method=args.method, K=args.ratio,
+                     qstates=args.qstates, error_feedback=args.ef,
+                     dense_below=args.ef_dense_below,
+                     momentum_correction=args.momentum_correction)]
+    for c in cfgs:
+        line = simulate_imagenet(args.simulate_world, dev, steps=args.steps,
+                                 warmup=max(3, args.warmup), model=args.model,
+                                 batch=args.batch, image_size=args.image_size, dtype=args.dtype,
+                                 bucket_mb=args.bucket_mb, **c)
+        line["data"] = "synthetic (random uint8 images, random-init weights)"
+        print(json.dumps(line), flush=True)
+        if args.json_out:
+            with open(args.json_out, "a") as f:
+                f.write(json.dumps(line) + "\n")
+
+
 def main():
     args = parse()
+    if args.simulate_world > 1:
+        simulate(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -80,7 +80,19 @@ def main():
                     help="on: capture the whole step as one HIP graph after the eager warm-up "
                          "steps; auto: also time graph vs eager in the warm-up and keep the "
                          "faster (train/graphs.py)")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="time a world of W ranks on this one GPU (train/simworld.py) and print "
+                         "one JSON line per configuration (exposed compression / exchange tail)")
     args = ap.parse_args()
+    if args.simulate_world > 1:
+        from layer_wise_aaai20_amd.train.simworld import simulate_cifar
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        names = [n for n in CONFIGS if n != "anchor"] if args.config == "all" else [args.config]
+        for n in names:
+            print(json.dumps(simulate_cifar(args.simulate_world, dev, n, CONFIGS[n], args.steps,
+                                            args.warmup)), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

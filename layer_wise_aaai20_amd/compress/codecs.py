@@ -69,6 +69,10 @@ class Codec:
     # carry (Top-K ties beyond the slack, threshold hits beyond a fixed sparse capacity); they
     # stay in the error-feedback residual (GradSyncEngine.read_overflow)
     overflow = None
+    # momentum correction (GradSyncEngine): the bucket's velocity while compress() runs; a codec
+    # with mc_fused zeroes it at the coordinates it selected (segments not sent whole only)
+    mc_mom = None
+    mc_fused = False
 
     def __init__(self, plan: SegPlan, world: int, rank: int, seed: int = 0,
                  error_feedback: bool = False):
@@ -121,6 +125,7 @@ class TopkCodec(Codec):
 
     # exact Top-K ignores the step; Random-K reads it from the device counter (step_t)
     graph_safe = True
+    mc_fused = True
 
     def __init__(self, plan, world, rank, K: float, seed=0, error_feedback=False,
                  dense_below: int = 0):
@@ -173,7 +178,7 @@ class TopkCodec(Codec):
                                 t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
                                 self._workspace(grad.device, lib), self.km, OUT_PAIRS, out, None,
                                 None, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
-                                self.step_t, self.overflow)
+                                self.step_t, self.overflow, self.mc_mom)
             return out
         self._compress_cpu(grad, ef, step, out)
         return out
@@ -202,8 +207,8 @@ class TopkCodec(Codec):
         pairs[:, 0] = SENT
         pairs[:, 1] = 0
         for s, x in self._segs(grad):
+            o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
             if ef is not None:
-                o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
                 x.add_(ef[o:o + n])
             idx = self._select_cpu(s, x, step)
             c0 = int(self.cap_off[s])
@@ -214,6 +219,8 @@ class TopkCodec(Codec):
                 e = ef[o:o + n]
                 e.copy_(x)
                 e[idx] = 0
+            if self.mc_mom is not None and k < n:    # (the kernels' momentum factor masking)
+                self.mc_mom[o:o + n][idx] = 0
 
     def decompress(self, send, recv, grad, world=None):
         world = world or self.world
@@ -300,7 +307,7 @@ class RandkCodec(RandkSparseCodec):
                                 t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
                                 self._workspace(grad.device, lib), KM_RANDK, OUT_VALIDX, None,
                                 vals, idx, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
-                                self.step_t)
+                                self.step_t, None, self.mc_mom)
             return vals
         for s, x in self._segs(grad):
             o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
@@ -313,6 +320,8 @@ class RandkCodec(RandkSparseCodec):
                 e = ef[o:o + n]
                 e.copy_(xe)
                 e[sel] = 0
+            if self.mc_mom is not None and sel.numel() < n:
+                self.mc_mom[o:o + n][sel] = 0
         return vals
 
     def decompress(self, send, recv, grad, world=None):
@@ -348,6 +357,7 @@ class ThresholdCodec(TopkCodec):
     """
     name = "threshold"
     km = KM_THRESH
+    mc_fused = False               # (the engine masks the velocity where the residual is 0)
 
     def __init__(self, plan, world, rank, V=None, adaptive=False, seed=0, error_feedback=False,
                  count_exchange=None, max_density=None):

@@ -166,10 +166,17 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
                      Tensor tasks, Tensor task_lo, Tensor ws, int64_t km, int64_t out,
                      c10::optional<Tensor> pairs, c10::optional<Tensor> vals,
                      c10::optional<Tensor> idx, int64_t gid_base, int64_t step, int64_t seed,
-                     c10::optional<Tensor> step_t, c10::optional<Tensor> overflow) {
+                     c10::optional<Tensor> step_t, c10::optional<Tensor> overflow,
+                     c10::optional<Tensor> mom) {
   const c10::DeviceGuard guard(g.device());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, keep, cap_off, small_segs, large_segs,
                                       tasks, task_lo, ws);
+  if (mom.has_value() && mom->defined()) {
+    check_cuda(*mom, "mom");
+    check_dtype(*mom, at::kFloat, "mom");
+    TORCH_CHECK(mom->numel() >= g.numel() && mom->is_contiguous(), "mom: g's layout");
+    a.mom = ptr<float>(*mom);
+  }
   a.pairs = optr<int2>(pairs);
   a.vals = optr<float>(vals);
   a.idx_out = optr<int32_t>(idx);
@@ -318,6 +325,52 @@ void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor
   TORCH_CHECK(wpr % 4 == 0, "payload words per rank must be a multiple of 4");
   lw::dequantize(a, (int)q, ptr<uint32_t>(gathered), wpr, (int)world, cur_stream());
   launched("dequantize");
+}
+
+// momentum correction prologue / masking (optim.hip k_mc_prep, k_mc_mask)
+void mc_prep(Tensor g, Tensor u, c10::optional<Tensor> p, Tensor seg_off, Tensor seg_n,
+             Tensor segs, Tensor tasks, c10::optional<Tensor> seg_wd, double mc, double wmul) {
+  const c10::DeviceGuard guard(g.device());
+  check_cuda(g, "g");
+  check_cuda(u, "u");
+  check_dtype(g, at::kFloat, "g");
+  check_dtype(u, at::kFloat, "u");
+  TORCH_CHECK(g.is_contiguous() && u.is_contiguous() && u.numel() == g.numel(),
+              "mc_prep: g and u must be contiguous and of one size");
+  check_aligned16(g.data_ptr(), "g");
+  check_aligned16(u.data_ptr(), "u");
+  const float* pp = nullptr;
+  const float* wd = nullptr;
+  if (p.has_value() && p->defined() && seg_wd.has_value() && seg_wd->defined()) {
+    check_cuda(*p, "p");
+    check_dtype(*p, at::kFloat, "p");
+    TORCH_CHECK(p->is_contiguous() && p->numel() == g.numel(), "mc_prep: p must have g's layout");
+    check_aligned16(p->data_ptr(), "p");
+    check_dtype(*seg_wd, at::kFloat, "seg_wd");
+    pp = ptr<float>(*p);
+    wd = ptr<float>(*seg_wd);
+  }
+  check_dtype(seg_off, at::kLong, "seg_off");
+  check_dtype(seg_n, at::kInt, "seg_n");
+  check_dtype(tasks, at::kInt, "tasks");
+  lw::mc_prep(ptr<float>(g), ptr<float>(u), pp, ptr<int64_t>(seg_off), ptr<int32_t>(seg_n),
+              ptr<int32_t>(segs), ptr<int2>(tasks), (int)(tasks.numel() / 2), wd, (float)mc,
+              (float)wmul, cur_stream());
+  launched("mc_prep");
+}
+
+void mc_mask(Tensor u, Tensor e) {
+  const c10::DeviceGuard guard(u.device());
+  check_cuda(u, "u");
+  check_cuda(e, "e");
+  check_dtype(u, at::kFloat, "u");
+  check_dtype(e, at::kFloat, "e");
+  TORCH_CHECK(u.is_contiguous() && e.is_contiguous() && u.numel() == e.numel(),
+              "mc_mask: u and e must be contiguous and of one size");
+  check_aligned16(u.data_ptr(), "u");
+  check_aligned16(e.data_ptr(), "e");
+  lw::mc_mask(ptr<float>(u), ptr<float>(e), u.numel(), cur_stream());
+  launched("mc_mask");
 }
 
 void sgd_step(Tensor p, Tensor g, Tensor buf, Tensor seg_off, Tensor seg_n, Tensor segs,
@@ -820,7 +873,8 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
   TORCH_CHECK(b_kcontig || N % 8 == 0, "N must be a multiple of 8 for an N-contiguous B");
   TORCH_CHECK(A.numel() >= (a_kcontig ? (M - 1) * lda + K : (K - 1) * lda + M), "A too small");
   TORCH_CHECK(B.numel() >= (b_kcontig ? (N - 1) * ldb + K : (K - 1) * ldb + N), "B too small");
-  TORCH_CHECK((tile >= 0 && tile <= 6) || (tile >= 11 && tile <= 13) || (tile >= 21 && tile <= 24),
+  TORCH_CHECK((tile >= 0 && tile <= 6) || (tile >= 11 && tile <= 13) || (tile >= 21 && tile <= 24) ||
+                  lw::gemm_is_mf32((int)tile),
               "tile id");
   if (ldc <= 0) ldc = N;
   TORCH_CHECK(ldc >= N, "ldc must be >= N");
@@ -907,7 +961,7 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
   }
   set_bstats(g, bst_x, bst_mean, bst_scale_shift, bst_bits, M, N, ldc, out_bf16);
   if (g.bst_x) {
-    TORCH_CHECK(want_stats && a_kcontig && !b_kcontig && !pro && tile < 11,
+    TORCH_CHECK(want_stats && a_kcontig && !b_kcontig && !pro && (tile < 11 || lw::gemm_is_mf32((int)tile)),
                 "backward statistics: a tiled data-gradient GEMM (K-contiguous A, N-contiguous "
                 "B, no prologue) with want_stats");
   }
@@ -1595,7 +1649,8 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "select_compress(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor keep, "
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
       "Tensor(c!) ws, int km, int out, Tensor(d!)? pairs, Tensor(e!)? vals, Tensor(f!)? idx, "
-      "int gid_base, int step, int seed, Tensor? step_t=None, Tensor(g!)? overflow=None) -> ()");
+      "int gid_base, int step, int seed, Tensor? step_t=None, Tensor(g!)? overflow=None, "
+      "Tensor(h!)? mom=None) -> ()");
   m.def(
       "thresh_count(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor large_segs, "
       "Tensor tasks, Tensor task_lo, Tensor(c!) ws, float V, int adaptive, Tensor(d!) counts_out) "
@@ -1620,6 +1675,10 @@ LW_LIBRARY(LW_OPS_NS, m) {
   m.def(
       "dequantize(Tensor gathered, int world, Tensor(a!) g, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor task_lo, Tensor rec_off, int q, int qstates) -> ()");
+  m.def(
+      "mc_prep(Tensor(a!) g, Tensor(b!) u, Tensor? p, Tensor seg_off, Tensor seg_n, Tensor segs, "
+      "Tensor tasks, Tensor? seg_wd, float mc, float wmul) -> ()");
+  m.def("mc_mask(Tensor(a!) u, Tensor e) -> ()");
   m.def(
       "sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
@@ -1697,6 +1756,8 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("quantize", &quantize);
   m.impl("dequantize", &dequantize);
   m.impl("sgd_step", &sgd_step);
+  m.impl("mc_prep", &mc_prep);
+  m.impl("mc_mask", &mc_mask);
   m.impl("normalize_u8", &normalize_u8);
   m.impl("cifar_augment", &cifar_augment);
   m.impl("gap_fwd", &gap_fwd);

@@ -62,8 +62,15 @@ def _digest(paths, flags=()) -> str:
     return h.hexdigest()[:16]
 
 
-def _compile(src, inc, abi, bdir=BUILD, flags=()):
+def _compile(src, inc, abi, bdir=BUILD, flags=(), dig=""):
+    """One object; skipped when ``obj.stamp`` holds the digest of (this source, every header,
+    the flags) — an edit to one kernel file recompiles that file only."""
     obj = os.path.join(bdir, os.path.basename(src) + ".o")
+    ostamp = obj + ".stamp"
+    if dig and os.path.exists(obj) and os.path.exists(ostamp):
+        with open(ostamp) as f:
+            if f.read().strip() == dig:
+                return obj
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM", "-D__HIP_PLATFORM_AMD__=1",
            "-Wno-unused-result", "-Wno-deprecated-declarations", f"-I{HERE}"] + EXTRA + list(flags)
@@ -72,6 +79,9 @@ def _compile(src, inc, abi, bdir=BUILD, flags=()):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if dig:
+        with open(ostamp, "w") as f:
+            f.write(dig)
     return obj
 
 
@@ -98,8 +108,10 @@ def _build_one(out, bdir, flags, srcs, force, jobs, verbose):
     if verbose:
         print(f"[lwaaai] compiling {len(srcs)} sources for {ARCH} ({' '.join(flags) or 'bf16'}) "
               f"with {jobs} jobs")
+    odig = {s: ("" if force else _digest([s] + headers + [os.path.abspath(__file__)], flags))
+            for s in srcs}
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, inc, abi, bdir, flags), srcs))
+        objs = list(ex.map(lambda s: _compile(s, inc, abi, bdir, flags, odig[s]), srcs))
     tmp = out + ".tmp"
     cmd = ["g++", "-shared", "-o", tmp] + objs + [
         f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(NT) void k_small_select(
     const int64_t* __restrict__ cap_off, const int32_t* __restrict__ small_segs,
     int2* __restrict__ pairs, float* __restrict__ vals, int32_t* __restrict__ idx_out,
     SelState* __restrict__ st_small, uint32_t gid_base, uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp,
-    unsigned long long* __restrict__ overflow) {
+    unsigned long long* __restrict__ overflow, float* __restrict__ mom) {
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t h[2048];
@@ -218,6 +218,9 @@ __global__ __launch_bounds__(NT) void k_small_select(
       else { vals[c0 + pos] = v[k]; idx_out[c0 + pos] = i; }
     }
     if (EF) ep[i] = sel ? 0.f : v[k];
+    // momentum factor masking (DGC): a sent coordinate restarts its velocity, unless the whole
+    // segment was sent (it then keeps ordinary momentum)
+    if (mom != nullptr && sel && S.total < (uint32_t)n) mom[off + i] = 0.f;
   }
   if (OUT == OUT_PAIRS)
     for (uint32_t p = S.total + threadIdx.x; p < cap; p += NT) pairs[c0 + p] = make_int2(SENT, 0);
@@ -501,7 +504,8 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
                                               const int64_t* __restrict__ cap_off,
                                               int2* __restrict__ pairs, float* __restrict__ vals,
                                               int32_t* __restrict__ idx_out, uint32_t gid_base,
-                                              uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp) {
+                                              uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp,
+                                              float* __restrict__ mom) {
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t scr[NT / WAVE];
@@ -512,6 +516,8 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   const int64_t off = seg_off[s];
   const SelState S = st[li];
   const uint2 bp = pre[blockIdx.x];
+  // momentum factor masking (see k_small_select): only in segments not sent whole
+  float* mp = (mom != nullptr && S.total < (uint32_t)n) ? mom + off : nullptr;
   const int64_t c0 = cap_off[s];
   float* gp = g + off;
   float* ep = EF ? ef + off : nullptr;
@@ -573,6 +579,7 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
     if (sel) {
       if (OUT == OUT_PAIRS) pairs[c0 + pos] = make_int2(i, __float_as_int(v[k]));
       else { vals[c0 + pos] = v[k]; idx_out[c0 + pos] = i; }
+      if (mp != nullptr) mp[i] = 0.f;
     }
     if (EF) ep[i] = sel ? 0.f : v[k];
   }
@@ -965,7 +972,7 @@ static void select_compress_t(const SelectArgs& a, hipStream_t st) {
   if (a.n_small > 0)
     LW_LAUNCH((k_small_select<KM, OUT, EF>), a.n_small, st, a.g, a.ef, a.seg_off, a.seg_n, a.keep,
               a.cap_off, a.small_segs, a.pairs, a.vals, a.idx_out, a.st_small, a.gid_base, a.step,
-              a.seed0, a.seed1, a.step_ptr, a.overflow);
+              a.seed0, a.seed1, a.step_ptr, a.overflow, a.mom);
   if (a.n_large == 0) return;
   {
     const int64_t words = (int64_t)HIST_WORDS * a.n_large;
@@ -991,7 +998,7 @@ static void select_compress_t(const SelectArgs& a, hipStream_t st) {
     LW_LAUNCH(k_fill_tail, a.n_large, st, a.pairs, a.cap_off, a.large_segs, a.st_large);
   LW_LAUNCH((k_write<KM, OUT, EF>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
             a.tasks, a.st_large, a.pre, a.cap_off, a.pairs, a.vals, a.idx_out, a.gid_base, a.step,
-            a.seed0, a.seed1, a.step_ptr);
+            a.seed0, a.seed1, a.step_ptr, a.mom);
 }
 
 void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st) {
@@ -1055,11 +1062,11 @@ void thresh_write(const SelectArgs& a, bool ef, hipStream_t st) {
   if (ef)
     LW_LAUNCH((k_write<KM_THRESH, OUT_PAIRS, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
               a.large_segs, a.tasks, a.st_large, a.pre, a.cap_off, a.pairs, a.vals, a.idx_out, 0u,
-               0u, 0u, 0u, (const uint32_t*)nullptr);
+               0u, 0u, 0u, (const uint32_t*)nullptr, a.mom);
   else
     LW_LAUNCH((k_write<KM_THRESH, OUT_PAIRS, false>), a.n_tasks, st, a.g, a.ef, a.seg_off,
               a.seg_n, a.large_segs, a.tasks, a.st_large, a.pre, a.cap_off, a.pairs, a.vals,
-              a.idx_out, 0u,  0u, 0u, 0u, (const uint32_t*)nullptr);
+              a.idx_out, 0u,  0u, 0u, 0u, (const uint32_t*)nullptr, a.mom);
 }
 
 void unpack_pairs(const int2* gathered, int64_t cap_total, int ws, float* g, const int64_t* seg_off,

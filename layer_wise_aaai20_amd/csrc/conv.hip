@@ -144,9 +144,9 @@ static ConvGeom to_device(const ConvGeomHost& h) {
 }
 
 #define LW_LAUNCH(AKC, BKC, EPI, PRO, CVM) \
-  hipLaunchKernelGGL((k_gemm<BM, BN, BK, AKC, BKC, EPI, PRO, CVM>), grid, dim3(GT), 0, st, k)
+  hipLaunchKernelGGL((k_gemm<BM, BN, BK, AKC, BKC, EPI, PRO, CVM, MF>), grid, dim3(GT), 0, st, k)
 
-template <int BM, int BN, int BK, int CVM>
+template <int BM, int BN, int BK, int CVM, int MF>
 static void conv_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, hipStream_t st) {
   const bool pro = g.pro_scale != nullptr;
   if constexpr (CVM == CV_A) {
@@ -179,6 +179,7 @@ void conv_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st);   // g
 
 bool conv_tile_ok(int mode, int tile) {
   if ((mode == CV_A || mode == CV_B) && (tile == GEMM_B256 || tile == GEMM_B256x128)) return true;
+  tile = gemm_base_tile(tile);         // the MF = 32 twins are built for the same tiles
   if (mode == CV_A || mode == CV_A4)
     return tile == GEMM_T128x128x32 || tile == GEMM_T128x128x64 || tile == GEMM_T256x64x32 ||
            tile == GEMM_T256x64x64 || tile == GEMM_T64x64x64;
@@ -186,24 +187,31 @@ bool conv_tile_ok(int mode, int tile) {
          tile == GEMM_T64x64x64;
 }
 
-template <int CVM>
-static void conv_dispatch(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, hipStream_t st) {
+template <int CVM, int MF>
+static void conv_dispatch_mf(const GemmArgs& g, const GemmK& k, int epi, dim3 grid,
+                             hipStream_t st) {
   if constexpr (CVM == CV_A || CVM == CV_A4) {
-    switch (g.tile) {
-      case GEMM_T128x128x64: conv_tile<128, 128, 64, CVM>(g, k, epi, grid, st); break;
-      case GEMM_T256x64x32: conv_tile<256, 64, 32, CVM>(g, k, epi, grid, st); break;
-      case GEMM_T256x64x64: conv_tile<256, 64, 64, CVM>(g, k, epi, grid, st); break;
-      case GEMM_T64x64x64: conv_tile<64, 64, 64, CVM>(g, k, epi, grid, st); break;
-      default: conv_tile<128, 128, 32, CVM>(g, k, epi, grid, st); break;
+    switch (gemm_base_tile(g.tile)) {
+      case GEMM_T128x128x64: conv_tile<128, 128, 64, CVM, MF>(g, k, epi, grid, st); break;
+      case GEMM_T256x64x32: conv_tile<256, 64, 32, CVM, MF>(g, k, epi, grid, st); break;
+      case GEMM_T256x64x64: conv_tile<256, 64, 64, CVM, MF>(g, k, epi, grid, st); break;
+      case GEMM_T64x64x64: conv_tile<64, 64, 64, CVM, MF>(g, k, epi, grid, st); break;
+      default: conv_tile<128, 128, 32, CVM, MF>(g, k, epi, grid, st); break;
     }
   } else {
-    switch (g.tile) {
-      case GEMM_T128x128x64: conv_tile<128, 128, 64, CVM>(g, k, epi, grid, st); break;
-      case GEMM_T64x256x32: conv_tile<64, 256, 32, CVM>(g, k, epi, grid, st); break;
-      case GEMM_T64x64x64: conv_tile<64, 64, 64, CVM>(g, k, epi, grid, st); break;
-      default: conv_tile<128, 128, 32, CVM>(g, k, epi, grid, st); break;
+    switch (gemm_base_tile(g.tile)) {
+      case GEMM_T128x128x64: conv_tile<128, 128, 64, CVM, MF>(g, k, epi, grid, st); break;
+      case GEMM_T64x256x32: conv_tile<64, 256, 32, CVM, MF>(g, k, epi, grid, st); break;
+      case GEMM_T64x64x64: conv_tile<64, 64, 64, CVM, MF>(g, k, epi, grid, st); break;
+      default: conv_tile<128, 128, 32, CVM, MF>(g, k, epi, grid, st); break;
     }
   }
+}
+
+template <int CVM>
+static void conv_dispatch(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, hipStream_t st) {
+  if (gemm_is_mf32(g.tile)) conv_dispatch_mf<CVM, 32>(g, k, epi, grid, st);
+  else conv_dispatch_mf<CVM, 16>(g, k, epi, grid, st);
 }
 
 int conv_splits_used(const GemmArgs& g) {

@@ -4,7 +4,8 @@
 // instruction depend on the format. The default build is bf16. The lwaaai16 build (csrc/build.py
 // PRECISIONS, compiled with -DLW_FP16) is the same kernels for IEEE fp16 — the reference's --fp16
 // recipe (IMAGENET/training/train_imagenet_nv.py:410-428, fp16util.py:21-138) on the MFMA path:
-// v_mfma_f32_16x16x32_f16 instead of _bf16, fp32 accumulation and fp32 epilogue math in both.
+// v_mfma_f32_16x16x32_f16 / _32x32x16_f16 instead of _bf16, fp32 accumulation and fp32 epilogue
+// math in both.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -12,6 +13,7 @@
 namespace lw {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 struct ElemBF16 {
   typedef __bf16 V8 __attribute__((ext_vector_type(8)));
@@ -24,6 +26,9 @@ struct ElemBF16 {
   }
   static __device__ __forceinline__ f32x4 mfma(V8 a, V8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x16 mfma32(V8 a, V8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
   }
 };
 
@@ -41,6 +46,9 @@ struct ElemF16 {
   }
   static __device__ __forceinline__ f32x4 mfma(V8 a, V8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x16 mfma32(V8 a, V8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
   }
 };
 
@@ -61,5 +69,8 @@ __device__ __forceinline__ uint32_t pack2h(float a, float b) {
   return (uint32_t)f2h(a) | ((uint32_t)f2h(b) << 16);
 }
 __device__ __forceinline__ f32x4 mfma16(h16x8 a, h16x8 b, f32x4 c) { return E16::mfma(a, b, c); }
+// v_mfma_f32_32x32x16_{bf16,f16}: lane l holds A[row l&31][k = 8(l>>5) + j] and B[k][col l&31]
+// (j = 0..7); result register r of lane l is D[row (r&3) + 8(r>>2) + 4(l>>5)][col l&31]
+__device__ __forceinline__ f32x16 mfma32(h16x8 a, h16x8 b, f32x16 c) { return E16::mfma32(a, b, c); }
 
 }  // namespace lw

@@ -334,7 +334,7 @@ static bool is_big_tile(int t) {
   return t == GEMM_B256 || t == GEMM_B256x128 || t == GEMM_P256 || t == GEMM_P256x128;
 }
 static TileShape tile_shape(int t) {
-  switch (t) {
+  switch (gemm_base_tile(t)) {
     case GEMM_T128x128x64: return {128, 128, 64};
     case GEMM_T256x64x32: return {256, 64, 32};
     case GEMM_T64x256x32: return {64, 256, 32};
@@ -387,37 +387,39 @@ int gemm_splits_used(const GemmArgs& g) {
   return (g.K + kps - 1) / kps;
 }
 
-template <int BM, int BN, int BK, int EPI, int PRO>
+template <int BM, int BN, int BK, int EPI, int PRO, int MF>
 static void launch_layout(const GemmArgs& g, const GemmK& k, dim3 grid, hipStream_t st) {
   const dim3 block(GT);
+#define LW_K(AK, BKC) (k_gemm<BM, BN, BK, AK, BKC, EPI, PRO, CV_NONE, MF>)
   if constexpr (PRO == PRO_A) {
-    if (g.b_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, true, EPI, PRO>), grid, block, 0, st, k);
-    else hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI, PRO>), grid, block, 0, st, k);
+    if (g.b_kcontig) hipLaunchKernelGGL(LW_K(true, true), grid, block, 0, st, k);
+    else hipLaunchKernelGGL(LW_K(true, false), grid, block, 0, st, k);
   } else if constexpr (PRO == PRO_B) {
-    if (g.a_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI, PRO>), grid, block, 0, st, k);
-    else hipLaunchKernelGGL((k_gemm<BM, BN, BK, false, false, EPI, PRO>), grid, block, 0, st, k);
+    if (g.a_kcontig) hipLaunchKernelGGL(LW_K(true, false), grid, block, 0, st, k);
+    else hipLaunchKernelGGL(LW_K(false, false), grid, block, 0, st, k);
   } else {
-    if (g.a_kcontig && g.b_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, true, EPI, PRO>), grid, block, 0, st, k);
-    else if (g.a_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI, PRO>), grid, block, 0, st, k);
-    else if (g.b_kcontig) hipLaunchKernelGGL((k_gemm<BM, BN, BK, false, true, EPI, PRO>), grid, block, 0, st, k);
-    else hipLaunchKernelGGL((k_gemm<BM, BN, BK, false, false, EPI, PRO>), grid, block, 0, st, k);
+    if (g.a_kcontig && g.b_kcontig) hipLaunchKernelGGL(LW_K(true, true), grid, block, 0, st, k);
+    else if (g.a_kcontig) hipLaunchKernelGGL(LW_K(true, false), grid, block, 0, st, k);
+    else if (g.b_kcontig) hipLaunchKernelGGL(LW_K(false, true), grid, block, 0, st, k);
+    else hipLaunchKernelGGL(LW_K(false, false), grid, block, 0, st, k);
   }
+#undef LW_K
 }
 
-template <int BM, int BN, int BK>
+template <int BM, int BN, int BK, int MF>
 static void launch_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, hipStream_t st) {
   const int pro = g.pro_scale ? (g.pro_on_a ? PRO_A : PRO_B) : PRO_NONE;
 #define LW_E(E)                                                                                  \
-  if (pro == PRO_A) launch_layout<BM, BN, BK, E, PRO_A>(g, k, grid, st);                         \
-  else if (pro == PRO_B) launch_layout<BM, BN, BK, E, PRO_B>(g, k, grid, st);                    \
-  else launch_layout<BM, BN, BK, E, PRO_NONE>(g, k, grid, st);
+  if (pro == PRO_A) launch_layout<BM, BN, BK, E, PRO_A, MF>(g, k, grid, st);                     \
+  else if (pro == PRO_B) launch_layout<BM, BN, BK, E, PRO_B, MF>(g, k, grid, st);                \
+  else launch_layout<BM, BN, BK, E, PRO_NONE, MF>(g, k, grid, st);
   if (epi == EPI_PARTIAL) { LW_E(EPI_PARTIAL) }
   else if (epi == EPI_STATS) { LW_E(EPI_STATS) }
   else if (epi == EPI_BSTATS) {
     // a data-gradient GEMM (dy·W: K-contiguous dy, N-contiguous W) that also does the reduce
     // pass of the BatchNorm its output feeds (the host checks the layout and no prologue)
-    hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI_BSTATS, PRO_NONE>), grid, dim3(GT), 0,
-                       st, k);
+    hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI_BSTATS, PRO_NONE, CV_NONE, MF>), grid,
+                       dim3(GT), 0, st, k);
   }
   else { LW_E(EPI_STORE) }
 #undef LW_E
@@ -474,13 +476,24 @@ void gemm_bf16(const GemmArgs& g, hipStream_t st) {
     if (zs > 1) splitk_reduce(g, zs, st);
     return;
   }
-  switch (t) {
-    case GEMM_T128x128x64: launch_tile<128, 128, 64>(g, k, epi, grid, st); break;
-    case GEMM_T256x64x32: launch_tile<256, 64, 32>(g, k, epi, grid, st); break;
-    case GEMM_T64x256x32: launch_tile<64, 256, 32>(g, k, epi, grid, st); break;
-    case GEMM_T256x64x64: launch_tile<256, 64, 64>(g, k, epi, grid, st); break;
-    case GEMM_T64x64x64: launch_tile<64, 64, 64>(g, k, epi, grid, st); break;
-    default: launch_tile<128, 128, 32>(g, k, epi, grid, st); break;
+  if (gemm_is_mf32(t)) {
+    switch (gemm_base_tile(t)) {
+      case GEMM_T128x128x64: launch_tile<128, 128, 64, 32>(g, k, epi, grid, st); break;
+      case GEMM_T256x64x32: launch_tile<256, 64, 32, 32>(g, k, epi, grid, st); break;
+      case GEMM_T64x256x32: launch_tile<64, 256, 32, 32>(g, k, epi, grid, st); break;
+      case GEMM_T256x64x64: launch_tile<256, 64, 64, 32>(g, k, epi, grid, st); break;
+      case GEMM_T64x64x64: launch_tile<64, 64, 64, 32>(g, k, epi, grid, st); break;
+      default: launch_tile<128, 128, 32, 32>(g, k, epi, grid, st); break;
+    }
+  } else {
+    switch (t) {
+      case GEMM_T128x128x64: launch_tile<128, 128, 64, 16>(g, k, epi, grid, st); break;
+      case GEMM_T256x64x32: launch_tile<256, 64, 32, 16>(g, k, epi, grid, st); break;
+      case GEMM_T64x256x32: launch_tile<64, 256, 32, 16>(g, k, epi, grid, st); break;
+      case GEMM_T256x64x64: launch_tile<256, 64, 64, 16>(g, k, epi, grid, st); break;
+      case GEMM_T64x64x64: launch_tile<64, 64, 64, 16>(g, k, epi, grid, st); break;
+      default: launch_tile<128, 128, 32, 16>(g, k, epi, grid, st); break;
+    }
   }
   if (zs > 1) splitk_reduce(g, zs, st);
 }

@@ -71,10 +71,21 @@ __device__ __forceinline__ float masked_addend1(const uint16_t* __restrict__ add
 }
 
 // R = extent of the tile along m (A) or n (B). K-contiguous (KC) tiles are stored [R][BK]: at
-// BK = 64 unpadded with the 16-byte chunks of row r XOR-swizzled by (r & 7) (conflict-free
-// ds_read_b128 fragment reads and ds_write_b128 row stores, cdna_hip_programming.md T2), at
-// BK = 32 padded to BK + 8. The M/N-contiguous tiles are stored [BK][R+PAD] and read with the
-// transposing ds_read_b64_tr_b16. Both are moved as 16-byte chunks of 8 contiguous elements.
+// BK = 64 unpadded with the 16-byte chunks of row r XOR-swizzled (conflict-free ds_read_b128
+// fragment reads, cdna_hip_programming.md T2), at BK = 32 padded to BK + 8. The M/N-contiguous
+// tiles are stored [BK][R+PAD] and read with the transposing ds_read_b64_tr_b16. Both are moved as
+// 16-byte chunks of 8 contiguous elements.
+//
+// MF is the MFMA shape the tile feeds: 16 (v_mfma_f32_16x16x32: a fragment read is 16 rows x one
+// 8-k chunk per 16-lane group) or 32 (v_mfma_f32_32x32x16: 32 rows x one chunk per 32-lane half).
+// The swizzle key differs: a ds_read_b128 is served in the lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31} (+32), so the 16 rows one group reads must hit 16 distinct 16-byte slots of
+// the 256-byte bank row. Two 128-byte rows share a bank row (slot = 8*(r&1) + chunk'): for the
+// 16x16 read (rows r&15 at chunks c, c+1) the key r & 7 does it; for the 32x32 read (rows
+// {0-3,12-15,20-27} at ONE chunk) the key (r >> 1) & 7 does (r & 7 would leave it 2-way).
+template <int MF>
+__host__ __device__ constexpr int swz_key(int r) { return MF == 32 ? ((r >> 1) & 7) : (r & 7); }
+
 template <int R, int BK, bool KC> struct Tile {
   static constexpr bool SWZ = KC && BK == 64;
   static constexpr int LD = KC ? (SWZ ? BK : BK + PAD) : R + PAD;
@@ -85,10 +96,10 @@ template <int R, int BK, bool KC> struct Tile {
 };
 
 // element offset of chunk c of stored row r
-template <int R, int BK, bool KC>
+template <int R, int BK, bool KC, int MF = 16>
 __device__ __forceinline__ int tile_off(int r, int c) {
   using T = Tile<R, BK, KC>;
-  return r * T::LD + (T::SWZ ? (c ^ (r & 7)) : c) * 8;
+  return r * T::LD + (T::SWZ ? (c ^ swz_key<MF>(r)) : c) * 8;
 }
 
 // Chunk i of the workgroup (thread t stages chunks t + h*GT): stored row rr, chunk column cc.
@@ -130,11 +141,11 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, uint16_t* wave_
 
 // A K-contiguous BK = 64 tile filled by LDS-DMA: every wave-instruction writes 1 KiB = 8 whole
 // 128-byte rows in lane order, so the XOR swizzle moves to the SOURCE: the lane that lands in
-// stored chunk slot cc of row rr fetches logical chunk cc ^ (rr & 7). A thread's rows all share
-// rr & 7 (they differ by multiples of GT / 8 rows), so one per-thread chunk column serves all.
-template <int R, int BK, bool KC, bool DMA>
+// stored chunk slot cc of row rr fetches logical chunk cc ^ key(rr). A thread's rows all share
+// the key (they differ by multiples of GT / 8 = 32 rows), so one per-thread chunk column serves all.
+template <int R, int BK, bool KC, bool DMA, int MF = 16>
 __device__ __forceinline__ int src_chunk(int cc, int rr) {
-  return (DMA && Tile<R, BK, KC>::SWZ) ? (cc ^ (rr & 7)) : cc;
+  return (DMA && Tile<R, BK, KC>::SWZ) ? (cc ^ swz_key<MF>(rr)) : cc;
 }
 
 // LDS element offset of the first row of wave-instruction h of this thread's wave
@@ -146,7 +157,7 @@ __device__ __forceinline__ int dma_wave_off(int h) {
 
 // Plain operand tile: byte offset of each of this thread's chunks at k = 0 (OOB outside the
 // matrix); a K-step adds k*2 (KC) or k*ld*2 (M/N-contiguous) and masks the K tail.
-template <int R, int BK, bool KC>
+template <int R, int BK, bool KC, int MF = 16>
 struct PlainLoader {
   static constexpr int PT = Tile<R, BK, KC>::PER_T;
   __amdgpu_buffer_rsrc_t rs;
@@ -163,7 +174,7 @@ struct PlainLoader {
     for (int h = 0; h < PT; ++h) {
       int rr, cc;
       chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
-      cc = src_chunk<R, BK, KC, DMA>(cc, rr);
+      cc = src_chunk<R, BK, KC, DMA, MF>(cc, rr);
       if (KC) {
         const int gr = row0 + rr;
         voff[h] = gr < rows ? (uint32_t)(((int64_t)gr * ld + cc * 8) * 2) : OOB;
@@ -234,7 +245,7 @@ __device__ __forceinline__ uint4 affine_relu8(uint4 v, const Coef8& c) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <int R, int BK, bool KC, bool PRO>
+template <int R, int BK, bool KC, bool PRO, int MF = 16>
 __device__ __forceinline__ void store_tile(uint16_t* __restrict__ S,
                                            const uint4 (&r)[Tile<R, BK, KC>::PER_T],
                                            uint32_t okmask, const Coef8& co) {
@@ -246,16 +257,36 @@ __device__ __forceinline__ void store_tile(uint16_t* __restrict__ S,
     chunk_pos<R, BK, KC>(threadIdx.x + h * GT, rr, cc);
     uint4 v = r[h];
     if (PRO && ((okmask >> h) & 1u)) v = affine_relu8(v, co);
-    *reinterpret_cast<uint4*>(S + tile_off<R, BK, KC>(rr, cc)) = v;
+    *reinterpret_cast<uint4*>(S + tile_off<R, BK, KC, MF>(rr, cc)) = v;
   }
 }
 
-// MFMA operand fragment (8 bf16 along k, k-group g = lane>>4, sub-step s of 32 k) for tile
-// row/col i_base + (lane&15).
-template <int R, int BK, bool KC>
+// MFMA operand fragment: 8 bf16 along k.
+//   MF = 16: k-group g = lane>>4, sub-step s of 32 k, tile row/col i_base + (lane&15);
+//   MF = 32: k-group h = lane>>5, sub-step s of 16 k, tile row/col i_base + (lane&31).
+// The transposing read (M/N-contiguous tiles): per 16-lane group, lane 4q+p addresses row q of a
+// 4-row block at columns 4p..4p+3 and receives column (lane&15) of those 4 rows (T10); two reads
+// (rows +0..3, +4..7) make the 8 k of a fragment. For MF = 32 the group's 16 columns are
+// i_base + 16(g&1) + (lane&15) and its rows start at 16s + 8(g>>1).
+template <int R, int BK, bool KC, int MF = 16>
 __device__ __forceinline__ h16x8 load_frag(const uint16_t* S, int i_base, int s) {
   using T = Tile<R, BK, KC>;
   const int l = threadIdx.x & 63;
+  if (MF == 32) {
+    if (KC) {
+      const uint16_t* p = S + tile_off<R, BK, KC, MF>(i_base + (l & 31), 2 * s + (l >> 5));
+      return *reinterpret_cast<const h16x8*>(p);
+    }
+    const int g = l >> 4, t = l & 15, q = t >> 2, p4 = t & 3;
+    typedef __attribute__((address_space(3))) i16x4 lds_v4;
+    const uint16_t* p0 = S + (16 * s + 8 * (g >> 1) + q) * T::LD + i_base + 16 * (g & 1) + 4 * p4;
+    const uint16_t* p1 = p0 + 4 * T::LD;
+    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0));
+    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p1));
+    typedef short i16x8 __attribute__((ext_vector_type(8)));
+    const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(h16x8, v);
+  }
   if (KC) {
     const uint16_t* p = S + tile_off<R, BK, KC>(i_base + (l & 15), 4 * s + (l >> 4));
     return *reinterpret_cast<const h16x8*>(p);
@@ -363,14 +394,14 @@ struct RowGather {
   int c4_drow, c4_js;   // 4-channel image: the thread's tap relative to the step's first row
 };
 
-template <int R, int BK, bool DMA = false>
+template <int R, int BK, bool DMA = false, int MF = 16>
 __device__ __forceinline__ void row_gather_init(RowGather<R, BK>& g, const uint16_t* X,
                                                 uint32_t bytes, const ConvGeom& cv,
                                                 const ConvClass& cc, int m0) {
   using T = Tile<R, BK, true>;
   g.rs = make_rsrc(X, bytes);
   const int hw = cc.Hg * cc.Wg;
-  g.kc = src_chunk<R, BK, true, DMA>((int)(threadIdx.x % T::CPR), (int)(threadIdx.x / T::CPR)) * 8;
+  g.kc = src_chunk<R, BK, true, DMA, MF>((int)(threadIdx.x % T::CPR), (int)(threadIdx.x / T::CPR)) * 8;
   // 4-channel gather with BK a multiple of a whole filter row (4*TS elements): a K-step covers
   // whole rows, so the thread's tap offset within them is fixed (no per-chunk division)
   g.c4_drow = (g.kc >> 2) / cc.TS;
@@ -629,11 +660,32 @@ __device__ __forceinline__ void tile_split_of(int tiles_m, int tiles_n, int& tm,
   tile_of(lin - split * tiles, tiles_m, tiles_n, tm, tn);
 }
 
-template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int PRO, int CV = CV_NONE>
+template <int MF> struct AccOf { typedef f32x4 T; };
+template <> struct AccOf<32> { typedef f32x16 T; };
+
+// Sum over the 32 lanes of one half-wave, every lane getting the total: the 16-lane DPP fold,
+// then the other DPP row of the half (ds_swizzle bit mode, xor 16): both lanes of a pair add the
+// same two values, so every lane holds the bit-identical total.
+__device__ __forceinline__ float sum32(float v) {
+  v = sum16(v);
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v),
+                                                                    0x401F));
+}
+
+// MF: the MFMA shape (16: v_mfma_f32_16x16x32, 32: v_mfma_f32_32x32x16). Same tiles, waves and
+// LDS traffic per FLOP (a wave's WTM x WTN block reads (WTM + WTN) x BK operands per K-step either
+// way); the 32x32 shape issues half the MFMA instructions, its operand fragments cover 32 rows,
+// and its accumulators hold four runs of 4 consecutive columns per lane.
+template <int BM, int BN, int BK, bool AKC, bool BKC, int EPI, int PRO, int CV = CV_NONE,
+          int MF = 16>
 __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   using TA = Tile<BM, BK, AKC>;
   using TB = Tile<BN, BK, BKC>;
-  constexpr int WTM = BM / 2, WTN = BN / 2, FM = WTM / 16, FN = WTN / 16;
+  using Acc = typename AccOf<MF>::T;
+  constexpr int WTM = BM / 2, WTN = BN / 2, FM = WTM / MF, FN = WTN / MF;
+  constexpr int NG = MF == 32 ? 4 : 1;         // runs of 4 consecutive columns per accumulator
+  constexpr int NR = MF == 32 ? 16 : 4;        // accumulator registers
+  static_assert(WTM % MF == 0 && WTN % MF == 0, "wave tile must hold whole MFMA blocks");
   constexpr int STAGE = TA::ELEMS + TB::ELEMS;
   constexpr int LDC = BN + 4;                  // fp32 staging row (≡ 4 dwords mod 64 banks)
   constexpr int LDH = BN + 16;                 // bf16 staging row (≡ 8 dwords mod 64 banks)
@@ -675,11 +727,13 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   const int wr = w >> 1, wc = w & 1;
 
-  f32x4 acc[FM][FN];
+  Acc acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
 
   // One register staging set: the next K-step's global loads are issued before this step's
   // MFMAs and written to the other LDS buffer after them. (A second set — loads two steps
@@ -694,10 +748,10 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   Coef8 coB;
   RowGather<BM, BK> rg;
   ColGather<BN, BK> cg;
-  PlainLoader<BM, BK, AKC> la;
-  PlainLoader<BN, BK, BKC> lb;
+  PlainLoader<BM, BK, AKC, MF> la;
+  PlainLoader<BN, BK, BKC, MF> lb;
   if constexpr (GA) {
-    row_gather_init<BM, BK, GL>(rg, p.A, p.a_bytes, p.cv, ccl, m0);
+    row_gather_init<BM, BK, GL, MF>(rg, p.A, p.a_bytes, p.cv, ccl, m0);
     if (!G4 && p.cv.C % BK == 0) row_gather_seek<BM, BK>(rg, p.cv, ccl, kbeg);
   } else {
     la.template init<GL>(p.A, p.a_bytes, p.lda, m0, p.M);
@@ -718,24 +772,27 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
     if (PRO == PRO_A) load_coef8(r.coA, p.pro_scale, p.pro_shift, a_ch, GA ? p.cv.C : kend);
   };
   auto stage = [&](uint16_t* dst, const Regs& r) {
-    store_tile<BM, BK, AKC, PRO == PRO_A>(dst, r.a, r.oka, r.coA);
+    store_tile<BM, BK, AKC, PRO == PRO_A, MF>(dst, r.a, r.oka, r.coA);
     if constexpr (GB) store_tile_rows<BN, BK>(dst + TA::ELEMS, r.b);
-    else store_tile<BN, BK, BKC, PRO == PRO_B>(dst + TA::ELEMS, r.b, r.okb, coB);
+    else store_tile<BN, BK, BKC, PRO == PRO_B, MF>(dst + TA::ELEMS, r.b, r.okb, coB);
   };
   auto compute = [&](const uint16_t* As) {
     const uint16_t* Bs = As + TA::ELEMS;
+    constexpr int KS = MF == 32 ? 16 : 32;       // k per MFMA
 #pragma unroll
-    for (int s = 0; s < BK / 32; ++s) {
+    for (int s = 0; s < BK / KS; ++s) {
       h16x8 fa[FM], fb[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) fa[i] = load_frag<BM, BK, AKC>(As, wr * WTM + i * 16, s);
+      for (int i = 0; i < FM; ++i) fa[i] = load_frag<BM, BK, AKC, MF>(As, wr * WTM + i * MF, s);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) fb[j] = load_frag<BN, BK, BKC>(Bs, wc * WTN + j * 16, s);
+      for (int j = 0; j < FN; ++j) fb[j] = load_frag<BN, BK, BKC, MF>(Bs, wc * WTN + j * MF, s);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (MF == 32) acc[i][j] = mfma32(fb[j], fa[i], acc[i][j]);
+          else acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+        }
     }
   };
   const int nsteps = kbeg < kend ? (kend - kbeg + BK - 1) / BK : 0;
@@ -788,8 +845,9 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   }
 
   // ---- epilogue. B is the MFMA's first operand, so each accumulator holds Cᵀ: lane l has
-  // C[m = .. + (l&15)][n = .. + 4*(l>>4) + r], r = 0..3 (four consecutive columns of one row).
-  const int lm = l & 15, ln = 4 * (l >> 4);
+  // MF = 16: C[m = .. + (l&15)][n = .. + 4*(l>>4) + r], r = 0..3 (four consecutive columns);
+  // MF = 32: C[m = .. + (l&31)][n = .. + 8*g + 4*(l>>5) + r] in register 4g + r, g = 0..3.
+  const int lm = l & (MF - 1), ln = MF == 32 ? 4 * (l >> 5) : 4 * (l >> 4);
   const bool bf_out = EPI != EPI_PARTIAL && p.out_bf16;
   static_assert(EPI != EPI_BSTATS || GA || CV == CV_NONE, "backward statistics: row outputs only");
   uint16_t* Ch = reinterpret_cast<uint16_t*>(lds);                  // bf16 tile [BM][LDH]
@@ -797,8 +855,9 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   if (EPI != EPI_PARTIAL) {
     // bias / ReLU / rounding in registers; column statistics; bf16 staging of the whole tile
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int nl = wc * WTN + j * 16 + ln;
+    for (int jg = 0; jg < FN * NG; ++jg) {
+      const int j = jg / NG, g4 = jg % NG;
+      const int nl = wc * WTN + j * MF + 8 * g4 + ln;
       const int n = n0 + nl;
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       if (p.bias) {
@@ -808,11 +867,11 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
       float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
-        const int ml = wr * WTM + i * 16 + lm;
+        const int ml = wr * WTM + i * MF + lm;
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float x = acc[i][j][r] + bv[r];
+          float x = acc[i][j][4 * g4 + r] + bv[r];
           if (p.relu) x = fmaxf(x, 0.f);
           v[r] = x;
         }
@@ -827,7 +886,7 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
               make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
         } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+          for (int r = 0; r < 4; ++r) acc[i][j][4 * g4 + r] = v[r];
         }
         // column statistics of the stored values (bf16-rounded when the output is bf16), from
         // the accumulators: a per-lane sum over the FM row blocks, then a 16-lane butterfly
@@ -837,11 +896,12 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
         }
       }
       if (EPI == EPI_STATS) {
-        // the 16 rows held by lanes sharing l>>4 (one DPP row), fixed pairing order
+        // the MF rows held by lanes sharing the column run (one DPP row / one half-wave), fixed
+        // pairing order
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          s1[r] = sum16(s1[r]);
-          s2[r] = sum16(s2[r]);
+          s1[r] = MF == 32 ? sum32(s1[r]) : sum16(s1[r]);
+          s2[r] = MF == 32 ? sum32(s2[r]) : sum16(s2[r]);
         }
         if (lm == 0) {
 #pragma unroll
@@ -985,8 +1045,11 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            *reinterpret_cast<float4*>(Cs + (i * 16 + lm) * LDC + wc * WTN + j * 16 + ln) =
-                make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+#pragma unroll
+            for (int g4 = 0; g4 < NG; ++g4)
+              *reinterpret_cast<float4*>(Cs + (i * MF + lm) * LDC + wc * WTN + j * MF + 8 * g4 + ln) =
+                  make_float4(acc[i][j][4 * g4], acc[i][j][4 * g4 + 1], acc[i][j][4 * g4 + 2],
+                              acc[i][j][4 * g4 + 3]);
       }
       __syncthreads();
       const int mb = m0 + half * WTM;

@@ -54,6 +54,9 @@ struct SelectArgs {
   // rng
   uint32_t gid_base, step, seed0, seed1;
   const uint32_t* step_ptr;    // optional device step counter (overrides `step`; HIP graphs)
+  // optional momentum-correction velocity (same layout as g): zeroed at every coordinate that was
+  // sent, in segments that were not sent whole (those keep ordinary momentum)
+  float* mom;
   // optional device counter: elements the reference rule would send that did not fit the
   // payload (Top-K ties beyond the tie slack; threshold hits beyond a fixed sparse capacity)
   unsigned long long* overflow;
@@ -109,6 +112,13 @@ struct SgdArgs {
   uint16_t* pb;                // optional bf16 mirror of p (same layout), written in the same pass
 };
 void sgd_step(const SgdArgs& a, hipStream_t st);
+// momentum correction (optim.hip): the compressor prologue g' = g + wmul·wd·p, u = mc·u + g',
+// g = u over a bucket's arena segments (p / seg_wd null: no weight decay), and the velocity masking
+// u = 0 where e == 0 for codecs without a selection
+void mc_prep(float* g, float* u, const float* p, const int64_t* seg_off, const int32_t* seg_n,
+             const int32_t* segs, const int2* tasks, int n_tasks, const float* seg_wd, float mc,
+             float wmul, hipStream_t st);
+void mc_mask(float* u, const float* e, int64_t n, hipStream_t st);
 
 // fused BatchNorm (+add) (+ReLU), NHWC (bn.hip)
 struct BNArgs {
@@ -236,7 +246,11 @@ enum GemmTile { GEMM_AUTO = 0, GEMM_T128x128x32 = 1, GEMM_T128x128x64 = 2, GEMM_
                 // the same tiles as a persistent kernel (one workgroup per CU walking tiles, the
                 // next tile's first K-tiles loaded during this tile's epilogue): K-contiguous A/B,
                 // bf16 output (+ statistics rows, + masked addend), K > 64
-                GEMM_P256 = 23, GEMM_P256x128 = 24 };
+                GEMM_P256 = 23, GEMM_P256x128 = 24,
+                // the tiles 1..6 on v_mfma_f32_32x32x16 (tile id + 40, gemm_core.h k_gemm MF = 32)
+                GEMM_M32 = 40 };
+inline bool gemm_is_mf32(int t) { return t > GEMM_M32 && t <= GEMM_M32 + 6; }
+inline int gemm_base_tile(int t) { return gemm_is_mf32(t) ? t - GEMM_M32 : t; }
 void gemm_bf16(const GemmArgs& g, hipStream_t st);
 int gemm_pick_tile(const GemmArgs& g);
 int gemm_tiles_m(const GemmArgs& g);

@@ -85,6 +85,95 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
   }
 }
 
+// Momentum correction (Lin et al. 2018, DGC; parallel/engine.py), the per-bucket prologue of the
+// compressor, over the bucket's ARENA segments (one task = 8192 elements of one segment):
+//   g' = g + wmul·wd_s·p      weight decay folded into the gradient BEFORE the velocity, as DGC
+//                             does (wmul = 1 / grad_scale keeps it in a loss-scaled gradient's units)
+//   u  = mc·u + g'            local velocity
+//   g  = u                    the compressor (and its error-feedback residual) sees the velocity
+// One read of g, u (and p), one write of g and u: it replaces four ATen passes. Products and sums
+// are rounded separately (no fma contraction), as the CPU mirror (parallel/engine.py) computes them. The masking of the
+// velocity at the coordinates that were sent happens inside the select kernels (compress.hip
+// k_small_select / k_write, SelectArgs::mom) or, for the other codecs, in k_mc_mask.
+template <bool WD>
+__global__ __launch_bounds__(SNT) void k_mc_prep(float* __restrict__ g, float* __restrict__ u,
+                                                 const float* __restrict__ p,
+                                                 const int64_t* __restrict__ seg_off,
+                                                 const int32_t* __restrict__ seg_n,
+                                                 const int32_t* __restrict__ segs,
+                                                 const int2* __restrict__ tasks,
+                                                 const float* __restrict__ seg_wd, float mc,
+                                                 float wmul) {
+  const int2 t = tasks[blockIdx.x];
+  const int s = segs[t.x];
+  const int n = seg_n[s];
+  const int64_t off = seg_off[s];
+  const float wd = WD ? seg_wd[s] * wmul : 0.f;
+  const int end = min(t.y + SEPB, n);
+  const bool vec = (off & 3) == 0;
+  for (int i0 = t.y + threadIdx.x * 4; i0 < end; i0 += SNT * 4) {
+    if (vec && i0 + 3 < end) {
+      float4 gg = *reinterpret_cast<const float4*>(g + off + i0);
+      float4 uu = *reinterpret_cast<const float4*>(u + off + i0);
+      if (WD && wd != 0.f) {
+        const float4 pp = *reinterpret_cast<const float4*>(p + off + i0);
+        gg.x = __fadd_rn(gg.x, __fmul_rn(pp.x, wd)); gg.y = __fadd_rn(gg.y, __fmul_rn(pp.y, wd));
+        gg.z = __fadd_rn(gg.z, __fmul_rn(pp.z, wd)); gg.w = __fadd_rn(gg.w, __fmul_rn(pp.w, wd));
+      }
+      uu.x = __fadd_rn(__fmul_rn(uu.x, mc), gg.x); uu.y = __fadd_rn(__fmul_rn(uu.y, mc), gg.y);
+      uu.z = __fadd_rn(__fmul_rn(uu.z, mc), gg.z); uu.w = __fadd_rn(__fmul_rn(uu.w, mc), gg.w);
+      *reinterpret_cast<float4*>(u + off + i0) = uu;
+      *reinterpret_cast<float4*>(g + off + i0) = uu;
+    } else {
+      for (int k = 0; k < 4 && i0 + k < end; ++k) {
+        const int64_t i = off + i0 + k;
+        float x = g[i];
+        if (WD && wd != 0.f) x = __fadd_rn(x, __fmul_rn(p[i], wd));
+        const float v = __fadd_rn(__fmul_rn(u[i], mc), x);
+        u[i] = v;
+        g[i] = v;
+      }
+    }
+  }
+}
+
+void mc_prep(float* g, float* u, const float* p, const int64_t* seg_off, const int32_t* seg_n,
+             const int32_t* segs, const int2* tasks, int n_tasks, const float* seg_wd, float mc,
+             float wmul, hipStream_t st) {
+  if (n_tasks == 0) return;
+  if (p != nullptr && seg_wd != nullptr)
+    hipLaunchKernelGGL((k_mc_prep<true>), dim3(n_tasks), dim3(SNT), 0, st, g, u, p, seg_off,
+                       seg_n, segs, tasks, seg_wd, mc, wmul);
+  else
+    hipLaunchKernelGGL((k_mc_prep<false>), dim3(n_tasks), dim3(SNT), 0, st, g, u, p, seg_off,
+                       seg_n, segs, tasks, seg_wd, mc, wmul);
+}
+
+// Momentum factor masking for codecs without a selection (quantisers, thresholds on the dense
+// wire): u = 0 where the error-feedback residual is 0, i.e. where the value was sent whole.
+__global__ __launch_bounds__(SNT) void k_mc_mask(float* __restrict__ u, const float* __restrict__ e,
+                                                 int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * SNT * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * SNT + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 3 < n) {
+      float4 uu = *reinterpret_cast<const float4*>(u + i);
+      const float4 ee = *reinterpret_cast<const float4*>(e + i);
+      uu.x = ee.x == 0.f ? 0.f : uu.x; uu.y = ee.y == 0.f ? 0.f : uu.y;
+      uu.z = ee.z == 0.f ? 0.f : uu.z; uu.w = ee.w == 0.f ? 0.f : uu.w;
+      *reinterpret_cast<float4*>(u + i) = uu;
+    } else {
+      for (int64_t k = i; k < n; ++k) u[k] = e[k] == 0.f ? 0.f : u[k];
+    }
+  }
+}
+
+void mc_mask(float* u, const float* e, int64_t n, hipStream_t st) {
+  if (n <= 0) return;
+  int64_t blocks = (n + SNT * 4 - 1) / (SNT * 4);
+  blocks = blocks > 2048 ? 2048 : blocks;
+  hipLaunchKernelGGL(k_mc_mask, dim3((unsigned)blocks), dim3(SNT), 0, st, u, e, n);
+}
+
 void sgd_step(const SgdArgs& a, hipStream_t st) {
   if (a.n_tasks == 0) return;
   const bool mom = a.momentum != 0.f;

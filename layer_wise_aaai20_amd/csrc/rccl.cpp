@@ -68,7 +68,23 @@ Tensor rccl_unique_id() {
   return out;
 }
 
-int64_t rccl_init(Tensor uid, int64_t world, int64_t rank, int64_t device) {
+// An RCCL call on a non-blocking communicator may return ncclInProgress: poll the communicator
+// state until the call has completed (or failed). Blocking communicators never return it.
+ncclResult_t settle(ncclComm_t comm, ncclResult_t r) {
+  while (r == ncclInProgress) {
+    std::this_thread::yield();
+    if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) return ncclInternalError;
+  }
+  return r;
+}
+
+// timeout_s > 0: the communicator is created non-blocking (ncclConfig_t.blocking = 0) and its
+// initialisation is polled against a deadline. A peer that never joins (a rank that failed
+// before reaching ncclCommInitRank, after the ranks agreed to create the communicator) would
+// otherwise block this rank inside the init forever; here the init is aborted with
+// ncclCommAbort and the call raises, so the rank reaches the fallback agreement
+// (parallel/comm.py _init_native_agreed). timeout_s <= 0: the blocking ncclCommInitRank.
+int64_t rccl_init(Tensor uid, int64_t world, int64_t rank, int64_t device, double timeout_s) {
   TORCH_CHECK(uid.device().is_cpu() && uid.scalar_type() == at::kByte &&
                   uid.numel() == NCCL_UNIQUE_ID_BYTES && uid.is_contiguous(),
               "rccl_init: uid must be a contiguous CPU uint8 tensor of ", NCCL_UNIQUE_ID_BYTES,
@@ -78,7 +94,29 @@ int64_t rccl_init(Tensor uid, int64_t world, int64_t rank, int64_t device) {
   ncclUniqueId id;
   std::memcpy(&id, uid.data_ptr(), NCCL_UNIQUE_ID_BYTES);
   ncclComm_t comm = nullptr;
-  check(ncclCommInitRank(&comm, (int)world, id, (int)rank), "ncclCommInitRank");
+  if (timeout_s <= 0) {
+    check(ncclCommInitRank(&comm, (int)world, id, (int)rank), "ncclCommInitRank");
+    return reinterpret_cast<int64_t>(comm);
+  }
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&comm, (int)world, id, (int)rank, &cfg);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress && comm != nullptr) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) r = ncclInternalError;
+    const double waited =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (r == ncclInProgress && waited > timeout_s) {
+      ncclCommAbort(comm);
+      TORCH_CHECK(false, "ncclCommInitRank: not complete after ", waited,
+                  " s (a peer rank never joined); communicator aborted");
+    }
+  }
+  if (r != ncclSuccess) {
+    if (comm != nullptr) ncclCommAbort(comm);
+    TORCH_CHECK(false, "RCCL ncclCommInitRankConfig failed: ", ncclGetErrorString(r));
+  }
   return reinterpret_cast<int64_t>(comm);
 }
 
@@ -101,8 +139,8 @@ void rccl_all_gather(int64_t h, Tensor send, Tensor recv) {
   check(ncclCommCount(comm_of(h), &n), "ncclCommCount");
   TORCH_CHECK(recv.numel() == send.numel() * n, "rccl_all_gather: recv must hold world * send");
   const c10::DeviceGuard guard(send.device());
-  check(ncclAllGather(send.data_ptr(), recv.data_ptr(), (size_t)send.numel(), dtype_of(send),
-                      comm_of(h), cur_stream()),
+  check(settle(comm_of(h), ncclAllGather(send.data_ptr(), recv.data_ptr(), (size_t)send.numel(),
+                                         dtype_of(send), comm_of(h), cur_stream())),
         "ncclAllGather");
 }
 
@@ -110,16 +148,16 @@ void rccl_all_reduce(int64_t h, Tensor t, int64_t op) {
   check_dev(t, "tensor");
   const c10::DeviceGuard guard(t.device());
   const ncclRedOp_t rop = op == 1 ? ncclMax : (op == 2 ? ncclMin : ncclSum);
-  check(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), rop,
-                      comm_of(h), cur_stream()),
+  check(settle(comm_of(h), ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(),
+                                         dtype_of(t), rop, comm_of(h), cur_stream())),
         "ncclAllReduce");
 }
 
 void rccl_broadcast(int64_t h, Tensor t, int64_t root) {
   check_dev(t, "tensor");
   const c10::DeviceGuard guard(t.device());
-  check(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), dtype_of(t), (int)root,
-                      comm_of(h), cur_stream()),
+  check(settle(comm_of(h), ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(),
+                                         dtype_of(t), (int)root, comm_of(h), cur_stream())),
         "ncclBroadcast");
 }
 
@@ -268,7 +306,8 @@ TORCH_LIBRARY_FRAGMENT(lwaaai, m) {
   m.def("rccl_watch_status(int watch) -> str", &rccl_watch_status);
   m.def("rccl_watch_stop(int watch) -> ()", &rccl_watch_stop);
   m.def("rccl_unique_id() -> Tensor", &rccl_unique_id);
-  m.def("rccl_init(Tensor uid, int world, int rank, int device) -> int", &rccl_init);
+  m.def("rccl_init(Tensor uid, int world, int rank, int device, float timeout_s) -> int",
+        &rccl_init);
   m.def("rccl_destroy(int comm) -> ()", &rccl_destroy);
   m.def("rccl_abort(int comm) -> ()", &rccl_abort);
   m.def("rccl_all_gather(int comm, Tensor send, Tensor(a!) recv) -> ()", &rccl_all_gather);

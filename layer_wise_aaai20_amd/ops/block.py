@@ -52,7 +52,7 @@ import torch.nn.functional as F
 
 from ._ext import h16, load
 from .conv import conv_dgrad, conv_fwd, conv_wgrad
-from .tuning import Tuner
+from .tuning import MF32, Tuner, with_mf32
 
 CL = torch.channels_last
 # materialise relu(bn1(c1)) / relu(bn2(c2)) with one apply pass instead of re-normalising in the
@@ -69,7 +69,7 @@ BSTATS = os.environ.get("LWAAAI_BSTATS", "0") == "1"
 # reduce + one dual apply pass (csrc bn.hip k_bn_reduce DUAL / k_bn_bwd_apply_dual) read them once
 # for both. LWAAAI_BN_DUAL=0: two separate BN backwards.
 BN_DUAL = os.environ.get("LWAAAI_BN_DUAL", "1") != "0"
-TILES = (1, 2, 3, 4, 5, 6)          # csrc GemmTile ids (0 = heuristic)
+TILES = with_mf32((1, 2, 3, 4, 5, 6))   # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
 BIG = (21, 22)                      # 256x256 / 256x128 8-wave LDS-DMA kernel (csrc/gemm_big.hip)
 # the same tiles as a persistent kernel (csrc/gemm_big.hip k_gemm_bigp: one workgroup per CU, the
@@ -94,6 +94,8 @@ def _splits(tiles: int, K: int) -> int:
 
 
 def _tile_dims(t: int) -> Tuple[int, int]:
+    if MF32 < t <= MF32 + 6:
+        t -= MF32
     return {1: (128, 128), 2: (128, 128), 3: (256, 64), 4: (64, 256), 5: (256, 64),
             6: (64, 64), 21: (256, 256), 22: (256, 128), 23: (256, 256), 24: (256, 128)}[t]
 

@@ -28,12 +28,14 @@ import torch.nn.functional as F
 from torch import nn
 
 from ._ext import h16, load
-from .tuning import Tuner
+from .tuning import MF32, Tuner, with_mf32
 
 CL = torch.channels_last
 CV_A, CV_A4, CV_B, CV_B4 = 1, 2, 3, 4
-ROW_TILES = (1, 2, 3, 5, 6)          # forward / dgrad (csrc GemmTile ids)
-COL_TILES = (1, 2, 4, 6)             # weight gradient
+# forward / dgrad and weight-gradient tiles (csrc GemmTile ids), each with its 32x32x16-MFMA twin
+# (id + 40, ops/block.py with_mf32)
+ROW_TILES = with_mf32((1, 2, 3, 5, 6))
+COL_TILES = with_mf32((1, 2, 4, 6))
 # 256x256 / 256x128 8-wave LDS-DMA tiles (csrc/gemm_big.hip, row gather): one stride-1 class,
 # C % 64 == 0 (a K-tile inside one tap), K-contiguous weight, no prologue / addend / statistics
 # of the backward; LWAAAI_CONV_BIG=0 leaves them out of the tuner's candidates
@@ -90,6 +92,7 @@ def tap_dgrad_weight(w: torch.Tensor) -> torch.Tensor:
 
 _TILE_DIMS = {1: (128, 128, 32), 2: (128, 128, 64), 3: (256, 64, 32), 4: (64, 256, 32),
               5: (256, 64, 64), 6: (64, 64, 64), 21: (256, 256, 64), 22: (256, 128, 64)}
+_TILE_DIMS.update({MF32 + t: _TILE_DIMS[t] for t in range(1, 7)})
 
 
 def _pair(v) -> Tuple[int, int]:

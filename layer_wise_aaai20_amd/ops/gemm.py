@@ -15,7 +15,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ._ext import h16, load
-from .tuning import Tuner
+from .tuning import Tuner, with_mf32
 
 
 def _splits(tiles: int, K: int) -> int:
@@ -25,6 +25,8 @@ def _splits(tiles: int, K: int) -> int:
 
 TILES = {"auto": 0, "128x128x32": 1, "128x128x64": 2, "256x64x32": 3, "64x256x32": 4,
          "256x64x64": 5, "64x64x64": 6, "256x256x64": 21, "256x128x64": 22}
+# the 32x32x16-MFMA twins of tiles 1..6 (csrc GemmTile id + 40), e.g. "128x128x64/mf32"
+TILES.update({f"{k}/mf32": v + 40 for k, v in list(TILES.items()) if 1 <= v <= 6})
 
 
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, bias=None, relu=False, splits=1, out_bf16=True):
@@ -48,7 +50,7 @@ class LinearTuner(Tuner):
     M (batch 256-512) and span K = 1k-25k, so the right tile and split count differ per layer and
     pass (``profiles/r2_linear_vs_blas*.log``)."""
 
-    TILES = (1, 2, 3, 4, 5, 6)
+    TILES = with_mf32((1, 2, 3, 4, 5, 6))
     BIG = (21, 22)                    # 8-wave LDS-DMA tiles: K-/K-, K-/N- or M-/N-contiguous operands
     SPLITS = (1, 2, 4, 8, 16)
 

@@ -45,6 +45,17 @@ if _READ and os.path.exists(_READ):
 
 _AGREE: list = []          # stack of (process group, device) set by rank_agreement()
 
+# The GEMM tiles 1..6 also exist on v_mfma_f32_32x32x16 (csrc GemmTile id + 40: gemm_core.h k_gemm
+# MF = 32); every tuner times them as further candidates. LWAAAI_MF32=0 leaves them out.
+MF32 = 40
+MF32_ON = os.environ.get("LWAAAI_MF32", "1") != "0"
+
+
+def with_mf32(tiles) -> tuple:
+    """``tiles`` plus the 32x32x16-MFMA twins of those among ids 1..6, when enabled."""
+    tiles = tuple(tiles)
+    return tiles + (tuple(MF32 + t for t in tiles if 1 <= t <= 6) if MF32_ON else ())
+
 
 @contextlib.contextmanager
 def rank_agreement(group=None, device=None):

@@ -139,7 +139,12 @@ class NativeRccl:
             uid = self.lib.rccl_unique_id() if self.rank == 0 else \
                 torch.zeros(128, dtype=torch.uint8)
             uid = _bcast_uid(uid, group, dev)
-        self.handle = int(self.lib.rccl_init(uid, self.world, self.rank, dev.index or 0))
+        if os.environ.get("LWAAAI_FAKE_NATIVE_INIT_FAIL", "") == str(self.rank):
+            # test hook: this rank fails BEFORE joining ncclCommInitRank, so its peers are left
+            # waiting inside their (non-blocking) init until the deadline aborts it
+            raise RuntimeError("injected native init failure (LWAAAI_FAKE_NATIVE_INIT_FAIL)")
+        self.handle = int(self.lib.rccl_init(uid, self.world, self.rank, dev.index or 0,
+                                             init_timeout()))
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
         self.lib.rccl_all_gather(self.handle, inp, out)
@@ -239,12 +244,31 @@ def native_rccl(group=None, device=None) -> Optional[NativeRccl]:
     return _NATIVE[key]
 
 
+def init_timeout() -> float:
+    """Deadline (s) on ``ncclCommInitRank`` (``LWAAAI_RCCL_INIT_TIMEOUT``, default 300; 0 = the
+    blocking init with no deadline)."""
+    return float(os.environ.get("LWAAAI_RCCL_INIT_TIMEOUT", "300"))
+
+
 def _init_native_agreed(group, device) -> Optional[NativeRccl]:
-    """Create the native communicator as one collective decision: every rank first checks that it
-    can (extension loaded, unique id obtained), the ranks agree, and only then do they all enter
-    ``ncclCommInitRank``; a rank whose init then fails makes every rank drop its communicator.
-    On a no, all ranks fall back to the c10d collectives (eager steps at world > 1) instead of
-    some ranks waiting in an init that one of them never joins."""
+    """Create the native communicator as one collective decision.
+
+    1. Every rank checks that it can (extension loaded, unique id obtained) and the ranks agree
+       (an all-reduce over the c10d group); on a no, nobody enters the RCCL init.
+    2. Every rank enters ``ncclCommInitRank`` on a *non-blocking* communicator whose init is
+       polled against a deadline (``LWAAAI_RCCL_INIT_TIMEOUT``, ``csrc/rccl.cpp rccl_init``), then
+       validates it with a probe all-reduce. A rank that raises anywhere in this block — before
+       it reached the init, inside it, or at the probe — goes straight to step 3. Its peers are
+       then waiting inside an init (or a probe on a half-built communicator) that cannot
+       complete: the init deadline aborts their communicator and they raise as well.
+    3. The ranks agree again; if any rank has no communicator, every rank closes its own and all
+       fall back to the c10d collectives (eager steps at world > 1), instead of some ranks
+       waiting in a collective the others never join.
+
+    What is not covered: a peer that hangs (rather than raises) after the init succeeded
+    everywhere leaves the probe blocked; the step watchdog does not run yet at that point. With
+    ``LWAAAI_RCCL_INIT_TIMEOUT=0`` the init is the blocking call and step 2's guarantee only
+    holds for failures after every rank has finished it."""
     uid = torch.zeros(128, dtype=torch.uint8)
     try:
         from ..ops._ext import load_main as load
@@ -270,10 +294,9 @@ def _init_native_agreed(group, device) -> Optional[NativeRccl]:
         comm.all_reduce(probe)
         if int(probe.item()) != comm.world:
             raise RuntimeError(f"probe all-reduce gave {probe.item()}, expected {comm.world}")
-        if os.environ.get("LWAAAI_FAKE_NATIVE_INIT_FAIL", "") == str(rank(group)):
-            raise RuntimeError("injected native init failure (LWAAAI_FAKE_NATIVE_INIT_FAIL)")
     except Exception as e:                     # noqa: BLE001
         err = e
+        print(f"[lwaaai] native RCCL init failed on rank {rank(group)}: {e}", flush=True)
         if comm is not None:
             comm.close()
             comm = None

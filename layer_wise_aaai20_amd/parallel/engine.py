@@ -100,12 +100,20 @@ class GradSyncEngine:
             if self.rank == 0:
                 print(f"[lwaaai] warning: {msg}", flush=True)
         # DGC-style momentum correction (opt-in, Lin et al. 2018; profiles/r4/ef_root_cause.md):
-        # each rank accumulates its velocity u = m·u + g locally and the error-feedback residual
-        # accumulates u instead of g; the coordinates that were sent have their velocity zeroed
-        # (momentum factor masking). The optimizer then runs WITHOUT momentum (the trainers
-        # switch it off). Needs error feedback.
+        # each rank accumulates its velocity u = m·u + (g + wd·p) locally and the error-feedback
+        # residual accumulates u instead of g; the coordinates that were sent have their velocity
+        # zeroed (momentum factor masking), except in tensors that were sent whole (dense_below,
+        # or every element kept): those keep ordinary momentum. Weight decay enters the gradient
+        # BEFORE the velocity, as in DGC (set_mc_weight_decay; the optimizer then runs without
+        # momentum and without weight decay — the trainers switch both off). One kernel does the
+        # prologue (csrc/optim.hip k_mc_prep); the masking runs inside the select kernels
+        # (csrc/compress.hip, SelectArgs::mom) or, for codecs without a selection, in k_mc_mask.
+        # Needs error feedback.
         self.mc = float(momentum_correction or 0.0)
         self.mom = None
+        self._mc_wd = None                # per arena segment (device fp32) or None
+        self._mc_wmul = 1.0
+        self._mc_plans = {}
         if self.mc > 0:
             if self.ef is None:
                 raise ValueError("momentum correction needs error_feedback=True")
@@ -218,6 +226,55 @@ class GradSyncEngine:
                 f"{mine.tolist()} vs min {lo.tolist()} / max {hi.tolist()}): the model, the "
                 f"compression settings or the bucket size are not identical on every rank")
 
+    def set_mc_weight_decay(self, opt) -> None:
+        """Momentum correction: take the weight decay of ``opt`` (a :class:`FlatSGD` over this
+        engine's arena) into the velocity update, ``u = mc·u + g + wd·p`` per segment with each
+        param group's decay (so ``--no-bn-wd`` still holds), and set the optimizer's groups to no
+        decay. Without it, decay applied by the optimizer after the exchange never enters u and
+        acts ~1/(1-mc) times weaker than in the momentum-SGD baseline."""
+        if self.mom is None:
+            raise RuntimeError("set_mc_weight_decay: momentum correction is off")
+        if self.arena.param_buf is None:
+            raise RuntimeError("set_mc_weight_decay: the arena has no flat parameter buffer")
+        wd = opt._seg_wd(self.device).clone()
+        self._mc_wd = wd if bool((wd != 0).any()) else None
+        self._mc_wmul = 1.0 / float(getattr(opt, "grad_scale", 1.0) or 1.0)
+        for g in opt.param_groups:
+            g["weight_decay"] = 0.0
+        self._mc_plans = {}
+
+    def _mc_plan(self, bi: int):
+        """The bucket's arena segments (a plan of its own: in entire-model mode the codec sees
+        one segment, but weight decay is per parameter) and their weight decays."""
+        if bi not in self._mc_plans:
+            b = self.buckets[bi]
+            segs = self.arena.segments[b.seg_lo:b.seg_hi]
+            plan = SegPlan([s.offset - b.start for s in segs], [s.numel for s in segs])
+            wd = self._mc_wd[b.seg_lo:b.seg_hi].contiguous() if self._mc_wd is not None else None
+            self._mc_plans[bi] = (plan, wd)
+        return self._mc_plans[bi]
+
+    def _mc_prologue(self, bi: int, g: torch.Tensor, u: torch.Tensor) -> None:
+        """g' = g + wd·p/grad_scale ; u = mc·u + g' ; g = u over bucket ``bi``."""
+        from ..ops._ext import ops_for
+        b = self.buckets[bi]
+        plan, wd = self._mc_plan(bi)
+        p = self.arena.param_buf[b.start:b.end] if wd is not None else None
+        lib = ops_for(g)
+        if lib is not None:
+            t = plan.all_large_tables(g.device)
+            lib.mc_prep(g, u, p, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], wd, self.mc,
+                        self._mc_wmul)
+            return
+        for i in range(plan.S):                  # (segments may be padded apart: align 64)
+            o, n = int(plan.offsets[i]), int(plan.sizes[i])
+            if wd is not None and float(wd[i]) != 0.0:       # (product, then sum: the kernel's
+                w32 = torch.tensor(float(wd[i]), dtype=torch.float32) * \
+                    torch.tensor(self._mc_wmul, dtype=torch.float32)   # roundings)
+                g[o:o + n].add_(p[o:o + n] * w32)
+            u[o:o + n].mul_(self.mc).add_(g[o:o + n])
+            g[o:o + n].copy_(u[o:o + n])
+
     def use_communicator(self, native) -> None:
         """Route the bucket collectives through ``native`` (a :class:`~.comm.NativeRccl`-like
         object: stream-ordered ``all_gather(out, inp)`` / ``all_reduce(t)`` / ``broadcast``),
@@ -312,13 +369,16 @@ class GradSyncEngine:
             if self.lr_scaled:
                 e.mul_(self._lr_ratio)                   # residual re-expressed at this step's LR
             u = None
+            sel = codec.inner if isinstance(codec, DenseWrap) else codec
             if self.mom is not None:
                 u = self.mom[b.start:b.end]
-                u.mul_(self.mc).add_(g)                  # local velocity
-                g.copy_(u)                               # the residual accumulates velocity
+                self._mc_prologue(bi, g, u)              # velocity; the residual accumulates it
+                sel.mc_mom = u                           # masked by the select kernels
             send = codec.compress(g, e, self.step)
             if u is not None:
-                u.mul_(e != 0)                           # momentum factor masking: sent -> 0
+                sel.mc_mom = None
+                if not getattr(sel, "mc_fused", False):  # no selection: sent <=> residual 0
+                    self._mc_mask(u, e)
             t1 = self._event() if self.timing else None
             self._payload += codec.last_payload_bytes
             if codec.collective == "all_reduce":
@@ -340,6 +400,15 @@ class GradSyncEngine:
                 done = torch.cuda.Event()
                 done.record(side)
         self._pending.append((bi, work, send, recv, (t0, t1, tx), done, ready))
+
+    @staticmethod
+    def _mc_mask(u: torch.Tensor, e: torch.Tensor) -> None:
+        from ..ops._ext import ops_for
+        lib = ops_for(u)
+        if lib is not None:
+            lib.mc_mask(u, e)
+        else:
+            u.mul_(e != 0)
 
     def finish(self) -> None:
         """Launch buckets that never became ready (unused params keep zero grads), wait for every

@@ -30,8 +30,15 @@ class PeerSim:
     """The W-1 simulated peers of one engine: per-peer codecs (built for the peer's rank), peer
     error-feedback residuals and a fixed stored gradient arena per peer."""
 
-    def __init__(self, engine, peer_grads: Sequence[torch.Tensor], rank: int = 0):
+    def __init__(self, engine, peer_grads: Sequence[torch.Tensor], rank: int = 0,
+                 frozen: bool = False):
         self.engine = engine
+        # frozen (timing runs, bench.py --simulate-world): each bucket's peer payloads are
+        # compressed once and replayed; a step then costs this rank what it costs a real rank —
+        # its own compression, the received bytes landing in memory, the W-rank decode — without
+        # the W-1 peers' compressions a real node runs on the other GPUs
+        self.frozen = bool(frozen)
+        self._frozen = {}
         self.world = engine.world
         self.rank = rank
         self.peers = [r for r in range(self.world) if r != rank]
@@ -75,6 +82,8 @@ class PeerSim:
 
     def payloads(self, bi: int) -> List[torch.Tensor]:
         """Every peer's payload for bucket ``bi`` this step (stream-ordered, capturable)."""
+        if self.frozen and bi in self._frozen:
+            return self._frozen[bi]
         b = self.engine.buckets[bi]
         out = []
         for j, r in enumerate(self.peers):
@@ -82,6 +91,9 @@ class PeerSim:
             g.copy_(self.grads[j][b.start:b.end])       # compressors fold EF into g in place
             e = self.ef[j][b.start:b.end] if self.ef[j] is not None else None
             out.append(self.codecs[j][bi].compress(g, e, self.engine.step))
+        if self.frozen:
+            out = [t.clone() for t in out]
+            self._frozen[bi] = out
         return out
 
 
@@ -128,10 +140,11 @@ class LoopbackRccl:
 
 
 def attach_loopback(engine, peer_grads: Sequence[torch.Tensor],
-                    rank: int = 0) -> LoopbackRccl:
+                    rank: int = 0, frozen: bool = False) -> LoopbackRccl:
     """Give ``engine`` (built with ``world_size=W``) a loopback communicator whose W-1 peers
-    compress ``peer_grads`` (one arena-sized fp32 tensor per peer) every step."""
-    lb = LoopbackRccl(PeerSim(engine, peer_grads, rank))
+    compress ``peer_grads`` (one arena-sized fp32 tensor per peer) every step (``frozen``: once,
+    then their payloads are replayed — for timing)."""
+    lb = LoopbackRccl(PeerSim(engine, peer_grads, rank, frozen))
     engine.use_communicator(lb)
     return lb
 

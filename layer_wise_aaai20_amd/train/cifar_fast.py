@@ -30,7 +30,7 @@ class CifarTrainer:
                  momentum=0.9, dtype=torch.bfloat16, bucket_cap_mb=25.0, wire="auto",
                  n_train=50000, seed=0, fused=True, graph=None, n_test=1000,
                  task="textures", amp=None, dense_below=0, momentum_correction=False,
-                 lr_scale=1.0, ef_lr_scaled=False):
+                 lr_scale=1.0, ef_lr_scaled=False, world_size=None):
         self.device = torch.device(device or "cuda")
         self.dtype = dtype
         self.bs = batch_size
@@ -54,10 +54,12 @@ class CifarTrainer:
                                  qstates=qstates, error_feedback=error_feedback,
                                  bucket_cap_mb=bucket_cap_mb, wire=wire, flat_params=True,
                                  dense_below=dense_below, momentum_correction=mc,
-                                 ef_lr_scaled=ef_lr_scaled)
+                                 ef_lr_scaled=ef_lr_scaled, world_size=world_size)
         om = 0.0 if mc > 0 else momentum
         self.opt = FlatSGD(net.parameters(), self.ddp.arena, lr=0.0, momentum=om,
                            nesterov=om > 0, weight_decay=5e-4 * batch_size)
+        if mc > 0:           # weight decay enters the velocity (and leaves the optimizer)
+            self.ddp.engine.set_mc_weight_decay(self.opt)
         if ef_lr_scaled:
             self.ddp.engine.lr_source = self.opt.lr_device
         ds = D.synthetic_cifar10(n_train, n_test, seed, task=task, amp=amp)

@@ -124,7 +124,9 @@ class StepGraph:
                 if os.environ.get("LWAAAI_FAKE_CAPTURE_FAIL", "") == str(self._rank()):
                     raise RuntimeError("injected capture failure (LWAAAI_FAKE_CAPTURE_FAIL)")
                 g = self._capture(inputs, sig)
-            except RuntimeError as e:          # capture unsupported here
+            except Exception as e:             # noqa: BLE001 — any failure joins the agreement
+                # (a rank that skipped _agree would leave its peers blocked in it until the
+                # process group times out; every rank falls back to eager instead)
                 err = e
             # one decision for all ranks: a rank replaying while another runs eagerly would
             # still pair its collectives, but the whole job would then run at the slow mode

@@ -149,5 +149,7 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
     om = 0.0 if mc > 0 else momentum
     opt = FlatSGD(groups, ddp.arena, lr=lr, momentum=om, nesterov=om > 0,
                   weight_decay=weight_decay, grad_scale=1.0 / float(loss_scale))
+    if mc > 0:               # weight decay enters the velocity (and leaves the optimizer)
+        ddp.engine.set_mc_weight_decay(opt)
     return ImageNetTrainer(ddp, opt, device, tdtype, graph=graph, graph_warmup=graph_warmup,
                            graph_auto=graph_auto, loss_scale=loss_scale)

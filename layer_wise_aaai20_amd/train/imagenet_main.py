@@ -615,6 +615,8 @@ def main(argv=None):
         optimizer = FlatSGD(groups, model.arena, lr=0.0, momentum=om,
                             nesterov=om > 0, weight_decay=args.weight_decay,
                             grad_scale=1.0 / args.loss_scale if args.fp16 else 1.0)
+        if mc > 0 and getattr(model, "engine", None) is not None:
+            model.engine.set_mc_weight_decay(optimizer)   # decay enters the velocity
     elif args.fp16:
         master = fp16util.prep_param_lists(model)
         opt_params = _bn_groups(base_model, None, args.weight_decay) if args.no_bn_wd else None

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${1:-step}; shift
 mkdir -p gpurun_out /tmp/prof
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/prof/$TAG -o run --output-format csv \
-  -- python bench.py --steps 6 --warmup 6 "$@" > gpurun_out/${TAG}_bench.log 2>&1 || exit $?
+  -- python bench.py --steps 6 --warmup 6 --acc-steps 0 "$@" > gpurun_out/${TAG}_bench.log 2>&1 || exit $?
 KT=$(find /tmp/prof/$TAG -name '*kernel_trace.csv' | head -1)
 ST=$(find /tmp/prof/$TAG -name '*kernel_stats.csv' | head -1)
 cp "$ST" gpurun_out/${TAG}_kernel_stats.csv

@@ -231,6 +231,17 @@ def test_dense_below_sends_small_tensors_whole():
     assert r.keep.tolist()[0] == 64
 
 
+def _mc_expect(eng, u, sent):
+    """Momentum factor masking: u at the sent coordinates -> 0, unless the segment went whole."""
+    out = u.clone()
+    for s in eng.arena.segments:
+        sl = slice(s.offset, s.offset + s.numel)
+        m = sent[sl] != 0
+        if int(m.sum()) < s.numel:
+            out[sl][m] = 0
+    return out
+
+
 def test_momentum_correction_accumulates_velocity_and_masks():
     """DGC momentum correction: u = m·u + g; the residual accumulates u; sent coordinates have
     their velocity zeroed; decoded + e_new == e_old + u (what was sent is exactly removed)."""
@@ -249,8 +260,8 @@ def test_momentum_correction_accumulates_velocity_and_masks():
         u_expect = 0.9 * u_prev + g
         sent = eng.arena.grad                                     # world 1: decoded = sent
         torch.testing.assert_close(sent + eng.ef, e_old + u_expect, rtol=1e-5, atol=1e-6)
-        # velocity zeroed exactly where something was sent (residual zeroed)
-        torch.testing.assert_close(eng.mom, u_expect * (eng.ef != 0), rtol=0, atol=0)
+        # velocity zeroed exactly where something was sent, except in a segment sent whole
+        torch.testing.assert_close(eng.mom, _mc_expect(eng, u_expect, sent), rtol=0, atol=0)
         u_prev = eng.mom.clone()
     with pytest.raises(ValueError):
         GradSyncEngine(list(net.named_parameters()), mode="layerwise", method="Topk", K=0.05,
@@ -283,3 +294,61 @@ def test_lr_scaled_residual_rescales_by_lr_ratio():
     with pytest.raises(ValueError):
         GradSyncEngine(list(net.named_parameters()), mode="layerwise", method="Topk", K=0.05,
                        error_feedback=False, ef_lr_scaled=True)
+
+
+def test_momentum_correction_dense_segments_keep_ordinary_momentum():
+    """a tensor that travels whole (dense_below) keeps u = m·u + g every step (its
+    velocity is never reset), so under MC it trains with ordinary momentum; the compressed ones
+    are masked where sent."""
+    torch.manual_seed(1)
+    net = small_net()
+    eng = GradSyncEngine(list(net.named_parameters()), mode="layerwise", method="Topk", K=0.05,
+                         error_feedback=True, momentum_correction=0.9, dense_below=64)
+    small = [s for s in eng.arena.segments if s.numel <= 64]
+    assert small, "small_net has tensors under the dense_below bound"
+    u = torch.zeros(eng.arena.numel)
+    for _ in range(3):
+        g = torch.zeros(eng.arena.numel)
+        for s in eng.arena.segments:
+            g[s.offset:s.offset + s.numel] = torch.randn(s.numel)
+        eng.arena.grad.copy_(g)
+        eng.sync_now()
+        u = 0.9 * u + g
+        for s in small:
+            sl = slice(s.offset, s.offset + s.numel)
+            torch.testing.assert_close(eng.mom[sl], u[sl], rtol=1e-6, atol=1e-7)
+            torch.testing.assert_close(eng.arena.grad[sl], u[sl], rtol=1e-6, atol=1e-7)
+        u = eng.mom.clone()
+
+
+@pytest.mark.parametrize("mode", ["layerwise", "entiremodel"])
+def test_momentum_correction_folds_weight_decay_per_group(mode):
+    """with MC the weight decay enters the gradient before the velocity,
+    u = m·u + g + wd·p with each param group's wd (no_bn_wd groups stay at 0), and the optimizer
+    then applies none (its groups are set to 0); the loss-scaled gradient gets wd·p/grad_scale."""
+    from layer_wise_aaai20_amd.optim.flat_sgd import FlatSGD
+    torch.manual_seed(2)
+    net = small_net()
+    eng = GradSyncEngine(list(net.named_parameters()), mode=mode, method="Topk", K=0.05,
+                         error_feedback=True, momentum_correction=0.9, flat_params=True)
+    params = [p for p in net.parameters()]
+    groups = [{"params": params[:1], "weight_decay": 0.0},
+              {"params": params[1:], "weight_decay": 1e-2}]
+    opt = FlatSGD(groups, eng.arena, lr=0.1, momentum=0.0, weight_decay=1e-2, grad_scale=0.5)
+    eng.set_mc_weight_decay(opt)
+    assert all(g["weight_decay"] == 0.0 for g in opt.param_groups)
+    wd = torch.zeros(eng.arena.numel)
+    assert sum(s.param is params[0] for s in eng.arena.segments) == 1
+    for s in eng.arena.segments:
+        if s.param is not params[0]:
+            wd[s.offset:s.offset + s.numel] = 1e-2
+    p = eng.arena.param_buf.clone()
+    g = torch.zeros(eng.arena.numel)
+    for s in eng.arena.segments:                 # (layer-wise segments are padded apart)
+        g[s.offset:s.offset + s.numel] = torch.randn(s.numel)
+    e_old = eng.ef.clone()
+    eng.arena.grad.copy_(g)
+    eng.sync_now()
+    u = g + wd * p / 0.5
+    torch.testing.assert_close(eng.arena.grad + eng.ef, e_old + u, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(eng.mom, _mc_expect(eng, u, eng.arena.grad), rtol=1e-6, atol=1e-7)

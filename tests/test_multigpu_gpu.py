@@ -91,6 +91,9 @@ def test_capture_failure_is_a_collective_decision():
 
 @need2
 def test_native_init_failure_falls_back_everywhere():
-    res = run_world(native_init_fallback, 2, env={"LWAAAI_FAKE_NATIVE_INIT_FAIL": "1"})
+    # rank 1 fails before it joins ncclCommInitRank: rank 0's non-blocking init must hit its
+    # deadline, abort, and both ranks then agree on the c10d fallback (no hang)
+    res = run_world(native_init_fallback, 2, env={"LWAAAI_FAKE_NATIVE_INIT_FAIL": "1",
+                                                  "LWAAAI_RCCL_INIT_TIMEOUT": "20"})
     for native, same in res:
         assert not native and same

@@ -178,3 +178,14 @@ def test_env_local_rank(monkeypatch):
     monkeypatch.setenv("LOCAL_RANK", "2")
     assert comm.env_local_rank() == 2
     assert comm.bind_rank_device(5).type == "cpu"        # no GPU in this container
+
+
+def test_ddp_rejects_single_process_multi_gpu():
+    """Deliberate deviation (PARITY.md row 39): one process per GPU; the reference DDP's
+    single-process replicate/scatter/gather mode (IMAGENET/training/ddp.py:207-219) is refused."""
+    from torch import nn
+    from layer_wise_aaai20_amd.parallel.ddp import DistributedDataParallel
+    with pytest.raises(RuntimeError, match="one process per GPU"):
+        DistributedDataParallel(nn.Linear(4, 4), device_ids=[0, 1])
+    m = DistributedDataParallel(nn.Linear(4, 4), device_ids=[0])     # one device: fine
+    assert m.engine.world == 1

@@ -73,6 +73,12 @@ class Codec:
     # with mc_fused zeroes it at the coordinates it selected (segments not sent whole only)
     mc_mom = None
     mc_fused = False
+    # entire-model staging (GradSyncEngine): codecs with `stage` run their first pass per arena
+    # slice during backward; `_staged` tells compress() that pass is done for this step
+    _staged = False
+
+    def can_stage(self) -> bool:
+        return False
 
     def __init__(self, plan: SegPlan, world: int, rank: int, seed: int = 0,
                  error_feedback: bool = False):
@@ -168,6 +174,24 @@ class TopkCodec(Codec):
                                         device=device)
         return self._send[k]
 
+    def can_stage(self) -> bool:
+        """One large segment (entire-model mode): its radix pass 0 can run per task range."""
+        small, large = self.plan.split(SMALL_MAX)
+        return self.plan.S == 1 and len(large) == 1
+
+    def stage(self, grad, ef, step, t_lo: int, t_hi: int, first: bool) -> None:
+        """Radix pass 0 (+ the error-feedback fold for Top-K) over tasks [t_lo, t_hi) of the one
+        segment; ``first`` zeroes the histograms (csrc/compress.hip select_stage)."""
+        lib = ops_for(grad)
+        if lib is None:
+            return                      # (the CPU mirror does everything in compress)
+        t = self._dev_tables(grad.device)
+        lib.select_stage(grad, ef, t["seg_off"], t["seg_n"], t["keep"], t["cap_off"],
+                         t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
+                         self._workspace(grad.device, lib), self.km, int(t_lo), int(t_hi),
+                         bool(first), self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
+                         self.step_t)
+
     def compress(self, grad, ef, step):
         lib = ops_for(grad)
         out = self.send_buffer(grad.device)
@@ -178,7 +202,7 @@ class TopkCodec(Codec):
                                 t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
                                 self._workspace(grad.device, lib), self.km, OUT_PAIRS, out, None,
                                 None, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
-                                self.step_t, self.overflow, self.mc_mom)
+                                self.step_t, self.overflow, self.mc_mom, self._staged)
             return out
         self._compress_cpu(grad, ef, step, out)
         return out
@@ -307,7 +331,7 @@ class RandkCodec(RandkSparseCodec):
                                 t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
                                 self._workspace(grad.device, lib), KM_RANDK, OUT_VALIDX, None,
                                 vals, idx, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
-                                self.step_t, None, self.mc_mom)
+                                self.step_t, None, self.mc_mom, self._staged)
             return vals
         for s, x in self._segs(grad):
             o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])
@@ -358,6 +382,9 @@ class ThresholdCodec(TopkCodec):
     name = "threshold"
     km = KM_THRESH
     mc_fused = False               # (the engine masks the velocity where the residual is 0)
+
+    def can_stage(self) -> bool:
+        return False
 
     def __init__(self, plan, world, rank, V=None, adaptive=False, seed=0, error_feedback=False,
                  count_exchange=None, max_density=None):
@@ -520,6 +547,26 @@ class _QuantCodec(Codec):
             self._send[k] = torch.zeros(self.words, dtype=torch.int32, device=device)
         return self._send[k]
 
+    def _qws(self, grad, lib, t):
+        k = str(grad.device)
+        if k not in self._ws:
+            nb = lib.workspace_bytes(0, self.plan.S, int(t["tasks"].shape[0]))
+            self._ws[k] = _ws_tensor(nb, grad.device)
+        return self._ws[k]
+
+    def can_stage(self) -> bool:
+        return self.plan.S == 1
+
+    def stage(self, grad, ef, step, t_lo: int, t_hi: int, first: bool) -> None:
+        """The per-task (abs-max, sum of squares) partials with the error-feedback fold over
+        tasks [t_lo, t_hi) of the one segment (csrc/compress.hip quant_stage)."""
+        lib = ops_for(grad)
+        if lib is None:
+            return
+        t = self.plan.all_large_tables(grad.device)
+        lib.quant_stage(grad, ef, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], t["task_lo"],
+                        t["rec_off"], self._qws(grad, lib, t), self.qstates, int(t_lo), int(t_hi))
+
     def compress(self, grad, ef, step):
         lib = ops_for(grad)
         out = self.send_buffer(grad.device)
@@ -527,13 +574,10 @@ class _QuantCodec(Codec):
         tag = self.tag | (self.rank & 0xFFFFFF)
         if lib is not None:
             t = self.plan.all_large_tables(grad.device)
-            k = str(grad.device)
-            if k not in self._ws:
-                nb = lib.workspace_bytes(0, self.plan.S, int(t["tasks"].shape[0]))
-                self._ws[k] = _ws_tensor(nb, grad.device)
             lib.quantize(grad, ef, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], t["task_lo"],
-                         t["rec_off"], self._ws[k], out, self.q, self.qstates, self.plan.gid_base,
-                         int(step) & 0xFFFFFFFF, tag, self.seed, self.step_t)
+                         t["rec_off"], self._qws(grad, lib, t), out, self.q, self.qstates,
+                         self.plan.gid_base, int(step) & 0xFFFFFFFF, tag, self.seed, self.step_t,
+                         self._staged)
             return out
         self._quant_cpu(grad, ef, step, out, tag)
         return out

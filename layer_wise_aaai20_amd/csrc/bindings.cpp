@@ -167,7 +167,7 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
                      c10::optional<Tensor> pairs, c10::optional<Tensor> vals,
                      c10::optional<Tensor> idx, int64_t gid_base, int64_t step, int64_t seed,
                      c10::optional<Tensor> step_t, c10::optional<Tensor> overflow,
-                     c10::optional<Tensor> mom) {
+                     c10::optional<Tensor> mom, bool staged) {
   const c10::DeviceGuard guard(g.device());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, keep, cap_off, small_segs, large_segs,
                                       tasks, task_lo, ws);
@@ -188,8 +188,27 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
   a.overflow = overflow_ptr(overflow);
   a.seed0 = (uint32_t)(seed & 0xffffffff);
   a.seed1 = (uint32_t)((uint64_t)seed >> 32);
-  lw::select_compress(a, (int)km, (int)out, a.ef != nullptr, cur_stream());
+  lw::select_compress(a, (int)km, (int)out, a.ef != nullptr, cur_stream(), staged);
   launched("select_compress");
+}
+
+// entire-model staging (compress.hip select_stage): pass 0 over tasks [t_lo, t_hi)
+void select_stage(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, Tensor keep,
+                  Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks,
+                  Tensor task_lo, Tensor ws, int64_t km, int64_t t_lo, int64_t t_hi, bool zero,
+                  int64_t gid_base, int64_t step, int64_t seed, c10::optional<Tensor> step_t) {
+  const c10::DeviceGuard guard(g.device());
+  lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, keep, cap_off, small_segs, large_segs,
+                                      tasks, task_lo, ws);
+  TORCH_CHECK(0 <= t_lo && t_lo <= t_hi && t_hi <= a.n_tasks, "select_stage: task range");
+  TORCH_CHECK(km == lw::KM_TOPK || km == lw::KM_RANDK, "select_stage: Top-K / Random-K");
+  a.gid_base = (uint32_t)gid_base;
+  a.step = (uint32_t)step;
+  a.step_ptr = step_ptr(step_t);
+  a.seed0 = (uint32_t)(seed & 0xffffffff);
+  a.seed1 = (uint32_t)((uint64_t)seed >> 32);
+  lw::select_stage(a, (int)km, a.ef != nullptr, (int)t_lo, (int)t_hi, zero, cur_stream());
+  launched("select_stage");
 }
 
 void thresh_count(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n,
@@ -289,7 +308,7 @@ lw::QuantArgs make_quant_args(const Tensor& g, const c10::optional<Tensor>& ef,
 void quantize(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, Tensor segs,
               Tensor tasks, Tensor task_lo, Tensor rec_off, Tensor ws, Tensor payload, int64_t q,
               int64_t qstates, int64_t gid_base, int64_t step, int64_t tag, int64_t seed,
-              c10::optional<Tensor> step_t) {
+              c10::optional<Tensor> step_t, bool staged) {
   const c10::DeviceGuard guard(g.device());
   lw::QuantArgs a = make_quant_args(g, ef, seg_off, seg_n, segs, tasks, task_lo, rec_off, qstates);
   check_cuda(payload, "payload");
@@ -306,11 +325,26 @@ void quantize(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, 
   a.seed0 = (uint32_t)(seed & 0xffffffff);
   a.seed1 = (uint32_t)((uint64_t)seed >> 32);
   lw::seg_reduce(a, a.ef != nullptr, q == lw::Q_TERN ? 0 : 1, a.scale,
-                 reinterpret_cast<float2*>(base + L.partial), cur_stream());
+                 reinterpret_cast<float2*>(base + L.partial), cur_stream(), staged);
   launched("seg_reduce");
   // after seg_reduce the EF add is already folded into g (g' = g + e)
   lw::quantize(a, (int)q, a.ef != nullptr, cur_stream());
   launched("quantize");
+}
+
+// entire-model staging of the quantisers (compress.hip quant_stage)
+void quant_stage(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg_n, Tensor segs,
+                 Tensor tasks, Tensor task_lo, Tensor rec_off, Tensor ws, int64_t qstates,
+                 int64_t t_lo, int64_t t_hi) {
+  const c10::DeviceGuard guard(g.device());
+  lw::QuantArgs a = make_quant_args(g, ef, seg_off, seg_n, segs, tasks, task_lo, rec_off, qstates);
+  TORCH_CHECK(0 <= t_lo && t_lo <= t_hi && t_hi <= a.n_tasks, "quant_stage: task range");
+  const WsLayout L = layout(0, a.nseg, a.n_tasks);
+  TORCH_CHECK(ws.numel() >= L.total, "workspace too small");
+  uint8_t* base = ptr<uint8_t>(ws);
+  lw::quant_stage(a, a.ef != nullptr, (int)t_lo, (int)t_hi,
+                  reinterpret_cast<float2*>(base + L.partial), cur_stream());
+  launched("quant_stage");
 }
 
 void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor seg_n,
@@ -1650,7 +1684,16 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
       "Tensor(c!) ws, int km, int out, Tensor(d!)? pairs, Tensor(e!)? vals, Tensor(f!)? idx, "
       "int gid_base, int step, int seed, Tensor? step_t=None, Tensor(g!)? overflow=None, "
-      "Tensor(h!)? mom=None) -> ()");
+      "Tensor(h!)? mom=None, bool staged=False) -> ()");
+  m.def(
+      "select_stage(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor keep, "
+      "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
+      "Tensor(c!) ws, int km, int t_lo, int t_hi, bool zero, int gid_base, int step, int seed, "
+      "Tensor? step_t=None) -> ()");
+  m.def(
+      "quant_stage(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor segs, "
+      "Tensor tasks, Tensor task_lo, Tensor rec_off, Tensor(c!) ws, int qstates, int t_lo, "
+      "int t_hi) -> ()");
   m.def(
       "thresh_count(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor large_segs, "
       "Tensor tasks, Tensor task_lo, Tensor(c!) ws, float V, int adaptive, Tensor(d!) counts_out) "
@@ -1671,7 +1714,8 @@ LW_LIBRARY(LW_OPS_NS, m) {
   m.def(
       "quantize(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor segs, "
       "Tensor tasks, Tensor task_lo, Tensor rec_off, Tensor(c!) ws, Tensor(d!) payload, int q, "
-      "int qstates, int gid_base, int step, int tag, int seed, Tensor? step_t=None) -> ()");
+      "int qstates, int gid_base, int step, int tag, int seed, Tensor? step_t=None, "
+      "bool staged=False) -> ()");
   m.def(
       "dequantize(Tensor gathered, int world, Tensor(a!) g, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor task_lo, Tensor rec_off, int q, int qstates) -> ()");
@@ -1748,6 +1792,8 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("selftest_bad_launch", &selftest_bad_launch);
   m.impl("selftest_spin", &selftest_spin);
   m.impl("select_compress", &select_compress);
+  m.impl("select_stage", &select_stage);
+  m.impl("quant_stage", &quant_stage);
   m.impl("thresh_count", &thresh_count);
   m.impl("thresh_write", &thresh_write);
   m.impl("thresh_dense", &thresh_dense);

@@ -968,19 +968,20 @@ __global__ __launch_bounds__(NT) void k_zero_words(uint32_t* __restrict__ p, int
 }
 
 template <int KM, int OUT, bool EF>
-static void select_compress_t(const SelectArgs& a, hipStream_t st) {
+static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) {
   if (a.n_small > 0)
     LW_LAUNCH((k_small_select<KM, OUT, EF>), a.n_small, st, a.g, a.ef, a.seg_off, a.seg_n, a.keep,
               a.cap_off, a.small_segs, a.pairs, a.vals, a.idx_out, a.st_small, a.gid_base, a.step,
               a.seed0, a.seed1, a.step_ptr, a.overflow, a.mom);
   if (a.n_large == 0) return;
-  {
+  if (!staged) {      // (staged: select_stage already zeroed the histograms and ran pass 0)
     const int64_t words = (int64_t)HIST_WORDS * a.n_large;
     const int64_t nb = (words + NT - 1) / NT;
     LW_LAUNCH(k_zero_words, (int)(nb < 1024 ? nb : 1024), st, a.hist, words);
+    LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.large_segs, a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+              a.step_ptr);
   }
-  LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
-            a.large_segs, a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
   LW_LAUNCH((k_select<KM, 0>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off,
             a.overflow);
   LW_LAUNCH((k_hist<KM, 1, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
@@ -1001,19 +1002,49 @@ static void select_compress_t(const SelectArgs& a, hipStream_t st) {
             a.seed0, a.seed1, a.step_ptr, a.mom);
 }
 
-void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st) {
+void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st, bool staged) {
   if (km == KM_TOPK && out == OUT_PAIRS) {
-    ef ? select_compress_t<KM_TOPK, OUT_PAIRS, true>(a, st)
-       : select_compress_t<KM_TOPK, OUT_PAIRS, false>(a, st);
+    ef ? select_compress_t<KM_TOPK, OUT_PAIRS, true>(a, staged, st)
+       : select_compress_t<KM_TOPK, OUT_PAIRS, false>(a, staged, st);
   } else if (km == KM_RANDK && out == OUT_VALIDX) {
-    ef ? select_compress_t<KM_RANDK, OUT_VALIDX, true>(a, st)
-       : select_compress_t<KM_RANDK, OUT_VALIDX, false>(a, st);
+    ef ? select_compress_t<KM_RANDK, OUT_VALIDX, true>(a, staged, st)
+       : select_compress_t<KM_RANDK, OUT_VALIDX, false>(a, staged, st);
   } else if (km == KM_RANDK && out == OUT_PAIRS) {
-    ef ? select_compress_t<KM_RANDK, OUT_PAIRS, true>(a, st)
-       : select_compress_t<KM_RANDK, OUT_PAIRS, false>(a, st);
+    ef ? select_compress_t<KM_RANDK, OUT_PAIRS, true>(a, staged, st)
+       : select_compress_t<KM_RANDK, OUT_PAIRS, false>(a, staged, st);
   } else {
-    ef ? select_compress_t<KM_TOPK, OUT_VALIDX, true>(a, st)
-       : select_compress_t<KM_TOPK, OUT_VALIDX, false>(a, st);
+    ef ? select_compress_t<KM_TOPK, OUT_VALIDX, true>(a, staged, st)
+       : select_compress_t<KM_TOPK, OUT_VALIDX, false>(a, staged, st);
+  }
+}
+
+// Entire-model staging (parallel/engine.py): the one segment's first pass — the radix pass-0
+// histogram with the error-feedback fold g' = g + e (Top-K), or the histogram of the Philox keys
+// (Random-K) — over tasks [t_lo, t_hi), launched while backward still runs, as the arena slice
+// those tasks cover completes. The counts are integers added atomically, so any split of the tasks
+// gives the histogram of one launch; select_compress(staged) then runs the rest of the chain.
+void select_stage(const SelectArgs& a, int km, bool ef, int t_lo, int t_hi, bool zero,
+                  hipStream_t st) {
+  if (zero) {
+    const int64_t words = (int64_t)HIST_WORDS * a.n_large;
+    const int64_t nb = (words + NT - 1) / NT;
+    LW_LAUNCH(k_zero_words, (int)(nb < 1024 ? nb : 1024), st, a.hist, words);
+  }
+  if (t_hi <= t_lo) return;
+  const int2* tk = a.tasks + t_lo;
+  if (km == KM_TOPK) {
+    if (ef)
+      LW_LAUNCH((k_hist<KM_TOPK, 0, true>), t_hi - t_lo, st, a.g, a.ef, a.seg_off, a.seg_n,
+                a.large_segs, tk, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+                a.step_ptr);
+    else
+      LW_LAUNCH((k_hist<KM_TOPK, 0, false>), t_hi - t_lo, st, a.g, a.ef, a.seg_off, a.seg_n,
+                a.large_segs, tk, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+                a.step_ptr);
+  } else {
+    LW_LAUNCH((k_hist<KM_RANDK, 0, false>), t_hi - t_lo, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.large_segs, tk, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+              a.step_ptr);
   }
 }
 
@@ -1085,10 +1116,22 @@ void unpack_validx(const float* vals, const int32_t* idx, const int32_t* slot_se
 }
 
 void seg_reduce(const QuantArgs& a, bool ef_add, int what, float* out, float2* partial,
-                hipStream_t st) {
-  if (ef_add) LW_LAUNCH((k_partial<true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks, partial);
-  else LW_LAUNCH((k_partial<false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks, partial);
+                hipStream_t st, bool staged) {
+  if (!staged) {      // (staged: quant_stage already wrote every task's partial)
+    if (ef_add) LW_LAUNCH((k_partial<true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks, partial);
+    else LW_LAUNCH((k_partial<false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks, partial);
+  }
   LW_LAUNCH(k_finalize, a.nseg, st, partial, a.task_lo, out, what);
+}
+
+// Entire-model staging of the quantisers: the per-task (abs-max, sum of squares) partials with the
+// error-feedback fold, for tasks [t_lo, t_hi), each into its own slot — the finalize then folds
+// the slots in task order, exactly as after one launch.
+void quant_stage(const QuantArgs& a, bool ef_add, int t_lo, int t_hi, float2* partial,
+                 hipStream_t st) {
+  if (t_hi <= t_lo) return;
+  if (ef_add) LW_LAUNCH((k_partial<true>), t_hi - t_lo, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks + t_lo, partial + t_lo);
+  else LW_LAUNCH((k_partial<false>), t_hi - t_lo, st, a.g, a.ef, a.seg_off, a.seg_n, a.segs, a.tasks + t_lo, partial + t_lo);
 }
 
 template <int Q>

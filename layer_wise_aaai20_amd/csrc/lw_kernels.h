@@ -78,7 +78,11 @@ struct QuantArgs {
   const uint32_t* step_ptr;    // optional device step counter (overrides `step`; HIP graphs)
 };
 
-void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st);
+void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st,
+                     bool staged = false);
+// entire-model staging (compress.hip): pass 0 over tasks [t_lo, t_hi) while backward runs
+void select_stage(const SelectArgs& a, int km, bool ef, int t_lo, int t_hi, bool zero,
+                  hipStream_t st);
 void thresh_count(const SelectArgs& a, float V, int adaptive, bool ef, float* segmax,
                   float2* partial, int32_t* count_out, hipStream_t st);
 void thresh_write(const SelectArgs& a, bool ef, hipStream_t st);
@@ -90,7 +94,9 @@ void unpack_pairs(const int2* gathered, int64_t cap_total, int ws, float* g, con
 void unpack_validx(const float* vals, const int32_t* idx, const int32_t* slot_seg, int64_t nslots,
                    int ws, float* g, const int64_t* seg_off, hipStream_t st);
 void seg_reduce(const QuantArgs& a, bool ef_add, int what, float* out, float2* partial,
-                hipStream_t st);
+                hipStream_t st, bool staged = false);
+void quant_stage(const QuantArgs& a, bool ef_add, int t_lo, int t_hi, float2* partial,
+                 hipStream_t st);
 void quantize(const QuantArgs& a, int q, bool ef, hipStream_t st);
 void dequantize(const QuantArgs& a, int q, const uint32_t* gathered, int64_t words_per_rank, int ws,
                 hipStream_t st);

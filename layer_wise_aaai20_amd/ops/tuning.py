@@ -42,6 +42,26 @@ _TABLE: Dict[str, object] = {}
 if _READ and os.path.exists(_READ):
     with open(_READ) as f:
         _TABLE = json.load(f)
+# The shipped table pins choices timed on gfx950 (MI355X): on any other device they were never
+# timed, so it is used only where the device is gfx950 (checked on the first pick); a table named
+# by LWAAAI_TUNE_FILE is the user's own and always used.
+_ARCH_OK = None if (_READ == SHIPPED and _TABLE) else True
+
+
+def _pinned(key: str):
+    global _ARCH_OK
+    if _ARCH_OK is None:
+        arch = ""
+        try:
+            if torch.cuda.is_available():
+                arch = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName
+        except Exception:                  # noqa: BLE001 — no device / no property: not gfx950
+            arch = ""
+        _ARCH_OK = arch.startswith("gfx950")
+        if not _ARCH_OK and _TABLE:
+            warnings.warn(f"shipped tuning table (gfx950) ignored on device arch {arch!r}: "
+                          f"every kernel choice is timed instead", stacklevel=3)
+    return _TABLE.get(key) if _ARCH_OK else None
 
 _AGREE: list = []          # stack of (process group, device) set by rank_agreement()
 
@@ -127,7 +147,7 @@ class Tuner:
         c = self.best.get(key)
         if c is not None:
             return c
-        pinned = _TABLE.get(self._tkey(key))
+        pinned = _pinned(self._tkey(key))
         if pinned is not None:
             c = _decode(pinned)
             if any(c == _decode(_encode(x)) for x in candidates) or \

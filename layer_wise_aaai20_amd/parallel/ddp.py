@@ -62,6 +62,7 @@ class CompressedDDP(nn.Module):
                                      momentum_correction=momentum_correction,
                                      ef_lr_scaled=ef_lr_scaled)
         self._buffers_list = self._flatten_buffers(module) if broadcast_buffers else []
+        self._bcast_events = []          # (ready, done) of the last buffer broadcasts
         self._hooks = []
         self._register_hooks()
         self._callback_queued = False
@@ -132,17 +133,54 @@ class CompressedDDP(nn.Module):
     # ------------------------------------------------------------------ module API
     def forward(self, *inputs, **kwargs):
         if not self.training:
+            if self._bcast_events:          # (evaluation reads the broadcast running statistics)
+                torch.cuda.current_stream(self.engine.device).wait_event(self._bcast_events[-1][1])
             return self.module(*inputs, **kwargs)
         if self.check_reduction and self.engine._active:
             raise RuntimeError("Not all gradients have been reduced from the backward of the "
                                "previous iteration (ddp.py:312-327 check_reduction).")
-        if self.broadcast_buffers and self._buffers_list:
+        side = self._buffer_side()
+        if side is not None:
+            # the buffers were broadcast on the side stream right after the previous forward,
+            # overlapped with its backward: only their use waits for it
+            if self._bcast_events:
+                torch.cuda.current_stream(self.engine.device).wait_event(self._bcast_events[-1][1])
+        elif self.broadcast_buffers and self._buffers_list:
             comm.broadcast_coalesced(self._buffers_list, 0, self.process_group,
                                      native=self.engine._native)
         self.engine.begin_step()
         if self.bf16_weights and self.engine.arena.device.type == "cuda":
             self.engine.arena.refresh_bf16()
-        return self.module(*inputs, **kwargs)
+        out = self.module(*inputs, **kwargs)
+        if side is not None:
+            self._broadcast_after_forward(side)
+        return out
+
+    def _buffer_side(self):
+        """The side stream the buffer broadcast runs on, or None (eager broadcast at forward)."""
+        eng = self.engine
+        if not (self.broadcast_buffers and self._buffers_list) or eng._native is None or \
+                eng._side is None or eng.world <= 1:
+            return None
+        return eng._side
+
+    def _broadcast_after_forward(self, side) -> None:
+        """The reference broadcasts the buffers (BN running statistics) at the start of every
+        forward (``ddp.py:361-386``). No kernel touches them between the end of one forward and
+        the start of the next, so broadcasting right after the forward sends the same values;
+        done on the side stream, the broadcast overlaps this step's backward instead of
+        delaying the next forward. The events stay alive for a few steps (a HIP event
+        destroyed while a queued wait references it faults: profiles/r2_vgg_fault.md)."""
+        cur = torch.cuda.current_stream(self.engine.device)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        side.wait_event(ready)
+        with torch.cuda.stream(side):
+            comm.broadcast_coalesced(self._buffers_list, 0, self.process_group,
+                                     native=self.engine._native)
+            done = torch.cuda.Event()
+            done.record(side)
+        self._bcast_events = (self._bcast_events + [(ready, done)])[-4:]
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         """Keep ``.grad`` as arena views: zeroing means clearing the arena."""

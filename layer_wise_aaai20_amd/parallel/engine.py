@@ -166,6 +166,7 @@ class GradSyncEngine:
         for b in self.buckets:
             for i in range(b.seg_lo, b.seg_hi):
                 self.seg_bucket[i] = b.index
+        self._plan_stages(cap)
         self.step = 0
         self.stats = SyncStats(dense_bytes=self.arena.numel * 4, buckets=len(self.buckets))
         self.timing = timing and self.device.type == "cuda"
@@ -225,6 +226,73 @@ class GradSyncEngine:
                 f"rank {self.rank}: gradient bucket plans differ across ranks (signature "
                 f"{mine.tolist()} vs min {lo.tolist()} / max {hi.tolist()}): the model, the "
                 f"compression settings or the bucket size are not identical on every rank")
+
+    # ----------------------------------------------------------------- entire-model staging
+    def _plan_stages(self, cap_bytes: int) -> None:
+        """Entire-model mode compresses the flattened model as ONE segment, so its statistic —
+        the Top-K radix pass-0 histogram, the QSGD norm / TernGrad max — covers every gradient and
+        the whole chain used to run after backward. Here the arena is cut into slices of whole
+        8192-element tasks (about ``bucket_cap_mb`` each); when every parameter overlapping a
+        slice has its gradient, that slice's share of the first pass runs (with the
+        error-feedback fold) on the side stream, overlapped with the rest of backward. The
+        histogram counts are integers and the quantisers' partials land in per-task slots, so
+        the result is bit-identical to the single launch (tests/test_loopback_gpu.py); only the
+        rest of the chain stays after backward. ``LWAAAI_EM_STAGE=0``: off. (Momentum correction
+        and LR-scaled residuals rewrite the gradient in their prologue: no staging with them.)"""
+        self._stages = []
+        if not (self.mode == "entiremodel" and self.device.type == "cuda" and self.mom is None
+                and not self.lr_scaled and len(self.codecs) == 1
+                and os.environ.get("LWAAAI_EM_STAGE", "1") != "0"):
+            return
+        codec = self.codecs[0]
+        sel = codec.inner if isinstance(codec, DenseWrap) else codec
+        if not sel.can_stage():
+            return
+        from ..compress.plan import LARGE_EPB
+        n = self.arena.numel
+        per = max(LARGE_EPB, (cap_bytes // 4) // LARGE_EPB * LARGE_EPB)
+        if n <= per:
+            return
+        bounds = list(range(0, n, per)) + [n]
+        segs = self.arena.segments
+        self._stages = [(lo, hi, -(-hi // LARGE_EPB) if hi == n else hi // LARGE_EPB)
+                        for lo, hi in zip(bounds[:-1], bounds[1:])]
+        self._stage_need = [0] * len(self._stages)
+        self._seg_stages = [[] for _ in segs]
+        for i, s in enumerate(segs):
+            for si, (lo, hi, _) in enumerate(self._stages):
+                if s.offset < hi and s.offset + s.numel > lo:
+                    self._seg_stages[i].append(si)
+                    self._stage_need[si] += 1
+
+    def _stage_reset(self) -> None:
+        self._stage_cnt = [0] * len(self._stages)
+        self._stage_next = 0
+        self._stage_events = []
+
+    def _stage_in_order(self, force: bool = False) -> None:
+        while self._stage_next < len(self._stages) and (
+                force or self._stage_cnt[self._stage_next] == self._stage_need[self._stage_next]):
+            self._stage(self._stage_next)
+            self._stage_next += 1
+
+    def _stage(self, si: int) -> None:
+        lo, hi, t_hi = self._stages[si]
+        t_lo = lo // 8192 if si > 0 else 0
+        codec = self.codecs[0]
+        sel = codec.inner if isinstance(codec, DenseWrap) else codec
+        e = self.ef if self.ef is not None else None
+        side = self._side
+        if side is not None and not self._graph_overlap and \
+                torch.cuda.is_current_stream_capturing():
+            side = None                      # (inline inside a world-1 capture, as _launch)
+        if side is not None:
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(self.device))
+            side.wait_event(ready)
+            self._stage_events.append(ready)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            sel.stage(self.arena.grad, e, self.step, t_lo, t_hi, si == 0)
 
     def set_mc_weight_decay(self, opt) -> None:
         """Momentum correction: take the weight decay of ``opt`` (a :class:`FlatSGD` over this
@@ -288,6 +356,7 @@ class GradSyncEngine:
 
     # ----------------------------------------------------------------- state machine
     def _reset_state(self):
+        self._stage_reset()
         self._marked = bytearray(len(self.arena.segments))
         nb = len(self.buckets)
         self._ready_cnt = [0] * nb
@@ -327,6 +396,10 @@ class GradSyncEngine:
             raise RuntimeError(f"segment {self.arena.segments[seg_index].name} marked ready "
                                f"after its bucket {self.seg_bucket[seg_index]} was launched")
         self._active = True
+        if self._stages:
+            for si in self._seg_stages[seg_index]:
+                self._stage_cnt[si] += 1
+            self._stage_in_order()
         b = self.seg_bucket[seg_index]
         self._ready_cnt[b] += 1
         n = self.buckets[b].seg_hi - self.buckets[b].seg_lo
@@ -370,11 +443,15 @@ class GradSyncEngine:
                 e.mul_(self._lr_ratio)                   # residual re-expressed at this step's LR
             u = None
             sel = codec.inner if isinstance(codec, DenseWrap) else codec
+            if self._stages:
+                self._stage_in_order(force=True)  # (slices of parameters that got no gradient)
+                sel._staged = True
             if self.mom is not None:
                 u = self.mom[b.start:b.end]
                 self._mc_prologue(bi, g, u)              # velocity; the residual accumulates it
                 sel.mc_mom = u                           # masked by the select kernels
             send = codec.compress(g, e, self.step)
+            sel._staged = False
             if u is not None:
                 sel.mc_mom = None
                 if not getattr(sel, "mc_fused", False):  # no selection: sent <=> residual 0
@@ -417,7 +494,7 @@ class GradSyncEngine:
             self._ready[i] = True
         self._launch_in_order()
         rec = []
-        hold = []                                # events some stream still waits on (see below)
+        hold = list(self._stage_events)          # events some stream still waits on (see below)
         for bi, work, send, recv, (t0, t1, tx), done, ready in self._pending:
             hold += [e for e in (ready, done) if e is not None]
             work.wait()

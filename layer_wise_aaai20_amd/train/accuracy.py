@@ -36,23 +36,32 @@ def class_conditional_batches(batch: int, size: int, device, seed_bias: int = 7)
     return make_batch
 
 
+def lr_at(i: int, steps: int, peak: float, warmup: int, decay: str) -> float:
+    """Linear warm-up over ``warmup`` steps to ``peak``, then constant (``decay="none"``, the
+    reference's phase 0) or a linear decay to 0 at ``steps`` (``"linear"``)."""
+    lr = peak * min(1.0, (i + 1) / warmup)
+    if decay == "linear" and i >= warmup:
+        lr = peak * max(0.0, (steps - i) / max(1, steps - warmup))
+    return lr
+
+
 def short_run_top1(device, steps: int = 300, size: int = 128, batch: int = 256,
                    peak_lr_512: float = 2.0, warmup: int = 100, eval_batches: int = 8,
-                   rank: int = 0, world: int = 1, seed: int = 0,
-                   **method_kw) -> dict:
+                   rank: int = 0, world: int = 1, seed: int = 0, decay: str = "none",
+                   momentum: float = 0.9, **method_kw) -> dict:
     """Train a fresh ResNet-50 for ``steps`` steps with the given compression settings
     (``compress=``, ``method=``, ``K=``, ``error_feedback=`` ...) and return held-out accuracy."""
     dev = torch.device(device)
     torch.manual_seed(seed)
-    tr = build_trainer("resnet50", device=dev, momentum=0.9, weight_decay=1e-4, no_bn_wd=True,
-                       lr=0.0, bucket_cap_mb=50.0, graph_auto=False, **method_kw)
+    tr = build_trainer("resnet50", device=dev, momentum=momentum, weight_decay=1e-4,
+                       no_bn_wd=True, lr=0.0, bucket_cap_mb=50.0, graph_auto=False, **method_kw)
     make_batch = class_conditional_batches(batch, size, dev)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     peak = peak_lr_512 * batch * world / 512
     losses = []
     for i in range(steps):
         for grp in tr.opt.param_groups:
-            grp["lr"] = peak * min(1.0, (i + 1) / warmup)
+            grp["lr"] = lr_at(i, steps, peak, warmup, decay)
         losses.append(tr.step(*make_batch(g)))
     model = tr.ddp.module
     model.eval()
@@ -76,4 +85,5 @@ def short_run_top1(device, steps: int = 300, size: int = 128, batch: int = 256,
     return {"top1": round(100.0 * c1 / n, 3), "top5": round(100.0 * c5 / n, 3),
             "steps": steps, "image_size": size, "per_gpu_batch": batch,
             "loss_first20": round(first, 4), "loss_last20": round(last, 4),
+            "peak_lr_512": peak_lr_512, "warmup": warmup, "decay": decay, "momentum": momentum,
             "graph_replays": tr.graph_replays}

@@ -420,16 +420,20 @@ def train(run, trn_loader, model, criterion, optimizer, scheduler, epoch, sync, 
             corr1, corr5 = correct(output.data, target, topk=(1, 5))
         metrics = torch.cat([torch.tensor([float(inp.size(0))], device=loss.device),
                              loss.detach().float().reshape(1) * inp.size(0), corr1, corr5])
-        if args.distributed:
+        if args.distributed and not fast:
             metrics = comm.sum_tensor(metrics)
         if fast:
-            # no host sync per step (the reference reads the metrics every step): accumulate on
-            # the device, read once per print interval
+            # no host sync and no collective per step (the reference all-reduces and reads the
+            # metrics every step, train_imagenet_nv.py:421-424): accumulate this rank's sums on
+            # the device and all-reduce the accumulated sums once per print interval — the same
+            # totals, since summing over steps and over ranks commute
             acc = metrics.clone() if acc is None else acc.add_(metrics)
             timer.start = time.time()            # (data time only; step time per interval)
             if not should_print:
                 run.tb.update_step_count(inp.size(0) * run.world)
                 continue
+            if args.distributed:
+                acc = comm.sum_tensor(acc)
             batch_total, loss_sum, c1, c5 = acc.cpu().tolist()   # (waits for the GPU)
             acc = None
             # the interval's mean step time, GPU-complete (host time per step is not: the host

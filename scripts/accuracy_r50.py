@@ -60,6 +60,9 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--lr", type=float, default=2.0, help="peak LR at batch 512 (phase 0)")
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--decay", default="none", choices=["none", "linear"],
+                    help="after the warm-up: constant LR, or a linear decay to 0")
+    ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--eval-batches", type=int, default=8)
     ap.add_argument("--methods", default="none,topk0.1%,topk0.1%+ef")
     ap.add_argument("--seeds", default="0", help="comma list: model-init seeds")
@@ -70,7 +73,8 @@ def main():
     for seed, name in runs:
         t0 = time.time()
         r = short_run_top1("cuda:0", steps=args.steps, size=args.size, batch=args.batch,
-                           peak_lr_512=args.lr, warmup=args.warmup,
+                           peak_lr_512=args.lr, warmup=args.warmup, decay=args.decay,
+                           momentum=args.momentum,
                            eval_batches=args.eval_batches, seed=seed, **METHODS[name])
         print(json.dumps(dict(method=name, seed=seed, chance_top1=0.1,
                               wall_s=round(time.time() - t0, 1),

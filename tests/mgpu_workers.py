@@ -129,12 +129,14 @@ def exchange_vs_oracle(rank, world, dev, mode, method, ef, kw, steps=3):
                 exp[sl] = part
             errs.append(float((got.cpu() - exp).abs().max()))
             tol = 1e-6 * float(exp.abs().max())
-        elif method == "Topk":
+        elif method in ("Topk", "Thresholdv"):
+            # the reference compressor (core.py:175-215) on every rank's raw gradient, averaged
+            arg = {"K": kw["K"]} if method == "Topk" else {"V": kw["V"]}
             exp = torch.zeros(eng.arena.numel)
             for r in range(world):
                 for s in eng.arena.segments:
                     sl = slice(s.offset, s.offset + s.numel)
-                    exp[sl] += ref.compress(raws[r][sl], "Topk", **{"K": kw["K"]})
+                    exp[sl] += ref.compress(raws[r][sl], method, **arg)
             exp /= world
             errs.append(float((got.cpu() - exp).abs().max()))
             tol = 1e-8
@@ -171,6 +173,31 @@ def train_graph_vs_eager(rank, world, dev, compress, method, ef, kw, steps=8):
         p = torch.cat([q.detach().float().reshape(-1) for q in tr.ddp.module.parameters()])
         allp = _gather_cpu(p)
         out[graph] = (p.cpu(), losses, tr.graph_replays,
+                      all(torch.equal(allp[0], a) for a in allp[1:]))
+        del tr
+        torch.cuda.empty_cache()
+    return out
+
+
+def cifar_graph_vs_eager(rank, world, dev, network, compress, method, ef, kw, steps=6):
+    """CifarTrainer (BASELINE configs 2 and 3: VGG-16 layer-wise Top-K 0.1 %, AlexNet
+    entire-model Top-K + EF) on real RCCL ranks, each rank on its own data order: eager vs
+    HIP-graph step, parameters bit-identical across ranks and between the two modes."""
+    from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
+    out = {}
+    for graph in (False, True):
+        torch.manual_seed(0)
+        tr = CifarTrainer(network, device=dev, compress=compress, method=method,
+                          error_feedback=ef, batch_size=128, n_train=128 * 8, n_test=128,
+                          seed=rank, graph=graph, **kw)
+        tr.graphed.auto = False
+        tr.graphed.decided = True
+        assert tr.ddp.engine._native is not None
+        losses = [float(tr.step()) for _ in range(steps)]
+        torch.cuda.synchronize(dev)
+        p = torch.cat([q.detach().float().reshape(-1) for q in tr.model.parameters()])
+        allp = _gather_cpu(p)
+        out[graph] = (p.cpu(), losses, tr.graphed.replays,
                       all(torch.equal(allp[0], a) for a in allp[1:]))
         del tr
         torch.cuda.empty_cache()

@@ -134,3 +134,43 @@ def test_resnet50_step_world8_graph_matches_eager(monkeypatch):
     assert all(l == l for l in runs[True][1])
     assert runs[False][1] == runs[True][1]
     assert torch.equal(runs[False][0], runs[True][0])
+
+
+EM_CASES = [("Topk", True, {"K": 0.001}), ("RandomDithering", False, {"qstates": 255}),
+            ("TernGrad", True, {}), ("Randomk", True, {"K": 0.01})]
+
+
+@pytest.mark.parametrize("method,ef,kw", EM_CASES, ids=[c[0] for c in EM_CASES])
+def test_entiremodel_staged_equals_single_launch(method, ef, kw, monkeypatch):
+    """Entire-model mode with its first pass staged per arena slice during backward (VERDICT r4
+    item 3; parallel/engine.py _plan_stages) vs the same step with the whole chain after backward
+    (LWAAAI_EM_STAGE=0): a world-8 ResNet-50 step with the loopback peers, HIP-graph replay,
+    parameters bit-identical after 6 steps."""
+    monkeypatch.setenv("LWAAAI_GRAPH_AUTO", "0")
+    from layer_wise_aaai20_amd.train.imagenet import build_trainer
+    runs = {}
+    for stage in ("1", "0"):
+        monkeypatch.setenv("LWAAAI_EM_STAGE", stage)
+        torch.manual_seed(0)
+        tr = build_trainer("resnet50", device="cuda", compress="entiremodel", method=method,
+                           error_feedback=ef, graph=True, world_size=W, bucket_cap_mb=16.0, **kw)
+        eng = tr.ddp.engine
+        assert bool(eng._stages) == (stage == "1"), len(eng._stages)
+        attach_loopback(eng, [_rand_arena(eng, 300 + r, 1e-3) for r in range(1, W)])
+        g = torch.Generator(device="cuda").manual_seed(4)
+        losses = []
+        for _ in range(6):
+            x = torch.randint(0, 256, (8, 64, 64, 3), dtype=torch.uint8, device="cuda",
+                              generator=g)
+            t = torch.randint(0, 1000, (8,), device="cuda", generator=g)
+            losses.append(float(tr.step(x, t)))
+        torch.cuda.synchronize()
+        p = torch.cat([q.detach().float().reshape(-1) for q in tr.ddp.module.parameters()])
+        runs[stage] = (p, losses, tr.graph_replays, eng.ef.clone() if ef else None)
+        del tr
+        torch.cuda.empty_cache()
+    assert runs["1"][2] > 0 and runs["0"][2] > 0
+    assert runs["1"][1] == runs["0"][1]
+    assert torch.equal(runs["1"][0], runs["0"][0])
+    if ef:
+        assert torch.equal(runs["1"][3], runs["0"][3])

@@ -19,8 +19,8 @@ import os
 import pytest
 import torch
 
-from mgpu_workers import (capture_fallback_collective, exchange_vs_oracle, native_init_fallback,
-                          run_world, train_graph_vs_eager)
+from mgpu_workers import (capture_fallback_collective, cifar_graph_vs_eager, exchange_vs_oracle,
+                          native_init_fallback, run_world, train_graph_vs_eager)
 
 pytestmark = pytest.mark.gpu
 
@@ -53,8 +53,19 @@ need2 = pytest.mark.skipif(_ngpu() < 2 and not _share(),
 CASES = [("layerwise", "Topk", False, {"K": 0.001}),
          ("layerwise", "Topk", True, {"K": 0.001}),
          ("entiremodel", "RandomDithering", False, {"qstates": 255}),
-         ("none", "none", False, {})]
-IDS = [f"{c[1]}-{c[0]}-{'ef' if c[2] else 'noef'}" for c in CASES]
+         ("none", "none", False, {}),
+         # every wire on real ranks
+         ("layerwise", "Randomk", True, {"K": 0.01}),          # index-free all-reduce + EF
+         ("layerwise", "Thresholdv", False, {"V": 1e-2, "wire": "sparse"}),   # count exchange
+         ("layerwise", "TernGrad", False, {}),
+         ("entiremodel", "Topk", True, {"K": 0.001})]
+IDS = [f"{c[1]}-{c[0]}-{'ef' if c[2] else 'noef'}{'-' + c[3]['wire'] if 'wire' in c[3] else ''}"
+       for c in CASES]
+# the exact sparse threshold wire agrees its payload size by a count all-reduce read on the host
+# in the middle of backward: that step is never captured (both trainers run eagerly)
+EAGER_ONLY = {"Thresholdv"}
+CIFAR_CASES = [("vgg16", "layerwise", "Topk", False, {"K": 0.001}),
+               ("alexnet", "entiremodel", "Topk", True, {"K": 0.01})]
 
 
 @need2
@@ -73,6 +84,19 @@ def test_training_ranks_agree_and_graph_matches_eager(world, mode, method, ef, k
     if method == "Topk":
         kw["K"] = 0.01
     res = run_world(train_graph_vs_eager, world, (mode, method, ef, kw))
+    for r in res:
+        (pe, le, _, same_e), (pg, lg, replays, same_g) = r[False], r[True]
+        assert same_e and same_g, "parameters differ across ranks"
+        assert (replays == 0) if method in EAGER_ONLY else (replays > 0)
+        assert le == lg
+        assert torch.equal(pe, pg), (pe - pg).abs().max().item()
+    assert all(torch.equal(res[0][True][0], r[True][0]) for r in res[1:])
+
+
+@need2
+@pytest.mark.parametrize("net,mode,method,ef,kw", CIFAR_CASES, ids=[c[0] for c in CIFAR_CASES])
+def test_cifar_trainer_ranks_agree_and_graph_matches_eager(net, mode, method, ef, kw):
+    res = run_world(cifar_graph_vs_eager, 2, (net, mode, method, ef, kw))
     for r in res:
         (pe, le, _, same_e), (pg, lg, replays, same_g) = r[False], r[True]
         assert same_e and same_g, "parameters differ across ranks"

@@ -45,7 +45,9 @@ Q_TERN, Q_QS8, Q_QS9, Q_QS16 = 0, 1, 2, 3
 
 
 def _ws_tensor(nbytes: int, device) -> torch.Tensor:
-    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+    # zeroed: the fused select chain expects zero radix histograms on its first call and leaves
+    # them zeroed for the next (csrc/compress.hip k_write FW)
+    return torch.zeros(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
 def tie_slack(m: int) -> int:
@@ -823,4 +825,12 @@ def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qst
         # (index-free Random-K sends only its values, one all-reduce: never worth densifying)
         if c.cap_total * max(world, 2) > plan.numel:
             return DenseWrap(c)
+    if wire == "auto" and isinstance(c, _QuantCodec) and world > 1 and \
+            c.words * 4 * world > 8 * plan.numel:
+        # an all-gather of codes brings (W-1)·b·n bytes to every rank (b bytes per element) and
+        # decodes W·n elements; a ring all-reduce of the dequantised fp32 vector moves
+        # 2(W-1)/W·4n and decodes n: the codes stop paying once b·W > 8 — QSGD-255 (9 bits +
+        # headers) from 8 ranks on, 8-bit QSGD from 16, 16-bit QSGD (just under 2 B with its
+        # packing) from 8, TernGrad (2 bits) only past 32
+        return DenseWrap(c)
     return c

@@ -393,6 +393,16 @@ void mc_prep(Tensor g, Tensor u, c10::optional<Tensor> p, Tensor seg_off, Tensor
   launched("mc_prep");
 }
 
+// the engine's device step counter (+1 per step inside the captured graph; csrc/optim.hip)
+void step_bump(Tensor c) {
+  const c10::DeviceGuard guard(c.device());
+  check_cuda(c, "c");
+  check_dtype(c, at::kLong, "c");
+  TORCH_CHECK(c.numel() >= 1, "step_bump: empty counter");
+  lw::step_bump(ptr<int64_t>(c), cur_stream());
+  launched("step_bump");
+}
+
 void mc_mask(Tensor u, Tensor e) {
   const c10::DeviceGuard guard(u.device());
   check_cuda(u, "u");
@@ -1723,6 +1733,7 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "mc_prep(Tensor(a!) g, Tensor(b!) u, Tensor? p, Tensor seg_off, Tensor seg_n, Tensor segs, "
       "Tensor tasks, Tensor? seg_wd, float mc, float wmul) -> ()");
   m.def("mc_mask(Tensor(a!) u, Tensor e) -> ()");
+  m.def("step_bump(Tensor(a!) c) -> ()");
   m.def(
       "sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
@@ -1804,6 +1815,7 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("sgd_step", &sgd_step);
   m.impl("mc_prep", &mc_prep);
   m.impl("mc_mask", &mc_mask);
+  m.impl("step_bump", &step_bump);
   m.impl("normalize_u8", &normalize_u8);
   m.impl("cifar_augment", &cifar_augment);
   m.impl("gap_fwd", &gap_fwd);

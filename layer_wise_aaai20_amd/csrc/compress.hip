@@ -34,6 +34,15 @@ constexpr int NT = 256;
 #define LW_HIST_CP 4             // interleaved LDS histogram copies in the first radix pass
 #endif
 static_assert((LW_HIST_CP & (LW_HIST_CP - 1)) == 0, "LW_HIST_CP: a power of two");
+#ifndef LW_FUSED_SELECT
+#define LW_FUSED_SELECT 1        // 0: the 9-launch chain (k_select per pass, k_count, k_fill_tail)
+#endif
+#ifndef LW_HIST_TPB
+#define LW_HIST_TPB 4            // 8192-element tasks per histogram workgroup (see k_hist) once a
+#endif                           // launch has LW_HIST_TPB_MIN tasks; 1 below that
+#ifndef LW_HIST_TPB_MIN
+#define LW_HIST_TPB_MIN 2048
+#endif
 constexpr int EPB = kLargeEPB;       // elements per block in the multi-block passes (8192)
 constexpr int EPT = EPB / NT;        // 32 contiguous elements per thread in k_write / k_quant
 constexpr int SEPT = kSmallMax / NT; // 16 per thread in k_small_select
@@ -262,15 +271,42 @@ __device__ __forceinline__ void load4_keys(float* gp, const float* ep, int i0, i
   k[0] = abs_key(v.x); k[1] = abs_key(v.y); k[2] = abs_key(v.z); k[3] = abs_key(v.w);
 }
 
-template <int KM, int PASS, bool EFADD>
+// Fused radix chain (FUSED = true, passes 1 and 2): a workgroup reaching a segment redoes the
+// previous pass's digit selection itself, from that pass's complete integer histogram, instead of
+// a k_select launch of its own — every workgroup derives the identical digit. The workgroup that
+// holds the segment's first task publishes it (SelState p0/m0 after pass 0, p1/m1 after pass 1)
+// for the next launch; no workgroup of this launch reads those fields.
+template <int PASS>
+__device__ __forceinline__ void fused_prev_select(const uint32_t* __restrict__ hist_all,
+                                                  SelState* __restrict__ st,
+                                                  const int32_t* __restrict__ keep, int li, int s,
+                                                  bool publish, uint32_t& prefix, uint32_t* arr,
+                                                  uint32_t* scr, uint32_t* res) {
+  const uint32_t* hb = hist_all + (size_t)li * HIST_WORDS;
+  uint32_t d, mn;
+  if constexpr (PASS == 1) {
+    select_digit<2048>(hb + PassCfg<0>::HOFF, (uint32_t)keep[s], d, mn, arr, scr, res);
+    prefix = d;
+    if (publish && threadIdx.x == 0) { st[li].p0 = prefix; st[li].m0 = mn; }
+  } else {
+    const uint32_t p0 = st[li].p0;
+    select_digit<1024>(hb + PassCfg<1>::HOFF, st[li].m0, d, mn, arr, scr, res);
+    prefix = (p0 << PassCfg<1>::BITS) | d;
+    if (publish && threadIdx.x == 0) { st[li].p1 = prefix; st[li].m1 = mn; }
+  }
+}
+
+template <int KM, int PASS, bool EFADD, bool FUSED = false>
 __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float* __restrict__ ef,
                                              const int64_t* __restrict__ seg_off,
                                              const int32_t* __restrict__ seg_n,
                                              const int32_t* __restrict__ large_segs,
-                                             const int2* __restrict__ tasks,
-                                             const SelState* __restrict__ st,
+                                             const int2* __restrict__ tasks, int ntasks, int tpb,
+                                             SelState* __restrict__ st,
                                              uint32_t* __restrict__ hist_all, uint32_t gid_base,
-                                             uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp) {
+                                             uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp,
+                                             const int32_t* __restrict__ keep = nullptr,
+                                             const int32_t* __restrict__ task_lo = nullptr) {
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   using C = PassCfg<PASS>;
@@ -280,38 +316,65 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
   // (copy = lane % CP, bin-major so a bin's copies sit in adjacent banks) split those lanes;
   // passes 1/2 count only the keys under the selected prefix and keep one copy.
   constexpr int CP = PASS == 0 ? LW_HIST_CP : 1;
+  static_assert(!FUSED || PASS > 0, "pass 0 has no previous selection");
   __shared__ uint32_t h[NB * CP];
-  const int2 t = tasks[blockIdx.x];
-  const int li = t.x, begin = t.y;
-  const int s = large_segs[li];
-  const int n = seg_n[s];
-  const int64_t off = seg_off[s];
-  for (int b = threadIdx.x; b < NB * CP; b += NT) h[b] = 0;
-  const uint32_t prefix = PASS > 0 ? st[li].prefix : 0u;
-  __syncthreads();
-  float* gp = g + off;
-  const float* ep = EFADD ? ef + off : nullptr;
-  const int end = min(begin + EPB, n);
+  __shared__ uint32_t sarr[FUSED ? NT : 1], sscr[NT / WAVE], sres[2];
+  // A workgroup takes `tpb` consecutive tasks (LW_HIST_TPB on large launches): zeroing the LDS
+  // histogram (NB * CP words) and merging it into the segment's global one cost about as much LDS
+  // traffic as counting one task's 8192 keys, so they are paid once per segment run of the
+  // workgroup's tasks, not per task; a small launch keeps one task per workgroup so that it
+  // still spreads over the CUs. Integer counts: the result does not depend on the grouping.
+  const int ta = blockIdx.x * tpb, tb = min(ntasks, ta + tpb);
+  auto flush = [&](int li) {
+    uint32_t* gh = hist_all + (size_t)li * HIST_WORDS + C::HOFF;
+    for (int b = threadIdx.x; b < NB; b += NT) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int j = 0; j < CP; ++j) c += h[b * CP + j];
+      if (c) atomicAdd(gh + b, c);
+    }
+  };
+  int cur = -1;
+  uint32_t prefix = 0u;
+  for (int ti = ta; ti < tb; ++ti) {
+    const int2 t = tasks[ti];
+    const int li = t.x, begin = t.y;
+    if (li != cur) {                     // (uniform: the whole workgroup switches segment)
+      if (cur >= 0) {
+        __syncthreads();
+        flush(cur);
+      }
+      __syncthreads();
+      for (int b = threadIdx.x; b < NB * CP; b += NT) h[b] = 0;
+      cur = li;
+      if constexpr (FUSED)
+        fused_prev_select<PASS>(hist_all, st, keep, li, large_segs[li], ti == task_lo[li], prefix,
+                                sarr, sscr, sres);
+      else
+        prefix = PASS > 0 ? st[li].prefix : 0u;
+      __syncthreads();
+    }
+    const int s = large_segs[li];
+    const int n = seg_n[s];
+    const int64_t off = seg_off[s];
+    float* gp = g + off;
+    const float* ep = EFADD ? ef + off : nullptr;
+    const int end = min(begin + EPB, n);
 #pragma unroll 2
-  for (int j = 0; j < EPB / (NT * 4); ++j) {
-    const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
-    if (i0 >= end) break;
-    uint32_t k[4];
-    bool valid[4];
-    load4_keys<KM, EFADD>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid);
+    for (int j = 0; j < EPB / (NT * 4); ++j) {
+      const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
+      if (i0 >= end) break;
+      uint32_t k[4];
+      bool valid[4];
+      load4_keys<KM, EFADD>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid);
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (valid[q] && (k[q] >> (C::SHIFT + C::BITS)) == prefix)
-        atomicAdd(&h[((k[q] >> C::SHIFT) & (NB - 1)) * CP + (threadIdx.x & (CP - 1))], 1u);
+      for (int q = 0; q < 4; ++q)
+        if (valid[q] && (k[q] >> (C::SHIFT + C::BITS)) == prefix)
+          atomicAdd(&h[((k[q] >> C::SHIFT) & (NB - 1)) * CP + (threadIdx.x & (CP - 1))], 1u);
+    }
   }
   __syncthreads();
-  uint32_t* gh = hist_all + (size_t)li * HIST_WORDS + C::HOFF;
-  for (int b = threadIdx.x; b < NB; b += NT) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 0; j < CP; ++j) c += h[b * CP + j];
-    if (c) atomicAdd(gh + b, c);
-  }
+  if (cur >= 0) flush(cur);
 }
 
 template <int KM, int PASS>
@@ -397,6 +460,79 @@ __global__ __launch_bounds__(NT) void k_count(float* __restrict__ g, const float
   block_excl_scan<NT>(cg, scr, tg);
   block_excl_scan<NT>(ce, scr, te);
   if (threadIdx.x == 0) cnt[blockIdx.x] = make_uint2(tg, te);
+}
+
+// Fused chain: the pass-2 digit selection and finish_state (k_select<2>) in every workgroup at a
+// segment switch, then the per-task (gt, eq) counts of k_count for `tpb` tasks per workgroup.
+// The workgroup holding the segment's first task publishes the final state (and counts the
+// Top-K ties that did not fit) for k_scan / k_write.
+template <int KM>
+__global__ __launch_bounds__(NT) void k_count_sel(float* __restrict__ g,
+                                                  const int64_t* __restrict__ seg_off,
+                                                  const int32_t* __restrict__ seg_n,
+                                                  const int32_t* __restrict__ large_segs,
+                                                  const int2* __restrict__ tasks, int ntasks,
+                                                  int tpb, const int32_t* __restrict__ task_lo,
+                                                  SelState* __restrict__ st,
+                                                  const uint32_t* __restrict__ hist_all,
+                                                  const int32_t* __restrict__ keep,
+                                                  const int64_t* __restrict__ cap_off,
+                                                  unsigned long long* __restrict__ overflow,
+                                                  uint2* __restrict__ cnt, uint32_t gid_base,
+                                                  uint32_t step_arg, uint32_t s0, uint32_t s1,
+                                                  const uint32_t* __restrict__ stepp) {
+  const uint32_t step = stepp != nullptr ? *stepp : step_arg;
+  __shared__ uint32_t arr[NT], scr[NT / WAVE], res[2];
+  const int ta = blockIdx.x * tpb, tb = min(ntasks, ta + tpb);
+  int cur = -1;
+  uint32_t tk = 0;
+  for (int ti = ta; ti < tb; ++ti) {
+    const int2 t = tasks[ti];
+    const int li = t.x, begin = t.y;
+    const int s = large_segs[li];
+    if (li != cur) {                     // (uniform across the workgroup)
+      cur = li;
+      const uint32_t* h = hist_all + (size_t)li * HIST_WORDS + PassCfg<2>::HOFF;
+      const uint32_t p1 = st[li].p1;
+      uint32_t d, mn;
+      select_digit<1024>(h, st[li].m1, d, mn, arr, scr, res);
+      SelState S;
+      S.prefix = (p1 << PassCfg<2>::BITS) | d;
+      S.m = mn;
+      S.tkey = S.prefix;
+      const uint32_t hd = h[d];
+      finish_state(S, KM, (uint32_t)keep[s], mn, hd, (uint32_t)(cap_off[s + 1] - cap_off[s]));
+      tk = S.tkey;
+      if (ti == task_lo[li] && threadIdx.x == 0) {
+        SelState& o = st[li];
+        o.prefix = S.prefix; o.m = S.m; o.tkey = S.tkey; o.quota = S.quota;
+        o.cnt_gt = S.cnt_gt; o.total = S.total; o.cap = S.cap;
+        if (KM == KM_TOPK && overflow != nullptr && S.tkey != 0 && hd > S.quota)
+          atomicAdd(overflow, (unsigned long long)(hd - S.quota));
+      }
+    }
+    const int n = seg_n[s];
+    const int64_t off = seg_off[s];
+    float* gp = g + off;
+    const int end = min(begin + EPB, n);
+    uint32_t cg = 0, ce = 0;
+#pragma unroll 2
+    for (int j = 0; j < EPB / (NT * 4); ++j) {
+      const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
+      if (i0 >= end) break;
+      uint32_t k[4];
+      bool valid[4];
+      load4_keys<KM, false>(gp, nullptr, i0, end, gid_base + s, step, s0, s1, k, valid);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (valid[q]) { cg += k[q] > tk; ce += k[q] == tk; }
+    }
+    uint32_t tg, te;
+    block_excl_scan<NT>(cg, scr, tg);
+    block_excl_scan<NT>(ce, scr, te);
+    if (threadIdx.x == 0) cnt[ti] = make_uint2(tg, te);
+    __syncthreads();                     // scr / arr reuse by the next task
+  }
 }
 
 // One workgroup per large segment: exclusive scan of the per-block (gt, eq) counts.
@@ -493,7 +629,11 @@ __global__ __launch_bounds__(NT) void k_fill_tail(int2* __restrict__ pairs,
 }
 
 // Order-preserving compaction. Thread owns EPT contiguous elements.
-template <int KM, int OUT, bool EF>
+// FW (the fused chain): no k_scan — the workgroup adds up the (gt, eq) counts of its segment's
+// earlier tasks itself (`pre` is then the count array); the workgroup of the segment's last task
+// pads the unused pair slots (k_fill_tail) and zeroes the segment's radix histograms for the next
+// call (so the chain needs no k_zero_words; the workspace starts zeroed).
+template <int KM, int OUT, bool EF, bool FW = false>
 __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __restrict__ ef,
                                               const int64_t* __restrict__ seg_off,
                                               const int32_t* __restrict__ seg_n,
@@ -505,7 +645,9 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
                                               int2* __restrict__ pairs, float* __restrict__ vals,
                                               int32_t* __restrict__ idx_out, uint32_t gid_base,
                                               uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp,
-                                              float* __restrict__ mom) {
+                                              float* __restrict__ mom,
+                                              const int32_t* __restrict__ task_lo = nullptr,
+                                              uint32_t* __restrict__ hist_all = nullptr) {
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t scr[NT / WAVE];
@@ -515,7 +657,23 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   const int n = seg_n[s];
   const int64_t off = seg_off[s];
   const SelState S = st[li];
-  const uint2 bp = pre[blockIdx.x];
+  uint2 bp;
+  if constexpr (FW) {
+    uint32_t sg = 0, se = 0;
+    for (int q = task_lo[li] + (int)threadIdx.x; q < (int)blockIdx.x; q += NT) {
+      const uint2 c = pre[q];
+      sg += c.x;
+      se += c.y;
+    }
+    block_excl_scan<NT>(sg, scr, bp.x);
+    block_excl_scan<NT>(se, scr, bp.y);
+    if ((int)blockIdx.x == task_lo[li + 1] - 1) {
+      uint32_t* hz = hist_all + (size_t)li * HIST_WORDS;
+      for (int q = threadIdx.x; q < HIST_WORDS; q += NT) hz[q] = 0u;
+    }
+  } else {
+    bp = pre[blockIdx.x];
+  }
   // momentum factor masking (see k_small_select): only in segments not sent whole
   float* mp = (mom != nullptr && S.total < (uint32_t)n) ? mom + off : nullptr;
   const int64_t c0 = cap_off[s];
@@ -583,6 +741,10 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
     }
     if (EF) ep[i] = sel ? 0.f : v[k];
   }
+  // (k_fill_tail folded in: the workgroup of the segment's last task pads the unused pair slots;
+  // no workgroup writes a slot at or past S.total)
+  if (FW && OUT == OUT_PAIRS && (int)blockIdx.x == task_lo[li + 1] - 1)
+    for (uint32_t q = S.total + threadIdx.x; q < S.cap; q += NT) pairs[c0 + q] = make_int2(SENT, 0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -967,6 +1129,9 @@ __global__ __launch_bounds__(NT) void k_zero_words(uint32_t* __restrict__ p, int
     p[i] = 0u;
 }
 
+static int hist_tpb(int ntasks) { return ntasks >= LW_HIST_TPB_MIN ? LW_HIST_TPB : 1; }
+static int hist_blocks(int ntasks) { return (ntasks + hist_tpb(ntasks) - 1) / hist_tpb(ntasks); }
+
 template <int KM, int OUT, bool EF>
 static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) {
   if (a.n_small > 0)
@@ -975,21 +1140,41 @@ static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) 
               a.seed0, a.seed1, a.step_ptr, a.overflow, a.mom);
   if (a.n_large == 0) return;
   if (!staged) {      // (staged: select_stage already zeroed the histograms and ran pass 0)
-    const int64_t words = (int64_t)HIST_WORDS * a.n_large;
-    const int64_t nb = (words + NT - 1) / NT;
-    LW_LAUNCH(k_zero_words, (int)(nb < 1024 ? nb : 1024), st, a.hist, words);
-    LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
-              a.large_segs, a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+    if (!LW_FUSED_SELECT) {    // (fused: the previous call's k_write left them zeroed)
+      const int64_t words = (int64_t)HIST_WORDS * a.n_large;
+      const int64_t nb = (words + NT - 1) / NT;
+      LW_LAUNCH(k_zero_words, (int)(nb < 1024 ? nb : 1024), st, a.hist, words);
+    }
+    LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), hist_blocks(a.n_tasks), st, a.g, a.ef,
+              a.seg_off, a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
               a.step_ptr);
+  }
+  if (LW_FUSED_SELECT) {
+    // 4 launches instead of 11: the digit selections ride in the next pass's workgroups; the
+    // count scan, the payload tail padding and the histogram reset in k_write
+    LW_LAUNCH((k_hist<KM, 1, false, true>), hist_blocks(a.n_tasks), st, a.g, a.ef, a.seg_off,
+              a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.st_large, a.hist, a.gid_base, a.step,
+              a.seed0, a.seed1, a.step_ptr, a.keep, a.task_lo);
+    LW_LAUNCH((k_hist<KM, 2, false, true>), hist_blocks(a.n_tasks), st, a.g, a.ef, a.seg_off,
+              a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.st_large, a.hist, a.gid_base, a.step,
+              a.seed0, a.seed1, a.step_ptr, a.keep, a.task_lo);
+    LW_LAUNCH((k_count_sel<KM>), hist_blocks(a.n_tasks), st, a.g, a.seg_off, a.seg_n,
+              a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.task_lo, a.st_large, a.hist,
+              a.keep, a.cap_off,
+              a.overflow, a.cnt, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
+    LW_LAUNCH((k_write<KM, OUT, EF, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.large_segs, a.tasks, a.st_large, a.cnt, a.cap_off, a.pairs, a.vals, a.idx_out,
+              a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr, a.mom, a.task_lo, a.hist);
+    return;
   }
   LW_LAUNCH((k_select<KM, 0>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off,
             a.overflow);
-  LW_LAUNCH((k_hist<KM, 1, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
-            a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
+  LW_LAUNCH((k_hist<KM, 1, false>), hist_blocks(a.n_tasks), st, a.g, a.ef, a.seg_off, a.seg_n,
+            a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
   LW_LAUNCH((k_select<KM, 1>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off,
             a.overflow);
-  LW_LAUNCH((k_hist<KM, 2, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
-            a.tasks, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
+  LW_LAUNCH((k_hist<KM, 2, false>), hist_blocks(a.n_tasks), st, a.g, a.ef, a.seg_off, a.seg_n,
+            a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
   LW_LAUNCH((k_select<KM, 2>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off,
             a.overflow);
   LW_LAUNCH((k_count<KM, false>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs,
@@ -1034,16 +1219,16 @@ void select_stage(const SelectArgs& a, int km, bool ef, int t_lo, int t_hi, bool
   const int2* tk = a.tasks + t_lo;
   if (km == KM_TOPK) {
     if (ef)
-      LW_LAUNCH((k_hist<KM_TOPK, 0, true>), t_hi - t_lo, st, a.g, a.ef, a.seg_off, a.seg_n,
-                a.large_segs, tk, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+      LW_LAUNCH((k_hist<KM_TOPK, 0, true>), hist_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
+                a.seg_n, a.large_segs, tk, t_hi - t_lo, hist_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
                 a.step_ptr);
     else
-      LW_LAUNCH((k_hist<KM_TOPK, 0, false>), t_hi - t_lo, st, a.g, a.ef, a.seg_off, a.seg_n,
-                a.large_segs, tk, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+      LW_LAUNCH((k_hist<KM_TOPK, 0, false>), hist_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
+                a.seg_n, a.large_segs, tk, t_hi - t_lo, hist_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
                 a.step_ptr);
   } else {
-    LW_LAUNCH((k_hist<KM_RANDK, 0, false>), t_hi - t_lo, st, a.g, a.ef, a.seg_off, a.seg_n,
-              a.large_segs, tk, a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+    LW_LAUNCH((k_hist<KM_RANDK, 0, false>), hist_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
+              a.seg_n, a.large_segs, tk, t_hi - t_lo, hist_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
               a.step_ptr);
   }
 }

@@ -27,6 +27,9 @@ struct SelState {
   uint32_t total;    // emitted elements
   uint32_t cap;      // payload slots of the segment
   uint32_t pad;
+  // the fused radix chain (compress.hip k_hist_sel / k_count_sel): the digit state after passes
+  // 0 and 1, published by one workgroup for the next launch in fields that launch does not write
+  uint32_t p0, m0, p1, m1;
 };
 
 struct SelectArgs {
@@ -125,6 +128,7 @@ void mc_prep(float* g, float* u, const float* p, const int64_t* seg_off, const i
              const int32_t* segs, const int2* tasks, int n_tasks, const float* seg_wd, float mc,
              float wmul, hipStream_t st);
 void mc_mask(float* u, const float* e, int64_t n, hipStream_t st);
+void step_bump(int64_t* c, hipStream_t st);
 
 // fused BatchNorm (+add) (+ReLU), NHWC (bn.hip)
 struct BNArgs {

@@ -92,8 +92,8 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
 //   u  = mc·u + g'            local velocity
 //   g  = u                    the compressor (and its error-feedback residual) sees the velocity
 // One read of g, u (and p), one write of g and u: it replaces four ATen passes. Products and sums
-// are rounded separately (no fma contraction), as the CPU mirror (parallel/engine.py) computes them. The masking of the
-// velocity at the coordinates that were sent happens inside the select kernels (compress.hip
+// are rounded separately (no fma contraction), as the CPU mirror (parallel/engine.py) computes
+// them. The masking of the velocity at the coordinates that were sent happens inside the select kernels (compress.hip
 // k_small_select / k_write, SelectArgs::mom) or, for the other codecs, in k_mc_mask.
 template <bool WD>
 __global__ __launch_bounds__(SNT) void k_mc_prep(float* __restrict__ g, float* __restrict__ u,
@@ -104,6 +104,10 @@ __global__ __launch_bounds__(SNT) void k_mc_prep(float* __restrict__ g, float* _
                                                  const int2* __restrict__ tasks,
                                                  const float* __restrict__ seg_wd, float mc,
                                                  float wmul) {
+  // Plain * and + under contract(off): __fmul_rn / __fadd_rn are * / + inside the toolchain's
+  // header, where contraction stays on, so after inlining u*mc + g still became one fma (a 1-ulp
+  // difference from the CPU mirror)
+#pragma clang fp contract(off)
   const int2 t = tasks[blockIdx.x];
   const int s = segs[t.x];
   const int n = seg_n[s];
@@ -117,19 +121,19 @@ __global__ __launch_bounds__(SNT) void k_mc_prep(float* __restrict__ g, float* _
       float4 uu = *reinterpret_cast<const float4*>(u + off + i0);
       if (WD && wd != 0.f) {
         const float4 pp = *reinterpret_cast<const float4*>(p + off + i0);
-        gg.x = __fadd_rn(gg.x, __fmul_rn(pp.x, wd)); gg.y = __fadd_rn(gg.y, __fmul_rn(pp.y, wd));
-        gg.z = __fadd_rn(gg.z, __fmul_rn(pp.z, wd)); gg.w = __fadd_rn(gg.w, __fmul_rn(pp.w, wd));
+        gg.x = gg.x + pp.x * wd; gg.y = gg.y + pp.y * wd;
+        gg.z = gg.z + pp.z * wd; gg.w = gg.w + pp.w * wd;
       }
-      uu.x = __fadd_rn(__fmul_rn(uu.x, mc), gg.x); uu.y = __fadd_rn(__fmul_rn(uu.y, mc), gg.y);
-      uu.z = __fadd_rn(__fmul_rn(uu.z, mc), gg.z); uu.w = __fadd_rn(__fmul_rn(uu.w, mc), gg.w);
+      uu.x = uu.x * mc + gg.x; uu.y = uu.y * mc + gg.y;
+      uu.z = uu.z * mc + gg.z; uu.w = uu.w * mc + gg.w;
       *reinterpret_cast<float4*>(u + off + i0) = uu;
       *reinterpret_cast<float4*>(g + off + i0) = uu;
     } else {
       for (int k = 0; k < 4 && i0 + k < end; ++k) {
         const int64_t i = off + i0 + k;
         float x = g[i];
-        if (WD && wd != 0.f) x = __fadd_rn(x, __fmul_rn(p[i], wd));
-        const float v = __fadd_rn(__fmul_rn(u[i], mc), x);
+        if (WD && wd != 0.f) x = x + p[i] * wd;
+        const float v = u[i] * mc + x;
         u[i] = v;
         g[i] = v;
       }
@@ -186,6 +190,16 @@ void sgd_step(const SgdArgs& a, hipStream_t st) {
   else if (a.nesterov) { if (a.first_step) LW_SGD(true, true, true); else LW_SGD(true, true, false); }
   else { if (a.first_step) LW_SGD(true, false, true); else LW_SGD(true, false, false); }
 #undef LW_SGD
+}
+
+// One lane adds 1 to a device counter with a vector store (the step count the Philox streams and
+// the captured select kernels read; bumped in the graph, not by an ATen add).
+__global__ void k_step_bump(int64_t* __restrict__ c) {
+  if (threadIdx.x == 0) c[0] = c[0] + 1;
+}
+
+void step_bump(int64_t* c, hipStream_t st) {
+  hipLaunchKernelGGL(k_step_bump, dim3(1), dim3(64), 0, st, c);
 }
 
 }  // namespace lw

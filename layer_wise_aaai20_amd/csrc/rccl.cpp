@@ -83,7 +83,8 @@ ncclResult_t settle(ncclComm_t comm, ncclResult_t r) {
 // before reaching ncclCommInitRank, after the ranks agreed to create the communicator) would
 // otherwise block this rank inside the init forever; here the init is aborted with
 // ncclCommAbort and the call raises, so the rank reaches the fallback agreement
-// (parallel/comm.py _init_native_agreed). timeout_s <= 0: the blocking ncclCommInitRank.
+// (parallel/comm.py _init_native_agreed); once it completes, the communicator returned is a
+// blocking split of it (below). timeout_s <= 0: the blocking ncclCommInitRank.
 int64_t rccl_init(Tensor uid, int64_t world, int64_t rank, int64_t device, double timeout_s) {
   TORCH_CHECK(uid.device().is_cpu() && uid.scalar_type() == at::kByte &&
                   uid.numel() == NCCL_UNIQUE_ID_BYTES && uid.is_contiguous(),
@@ -117,7 +118,37 @@ int64_t rccl_init(Tensor uid, int64_t world, int64_t rank, int64_t device, doubl
     if (comm != nullptr) ncclCommAbort(comm);
     TORCH_CHECK(false, "RCCL ncclCommInitRankConfig failed: ", ncclGetErrorString(r));
   }
-  return reinterpret_cast<int64_t>(comm);
+  // Every rank is in: trade the non-blocking communicator for a BLOCKING one (a split of it, same
+  // ranks and order). On a non-blocking communicator RCCL may finish a collective's launch
+  // asynchronously, which a HIP-graph capture of the step cannot take (the captured 2-rank
+  // training tests crashed in capture with it); the split is collective over ranks that have all
+  // just finished the init, and is polled against the same deadline.
+  ncclConfig_t bcfg = NCCL_CONFIG_INITIALIZER;
+  bcfg.blocking = 1;
+  ncclComm_t child = nullptr;
+  r = ncclCommSplit(comm, 0, (int)rank, &child, &bcfg);
+  while (r == ncclInProgress) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+    if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) r = ncclInternalError;
+    const double waited =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (r == ncclInProgress && waited > timeout_s) {
+      ncclCommAbort(comm);
+      TORCH_CHECK(false, "ncclCommSplit: not complete after ", waited, " s; aborted");
+    }
+  }
+  if (r == ncclSuccess && child != nullptr) {
+    ncclResult_t cr = ncclSuccess;
+    if (ncclCommGetAsyncError(child, &cr) != ncclSuccess) cr = ncclInternalError;
+    r = cr;
+  }
+  ncclCommAbort(comm);               // (local: the peers drop their own parent the same way)
+  if (r != ncclSuccess || child == nullptr) {
+    if (child != nullptr) ncclCommAbort(child);
+    TORCH_CHECK(false, "RCCL ncclCommSplit (blocking communicator) failed: ",
+                ncclGetErrorString(r == ncclSuccess ? ncclInternalError : r));
+  }
+  return reinterpret_cast<int64_t>(child);
 }
 
 void rccl_destroy(int64_t h) {

@@ -183,7 +183,6 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
 
 
 LAYOUT_TUNER = Tuner("dgrad-layout", "LWAAAI_GEMM_TUNE")
-DGRAD_BLAS = os.environ.get("LWAAAI_DGRAD_BLAS", "0") == "1"
 
 
 def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
@@ -191,26 +190,10 @@ def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
     [out = K][in = N], N-contiguous as a GEMM B operand). Two layouts are timed on first sight:
     W as stored (the kernel's transposing LDS reads), or Wᵀ copied to [N][K] (a few µs: at most
     2048x512) so that both operands are K-contiguous and the LDS-DMA staging and the big tiles
-    apply. ``bst`` (backward statistics) needs the stored layout.
-
-    A dgrad with no fused epilogue (no statistics, no masked addend) is a plain library GEMM, so
-    hipBLASLt (``torch.mm``) can be a third candidate (``LWAAAI_DGRAD_BLAS=1``): it wins some
-    short-K layer-3/4 shapes (``profiles/r3s2/op_roofline_vendor_start.txt``: M50176 N256 K1024
-    33 vs 49 µs), but the whole step gains only 0.3 % (11,354-11,370 vs 11,327-11,328 img/s on one
-    box, ``profiles/r4/dgrad_blas_ab.txt``), so by default every kernel of the step is ours."""
+    apply. ``bst`` (backward statistics) needs the stored layout. (Round 4's opt-in hipBLASLt
+    candidate is gone: every kernel of the step is ours.)"""
     def run(layout, **over):
         args = dict(kw, **over)
-        if layout == "blas":
-            a = dy.as_strided((M, K), (ldy, 1))
-            w = W.reshape(K, N)
-            out, add = args.get("out"), args.get("addend")
-            if add is not None:
-                if out is None:
-                    return torch.addmm(add, a, w), None
-                if out.data_ptr() != add.data_ptr():
-                    out.copy_(add)
-                return out.addmm_(a, w), None
-            return (torch.mm(a, w) if out is None else torch.mm(a, w, out=out)), None
         if layout == "kc":            # Wᵀ by one pack launch, timed with the GEMM
             kp = -(-K // 8) * 8
             wt = load().pack_dgrad_kc(W.reshape(K, N, 1, 1), [0, 0, 1, 1], 1, 1, kp)
@@ -218,10 +201,7 @@ def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
         return gemm(dy, ldy, True, W, N, False, M, N, K, **args)
     if kw.get("bst") is not None:
         return run("nkc")
-    plain = (not kw.get("stats") and kw.get("addend_bits") is None and
-             kw.get("out_bf16", True) and not kw.get("accumulate") and
-             dy.dtype == W.dtype)
-    cands = ("nkc", "kc") + (("blas",) if plain and DGRAD_BLAS else ())
+    cands = ("nkc", "kc")
     key = (M, N, K, kw.get("addend") is not None, kw.get("out") is not None)
     # timed on a scratch output (``out`` may also be the addend: dx += ... in place)
     layout = LAYOUT_TUNER.pick(key, lambda c: run(c, out=None), cands, "nkc")

@@ -218,12 +218,17 @@ def replicated_linear(x, lin, reps: int):
                                                                            False)), reps)
 
 
-def _gemm_ok(x, weight):
-    return x.is_cuda and weight.shape[1] % 8 == 0
-
-
 def mfma_linear(x, weight, bias=None, relu=False, out_fp32=False):
-    if _gemm_ok(x, weight):
+    """Every GPU Linear runs on the MFMA GEMM. The kernels move K in 16-byte chunks, so an
+    in_features that is not a multiple of 8 is zero-padded on both operands (the padded products
+    are exact zeros; autograd slices the padding off the gradients). The CPU path (tests, the
+    CPU mirror of a model) is torch's."""
+    if x.is_cuda:
+        K = weight.shape[1]
+        if K % 8:
+            kp = -(-K // 8) * 8
+            x = F.pad(x, (0, kp - K))
+            weight = F.pad(weight, (0, kp - K))
         return _LinearFn.apply(x, weight, bias, relu, out_fp32)
     y = F.linear(x, weight, bias)
     return F.relu(y) if relu else y

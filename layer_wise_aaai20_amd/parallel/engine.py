@@ -177,12 +177,22 @@ class GradSyncEngine:
         overlap_compress = overlap_compress and os.environ.get("LWAAAI_OVERLAP", "1") != "0"
         self._side = (torch.cuda.Stream(device=self.device)
                       if overlap_compress and self.device.type == "cuda" else None)
-        # inside a captured step: at world 1 the exchange is a no-op and the side-stream branch
-        # only costs (24.67 vs 24.17 ms/step, profiles/r2_graph_overlap_ab.log), so buckets are
-        # compressed inline; at world > 1 each bucket's compression AND its RCCL collective run on
-        # the side branch, overlapped with the rest of backward
-        self._graph_overlap = os.environ.get(
-            "LWAAAI_GRAPH_OVERLAP", "1" if self.world > 1 else "0") == "1"
+        # inside a captured step (LWAAAI_GRAPH_OVERLAP):
+        #   "0"    (default) each bucket is compressed, exchanged and decoded inline on the compute
+        #          stream, in backward order as its gradients complete;
+        #   "comm" compression inline, only the bucket's RCCL collective on a side branch;
+        #   "1"    compression and collective both on the side branch (the round-2..4 default at
+        #          world > 1).
+        # A fork/join pair in a replayed HIP graph costs far more than it hides here: ResNet-50,
+        # simulated world 8, layer-wise Top-K 0.1 % (3 buckets): step exposed over compute-only
+        # 0.36 ms inline, 1.00 ms "1", 1.45 ms "comm" (profiles/r5/sim8_overlap_modes.jsonl;
+        # 1 GPU at world 1: 24.67 vs 24.17 ms/step, profiles/r2_graph_overlap_ab.log). Eager
+        # (uncaptured) steps keep the side stream.
+        mode = os.environ.get("LWAAAI_GRAPH_OVERLAP", "0")
+        if mode not in ("0", "1", "comm"):
+            raise ValueError(f"LWAAAI_GRAPH_OVERLAP={mode!r}: expected 0, 1 or comm")
+        self._graph_overlap = mode != "0"
+        self._comm_only = mode == "comm"
         self._retired = []            # (fence event, events held until it completes)
         self._check = os.environ.get("LWAAAI_ENGINE_CHECK", "0") == "1"
         # bucket collectives on a native RCCL communicator (csrc/rccl.cpp) when the group is
@@ -283,9 +293,9 @@ class GradSyncEngine:
         sel = codec.inner if isinstance(codec, DenseWrap) else codec
         e = self.ef if self.ef is not None else None
         side = self._side
-        if side is not None and not self._graph_overlap and \
+        if side is not None and (not self._graph_overlap or self._comm_only) and \
                 torch.cuda.is_current_stream_capturing():
-            side = None                      # (inline inside a world-1 capture, as _launch)
+            side = None                      # (inline inside a capture, as _launch's compression)
         if side is not None:
             ready = torch.cuda.Event()
             ready.record(torch.cuda.current_stream(self.device))
@@ -429,22 +439,33 @@ class GradSyncEngine:
             # 1 GPU: 24.67 ms/step with it, 24.17 ms without; profiles/r2_graph_overlap_ab.log):
             # the bucket is compressed and exchanged inline on the compute stream
             side = None
+        # "comm" mode inside a capture: compress on the compute stream, fork before the collective
+        late = side is not None and self._comm_only and torch.cuda.is_current_stream_capturing()
+        if self._stages:
+            # slices of parameters that got no gradient (or every slice, after backward: sync_now)
+            # are staged now — on the compute stream's side of the fork below, in order
+            self._stage_in_order(force=True)
         ready = None
-        if side is not None:
+
+        def fork():
             # the event must outlive the side stream's wait on it: it stays in _pending until
             # finish() (a HIP event destroyed while a queued wait still references it faulted
             # the VGG-16 run: hipErrorIllegalAddress, profiles/r2_vgg_fault.md)
-            ready = torch.cuda.Event()
-            ready.record(torch.cuda.current_stream(self.device))
-            side.wait_event(ready)
-        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            side.wait_event(ev)
+            return ev
+
+        if side is not None and not late:
+            ready = fork()
+        with torch.cuda.stream(side) if side is not None and not late else \
+                contextlib.nullcontext():
             t0 = self._event() if self.timing else None
             if self.lr_scaled:
                 e.mul_(self._lr_ratio)                   # residual re-expressed at this step's LR
             u = None
             sel = codec.inner if isinstance(codec, DenseWrap) else codec
             if self._stages:
-                self._stage_in_order(force=True)  # (slices of parameters that got no gradient)
                 sel._staged = True
             if self.mom is not None:
                 u = self.mom[b.start:b.end]
@@ -458,6 +479,9 @@ class GradSyncEngine:
                     self._mc_mask(u, e)
             t1 = self._event() if self.timing else None
             self._payload += codec.last_payload_bytes
+        if late:
+            ready = fork()
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             if codec.collective == "all_reduce":
                 work = (self._native.all_reduce(send) if self._native is not None
                         else comm.all_reduce(send, self.pg))
@@ -511,7 +535,12 @@ class GradSyncEngine:
                 rec.append((bi, t0, t1, tx, t2, self._event()))
         self._pending = []
         if self._dstep is not None:
-            self._dstep.add_(1)
+            from ..ops._ext import ops_for
+            lib = ops_for(self._dstep)
+            if lib is not None:
+                lib.step_bump(self._dstep)          # (a native kernel, no ATen elementwise add)
+            else:
+                self._dstep.add_(1)
         if not torch.cuda.is_available() or not torch.cuda.is_current_stream_capturing():
             self.heartbeat()
         if hold and not torch.cuda.is_current_stream_capturing():

@@ -105,12 +105,29 @@ class LoopbackRccl:
         self.world = peers.world
         self.rank = peers.rank
         self.calls: List[tuple] = []
+        self._frozen_sum = {}
+        self._frozen_cat = {}
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor):
         bi = self.sim.bucket_of(inp)
         self.calls.append(("all_gather", bi))
         parts = self.sim.payloads(bi)
         chunks = out.view(self.world, -1)
+        if self.sim.frozen:
+            # timing mode: the W-1 frozen peer payloads land with one copy (the peers' block of
+            # the output is contiguous around this rank's own chunk), as one RCCL kernel would
+            # write them — not W-1 copy launches
+            cat = self._frozen_cat.get(bi)
+            if cat is None:
+                cat = torch.stack([p.reshape(-1) for p in parts])
+                self._frozen_cat[bi] = cat
+            r = self.rank
+            if r > 0:
+                chunks[:r].copy_(cat[:r])
+            if r < self.world - 1:
+                chunks[r + 1:].copy_(cat[r:])
+            chunks[r].copy_(inp.reshape(-1))
+            return _Done()
         it = iter(parts)
         for r in range(self.world):
             chunks[r].copy_(inp.reshape(-1) if r == self.rank else next(it).reshape(-1))
@@ -123,6 +140,17 @@ class LoopbackRccl:
             raise NotImplementedError("loopback all_reduce: sum only")
         # rank-ordered sum, as a ring/tree would produce bit-identically on every rank only up to
         # fp32 reassociation: RCCL's order is not ours, so the oracle compares with a tolerance
+        if self.sim.frozen:
+            # timing mode: the peers' sum is formed once; a step then pays one pass over the
+            # vector, about the local memory work of a ring all-reduce (its reduce-scatter reads
+            # and adds (W-1)/W of the vector, its all-gather writes it), not W-1 full adds
+            tot = self._frozen_sum.get(bi)
+            if tot is None:
+                tot = torch.stack([p.reshape(-1) for p in self.sim.payloads(bi)]).sum(0)
+                self._frozen_sum[bi] = tot.view_as(t)
+                tot = self._frozen_sum[bi]
+            t.add_(tot)
+            return _Done()
         acc = None
         it = iter(self.sim.payloads(bi))
         for r in range(self.world):

@@ -167,6 +167,15 @@ def test_make_codec_factory_and_auto_wire():
     assert isinstance(codecs.make_codec("QSGD", plan, 2, 0, qstates=255), codecs.QSGDCodec)
     assert isinstance(codecs.make_codec("Topk", plan, 2, 0, K=0.01, wire="dense"),
                       codecs.DenseWrap)
+    # quantisers: codes all-gathered while bytes/element x world <= 8 (all-reduce of the
+    # dequantised fp32 vector past that)
+    for q, w_dense in ((255, 8), (32767, 8), (127, 16)):
+        for w in (2, 4, 8, 16):
+            c = codecs.make_codec("QSGD", plan, w, 0, qstates=q)
+            assert isinstance(c, codecs.DenseWrap) == (w >= w_dense), (q, w, c)
+    assert isinstance(codecs.make_codec("TernGrad", plan, 16, 0), codecs.TernGradCodec)
+    assert isinstance(codecs.make_codec("QSGD", plan, 8, 0, qstates=255, wire="sparse"),
+                      codecs.QSGDCodec)
 
 
 def test_dense_wrap_matches_reference_wire():

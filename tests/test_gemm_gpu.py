@@ -412,3 +412,22 @@ def test_vgg_replicated_fc1_matches_pool_and_full_gemm(monkeypatch):
         out["loss"].float().sum().backward()
         assert m.classifier[0].weight.grad is not None
     assert abs(loss[True] - loss[False]) < 1e-2 * abs(loss[False]), loss
+
+
+def test_linear_with_unaligned_in_features_runs_padded_on_mfma():
+    """in_features % 8 != 0: both operands zero-padded to a multiple of 8 and run on the MFMA
+    GEMM (no vendor fallback); forward and gradients vs fp32 torch, gradient shapes unpadded."""
+    torch.manual_seed(9)
+    x = torch.randn(96, 100, device="cuda").bfloat16().float().requires_grad_()
+    w = torch.randn(40, 100, device="cuda").bfloat16().float().requires_grad_()
+    b = torch.randn(40, device="cuda").requires_grad_()
+    y = G.mfma_linear(x.bfloat16(), w.bfloat16(), b)
+    xr, wr, br = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    yr = xr @ wr.t() + br
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=5e-2)
+    g = torch.randn_like(yr).bfloat16()
+    y.backward(g)
+    yr.backward(g.float())
+    assert x.grad.shape == (96, 100) and w.grad.shape == (40, 100)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=3e-2, atol=1e-1)
+    torch.testing.assert_close(w.grad, wr.grad, rtol=3e-2, atol=1e-1)

@@ -121,7 +121,9 @@ class DenseCodec(Codec):
         return grad
 
     def decompress(self, send, recv, grad, world=None):
-        grad.div_(float(world or self.world))
+        w = int(world or self.world)
+        if w != 1:                              # (world 1: no kernel for a division by 1)
+            grad.div_(float(w))
 
 
 # ================================================================================= Top-K
@@ -259,6 +261,24 @@ class TopkCodec(Codec):
                              self.plan.utasks(grad.device))
             return
         self.unpack_pairs_cpu(gathered, world, grad, self.cap_off)
+
+    def decompress_sgd(self, send, recv, sgd: dict, world=None):
+        """Decode fused with the SGD step of the bucket's parameters (GPU only;
+        ``parallel/engine.py set_fused_sgd``): ``sgd`` holds the bucket's slices of the
+        parameter / momentum / bf16-mirror arenas, its segments' weight decay and the optimizer's
+        hyper-parameters."""
+        world = world or self.world
+        gathered = send if recv is None else recv
+        p = sgd["p"]
+        lib = ops_for(p)
+        if lib is None:
+            raise RuntimeError("decompress_sgd: GPU only")
+        t = self.plan.common(p.device)
+        lib.unpack_pairs_sgd(gathered, world, t["seg_off"], t["seg_n"],
+                             self._dev_tables(p.device)["cap_off"], self.plan.utasks(p.device),
+                             p, sgd["buf"], sgd["seg_wd"], sgd["lr"], sgd["momentum"],
+                             sgd["dampening"], int(sgd["nesterov"]), int(sgd["first"]),
+                             sgd["grad_scale"], sgd["hyper"], sgd["pb"])
 
     def unpack_pairs_cpu(self, gathered, world, grad, cap_off):
         cap_total = gathered.numel() // 2 // world
@@ -762,7 +782,9 @@ class DenseWrap(Codec):
         return grad
 
     def decompress(self, send, recv, grad, world=None):
-        grad.div_(float(world or self.world))
+        w = int(world or self.world)
+        if w != 1:                              # (world 1: no kernel for a division by 1)
+            grad.div_(float(w))
 
 
 # ================================================================================= factory

@@ -273,6 +273,57 @@ void unpack_pairs(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tens
   launched("unpack_pairs");
 }
 
+// decode of a layer-wise Top-K bucket fused with its SGD step (compress.hip k_unpack_sgd): p, buf,
+// pb are the bucket's slices of the parameter / momentum / bf16-mirror arenas, seg_wd the decay of
+// its segments
+void unpack_pairs_sgd(Tensor gathered, int64_t world, Tensor seg_off, Tensor seg_n,
+                      Tensor cap_off, Tensor utasks, Tensor p, Tensor buf, Tensor seg_wd,
+                      double lr, double momentum, double dampening, int64_t nesterov,
+                      int64_t first_step, double grad_scale, c10::optional<Tensor> hyper,
+                      c10::optional<Tensor> pb) {
+  const c10::DeviceGuard guard(p.device());
+  check_cuda(gathered, "gathered");
+  check_cuda(p, "p");
+  check_dtype(p, at::kFloat, "p");
+  check_dtype(seg_wd, at::kFloat, "seg_wd");
+  TORCH_CHECK(world >= 1 && world <= lw::kMaxWorld, "world size out of range");
+  TORCH_CHECK(p.is_contiguous() && seg_wd.is_contiguous(), "unpack_pairs_sgd: contiguous p");
+  lw::SgdArgs a{};
+  a.p = ptr<float>(p);
+  a.g = nullptr;
+  a.buf = nullptr;
+  if (momentum != 0.0) {
+    check_cuda(buf, "buf");
+    TORCH_CHECK(buf.scalar_type() == at::kFloat && buf.numel() == p.numel() && buf.is_contiguous(),
+                "unpack_pairs_sgd: momentum slice must match p");
+    a.buf = ptr<float>(buf);
+  }
+  a.seg_wd = ptr<float>(seg_wd);
+  a.lr = (float)lr;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.grad_scale = (float)grad_scale;
+  a.nesterov = (int)nesterov;
+  a.first_step = (int)first_step;
+  if (hyper.has_value() && hyper->defined()) {
+    check_cuda(*hyper, "hyper");
+    TORCH_CHECK(hyper->scalar_type() == at::kFloat && hyper->numel() >= 2 &&
+                    hyper->is_contiguous(), "hyper must be a contiguous float32 [lr, grad_scale]");
+    a.hyper = hyper->data_ptr<float>();
+  }
+  if (pb.has_value() && pb->defined()) {
+    check_cuda(*pb, "pb");
+    TORCH_CHECK(pb->scalar_type() == kH16 && pb->numel() == p.numel() && pb->is_contiguous(),
+                "pb must be a 16-bit tensor with p's layout");
+    a.pb = reinterpret_cast<uint16_t*>(pb->data_ptr());
+  }
+  const int64_t cap_total = gathered.numel() / 2 / world;
+  lw::unpack_pairs_sgd(ptr<int2>(gathered), cap_total, (int)world, ptr<int64_t>(seg_off),
+                       ptr<int32_t>(seg_n), ptr<int64_t>(cap_off), ptr<int2>(utasks),
+                       (int)(utasks.numel() / 2), a, cur_stream());
+  launched("unpack_pairs_sgd");
+}
+
 void unpack_validx(Tensor vals, Tensor idx, Tensor slot_seg, int64_t world, Tensor g,
                    Tensor seg_off) {
   const c10::DeviceGuard guard(g.device());
@@ -1719,6 +1770,11 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "unpack_pairs(Tensor gathered, int world, Tensor(a!) g, Tensor seg_off, Tensor seg_n, "
       "Tensor cap_off, Tensor utasks) -> ()");
   m.def(
+      "unpack_pairs_sgd(Tensor gathered, int world, Tensor seg_off, Tensor seg_n, Tensor cap_off, "
+      "Tensor utasks, Tensor(a!) p, Tensor(b!) buf, Tensor seg_wd, float lr, float momentum, "
+      "float dampening, int nesterov, int first_step, float grad_scale, Tensor? hyper, "
+      "Tensor(c!)? pb) -> ()");
+  m.def(
       "unpack_validx(Tensor vals, Tensor idx, Tensor slot_seg, int world, Tensor(a!) g, "
       "Tensor seg_off) -> ()");
   m.def(
@@ -1809,6 +1865,7 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("thresh_write", &thresh_write);
   m.impl("thresh_dense", &thresh_dense);
   m.impl("unpack_pairs", &unpack_pairs);
+  m.impl("unpack_pairs_sgd", &unpack_pairs_sgd);
   m.impl("unpack_validx", &unpack_validx);
   m.impl("quantize", &quantize);
   m.impl("dequantize", &dequantize);

@@ -26,6 +26,8 @@
 // forced odd for Random-K (so padding/invalid keys of 0 never win).
 #include "common.h"
 #include "lw_kernels.h"
+#include "elem16.h"
+#include "sgd_elem.h"
 
 namespace lw {
 
@@ -1053,19 +1055,11 @@ __device__ __forceinline__ int wave_lower_bound(const int2* __restrict__ a, int 
 
 constexpr int UCH = kUnpackChunk;   // 4096 elements per workgroup
 
-__global__ __launch_bounds__(NT) void k_unpack_pairs(const int2* __restrict__ gathered,
-                                                     int64_t cap_total, int ws,
-                                                     float* __restrict__ g,
-                                                     const int64_t* __restrict__ seg_off,
-                                                     const int32_t* __restrict__ seg_n,
-                                                     const int64_t* __restrict__ cap_off,
-                                                     const int2* __restrict__ utasks) {
-  __shared__ float acc[UCH];
-  __shared__ int lo_s[kMaxWorld], hi_s[kMaxWorld];
-  const int2 t = utasks[blockIdx.x];
-  const int s = t.x, cb = t.y;
-  const int n = seg_n[s];
-  const int ce = min(cb + UCH, n);
+// Rank-ordered LDS accumulation of every rank's pairs that fall in the 4096-element chunk
+// [cb, ce) of segment s (deterministic: ranks in order, a rank's pairs in index order).
+__device__ __forceinline__ void unpack_acc(const int2* __restrict__ gathered, int64_t cap_total,
+                                           int ws, const int64_t* __restrict__ cap_off, int s,
+                                           int cb, int ce, float* acc, int* lo_s, int* hi_s) {
   const int64_t c0 = cap_off[s];
   const int cap = (int)(cap_off[s + 1] - c0);
   for (int j = threadIdx.x; j < UCH; j += NT) acc[j] = 0.f;
@@ -1085,6 +1079,21 @@ __global__ __launch_bounds__(NT) void k_unpack_pairs(const int2* __restrict__ ga
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(NT) void k_unpack_pairs(const int2* __restrict__ gathered,
+                                                     int64_t cap_total, int ws,
+                                                     float* __restrict__ g,
+                                                     const int64_t* __restrict__ seg_off,
+                                                     const int32_t* __restrict__ seg_n,
+                                                     const int64_t* __restrict__ cap_off,
+                                                     const int2* __restrict__ utasks) {
+  __shared__ float acc[UCH];
+  __shared__ int lo_s[kMaxWorld], hi_s[kMaxWorld];
+  const int2 t = utasks[blockIdx.x];
+  const int s = t.x, cb = t.y;
+  const int ce = min(cb + UCH, seg_n[s]);
+  unpack_acc(gathered, cap_total, ws, cap_off, s, cb, ce, acc, lo_s, hi_s);
   float* gp = g + seg_off[s] + cb;
   const float fws = (float)ws;
   const int len = ce - cb;
@@ -1094,6 +1103,69 @@ __global__ __launch_bounds__(NT) void k_unpack_pairs(const int2* __restrict__ ga
           make_float4(acc[j] / fws, acc[j + 1] / fws, acc[j + 2] / fws, acc[j + 3] / fws);
   } else {
     for (int j = threadIdx.x; j < len; j += NT) gp[j] = acc[j] / fws;
+  }
+}
+
+// Decode and optimizer step in one pass (layer-wise Top-K buckets whose codec segments are the
+// arena's parameters; parallel/engine.py set_fused_sgd): the chunk's averaged gradient goes from
+// LDS straight into the SGD update of the same elements (sgd_elem, as k_sgd) — the dense gradient
+// is neither written by the decode nor read back by the optimizer. `a` points at the bucket:
+// a.p / a.buf / a.pb at its first element, a.seg_wd at its first segment's decay.
+template <bool MOM, bool NEST, bool FIRST>
+__global__ __launch_bounds__(NT) void k_unpack_sgd(const int2* __restrict__ gathered,
+                                                   int64_t cap_total, int ws,
+                                                   const int64_t* __restrict__ seg_off,
+                                                   const int32_t* __restrict__ seg_n,
+                                                   const int64_t* __restrict__ cap_off,
+                                                   const int2* __restrict__ utasks,
+                                                   const SgdArgs a) {
+  __shared__ float acc[UCH];
+  __shared__ int lo_s[kMaxWorld], hi_s[kMaxWorld];
+  const int2 t = utasks[blockIdx.x];
+  const int s = t.x, cb = t.y;
+  const int ce = min(cb + UCH, seg_n[s]);
+  unpack_acc(gathered, cap_total, ws, cap_off, s, cb, ce, acc, lo_s, hi_s);
+  float lr = a.lr, grad_scale = a.grad_scale;
+  if (a.hyper != nullptr) {
+    lr = a.hyper[0];
+    grad_scale = a.hyper[1];
+  }
+  const float wd = a.seg_wd[s];
+  const int64_t off = seg_off[s] + cb;
+  float* pp = a.p + off;
+  float* bp = a.buf + off;
+  uint16_t* hp = a.pb != nullptr ? a.pb + off : nullptr;
+  const float fws = (float)ws;
+  const int len = ce - cb;
+  if (len == UCH && (off & 3) == 0) {
+    for (int j = threadIdx.x * 4; j < UCH; j += NT * 4) {
+      const float4 x4 = *reinterpret_cast<const float4*>(pp + j);
+      float x[4] = {x4.x, x4.y, x4.z, x4.w};
+      float b[4] = {0.f, 0.f, 0.f, 0.f};
+      if (MOM && !FIRST) {
+        const float4 b4 = *reinterpret_cast<const float4*>(bp + j);
+        b[0] = b4.x; b[1] = b4.y; b[2] = b4.z; b[3] = b4.w;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        x[k] = sgd_elem<MOM, NEST, FIRST>(x[k], acc[j + k] / fws, b[k], lr, wd, a.momentum,
+                                          a.dampening, grad_scale);
+      *reinterpret_cast<float4*>(pp + j) = make_float4(x[0], x[1], x[2], x[3]);
+      if (MOM) *reinterpret_cast<float4*>(bp + j) = make_float4(b[0], b[1], b[2], b[3]);
+      if (hp != nullptr)
+        *reinterpret_cast<uint2*>(hp + j) =
+            make_uint2((uint32_t)f2h(x[0]) | ((uint32_t)f2h(x[1]) << 16),
+                       (uint32_t)f2h(x[2]) | ((uint32_t)f2h(x[3]) << 16));
+    }
+  } else {
+    for (int j = threadIdx.x; j < len; j += NT) {
+      float b = MOM && !FIRST ? bp[j] : 0.f;
+      const float x = sgd_elem<MOM, NEST, FIRST>(pp[j], acc[j] / fws, b, lr, wd, a.momentum,
+                                                 a.dampening, grad_scale);
+      pp[j] = x;
+      if (MOM) bp[j] = b;
+      if (hp != nullptr) hp[j] = f2h(x);
+    }
   }
 }
 
@@ -1291,6 +1363,20 @@ void unpack_pairs(const int2* gathered, int64_t cap_total, int ws, float* g, con
   if (n_utasks == 0) return;
   LW_LAUNCH(k_unpack_pairs, n_utasks, st, gathered, cap_total, ws, g, seg_off, seg_n, cap_off,
             utasks);
+}
+
+void unpack_pairs_sgd(const int2* gathered, int64_t cap_total, int ws, const int64_t* seg_off,
+                      const int32_t* seg_n, const int64_t* cap_off, const int2* utasks,
+                      int n_utasks, const SgdArgs& a, hipStream_t st) {
+  if (n_utasks == 0) return;
+  const bool mom = a.momentum != 0.f;
+#define LW_USGD(M, N, F) \
+  LW_LAUNCH((k_unpack_sgd<M, N, F>), n_utasks, st, gathered, cap_total, ws, seg_off, seg_n, \
+            cap_off, utasks, a)
+  if (!mom) LW_USGD(false, false, false);
+  else if (a.nesterov) { if (a.first_step) LW_USGD(true, true, true); else LW_USGD(true, true, false); }
+  else { if (a.first_step) LW_USGD(true, false, true); else LW_USGD(true, false, false); }
+#undef LW_USGD
 }
 
 void unpack_validx(const float* vals, const int32_t* idx, const int32_t* slot_seg, int64_t nslots,

@@ -8,6 +8,7 @@
 #include "common.h"
 #include "lw_kernels.h"
 #include "elem16.h"
+#include "sgd_elem.h"
 
 namespace lw {
 
@@ -52,15 +53,9 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
         b[0] = bb.x; b[1] = bb.y; b[2] = bb.z; b[3] = bb.w;
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float dp = d[k] * grad_scale;
-        if (wd != 0.f) dp = dp + wd * x[k];
-        if (MOM) {
-          b[k] = FIRST ? dp : momentum * b[k] + (1.f - dampening) * dp;
-          dp = NEST ? dp + momentum * b[k] : b[k];
-        }
-        x[k] = x[k] - lr * dp;
-      }
+      for (int k = 0; k < 4; ++k)
+        x[k] = sgd_elem<MOM, NEST, FIRST>(x[k], d[k], b[k], lr, wd, momentum, dampening,
+                                          grad_scale);
       *reinterpret_cast<float4*>(p + off + i0) = make_float4(x[0], x[1], x[2], x[3]);
       if (MOM) *reinterpret_cast<float4*>(buf + off + i0) = make_float4(b[0], b[1], b[2], b[3]);
       if (pb != nullptr)
@@ -70,15 +65,10 @@ __global__ __launch_bounds__(SNT) void k_sgd(float* __restrict__ p, const float*
     } else {
       for (int k = 0; k < 4 && i0 + k < end; ++k) {
         const int64_t i = off + i0 + k;
-        float x = p[i];
-        float dp = g[i] * grad_scale;
-        if (wd != 0.f) dp = dp + wd * x;
-        if (MOM) {
-          const float bv = FIRST ? dp : momentum * buf[i] + (1.f - dampening) * dp;
-          buf[i] = bv;
-          dp = NEST ? dp + momentum * bv : bv;
-        }
-        p[i] = x - lr * dp;
+        float bv = MOM && !FIRST ? buf[i] : 0.f;
+        p[i] = sgd_elem<MOM, NEST, FIRST>(p[i], g[i], bv, lr, wd, momentum, dampening,
+                                          grad_scale);
+        if (MOM) buf[i] = bv;
         if (pb != nullptr) pb[i] = f2h(p[i]);
       }
     }

@@ -78,13 +78,25 @@ ncclResult_t settle(ncclComm_t comm, ncclResult_t r) {
   return r;
 }
 
-// timeout_s > 0: the communicator is created non-blocking (ncclConfig_t.blocking = 0) and its
-// initialisation is polled against a deadline. A peer that never joins (a rank that failed
-// before reaching ncclCommInitRank, after the ranks agreed to create the communicator) would
-// otherwise block this rank inside the init forever; here the init is aborted with
-// ncclCommAbort and the call raises, so the rank reaches the fallback agreement
-// (parallel/comm.py _init_native_agreed); once it completes, the communicator returned is a
-// blocking split of it (below). timeout_s <= 0: the blocking ncclCommInitRank.
+// timeout_s > 0: the blocking ncclCommInitRank runs on a helper thread and this call waits for
+// it against a deadline. A peer that never joins (a rank that failed before reaching the init,
+// after the ranks agreed to create the communicator) would otherwise block this rank inside the
+// init forever; here the call raises instead (the helper thread is left behind, blocked, and its
+// communicator — should the init ever complete — is never used), so the rank reaches the fallback
+// agreement (parallel/comm.py _init_native_agreed). The communicator itself is an ordinary
+// BLOCKING one: on a non-blocking communicator (ncclConfig_t.blocking = 0, tried in round 5) RCCL
+// may finish a collective's launch asynchronously, and the captured 2-rank training steps crashed
+// in capture with it. timeout_s <= 0: the init on this thread, no deadline.
+namespace {
+struct InitJob {
+  std::mutex mu;
+  bool done = false;
+  bool abandoned = false;
+  ncclResult_t r = ncclSuccess;
+  ncclComm_t comm = nullptr;
+};
+}  // namespace
+
 int64_t rccl_init(Tensor uid, int64_t world, int64_t rank, int64_t device, double timeout_s) {
   TORCH_CHECK(uid.device().is_cpu() && uid.scalar_type() == at::kByte &&
                   uid.numel() == NCCL_UNIQUE_ID_BYTES && uid.is_contiguous(),
@@ -94,61 +106,40 @@ int64_t rccl_init(Tensor uid, int64_t world, int64_t rank, int64_t device, doubl
   const c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
   ncclUniqueId id;
   std::memcpy(&id, uid.data_ptr(), NCCL_UNIQUE_ID_BYTES);
-  ncclComm_t comm = nullptr;
   if (timeout_s <= 0) {
+    ncclComm_t comm = nullptr;
     check(ncclCommInitRank(&comm, (int)world, id, (int)rank), "ncclCommInitRank");
     return reinterpret_cast<int64_t>(comm);
   }
-  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = 0;
-  ncclResult_t r = ncclCommInitRankConfig(&comm, (int)world, id, (int)rank, &cfg);
+  auto job = std::make_shared<InitJob>();
+  std::thread([job, id, world, rank, device]() {
+    hipSetDevice((int)device);
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&comm, (int)world, id, (int)rank);
+    std::lock_guard<std::mutex> lk(job->mu);
+    job->r = r;
+    job->comm = comm;
+    job->done = true;
+  }).detach();
   const auto t0 = std::chrono::steady_clock::now();
-  while (r == ncclInProgress && comm != nullptr) {
-    std::this_thread::sleep_for(std::chrono::milliseconds(2));
-    if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) r = ncclInternalError;
-    const double waited =
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (r == ncclInProgress && waited > timeout_s) {
-      ncclCommAbort(comm);
-      TORCH_CHECK(false, "ncclCommInitRank: not complete after ", waited,
-                  " s (a peer rank never joined); communicator aborted");
+  for (;;) {
+    {
+      std::lock_guard<std::mutex> lk(job->mu);
+      if (job->done) {
+        TORCH_CHECK(job->r == ncclSuccess, "RCCL ncclCommInitRank failed: ",
+                    ncclGetErrorString(job->r));
+        return reinterpret_cast<int64_t>(job->comm);
+      }
+      const double waited =
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (waited > timeout_s) {
+        job->abandoned = true;
+        TORCH_CHECK(false, "ncclCommInitRank: not complete after ", waited,
+                    " s (a peer rank never joined); communicator abandoned");
+      }
     }
-  }
-  if (r != ncclSuccess) {
-    if (comm != nullptr) ncclCommAbort(comm);
-    TORCH_CHECK(false, "RCCL ncclCommInitRankConfig failed: ", ncclGetErrorString(r));
-  }
-  // Every rank is in: trade the non-blocking communicator for a BLOCKING one (a split of it, same
-  // ranks and order). On a non-blocking communicator RCCL may finish a collective's launch
-  // asynchronously, which a HIP-graph capture of the step cannot take (the captured 2-rank
-  // training tests crashed in capture with it); the split is collective over ranks that have all
-  // just finished the init, and is polled against the same deadline.
-  ncclConfig_t bcfg = NCCL_CONFIG_INITIALIZER;
-  bcfg.blocking = 1;
-  ncclComm_t child = nullptr;
-  r = ncclCommSplit(comm, 0, (int)rank, &child, &bcfg);
-  while (r == ncclInProgress) {
     std::this_thread::sleep_for(std::chrono::milliseconds(2));
-    if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) r = ncclInternalError;
-    const double waited =
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (r == ncclInProgress && waited > timeout_s) {
-      ncclCommAbort(comm);
-      TORCH_CHECK(false, "ncclCommSplit: not complete after ", waited, " s; aborted");
-    }
   }
-  if (r == ncclSuccess && child != nullptr) {
-    ncclResult_t cr = ncclSuccess;
-    if (ncclCommGetAsyncError(child, &cr) != ncclSuccess) cr = ncclInternalError;
-    r = cr;
-  }
-  ncclCommAbort(comm);               // (local: the peers drop their own parent the same way)
-  if (r != ncclSuccess || child == nullptr) {
-    if (child != nullptr) ncclCommAbort(child);
-    TORCH_CHECK(false, "RCCL ncclCommSplit (blocking communicator) failed: ",
-                ncclGetErrorString(r == ncclSuccess ? ncclInternalError : r));
-  }
-  return reinterpret_cast<int64_t>(child);
 }
 
 void rccl_destroy(int64_t h) {

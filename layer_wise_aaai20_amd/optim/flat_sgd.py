@@ -50,6 +50,9 @@ class FlatSGD(Optimizer):
         self.device_hyper = False
         self._hyper = None
         self._hyper_host = None
+        # segments a GradSyncEngine updates itself, fused with their decode (set_fused_sgd)
+        self._exclude = frozenset()
+        self._sub = None
 
     # torch.optim.SGD-compatible state: momentum_buffer views into the flat buffer
     def _bind_state(self):
@@ -69,6 +72,27 @@ class FlatSGD(Optimizer):
                     wd[self._seg_of[id(p)]] = g["weight_decay"]
             self._wd_cache = (key, torch.from_numpy(wd).to(device))
         return self._wd_cache[1]
+
+    def exclude_segments(self, segs) -> None:
+        """Leave arena segments ``segs`` to the gradient engine's fused decode-and-step
+        (``GradSyncEngine.set_fused_sgd``): :meth:`step` updates the others only."""
+        self._exclude = frozenset(int(i) for i in segs)
+        self._sub = None
+
+    def _tables(self, device):
+        """(plan tables, per-table-segment weight decay) over the segments step() updates."""
+        wd = self._seg_wd(device)
+        if not self._exclude:
+            return self.plan.all_large_tables(device), wd
+        if self._sub is None or self._sub[0] is not wd:
+            keep = [s for s in self.arena.segments if s.index not in self._exclude]
+            if not keep:
+                self._sub = (wd, None, None)
+            else:
+                plan = SegPlan([s.offset for s in keep], [s.numel for s in keep])
+                idx = torch.tensor([s.index for s in keep], dtype=torch.long, device=device)
+                self._sub = (wd, plan.all_large_tables(device), wd[idx].contiguous())
+        return self._sub[1], self._sub[2]
 
     def _uniform(self, k):
         vals = {g[k] for g in self.param_groups}
@@ -115,13 +139,14 @@ class FlatSGD(Optimizer):
         if self.device_hyper and not torch.cuda.is_current_stream_capturing():
             self.load_hyper()
         if lib is not None:
-            t = self.plan.all_large_tables(p.device)
+            t, wd = self._tables(p.device)
             # the bf16 weight mirror the next forward reads is written by the same kernel
             # (master -> model copy of fp16util.py:103-138 fused: no separate cast pass)
             pb = getattr(self.arena, "param_bf16", None)
-            lib.sgd_step(p, g, self.buf, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], wd, lr,
-                         mom, damp, int(nest), int(self._first), float(self.grad_scale),
-                         self._hyper if self.device_hyper else None, pb)
+            if t is not None:        # (None: every segment was stepped with its decode)
+                lib.sgd_step(p, g, self.buf, t["seg_off"], t["seg_n"], t["segs"], t["tasks"], wd,
+                             lr, mom, damp, int(nest), int(self._first), float(self.grad_scale),
+                             self._hyper if self.device_hyper else None, pb)
             if pb is not None:
                 self.arena.mark_bf16_fresh()
         else:

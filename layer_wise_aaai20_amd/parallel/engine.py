@@ -29,7 +29,7 @@ import torch.distributed as dist
 from . import comm
 from .arena import Bucket, GradArena, plan_buckets
 from ..compress import reference as ref
-from ..compress.codecs import Codec, DenseCodec, DenseWrap, make_codec
+from ..compress.codecs import Codec, DenseCodec, DenseWrap, TopkCodec, make_codec
 from ..compress.plan import SegPlan
 
 MODES = ("layerwise", "entiremodel", "none")
@@ -167,6 +167,8 @@ class GradSyncEngine:
             for i in range(b.seg_lo, b.seg_hi):
                 self.seg_bucket[i] = b.index
         self._plan_stages(cap)
+        self._sgd = None                 # set_fused_sgd: decode + optimizer step in one pass
+        self._sgd_buckets = frozenset()
         self.step = 0
         self.stats = SyncStats(dense_bytes=self.arena.numel * 4, buckets=len(self.buckets))
         self.timing = timing and self.device.type == "cuda"
@@ -320,6 +322,54 @@ class GradSyncEngine:
         for g in opt.param_groups:
             g["weight_decay"] = 0.0
         self._mc_plans = {}
+
+    def set_fused_sgd(self, opt) -> int:
+        """Decode the layer-wise Top-K buckets straight into the SGD step of ``opt`` (a
+        :class:`FlatSGD` over this engine's arena): each 4096-element chunk's averaged gradient
+        goes from LDS into the update of the same parameters (``csrc/compress.hip
+        k_unpack_sgd``), so the dense gradient is neither written by the decode nor read back by
+        the optimizer, and ``opt.step()`` then updates only the other
+        buckets' segments. Same arithmetic as the separate passes (``csrc/sgd_elem.h``;
+        tests/test_fused_sgd_gpu.py pins it bit for bit).
+
+        Needs the trainer's order of operations: the step's LR set before backward (a captured
+        step reads it from ``opt``'s device hyper tensor), ``opt.step()`` after backward. Returns
+        the number of buckets fused (0: nothing changes)."""
+        self._sgd, self._sgd_buckets = None, frozenset()
+        if self.device.type != "cuda" or self.arena.param_buf is None or \
+                os.environ.get("LWAAAI_FUSED_SGD", "1") == "0":
+            opt.exclude_segments(())
+            return 0
+        fused, segs = [], []
+        for bi, b in enumerate(self.buckets):
+            c = self.codecs[bi]
+            if type(c) is not TopkCodec or self.mode != "layerwise":
+                continue
+            plan = self.plans[bi]
+            ours = self.arena.segments[b.seg_lo:b.seg_hi]
+            if plan.S != len(ours) or any(int(plan.offsets[i]) != s.offset - b.start or
+                                          int(plan.sizes[i]) != s.numel
+                                          for i, s in enumerate(ours)):
+                continue
+            fused.append(bi)
+            segs.extend(range(b.seg_lo, b.seg_hi))
+        opt.exclude_segments(segs)
+        if fused:
+            self._sgd, self._sgd_buckets = opt, frozenset(fused)
+        return len(fused)
+
+    def _sgd_args(self, bi: int) -> dict:
+        opt, b = self._sgd, self.buckets[bi]
+        pb = getattr(self.arena, "param_bf16", None)
+        hyper = opt._hyper if (opt.device_hyper and opt._hyper is not None and
+                               torch.cuda.is_current_stream_capturing()) else None
+        return dict(p=self.arena.param_buf[b.start:b.end], buf=opt.buf[b.start:b.end],
+                    pb=pb[b.start:b.end] if pb is not None else None,
+                    seg_wd=opt._seg_wd(self.device)[b.seg_lo:b.seg_hi],
+                    lr=float(opt._uniform("lr")), momentum=float(opt._uniform("momentum")),
+                    dampening=float(opt._uniform("dampening")),
+                    nesterov=bool(opt._uniform("nesterov")), first=bool(opt._first),
+                    grad_scale=float(opt.grad_scale), hyper=hyper)
 
     def _mc_plan(self, bi: int):
         """The bucket's arena segments (a plan of its own: in entire-model mode the codec sees
@@ -530,7 +580,10 @@ class GradSyncEngine:
                         t.record_stream(cur)
             t2 = self._event() if self.timing else None
             b = self.buckets[bi]
-            self.codecs[bi].decompress(send, recv, self.arena.grad[b.start:b.end])
+            if bi in self._sgd_buckets:
+                self.codecs[bi].decompress_sgd(send, recv, self._sgd_args(bi))
+            else:
+                self.codecs[bi].decompress(send, recv, self.arena.grad[b.start:b.end])
             if self.timing:
                 rec.append((bi, t0, t1, tx, t2, self._event()))
         self._pending = []

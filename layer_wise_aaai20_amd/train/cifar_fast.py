@@ -62,6 +62,8 @@ class CifarTrainer:
             self.ddp.engine.set_mc_weight_decay(self.opt)
         if ef_lr_scaled:
             self.ddp.engine.lr_source = self.opt.lr_device
+        # layer-wise Top-K buckets: decode and SGD step in one pass (step() sets the LR first)
+        self.ddp.engine.set_fused_sgd(self.opt)
         ds = D.synthetic_cifar10(n_train, n_test, seed, task=task, amp=amp)
         x = D.transpose(D.normalise(D.pad(ds["train"]["data"], 4)))
         tx = D.transpose(D.normalise(ds["test"]["data"]))

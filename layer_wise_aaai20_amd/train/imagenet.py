@@ -151,5 +151,7 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
                   weight_decay=weight_decay, grad_scale=1.0 / float(loss_scale))
     if mc > 0:               # weight decay enters the velocity (and leaves the optimizer)
         ddp.engine.set_mc_weight_decay(opt)
+    # layer-wise Top-K buckets: decode and SGD step in one pass (the LR is set before each step)
+    ddp.engine.set_fused_sgd(opt)
     return ImageNetTrainer(ddp, opt, device, tdtype, graph=graph, graph_warmup=graph_warmup,
                            graph_auto=graph_auto, loss_scale=loss_scale)

@@ -27,6 +27,7 @@ def _worker(rank, world, port, fn, outdir, args, env):
         os.environ["NCCL_HOSTID"] = f"lwaaai-rank{rank}"
     import faulthandler
     import sys
+    faulthandler.enable(file=sys.stderr)          # a rank's fatal signal names its Python frame
     # a rank stuck in a collective prints every thread's stack before the harness gives up on it
     faulthandler.dump_traceback_later(int(os.environ.get("LWAAAI_TEST_STACK_AFTER", "100")),
                                       exit=False, file=sys.stderr)

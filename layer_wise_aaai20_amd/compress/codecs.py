@@ -67,6 +67,7 @@ class Codec:
     # device step counter (GradSyncEngine._dstep) the Philox-keyed kernels read instead of the
     # host `step` argument, so a replayed HIP graph draws fresh random keys every step
     step_t = None
+    uses_step = False           # reads the device step counter step_t (Philox-keyed codecs)
     # device int32 counter of elements the reference rule selects that the payload could not
     # carry (Top-K ties beyond the slack, threshold hits beyond a fixed sparse capacity); they
     # stay in the error-feedback residual (GradSyncEngine.read_overflow)
@@ -274,9 +275,8 @@ class TopkCodec(Codec):
         if lib is None:
             raise RuntimeError("decompress_sgd: GPU only")
         t = self.plan.common(p.device)
-        lib.unpack_pairs_sgd(gathered, world, t["seg_off"], t["seg_n"],
-                             self._dev_tables(p.device)["cap_off"], self.plan.utasks(p.device),
-                             p, sgd["buf"], sgd["seg_wd"], sgd["lr"], sgd["momentum"],
+        lib.unpack_pairs_sgd(gathered, world, t["seg_off"], self._dev_tables(p.device)["cap_off"],
+                             sgd["tasks"], p, sgd["buf"], sgd["seg_wd"], sgd["lr"], sgd["momentum"],
                              sgd["dampening"], int(sgd["nesterov"]), int(sgd["first"]),
                              sgd["grad_scale"], sgd["hyper"], sgd["pb"])
 
@@ -299,6 +299,7 @@ class RandkSparseCodec(TopkCodec):
     """Random-K with explicit indices (masks need not be rank-coherent)."""
     name = "randk-sparse"
     km = KM_RANDK
+    uses_step = True
     # Philox masks keyed by the device step counter (step_t): replays draw fresh masks. (Its
     # round-2 replay divergence was the runtime memset node that reset the radix histogram,
     # profiles/r3_graph_divergence_root_cause.md; graph == eager bit for bit since.)
@@ -548,6 +549,7 @@ class ThresholdCodec(TopkCodec):
 class _QuantCodec(Codec):
     collective = "all_gather"
     graph_safe = True           # stochastic rounding keyed by the device step counter (step_t)
+    uses_step = True
     q = Q_TERN
     tag = philox.TAG_TERNGRAD
     qstates = 1
@@ -761,6 +763,7 @@ class DenseWrap(Codec):
     def __init__(self, inner: Codec):
         super().__init__(inner.plan, inner.world, inner.rank, inner.seed, inner.error_feedback)
         self.inner = inner
+        self.uses_step = inner.uses_step
         self.name = f"dense({inner.name})"
 
     @property

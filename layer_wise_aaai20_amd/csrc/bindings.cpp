@@ -276,8 +276,8 @@ void unpack_pairs(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tens
 // decode of a layer-wise Top-K bucket fused with its SGD step (compress.hip k_unpack_sgd): p, buf,
 // pb are the bucket's slices of the parameter / momentum / bf16-mirror arenas, seg_wd the decay of
 // its segments
-void unpack_pairs_sgd(Tensor gathered, int64_t world, Tensor seg_off, Tensor seg_n,
-                      Tensor cap_off, Tensor utasks, Tensor p, Tensor buf, Tensor seg_wd,
+void unpack_pairs_sgd(Tensor gathered, int64_t world, Tensor seg_off, Tensor cap_off,
+                      Tensor ftasks, Tensor p, Tensor buf, Tensor seg_wd,
                       double lr, double momentum, double dampening, int64_t nesterov,
                       int64_t first_step, double grad_scale, c10::optional<Tensor> hyper,
                       c10::optional<Tensor> pb) {
@@ -318,9 +318,13 @@ void unpack_pairs_sgd(Tensor gathered, int64_t world, Tensor seg_off, Tensor seg
     a.pb = reinterpret_cast<uint16_t*>(pb->data_ptr());
   }
   const int64_t cap_total = gathered.numel() / 2 / world;
+  check_cuda(ftasks, "ftasks");
+  check_dtype(ftasks, at::kInt, "ftasks");
+  TORCH_CHECK(ftasks.dim() == 2 && ftasks.size(1) == 4 && ftasks.is_contiguous(),
+              "unpack_pairs_sgd: ftasks must be a contiguous [T, 4] int32 table");
   lw::unpack_pairs_sgd(ptr<int2>(gathered), cap_total, (int)world, ptr<int64_t>(seg_off),
-                       ptr<int32_t>(seg_n), ptr<int64_t>(cap_off), ptr<int2>(utasks),
-                       (int)(utasks.numel() / 2), a, cur_stream());
+                       ptr<int64_t>(cap_off), reinterpret_cast<const int4*>(ftasks.data_ptr()),
+                       (int)ftasks.size(0), a, cur_stream());
   launched("unpack_pairs_sgd");
 }
 
@@ -1770,8 +1774,8 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "unpack_pairs(Tensor gathered, int world, Tensor(a!) g, Tensor seg_off, Tensor seg_n, "
       "Tensor cap_off, Tensor utasks) -> ()");
   m.def(
-      "unpack_pairs_sgd(Tensor gathered, int world, Tensor seg_off, Tensor seg_n, Tensor cap_off, "
-      "Tensor utasks, Tensor(a!) p, Tensor(b!) buf, Tensor seg_wd, float lr, float momentum, "
+      "unpack_pairs_sgd(Tensor gathered, int world, Tensor seg_off, Tensor cap_off, "
+      "Tensor ftasks, Tensor(a!) p, Tensor(b!) buf, Tensor seg_wd, float lr, float momentum, "
       "float dampening, int nesterov, int first_step, float grad_scale, Tensor? hyper, "
       "Tensor(c!)? pb) -> ()");
   m.def(

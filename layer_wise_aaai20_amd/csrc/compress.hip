@@ -1106,31 +1106,31 @@ __global__ __launch_bounds__(NT) void k_unpack_pairs(const int2* __restrict__ ga
   }
 }
 
-// Decode and optimizer step in one pass (layer-wise Top-K buckets whose codec segments are the
-// arena's parameters; parallel/engine.py set_fused_sgd): the chunk's averaged gradient goes from
-// LDS straight into the SGD update of the same elements (sgd_elem, as k_sgd) — the dense gradient
-// is neither written by the decode nor read back by the optimizer. `a` points at the bucket:
-// a.p / a.buf / a.pb at its first element, a.seg_wd at its first segment's decay.
+// Decode and optimizer step in one pass (Top-K buckets; parallel/engine.py set_fused_sgd): the
+// chunk's averaged gradient goes from LDS straight into the SGD update of the same elements
+// (sgd_elem, as k_sgd) — the dense gradient is neither written by the decode nor read back by the
+// optimizer. A task {codec segment, chunk begin, chunk end, parameter} never crosses a parameter
+// (entire-model buckets: chunks are cut at the arena's segment boundaries), so its weight decay
+// is a.seg_wd[parameter]. `a` points at the bucket: a.p / a.buf / a.pb at its first element,
+// a.seg_wd at its first parameter.
 template <bool MOM, bool NEST, bool FIRST>
 __global__ __launch_bounds__(NT) void k_unpack_sgd(const int2* __restrict__ gathered,
                                                    int64_t cap_total, int ws,
                                                    const int64_t* __restrict__ seg_off,
-                                                   const int32_t* __restrict__ seg_n,
                                                    const int64_t* __restrict__ cap_off,
-                                                   const int2* __restrict__ utasks,
+                                                   const int4* __restrict__ ftasks,
                                                    const SgdArgs a) {
   __shared__ float acc[UCH];
   __shared__ int lo_s[kMaxWorld], hi_s[kMaxWorld];
-  const int2 t = utasks[blockIdx.x];
-  const int s = t.x, cb = t.y;
-  const int ce = min(cb + UCH, seg_n[s]);
+  const int4 t = ftasks[blockIdx.x];
+  const int s = t.x, cb = t.y, ce = t.z;
   unpack_acc(gathered, cap_total, ws, cap_off, s, cb, ce, acc, lo_s, hi_s);
   float lr = a.lr, grad_scale = a.grad_scale;
   if (a.hyper != nullptr) {
     lr = a.hyper[0];
     grad_scale = a.hyper[1];
   }
-  const float wd = a.seg_wd[s];
+  const float wd = a.seg_wd[t.w];
   const int64_t off = seg_off[s] + cb;
   float* pp = a.p + off;
   float* bp = a.buf + off;
@@ -1366,13 +1366,13 @@ void unpack_pairs(const int2* gathered, int64_t cap_total, int ws, float* g, con
 }
 
 void unpack_pairs_sgd(const int2* gathered, int64_t cap_total, int ws, const int64_t* seg_off,
-                      const int32_t* seg_n, const int64_t* cap_off, const int2* utasks,
-                      int n_utasks, const SgdArgs& a, hipStream_t st) {
-  if (n_utasks == 0) return;
+                      const int64_t* cap_off, const int4* ftasks, int n_ftasks, const SgdArgs& a,
+                      hipStream_t st) {
+  if (n_ftasks == 0) return;
   const bool mom = a.momentum != 0.f;
 #define LW_USGD(M, N, F) \
-  LW_LAUNCH((k_unpack_sgd<M, N, F>), n_utasks, st, gathered, cap_total, ws, seg_off, seg_n, \
-            cap_off, utasks, a)
+  LW_LAUNCH((k_unpack_sgd<M, N, F>), n_ftasks, st, gathered, cap_total, ws, seg_off, cap_off, \
+            ftasks, a)
   if (!mom) LW_USGD(false, false, false);
   else if (a.nesterov) { if (a.first_step) LW_USGD(true, true, true); else LW_USGD(true, true, false); }
   else { if (a.first_step) LW_USGD(true, false, true); else LW_USGD(true, false, false); }

@@ -121,12 +121,12 @@ struct SgdArgs {
   uint16_t* pb;                // optional bf16 mirror of p (same layout), written in the same pass
 };
 void sgd_step(const SgdArgs& a, hipStream_t st);
-// decode of a layer-wise Top-K bucket fused with the SGD step of its elements (compress.hip
-// k_unpack_sgd; `a` points at the bucket: p / buf / pb / seg_wd offset to its first element /
-// segment, g unused)
+// decode of a Top-K bucket fused with the SGD step of its elements (compress.hip k_unpack_sgd;
+// ftasks: {codec segment, chunk begin, chunk end, parameter}; `a` points at the bucket: p / buf /
+// pb / seg_wd offset to its first element / parameter, g unused)
 void unpack_pairs_sgd(const int2* gathered, int64_t cap_total, int ws, const int64_t* seg_off,
-                      const int32_t* seg_n, const int64_t* cap_off, const int2* utasks,
-                      int n_utasks, const SgdArgs& a, hipStream_t st);
+                      const int64_t* cap_off, const int4* ftasks, int n_ftasks, const SgdArgs& a,
+                      hipStream_t st);
 // momentum correction (optim.hip): the compressor prologue g' = g + wmul·wd·p, u = mc·u + g',
 // g = u over a bucket's arena segments (p / seg_wd null: no weight decay), and the velocity masking
 // u = 0 where e == 0 for codecs without a selection

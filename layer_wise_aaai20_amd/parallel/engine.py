@@ -324,7 +324,7 @@ class GradSyncEngine:
         self._mc_plans = {}
 
     def set_fused_sgd(self, opt) -> int:
-        """Decode the layer-wise Top-K buckets straight into the SGD step of ``opt`` (a
+        """Decode the Top-K buckets straight into the SGD step of ``opt`` (a
         :class:`FlatSGD` over this engine's arena): each 4096-element chunk's averaged gradient
         goes from LDS into the update of the same parameters (``csrc/compress.hip
         k_unpack_sgd``), so the dense gradient is neither written by the decode nor read back by
@@ -340,17 +340,35 @@ class GradSyncEngine:
                 os.environ.get("LWAAAI_FUSED_SGD", "1") == "0":
             opt.exclude_segments(())
             return 0
+        from ..compress.plan import UNPACK_CHUNK
         fused, segs = [], []
+        self._sgd_tasks = {}
         for bi, b in enumerate(self.buckets):
             c = self.codecs[bi]
-            if type(c) is not TopkCodec or self.mode != "layerwise":
+            if type(c) is not TopkCodec:
                 continue
             plan = self.plans[bi]
             ours = self.arena.segments[b.seg_lo:b.seg_hi]
-            if plan.S != len(ours) or any(int(plan.offsets[i]) != s.offset - b.start or
-                                          int(plan.sizes[i]) != s.numel
-                                          for i, s in enumerate(ours)):
-                continue
+            rows = []
+            if self.mode == "layerwise":
+                if plan.S != len(ours) or any(int(plan.offsets[i]) != s.offset - b.start or
+                                              int(plan.sizes[i]) != s.numel
+                                              for i, s in enumerate(ours)):
+                    continue
+                for i, s in enumerate(ours):
+                    rows += [(i, cb, min(cb + UNPACK_CHUNK, s.numel), i)
+                             for cb in range(0, s.numel, UNPACK_CHUNK)]
+            else:
+                # one codec segment over the bucket: chunks cut at every parameter's bounds, so
+                # each task has one weight decay
+                if plan.S != 1 or int(plan.offsets[0]) != 0:
+                    continue
+                for i, s in enumerate(ours):
+                    lo, hi = s.offset - b.start, s.offset - b.start + s.numel
+                    rows += [(0, cb, min(cb + UNPACK_CHUNK, hi), i)
+                             for cb in range(lo, hi, UNPACK_CHUNK)]
+            self._sgd_tasks[bi] = torch.tensor(rows, dtype=torch.int32,
+                                               device=self.device).reshape(-1, 4)
             fused.append(bi)
             segs.extend(range(b.seg_lo, b.seg_hi))
         opt.exclude_segments(segs)
@@ -363,7 +381,8 @@ class GradSyncEngine:
         pb = getattr(self.arena, "param_bf16", None)
         hyper = opt._hyper if (opt.device_hyper and opt._hyper is not None and
                                torch.cuda.is_current_stream_capturing()) else None
-        return dict(p=self.arena.param_buf[b.start:b.end], buf=opt.buf[b.start:b.end],
+        return dict(tasks=self._sgd_tasks[bi],
+                    p=self.arena.param_buf[b.start:b.end], buf=opt.buf[b.start:b.end],
                     pb=pb[b.start:b.end] if pb is not None else None,
                     seg_wd=opt._seg_wd(self.device)[b.seg_lo:b.seg_hi],
                     lr=float(opt._uniform("lr")), momentum=float(opt._uniform("momentum")),
@@ -587,7 +606,7 @@ class GradSyncEngine:
             if self.timing:
                 rec.append((bi, t0, t1, tx, t2, self._event()))
         self._pending = []
-        if self._dstep is not None:
+        if self._dstep is not None and any(c.uses_step for c in self.codecs):
             from ..ops._ext import ops_for
             lib = ops_for(self._dstep)
             if lib is not None:

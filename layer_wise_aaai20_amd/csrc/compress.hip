@@ -336,6 +336,15 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
       if (c) atomicAdd(gh + b, c);
     }
   };
+  // Exact zeros (a ReLU / dropout layer's weight gradient is full of them: VGG-16's 103 M-weight
+  // classifier input) all land in bin 0 and would serialise every wave's LDS atomic on one word;
+  // a thread counts them in a register and adds its count once per segment run (Top-K keys only:
+  // Random-K keys are odd, never 0).
+  uint32_t zc = 0;
+  auto add_zeros = [&]() {
+    if (zc) atomicAdd(&h[threadIdx.x & (CP - 1)], zc);
+    zc = 0;
+  };
   int cur = -1;
   uint32_t prefix = 0u;
   for (int ti = ta; ti < tb; ++ti) {
@@ -343,6 +352,7 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
     const int li = t.x, begin = t.y;
     if (li != cur) {                     // (uniform: the whole workgroup switches segment)
       if (cur >= 0) {
+        add_zeros();
         __syncthreads();
         flush(cur);
       }
@@ -371,10 +381,13 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
       load4_keys<KM, EFADD>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (valid[q] && (k[q] >> (C::SHIFT + C::BITS)) == prefix)
-          atomicAdd(&h[((k[q] >> C::SHIFT) & (NB - 1)) * CP + (threadIdx.x & (CP - 1))], 1u);
+        if (valid[q] && (k[q] >> (C::SHIFT + C::BITS)) == prefix) {
+          if (KM != KM_RANDK && k[q] == 0u) ++zc;
+          else atomicAdd(&h[((k[q] >> C::SHIFT) & (NB - 1)) * CP + (threadIdx.x & (CP - 1))], 1u);
+        }
     }
   }
+  add_zeros();
   __syncthreads();
   if (cur >= 0) flush(cur);
 }

@@ -58,6 +58,7 @@ def test_cifar_graph_step_fused_sgd_bitwise():
     outs = []
     for flag in ("0", "1"):
         os.environ["LWAAAI_FUSED_SGD"] = flag
+        torch.manual_seed(0)                        # (the same initial weights for both runs)
         try:
             tr = CifarTrainer(device="cuda", n_train=512 * 6, graph=True, network="resnet9",
                               compress="layerwise", method="Topk", K=0.01, error_feedback=True,

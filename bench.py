@@ -127,6 +127,30 @@ class _Heartbeat:
         self._stop.set()
 
 
+def _reference_key(args) -> str:
+    """accuracy_reference.json's name for this run's method ('' when it has none)."""
+    if args.compress == "none" or args.method == "none":
+        return "none"
+    if args.compress != "layerwise" or args.method != "Topk" or args.ratio != 0.001:
+        return ""
+    return ("topk0.1%" + ("+ef" if args.ef else "") + ("+mc" if args.momentum_correction else "")
+            + ("+dense4k" if args.ef_dense_below == 4096 else ""))
+
+
+def _reference_mean(steps: int, key: str):
+    """(3-seed mean, per-seed top-1) of ``key`` at this step budget from accuracy_reference.json,
+    or (None, None)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "layer_wise_aaai20_amd",
+                        "train", "accuracy_reference.json")
+    try:
+        with open(path) as f:
+            ref = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    v = ref.get("methods", {}).get(key) if int(ref.get("steps", -1)) == int(steps) else None
+    return (v["mean"], v["top1"]) if v else (None, None)
+
+
 def _reference_points(steps: int) -> str:
     """Reference points for the printed top-1, measured at the same step budget over several
     seeds (layer_wise_aaai20_amd/train/accuracy_reference.json, folded by scripts/acc_reference.py
@@ -291,6 +315,11 @@ def main():
         "data": "synthetic (class-conditional random uint8 224x224 images, pool of 4 batches; "
                 "random-init weights)",
         "top1": acc["top1"] if acc else None,
+        # the same method's 3-seed mean at this budget (this run is seed 0 of it)
+        "top1_3seed_mean": (_reference_mean(acc["steps"], _reference_key(args))[0]
+                            if acc else None),
+        "top1_3seed": (_reference_mean(acc["steps"], _reference_key(args))[1]
+                       if acc else None),
         "top1_note": (f"held-out top-1 (%) of a fresh ResNet-50 trained {acc['steps']} steps with "
                       f"the same compression at {acc['image_size']} px, {acc['per_gpu_batch']}/GPU "
                       f"(linear LR warm-up, graph step, kernel choices pinned by the shipped "

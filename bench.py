@@ -322,7 +322,8 @@ def main():
                        if acc else None),
         "top1_note": (f"held-out top-1 (%) of a fresh ResNet-50 trained {acc['steps']} steps with "
                       f"the same compression at {acc['image_size']} px, {acc['per_gpu_batch']}/GPU "
-                      f"(linear LR warm-up, graph step, kernel choices pinned by the shipped "
+                      f"(linear LR warm-up to 1.0 at batch 512, linear decay to 0, graph step, "
+                      f"kernel choices pinned by the shipped "
                       f"gfx950 tuning table) on the class-conditional synthetic task; "
                       f"chance 0.1%; top-5 {acc['top5']}%; train loss {acc['loss_first20']} -> "
                       f"{acc['loss_last20']} (train/accuracy.py)" + _reference_points(acc['steps'])

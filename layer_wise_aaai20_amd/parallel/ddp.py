@@ -162,6 +162,12 @@ class CompressedDDP(nn.Module):
         if not (self.broadcast_buffers and self._buffers_list) or eng._native is None or \
                 eng._side is None or eng.world <= 1:
             return None
+        if eng.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            # a captured step broadcasts inline at the forward's start, as the reference: a
+            # side-stream broadcast would only be joined by the NEXT forward, i.e. never inside
+            # this capture — an unjoined branch at capture end crashed (SIGSEGV in capture_end)
+            # or hung the 2-rank captured training tests
+            return None
         return eng._side
 
     def _broadcast_after_forward(self, side) -> None:

@@ -11,10 +11,13 @@ import sys
 def main():
     src = sys.argv[1]
     dst = sys.argv[2] if len(sys.argv) > 2 else "layer_wise_aaai20_amd/train/accuracy_reference.json"
-    by, steps = {}, None
+    by, steps, sched = {}, None, None
     for line in open(src):
         d = json.loads(line)
         steps = d["steps"] if steps is None else steps
+        sc = {k: d.get(k) for k in ("peak_lr_512", "warmup", "decay", "momentum")}
+        sched = sc if sched is None else sched
+        assert sc == sched, "one schedule per table"
         assert d["steps"] == steps, "one step budget per table"
         by.setdefault(d["method"], []).append((d.get("seed", 0), d["top1"]))
     methods = {}
@@ -24,7 +27,8 @@ def main():
                       "stdev": round(statistics.stdev(top), 3) if len(top) > 1 else 0.0,
                       "seeds": [s for s, _ in sorted(runs)], "top1": top}
     with open(dst, "w") as f:
-        json.dump({"steps": steps, "source": src, "methods": methods}, f, indent=1)
+        json.dump({"steps": steps, "source": src, "schedule": sched, "methods": methods}, f,
+                  indent=1)
     print(json.dumps(methods, indent=1))
 
 

@@ -9,8 +9,10 @@ convolutions, CompressedDDP compression inline in the HIP-graph step, and FlatSG
 
 * data: bench.py's class-conditional synthetic ImageNet (uint8 noise plus a per-class colour
   offset, 1000 classes), 128 px;
-* schedule: the reference's first phase, a linear LR warm-up then constant
-  (``train_imagenet_nv.py:204-218``);
+* schedule: a linear LR warm-up (the reference's first phase, ``train_imagenet_nv.py:204-218``)
+  to a peak of 1.0 at batch 512, then a linear decay to 0 — calibrated so that the uncompressed
+  run is the ceiling (``train/accuracy.py`` PEAK_LR_512 / DECAY,
+  ``profiles/r5/acc_schedule_sweep.jsonl``), the same for every method;
 * evaluation: held-out top-1 / top-5 on fresh batches of the same distribution.
 
 The methods are compared at the same step budget:
@@ -58,9 +60,10 @@ def main():
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--size", type=int, default=128)
     ap.add_argument("--batch", type=int, default=256)
-    ap.add_argument("--lr", type=float, default=2.0, help="peak LR at batch 512 (phase 0)")
+    from layer_wise_aaai20_amd.train.accuracy import DECAY, PEAK_LR_512
+    ap.add_argument("--lr", type=float, default=PEAK_LR_512, help="peak LR at batch 512")
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--decay", default="none", choices=["none", "linear"],
+    ap.add_argument("--decay", default=DECAY, choices=["none", "linear"],
                     help="after the warm-up: constant LR, or a linear decay to 0")
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--eval-batches", type=int, default=8)

@@ -207,7 +207,8 @@ class TopkCodec(Codec):
                                 t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
                                 self._workspace(grad.device, lib), self.km, OUT_PAIRS, out, None,
                                 None, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
-                                self.step_t, self.overflow, self.mc_mom, self._staged)
+                                self.step_t, self.overflow, self.mc_mom, self._staged,
+                                self.plan.max_large_tasks())
             return out
         self._compress_cpu(grad, ef, step, out)
         return out
@@ -354,7 +355,8 @@ class RandkCodec(RandkSparseCodec):
                                 t["small_segs"], t["large_segs"], t["tasks"], t["task_lo"],
                                 self._workspace(grad.device, lib), KM_RANDK, OUT_VALIDX, None,
                                 vals, idx, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
-                                self.step_t, None, self.mc_mom, self._staged)
+                                self.step_t, None, self.mc_mom, self._staged,
+                                self.plan.max_large_tasks())
             return vals
         for s, x in self._segs(grad):
             o, n = int(self.plan.offsets[s]), int(self.plan.sizes[s])

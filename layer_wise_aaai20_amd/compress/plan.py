@@ -113,6 +113,14 @@ class SegPlan:
         )
         return t
 
+    def max_large_tasks(self) -> int:
+        """The most 8192-element tasks of one large (> SMALL_MAX) segment (0: none)."""
+        if not hasattr(self, "_max_large_tasks"):
+            _, large = self.split(SMALL_MAX)
+            self._max_large_tasks = max([-(-int(self.sizes[s]) // LARGE_EPB) for s in large],
+                                        default=0)
+        return self._max_large_tasks
+
     def utasks(self, device):
         return self.dev(torch.device(device), "utasks", lambda: torch.from_numpy(self.unpack_tasks()))
 

@@ -167,10 +167,11 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
                      c10::optional<Tensor> pairs, c10::optional<Tensor> vals,
                      c10::optional<Tensor> idx, int64_t gid_base, int64_t step, int64_t seed,
                      c10::optional<Tensor> step_t, c10::optional<Tensor> overflow,
-                     c10::optional<Tensor> mom, bool staged) {
+                     c10::optional<Tensor> mom, bool staged, int64_t max_seg_tasks) {
   const c10::DeviceGuard guard(g.device());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, keep, cap_off, small_segs, large_segs,
                                       tasks, task_lo, ws);
+  a.max_seg_tasks = (int)max_seg_tasks;
   if (mom.has_value() && mom->defined()) {
     check_cuda(*mom, "mom");
     check_dtype(*mom, at::kFloat, "mom");
@@ -1749,7 +1750,7 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
       "Tensor(c!) ws, int km, int out, Tensor(d!)? pairs, Tensor(e!)? vals, Tensor(f!)? idx, "
       "int gid_base, int step, int seed, Tensor? step_t=None, Tensor(g!)? overflow=None, "
-      "Tensor(h!)? mom=None, bool staged=False) -> ()");
+      "Tensor(h!)? mom=None, bool staged=False, int max_seg_tasks=0) -> ()");
   m.def(
       "select_stage(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor keep, "
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "

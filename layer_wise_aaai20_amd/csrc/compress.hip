@@ -39,6 +39,9 @@ static_assert((LW_HIST_CP & (LW_HIST_CP - 1)) == 0, "LW_HIST_CP: a power of two"
 #ifndef LW_FUSED_SELECT
 #define LW_FUSED_SELECT 1        // 0: the 9-launch chain (k_select per pass, k_count, k_fill_tail)
 #endif
+#ifndef LW_FW_SCAN_MAX
+#define LW_FW_SCAN_MAX 512       // k_write sums its segment's earlier task counts up to this many
+#endif
 #ifndef LW_HIST_TPB
 #define LW_HIST_TPB 4            // 8192-element tasks per histogram workgroup (see k_hist) once a
 #endif                           // launch has LW_HIST_TPB_MIN tasks; 1 below that
@@ -644,10 +647,12 @@ __global__ __launch_bounds__(NT) void k_fill_tail(int2* __restrict__ pairs,
 }
 
 // Order-preserving compaction. Thread owns EPT contiguous elements.
-// FW (the fused chain): no k_scan — the workgroup adds up the (gt, eq) counts of its segment's
-// earlier tasks itself (`pre` is then the count array); the workgroup of the segment's last task
-// pads the unused pair slots (k_fill_tail) and zeroes the segment's radix histograms for the next
-// call (so the chain needs no k_zero_words; the workspace starts zeroed).
+// FW (the fused chain): the workgroup of the segment's last task pads the unused pair slots
+// (k_fill_tail) and zeroes the segment's radix histograms for the next call (so the chain needs
+// no k_zero_words; the workspace starts zeroed). With prefix_from_cnt there is no k_scan either:
+// the workgroup adds up the (gt, eq) counts of its segment's earlier tasks itself (`pre` is then
+// the count array) — O(tasks²) loads per segment, so only when no segment has more than
+// LW_FW_SCAN_MAX tasks (VGG-16's 103 M-weight layer has 12.6 k: it keeps k_scan).
 template <int KM, int OUT, bool EF, bool FW = false>
 __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __restrict__ ef,
                                               const int64_t* __restrict__ seg_off,
@@ -662,7 +667,8 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
                                               uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp,
                                               float* __restrict__ mom,
                                               const int32_t* __restrict__ task_lo = nullptr,
-                                              uint32_t* __restrict__ hist_all = nullptr) {
+                                              uint32_t* __restrict__ hist_all = nullptr,
+                                              int prefix_from_cnt = 0) {
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t scr[NT / WAVE];
@@ -673,7 +679,7 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   const int64_t off = seg_off[s];
   const SelState S = st[li];
   uint2 bp;
-  if constexpr (FW) {
+  if (FW && prefix_from_cnt) {
     uint32_t sg = 0, se = 0;
     for (int q = task_lo[li] + (int)threadIdx.x; q < (int)blockIdx.x; q += NT) {
       const uint2 c = pre[q];
@@ -682,12 +688,12 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
     }
     block_excl_scan<NT>(sg, scr, bp.x);
     block_excl_scan<NT>(se, scr, bp.y);
-    if ((int)blockIdx.x == task_lo[li + 1] - 1) {
-      uint32_t* hz = hist_all + (size_t)li * HIST_WORDS;
-      for (int q = threadIdx.x; q < HIST_WORDS; q += NT) hz[q] = 0u;
-    }
   } else {
     bp = pre[blockIdx.x];
+  }
+  if (FW && (int)blockIdx.x == task_lo[li + 1] - 1) {
+    uint32_t* hz = hist_all + (size_t)li * HIST_WORDS;
+    for (int q = threadIdx.x; q < HIST_WORDS; q += NT) hz[q] = 0u;
   }
   // momentum factor masking (see k_small_select): only in segments not sent whole
   float* mp = (mom != nullptr && S.total < (uint32_t)n) ? mom + off : nullptr;
@@ -1235,8 +1241,8 @@ static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) 
               a.step_ptr);
   }
   if (LW_FUSED_SELECT) {
-    // 4 launches instead of 11: the digit selections ride in the next pass's workgroups; the
-    // count scan, the payload tail padding and the histogram reset in k_write
+    // 4-5 launches instead of 11: the digit selections ride in the next pass's workgroups; the
+    // payload tail padding, the histogram reset and (short segments) the count scan in k_write
     LW_LAUNCH((k_hist<KM, 1, false, true>), hist_blocks(a.n_tasks), st, a.g, a.ef, a.seg_off,
               a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.st_large, a.hist, a.gid_base, a.step,
               a.seed0, a.seed1, a.step_ptr, a.keep, a.task_lo);
@@ -1247,9 +1253,14 @@ static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) 
               a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.task_lo, a.st_large, a.hist,
               a.keep, a.cap_off,
               a.overflow, a.cnt, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr);
+    const bool own_prefix = a.max_seg_tasks > 0 && a.max_seg_tasks <= LW_FW_SCAN_MAX;
+    if (!own_prefix)
+      LW_LAUNCH((k_scan<KM>), a.n_large, st, a.cnt, a.pre, a.task_lo, a.st_large,
+                (int32_t*)nullptr);
     LW_LAUNCH((k_write<KM, OUT, EF, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
-              a.large_segs, a.tasks, a.st_large, a.cnt, a.cap_off, a.pairs, a.vals, a.idx_out,
-              a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr, a.mom, a.task_lo, a.hist);
+              a.large_segs, a.tasks, a.st_large, own_prefix ? a.cnt : a.pre, a.cap_off, a.pairs,
+              a.vals, a.idx_out, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr, a.mom,
+              a.task_lo, a.hist, own_prefix ? 1 : 0);
     return;
   }
   LW_LAUNCH((k_select<KM, 0>), a.n_large, st, a.hist, a.st_large, a.large_segs, a.keep, a.cap_off,

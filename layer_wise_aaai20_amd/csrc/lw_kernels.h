@@ -44,6 +44,7 @@ struct SelectArgs {
   const int2* tasks;           // [n_tasks] (large index, begin)
   const int32_t* task_lo;      // [n_large+1]
   int n_small, n_large, n_tasks;
+  int max_seg_tasks;           // most tasks of one large segment (0: unknown)
   // scratch
   uint32_t* hist;              // [n_large*4096]
   SelState* st_small;          // [n_small]

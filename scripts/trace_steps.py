@@ -1,7 +1,9 @@
 #!/usr/bin/env python
-"""Steady-state per-step breakdown from a rocprofv3 kernel_trace.csv: step boundaries are the
-fused-SGD kernel launches (one per step); only the last N steps are summarised, so MIOpen's
-find-mode search in the warm-up does not pollute the numbers."""
+"""Steady-state per-step breakdown from a rocprofv3 kernel_trace.csv: step boundaries are a
+kernel launched once per step — the arena SGD (`k_sgd<`), or, when every bucket's step is fused
+into its decode (k_unpack_sgd), the input kernel (CIFAR augmentation / ImageNet normalisation);
+only the last N steps are summarised, so MIOpen's find-mode search in the warm-up does not
+pollute the numbers."""
 import csv
 import re
 import sys
@@ -13,7 +15,11 @@ from prof_summary import CATS  # noqa: E402
 def main(path, last=5, verbose=False):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    sgd = [i for i, r in enumerate(rows) if "k_sgd" in r["Kernel_Name"]]
+    sgd = []
+    for marker in (r"k_sgd<", r"k_cifar_augment", r"k_normalize_u8"):
+        sgd = [i for i, r in enumerate(rows) if re.search(marker, r["Kernel_Name"])]
+        if len(sgd) >= last + 1:
+            break
     if len(sgd) < last + 1:
         raise SystemExit(f"only {len(sgd)} steps in trace")
     lo, hi = sgd[-last - 1] + 1, sgd[-1] + 1

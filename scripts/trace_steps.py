@@ -15,11 +15,23 @@ from prof_summary import CATS  # noqa: E402
 def main(path, last=5, verbose=False):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    sgd = []
-    for marker in (r"k_sgd<", r"k_cifar_augment", r"k_normalize_u8"):
-        sgd = [i for i, r in enumerate(rows) if re.search(marker, r["Kernel_Name"])]
-        if len(sgd) >= last + 1:
-            break
+    sgd = [i for i, r in enumerate(rows) if re.search(r"k_sgd<", r["Kernel_Name"])]
+    if len(sgd) < last + 1:
+        # every bucket's step fused into its decode: the step is the period of the replayed
+        # graph's kernel-name sequence (the smallest P whose last `last` periods are identical)
+        # (the run may end with a few non-step kernels: trim up to 1000 from the end)
+        names = [r["Kernel_Name"] for r in rows]
+        for trim in range(0, min(1001, len(names) // 2), 25):
+            n = len(names) - trim
+            for P in range(8, n // (last + 1) + 1):
+                if names[n - 1] != names[n - 1 - P]:
+                    continue
+                tail = names[n - P:n]
+                if all(names[n - (k + 1) * P:n - k * P] == tail for k in range(1, last + 1)):
+                    sgd = [n - 1 - k * P for k in range(last, -1, -1)]
+                    break
+            if sgd:
+                break
     if len(sgd) < last + 1:
         raise SystemExit(f"only {len(sgd)} steps in trace")
     lo, hi = sgd[-last - 1] + 1, sgd[-1] + 1

@@ -79,9 +79,25 @@ class Codec:
     # entire-model staging (GradSyncEngine): codecs with `stage` run their first pass per arena
     # slice during backward; `_staged` tells compress() that pass is done for this step
     _staged = False
+    # in-place all-gather (GradSyncEngine sets it with a stream-ordered native communicator): the
+    # payload is written straight into this rank's row of a persistent [world, payload] buffer,
+    # which is then the collective's output — RCCL's in-place form, no local copy of our own row
+    inplace_gather = False
 
     def can_stage(self) -> bool:
         return False
+
+    def _inplace_slot(self, device, n: int, dtype, zero: bool = False) -> torch.Tensor:
+        """This rank's row of the persistent in-place all-gather buffer ([world * n])."""
+        if not hasattr(self, "_gather"):
+            self._gather = {}
+        k = str(device)
+        buf = self._gather.get(k)
+        if buf is None or buf.numel() != self.world * n:
+            buf = (torch.zeros if zero else torch.empty)(self.world * n, dtype=dtype,
+                                                         device=device)
+            self._gather[k] = buf
+        return buf[self.rank * n:(self.rank + 1) * n]
 
     def __init__(self, plan: SegPlan, world: int, rank: int, seed: int = 0,
                  error_feedback: bool = False):
@@ -97,6 +113,11 @@ class Codec:
 
     def recv_buffer(self, send: torch.Tensor) -> Optional[torch.Tensor]:
         if self.collective == "all_gather":
+            buf = getattr(self, "_gather", {}).get(str(send.device))
+            if buf is not None and buf.dtype == send.dtype and \
+                    send.data_ptr() == buf.data_ptr() + self.rank * send.numel() * \
+                    send.element_size():
+                return buf                       # (in place: send is our row of it)
             return torch.empty(send.numel() * self.world, dtype=send.dtype, device=send.device)
         return None
 
@@ -173,6 +194,8 @@ class TopkCodec(Codec):
         return self._ws[k]
 
     def send_buffer(self, device):
+        if self.inplace_gather:
+            return self._inplace_slot(device, 2 * max(self.cap_total, 1), torch.int32)
         k = str(device)
         if k not in self._send:
             self._send[k] = torch.empty(2 * max(self.cap_total, 1), dtype=torch.int32,
@@ -568,6 +591,8 @@ class _QuantCodec(Codec):
         self._send = {}
 
     def send_buffer(self, device):
+        if self.inplace_gather:
+            return self._inplace_slot(device, self.words, torch.int32, zero=True)
         k = str(device)
         if k not in self._send:
             self._send[k] = torch.zeros(self.words, dtype=torch.int32, device=device)

@@ -211,6 +211,7 @@ class GradSyncEngine:
         if self._native is not None and self.world > 1 and comm.comm_timeout() > 0:
             self._watch = (getattr(self._native, "watch", None) or
                            self._native.start_watchdog(comm.comm_timeout()))
+        self._set_inplace_gather()
         self._reset_state()
         self.all_reduced_last = True
         self.verify_plan()
@@ -422,6 +423,13 @@ class GradSyncEngine:
             u[o:o + n].mul_(self.mc).add_(g[o:o + n])
             g[o:o + n].copy_(u[o:o + n])
 
+    def _set_inplace_gather(self) -> None:
+        """All-gather codecs write their payload into their row of the collective's output when
+        the communicator is a stream-ordered native one (RCCL's in-place all-gather; the loopback
+        stand-in then copies only the peers' rows). c10d keeps separate buffers."""
+        for c in self.codecs:
+            c.inplace_gather = self._native is not None and c.collective == "all_gather"
+
     def use_communicator(self, native) -> None:
         """Route the bucket collectives through ``native`` (a :class:`~.comm.NativeRccl`-like
         object: stream-ordered ``all_gather(out, inp)`` / ``all_reduce(t)`` / ``broadcast``),
@@ -432,6 +440,7 @@ class GradSyncEngine:
             raise ValueError(f"communicator world {w} != engine world {self.world}")
         self._native = native
         self._stream_waitable = True
+        self._set_inplace_gather()
 
     # ----------------------------------------------------------------- state machine
     def _reset_state(self):

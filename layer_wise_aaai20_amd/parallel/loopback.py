@@ -126,11 +126,16 @@ class LoopbackRccl:
                 chunks[:r].copy_(cat[:r])
             if r < self.world - 1:
                 chunks[r + 1:].copy_(cat[r:])
-            chunks[r].copy_(inp.reshape(-1))
+            if inp.data_ptr() != chunks[r].data_ptr():       # (in place: already there)
+                chunks[r].copy_(inp.reshape(-1))
             return _Done()
         it = iter(parts)
         for r in range(self.world):
-            chunks[r].copy_(inp.reshape(-1) if r == self.rank else next(it).reshape(-1))
+            if r == self.rank:
+                if inp.data_ptr() != chunks[r].data_ptr():
+                    chunks[r].copy_(inp.reshape(-1))
+            else:
+                chunks[r].copy_(next(it).reshape(-1))
         return _Done()
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum"):

@@ -27,6 +27,9 @@ def main(path, last=5, verbose=False):
                 if names[n - 1] != names[n - 1 - P]:
                     continue
                 tail = names[n - P:n]
+                # (a step, not a repeated block inside one: the period holds the optimizer step)
+                if not any("k_unpack_sgd" in x or "k_sgd<" in x for x in tail):
+                    continue
                 if all(names[n - (k + 1) * P:n - k * P] == tail for k in range(1, last + 1)):
                     sgd = [n - 1 - k * P for k in range(last, -1, -1)]
                     break

@@ -36,25 +36,31 @@ FLOOR = {("none", "layerwise"): 0.35}
 DEFAULT_FLOOR = 0.2
 
 
-def run_short(method, kw, mode, seed=0, steps=STEPS):
+PEAK = 0.4            # peak LR of the short schedule (summed loss, per-sample LR = PEAK / batch)
+
+
+def run_short(method, kw, mode, seed=0, steps=STEPS, amp=None, peak=None):
     """One short run; returns (held-out accuracy, mean loss of the first / last 20 steps)."""
+    amp = AMP if amp is None else amp
+    peak = PEAK if peak is None else peak
     from layer_wise_aaai20_amd.data import cifar as D
     from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
     from layer_wise_aaai20_amd.utils.logging import PiecewiseLinear
     torch.manual_seed(seed)
     tr = CifarTrainer("resnet9", compress=mode if method != "none" else "none", method=method,
                       error_feedback=method != "none", batch_size=BATCH, epochs=2,
-                      n_train=BATCH * 50, n_test=16, seed=seed, task="textures", amp=AMP, **kw)
+                      n_train=BATCH * 50, n_test=16, seed=seed, task="textures", amp=amp, **kw)
     tr.steps_per_epoch = 1                           # schedule in steps: warm-up, decay to 0
     # entire-model TernGrad scales the ternary code by max|g| over all 6.6 M parameters, so its
     # variance dwarfs ||g||²: it trains at a quarter of the peak LR
-    peak = 0.1 if (method, mode) == ("TernGrad", "entiremodel") else 0.4
+    if (method, mode) == ("TernGrad", "entiremodel"):
+        peak = peak / 4
     tr.sched = PiecewiseLinear([0, steps // 5, steps], [0, peak, 0])
     losses = [float(tr.step()) / tr.bs for _ in range(steps)]
     first, last = sum(losses[:20]) / 20, sum(losses[-20:]) / 20
     if not all(v == v for v in losses):
         return float("nan"), first, last
-    ds = D.synthetic_cifar10(16, 2048, seed=1000 + seed, task="textures", amp=AMP)["test"]
+    ds = D.synthetic_cifar10(16, 2048, seed=1000 + seed, task="textures", amp=amp)["test"]
     x = torch.from_numpy(D.transpose(D.normalise(ds["data"]))).cuda()
     x = x.contiguous(memory_format=torch.channels_last)
     y = torch.as_tensor(ds["labels"]).cuda()

@@ -564,6 +564,8 @@ class GradSyncEngine:
                 work = (self._native.all_reduce(send) if self._native is not None
                         else comm.all_reduce(send, self.pg))
                 recv = None
+            elif self.world == 1:
+                recv, work = None, comm._Done()       # (one rank: decode straight from send)
             else:
                 recv = codec.recv_buffer(send)
                 work = (self._native.all_gather(recv, send) if self._native is not None

@@ -13,7 +13,8 @@ Reported per configuration (one JSON line):
 
 * ``ms_per_step`` — the simulated world-W step (HIP graph replay);
 * ``ms_compute_only`` — the same model and batch with no compression and no exchange (world 1,
-  method none): forward, backward and SGD only;
+  method none): forward, backward and SGD only; both timed in alternating windows (3 rounds,
+  medians) in one process;
 * ``exposed_ms`` / ``exposed_pct`` — their difference, as a share of the simulated step: the
   compression / decode work not hidden behind backward plus the in-memory exchange. The xGMI
   transfer itself is not in it: ``xgmi_model_ms`` prices the last bucket's exchange (the one that
@@ -44,6 +45,20 @@ def _time(step: Callable[[], None], warmup: int, steps: int) -> float:
         step()
     torch.cuda.synchronize()
     return (time.perf_counter() - t0) / steps * 1e3
+
+
+def _alternate(step_a: Callable[[], None], step_b: Callable[[], None], warmup: int, steps: int,
+               rounds: int = 3):
+    """Median ms/step of two steps timed in alternating windows (A B A B ...): the difference of
+    two configurations is then measured under the same clock / thermal state, which one-shot
+    windows on different boxes were not (the same simulated AlexNet step read 0.845 and
+    0.866 ms)."""
+    import statistics
+    ta, tb = [], []
+    for r in range(rounds):
+        ta.append(_time(step_a, warmup if r == 0 else 2, steps))
+        tb.append(_time(step_b, warmup if r == 0 else 2, steps))
+    return statistics.median(ta), statistics.median(tb)
 
 
 def _frozen_peers(engine, world: int, seed: int = 0, scale: float = 1e-3):
@@ -99,16 +114,15 @@ def simulate_imagenet(world: int, device, steps: int = 10, warmup: int = 6, mode
     common = dict(model=model, device=dev, dtype=dtype, bucket_cap_mb=bucket_mb, lr=0.1,
                   graph=True, graph_warmup=2, graph_auto=False)
     base = build_trainer(compress="none", method="none", world_size=1, **common)
-    t_base = _time(lambda: base.step(x, t), warmup, steps)
-    del base
-    torch.cuda.empty_cache()
     tr = build_trainer(compress=compress, method=method, K=K, qstates=qstates,
                        error_feedback=error_feedback, wire=wire, world_size=world,
                        dense_below=dense_below, momentum_correction=momentum_correction,
                        **common)
     eng = tr.ddp.engine
     _frozen_peers(eng, world)
-    t_sim = _time(lambda: tr.step(x, t), warmup, steps)
+    t_base, t_sim = _alternate(lambda: base.step(x, t), lambda: tr.step(x, t), warmup, steps)
+    del base
+    torch.cuda.empty_cache()
     replays = tr.graph_replays
     eng.timing = True
     tr.step(x, t)
@@ -138,14 +152,13 @@ def simulate_cifar(world: int, device, name: str, cfg: Dict, steps: int = 30,
     base = CifarTrainer(device=dev, n_train=512 * 12, graph=True, network=cfg["network"],
                         compress="none", method="none")
     base.graphed.warmup = 2
-    t_base = _time(lambda: base.step(), warmup, steps)
-    del base
-    torch.cuda.empty_cache()
     tr = CifarTrainer(device=dev, n_train=512 * 12, graph=True, world_size=world, **cfg)
     tr.graphed.warmup = 2
     eng = tr.ddp.engine
     _frozen_peers(eng, world)
-    t_sim = _time(lambda: tr.step(), warmup, steps)
+    t_base, t_sim = _alternate(lambda: base.step(), lambda: tr.step(), warmup, steps)
+    del base
+    torch.cuda.empty_cache()
     replays = tr.graphed.replays
     eng.timing = True
     tr.step()

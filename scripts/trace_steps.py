@@ -23,12 +23,13 @@ def main(path, last=5, verbose=False):
         names = [r["Kernel_Name"] for r in rows]
         for trim in range(0, min(1001, len(names) // 2), 25):
             n = len(names) - trim
-            for P in range(8, n // (last + 1) + 1):
+            for P in range(16, n // (last + 1) + 1):
                 if names[n - 1] != names[n - 1 - P]:
                     continue
                 tail = names[n - P:n]
                 # (a step, not a repeated block inside one: the period holds the optimizer step)
-                if not any("k_unpack_sgd" in x or "k_sgd<" in x for x in tail):
+                if not any("k_unpack_sgd" in x or "k_sgd<" in x for x in tail) or \
+                        not any("k_gemm" in x for x in tail):
                     continue
                 if all(names[n - (k + 1) * P:n - k * P] == tail for k in range(1, last + 1)):
                     sgd = [n - 1 - k * P for k in range(last, -1, -1)]

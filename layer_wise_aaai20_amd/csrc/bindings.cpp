@@ -86,8 +86,9 @@ WsLayout layout(int64_t n_small, int64_t n_large, int64_t n_tasks) {
   w.hist = c.take<uint32_t>(n_large * 4096);
   w.st_small = c.take<lw::SelState>(n_small);
   w.st_large = c.take<lw::SelState>(n_large);
-  w.cnt = c.take<uint2>(n_tasks);
-  w.pre = c.take<uint2>(n_tasks);
+  // (per quarter task: the fused select chain counts and writes 2048-element sub-tasks)
+  w.cnt = c.take<uint2>(n_tasks * lw::kWriteSub);
+  w.pre = c.take<uint2>(n_tasks * lw::kWriteSub);
   w.partial = c.take<float2>(n_tasks);
   w.segmax = c.take<float>(n_large);
   w.total = c.off;

@@ -533,9 +533,14 @@ __global__ __launch_bounds__(NT) void k_count_sel(float* __restrict__ g,
     const int64_t off = seg_off[s];
     float* gp = g + off;
     const int end = min(begin + EPB, n);
-    uint32_t cg = 0, ce = 0;
-#pragma unroll 2
-    for (int j = 0; j < EPB / (NT * 4); ++j) {
+    // (gt, eq) per sub-task of EPB / kWriteSub elements, packed gt | eq << 16 (each <= 2048)
+    constexpr int STRIDES = EPB / (NT * 4), PER_SUB = STRIDES / kWriteSub;
+    static_assert(PER_SUB >= 1 && STRIDES % kWriteSub == 0, "sub-task = whole strides");
+    uint32_t c[kWriteSub];
+#pragma unroll
+    for (int q = 0; q < kWriteSub; ++q) c[q] = 0;
+#pragma unroll
+    for (int j = 0; j < STRIDES; ++j) {
       const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
       if (i0 >= end) break;
       uint32_t k[4];
@@ -543,12 +548,14 @@ __global__ __launch_bounds__(NT) void k_count_sel(float* __restrict__ g,
       load4_keys<KM, false>(gp, nullptr, i0, end, gid_base + s, step, s0, s1, k, valid);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (valid[q]) { cg += k[q] > tk; ce += k[q] == tk; }
+        if (valid[q]) c[j / PER_SUB] += (k[q] > tk ? 1u : 0u) + (k[q] == tk ? 0x10000u : 0u);
     }
-    uint32_t tg, te;
-    block_excl_scan<NT>(cg, scr, tg);
-    block_excl_scan<NT>(ce, scr, te);
-    if (threadIdx.x == 0) cnt[ti] = make_uint2(tg, te);
+#pragma unroll
+    for (int q = 0; q < kWriteSub; ++q) {
+      uint32_t tot;
+      block_excl_scan<NT>(c[q], scr, tot);
+      if (threadIdx.x == 0) cnt[ti * kWriteSub + q] = make_uint2(tot & 0xffffu, tot >> 16);
+    }
     __syncthreads();                     // scr / arr reuse by the next task
   }
 }
@@ -558,10 +565,10 @@ template <int KM>
 __global__ __launch_bounds__(NT) void k_scan(const uint2* __restrict__ cnt, uint2* __restrict__ pre,
                                              const int32_t* __restrict__ task_lo,
                                              SelState* __restrict__ st,
-                                             int32_t* __restrict__ count_out) {
+                                             int32_t* __restrict__ count_out, int sub = 1) {
   __shared__ uint32_t scr[NT / WAVE];
   const int li = blockIdx.x;
-  const int lo = task_lo[li], hi = task_lo[li + 1];
+  const int lo = task_lo[li] * sub, hi = task_lo[li + 1] * sub;   // (sub-tasks per task)
   uint32_t carry_g = 0, carry_e = 0;
   for (int b = lo; b < hi; b += NT) {
     const int i = b + threadIdx.x;
@@ -672,8 +679,13 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t scr[NT / WAVE];
-  const int2 t = tasks[blockIdx.x];
-  const int li = t.x, begin = t.y;
+  // FW: kWriteSub workgroups per task, one per EPB / kWriteSub elements (a small bucket's write
+  // then spreads over 4x the workgroups); `pre` / the count array are per sub-task
+  constexpr int SUB = FW ? kWriteSub : 1;
+  constexpr int EW = EPT / SUB;                 // elements per thread
+  const int wi = (int)blockIdx.x;               // (sub-)task index
+  const int2 t = tasks[wi / SUB];
+  const int li = t.x, begin = t.y + (wi % SUB) * (EPB / SUB);
   const int s = large_segs[li];
   const int n = seg_n[s];
   const int64_t off = seg_off[s];
@@ -681,7 +693,7 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   uint2 bp;
   if (FW && prefix_from_cnt) {
     uint32_t sg = 0, se = 0;
-    for (int q = task_lo[li] + (int)threadIdx.x; q < (int)blockIdx.x; q += NT) {
+    for (int q = task_lo[li] * SUB + (int)threadIdx.x; q < wi; q += NT) {
       const uint2 c = pre[q];
       sg += c.x;
       se += c.y;
@@ -689,9 +701,10 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
     block_excl_scan<NT>(sg, scr, bp.x);
     block_excl_scan<NT>(se, scr, bp.y);
   } else {
-    bp = pre[blockIdx.x];
+    bp = pre[wi];
   }
-  if (FW && (int)blockIdx.x == task_lo[li + 1] - 1) {
+  const bool seg_last = FW && wi == task_lo[li + 1] * SUB - 1;
+  if (seg_last) {
     uint32_t* hz = hist_all + (size_t)li * HIST_WORDS;
     for (int q = threadIdx.x; q < HIST_WORDS; q += NT) hz[q] = 0u;
   }
@@ -700,16 +713,16 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   const int64_t c0 = cap_off[s];
   float* gp = g + off;
   float* ep = EF ? ef + off : nullptr;
-  const int i_base = begin + threadIdx.x * EPT;
-  const int end = min(begin + EPB, n);
+  const int i_base = begin + threadIdx.x * EW;
+  const int end = min(begin + EPB / SUB, n);
   // RANDK never touched g in the histogram passes, so its EF add happens here.
   constexpr bool ADD_EF_HERE = EF && (KM == KM_RANDK);
 
-  float v[EPT];
-  uint32_t key[EPT];
-  if (i_base + EPT <= end) {
+  float v[EW];
+  uint32_t key[EW];
+  if (i_base + EW <= end) {
 #pragma unroll
-    for (int q = 0; q < EPT / 4; ++q) {
+    for (int q = 0; q < EW / 4; ++q) {
       float4 x = *reinterpret_cast<const float4*>(gp + i_base + 4 * q);
       if (ADD_EF_HERE) {
         const float4 e = *reinterpret_cast<const float4*>(ep + i_base + 4 * q);
@@ -719,7 +732,7 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
+    for (int k = 0; k < EW; ++k) {
       const int i = i_base + k;
       float x = 0.f;
       if (i < end) { x = gp[i]; if (ADD_EF_HERE) x += ep[i]; }
@@ -728,18 +741,18 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   }
   if (KM == KM_RANDK) {
 #pragma unroll
-    for (int k = 0; k < EPT; k += 4) {
+    for (int k = 0; k < EW; k += 4) {
       uint32_t q[4];
       randk_key4(i_base + k, gid_base + s, step, s0, s1, q);
       key[k] = q[0]; key[k + 1] = q[1]; key[k + 2] = q[2]; key[k + 3] = q[3];
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) key[k] = abs_key(v[k]);
+    for (int k = 0; k < EW; ++k) key[k] = abs_key(v[k]);
   }
   uint32_t cg = 0, ce = 0;
 #pragma unroll
-  for (int k = 0; k < EPT; ++k) {
+  for (int k = 0; k < EW; ++k) {
     const bool ok = i_base + k < end;
     cg += ok && key[k] > S.tkey;
     ce += ok && key[k] == S.tkey;
@@ -748,7 +761,7 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   const uint32_t p = block_excl_scan<NT>(cg | (ce << 16), scr, tot);
   uint32_t gb = bp.x + (p & 0xffffu), eb = bp.y + (p >> 16);
 #pragma unroll
-  for (int k = 0; k < EPT; ++k) {
+  for (int k = 0; k < EW; ++k) {
     const int i = i_base + k;
     if (i >= end) break;
     bool sel = false;
@@ -764,7 +777,7 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   }
   // (k_fill_tail folded in: the workgroup of the segment's last task pads the unused pair slots;
   // no workgroup writes a slot at or past S.total)
-  if (FW && OUT == OUT_PAIRS && (int)blockIdx.x == task_lo[li + 1] - 1)
+  if (OUT == OUT_PAIRS && seg_last)
     for (uint32_t q = S.total + threadIdx.x; q < S.cap; q += NT) pairs[c0 + q] = make_int2(SENT, 0);
 }
 
@@ -1256,8 +1269,9 @@ static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) 
     const bool own_prefix = a.max_seg_tasks > 0 && a.max_seg_tasks <= LW_FW_SCAN_MAX;
     if (!own_prefix)
       LW_LAUNCH((k_scan<KM>), a.n_large, st, a.cnt, a.pre, a.task_lo, a.st_large,
-                (int32_t*)nullptr);
-    LW_LAUNCH((k_write<KM, OUT, EF, true>), a.n_tasks, st, a.g, a.ef, a.seg_off, a.seg_n,
+                (int32_t*)nullptr, kWriteSub);
+    LW_LAUNCH((k_write<KM, OUT, EF, true>), a.n_tasks * kWriteSub, st, a.g, a.ef, a.seg_off,
+              a.seg_n,
               a.large_segs, a.tasks, a.st_large, own_prefix ? a.cnt : a.pre, a.cap_off, a.pairs,
               a.vals, a.idx_out, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr, a.mom,
               a.task_lo, a.hist, own_prefix ? 1 : 0);

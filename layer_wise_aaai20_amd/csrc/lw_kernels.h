@@ -8,6 +8,7 @@
 namespace lw {
 
 constexpr int kLargeEPB = 8192;    // elements per workgroup in multi-block passes
+constexpr int kWriteSub = 4;          // sub-tasks per task in the fused chain's count / write
 constexpr int kSmallMax = 4096;    // segments up to this size use the single-workgroup path
 constexpr int kUnpackChunk = 4096; // elements per workgroup in the pair unpack
 constexpr int kMaxWorld = 64;

@@ -15,7 +15,7 @@ from prof_summary import CATS  # noqa: E402
 def main(path, last=5, verbose=False):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    sgd = [i for i, r in enumerate(rows) if re.search(r"k_sgd<", r["Kernel_Name"])]
+    sgd = [i for i, r in enumerate(rows) if re.search(r"lw::k_sgd<", r["Kernel_Name"])]
     if len(sgd) < last + 1:
         # every bucket's step fused into its decode: the step is the period of the replayed
         # graph's kernel-name sequence (the smallest P whose last `last` periods are identical)
@@ -28,7 +28,7 @@ def main(path, last=5, verbose=False):
                     continue
                 tail = names[n - P:n]
                 # (a step, not a repeated block inside one: the period holds the optimizer step)
-                if not any("k_unpack_sgd" in x or "k_sgd<" in x for x in tail) or \
+                if not any("k_unpack_sgd" in x or "lw::k_sgd<" in x for x in tail) or \
                         not any("k_gemm" in x for x in tail):
                     continue
                 if all(names[n - (k + 1) * P:n - k * P] == tail for k in range(1, last + 1)):

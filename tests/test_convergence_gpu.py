@@ -45,7 +45,7 @@ DEFAULT_FLOOR = 0.2
 PEAK = 0.1            # peak LR of the short schedule (summed loss, per-sample LR = PEAK / batch)
 
 
-def run_short(method, kw, mode, seed=0, steps=STEPS, amp=None, peak=None):
+def run_short(method, kw, mode, seed=0, steps=STEPS, amp=None, peak=None, ef=None):
     """One short run; returns (held-out accuracy, mean loss of the first / last 20 steps)."""
     amp = AMP if amp is None else amp
     peak = PEAK if peak is None else peak
@@ -53,8 +53,9 @@ def run_short(method, kw, mode, seed=0, steps=STEPS, amp=None, peak=None):
     from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
     from layer_wise_aaai20_amd.utils.logging import PiecewiseLinear
     torch.manual_seed(seed)
+    ef = method != "none" if ef is None else ef
     tr = CifarTrainer("resnet9", compress=mode if method != "none" else "none", method=method,
-                      error_feedback=method != "none", batch_size=BATCH, epochs=2,
+                      error_feedback=ef, batch_size=BATCH, epochs=2,
                       n_train=BATCH * 50, n_test=16, seed=seed, task="textures", amp=amp, **kw)
     tr.steps_per_epoch = 1                           # schedule in steps: warm-up, decay to 0
     # entire-model TernGrad scales the ternary code by max|g| over all 6.6 M parameters, so its

@@ -204,7 +204,13 @@ class _ReplicatedLinearFn(torch.autograd.Function):
             O, C = g1.shape
             g = p.grad if getattr(p, "_lw_grad_ready", None) is not None else None
             if g is not None and g.dtype == torch.float32 and g.is_contiguous():
-                g.view(O, C, reps).add_(g1.unsqueeze(-1))
+                claim = getattr(p, "_lw_grad_overwrite", None)
+                if claim is not None and claim():
+                    # the only contribution this step and the arena slice was not zeroed: one
+                    # write pass instead of zero + read + write (engine.claim_overwrite)
+                    g.view(O, C, reps).copy_(g1.unsqueeze(-1).expand(O, C, reps))
+                else:
+                    g.view(O, C, reps).add_(g1.unsqueeze(-1))
                 p._lw_grad_ready(p)
             else:
                 dw = g1.unsqueeze(-1).expand(O, C, reps).reshape(O, C * reps).to(p.dtype)

@@ -119,6 +119,16 @@ class GradArena:
     def zero_(self) -> None:
         self.grad.zero_()
 
+    def zero_except(self, keep) -> None:
+        """Zero the gradient arena but for the segments in ``keep`` (one fill per gap)."""
+        lo = 0
+        for s in sorted((self.segments[i] for i in keep), key=lambda s: s.offset):
+            if s.offset > lo:
+                self.grad[lo:s.offset].zero_()
+            lo = s.offset + s.numel
+        if lo < self.numel:
+            self.grad[lo:].zero_()
+
     def _flatten_params(self) -> None:
         self.param_buf = torch.zeros(self.numel, dtype=self.segments[0].param.dtype,
                                      device=self.device)

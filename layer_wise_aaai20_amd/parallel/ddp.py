@@ -107,6 +107,8 @@ class CompressedDDP(nn.Module):
             # fused ops (ops/block.py) write this parameter's gradient straight into its arena
             # view and then call the same hook, bypassing AccumulateGrad
             p._lw_grad_ready = hook
+            # may a fused op overwrite (not accumulate into) this gradient? (engine.claim_overwrite)
+            p._lw_grad_overwrite = (lambda i=seg.index: self.engine.claim_overwrite(i))
 
     def _make_hook(self, seg_index: int):
         engine = self.engine

@@ -169,6 +169,9 @@ class GradSyncEngine:
         self._plan_stages(cap)
         self._sgd = None                 # set_fused_sgd: decode + optimizer step in one pass
         self._sgd_buckets = frozenset()
+        # claimed overwrites (claim_overwrite): segments left out of the per-step zeroing
+        self._claims = [0] * len(self.arena.segments)
+        self._no_zero = frozenset()
         self.step = 0
         self.stats = SyncStats(dense_bytes=self.arena.numel * 4, buckets=len(self.buckets))
         self.timing = timing and self.device.type == "cuda"
@@ -457,9 +460,29 @@ class GradSyncEngine:
     def _count_exchange(self, caps: torch.Tensor) -> torch.Tensor:
         return comm.all_reduce_max(caps, self.pg)
 
+    def claim_overwrite(self, seg_index: int) -> bool:
+        """A fused op about to write segment ``seg_index``'s whole gradient asks whether it may
+        overwrite (True) instead of accumulating into the arena view (False). True only for a
+        segment that the previous step's backward wrote through exactly one claim — those are
+        left out of begin_step's zeroing — and only for its first claim of this step (a second
+        use of the weight in the same step accumulates, and the segment is zeroed again from the
+        next step on). The caller must be the segment's only gradient contribution when it
+        overwrites (ops/gemm.py _ReplicatedLinearFn: VGG-16's 103 M-weight fc1, whose zeroing
+        plus read-add-write cost about three passes over 412 MB a step)."""
+        self._claims[seg_index] += 1
+        return self._claims[seg_index] == 1 and seg_index in self._no_zero and \
+            os.environ.get("LWAAAI_CLAIM_OVERWRITE", "1") != "0"
+
     def begin_step(self) -> None:
-        """Zero the arena and re-point ``.grad`` at it (called before forward/backward)."""
-        self.arena.zero_()
+        """Zero the arena (but for the segments whole-written by a claimed overwrite in the last
+        step) and re-point ``.grad`` at it (called before forward/backward)."""
+        if any(self._claims):            # (a backward ran since the last call)
+            self._no_zero = frozenset(i for i, c in enumerate(self._claims) if c == 1)
+            self._claims = [0] * len(self.arena.segments)
+        if not self._no_zero:
+            self.arena.zero_()
+        else:
+            self.arena.zero_except(self._no_zero)
         if not self.arena.grads_attached():
             self.arena.attach_grads()
         if self.lr_scaled:
@@ -594,6 +617,9 @@ class GradSyncEngine:
     def finish(self) -> None:
         """Launch buckets that never became ready (unused params keep zero grads), wait for every
         collective and decode into the arena."""
+        for i in self._no_zero:
+            if self._claims[i] == 0:     # (not zeroed by begin_step and not written this step)
+                self.arena.grad_view(self.arena.segments[i]).zero_()
         for i in range(self._next, len(self.buckets)):
             self._ready[i] = True
         self._launch_in_order()

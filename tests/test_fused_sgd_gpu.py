@@ -77,3 +77,28 @@ def test_cifar_graph_step_fused_sgd_bitwise():
     (pa, ba), (pb, bb) = outs
     assert torch.equal(pa, pb), (pa - pb).abs().max().item()
     assert torch.equal(ba, bb)
+
+
+def test_vgg_claimed_overwrite_matches_zero_and_accumulate():
+    """VGG-16's fc1 weight gradient is written by one copy into an arena slice the step did not
+    zero (engine.claim_overwrite) instead of zero + add: the trained parameters equal the
+    zero-and-accumulate path's (LWAAAI_CLAIM_OVERWRITE=0), graph-captured steps included."""
+    from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
+    outs = []
+    for flag in ("0", "1"):
+        os.environ["LWAAAI_CLAIM_OVERWRITE"] = flag
+        torch.manual_seed(0)
+        try:
+            tr = CifarTrainer(device="cuda", n_train=512 * 6, graph=True, network="vgg16",
+                              compress="layerwise", method="Topk", K=0.001, seed=0)
+            tr.graphed.warmup = 2
+            for _ in range(6):
+                tr.step()
+            torch.cuda.synchronize()
+            if flag == "1":
+                assert tr.ddp.engine._no_zero, "fc1 should be written by a claimed overwrite"
+            outs.append(tr.ddp.arena.param_buf.clone())
+        finally:
+            os.environ.pop("LWAAAI_CLAIM_OVERWRITE", None)
+        del tr
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()

@@ -352,3 +352,36 @@ def test_momentum_correction_folds_weight_decay_per_group(mode):
     u = g + wd * p / 0.5
     torch.testing.assert_close(eng.arena.grad + eng.ef, e_old + u, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(eng.mom, _mc_expect(eng, u, eng.arena.grad), rtol=1e-6, atol=1e-7)
+
+
+def test_claimed_overwrite_skips_zeroing_once_whole_written():
+    """engine.claim_overwrite: a segment whole-written by exactly one claim in a step is left out
+    of the next begin_step's zeroing and may be overwritten; a second claim (a shared weight)
+    puts it back under zeroing; a left-out segment nobody wrote is zeroed before the exchange."""
+    m = small_net()
+    eng = GradSyncEngine(list(m.named_parameters()), mode="layerwise", method="none")
+    seg = eng.arena.segments[-1]                  # (the conv weight)
+    view = eng.arena.grad_view(seg)
+    eng.begin_step()
+    assert eng.claim_overwrite(seg.index) is False          # nothing left unzeroed yet
+    view.fill_(3.0)
+    eng.begin_step()
+    assert seg.index in eng._no_zero
+    assert float(view.abs().min()) == 3.0                   # not zeroed: it will be overwritten
+    others = [s for s in eng.arena.segments if s.index != seg.index]
+    for s in others:
+        eng.arena.grad_view(s).fill_(1.0)
+    eng.begin_step()                                        # (no backward ran: same set)
+    assert all(float(eng.arena.grad_view(s).abs().max()) == 0.0 for s in others)
+    assert eng.claim_overwrite(seg.index) is True
+    assert eng.claim_overwrite(seg.index) is False          # a second use accumulates
+    eng.begin_step()
+    assert seg.index not in eng._no_zero and float(view.abs().max()) == 0.0
+    # left out but not written this step: zeroed in finish, before its bucket is exchanged
+    eng._claims = [0] * len(eng.arena.segments)
+    eng._claims[seg.index] = 1
+    eng.begin_step()
+    assert seg.index in eng._no_zero
+    view.fill_(5.0)
+    eng.finish()
+    assert float(view.abs().max()) == 0.0

@@ -575,6 +575,22 @@ void normalize_u8(Tensor in, Tensor out, std::vector<double> mean, std::vector<d
 
 // global average pool (nn.hip): x channels_last bf16 [N, C, H, W] -> [N, C] bf16
 // w [..., R] contiguous 16-bit -> [...] = Σ over the last dim (fp32 sum, 16-bit out)
+// out.view(-1, R)[i, :] (=|+=) g[i] (nn.hip k_repeat_store): fp32 g [n], out [n * R] in place
+void repeat_store(Tensor g, Tensor out, int64_t R, bool accumulate) {
+  const c10::DeviceGuard guard(out.device());
+  check_cuda(g, "g");
+  check_cuda(out, "out");
+  check_dtype(g, at::kFloat, "g");
+  check_dtype(out, at::kFloat, "out");
+  TORCH_CHECK(g.is_contiguous() && out.is_contiguous() && R >= 1 &&
+                  out.numel() == g.numel() * R, "repeat_store: out must be contiguous [n * R]");
+  check_aligned16(out.data_ptr(), "out");
+  if (out.numel() > 0)
+    lw::repeat_store(ptr<float>(g), ptr<float>(out), out.numel(), (int)R, accumulate,
+                     cur_stream());
+  launched("repeat_store");
+}
+
 Tensor sum_repeats(Tensor w, int64_t R) {
   const c10::DeviceGuard guard(w.device());
   TORCH_CHECK(w.is_cuda() && w.is_contiguous(), "sum_repeats: contiguous GPU tensor");
@@ -1806,6 +1822,7 @@ LW_LIBRARY(LW_OPS_NS, m) {
         "Tensor(a!) out) -> ()");
   m.def("gap_fwd(Tensor x) -> Tensor");
   m.def("sum_repeats(Tensor w, int R) -> Tensor");
+  m.def("repeat_store(Tensor g, Tensor(a!) out, int R, bool accumulate) -> ()");
   m.def("pack_dgrad_nkc(Tensor w, int[] cls, int sh, int sw) -> Tensor");
   m.def("relu_bias_bwd(Tensor dy, Tensor? y, Tensor(a!)? db_out) -> (Tensor, Tensor)");
   m.def("xent(Tensor logits, Tensor target, float gscale, int ignore_index, bool want_grad) "
@@ -1883,6 +1900,7 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("cifar_augment", &cifar_augment);
   m.impl("gap_fwd", &gap_fwd);
   m.impl("sum_repeats", &sum_repeats);
+  m.impl("repeat_store", &repeat_store);
   m.impl("pack_dgrad_nkc", &pack_dgrad_nkc);
   m.impl("relu_bias_bwd", &relu_bias_bwd);
   m.impl("xent", &xent);

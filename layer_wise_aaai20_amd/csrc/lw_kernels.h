@@ -344,6 +344,7 @@ void spin_for_test(double ms, hipStream_t st);
 void gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
 // out[i] = Σ_r w[i*R + r] over 16-bit values, R <= 64 (nn.hip)
 void sum_repeats(const uint16_t* w, uint16_t* out, int64_t n, int R, hipStream_t st);
+void repeat_store(const float* g, float* out, int64_t n_out, int R, bool acc, hipStream_t st);
 void gap_bwd(const void* dy, bool dy_f32, uint16_t* dx, int N, int HW, int C, hipStream_t st);
 // fused softmax cross-entropy (nn.hip): per-row loss, top-1/top-5 correctness [B][2] and, when
 // `grad` is non-null, the logit gradient (softmax - onehot)·gscale (0 for ignored targets)

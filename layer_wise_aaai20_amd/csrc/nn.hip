@@ -233,6 +233,35 @@ void sum_repeats(const uint16_t* w, uint16_t* out, int64_t n, int R, hipStream_t
                      n, R);
 }
 
+// out[i*R + r] (=|+=) g[i], r < R: the weight gradient of a replicated Linear (the same for every
+// repeat of a feature) into the fp32 gradient arena. Four consecutive outputs per thread, one
+// float4 store; the source value is read from cache by the R/4 threads that share it.
+template <bool ACC>
+__global__ __launch_bounds__(256) void k_repeat_store(const float* __restrict__ g,
+                                                      float* __restrict__ out, int64_t n_out,
+                                                      int R) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n_out) return;
+  if (i + 3 < n_out) {
+    float4 v = make_float4(g[i / R], g[(i + 1) / R], g[(i + 2) / R], g[(i + 3) / R]);
+    if (ACC) {
+      const float4 o = *reinterpret_cast<const float4*>(out + i);
+      v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    *reinterpret_cast<float4*>(out + i) = v;
+  } else {
+    for (int64_t j = i; j < n_out; ++j) out[j] = ACC ? out[j] + g[j / R] : g[j / R];
+  }
+}
+
+void repeat_store(const float* g, float* out, int64_t n_out, int R, bool acc, hipStream_t st) {
+  const unsigned blocks = (unsigned)((n_out / 4 + 256) / 256);
+  if (acc)
+    hipLaunchKernelGGL(k_repeat_store<true>, dim3(blocks), dim3(256), 0, st, g, out, n_out, R);
+  else
+    hipLaunchKernelGGL(k_repeat_store<false>, dim3(blocks), dim3(256), 0, st, g, out, n_out, R);
+}
+
 void gap_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st) {
   const int thr = N * (C / 8);
   hipLaunchKernelGGL(k_gap_fwd, dim3((thr + 255) / 256), dim3(256), 0, st, x, y, N, HW, C,

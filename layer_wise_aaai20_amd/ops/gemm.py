@@ -205,12 +205,12 @@ class _ReplicatedLinearFn(torch.autograd.Function):
             g = p.grad if getattr(p, "_lw_grad_ready", None) is not None else None
             if g is not None and g.dtype == torch.float32 and g.is_contiguous():
                 claim = getattr(p, "_lw_grad_overwrite", None)
-                if claim is not None and claim():
-                    # the only contribution this step and the arena slice was not zeroed: one
-                    # write pass instead of zero + read + write (engine.claim_overwrite)
-                    g.view(O, C, reps).copy_(g1.unsqueeze(-1).expand(O, C, reps))
-                else:
-                    g.view(O, C, reps).add_(g1.unsqueeze(-1))
+                # the only contribution this step and the arena slice was not zeroed: one write
+                # pass instead of zero + read + write (engine.claim_overwrite); nn.hip
+                # k_repeat_store either way (the broadcast add / copy ran ATen's generic
+                # strided kernel)
+                load().repeat_store(g1.reshape(-1), g.view(-1), reps,
+                                    not (claim is not None and claim()))
                 p._lw_grad_ready(p)
             else:
                 dw = g1.unsqueeze(-1).expand(O, C, reps).reshape(O, C * reps).to(p.dtype)

@@ -255,12 +255,13 @@ def _init_native_agreed(group, device) -> Optional[NativeRccl]:
 
     1. Every rank checks that it can (extension loaded, unique id obtained) and the ranks agree
        (an all-reduce over the c10d group); on a no, nobody enters the RCCL init.
-    2. Every rank enters ``ncclCommInitRank`` on a *non-blocking* communicator whose init is
-       polled against a deadline (``LWAAAI_RCCL_INIT_TIMEOUT``, ``csrc/rccl.cpp rccl_init``), then
+    2. Every rank enters ``ncclCommInitRank``, run on a helper thread that this rank waits for
+       against a deadline (``LWAAAI_RCCL_INIT_TIMEOUT``, ``csrc/rccl.cpp rccl_init``; the
+       communicator itself is a blocking one: a non-blocking one crashed captured steps), then
        validates it with a probe all-reduce. A rank that raises anywhere in this block — before
        it reached the init, inside it, or at the probe — goes straight to step 3. Its peers are
        then waiting inside an init (or a probe on a half-built communicator) that cannot
-       complete: the init deadline aborts their communicator and they raise as well.
+       complete: the init deadline abandons their init and they raise as well.
     3. The ranks agree again; if any rank has no communicator, every rank closes its own and all
        fall back to the c10d collectives (eager steps at world > 1), instead of some ranks
        waiting in a collective the others never join.

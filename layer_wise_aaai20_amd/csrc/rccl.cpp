@@ -84,9 +84,9 @@ ncclResult_t settle(ncclComm_t comm, ncclResult_t r) {
 // init forever; here the call raises instead (the helper thread is left behind, blocked, and its
 // communicator — should the init ever complete — is never used), so the rank reaches the fallback
 // agreement (parallel/comm.py _init_native_agreed). The communicator itself is an ordinary
-// BLOCKING one: on a non-blocking communicator (ncclConfig_t.blocking = 0, tried in round 5) RCCL
-// may finish a collective's launch asynchronously, and the captured 2-rank training steps crashed
-// in capture with it. timeout_s <= 0: the init on this thread, no deadline.
+// BLOCKING one (a non-blocking one, ncclConfig_t.blocking = 0, lets any call return
+// ncclInProgress and finish its launch later, which a captured step should not depend on).
+// timeout_s <= 0: the init on this thread, no deadline.
 namespace {
 struct InitJob {
   std::mutex mu;

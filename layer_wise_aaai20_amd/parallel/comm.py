@@ -257,7 +257,8 @@ def _init_native_agreed(group, device) -> Optional[NativeRccl]:
        (an all-reduce over the c10d group); on a no, nobody enters the RCCL init.
     2. Every rank enters ``ncclCommInitRank``, run on a helper thread that this rank waits for
        against a deadline (``LWAAAI_RCCL_INIT_TIMEOUT``, ``csrc/rccl.cpp rccl_init``; the
-       communicator itself is a blocking one: a non-blocking one crashed captured steps), then
+       communicator itself is an ordinary blocking one, so no collective can return
+       ``ncclInProgress`` inside a captured step), then
        validates it with a probe all-reduce. A rank that raises anywhere in this block — before
        it reached the init, inside it, or at the probe — goes straight to step 3. Its peers are
        then waiting inside an init (or a probe on a half-built communicator) that cannot

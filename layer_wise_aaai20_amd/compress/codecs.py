@@ -76,6 +76,9 @@ class Codec:
     # with mc_fused zeroes it at the coordinates it selected (segments not sent whole only)
     mc_mom = None
     mc_fused = False
+    # (p, seg_wd, mc, wmul): the velocity update itself runs in the first select pass (Top-K,
+    # layer-wise; GradSyncEngine._launch), with mc_mom as u
+    mc_fuse = None
     # entire-model staging (GradSyncEngine): codecs with `stage` run their first pass per arena
     # slice during backward; `_staged` tells compress() that pass is done for this step
     _staged = False
@@ -231,7 +234,8 @@ class TopkCodec(Codec):
                                 self._workspace(grad.device, lib), self.km, OUT_PAIRS, out, None,
                                 None, self.plan.gid_base, int(step) & 0xFFFFFFFF, self.seed,
                                 self.step_t, self.overflow, self.mc_mom, self._staged,
-                                self.plan.max_large_tasks())
+                                self.plan.max_large_tasks(),
+                                *(self.mc_fuse if self.mc_fuse is not None else ()))
             return out
         self._compress_cpu(grad, ef, step, out)
         return out

@@ -168,7 +168,9 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
                      c10::optional<Tensor> pairs, c10::optional<Tensor> vals,
                      c10::optional<Tensor> idx, int64_t gid_base, int64_t step, int64_t seed,
                      c10::optional<Tensor> step_t, c10::optional<Tensor> overflow,
-                     c10::optional<Tensor> mom, bool staged, int64_t max_seg_tasks) {
+                     c10::optional<Tensor> mom, bool staged, int64_t max_seg_tasks,
+                     c10::optional<Tensor> mc_p, c10::optional<Tensor> mc_wd, double mc,
+                     double mc_wmul) {
   const c10::DeviceGuard guard(g.device());
   lw::SelectArgs a = make_select_args(g, ef, seg_off, seg_n, keep, cap_off, small_segs, large_segs,
                                       tasks, task_lo, ws);
@@ -184,6 +186,23 @@ void select_compress(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor 
   a.idx_out = optr<int32_t>(idx);
   TORCH_CHECK(out == lw::OUT_PAIRS ? a.pairs != nullptr : (a.vals && a.idx_out),
               "missing output buffers");
+  if (mc != 0.0) {                 // momentum correction fused into the first pass (McArgs)
+    TORCH_CHECK(a.mom != nullptr, "select_compress: fused momentum correction needs mom (u)");
+    TORCH_CHECK(km == lw::KM_TOPK && out == lw::OUT_PAIRS && !staged,
+                "select_compress: fused momentum correction is Top-K pairs, unstaged");
+    a.mcx.u = a.mom;
+    a.mcx.mc = (float)mc;
+    a.mcx.wmul = (float)mc_wmul;
+    if (mc_wd.has_value() && mc_wd->defined() && mc_p.has_value() && mc_p->defined()) {
+      check_cuda(*mc_p, "mc_p");
+      check_dtype(*mc_p, at::kFloat, "mc_p");
+      check_dtype(*mc_wd, at::kFloat, "mc_wd");
+      TORCH_CHECK(mc_p->is_contiguous() && mc_p->numel() >= g.numel(), "mc_p: g's layout");
+      check_aligned16(mc_p->data_ptr(), "mc_p");
+      a.mcx.p = ptr<float>(*mc_p);
+      a.mcx.wd = ptr<float>(*mc_wd);
+    }
+  }
   a.gid_base = (uint32_t)gid_base;
   a.step = (uint32_t)step;
   a.step_ptr = step_ptr(step_t);
@@ -1767,7 +1786,8 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "
       "Tensor(c!) ws, int km, int out, Tensor(d!)? pairs, Tensor(e!)? vals, Tensor(f!)? idx, "
       "int gid_base, int step, int seed, Tensor? step_t=None, Tensor(g!)? overflow=None, "
-      "Tensor(h!)? mom=None, bool staged=False, int max_seg_tasks=0) -> ()");
+      "Tensor(h!)? mom=None, bool staged=False, int max_seg_tasks=0, Tensor? mc_p=None, "
+      "Tensor? mc_wd=None, float mc=0.0, float mc_wmul=1.0) -> ()");
   m.def(
       "select_stage(Tensor(a!) g, Tensor(b!)? ef, Tensor seg_off, Tensor seg_n, Tensor keep, "
       "Tensor cap_off, Tensor small_segs, Tensor large_segs, Tensor tasks, Tensor task_lo, "

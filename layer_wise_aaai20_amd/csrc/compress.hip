@@ -56,6 +56,15 @@ constexpr int HIST_WORDS = 4096;     // 2048 + 1024 + 1024 bins per large segmen
 
 __device__ __forceinline__ uint32_t abs_key(float x) { return __float_as_uint(x) & 0x7fffffffu; }
 
+// Momentum correction of one element (optim.hip k_mc_prep, parallel/engine.py _mc_prologue):
+// g' = g + wd·p, u = mc·u + g', returns u — every product and sum rounded on its own.
+__device__ __forceinline__ float mc_step(float g, float& u, float p, float wd, float mc) {
+#pragma clang fp contract(off)
+  const float gw = wd != 0.f ? g + p * wd : g;
+  u = u * mc + gw;
+  return u;
+}
+
 __device__ __forceinline__ uint32_t randk_key(uint32_t i, uint32_t gid, uint32_t step, uint32_t s0,
                                               uint32_t s1) {
   const u4 r = philox4x32_10(u4{i >> 2, gid, step, 1u << 24}, s0, s1);
@@ -127,14 +136,14 @@ __device__ __forceinline__ void finish_state(SelState& s, int km, uint32_t keep,
 // ------------------------------------------------------------------------------------------
 // Small segments: whole selection + compaction in one workgroup.
 // ------------------------------------------------------------------------------------------
-template <int KM, int OUT, bool EF>
+template <int KM, int OUT, bool EF, bool MC = false>
 __global__ __launch_bounds__(NT) void k_small_select(
     float* __restrict__ g, float* __restrict__ ef, const int64_t* __restrict__ seg_off,
     const int32_t* __restrict__ seg_n, const int32_t* __restrict__ keep,
     const int64_t* __restrict__ cap_off, const int32_t* __restrict__ small_segs,
     int2* __restrict__ pairs, float* __restrict__ vals, int32_t* __restrict__ idx_out,
     SelState* __restrict__ st_small, uint32_t gid_base, uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp,
-    unsigned long long* __restrict__ overflow, float* __restrict__ mom) {
+    unsigned long long* __restrict__ overflow, float* __restrict__ mom, McArgs mcx = McArgs{}) {
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t h[2048];
@@ -153,12 +162,21 @@ __global__ __launch_bounds__(NT) void k_small_select(
 
   float v[SEPT];
   uint32_t key[SEPT];
+  // fused momentum correction (McArgs): the compressor sees u = mc·u + g'
+  float* up = MC ? mcx.u + off : nullptr;
+  const float* pw = MC && mcx.p != nullptr ? mcx.p + off : nullptr;
+  const float wd = MC && mcx.wd != nullptr ? mcx.wd[s] * mcx.wmul : 0.f;
 #pragma unroll
   for (int k = 0; k < SEPT; ++k) {
     const int i = base + k;
     float x = 0.f;
     if (i < n) {
       x = gp[i];
+      if (MC) {
+        float u = up[i];
+        x = mc_step(x, u, pw != nullptr ? pw[i] : 0.f, wd, mcx.mc);
+        up[i] = u;
+      }
       if (EF) x += ep[i];
     }
     v[k] = x;
@@ -244,31 +262,49 @@ __global__ __launch_bounds__(NT) void k_small_select(
 // Large segments: multi-block radix select.
 // Coalesced layout for histogram/count passes: element = begin + j*NT*4 + tid*4 + {0..3}.
 // ------------------------------------------------------------------------------------------
-template <int KM, bool EFADD>
+template <int KM, bool EFADD, bool MC = false>
 __device__ __forceinline__ void load4_keys(float* gp, const float* ep, int i0, int end, uint32_t gid,
                                            uint32_t step, uint32_t s0, uint32_t s1, uint32_t k[4],
-                                           bool valid[4]) {
+                                           bool valid[4], float* up = nullptr,
+                                           const float* pp = nullptr, float wd = 0.f,
+                                           float mc = 0.f) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) valid[t] = i0 + t < end;
   if (KM == KM_RANDK) {
     randk_key4(i0, gid, step, s0, s1, k);
     return;
   }
+  // MC: the first pass turns g into the velocity u = mc·u + g' (stored to u) and, with EF, into
+  // u + e — stored back to g either way, so the later passes read what the compressor sees
   float4 v;
   if (i0 + 3 < end) {
     v = *reinterpret_cast<const float4*>(gp + i0);
+    if (MC) {
+      float4 u = *reinterpret_cast<const float4*>(up + i0);
+      float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (pp != nullptr) p = *reinterpret_cast<const float4*>(pp + i0);
+      v.x = mc_step(v.x, u.x, p.x, wd, mc); v.y = mc_step(v.y, u.y, p.y, wd, mc);
+      v.z = mc_step(v.z, u.z, p.z, wd, mc); v.w = mc_step(v.w, u.w, p.w, wd, mc);
+      *reinterpret_cast<float4*>(up + i0) = u;
+    }
     if (EFADD) {
       const float4 e = *reinterpret_cast<const float4*>(ep + i0);
       v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
-      *reinterpret_cast<float4*>(gp + i0) = v;
     }
+    if (EFADD || MC) *reinterpret_cast<float4*>(gp + i0) = v;
   } else {
     float t4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       if (valid[t]) {
         float x = gp[i0 + t];
-        if (EFADD) { x += ep[i0 + t]; gp[i0 + t] = x; }
+        if (MC) {
+          float u = up[i0 + t];
+          x = mc_step(x, u, pp != nullptr ? pp[i0 + t] : 0.f, wd, mc);
+          up[i0 + t] = u;
+        }
+        if (EFADD) x += ep[i0 + t];
+        if (EFADD || MC) gp[i0 + t] = x;
         t4[t] = x;
       }
     v = make_float4(t4[0], t4[1], t4[2], t4[3]);
@@ -301,7 +337,7 @@ __device__ __forceinline__ void fused_prev_select(const uint32_t* __restrict__ h
   }
 }
 
-template <int KM, int PASS, bool EFADD, bool FUSED = false>
+template <int KM, int PASS, bool EFADD, bool FUSED = false, bool MC = false>
 __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float* __restrict__ ef,
                                              const int64_t* __restrict__ seg_off,
                                              const int32_t* __restrict__ seg_n,
@@ -311,7 +347,8 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
                                              uint32_t* __restrict__ hist_all, uint32_t gid_base,
                                              uint32_t step_arg, uint32_t s0, uint32_t s1, const uint32_t* __restrict__ stepp,
                                              const int32_t* __restrict__ keep = nullptr,
-                                             const int32_t* __restrict__ task_lo = nullptr) {
+                                             const int32_t* __restrict__ task_lo = nullptr,
+                                             McArgs mcx = McArgs{}) {
   // graph-captured steps read the step counter from device memory (csrc/lw_kernels.h)
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   using C = PassCfg<PASS>;
@@ -375,13 +412,17 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
     float* gp = g + off;
     const float* ep = EFADD ? ef + off : nullptr;
     const int end = min(begin + EPB, n);
+    float* up = MC ? mcx.u + off : nullptr;
+    const float* pw = MC && mcx.p != nullptr ? mcx.p + off : nullptr;
+    const float wd = MC && mcx.wd != nullptr ? mcx.wd[s] * mcx.wmul : 0.f;
 #pragma unroll 2
     for (int j = 0; j < EPB / (NT * 4); ++j) {
       const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
       if (i0 >= end) break;
       uint32_t k[4];
       bool valid[4];
-      load4_keys<KM, EFADD>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid);
+      load4_keys<KM, EFADD, MC>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid, up, pw,
+                                wd, MC ? mcx.mc : 0.f);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if (valid[q] && (k[q] >> (C::SHIFT + C::BITS)) == prefix) {
@@ -1252,12 +1293,12 @@ __global__ __launch_bounds__(NT) void k_zero_words(uint32_t* __restrict__ p, int
 static int hist_tpb(int ntasks) { return ntasks >= LW_HIST_TPB_MIN ? LW_HIST_TPB : 1; }
 static int hist_blocks(int ntasks) { return (ntasks + hist_tpb(ntasks) - 1) / hist_tpb(ntasks); }
 
-template <int KM, int OUT, bool EF>
+template <int KM, int OUT, bool EF, bool MC = false>
 static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) {
   if (a.n_small > 0)
-    LW_LAUNCH((k_small_select<KM, OUT, EF>), a.n_small, st, a.g, a.ef, a.seg_off, a.seg_n, a.keep,
-              a.cap_off, a.small_segs, a.pairs, a.vals, a.idx_out, a.st_small, a.gid_base, a.step,
-              a.seed0, a.seed1, a.step_ptr, a.overflow, a.mom);
+    LW_LAUNCH((k_small_select<KM, OUT, EF, MC>), a.n_small, st, a.g, a.ef, a.seg_off, a.seg_n,
+              a.keep, a.cap_off, a.small_segs, a.pairs, a.vals, a.idx_out, a.st_small,
+              a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr, a.overflow, a.mom, a.mcx);
   if (a.n_large == 0) return;
   if (!staged) {      // (staged: select_stage already zeroed the histograms and ran pass 0)
     if (!LW_FUSED_SELECT) {    // (fused: the previous call's k_write left them zeroed)
@@ -1265,9 +1306,10 @@ static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) 
       const int64_t nb = (words + NT - 1) / NT;
       LW_LAUNCH(k_zero_words, (int)(nb < 1024 ? nb : 1024), st, a.hist, words);
     }
-    LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK>), hist_blocks(a.n_tasks), st, a.g, a.ef,
-              a.seg_off, a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
-              a.step_ptr);
+    LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK, false, MC>), hist_blocks(a.n_tasks), st, a.g,
+              a.ef, a.seg_off, a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks),
+              a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr,
+              (const int32_t*)nullptr, (const int32_t*)nullptr, a.mcx);
   }
   if (LW_FUSED_SELECT) {
     // 4-5 launches instead of 11: the digit selections ride in the next pass's workgroups; the
@@ -1314,6 +1356,12 @@ static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) 
 }
 
 void select_compress(const SelectArgs& a, int km, int out, bool ef, hipStream_t st, bool staged) {
+  if (a.mcx.u != nullptr) {      // fused momentum correction: Top-K pairs, unstaged
+    if (km != KM_TOPK || out != OUT_PAIRS || staged) return;   // (rejected by the binding)
+    ef ? select_compress_t<KM_TOPK, OUT_PAIRS, true, true>(a, false, st)
+       : select_compress_t<KM_TOPK, OUT_PAIRS, false, true>(a, false, st);
+    return;
+  }
   if (km == KM_TOPK && out == OUT_PAIRS) {
     ef ? select_compress_t<KM_TOPK, OUT_PAIRS, true>(a, staged, st)
        : select_compress_t<KM_TOPK, OUT_PAIRS, false>(a, staged, st);

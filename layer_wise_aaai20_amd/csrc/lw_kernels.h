@@ -33,6 +33,16 @@ struct SelState {
   uint32_t p0, m0, p1, m1;
 };
 
+// Momentum correction fused into the first pass of the Top-K chain (layer-wise buckets;
+// compress.hip mc_step): u = mc·u + (g + wmul·wd_s·p) per element, and the compressor sees u.
+// u == nullptr: no fused prologue (parallel/engine.py runs optim.hip k_mc_prep instead, or none).
+struct McArgs {
+  float* u;                    // velocity (the bucket's layout)
+  const float* p;              // parameters (nullptr: no weight decay)
+  const float* wd;             // [S] weight decay per codec segment (nullptr: none)
+  float mc, wmul;
+};
+
 struct SelectArgs {
   float* g;                    // bucket base (fp32 gradient arena slice)
   float* ef;                   // error-feedback residual (same layout) or nullptr
@@ -62,6 +72,7 @@ struct SelectArgs {
   // optional momentum-correction velocity (same layout as g): zeroed at every coordinate that was
   // sent, in segments that were not sent whole (those keep ordinary momentum)
   float* mom;
+  McArgs mcx;                  // fused momentum-correction prologue (mcx.u == nullptr: none)
   // optional device counter: elements the reference rule would send that did not fit the
   // payload (Top-K ties beyond the tie slack; threshold hits beyond a fixed sparse capacity)
   unsigned long long* overflow;

@@ -405,6 +405,13 @@ class GradSyncEngine:
             self._mc_plans[bi] = (plan, wd)
         return self._mc_plans[bi]
 
+    def _mc_fusable(self, bi: int, sel, g: torch.Tensor) -> bool:
+        """The velocity update can run inside the Top-K chain's first pass: a GPU Top-K codec
+        whose segments are the bucket's parameters (layer-wise), unstaged."""
+        return (g.device.type == "cuda" and type(sel) is TopkCodec and
+                self.mode == "layerwise" and not self._stages and
+                os.environ.get("LWAAAI_MC_FUSE", "1") != "0")
+
     def _mc_prologue(self, bi: int, g: torch.Tensor, u: torch.Tensor) -> None:
         """g' = g + wd·p/grad_scale ; u = mc·u + g' ; g = u over bucket ``bi``."""
         from ..ops._ext import ops_for
@@ -469,9 +476,10 @@ class GradSyncEngine:
         next step on). The caller must be the segment's only gradient contribution when it
         overwrites (ops/gemm.py _ReplicatedLinearFn: VGG-16's 103 M-weight fc1, whose zeroing
         plus read-add-write cost about three passes over 412 MB a step)."""
+        if os.environ.get("LWAAAI_CLAIM_OVERWRITE", "1") == "0":
+            return False                 # (not counted: the segment stays under zeroing)
         self._claims[seg_index] += 1
-        return self._claims[seg_index] == 1 and seg_index in self._no_zero and \
-            os.environ.get("LWAAAI_CLAIM_OVERWRITE", "1") != "0"
+        return self._claims[seg_index] == 1 and seg_index in self._no_zero
 
     def begin_step(self) -> None:
         """Zero the arena (but for the segments whole-written by a claimed overwrite in the last
@@ -570,12 +578,19 @@ class GradSyncEngine:
                 sel._staged = True
             if self.mom is not None:
                 u = self.mom[b.start:b.end]
-                self._mc_prologue(bi, g, u)              # velocity; the residual accumulates it
+                if self._mc_fusable(bi, sel, g):
+                    # velocity update in the first select pass (compress.hip McArgs)
+                    _, wd = self._mc_plan(bi)
+                    p = self.arena.param_buf[b.start:b.end] if wd is not None else None
+                    sel.mc_fuse = (p, wd, float(self.mc), float(self._mc_wmul))
+                else:
+                    self._mc_prologue(bi, g, u)          # velocity; the residual accumulates it
                 sel.mc_mom = u                           # masked by the select kernels
             send = codec.compress(g, e, self.step)
             sel._staged = False
             if u is not None:
                 sel.mc_mom = None
+                sel.mc_fuse = None
                 if not getattr(sel, "mc_fused", False):  # no selection: sent <=> residual 0
                     self._mc_mask(u, e)
             t1 = self._event() if self.timing else None

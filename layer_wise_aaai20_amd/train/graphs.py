@@ -29,6 +29,7 @@ correctly, but the step would then be as slow as the slowest mode).
 """
 from __future__ import annotations
 
+import gc
 import os
 import time
 import weakref
@@ -224,12 +225,21 @@ class StepGraph:
         graph = torch.cuda.CUDAGraph()
         # (each signature keeps its own private memory pool: graphs sharing a pool would alias
         # each other's step temporaries; 288 GB of HBM affords a few copies of the activations)
+        # no garbage collection while capturing: a collection triggered by the step's own
+        # allocations can free an unreachable object holding another HIP graph, whose destructor
+        # is not permitted during a capture (it aborted a process that built many trainers:
+        # "operation not permitted when stream is capturing" in ~CUDAGraph)
+        gc_on = gc.isenabled()
+        gc.collect()
+        gc.disable()
         try:
             # thread_local: RCCL's watchdog thread queries events while this thread captures
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 static_out = self.fn(*static_in)
             torch.cuda.synchronize(self.device)
         finally:
+            if gc_on:
+                gc.enable()
             # the capture ran the step's Python (finish() counted a step) but no kernel
             self.engine.step, self.engine.stats.steps = host_step
         while len(self._graphs) >= self.MAX_GRAPHS:

@@ -366,7 +366,11 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
   // traffic as counting one task's 8192 keys, so they are paid once per segment run of the
   // workgroup's tasks, not per task; a small launch keeps one task per workgroup so that it
   // still spreads over the CUs. Integer counts: the result does not depend on the grouping.
-  const int ta = blockIdx.x * tpb, tb = min(ntasks, ta + tpb);
+  // tpb < 0: the other way round, -tpb workgroups per task (a small launch spread over 4x the
+  // workgroups; each takes its share of the task's strides)
+  const int split = tpb < 0 ? -tpb : 1, per = tpb > 0 ? tpb : 1;
+  const int ta = (int)(blockIdx.x / split) * per, tb = min(ntasks, ta + per);
+  const int q_sub = (int)(blockIdx.x % split);
   auto flush = [&](int li) {
     uint32_t* gh = hist_all + (size_t)li * HIST_WORDS + C::HOFF;
     for (int b = threadIdx.x; b < NB; b += NT) {
@@ -400,8 +404,8 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
       for (int b = threadIdx.x; b < NB * CP; b += NT) h[b] = 0;
       cur = li;
       if constexpr (FUSED)
-        fused_prev_select<PASS>(hist_all, st, keep, li, large_segs[li], ti == task_lo[li], prefix,
-                                sarr, sscr, sres);
+        fused_prev_select<PASS>(hist_all, st, keep, li, large_segs[li],
+                                ti == task_lo[li] && q_sub == 0, prefix, sarr, sscr, sres);
       else
         prefix = PASS > 0 ? st[li].prefix : 0u;
       __syncthreads();
@@ -415,8 +419,9 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
     float* up = MC ? mcx.u + off : nullptr;
     const float* pw = MC && mcx.p != nullptr ? mcx.p + off : nullptr;
     const float wd = MC && mcx.wd != nullptr ? mcx.wd[s] * mcx.wmul : 0.f;
+    const int nstr = EPB / (NT * 4) / split;          // strides of NT*4 keys for this workgroup
 #pragma unroll 2
-    for (int j = 0; j < EPB / (NT * 4); ++j) {
+    for (int j = q_sub * nstr; j < (q_sub + 1) * nstr; ++j) {
       const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
       if (i0 >= end) break;
       uint32_t k[4];
@@ -542,7 +547,9 @@ __global__ __launch_bounds__(NT) void k_count_sel(float* __restrict__ g,
                                                   const uint32_t* __restrict__ stepp) {
   const uint32_t step = stepp != nullptr ? *stepp : step_arg;
   __shared__ uint32_t arr[NT], scr[NT / WAVE], res[2];
-  const int ta = blockIdx.x * tpb, tb = min(ntasks, ta + tpb);
+  const int split = tpb < 0 ? -tpb : 1, per = tpb > 0 ? tpb : 1;     // (as k_hist)
+  const int ta = (int)(blockIdx.x / split) * per, tb = min(ntasks, ta + per);
+  const int q_sub = (int)(blockIdx.x % split);
   int cur = -1;
   uint32_t tk = 0;
   for (int ti = ta; ti < tb; ++ti) {
@@ -562,7 +569,7 @@ __global__ __launch_bounds__(NT) void k_count_sel(float* __restrict__ g,
       const uint32_t hd = h[d];
       finish_state(S, KM, (uint32_t)keep[s], mn, hd, (uint32_t)(cap_off[s + 1] - cap_off[s]));
       tk = S.tkey;
-      if (ti == task_lo[li] && threadIdx.x == 0) {
+      if (ti == task_lo[li] && q_sub == 0 && threadIdx.x == 0) {
         SelState& o = st[li];
         o.prefix = S.prefix; o.m = S.m; o.tkey = S.tkey; o.quota = S.quota;
         o.cnt_gt = S.cnt_gt; o.total = S.total; o.cap = S.cap;
@@ -580,10 +587,12 @@ __global__ __launch_bounds__(NT) void k_count_sel(float* __restrict__ g,
     uint32_t c[kWriteSub];
 #pragma unroll
     for (int q = 0; q < kWriteSub; ++q) c[q] = 0;
+    // split == kWriteSub: this workgroup counts sub-task q_sub only
+    const int jlo = split > 1 ? q_sub * PER_SUB : 0, jhi = split > 1 ? jlo + PER_SUB : STRIDES;
 #pragma unroll
     for (int j = 0; j < STRIDES; ++j) {
       const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
-      if (i0 >= end) break;
+      if (j < jlo || j >= jhi || i0 >= end) continue;
       uint32_t k[4];
       bool valid[4];
       load4_keys<KM, false>(gp, nullptr, i0, end, gid_base + s, step, s0, s1, k, valid);
@@ -593,6 +602,7 @@ __global__ __launch_bounds__(NT) void k_count_sel(float* __restrict__ g,
     }
 #pragma unroll
     for (int q = 0; q < kWriteSub; ++q) {
+      if (split > 1 && q != q_sub) continue;        // (uniform)
       uint32_t tot;
       block_excl_scan<NT>(c[q], scr, tot);
       if (threadIdx.x == 0) cnt[ti * kWriteSub + q] = make_uint2(tot & 0xffffu, tot >> 16);
@@ -1290,8 +1300,13 @@ __global__ __launch_bounds__(NT) void k_zero_words(uint32_t* __restrict__ p, int
     p[i] = 0u;
 }
 
-static int hist_tpb(int ntasks) { return ntasks >= LW_HIST_TPB_MIN ? LW_HIST_TPB : 1; }
-static int hist_blocks(int ntasks) { return (ntasks + hist_tpb(ntasks) - 1) / hist_tpb(ntasks); }
+// tasks per histogram / count workgroup: LW_HIST_TPB on large launches; below LW_HIST_TPB_MIN
+// tasks, -kWriteSub: each task split over kWriteSub workgroups (k_hist, k_count_sel)
+static int hist_tpb(int ntasks) { return ntasks >= LW_HIST_TPB_MIN ? LW_HIST_TPB : -kWriteSub; }
+static int hist_blocks(int ntasks) {
+  const int t = hist_tpb(ntasks);
+  return t > 0 ? (ntasks + t - 1) / t : ntasks * -t;
+}
 
 template <int KM, int OUT, bool EF, bool MC = false>
 static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) {

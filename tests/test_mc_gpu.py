@@ -1,10 +1,11 @@
 """Momentum correction (DGC) fused into the compressor kernels:
 
-* the per-bucket prologue g' = g + wd·p/grad_scale, u = mc·u + g', g = u is one kernel
-  (csrc/optim.hip k_mc_prep) and the momentum factor masking (u = 0 at the sent coordinates of
-  tensors not sent whole) runs inside the select kernels (csrc/compress.hip k_small_select /
-  k_write) — the decoded gradient, the residual and the velocity equal the CPU mirror
-  (parallel/engine.py, codecs.py) bit for bit, step after step;
+* the per-bucket prologue g' = g + wd·p/grad_scale, u = mc·u + g', g = u runs inside the first
+  pass of the Top-K chain for layer-wise buckets (csrc/compress.hip McArgs in k_hist pass 0 /
+  k_small_select; one kernel, csrc/optim.hip k_mc_prep, otherwise) and the momentum factor
+  masking (u = 0 at the sent coordinates of tensors not sent whole) inside the select kernels
+  (k_small_select / k_write) — the decoded gradient, the residual and the velocity equal the CPU
+  mirror (parallel/engine.py, codecs.py) bit for bit, step after step;
 * the engine's step issues no ATen elementwise kernel for it (the four ATen passes it replaces:
   u.mul_().add_(), g.copy_(u), u.mul_(e != 0));
 * codecs without a selection (QSGD) mask with k_mc_mask, equal to u·[e != 0].
@@ -83,7 +84,9 @@ def test_fused_mc_issues_no_aten_elementwise_kernels():
         eng.sync_now()
         torch.cuda.synchronize()
     names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
-    assert any("k_mc_prep" in n for n in names), names
+    # the velocity update runs inside the first select pass (McArgs) — no k_mc_prep launch
+    assert any("McArgs" in n for n in names), names
+    assert not any("k_mc_prep" in n for n in names), names
     # what the fused path replaces: u.mul_(mc).add_(g), g.copy_(u), u.mul_(e != 0)
     bad = ("Mul", "mul", "Add", "add", "compare", "copy", "NE", "ne_kernel")
     aten = [n for n in names if "at::native" in n and any(k in n for k in bad)]

@@ -1300,9 +1300,16 @@ __global__ __launch_bounds__(NT) void k_zero_words(uint32_t* __restrict__ p, int
     p[i] = 0u;
 }
 
-// tasks per histogram / count workgroup: LW_HIST_TPB on large launches; below LW_HIST_TPB_MIN
-// tasks, -kWriteSub: each task split over kWriteSub workgroups (k_hist, k_count_sel)
-static int hist_tpb(int ntasks) { return ntasks >= LW_HIST_TPB_MIN ? LW_HIST_TPB : -kWriteSub; }
+// tasks per histogram / count workgroup: LW_HIST_TPB on large launches, 1 on mid-sized ones and,
+// below LW_HIST_SPLIT_MAX tasks, -kWriteSub: each task split over kWriteSub workgroups (k_hist,
+// k_count_sel). (Every workgroup zeroes and flushes a whole LDS histogram per segment: splitting a
+// ResNet-50 bucket's ~1.2 k tasks 4 ways cost 0.3 ms a step; AlexNet's one 281-task bucket gains.)
+#ifndef LW_HIST_SPLIT_MAX
+#define LW_HIST_SPLIT_MAX 512
+#endif
+static int hist_tpb(int ntasks) {
+  return ntasks >= LW_HIST_TPB_MIN ? LW_HIST_TPB : (ntasks < LW_HIST_SPLIT_MAX ? -kWriteSub : 1);
+}
 static int hist_blocks(int ntasks) {
   const int t = hist_tpb(ntasks);
   return t > 0 ? (ntasks + t - 1) / t : ntasks * -t;

@@ -428,12 +428,25 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
       bool valid[4];
       load4_keys<KM, EFADD, MC>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid, up, pw,
                                 wd, MC ? mcx.mc : 0.f);
+      // four consecutive keys with one digit (a replicated layer's gradient — VGG-16 fc1 repeats
+      // each value 49 times — or a flat region) are counted with one atomic
+      uint32_t bin[4];
+      bool in[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (valid[q] && (k[q] >> (C::SHIFT + C::BITS)) == prefix) {
-          if (KM != KM_RANDK && k[q] == 0u) ++zc;
-          else atomicAdd(&h[((k[q] >> C::SHIFT) & (NB - 1)) * CP + (threadIdx.x & (CP - 1))], 1u);
-        }
+      for (int q = 0; q < 4; ++q) {
+        in[q] = valid[q] && (k[q] >> (C::SHIFT + C::BITS)) == prefix;
+        if (KM != KM_RANDK && in[q] && k[q] == 0u) { ++zc; in[q] = false; }
+        bin[q] = (k[q] >> C::SHIFT) & (NB - 1);
+      }
+      uint32_t* hb = h + (threadIdx.x & (CP - 1));
+      if (in[0] && in[1] && in[2] && in[3] && bin[0] == bin[1] && bin[1] == bin[2] &&
+          bin[2] == bin[3]) {
+        atomicAdd(hb + bin[0] * CP, 4u);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (in[q]) atomicAdd(hb + bin[q] * CP, 1u);
+      }
     }
   }
   add_zeros();

@@ -45,6 +45,11 @@ static_assert((LW_HIST_CP & (LW_HIST_CP - 1)) == 0, "LW_HIST_CP: a power of two"
 #ifndef LW_HIST_TPB
 #define LW_HIST_TPB 4            // 8192-element tasks per histogram workgroup (see k_hist) once a
 #endif                           // launch has LW_HIST_TPB_MIN tasks; 1 below that
+#define LW_STR_(x) #x
+#define LW_PRAGMA_UNROLL(n) _Pragma(LW_STR_(unroll n))
+#ifndef LW_HIST_UNROLL
+#define LW_HIST_UNROLL 2         // strides of NT*4 keys in flight per k_hist loop iteration
+#endif
 #ifndef LW_HIST_TPB_MIN
 #define LW_HIST_TPB_MIN 2048
 #endif
@@ -420,16 +425,9 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
     const float* pw = MC && mcx.p != nullptr ? mcx.p + off : nullptr;
     const float wd = MC && mcx.wd != nullptr ? mcx.wd[s] * mcx.wmul : 0.f;
     const int nstr = EPB / (NT * 4) / split;          // strides of NT*4 keys for this workgroup
-#pragma unroll 2
-    for (int j = q_sub * nstr; j < (q_sub + 1) * nstr; ++j) {
-      const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
-      if (i0 >= end) break;
-      uint32_t k[4];
-      bool valid[4];
-      load4_keys<KM, EFADD, MC>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid, up, pw,
-                                wd, MC ? mcx.mc : 0.f);
-      // four consecutive keys with one digit (a replicated layer's gradient — VGG-16 fc1 repeats
-      // each value 49 times — or a flat region) are counted with one atomic
+    // four consecutive keys with one digit (a replicated layer's gradient — VGG-16 fc1 repeats
+    // each value 49 times — or a flat region) are counted with one atomic
+    auto count4 = [&](const uint32_t k[4], const bool valid[4]) {
       uint32_t bin[4];
       bool in[4];
 #pragma unroll
@@ -447,6 +445,66 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
         for (int q = 0; q < 4; ++q)
           if (in[q]) atomicAdd(hb + bin[q] * CP, 1u);
       }
+    };
+    const int j0 = q_sub * nstr;
+    if (KM != KM_RANDK && begin + (j0 + nstr) * NT * 4 <= end) {
+      // Every stride of this workgroup in bounds (all but a segment's last task): issue all its
+      // loads before the first use — up to 8 float4 per operand in flight per thread instead of
+      // the loop's 2, which a data-dependent bound keeps from being hoisted. One workgroup per CU
+      // (a 276-task entire-model bucket) was latency-bound at 2 strides in flight.
+      constexpr int MS = EPB / (NT * 4);
+      // momentum correction streams four operands: two batches of half the strides keep it
+      // below 256 VGPRs
+      constexpr int BATCH = MC ? MS / 2 : MS;
+      // (no early exit in these loops: they must unroll fully so the arrays stay in registers)
+#pragma unroll
+      for (int h = 0; h < MS; h += BATCH) {
+        float4 gv[BATCH], ev[BATCH], uv[BATCH], pv[BATCH];
+#pragma unroll
+        for (int jj = 0; jj < BATCH; ++jj) {
+          const int j = h + jj;
+          if (j < nstr) {
+            const int i0 = begin + (j0 + j) * NT * 4 + threadIdx.x * 4;
+            gv[jj] = *reinterpret_cast<const float4*>(gp + i0);
+            if (EFADD) ev[jj] = *reinterpret_cast<const float4*>(ep + i0);
+            if (MC) {
+              uv[jj] = *reinterpret_cast<const float4*>(up + i0);
+              pv[jj] = pw != nullptr ? *reinterpret_cast<const float4*>(pw + i0)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < BATCH; ++jj) {
+          const int j = h + jj;
+          if (j >= nstr) continue;
+          const int i0 = begin + (j0 + j) * NT * 4 + threadIdx.x * 4;
+          float4 v = gv[jj];
+          if (MC) {
+            const float mc = mcx.mc;
+            float4 u = uv[jj];
+            v.x = mc_step(v.x, u.x, pv[jj].x, wd, mc); v.y = mc_step(v.y, u.y, pv[jj].y, wd, mc);
+            v.z = mc_step(v.z, u.z, pv[jj].z, wd, mc); v.w = mc_step(v.w, u.w, pv[jj].w, wd, mc);
+            *reinterpret_cast<float4*>(up + i0) = u;
+          }
+          if (EFADD) { v.x += ev[jj].x; v.y += ev[jj].y; v.z += ev[jj].z; v.w += ev[jj].w; }
+          if (EFADD || MC) *reinterpret_cast<float4*>(gp + i0) = v;
+          const uint32_t k[4] = {abs_key(v.x), abs_key(v.y), abs_key(v.z), abs_key(v.w)};
+          const bool valid[4] = {true, true, true, true};
+          count4(k, valid);
+        }
+      }
+      continue;
+    }
+    LW_PRAGMA_UNROLL(LW_HIST_UNROLL)
+    for (int j = j0; j < j0 + nstr; ++j) {
+      const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
+      if (i0 >= end) break;
+      uint32_t k[4];
+      bool valid[4];
+      load4_keys<KM, EFADD, MC>(gp, ep, i0, end, gid_base + s, step, s0, s1, k, valid, up, pw,
+                                wd, MC ? mcx.mc : 0.f);
+      count4(k, valid);
     }
   }
   add_zeros();
@@ -602,16 +660,35 @@ __global__ __launch_bounds__(NT) void k_count_sel(float* __restrict__ g,
     for (int q = 0; q < kWriteSub; ++q) c[q] = 0;
     // split == kWriteSub: this workgroup counts sub-task q_sub only
     const int jlo = split > 1 ? q_sub * PER_SUB : 0, jhi = split > 1 ? jlo + PER_SUB : STRIDES;
+    if (KM != KM_RANDK && begin + jhi * NT * 4 <= end) {
+      // all of this workgroup's strides in bounds: every load issued before the first compare
+      // (as k_hist's fast path)
+      float4 gv[STRIDES];
 #pragma unroll
-    for (int j = 0; j < STRIDES; ++j) {
-      const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
-      if (j < jlo || j >= jhi || i0 >= end) continue;
-      uint32_t k[4];
-      bool valid[4];
-      load4_keys<KM, false>(gp, nullptr, i0, end, gid_base + s, step, s0, s1, k, valid);
+      for (int j = 0; j < STRIDES; ++j)
+        if (j >= jlo && j < jhi)
+          gv[j] = *reinterpret_cast<const float4*>(gp + begin + j * NT * 4 + threadIdx.x * 4);
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (valid[q]) c[j / PER_SUB] += (k[q] > tk ? 1u : 0u) + (k[q] == tk ? 0x10000u : 0u);
+      for (int j = 0; j < STRIDES; ++j) {
+        if (j < jlo || j >= jhi) continue;
+        const uint32_t k[4] = {abs_key(gv[j].x), abs_key(gv[j].y), abs_key(gv[j].z),
+                               abs_key(gv[j].w)};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          c[j / PER_SUB] += (k[q] > tk ? 1u : 0u) + (k[q] == tk ? 0x10000u : 0u);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < STRIDES; ++j) {
+        const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
+        if (j < jlo || j >= jhi || i0 >= end) continue;
+        uint32_t k[4];
+        bool valid[4];
+        load4_keys<KM, false>(gp, nullptr, i0, end, gid_base + s, step, s0, s1, k, valid);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (valid[q]) c[j / PER_SUB] += (k[q] > tk ? 1u : 0u) + (k[q] == tk ? 0x10000u : 0u);
+      }
     }
 #pragma unroll
     for (int q = 0; q < kWriteSub; ++q) {
@@ -840,9 +917,11 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
   uint32_t tot;
   const uint32_t p = block_excl_scan<NT>(cg | (ce << 16), scr, tot);
   uint32_t gb = bp.x + (p & 0xffffu), eb = bp.y + (p >> 16);
+  float eo[EW];                                 // the residual left at each element
 #pragma unroll
   for (int k = 0; k < EW; ++k) {
     const int i = i_base + k;
+    eo[k] = v[k];
     if (i >= end) break;
     bool sel = false;
     uint32_t pos = 0;
@@ -852,8 +931,21 @@ __global__ __launch_bounds__(NT) void k_write(float* __restrict__ g, float* __re
       if (OUT == OUT_PAIRS) pairs[c0 + pos] = make_int2(i, __float_as_int(v[k]));
       else { vals[c0 + pos] = v[k]; idx_out[c0 + pos] = i; }
       if (mp != nullptr) mp[i] = 0.f;
+      eo[k] = 0.f;
     }
-    if (EF) ep[i] = sel ? 0.f : v[k];
+  }
+  // the residual as whole float4 stores (one per 4 elements, not one dword per lane each)
+  if (EF) {
+    if (i_base + EW <= end) {
+#pragma unroll
+      for (int q = 0; q < EW / 4; ++q)
+        *reinterpret_cast<float4*>(ep + i_base + 4 * q) =
+            make_float4(eo[4 * q], eo[4 * q + 1], eo[4 * q + 2], eo[4 * q + 3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < EW; ++k)
+        if (i_base + k < end) ep[i_base + k] = eo[k];
+    }
   }
   // (k_fill_tail folded in: the workgroup of the segment's last task pads the unused pair slots;
   // no workgroup writes a slot at or past S.total)
@@ -1327,6 +1419,22 @@ static int hist_blocks(int ntasks) {
   const int t = hist_tpb(ntasks);
   return t > 0 ? (ntasks + t - 1) / t : ntasks * -t;
 }
+// Pass 0 of a split launch: LW_HIST0_SPLIT workgroups per task (1, 2 or 4). Not split: pass 0
+// counts every key, so each of its workgroups merges a dense 2048-bin histogram into the
+// segment's one with global atomics — executed at the memory side, where adds to one word
+// serialise — and 4x the workgroups meant 4x those merges: AlexNet's 276-task entire-model
+// bucket 25 -> 14 µs (scripts/probes/select_probe.hip, profiles/r5/select_probe.jsonl).
+#ifndef LW_HIST0_SPLIT
+#define LW_HIST0_SPLIT 1
+#endif
+static int hist0_tpb(int ntasks) {
+  const int t = hist_tpb(ntasks);
+  return t > 0 ? t : -LW_HIST0_SPLIT;
+}
+static int hist0_blocks(int ntasks) {
+  const int t = hist0_tpb(ntasks);
+  return t > 0 ? (ntasks + t - 1) / t : ntasks * -t;
+}
 
 template <int KM, int OUT, bool EF, bool MC = false>
 static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) {
@@ -1341,8 +1449,8 @@ static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) 
       const int64_t nb = (words + NT - 1) / NT;
       LW_LAUNCH(k_zero_words, (int)(nb < 1024 ? nb : 1024), st, a.hist, words);
     }
-    LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK, false, MC>), hist_blocks(a.n_tasks), st, a.g,
-              a.ef, a.seg_off, a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks),
+    LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK, false, MC>), hist0_blocks(a.n_tasks), st, a.g,
+              a.ef, a.seg_off, a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist0_tpb(a.n_tasks),
               a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr,
               (const int32_t*)nullptr, (const int32_t*)nullptr, a.mcx);
   }
@@ -1428,16 +1536,16 @@ void select_stage(const SelectArgs& a, int km, bool ef, int t_lo, int t_hi, bool
   const int2* tk = a.tasks + t_lo;
   if (km == KM_TOPK) {
     if (ef)
-      LW_LAUNCH((k_hist<KM_TOPK, 0, true>), hist_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
-                a.seg_n, a.large_segs, tk, t_hi - t_lo, hist_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+      LW_LAUNCH((k_hist<KM_TOPK, 0, true>), hist0_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
+                a.seg_n, a.large_segs, tk, t_hi - t_lo, hist0_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
                 a.step_ptr);
     else
-      LW_LAUNCH((k_hist<KM_TOPK, 0, false>), hist_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
-                a.seg_n, a.large_segs, tk, t_hi - t_lo, hist_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+      LW_LAUNCH((k_hist<KM_TOPK, 0, false>), hist0_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
+                a.seg_n, a.large_segs, tk, t_hi - t_lo, hist0_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
                 a.step_ptr);
   } else {
-    LW_LAUNCH((k_hist<KM_RANDK, 0, false>), hist_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
-              a.seg_n, a.large_segs, tk, t_hi - t_lo, hist_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
+    LW_LAUNCH((k_hist<KM_RANDK, 0, false>), hist0_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
+              a.seg_n, a.large_segs, tk, t_hi - t_lo, hist0_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
               a.step_ptr);
   }
 }

@@ -90,24 +90,24 @@ template <> struct PassCfg<2> { static constexpr int BITS = 10, SHIFT = 0, HOFF 
 
 // Find the digit d holding the m-th largest key of histogram h (NB bins) and the rank of that key
 // within bin d. Block-wide; all threads return the same values.
-template <int NB>
+template <int NB, int TB = NT>
 __device__ __forceinline__ void select_digit(const uint32_t* h, uint32_t m, uint32_t& d_out,
-                                             uint32_t& m_out, uint32_t* arr /*NT*/,
-                                             uint32_t* scr /*4*/, uint32_t* res /*2*/) {
-  constexpr int BPT = NB / NT;
+                                             uint32_t& m_out, uint32_t* arr /*TB*/,
+                                             uint32_t* scr /*TB/WAVE*/, uint32_t* res /*2*/) {
+  constexpr int BPT = NB / TB;
   const int j = threadIdx.x;
   uint32_t loc[BPT];
   uint32_t sum = 0;
 #pragma unroll
   for (int b = 0; b < BPT; ++b) { loc[b] = h[j * BPT + b]; sum += loc[b]; }
   if (j == 0) { res[0] = 0; res[1] = m; }
-  arr[NT - 1 - j] = sum;
+  arr[TB - 1 - j] = sum;
   __syncthreads();
   uint32_t tot;
-  const uint32_t e = block_excl_scan<NT>(arr[j], scr, tot);
+  const uint32_t e = block_excl_scan<TB>(arr[j], scr, tot);
   arr[j] = e;
   __syncthreads();
-  const uint32_t above = arr[NT - 1 - j];   // keys in bins above this thread's range
+  const uint32_t above = arr[TB - 1 - j];   // keys in bins above this thread's range
   if (above < m && m <= above + sum) {
     uint32_t cum = above;
 #pragma unroll

@@ -50,6 +50,9 @@ static_assert((LW_HIST_CP & (LW_HIST_CP - 1)) == 0, "LW_HIST_CP: a power of two"
 #ifndef LW_HIST_UNROLL
 #define LW_HIST_UNROLL 2         // strides of NT*4 keys in flight per k_hist loop iteration
 #endif
+#ifndef LW_HIST_MC_FAST
+#define LW_HIST_MC_FAST 1        // momentum-corrected pass 0 takes k_hist's batched-load path too
+#endif
 #ifndef LW_HIST_TPB_MIN
 #define LW_HIST_TPB_MIN 2048
 #endif
@@ -447,7 +450,7 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
       }
     };
     const int j0 = q_sub * nstr;
-    if (KM != KM_RANDK && begin + (j0 + nstr) * NT * 4 <= end) {
+    if (KM != KM_RANDK && (!MC || LW_HIST_MC_FAST) && begin + (j0 + nstr) * NT * 4 <= end) {
       // Every stride of this workgroup in bounds (all but a segment's last task): issue all its
       // loads before the first use — up to 8 float4 per operand in flight per thread instead of
       // the loop's 2, which a data-dependent bound keeps from being hoisted. One workgroup per CU

@@ -4,7 +4,7 @@
 // binaries so variants can be compared on one box without rebuilding the extension:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I layer_wise_aaai20_amd/csrc [-D...] \
 //     scripts/probes/select_probe.hip -o /tmp/select_probe
-//   select_probe [N] [K fraction] [iters]
+//   select_probe [N] [K fraction] [iters] [mc]
 // Prints one JSON line: mean µs of the chain (events around select_compress only; the gradient
 // and residual are restored from pristine copies before every call).
 #include "compress.hip"
@@ -43,6 +43,7 @@ int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? std::atoll(argv[1]) : 9042734;
   const double kf = argc > 2 ? std::atof(argv[2]) : 0.01;
   const int iters = argc > 3 ? std::atoi(argv[3]) : 50;
+  const bool mc = argc > 4 && std::atoi(argv[4]) != 0;   // fused momentum correction (u, p, wd)
   const int m = (int)std::max<int64_t>(1, (int64_t)(kf * (double)n));
   const int cap = m + std::max(64, m / 64);
   const int ntasks = (int)((n + lw::kLargeEPB - 1) / lw::kLargeEPB);
@@ -85,6 +86,15 @@ int main(int argc, char** argv) {
   CK(hipMemset(ovf, 0, 8));
   a.overflow = ovf;
 
+  if (mc) {                              // u = 0.9·u + g + 1e-4·p in the first pass
+    float *u, *p, *wd;
+    CK(hipMalloc(&u, n * 4)); CK(hipMalloc(&p, n * 4)); CK(hipMalloc(&wd, 4));
+    hipLaunchKernelGGL(k_fill, dim3(fb), dim3(256), 0, 0, u, n, 7u, 0.1f);
+    hipLaunchKernelGGL(k_fill, dim3(fb), dim3(256), 0, 0, p, n, 11u, 1.f);
+    const float w = 1e-4f;
+    CK(hipMemcpy(wd, &w, 4, hipMemcpyHostToDevice));
+    a.mcx = lw::McArgs{u, p, wd, 0.9f, 1.f};
+  }
   hipStream_t st;
   CK(hipStreamCreate(&st));
   hipEvent_t ea, eb;

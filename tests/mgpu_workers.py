@@ -29,7 +29,7 @@ def _worker(rank, world, port, fn, outdir, args, env):
     import sys
     faulthandler.enable(file=sys.stderr)          # a rank's fatal signal names its Python frame
     # a rank stuck in a collective prints every thread's stack before the harness gives up on it
-    faulthandler.dump_traceback_later(int(os.environ.get("LWAAAI_TEST_STACK_AFTER", "100")),
+    faulthandler.dump_traceback_later(int(os.environ.get("LWAAAI_TEST_STACK_AFTER", "90")),
                                       exit=False, file=sys.stderr)
     res = None
     try:
@@ -56,10 +56,26 @@ def _worker(rank, world, port, fn, outdir, args, env):
 
 
 def run_world(fn, world, args=(), env=None):
+    """Run ``fn`` on ``world`` spawned ranks. A world that has not finished after
+    ``LWAAAI_TEST_WORLD_TIMEOUT`` seconds (default 150; each rank prints every thread's stack at
+    ``LWAAAI_TEST_STACK_AFTER``, 90 s) is killed — its own child processes, by PID — and the test
+    fails, so a rank stuck in a collective cannot stall the rest of the suite."""
+    import time
     port = free_port()
+    limit = float(os.environ.get("LWAAAI_TEST_WORLD_TIMEOUT", "150"))
     with tempfile.TemporaryDirectory() as d:
-        mp.start_processes(_worker, args=(world, port, fn, d, args, dict(env or {})),
-                           nprocs=world, start_method="spawn", join=True)
+        ctx = mp.start_processes(_worker, args=(world, port, fn, d, args, dict(env or {})),
+                                 nprocs=world, start_method="spawn", join=False)
+        t0 = time.monotonic()
+        while not ctx.join(timeout=5):
+            if time.monotonic() - t0 > limit:
+                for p in ctx.processes:
+                    if p.is_alive():
+                        p.kill()
+                for p in ctx.processes:
+                    p.join(10)
+                raise AssertionError(f"the {world} ranks did not finish within {limit:.0f} s "
+                                     "(their stacks are in the captured stderr)")
         out = []
         for r in range(world):
             with open(os.path.join(d, f"r{r}.pkl"), "rb") as f:

@@ -228,6 +228,8 @@ void select_stage(Tensor g, c10::optional<Tensor> ef, Tensor seg_off, Tensor seg
   a.step_ptr = step_ptr(step_t);
   a.seed0 = (uint32_t)(seed & 0xffffffff);
   a.seed1 = (uint32_t)((uint64_t)seed >> 32);
+  // (one entire-model segment: this stage's tasks all add into its one histogram)
+  a.max_seg_tasks = a.n_large == 1 ? (int)(t_hi - t_lo) : 0;
   lw::select_stage(a, (int)km, a.ef != nullptr, (int)t_lo, (int)t_hi, zero, cur_stream());
   launched("select_stage");
 }

@@ -29,6 +29,9 @@
 #include "elem16.h"
 #include "sgd_elem.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace lw {
 
 constexpr int NT = 256;
@@ -345,8 +348,8 @@ __device__ __forceinline__ void fused_prev_select(const uint32_t* __restrict__ h
   }
 }
 
-template <int KM, int PASS, bool EFADD, bool FUSED = false, bool MC = false>
-__global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float* __restrict__ ef,
+template <int KM, int PASS, bool EFADD, bool FUSED = false, bool MC = false, int TB = NT>
+__global__ __launch_bounds__(TB) void k_hist(float* __restrict__ g, const float* __restrict__ ef,
                                              const int64_t* __restrict__ seg_off,
                                              const int32_t* __restrict__ seg_n,
                                              const int32_t* __restrict__ large_segs,
@@ -367,6 +370,8 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
   // passes 1/2 count only the keys under the selected prefix and keep one copy.
   constexpr int CP = PASS == 0 ? LW_HIST_CP : 1;
   static_assert(!FUSED || PASS > 0, "pass 0 has no previous selection");
+  static_assert(!FUSED || TB == NT, "the fused digit selection runs on NT threads");
+  static_assert(EPB % (TB * 4) == 0, "whole strides per task");
   __shared__ uint32_t h[NB * CP];
   __shared__ uint32_t sarr[FUSED ? NT : 1], sscr[NT / WAVE], sres[2];
   // A workgroup takes `tpb` consecutive tasks (LW_HIST_TPB on large launches): zeroing the LDS
@@ -381,7 +386,7 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
   const int q_sub = (int)(blockIdx.x % split);
   auto flush = [&](int li) {
     uint32_t* gh = hist_all + (size_t)li * HIST_WORDS + C::HOFF;
-    for (int b = threadIdx.x; b < NB; b += NT) {
+    for (int b = threadIdx.x; b < NB; b += TB) {
       uint32_t c = 0;
 #pragma unroll
       for (int j = 0; j < CP; ++j) c += h[b * CP + j];
@@ -409,7 +414,7 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
         flush(cur);
       }
       __syncthreads();
-      for (int b = threadIdx.x; b < NB * CP; b += NT) h[b] = 0;
+      for (int b = threadIdx.x; b < NB * CP; b += TB) h[b] = 0;
       cur = li;
       if constexpr (FUSED)
         fused_prev_select<PASS>(hist_all, st, keep, li, large_segs[li],
@@ -427,7 +432,7 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
     float* up = MC ? mcx.u + off : nullptr;
     const float* pw = MC && mcx.p != nullptr ? mcx.p + off : nullptr;
     const float wd = MC && mcx.wd != nullptr ? mcx.wd[s] * mcx.wmul : 0.f;
-    const int nstr = EPB / (NT * 4) / split;          // strides of NT*4 keys for this workgroup
+    const int nstr = EPB / (TB * 4) / split;          // strides of TB*4 keys for this workgroup
     // four consecutive keys with one digit (a replicated layer's gradient — VGG-16 fc1 repeats
     // each value 49 times — or a flat region) are counted with one atomic
     auto count4 = [&](const uint32_t k[4], const bool valid[4]) {
@@ -450,15 +455,15 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
       }
     };
     const int j0 = q_sub * nstr;
-    if (KM != KM_RANDK && (!MC || LW_HIST_MC_FAST) && begin + (j0 + nstr) * NT * 4 <= end) {
+    if (KM != KM_RANDK && (!MC || LW_HIST_MC_FAST) && begin + (j0 + nstr) * TB * 4 <= end) {
       // Every stride of this workgroup in bounds (all but a segment's last task): issue all its
       // loads before the first use — up to 8 float4 per operand in flight per thread instead of
       // the loop's 2, which a data-dependent bound keeps from being hoisted. One workgroup per CU
       // (a 276-task entire-model bucket) was latency-bound at 2 strides in flight.
-      constexpr int MS = EPB / (NT * 4);
+      constexpr int MS = EPB / (TB * 4);
       // momentum correction streams four operands: two batches of half the strides keep it
       // below 256 VGPRs
-      constexpr int BATCH = MC ? MS / 2 : MS;
+      constexpr int BATCH = MC && MS > 1 ? MS / 2 : MS;
       // (no early exit in these loops: they must unroll fully so the arrays stay in registers)
 #pragma unroll
       for (int h = 0; h < MS; h += BATCH) {
@@ -467,7 +472,7 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
         for (int jj = 0; jj < BATCH; ++jj) {
           const int j = h + jj;
           if (j < nstr) {
-            const int i0 = begin + (j0 + j) * NT * 4 + threadIdx.x * 4;
+            const int i0 = begin + (j0 + j) * TB * 4 + threadIdx.x * 4;
             gv[jj] = *reinterpret_cast<const float4*>(gp + i0);
             if (EFADD) ev[jj] = *reinterpret_cast<const float4*>(ep + i0);
             if (MC) {
@@ -481,7 +486,7 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
         for (int jj = 0; jj < BATCH; ++jj) {
           const int j = h + jj;
           if (j >= nstr) continue;
-          const int i0 = begin + (j0 + j) * NT * 4 + threadIdx.x * 4;
+          const int i0 = begin + (j0 + j) * TB * 4 + threadIdx.x * 4;
           float4 v = gv[jj];
           if (MC) {
             const float mc = mcx.mc;
@@ -501,7 +506,7 @@ __global__ __launch_bounds__(NT) void k_hist(float* __restrict__ g, const float*
     }
     LW_PRAGMA_UNROLL(LW_HIST_UNROLL)
     for (int j = j0; j < j0 + nstr; ++j) {
-      const int i0 = begin + j * NT * 4 + threadIdx.x * 4;
+      const int i0 = begin + j * TB * 4 + threadIdx.x * 4;
       if (i0 >= end) break;
       uint32_t k[4];
       bool valid[4];
@@ -1438,6 +1443,41 @@ static int hist0_blocks(int ntasks) {
   const int t = hist0_tpb(ntasks);
   return t > 0 ? (ntasks + t - 1) / t : ntasks * -t;
 }
+// Pass 0 of a launch whose longest segment has LW_HIST0_BIG_MIN tasks or more: 1024-thread
+// workgroups of several tasks each (LWAAAI_HIST0_BIG=0: the 256-thread grid above). The histogram
+// merges execute one per word at the memory side, so their time grows with how many workgroups
+// add into one segment's hot bins, not with the workgroup size. Tasks per workgroup = the longest
+// segment's tasks / 64 (2..16): about 64 merges per hot bin while a layer-wise bucket keeps
+// hundreds of workgroups for its bandwidth. Same keys per thread, same waves per launch.
+// AlexNet's 276-task entire-model bucket: pass 0 13.8 -> 10.7 µs on its real gradient; 9 M
+// elements 39 -> 29 µs (profiles/r5/select_probe_hist0_big.jsonl).
+#ifndef LW_HIST0_BIG_MIN
+#define LW_HIST0_BIG_MIN 128
+#endif
+constexpr int TB0 = 1024;
+static int hist0_big_tpb(int max_seg_tasks) {
+  static const bool on = [] {
+    const char* e = std::getenv("LWAAAI_HIST0_BIG");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  if (!on || max_seg_tasks < LW_HIST0_BIG_MIN) return 0;
+  return std::min(16, std::max(2, max_seg_tasks / 64));
+}
+
+template <int KM, bool EFADD, bool MC>
+static void launch_hist0(const SelectArgs& a, const int2* tk, int nt, hipStream_t st) {
+  if (const int t = hist0_big_tpb(a.max_seg_tasks)) {
+    hipLaunchKernelGGL((k_hist<KM, 0, EFADD, false, MC, TB0>), dim3((nt + t - 1) / t), dim3(TB0),
+                       0, st, a.g, a.ef, a.seg_off, a.seg_n, a.large_segs, tk, nt, t, a.st_large,
+                       a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr,
+                       (const int32_t*)nullptr, (const int32_t*)nullptr, a.mcx);
+  } else {
+    LW_LAUNCH((k_hist<KM, 0, EFADD, false, MC>), hist0_blocks(nt), st, a.g, a.ef, a.seg_off,
+              a.seg_n, a.large_segs, tk, nt, hist0_tpb(nt), a.st_large, a.hist, a.gid_base,
+              a.step, a.seed0, a.seed1, a.step_ptr, (const int32_t*)nullptr,
+              (const int32_t*)nullptr, a.mcx);
+  }
+}
 
 template <int KM, int OUT, bool EF, bool MC = false>
 static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) {
@@ -1452,10 +1492,7 @@ static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) 
       const int64_t nb = (words + NT - 1) / NT;
       LW_LAUNCH(k_zero_words, (int)(nb < 1024 ? nb : 1024), st, a.hist, words);
     }
-    LW_LAUNCH((k_hist<KM, 0, EF && KM == KM_TOPK, false, MC>), hist0_blocks(a.n_tasks), st, a.g,
-              a.ef, a.seg_off, a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist0_tpb(a.n_tasks),
-              a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1, a.step_ptr,
-              (const int32_t*)nullptr, (const int32_t*)nullptr, a.mcx);
+    launch_hist0<KM, EF && KM == KM_TOPK, MC>(a, a.tasks, a.n_tasks, st);
   }
   if (LW_FUSED_SELECT) {
     // 4-5 launches instead of 11: the digit selections ride in the next pass's workgroups; the
@@ -1538,18 +1575,10 @@ void select_stage(const SelectArgs& a, int km, bool ef, int t_lo, int t_hi, bool
   if (t_hi <= t_lo) return;
   const int2* tk = a.tasks + t_lo;
   if (km == KM_TOPK) {
-    if (ef)
-      LW_LAUNCH((k_hist<KM_TOPK, 0, true>), hist0_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
-                a.seg_n, a.large_segs, tk, t_hi - t_lo, hist0_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
-                a.step_ptr);
-    else
-      LW_LAUNCH((k_hist<KM_TOPK, 0, false>), hist0_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
-                a.seg_n, a.large_segs, tk, t_hi - t_lo, hist0_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
-                a.step_ptr);
+    if (ef) launch_hist0<KM_TOPK, true, false>(a, tk, t_hi - t_lo, st);
+    else launch_hist0<KM_TOPK, false, false>(a, tk, t_hi - t_lo, st);
   } else {
-    LW_LAUNCH((k_hist<KM_RANDK, 0, false>), hist0_blocks(t_hi - t_lo), st, a.g, a.ef, a.seg_off,
-              a.seg_n, a.large_segs, tk, t_hi - t_lo, hist0_tpb(t_hi - t_lo), a.st_large, a.hist, a.gid_base, a.step, a.seed0, a.seed1,
-              a.step_ptr);
+    launch_hist0<KM_RANDK, false, false>(a, tk, t_hi - t_lo, st);
   }
 }
 

@@ -4,7 +4,7 @@
 // binaries so variants can be compared on one box without rebuilding the extension:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I layer_wise_aaai20_amd/csrc [-D...] \
 //     scripts/probes/select_probe.hip -o /tmp/select_probe
-//   select_probe [N] [K fraction] [iters] [mc]
+//   select_probe [N] [K fraction] [iters] [mc] [g.f32 e.f32]
 // Prints one JSON line: mean µs of the chain (events around select_compress only; the gradient
 // and residual are restored from pristine copies before every call).
 #include "compress.hip"
@@ -54,6 +54,18 @@ int main(int argc, char** argv) {
   const int fb = (int)((n + 255) / 256);
   hipLaunchKernelGGL(k_fill, dim3(fb), dim3(256), 0, 0, g0, n, 1u, 1.f);
   hipLaunchKernelGGL(k_fill, dim3(fb), dim3(256), 0, 0, e0, n, 99u, 0.3f);
+  if (argc > 6) {                        // real gradient / residual (scripts/probes/dump_em_grad.py)
+    for (int w = 0; w < 2; ++w) {
+      std::vector<float> h(n);
+      FILE* f = std::fopen(argv[5 + w], "rb");
+      if (f == nullptr || std::fread(h.data(), 4, n, f) != (size_t)n) {
+        std::fprintf(stderr, "cannot read %lld floats from %s\n", (long long)n, argv[5 + w]);
+        return 2;
+      }
+      std::fclose(f);
+      CK(hipMemcpy(w == 0 ? g0 : e0, h.data(), 4 * n, hipMemcpyHostToDevice));
+    }
+  }
 
   std::vector<int64_t> seg_off = {0, n}, cap_off = {0, cap};
   std::vector<int32_t> seg_n = {(int32_t)n}, keep = {m}, large = {0}, task_lo = {0, ntasks};

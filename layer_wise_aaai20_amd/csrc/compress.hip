@@ -328,7 +328,7 @@ __device__ __forceinline__ void load4_keys(float* gp, const float* ep, int i0, i
 // a k_select launch of its own — every workgroup derives the identical digit. The workgroup that
 // holds the segment's first task publishes it (SelState p0/m0 after pass 0, p1/m1 after pass 1)
 // for the next launch; no workgroup of this launch reads those fields.
-template <int PASS>
+template <int PASS, int TB = NT>
 __device__ __forceinline__ void fused_prev_select(const uint32_t* __restrict__ hist_all,
                                                   SelState* __restrict__ st,
                                                   const int32_t* __restrict__ keep, int li, int s,
@@ -337,12 +337,12 @@ __device__ __forceinline__ void fused_prev_select(const uint32_t* __restrict__ h
   const uint32_t* hb = hist_all + (size_t)li * HIST_WORDS;
   uint32_t d, mn;
   if constexpr (PASS == 1) {
-    select_digit<2048>(hb + PassCfg<0>::HOFF, (uint32_t)keep[s], d, mn, arr, scr, res);
+    select_digit<2048, TB>(hb + PassCfg<0>::HOFF, (uint32_t)keep[s], d, mn, arr, scr, res);
     prefix = d;
     if (publish && threadIdx.x == 0) { st[li].p0 = prefix; st[li].m0 = mn; }
   } else {
     const uint32_t p0 = st[li].p0;
-    select_digit<1024>(hb + PassCfg<1>::HOFF, st[li].m0, d, mn, arr, scr, res);
+    select_digit<1024, TB>(hb + PassCfg<1>::HOFF, st[li].m0, d, mn, arr, scr, res);
     prefix = (p0 << PassCfg<1>::BITS) | d;
     if (publish && threadIdx.x == 0) { st[li].p1 = prefix; st[li].m1 = mn; }
   }
@@ -370,10 +370,9 @@ __global__ __launch_bounds__(TB) void k_hist(float* __restrict__ g, const float*
   // passes 1/2 count only the keys under the selected prefix and keep one copy.
   constexpr int CP = PASS == 0 ? LW_HIST_CP : 1;
   static_assert(!FUSED || PASS > 0, "pass 0 has no previous selection");
-  static_assert(!FUSED || TB == NT, "the fused digit selection runs on NT threads");
   static_assert(EPB % (TB * 4) == 0, "whole strides per task");
   __shared__ uint32_t h[NB * CP];
-  __shared__ uint32_t sarr[FUSED ? NT : 1], sscr[NT / WAVE], sres[2];
+  __shared__ uint32_t sarr[FUSED ? TB : 1], sscr[TB / WAVE], sres[2];
   // A workgroup takes `tpb` consecutive tasks (LW_HIST_TPB on large launches): zeroing the LDS
   // histogram (NB * CP words) and merging it into the segment's global one cost about as much LDS
   // traffic as counting one task's 8192 keys, so they are paid once per segment run of the
@@ -417,7 +416,7 @@ __global__ __launch_bounds__(TB) void k_hist(float* __restrict__ g, const float*
       for (int b = threadIdx.x; b < NB * CP; b += TB) h[b] = 0;
       cur = li;
       if constexpr (FUSED)
-        fused_prev_select<PASS>(hist_all, st, keep, li, large_segs[li],
+        fused_prev_select<PASS, TB>(hist_all, st, keep, li, large_segs[li],
                                 ti == task_lo[li] && q_sub == 0, prefix, sarr, sscr, sres);
       else
         prefix = PASS > 0 ? st[li].prefix : 0u;
@@ -1497,6 +1496,8 @@ static void select_compress_t(const SelectArgs& a, bool staged, hipStream_t st) 
   if (LW_FUSED_SELECT) {
     // 4-5 launches instead of 11: the digit selections ride in the next pass's workgroups; the
     // payload tail padding, the histogram reset and (short segments) the count scan in k_write
+    // (passes 1 / 2 stay on the 256-thread grid: on pass 0's multi-task 1024-thread grid they
+    // measured slower — AlexNet pass 2 5.6 -> 8.8 µs, VGG-16 113.2 k -> 111.2 k img/s)
     LW_LAUNCH((k_hist<KM, 1, false, true>), hist_blocks(a.n_tasks), st, a.g, a.ef, a.seg_off,
               a.seg_n, a.large_segs, a.tasks, a.n_tasks, hist_tpb(a.n_tasks), a.st_large, a.hist, a.gid_base, a.step,
               a.seed0, a.seed1, a.step_ptr, a.keep, a.task_lo);

@@ -230,19 +230,23 @@ __global__ __launch_bounds__(BNT) void k_bn_reduce(const T* __restrict__ x, cons
 
 // Fold the block partials: one wave per channel, lanes stride over blocks (coalesced, fixed
 // order), then a fixed butterfly in fp64. Lane 0 of each wave gets the sums.
+// rstride > 0: `partial` is instead the GEMM epilogue's statistics rows themselves, [nblocks][rstride]
+// (column c: Σv, C + c: Σv²) — k_colsum with one row per block wrote exactly those values, so
+// the fold is the same bit for bit without that launch.
 __device__ __forceinline__ bool fold_channel(const float* __restrict__ partial, int nblocks, int C,
-                                             int c, double& s1, double& s2);
+                                             int c, double& s1, double& s2, int rstride = 0);
 __device__ __forceinline__ bool fold_partials(const float* __restrict__ partial, int nblocks, int C,
-                                              double& s1, double& s2, int& c) {
+                                              double& s1, double& s2, int& c, int rstride = 0) {
   c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return false;
-  return fold_channel(partial, nblocks, C, c, s1, s2);
+  return fold_channel(partial, nblocks, C, c, s1, s2, rstride);
 }
 __device__ __forceinline__ bool fold_channel(const float* __restrict__ partial, int nblocks, int C,
-                                             int c, double& s1, double& s2) {
+                                             int c, double& s1, double& s2, int rstride) {
   const int lane = threadIdx.x & 63;
-  const float* p1 = partial + (int64_t)c * nblocks;
-  const float* p2 = partial + ((int64_t)C + c) * nblocks;
+  const int64_t bs = rstride > 0 ? rstride : 1;          // element stride between blocks
+  const float* p1 = partial + (rstride > 0 ? (int64_t)c : (int64_t)c * nblocks);
+  const float* p2 = partial + (rstride > 0 ? (int64_t)C + c : ((int64_t)C + c) * nblocks);
   float a = 0.f, b = 0.f;
   // 16 strided loads per lane issued together, then added in block order (a plain strided loop
   // waited for each load in turn: ~8 µs of HBM latency per launch)
@@ -251,8 +255,8 @@ __device__ __forceinline__ bool fold_channel(const float* __restrict__ partial, 
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int blk = base + u * 64 + lane;
-      va[u] = blk < nblocks ? p1[blk] : 0.f;
-      vb[u] = blk < nblocks ? p2[blk] : 0.f;
+      va[u] = blk < nblocks ? p1[blk * bs] : 0.f;
+      vb[u] = blk < nblocks ? p2[blk * bs] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) { a += va[u]; b += vb[u]; }
@@ -388,10 +392,11 @@ __global__ __launch_bounds__(256) void k_bn_finalize_fwd(
     const float* __restrict__ partial, int nblocks, int C, int64_t M,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
     float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ mean_out,
-    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
+    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift,
+    int rstride) {
   double s, q;
   int c;
-  if (!fold_partials(partial, nblocks, C, s, q, c)) return;
+  if (!fold_partials(partial, nblocks, C, s, q, c, rstride)) return;
   const double mean = s / (double)M;
   double var = q / (double)M - mean * mean;
   var = var < 0.0 ? 0.0 : var;
@@ -663,6 +668,11 @@ int colsum_fused_blocks(int64_t rows) {
   return (int)(rows < nb ? rows : nb);
 }
 
+// LWAAAI_COLSUM_DIRECT=0: k_colsum even when it would copy one row per block
+static bool colsum_direct() {
+  static const bool on = env_int("LWAAAI_COLSUM_DIRECT", 1) != 0;
+  return on;
+}
 int colsum_blocks(int64_t rows) {
   static const int cap = env_int("LWAAAI_COLSUM_BLOCKS", 1024);
   return (int)(rows < cap ? rows : cap);
@@ -722,13 +732,22 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
                        a.rmean, a.rvar, a.mean, a.invstd, a.scale, a.shift);
     return;
   }
+  const float* part = a.partial;
+  int rstride = 0;
   if (a.stat_rows) {                      // GEMM epilogue rows [R][2C] -> [2C][nb]
     const int64_t R = a.stats_rows_n;
     nb = colsum_blocks(R);
     const int64_t rpb = (R + nb - 1) / nb;
     nb = (int)((R + rpb - 1) / rpb);
-    hipLaunchKernelGGL(k_colsum, dim3(nb), dim3(256), 0, st, a.stat_rows, R, 2 * a.C, rpb,
-                       a.partial);
+    if (rpb == 1 && colsum_direct()) {
+      // one row per block: the finalize folds the rows where they are (layers 3-4 of a
+      // ResNet-50: 29 fewer launches a step)
+      part = a.stat_rows;
+      rstride = 2 * a.C;
+    } else {
+      hipLaunchKernelGGL(k_colsum, dim3(nb), dim3(256), 0, st, a.stat_rows, R, 2 * a.C, rpb,
+                         a.partial);
+    }
   } else if (nb <= 0) {
     int64_t rpb;
     reduce_geometry(a.M, a.C, rpb, nb);
@@ -739,9 +758,9 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
                        (const float*)nullptr, (const float*)nullptr, a.M, a.C, rpb, a.partial,
                        (const T*)nullptr, (const float*)nullptr, (float*)nullptr);
   }
-  hipLaunchKernelGGL(k_bn_finalize_fwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
+  hipLaunchKernelGGL(k_bn_finalize_fwd, dim3((a.C + 3) / 4), dim3(256), 0, st, part, nb,
                      a.C, a.M, a.gamma, a.beta, a.eps, a.momentum, a.rmean, a.rvar, a.mean,
-                     a.invstd, a.scale, a.shift);
+                     a.invstd, a.scale, a.shift, rstride);
 }
 
 template <typename T>

@@ -668,10 +668,11 @@ int colsum_fused_blocks(int64_t rows) {
   return (int)(rows < nb ? rows : nb);
 }
 
-// LWAAAI_COLSUM_DIRECT=0: k_colsum even when it would copy one row per block
-static bool colsum_direct() {
-  static const bool on = env_int("LWAAAI_COLSUM_DIRECT", 1) != 0;
-  return on;
+// statistics rows up to LWAAAI_COLSUM_DIRECT_MAX are folded by the finalize itself (0: always
+// k_colsum first)
+static int64_t colsum_direct_max() {
+  static const int v = env_int("LWAAAI_COLSUM_DIRECT_MAX", 1024);
+  return v;
 }
 int colsum_blocks(int64_t rows) {
   static const int cap = env_int("LWAAAI_COLSUM_BLOCKS", 1024);
@@ -739,11 +740,14 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
     nb = colsum_blocks(R);
     const int64_t rpb = (R + nb - 1) / nb;
     nb = (int)((R + rpb - 1) / rpb);
-    if (rpb == 1 && colsum_direct()) {
-      // one row per block: the finalize folds the rows where they are (layers 3-4 of a
-      // ResNet-50: 29 fewer launches a step)
+    if (R <= colsum_direct_max()) {
+      // few rows: the finalize folds the rows where they are, one launch fewer. Up to 1024 rows
+      // k_colsum ran one row per block, so the sums are its own bit for bit (layers 3-4 of a
+      // ResNet-50, 29 BatchNorms: 11,332-11,372 -> 11,439-11,465 img/s on one box; a cap of
+      // 2048 / 8192 rows measured 11,429-11,438 / 11,375, profiles/r5/colsum_direct_ab.jsonl)
       part = a.stat_rows;
       rstride = 2 * a.C;
+      nb = (int)R;
     } else {
       hipLaunchKernelGGL(k_colsum, dim3(nb), dim3(256), 0, st, a.stat_rows, R, 2 * a.C, rpb,
                          a.partial);

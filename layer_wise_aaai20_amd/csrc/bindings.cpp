@@ -986,6 +986,29 @@ static void set_bstats(lw::GemmArgs& g, const c10::optional<Tensor>& bx,
   }
 }
 
+// fp32 slab sets whose split-K reduce was deferred (gemm.hip splitk_flush): held until the flush
+// has queued the reduce that reads them
+std::vector<Tensor>& splitk_keep() {
+  static std::vector<Tensor> keep;
+  return keep;
+}
+
+// splitk_defer(dev, on): while on, this device's fp32 split-K outputs without bias / ReLU /
+// addend (weight gradients accumulated into the gradient arena, ops/block.py) are reduced at
+// the next splitk_flush instead of right away. `dev`: any tensor on the device (dispatch).
+void splitk_defer(Tensor dev, bool on) {
+  const c10::DeviceGuard guard(dev.device());
+  lw::splitk_set_defer(on);
+}
+
+int64_t splitk_flush(Tensor dev) {
+  const c10::DeviceGuard guard(dev.device());
+  const int n = lw::splitk_flush(cur_stream());
+  splitk_keep().clear();
+  if (n > 0) launched("splitk_flush");
+  return n;
+}
+
 std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb,
                                    bool b_kcontig, int64_t M, int64_t N, int64_t K,
                                    c10::optional<Tensor> bias, bool relu, int64_t splits,
@@ -1111,6 +1134,7 @@ std::tuple<Tensor, Tensor> gemm_ex(Tensor A, int64_t lda, bool a_kcontig, Tensor
     stats = at::empty({0}, A.options().dtype(at::kFloat));
   }
   lw::gemm_bf16(g, cur_stream());
+  if (zs > 1 && lw::splitk_take_deferred()) splitk_keep().push_back(partial);
   launched("gemm_bf16");
   return {C, stats};
 }
@@ -1390,6 +1414,7 @@ std::tuple<Tensor, Tensor> conv_ex(Tensor G, Tensor Op, int64_t mode, std::vecto
                 "conv big tiles: one-class row gather, C % 64 == 0, K-contiguous weight, no "
                 "prologue / addend / backward statistics");
   lw::conv_gemm(g, h, (int)mode, cur_stream());
+  if (zs > 1 && lw::splitk_take_deferred()) splitk_keep().push_back(partial);
   launched("conv_gemm");
   return {C, stats};
 }
@@ -1834,6 +1859,8 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "Tensor tasks, Tensor? seg_wd, float mc, float wmul) -> ()");
   m.def("mc_mask(Tensor(a!) u, Tensor e) -> ()");
   m.def("step_bump(Tensor(a!) c) -> ()");
+  m.def("splitk_defer(Tensor dev, bool on) -> ()");
+  m.def("splitk_flush(Tensor dev) -> int");
   m.def(
       "sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
@@ -1918,6 +1945,8 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("mc_prep", &mc_prep);
   m.impl("mc_mask", &mc_mask);
   m.impl("step_bump", &step_bump);
+  m.impl("splitk_defer", &splitk_defer);
+  m.impl("splitk_flush", &splitk_flush);
   m.impl("normalize_u8", &normalize_u8);
   m.impl("cifar_augment", &cifar_augment);
   m.impl("gap_fwd", &gap_fwd);

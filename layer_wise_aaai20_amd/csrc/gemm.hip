@@ -28,6 +28,9 @@
 #include "common.h"
 #include "gemm_core.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace lw {
 
 void gemm_big(const GemmArgs& g, const GemmK& k, int zs, hipStream_t st);   // gemm_big.hip
@@ -425,10 +428,111 @@ static void launch_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, h
 #undef LW_E
 }
 
-void splitk_reduce(const GemmArgs& g, int zs, hipStream_t st) {
-  const int64_t total = (int64_t)g.M * g.N;
+// ------------------------------------------------------------------------------------------
+// Deferred split-K reduces. Inside a splitk_defer(true) scope (ops/block.py: a bottleneck's
+// weight gradients accumulated straight into the gradient arena) a split GEMM / conv leaves its
+// fp32 slabs for splitk_flush, which the gradient engine calls before it reads the arena
+// (parallel/engine.py): one launch reduces every pending slab set — ResNet-50 ran 54 reduce
+// launches a step, at ~5 µs of launch floor each in the replayed graph. Per element the sum is
+// k_splitk_reduce's, same split lanes and fold order, so the result is identical.
+// ------------------------------------------------------------------------------------------
+struct ReduceJob {
+  const float* partial;
+  float* C;
+  int64_t ldc, blk_lo;       // output row stride; first block of this job in the launch
+  int splits, zl, M, N, accumulate;
+};
+constexpr int kMaxReduceJobs = 24;
+struct ReduceJobs {
+  ReduceJob j[kMaxReduceJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(GT) void k_splitk_reduce_multi(const ReduceJobs jobs) {
+  __shared__ float4 red[GT];
+  int ji = 0;
+  for (int q = 1; q < jobs.n; ++q)
+    if ((int64_t)blockIdx.x >= jobs.j[q].blk_lo) ji = q;
+  const ReduceJob J = jobs.j[ji];
+  const int ZT = 1 << J.zl, OT = GT >> J.zl;
+  const int z = threadIdx.x / OT, o = threadIdx.x % OT;
+  const int64_t total = (int64_t)J.M * J.N;
+  const int64_t i0 = (((int64_t)blockIdx.x - J.blk_lo) * OT + o) * 4;
+  const bool vec = (J.N & 3) == 0;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i0 < total) {
+    if (vec) {
+#pragma unroll 8
+      for (int zz = z; zz < J.splits; zz += ZT) {
+        const float4 v = *reinterpret_cast<const float4*>(J.partial + (int64_t)zz * total + i0);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+    } else {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int zz = z; zz < J.splits; zz += ZT)
+        for (int k = 0; k < 4 && i0 + k < total; ++k) t[k] += J.partial[(int64_t)zz * total + i0 + k];
+      s = make_float4(t[0], t[1], t[2], t[3]);
+    }
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (z != 0 || i0 >= total) return;
+  for (int q = 1; q < ZT; ++q) {
+    const float4 v = red[q * OT + o];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const float out[4] = {s.x, s.y, s.z, s.w};
+  for (int k = 0; k < 4 && i0 + k < total; ++k) {
+    const int64_t i = i0 + k;
+    float* c = J.C + (i / J.N) * J.ldc + (int)(i % J.N);
+    *c = J.accumulate ? *c + out[k] : out[k];
+  }
+}
+
+static bool g_defer = false, g_last_deferred = false;
+static std::vector<ReduceJob> g_pending;
+
+void splitk_set_defer(bool on) { g_defer = on; }
+bool splitk_take_deferred() {
+  const bool r = g_last_deferred;
+  g_last_deferred = false;
+  return r;
+}
+
+static int splitk_lanes(int zs) {
   int zl = 0;                                    // split lanes: up to 32, no more than splits
   while (zl < 5 && (2 << zl) <= zs) ++zl;
+  return zl;
+}
+
+int splitk_flush(hipStream_t st) {
+  const int n = (int)g_pending.size();
+  for (int b = 0; b < n; b += kMaxReduceJobs) {
+    ReduceJobs jobs{};
+    jobs.n = std::min(kMaxReduceJobs, n - b);
+    int64_t blocks = 0;
+    for (int q = 0; q < jobs.n; ++q) {
+      ReduceJob r = g_pending[b + q];
+      const int64_t groups = ((int64_t)r.M * r.N + 3) / 4, ot = GT >> r.zl;
+      r.blk_lo = blocks;
+      blocks += (groups + ot - 1) / ot;
+      jobs.j[q] = r;
+    }
+    hipLaunchKernelGGL(k_splitk_reduce_multi, dim3((unsigned)blocks), dim3(GT), 0, st, jobs);
+  }
+  g_pending.clear();
+  return n;
+}
+
+void splitk_reduce(const GemmArgs& g, int zs, hipStream_t st) {
+  if (g_defer && !g.out_bf16 && g.bias == nullptr && !g.relu && g.addend == nullptr) {
+    g_pending.push_back(ReduceJob{g.partial, static_cast<float*>(g.C), g.ldc, 0, zs,
+                                  splitk_lanes(zs), g.M, g.N, g.accumulate ? 1 : 0});
+    g_last_deferred = true;
+    return;
+  }
+  const int64_t total = (int64_t)g.M * g.N;
+  const int zl = splitk_lanes(zs);
   const int64_t groups = (total + 3) / 4, ot = GT >> zl;
   const dim3 rg((unsigned)((groups + ot - 1) / ot));
   hipLaunchKernelGGL(k_splitk_reduce, rg, dim3(GT), 0, st, g.partial, zs, zl, g.C, g.ldc, g.bias,

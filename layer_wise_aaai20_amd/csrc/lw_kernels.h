@@ -295,6 +295,12 @@ void pack_dgrad_kc(const uint16_t* w, uint16_t* out, int Co, int C, int R, int S
 bool gemm_big_ok(const GemmArgs& g);
 bool gemm_bigp_ok(const GemmArgs& g);
 void splitk_reduce(const GemmArgs& g, int splits, hipStream_t st);   // fixed-order slab reduce
+// deferred reduces (gemm.hip): while on, fp32 split-K outputs without bias / ReLU / addend are
+// queued; splitk_take_deferred reports (and clears) whether the last splitk_reduce was queued;
+// splitk_flush reduces every queued one in one launch per 24 and returns how many there were
+void splitk_set_defer(bool on);
+bool splitk_take_deferred();
+int splitk_flush(hipStream_t st);
 void gemm_tile_shape(int tile, int& bm, int& bn, int& bk);
 int stats_rows_bm(int tile);      // rows of C per column-statistics row of a tile
 int gemm_k_per_split(int K, int splits, int bk);

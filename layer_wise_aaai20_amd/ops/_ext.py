@@ -101,3 +101,29 @@ def ops_for(t: torch.Tensor):
 
 def is_loaded() -> bool:
     return _loaded or _loaded16
+
+
+# Deferred split-K reduces (csrc/gemm.hip splitk_flush; ops/block.py turns them on around a
+# block's arena weight gradients). _DEFER holds a tensor on the deferring device while on.
+_DEFER = [None]
+
+
+def set_splitk_defer(t: torch.Tensor, on: bool) -> None:
+    load().splitk_defer(t, on)
+    _DEFER[0] = t if on else None
+
+
+class splitk_paused:
+    """Reduce split-K outputs right away inside this scope (the tuner's timing runs: a
+    deferred reduce would neither be timed nor target a real gradient)."""
+
+    def __enter__(self):
+        self.t = _DEFER[0]
+        if self.t is not None:
+            set_splitk_defer(self.t, False)
+        return self
+
+    def __exit__(self, *exc):
+        if self.t is not None:
+            set_splitk_defer(self.t, True)
+        return False

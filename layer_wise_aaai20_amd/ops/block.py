@@ -44,13 +44,14 @@ returned through autograd as usual.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
 
-from ._ext import h16, load
+from ._ext import h16, load, set_splitk_defer
 from .conv import conv_dgrad, conv_fwd, conv_wgrad
 from .tuning import MF32, Tuner, with_mf32
 
@@ -321,6 +322,25 @@ class _WgradLane:
         self.ready = []
 
 
+# Split-K weight gradients accumulated straight into the gradient arena leave their slab reduce
+# to the gradient engine's next flush (csrc/gemm.hip splitk_flush, parallel/engine.py), which
+# runs them in one launch before it reads the arena — ResNet-50 spent 54 launches a step on
+# these reduces. LWAAAI_SPLITK_DEFER=0: each reduce right after its GEMM.
+SPLITK_DEFER = os.environ.get("LWAAAI_SPLITK_DEFER", "1") != "0"
+
+
+@contextlib.contextmanager
+def _deferred_reduce(t: torch.Tensor, direct: bool):
+    on = SPLITK_DEFER and direct and t.is_cuda
+    if on:
+        set_splitk_defer(t, True)
+    try:
+        yield
+    finally:
+        if on:
+            set_splitk_defer(t, False)
+
+
 def _wgrad_done(lane: _WgradLane, p: torch.Tensor, dst: torch.Tensor, direct: bool):
     if direct:
         lane.finish(lambda: _finish_param(p, None, True))
@@ -461,10 +481,11 @@ class _BottleneckFn(torch.autograd.Function):
         # accumulated into the arena
         lane = _WgradLane(dc3.device)
         dst3, d3 = _wgrad_target(w3, (cout, width))
-        lane.run(lambda: gemm(dc3, cout, False, c2 if a2 is None else a2, width, False, cout,
-                              width, M2, out_bf16=False,
-                              pro=(ss2[:width], ss2[width:]) if a2 is None else None,
-                              pro_on_a=False, out=dst3, accumulate=True, split_k=True))
+        with _deferred_reduce(dc3, d3):
+            lane.run(lambda: gemm(dc3, cout, False, c2 if a2 is None else a2, width, False, cout,
+                                  width, M2, out_bf16=False,
+                                  pro=(ss2[:width], ss2[width:]) if a2 is None else None,
+                                  pro_on_a=False, out=dst3, accumulate=True, split_k=True))
         grads["w3"] = _wgrad_done(lane, w3, dst3, d3)
         # da2 = dc3·W3, its epilogue doing BN2's backward reduction (mask from c2 via ss2)
         da2, rows2 = gemm_dgrad(dc3, cout, W3, M2, width, cout, stats=BSTATS,
@@ -481,8 +502,9 @@ class _BottleneckFn(torch.autograd.Function):
         c1n = _nchw(c1 if a1 is None else a1, N, H, W)
         pro1 = (ss1[:width], ss1[width:]) if a1 is None else None
         if _direct(w2) and w2.grad.is_contiguous(memory_format=CL):
-            lane.run(lambda: conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1,
-                                        out=w2.grad))
+            with _deferred_reduce(dc2n, True):
+                lane.run(lambda: conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1,
+                                            out=w2.grad))
             lane.finish(lambda: _finish_param(w2, None, True))
             grads["w2"] = None
         else:
@@ -505,8 +527,9 @@ class _BottleneckFn(torch.autograd.Function):
         grads["g1"], grads["b1"] = _finish_bn(g1p, b1p, dg1, db1, o1)
         xr = _rows(x)
         dst1, d1 = _wgrad_target(w1, (width, Cin))
-        lane.run(lambda: gemm(dc1, width, False, xr, Cin, False, width, Cin, M, out_bf16=False,
-                              out=dst1, accumulate=True, split_k=True))
+        with _deferred_reduce(dc1, d1):
+            lane.run(lambda: gemm(dc1, width, False, xr, Cin, False, width, Cin, M,
+                                  out_bf16=False, out=dst1, accumulate=True, split_k=True))
         grads["w1"] = _wgrad_done(lane, w1, dst1, d1)
         if has_down:
             xsr, cd, Wd, gd, meand, invd = saved[21:]
@@ -519,12 +542,14 @@ class _BottleneckFn(torch.autograd.Function):
                                               False, bits3, od[0], od[1])
             grads["gd"], grads["bd"] = _finish_bn(gdp, bdp, dgd, dbd, od)
             dstd, dd = _wgrad_target(wd, (cout, Cin))
-            if s == 1:
-                lane.run(lambda: gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2,
-                                      out_bf16=False, out=dstd, accumulate=True, split_k=True))
-            else:                     # strided pixel gather of x in the weight-gradient conv
-                lane.run(lambda: conv_wgrad(_nchw(dcd, N2, H2, W2_), x, (cout, Cin, 1, 1), s, 0,
-                                            out=dstd.view(cout, Cin, 1, 1)))
+            with _deferred_reduce(dcd, dd):
+                if s == 1:
+                    lane.run(lambda: gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2,
+                                          out_bf16=False, out=dstd, accumulate=True,
+                                          split_k=True))
+                else:                 # strided pixel gather of x in the weight-gradient conv
+                    lane.run(lambda: conv_wgrad(_nchw(dcd, N2, H2, W2_), x, (cout, Cin, 1, 1), s,
+                                                0, out=dstd.view(cout, Cin, 1, 1)))
             grads["wd"] = _wgrad_done(lane, wd, dstd, dd)
             dx, _ = gemm_dgrad(dc1, width, W1, M, Cin, width)
             if s == 1:

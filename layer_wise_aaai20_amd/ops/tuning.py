@@ -162,16 +162,18 @@ class Tuner:
         if not self.enabled or len(candidates) <= 1:
             self.best[key] = default
             return default
+        from ._ext import splitk_paused
         times = []
-        for cand in candidates:
-            run(cand)
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(self.reps):
+        with splitk_paused():          # (every candidate timed with its split-K reduce)
+            for cand in candidates:
                 run(cand)
-            e.record()
-            e.synchronize()
-            times.append((s.elapsed_time(e), cand))
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(self.reps):
+                    run(cand)
+                e.record()
+                e.synchronize()
+                times.append((s.elapsed_time(e), cand))
         times = _agree_times(times)
         c = min(times, key=lambda t: t[0])[1]
         self.best[key] = c

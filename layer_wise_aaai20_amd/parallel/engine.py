@@ -293,6 +293,7 @@ class GradSyncEngine:
             self._stage_next += 1
 
     def _stage(self, si: int) -> None:
+        self._flush_splitk()
         lo, hi, t_hi = self._stages[si]
         t_lo = lo // 8192 if si > 0 else 0
         codec = self.codecs[0]
@@ -536,7 +537,16 @@ class GradSyncEngine:
         ev.record()
         return ev
 
+    def _flush_splitk(self) -> None:
+        """Run the split-K reduces the fused blocks deferred (ops/block.py _deferred_reduce,
+        csrc/gemm.hip splitk_flush) before anything reads the arena."""
+        if self.device.type == "cuda":
+            from ..ops._ext import is_loaded, load
+            if is_loaded():
+                load().splitk_flush(self.arena.grad)
+
     def _launch(self, bi: int) -> None:
+        self._flush_splitk()
         b = self.buckets[bi]
         codec = self.codecs[bi]
         g = self.arena.grad[b.start:b.end]
@@ -632,6 +642,7 @@ class GradSyncEngine:
     def finish(self) -> None:
         """Launch buckets that never became ready (unused params keep zero grads), wait for every
         collective and decode into the arena."""
+        self._flush_splitk()
         for i in self._no_zero:
             if self._claims[i] == 0:     # (not zeroed by begin_step and not written this step)
                 self.arena.grad_view(self.arena.segments[i]).zero_()

@@ -292,7 +292,21 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
         if out is not None:
             return _nchw_rows(out, Nb, H, W)
         return torch.zeros((Nb, c, H, W), dtype=h16(), device=dy.device, memory_format=CL)
-    wt, offs = wpack if wpack is not None else pack_dgrad_weight(w, classes, sh, sw)
+    # the [K][C] slabs are packed only if that layout runs (a "kc" / "tap" / "direct" pick packs
+    # its own); their offsets are known without packing
+    if wpack is not None:
+        offs = wpack[1]
+    else:
+        offs, o = [], 0
+        for (_ch, _cw, _r0, _s0, TR, TS, *_r) in classes:
+            offs.append(o)
+            o += TR * TS * co * c
+    nkc_pack = [wpack[0] if wpack is not None else None]
+
+    def nkc_weight():
+        if nkc_pack[0] is None:
+            nkc_pack[0] = pack_dgrad_weight(w, classes, sh, sw)[0]
+        return nkc_pack[0]
     geom = [Nb, Ho, Wo, co, 1, 1, -1, -1, H, W, sh, sw, len(classes)]
     for (ch, cw, r0, s0, TR, TS, Hg, Wg, oh, ow), off in zip(classes, offs):
         geom += [TR, TS, oh, ow, Hg, Wg, ch, cw, TR * TS * co, off]
@@ -317,8 +331,8 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
                 g[13 + 10 * i + 9] = off
             return lib.conv_ex(dyc, wk, CV_A, g, c, tile, 1, True, None, None, False, dst, False,
                                0, True, kmax, add)
-        return lib.conv_ex(dyc, wt, CV_A, geom, c, tile, 1, True, None, None, bst is not None,
-                           dst, False, 0, False, c, add, bx, bm, bss, bb)
+        return lib.conv_ex(dyc, nkc_weight(), CV_A, geom, c, tile, 1, True, None, None,
+                           bst is not None, dst, False, 0, False, c, add, bx, bm, bss, bb)
     key = ("d", tuple(dyc.shape), tuple(w.shape), H, W, sh, sw, ph, pw, addend is not None,
            bst is not None)
     # the weight as [K][C] (the kernel's transposing LDS reads) or packed K-contiguous [C][K]

@@ -214,7 +214,7 @@ def pack_dgrad_weight_kc(w: torch.Tensor, classes, sh: int, sw: int):
 
 # ----------------------------------------------------------------------------- the three passes
 def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=False,
-             wpack=None, bias=None, relu=False):
+             wpack=None, bias=None, relu=False, xin=None):
     """y = conv2d(x, w) as bf16 channels_last [N, Co, Ho, Wo]; optionally the input BN-apply+ReLU
     ``pro = (scale, shift)`` (fp32 [C]), the per-M-tile column statistics of y, and an fp32
     ``bias`` [Co] / ReLU applied in the epilogue before the bf16 rounding."""
@@ -223,7 +223,8 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
     ph, pw = _pair(padding)
     co, c, R, S = w.shape
     c4 = c % 8 != 0
-    xin = _c4_input(x) if c4 else x.to(h16()).contiguous(memory_format=CL)
+    if xin is None:                   # (``xin``: the caller's _c4_input(x) for a C = 3/4 input)
+        xin = _c4_input(x) if c4 else x.to(h16()).contiguous(memory_format=CL)
     Nb, _, H, W = xin.shape
     Ho, Wo = out_size(H, R, sh, ph), out_size(W, S, sw, pw)
     op, K, TS = wpack if wpack is not None else pack_fwd_weight(w)
@@ -364,7 +365,7 @@ def _wgrad_splits(tiles: int, pixels: int, bk: int) -> int:
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, pro=None,
-               out: Optional[torch.Tensor] = None):
+               out: Optional[torch.Tensor] = None, xin=None):
     """dW of conv2d(x, w): fp32 [Co][R][S'][C'] GEMM output. With ``out`` (a dense fp32 view of
     the weight's gradient in [Co][R][S][C] memory order, C % 8 == 0) the result is accumulated
     into it in place and ``out`` is returned; otherwise a fresh [Co, C, R, S] tensor (channels_last
@@ -380,7 +381,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, w_shape, stride, padding, pro=
         xa = x.to(h16()).contiguous(memory_format=CL)
         x = lib.bn_apply(xa, torch.cat([pro[0][:c], pro[1][:c]]).contiguous(), None, None, True)
         pro = None
-    xin = _c4_input(x) if c4 else x.to(h16()).contiguous(memory_format=CL)
+    if xin is None:
+        xin = _c4_input(x) if c4 else x.to(h16()).contiguous(memory_format=CL)
     dyc = dy.to(h16()).contiguous(memory_format=CL)
     Nb, C, H, W = xin.shape
     _, _, Ho, Wo = dyc.shape
@@ -458,8 +460,14 @@ class _ConvFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, stride, padding, relu):
         from .block import _bf16_weight
         wb = _bf16_weight(weight)
-        y, _ = conv_fwd(x, wb, stride, padding, bias=bias, relu=relu)
-        xs = x.to(h16()).contiguous(memory_format=CL) if x.shape[1] % 8 == 0 else x
+        if weight.shape[1] % 8 != 0:
+            # a 3/4-channel image: its zero-padded 4-channel copy is built once and kept for the
+            # weight gradient (three launches fewer in backward)
+            xs = _c4_input(x)
+            y, _ = conv_fwd(x, wb, stride, padding, bias=bias, relu=relu, xin=xs)
+        else:
+            y, _ = conv_fwd(x, wb, stride, padding, bias=bias, relu=relu)
+            xs = x.to(h16()).contiguous(memory_format=CL)
         ctx.save_for_backward(xs, wb, y if relu else None)
         ctx.geom = (stride, padding, tuple(x.shape[2:]), x.dtype)
         ctx.weight = weight
@@ -493,11 +501,18 @@ class _ConvFn(torch.autograd.Function):
             dx = conv_dgrad(dy, wb, hw, stride, padding).to(xdtype)
         if ctx.needs_input_grad[1]:
             dst = _arena_view(w)
-            if dst is not None and w.shape[1] % 8 == 0:
+            c4 = w.shape[1] % 8 != 0
+            if dst is not None and not c4:
                 conv_wgrad(dy, xs, tuple(w.shape), stride, padding, out=dst)
                 w._lw_grad_ready(w)
+            elif dst is not None:
+                # [Co][R][TS][4] GEMM output: its [:, :, :S, :C] slice added into the arena view
+                # by one strided add (no contiguous copy, no AccumulateGrad add)
+                dst.add_(conv_wgrad(dy, xs, tuple(w.shape), stride, padding, xin=xs))
+                w._lw_grad_ready(w)
             else:
-                dw = conv_wgrad(dy, xs, tuple(w.shape), stride, padding).to(w.dtype)
+                dw = conv_wgrad(dy, xs, tuple(w.shape), stride, padding,
+                                xin=xs if c4 else None).to(w.dtype)
                 dw = dw.contiguous(memory_format=CL) if w.is_contiguous(memory_format=CL) \
                     else dw.contiguous()
         return dx, dw, db, None, None, None

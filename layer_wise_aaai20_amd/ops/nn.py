@@ -72,18 +72,29 @@ class _FusedBN(torch.autograd.Function):
         else:
             ctx.save_for_backward(x, y if relu else None, weight, mean, invstd, None)
         ctx.flags = (bool(training), bool(relu), residual is not None)
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        from . import block
         x, y, weight, mean, invstd, scale_shift = ctx.saved_tensors
         training, relu, has_res = ctx.flags
         lib = load()
         dy = _nhwc(dy).to(x.dtype)
-        dx, dgamma, dbeta, dres = lib.bn_bwd(dy, x, y, weight, mean, invstd, scale_shift,
-                                             training, relu, has_res)
+        w, b = ctx.params
         need_w = weight is not None and ctx.needs_input_grad[2]
         need_b = ctx.needs_input_grad[3]
+        # arena-managed gamma / beta: the kernel accumulates their gradients in place (as the
+        # fused blocks do), no AccumulateGrad add kernels
+        outs = block._bn_grad_outs(w, b) if (need_w and need_b and w is not None and
+                                             b is not None) else (None, None)
+        dx, dgamma, dbeta, dres = lib.bn_bwd(dy, x, y, weight, mean, invstd, scale_shift,
+                                             training, relu, has_res, None, outs[0], outs[1])
+        if outs[0] is not None:
+            block._finish_bn(w, b, dgamma, dbeta, outs)
+            return (dx, dres if has_res else None, None, None, None, None, None, None, None,
+                    None)
         return (dx, dres if has_res else None, dgamma if need_w else None,
                 dbeta if need_b else None, None, None, None, None, None, None)
 
@@ -452,9 +463,19 @@ def fuse_graph_network(net: nn.Module, pool: bool = True) -> nn.Module:
     graph = getattr(net, "graph", None)
     if graph is None:
         return net
-    for mod, _ in graph.values():          # the loss node on the fused cross-entropy kernel
+    loss_of = {}                           # the loss node on the fused cross-entropy kernel
+    for k, (mod, ins) in graph.items():
         if type(mod) is nn.CrossEntropyLoss:
             mod.__class__ = FusedCrossEntropyLoss
+            loss_of[tuple(ins)] = mod
+    # a top-1 "correct" node on the same (logits, target) as a fused loss reads the loss kernel's
+    # correctness instead of its own max-reduce + compare
+    from ..models.graph import Correct
+    for k, (mod, ins) in list(graph.items()):
+        if type(mod) is Correct and tuple(ins) in loss_of:
+            cm = _XentCorrect(loss_of[tuple(ins)])
+            graph[k] = (cm, ins)
+            net._modules[k] = cm
     names = list(graph)
     consumers = {}
     for k, (_, ins) in graph.items():
@@ -485,6 +506,19 @@ def fuse_graph_network(net: nn.Module, pool: bool = True) -> nn.Module:
                     pid = Identity()
                     graph[pu[0]] = (pid, pins)
                     net._modules[pu[0]] = pid
+    # a max-pool of a map that is already post-ReLU (the graph AlexNet's last pool after layer4's
+    # BN-ReLU-pool): the relu-pool kernels (their ReLU mask is a no-op on x >= 0) instead of
+    # ATen's max-pool forward / backward and the zero fill the latter needs
+    for k in names:
+        mod, ins = graph[k]
+        if type(mod) is not nn.MaxPool2d or len(ins) != 1 or _pool_geom(mod) is None:
+            continue
+        src = ins[0]
+        while src in graph and isinstance(graph[src][0], Identity) and len(graph[src][1]) == 1:
+            src = graph[src][1][0]
+        smod = graph[src][0] if src in graph else None
+        if isinstance(smod, FusedBatchNorm2d) and smod.fuse_relu:
+            mod.__class__ = ReluMaxPool2d
     return net
 
 
@@ -540,6 +574,23 @@ def fused_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index
     ok = top.eq(target.view(-1, 1))
     corr = torch.stack([ok[:, 0].float(), ok.any(1).float()], 1)
     return loss, corr
+
+
+class _XentCorrect(nn.Module):
+    """``Correct`` (argmax == target) of a graph whose loss node runs the fused kernel on the same
+    inputs: that kernel's top-1 column (one compare launch instead of a max-reduce and an equality;
+    the graph runs the loss node first). A tie at the maximum counts as correct here (no logit
+    strictly greater than the target's), where argmax picks the first maximal index."""
+
+    def __init__(self, loss: "FusedCrossEntropyLoss"):
+        super().__init__()
+        self.__dict__["_loss"] = loss      # (not a submodule: no second state_dict entry)
+
+    def forward(self, classifier, target):
+        corr = getattr(self._loss, "last_correct", None)
+        if corr is None or corr.shape[0] != target.shape[0]:
+            return classifier.max(dim=1)[1] == target
+        return corr[:, 0] > 0
 
 
 class FusedCrossEntropyLoss(nn.CrossEntropyLoss):

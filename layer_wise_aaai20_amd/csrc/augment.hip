@@ -18,12 +18,17 @@ __global__ __launch_bounds__(256) void k_cifar_augment(const float* __restrict__
                                                        const int32_t* __restrict__ prm,
                                                        void* __restrict__ out, int B, int C,
                                                        int Hp, int Wp, int crop, int cutout,
-                                                       int64_t offset) {
+                                                       int64_t offset, int Co) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = (int64_t)B * crop * crop * C;
+  const int64_t total = (int64_t)B * crop * crop * Co;
   if (t >= total) return;
-  const int c = (int)(t % C);
-  int64_t r = t / C;
+  const int c = (int)(t % Co);
+  int64_t r = t / Co;
+  if (c >= C) {                               // the zero channels of a padded (Co = 4) batch
+    if (BF16) static_cast<uint16_t*>(out)[t] = 0;
+    else static_cast<float*>(out)[t] = 0.f;
+    return;
+  }
   const int x = (int)(r % crop);
   r /= crop;
   const int y = (int)(r % crop);
@@ -39,18 +44,21 @@ __global__ __launch_bounds__(256) void k_cifar_augment(const float* __restrict__
   else static_cast<float*>(out)[t] = v;
 }
 
+// Co >= C output channels: the ones past C are written as zeros (a 4-channel stem input for the
+// MFMA image convolution, ops/conv.py _c4_input, built here instead of by a cast, a fill and a copy)
 void cifar_augment(const float* data, const int64_t* idx, const int32_t* prm, void* out, int B,
                    int C, int Hp, int Wp, int crop, int cutout, int64_t offset, bool bf16,
-                   hipStream_t st) {
-  const int64_t total = (int64_t)B * crop * crop * C;
+                   hipStream_t st, int Co) {
+  if (Co < C) Co = C;
+  const int64_t total = (int64_t)B * crop * crop * Co;
   if (total == 0) return;
   const dim3 grid((unsigned)((total + 255) / 256)), block(256);
   if (bf16)
     hipLaunchKernelGGL(k_cifar_augment<true>, grid, block, 0, st, data, idx, prm, out, B, C, Hp,
-                       Wp, crop, cutout, offset);
+                       Wp, crop, cutout, offset, Co);
   else
     hipLaunchKernelGGL(k_cifar_augment<false>, grid, block, 0, st, data, idx, prm, out, B, C, Hp,
-                       Wp, crop, cutout, offset);
+                       Wp, crop, cutout, offset, Co);
 }
 
 }  // namespace lw

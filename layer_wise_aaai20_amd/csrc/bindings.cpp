@@ -555,15 +555,17 @@ void cifar_augment(Tensor data, Tensor idx, Tensor prm, int64_t offset, int64_t 
   TORCH_CHECK(crop >= 1 && crop <= Hp && crop <= Wp && cutout >= 0 && cutout <= crop,
               "cifar_augment: crop / cutout out of range");
   TORCH_CHECK(offset >= 0 && offset + B <= prm.size(0), "cifar_augment: choice rows out of range");
-  TORCH_CHECK(out.is_cuda() && out.dim() == 4 && out.size(0) == B && out.size(1) == C &&
+  // out: [B, C, crop, crop], or [B, 4, crop, crop] for a 3-channel dataset (zero 4th channel)
+  TORCH_CHECK(out.is_cuda() && out.dim() == 4 && out.size(0) == B &&
+                  (out.size(1) == C || (C == 3 && out.size(1) == 4)) &&
                   out.size(2) == crop && out.size(3) == crop &&
                   out.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "cifar_augment: out must be a channels_last [B, C, crop, crop] GPU tensor");
+              "cifar_augment: out must be a channels_last [B, C (or 4), crop, crop] GPU tensor");
   TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == kH16,
               "cifar_augment: out must be float32 or bfloat16");
   lw::cifar_augment(ptr<float>(data), ptr<int64_t>(idx), ptr<int32_t>(prm), out.data_ptr(),
                     (int)B, (int)C, (int)Hp, (int)Wp, (int)crop, (int)cutout, offset,
-                    out.scalar_type() == kH16, cur_stream());
+                    out.scalar_type() == kH16, cur_stream(), (int)out.size(1));
   launched("cifar_augment");
 }
 

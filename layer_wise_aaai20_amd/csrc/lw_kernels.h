@@ -380,6 +380,6 @@ void normalize_u8_c4(const uint8_t* in, uint16_t* out, int64_t npix, const float
 // NHWC batch (fp32 or bf16); prm is the epoch's [n][5] int32 table (x0, y0, flip, cx, cy)
 void cifar_augment(const float* data, const int64_t* idx, const int32_t* prm, void* out, int B,
                    int C, int Hp, int Wp, int crop, int cutout, int64_t offset, bool bf16,
-                   hipStream_t st);
+                   hipStream_t st, int Co = 0);
 
 }  // namespace lw

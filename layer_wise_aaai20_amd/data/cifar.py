@@ -255,7 +255,8 @@ class GPUBatches:
 
     def __init__(self, data: torch.Tensor, labels: torch.Tensor, batch_size: int, shuffle: bool,
                  augment: bool = False, crop: int = 32, cutout: int = 8, drop_last: bool = False,
-                 shard=(0, 1), seed: int = 0, channels_last: bool = False, dtype=torch.float32):
+                 shard=(0, 1), seed: int = 0, channels_last: bool = False, dtype=torch.float32,
+                 pad4: bool = False):
         self.data = data
         self.labels = labels
         self.batch_size = batch_size
@@ -272,6 +273,10 @@ class GPUBatches:
         # GPU: crop / flip / cutout + NHWC layout + dtype cast in one HIP kernel per batch
         # (csrc/augment.hip); False keeps the torch gather path (the reference-shaped fallback)
         self.use_kernel = True
+        # pad4 (kernel path, 3-channel data): batches come as [B, 4, crop, crop] with a zero 4th
+        # channel — the MFMA image convolution's input layout (ops/conv.py _c4_input) — so the
+        # step builds no padded copy of its own
+        self.pad4 = pad4
 
     def _kernel_ok(self) -> bool:
         return (self.use_kernel and self.augment and self.data.is_cuda and self.channels_last and
@@ -315,7 +320,8 @@ class GPUBatches:
         for s in range(0, stop, bs):
             b = idx[s:s + bs]
             if kern:
-                x = torch.empty((b.numel(), self.data.shape[1], self.crop, self.crop),
+                ch = 4 if (self.pad4 and self.data.shape[1] == 3) else self.data.shape[1]
+                x = torch.empty((b.numel(), ch, self.crop, self.crop),
                                 dtype=self.dtype, device=dev, memory_format=torch.channels_last)
                 lib.cifar_augment(self.data, b.contiguous(), prm, s, self.crop, self.cutout, x)
                 yield {"input": x, "target": self.labels[b]}

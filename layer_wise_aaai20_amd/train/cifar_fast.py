@@ -18,10 +18,22 @@ import torch
 from ..data import cifar as D
 from ..models.cifar import build_network
 from ..ops import nn as lwnn
+from ..ops._ext import h16
 from ..optim.flat_sgd import FlatSGD
 from ..parallel.ddp import CompressedDDP
 from ..utils.logging import PiecewiseLinear
 from .graphs import StepGraph
+
+
+def _first_conv_pads(net) -> bool:
+    """The graph net's input feeds exactly one node, an MFMA convolution of 3 input channels
+    (which reads a zero-padded 4-channel copy of its input, ops/conv.py _c4_input)."""
+    from ..ops.conv import MFMAConv2d
+    graph = getattr(net, "graph", None)
+    if graph is None:
+        return False
+    users = [m for m, ins in graph.values() if "input" in ins]
+    return len(users) == 1 and isinstance(users[0], MFMAConv2d) and users[0].in_channels == 3
 
 
 class CifarTrainer:
@@ -71,11 +83,16 @@ class CifarTrainer:
             torch.from_numpy(np.ascontiguousarray(tx)).to(self.device),
             torch.as_tensor(ds["test"]["labels"]).to(self.device), batch_size, shuffle=False,
             channels_last=self.device.type == "cuda", dtype=torch.float32)
+        # fused GPU nets: training batches in the compute dtype, already zero-padded to the 4
+        # channels the MFMA image convolution reads (csrc/augment.hip) — the image conv then
+        # casts / pads nothing (the same bf16 values: the conv rounded the fp32 batch itself)
+        gpu_fused = fused and self.device.type == "cuda" and _first_conv_pads(net)
         self.batches = D.GPUBatches(torch.from_numpy(np.ascontiguousarray(x)).to(self.device),
                                     torch.as_tensor(ds["train"]["labels"]).to(self.device),
                                     batch_size, shuffle=True, augment=True, drop_last=True,
                                     seed=seed, channels_last=self.device.type == "cuda",
-                                    dtype=torch.float32)
+                                    dtype=h16() if gpu_fused else torch.float32,
+                                    pad4=gpu_fused)
         # lr_scale: the peak LR as a multiple of the dawn recipe's 0.4 (the Random-K + EF
         # stability sweep, scripts/ef_trace.py)
         self.sched = PiecewiseLinear([0, 5, epochs], [0, 0.4 * float(lr_scale), 0])

@@ -256,3 +256,21 @@ def test_cifar_augment_kernel_matches_torch_gathers(dtype):
         assert xk.is_contiguous(memory_format=torch.channels_last) and xk.dtype == dtype
         assert torch.equal(tk, tt)
         assert torch.equal(xk, xt)
+
+
+def test_cifar_augment_pad4_zero_channel():
+    """pad4: the same augmented batch with a zero 4th channel (the MFMA image convolution's
+    input layout, ops/conv.py _c4_input), bit for bit in its first three channels."""
+    from layer_wise_aaai20_amd.data.cifar import GPUBatches
+    torch.manual_seed(0)
+    data = torch.randn(200, 3, 40, 40, device="cuda")
+    labels = torch.randint(0, 10, (200,), device="cuda")
+    outs = []
+    for pad4 in (False, True):
+        gb = GPUBatches(data, labels, 64, shuffle=True, augment=True, seed=3,
+                        channels_last=True, dtype=torch.bfloat16, pad4=pad4)
+        outs.append([b["input"] for b in gb])
+    for x3, x4 in zip(*outs):
+        assert x4.shape[1] == 4 and x4.is_contiguous(memory_format=torch.channels_last)
+        assert torch.equal(x4[:, :3], x3)
+        assert int((x4[:, 3] != 0).sum()) == 0

@@ -317,6 +317,9 @@ class GPUBatches:
         bs = self.batch_size
         stop = (n // bs) * bs if self.drop_last else n
         ar = torch.arange(self.crop, device=dev)
+        # the epoch's labels in batch order, gathered once (each batch's targets are then a view,
+        # not one index kernel per step)
+        lab = self.labels[idx] if kern else None
         for s in range(0, stop, bs):
             b = idx[s:s + bs]
             if kern:
@@ -324,7 +327,7 @@ class GPUBatches:
                 x = torch.empty((b.numel(), ch, self.crop, self.crop),
                                 dtype=self.dtype, device=dev, memory_format=torch.channels_last)
                 lib.cifar_augment(self.data, b.contiguous(), prm, s, self.crop, self.cutout, x)
-                yield {"input": x, "target": self.labels[b]}
+                yield {"input": x, "target": lab[s:s + b.numel()]}
                 continue
             x = self.data[b]
             if self.augment:

@@ -506,18 +506,30 @@ def fuse_graph_network(net: nn.Module, pool: bool = True) -> nn.Module:
                     pid = Identity()
                     graph[pu[0]] = (pid, pins)
                     net._modules[pu[0]] = pid
-    # a max-pool of a map that is already post-ReLU (the graph AlexNet's last pool after layer4's
-    # BN-ReLU-pool): the relu-pool kernels (their ReLU mask is a no-op on x >= 0) instead of
-    # ATen's max-pool forward / backward and the zero fill the latter needs
+    # a max-pool of a map that is already non-negative (post-ReLU, or a sum of post-ReLU maps:
+    # the graph AlexNet's last pool after layer4's BN-ReLU-pool, ResNet-9's after its residual
+    # add): the relu-pool kernels (their ReLU mask is a no-op on x >= 0) instead of ATen's
+    # max-pool forward / backward and the zero fill the latter needs
+    from ..models.graph import Add
+
+    def nonneg(node, depth=0):
+        if node not in graph or depth > 16:
+            return False
+        m, ins_ = graph[node]
+        if isinstance(m, FusedBatchNorm2d):
+            return bool(m.fuse_relu)
+        if isinstance(m, (ReluMaxPool2d, nn.ReLU)):
+            return True
+        if isinstance(m, (Identity, nn.MaxPool2d)) and len(ins_) == 1:
+            return nonneg(ins_[0], depth + 1)
+        if isinstance(m, Add):
+            return all(nonneg(i, depth + 1) for i in ins_)
+        return False
+
     for k in names:
         mod, ins = graph[k]
-        if type(mod) is not nn.MaxPool2d or len(ins) != 1 or _pool_geom(mod) is None:
-            continue
-        src = ins[0]
-        while src in graph and isinstance(graph[src][0], Identity) and len(graph[src][1]) == 1:
-            src = graph[src][1][0]
-        smod = graph[src][0] if src in graph else None
-        if isinstance(smod, FusedBatchNorm2d) and smod.fuse_relu:
+        if type(mod) is nn.MaxPool2d and len(ins) == 1 and _pool_geom(mod) is not None and \
+                nonneg(ins[0]):
             mod.__class__ = ReluMaxPool2d
     return net
 

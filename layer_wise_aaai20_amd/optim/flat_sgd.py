@@ -101,16 +101,18 @@ class FlatSGD(Optimizer):
         return vals.pop()
 
     def load_hyper(self) -> None:
-        """Write the current (lr, grad_scale) into the device tensor a captured step reads (two
-        stream-ordered fills, only when they changed; call outside graph capture)."""
+        """Write the current (lr, grad_scale) into the device tensor a captured step reads (a
+        stream-ordered fill per value that changed — usually the LR alone; call outside graph
+        capture)."""
         vals = (float(self._uniform("lr")), float(self.grad_scale))
         if self._hyper is None:
             self._hyper = torch.empty(2, dtype=torch.float32, device=self.arena.param_buf.device)
             self._hyper_host = None
-        if vals != self._hyper_host:
-            self._hyper[0].fill_(vals[0])
-            self._hyper[1].fill_(vals[1])
-            self._hyper_host = vals
+        old = self._hyper_host or (None, None)
+        for i in (0, 1):
+            if vals[i] != old[i]:
+                self._hyper[i].fill_(vals[i])
+        self._hyper_host = vals
 
     def lr_device(self) -> torch.Tensor:
         """The current LR as a 1-element device tensor (the one a captured step reads; refreshed

@@ -675,7 +675,8 @@ std::tuple<Tensor, Tensor> relu_bias_bwd(Tensor dy, c10::optional<Tensor> y,
   const bool cl = dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(cl || (dy.dim() == 2 && dy.is_contiguous()), "dy: channels_last NCHW or [M, C]");
   const int64_t C = dy.size(1), M = dy.numel() / std::max<int64_t>(C, 1);
-  TORCH_CHECK(C % 8 == 0 && C > 0 && C <= 2048 && M < (1LL << 40), "relu_bias_bwd: C % 8, <= 2048");
+  TORCH_CHECK(C % 8 == 0 && C > 0 && (C <= 2048 || C % 2048 == 0) && C <= 16384 &&
+              M < (1LL << 40), "relu_bias_bwd: C % 8, <= 2048 or a multiple of 2048");
   check_aligned16(dy.data_ptr(), "dy");
   const bool relu = y.has_value() && y->defined();
   if (relu) {

@@ -385,48 +385,54 @@ __global__ __launch_bounds__(256) void k_relu_bias_bwd(const uint16_t* __restric
                                                        float* __restrict__ partial, int64_t M,
                                                        int C, int64_t rows_per_block) {
   __shared__ float sa[256 * 8];
-  const int G = C / 8, R = 256 / G;
-  const int cg = threadIdx.x % G, r = threadIdx.x / G;
-  const bool active = r < R;
-  float a[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) a[j] = 0.f;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(r0 + rows_per_block, M);
-  if (active) {
-    for (int64_t row = r0 + r; row < r1; row += R) {
-      const int64_t o = row * C + cg * 8;
-      uint4 d = *reinterpret_cast<const uint4*>(dy + o);
-      if (RELU) {
-        const uint4 v = *reinterpret_cast<const uint4*>(y + o);
-        const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
-        uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+  // channel slices of up to 2048 (256 groups of 8, the LDS fold's width): one slice for the
+  // convolutions, two for a 4096-wide classifier layer (VGG-16 fc1 / fc2)
+  for (int c0 = 0; c0 < C; c0 += 2048) {
+    const int Cs = min(2048, C - c0);
+    const int G = Cs / 8, R = 256 / G;
+    const int cg = threadIdx.x % G, r = threadIdx.x / G;
+    const bool active = r < R;
+    float a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = 0.f;
+    if (active) {
+      for (int64_t row = r0 + r; row < r1; row += R) {
+        const int64_t o = row * C + c0 + cg * 8;
+        uint4 d = *reinterpret_cast<const uint4*>(dy + o);
+        if (RELU) {
+          const uint4 v = *reinterpret_cast<const uint4*>(y + o);
+          const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+          uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            // 16-bit float > 0: sign bit clear and not +0
+            const uint32_t lo = ((vw[k] & 0x8000u) == 0u && (vw[k] & 0x7fffu) != 0u) ? 0xffffu : 0u;
+            const uint32_t hi = ((vw[k] & 0x80000000u) == 0u && (vw[k] & 0x7fff0000u) != 0u)
+                                    ? 0xffff0000u : 0u;
+            dw[k] &= lo | hi;
+          }
+          d = make_uint4(dw[0], dw[1], dw[2], dw[3]);
+          *reinterpret_cast<uint4*>(dym + o) = d;
+        }
+        const uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          // 16-bit float > 0: sign bit clear and not +0
-          const uint32_t lo = ((vw[k] & 0x8000u) == 0u && (vw[k] & 0x7fffu) != 0u) ? 0xffffu : 0u;
-          const uint32_t hi = ((vw[k] & 0x80000000u) == 0u && (vw[k] & 0x7fff0000u) != 0u)
-                                  ? 0xffff0000u : 0u;
-          dw[k] &= lo | hi;
+          a[2 * k] += hlo(w[k]);
+          a[2 * k + 1] += hhi(w[k]);
         }
-        d = make_uint4(dw[0], dw[1], dw[2], dw[3]);
-        *reinterpret_cast<uint4*>(dym + o) = d;
       }
-      const uint32_t w[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        a[2 * k] += hlo(w[k]);
-        a[2 * k + 1] += hhi(w[k]);
-      }
+      for (int j = 0; j < 8; ++j) sa[r * Cs + cg * 8 + j] = a[j];
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sa[r * C + cg * 8 + j] = a[j];
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f;
-    for (int q = 0; q < R; ++q) s += sa[q * C + c];
-    partial[(int64_t)blockIdx.x * C + c] = s;
+    __syncthreads();
+    for (int c = threadIdx.x; c < Cs; c += 256) {
+      float s = 0.f;
+      for (int q = 0; q < R; ++q) s += sa[q * Cs + c];
+      partial[(int64_t)blockIdx.x * C + c0 + c] = s;
+    }
+    __syncthreads();                     // (sa reused by the next slice)
   }
 }
 

@@ -119,6 +119,29 @@ def _pad_rows(w: torch.Tensor, n: int) -> torch.Tensor:
     return out
 
 
+def _relu_bias_native(ctx, dyf, y, dense_y: bool):
+    """ReLU mask + bias gradient of a bf16 [M, N] linear output in one native pass
+    (csrc/nn.hip k_relu_bias_bwd), an arena-managed bias accumulated in place (no AccumulateGrad
+    add): (masked dy, db or None), or None where it does not apply (fp32 dy, odd widths, a sliced
+    padded output) and the torch ops run instead."""
+    from .conv import _bias_arena_view
+    need_db = ctx.has_bias and ctx.needs_input_grad[2]
+    N = dyf.shape[1]
+    if not (ctx.relu or need_db) or not dyf.is_cuda or dyf.dtype != h16() or not dense_y or \
+            N % 8 != 0 or not (N <= 2048 or N % 2048 == 0) or N > 16384:
+        return None
+    dyc = dyf.contiguous()
+    b = ctx.bias
+    dst = _bias_arena_view(b) if need_db else None
+    dym, db = load().relu_bias_bwd(dyc, y.contiguous() if ctx.relu else None, dst)
+    if dst is not None:
+        b._lw_grad_ready(b)
+        db = None
+    elif not need_db:
+        db = None
+    return dym, db
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, relu, out_fp32=False):
@@ -138,6 +161,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w, y if relu else None)
         ctx.relu, ctx.has_bias, ctx.shape, ctx.N, ctx.Np = relu, bias is not None, shp, N, Np
         ctx.weight = weight
+        ctx.bias = bias
         return y.reshape(*shp[:-1], N)
 
     @staticmethod
@@ -145,11 +169,16 @@ class _LinearFn(torch.autograd.Function):
         x2, w, y = ctx.saved_tensors
         N, Np = ctx.N, ctx.Np
         dyf = dy.reshape(-1, N)
-        if ctx.relu:
-            dyf = dyf * (y > 0)
-        # the bias gradient from dy as it arrives (fp32 for an fp32-output classifier: a bf16 dy
-        # makes many logits' bias gradients exactly equal — Top-K ties at the threshold)
-        db = dyf.float().sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        need_db = ctx.has_bias and ctx.needs_input_grad[2]
+        done = _relu_bias_native(ctx, dyf, y, N == Np)
+        if done is not None:
+            dyf, db = done
+        else:
+            if ctx.relu:
+                dyf = dyf * (y > 0)
+            # the bias gradient from dy as it arrives (fp32 for an fp32-output classifier: a bf16
+            # dy makes many logits' bias gradients exactly equal — Top-K ties at the threshold)
+            db = dyf.float().sum(0) if need_db else None
         dy2 = dyf.to(h16())
         if Np != N:
             dy2 = torch.cat([dy2, dy2.new_zeros(dy2.shape[0], Np - N)], 1)
@@ -188,14 +217,19 @@ class _ReplicatedLinearFn(torch.autograd.Function):
         y = linear_fwd(x2, weff, b, relu)
         ctx.save_for_backward(x2, weff, y if relu else None)
         ctx.weight, ctx.reps, ctx.relu, ctx.has_bias = weight, reps, relu, bias is not None
+        ctx.bias = bias
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x2, weff, y = ctx.saved_tensors
         p, reps = ctx.weight, ctx.reps
-        dyf = dy * (y > 0) if ctx.relu else dy
-        db = dyf.float().sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        done = _relu_bias_native(ctx, dy, y, True)
+        if done is not None:
+            dyf, db = done
+        else:
+            dyf = dy * (y > 0) if ctx.relu else dy
+            db = dyf.float().sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
         dy2 = dyf.to(h16()).contiguous()
         dx = linear_dgrad(dy2, weff) if ctx.needs_input_grad[0] else None
         dw = None

@@ -588,6 +588,19 @@ def fused_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index
     return loss, corr
 
 
+def fuse_dict_losses(model: nn.Module) -> nn.Module:
+    """A CIFAR nn.Module model's ``loss = (CrossEntropyLoss, Correct)`` heads
+    (models/cifar.py _DictLossMixin: VGG-16, the module AlexNet) on the fused cross-entropy
+    kernel, the correctness read from it (as fuse_graph_network does for the graph nets)."""
+    from ..models.graph import Correct
+    heads = getattr(model, "loss", None)
+    if isinstance(heads, tuple) and len(heads) == 2 and type(heads[0]) is nn.CrossEntropyLoss \
+            and type(heads[1]) is Correct:
+        heads[0].__class__ = FusedCrossEntropyLoss
+        model.loss = (heads[0], _XentCorrect(heads[0]))
+    return model
+
+
 class _XentCorrect(nn.Module):
     """``Correct`` (argmax == target) of a graph whose loss node runs the fused kernel on the same
     inputs: that kernel's top-1 column (one compare launch instead of a max-reduce and an equality;

@@ -26,12 +26,16 @@ from .graphs import StepGraph
 
 
 def _first_conv_pads(net) -> bool:
-    """The graph net's input feeds exactly one node, an MFMA convolution of 3 input channels
-    (which reads a zero-padded 4-channel copy of its input, ops/conv.py _c4_input)."""
+    """The net's input feeds exactly one MFMA convolution of 3 input channels (which reads a
+    zero-padded 4-channel copy of its input, ops/conv.py _c4_input)."""
     from ..ops.conv import MFMAConv2d
     graph = getattr(net, "graph", None)
     if graph is None:
-        return False
+        # the module nets (VGG-16, the module AlexNet: models/cifar.py) feed batch["input"]
+        # straight into features[0]
+        feats = getattr(net, "features", None)
+        first = feats[0] if isinstance(feats, torch.nn.Sequential) and len(feats) else None
+        return isinstance(first, MFMAConv2d) and first.in_channels == 3
     users = [m for m, ins in graph.values() if "input" in ins]
     return len(users) == 1 and isinstance(users[0], MFMAConv2d) and users[0].in_channels == 3
 
@@ -51,6 +55,7 @@ class CifarTrainer:
             from ..ops.conv import fuse_convs
             from ..ops.gemm import fuse_linears
             lwnn.fuse_graph_network(net)
+            lwnn.fuse_dict_losses(net)
             fuse_convs(net)          # every conv / Linear on the MFMA kernels
             fuse_linears(net)
         net = net.to(self.device)

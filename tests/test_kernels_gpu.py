@@ -274,3 +274,22 @@ def test_cifar_augment_pad4_zero_channel():
         assert x4.shape[1] == 4 and x4.is_contiguous(memory_format=torch.channels_last)
         assert torch.equal(x4[:, :3], x3)
         assert int((x4[:, 3] != 0).sum()) == 0
+
+
+@pytest.mark.parametrize("M,C", [(512, 64), (1000, 2048), (512, 4096), (96, 6144)])
+def test_relu_bias_bwd_matches_torch(M, C):
+    """csrc/nn.hip k_relu_bias_bwd (the bias + ReLU epilogue backward, channel slices of 2048 for
+    the 4096-wide classifier layers): dy·[y > 0] bit for bit and the fp32 bias gradient, also
+    accumulated into a given buffer."""
+    from layer_wise_aaai20_amd.ops._ext import h16, load
+    torch.manual_seed(0)
+    dy = torch.randn(M, C, device="cuda").to(h16())
+    y = torch.randn(M, C, device="cuda").to(h16())
+    dym, db = load().relu_bias_bwd(dy, y, None)
+    ref = dy * (y > 0)
+    assert torch.equal(dym, ref)
+    exp = ref.float().sum(0)
+    assert torch.allclose(db, exp, rtol=1e-5, atol=1e-3)
+    acc = torch.ones(C, device="cuda")
+    load().relu_bias_bwd(dy, y, acc)
+    assert torch.allclose(acc, exp + 1, rtol=1e-5, atol=1e-3)

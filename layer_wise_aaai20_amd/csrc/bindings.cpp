@@ -694,7 +694,7 @@ std::tuple<Tensor, Tensor> relu_bias_bwd(Tensor dy, c10::optional<Tensor> y,
   } else {
     db = at::empty({C}, dy.options().dtype(at::kFloat));
   }
-  Tensor partial = at::empty({(int64_t)lw::relu_bias_bwd_blocks(M) * C}, db.options());
+  Tensor partial = at::empty({(int64_t)lw::relu_bias_bwd_blocks(M, (int)C) * C}, db.options());
   lw::relu_bias_bwd(ptr<uint16_t>(dy), relu ? ptr<uint16_t>(*y) : nullptr,
                     relu ? ptr<uint16_t>(dym) : nullptr, ptr<float>(partial), ptr<float>(db), M,
                     (int)C, acc, cur_stream());

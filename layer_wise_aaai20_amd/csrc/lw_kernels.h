@@ -370,7 +370,7 @@ void xent(const float* logits, const int64_t* target, int B, int C, float gscale
 // backward of a fused bias + ReLU epilogue (nn.hip): dym = dy·[y > 0] (y null: no ReLU, dym
 // unused) and db (+)= Σ_rows dym; rows [M][C] bf16, C % 8 == 0, C <= 2048; partial holds
 // relu_bias_bwd_blocks(M) * C floats
-int relu_bias_bwd_blocks(int64_t M);
+int relu_bias_bwd_blocks(int64_t M, int C);
 void relu_bias_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dym, float* partial,
                    float* db, int64_t M, int C, bool accumulate, hipStream_t st);
 void normalize_u8_c4(const uint8_t* in, uint16_t* out, int64_t npix, const float mean[3],

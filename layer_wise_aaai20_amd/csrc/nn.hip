@@ -6,6 +6,8 @@
 //                   (IMAGENET/training/dataloader.py:81-93) with one pass:
 //                   16 input bytes per lane (one dwordx4 load), two or four 16-B stores.
 #include "common.h"
+
+#include <algorithm>
 #include "lw_kernels.h"
 #include "elem16.h"
 
@@ -472,14 +474,19 @@ __global__ __launch_bounds__(64 * FOLD_LANES) void k_fold_rows(const float* __re
 
 // up to 2048 blocks of >= 256 rows: 512 blocks (2 per CU) left the pass latency-bound at ~1.6 TB/s
 // on the CIFAR VGG-16 / AlexNet feature maps
-int relu_bias_bwd_blocks(int64_t M) {
-  const int64_t nb = (M + 255) / 256;
+// Row blocks: one per 256 rows, and for wide layers enough that a block's share stays near 32 K
+// elements (a 4096-wide classifier layer of a 512 batch ran as 2 blocks walking 256 rows each:
+// ~200 µs of latency instead of a few)
+int relu_bias_bwd_blocks(int64_t M, int C) {
+  int64_t nb = (M + 255) / 256;
+  const int64_t wide = std::min<int64_t>(M, (M * (int64_t)C + 32767) / 32768);
+  if (wide > nb) nb = wide;
   return (int)(nb < 2048 ? (nb < 1 ? 1 : nb) : 2048);
 }
 
 void relu_bias_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dym, float* partial,
                    float* db, int64_t M, int C, bool accumulate, hipStream_t st) {
-  const int nb = relu_bias_bwd_blocks(M);
+  const int nb = relu_bias_bwd_blocks(M, C);
   const int64_t rpb = (M + nb - 1) / nb;
   if (y)
     hipLaunchKernelGGL(k_relu_bias_bwd<true>, dim3(nb), dim3(256), 0, st, dy, y, dym, partial, M,

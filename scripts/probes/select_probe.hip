@@ -124,7 +124,7 @@ int main(int argc, char** argv) {
     if (it >= 10) tot += ms;
   }
   // one more call from the pristine inputs: FNV hashes of the payload and the residual, so runs
-  // with LWAAAI_SELECT_PERSIST=0 / 1 can be compared bit for bit
+  // of different builds (-D knobs) can be compared bit for bit
   CK(hipMemcpyAsync(g, g0, n * 4, hipMemcpyDeviceToDevice, st));
   CK(hipMemcpyAsync(e, e0, n * 4, hipMemcpyDeviceToDevice, st));
   lw::select_compress(a, lw::KM_TOPK, lw::OUT_PAIRS, true, st, false);

@@ -665,6 +665,40 @@ std::tuple<Tensor, Tensor, Tensor> xent(Tensor logits, Tensor target, double gsc
   return {loss, corr, grad};
 }
 
+// (mean, count) of xent's per-row losses over the non-ignored targets (one launch): a 0-dim loss
+// and a [1] count
+std::tuple<Tensor, Tensor> xent_mean(Tensor rows, Tensor target, int64_t ignore_index) {
+  const c10::DeviceGuard guard(rows.device());
+  check_cuda(rows, "rows");
+  check_dtype(rows, at::kFloat, "rows");
+  check_cuda(target, "target");
+  check_dtype(target, at::kLong, "target");
+  TORCH_CHECK(rows.dim() == 1 && target.dim() == 1 && rows.size(0) == target.size(0) &&
+              rows.size(0) < (1LL << 30), "xent_mean: rows / target [B]");
+  Tensor out = at::empty({}, rows.options());
+  Tensor n = at::empty({1}, rows.options());
+  lw::xent_mean(ptr<float>(rows), ptr<int64_t>(target), (int)rows.size(0), (int)ignore_index,
+                ptr<float>(out), ptr<float>(n), cur_stream());
+  launched("xent_mean");
+  return {out, n};
+}
+
+// grad · (gl / n) with gl, n one-element fp32 device tensors
+Tensor xent_scale(Tensor grad, Tensor gl, Tensor n) {
+  const c10::DeviceGuard guard(grad.device());
+  check_cuda(grad, "grad");
+  check_dtype(grad, at::kFloat, "grad");
+  check_dtype(gl, at::kFloat, "gl");
+  check_dtype(n, at::kFloat, "n");
+  TORCH_CHECK(gl.is_cuda() && n.is_cuda() && gl.numel() == 1 && n.numel() >= 1,
+              "xent_scale: gl / n device scalars");
+  Tensor out = at::empty_like(grad);
+  lw::xent_scale(ptr<float>(grad), ptr<float>(gl), ptr<float>(n), grad.numel(), ptr<float>(out),
+                 cur_stream());
+  launched("xent_scale");
+  return out;
+}
+
 // bias + ReLU epilogue backward (nn.hip): dy, y bf16 rows [M, C] (channels_last NCHW or 2-D) ->
 // (dy·[y > 0] (or dy itself without y), db fp32 [C]; accumulated into db_out when given)
 std::tuple<Tensor, Tensor> relu_bias_bwd(Tensor dy, c10::optional<Tensor> y,
@@ -1863,6 +1897,8 @@ LW_LIBRARY(LW_OPS_NS, m) {
   m.def("mc_mask(Tensor(a!) u, Tensor e) -> ()");
   m.def("step_bump(Tensor(a!) c) -> ()");
   m.def("splitk_defer(Tensor dev, bool on) -> ()");
+  m.def("xent_mean(Tensor rows, Tensor target, int ignore_index) -> (Tensor, Tensor)");
+  m.def("xent_scale(Tensor grad, Tensor gl, Tensor n) -> Tensor");
   m.def("splitk_flush(Tensor dev) -> int");
   m.def(
       "sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor seg_off, Tensor seg_n, "
@@ -1949,6 +1985,8 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("mc_mask", &mc_mask);
   m.impl("step_bump", &step_bump);
   m.impl("splitk_defer", &splitk_defer);
+  m.impl("xent_mean", &xent_mean);
+  m.impl("xent_scale", &xent_scale);
   m.impl("splitk_flush", &splitk_flush);
   m.impl("normalize_u8", &normalize_u8);
   m.impl("cifar_augment", &cifar_augment);

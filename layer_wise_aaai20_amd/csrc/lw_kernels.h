@@ -371,6 +371,11 @@ void xent(const float* logits, const int64_t* target, int B, int C, float gscale
 // unused) and db (+)= Σ_rows dym; rows [M][C] bf16, C % 8 == 0, C <= 2048; partial holds
 // relu_bias_bwd_blocks(M) * C floats
 int relu_bias_bwd_blocks(int64_t M, int C);
+// mean cross-entropy [mean, count] of k_xent's rows, and its backward grad · gl / n (nn.hip)
+void xent_mean(const float* rows, const int64_t* target, int B, int ignore_index, float* out,
+               float* out_n, hipStream_t st);
+void xent_scale(const float* grad, const float* gl, const float* n, int64_t total, float* out,
+                hipStream_t st);
 void relu_bias_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dym, float* partial,
                    float* db, int64_t M, int C, bool accumulate, hipStream_t st);
 void normalize_u8_c4(const uint8_t* in, uint16_t* out, int64_t npix, const float mean[3],

@@ -371,6 +371,62 @@ void xent(const float* logits, const int64_t* target, int B, int C, float gscale
                      C, gscale, ignore_index, loss, corr, grad);
 }
 
+// Mean cross-entropy over the rows whose target is not ignore_index, in one workgroup (the torch
+// path ran a compare, a cast, two reductions, a clamp and a division: six launches). Thread-strided
+// partial sums folded in a fixed order: deterministic. out = mean, out_n = max(count, 1).
+__global__ __launch_bounds__(256) void k_xent_mean(const float* __restrict__ rows,
+                                                   const int64_t* __restrict__ target, int B,
+                                                   int ignore_index, float* __restrict__ out,
+                                                   float* __restrict__ out_n) {
+  __shared__ float ss[256];
+  __shared__ int sn[256];
+  float s = 0.f;
+  int n = 0;
+  for (int i = threadIdx.x; i < B; i += 256) {
+    s += rows[i];
+    n += target[i] != ignore_index ? 1 : 0;
+  }
+  ss[threadIdx.x] = s;
+  sn[threadIdx.x] = n;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      ss[threadIdx.x] += ss[threadIdx.x + w];
+      sn[threadIdx.x] += sn[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float cnt = (float)(sn[0] > 0 ? sn[0] : 1);
+    out[0] = ss[0] / cnt;
+    out_n[0] = cnt;
+  }
+}
+
+// Backward of the mean: d(logits) = grad · (gl / n), gl and n device scalars (one launch).
+__global__ __launch_bounds__(256) void k_xent_scale(const float* __restrict__ grad,
+                                                    const float* __restrict__ gl,
+                                                    const float* __restrict__ n, int64_t total,
+                                                    float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const float f = gl[0] / n[0];
+  out[i] = grad[i] * f;
+}
+
+void xent_mean(const float* rows, const int64_t* target, int B, int ignore_index, float* out,
+               float* out_n, hipStream_t st) {
+  hipLaunchKernelGGL(k_xent_mean, dim3(1), dim3(256), 0, st, rows, target, B, ignore_index, out,
+                     out_n);
+}
+
+void xent_scale(const float* grad, const float* gl, const float* n, int64_t total, float* out,
+                hipStream_t st) {
+  if (total == 0) return;
+  hipLaunchKernelGGL(k_xent_scale, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, grad,
+                     gl, n, total, out);
+}
+
 }  // namespace lw
 
 namespace lw {

@@ -548,8 +548,8 @@ class _XentFn(torch.autograd.Function):
         ctx.reduction = reduction
         ctx.dtype = logits.dtype
         if reduction == "mean":
-            n = (target != ignore_index).sum().clamp_min(1).to(torch.float32)
-            loss = rows.sum() / n
+            # mean and valid count in one launch (csrc/nn.hip k_xent_mean)
+            loss, n = load().xent_mean(rows, target.contiguous(), int(ignore_index))
         elif reduction == "sum":
             n = None
             loss = rows.sum()
@@ -566,7 +566,10 @@ class _XentFn(torch.autograd.Function):
         if ctx.reduction == "none":
             g = grad * gl.view(-1, 1)
         elif ctx.reduction == "mean":
-            g = grad * (gl / n)
+            if gl.is_cuda and gl.dtype == torch.float32 and gl.numel() == 1:
+                g = load().xent_scale(grad, gl.reshape(1), n)       # (k_xent_scale)
+            else:
+                g = grad * (gl / n)
         else:
             g = grad * gl
         return g.to(ctx.dtype), None, None, None

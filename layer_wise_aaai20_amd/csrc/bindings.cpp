@@ -1193,6 +1193,36 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
 // Every index the kernels can form is checked here against the tensors' sizes.
 // K-contiguous data-gradient weight pack (csrc/conv.hip k_pack_dgrad_kc): w is a bf16
 // channels_last [Co, C, R, S] weight; cls = 4 ints (r0, s0, TR, TS) per parity class.
+// pack_dgrad_kc of several 1x1 weights [Co][C] (2-D or [Co][C][1][1], bf16/fp16, contiguous)
+// into the given [C][kmax] buffers, one launch
+void pack_t_multi(std::vector<Tensor> w, std::vector<Tensor> out, std::vector<int64_t> kmax) {
+  TORCH_CHECK(w.size() == out.size() && w.size() == kmax.size(), "pack_t_multi: list sizes");
+  if (w.empty()) return;
+  const c10::DeviceGuard guard(w[0].device());
+  std::vector<const uint16_t*> wp;
+  std::vector<uint16_t*> op;
+  std::vector<int> co, c, km;
+  for (size_t i = 0; i < w.size(); ++i) {
+    check_dtype(w[i], kH16, "weight");
+    check_dtype(out[i], kH16, "out");
+    TORCH_CHECK(w[i].is_cuda() && w[i].is_contiguous() && out[i].is_contiguous() &&
+                out[i].device() == w[0].device() && w[i].device() == w[0].device(),
+                "pack_t_multi: contiguous GPU tensors on one device");
+    const int64_t Co = w[i].size(0), C = w[i].numel() / Co;
+    TORCH_CHECK(kmax[i] % 8 == 0 && kmax[i] >= Co && out[i].numel() == C * kmax[i],
+                "pack_t_multi: out [C][kmax], kmax % 8 == 0, kmax >= Co");
+    check_aligned16(out[i].data_ptr(), "out");
+    wp.push_back(ptr<uint16_t>(w[i]));
+    op.push_back(ptr<uint16_t>(out[i]));
+    co.push_back((int)Co);
+    c.push_back((int)C);
+    km.push_back((int)kmax[i]);
+  }
+  lw::pack_t_multi(wp.data(), op.data(), co.data(), c.data(), km.data(), (int)w.size(),
+                   cur_stream());
+  launched("pack_t_multi");
+}
+
 Tensor pack_dgrad_kc(Tensor w, std::vector<int64_t> cls, int64_t sh, int64_t sw, int64_t kmax) {
   const c10::DeviceGuard guard(w.device());
   TORCH_CHECK(w.is_cuda() && w.dim() == 4, "pack_dgrad_kc: a 4-d GPU weight");
@@ -1898,6 +1928,7 @@ LW_LIBRARY(LW_OPS_NS, m) {
   m.def("step_bump(Tensor(a!) c) -> ()");
   m.def("splitk_defer(Tensor dev, bool on) -> ()");
   m.def("xent_mean(Tensor rows, Tensor target, int ignore_index) -> (Tensor, Tensor)");
+  m.def("pack_t_multi(Tensor[] w, Tensor(a!)[] out, int[] kmax) -> ()");
   m.def("xent_scale(Tensor grad, Tensor gl, Tensor n) -> Tensor");
   m.def("splitk_flush(Tensor dev) -> int");
   m.def(
@@ -1986,6 +2017,7 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("step_bump", &step_bump);
   m.impl("splitk_defer", &splitk_defer);
   m.impl("xent_mean", &xent_mean);
+  m.impl("pack_t_multi", &pack_t_multi);
   m.impl("xent_scale", &xent_scale);
   m.impl("splitk_flush", &splitk_flush);
   m.impl("normalize_u8", &normalize_u8);

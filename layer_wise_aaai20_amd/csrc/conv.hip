@@ -69,6 +69,57 @@ __global__ __launch_bounds__(256) void k_pack_dgrad_kc(const uint16_t* __restric
   }
 }
 
+// Several 1x1 transposes Wᵀ (pack_dgrad_kc with one R = S = 1 class) in one launch: out[c][k] =
+// w[k][c] for k < Co, zero up to kmax. The 1x1 data-gradient GEMMs that run on the K-contiguous
+// layout pack their weights this way once per step (ops/block.py _kc_weight), not one launch each.
+struct TJob {
+  const uint16_t* w;
+  uint16_t* out;
+  int Co, C, kmax;
+  int64_t blk_lo;
+};
+constexpr int kMaxTJobs = 32;
+struct TJobs {
+  TJob j[kMaxTJobs];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void k_pack_t_multi(const TJobs jobs) {
+  int ji = 0;
+  for (int q = 1; q < jobs.n; ++q)
+    if ((int64_t)blockIdx.x >= jobs.j[q].blk_lo) ji = q;
+  const TJob J = jobs.j[ji];
+  const int64_t per_row = J.kmax / 8, total = (int64_t)J.C * per_row;
+  const int64_t t = ((int64_t)blockIdx.x - J.blk_lo) * 256 + threadIdx.x;
+  if (t >= total) return;
+  const int c = (int)(t / per_row);
+  const int k0 = (int)(t - (int64_t)c * per_row) * 8;
+  uint16_t v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int k = k0 + q;
+    v[q] = k < J.Co ? J.w[(int64_t)k * J.C + c] : (uint16_t)0;
+  }
+  *reinterpret_cast<uint4*>(J.out + (int64_t)c * J.kmax + k0) =
+      make_uint4((uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
+                 (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16));
+}
+
+void pack_t_multi(const uint16_t* const* w, uint16_t* const* out, const int* Co, const int* C,
+                  const int* kmax, int n, hipStream_t st) {
+  for (int b = 0; b < n; b += kMaxTJobs) {
+    TJobs jobs{};
+    jobs.n = n - b < kMaxTJobs ? n - b : kMaxTJobs;
+    int64_t blocks = 0;
+    for (int q = 0; q < jobs.n; ++q) {
+      const int i = b + q;
+      jobs.j[q] = TJob{w[i], out[i], Co[i], C[i], kmax[i], blocks};
+      blocks += ((int64_t)C[i] * (kmax[i] / 8) + 255) / 256;
+    }
+    hipLaunchKernelGGL(k_pack_t_multi, dim3((unsigned)blocks), dim3(256), 0, st, jobs);
+  }
+}
+
 // The [K][C] form (the data-gradient GEMM's B operand read with the transposing LDS loads): class
 // i's slab Wt_i[jr][js][co][ci] = w[co][r0 + sh*jr][s0 + sw*js][ci], slabs back to back. Each
 // thread moves 8 consecutive ci (one 16-byte load and store; C % 8 == 0). Replaces a permute +

@@ -185,6 +185,44 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
 
 LAYOUT_TUNER = Tuner("dgrad-layout", "LWAAAI_GEMM_TUNE")
 
+# 1x1 data-gradient weights in the K-contiguous layout (Wᵀ, gemm_dgrad "kc"): at a step's first
+# request every layer that asked last step is packed in one launch (csrc/conv.hip
+# k_pack_t_multi; ResNet-50 ran ~15 pack launches a step), a layer not seen before packs alone and
+# joins. The weights are the bf16 mirror's views (refreshed in place every step), so the list
+# stays valid; entries not asked for in a step are dropped. The gradient engine's begin_step
+# starts a new step (new_step). LWAAAI_KC_BATCH=0: one pack per request.
+KC_BATCH = os.environ.get("LWAAAI_KC_BATCH", "1") != "0"
+_KC = {"gen": -1, "reg": {}, "cache": {}, "used": set()}
+_STEP_GEN = [0]
+
+
+def new_step() -> None:
+    _STEP_GEN[0] += 1
+
+
+def _kc_weight(W: torch.Tensor, K: int, N: int, kp: int, fresh: bool = False) -> torch.Tensor:
+    if fresh or not KC_BATCH or not W.is_cuda or not W.is_contiguous():
+        return load().pack_dgrad_kc(W.reshape(K, N, 1, 1), [0, 0, 1, 1], 1, 1, kp)
+    key = (W.data_ptr(), K, N, kp)
+    if _KC["gen"] != _STEP_GEN[0]:
+        _KC["gen"] = _STEP_GEN[0]
+        _KC["reg"] = {k: w for k, w in _KC["reg"].items() if k in _KC["used"]}
+        _KC["used"] = set()
+        _KC["cache"] = {}
+        reg = list(_KC["reg"].items())
+        if reg:
+            outs = [torch.empty(k[2] * k[3], dtype=w.dtype, device=w.device) for k, w in reg]
+            load().pack_t_multi([w for _, w in reg], outs, [k[3] for k, _ in reg])
+            _KC["cache"] = {k: o for (k, _), o in zip(reg, outs)}
+    _KC["used"].add(key)
+    hit = _KC["cache"].get(key)
+    if hit is not None:
+        return hit
+    out = load().pack_dgrad_kc(W.reshape(K, N, 1, 1), [0, 0, 1, 1], 1, 1, kp)
+    _KC["reg"][key] = W
+    _KC["cache"][key] = out
+    return out
+
 
 def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
     """Data-gradient GEMM ``dy[M, K] · W[K, N]`` of a 1x1 convolution (W is the forward weight
@@ -193,11 +231,11 @@ def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
     2048x512) so that both operands are K-contiguous and the LDS-DMA staging and the big tiles
     apply. ``bst`` (backward statistics) needs the stored layout. (Round 4's opt-in hipBLASLt
     candidate is gone: every kernel of the step is ours.)"""
-    def run(layout, **over):
+    def run(layout, fresh=False, **over):
         args = dict(kw, **over)
-        if layout == "kc":            # Wᵀ by one pack launch, timed with the GEMM
+        if layout == "kc":            # Wᵀ (the tuner times a pack of its own with the GEMM)
             kp = -(-K // 8) * 8
-            wt = load().pack_dgrad_kc(W.reshape(K, N, 1, 1), [0, 0, 1, 1], 1, 1, kp)
+            wt = _kc_weight(W, K, N, kp, fresh)
             return gemm(dy, ldy, True, wt, kp, True, M, N, K, **args)
         return gemm(dy, ldy, True, W, N, False, M, N, K, **args)
     if kw.get("bst") is not None:
@@ -205,7 +243,7 @@ def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
     cands = ("nkc", "kc")
     key = (M, N, K, kw.get("addend") is not None, kw.get("out") is not None)
     # timed on a scratch output (``out`` may also be the addend: dx += ... in place)
-    layout = LAYOUT_TUNER.pick(key, lambda c: run(c, out=None), cands, "nkc")
+    layout = LAYOUT_TUNER.pick(key, lambda c: run(c, fresh=True, out=None), cands, "nkc")
     return run(layout)
 
 

@@ -492,6 +492,9 @@ class GradSyncEngine:
             self.arena.zero_()
         else:
             self.arena.zero_except(self._no_zero)
+        if self.device.type == "cuda":
+            from ..ops import block as _block
+            _block.new_step()            # (per-step caches of the fused blocks: _kc_weight)
         if not self.arena.grads_attached():
             self.arena.attach_grads()
         if self.lr_scaled:

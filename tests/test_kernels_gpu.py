@@ -293,3 +293,18 @@ def test_relu_bias_bwd_matches_torch(M, C):
     acc = torch.ones(C, device="cuda")
     load().relu_bias_bwd(dy, y, acc)
     assert torch.allclose(acc, exp + 1, rtol=1e-5, atol=1e-3)
+
+
+def test_pack_t_multi_matches_single_packs():
+    """csrc/conv.hip k_pack_t_multi (several 1x1 Wᵀ packs in one launch, ops/block.py
+    _kc_weight) against one pack_dgrad_kc per weight, bit for bit (zero-padded rows)."""
+    from layer_wise_aaai20_amd.ops._ext import h16, load
+    torch.manual_seed(0)
+    shapes = [(256, 64), (64, 256), (1000, 512), (2048, 1024), (24, 40)]
+    ws = [torch.randn(k, n, device="cuda").to(h16()) for k, n in shapes]
+    kps = [-(-k // 8) * 8 for k, _ in shapes]
+    outs = [torch.empty(n * kp, dtype=h16(), device="cuda") for (_, n), kp in zip(shapes, kps)]
+    load().pack_t_multi(ws, outs, kps)
+    for w, o, (k, n), kp in zip(ws, outs, shapes, kps):
+        ref = load().pack_dgrad_kc(w.reshape(k, n, 1, 1), [0, 0, 1, 1], 1, 1, kp)
+        assert torch.equal(o, ref)

@@ -1193,34 +1193,49 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
 // Every index the kernels can form is checked here against the tensors' sizes.
 // K-contiguous data-gradient weight pack (csrc/conv.hip k_pack_dgrad_kc): w is a bf16
 // channels_last [Co, C, R, S] weight; cls = 4 ints (r0, s0, TR, TS) per parity class.
-// pack_dgrad_kc of several 1x1 weights [Co][C] (2-D or [Co][C][1][1], bf16/fp16, contiguous)
-// into the given [C][kmax] buffers, one launch
-void pack_t_multi(std::vector<Tensor> w, std::vector<Tensor> out, std::vector<int64_t> kmax) {
-  TORCH_CHECK(w.size() == out.size() && w.size() == kmax.size(), "pack_t_multi: list sizes");
+// pack_dgrad_kc of several weights in one launch: w[i] (channels_last [Co][C][R][S] memory, or a
+// contiguous [Co][C] for a 1x1) into out[i] ([nclass][C][kmax]); prm: 20 ints per job —
+// [sh, sw, kmax, nclass, r0 x4, s0 x4, TR x4, TS x4] as pack_dgrad_kc's arguments (padded to 4
+// classes)
+void pack_kc_multi(std::vector<Tensor> w, std::vector<Tensor> out, std::vector<int64_t> prm) {
+  TORCH_CHECK(w.size() == out.size() && prm.size() == 20 * w.size(), "pack_kc_multi: list sizes");
   if (w.empty()) return;
   const c10::DeviceGuard guard(w[0].device());
   std::vector<const uint16_t*> wp;
   std::vector<uint16_t*> op;
-  std::vector<int> co, c, km;
+  std::vector<int> p;
   for (size_t i = 0; i < w.size(); ++i) {
     check_dtype(w[i], kH16, "weight");
     check_dtype(out[i], kH16, "out");
-    TORCH_CHECK(w[i].is_cuda() && w[i].is_contiguous() && out[i].is_contiguous() &&
-                out[i].device() == w[0].device() && w[i].device() == w[0].device(),
-                "pack_t_multi: contiguous GPU tensors on one device");
-    const int64_t Co = w[i].size(0), C = w[i].numel() / Co;
-    TORCH_CHECK(kmax[i] % 8 == 0 && kmax[i] >= Co && out[i].numel() == C * kmax[i],
-                "pack_t_multi: out [C][kmax], kmax % 8 == 0, kmax >= Co");
+    const bool cl = w[i].dim() == 4 && (w[i].is_contiguous(at::MemoryFormat::ChannelsLast) ||
+                                        (w[i].size(2) == 1 && w[i].size(3) == 1 &&
+                                         w[i].is_contiguous()));
+    TORCH_CHECK(w[i].is_cuda() && cl && out[i].is_contiguous() && w[i].device() == w[0].device()
+                && out[i].device() == w[0].device(),
+                "pack_kc_multi: channels_last 4-d GPU weights on one device");
+    const int64_t* q = prm.data() + 20 * i;
+    const int Co = (int)w[i].size(0), C = (int)w[i].size(1), R = (int)w[i].size(2),
+              S = (int)w[i].size(3);
+    const int sh = (int)q[0], sw = (int)q[1], kmax = (int)q[2], nclass = (int)q[3];
+    TORCH_CHECK(nclass >= 1 && nclass <= 4 && kmax % 8 == 0 && (sh >= 1 || sh == -1) &&
+                (sw >= 1 || sw == -1) && out[i].numel() == (int64_t)nclass * C * kmax,
+                "pack_kc_multi: classes / kmax / out size");
+    for (int k = 0; k < nclass; ++k) {
+      const int64_t r0 = q[4 + k], s0 = q[8 + k], TR = q[12 + k], TS = q[16 + k];
+      const int64_t rl = r0 + sh * (TR - 1), sl = s0 + sw * (TS - 1);
+      TORCH_CHECK(r0 >= 0 && s0 >= 0 && TR >= 1 && TS >= 1 && r0 < R && s0 < S && rl >= 0 &&
+                  rl < R && sl >= 0 && sl < S && TR * TS * Co <= kmax,
+                  "pack_kc_multi: class taps outside the kernel window");
+    }
     check_aligned16(out[i].data_ptr(), "out");
     wp.push_back(ptr<uint16_t>(w[i]));
     op.push_back(ptr<uint16_t>(out[i]));
-    co.push_back((int)Co);
-    c.push_back((int)C);
-    km.push_back((int)kmax[i]);
+    const int row[8] = {Co, C, R, S, sh, sw, nclass, kmax};
+    for (int k = 0; k < 8; ++k) p.push_back(row[k]);
+    for (int k = 0; k < 16; ++k) p.push_back((int)q[4 + k]);
   }
-  lw::pack_t_multi(wp.data(), op.data(), co.data(), c.data(), km.data(), (int)w.size(),
-                   cur_stream());
-  launched("pack_t_multi");
+  lw::pack_kc_multi(wp.data(), op.data(), p.data(), (int)w.size(), cur_stream());
+  launched("pack_kc_multi");
 }
 
 Tensor pack_dgrad_kc(Tensor w, std::vector<int64_t> cls, int64_t sh, int64_t sw, int64_t kmax) {
@@ -1928,7 +1943,7 @@ LW_LIBRARY(LW_OPS_NS, m) {
   m.def("step_bump(Tensor(a!) c) -> ()");
   m.def("splitk_defer(Tensor dev, bool on) -> ()");
   m.def("xent_mean(Tensor rows, Tensor target, int ignore_index) -> (Tensor, Tensor)");
-  m.def("pack_t_multi(Tensor[] w, Tensor(a!)[] out, int[] kmax) -> ()");
+  m.def("pack_kc_multi(Tensor[] w, Tensor(a!)[] out, int[] prm) -> ()");
   m.def("xent_scale(Tensor grad, Tensor gl, Tensor n) -> Tensor");
   m.def("splitk_flush(Tensor dev) -> int");
   m.def(
@@ -2017,7 +2032,7 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("step_bump", &step_bump);
   m.impl("splitk_defer", &splitk_defer);
   m.impl("xent_mean", &xent_mean);
-  m.impl("pack_t_multi", &pack_t_multi);
+  m.impl("pack_kc_multi", &pack_kc_multi);
   m.impl("xent_scale", &xent_scale);
   m.impl("splitk_flush", &splitk_flush);
   m.impl("normalize_u8", &normalize_u8);

@@ -69,54 +69,79 @@ __global__ __launch_bounds__(256) void k_pack_dgrad_kc(const uint16_t* __restric
   }
 }
 
-// Several 1x1 transposes Wᵀ (pack_dgrad_kc with one R = S = 1 class) in one launch: out[c][k] =
-// w[k][c] for k < Co, zero up to kmax. The 1x1 data-gradient GEMMs that run on the K-contiguous
-// layout pack their weights this way once per step (ops/block.py _kc_weight), not one launch each.
-struct TJob {
+// Several pack_dgrad_kc packs in one launch (ops/conv.py kc_pack_step: the K-contiguous
+// data-gradient weights of a step — 1x1 transposes and strided / 3x3 class slabs — packed once
+// per step at the first request instead of one launch each). Per job the body of k_pack_dgrad_kc.
+struct KcJob {
   const uint16_t* w;
   uint16_t* out;
-  int Co, C, kmax;
+  int Co, C, R, S, sh, sw, nclass, kmax;
+  PackClasses pc;
   int64_t blk_lo;
 };
-constexpr int kMaxTJobs = 32;
-struct TJobs {
-  TJob j[kMaxTJobs];
+constexpr int kMaxKcJobs = 24;
+struct KcJobs {
+  KcJob j[kMaxKcJobs];
   int n;
 };
 
-__global__ __launch_bounds__(256) void k_pack_t_multi(const TJobs jobs) {
+__global__ __launch_bounds__(256) void k_pack_kc_multi(const KcJobs jobs) {
   int ji = 0;
   for (int q = 1; q < jobs.n; ++q)
     if ((int64_t)blockIdx.x >= jobs.j[q].blk_lo) ji = q;
-  const TJob J = jobs.j[ji];
-  const int64_t per_row = J.kmax / 8, total = (int64_t)J.C * per_row;
+  const KcJob& J = jobs.j[ji];
+  const int64_t per_row = J.kmax / 8, per_class = (int64_t)J.C * per_row;
   const int64_t t = ((int64_t)blockIdx.x - J.blk_lo) * 256 + threadIdx.x;
-  if (t >= total) return;
-  const int c = (int)(t / per_row);
-  const int k0 = (int)(t - (int64_t)c * per_row) * 8;
+  if (t >= J.nclass * per_class) return;
+  const int i = (int)(t / per_class);
+  const int64_t rem = t - i * per_class;
+  const int c = (int)(rem / per_row);
+  const int k0 = (int)(rem - (int64_t)c * per_row) * 8;
+  const int r0 = i == 0 ? J.pc.r0[0] : i == 1 ? J.pc.r0[1] : i == 2 ? J.pc.r0[2] : J.pc.r0[3];
+  const int s0 = i == 0 ? J.pc.s0[0] : i == 1 ? J.pc.s0[1] : i == 2 ? J.pc.s0[2] : J.pc.s0[3];
+  const int TR = i == 0 ? J.pc.TR[0] : i == 1 ? J.pc.TR[1] : i == 2 ? J.pc.TR[2] : J.pc.TR[3];
+  const int TS = i == 0 ? J.pc.TS[0] : i == 1 ? J.pc.TS[1] : i == 2 ? J.pc.TS[2] : J.pc.TS[3];
+  const int Kc = TR * TS * J.Co;
   uint16_t v[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int k = k0 + q;
-    v[q] = k < J.Co ? J.w[(int64_t)k * J.C + c] : (uint16_t)0;
+    uint16_t x = 0;
+    if (k < Kc) {
+      const int tap = k / J.Co, o = k - tap * J.Co;
+      const int jr = tap / TS, js = tap - jr * TS;
+      const int r = r0 + J.sh * jr, sx = s0 + J.sw * js;
+      x = J.w[(((int64_t)o * J.R + r) * J.S + sx) * J.C + c];
+    }
+    v[q] = x;
   }
-  *reinterpret_cast<uint4*>(J.out + (int64_t)c * J.kmax + k0) =
+  *reinterpret_cast<uint4*>(J.out + (int64_t)i * J.C * J.kmax + (int64_t)c * J.kmax + k0) =
       make_uint4((uint32_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)v[2] | ((uint32_t)v[3] << 16),
                  (uint32_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)v[6] | ((uint32_t)v[7] << 16));
 }
 
-void pack_t_multi(const uint16_t* const* w, uint16_t* const* out, const int* Co, const int* C,
-                  const int* kmax, int n, hipStream_t st) {
-  for (int b = 0; b < n; b += kMaxTJobs) {
-    TJobs jobs{};
-    jobs.n = n - b < kMaxTJobs ? n - b : kMaxTJobs;
+// prm: per job [Co, C, R, S, sh, sw, nclass, kmax, r0 x4, s0 x4, TR x4, TS x4] (24 ints)
+void pack_kc_multi(const uint16_t* const* w, uint16_t* const* out, const int* prm, int n,
+                   hipStream_t st) {
+  for (int b = 0; b < n; b += kMaxKcJobs) {
+    KcJobs jobs{};
+    jobs.n = n - b < kMaxKcJobs ? n - b : kMaxKcJobs;
     int64_t blocks = 0;
     for (int q = 0; q < jobs.n; ++q) {
-      const int i = b + q;
-      jobs.j[q] = TJob{w[i], out[i], Co[i], C[i], kmax[i], blocks};
-      blocks += ((int64_t)C[i] * (kmax[i] / 8) + 255) / 256;
+      const int* p = prm + 24 * (b + q);
+      KcJob J{};
+      J.w = w[b + q];
+      J.out = out[b + q];
+      J.Co = p[0]; J.C = p[1]; J.R = p[2]; J.S = p[3]; J.sh = p[4]; J.sw = p[5];
+      J.nclass = p[6]; J.kmax = p[7];
+      for (int i = 0; i < 4; ++i) {
+        J.pc.r0[i] = p[8 + i]; J.pc.s0[i] = p[12 + i]; J.pc.TR[i] = p[16 + i]; J.pc.TS[i] = p[20 + i];
+      }
+      J.blk_lo = blocks;
+      blocks += ((int64_t)J.nclass * J.C * (J.kmax / 8) + 255) / 256;
+      jobs.j[q] = J;
     }
-    hipLaunchKernelGGL(k_pack_t_multi, dim3((unsigned)blocks), dim3(256), 0, st, jobs);
+    hipLaunchKernelGGL(k_pack_kc_multi, dim3((unsigned)blocks), dim3(256), 0, st, jobs);
   }
 }
 

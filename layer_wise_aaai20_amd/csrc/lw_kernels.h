@@ -371,9 +371,9 @@ void xent(const float* logits, const int64_t* target, int B, int C, float gscale
 // unused) and db (+)= Σ_rows dym; rows [M][C] bf16, C % 8 == 0, C <= 2048; partial holds
 // relu_bias_bwd_blocks(M) * C floats
 int relu_bias_bwd_blocks(int64_t M, int C);
-// several 1x1 weight transposes Wᵀ (zero-padded rows of kmax) in one launch (conv.hip)
-void pack_t_multi(const uint16_t* const* w, uint16_t* const* out, const int* Co, const int* C,
-                  const int* kmax, int n, hipStream_t st);
+// several pack_dgrad_kc packs in one launch (conv.hip); prm: 24 ints per job
+void pack_kc_multi(const uint16_t* const* w, uint16_t* const* out, const int* prm, int n,
+                   hipStream_t st);
 // mean cross-entropy [mean, count] of k_xent's rows, and its backward grad · gl / n (nn.hip)
 void xent_mean(const float* rows, const int64_t* target, int B, int ignore_index, float* out,
                float* out_n, hipStream_t st);

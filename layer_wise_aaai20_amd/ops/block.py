@@ -52,7 +52,7 @@ import torch
 import torch.nn.functional as F
 
 from ._ext import h16, load, set_splitk_defer
-from .conv import conv_dgrad, conv_fwd, conv_wgrad
+from .conv import conv_dgrad, conv_fwd, conv_wgrad, kc_end_step, kc_new_step, kc_pack
 from .tuning import MF32, Tuner, with_mf32
 
 CL = torch.channels_last
@@ -185,43 +185,19 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
 
 LAYOUT_TUNER = Tuner("dgrad-layout", "LWAAAI_GEMM_TUNE")
 
-# 1x1 data-gradient weights in the K-contiguous layout (Wᵀ, gemm_dgrad "kc"): at a step's first
-# request every layer that asked last step is packed in one launch (csrc/conv.hip
-# k_pack_t_multi; ResNet-50 ran ~15 pack launches a step), a layer not seen before packs alone and
-# joins. The weights are the bf16 mirror's views (refreshed in place every step), so the list
-# stays valid; entries not asked for in a step are dropped. The gradient engine's begin_step
-# starts a new step (new_step). LWAAAI_KC_BATCH=0: one pack per request.
-KC_BATCH = os.environ.get("LWAAAI_KC_BATCH", "1") != "0"
-_KC = {"gen": -1, "reg": {}, "cache": {}, "used": set()}
-_STEP_GEN = [0]
-
-
+# 1x1 data-gradient weights in the K-contiguous layout (Wᵀ, gemm_dgrad "kc"): through the per-step
+# pack batch of ops/conv.py kc_pack (one k_pack_kc_multi launch for the step's packs).
 def new_step() -> None:
-    _STEP_GEN[0] += 1
+    kc_new_step()
+
+
+def end_step() -> None:
+    kc_end_step()
 
 
 def _kc_weight(W: torch.Tensor, K: int, N: int, kp: int, fresh: bool = False) -> torch.Tensor:
-    if fresh or not KC_BATCH or not W.is_cuda or not W.is_contiguous():
-        return load().pack_dgrad_kc(W.reshape(K, N, 1, 1), [0, 0, 1, 1], 1, 1, kp)
-    key = (W.data_ptr(), K, N, kp)
-    if _KC["gen"] != _STEP_GEN[0]:
-        _KC["gen"] = _STEP_GEN[0]
-        _KC["reg"] = {k: w for k, w in _KC["reg"].items() if k in _KC["used"]}
-        _KC["used"] = set()
-        _KC["cache"] = {}
-        reg = list(_KC["reg"].items())
-        if reg:
-            outs = [torch.empty(k[2] * k[3], dtype=w.dtype, device=w.device) for k, w in reg]
-            load().pack_t_multi([w for _, w in reg], outs, [k[3] for k, _ in reg])
-            _KC["cache"] = {k: o for (k, _), o in zip(reg, outs)}
-    _KC["used"].add(key)
-    hit = _KC["cache"].get(key)
-    if hit is not None:
-        return hit
-    out = load().pack_dgrad_kc(W.reshape(K, N, 1, 1), [0, 0, 1, 1], 1, 1, kp)
-    _KC["reg"][key] = W
-    _KC["cache"][key] = out
-    return out
+    return kc_pack(W.reshape(K, N, 1, 1), (0, 0, 1, 1), 1, 1, kp,
+                   fresh or not W.is_contiguous())
 
 
 def gemm_dgrad(dy, ldy, W, M, N, K, **kw):

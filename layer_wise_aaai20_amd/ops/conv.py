@@ -78,7 +78,62 @@ _TAP_PACK = os.environ.get("LWAAAI_TAP_PACK", "1") != "0"
 _NKC_PACK = os.environ.get("LWAAAI_NKC_PACK", "1") != "0"
 
 
-def tap_dgrad_weight(w: torch.Tensor) -> torch.Tensor:
+# K-contiguous data-gradient weight packs (csrc/conv.hip k_pack_dgrad_kc: 1x1 transposes Wᵀ, the
+# strided / 3x3 class slabs, the flipped 3x3 window) batched per step: at a step's first request
+# every pack asked for in the last step is made in one launch (k_pack_kc_multi; ResNet-50 ran ~15
+# pack launches a step), a pack not seen before runs alone and joins. The registry holds the weight
+# tensors (the bf16 mirror's views, refreshed in place every step, or bf16 parameters updated in
+# place), so a key's data pointer cannot be reused by another tensor while listed; entries not
+# asked for in a step are dropped. Only between the gradient engine's begin_step (kc_new_step)
+# and its finish (kc_end_step): a backward outside an engine step packs per request, as does
+# LWAAAI_KC_BATCH=0.
+KC_BATCH = os.environ.get("LWAAAI_KC_BATCH", "1") != "0"
+_KC = {"gen": -1, "armed": False, "reg": {}, "cache": {}, "used": set()}
+_STEP_GEN = [0]
+
+
+def kc_new_step() -> None:
+    _STEP_GEN[0] += 1
+    _KC["armed"] = True
+
+
+def kc_end_step() -> None:
+    _KC["armed"] = False
+
+
+def kc_pack(wb: torch.Tensor, cls, sh: int, sw: int, kmax: int, fresh: bool = False):
+    """``pack_dgrad_kc(wb, cls, sh, sw, kmax)`` through the per-step batch (``fresh``: a pack of
+    its own, e.g. timed by the tuner with its GEMM)."""
+    lib = load()
+    if fresh or not (KC_BATCH and _KC["armed"]) or not wb.is_cuda:
+        return lib.pack_dgrad_kc(wb, list(cls), sh, sw, kmax)
+    key = (wb.data_ptr(), tuple(wb.shape), tuple(cls), sh, sw, kmax)
+    if _KC["gen"] != _STEP_GEN[0]:
+        _KC["gen"] = _STEP_GEN[0]
+        _KC["reg"] = {k: w for k, w in _KC["reg"].items() if k in _KC["used"]}
+        _KC["used"] = set()
+        _KC["cache"] = {}
+        reg = list(_KC["reg"].items())
+        if reg:
+            outs, prm = [], []
+            for k, w in reg:
+                c4 = list(k[2]) + [0] * (16 - len(k[2]))
+                nc = len(k[2]) // 4
+                outs.append(torch.empty(nc * w.shape[1] * k[5], dtype=w.dtype, device=w.device))
+                prm += [k[3], k[4], k[5], nc] + c4[0::4] + c4[1::4] + c4[2::4] + c4[3::4]
+            lib.pack_kc_multi([w for _, w in reg], outs, prm)
+            _KC["cache"] = {k: o for (k, _), o in zip(reg, outs)}
+    _KC["used"].add(key)
+    hit = _KC["cache"].get(key)
+    if hit is not None:
+        return hit
+    out = lib.pack_dgrad_kc(wb, list(cls), sh, sw, kmax)
+    _KC["reg"][key] = wb
+    _KC["cache"][key] = out
+    return out
+
+
+def tap_dgrad_weight(w: torch.Tensor, fresh: bool = True) -> torch.Tensor:
     """The data gradient of a 3x3/1/1 conv as a forward conv of dy: W'[ci][r][s][co] =
     w[co][ci][2-r][2-s], K-contiguous [C][9 Co]."""
     co, c, R, S = w.shape
@@ -86,7 +141,7 @@ def tap_dgrad_weight(w: torch.Tensor) -> torch.Tensor:
     if (_TAP_PACK and wb.is_cuda and (R, S) == (3, 3) and co % 8 == 0 and
             wb.is_contiguous(memory_format=CL)):
         # one pack kernel walking the window backwards (was flip + two copies, ~15 µs a call)
-        return load().pack_dgrad_kc(wb, [2, 2, 3, 3], -1, -1, 9 * co).view(c, 9 * co)
+        return kc_pack(wb, [2, 2, 3, 3], -1, -1, 9 * co, fresh or wb is not w).view(c, 9 * co)
     return wb.flip(2, 3).permute(1, 2, 3, 0).reshape(c, -1).contiguous()
 
 
@@ -196,7 +251,7 @@ def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int) -> Tuple[torch
     return torch.cat(parts), offs
 
 
-def pack_dgrad_weight_kc(w: torch.Tensor, classes, sh: int, sw: int):
+def pack_dgrad_weight_kc(w: torch.Tensor, classes, sh: int, sw: int, fresh: bool = True):
     """K-contiguous per-class slabs Wk_c[ci][jr][js][co] = w[co, ci, r0 + sh*jr, s0 + sw*js]
     (the transpose of :func:`pack_dgrad_weight`'s slabs), each row padded to the largest class K
     so that one row stride serves every class; one launch (``csrc/conv.hip k_pack_dgrad_kc``).
@@ -208,7 +263,7 @@ def pack_dgrad_weight_kc(w: torch.Tensor, classes, sh: int, sw: int):
     for (_c, _w, r0, s0, TR, TS, *_x) in classes:
         cls += [r0, s0, TR, TS]
     wb = w.to(h16()).contiguous(memory_format=CL)
-    packed = load().pack_dgrad_kc(wb, cls, sh, sw, kmax)
+    packed = kc_pack(wb, cls, sh, sw, kmax, fresh or wb is not w)
     return packed, [i * c * kmax for i in range(len(classes))], kmax
 
 
@@ -315,18 +370,18 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
 
     bx, bm, bss, bb = bst if bst is not None else (None, None, None, None)
 
-    def run(cand, dst=None, add=None):
+    def run(cand, dst=None, add=None, fresh=True):
         layout, tile = cand
         if layout in ("direct", "tap") and (dst is not None or add is not None):
             layout, tile = "kc", 2            # the direct kernels write a fresh tensor only
         if layout == "direct":        # conv of dy with W'[ci][r][s][co] = w[co][ci][2-r][2-s]
-            ys, _ = lib.conv3_direct(dyc, tap_dgrad_weight(w), False)
+            ys, _ = lib.conv3_direct(dyc, tap_dgrad_weight(w, fresh), False)
             return ys.permute(0, 2, 3, 1).reshape(-1, c), None
         if layout == "tap":           # (the flip + transpose pack is timed with the conv)
-            ys, _ = lib.conv3_tap(dyc, tap_dgrad_weight(w), c, False)
+            ys, _ = lib.conv3_tap(dyc, tap_dgrad_weight(w, fresh), c, False)
             return ys.permute(0, 2, 3, 1).reshape(-1, c), None
-        if layout == "kc":            # packed per call: the tuner times the pack with the conv
-            wk, koffs, kmax = pack_dgrad_weight_kc(w, classes, sh, sw)
+        if layout == "kc":            # (the tuner times a pack of its own with the conv)
+            wk, koffs, kmax = pack_dgrad_weight_kc(w, classes, sh, sw, fresh)
             g = list(geom)
             for i, off in enumerate(koffs):
                 g[13 + 10 * i + 9] = off
@@ -349,7 +404,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
             _conv3_tap_fits(co, c, R, S, sh, sw, ph, pw, Ho, Wo) and (H, W) == (Ho, Wo)):
         cands.append(("tap", CONV3_TAP))
     cand = TUNER.pick(key, run, cands, ("nkc", _row_default(M, c)))   # (timed on scratch outputs)
-    dx, st = run(cand, out, addend)
+    dx, st = run(cand, out, addend, False)
     if bst is not None:
         return _nchw_rows(dx, Nb, H, W), st
     return _nchw_rows(dx, Nb, H, W)

@@ -494,7 +494,7 @@ class GradSyncEngine:
             self.arena.zero_except(self._no_zero)
         if self.device.type == "cuda":
             from ..ops import block as _block
-            _block.new_step()            # (per-step caches of the fused blocks: _kc_weight)
+            _block.new_step()            # (per-step weight-pack batch: ops/conv.py kc_pack)
         if not self.arena.grads_attached():
             self.arena.attach_grads()
         if self.lr_scaled:
@@ -646,6 +646,9 @@ class GradSyncEngine:
         """Launch buckets that never became ready (unused params keep zero grads), wait for every
         collective and decode into the arena."""
         self._flush_splitk()
+        if self.device.type == "cuda":
+            from ..ops import block as _block
+            _block.end_step()
         for i in self._no_zero:
             if self._claims[i] == 0:     # (not zeroed by begin_step and not written this step)
                 self.arena.grad_view(self.arena.segments[i]).zero_()

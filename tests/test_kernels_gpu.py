@@ -295,16 +295,70 @@ def test_relu_bias_bwd_matches_torch(M, C):
     assert torch.allclose(acc, exp + 1, rtol=1e-5, atol=1e-3)
 
 
-def test_pack_t_multi_matches_single_packs():
-    """csrc/conv.hip k_pack_t_multi (several 1x1 Wᵀ packs in one launch, ops/block.py
-    _kc_weight) against one pack_dgrad_kc per weight, bit for bit (zero-padded rows)."""
-    from layer_wise_aaai20_amd.ops._ext import h16, load
+def _kc_jobs():
+    """(weight, cls, sh, sw, kmax) of every pack_dgrad_kc form a step asks for: 1x1 Wᵀ, a 3x3/1
+    slab, the four parity classes of a 3x3/2 and of a strided 1x1, the flipped 3x3 window."""
+    from layer_wise_aaai20_amd.ops import conv as CV
+    from layer_wise_aaai20_amd.ops._ext import h16
     torch.manual_seed(0)
-    shapes = [(256, 64), (64, 256), (1000, 512), (2048, 1024), (24, 40)]
-    ws = [torch.randn(k, n, device="cuda").to(h16()) for k, n in shapes]
-    kps = [-(-k // 8) * 8 for k, _ in shapes]
-    outs = [torch.empty(n * kp, dtype=h16(), device="cuda") for (_, n), kp in zip(shapes, kps)]
-    load().pack_t_multi(ws, outs, kps)
-    for w, o, (k, n), kp in zip(ws, outs, shapes, kps):
-        ref = load().pack_dgrad_kc(w.reshape(k, n, 1, 1), [0, 0, 1, 1], 1, 1, kp)
-        assert torch.equal(o, ref)
+    CL = torch.channels_last
+    jobs = []
+    for k, n in [(256, 64), (64, 256), (1000, 512), (24, 40)]:
+        w = torch.randn(k, n, device="cuda").to(h16())
+        jobs.append((w.reshape(k, n, 1, 1), [0, 0, 1, 1], 1, 1, -(-k // 8) * 8))
+    for co, c, R, st, pad, hw in [(64, 64, 3, 1, 1, 56), (128, 64, 3, 2, 1, 56),
+                                  (256, 128, 1, 2, 0, 28)]:
+        w = torch.randn(co, c, R, R, device="cuda").to(h16()).contiguous(memory_format=CL)
+        classes = CV._dgrad_classes(hw, hw, R, R, st, st, pad, pad)
+        cls = []
+        for (_c, _w, r0, s0, TR, TS, *_x) in classes:
+            cls += [r0, s0, TR, TS]
+        kmax = -(-max(TR * TS * co for (_c, _w, _r, _s, TR, TS, *_x) in classes) // 8) * 8
+        jobs.append((w, cls, st, st, kmax))
+        if R == 3 and st == 1:
+            jobs.append((w, [2, 2, 3, 3], -1, -1, 9 * co))
+    return jobs
+
+
+def test_pack_kc_multi_matches_single_packs():
+    """csrc/conv.hip k_pack_kc_multi (a step's data-gradient weight packs in one launch,
+    ops/conv.py kc_pack) against one pack_dgrad_kc per weight, bit for bit (zero-padded rows)."""
+    from layer_wise_aaai20_amd.ops._ext import load
+    jobs = _kc_jobs()
+    outs, prm = [], []
+    for w, cls, sh, sw, kmax in jobs:
+        nc = len(cls) // 4
+        c4 = cls + [0] * (16 - len(cls))
+        outs.append(torch.empty(nc * w.shape[1] * kmax, dtype=w.dtype, device="cuda"))
+        prm += [sh, sw, kmax, nc] + c4[0::4] + c4[1::4] + c4[2::4] + c4[3::4]
+    load().pack_kc_multi([j[0] for j in jobs], outs, prm)
+    for (w, cls, sh, sw, kmax), o in zip(jobs, outs):
+        assert torch.equal(o, load().pack_dgrad_kc(w, cls, sh, sw, kmax))
+
+
+def test_kc_pack_step_batch_follows_weight_updates():
+    """ops/conv.py kc_pack: within engine steps the second step's packs come from the batched
+    launch and equal fresh packs of the weights as updated in place between the steps; outside
+    a step (kc_end_step) every request packs afresh."""
+    from layer_wise_aaai20_amd.ops import conv as CV
+    from layer_wise_aaai20_amd.ops._ext import load
+    jobs = _kc_jobs()
+    try:
+        for step in range(3):
+            CV.kc_new_step()
+            for w, cls, sh, sw, kmax in jobs:
+                got = CV.kc_pack(w, cls, sh, sw, kmax)
+                assert torch.equal(got, load().pack_dgrad_kc(w, cls, sh, sw, kmax)), step
+            if step >= 1:
+                assert len(CV._KC["reg"]) == len(jobs)
+            CV.kc_end_step()
+            for w, *_ in jobs:
+                w.mul_(0.5).add_(0.25)      # the optimizer's in-place update
+        w, cls, sh, sw, kmax = jobs[0]
+        before = dict(CV._KC["cache"])
+        CV.kc_pack(w, cls, sh, sw, kmax)
+        assert CV._KC["cache"].keys() == before.keys() and \
+            all(CV._KC["cache"][k] is v for k, v in before.items())   # unarmed: untouched
+    finally:
+        CV.kc_end_step()
+        CV._KC.update(reg={}, cache={}, used=set())

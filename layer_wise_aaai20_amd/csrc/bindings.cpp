@@ -1196,7 +1196,7 @@ Tensor gemm(Tensor A, int64_t lda, bool a_kcontig, Tensor B, int64_t ldb, bool b
 // pack_dgrad_kc of several weights in one launch: w[i] (channels_last [Co][C][R][S] memory, or a
 // contiguous [Co][C] for a 1x1) into out[i] ([nclass][C][kmax]); prm: 20 ints per job —
 // [sh, sw, kmax, nclass, r0 x4, s0 x4, TR x4, TS x4] as pack_dgrad_kc's arguments (padded to 4
-// classes)
+// classes); kmax = 0 packs pack_dgrad_nkc's [K][C] slabs instead
 void pack_kc_multi(std::vector<Tensor> w, std::vector<Tensor> out, std::vector<int64_t> prm) {
   TORCH_CHECK(w.size() == out.size() && prm.size() == 20 * w.size(), "pack_kc_multi: list sizes");
   if (w.empty()) return;
@@ -1217,16 +1217,22 @@ void pack_kc_multi(std::vector<Tensor> w, std::vector<Tensor> out, std::vector<i
     const int Co = (int)w[i].size(0), C = (int)w[i].size(1), R = (int)w[i].size(2),
               S = (int)w[i].size(3);
     const int sh = (int)q[0], sw = (int)q[1], kmax = (int)q[2], nclass = (int)q[3];
-    TORCH_CHECK(nclass >= 1 && nclass <= 4 && kmax % 8 == 0 && (sh >= 1 || sh == -1) &&
-                (sw >= 1 || sw == -1) && out[i].numel() == (int64_t)nclass * C * kmax,
-                "pack_kc_multi: classes / kmax / out size");
+    // kmax == 0: the [K][C] form (pack_dgrad_nkc: positive strides, C % 8, 16-byte loads)
+    const bool nkc = kmax == 0;
+    TORCH_CHECK(nclass >= 1 && nclass <= 4 && kmax >= 0 && kmax % 8 == 0 &&
+                (sh >= 1 || (sh == -1 && !nkc)) && (sw >= 1 || (sw == -1 && !nkc)) &&
+                (!nkc || C % 8 == 0), "pack_kc_multi: classes / kmax / strides");
+    int64_t total = 0;
     for (int k = 0; k < nclass; ++k) {
       const int64_t r0 = q[4 + k], s0 = q[8 + k], TR = q[12 + k], TS = q[16 + k];
       const int64_t rl = r0 + sh * (TR - 1), sl = s0 + sw * (TS - 1);
       TORCH_CHECK(r0 >= 0 && s0 >= 0 && TR >= 1 && TS >= 1 && r0 < R && s0 < S && rl >= 0 &&
-                  rl < R && sl >= 0 && sl < S && TR * TS * Co <= kmax,
+                  rl < R && sl >= 0 && sl < S && (nkc || TR * TS * Co <= kmax),
                   "pack_kc_multi: class taps outside the kernel window");
+      total += nkc ? TR * TS * Co * C : (int64_t)C * kmax;
     }
+    TORCH_CHECK(out[i].numel() == total, "pack_kc_multi: out size");
+    if (nkc) check_aligned16(w[i].data_ptr(), "weight");
     check_aligned16(out[i].data_ptr(), "out");
     wp.push_back(ptr<uint16_t>(w[i]));
     op.push_back(ptr<uint16_t>(out[i]));

@@ -69,9 +69,10 @@ __global__ __launch_bounds__(256) void k_pack_dgrad_kc(const uint16_t* __restric
   }
 }
 
-// Several pack_dgrad_kc packs in one launch (ops/conv.py kc_pack_step: the K-contiguous
-// data-gradient weights of a step — 1x1 transposes and strided / 3x3 class slabs — packed once
-// per step at the first request instead of one launch each). Per job the body of k_pack_dgrad_kc.
+// Several data-gradient weight packs in one launch (ops/conv.py kc_pack: the packed weights of a
+// step — 1x1 transposes, strided / 3x3 class slabs, flipped 3x3 windows, [K][C] slabs — made once
+// per step at the first request instead of one launch each). Per job the body of k_pack_dgrad_kc,
+// or of k_pack_dgrad_nkc for kmax == 0.
 struct KcJob {
   const uint16_t* w;
   uint16_t* out;
@@ -90,8 +91,34 @@ __global__ __launch_bounds__(256) void k_pack_kc_multi(const KcJobs jobs) {
   for (int q = 1; q < jobs.n; ++q)
     if ((int64_t)blockIdx.x >= jobs.j[q].blk_lo) ji = q;
   const KcJob& J = jobs.j[ji];
+  int64_t t = ((int64_t)blockIdx.x - J.blk_lo) * 256 + threadIdx.x;
+  if (J.kmax == 0) {                 // the [K][C] form: k_pack_dgrad_nkc's body, 16-byte chunks
+    const int C8 = J.C / 8;
+    int64_t base = 0;
+    for (int i = 0; i < J.nclass; ++i) {
+      const int r0 = i == 0 ? J.pc.r0[0] : i == 1 ? J.pc.r0[1] : i == 2 ? J.pc.r0[2] : J.pc.r0[3];
+      const int s0 = i == 0 ? J.pc.s0[0] : i == 1 ? J.pc.s0[1] : i == 2 ? J.pc.s0[2] : J.pc.s0[3];
+      const int TR = i == 0 ? J.pc.TR[0] : i == 1 ? J.pc.TR[1] : i == 2 ? J.pc.TR[2] : J.pc.TR[3];
+      const int TS = i == 0 ? J.pc.TS[0] : i == 1 ? J.pc.TS[1] : i == 2 ? J.pc.TS[2] : J.pc.TS[3];
+      const int64_t n = (int64_t)TR * TS * J.Co * C8;
+      if (t < n) {
+        const int cg = (int)(t % C8);
+        const int64_t row = t / C8;                      // (jr, js, co)
+        const int o = (int)(row % J.Co);
+        const int tap = (int)(row / J.Co);
+        const int jr = tap / TS, js = tap - jr * TS;
+        const int r = r0 + J.sh * jr, sx = s0 + J.sw * js;
+        const uint4 v = *reinterpret_cast<const uint4*>(
+            J.w + (((int64_t)o * J.R + r) * J.S + sx) * J.C + cg * 8);
+        *reinterpret_cast<uint4*>(J.out + base + row * J.C + cg * 8) = v;
+        return;
+      }
+      t -= n;
+      base += (int64_t)TR * TS * J.Co * J.C;
+    }
+    return;
+  }
   const int64_t per_row = J.kmax / 8, per_class = (int64_t)J.C * per_row;
-  const int64_t t = ((int64_t)blockIdx.x - J.blk_lo) * 256 + threadIdx.x;
   if (t >= J.nclass * per_class) return;
   const int i = (int)(t / per_class);
   const int64_t rem = t - i * per_class;
@@ -138,7 +165,13 @@ void pack_kc_multi(const uint16_t* const* w, uint16_t* const* out, const int* pr
         J.pc.r0[i] = p[8 + i]; J.pc.s0[i] = p[12 + i]; J.pc.TR[i] = p[16 + i]; J.pc.TS[i] = p[20 + i];
       }
       J.blk_lo = blocks;
-      blocks += ((int64_t)J.nclass * J.C * (J.kmax / 8) + 255) / 256;
+      int64_t chunks = (int64_t)J.nclass * J.C * (J.kmax / 8);
+      if (J.kmax == 0) {
+        chunks = 0;
+        for (int i = 0; i < J.nclass; ++i)
+          chunks += (int64_t)J.pc.TR[i] * J.pc.TS[i] * J.Co * (J.C / 8);
+      }
+      blocks += (chunks + 255) / 256;
       jobs.j[q] = J;
     }
     hipLaunchKernelGGL(k_pack_kc_multi, dim3((unsigned)blocks), dim3(256), 0, st, jobs);

@@ -101,16 +101,25 @@ def kc_end_step() -> None:
     _KC["armed"] = False
 
 
+def _pack1(lib, wb, cls, sh, sw, kmax):
+    if kmax == 0:
+        return lib.pack_dgrad_nkc(wb, list(cls), sh, sw)
+    return lib.pack_dgrad_kc(wb, list(cls), sh, sw, kmax)
+
+
 def kc_pack(wb: torch.Tensor, cls, sh: int, sw: int, kmax: int, fresh: bool = False):
-    """``pack_dgrad_kc(wb, cls, sh, sw, kmax)`` through the per-step batch (``fresh``: a pack of
-    its own, e.g. timed by the tuner with its GEMM)."""
+    """``pack_dgrad_kc(wb, cls, sh, sw, kmax)`` — or ``pack_dgrad_nkc(wb, cls, sh, sw)`` for
+    ``kmax == 0`` — through the per-step batch (``fresh``: a pack of its own, e.g. timed by the
+    tuner with its GEMM)."""
     lib = load()
     if fresh or not (KC_BATCH and _KC["armed"]) or not wb.is_cuda:
-        return lib.pack_dgrad_kc(wb, list(cls), sh, sw, kmax)
+        return _pack1(lib, wb, cls, sh, sw, kmax)
     key = (wb.data_ptr(), tuple(wb.shape), tuple(cls), sh, sw, kmax)
     if _KC["gen"] != _STEP_GEN[0]:
         _KC["gen"] = _STEP_GEN[0]
-        _KC["reg"] = {k: w for k, w in _KC["reg"].items() if k in _KC["used"]}
+        # (a model of the other precision's build, or on another device, may have filled it)
+        _KC["reg"] = {k: w for k, w in _KC["reg"].items()
+                      if k in _KC["used"] and w.dtype == wb.dtype and w.device == wb.device}
         _KC["used"] = set()
         _KC["cache"] = {}
         reg = list(_KC["reg"].items())
@@ -119,7 +128,9 @@ def kc_pack(wb: torch.Tensor, cls, sh: int, sw: int, kmax: int, fresh: bool = Fa
             for k, w in reg:
                 c4 = list(k[2]) + [0] * (16 - len(k[2]))
                 nc = len(k[2]) // 4
-                outs.append(torch.empty(nc * w.shape[1] * k[5], dtype=w.dtype, device=w.device))
+                n = (nc * w.shape[1] * k[5] if k[5] else
+                     sum(c4[4 * i + 2] * c4[4 * i + 3] for i in range(nc)) * w.shape[0] * w.shape[1])
+                outs.append(torch.empty(n, dtype=w.dtype, device=w.device))
                 prm += [k[3], k[4], k[5], nc] + c4[0::4] + c4[1::4] + c4[2::4] + c4[3::4]
             lib.pack_kc_multi([w for _, w in reg], outs, prm)
             _KC["cache"] = {k: o for (k, _), o in zip(reg, outs)}
@@ -127,7 +138,7 @@ def kc_pack(wb: torch.Tensor, cls, sh: int, sw: int, kmax: int, fresh: bool = Fa
     hit = _KC["cache"].get(key)
     if hit is not None:
         return hit
-    out = lib.pack_dgrad_kc(wb, list(cls), sh, sw, kmax)
+    out = _pack1(lib, wb, cls, sh, sw, kmax)
     _KC["reg"][key] = wb
     _KC["cache"][key] = out
     return out
@@ -225,7 +236,8 @@ def _dgrad_classes(H, W, R, S, sh, sw, ph, pw):
     return out
 
 
-def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int) -> Tuple[torch.Tensor, List[int]]:
+def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int,
+                      fresh: bool = True) -> Tuple[torch.Tensor, List[int]]:
     """Per-class slabs Wt_c[jr][js][co][ci] = w[co, ci, r0 + sh*jr, s0 + sw*js], concatenated:
     one pack launch (``csrc/conv.hip k_pack_dgrad_nkc``) for a channels_last GPU weight, else the
     permute / slice / cat form (the reference implementation of the same layout)."""
@@ -238,7 +250,7 @@ def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int) -> Tuple[torch
             cls += [r0, s0, TR, TS]
             offs.append(off)
             off += TR * TS * co * c
-        return load().pack_dgrad_nkc(wb, cls, sh, sw), offs
+        return kc_pack(wb, cls, sh, sw, 0, fresh or wb is not w), offs
     wt = wb.permute(2, 3, 0, 1)                               # [R, S, Co, C]
     if len(classes) == 1 and classes[0][4] == R and classes[0][5] == S:
         return wt.contiguous().view(-1), [0]
@@ -359,9 +371,9 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
             o += TR * TS * co * c
     nkc_pack = [wpack[0] if wpack is not None else None]
 
-    def nkc_weight():
+    def nkc_weight(fresh):
         if nkc_pack[0] is None:
-            nkc_pack[0] = pack_dgrad_weight(w, classes, sh, sw)[0]
+            nkc_pack[0] = pack_dgrad_weight(w, classes, sh, sw, fresh)[0]
         return nkc_pack[0]
     geom = [Nb, Ho, Wo, co, 1, 1, -1, -1, H, W, sh, sw, len(classes)]
     for (ch, cw, r0, s0, TR, TS, Hg, Wg, oh, ow), off in zip(classes, offs):
@@ -387,7 +399,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
                 g[13 + 10 * i + 9] = off
             return lib.conv_ex(dyc, wk, CV_A, g, c, tile, 1, True, None, None, False, dst, False,
                                0, True, kmax, add)
-        return lib.conv_ex(dyc, nkc_weight(), CV_A, geom, c, tile, 1, True, None, None,
+        return lib.conv_ex(dyc, nkc_weight(fresh), CV_A, geom, c, tile, 1, True, None, None,
                            bst is not None, dst, False, 0, False, c, add, bx, bm, bss, bb)
     key = ("d", tuple(dyc.shape), tuple(w.shape), H, W, sh, sw, ph, pw, addend is not None,
            bst is not None)

@@ -18,6 +18,8 @@ def free_port():
 
 
 def _worker(rank, world, port, fn, outdir, args, env):
+    import datetime
+
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), **env)
@@ -35,7 +37,10 @@ def _worker(rank, world, port, fn, outdir, args, env):
     try:
         from layer_wise_aaai20_amd.parallel.comm import bind_rank_device
         dev = bind_rank_device(rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        # every rank a client of the parent's store (run_world): no rank binds the port itself
+        store = dist.TCPStore("127.0.0.1", port, world, is_master=False,
+                              timeout=datetime.timedelta(seconds=120))
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev, store=store)
         res = ("ok", fn(rank, world, dev, *args))
         faulthandler.cancel_dump_traceback_later()
     except Exception:  # noqa: BLE001
@@ -60,22 +65,43 @@ def run_world(fn, world, args=(), env=None):
     ``LWAAAI_TEST_WORLD_TIMEOUT`` seconds (default 150; each rank prints every thread's stack at
     ``LWAAAI_TEST_STACK_AFTER``, 90 s) is killed — its own child processes, by PID — and the test
     fails, so a rank stuck in a collective cannot stall the rest of the suite."""
+    import datetime
     import time
-    port = free_port()
+
+    import torch.distributed as dist
     limit = float(os.environ.get("LWAAAI_TEST_WORLD_TIMEOUT", "150"))
+    # the rendezvous store lives here, on a port the OS picked and this process holds, so no rank
+    # races another program for a port found free a moment earlier (a rank then waited in
+    # _create_c10d_store until the deadline)
+    store = dist.TCPStore("127.0.0.1", 0, world, is_master=True, wait_for_workers=False,
+                          timeout=datetime.timedelta(seconds=limit))
+    port = store.port
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.start_processes(_worker, args=(world, port, fn, d, args, dict(env or {})),
                                  nprocs=world, start_method="spawn", join=False)
         t0 = time.monotonic()
+
+        def stop(msg):
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.kill()
+            for p in ctx.processes:
+                p.join(10)
+            raise AssertionError(msg)
         while not ctx.join(timeout=5):
+            for r in range(world):           # a rank that failed: its peers would wait for it
+                f = os.path.join(d, f"r{r}.pkl")
+                if os.path.exists(f) and os.path.getsize(f) > 0:
+                    try:
+                        with open(f, "rb") as fh:
+                            status, val = pickle.load(fh)   # written by _worker above
+                    except Exception:  # noqa: BLE001  (still being written)
+                        continue
+                    if status != "ok":
+                        stop(f"rank {r} failed:\n{val}")
             if time.monotonic() - t0 > limit:
-                for p in ctx.processes:
-                    if p.is_alive():
-                        p.kill()
-                for p in ctx.processes:
-                    p.join(10)
-                raise AssertionError(f"the {world} ranks did not finish within {limit:.0f} s "
-                                     "(their stacks are in the captured stderr)")
+                stop(f"the {world} ranks did not finish within {limit:.0f} s "
+                     "(their stacks are in the captured stderr)")
         out = []
         for r in range(world):
             with open(os.path.join(d, f"r{r}.pkl"), "rb") as f:
@@ -83,6 +109,7 @@ def run_world(fn, world, args=(), env=None):
             if status != "ok":
                 raise AssertionError(f"rank {r} failed:\n{val}")
             out.append(val)
+    del store
     return out
 
 

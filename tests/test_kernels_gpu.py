@@ -315,6 +315,7 @@ def _kc_jobs():
             cls += [r0, s0, TR, TS]
         kmax = -(-max(TR * TS * co for (_c, _w, _r, _s, TR, TS, *_x) in classes) // 8) * 8
         jobs.append((w, cls, st, st, kmax))
+        jobs.append((w, cls, st, st, 0))            # the [K][C] slabs (pack_dgrad_nkc)
         if R == 3 and st == 1:
             jobs.append((w, [2, 2, 3, 3], -1, -1, 9 * co))
     return jobs
@@ -323,17 +324,20 @@ def _kc_jobs():
 def test_pack_kc_multi_matches_single_packs():
     """csrc/conv.hip k_pack_kc_multi (a step's data-gradient weight packs in one launch,
     ops/conv.py kc_pack) against one pack_dgrad_kc per weight, bit for bit (zero-padded rows)."""
+    from layer_wise_aaai20_amd.ops import conv as CV
     from layer_wise_aaai20_amd.ops._ext import load
     jobs = _kc_jobs()
     outs, prm = [], []
     for w, cls, sh, sw, kmax in jobs:
         nc = len(cls) // 4
         c4 = cls + [0] * (16 - len(cls))
-        outs.append(torch.empty(nc * w.shape[1] * kmax, dtype=w.dtype, device="cuda"))
+        n = (nc * w.shape[1] * kmax if kmax else
+             sum(cls[4 * i + 2] * cls[4 * i + 3] for i in range(nc)) * w.shape[0] * w.shape[1])
+        outs.append(torch.empty(n, dtype=w.dtype, device="cuda"))
         prm += [sh, sw, kmax, nc] + c4[0::4] + c4[1::4] + c4[2::4] + c4[3::4]
     load().pack_kc_multi([j[0] for j in jobs], outs, prm)
     for (w, cls, sh, sw, kmax), o in zip(jobs, outs):
-        assert torch.equal(o, load().pack_dgrad_kc(w, cls, sh, sw, kmax))
+        assert torch.equal(o, CV._pack1(load(), w, cls, sh, sw, kmax))
 
 
 def test_kc_pack_step_batch_follows_weight_updates():
@@ -348,7 +352,7 @@ def test_kc_pack_step_batch_follows_weight_updates():
             CV.kc_new_step()
             for w, cls, sh, sw, kmax in jobs:
                 got = CV.kc_pack(w, cls, sh, sw, kmax)
-                assert torch.equal(got, load().pack_dgrad_kc(w, cls, sh, sw, kmax)), step
+                assert torch.equal(got, CV._pack1(load(), w, cls, sh, sw, kmax)), step
             if step >= 1:
                 assert len(CV._KC["reg"]) == len(jobs)
             CV.kc_end_step()

@@ -91,6 +91,12 @@ def parse():
                          "decode and captured side-stream branch for W ranks, loopback "
                          "communicator with replayed peer payloads) and print one JSON line per "
                          "configuration instead of the benchmark line")
+    ap.add_argument("--sim-wire", action="store_true",
+                    help="with --simulate-world: every collective also pays its modelled xGMI "
+                         "transfer time as a busy kernel (parallel/loopback.py WireModel)")
+    ap.add_argument("--sim-overlap", default="auto", choices=["auto", "0", "1", "comm"],
+                    help="with --simulate-world: the captured step's exchange placement "
+                         "(parallel/engine.py set_graph_overlap)")
     ap.add_argument("--sim-all", action="store_true",
                     help="with --simulate-world: the ResNet-50 BASELINE configs (layer-wise "
                          "Top-K 0.1 %%, entire-model QSGD 8-bit) instead of the given method")
@@ -187,7 +193,8 @@ def simulate(args) -> None:
         line = simulate_imagenet(args.simulate_world, dev, steps=args.steps,
                                  warmup=max(3, args.warmup), model=args.model,
                                  batch=args.batch, image_size=args.image_size, dtype=args.dtype,
-                                 bucket_mb=args.bucket_mb, **c)
+                                 bucket_mb=args.bucket_mb, sim_wire=args.sim_wire,
+                                 overlap=args.sim_overlap, **c)
         line["data"] = "synthetic (random uint8 images, random-init weights)"
         print(json.dumps(line), flush=True)
         if args.json_out:

@@ -83,6 +83,9 @@ def main():
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="time a world of W ranks on this one GPU (train/simworld.py) and print "
                          "one JSON line per configuration (exposed compression / exchange tail)")
+    ap.add_argument("--sim-wire", action="store_true",
+                    help="with --simulate-world: collectives pay their modelled xGMI time")
+    ap.add_argument("--sim-overlap", default="auto", choices=["auto", "0", "1", "comm"])
     args = ap.parse_args()
     if args.simulate_world > 1:
         from layer_wise_aaai20_amd.train.simworld import simulate_cifar
@@ -91,7 +94,8 @@ def main():
         names = [n for n in CONFIGS if n != "anchor"] if args.config == "all" else [args.config]
         for n in names:
             print(json.dumps(simulate_cifar(args.simulate_world, dev, n, CONFIGS[n], args.steps,
-                                            args.warmup)), flush=True)
+                                            args.warmup, sim_wire=args.sim_wire,
+                                            overlap=args.sim_overlap)), flush=True)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -14,6 +14,8 @@ RandkCodec         all_reduce      index-free values: shared-seed Philox masks (
 TernGradCodec      all_gather      one fp32 scale per layer + 2-bit codes
 QSGDCodec          all_gather      one fp32 norm per layer + int8 / 8+1 / int16-bit levels
 DenseWrap(inner)   all_reduce      reference wire format: dense compressed vector (parity mode)
+QuantRSCodec(q)    quant_rs        quantised reduce-scatter: all-to-all of each rank's codes for
+                                   shard r to rank r, shard dequant-sum, bf16 all-gather
 =================  ==============  ===========================================================
 
 GPU tensors run the HIP kernels (``csrc/compress.hip``); CPU tensors run the torch code below,
@@ -821,6 +823,187 @@ class DenseWrap(Codec):
             grad.div_(float(w))
 
 
+# ================================================================================= quantised RS
+class QuantRSCodec(Codec):
+    """Quantised reduce-scatter wire for TernGrad / QSGD at world > 1 (SURVEY.md §2.4
+    "Quantisers"; the reference all-reduces the dequantised dense vector, ``CIFAR10/core.py:207-225``).
+
+    Quantised codes do not sum, so the all-gather wire brings every rank all W code vectors —
+    ``(W-1)·b·n`` bytes in for ``b`` bytes of code per element — and the parity wire all-reduces
+    fp32 (``2(W-1)/W·4n``). Here each rank quantises its whole bucket exactly as the all-gather
+    codec does (same Philox streams, same error-feedback residual), then:
+
+    1. **all-to-all of codes** (grouped ``ncclSend``/``ncclRecv``, ``csrc/rccl.cpp``): rank ``q``
+       receives, from every rank, only the code records of ITS shard of the bucket's 32-element
+       groups plus the per-segment scale header — ``(W-1)/W·b·n`` bytes;
+    2. **shard dequant-sum** (``csrc/compress.hip k_dequant_shard``): the rank-ordered mean over the
+       W pieces — the all-gather decode's arithmetic, bit for bit — rounded once to bf16 into a
+       bucket image;
+    3. **bf16 all-gather of the shards** (grouped send/recv, shard sizes differ by at most one
+       group plus alignment gaps) — ``(W-1)/W·2n`` bytes — and one expand into the fp32 gradient.
+
+    QSGD-255 at world 8 moves ``(7/8)·(1.13 + 2) ≈ 2.7`` B/element instead of 7 (fp32
+    all-reduce) or 7.9 (code all-gather). The result is the mean over ranks of each rank's
+    dequantised vector rounded to bf16 — identical on every rank (every rank, the shard owner
+    included, keeps the rounded value). ``wire="auto"`` takes it when it moves the fewest bytes;
+    ``wire="qrs"`` forces it."""
+    collective = "quant_rs"
+
+    def __init__(self, inner: "_QuantCodec"):
+        super().__init__(inner.plan, inner.world, inner.rank, inner.seed, inner.error_feedback)
+        self.inner = inner
+        self.uses_step = inner.uses_step
+        self.name = f"qrs({inner.name})"
+        plan, W = inner.plan, self.world
+        self.q = inner.q
+        self.RL = {Q_TERN: 2, Q_QS8: 8, Q_QS9: 8, Q_QS16: 16}[inner.q]
+        self.signs = inner.q == Q_QS9
+        self.hdr = inner.hdr
+        self.Gtot = inner.Gtot
+        G = plan.groups().astype(np.int64)
+        seg = np.repeat(np.arange(plan.S, dtype=np.int64), G)
+        j = np.arange(self.Gtot, dtype=np.int64) - inner.rec_off[seg]
+        off = plan.offsets[seg] + GROUP * j
+        nval = np.minimum(GROUP, plan.sizes[seg] - GROUP * j)
+        self.gtab = np.stack([seg, off, nval, np.zeros_like(seg)], 1).astype(np.int32)
+        self.n = int(plan.numel)
+        self.g_lo = [r * self.Gtot // W for r in range(W + 1)]
+        self.A = [int(off[g]) if g < self.Gtot else self.n for g in self.g_lo[:-1]] + [self.n]
+        per = self.RL + (1 if self.signs else 0)
+        self.wpr = [(self.hdr + (self.g_lo[r + 1] - self.g_lo[r]) * per + 3) // 4 * 4
+                    for r in range(W)]
+        r = self.rank
+        sent = sum(self.hdr + (self.g_lo[p + 1] - self.g_lo[p]) * per for p in range(W) if p != r)
+        self.wire_bytes = 4 * sent + 2 * (W - 1) * (self.A[r + 1] - self.A[r])
+        self._bufs = {}
+        self._last_send = None
+
+    @property
+    def graph_safe(self) -> bool:
+        return bool(self.inner.graph_safe)
+
+    def can_stage(self) -> bool:
+        return self.inner.can_stage()
+
+    def stage(self, grad, ef, step, t_lo, t_hi, first):
+        return self.inner.stage(grad, ef, step, t_lo, t_hi, first)
+
+    def _buf(self, key, device, n, dtype):
+        k = (key, str(device))
+        b = self._bufs.get(k)
+        if b is None:
+            b = torch.zeros(n, dtype=dtype, device=device)
+            self._bufs[k] = b
+        return b
+
+    def gtab_dev(self, device) -> torch.Tensor:
+        return self.plan.dev(torch.device(device), "qrs_gtab", lambda: torch.from_numpy(self.gtab))
+
+    def compress(self, grad, ef, step):
+        self.inner._staged = self._staged
+        try:
+            out = self.inner.compress(grad, ef, step)
+        finally:
+            self.inner._staged = False
+        self.last_payload_bytes = self.wire_bytes
+        return out
+
+    # ---- phase 1: code pieces
+    def pieces(self, payload: torch.Tensor, dest: int):
+        """The records of shard ``dest`` in a full payload: header, level words, (QS9) sign words."""
+        h, g0, g1 = self.hdr, self.g_lo[dest], self.g_lo[dest + 1]
+        out = [payload[:h], payload[h + g0 * self.RL:h + g1 * self.RL]]
+        if self.signs:
+            s0 = h + self.Gtot * 8
+            out.append(payload[s0 + g0:s0 + g1])
+        return out
+
+    def piece_slots(self, row: torch.Tensor, shard: int):
+        """Where the pieces of :meth:`pieces` land in one rank's row of the shard receive buffer."""
+        h, ng = self.hdr, self.g_lo[shard + 1] - self.g_lo[shard]
+        out = [row[:h], row[h:h + ng * self.RL]]
+        if self.signs:
+            out.append(row[h + ng * self.RL:h + ng * self.RL + ng])
+        return out
+
+    def recv1(self, device, shard: int) -> torch.Tensor:
+        return self._buf(("r1", shard), device, self.world * self.wpr[shard], torch.int32)
+
+    def image(self, device) -> torch.Tensor:
+        return self._buf("img", device, self.n, torch.bfloat16)
+
+    def reduce_shard(self, recv1: torch.Tensor, shard: int, img: torch.Tensor) -> None:
+        """Rank-ordered dequantise-and-average of shard ``shard`` into the bf16 bucket image."""
+        W, g0 = self.world, self.g_lo[shard]
+        ng = self.g_lo[shard + 1] - g0
+        lib = ops_for(img) if img.is_cuda else None
+        if lib is not None:
+            lib.dequant_shard(recv1, W, self.hdr, self.gtab_dev(img.device), g0, ng, self.q,
+                              self.inner.qstates, img)
+            return
+        rows = recv1.view(W, -1).numpy().view(np.uint32)
+        h = self.hdr
+        gt = self.gtab[g0:g0 + ng]
+        acc = np.zeros(ng * GROUP, dtype=np.float32)
+        for r in range(W):
+            row = rows[r]
+            sc = row[:h].view(np.float32)[gt[:, 0]].repeat(GROUP)
+            lv = row[h:h + ng * self.RL]
+            if self.q == Q_TERN:
+                codes = ((lv.reshape(ng, 2, 1) >> (2 * np.arange(16, dtype=np.uint32))[None, None, :])
+                         & np.uint32(3)).reshape(-1)
+                acc += self.inner._deq(codes, sc)
+                continue
+            if self.q == Q_QS8:
+                signed = lv.copy().view(np.int8).astype(np.int64)
+            elif self.q == Q_QS9:
+                mag = lv.copy().view(np.uint8).astype(np.int64)
+                sw = row[h + ng * 8:h + ng * 9]
+                neg = ((sw[:, None] >> np.arange(32, dtype=np.uint32)[None, :]) & 1).reshape(-1)
+                signed = np.where(neg == 1, -mag, mag)
+            else:
+                signed = lv.copy().view(np.int16).astype(np.int64)
+            acc += self.inner._deq(signed, sc)
+        mean = torch.from_numpy(acc / np.float32(W)).to(torch.bfloat16)
+        for gi in range(ng):
+            o, nv = int(gt[gi, 1]), int(gt[gi, 2])
+            img[o:o + nv] = mean[gi * GROUP:gi * GROUP + nv]
+
+    def exchange(self, comm, send: torch.Tensor) -> torch.Tensor:
+        """Phases 1-3 over ``comm`` (``send_recv(sends, send_peers, recvs, recv_peers, key)``:
+        the native RCCL communicator, its loopback stand-in or the c10d adapter). Returns the bf16
+        bucket image every rank ends with."""
+        W, r, dev = self.world, self.rank, send.device
+        self._last_send = send
+        r1 = self.recv1(dev, r)
+        rows = r1.view(W, -1)
+        sends, sp, recvs, rp = [], [], [], []
+        for q in range(W):
+            ps = self.pieces(send, q)
+            sends += ps
+            sp += [q] * len(ps)
+            slots = self.piece_slots(rows[q], r)
+            recvs += slots
+            rp += [q] * len(slots)
+        comm.send_recv(sends, sp, recvs, rp, key=(self, 1))
+        img = self.image(dev)
+        self.reduce_shard(r1, r, img)
+        mine = img[self.A[r]:self.A[r + 1]]
+        peers = [q for q in range(W) if q != r]
+        comm.send_recv([mine] * len(peers), peers,
+                       [img[self.A[q]:self.A[q + 1]] for q in peers], peers, key=(self, 2))
+        return img
+
+    def decompress(self, send, recv, grad, world=None):
+        img = recv if recv is not None else self.image(grad.device)
+        dst = grad[:self.n]
+        lib = ops_for(dst) if dst.is_cuda else None
+        if lib is not None:
+            lib.bf16_expand(img, dst)
+        else:
+            dst.copy_(img.float())
+
+
 # ================================================================================= factory
 def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qstates=None,
                seed: int = 0, error_feedback: bool = False, wire: str = "auto",
@@ -870,6 +1053,11 @@ def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qst
         c = DenseCodec(plan, world, rank, seed)
     if wire == "dense" and not isinstance(c, DenseCodec):
         return DenseWrap(c)
+    if wire == "qrs":
+        if not isinstance(c, _QuantCodec):
+            raise ValueError(f"wire='qrs' (quantised reduce-scatter) needs TernGrad / QSGD, "
+                             f"not {method}")
+        return QuantRSCodec(c) if world > 1 else c
     if wire == "auto" and isinstance(c, ThresholdCodec):
         # data-dependent counts: the sparse wire needs the per-step count exchange and a host
         # read of the agreed capacity (a sync in the middle of backward); the reference's dense
@@ -881,12 +1069,17 @@ def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qst
         # (index-free Random-K sends only its values, one all-reduce: never worth densifying)
         if c.cap_total * max(world, 2) > plan.numel:
             return DenseWrap(c)
-    if wire == "auto" and isinstance(c, _QuantCodec) and world > 1 and \
-            c.words * 4 * world > 8 * plan.numel:
-        # an all-gather of codes brings (W-1)·b·n bytes to every rank (b bytes per element) and
-        # decodes W·n elements; a ring all-reduce of the dequantised fp32 vector moves
-        # 2(W-1)/W·4n and decodes n: the codes stop paying once b·W > 8 — QSGD-255 (9 bits +
-        # headers) from 8 ranks on, 8-bit QSGD from 16, 16-bit QSGD (just under 2 B with its
-        # packing) from 8, TernGrad (2 bits) only past 32
-        return DenseWrap(c)
+    if wire == "auto" and isinstance(c, _QuantCodec) and world > 1:
+        # bytes into each rank per element (b = code bytes per element): the code all-gather
+        # (W-1)·b; the quantised reduce-scatter (W-1)/W·(b + 2); the ring all-reduce of the
+        # dequantised fp32 vector 2(W-1)/W·4. QSGD-255 (b ≈ 1.13): all-gather at W = 2,
+        # reduce-scatter from 3 on; TernGrad (b ≈ 0.25): all-gather up to 9 ranks
+        n, W = max(plan.numel, 1), world
+        b = c.words * 4 / n
+        cost = {"ag": (W - 1) * b, "qrs": (W - 1) / W * (b + 2), "dense": 2 * (W - 1) / W * 4}
+        best = min(cost, key=lambda k: (cost[k], k != "ag"))
+        if best == "qrs":
+            return QuantRSCodec(c)
+        if best == "dense":
+            return DenseWrap(c)
     return c

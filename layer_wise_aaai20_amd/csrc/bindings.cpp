@@ -5,6 +5,7 @@
 // layer_wise_aaai20_amd/ops, and a GPU tensor reaching an op without this library loaded fails
 // loudly in ops/_ext.py.
 #include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 #include <map>
@@ -437,6 +438,51 @@ void dequantize(Tensor gathered, int64_t world, Tensor g, Tensor seg_off, Tensor
   TORCH_CHECK(wpr % 4 == 0, "payload words per rank must be a multiple of 4");
   lw::dequantize(a, (int)q, ptr<uint32_t>(gathered), wpr, (int)world, cur_stream());
   launched("dequantize");
+}
+
+// quantised reduce-scatter wire (compress.hip k_dequant_shard, k_bf16_expand)
+void dequant_shard(Tensor recv, int64_t world, int64_t hdr, Tensor gtab, int64_t g0, int64_t ng,
+                   int64_t q, int64_t qstates, Tensor out) {
+  const c10::DeviceGuard guard(out.device());
+  check_cuda(recv, "recv");
+  check_cuda(gtab, "gtab");
+  check_cuda(out, "out");
+  check_dtype(recv, at::kInt, "recv");
+  check_dtype(gtab, at::kInt, "gtab");
+  check_dtype(out, at::kBFloat16, "out");
+  check_aligned16(recv.data_ptr(), "recv");
+  check_aligned16(out.data_ptr(), "out");
+  TORCH_CHECK(world >= 1 && recv.numel() % world == 0, "dequant_shard: recv must hold world pieces");
+  const int64_t wpr = recv.numel() / world;
+  const int64_t rl = q == 0 ? 2 : (q == 3 ? 16 : 8);
+  TORCH_CHECK(wpr % 4 == 0 && hdr % 4 == 0, "dequant_shard: pieces must be 16-byte multiples");
+  TORCH_CHECK(wpr >= hdr + ng * rl + (q == 2 ? ng : 0), "dequant_shard: pieces too small");
+  TORCH_CHECK(gtab.dim() == 2 && gtab.size(1) == 4 && g0 >= 0 && g0 + ng <= gtab.size(0),
+              "dequant_shard: group table [G][4] does not cover the shard");
+  lw::dequantize_shard((int)q, ptr<uint32_t>(recv), wpr, (int)world, (int)hdr,
+                       reinterpret_cast<const int4*>(gtab.data_ptr()), g0, ng, (int)qstates,
+                       ptr<uint16_t>(out), out.numel(), cur_stream());
+  launched("dequant_shard");
+}
+
+void wire_wait(Tensor dev, double us, int64_t nwg) {
+  const c10::DeviceGuard guard(dev.device());
+  TORCH_CHECK(us < 1e6 && nwg >= 0 && nwg <= 1024, "wire_wait: at most 1 s on 1024 workgroups");
+  lw::wire_wait(us, (int)nwg, cur_stream());
+  launched("wire_wait");
+}
+
+void bf16_expand(Tensor in, Tensor out) {
+  const c10::DeviceGuard guard(out.device());
+  check_cuda(in, "in");
+  check_cuda(out, "out");
+  check_dtype(in, at::kBFloat16, "in");
+  check_dtype(out, at::kFloat, "out");
+  TORCH_CHECK(in.numel() == out.numel(), "bf16_expand: size mismatch");
+  check_aligned16(in.data_ptr(), "in");
+  check_aligned16(out.data_ptr(), "out");
+  lw::bf16_expand(ptr<uint16_t>(in), ptr<float>(out), in.numel(), cur_stream());
+  launched("bf16_expand");
 }
 
 // momentum correction prologue / masking (optim.hip k_mc_prep, k_mc_mask)
@@ -1030,6 +1076,15 @@ std::vector<Tensor>& splitk_keep() {
   return keep;
 }
 
+int64_t splitk_discard(Tensor dev) {
+  const c10::DeviceGuard guard(dev.device());
+  const int n = lw::splitk_discard();
+  splitk_keep().clear();
+  return n;
+}
+
+int64_t splitk_pending() { return lw::splitk_pending(); }
+
 // splitk_defer(dev, on): while on, this device's fp32 split-K outputs without bias / ReLU /
 // addend (weight gradients accumulated into the gradient arena, ops/block.py) are reduced at
 // the next splitk_flush instead of right away. `dev`: any tensor on the device (dispatch).
@@ -1041,6 +1096,13 @@ void splitk_defer(Tensor dev, bool on) {
 int64_t splitk_flush(Tensor dev) {
   const c10::DeviceGuard guard(dev.device());
   const int n = lw::splitk_flush(cur_stream());
+  // a slab allocated on another stream (LWAAAI_WGRAD_SIDE's weight-gradient stream) is read by
+  // the reduce just queued on this one: the allocator must not hand its memory out before that
+  // reduce has run
+  const auto fs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA();
+  for (const Tensor& t : splitk_keep())
+    c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(
+        t.storage().data_ptr(), fs);
   splitk_keep().clear();
   if (n > 0) launched("splitk_flush");
   return n;
@@ -1943,6 +2005,11 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "dequantize(Tensor gathered, int world, Tensor(a!) g, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor task_lo, Tensor rec_off, int q, int qstates) -> ()");
   m.def(
+      "dequant_shard(Tensor recv, int world, int hdr, Tensor gtab, int g0, int ng, int q, "
+      "int qstates, Tensor(a!) out) -> ()");
+  m.def("bf16_expand(Tensor x, Tensor(a!) out) -> ()");
+  m.def("wire_wait(Tensor dev, float us, int nwg) -> ()");
+  m.def(
       "mc_prep(Tensor(a!) g, Tensor(b!) u, Tensor? p, Tensor seg_off, Tensor seg_n, Tensor segs, "
       "Tensor tasks, Tensor? seg_wd, float mc, float wmul) -> ()");
   m.def("mc_mask(Tensor(a!) u, Tensor e) -> ()");
@@ -1952,6 +2019,8 @@ LW_LIBRARY(LW_OPS_NS, m) {
   m.def("pack_kc_multi(Tensor[] w, Tensor(a!)[] out, int[] prm) -> ()");
   m.def("xent_scale(Tensor grad, Tensor gl, Tensor n) -> Tensor");
   m.def("splitk_flush(Tensor dev) -> int");
+  m.def("splitk_discard(Tensor dev) -> int");
+  m.def("splitk_pending() -> int", &splitk_pending);
   m.def(
       "sgd_step(Tensor(a!) p, Tensor g, Tensor(b!) buf, Tensor seg_off, Tensor seg_n, "
       "Tensor segs, Tensor tasks, Tensor seg_wd, float lr, float momentum, float dampening, "
@@ -2032,6 +2101,9 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("unpack_validx", &unpack_validx);
   m.impl("quantize", &quantize);
   m.impl("dequantize", &dequantize);
+  m.impl("dequant_shard", &dequant_shard);
+  m.impl("bf16_expand", &bf16_expand);
+  m.impl("wire_wait", &wire_wait);
   m.impl("sgd_step", &sgd_step);
   m.impl("mc_prep", &mc_prep);
   m.impl("mc_mask", &mc_mask);
@@ -2041,6 +2113,7 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("pack_kc_multi", &pack_kc_multi);
   m.impl("xent_scale", &xent_scale);
   m.impl("splitk_flush", &splitk_flush);
+  m.impl("splitk_discard", &splitk_discard);
   m.impl("normalize_u8", &normalize_u8);
   m.impl("cifar_augment", &cifar_augment);
   m.impl("gap_fwd", &gap_fwd);

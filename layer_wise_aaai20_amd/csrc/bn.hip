@@ -686,15 +686,20 @@ int bn_reduce_blocks(int64_t M, int C) {
   return nb;
 }
 
-// grid with (gridDim * BNT) % G == 0 so every thread keeps one channel group
-static int apply_grid(int64_t n8, int C) {
+// grid with (gridDim * BNT) % G == 0 so every thread keeps one channel group. `cap` workgroups at
+// most: fewer, longer grid-stride sweeps keep each CU's accesses within fewer DRAM pages. Measured
+// on the 411 MB layer-1 tensors (scripts/probes/bn_stream_probe.hip, profiles/r6/bn_stream_probe*):
+// the residual forward apply 279 -> 221 us at 512 workgroups instead of 4096, the backward apply
+// 238 -> 224 us at 1024 (512 starves it of loads in flight: 287 us).
+constexpr int kApplyFwdGrid = 512, kApplyBwdGrid = 1024;
+static int apply_grid(int64_t n8, int C, int cap) {
   const int G = C / 8;
   int q = G;                                   // blocks must be a multiple of G / gcd(G, BNT)
   int a = G, b = BNT;
   while (b) { const int t = a % b; a = b; b = t; }
   q = G / a;
   int64_t g = (n8 + BNT - 1) / BNT;
-  g = g > 4096 ? 4096 : (g < 1 ? 1 : g);
+  g = g > cap ? cap : (g < 1 ? 1 : g);
   g = (g + q - 1) / q * q;
   return (int)g;
 }
@@ -705,7 +710,7 @@ static void bn_apply_t(const BNArgs& a, hipStream_t st) {
   const T* res = static_cast<const T*>(a.res);
   T* y = static_cast<T*>(a.y);
   const int64_t n8 = a.M * a.C / 8;
-  const dim3 grid(apply_grid(n8, a.C)), block(BNT);
+  const dim3 grid(apply_grid(n8, a.C, kApplyFwdGrid)), block(BNT);
 #define LW_AP(R, L)                                                                              \
   hipLaunchKernelGGL((k_bn_apply<T, R, L>), grid, block, 0, st, x, res, y, a.scale, a.shift,     \
                      a.res_scale, a.res_shift, a.bits, n8, a.C)
@@ -808,7 +813,7 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
                      a.C, a.M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
                      (int)a.training, (int)a.accum_dparams);
-  const dim3 grid(apply_grid(n8, a.C)), block(BNT);
+  const dim3 grid(apply_grid(n8, a.C, kApplyBwdGrid)), block(BNT);
 #define LW_BWD(R, D)                                                                            \
   hipLaunchKernelGGL((k_bn_bwd_apply<T, R, D>), grid, block, 0, st, x, dy, y, a.bits, a.scale,  \
                      a.shift, a.A, a.B, a.Cc, dx, dres, n8, a.C, bn_reverse() ? 1 : 0)
@@ -839,7 +844,7 @@ void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st) {
                        p->C, p->M, p->gamma, p->mean, p->invstd, p->dgamma, p->dbeta, p->A, p->B,
                        p->Cc, 1, (int)p->accum_dparams);
   const int64_t n8 = a.M * a.C / 8;
-  hipLaunchKernelGGL(k_bn_bwd_apply_dual, dim3(apply_grid(n8, a.C)), dim3(BNT), 0, st, x, x2, dy,
+  hipLaunchKernelGGL(k_bn_bwd_apply_dual, dim3(apply_grid(n8, a.C, kApplyBwdGrid)), dim3(BNT), 0, st, x, x2, dy,
                      a.bits, a.A, a.B, a.Cc, b.A, b.B, b.Cc, static_cast<uint16_t*>(a.dx),
                      static_cast<uint16_t*>(b.dx), n8, a.C, bn_reverse() ? 1 : 0);
 }

@@ -1726,4 +1726,151 @@ void dequantize(const QuantArgs& a, int q, const uint32_t* gathered, int64_t wor
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Quantised reduce-scatter wire (codecs.py QuantRSCodec). Every rank quantises its whole bucket
+// (k_quant); an all-to-all sends rank q only the records of ITS shard of the bucket's groups
+// (groups [g0_q, g0_q + ng_q)), each piece laid out [hdr scale words | ng level words x RL |
+// (Q_QS9) ng sign words]; rank q dequantises and averages its shard over the W pieces in rank
+// order — the arithmetic of k_dequant, so the mean is the all-gather wire's bit for bit before
+// its rounding — and writes it as bf16 into the bucket image, which a bf16 all-gather of the
+// shards then completes on every rank. gtab[g] = (segment, bucket element offset, valid
+// elements, 0) of global group g.
+// ------------------------------------------------------------------------------------------
+template <int Q>
+__global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict__ recv, int64_t wpr,
+                                                      int ws, int hdr, const int4* __restrict__ gtab,
+                                                      int64_t g0, int64_t ng, int qstates,
+                                                      uint16_t* __restrict__ out, int64_t n_out) {
+  const int64_t j = (int64_t)blockIdx.x * NT + threadIdx.x;
+  if (j >= ng) return;
+  const int4 gt = gtab[g0 + j];
+  // (a malformed table entry writes nothing rather than out of bounds)
+  if (gt.x < 0 || gt.x >= hdr || gt.y < 0 || gt.z < 0 || gt.z > EPT || gt.y + gt.z > n_out) return;
+  constexpr int RL = Q == Q_TERN ? 2 : (Q == Q_QS16 ? 16 : 8);
+  float acc[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) acc[k] = 0.f;
+  for (int r = 0; r < ws; ++r) {
+    const uint32_t* P = recv + (int64_t)r * wpr;
+    const float sc = __uint_as_float(P[gt.x]);
+    const uint32_t* rec = P + hdr + j * RL;
+    if (Q == Q_TERN) {
+      const uint2 w = *reinterpret_cast<const uint2*>(rec);
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const uint32_t c = ((k < 16 ? w.x : w.y) >> (2 * (k & 15))) & 3u;
+        acc[k] += c == 1u ? sc : (c == 2u ? -sc : 0.f);
+      }
+    } else if (Q == Q_QS8) {
+      const uint4* o = reinterpret_cast<const uint4*>(rec);
+      const uint4 a = o[0], b = o[1];
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int l = (int)(int8_t)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
+        const float sg = l > 0 ? 1.f : (l < 0 ? -1.f : 0.f);
+        acc[k] += sg * sc * ((float)(l < 0 ? -l : l) / (float)qstates);
+      }
+    } else if (Q == Q_QS9) {
+      const uint4* o = reinterpret_cast<const uint4*>(rec);
+      const uint4 a = o[0], b = o[1];
+      const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      const uint32_t sgn = P[hdr + ng * 8 + j];
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int l = (int)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
+        const float sg = l == 0 ? 0.f : (((sgn >> k) & 1u) ? -1.f : 1.f);
+        acc[k] += sg * sc * ((float)l / (float)qstates);
+      }
+    } else {
+      const uint4* o = reinterpret_cast<const uint4*>(rec);
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 x = o[q];
+        w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
+      }
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int l = (int)(int16_t)((w[k >> 1] >> (16 * (k & 1))) & 0xffff);
+        const float sg = l > 0 ? 1.f : (l < 0 ? -1.f : 0.f);
+        acc[k] += sg * sc * ((float)(l < 0 ? -l : l) / (float)qstates);
+      }
+    }
+  }
+  const float fws = (float)ws;
+  uint16_t* op = out + gt.y;
+  if (gt.z == EPT && (gt.y & 7) == 0) {
+#pragma unroll
+    for (int q = 0; q < EPT / 8; ++q) {
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[k] = (uint32_t)ElemBF16::rne(acc[8 * q + 2 * k] / fws) |
+               ((uint32_t)ElemBF16::rne(acc[8 * q + 2 * k + 1] / fws) << 16);
+      reinterpret_cast<uint4*>(op)[q] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  } else {
+    for (int k = 0; k < gt.z; ++k) op[k] = ElemBF16::rne(acc[k] / fws);
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_bf16_expand(const uint16_t* __restrict__ in,
+                                                    float* __restrict__ out, int64_t n) {
+  const int64_t step = (int64_t)gridDim.x * NT * 8;
+  for (int64_t i = ((int64_t)blockIdx.x * NT + threadIdx.x) * 8; i < n; i += step) {
+    if (i + 8 <= n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(in + i);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      float4* o = reinterpret_cast<float4*>(out + i);
+      o[0] = make_float4(ElemBF16::lo(w[0]), ElemBF16::hi(w[0]), ElemBF16::lo(w[1]), ElemBF16::hi(w[1]));
+      o[1] = make_float4(ElemBF16::lo(w[2]), ElemBF16::hi(w[2]), ElemBF16::lo(w[3]), ElemBF16::hi(w[3]));
+    } else {
+      for (int64_t k = i; k < n; ++k) out[k] = ElemBF16::f(in[k]);
+    }
+  }
+}
+
+void dequantize_shard(int q, const uint32_t* recv, int64_t wpr, int ws, int hdr, const int4* gtab,
+                      int64_t g0, int64_t ng, int qstates, uint16_t* out, int64_t n_out,
+                      hipStream_t st) {
+  if (ng <= 0) return;
+  const int64_t grid = (ng + NT - 1) / NT;
+  switch (q) {
+    case Q_TERN: LW_LAUNCH(k_dequant_shard<Q_TERN>, grid, st, recv, wpr, ws, hdr, gtab, g0, ng, qstates, out, n_out); break;
+    case Q_QS8: LW_LAUNCH(k_dequant_shard<Q_QS8>, grid, st, recv, wpr, ws, hdr, gtab, g0, ng, qstates, out, n_out); break;
+    case Q_QS9: LW_LAUNCH(k_dequant_shard<Q_QS9>, grid, st, recv, wpr, ws, hdr, gtab, g0, ng, qstates, out, n_out); break;
+    default: LW_LAUNCH(k_dequant_shard<Q_QS16>, grid, st, recv, wpr, ws, hdr, gtab, g0, ng, qstates, out, n_out); break;
+  }
+}
+
+void bf16_expand(const uint16_t* in, float* out, int64_t n, hipStream_t st) {
+  if (n <= 0) return;
+  int64_t grid = (n + NT * 8 - 1) / (NT * 8);
+  grid = grid > 2048 ? 2048 : grid;
+  LW_LAUNCH(k_bf16_expand, grid, st, in, out, n);
+}
+
+// Simulated wire time (parallel/loopback.py wire model, train/simworld.py): `nwg` single-wave
+// workgroups each hold a CU slot — as RCCL's channel workgroups do during a real transfer — until
+// `ticks` of the constant wall clock have passed since it started, sleeping between reads. Every
+// wave leaves once its own deadline passes, so the grid always drains.
+__global__ __launch_bounds__(64) void k_wire_wait(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void wire_wait(double us, int nwg, hipStream_t st) {
+  static int khz = 0;
+  if (khz == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+      khz = 100000;                              // the 100 MHz constant clock of CDNA3/4
+  }
+  if (us <= 0.0 || nwg <= 0) return;
+  const uint64_t ticks = (uint64_t)(us * (double)khz / 1000.0);
+  hipLaunchKernelGGL(k_wire_wait, dim3(nwg), dim3(64), 0, st, ticks);
+}
+
 }  // namespace lw

@@ -524,6 +524,19 @@ int splitk_flush(hipStream_t st) {
   return n;
 }
 
+// Drop every queued reduce without launching anything (a step that failed between a deferred
+// GEMM and the flush — a capture that fell back to eager, a backward that raised): the slabs it
+// names were never (or only partly) written, and reducing them into the arena would add garbage.
+int splitk_discard() {
+  const int n = (int)g_pending.size();
+  g_pending.clear();
+  g_defer = false;
+  g_last_deferred = false;
+  return n;
+}
+
+int splitk_pending() { return (int)g_pending.size(); }
+
 void splitk_reduce(const GemmArgs& g, int zs, hipStream_t st) {
   if (g_defer && !g.out_bf16 && g.bias == nullptr && !g.relu && g.addend == nullptr) {
     g_pending.push_back(ReduceJob{g.partial, static_cast<float*>(g.C), g.ldc, 0, zs,

@@ -116,6 +116,14 @@ void quant_stage(const QuantArgs& a, bool ef_add, int t_lo, int t_hi, float2* pa
 void quantize(const QuantArgs& a, int q, bool ef, hipStream_t st);
 void dequantize(const QuantArgs& a, int q, const uint32_t* gathered, int64_t words_per_rank, int ws,
                 hipStream_t st);
+// quantised reduce-scatter wire (compress.hip): one shard's rank-ordered dequantise-and-average
+// into a bf16 bucket image, and that image expanded into the fp32 gradient
+void dequantize_shard(int q, const uint32_t* recv, int64_t wpr, int ws, int hdr, const int4* gtab,
+                      int64_t g0, int64_t ng, int qstates, uint16_t* out, int64_t n_out,
+                      hipStream_t st);
+void bf16_expand(const uint16_t* in, float* out, int64_t n, hipStream_t st);
+// simulated xGMI transfer time: nwg workgroups busy for `us` microseconds (loopback wire model)
+void wire_wait(double us, int nwg, hipStream_t st);
 
 // optimizer (optim.hip)
 struct SgdArgs {
@@ -301,6 +309,8 @@ void splitk_reduce(const GemmArgs& g, int splits, hipStream_t st);   // fixed-or
 void splitk_set_defer(bool on);
 bool splitk_take_deferred();
 int splitk_flush(hipStream_t st);
+int splitk_discard();            // drop the queue (and its slabs) without launching anything
+int splitk_pending();
 void gemm_tile_shape(int tile, int& bm, int& bn, int& bk);
 int stats_rows_bm(int tile);      // rows of C per column-statistics row of a tile
 int gemm_k_per_split(int K, int splits, int bk);

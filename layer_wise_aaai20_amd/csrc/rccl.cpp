@@ -23,6 +23,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <vector>
 #include <unistd.h>
 
 namespace {
@@ -183,6 +184,76 @@ void rccl_broadcast(int64_t h, Tensor t, int64_t root) {
         "ncclBroadcast");
 }
 
+// Grouped point-to-point transfers: every send and receive of the two lists inside one
+// ncclGroupStart / ncclGroupEnd, so RCCL schedules them together over the xGMI links (one
+// channel set per peer) instead of serialising them; sends to and receives from this rank itself
+// are allowed (a local copy). Pairs must match across ranks in count, size and dtype, in order
+// per peer — what the all-to-all and variable-size all-gather of the quantised reduce-scatter
+// wire (compress/codecs.py QuantRSCodec) are built from. Empty tensors are skipped on both sides.
+void rccl_send_recv(int64_t h, std::vector<Tensor> sends, std::vector<int64_t> send_peers,
+                    std::vector<Tensor> recvs, std::vector<int64_t> recv_peers) {
+  TORCH_CHECK(sends.size() == send_peers.size() && recvs.size() == recv_peers.size(),
+              "rccl_send_recv: one peer per tensor");
+  int n = 0;
+  check(ncclCommCount(comm_of(h), &n), "ncclCommCount");
+  for (size_t i = 0; i < sends.size(); ++i) {
+    check_dev(sends[i], "send");
+    TORCH_CHECK(send_peers[i] >= 0 && send_peers[i] < n, "rccl_send_recv: bad send peer");
+  }
+  for (size_t i = 0; i < recvs.size(); ++i) {
+    check_dev(recvs[i], "recv");
+    TORCH_CHECK(recv_peers[i] >= 0 && recv_peers[i] < n, "rccl_send_recv: bad recv peer");
+  }
+  if (sends.empty() && recvs.empty()) return;
+  const c10::DeviceGuard guard((sends.empty() ? recvs[0] : sends[0]).device());
+  ncclComm_t c = comm_of(h);
+  hipStream_t st = cur_stream();
+  check(ncclGroupStart(), "ncclGroupStart");
+  for (size_t i = 0; i < sends.size(); ++i)
+    if (sends[i].numel() > 0)
+      check(ncclSend(sends[i].data_ptr(), (size_t)sends[i].numel(), dtype_of(sends[i]),
+                     (int)send_peers[i], c, st), "ncclSend");
+  for (size_t i = 0; i < recvs.size(); ++i)
+    if (recvs[i].numel() > 0)
+      check(ncclRecv(recvs[i].data_ptr(), (size_t)recvs[i].numel(), dtype_of(recvs[i]),
+                     (int)recv_peers[i], c, st), "ncclRecv");
+  check(settle(c, ncclGroupEnd()), "ncclGroupEnd (send/recv)");
+}
+
+// Equal-chunk all-to-all: chunk q of `send` goes to rank q, chunk q of `recv` comes from rank q.
+void rccl_all_to_all(int64_t h, Tensor send, Tensor recv) {
+  check_dev(send, "send");
+  check_dev(recv, "recv");
+  int n = 0;
+  check(ncclCommCount(comm_of(h), &n), "ncclCommCount");
+  TORCH_CHECK(send.scalar_type() == recv.scalar_type() && send.numel() == recv.numel() &&
+                  send.numel() % n == 0, "rccl_all_to_all: send / recv must be world equal chunks");
+  const int64_t chunk = send.numel() / n;
+  std::vector<Tensor> s, r;
+  std::vector<int64_t> p;
+  for (int q = 0; q < n; ++q) {
+    s.push_back(send.narrow(0, q * chunk, chunk));
+    r.push_back(recv.narrow(0, q * chunk, chunk));
+    p.push_back(q);
+  }
+  rccl_send_recv(h, s, p, r, p);
+}
+
+// Reduce-scatter: recv (numel = send / world) gets this rank's chunk of the element-wise reduction.
+void rccl_reduce_scatter(int64_t h, Tensor send, Tensor recv, int64_t op) {
+  check_dev(send, "send");
+  check_dev(recv, "recv");
+  int n = 0;
+  check(ncclCommCount(comm_of(h), &n), "ncclCommCount");
+  TORCH_CHECK(send.scalar_type() == recv.scalar_type() && send.numel() == recv.numel() * n,
+              "rccl_reduce_scatter: send must hold world * recv");
+  const c10::DeviceGuard guard(send.device());
+  const ncclRedOp_t rop = op == 1 ? ncclMax : (op == 2 ? ncclMin : ncclSum);
+  check(settle(comm_of(h), ncclReduceScatter(send.data_ptr(), recv.data_ptr(), (size_t)recv.numel(),
+                                             dtype_of(send), rop, comm_of(h), cur_stream())),
+        "ncclReduceScatter");
+}
+
 // ---------------------------------------------------------------------------------------------
 // Watchdog. c10d's ProcessGroup watchdog never sees these collectives (they bypass c10d), so a rank
 // that stops participating — a crashed peer, a rank whose control flow diverged, a mismatched
@@ -335,4 +406,9 @@ TORCH_LIBRARY_FRAGMENT(lwaaai, m) {
   m.def("rccl_all_gather(int comm, Tensor send, Tensor(a!) recv) -> ()", &rccl_all_gather);
   m.def("rccl_all_reduce(int comm, Tensor(a!) t, int op) -> ()", &rccl_all_reduce);
   m.def("rccl_broadcast(int comm, Tensor(a!) t, int root) -> ()", &rccl_broadcast);
+  m.def("rccl_send_recv(int comm, Tensor[] sends, int[] send_peers, Tensor(a!)[] recvs, "
+        "int[] recv_peers) -> ()", &rccl_send_recv);
+  m.def("rccl_all_to_all(int comm, Tensor send, Tensor(a!) recv) -> ()", &rccl_all_to_all);
+  m.def("rccl_reduce_scatter(int comm, Tensor send, Tensor(a!) recv, int op) -> ()",
+        &rccl_reduce_scatter);
 }

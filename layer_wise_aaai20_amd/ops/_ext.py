@@ -113,6 +113,23 @@ def set_splitk_defer(t: torch.Tensor, on: bool) -> None:
     _DEFER[0] = t if on else None
 
 
+def splitk_discard(dev: torch.Tensor) -> int:
+    """Drop the queued split-K reduces and their slabs without launching anything (a step that
+    failed between a deferred weight-gradient GEMM and the engine's flush: the capture that fell
+    back to eager, a backward that raised). Returns how many were dropped."""
+    _DEFER[0] = None
+    if not is_loaded():
+        return 0
+    return int(load().splitk_discard(dev))
+
+
+def splitk_pending() -> int:
+    """Split-K reduces queued and not yet flushed (0 between steps)."""
+    if not is_loaded():
+        return 0
+    return int(load().splitk_pending())
+
+
 class splitk_paused:
     """Reduce split-K outputs right away inside this scope (the tuner's timing runs: a
     deferred reduce would neither be timed nor target a real gradient)."""

@@ -158,6 +158,21 @@ class NativeRccl:
         self.lib.rccl_broadcast(self.handle, t, src)
         return _Done()
 
+    def send_recv(self, sends, send_peers, recvs, recv_peers, key=None):
+        """Every send / receive of the lists in one RCCL group (``csrc/rccl.cpp
+        rccl_send_recv``); ``key`` is for stand-ins that must know what the peers would send."""
+        self.lib.rccl_send_recv(self.handle, list(sends), [int(p) for p in send_peers],
+                                list(recvs), [int(p) for p in recv_peers])
+        return _Done()
+
+    def all_to_all(self, send: torch.Tensor, recv: torch.Tensor):
+        self.lib.rccl_all_to_all(self.handle, send, recv)
+        return _Done()
+
+    def reduce_scatter(self, send: torch.Tensor, recv: torch.Tensor, op: str = "sum"):
+        self.lib.rccl_reduce_scatter(self.handle, send, recv, {"sum": 0, "max": 1, "min": 2}[op])
+        return _Done()
+
     def start_watchdog(self, timeout_s: float, action: int = 0) -> "Watchdog":
         """Deadline + asynchronous-error watchdog on this communicator (``csrc/rccl.cpp``)."""
         self.watch = Watchdog(self.handle, self.device, timeout_s, action)
@@ -173,6 +188,39 @@ class NativeRccl:
         if self.handle:
             self.lib.rccl_abort(self.handle)
             self.handle = 0
+
+
+class C10dP2P:
+    """``send_recv`` over c10d point-to-point (``dist.batch_isend_irecv``: gloo on the CPU, or
+    the nccl process group when the native communicator is off) with the native communicator's
+    signature; transfers to this rank itself are local copies. Blocking: returns once every
+    transfer has completed."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = rank(group)
+
+    def _global(self, peer: int) -> int:
+        return dist.get_global_rank(self.group, peer) if self.group is not None else int(peer)
+
+    def send_recv(self, sends, send_peers, recvs, recv_peers, key=None):
+        ops = []
+        mine = [t for t, p in zip(sends, send_peers) if int(p) == self.rank]
+        into = [t for t, p in zip(recvs, recv_peers) if int(p) == self.rank]
+        if len(mine) != len(into):
+            raise ValueError("send_recv: sends to self and receives from self do not pair up")
+        for a, b in zip(mine, into):
+            b.copy_(a)
+        for t, p in zip(sends, send_peers):
+            if int(p) != self.rank and t.numel():
+                ops.append(dist.P2POp(dist.isend, t.contiguous(), self._global(p), self.group))
+        for t, p in zip(recvs, recv_peers):
+            if int(p) != self.rank and t.numel():
+                ops.append(dist.P2POp(dist.irecv, t, self._global(p), self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return _Done()
 
 
 class Watchdog:

@@ -9,8 +9,15 @@
 
 Start-up: module state (parameters AND buffers) is broadcast from rank 0, as in ``ddp.py:190-194``;
 unlike the reference's CIFAR path every mode starts from identical replicas.
-Buffers (BatchNorm running statistics) are re-broadcast before each training forward when
-``broadcast_buffers`` is set (``ddp.py:361-386``), as one coalesced message.
+Buffers (BatchNorm running statistics) follow rank 0 when ``broadcast_buffers`` is set. The
+reference re-broadcasts them before every forward (``ddp.py:361-386``); their training-mode
+readers never look at them (BatchNorm normalises with batch statistics), and rank 0 — the source —
+never receives, so its buffers evolve identically either way. ``buffer_sync="lazy"`` (default)
+therefore broadcasts them, as one coalesced message, only where they are read: the first
+eval-mode forward after training, :meth:`sync_buffers` (the trainers call it before evaluation
+and checkpoints, on every rank) — the values there are exactly the reference's. A captured
+training step then carries no per-step broadcast collective. ``buffer_sync="step"`` keeps the
+reference's per-forward broadcast.
 """
 from __future__ import annotations
 
@@ -33,8 +40,12 @@ class CompressedDDP(nn.Module):
                  output_device=None, dim: int = 0, timing: bool = False,
                  bf16_weights: bool = True, world_size: Optional[int] = None,
                  dense_below: int = 0, momentum_correction: float = 0.0,
-                 ef_lr_scaled: bool = False):
+                 ef_lr_scaled: bool = False, buffer_sync: str = "lazy"):
         super().__init__()
+        if buffer_sync not in ("lazy", "step"):
+            raise ValueError(f"buffer_sync={buffer_sync!r}: expected 'lazy' or 'step'")
+        self.buffer_sync = buffer_sync
+        self._buf_dirty = False
         self.module = module
         import os
         self.bf16_weights = (bf16_weights and flat_params and
@@ -133,14 +144,32 @@ class CompressedDDP(nn.Module):
         self.engine.finish()
 
     # ------------------------------------------------------------------ module API
+    def sync_buffers(self) -> None:
+        """Collective: give every rank rank 0's buffers now (a no-op when nothing changed since
+        the last sync, on one rank, or with ``broadcast_buffers=False``). Call on every rank."""
+        if self._bcast_events:
+            torch.cuda.current_stream(self.engine.device).wait_event(self._bcast_events[-1][1])
+        if self._buf_dirty and self.broadcast_buffers and self._buffers_list:
+            comm.broadcast_coalesced(self._buffers_list, 0, self.process_group,
+                                     native=self.engine._native)
+        self._buf_dirty = False
+
     def forward(self, *inputs, **kwargs):
         if not self.training:
-            if self._bcast_events:          # (evaluation reads the broadcast running statistics)
-                torch.cuda.current_stream(self.engine.device).wait_event(self._bcast_events[-1][1])
+            self.sync_buffers()             # (evaluation reads the broadcast running statistics)
             return self.module(*inputs, **kwargs)
         if self.check_reduction and self.engine._active:
             raise RuntimeError("Not all gradients have been reduced from the backward of the "
                                "previous iteration (ddp.py:312-327 check_reduction).")
+        if self.buffer_sync == "lazy":
+            # no collective in the training step: broadcast where the buffers are read
+            self._buf_dirty = self._buf_dirty or (self.broadcast_buffers and
+                                                  bool(self._buffers_list) and
+                                                  comm.world_size(self.process_group) > 1)
+            self.engine.begin_step()
+            if self.bf16_weights and self.engine.arena.device.type == "cuda":
+                self.engine.arena.refresh_bf16()
+            return self.module(*inputs, **kwargs)
         side = self._buffer_side()
         if side is not None:
             # the buffers were broadcast on the side stream right after the previous forward,

@@ -159,9 +159,10 @@ class GradSyncEngine:
         for c in self.codecs:
             c.step_t = self._dstep
             c.overflow = self._overflow
-            if isinstance(c, DenseWrap):
-                c.inner.step_t = self._dstep
-                c.inner.overflow = self._overflow
+            inner = getattr(c, "inner", None)          # (DenseWrap, QuantRSCodec)
+            if inner is not None:
+                inner.step_t = self._dstep
+                inner.overflow = self._overflow
         self.seg_bucket = [0] * len(self.arena.segments)
         for b in self.buckets:
             for i in range(b.seg_lo, b.seg_hi):
@@ -183,21 +184,24 @@ class GradSyncEngine:
         self._side = (torch.cuda.Stream(device=self.device)
                       if overlap_compress and self.device.type == "cuda" else None)
         # inside a captured step (LWAAAI_GRAPH_OVERLAP):
-        #   "0"    (default) each bucket is compressed, exchanged and decoded inline on the compute
-        #          stream, in backward order as its gradients complete;
+        #   "0"    each bucket is compressed, exchanged and decoded inline on the compute stream,
+        #          in backward order as its gradients complete;
         #   "comm" compression inline, only the bucket's RCCL collective on a side branch;
-        #   "1"    compression and collective both on the side branch (the round-2..4 default at
-        #          world > 1).
-        # A fork/join pair in a replayed HIP graph costs far more than it hides here: ResNet-50,
-        # simulated world 8, layer-wise Top-K 0.1 % (3 buckets): step exposed over compute-only
-        # 0.36 ms inline, 1.00 ms "1", 1.45 ms "comm" (profiles/r5/sim8_overlap_modes.jsonl;
-        # 1 GPU at world 1: 24.67 vs 24.17 ms/step, profiles/r2_graph_overlap_ab.log). Eager
-        # (uncaptured) steps keep the side stream.
-        mode = os.environ.get("LWAAAI_GRAPH_OVERLAP", "0")
-        if mode not in ("0", "1", "comm"):
-            raise ValueError(f"LWAAAI_GRAPH_OVERLAP={mode!r}: expected 0, 1 or comm")
-        self._graph_overlap = mode != "0"
-        self._comm_only = mode == "comm"
+        #   "1"    compression and collective both on the side branch, overlapping the rest of
+        #          backward (the reference's hook-driven DDP, sparsified_ddp.py:403-452);
+        #   "auto" (default) "1" with a real RCCL communicator at world > 1 — the xGMI transfer
+        #          then runs beside backward instead of on its critical path — "0" otherwise (one
+        #          rank, or the loopback stand-in without a wire model, where a fork/join pair in a
+        #          replayed HIP graph costs more than the in-memory "collective" it would hide:
+        #          profiles/r5/sim8_overlap_modes.jsonl). The wire-priced world-8 simulation
+        #          (profiles/r6/sim8_wire_*.jsonl) measures the modes with the transfer included.
+        # Eager (uncaptured) steps keep the side stream.
+        mode = os.environ.get("LWAAAI_GRAPH_OVERLAP", "auto")
+        if mode not in ("0", "1", "comm", "auto"):
+            raise ValueError(f"LWAAAI_GRAPH_OVERLAP={mode!r}: expected auto, 0, 1 or comm")
+        self._overlap_mode = mode
+        self._graph_overlap = False
+        self._comm_only = False
         self._retired = []            # (fence event, events held until it completes)
         self._check = os.environ.get("LWAAAI_ENGINE_CHECK", "0") == "1"
         # bucket collectives on a native RCCL communicator (csrc/rccl.cpp) when the group is
@@ -215,9 +219,26 @@ class GradSyncEngine:
             self._watch = (getattr(self._native, "watch", None) or
                            self._native.start_watchdog(comm.comm_timeout()))
         self._set_inplace_gather()
+        self.set_graph_overlap(self._overlap_mode)
         self._reset_state()
         self.all_reduced_last = True
         self.verify_plan()
+
+    def set_graph_overlap(self, mode: str) -> None:
+        """Where a captured step runs each bucket's exchange (see LWAAAI_GRAPH_OVERLAP above)."""
+        if mode not in ("0", "1", "comm", "auto"):
+            raise ValueError(f"graph overlap mode {mode!r}: expected auto, 0, 1 or comm")
+        self._overlap_mode = mode
+        if mode == "auto":
+            real = isinstance(self._native, comm.NativeRccl) or (
+                self._native is not None and getattr(self._native, "wire_model", None))
+            mode = "1" if self.world > 1 and real else "0"
+        self._graph_overlap = mode != "0"
+        self._comm_only = mode == "comm"
+
+    def graph_overlap_mode(self) -> str:
+        """The effective captured-step exchange mode: "0", "1" or "comm"."""
+        return "0" if not self._graph_overlap else ("comm" if self._comm_only else "1")
 
     # ----------------------------------------------------------------- failure detection
     def plan_signature(self) -> List[int]:
@@ -452,6 +473,7 @@ class GradSyncEngine:
         self._native = native
         self._stream_waitable = True
         self._set_inplace_gather()
+        self.set_graph_overlap(self._overlap_mode)
 
     # ----------------------------------------------------------------- state machine
     def _reset_state(self):
@@ -494,6 +516,13 @@ class GradSyncEngine:
             self.arena.zero_except(self._no_zero)
         if self.device.type == "cuda":
             from ..ops import block as _block
+            from ..ops._ext import splitk_discard, splitk_pending
+            if splitk_pending():
+                # left over from a step that never reached its flush (a backward that raised):
+                # their slabs belong to that step and must not be added into this one's arena
+                n = splitk_discard(self.arena.grad)
+                print(f"[lwaaai] dropped {n} split-K reduces left by an unfinished step",
+                      flush=True)
             _block.new_step()            # (per-step weight-pack batch: ops/conv.py kc_pack)
         if not self.arena.grads_attached():
             self.arena.attach_grads()
@@ -615,6 +644,12 @@ class GradSyncEngine:
                 work = (self._native.all_reduce(send) if self._native is not None
                         else comm.all_reduce(send, self.pg))
                 recv = None
+            elif codec.collective == "quant_rs":
+                # quantised reduce-scatter: code all-to-all, shard dequant-sum, bf16 all-gather
+                # (codecs.py QuantRSCodec); stream-ordered on the native communicator
+                recv = codec.exchange(self._native if self._native is not None
+                                      else comm.C10dP2P(self.pg), send)
+                work = comm._Done()
             elif self.world == 1:
                 recv, work = None, comm._Done()       # (one rank: decode straight from send)
             else:

@@ -71,6 +71,7 @@ def short_run_top1(device, steps: int = 300, size: int = 128, batch: int = 256,
         for grp in tr.opt.param_groups:
             grp["lr"] = lr_at(i, steps, peak, warmup, decay)
         losses.append(tr.step(*make_batch(g)))
+    tr.ddp.sync_buffers()                # rank 0's running statistics on every rank
     model = tr.ddp.module
     model.eval()
     counts = torch.zeros(3, dtype=torch.float64, device=dev)

@@ -59,6 +59,8 @@ def run_batches(model, batches, training, world_size=1, optimizer_step=None, sta
     its whole step is replayed as one HIP graph once warm (``graph``, default on:
     ``LWAAAI_CIFAR_GRAPH=0`` keeps it eager)."""
     stats = stats or StatsLogger(("loss", "correct"))
+    if not training and hasattr(model, "sync_buffers"):
+        model.sync_buffers()             # collective: rank 0's BN statistics before evaluation
     model.train(training)
     mode = canonical_mode(compress) if compress not in (None, "none") else "none"
     hooked = getattr(model, "engine", None) is not None

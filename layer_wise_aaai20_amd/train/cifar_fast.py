@@ -145,6 +145,7 @@ class CifarTrainer:
     @torch.no_grad()
     def evaluate(self) -> float:
         """Held-out accuracy on the synthetic test split (eval-mode BatchNorm)."""
+        self.ddp.sync_buffers()          # rank 0's running statistics on every rank
         self.model.eval()
         correct = total = 0
         for b in self.test_batches:

@@ -51,7 +51,7 @@ def get_parser() -> argparse.ArgumentParser:
     p.add_argument("--epochs", type=int, default=None)
     p.add_argument("--batch_size", type=int, default=512)
     p.add_argument("--error_feedback", action="store_true")
-    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "sparse-capped", "dense", "indexfree"])
+    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "sparse-capped", "dense", "indexfree", "qrs"])
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--n_train", type=int, default=50000)
     p.add_argument("--n_test", type=int, default=10000)

@@ -131,6 +131,11 @@ class StepGraph:
                 err = e
             # one decision for all ranks: a rank replaying while another runs eagerly would
             # still pair its collectives, but the whole job would then run at the slow mode
+            if err is not None:
+                # the failed capture may have queued deferred split-K reduces over slabs it never
+                # wrote: the eager step's flush must not add them into the arena
+                from ..ops._ext import splitk_discard
+                splitk_discard(torch.empty(0, device=self.device))
             if not self._agree(err is None):
                 self.enabled = False
                 self._graphs.clear()

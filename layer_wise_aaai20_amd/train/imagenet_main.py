@@ -96,7 +96,7 @@ def get_parser():
     p.add_argument("--momentum-correction", action="store_true",
                    help="DGC momentum correction: the velocity lives in the EF residual and the "
                         "optimizer runs without momentum")
-    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "sparse-capped", "dense", "indexfree"])
+    p.add_argument("--wire", default="auto", choices=["auto", "sparse", "sparse-exact", "sparse-capped", "dense", "indexfree", "qrs"])
     p.add_argument("--epochs", type=int, default=None, help="stop after this many epochs")
     p.add_argument("--synthetic-size", type=int, default=None,
                    help="synthetic train images per phase (default 64 batches)")
@@ -496,6 +496,8 @@ def validate(run, val_loader, model, criterion, epoch, start_time):
     args = run.args
     timer = TimeMeter()
     losses, top1, top5 = AverageMeter(), AverageMeter(), AverageMeter()
+    if hasattr(model, "sync_buffers"):
+        model.sync_buffers()              # collective, before any rank's (possibly empty) shard
     model.eval()
     t0 = time.time()
     for i, (inp, target) in enumerate(val_loader):
@@ -696,7 +698,9 @@ def main(argv=None):
         is_best = top5 > best_top5
         best_top5 = max(top5, best_top5)
         # every rank takes part: the error-feedback residuals are per rank (a collective
-        # gathers them to the checkpoint writer)
+        # gathers them to the checkpoint writer); the BN buffers saved are rank 0's, synced
+        if hasattr(model, "sync_buffers"):
+            model.sync_buffers()
         comp = model.compression_state() if args.extra_ckpt and \
             hasattr(model, "compression_state") else None
         if args.local_rank == 0 and run.is_master:

@@ -16,11 +16,15 @@ Reported per configuration (one JSON line):
   method none): forward, backward and SGD only; both timed in alternating windows (3 rounds,
   medians) in one process;
 * ``exposed_ms`` / ``exposed_pct`` — their difference, as a share of the simulated step: the
-  compression / decode work not hidden behind backward plus the in-memory exchange. The xGMI
-  transfer itself is not in it: ``xgmi_model_ms`` prices the last bucket's exchange (the one that
-  cannot overlap backward) with a link model — ``link_gbs`` GB/s per xGMI link, one link per peer
-  (MI355X: 7 links per GPU, full mesh), all-gather = payload / link, all-reduce (direct
-  reduce-scatter + all-gather) = 2 · bytes / (W · link), plus ``latency_us`` per collective;
+  compression / decode work not hidden behind backward plus the exchange. With ``wire=True``
+  (``bench.py --sim-wire``) every collective also pays its modelled xGMI transfer time as a busy
+  kernel on ``cus`` workgroups (``parallel/loopback.py WireModel``: ``link_gbs`` GB/s per xGMI
+  link, one link per peer — MI355X: 7 links per GPU, full mesh — all-gather = payload / link,
+  all-reduce = 2 · bytes / (W · link), grouped send/recv = largest message / link, plus
+  ``latency_us`` each), so the exposure includes the wire wherever the step's schedule leaves it
+  exposed; ``overlap`` picks the captured step's exchange placement (engine
+  ``set_graph_overlap``). Without the wire, ``xgmi_model_ms`` prices the last bucket's exchange
+  separately;
 * per-bucket ``compress_us`` / ``decode_us`` of one eager step (HIP events on the side stream).
 
 Reference the mechanism replaces: ``CIFAR10/core.py:227-301`` (entire-model exchange),
@@ -34,6 +38,7 @@ import torch
 
 LINK_GBS = 100.0          # effective xGMI GB/s per link and direction assumed by the model
 LATENCY_US = 15.0         # per collective
+WIRE_CUS = 16             # workgroups a simulated transfer keeps busy (RCCL channels)
 
 
 def _time(step: Callable[[], None], warmup: int, steps: int) -> float:
@@ -61,12 +66,26 @@ def _alternate(step_a: Callable[[], None], step_b: Callable[[], None], warmup: i
     return statistics.median(ta), statistics.median(tb)
 
 
-def _frozen_peers(engine, world: int, seed: int = 0, scale: float = 1e-3):
-    from ..parallel.loopback import attach_loopback
+def _frozen_peers(engine, world: int, seed: int = 0, scale: float = 1e-3, wire: bool = False,
+                  overlap: str = "auto"):
+    from ..parallel.loopback import WireModel, attach_loopback
     g = torch.Generator(device=engine.device).manual_seed(seed)
     peers = [torch.randn(engine.arena.numel, device=engine.device, generator=g) * scale
              for _ in range(world - 1)]
-    return attach_loopback(engine, peers, frozen=True)
+    wm = WireModel(LINK_GBS, LATENCY_US, WIRE_CUS) if wire else None
+    lb = attach_loopback(engine, peers, frozen=True, wire_model=wm)
+    engine.set_graph_overlap(overlap)
+    return lb
+
+
+def _wire_fields(lb, engine, overlap: str) -> Dict:
+    wm = lb.wire_model
+    out = {"overlap_mode": engine.graph_overlap_mode(), "overlap_requested": overlap,
+           "wire_priced": wm is not None}
+    if wm is not None:
+        out["wire_model"] = {"gbs_per_link": wm.link_gbs, "latency_us": wm.latency_us,
+                             "cus": wm.cus}
+    return out
 
 
 def xgmi_model_ms(codec, payload_bytes: int, world: int, link_gbs: float = LINK_GBS,
@@ -76,6 +95,8 @@ def xgmi_model_ms(codec, payload_bytes: int, world: int, link_gbs: float = LINK_
         return 0.0
     if codec.collective == "all_gather":
         t = payload_bytes / (link_gbs * 1e9)
+    elif codec.collective == "quant_rs":            # two grouped send/recv phases of ~1/W each
+        t = payload_bytes / ((world - 1) * link_gbs * 1e9)
     else:
         t = 2.0 * payload_bytes / (world * link_gbs * 1e9)
     return (t + latency_us * 1e-6) * 1e3
@@ -91,6 +112,7 @@ def _engine_report(engine, world: int, bucket_us: List[dict]) -> Dict:
             "wire_bytes_per_rank": int(engine.stats.payload_bytes),
             "recv_bytes_per_rank": int(sum(
                 (world - 1) * c.last_payload_bytes if c.collective == "all_gather" else
+                c.last_payload_bytes if c.collective == "quant_rs" else
                 2 * (world - 1) * c.last_payload_bytes // world for c in engine.codecs)),
             "last_bucket_payload_bytes": pay,
             "xgmi_model_ms_last_bucket": round(xgmi_model_ms(codec, pay, world), 4),
@@ -104,7 +126,8 @@ def simulate_imagenet(world: int, device, steps: int = 10, warmup: int = 6, mode
                       compress="layerwise", method="Topk", K=0.001, qstates=255,
                       error_feedback=False, batch=256, image_size=224, dtype="bf16",
                       bucket_mb=50.0, wire="auto", dense_below=0,
-                      momentum_correction=False) -> Dict:
+                      momentum_correction=False, sim_wire: bool = False,
+                      overlap: str = "auto") -> Dict:
     from .imagenet import build_trainer
     dev = torch.device(device)
     g = torch.Generator(device=dev).manual_seed(1234)
@@ -119,7 +142,7 @@ def simulate_imagenet(world: int, device, steps: int = 10, warmup: int = 6, mode
                        dense_below=dense_below, momentum_correction=momentum_correction,
                        **common)
     eng = tr.ddp.engine
-    _frozen_peers(eng, world)
+    lb = _frozen_peers(eng, world, wire=sim_wire, overlap=overlap)
     t_base, t_sim = _alternate(lambda: base.step(x, t), lambda: tr.step(x, t), warmup, steps)
     del base
     torch.cuda.empty_cache()
@@ -139,6 +162,7 @@ def simulate_imagenet(world: int, device, steps: int = 10, warmup: int = 6, mode
            "img_per_s_per_gpu": round(batch / t_sim * 1e3, 1),
            "hip_graph": replays >= steps, "wire": wire,
            "link_model": {"gbs_per_link": LINK_GBS, "latency_us": LATENCY_US}}
+    out.update(_wire_fields(lb, eng, overlap))
     out.update(_engine_report(eng, world, bucket_us))
     del tr
     torch.cuda.empty_cache()
@@ -146,7 +170,7 @@ def simulate_imagenet(world: int, device, steps: int = 10, warmup: int = 6, mode
 
 
 def simulate_cifar(world: int, device, name: str, cfg: Dict, steps: int = 30,
-                   warmup: int = 8) -> Dict:
+                   warmup: int = 8, sim_wire: bool = False, overlap: str = "auto") -> Dict:
     from .cifar_fast import CifarTrainer
     dev = torch.device(device)
     base = CifarTrainer(device=dev, n_train=512 * 12, graph=True, network=cfg["network"],
@@ -155,7 +179,7 @@ def simulate_cifar(world: int, device, name: str, cfg: Dict, steps: int = 30,
     tr = CifarTrainer(device=dev, n_train=512 * 12, graph=True, world_size=world, **cfg)
     tr.graphed.warmup = 2
     eng = tr.ddp.engine
-    _frozen_peers(eng, world)
+    lb = _frozen_peers(eng, world, wire=sim_wire, overlap=overlap)
     t_base, t_sim = _alternate(lambda: base.step(), lambda: tr.step(), warmup, steps)
     del base
     torch.cuda.empty_cache()
@@ -174,5 +198,6 @@ def simulate_cifar(world: int, device, name: str, cfg: Dict, steps: int = 30,
            "img_per_s_per_gpu": round(tr.bs / t_sim * 1e3, 1),
            "hip_graph": replays >= steps,
            "link_model": {"gbs_per_link": LINK_GBS, "latency_us": LATENCY_US}}
+    out.update(_wire_fields(lb, eng, overlap))
     out.update(_engine_report(eng, world, bucket_us))
     return out

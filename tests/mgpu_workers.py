@@ -164,13 +164,19 @@ def exchange_vs_oracle(rank, world, dev, mode, method, ef, kw, steps=3):
             # exchange and the rank-ordered dequantise-and-average (encoding: test_kernels_gpu)
             from layer_wise_aaai20_amd.compress.codecs import make_codec
             exp = torch.zeros(eng.arena.numel)
+            # the quantised reduce-scatter wire: the all-gather decode of the same codes, rounded
+            # to bf16 (the wire's shard all-gather) — bit for bit
+            ckw = dict(eng.codec_kw)
+            qrs = ckw.get("wire") == "qrs"
+            if qrs:
+                ckw["wire"] = "sparse"
             for bi, (b, plan) in enumerate(zip(eng.buckets, eng.plans)):
                 sl = slice(b.start, b.end)
                 pays = _gather_cpu(sent[bi].to(dev))
-                cod = make_codec(method, plan, world, rank, **eng.codec_kw)
+                cod = make_codec(method, plan, world, rank, **ckw)
                 part = torch.zeros(b.end - b.start)
                 cod.decompress(pays[rank], torch.cat(pays), part)
-                exp[sl] = part
+                exp[sl] = part.to(torch.bfloat16).float() if qrs else part
             errs.append(float((got.cpu() - exp).abs().max()))
             tol = 1e-6 * float(exp.abs().max())
         elif method in ("Topk", "Thresholdv"):

@@ -167,13 +167,22 @@ def test_make_codec_factory_and_auto_wire():
     assert isinstance(codecs.make_codec("QSGD", plan, 2, 0, qstates=255), codecs.QSGDCodec)
     assert isinstance(codecs.make_codec("Topk", plan, 2, 0, K=0.01, wire="dense"),
                       codecs.DenseWrap)
-    # quantisers: codes all-gathered while bytes/element x world <= 8 (all-reduce of the
-    # dequantised fp32 vector past that)
-    for q, w_dense in ((255, 8), (32767, 8), (127, 16)):
+    # quantisers: the wire that brings each rank the fewest bytes — code all-gather (W-1)·b,
+    # quantised reduce-scatter (W-1)/W·(b+2), fp32 all-reduce 2(W-1)/W·4 (never the cheapest)
+    for q in (255, 32767, 127):
         for w in (2, 4, 8, 16):
             c = codecs.make_codec("QSGD", plan, w, 0, qstates=q)
-            assert isinstance(c, codecs.DenseWrap) == (w >= w_dense), (q, w, c)
-    assert isinstance(codecs.make_codec("TernGrad", plan, 16, 0), codecs.TernGradCodec)
+            b = (c.inner if isinstance(c, codecs.QuantRSCodec) else c).words * 4 / plan.numel
+            want_rs = (w - 1) / w * (b + 2) < (w - 1) * b
+            assert isinstance(c, codecs.QuantRSCodec) == want_rs, (q, w, c)
+            assert not isinstance(c, codecs.DenseWrap)
+    assert isinstance(codecs.make_codec("QSGD", plan, 8, 0, qstates=255), codecs.QuantRSCodec)
+    assert isinstance(codecs.make_codec("QSGD", plan, 2, 0, qstates=255), codecs.QSGDCodec)
+    assert isinstance(codecs.make_codec("TernGrad", plan, 8, 0), codecs.TernGradCodec)
+    assert isinstance(codecs.make_codec("TernGrad", plan, 16, 0), codecs.QuantRSCodec)
+    assert isinstance(codecs.make_codec("TernGrad", plan, 2, 0, wire="qrs"), codecs.QuantRSCodec)
+    with pytest.raises(ValueError):
+        codecs.make_codec("Topk", plan, 2, 0, K=0.01, wire="qrs")
     assert isinstance(codecs.make_codec("QSGD", plan, 8, 0, qstates=255, wire="sparse"),
                       codecs.QSGDCodec)
 

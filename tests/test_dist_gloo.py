@@ -207,3 +207,82 @@ def test_threshold_count_exchange():
     assert c0 == c1 == [0, 20, 20]
     assert torch.equal(o0, o1)
     assert torch.equal(o0[:10], torch.ones(10)) and torch.equal(o0[10:20], torch.full((10,), .5))
+
+
+def _w_qrs(rank, world, mode, method, kw, steps):
+    """The quantised reduce-scatter wire (codecs.QuantRSCodec) against the code all-gather wire
+    on identical replicas: same codes (same Philox streams), so every step's averaged gradient is
+    the all-gather wire's fp32 mean rounded to bf16, on every rank."""
+    from layer_wise_aaai20_amd.compress.codecs import QuantRSCodec
+    from layer_wise_aaai20_amd.models import cifar
+    from layer_wise_aaai20_amd.parallel.ddp import CompressedDDP
+    torch.manual_seed(0)
+    ma, mb = cifar.build_network("resnet9"), cifar.build_network("resnet9")
+    mb.load_state_dict(ma.state_dict())
+    qa = CompressedDDP(ma, compress=mode, method=method, wire="qrs", bucket_cap_mb=1,
+                       flat_params=False, **kw)
+    ga = CompressedDDP(mb, compress=mode, method=method, wire="sparse", bucket_cap_mb=1,
+                       flat_params=False, **kw)
+    assert all(isinstance(c, QuantRSCodec) for c in qa.engine.codecs)
+    out = []
+    for s in range(steps):
+        b = _batch(rank * 10 + s)
+        for d in (qa, ga):
+            d.module.zero_grad()
+            d(b)["loss"].sum().backward()
+        got = [p.grad.detach().clone() for p in ma.parameters()]
+        exp = [p.grad.detach().to(torch.bfloat16).float() for p in mb.parameters()]
+        out.append((got, exp))
+    return out, qa.engine.stats.payload_bytes, ga.engine.stats.payload_bytes
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("mode,method,kw", [("entiremodel", "RandomDithering", {"qstates": 255}),
+                                            ("layerwise", "TernGrad", {}),
+                                            ("layerwise", "RandomDithering", {"qstates": 4000})])
+def test_quantised_reduce_scatter_wire(world, mode, method, kw):
+    res = run_world(_w_qrs, world, (mode, method, kw, 2))
+    for steps, pay_qrs, pay_ag in res:
+        for got, exp in steps:
+            for a, e in zip(got, exp):
+                assert torch.equal(a, e), (a - e).abs().max()
+        if world > 2 and kw.get("qstates") == 255:         # QSGD-255: fewer bytes than the
+            assert pay_qrs < pay_ag * (world - 1)          # code all-gather from 3 ranks on
+    for s in range(2):                                    # identical on every rank
+        for r in res[1:]:
+            for a, b in zip(res[0][0][s][0], r[0][s][0]):
+                assert torch.equal(a, b)
+
+
+def _w_buffer_sync(rank, world, sync):
+    from layer_wise_aaai20_amd.models import cifar
+    from layer_wise_aaai20_amd.parallel.ddp import CompressedDDP
+    torch.manual_seed(0)
+    m = cifar.build_network("resnet9")
+    ddp = CompressedDDP(m, compress="layerwise", method="Topk", K=0.01, buffer_sync=sync,
+                        flat_params=False)
+    for s in range(3):
+        ddp(_batch(rank * 10 + s))["loss"].sum().backward()
+    bufs = lambda: [b.detach().clone() for b in m.buffers() if b.is_floating_point()]  # noqa
+    before = bufs()
+    ddp.sync_buffers()
+    after = bufs()
+    ddp.eval()
+    ddp(_batch(99))
+    return before, after, bufs()
+
+
+def test_lazy_buffer_sync_matches_per_step_broadcast():
+    """BN running statistics are broadcast where they are read (evaluation,
+    checkpoints), not before every training forward. Rank 0's buffers — the ones every rank holds
+    at those points — are the reference's per-forward-broadcast values exactly."""
+    lazy = run_world(_w_buffer_sync, 2, ("lazy",))
+    step = run_world(_w_buffer_sync, 2, ("step",))
+    (b0, a0, e0), (b1, a1, e1) = lazy
+    assert any(not torch.equal(x, y) for x, y in zip(b0, b1))     # rank-local during training
+    for x, y in zip(a0, a1):
+        assert torch.equal(x, y)                                  # synced to rank 0's
+    for x, y in zip(a0, step[0][1]):
+        assert torch.equal(x, y)                                  # = the reference's values
+    for x, y in zip(e0, e1):
+        assert torch.equal(x, y)

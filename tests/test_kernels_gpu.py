@@ -366,3 +366,74 @@ def test_kc_pack_step_batch_follows_weight_updates():
     finally:
         CV.kc_end_step()
         CV._KC.update(reg={}, cache={}, used=set())
+
+
+@pytest.mark.parametrize("method,q", [("QSGD", 127), ("QSGD", 255), ("QSGD", 4000),
+                                      ("TernGrad", None)])
+@pytest.mark.parametrize("align", [64, 1])
+def test_dequant_shard_matches_cpu_mirror(method, q, align):
+    """k_dequant_shard (quantised reduce-scatter receive side) vs the CPU mirror, bit for bit, on
+    CPU-made payloads of 5 ranks: every shard's bf16 mean, and the assembled bucket image expanded
+    by k_bf16_expand equals the all-gather decode rounded to bf16."""
+    W = 5
+    plan, N = make_plan(SIZES, align)
+    cs = [codecs.make_codec(method, plan, W, r, qstates=q, wire="qrs", seed=9) for r in range(W)]
+    pays = [c.compress(rand_grad(N, 40 + r), None, 3).clone() for r, c in enumerate(cs)]
+    img_c = torch.zeros(cs[0].n, dtype=torch.bfloat16)
+    img_g = torch.zeros(cs[0].n, dtype=torch.bfloat16, device="cuda")
+    for r, c in enumerate(cs):
+        r1 = torch.zeros(W * c.wpr[r], dtype=torch.int32)
+        rows = r1.view(W, -1)
+        for p in range(W):
+            for d, x in zip(c.piece_slots(rows[p], r), c.pieces(pays[p], r)):
+                d.copy_(x)
+        c.reduce_shard(r1, r, img_c)
+        c.reduce_shard(r1.cuda(), r, img_g)
+    assert torch.equal(img_c, img_g.cpu())
+    ag = codecs.make_codec(method, plan, W, 0, qstates=q, wire="sparse", seed=9)
+    ref16 = torch.zeros(N)
+    ag.decompress(None, torch.cat(pays), ref16, world=W)
+    out = torch.zeros(N, device="cuda")
+    cs[0].decompress(None, img_g, out)
+    assert torch.equal(out.cpu(), ref16.to(torch.bfloat16).float())
+
+
+def test_wire_wait_holds_the_stream():
+    """The loopback wire model's busy kernel (k_wire_wait) lasts at least the requested time."""
+    from layer_wise_aaai20_amd.ops._ext import load
+    lib = load()
+    dev = torch.empty(0, device="cuda")
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    lib.wire_wait(dev, 50.0, 16)
+    a.record()
+    lib.wire_wait(dev, 300.0, 16)
+    b.record()
+    b.synchronize()
+    ms = a.elapsed_time(b)
+    assert 0.29 <= ms < 5.0, ms
+
+
+def test_splitk_discard_drops_queued_reduces():
+    """split-K reduces queued by a step that never reached its flush are dropped
+    (splitk_discard) instead of being added into the next step's arena."""
+    from layer_wise_aaai20_amd.ops import _ext
+    from layer_wise_aaai20_amd.ops.block import gemm
+    lib = _ext.load()
+    torch.manual_seed(0)
+    M, N, K = 128, 256, 8192
+    a = torch.randn(K, M, device="cuda", dtype=torch.bfloat16)
+    b = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
+    dst = torch.zeros(M, N, device="cuda")
+    _ext.set_splitk_defer(dst, True)
+    try:
+        gemm(a, M, False, b, N, False, M, N, K, out_bf16=False, out=dst, accumulate=True,
+             split_k=True)
+    finally:
+        _ext.set_splitk_defer(dst, False)
+    if _ext.splitk_pending() == 0:
+        pytest.skip("the tuner picked an unsplit tile: nothing was deferred")
+    assert _ext.splitk_discard(dst) >= 1
+    assert _ext.splitk_pending() == 0
+    assert int(lib.splitk_flush(dst)) == 0
+    torch.cuda.synchronize()
+    assert float(dst.abs().max()) == 0.0            # nothing was reduced into the target

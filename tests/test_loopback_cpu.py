@@ -53,13 +53,20 @@ def test_loopback_world4(method, kw, mode, ef):
         eng.sync_now()
         got = eng.arena.grad.clone()
         kinds = {c[0] for c in lb.calls}
-        assert [c[1] for c in lb.calls] == list(range(len(eng.buckets)))
-        assert len(kinds) == 1
+        # (the quantised reduce-scatter wire: two grouped send/recv phases per bucket)
+        per = 2 if kinds == {"send_recv1", "send_recv2"} else 1
+        assert [c[1] for c in lb.calls] == [b for b in range(len(eng.buckets))
+                                             for _ in range(per)]
+        assert len(kinds) == per
         raw = [g0] + peers
         if ef:
             e_new = [eng.ef] + lb.sim.ef
             sent = sum(raw[r] + e_old[r] - e_new[r] for r in range(W)) / W
-            torch.testing.assert_close(got, sent, rtol=1e-5, atol=1e-6)
+            if per == 2:                                 # bf16-rounded mean on that wire
+                torch.testing.assert_close(got, sent.to(torch.bfloat16).float(),
+                                           rtol=2 ** -7, atol=1e-6)
+            else:
+                torch.testing.assert_close(got, sent, rtol=1e-5, atol=1e-6)
             assert float(eng.ef.abs().sum()) > 0 or method == "none"
         elif method in ("none", "Topk", "Thresholdv", "AdaptiveThreshold"):
             exp = torch.zeros_like(got)
@@ -110,3 +117,52 @@ def test_fixed_capacity_threshold_wire(method, kw, density, monkeypatch):
         res[wire] = eng.arena.grad.clone()
     if density == 1.0:
         torch.testing.assert_close(res["sparse-capped"], res["dense"], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("mode", ["layerwise", "entiremodel"])
+@pytest.mark.parametrize("method,kw", [("RandomDithering", {"qstates": 255}), ("TernGrad", {}),
+                                       ("RandomDithering", {"qstates": 4000})])
+@pytest.mark.parametrize("world", [4, 8])
+def test_loopback_quantised_reduce_scatter(method, kw, mode, world):
+    """The quantised reduce-scatter wire at a simulated world of 4 / 8: the decoded arena is
+    the code all-gather wire's mean rounded to bf16 (same codes: same Philox streams), the
+    exchange is two grouped send/recv phases per bucket, and it moves fewer bytes than the
+    all-gather of codes whenever the factory picks it."""
+    from layer_wise_aaai20_amd.compress.codecs import QuantRSCodec
+    engs, lbs = [], []
+    for wire in ("qrs", "sparse"):
+        e = GradSyncEngine(_params(), mode=mode, method=method, bucket_cap_mb=0.01,
+                           world_size=world, wire=wire, **kw)
+        peers = [_grads(e, 100 + r) for r in range(1, world)]
+        lbs.append(attach_loopback(e, peers))
+        engs.append(e)
+    assert all(isinstance(c, QuantRSCodec) for c in engs[0].codecs)
+    g0 = _grads(engs[0], 100)
+    for step in range(2):
+        for e, lb in zip(engs, lbs):
+            e.arena.grad.copy_(g0)
+            lb.calls.clear()
+            e.sync_now()
+        q, a = engs[0].arena.grad, engs[1].arena.grad
+        assert torch.equal(q, a.to(torch.bfloat16).float()), (q - a).abs().max()
+        assert [c[0] for c in lbs[0].calls] == ["send_recv1", "send_recv2"] * len(engs[0].buckets)
+    if method == "RandomDithering" and kw["qstates"] == 255 and mode == "entiremodel":
+        assert engs[0].stats.payload_bytes < engs[1].stats.payload_bytes * (world - 1)
+
+
+def test_graph_overlap_auto_mode():
+    """LWAAAI_GRAPH_OVERLAP=auto: exchange on the side branch only with a (simulated-wire or
+    real) communicator at world > 1; inline at world 1 and for the wire-less loopback."""
+    from layer_wise_aaai20_amd.parallel.loopback import WireModel
+    e1 = GradSyncEngine(_params(), mode="layerwise", method="Topk", K=0.05)
+    assert e1.graph_overlap_mode() == "0"
+    e = GradSyncEngine(_params(), mode="layerwise", method="Topk", K=0.05, world_size=4)
+    lb = attach_loopback(e, [_grads(e, 100 + r) for r in range(1, 4)])
+    assert e.graph_overlap_mode() == "0"
+    lb.wire_model = WireModel()
+    e.set_graph_overlap("auto")
+    assert e.graph_overlap_mode() == "1"
+    e.set_graph_overlap("comm")
+    assert e.graph_overlap_mode() == "comm"
+    with pytest.raises(ValueError):
+        e.set_graph_overlap("sideways")

@@ -43,13 +43,17 @@ def _engine(mode, method, ef, **kw):
 
 CASES = [("layerwise", "Topk", False, {"K": 0.001}),
          ("layerwise", "Topk", True, {"K": 0.001}),
+         # world 8 QSGD-255: the quantised reduce-scatter wire (auto) and the code all-gather
          ("entiremodel", "RandomDithering", True, {"qstates": 255}),
+         ("entiremodel", "RandomDithering", True, {"qstates": 255, "wire": "sparse"}),
+         ("layerwise", "TernGrad", False, {"wire": "qrs"}),
          ("entiremodel", "Randomk", True, {"K": 0.01}),
          ("none", "none", False, {})]
 
 
 @pytest.mark.parametrize("mode,method,ef,kw", CASES,
-                         ids=[f"{c[1]}-{c[0]}-{'ef' if c[2] else 'noef'}" for c in CASES])
+                         ids=[f"{c[1]}-{c[0]}-{'ef' if c[2] else 'noef'}"
+                              f"{'-' + c[3]['wire'] if 'wire' in c[3] else ''}" for c in CASES])
 def test_captured_world8_exchange(mode, method, ef, kw):
     steps = 5
     local = []
@@ -88,15 +92,24 @@ def test_captured_world8_exchange(mode, method, ef, kw):
     (re_, calls_e, nb, raw_peers, eng), (rg, _, _, _, _) = runs[False], runs[True]
     for i in range(steps):                                   # captured == eager, bit for bit
         assert torch.equal(re_[i][0], rg[i][0]), (i, (re_[i][0] - rg[i][0]).abs().max().item())
-    # eager: one collective per bucket per step, in bucket order
-    assert [c[1] for c in calls_e] == list(range(nb)) * steps
+    # eager: one exchange per bucket per step, in bucket order (the quantised reduce-scatter
+    # wire: two grouped send/recv phases, and a bf16-rounded mean)
+    qrs = any(c[0].startswith("send_recv") for c in calls_e)
+    per = 2 if qrs else 1
+    assert [c[1] for c in calls_e] == [b for b in range(nb) for _ in range(per)] * steps
     for i in range(steps):
         got, e_old, e_new = re_[i]
         raw = [local[i]] + raw_peers
         if ef:
             sent = sum(raw[r] + e_old[r] - e_new[r] for r in range(W)) / W
             # (g + e_old) - e_new re-rounds each rank's contribution in fp32: ulp-level slack
-            torch.testing.assert_close(got, sent, rtol=1e-5, atol=1e-6)
+            if qrs:
+                torch.testing.assert_close(got, sent.to(torch.bfloat16).float(), rtol=2 ** -7,
+                                           atol=1e-6)
+            else:
+                torch.testing.assert_close(got, sent, rtol=1e-5, atol=1e-6)
+        elif qrs:
+            assert torch.isfinite(got).all()            # (the codes: test_kernels_gpu)
         elif method == "Topk":
             exp = torch.zeros_like(got)
             for r in range(W):

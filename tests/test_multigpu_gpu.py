@@ -58,7 +58,10 @@ CASES = [("layerwise", "Topk", False, {"K": 0.001}),
          ("layerwise", "Randomk", True, {"K": 0.01}),          # index-free all-reduce + EF
          ("layerwise", "Thresholdv", False, {"V": 1e-2, "wire": "sparse"}),   # count exchange
          ("layerwise", "TernGrad", False, {}),
-         ("entiremodel", "Topk", True, {"K": 0.001})]
+         ("entiremodel", "Topk", True, {"K": 0.001}),
+         # the quantised reduce-scatter wire (grouped RCCL send/recv)
+         ("entiremodel", "RandomDithering", False, {"qstates": 255, "wire": "qrs"}),
+         ("layerwise", "TernGrad", False, {"wire": "qrs"})]
 IDS = [f"{c[1]}-{c[0]}-{'ef' if c[2] else 'noef'}{'-' + c[3]['wire'] if 'wire' in c[3] else ''}"
        for c in CASES]
 # the exact sparse threshold wire agrees its payload size by a count all-reduce read on the host

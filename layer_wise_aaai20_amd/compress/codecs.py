@@ -1034,8 +1034,7 @@ def make_codec(method, plan: SegPlan, world: int, rank: int, K=None, V=None, qst
         # stay in the error-feedback residual — dropped without EF)
         dens = None
         if wire == "sparse-capped" or max_density is not None:
-            dens = float(max_density if max_density is not None else
-                         os.environ.get("LWAAAI_THRESH_DENSITY", "0.05"))
+            dens = float(max_density if max_density is not None else 0.05)
             if not error_feedback and rank == 0:
                 import warnings
                 msg = (f"{method} on the capped sparse wire without error feedback: hits beyond "

@@ -1040,33 +1040,17 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn_bwd_dual(
 // EPI_BSTATS operands (see lw_kernels.h GemmArgs): the BN input x laid out like the output rows
 // ([out_rows][N], ldc == N), its batch mean, and the ReLU mask source — the BN output's bitmap or
 // the BN's scale/shift (mask = x*scale+shift > 0).
+// The backward-statistics epilogue (gemm_core.h EPI_BSTATS: a data-gradient GEMM also reducing
+// the BatchNorm backward it feeds) lost 3.3 % of the ResNet-50 step twice
+// (profiles/r2_bstats_ab.log, profiles/r3s2/bstats_cross_ab.txt) and is no longer instantiated:
+// the bst_* arguments must be left unset.
 static void set_bstats(lw::GemmArgs& g, const c10::optional<Tensor>& bx,
                        const c10::optional<Tensor>& bmean, const c10::optional<Tensor>& bss,
                        const c10::optional<Tensor>& bbits, int64_t out_rows, int64_t N,
                        int64_t ldc, bool out_bf16) {
-  if (!(bx.has_value() && bx->defined())) return;
-  TORCH_CHECK(out_bf16 && ldc == N && N % 8 == 0,
-              "backward statistics need a bf16 output with ldc == N and N % 8 == 0");
-  check_dtype(*bx, kH16, "bst_x");
-  TORCH_CHECK(bx->is_cuda() && (bx->is_contiguous() ||
-              bx->is_contiguous(at::MemoryFormat::ChannelsLast)) && bx->numel() >= out_rows * N,
-              "bst_x must be a dense [rows, N] bf16 tensor");
-  check_aligned16(bx->data_ptr(), "bst_x");
-  TORCH_CHECK(bmean.has_value() && bmean->defined() && bmean->numel() >= N, "bst_mean [N]");
-  check_dtype(*bmean, at::kFloat, "bst_mean");
-  g.bst_x = ptr<uint16_t>(*bx);
-  g.bst_mean = ptr<float>(*bmean);
-  if (bbits.has_value() && bbits->defined()) {
-    TORCH_CHECK(bbits->scalar_type() == at::kByte && bbits->numel() * 8 >= out_rows * N,
-                "bst_bits: uint8 bitmap of the [rows, N] BN output");
-    g.bst_bits = ptr<uint8_t>(*bbits);
-  } else {
-    TORCH_CHECK(bss.has_value() && bss->defined() && bss->numel() == 2 * N && bss->is_contiguous(),
-                "bst_scale_shift: the BN's [2N] scale/shift (mask = x*scale+shift > 0)");
-    check_dtype(*bss, at::kFloat, "bst_scale_shift");
-    g.bst_scale = ptr<float>(*bss);
-    g.bst_shift = g.bst_scale + N;
-  }
+  (void)g; (void)bmean; (void)bss; (void)bbits; (void)out_rows; (void)N; (void)ldc; (void)out_bf16;
+  TORCH_CHECK(!(bx.has_value() && bx->defined()),
+              "the backward-statistics GEMM epilogue was removed in round 6 (it lost 3.3 %)");
 }
 
 // fp32 slab sets whose split-K reduce was deferred (gemm.hip splitk_flush): held until the flush
@@ -1096,9 +1080,8 @@ void splitk_defer(Tensor dev, bool on) {
 int64_t splitk_flush(Tensor dev) {
   const c10::DeviceGuard guard(dev.device());
   const int n = lw::splitk_flush(cur_stream());
-  // a slab allocated on another stream (LWAAAI_WGRAD_SIDE's weight-gradient stream) is read by
-  // the reduce just queued on this one: the allocator must not hand its memory out before that
-  // reduce has run
+  // a slab allocated on another stream is read by the reduce just queued on this one: the
+  // allocator must not hand its memory out before that reduce has run
   const auto fs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA();
   for (const Tensor& t : splitk_keep())
     c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(
@@ -1594,30 +1577,6 @@ std::tuple<Tensor, Tensor> stem_conv7(Tensor x, Tensor w) {
   return {y, st};
 }
 
-// Direct 3x3 / stride-1 / pad-1 convolution 64 -> 64 channels (conv.hip k_conv3_direct):
-// x [N, 64, H, W] bf16 channels_last, w the K-contiguous [64][576] operand ((r, s, ci) order);
-// returns (y [N, 64, H, W] channels_last, stats [N*H/8, 2, 64] or an empty tensor).
-std::tuple<Tensor, Tensor> conv3_direct(Tensor x, Tensor w, bool want_stats) {
-  const c10::DeviceGuard guard(x.device());
-  check_dtype(x, kH16, "x");
-  check_dtype(w, kH16, "w");
-  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 &&
-              x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: [N, 64, H, W] channels_last");
-  TORCH_CHECK(w.is_contiguous() && w.numel() == 64 * 576, "w: [64][576]");
-  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  TORCH_CHECK(lw::conv3_direct_ok((int)C, 64, (int)H, (int)W), "conv3_direct: unsupported geometry");
-  TORCH_CHECK(x.numel() * 2 < (1LL << 40), "conv3_direct size");
-  check_aligned16(x.data_ptr(), "x");
-  check_aligned16(w.data_ptr(), "w");
-  Tensor y = at::empty({N, 64, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  Tensor st = want_stats ? at::empty({N * H / 8, 2, 64}, x.options().dtype(at::kFloat))
-                         : at::empty({0}, x.options().dtype(at::kFloat));
-  lw::conv3_direct(ptr<uint16_t>(x), ptr<uint16_t>(w), ptr<uint16_t>(y),
-                   want_stats ? ptr<float>(st) : nullptr, (int)N, (int)H, (int)W, cur_stream());
-  launched("conv3_direct");
-  return {y, st};
-}
-
 // Tap-reuse 3x3 / stride-1 / pad-1 convolution (conv3tap.hip k_conv3_tap): x [N, C, H, W] bf16
 // channels_last, w the K-contiguous [Co][9C] operand ((r, s, ci) order; for a data gradient the
 // flipped, transposed weight); returns (y [N, Co, H, W] channels_last, stats [tiles_m, 2, Co] or
@@ -1685,30 +1644,6 @@ Tensor conv3_tap_wgrad(Tensor dy, Tensor x, c10::optional<Tensor> out, bool accu
 }
 
 // ---------------------------------------------------------------- BN pieces for fused blocks
-// Arrival tickets of the one-launch colsum + finalize (bn.hip k_colsum_finalize), one per 64-channel
-// slice: zeroed once per device (eagerly: never created inside a graph capture) and re-armed by the
-// kernel's last block. LWAAAI_COLSUM_FUSED=1 turns it on (default: the two-kernel path).
-static unsigned* colsum_tickets(const Tensor& like) {
-  static const bool on = [] {
-    const char* v = getenv("LWAAAI_COLSUM_FUSED");
-    return v && v[0] == '1';
-  }();
-  if (!on) return nullptr;
-  static std::mutex mu;
-  static std::map<int, Tensor> per_dev;
-  std::lock_guard<std::mutex> lock(mu);
-  const int dev = like.device().index();
-  auto it = per_dev.find(dev);
-  if (it == per_dev.end()) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(cur_stream(), &cs) != hipSuccess || cs != hipStreamCaptureStatusNone)
-      return nullptr;
-    Tensor t = at::zeros({kMaxBnC / 32 + 1}, like.options().dtype(at::kInt));
-    it = per_dev.emplace(dev, t).first;
-  }
-  return reinterpret_cast<unsigned*>(it->second.data_ptr());
-}
-
 // Batch statistics of x ([M, C] / channels_last), or — with `stats` [2, C, nb] from a GEMM's
 // column-statistics epilogue — only the finalize. Returns (mean, invstd, scale_shift[2C]).
 std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stats,
@@ -1747,9 +1682,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_stats(Tensor x, c10::optional<Tensor> stat
     TORCH_CHECK(stats->dim() == 3 && stats->size(1) == 2 && stats->size(2) == C &&
                 stats->is_contiguous(), "stats must be a contiguous [rows, 2, C] tensor");
     const int64_t R = stats->size(0);
-    a.tickets = colsum_tickets(x);
-    partial = at::empty({(int64_t)(a.tickets ? lw::colsum_fused_blocks(R) : lw::colsum_blocks(R)) *
-                         2 * C}, f32);
+    partial = at::empty({(int64_t)lw::colsum_blocks(R) * 2 * C}, f32);
     a.partial = ptr<float>(partial);
     a.stat_rows = ptr<float>(*stats);
     a.stats_rows_n = R;
@@ -2047,7 +1980,6 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "Tensor(a!)? dgamma_out=None, Tensor(b!)? dbeta_out=None, Tensor? stats_rows=None) "
       "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("stem_conv7(Tensor x, Tensor w) -> (Tensor, Tensor)");
-  m.def("conv3_direct(Tensor x, Tensor w, bool want_stats) -> (Tensor, Tensor)");
   m.def("conv3_tap(Tensor x, Tensor w, int Co, bool want_stats) -> (Tensor, Tensor)");
   m.def("conv3_tap_wgrad(Tensor dy, Tensor x, Tensor(a!)? out, bool accumulate) -> Tensor");
   m.def(
@@ -2127,7 +2059,6 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("bn_bwd", &bn_bwd);
   m.impl("bn_bwd_dual", &bn_bwd_dual);
   m.impl("stem_conv7", &stem_conv7);
-  m.impl("conv3_direct", &conv3_direct);
   m.impl("conv3_tap", &conv3_tap);
   m.impl("conv3_tap_wgrad", &conv3_tap_wgrad);
   m.impl("gemm", &gemm);

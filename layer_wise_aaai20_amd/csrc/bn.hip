@@ -298,96 +298,6 @@ __device__ __forceinline__ void finalize_fwd_channel(int c, double s, double q, 
   }
 }
 
-// Column statistics rows of a GEMM / conv epilogue [R][2C] -> the BatchNorm finalize in ONE launch
-// (opt-in, LWAAAI_COLSUM_FUSED=1: measured 0.25 ms per step SLOWER than k_colsum +
-// k_bn_finalize_fwd, profiles/r3s2/colsum_fused_ab.txt). The last block of a slice to arrive (an
-// agent-scope release / relaxed ticket / acquire, cdna_hip_programming.md §6 Guideline 16 — no
-// block ever waits) does the fold and finalize, then re-arms the slice's ticket. Block (x, y) sums rows
-// [x*rpb, (x+1)*rpb) of slice y's 64 columns (Σv and Σv² of 32 channels) with its 256 threads as
-// 4 row phases x 64 columns (fixed order, combined in LDS), and the slice's last-arriving block
-// folds the nb partials with all 256 threads (4 contiguous block ranges x 64 columns, fp64, fixed
-// order) before the finalize. nb ~ 2*sqrt(R) balances the two phases.
-constexpr int CS2_CH = 32;
-__global__ __launch_bounds__(256) void k_colsum_finalize2(
-    const float* __restrict__ rows, int64_t R, int C, int64_t rows_per_block,
-    float* __restrict__ partial, unsigned* __restrict__ tickets, int64_t M,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
-    float* __restrict__ rmean, float* __restrict__ rvar, float* __restrict__ mean_out,
-    float* __restrict__ invstd_out, float* __restrict__ scale, float* __restrict__ shift) {
-  __shared__ __attribute__((aligned(16))) double sh[4 * 64 + 1];   // one array: partial sums, flag
-  float* shf = reinterpret_cast<float*>(sh);
-  unsigned* sh_last = reinterpret_cast<unsigned*>(sh + 4 * 64);
-  const int nb = gridDim.x;
-  const int c0 = blockIdx.y * CS2_CH;
-  const int cs = min(CS2_CH, C - c0);
-  const int W = 2 * C;
-  const int cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const bool active = cl < 2 * cs;
-  const int col = cl < cs ? c0 + cl : C + c0 + (cl - cs);
-  {
-    const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-    const int64_t r1 = min(r0 + rows_per_block, R);
-    float a = 0.f;
-    if (active) {
-      int64_t r = r0 + ph;
-      for (; r + 12 < r1; r += 16) {      // 4 loads in flight, added in row order
-        const float v0 = rows[r * W + col], v1 = rows[(r + 4) * W + col];
-        const float v2 = rows[(r + 8) * W + col], v3 = rows[(r + 12) * W + col];
-        a += v0; a += v1; a += v2; a += v3;
-      }
-      for (; r < r1; r += 4) a += rows[r * W + col];
-    }
-    shf[ph * 64 + cl] = a;
-  }
-  __syncthreads();
-  if (threadIdx.x < 64 && active)
-    partial[(int64_t)col * nb + blockIdx.x] = ((shf[cl] + shf[64 + cl]) + shf[128 + cl]) + shf[192 + cl];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(tickets + blockIdx.y, 1u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    *sh_last = prev == (unsigned)(nb - 1) ? 1u : 0u;
-  }
-  __syncthreads();
-  if (*sh_last == 0u) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  // fold: thread (ph, cl) sums blocks [ph*q, (ph+1)*q) of column col in fp64, 8 loads in flight
-  double d = 0.0;
-  if (active) {
-    const int q = (nb + 3) / 4;
-    const int b0 = ph * q, b1 = min(nb, b0 + q);
-    const float* p = partial + (int64_t)col * nb;
-    int b = b0;
-    for (; b + 7 < b1; b += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[b + u];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) d += (double)v[u];
-    }
-    for (; b < b1; ++b) d += (double)p[b];
-  }
-  __syncthreads();                        // (shf is reused as the fp64 fold area)
-  sh[ph * 64 + cl] = d;
-  __syncthreads();
-  if (threadIdx.x < cs) {
-    const int c = threadIdx.x;
-    const double s = ((sh[c] + sh[64 + c]) + sh[128 + c]) + sh[192 + c];
-    const double qq = ((sh[cs + c] + sh[64 + cs + c]) + sh[128 + cs + c]) + sh[192 + cs + c];
-    finalize_fwd_channel(c0 + c, s, qq, M, gamma, beta, eps, momentum, rmean, rvar, mean_out,
-                         invstd_out, scale, shift);
-  }
-  if (threadIdx.x == 0)
-    __hip_atomic_store(tickets + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __global__ __launch_bounds__(256) void k_bn_finalize_fwd(
     const float* __restrict__ partial, int nblocks, int C, int64_t M,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float momentum,
@@ -545,14 +455,11 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, c
                                                       const float* __restrict__ B,
                                                       const float* __restrict__ Cc,
                                                       T* __restrict__ dx, T* __restrict__ dres,
-                                                      int64_t n8, int C, int rev) {
+                                                      int64_t n8, int C) {
   const int G = C / 8;
   const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
   const int64_t step = (int64_t)gridDim.x * BNT;
-  // rev: walk the rows last to first (element e = n8-1-i; n8 and step are multiples of G, so the
-  // channel group stays fixed per thread): the reduce pass just streamed the same dy / x first to
-  // last, so its most recent lines — the ones still in the 256 MB Infinity Cache — come first
-  const int c0 = (int)((rev ? n8 - 1 - t0 : t0) % G) * 8;
+  const int c0 = (int)(t0 % G) * 8;
   float ca[8], cb[8], cc[8], fs[8], fh[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -561,7 +468,7 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply(const T* __restrict__ x, c
     fh[k] = RELU == 2 ? fshift[c0 + k] : 0.f;
   }
   for (int64_t i0 = t0; i0 < n8; i0 += step) {
-    const int64_t i = rev ? n8 - 1 - i0 : i0;
+    const int64_t i = i0;
     const int64_t off = i * 8;
     float xv[8], d[8];
     V8<T>::load(x + off, xv);
@@ -592,11 +499,11 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply_dual(
     const uint16_t* __restrict__ dy, const uint8_t* __restrict__ bits,
     const float* __restrict__ A, const float* __restrict__ B, const float* __restrict__ Cc,
     const float* __restrict__ A2, const float* __restrict__ B2, const float* __restrict__ Cc2,
-    uint16_t* __restrict__ dx, uint16_t* __restrict__ dx2, int64_t n8, int C, int rev) {
+    uint16_t* __restrict__ dx, uint16_t* __restrict__ dx2, int64_t n8, int C) {
   const int G = C / 8;
   const int64_t t0 = (int64_t)blockIdx.x * BNT + threadIdx.x;
   const int64_t step = (int64_t)gridDim.x * BNT;
-  const int c0 = (int)((rev ? n8 - 1 - t0 : t0) % G) * 8;     // (rev: see k_bn_bwd_apply)
+  const int c0 = (int)(t0 % G) * 8;
   float ca[8], cb[8], cc[8], ca2[8], cb2[8], cc2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -604,7 +511,7 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply_dual(
     ca2[k] = A2[c0 + k]; cb2[k] = B2[c0 + k]; cc2[k] = Cc2[c0 + k];
   }
   for (int64_t i0 = t0; i0 < n8; i0 += step) {
-    const int64_t i = rev ? n8 - 1 - i0 : i0;
+    const int64_t i = i0;
     const int64_t off = i * 8;
     float xv[8], x2v[8], d[8];
     V8<uint16_t>::load(x + off, xv);
@@ -623,32 +530,20 @@ __global__ __launch_bounds__(BNT) void k_bn_bwd_apply_dual(
 }
 
 // ------------------------------------------------------------------------------------------
-// Tuning knobs (read once): rows unrolled per thread in the reduce loop, and the reduce grid size.
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
-// backward apply passes walk the rows last to first with LWAAAI_BN_REVERSE=1 (default: first to last)
-static bool bn_reverse() {
-  static const bool r = env_int("LWAAAI_BN_REVERSE", 0) != 0;
-  return r;
-}
-static int reduce_unroll() {
-  static const int u = env_int("LWAAAI_BN_UNROLL", 4);
-  return u;
-}
-
+// Geometry (measured constants; round 6 removed the environment knobs that tuned them).
 // Reduce grid: (row blocks) x (channel slices of Cb = 128 channels when C is a multiple of 128,
-// else the whole row). About LWAAAI_BN_BLOCKS workgroups in total; nblocks (row blocks) is the
-// number of partial sums per channel the finalize folds.
+// else the whole row), about kReduceBlocks workgroups in total; nblocks (row blocks) is the number
+// of partial sums per channel the finalize folds. 4 rows in flight per lane (8 measured slower:
+// profiles/r6/bn_stream_probe_a.txt, 143 vs 167 us at the layer-1 shape).
+constexpr int64_t kReduceBlocks = 512;
+constexpr int kReduceUnroll = 4;
 static int reduce_slices(int C) { return (C > 128 && C % 128 == 0) ? C / 128 : 1; }
 
 static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblocks) {
   const int nsl = reduce_slices(C);
   const int G = C / nsl / 8;
   const int R = BNT / G;
-  static const int64_t target = env_int("LWAAAI_BN_BLOCKS", 512);   // ≈ 4 blocks per CU
-  const int64_t rb = (target + nsl - 1) / nsl;
+  const int64_t rb = (kReduceBlocks + nsl - 1) / nsl;
   int64_t rpb = (M + rb - 1) / rb;
   rpb = (rpb + R - 1) / R * R;
   rpb = rpb < R ? R : rpb;
@@ -656,28 +551,12 @@ static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblo
   nblocks = (int)((M + rpb - 1) / rpb);
 }
 
-// GEMM statistics rows folded per block: a few rows each, so every block's loads are in flight at
-// once (the finalize then folds up to 1024 partials per channel with unrolled loads)
-// row blocks of the fused colsum + finalize: few enough that the last block's fold of a slice
-// (64 channels x 2 x nb partials) stays short
-int colsum_fused_blocks(int64_t rows) {
-  // ~2*sqrt(R) row blocks balance the row-sum phase against the last block's fold
-  static const int cap = env_int("LWAAAI_COLSUM_FUSED_BLOCKS", 256);
-  int nb = 2;
-  while ((int64_t)nb * nb < 4 * rows && nb < cap) ++nb;
-  return (int)(rows < nb ? rows : nb);
-}
-
-// statistics rows up to LWAAAI_COLSUM_DIRECT_MAX are folded by the finalize itself (0: always
-// k_colsum first)
-static int64_t colsum_direct_max() {
-  static const int v = env_int("LWAAAI_COLSUM_DIRECT_MAX", 1024);
-  return v;
-}
-int colsum_blocks(int64_t rows) {
-  static const int cap = env_int("LWAAAI_COLSUM_BLOCKS", 1024);
-  return (int)(rows < cap ? rows : cap);
-}
+// GEMM statistics rows folded by the finalize itself up to this many rows (k_colsum with one row
+// per block wrote exactly those values), else summed by k_colsum into at most kColsumBlocks
+// partials first
+constexpr int64_t kColsumDirectMax = 1024;
+constexpr int kColsumBlocks = 1024;
+int colsum_blocks(int64_t rows) { return (int)(rows < kColsumBlocks ? rows : kColsumBlocks); }
 
 int bn_reduce_blocks(int64_t M, int C) {
   int64_t rpb;
@@ -727,17 +606,6 @@ static void bn_apply_t(const BNArgs& a, hipStream_t st) {
 template <typename T>
 static void bn_stats_t(const BNArgs& a, hipStream_t st) {
   int nb = a.stats_blocks;
-  if (a.stat_rows && a.tickets) {         // rows -> statistics in one launch (k_colsum_finalize2)
-    const int64_t R = a.stats_rows_n;
-    int nbf = colsum_fused_blocks(R);
-    const int64_t rpb = (R + nbf - 1) / nbf;
-    nbf = (int)((R + rpb - 1) / rpb);
-    const int slices = (a.C + CS2_CH - 1) / CS2_CH;
-    hipLaunchKernelGGL(k_colsum_finalize2, dim3(nbf, slices), dim3(256), 0, st, a.stat_rows, R,
-                       a.C, rpb, a.partial, a.tickets, a.M, a.gamma, a.beta, a.eps, a.momentum,
-                       a.rmean, a.rvar, a.mean, a.invstd, a.scale, a.shift);
-    return;
-  }
   const float* part = a.partial;
   int rstride = 0;
   if (a.stat_rows) {                      // GEMM epilogue rows [R][2C] -> [2C][nb]
@@ -745,7 +613,7 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
     nb = colsum_blocks(R);
     const int64_t rpb = (R + nb - 1) / nb;
     nb = (int)((R + rpb - 1) / rpb);
-    if (R <= colsum_direct_max()) {
+    if (R <= kColsumDirectMax) {
       // few rows: the finalize folds the rows where they are, one launch fewer. Up to 1024 rows
       // k_colsum ran one row per block, so the sums are its own bit for bit (layers 3-4 of a
       // ResNet-50, 29 BatchNorms: 11,332-11,372 -> 11,439-11,465 img/s on one box; a cap of
@@ -760,7 +628,7 @@ static void bn_stats_t(const BNArgs& a, hipStream_t st) {
   } else if (nb <= 0) {
     int64_t rpb;
     reduce_geometry(a.M, a.C, rpb, nb);
-    auto kern = reduce_unroll() == 8 ? k_bn_reduce<T, 0, 0, 8> : k_bn_reduce<T, 0, 0, 4>;
+    auto kern = k_bn_reduce<T, 0, 0, kReduceUnroll>;
     hipLaunchKernelGGL(kern, dim3(nb, reduce_slices(a.C)), dim3(BNT), 0, st, static_cast<const T*>(a.x),
                        (const T*)nullptr, (const T*)nullptr, (const uint8_t*)nullptr,
                        (const float*)nullptr,
@@ -802,7 +670,7 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
                        a.partial);
   } else {
 #define LW_RED(R)                                                                                \
-  hipLaunchKernelGGL((reduce_unroll() == 8 ? k_bn_reduce<T, 1, R, 8> : k_bn_reduce<T, 1, R, 4>), \
+  hipLaunchKernelGGL((k_bn_reduce<T, 1, R, kReduceUnroll>),                                     \
                      dim3(nb, reduce_slices(a.C)), dim3(BNT), 0, st, x, dy, y, a.bits, a.mean, \
                      a.scale, a.shift, a.M, a.C, rpb, a.partial, (const T*)nullptr,      \
                      (const float*)nullptr, (float*)nullptr)
@@ -816,7 +684,7 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   const dim3 grid(apply_grid(n8, a.C, kApplyBwdGrid)), block(BNT);
 #define LW_BWD(R, D)                                                                            \
   hipLaunchKernelGGL((k_bn_bwd_apply<T, R, D>), grid, block, 0, st, x, dy, y, a.bits, a.scale,  \
-                     a.shift, a.A, a.B, a.Cc, dx, dres, n8, a.C, bn_reverse() ? 1 : 0)
+                     a.shift, a.A, a.B, a.Cc, dx, dres, n8, a.C)
   if (rmode == 3) { if (dres) LW_BWD(3, true); else LW_BWD(3, false); }
   else if (rmode == 1) { if (dres) LW_BWD(1, true); else LW_BWD(1, false); }
   else if (rmode == 2) { if (dres) LW_BWD(2, true); else LW_BWD(2, false); }
@@ -834,8 +702,7 @@ void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st) {
   const auto* x = static_cast<const uint16_t*>(a.x);
   const auto* x2 = static_cast<const uint16_t*>(b.x);
   const auto* dy = static_cast<const uint16_t*>(a.dy);
-  hipLaunchKernelGGL((reduce_unroll() == 8 ? k_bn_reduce<uint16_t, 1, 3, 8, true>
-                                            : k_bn_reduce<uint16_t, 1, 3, 4, true>),
+  hipLaunchKernelGGL((k_bn_reduce<uint16_t, 1, 3, kReduceUnroll, true>),
                      dim3(nb, reduce_slices(a.C)), dim3(BNT), 0, st, x, dy, (const uint16_t*)nullptr,
                      a.bits, a.mean, (const float*)nullptr, (const float*)nullptr, a.M, a.C, rpb,
                      a.partial, x2, b.mean, b.partial);
@@ -846,7 +713,7 @@ void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st) {
   const int64_t n8 = a.M * a.C / 8;
   hipLaunchKernelGGL(k_bn_bwd_apply_dual, dim3(apply_grid(n8, a.C, kApplyBwdGrid)), dim3(BNT), 0, st, x, x2, dy,
                      a.bits, a.A, a.B, a.Cc, b.A, b.B, b.Cc, static_cast<uint16_t*>(a.dx),
-                     static_cast<uint16_t*>(b.dx), n8, a.C, bn_reverse() ? 1 : 0);
+                     static_cast<uint16_t*>(b.dx), n8, a.C);
 }
 
 void bn_forward(const BNArgs& a, hipStream_t st) {

@@ -1443,7 +1443,7 @@ static int hist0_blocks(int ntasks) {
   return t > 0 ? (ntasks + t - 1) / t : ntasks * -t;
 }
 // Pass 0 of a launch whose longest segment has LW_HIST0_BIG_MIN tasks or more: 1024-thread
-// workgroups of several tasks each (LWAAAI_HIST0_BIG=0: the 256-thread grid above). The histogram
+// workgroups of several tasks each (shorter segments: the 256-thread grid above). The histogram
 // merges execute one per word at the memory side, so their time grows with how many workgroups
 // add into one segment's hot bins, not with the workgroup size. Tasks per workgroup = the longest
 // segment's tasks / 64 (2..16): about 64 merges per hot bin while a layer-wise bucket keeps
@@ -1455,11 +1455,7 @@ static int hist0_blocks(int ntasks) {
 #endif
 constexpr int TB0 = 1024;
 static int hist0_big_tpb(int max_seg_tasks) {
-  static const bool on = [] {
-    const char* e = std::getenv("LWAAAI_HIST0_BIG");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  if (!on || max_seg_tasks < LW_HIST0_BIG_MIN) return 0;
+  if (max_seg_tasks < LW_HIST0_BIG_MIN) return 0;
   return std::min(16, std::max(2, max_seg_tasks / 64));
 }
 
@@ -1759,7 +1755,7 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
         const uint32_t c = ((k < 16 ? w.x : w.y) >> (2 * (k & 15))) & 3u;
-        acc[k] += c == 1u ? sc : (c == 2u ? -sc : 0.f);
+        acc[k] = __fadd_rn(acc[k], c == 1u ? sc : (c == 2u ? -sc : 0.f));
       }
     } else if (Q == Q_QS8) {
       const uint4* o = reinterpret_cast<const uint4*>(rec);
@@ -1769,7 +1765,8 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
       for (int k = 0; k < EPT; ++k) {
         const int l = (int)(int8_t)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
         const float sg = l > 0 ? 1.f : (l < 0 ? -1.f : 0.f);
-        acc[k] += sg * sc * ((float)(l < 0 ? -l : l) / (float)qstates);
+        acc[k] = __fadd_rn(acc[k], __fmul_rn(__fmul_rn(sg, sc),
+                                             __fdiv_rn((float)(l < 0 ? -l : l), (float)qstates)));
       }
     } else if (Q == Q_QS9) {
       const uint4* o = reinterpret_cast<const uint4*>(rec);
@@ -1780,7 +1777,7 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
       for (int k = 0; k < EPT; ++k) {
         const int l = (int)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
         const float sg = l == 0 ? 0.f : (((sgn >> k) & 1u) ? -1.f : 1.f);
-        acc[k] += sg * sc * ((float)l / (float)qstates);
+        acc[k] = __fadd_rn(acc[k], __fmul_rn(__fmul_rn(sg, sc), __fdiv_rn((float)l, (float)qstates)));
       }
     } else {
       const uint4* o = reinterpret_cast<const uint4*>(rec);
@@ -1794,11 +1791,14 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
       for (int k = 0; k < EPT; ++k) {
         const int l = (int)(int16_t)((w[k >> 1] >> (16 * (k & 1))) & 0xffff);
         const float sg = l > 0 ? 1.f : (l < 0 ? -1.f : 0.f);
-        acc[k] += sg * sc * ((float)(l < 0 ? -l : l) / (float)qstates);
+        acc[k] = __fadd_rn(acc[k], __fmul_rn(__fmul_rn(sg, sc),
+                                             __fdiv_rn((float)(l < 0 ? -l : l), (float)qstates)));
       }
     }
   }
   const float fws = (float)ws;
+  // (explicitly rounded adds / products / quotients: no FMA contraction, so the CPU mirror —
+  // codecs.py QuantRSCodec.reduce_shard — reproduces every shard bit for bit)
   uint16_t* op = out + gt.y;
   if (gt.z == EPT && (gt.y & 7) == 0) {
 #pragma unroll
@@ -1806,12 +1806,12 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
       uint32_t w[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        w[k] = (uint32_t)ElemBF16::rne(acc[8 * q + 2 * k] / fws) |
-               ((uint32_t)ElemBF16::rne(acc[8 * q + 2 * k + 1] / fws) << 16);
+        w[k] = (uint32_t)ElemBF16::rne(__fdiv_rn(acc[8 * q + 2 * k], fws)) |
+               ((uint32_t)ElemBF16::rne(__fdiv_rn(acc[8 * q + 2 * k + 1], fws)) << 16);
       reinterpret_cast<uint4*>(op)[q] = make_uint4(w[0], w[1], w[2], w[3]);
     }
   } else {
-    for (int k = 0; k < gt.z; ++k) op[k] = ElemBF16::rne(acc[k] / fws);
+    for (int k = 0; k < gt.z; ++k) op[k] = ElemBF16::rne(__fdiv_rn(acc[k], fws));
   }
 }
 

@@ -260,8 +260,7 @@ static void conv_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, hip
   const bool pro = g.pro_scale != nullptr;
   if constexpr (CVM == CV_A) {
     if (!g.b_kcontig) {                                   // data gradient: Wt is [K][C]
-      if (epi == EPI_BSTATS) LW_LAUNCH(true, false, EPI_BSTATS, PRO_NONE, CV_A);
-      else LW_LAUNCH(true, false, EPI_STORE, PRO_NONE, CV_A);
+      LW_LAUNCH(true, false, EPI_STORE, PRO_NONE, CV_A);
     } else if (epi == EPI_STATS) {
       if (pro) LW_LAUNCH(true, true, EPI_STATS, PRO_A, CV_A);
       else LW_LAUNCH(true, true, EPI_STATS, PRO_NONE, CV_A);
@@ -551,14 +550,8 @@ bool stem_conv7_ok(int C, int Co, int R, int S, int sh, int sw, int ph, int pw, 
          Wo <= STEM_WOMAX && stem_conv7_smem(Wo) <= 64 * 1024;
 }
 
-// tiles per workgroup: enough workgroups for two resident per CU (the LDS footprint allows two),
-// LWAAAI_STEM_TPW overrides (1 = one tile per workgroup)
+// tiles per workgroup: enough workgroups for two resident per CU (the LDS footprint allows two)
 static int stem_tpw(int tiles) {
-  static const int env = [] {
-    const char* e = getenv("LWAAAI_STEM_TPW");
-    return e ? atoi(e) : 0;
-  }();
-  if (env > 0) return env;
   const int slots = 2 * cu_count();
   return std::max(1, (tiles + slots - 1) / slots);
 }
@@ -574,186 +567,10 @@ void stem_conv7(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats,
   const int tiles = N * (Ho / STEM_SY);
   const int tpw = stem_tpw(tiles);
   const int blocks = (tiles + tpw - 1) / tpw;
-  // default: no prefetch at 4 waves/SIMD. LWAAAI_STEM_PF=1 LWAAAI_STEM_OCC=3 (prefetch at 3
-  // waves/SIMD) is faster in isolation (213 vs 251 us, bs 256, profiles/r3s2/stem_ab.txt) but its
-  // one bench run came in lower (11,060-11,126 img/s) and no same-box A/B ran yet: opt-in
-  static const int var = [] {
-    const char* o = getenv("LWAAAI_STEM_OCC");
-    const char* f = getenv("LWAAAI_STEM_PF");
-    return (o && atoi(o) == 3 ? 1 : 0) + (f && atoi(f) == 1 ? 2 : 0);
-  }();
-  const int smem = stem_conv7_smem(Wo);
-  switch (var) {
-    case 1: hipLaunchKernelGGL((k_stem_conv7<3, false>), dim3(blocks), dim3(STEM_T), smem, st, x, w, y,
-                               stats, H, W, Ho, Wo, tiles, tpw); break;
-    case 2: hipLaunchKernelGGL((k_stem_conv7<4, true>), dim3(blocks), dim3(STEM_T), smem, st, x, w, y,
-                               stats, H, W, Ho, Wo, tiles, tpw); break;
-    case 3: hipLaunchKernelGGL((k_stem_conv7<3, true>), dim3(blocks), dim3(STEM_T), smem, st, x, w, y,
-                               stats, H, W, Ho, Wo, tiles, tpw); break;
-    default: hipLaunchKernelGGL((k_stem_conv7<4, false>), dim3(blocks), dim3(STEM_T), smem, st, x, w,
-                                y, stats, H, W, Ho, Wo, tiles, tpw);
-  }
-}
-
-}  // namespace lw
-
-namespace lw {
-
-// ---------------------------------------------------------------------------------------------
-// Direct 3x3 / stride-1 / pad-1 convolution of a 64-channel NHWC map into 64 channels (ResNet-50
-// layer-1 bottleneck conv2, its forward and — with the flipped, transposed weight — its data
-// gradient). The implicit GEMM gathers each input chunk from L2 once per tap (9x); with N = 64
-// output channels that gather traffic, not the MFMAs, set its speed (~430-490 TFLOP/s). Here a
-// workgroup owns 8 output rows of one image: it stages their (8 + 2) x (W + 2) x 64 input patch
-// (zero halo included; 16-byte channel chunks XOR-swizzled by the column) and the [64][576]
-// weight in LDS once, and all 9 taps read their MFMA operands from the patch. The k order
-// (tap, channel) in 32-wide MFMA steps is that of the GEMM path's packed weight, so the forward
-// is bit-identical to it. Epilogue: bf16 NHWC store (+ one column-statistics row per workgroup).
-constexpr int D3_RY = 8;                   // output rows per workgroup
-constexpr int D3_C = 64;                   // input / output channels
-constexpr int D3_K = 9 * D3_C;             // 576
-constexpr int D3_WLD = D3_K + 8;           // padded LDS weight row (conflict-free B reads)
-constexpr int D3_WAVES = 7;
-constexpr int D3_T = D3_WAVES * 64;
-constexpr int D3_MAXRB = 4;                // 16-pixel blocks per wave (W * 8 <= 448)
-
-template <bool STATS>
-__global__ __launch_bounds__(D3_T) void k_conv3_direct(const uint16_t* __restrict__ x,
-                                                       const uint16_t* __restrict__ w,
-                                                       uint16_t* __restrict__ y,
-                                                       float* __restrict__ stats, int H, int W) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int PW = W + 2, PR = D3_RY + 2;
-  uint16_t* patch = reinterpret_cast<uint16_t*>(smem);                 // [PR][PW][8 chunks][8]
-  uint16_t* ws = patch + PR * PW * D3_C;                                // [64][D3_WLD]
-  float* red = reinterpret_cast<float*>(ws + D3_C * D3_WLD);            // [waves][2][64]
-  const int tiles_y = H / D3_RY;
-  const int img = blockIdx.x / tiles_y, y0 = (blockIdx.x - img * tiles_y) * D3_RY;
-  const int64_t img_off = (int64_t)img * H * W * D3_C;
-  // ---- stage the patch: chunk q of pixel (pr, pc) at slot q ^ (pc & 7)
-  for (int e = threadIdx.x; e < PR * PW * 8; e += D3_T) {
-    const int q = e & 7, pix = e >> 3;
-    const int pr = pix / PW, pc = pix - pr * PW;
-    const int hi = y0 - 1 + pr, wi = pc - 1;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
-      v = *reinterpret_cast<const uint4*>(x + img_off + ((int64_t)hi * W + wi) * D3_C + q * 8);
-    *reinterpret_cast<uint4*>(patch + pix * D3_C + ((q ^ (pc & 7)) * 8)) = v;
-  }
-  for (int e = threadIdx.x; e < D3_C * (D3_K / 8); e += D3_T) {
-    const int co = e / (D3_K / 8), kc = e - co * (D3_K / 8);
-    *reinterpret_cast<uint4*>(ws + co * D3_WLD + kc * 8) =
-        *reinterpret_cast<const uint4*>(w + co * D3_K + kc * 8);
-  }
-  __syncthreads();
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, g = l >> 4, lr = l & 15;
-  const int RB = D3_RY * W / (D3_WAVES * 16);
-  f32x4 acc[D3_MAXRB][4];
-#pragma unroll
-  for (int i = 0; i < D3_MAXRB; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int py[D3_MAXRB], px[D3_MAXRB];
-#pragma unroll
-  for (int i = 0; i < D3_MAXRB; ++i) {
-    const int p = (wv + D3_WAVES * i) * 16 + lr;
-    py[i] = p / W;
-    px[i] = p - py[i] * W;
-  }
-  for (int ks = 0; ks < D3_K / 32; ++ks) {
-    const int t = ks >> 1, r = t / 3, s = t - r * 3;
-    const int q = (ks & 1) * 4 + g;                  // this lane's 8-channel chunk
-    h16x8 fb[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      fb[j] = *reinterpret_cast<const h16x8*>(ws + (j * 16 + lr) * D3_WLD + ks * 32 + g * 8);
-#pragma unroll
-    for (int i = 0; i < D3_MAXRB; ++i) {
-      if (i < RB) {
-        const int pc = px[i] + s;
-        const h16x8 fa = *reinterpret_cast<const h16x8*>(
-            patch + ((py[i] + r) * PW + pc) * D3_C + ((q ^ (pc & 7)) * 8));
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = mfma16(fb[j], fa, acc[i][j]);
-      }
-    }
-  }
-  // ---- epilogue: lane holds C[pixel (l & 15)][channel 4 * (l >> 4) + q] of each 16x16 block
-  float s1[4][4], s2[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) { s1[j][c] = 0.f; s2[j][c] = 0.f; }
-  const int64_t out_base = ((int64_t)img * H + y0) * W;
-#pragma unroll
-  for (int i = 0; i < D3_MAXRB; ++i) {
-    if (i >= RB) continue;
-    const int p = (wv + D3_WAVES * i) * 16 + lr;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint16_t h[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        h[c] = f2h(acc[i][j][c]);
-        const float v = h2f(h[c]);
-        s1[j][c] += v;
-        s2[j][c] += v * v;
-      }
-      *reinterpret_cast<uint2*>(y + (out_base + p) * D3_C + j * 16 + 4 * g) =
-          make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
-    }
-  }
-  if constexpr (STATS) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        s1[j][c] = sum16(s1[j][c]);
-        s2[j][c] = sum16(s2[j][c]);
-      }
-    if (lr == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          red[(wv * 2 + 0) * D3_C + j * 16 + 4 * g + c] = s1[j][c];
-          red[(wv * 2 + 1) * D3_C + j * 16 + 4 * g + c] = s2[j][c];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 2 * D3_C) {
-      const int sidx = threadIdx.x / D3_C, c = threadIdx.x - sidx * D3_C;
-      float tot = 0.f;
-#pragma unroll
-      for (int q2 = 0; q2 < D3_WAVES; ++q2) tot += red[(q2 * 2 + sidx) * D3_C + c];
-      stats[((int64_t)blockIdx.x * 2 + sidx) * D3_C + c] = tot;
-    }
-  }
-}
-
-static int conv3_direct_smem(int W) {
-  return (D3_RY + 2) * (W + 2) * D3_C * 2 + D3_C * D3_WLD * 2 + D3_WAVES * 2 * D3_C * 4;
-}
-
-bool conv3_direct_ok(int C, int Co, int H, int W) {
-  return C == D3_C && Co == D3_C && H % D3_RY == 0 && (D3_RY * W) % (D3_WAVES * 16) == 0 &&
-         D3_RY * W / (D3_WAVES * 16) <= D3_MAXRB && conv3_direct_smem(W) <= 160 * 1024;
-}
-
-void conv3_direct(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
-                  int W, hipStream_t st) {
-  const int blocks = N * (H / D3_RY);
-  const int smem = conv3_direct_smem(W);
-  if (stats) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3_direct<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    hipLaunchKernelGGL(k_conv3_direct<true>, dim3(blocks), dim3(D3_T), smem, st, x, w, y, stats, H, W);
-  } else {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3_direct<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    hipLaunchKernelGGL(k_conv3_direct<false>, dim3(blocks), dim3(D3_T), smem, st, x, w, y, stats, H, W);
-  }
+  // (the next-tile patch prefetch and 3 waves/SIMD variants were faster in isolation, 213 vs
+  // 251 us, but not in the step: profiles/r3s2/stem_ab.txt; round 6 removed them)
+  hipLaunchKernelGGL((k_stem_conv7<4, false>), dim3(blocks), dim3(STEM_T), stem_conv7_smem(Wo), st,
+                     x, w, y, stats, H, W, Ho, Wo, tiles, tpw);
 }
 
 }  // namespace lw

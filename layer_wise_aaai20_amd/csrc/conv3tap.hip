@@ -324,13 +324,8 @@ void conv3_tap(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, 
   const int tiles = conv3_tap_tiles_m(N, H, W) * (Co / bn);
   const uint32_t xb = (uint32_t)((int64_t)NH * W * C * 2);
   const uint32_t wb = (uint32_t)((int64_t)Co * 9 * C * 2);
-  // LWAAAI_TAP_VAR (A/B): 3 = ring of 3 slices, barrier per tap (default); 4 = ring of 4;
-  // 22 / 33 = 2 / 3 taps per barrier (ring 4 / 6)
-  static const int var = [] {
-    const char* e = getenv("LWAAAI_TAP_VAR");
-    const int v = e ? atoi(e) : 3;
-    return v == 4 || v == 22 || v == 33 ? v : 3;
-  }();
+  // a ring of 3 slices with one barrier per tap (rings of 4 / 6 slices with 1 / 2 / 3 taps per
+  // barrier measured no faster and were removed in round 6)
 #define LW_T3(BNV, ST, D, T)                                                                       \
   hipLaunchKernelGGL((k_conv3_tap<BNV, ST, D, T>), dim3(tiles), dim3(BNV * 4), 0, st, x, w, y,      \
                      stats, NH, H, W, C, Co, xb, wb)
@@ -344,12 +339,7 @@ void conv3_tap(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, 
       else LW_T3(64, false, D, T);                                                                 \
     }                                                                                              \
   } while (0)
-  switch (var) {
-    case 4: LW_T3V(4, 1); break;
-    case 22: LW_T3V(4, 2); break;
-    case 33: LW_T3V(6, 3); break;
-    default: LW_T3V(3, 1);
-  }
+  LW_T3V(3, 1);
 #undef LW_T3V
 #undef LW_T3
 }

@@ -418,12 +418,6 @@ static void launch_tile(const GemmArgs& g, const GemmK& k, int epi, dim3 grid, h
   else launch_layout<BM, BN, BK, E, PRO_NONE, MF>(g, k, grid, st);
   if (epi == EPI_PARTIAL) { LW_E(EPI_PARTIAL) }
   else if (epi == EPI_STATS) { LW_E(EPI_STATS) }
-  else if (epi == EPI_BSTATS) {
-    // a data-gradient GEMM (dy·W: K-contiguous dy, N-contiguous W) that also does the reduce
-    // pass of the BatchNorm its output feeds (the host checks the layout and no prologue)
-    hipLaunchKernelGGL((k_gemm<BM, BN, BK, true, false, EPI_BSTATS, PRO_NONE, CV_NONE, MF>), grid,
-                       dim3(GT), 0, st, k);
-  }
   else { LW_E(EPI_STORE) }
 #undef LW_E
 }

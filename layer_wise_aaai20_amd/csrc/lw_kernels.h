@@ -192,11 +192,8 @@ struct BNArgs {
   uint8_t* bits;           // ReLU bitmap, 1 bit/element: written by the forward apply, read back
                            // by the backward instead of the saved output (or nullptr)
   bool accum_dparams;      // backward: dgamma/dbeta += (into the gradient arena) instead of =
-  unsigned* tickets = nullptr;  // bn_stats with stat_rows: per-slice arrival tickets (zero, and
-                                // re-armed by the kernel) -> one-launch colsum + finalize
 };
 int bn_reduce_blocks(int64_t M, int C);
-int colsum_fused_blocks(int64_t rows);
 int colsum_blocks(int64_t rows);     // blocks folding R GEMM-epilogue statistics rows
 void bn_stats(const BNArgs& a, hipStream_t st);
 void bn_apply(const BNArgs& a, hipStream_t st);
@@ -343,8 +340,6 @@ bool stem_conv7_ok(int C, int Co, int R, int S, int sh, int sw, int ph, int pw, 
                    int Ho, int Wo);
 void stem_conv7(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
                 int W, int Ho, int Wo, hipStream_t st);
-// direct 3x3 / stride-1 / pad-1 convolution, 64 -> 64 channels, NHWC, from an LDS patch
-// (conv.hip k_conv3_direct); stats (optional): one column-statistics row per 8 output rows
 // tap-reuse 3x3 / stride-1 / pad-1 convolution (conv3tap.hip): x NHWC [N*H*W][C] bf16, w the
 // K-contiguous [Co][9C] operand ((r, s, ci) order); stats (optional) [tiles_m][2][Co]
 bool conv3_tap_ok(int C, int Co, int H, int W);
@@ -356,9 +351,6 @@ void conv3_tap(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, 
 int conv3_tap_wgrad_splits(int N, int H, int W, int C, int Co);
 void conv3_tap_wgrad(const uint16_t* dy, const uint16_t* x, float* part, float* out, int N,
                      int H, int W, int C, int Co, int accumulate, hipStream_t st);
-bool conv3_direct_ok(int C, int Co, int H, int W);
-void conv3_direct(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
-                  int W, hipStream_t st);
 
 // model-path elementwise (nn.hip)
 void normalize_u8(const uint8_t* in, void* out, int64_t nbytes, const float mean[3],

@@ -8,7 +8,6 @@ per-layer message list that drives layer-wise compression are 
 """
 from __future__ import annotations
 
-import os
 
 import torch
 from torch import nn
@@ -153,7 +152,7 @@ def make_layers(cfg, batch_norm: bool = False) -> nn.Sequential:
     return nn.Sequential(*layers)
 
 
-_VGG_FOLD = os.environ.get("LWAAAI_VGG_FOLD", "1") != "0"
+_VGG_FOLD = True          # (False, tests only: the pool + full-width GEMMs)
 
 
 def _pair_size(s):
@@ -191,7 +190,7 @@ class VGG(nn.Module, _DictLossMixin):
                 fc1.in_features == x.shape[1] * oh * ow and _VGG_FOLD):
             # 32x32 CIFAR images leave a 1x1 map, which the 7x7 adaptive pool only replicates:
             # fc1 runs on the folded weight (ops/gemm.py replicated_linear, exactly the same
-            # layer). LWAAAI_VGG_FOLD=0 keeps the pool + full-width GEMMs.
+            # layer).
             from ..ops.gemm import replicated_linear
             x = replicated_linear(torch.flatten(x, 1), fc1, oh * ow)
             x = self.classifier[1:](x)

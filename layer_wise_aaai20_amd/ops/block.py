@@ -45,7 +45,6 @@ returned through autograd as usual.
 from __future__ import annotations
 
 import contextlib
-import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -56,26 +55,21 @@ from .conv import conv_dgrad, conv_fwd, conv_wgrad, kc_end_step, kc_new_step, kc
 from .tuning import MF32, Tuner, with_mf32
 
 CL = torch.channels_last
-# materialise relu(bn1(c1)) / relu(bn2(c2)) with one apply pass instead of re-normalising in the
-# consumers' staging prologues (see _BottleneckFn.forward)
-MAT_A1 = os.environ.get("LWAAAI_MAT_A1", "1") != "0"
-MAT_A2 = os.environ.get("LWAAAI_MAT_A2", "1") != "0"
-# BN1 / BN2 backward reductions in the epilogues of the data-gradient GEMM / conv producing their
-# input gradient (csrc gemm_core.h EPI_BSTATS) instead of a separate pass over dy and x. Off by
-# default: it saves the reduce passes (-1.6 ms of BN kernels) but the extra epilogue operands raise
-# those GEMMs' registers and serialise their memory phases (+2.4 ms): 9,770 vs 10,297 img/s
-# (profiles/r2_bstats_ab.log). LWAAAI_BSTATS=1 / LWAAAI_CROSS_BN3=1 turn the two parts on.
-BSTATS = os.environ.get("LWAAAI_BSTATS", "0") == "1"
-# The downsample block's BN3 and shortcut-BN backwards share dy and the ReLU bitmap: one dual
-# reduce + one dual apply pass (csrc bn.hip k_bn_reduce DUAL / k_bn_bwd_apply_dual) read them once
-# for both. LWAAAI_BN_DUAL=0: two separate BN backwards.
-BN_DUAL = os.environ.get("LWAAAI_BN_DUAL", "1") != "0"
+# Design decisions measured in earlier rounds and fixed in round 6 (their switches removed):
+# * relu(bn1(c1)) / relu(bn2(c2)) are materialised by one apply pass each, not re-normalised in the
+#   consumers' staging prologues (a 3x3 conv redoes the affine for each of its 9 taps: 1.6x slower);
+# * the BN backward reductions run as their own pass: folding them into the epilogue of the GEMM
+#   producing dy saved 1.6 ms of BN kernels but cost 2.4 ms of GEMM (profiles/r2_bstats_ab.log;
+#   -3.3 % each part, profiles/r3s2/bstats_cross_ab.txt);
+# * the downsample block's BN3 and shortcut-BN backwards share dy and the ReLU bitmap: one dual
+#   reduce + one dual apply pass (csrc bn.hip k_bn_reduce DUAL / k_bn_bwd_apply_dual);
+# * weight gradients run inline (a side stream measured no gain: the step is throughput-bound).
 TILES = with_mf32((1, 2, 3, 4, 5, 6))   # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
 BIG = (21, 22)                      # 256x256 / 256x128 8-wave LDS-DMA kernel (csrc/gemm_big.hip)
 # the same tiles as a persistent kernel (csrc/gemm_big.hip k_gemm_bigp: one workgroup per CU, the
-# next tile's first K-tiles loaded during this tile's epilogue); LWAAAI_GEMM_PERSIST=0 drops them
-PERSIST = (23, 24) if os.environ.get("LWAAAI_GEMM_PERSIST", "1") != "0" else ()
+# next tile's first K-tiles loaded during this tile's epilogue)
+PERSIST = (23, 24)
 
 
 def _rows(t: torch.Tensor) -> torch.Tensor:
@@ -131,16 +125,10 @@ def stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro, pro_on_a, add, split
 
 def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro=None,
          pro_on_a=True, out=None, addend=None, accumulate=False, ldc=0, split_k=False,
-         addend_bits=None, bst=None):
-    """One MFMA GEMM launch (plus the split-K reduce when ``split_k``); see ``csrc/gemm.hip``.
-
-    ``bst = (x, mean, scale_shift, bits)``: the output is the gradient reaching a BN+ReLU whose
-    input was ``x``; with ``stats=True`` the epilogue also writes that BN backward's per-M-tile
-    (Σdy', Σdy'·(x−mean)) rows (mask from ``bits`` or x*scale+shift > 0), which
-    ``bn_bwd(..., stats_rows=)`` folds instead of running its reduce pass."""
+         addend_bits=None):
+    """One MFMA GEMM launch (plus the split-K reduce when ``split_k``); see ``csrc/gemm.hip``."""
     lib = load()
     ps, ph = (pro[0], pro[1]) if pro is not None else (None, None)
-    bx, bm, bss, bb = bst if bst is not None else (None, None, None, None)
 
     def splits_for(tile):
         if not split_k:
@@ -149,7 +137,7 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
         return _splits(-(-M // bm) * -(-N // bn), K)
 
     key = (M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None, pro_on_a, split_k,
-           addend is not None, bst is not None) + (("sk",) if split_k else ())
+           addend is not None, False) + (("sk",) if split_k else ())
 
     def unpack(c):
         return c if isinstance(c, tuple) else (c, splits_for(c))
@@ -157,21 +145,20 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
     def run(c):
         tile, sp = unpack(c)
         lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, sp, out_bf16,
-                    tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits,
-                    bx, bm, bss, bb)
+                    tile, ps, ph, pro_on_a, stats, None, addend, False, 0, addend_bits)
     # the big tiles: both operands K-contiguous (forward, transposed-weight dgrad), a K-contiguous
     # A with the weight as stored (dgrad), or both MN-contiguous (weight gradients); no prologue /
-    # addend / backward statistics
-    big = BIG if (pro is None and addend is None and bst is None and
+    # addend
+    big = BIG if (pro is None and addend is None and
                   ((a_kc and b_kc and K % 8 == 0) or
                    (a_kc and not b_kc and K % 8 == 0 and N % 8 == 0 and ldb % 8 == 0) or
                    (not a_kc and not b_kc and M % 8 == 0 and N % 8 == 0 and not stats))) else ()
-    persist = PERSIST if (pro is None and bst is None and a_kc and b_kc and out_bf16 and
+    persist = PERSIST if (pro is None and a_kc and b_kc and out_bf16 and
                           not accumulate and not split_k and K % 8 == 0 and K > 64 and
                           N % 8 == 0) else ()
-    cands = TILES + big + persist + (() if bst is not None else
-                           stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats, pro is not None,
-                                        pro_on_a, addend is not None, split_k, accumulate))
+    cands = TILES + big + persist + stream_tiles(M, N, K, a_kc, b_kc, out_bf16, stats,
+                                                 pro is not None, pro_on_a, addend is not None,
+                                                 split_k, accumulate)
     if split_k:
         # (tile, split-K) pairs: fewer, longer K-slices write fewer fp32 slabs for the fixed-order
         # reduce (the weight gradients are HBM-bound; fewer workgroups can still stream them)
@@ -180,7 +167,7 @@ def gemm(A, lda, a_kc, B, ldb, b_kc, M, N, K, *, out_bf16=True, stats=False, pro
     tile, sp = unpack(TUNER.pick(key, run, cands))
     return lib.gemm_ex(A, lda, a_kc, B, ldb, b_kc, M, N, K, None, False, sp,
                        out_bf16, tile, ps, ph, pro_on_a, stats, out, addend, accumulate, ldc,
-                       addend_bits, bx, bm, bss, bb)
+                       addend_bits)
 
 
 LAYOUT_TUNER = Tuner("dgrad-layout", "LWAAAI_GEMM_TUNE")
@@ -205,8 +192,7 @@ def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
     [out = K][in = N], N-contiguous as a GEMM B operand). Two layouts are timed on first sight:
     W as stored (the kernel's transposing LDS reads), or Wᵀ copied to [N][K] (a few µs: at most
     2048x512) so that both operands are K-contiguous and the LDS-DMA staging and the big tiles
-    apply. ``bst`` (backward statistics) needs the stored layout. (Round 4's opt-in hipBLASLt
-    candidate is gone: every kernel of the step is ours.)"""
+    apply. (Round 4's opt-in hipBLASLt candidate is gone: every kernel of the step is ours.)"""
     def run(layout, fresh=False, **over):
         args = dict(kw, **over)
         if layout == "kc":            # Wᵀ (the tuner times a pack of its own with the GEMM)
@@ -214,35 +200,11 @@ def gemm_dgrad(dy, ldy, W, M, N, K, **kw):
             wt = _kc_weight(W, K, N, kp, fresh)
             return gemm(dy, ldy, True, wt, kp, True, M, N, K, **args)
         return gemm(dy, ldy, True, W, N, False, M, N, K, **args)
-    if kw.get("bst") is not None:
-        return run("nkc")
     cands = ("nkc", "kc")
     key = (M, N, K, kw.get("addend") is not None, kw.get("out") is not None)
     # timed on a scratch output (``out`` may also be the addend: dx += ... in place)
     layout = LAYOUT_TUNER.pick(key, lambda c: run(c, fresh=True, out=None), cands, "nkc")
     return run(layout)
-
-
-# ----------------------------------------------------------------------------- cross-block BN3
-# The gradient reaching block i's output, dout_i, is the dx written by block i+1's last GEMM. When
-# block i+1 has an identity shortcut, that GEMM's epilogue also reduces block i's BN3 backward
-# statistics (Σ dout·[out>0], Σ dout·[out>0]·(c3 − mean3)), so block i skips its reduce pass over
-# dout and c3. Forward hands block i's (output, c3, mean3, ReLU bitmap) to the next block through
-# _FWD_SLOT; backward hands the statistics rows back through _BWD_SLOT, keyed by the gradient
-# tensor and checked against block i's own c3, so a mismatch just falls back to the reduce pass.
-_FWD_SLOT = [None]
-_BWD_SLOT = [None]
-CROSS_BN3 = os.environ.get("LWAAAI_CROSS_BN3", "0") == "1"
-
-
-def _take_prev(x: torch.Tensor):
-    prev, _FWD_SLOT[0] = _FWD_SLOT[0], None
-    if prev is None or not CROSS_BN3:
-        return None
-    out_ptr, shape, c3, mean3, bits3 = prev
-    if x.data_ptr() != out_ptr or tuple(x.shape) != shape:
-        return None
-    return c3, mean3, bits3
 
 
 # ----------------------------------------------------------------------------- grad sink
@@ -290,62 +252,13 @@ def _finish_wgrad(p: torch.Tensor, dst: torch.Tensor, direct: bool):
     return _finish_param(p, None, True) if direct else dst.view_as(p)
 
 
-# Weight gradients on a side stream: dW of a layer is independent of the data-gradient chain
-# that follows it, so the block's three (four) weight-gradient GEMMs run beside the dgrad GEMMs
-# and the latency-bound BN backward kernels instead of between them (fork/join by stream waits;
-# inside a HIP-graph capture the fork and join become graph edges). LWAAAI_WGRAD_SIDE=0: inline.
-WGRAD_SIDE = os.environ.get("LWAAAI_WGRAD_SIDE", "0") == "1"
-_SIDE: Dict[int, torch.cuda.Stream] = {}
-
-
-class _WgradLane:
-    def __init__(self, device: torch.device):
-        self.on = WGRAD_SIDE and device.type == "cuda"
-        self.main = torch.cuda.current_stream(device) if self.on else None
-        if self.on:
-            idx = device.index if device.index is not None else torch.cuda.current_device()
-            if idx not in _SIDE:
-                _SIDE[idx] = torch.cuda.Stream(device=idx)
-            self.side = _SIDE[idx]
-        self.ready = []
-        self.used = False
-
-    def run(self, fn):
-        """Launch ``fn`` after everything the main stream has queued so far."""
-        if not self.on:
-            return fn()
-        self.side.wait_stream(self.main)
-        with torch.cuda.stream(self.side):
-            out = fn()
-        self.used = True
-        return out
-
-    def finish(self, thunk) -> None:
-        """Grad-ready notifications wait for the join (the engine records its bucket events on
-        the main stream)."""
-        if self.on:
-            self.ready.append(thunk)
-        else:
-            thunk()
-
-    def join(self) -> None:
-        if self.on and self.used:
-            self.main.wait_stream(self.side)
-        for t in self.ready:
-            t()
-        self.ready = []
-
-
 # Split-K weight gradients accumulated straight into the gradient arena leave their slab reduce
 # to the gradient engine's next flush (csrc/gemm.hip splitk_flush, parallel/engine.py), which
 # runs them in one launch before it reads the arena — ResNet-50 spent 54 launches a step on
-# these reduces. LWAAAI_SPLITK_DEFER=0: each reduce right after its GEMM.
-SPLITK_DEFER = os.environ.get("LWAAAI_SPLITK_DEFER", "1") != "0"
-
-
+# these reduces (profiles/r5/splitk_defer_ab.jsonl).
 @contextlib.contextmanager
 def _deferred_reduce(t: torch.Tensor, direct: bool):
-    on = SPLITK_DEFER and direct and t.is_cuda
+    on = direct and t.is_cuda
     if on:
         set_splitk_defer(t, True)
     try:
@@ -355,9 +268,9 @@ def _deferred_reduce(t: torch.Tensor, direct: bool):
             set_splitk_defer(t, False)
 
 
-def _wgrad_done(lane: _WgradLane, p: torch.Tensor, dst: torch.Tensor, direct: bool):
+def _wgrad_done(p: torch.Tensor, dst: torch.Tensor, direct: bool):
     if direct:
-        lane.finish(lambda: _finish_param(p, None, True))
+        _finish_param(p, None, True)
         return None
     return dst.view_as(p)
 
@@ -390,8 +303,6 @@ class _BottleneckFn(torch.autograd.Function):
         bn1, bn2, bn3, conv2, bnd, down_stride = mods
         for bn in (bn1, bn2, bn3) + ((bnd,) if bnd is not None else ()):
             _bump(bn)                 # before the momentum is read (momentum=None: 1/n)
-        # the previous block's BN3 state, when x is its output (identity shortcut only)
-        ctx.prev = _take_prev(x) if bnd is None else None
         stride = conv2.stride
         N, Cin, H, W = x.shape
         x = x.to(h16()).contiguous(memory_format=CL)
@@ -406,26 +317,18 @@ class _BottleneckFn(torch.autograd.Function):
         c1, st1 = gemm(xr, Cin, True, W1, Cin, True, M, width, Cin, stats=True)
         mean1, inv1, ss1 = lib.bn_stats(c1, st1, g1, b1, bn1.running_mean, bn1.running_var,
                                         _bn_momentum(bn1), bn1.eps)
-        # conv2 (3x3, implicit GEMM) on a1 = relu(bn1(c1)), BN2's column statistics in its
-        # epilogue. a1 is materialised by one apply pass (MAT_A1): staging-time BN-apply would
-        # redo the affine for each of the 9 taps of every element (measured 1.6x slower conv);
-        # with MAT_A1=0 the prologue form is used instead.
-        pro1 = (ss1[:width], ss1[width:])
-        a1 = lib.bn_apply(c1, ss1, None, None, True) if MAT_A1 else None
-        c2n, st2 = conv_fwd(_nchw(a1 if MAT_A1 else c1, N, H, W), W2, stride, conv2.padding,
-                            pro=None if MAT_A1 else pro1, stats=True)
+        # conv2 (3x3, implicit GEMM) on a1 = relu(bn1(c1)), materialised by one apply pass, BN2's
+        # column statistics in its epilogue
+        a1 = lib.bn_apply(c1, ss1, None, None, True)
+        c2n, st2 = conv_fwd(_nchw(a1, N, H, W), W2, stride, conv2.padding, stats=True)
         N2, _, H2, W2_ = c2n.shape
         c2 = _rows(c2n)
         M2 = c2.shape[0]
         mean2, inv2, ss2 = lib.bn_stats(c2, st2, g2, b2, bn2.running_mean, bn2.running_var,
                                         _bn_momentum(bn2), bn2.eps)
-        # conv3 (1x1): BN2-apply+ReLU in the prologue (each A row-panel is re-normalised once
-        # per output-column tile) or on a2 materialised by one apply pass (MAT_A2); BN3
-        # statistics in the epilogue
-        pro2 = (ss2[:width], ss2[width:])
-        a2 = lib.bn_apply(c2, ss2, None, None, True) if MAT_A2 else None
-        c3, st3 = gemm(a2 if MAT_A2 else c2, width, True, W3, width, True, M2, cout, width,
-                       stats=True, pro=None if MAT_A2 else pro2, pro_on_a=True)
+        # conv3 (1x1) on a2 = relu(bn2(c2)), BN3 statistics in the epilogue
+        a2 = lib.bn_apply(c2, ss2, None, None, True)
+        c3, st3 = gemm(a2, width, True, W3, width, True, M2, cout, width, stats=True)
         mean3, inv3, ss3 = lib.bn_stats(c3, st3, g3, b3, bn3.running_mean, bn3.running_var,
                                         _bn_momentum(bn3), bn3.eps)
         if bnd is not None:
@@ -457,7 +360,6 @@ class _BottleneckFn(torch.autograd.Function):
         ctx.geom = (N, Cin, H, W, N2, H2, W2_, width, cout, M, M2)
         ctx.conv2 = (list(stride), list(conv2.padding), list(conv2.dilation))
         ctx.params = (w1, g1, b1, w2, g2, b2, w3, g3, b3, wd, gd, bd)
-        _FWD_SLOT[0] = (out.data_ptr(), (N2, cout, H2, W2_), c3, mean3, bits3)
         return _nchw(out, N2, H2, W2_)
 
     @staticmethod
@@ -474,13 +376,9 @@ class _BottleneckFn(torch.autograd.Function):
         o3 = _bn_grad_outs(g3p, b3p)
         # (the shortcut gradient dy·[out>0] is never materialised: its consumers read dy and
         # the bitmap — the dx GEMM as a masked addend, the shortcut BN through its ReLU mode)
-        rows3 = None
-        slot, _BWD_SLOT[0] = _BWD_SLOT[0], None
-        if slot is not None and slot[0] == dr.data_ptr() and slot[2] == c3.data_ptr():
-            rows3 = slot[1]             # reduced by the next block's dx GEMM epilogue
         grads = {}
         dual = None
-        if has_down and BN_DUAL and rows3 is None:
+        if has_down:
             cd, gd, meand, invd = saved[22], saved[24], saved[25], saved[26]
             od = _bn_grad_outs(gdp, bdp)
             dc3, dcd, dg3, db3, dgd, dbd = lib.bn_bwd_dual(dr, c3, cd, bits3, g3, mean3, inv3, gd,
@@ -489,82 +387,64 @@ class _BottleneckFn(torch.autograd.Function):
             dual = (dcd, dgd, dbd, od)
         else:
             dc3, dg3, db3, _ = lib.bn_bwd(dr, c3, None, g3, mean3, inv3, None, True, True, False,
-                                          bits3, o3[0], o3[1], rows3)
+                                          bits3, o3[0], o3[1])
         grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
-        # conv3: weight gradient on a2 (or with BN2-apply recomputed in the B prologue), fp32
-        # accumulated into the arena
-        lane = _WgradLane(dc3.device)
+        # conv3: weight gradient on a2, fp32 accumulated into the arena
         dst3, d3 = _wgrad_target(w3, (cout, width))
         with _deferred_reduce(dc3, d3):
-            lane.run(lambda: gemm(dc3, cout, False, c2 if a2 is None else a2, width, False, cout,
-                                  width, M2, out_bf16=False,
-                                  pro=(ss2[:width], ss2[width:]) if a2 is None else None,
-                                  pro_on_a=False, out=dst3, accumulate=True, split_k=True))
-        grads["w3"] = _wgrad_done(lane, w3, dst3, d3)
-        # da2 = dc3·W3, its epilogue doing BN2's backward reduction (mask from c2 via ss2)
-        da2, rows2 = gemm_dgrad(dc3, cout, W3, M2, width, cout, stats=BSTATS,
-                                bst=(c2, mean2, ss2, None) if BSTATS else None)
+            gemm(dc3, cout, False, a2, width, False, cout, width, M2, out_bf16=False, out=dst3,
+                 accumulate=True, split_k=True)
+        grads["w3"] = _wgrad_done(w3, dst3, d3)
+        # da2 = dc3·W3
+        da2, _ = gemm_dgrad(dc3, cout, W3, M2, width, cout)
         o2 = _bn_grad_outs(g2p, b2p)
         dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False,
-                                      None, o2[0], o2[1], rows2 if BSTATS else None)
+                                      None, o2[0], o2[1])
         grads["g2"], grads["b2"] = _finish_bn(g2p, b2p, dg2, db2, o2)
-        # conv2 (3x3) backward on the implicit GEMM: the weight gradient reads a1 (or
-        # recomputes relu(bn1(c1)) in its staging prologue) and accumulates fp32 straight into
-        # the arena
+        # conv2 (3x3) backward on the implicit GEMM: the weight gradient reads a1 and accumulates
+        # fp32 straight into the arena
         stride, padding, dilation = ctx.conv2
         dc2n = _nchw(dc2, N2, H2, W2_)
-        c1n = _nchw(c1 if a1 is None else a1, N, H, W)
-        pro1 = (ss1[:width], ss1[width:]) if a1 is None else None
+        a1n = _nchw(a1, N, H, W)
         if _direct(w2) and w2.grad.is_contiguous(memory_format=CL):
             with _deferred_reduce(dc2n, True):
-                lane.run(lambda: conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding, pro=pro1,
-                                            out=w2.grad))
-            lane.finish(lambda: _finish_param(w2, None, True))
+                conv_wgrad(dc2n, a1n, tuple(w2.shape), stride, padding, out=w2.grad)
+            _finish_param(w2, None, True)
             grads["w2"] = None
         else:
-            dW2 = lane.run(lambda: conv_wgrad(dc2n, c1n, tuple(w2.shape), stride, padding,
-                                              pro=pro1).contiguous(memory_format=CL))
+            dW2 = conv_wgrad(dc2n, a1n, tuple(w2.shape), stride, padding).contiguous(
+                memory_format=CL)
             if _direct(w2):
-                lane.finish(lambda: _finish_param(w2, dW2, True))
+                _finish_param(w2, dW2, True)
                 grads["w2"] = None
             else:
                 grads["w2"] = dW2.view_as(w2)
-        # da1 = conv3x3ᵀ(dc2), its epilogue doing BN1's backward reduction
-        if BSTATS:
-            da1n, rows1 = conv_dgrad(dc2n, W2, (H, W), stride, padding, bst=(c1, mean1, ss1, None))
-        else:
-            da1n, rows1 = conv_dgrad(dc2n, W2, (H, W), stride, padding), None
-        da1 = _rows(da1n)
+        # da1 = conv3x3ᵀ(dc2)
+        da1 = _rows(conv_dgrad(dc2n, W2, (H, W), stride, padding))
         o1 = _bn_grad_outs(g1p, b1p)
         dc1, dg1, db1, _ = lib.bn_bwd(da1, c1, None, g1, mean1, inv1, ss1, True, True, False,
-                                      None, o1[0], o1[1], rows1)
+                                      None, o1[0], o1[1])
         grads["g1"], grads["b1"] = _finish_bn(g1p, b1p, dg1, db1, o1)
         xr = _rows(x)
         dst1, d1 = _wgrad_target(w1, (width, Cin))
         with _deferred_reduce(dc1, d1):
-            lane.run(lambda: gemm(dc1, width, False, xr, Cin, False, width, Cin, M,
-                                  out_bf16=False, out=dst1, accumulate=True, split_k=True))
-        grads["w1"] = _wgrad_done(lane, w1, dst1, d1)
+            gemm(dc1, width, False, xr, Cin, False, width, Cin, M, out_bf16=False, out=dst1,
+                 accumulate=True, split_k=True)
+        grads["w1"] = _wgrad_done(w1, dst1, d1)
         if has_down:
             xsr, cd, Wd, gd, meand, invd = saved[21:]
             s = ctx.down_stride
-            if dual is not None:
-                dcd, dgd, dbd, od = dual
-            else:
-                od = _bn_grad_outs(gdp, bdp)
-                dcd, dgd, dbd, _ = lib.bn_bwd(dr, cd, None, gd, meand, invd, None, True, True,
-                                              False, bits3, od[0], od[1])
+            dcd, dgd, dbd, od = dual
             grads["gd"], grads["bd"] = _finish_bn(gdp, bdp, dgd, dbd, od)
             dstd, dd = _wgrad_target(wd, (cout, Cin))
             with _deferred_reduce(dcd, dd):
                 if s == 1:
-                    lane.run(lambda: gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2,
-                                          out_bf16=False, out=dstd, accumulate=True,
-                                          split_k=True))
+                    gemm(dcd, cout, False, xsr, Cin, False, cout, Cin, M2, out_bf16=False,
+                         out=dstd, accumulate=True, split_k=True)
                 else:                 # strided pixel gather of x in the weight-gradient conv
-                    lane.run(lambda: conv_wgrad(_nchw(dcd, N2, H2, W2_), x, (cout, Cin, 1, 1), s,
-                                                0, out=dstd.view(cout, Cin, 1, 1)))
-            grads["wd"] = _wgrad_done(lane, wd, dstd, dd)
+                    conv_wgrad(_nchw(dcd, N2, H2, W2_), x, (cout, Cin, 1, 1), s, 0,
+                               out=dstd.view(cout, Cin, 1, 1))
+            grads["wd"] = _wgrad_done(wd, dstd, dd)
             dx, _ = gemm_dgrad(dc1, width, W1, M, Cin, width)
             if s == 1:
                 gemm_dgrad(dcd, cout, Wd, M2, Cin, cout, out=dx, addend=dx)
@@ -574,15 +454,8 @@ class _BottleneckFn(torch.autograd.Function):
                 conv_dgrad(_nchw(dcd, N2, H2, W2_), Wd.view(cout, Cin, 1, 1), (H, W), s, 0,
                            out=dx, addend=dx)
         else:
-            prev = ctx.prev           # the previous block's (c3, mean3, bits3): reduce its BN3
-            dx, rows_prev = gemm_dgrad(dc1, width, W1, M, Cin, width, addend=dr,
-                                       addend_bits=bits3, stats=prev is not None,
-                                       bst=(prev[0], prev[1], None, prev[2]) if prev is not None
-                                       else None)
-            if prev is not None:
-                _BWD_SLOT[0] = (dx.data_ptr(), rows_prev, prev[0].data_ptr())
-        ctx.prev = None
-        lane.join()                   # the weight gradients are done before anything reads them
+            # dx = dc1·W1 + dy·[out>0]: the masked shortcut gradient added in the epilogue
+            dx, _ = gemm_dgrad(dc1, width, W1, M, Cin, width, addend=dr, addend_bits=bits3)
         dxn = _nchw(dx, N, H, W)
         return (dxn, grads["w1"], grads["g1"], grads["b1"], grads["w2"], grads["g2"], grads["b2"],
                 grads["w3"], grads["g3"], grads["b3"], grads.get("wd"), grads.get("gd"),

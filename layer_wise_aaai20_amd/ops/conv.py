@@ -20,7 +20,6 @@ A 3-channel input (the image) runs as a 4-channel one whose chunks are two adjac
 from __future__ import annotations
 
 import math
-import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -38,44 +37,27 @@ ROW_TILES = with_mf32((1, 2, 3, 5, 6))
 COL_TILES = with_mf32((1, 2, 4, 6))
 # 256x256 / 256x128 8-wave LDS-DMA tiles (csrc/gemm_big.hip, row gather): one stride-1 class,
 # C % 64 == 0 (a K-tile inside one tap), K-contiguous weight, no prologue / addend / statistics
-# of the backward; LWAAAI_CONV_BIG=0 leaves them out of the tuner's candidates
-BIG_TILES = (21, 22) if os.environ.get("LWAAAI_CONV_BIG", "1") != "0" else ()
+# of the backward
+BIG_TILES = (21, 22)
 # the direct 7x7/2 stem convolution from an LDS patch (csrc/conv.hip k_stem_conv7), a tuner
-# candidate of the ResNet stem's forward (337 vs 392 us at bs 256, profiles/r3s2/);
-# LWAAAI_STEM_DIRECT=0 leaves it out
+# candidate of the ResNet stem's forward (337 vs 392 us at bs 256, profiles/r3s2/). (A direct
+# 3x3/1 64-channel kernel from an LDS patch measured 130 / 151 us against 127 / 117 us for the
+# implicit GEMM, profiles/r3s2/direct_probe.txt, and was removed in round 6.)
 STEM_DIRECT = 31
-STEM_DIRECT_ON = os.environ.get("LWAAAI_STEM_DIRECT", "1") != "0"
-# the direct 3x3/1 convolution 64 -> 64 channels from an LDS patch (csrc/conv.hip
-# k_conv3_direct), for that forward and its data gradient (flipped, transposed weight). Opt-in
-# (LWAAAI_CONV3_DIRECT=1): at bs 256 it measured 130 us forward / 151 us data gradient against
-# 127 / 117 us for the implicit-GEMM tiles (profiles/r3s2/direct_probe.txt) — its 149 KB of LDS
-# (patch + the whole weight) leave one workgroup per CU, so staging and MFMAs do not overlap
-CONV3_DIRECT = 32
-CONV3_DIRECT_ON = os.environ.get("LWAAAI_CONV3_DIRECT", "0") != "0"
-
-
-def _conv3_direct_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
-    return (CONV3_DIRECT_ON and c == 64 and co == 64 and (R, S) == (3, 3) and (sh, sw) == (1, 1)
-            and (ph, pw) == (1, 1) and H % 8 == 0 and (8 * W) % 112 == 0 and 8 * W <= 448)
 # the tap-reuse 3x3/1 convolution (csrc/conv3tap.hip k_conv3_tap): the input patch of a
 # 224-pixel tile is staged once per 32-channel chunk and read by all 9 taps (the implicit GEMM
 # gathers it 9 times), forward and — flipped, transposed weight — data gradient. C % 32 == 0,
-# Co == 64 or Co % 128 == 0, image width dividing 224. LWAAAI_CONV3_TAP=0 leaves it out.
+# Co == 64 or Co % 128 == 0, image width dividing 224.
 CONV3_TAP = 33
-CONV3_TAP_ON = os.environ.get("LWAAAI_CONV3_TAP", "1") != "0"
 
 
 def _conv3_tap_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
-    if not (CONV3_TAP_ON and (R, S) == (3, 3) and (sh, sw) == (1, 1) and (ph, pw) == (1, 1)):
+    if not ((R, S) == (3, 3) and (sh, sw) == (1, 1) and (ph, pw) == (1, 1)):
         return False
     if c % 32 or c < 32 or not (co == 64 or co % 128 == 0) or W < 4 or 224 % W:
         return False
     rows = 224 // W
     return ((rows + 2) * W + 2) * 64 <= 24 * 1024
-
-
-_TAP_PACK = os.environ.get("LWAAAI_TAP_PACK", "1") != "0"
-_NKC_PACK = os.environ.get("LWAAAI_NKC_PACK", "1") != "0"
 
 
 # K-contiguous data-gradient weight packs (csrc/conv.hip k_pack_dgrad_kc: 1x1 transposes Wᵀ, the
@@ -85,9 +67,7 @@ _NKC_PACK = os.environ.get("LWAAAI_NKC_PACK", "1") != "0"
 # tensors (the bf16 mirror's views, refreshed in place every step, or bf16 parameters updated in
 # place), so a key's data pointer cannot be reused by another tensor while listed; entries not
 # asked for in a step are dropped. Only between the gradient engine's begin_step (kc_new_step)
-# and its finish (kc_end_step): a backward outside an engine step packs per request, as does
-# LWAAAI_KC_BATCH=0.
-KC_BATCH = os.environ.get("LWAAAI_KC_BATCH", "1") != "0"
+# and its finish (kc_end_step): a backward outside an engine step packs per request.
 _KC = {"gen": -1, "armed": False, "reg": {}, "cache": {}, "used": set()}
 _STEP_GEN = [0]
 
@@ -112,7 +92,7 @@ def kc_pack(wb: torch.Tensor, cls, sh: int, sw: int, kmax: int, fresh: bool = Fa
     ``kmax == 0`` — through the per-step batch (``fresh``: a pack of its own, e.g. timed by the
     tuner with its GEMM)."""
     lib = load()
-    if fresh or not (KC_BATCH and _KC["armed"]) or not wb.is_cuda:
+    if fresh or not _KC["armed"] or not wb.is_cuda:
         return _pack1(lib, wb, cls, sh, sw, kmax)
     key = (wb.data_ptr(), tuple(wb.shape), tuple(cls), sh, sw, kmax)
     if _KC["gen"] != _STEP_GEN[0]:
@@ -149,7 +129,7 @@ def tap_dgrad_weight(w: torch.Tensor, fresh: bool = True) -> torch.Tensor:
     w[co][ci][2-r][2-s], K-contiguous [C][9 Co]."""
     co, c, R, S = w.shape
     wb = w.to(h16())
-    if (_TAP_PACK and wb.is_cuda and (R, S) == (3, 3) and co % 8 == 0 and
+    if (wb.is_cuda and (R, S) == (3, 3) and co % 8 == 0 and
             wb.is_contiguous(memory_format=CL)):
         # one pack kernel walking the window backwards (was flip + two copies, ~15 µs a call)
         return kc_pack(wb, [2, 2, 3, 3], -1, -1, 9 * co, fresh or wb is not w).view(c, 9 * co)
@@ -178,11 +158,11 @@ def supported(cin: int, cout: int, groups: int = 1, dilation=(1, 1)) -> bool:
 class ConvTuner(Tuner):
     """First sight of a problem key: time every candidate (tile, or (tile, splits)) with HIP
     events on scratch outputs and keep the fastest — MIOpen-find-style, but over our own
-    kernels only. ``LWAAAI_CONV_TUNE=0`` keeps the heuristic choice; ``LWAAAI_TUNE_FILE`` pins
+    kernels only. ``LWAAAI_GEMM_TUNE=0`` keeps the heuristic choice; ``LWAAAI_TUNE_FILE`` pins
     the choices (``ops/tuning.py``)."""
 
     def __init__(self):
-        super().__init__("conv", "LWAAAI_CONV_TUNE")
+        super().__init__("conv", "LWAAAI_GEMM_TUNE")
 
 
 TUNER = ConvTuner()
@@ -243,7 +223,7 @@ def pack_dgrad_weight(w: torch.Tensor, classes, sh: int, sw: int,
     permute / slice / cat form (the reference implementation of the same layout)."""
     co, c, R, S = w.shape
     wb = w.to(h16())
-    if (_NKC_PACK and wb.is_cuda and c % 8 == 0 and wb.is_contiguous(memory_format=CL) and
+    if (wb.is_cuda and c % 8 == 0 and wb.is_contiguous(memory_format=CL) and
             wb.data_ptr() % 16 == 0):
         cls, offs, off = [], [], 0
         for (_ch, _cw, r0, s0, TR, TS, *_r) in classes:
@@ -308,9 +288,6 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
         if tile == STEM_DIRECT:               # NHWC output: as the [pixels, Co] GEMM rows
             ys, sts = lib.stem_conv7(xin, op)
             return ys.permute(0, 2, 3, 1).reshape(M, co), sts
-        if tile == CONV3_DIRECT:
-            ys, sts = lib.conv3_direct(xin, op, True)
-            return ys.permute(0, 2, 3, 1).reshape(M, co), sts
         if tile == CONV3_TAP:
             ys, sts = lib.conv3_tap(xin, op, co, bool(stats))
             return ys.permute(0, 2, 3, 1).reshape(M, co), (sts if stats else None)
@@ -319,13 +296,10 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
     key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats,
            bias is not None, bool(relu))
     big = BIG_TILES if (not c4 and C % 64 == 0 and pro is None and co % 8 == 0) else ()
-    direct = (STEM_DIRECT,) if (STEM_DIRECT_ON and c4 and co == 64 and (R, S) == (7, 7) and
+    direct = (STEM_DIRECT,) if (c4 and co == 64 and (R, S) == (7, 7) and
                                 (sh, sw) == (2, 2) and (ph, pw) == (3, 3) and pro is None and
                                 bias is None and not relu and Ho % 4 == 0 and
                                 (4 * Wo) % 112 == 0 and 4 * Wo <= 448) else ()
-    if (pro is None and bias is None and not relu and not c4 and
-            _conv3_direct_fits(C, co, R, S, sh, sw, ph, pw, H, W)):
-        direct = direct + (CONV3_DIRECT,)
     if (pro is None and bias is None and not relu and not c4 and
             _conv3_tap_fits(C, co, R, S, sh, sw, ph, pw, H, W)):
         direct = direct + (CONV3_TAP,)
@@ -335,18 +309,13 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
 
 
 def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=None,
-               out: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None,
-               bst=None):
+               out: Optional[torch.Tensor] = None, addend: Optional[torch.Tensor] = None):
     """dx [N, C, H, W] (bf16 channels_last) of conv2d(x, w) given dy [N, Co, Ho, Wo].
 
     ``out`` (bf16 [N*H*W, C] rows) receives the result — only the pixels some tap reaches are
     written — and ``addend`` (same layout, may be ``out`` itself) is added to them after rounding:
     ``conv_dgrad(dy, w, hw, 2, 0, out=dx, addend=dx)`` accumulates a strided 1x1 shortcut's data
-    gradient into dx in place.
-
-    ``bst = (x, mean, scale_shift, bits)`` (see ``ops/block.py gemm``): also return the per-tile
-    backward statistics of the BN+ReLU whose input was ``x`` (rows per parity class), i.e.
-    ``(dx, stats_rows)``."""
+    gradient into dx in place."""
     lib = load()
     sh, sw = _pair(stride)
     ph, pw = _pair(padding)
@@ -356,7 +325,6 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
     Nb, _, Ho, Wo = dyc.shape
     classes = _dgrad_classes(H, W, R, S, sh, sw, ph, pw)
     if not classes:
-        assert bst is None, "backward statistics of an all-zero gradient"
         if out is not None:
             return _nchw_rows(out, Nb, H, W)
         return torch.zeros((Nb, c, H, W), dtype=h16(), device=dy.device, memory_format=CL)
@@ -380,15 +348,10 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
         geom += [TR, TS, oh, ow, Hg, Wg, ch, cw, TR * TS * co, off]
     M = max(Nb * cl[6] * cl[7] for cl in classes)
 
-    bx, bm, bss, bb = bst if bst is not None else (None, None, None, None)
-
     def run(cand, dst=None, add=None, fresh=True):
         layout, tile = cand
-        if layout in ("direct", "tap") and (dst is not None or add is not None):
+        if layout == "tap" and (dst is not None or add is not None):
             layout, tile = "kc", 2            # the direct kernels write a fresh tensor only
-        if layout == "direct":        # conv of dy with W'[ci][r][s][co] = w[co][ci][2-r][2-s]
-            ys, _ = lib.conv3_direct(dyc, tap_dgrad_weight(w, fresh), False)
-            return ys.permute(0, 2, 3, 1).reshape(-1, c), None
         if layout == "tap":           # (the flip + transpose pack is timed with the conv)
             ys, _ = lib.conv3_tap(dyc, tap_dgrad_weight(w, fresh), c, False)
             return ys.permute(0, 2, 3, 1).reshape(-1, c), None
@@ -400,25 +363,19 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
             return lib.conv_ex(dyc, wk, CV_A, g, c, tile, 1, True, None, None, False, dst, False,
                                0, True, kmax, add)
         return lib.conv_ex(dyc, nkc_weight(fresh), CV_A, geom, c, tile, 1, True, None, None,
-                           bst is not None, dst, False, 0, False, c, add, bx, bm, bss, bb)
+                           False, dst, False, 0, False, c, add)
     key = ("d", tuple(dyc.shape), tuple(w.shape), H, W, sh, sw, ph, pw, addend is not None,
-           bst is not None)
+           False)
     # the weight as [K][C] (the kernel's transposing LDS reads) or packed K-contiguous [C][K]
-    # (LDS-DMA staging of both operands); backward statistics need the first
+    # (LDS-DMA staging of both operands)
     big = BIG_TILES if (len(classes) == 1 and sh == 1 and sw == 1 and co % 64 == 0 and
-                        c % 8 == 0 and addend is None and bst is None) else ()
-    cands = [("nkc", t) for t in ROW_TILES] + \
-        ([("kc", t) for t in ROW_TILES + big] if bst is None else [])
-    if (addend is None and bst is None and out is None and
-            _conv3_direct_fits(co, c, R, S, sh, sw, ph, pw, Ho, Wo) and (H, W) == (Ho, Wo)):
-        cands.append(("direct", CONV3_DIRECT))
-    if (addend is None and bst is None and out is None and
+                        c % 8 == 0 and addend is None) else ()
+    cands = [("nkc", t) for t in ROW_TILES] + [("kc", t) for t in ROW_TILES + big]
+    if (addend is None and out is None and
             _conv3_tap_fits(co, c, R, S, sh, sw, ph, pw, Ho, Wo) and (H, W) == (Ho, Wo)):
         cands.append(("tap", CONV3_TAP))
     cand = TUNER.pick(key, run, cands, ("nkc", _row_default(M, c)))   # (timed on scratch outputs)
-    dx, st = run(cand, out, addend, False)
-    if bst is not None:
-        return _nchw_rows(dx, Nb, H, W), st
+    dx, _ = run(cand, out, addend, False)
     return _nchw_rows(dx, Nb, H, W)
 
 

@@ -5,7 +5,6 @@ without changing a single parameter / buffer name (checkpoints stay compatible).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn.functional as F
@@ -212,8 +211,8 @@ def _fused_basic_forward(self, x):
 
 # The stem backward's BN statistics pass reads the pooled gradient and the pooled map (saved from
 # the forward) instead of the 112x112 conv output and the slot bytes (csrc/bn.hip
-# k_stem_pool_reduce_out); LWAAAI_STEM_POOLED=0 keeps the full-resolution reduce
-STEM_POOLED = os.environ.get("LWAAAI_STEM_POOLED", "1") != "0"
+# k_stem_pool_reduce_out); False (tests only) keeps the full-resolution reduce
+STEM_POOLED = True
 
 
 class _StemPoolFn(torch.autograd.Function):

@@ -66,9 +66,10 @@ def _pinned(key: str):
 _AGREE: list = []          # stack of (process group, device) set by rank_agreement()
 
 # The GEMM tiles 1..6 also exist on v_mfma_f32_32x32x16 (csrc GemmTile id + 40: gemm_core.h k_gemm
-# MF = 32); every tuner times them as further candidates. LWAAAI_MF32=0 leaves them out.
+# MF = 32); every tuner times them as further candidates (profiles/r5/mf32_ab.txt: they win
+# on some shapes and lose overall, so the tuner decides per shape).
 MF32 = 40
-MF32_ON = os.environ.get("LWAAAI_MF32", "1") != "0"
+MF32_ON = True
 
 
 def with_mf32(tiles) -> tuple:

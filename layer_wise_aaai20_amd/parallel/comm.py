@@ -17,6 +17,14 @@ import torch.distributed as dist
 dist = dist  # re-exported for callers that need ReduceOp / backend queries
 
 
+def inject_fault(kind: str, rank_: int) -> bool:
+    """Test hook: ``LWAAAI_INJECT_FAULT=<kind>:<rank>`` (kinds: ``capture`` — the step-graph
+    capture raises, ``native_init`` — the native RCCL init raises before joining) fires on that
+    rank only."""
+    spec = os.environ.get("LWAAAI_INJECT_FAULT", "")
+    return spec == f"{kind}:{int(rank_)}"
+
+
 def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized()
 
@@ -139,10 +147,10 @@ class NativeRccl:
             uid = self.lib.rccl_unique_id() if self.rank == 0 else \
                 torch.zeros(128, dtype=torch.uint8)
             uid = _bcast_uid(uid, group, dev)
-        if os.environ.get("LWAAAI_FAKE_NATIVE_INIT_FAIL", "") == str(self.rank):
+        if inject_fault("native_init", self.rank):
             # test hook: this rank fails BEFORE joining ncclCommInitRank, so its peers are left
             # waiting inside their (non-blocking) init until the deadline aborts it
-            raise RuntimeError("injected native init failure (LWAAAI_FAKE_NATIVE_INIT_FAIL)")
+            raise RuntimeError("injected native init failure (LWAAAI_INJECT_FAULT)")
         self.handle = int(self.lib.rccl_init(uid, self.world, self.rank, dev.index or 0,
                                              init_timeout()))
 

@@ -47,9 +47,7 @@ class CompressedDDP(nn.Module):
         self.buffer_sync = buffer_sync
         self._buf_dirty = False
         self.module = module
-        import os
-        self.bf16_weights = (bf16_weights and flat_params and
-                             os.environ.get("LWAAAI_BF16_MIRROR", "1") != "0")
+        self.bf16_weights = bf16_weights and flat_params
         self.process_group = process_group
         self.broadcast_buffers = broadcast_buffers
         self.check_reduction = check_reduction

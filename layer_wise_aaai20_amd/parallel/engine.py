@@ -33,6 +33,9 @@ from ..compress.codecs import Codec, DenseCodec, DenseWrap, TopkCodec, make_code
 from ..compress.plan import SegPlan
 
 MODES = ("layerwise", "entiremodel", "none")
+# entire-model first-pass staging during backward (_plan_stages); False (tests only): the whole
+# chain after backward, the single-launch form the staged one must equal bit for bit
+EM_STAGE = True
 MODE_ALIASES = {"enitremodel": "entiremodel", "entire": "entiremodel", "entire-model": "entiremodel",
                 "layer-wise": "layerwise", "layer": "layerwise", None: "none", "": "none",
                 "None": "none"}
@@ -67,7 +70,8 @@ class GradSyncEngine:
                  seed: int = 2147483647, process_group=None, flat_params: bool = False,
                  world_size: Optional[int] = None, timing: bool = False,
                  overlap_compress: bool = True, dense_below: int = 0,
-                 momentum_correction: float = 0.0, ef_lr_scaled: bool = False):
+                 momentum_correction: float = 0.0, ef_lr_scaled: bool = False,
+                 max_density: Optional[float] = None):
         self.mode = canonical_mode(mode)
         self.method = ref.canonical_method(method) if self.mode != "none" else "none"
         self.pg = process_group
@@ -79,7 +83,6 @@ class GradSyncEngine:
         self.device = self.arena.device
         cap = int(bucket_cap_mb * 2 ** 20)
         first = int(first_bucket_mb * 2 ** 20) if first_bucket_mb else None
-        last_bucket_mb = float(os.environ.get("LWAAAI_LAST_BUCKET_MB", last_bucket_mb or 0))
         last = int(last_bucket_mb * 2 ** 20) if last_bucket_mb else None
         self.buckets: List[Bucket] = plan_buckets(self.arena, self.mode, cap, first,
                                                   last if last and last < cap else None)
@@ -132,9 +135,10 @@ class GradSyncEngine:
             self._lr_prev = torch.zeros(1, dtype=torch.float32, device=self.device)
             self._lr_ratio = torch.ones(1, dtype=torch.float32, device=self.device)
         # what a peer needs to build this engine's codecs for another rank (loopback tests)
+        # (max_density: the capped sparse threshold wire's per-segment capacity, default 5 %)
         self.codec_kw = dict(K=K, V=V, qstates=qstates, seed=self.seed,
                              error_feedback=self.ef is not None, wire=wire,
-                             dense_below=int(dense_below or 0))
+                             dense_below=int(dense_below or 0), max_density=max_density)
         self.codecs: List[Codec] = []
         self.plans: List[SegPlan] = []
         for b in self.buckets:
@@ -180,7 +184,6 @@ class GradSyncEngine:
         # compression + collective launch run on a side HIP stream, ordered after the bucket's
         # last gradient by an event, so they overlap the rest of the backward pass; the compute
         # stream waits on a second event only when it decodes in finish()
-        overlap_compress = overlap_compress and os.environ.get("LWAAAI_OVERLAP", "1") != "0"
         self._side = (torch.cuda.Stream(device=self.device)
                       if overlap_compress and self.device.type == "cuda" else None)
         # inside a captured step (LWAAAI_GRAPH_OVERLAP):
@@ -189,12 +192,15 @@ class GradSyncEngine:
         #   "comm" compression inline, only the bucket's RCCL collective on a side branch;
         #   "1"    compression and collective both on the side branch, overlapping the rest of
         #          backward (the reference's hook-driven DDP, sparsified_ddp.py:403-452);
-        #   "auto" (default) "1" with a real RCCL communicator at world > 1 — the xGMI transfer
-        #          then runs beside backward instead of on its critical path — "0" otherwise (one
-        #          rank, or the loopback stand-in without a wire model, where a fork/join pair in a
-        #          replayed HIP graph costs more than the in-memory "collective" it would hide:
-        #          profiles/r5/sim8_overlap_modes.jsonl). The wire-priced world-8 simulation
-        #          (profiles/r6/sim8_wire_*.jsonl) measures the modes with the transfer included.
+        #   "auto" (default) = "0": the measured winner with the xGMI transfer priced in. The
+        #          world-8 simulation with every collective paying its modelled wire time on 16
+        #          busy workgroups (profiles/r6/sim8_wire_r50.jsonl, train/simworld.py) exposed
+        #          ResNet-50 layer-wise Top-K 0.1 % by 0.22 ms inline vs 0.74 ms ("1") and 0.87 ms
+        #          ("comm"); entire-model QSGD-255 on the quantised reduce-scatter wire 0.48 /
+        #          0.83 / 0.41 ms; AlexNet entire-model Top-K 0.07 ms in all three. The step is
+        #          throughput-bound: side-branch kernels slow the backward GEMMs they run beside
+        #          by more than the transfers they hide (3 x ~75 KB / 15 us latency per step for
+        #          Top-K).
         # Eager (uncaptured) steps keep the side stream.
         mode = os.environ.get("LWAAAI_GRAPH_OVERLAP", "auto")
         if mode not in ("0", "1", "comm", "auto"):
@@ -230,9 +236,7 @@ class GradSyncEngine:
             raise ValueError(f"graph overlap mode {mode!r}: expected auto, 0, 1 or comm")
         self._overlap_mode = mode
         if mode == "auto":
-            real = isinstance(self._native, comm.NativeRccl) or (
-                self._native is not None and getattr(self._native, "wire_model", None))
-            mode = "1" if self.world > 1 and real else "0"
+            mode = "0"
         self._graph_overlap = mode != "0"
         self._comm_only = mode == "comm"
 
@@ -274,12 +278,11 @@ class GradSyncEngine:
         error-feedback fold) on the side stream, overlapped with the rest of backward. The
         histogram counts are integers and the quantisers' partials land in per-task slots, so
         the result is bit-identical to the single launch (tests/test_loopback_gpu.py); only the
-        rest of the chain stays after backward. ``LWAAAI_EM_STAGE=0``: off. (Momentum correction
+        rest of the chain stays after backward. (Momentum correction
         and LR-scaled residuals rewrite the gradient in their prologue: no staging with them.)"""
         self._stages = []
         if not (self.mode == "entiremodel" and self.device.type == "cuda" and self.mom is None
-                and not self.lr_scaled and len(self.codecs) == 1
-                and os.environ.get("LWAAAI_EM_STAGE", "1") != "0"):
+                and not self.lr_scaled and len(self.codecs) == 1 and EM_STAGE):
             return
         codec = self.codecs[0]
         sel = codec.inner if isinstance(codec, DenseWrap) else codec
@@ -362,8 +365,7 @@ class GradSyncEngine:
         step reads it from ``opt``'s device hyper tensor), ``opt.step()`` after backward. Returns
         the number of buckets fused (0: nothing changes)."""
         self._sgd, self._sgd_buckets = None, frozenset()
-        if self.device.type != "cuda" or self.arena.param_buf is None or \
-                os.environ.get("LWAAAI_FUSED_SGD", "1") == "0":
+        if self.device.type != "cuda" or self.arena.param_buf is None:
             opt.exclude_segments(())
             return 0
         from ..compress.plan import UNPACK_CHUNK
@@ -431,8 +433,7 @@ class GradSyncEngine:
         """The velocity update can run inside the Top-K chain's first pass: a GPU Top-K codec
         whose segments are the bucket's parameters (layer-wise), unstaged."""
         return (g.device.type == "cuda" and type(sel) is TopkCodec and
-                self.mode == "layerwise" and not self._stages and
-                os.environ.get("LWAAAI_MC_FUSE", "1") != "0")
+                self.mode == "layerwise" and not self._stages)
 
     def _mc_prologue(self, bi: int, g: torch.Tensor, u: torch.Tensor) -> None:
         """g' = g + wd·p/grad_scale ; u = mc·u + g' ; g = u over bucket ``bi``."""
@@ -499,8 +500,6 @@ class GradSyncEngine:
         next step on). The caller must be the segment's only gradient contribution when it
         overwrites (ops/gemm.py _ReplicatedLinearFn: VGG-16's 103 M-weight fc1, whose zeroing
         plus read-add-write cost about three passes over 412 MB a step)."""
-        if os.environ.get("LWAAAI_CLAIM_OVERWRITE", "1") == "0":
-            return False                 # (not counted: the segment stays under zeroing)
         self._claims[seg_index] += 1
         return self._claims[seg_index] == 1 and seg_index in self._no_zero
 

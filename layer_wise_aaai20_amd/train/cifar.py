@@ -57,7 +57,7 @@ def run_batches(model, batches, training, world_size=1, optimizer_step=None, sta
     :class:`~..parallel.ddp.CompressedDDP` synchronises its gradients from backward hooks and
     zeroes its gradient arena at the next forward, so no post-backward sync / zero_grad here;
     its whole step is replayed as one HIP graph once warm (``graph``, default on:
-    ``LWAAAI_CIFAR_GRAPH=0`` keeps it eager)."""
+    ``LWAAAI_GRAPH=0`` keeps it eager)."""
     stats = stats or StatsLogger(("loss", "correct"))
     if not training and hasattr(model, "sync_buffers"):
         model.sync_buffers()             # collective: rank 0's BN statistics before evaluation
@@ -67,7 +67,7 @@ def run_batches(model, batches, training, world_size=1, optimizer_step=None, sta
     dev_type = next(model.parameters()).device.type
     if graph is None:
         import os
-        graph = os.environ.get("LWAAAI_CIFAR_GRAPH", "1") == "1"
+        graph = os.environ.get("LWAAAI_GRAPH", "1") != "0"
     gs = _graphed_step(model, optimizer_step, autocast, dev_type, graph) \
         if training and hooked else None
     for i, batch in enumerate(batches):

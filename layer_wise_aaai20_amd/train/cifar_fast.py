@@ -107,8 +107,8 @@ class CifarTrainer:
         self.last = None
         # whole step as one HIP graph after 3 eager steps (train/graphs.py): at 1.5-6 ms per
         # step the per-kernel host launch cost is a large share of an eager CIFAR step
-        if graph is None:          # LWAAAI_CIFAR_GRAPH=0 keeps the CIFAR step eager
-            graph = os.environ.get("LWAAAI_CIFAR_GRAPH", "1") == "1"
+        if graph is None:          # LWAAAI_GRAPH=0 keeps the CIFAR step eager
+            graph = os.environ.get("LWAAAI_GRAPH", "1") != "0"
         self.graphed = StepGraph(self._eager, self.ddp.engine, self.opt, self.device, 3, graph)
 
     def next_batch(self):

@@ -122,8 +122,9 @@ class StepGraph:
                 return self._eager_timed(inputs, n)
             err = None
             try:
-                if os.environ.get("LWAAAI_FAKE_CAPTURE_FAIL", "") == str(self._rank()):
-                    raise RuntimeError("injected capture failure (LWAAAI_FAKE_CAPTURE_FAIL)")
+                from ..parallel.comm import inject_fault
+                if inject_fault("capture", self._rank()):
+                    raise RuntimeError("injected capture failure (LWAAAI_INJECT_FAULT)")
                 g = self._capture(inputs, sig)
             except Exception as e:             # noqa: BLE001 — any failure joins the agreement
                 # (a rank that skipped _agree would leave its peers blocked in it until the

@@ -4,13 +4,12 @@ compute stream and priced against max(FLOP / dense bf16 peak, minimum bytes / HB
 the calls sorted by the time they spend above that floor, then totals per kind.
 
 usage: python scripts/op_roofline.py [--peak-tf 2300] [--hbm-tbs 6.3] [--top 40]
-(LWAAAI_OVERLAP=0 is set so the compression side stream does not interleave with the events.)"""
+(the engine's side stream is dropped so compression does not interleave with the events.)"""
 import argparse
 import collections
 import os
 import sys
 
-os.environ.setdefault("LWAAAI_OVERLAP", "0")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
@@ -252,6 +251,7 @@ def main():
         setattr(lwconv, nm, wrap_conv(nm.replace("_", "-"), getattr(lwconv, nm)))
     tr = build_trainer("resnet50", device=dev, compress="layerwise", method="Topk", K=0.001,
                        graph=False)
+    tr.ddp.engine._side = None          # compression inline: no side stream between the events
     B = a.batch
     imgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, device=dev)
     tgt = torch.randint(0, 1000, (B,), device=dev)

@@ -255,7 +255,7 @@ def cifar_graph_vs_eager(rank, world, dev, network, compress, method, ef, kw, st
 
 
 def capture_fallback_collective(rank, world, dev):
-    """LWAAAI_FAKE_CAPTURE_FAIL=1 makes rank 1's capture fail: every rank must then run eagerly
+    """LWAAAI_INJECT_FAULT=capture:1 makes rank 1's capture fail: every rank must then run eagerly
     (no replays anywhere) and the parameters must still agree."""
     os.environ["LWAAAI_GRAPH_AUTO"] = "0"
     from layer_wise_aaai20_amd.train.imagenet import build_trainer
@@ -274,7 +274,7 @@ def capture_fallback_collective(rank, world, dev):
 
 
 def native_init_fallback(rank, world, dev):
-    """LWAAAI_FAKE_NATIVE_INIT_FAIL=1: rank 1 rejects its native communicator; every rank must
+    """LWAAAI_INJECT_FAULT=native_init:1: rank 1 rejects its native communicator; every rank must
     fall back to c10d (no native communicator anywhere) and still train in agreement."""
     from layer_wise_aaai20_amd.train.imagenet import build_trainer
     torch.manual_seed(0)

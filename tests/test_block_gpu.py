@@ -230,31 +230,3 @@ def test_stem_pool_backward_ill_conditioned_channels(shape, monkeypatch):
     # (dx is not compared with fp32 elementwise: bf16 ties in a 3x3 window send a pixel's
     # gradient to a different argmax than fp32 picks; test_stem_bn_relu_pool_matches_layers
     # pins dx against the unfused bf16 layers instead)
-
-
-def test_backward_stats_epilogues_match_reduce_pass(monkeypatch):
-    """LWAAAI_BSTATS / LWAAAI_CROSS_BN3 (BN backward reductions in the data-gradient GEMM / conv
-    epilogues, off by default — slower on MI355X, see profiles/r2_bstats_ab.log): a 3-block
-    stack (stride-2 downsample block, then identity blocks, so the cross-block BN3 hand-off runs)
-    gives the same gradients as the reduce-pass path up to summation order."""
-    torch.manual_seed(5)
-    stack = torch.nn.Sequential(_make(256, 128, 2, True), _make(512, 128, 1, False),
-                                _make(512, 128, 1, False)).cuda().to(memory_format=CL)
-    x = torch.randn(4, 256, 16, 16, device="cuda").to(torch.bfloat16).contiguous(
-        memory_format=CL)
-    g = torch.randn(4, 512, 8, 8, device="cuda").to(torch.bfloat16).contiguous(
-        memory_format=CL)
-    grads = {}
-    for on in (False, True):
-        monkeypatch.setattr(blk, "BSTATS", on)
-        monkeypatch.setattr(blk, "CROSS_BN3", on)
-        m = copy.deepcopy(stack)
-        for b in m:
-            fuse_resnet(b, block=True)
-        xb = x.clone().requires_grad_()
-        with torch.autocast("cuda", dtype=torch.bfloat16):
-            y = m(xb)
-        y.backward(g)
-        grads[on] = [xb.grad] + [p.grad for p in m.parameters()]
-    for a, b in zip(grads[True], grads[False]):
-        assert _rel(a, b) < 2e-2, _rel(a, b)

@@ -186,67 +186,6 @@ def _unpack_bits(bits, n):
     return out.bool()
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
-@pytest.mark.parametrize("mask", ["bits", "affine"])
-def test_gemm_backward_bn_stats_epilogue(tile, mask):
-    """EPI_BSTATS: dy = A·B (+ masked addend) and, per M-tile, (Σdy', Σdy'·(x−mean)) with
-    dy' = dy·mask — the reduce pass of the BN backward the output feeds — vs fp32 torch on the
-    stored bf16 output."""
-    G = _lib()
-    torch.manual_seed(tile)
-    M, N, K = 1000, 96, 128
-    A = (torch.randn(M, K, device="cuda") * 0.5).to(torch.bfloat16)
-    B = (torch.randn(K, N, device="cuda") * 0.5).to(torch.bfloat16)
-    add = torch.randn(M, N, device="cuda").to(torch.bfloat16)
-    add_bits = torch.randint(0, 256, (M * N // 8,), dtype=torch.uint8, device="cuda")
-    x = torch.randn(M, N, device="cuda").to(torch.bfloat16)
-    mean = torch.randn(N, device="cuda") * 0.1
-    ss = torch.cat([torch.randn(N, device="cuda"), torch.randn(N, device="cuda") * 0.2])
-    bits = torch.randint(0, 256, (M * N // 8,), dtype=torch.uint8, device="cuda")
-    C, st = G.gemm_ex(A, K, True, B, N, False, M, N, K, None, False, 1, True, tile, None, None,
-                      True, True, None, add, False, 0, add_bits, x, mean,
-                      None if mask == "bits" else ss, bits if mask == "bits" else None)
-    ref = (A.float() @ B.float()).to(torch.bfloat16).float() + \
-        add.float() * _unpack_bits(add_bits, M * N).view(M, N)
-    torch.testing.assert_close(C.float(), ref.to(torch.bfloat16).float(), atol=2e-2, rtol=2e-2)
-    if mask == "bits":
-        m = _unpack_bits(bits, M * N).view(M, N)
-    else:
-        m = x.float() * ss[:N] + ss[N:] > 0
-    d = C.float() * m
-    s = st.sum(0)
-    torch.testing.assert_close(s[0], d.sum(0), atol=1e-2, rtol=1e-3)
-    torch.testing.assert_close(s[1], (d * (x.float() - mean)).sum(0), atol=1e-2, rtol=1e-3)
-
-
-@pytest.mark.parametrize("stride", [1, 2])
-def test_conv_dgrad_backward_bn_stats_epilogue(stride):
-    """The data-gradient conv's EPI_BSTATS rows (one block of rows per parity class) fold to the
-    BN backward reduction of its own output."""
-    from layer_wise_aaai20_amd.ops.conv import conv_dgrad
-    torch.manual_seed(stride)
-    Nb, C, Co, H, W = 3, 64, 64, 14, 14
-    Ho = (H + 2 - 3) // stride + 1
-    dy = torch.randn(Nb, Co, Ho, Ho, device="cuda").to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    w = (torch.randn(Co, C, 3, 3, device="cuda") * 0.1).to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    x = torch.randn(Nb, C, H, W, device="cuda").to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    mean = torch.randn(C, device="cuda") * 0.1
-    ss = torch.cat([torch.randn(C, device="cuda"), torch.randn(C, device="cuda") * 0.2])
-    xr = x.permute(0, 2, 3, 1).reshape(-1, C)
-    dx, st = conv_dgrad(dy, w, (H, W), stride, 1, bst=(xr, mean, ss, None))
-    ref = torch.nn.grad.conv2d_input(x.shape, w.float(), dy.float(), stride=stride, padding=1)
-    torch.testing.assert_close(dx.float(), ref, atol=5e-2, rtol=2e-2)
-    d = dx.permute(0, 2, 3, 1).reshape(-1, C).float()
-    m = xr.float() * ss[:C] + ss[C:] > 0
-    d = d * m
-    s = st.sum(0)
-    torch.testing.assert_close(s[0], d.sum(0), atol=1e-2, rtol=1e-3)
-    torch.testing.assert_close(s[1], (d * (xr.float() - mean)).sum(0), atol=1e-2, rtol=1e-3)
-
-
 @pytest.mark.parametrize("M,N,K", [(512, 512, 512), (520, 264, 328), (1000, 136, 72),
                                    (256, 1024, 2048), (64, 40, 8)])
 @pytest.mark.parametrize("splits", [1, 3])

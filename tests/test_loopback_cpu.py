@@ -98,11 +98,11 @@ def test_fixed_capacity_threshold_wire(method, kw, density, monkeypatch):
     """The graph-capturable sparse threshold wire (fixed per-segment capacity): with room for
     every hit it equals the exact dense-wire result; with too little room the hits that do not
     fit stay in the error-feedback residual, so decoded == mean_r(what each rank sent)."""
-    monkeypatch.setenv("LWAAAI_THRESH_DENSITY", str(density))
     res = {}
     for wire in ("dense", "sparse-capped"):
         eng = GradSyncEngine(_params(), mode="layerwise", method=method, error_feedback=True,
-                             bucket_cap_mb=0.01, world_size=W, wire=wire, **kw)
+                             bucket_cap_mb=0.01, world_size=W, wire=wire,
+                             max_density=density if wire == "sparse-capped" else None, **kw)
         if wire == "sparse-capped":
             assert all(c.graph_safe and c.name == "threshold" for c in eng.codecs)
         peers = [_grads(eng, 100 + r) for r in range(1, W)]
@@ -150,9 +150,9 @@ def test_loopback_quantised_reduce_scatter(method, kw, mode, world):
         assert engs[0].stats.payload_bytes < engs[1].stats.payload_bytes * (world - 1)
 
 
-def test_graph_overlap_auto_mode():
-    """LWAAAI_GRAPH_OVERLAP=auto: exchange on the side branch only with a (simulated-wire or
-    real) communicator at world > 1; inline at world 1 and for the wire-less loopback."""
+def test_graph_overlap_modes():
+    """LWAAAI_GRAPH_OVERLAP=auto is the measured winner with the wire priced in (inline, "0"),
+    at any world size and with any communicator; "1" / "comm" remain selectable."""
     from layer_wise_aaai20_amd.parallel.loopback import WireModel
     e1 = GradSyncEngine(_params(), mode="layerwise", method="Topk", K=0.05)
     assert e1.graph_overlap_mode() == "0"
@@ -161,6 +161,8 @@ def test_graph_overlap_auto_mode():
     assert e.graph_overlap_mode() == "0"
     lb.wire_model = WireModel()
     e.set_graph_overlap("auto")
+    assert e.graph_overlap_mode() == "0"
+    e.set_graph_overlap("1")
     assert e.graph_overlap_mode() == "1"
     e.set_graph_overlap("comm")
     assert e.graph_overlap_mode() == "comm"

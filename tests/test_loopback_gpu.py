@@ -157,13 +157,14 @@ EM_CASES = [("Topk", True, {"K": 0.001}), ("RandomDithering", False, {"qstates":
 def test_entiremodel_staged_equals_single_launch(method, ef, kw, monkeypatch):
     """Entire-model mode with its first pass staged per arena slice during backward (VERDICT r4
     item 3; parallel/engine.py _plan_stages) vs the same step with the whole chain after backward
-    (LWAAAI_EM_STAGE=0): a world-8 ResNet-50 step with the loopback peers, HIP-graph replay,
+    (engine.EM_STAGE = False): a world-8 ResNet-50 step with the loopback peers, HIP-graph replay,
     parameters bit-identical after 6 steps."""
     monkeypatch.setenv("LWAAAI_GRAPH_AUTO", "0")
+    from layer_wise_aaai20_amd.parallel import engine as E
     from layer_wise_aaai20_amd.train.imagenet import build_trainer
     runs = {}
     for stage in ("1", "0"):
-        monkeypatch.setenv("LWAAAI_EM_STAGE", stage)
+        monkeypatch.setattr(E, "EM_STAGE", stage == "1")
         torch.manual_seed(0)
         tr = build_trainer("resnet50", device="cuda", compress="entiremodel", method=method,
                            error_feedback=ef, graph=True, world_size=W, bucket_cap_mb=16.0, **kw)

@@ -90,8 +90,8 @@ def _bits_of(keep):
 
 
 @pytest.mark.parametrize("tile", MF32)
-def test_mf32_masked_addend_and_backward_stats(tile):
-    """dy·W + dres·[bit] rounded as the MF = 16 twin rounds it, and the EPI_BSTATS reduce."""
+def test_mf32_masked_addend(tile):
+    """dy·W + dres·[bit] rounded as the MF = 16 twin rounds it."""
     lib = _lib()
     torch.manual_seed(6 + tile)
     M, N, K = 1000, 96, 128
@@ -100,19 +100,11 @@ def test_mf32_masked_addend_and_backward_stats(tile):
     add = torch.randn(M, N, device="cuda").bfloat16()
     keep = torch.rand(M, N, device="cuda") > 0.4
     add_bits = _bits_of(keep)
-    x = torch.randn(M, N, device="cuda").bfloat16()
-    mean = torch.randn(N, device="cuda") * 0.1
-    bits = torch.randint(0, 256, (M * N // 8,), dtype=torch.uint8, device="cuda")
-    C, st = lib.gemm_ex(A, K, True, B, N, False, M, N, K, None, False, 1, True, tile, None, None,
-                        True, True, None, add, False, 0, add_bits, x, mean, None, bits)
+    C, _ = lib.gemm_ex(A, K, True, B, N, False, M, N, K, None, False, 1, True, tile, None, None,
+                       True, False, None, add, False, 0, add_bits)
     base = (A.float() @ B.float()).bfloat16().float()
     ref = (base + add.float() * keep).bfloat16().float()
     torch.testing.assert_close(C.float(), ref, atol=3e-2, rtol=2e-2)
-    m = torch.stack([(bits.to(torch.int32) >> k) & 1 for k in range(8)], 1).reshape(M, N).bool()
-    d = C.float() * m
-    s = st.sum(0)
-    torch.testing.assert_close(s[0], d.sum(0), atol=1e-2, rtol=1e-3)
-    torch.testing.assert_close(s[1], (d * (x.float() - mean)).sum(0), atol=1e-2, rtol=1e-3)
 
 
 def _pin(monkeypatch, choice):
@@ -177,6 +169,6 @@ def test_mf32_twins_are_tuner_candidates():
     from layer_wise_aaai20_amd.ops import block as BK
     from layer_wise_aaai20_amd.ops.tuning import MF32_ON
     if not MF32_ON:
-        pytest.skip("LWAAAI_MF32=0")
+        pytest.skip("32x32 twins disabled")
     assert set(MF32) <= set(BK.TILES)
     assert {41, 42, 43, 45, 46} <= set(CV.ROW_TILES) and {41, 42, 44, 46} <= set(CV.COL_TILES)

@@ -111,7 +111,7 @@ def test_cifar_trainer_ranks_agree_and_graph_matches_eager(net, mode, method, ef
 
 @need2
 def test_capture_failure_is_a_collective_decision():
-    res = run_world(capture_fallback_collective, 2, env={"LWAAAI_FAKE_CAPTURE_FAIL": "1"})
+    res = run_world(capture_fallback_collective, 2, env={"LWAAAI_INJECT_FAULT": "capture:1"})
     for replays, enabled, same in res:
         assert replays == 0 and not enabled and same
 
@@ -120,7 +120,7 @@ def test_capture_failure_is_a_collective_decision():
 def test_native_init_failure_falls_back_everywhere():
     # rank 1 fails before it joins ncclCommInitRank: rank 0's non-blocking init must hit its
     # deadline, abort, and both ranks then agree on the c10d fallback (no hang)
-    res = run_world(native_init_fallback, 2, env={"LWAAAI_FAKE_NATIVE_INIT_FAIL": "1",
+    res = run_world(native_init_fallback, 2, env={"LWAAAI_INJECT_FAULT": "native_init:1",
                                                   "LWAAAI_RCCL_INIT_TIMEOUT": "20"})
     for native, same in res:
         assert not native and same

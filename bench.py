@@ -6,11 +6,20 @@ BASELINE.json metric: "images/sec/node + top-1 acc, ResNet-50 Top-K k=0.1% layer
 GPUs". The reference (``IMAGENET/training/train_imagenet_nv.py:388-478``) measures the same step:
 forward, cross-entropy, backward, layer-wise Top-K compression + gradient exchange, SGD step.
 
-What one timed step does here (nothing skipped):
-  uint8 synthetic batch -> fused normalise to bf16 NHWC -> ResNet-50 forward/backward (bf16
-  autocast, channels_last) -> per-bucket HIP Top-K select + pack overlapped with backward ->
-  RCCL all-gather of (index, value) pairs -> rank-ordered unpack/average -> fused SGD (Nesterov,
-  momentum 0.9, wd 1e-4 with BN excluded) over the flat parameter arena.
+What one timed step does here (nothing skipped). The whole step is one captured HIP graph
+(train/graphs.py StepGraph), replayed once per step:
+  uint8 synthetic batch -> fused normalise to bf16 NHWC -> ResNet-50 forward/backward (bf16,
+  channels_last, hand-written MFMA / BN kernels) -> as each gradient bucket (reverse layer order)
+  completes during backward: HIP Top-K select + pack, RCCL all-gather of
+  (index, value) pairs, rank-ordered unpack/average fused with the SGD update (Nesterov, momentum
+  0.9, wd 1e-4 with BN excluded) of that bucket's slice of the flat parameter arena.
+Inside the graph a bucket's compress + collective + decode run inline on the compute stream, in
+backward order, between the layers' kernels (LWAAAI_GRAPH_OVERLAP=0, parallel/engine.py): a side
+stream branch per bucket ("1") measured slower under the wire-priced world-8 simulation
+(README "Overlap of the exchange"; profiles/r6/sim8_wire_*_overlap_modes.jsonl). At world 1 the
+exchange is a no-op and decode+SGD still run. Eager steps (no graph) do overlap the exchange on a
+side stream. --simulate-world W replays the exchange of W ranks on one GPU (parallel/loopback.py) and
+--sim-wire adds the modelled xGMI transfer time as CU-holding busy kernels.
 
 Usage:
   python bench.py                                   # 1 GPU
@@ -102,8 +111,9 @@ def parse():
                          "Top-K 0.1 %%, entire-model QSGD 8-bit) instead of the given method")
     ap.add_argument("--graph", default="on", choices=["on", "off"],
                     help="on: after 3 eager warm-up steps capture the whole step (fwd, bwd, "
-                         "overlapped compression + collectives, SGD) as one HIP graph and "
-                         "replay it (train/imagenet.py ImageNetTrainer)")
+                         "per-bucket compression + collectives + decode/SGD inline in backward "
+                         "order) as one HIP graph and replay it (train/imagenet.py "
+                         "ImageNetTrainer)")
     ap.add_argument("--miopen-find", type=int, default=1,
                     help="1: let MIOpen benchmark conv solvers once (cudnn.benchmark)")
     return ap.parse_args()

@@ -539,11 +539,17 @@ constexpr int64_t kReduceBlocks = 512;
 constexpr int kReduceUnroll = 4;
 static int reduce_slices(int C) { return (C > 128 && C % 128 == 0) ? C / 128 : 1; }
 
-static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblocks) {
+// The dual reduce (three activation streams + the bitmap) on tensors beyond the Infinity Cache:
+// half the workgroups, 228 vs 247 us at the layer-1 shape (profiles/r6/bn_stream_probe2.txt)
+constexpr int64_t kDualReduceBlocks = 256;
+constexpr int64_t kDualFewBlocksMin = int64_t(128) << 20;   // elements per stream
+
+static void reduce_geometry(int64_t M, int C, int64_t& rows_per_block, int& nblocks,
+                            int64_t target = kReduceBlocks) {
   const int nsl = reduce_slices(C);
   const int G = C / nsl / 8;
   const int R = BNT / G;
-  const int64_t rb = (kReduceBlocks + nsl - 1) / nsl;
+  const int64_t rb = (target + nsl - 1) / nsl;
   int64_t rpb = (M + rb - 1) / rb;
   rpb = (rpb + R - 1) / R * R;
   rpb = rpb < R ? R : rpb;
@@ -698,7 +704,7 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
 void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st) {
   int64_t rpb;
   int nb;
-  reduce_geometry(a.M, a.C, rpb, nb);
+  reduce_geometry(a.M, a.C, rpb, nb, a.M * a.C >= kDualFewBlocksMin ? kDualReduceBlocks : kReduceBlocks);
   const auto* x = static_cast<const uint16_t*>(a.x);
   const auto* x2 = static_cast<const uint16_t*>(b.x);
   const auto* dy = static_cast<const uint16_t*>(a.dy);
@@ -1121,6 +1127,14 @@ static void pool_apply_geometry(int64_t rows, int C, int64_t& rpb, int& nb) {
   reduce_geometry(rows, C, rpb, nb);
 }
 
+// The stride-2 2x2-block apply (one output grid point's four input pixels per row): ~4k
+// workgroups, 229 vs 267 us for the stem's 112 -> 56 backward at 512 (profiles/r6/
+// bn_stream_probe2.txt; the statistics pass stays at the reduce geometry, 39 us there)
+constexpr int64_t kPoolS2ApplyBlocks = 4096;
+static void pool_s2_apply_geometry(int64_t rows, int C, int64_t& rpb, int& nb) {
+  reduce_geometry(rows, C, rpb, nb, kPoolS2ApplyBlocks);
+}
+
 // Max-pool of a post-ReLU map without a BatchNorm (VGG / AlexNet conv+ReLU -> MaxPool2d): the
 // forward is k_stem_pool_fwd with scale 1 / shift 0 (relu(v) == v there), the backward only the
 // apply pass with (A, B, C) = (1, 0, 0): dx = the routed pooled gradient masked by [x > 0], i.e.
@@ -1149,7 +1163,7 @@ void relu_pool_bwd(const StemArgs& a, hipStream_t st) {
     const int64_t P = (int64_t)a.N * a.Ho * a.Wo;
     int64_t rpb;
     int nb;
-    pool_apply_geometry(P, a.C, rpb, nb);
+    pool_s2_apply_geometry(P, a.C, rpb, nb);
     hipLaunchKernelGGL((k_stem_pool_bwd_s2<1>), dim3(nb), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                        a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
                        (float*)nullptr, g, rpb);
@@ -1196,7 +1210,7 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
     }
     int64_t rpa;
     int nba;
-    pool_apply_geometry(P, a.C, rpa, nba);
+    pool_s2_apply_geometry(P, a.C, rpa, nba);
     hipLaunchKernelGGL((k_stem_pool_bwd_s2<1>), dim3(nba), dim3(BNT), 0, st, dp, a.idx, x, a.scale,
                        a.shift, a.mean, a.A, a.B, a.Cc, static_cast<uint16_t*>(a.dx),
                        (float*)nullptr, g, rpa);

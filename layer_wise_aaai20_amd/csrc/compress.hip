@@ -1737,6 +1737,10 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
                                                       int ws, int hdr, const int4* __restrict__ gtab,
                                                       int64_t g0, int64_t ng, int qstates,
                                                       uint16_t* __restrict__ out, int64_t n_out) {
+  // no FMA contraction: each product and sum rounds on its own, as the CPU mirror's numpy does.
+  // (The pragma only reaches operators written here: the __f*_rn header helpers carry the file's
+  // fast contraction into the inlined code, where they were fused back into FMAs.)
+#pragma clang fp contract(off)
   const int64_t j = (int64_t)blockIdx.x * NT + threadIdx.x;
   if (j >= ng) return;
   const int4 gt = gtab[g0 + j];
@@ -1755,7 +1759,7 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
         const uint32_t c = ((k < 16 ? w.x : w.y) >> (2 * (k & 15))) & 3u;
-        acc[k] = __fadd_rn(acc[k], c == 1u ? sc : (c == 2u ? -sc : 0.f));
+        acc[k] = acc[k] + (c == 1u ? sc : (c == 2u ? -sc : 0.f));
       }
     } else if (Q == Q_QS8) {
       const uint4* o = reinterpret_cast<const uint4*>(rec);
@@ -1765,8 +1769,7 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
       for (int k = 0; k < EPT; ++k) {
         const int l = (int)(int8_t)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
         const float sg = l > 0 ? 1.f : (l < 0 ? -1.f : 0.f);
-        acc[k] = __fadd_rn(acc[k], __fmul_rn(__fmul_rn(sg, sc),
-                                             __fdiv_rn((float)(l < 0 ? -l : l), (float)qstates)));
+        acc[k] = acc[k] + sg * sc * ((float)(l < 0 ? -l : l) / (float)qstates);
       }
     } else if (Q == Q_QS9) {
       const uint4* o = reinterpret_cast<const uint4*>(rec);
@@ -1777,7 +1780,7 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
       for (int k = 0; k < EPT; ++k) {
         const int l = (int)((w[k >> 2] >> (8 * (k & 3))) & 0xff);
         const float sg = l == 0 ? 0.f : (((sgn >> k) & 1u) ? -1.f : 1.f);
-        acc[k] = __fadd_rn(acc[k], __fmul_rn(__fmul_rn(sg, sc), __fdiv_rn((float)l, (float)qstates)));
+        acc[k] = acc[k] + sg * sc * ((float)l / (float)qstates);
       }
     } else {
       const uint4* o = reinterpret_cast<const uint4*>(rec);
@@ -1791,13 +1794,12 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
       for (int k = 0; k < EPT; ++k) {
         const int l = (int)(int16_t)((w[k >> 1] >> (16 * (k & 1))) & 0xffff);
         const float sg = l > 0 ? 1.f : (l < 0 ? -1.f : 0.f);
-        acc[k] = __fadd_rn(acc[k], __fmul_rn(__fmul_rn(sg, sc),
-                                             __fdiv_rn((float)(l < 0 ? -l : l), (float)qstates)));
+        acc[k] = acc[k] + sg * sc * ((float)(l < 0 ? -l : l) / (float)qstates);
       }
     }
   }
   const float fws = (float)ws;
-  // (explicitly rounded adds / products / quotients: no FMA contraction, so the CPU mirror —
+  // (uncontracted adds / products, correctly rounded quotients, so the CPU mirror —
   // codecs.py QuantRSCodec.reduce_shard — reproduces every shard bit for bit)
   uint16_t* op = out + gt.y;
   if (gt.z == EPT && (gt.y & 7) == 0) {
@@ -1806,12 +1808,12 @@ __global__ __launch_bounds__(NT) void k_dequant_shard(const uint32_t* __restrict
       uint32_t w[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        w[k] = (uint32_t)ElemBF16::rne(__fdiv_rn(acc[8 * q + 2 * k], fws)) |
-               ((uint32_t)ElemBF16::rne(__fdiv_rn(acc[8 * q + 2 * k + 1], fws)) << 16);
+        w[k] = (uint32_t)ElemBF16::rne(acc[8 * q + 2 * k] / fws) |
+               ((uint32_t)ElemBF16::rne(acc[8 * q + 2 * k + 1] / fws) << 16);
       reinterpret_cast<uint4*>(op)[q] = make_uint4(w[0], w[1], w[2], w[3]);
     }
   } else {
-    for (int k = 0; k < gt.z; ++k) op[k] = ElemBF16::rne(__fdiv_rn(acc[k], fws));
+    for (int k = 0; k < gt.z; ++k) op[k] = ElemBF16::rne(acc[k] / fws);
   }
 }
 

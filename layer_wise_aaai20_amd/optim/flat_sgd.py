@@ -50,9 +50,11 @@ class FlatSGD(Optimizer):
         self.device_hyper = False
         self._hyper = None
         self._hyper_host = None
-        # segments a GradSyncEngine updates itself, fused with their decode (set_fused_sgd)
+        # segments a GradSyncEngine updates itself, fused with their decode (set_fused_sgd), and
+        # the hyper-parameters that update used (None: no fused update since the last step)
         self._exclude = frozenset()
         self._sub = None
+        self._fused_mark = None
 
     # torch.optim.SGD-compatible state: momentum_buffer views into the flat buffer
     def _bind_state(self):
@@ -94,6 +96,25 @@ class FlatSGD(Optimizer):
                 self._sub = (wd, plan.all_large_tables(device), wd[idx].contiguous())
         return self._sub[1], self._sub[2]
 
+    def fused_hyper(self) -> tuple:
+        """What a fused decode-and-step reads: (lr, momentum, dampening, nesterov, first-step
+        flag, grad_scale, weight decays)."""
+        return (float(self._uniform("lr")), float(self._uniform("momentum")),
+                float(self._uniform("dampening")), bool(self._uniform("nesterov")),
+                bool(self._first), float(self.grad_scale),
+                tuple(float(g["weight_decay"]) for g in self.param_groups))
+
+    def mark_fused_update(self, hyper: tuple) -> None:
+        """Called by the gradient engine when backward has already updated the excluded segments
+        (``GradSyncEngine.set_fused_sgd``). A second backward before :meth:`step` would update
+        them twice — the fused contract is one backward, then one step."""
+        if self._fused_mark is not None:
+            raise RuntimeError("a second backward ran before optimizer.step(): the segments "
+                               "updated inside backward (GradSyncEngine.set_fused_sgd) would be "
+                               "stepped twice; call step() after every backward, or build the "
+                               "trainer with fused_sgd=False for gradient accumulation")
+        self._fused_mark = hyper
+
     def _uniform(self, k):
         vals = {g[k] for g in self.param_groups}
         if len(vals) != 1:
@@ -131,6 +152,14 @@ class FlatSGD(Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        if self._exclude:
+            # the segments the engine stepped inside backward used the hyper-parameters of that
+            # moment: a change since then would update the two halves of the model differently
+            mark, self._fused_mark = self._fused_mark, None
+            if mark is not None and mark != self.fused_hyper():
+                raise RuntimeError(f"optimizer hyper-parameters changed between backward and "
+                                   f"step() (fused decode used {mark}, step sees "
+                                   f"{self.fused_hyper()}): set the LR before backward")
         lr = float(self._uniform("lr"))
         mom = float(self._uniform("momentum"))
         damp = float(self._uniform("dampening"))

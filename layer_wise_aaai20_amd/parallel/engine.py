@@ -36,6 +36,8 @@ MODES = ("layerwise", "entiremodel", "none")
 # entire-model first-pass staging during backward (_plan_stages); False (tests only): the whole
 # chain after backward, the single-launch form the staged one must equal bit for bit
 EM_STAGE = True
+# claimed overwrites (claim_overwrite); False (tests only): zero every segment and accumulate
+CLAIM_OVERWRITE = True
 MODE_ALIASES = {"enitremodel": "entiremodel", "entire": "entiremodel", "entire-model": "entiremodel",
                 "layer-wise": "layerwise", "layer": "layerwise", None: "none", "": "none",
                 "None": "none"}
@@ -105,8 +107,11 @@ class GradSyncEngine:
         # DGC-style momentum correction (opt-in, Lin et al. 2018; profiles/r4/ef_root_cause.md):
         # each rank accumulates its velocity u = m·u + (g + wd·p) locally and the error-feedback
         # residual accumulates u instead of g; the coordinates that were sent have their velocity
-        # zeroed (momentum factor masking), except in tensors that were sent whole (dense_below,
-        # or every element kept): those keep ordinary momentum. Weight decay enters the gradient
+        # zeroed (momentum factor masking). With the Top-K / Random-K selection kernels, tensors
+        # sent whole (dense_below, or every element kept) keep ordinary momentum; codecs without
+        # a selection (thresholds, quantisers, the dense parity wire) are masked by k_mc_mask
+        # wherever the residual is zero, so a tensor they send whole restarts its velocity every
+        # step (pinned by tests/test_engine_cpu.py::test_mc_mask_resets_whole_segments). Weight decay enters the gradient
         # BEFORE the velocity, as in DGC (set_mc_weight_decay; the optimizer then runs without
         # momentum and without weight decay — the trainers switch both off). One kernel does the
         # prologue (csrc/optim.hip k_mc_prep); the masking runs inside the select kernels
@@ -500,6 +505,8 @@ class GradSyncEngine:
         next step on). The caller must be the segment's only gradient contribution when it
         overwrites (ops/gemm.py _ReplicatedLinearFn: VGG-16's 103 M-weight fc1, whose zeroing
         plus read-add-write cost about three passes over 412 MB a step)."""
+        if not CLAIM_OVERWRITE:
+            return False                 # (not counted: the segment stays under zeroing)
         self._claims[seg_index] += 1
         return self._claims[seg_index] == 1 and seg_index in self._no_zero
 
@@ -690,6 +697,7 @@ class GradSyncEngine:
             self._ready[i] = True
         self._launch_in_order()
         rec = []
+        fused = False
         hold = list(self._stage_events)          # events some stream still waits on (see below)
         for bi, work, send, recv, (t0, t1, tx), done, ready in self._pending:
             hold += [e for e in (ready, done) if e is not None]
@@ -703,6 +711,9 @@ class GradSyncEngine:
             t2 = self._event() if self.timing else None
             b = self.buckets[bi]
             if bi in self._sgd_buckets:
+                if not fused:
+                    self._sgd.mark_fused_update(self._sgd.fused_hyper())
+                    fused = True
                 self.codecs[bi].decompress_sgd(send, recv, self._sgd_args(bi))
             else:
                 self.codecs[bi].decompress(send, recv, self.arena.grad[b.start:b.end])

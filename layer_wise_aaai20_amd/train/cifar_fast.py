@@ -46,7 +46,7 @@ class CifarTrainer:
                  momentum=0.9, dtype=torch.bfloat16, bucket_cap_mb=25.0, wire="auto",
                  n_train=50000, seed=0, fused=True, graph=None, n_test=1000,
                  task="textures", amp=None, dense_below=0, momentum_correction=False,
-                 lr_scale=1.0, ef_lr_scaled=False, world_size=None):
+                 lr_scale=1.0, ef_lr_scaled=False, world_size=None, fused_sgd=True):
         self.device = torch.device(device or "cuda")
         self.dtype = dtype
         self.bs = batch_size
@@ -79,8 +79,10 @@ class CifarTrainer:
             self.ddp.engine.set_mc_weight_decay(self.opt)
         if ef_lr_scaled:
             self.ddp.engine.lr_source = self.opt.lr_device
-        # layer-wise Top-K buckets: decode and SGD step in one pass (step() sets the LR first)
-        self.ddp.engine.set_fused_sgd(self.opt)
+        # layer-wise Top-K buckets: decode and SGD step in one pass (step() sets the LR first;
+        # fused_sgd=False for gradient accumulation / clipping between backward and the step)
+        if fused_sgd:
+            self.ddp.engine.set_fused_sgd(self.opt)
         ds = D.synthetic_cifar10(n_train, n_test, seed, task=task, amp=amp)
         x = D.transpose(D.normalise(D.pad(ds["train"]["data"], 4)))
         tx = D.transpose(D.normalise(ds["test"]["data"]))

@@ -137,6 +137,8 @@ class StepGraph:
                 # wrote: the eager step's flush must not add them into the arena
                 from ..ops._ext import splitk_discard
                 splitk_discard(torch.empty(0, device=self.device))
+                if hasattr(self.opt, "_fused_mark"):
+                    self.opt._fused_mark = None  # (its fused update never ran either)
             if not self._agree(err is None):
                 self.enabled = False
                 self._graphs.clear()

@@ -117,14 +117,21 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
                   fused=True, momentum=0.9, weight_decay=1e-4, no_bn_wd=True, lr=0.1,
                   bn0=True, wire="auto", graph=None, graph_warmup: int = 3,
                   world_size=None, graph_auto=None, dense_below=0,
-                  momentum_correction=False, loss_scale=None) -> ImageNetTrainer:
+                  momentum_correction=False, loss_scale=None,
+                  fused_sgd: bool = True) -> ImageNetTrainer:
     """``world_size``: build the codecs for that many ranks without a process group (a simulated
     world driven by ``parallel/loopback.py``); default: the process group's size.
 
     ``dtype="fp16"`` with ``fused``: the reference's fp16 recipe on the MFMA kernels — the fp16
     build of the kernel library (``ops/_ext.py set_half``), fp32 master weights with an fp16
     mirror written by the SGD kernel, and a static loss scale (default 1024, as the reference's
-    ``--loss-scale``) unscaled inside that kernel."""
+    ``--loss-scale``) unscaled inside that kernel.
+
+    ``fused_sgd`` (default on): the layer-wise Top-K buckets' decode and their SGD step run in
+    one pass inside backward (``GradSyncEngine.set_fused_sgd``). The contract is one backward,
+    then ``opt.step()`` with the hyper-parameters unchanged in between — FlatSGD raises
+    otherwise; ``fused_sgd=False`` for callers that accumulate, clip or read gradients between
+    backward and the step."""
     device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     tdtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[dtype] \
         if isinstance(dtype, str) else dtype
@@ -152,6 +159,7 @@ def build_trainer(model="resnet50", device=None, compress="layerwise", method="T
     if mc > 0:               # weight decay enters the velocity (and leaves the optimizer)
         ddp.engine.set_mc_weight_decay(opt)
     # layer-wise Top-K buckets: decode and SGD step in one pass (the LR is set before each step)
-    ddp.engine.set_fused_sgd(opt)
+    if fused_sgd:
+        ddp.engine.set_fused_sgd(opt)
     return ImageNetTrainer(ddp, opt, device, tdtype, graph=graph, graph_warmup=graph_warmup,
                            graph_auto=graph_auto, loss_scale=loss_scale)

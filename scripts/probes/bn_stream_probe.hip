@@ -193,7 +193,7 @@ int main(int argc, char** argv) {
       snprintf(nm, 64, "k_bn_bwd_apply<3> grid %d", g);
       rep(nm, T.run([&] {
         hipLaunchKernelGGL((k_bn_bwd_apply<uint16_t, 3, false>), dim3(g), dim3(BNT), 0, 0, x, dy,
-                           (const uint16_t*)nullptr, bits, sc, sh, sc, sh, sh, dx, (uint16_t*)nullptr, n8, C, 0); }),
+                           (const uint16_t*)nullptr, bits, sc, sh, sc, sh, sh, dx, (uint16_t*)nullptr, n8, C); }),
           3 * MB + n8 / 1e6);
       snprintf(nm, 64, "k_bn_apply<0,relu> grid %d", g);
       rep(nm, T.run([&] {
@@ -262,7 +262,7 @@ int main(int argc, char** argv) {
     const double ab = 3 * MB + n8 / 1e6;
     rep("k_bn_bwd_apply<3> (shipped)", T.run([&] {
       hipLaunchKernelGGL((k_bn_bwd_apply<uint16_t, 3, false>), dim3(ag), dim3(BNT), 0, 0, x, dy,
-                         (const uint16_t*)nullptr, bits, sc, sh, A, B, Cc, dx, (uint16_t*)nullptr, n8, C, 0); }), ab);
+                         (const uint16_t*)nullptr, bits, sc, sh, A, B, Cc, dx, (uint16_t*)nullptr, n8, C); }), ab);
     for (int g : {2048, 4096, 8192}) {
       char nm[64];
       snprintf(nm, 64, "bwd_apply_v U2 grid %d", g);

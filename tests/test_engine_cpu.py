@@ -385,3 +385,40 @@ def test_claimed_overwrite_skips_zeroing_once_whole_written():
     view.fill_(5.0)
     eng.finish()
     assert float(view.abs().max()) == 0.0
+
+
+def test_fused_sgd_contract_is_enforced():
+    """with the decode fused into the SGD step, a second backward before step(), or an
+    LR change between backward and step(), raises instead of silently diverging."""
+    import pytest as _pt
+    from layer_wise_aaai20_amd.optim.flat_sgd import FlatSGD
+    from layer_wise_aaai20_amd.parallel.arena import GradArena
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(10, 4)), torch.nn.Parameter(torch.randn(7))]
+    arena = GradArena(list(zip(["a", "b"], ps)), flat_params=True)
+    opt = FlatSGD(ps, arena, lr=0.1, momentum=0.9, nesterov=True)
+    opt.exclude_segments([0])                 # as GradSyncEngine.set_fused_sgd leaves it
+    opt.mark_fused_update(opt.fused_hyper())
+    opt.step()                                # consumes the mark
+    opt.mark_fused_update(opt.fused_hyper())
+    with _pt.raises(RuntimeError, match="second backward"):
+        opt.mark_fused_update(opt.fused_hyper())
+    opt.param_groups[0]["lr"] = 0.05          # LR changed after backward
+    with _pt.raises(RuntimeError, match="changed between backward"):
+        opt.step()
+
+
+def test_mc_mask_resets_whole_segments():
+    """ADVICE r5 (pinned behaviour): on the k_mc_mask path (a threshold codec here) the velocity
+    is zeroed wherever the residual is zero — a segment sent whole restarts its velocity every
+    step, unlike Top-K's selection kernels, which keep momentum for whole segments."""
+    from layer_wise_aaai20_amd.parallel.engine import GradSyncEngine
+    torch.manual_seed(0)
+    ps = [("w", torch.nn.Parameter(torch.randn(64, 8))), ("b", torch.nn.Parameter(torch.randn(8)))]
+    eng = GradSyncEngine(ps, mode="layerwise", method="Thresholdv", V=1e-12, error_feedback=True,
+                         momentum_correction=0.9, bucket_cap_mb=1.0, flat_params=True)
+    for _ in range(2):
+        eng.arena.grad.copy_(torch.randn(eng.arena.numel).sign() * (1 + torch.rand(eng.arena.numel)))
+        eng.sync_now()
+        assert float(eng.ef.abs().max()) == 0.0        # every element above V: sent whole
+        assert float(eng.mom.abs().max()) == 0.0       # ... so its velocity was reset

@@ -57,14 +57,10 @@ def test_cifar_graph_step_fused_sgd_bitwise():
     from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
     outs = []
     for flag in ("0", "1"):
-        os.environ["LWAAAI_FUSED_SGD"] = flag
         torch.manual_seed(0)                        # (the same initial weights for both runs)
-        try:
-            tr = CifarTrainer(device="cuda", n_train=512 * 6, graph=True, network="resnet9",
-                              compress="layerwise", method="Topk", K=0.01, error_feedback=True,
-                              seed=0)
-        finally:
-            os.environ.pop("LWAAAI_FUSED_SGD", None)
+        tr = CifarTrainer(device="cuda", n_train=512 * 6, graph=True, network="resnet9",
+                          compress="layerwise", method="Topk", K=0.01, error_feedback=True,
+                          seed=0, fused_sgd=flag == "1")
         tr.graphed.warmup = 2
         fused = len(tr.ddp.engine._sgd_buckets)
         assert (fused > 0) == (flag == "1")
@@ -82,11 +78,12 @@ def test_cifar_graph_step_fused_sgd_bitwise():
 def test_vgg_claimed_overwrite_matches_zero_and_accumulate():
     """VGG-16's fc1 weight gradient is written by one copy into an arena slice the step did not
     zero (engine.claim_overwrite) instead of zero + add: the trained parameters equal the
-    zero-and-accumulate path's (LWAAAI_CLAIM_OVERWRITE=0), graph-captured steps included."""
+    zero-and-accumulate path's (engine.CLAIM_OVERWRITE = False), graph-captured steps included."""
+    from layer_wise_aaai20_amd.parallel import engine as E
     from layer_wise_aaai20_amd.train.cifar_fast import CifarTrainer
     outs = []
     for flag in ("0", "1"):
-        os.environ["LWAAAI_CLAIM_OVERWRITE"] = flag
+        E.CLAIM_OVERWRITE = flag == "1"
         torch.manual_seed(0)
         try:
             tr = CifarTrainer(device="cuda", n_train=512 * 6, graph=True, network="vgg16",
@@ -99,6 +96,6 @@ def test_vgg_claimed_overwrite_matches_zero_and_accumulate():
                 assert tr.ddp.engine._no_zero, "fc1 should be written by a claimed overwrite"
             outs.append(tr.ddp.arena.param_buf.clone())
         finally:
-            os.environ.pop("LWAAAI_CLAIM_OVERWRITE", None)
+            E.CLAIM_OVERWRITE = True
         del tr
     assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max().item()

@@ -4,7 +4,7 @@ compressor ``ref.topk`` (``kthvalue`` threshold, ``>=`` keeps every tie; ``CIFAR
 bit for bit. All gradients reach the arena in fp32 (the MFMA convolutions / GEMMs accumulate
 their weight gradients in fp32 straight into it), so value ties at the threshold are as rare as
 in the reference's fp32 path and the tie slots of the sparse payload suffice. The decode writes
-the arena gradient (``LWAAAI_FUSED_SGD=0``): the fused decode + SGD step never materialises it."""
+the arena gradient (``fused_sgd=False``): the fused decode + SGD step never materialises it."""
 import pytest
 import torch
 
@@ -15,11 +15,10 @@ pytestmark = pytest.mark.gpu
 
 def test_resnet50_layerwise_topk_bit_exact(monkeypatch):
     from layer_wise_aaai20_amd.train.imagenet import build_trainer
-    monkeypatch.setenv("LWAAAI_FUSED_SGD", "0")
     torch.manual_seed(0)
     K = 0.001
     tr = build_trainer("resnet50", device="cuda", compress="layerwise", method="Topk", K=K,
-                       bn0=False)
+                       bn0=False, fused_sgd=False)
     eng = tr.ddp.engine
     raw = {}
     for bi, codec in enumerate(eng.codecs):

@@ -207,6 +207,10 @@ class GradSyncEngine:
         #          by more than the transfers they hide (3 x ~75 KB / 15 us latency per step for
         #          Top-K).
         # Eager (uncaptured) steps keep the side stream.
+        # Known issue: in the one-GPU rehearsal (2 ranks sharing the card, RCCL over its socket
+        # transport) capturing "1" or "comm" segfaults inside hipStreamEndCapture (profiles/r6/
+        # multigpu_overlap1_r6d.txt, multigpu_overlap_comm_r6f.txt): an RCCL collective on a
+        # forked capture branch; "0" captures and matches eager there (tests/test_multigpu_gpu.py).
         mode = os.environ.get("LWAAAI_GRAPH_OVERLAP", "auto")
         if mode not in ("0", "1", "comm", "auto"):
             raise ValueError(f"LWAAAI_GRAPH_OVERLAP={mode!r}: expected auto, 0, 1 or comm")

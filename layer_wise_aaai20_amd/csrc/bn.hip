@@ -687,6 +687,7 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
                      a.C, a.M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
                      (int)a.training, (int)a.accum_dparams);
+  if (a.coeffs_only) return;
   const dim3 grid(apply_grid(n8, a.C, kApplyBwdGrid)), block(BNT);
 #define LW_BWD(R, D)                                                                            \
   hipLaunchKernelGGL((k_bn_bwd_apply<T, R, D>), grid, block, 0, st, x, dy, y, a.bits, a.scale,  \

@@ -192,6 +192,7 @@ struct BNArgs {
   uint8_t* bits;           // ReLU bitmap, 1 bit/element: written by the forward apply, read back
                            // by the backward instead of the saved output (or nullptr)
   bool accum_dparams;      // backward: dgamma/dbeta += (into the gradient arena) instead of =
+  bool coeffs_only;        // backward: reduce + finalize only (dx formed by a fused consumer)
 };
 int bn_reduce_blocks(int64_t M, int C);
 int colsum_blocks(int64_t rows);     // blocks folding R GEMM-epilogue statistics rows
@@ -201,6 +202,13 @@ void bn_forward(const BNArgs& a, hipStream_t st);
 void bn_backward(const BNArgs& a, hipStream_t st);
 // two BN+ReLU backwards sharing dy and the ReLU bitmap (a bottleneck's BN3 and downsample BN)
 void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st);
+// BN3 backward apply fused with dW3 += dc3ᵀ·a2 and da2 = dc3·W3 (bnfuse.hip): C = 256, Ci = 64;
+// slab [bn3_bwd_dgemm_blocks(M)][256][64] fp32 partials of dW3 (summed by splitk_reduce)
+bool bn3_bwd_dgemm_ok(int64_t M, int C, int Ci);
+int bn3_bwd_dgemm_blocks(int64_t M);
+void bn3_bwd_dgemm(const uint16_t* dr, const uint16_t* c3, const uint8_t* bits, const float* A,
+                   const float* B, const float* Cc, const uint16_t* w3t, const uint16_t* a2,
+                   uint16_t* da2, float* slab, int64_t M, hipStream_t st);
 
 // fused stem: BN-apply + ReLU + max-pool (bn.hip), bf16 NHWC
 struct StemArgs {
@@ -346,6 +354,10 @@ bool conv3_tap_ok(int C, int Co, int H, int W);
 int conv3_tap_tiles_m(int N, int H, int W);
 void conv3_tap(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
                int W, int C, int Co, hipStream_t st);
+// the weight-resident persistent form for C = Co = 64 (same operands, bit-identical output)
+bool conv3_res_ok(int C, int Co, int H, int W);
+void conv3_res(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
+               int W, hipStream_t st);
 // its weight gradient: fp32 dW [Co][3][3][C] (= out, accumulated when `accumulate`), `part` a
 // [splits][Co][9][C] fp32 workspace (splits: conv3_tap_wgrad_splits)
 int conv3_tap_wgrad_splits(int N, int H, int W, int C, int Co);

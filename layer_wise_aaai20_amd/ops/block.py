@@ -45,6 +45,7 @@ returned through autograd as usual.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -64,6 +65,10 @@ CL = torch.channels_last
 # * the downsample block's BN3 and shortcut-BN backwards share dy and the ReLU bitmap: one dual
 #   reduce + one dual apply pass (csrc bn.hip k_bn_reduce DUAL / k_bn_bwd_apply_dual);
 # * weight gradients run inline (a side stream measured no gain: the step is throughput-bound).
+# * the BN3 backward of a 256-channel block (ResNet-50 stage 1, no downsample) runs its apply
+#   inside one kernel with both GEMMs that read dc3 (csrc/bnfuse.hip): dy, c3 and the bitmap are
+#   read once instead of dc3 being written and read twice (LWAAAI_FUSE_BN3=0: the three passes).
+FUSE_BN3 = os.environ.get("LWAAAI_FUSE_BN3", "1") != "0"
 TILES = with_mf32((1, 2, 3, 4, 5, 6))   # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
 BIG = (21, 22)                      # 256x256 / 256x128 8-wave LDS-DMA kernel (csrc/gemm_big.hip)
@@ -385,18 +390,29 @@ class _BottleneckFn(torch.autograd.Function):
                                                            meand, invd, o3[0], o3[1], od[0],
                                                            od[1])
             dual = (dcd, dgd, dbd, od)
+        elif FUSE_BN3 and (cout, width) == (256, 64) and dr.dtype == h16():
+            # BN3's apply fused into both consumers of dc3 (csrc/bnfuse.hip): da2 = dc3·W3 and
+            # dW3 = dc3ᵀ·a2 from one pass over dy, c3 and the bitmap; dc3 is never written
+            dst3, d3 = _wgrad_target(w3, (cout, width))
+            with _deferred_reduce(dr, d3):
+                da2, _, dg3, db3 = lib.bn3_bwd_fused(dr, c3, bits3, g3, mean3, inv3,
+                                                     _kc_weight(W3, cout, width, cout).view(
+                                                         width, cout), a2, dst3, o3[0], o3[1])
+            grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
+            grads["w3"] = _wgrad_done(w3, dst3, d3)
         else:
             dc3, dg3, db3, _ = lib.bn_bwd(dr, c3, None, g3, mean3, inv3, None, True, True, False,
                                           bits3, o3[0], o3[1])
-        grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
-        # conv3: weight gradient on a2, fp32 accumulated into the arena
-        dst3, d3 = _wgrad_target(w3, (cout, width))
-        with _deferred_reduce(dc3, d3):
-            gemm(dc3, cout, False, a2, width, False, cout, width, M2, out_bf16=False, out=dst3,
-                 accumulate=True, split_k=True)
-        grads["w3"] = _wgrad_done(w3, dst3, d3)
-        # da2 = dc3·W3
-        da2, _ = gemm_dgrad(dc3, cout, W3, M2, width, cout)
+        if "w3" not in grads:
+            grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
+            # conv3: weight gradient on a2, fp32 accumulated into the arena
+            dst3, d3 = _wgrad_target(w3, (cout, width))
+            with _deferred_reduce(dc3, d3):
+                gemm(dc3, cout, False, a2, width, False, cout, width, M2, out_bf16=False,
+                     out=dst3, accumulate=True, split_k=True)
+            grads["w3"] = _wgrad_done(w3, dst3, d3)
+            # da2 = dc3·W3
+            da2, _ = gemm_dgrad(dc3, cout, W3, M2, width, cout)
         o2 = _bn_grad_outs(g2p, b2p)
         dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False,
                                       None, o2[0], o2[1])

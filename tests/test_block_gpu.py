@@ -103,6 +103,24 @@ def test_block_direct_arena_gradients():
         assert _rel(p.grad, q.grad) < 0.15, n
 
 
+def test_fused_bn3_backward_matches_three_pass_block(monkeypatch):
+    """A 256-channel bottleneck with BN3's backward fused into its two GEMMs (csrc/bnfuse.hip)
+    gives the three-pass block's input and parameter gradients to bf16 / summation-order noise."""
+    torch.manual_seed(3)
+    ref = _make(256, 64, 1, False).cuda().to(memory_format=CL)
+    x = torch.randn(8, 256, 28, 28, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
+    gy = torch.randn(8, 256, 28, 28, device="cuda").contiguous(memory_format=CL)
+    outs = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(blk, "FUSE_BN3", fuse)
+        m, y, gx = _run(copy.deepcopy(ref), x.float(), gy, True)
+        outs[fuse] = (y.float(), gx.float(), [p.grad.float() for p in m.parameters()])
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert _rel(outs[True][1], outs[False][1]) < 2e-2
+    for a, b in zip(outs[True][2], outs[False][2]):
+        assert _rel(a, b) < 2e-2
+
+
 def test_resnet50_block_vs_layer_path():
     """Whole ResNet-50 step. Deep BN-parameter gradients of a random-init net are chaotic in bf16
     (both fused paths sit ~100 % away from fp32 on some), so the check is statistical: the loss

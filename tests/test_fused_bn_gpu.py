@@ -215,3 +215,41 @@ def test_bn_stats_from_rows_one_launch(M, C, R, monkeypatch):
     for o in outs[1:]:
         assert all(torch.equal(a, b) for a, b in zip(o, outs[0]))
     assert torch.isfinite(rm).all() and not torch.equal(rm, torch.zeros_like(rm))
+
+
+@pytest.mark.parametrize("M", [4096, 3000, 802816 // 16])
+def test_bn3_bwd_fused_matches_three_passes(M):
+    """bn3_bwd_fused (csrc/bnfuse.hip: BN3's apply inside one kernel with da2 = dc3·W3 and
+    dW3 = dc3ᵀ·a2) vs bn_bwd + fp32 products of its dc3: dgamma/dbeta bit-identical (the same
+    reduce + finalize), da2 within bf16 rounding, dW3 within fp32 summation-order noise, and the
+    weight gradient accumulated into a given view. M = 3000 ends in a partial 64-row tile."""
+    from layer_wise_aaai20_amd.ops._ext import h16, load
+    lib = load()
+    C, Ci = 256, 64
+    g = torch.Generator(device="cuda").manual_seed(M)
+    dy = torch.randn(M, C, device="cuda", generator=g).to(h16())
+    x = torch.randn(M, C, device="cuda", generator=g).to(h16())
+    a2 = torch.randn(M, Ci, device="cuda", generator=g).to(h16())
+    w3 = (torch.randn(C, Ci, device="cuda", generator=g) / 16).to(h16())
+    bits = torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device="cuda", generator=g)
+    gam = torch.rand(C, device="cuda", generator=g) + 0.5
+    mean = torch.randn(C, device="cuda", generator=g) * 0.1
+    inv = torch.rand(C, device="cuda", generator=g) + 0.5
+    dgo, dbo = torch.randn(C, device="cuda", generator=g), torch.randn(C, device="cuda", generator=g)
+    rdg, rdb = dgo.clone(), dbo.clone()
+    dc3, _, _, _ = lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits, rdg, rdb)
+    dw = torch.full((C, Ci), 0.25, device="cuda")
+    da2, dwr, dg, db = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3.t().contiguous(), a2, dw,
+                                         dgo, dbo)
+    assert torch.equal(dg, rdg) and torch.equal(db, rdb)
+    assert dwr.data_ptr() == dw.data_ptr()
+    ref_da2 = dc3.float() @ w3.float()
+    err = (da2.float() - ref_da2).abs().max().item()
+    assert err <= 1e-2 * ref_da2.abs().max().item(), err
+    ref_dw = dc3.float().t() @ a2.float()
+    err = ((dw - 0.25) - ref_dw).abs().max().item()
+    assert err <= 1e-4 * ref_dw.abs().max().item() + 1e-3, err
+    # without a destination: a fresh [C, Ci] result
+    _, dw2, _, _ = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3.t().contiguous(), a2, None,
+                                     None, None)
+    torch.testing.assert_close(dw2, dw - 0.25, rtol=1e-5, atol=1e-4)

@@ -1604,41 +1604,22 @@ std::tuple<Tensor, Tensor> conv3_tap(Tensor x, Tensor w, int64_t Co, bool want_s
   return {y, st};
 }
 
-// The weight-resident persistent form (conv3tap.hip k_conv3_res) of conv3_tap for C = Co = 64:
-// the same operands and outputs, bit-identical.
-std::tuple<Tensor, Tensor> conv3_res(Tensor x, Tensor w, bool want_stats) {
-  const c10::DeviceGuard guard(x.device());
-  check_dtype(x, kH16, "x");
-  check_dtype(w, kH16, "w");
-  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 &&
-              x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: [N, C, H, W] channels_last");
-  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  TORCH_CHECK(w.is_contiguous() && w.numel() == 64 * 9 * C, "w: [64][9C] K-contiguous");
-  TORCH_CHECK(lw::conv3_res_ok((int)C, 64, (int)H, (int)W), "conv3_res: unsupported geometry");
-  TORCH_CHECK(x.numel() * 2 < (1LL << 31), "conv3_res: operand > 2 GiB");
-  check_aligned16(x.data_ptr(), "x");
-  check_aligned16(w.data_ptr(), "w");
-  Tensor y = at::empty({N, 64, H, W}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int64_t rows = lw::conv3_tap_tiles_m((int)N, (int)H, (int)W);
-  Tensor st = want_stats ? at::empty({rows, 2, 64}, x.options().dtype(at::kFloat))
-                         : at::empty({0}, x.options().dtype(at::kFloat));
-  lw::conv3_res(ptr<uint16_t>(x), ptr<uint16_t>(w), ptr<uint16_t>(y),
-                want_stats ? ptr<float>(st) : nullptr, (int)N, (int)H, (int)W, cur_stream());
-  launched("conv3_res");
-  return {y, st};
-}
-
 // A bottleneck's BN3 backward (bf16, training, ReLU bitmap) with its apply fused into the two
 // GEMMs that consume dc3 (bnfuse.hip k_bn3_bwd_dgemm): reduce + finalize as bn_bwd, then one
 // kernel forms dc3 tile by tile and writes da2 = dc3·W3 ([M, Ci] bf16) and dW3 = dc3ᵀ·a2 as fp32
-// slabs, summed into dw_out (accumulated: the gradient arena view [C][Ci]) or a fresh [C, Ci]
+// slabs ((C, Ci) = (256, 64) or (512, 128): the ResNet-50 stage-1 / stage-2 BN3), summed into dw_out (accumulated: the gradient arena view [C][Ci]) or a fresh [C, Ci]
 // by the fixed-order split-K reduce (deferred inside a splitk_defer scope). w3t is W3ᵀ [Ci][C].
-// Returns (da2, dW3, dgamma, dbeta); dc3 is never materialised.
-std::tuple<Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused(
+// With x2 (a downsample block: the shortcut BN's input, fed by the same dy and bitmap) the dual
+// reduce runs and the same pass also writes that BN's dx2 (as bn_bwd_dual's). Returns (da2, dW3,
+// dgamma, dbeta, dx2, dgamma2, dbeta2) (the last three empty without x2); dc3 is never written.
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused(
     Tensor dy, Tensor x, Tensor bits, c10::optional<Tensor> weight, Tensor mean, Tensor invstd,
     Tensor w3t, Tensor a2, c10::optional<Tensor> dw_out, c10::optional<Tensor> dgamma_out,
-    c10::optional<Tensor> dbeta_out) {
+    c10::optional<Tensor> dbeta_out, c10::optional<Tensor> x2, c10::optional<Tensor> weight2,
+    c10::optional<Tensor> mean2, c10::optional<Tensor> invstd2,
+    c10::optional<Tensor> dgamma2_out, c10::optional<Tensor> dbeta2_out) {
   const c10::DeviceGuard guard(x.device());
+  const bool dual = x2.has_value() && x2->defined();
   for (const Tensor* t : {&dy, &x, &w3t, &a2}) {
     check_dtype(*t, kH16, "bn3_bwd_fused operand");
     TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->is_contiguous(),
@@ -1648,28 +1629,41 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused(
   const int64_t M = x.size(0), C = x.size(1), Ci = a2.size(1);
   TORCH_CHECK(dy.sizes() == x.sizes() && a2.size(0) == M, "dy / a2 rows must match x");
   TORCH_CHECK(w3t.size(0) == Ci && w3t.size(1) == C, "w3t must be W3ᵀ [Ci][C]");
-  TORCH_CHECK(lw::bn3_bwd_dgemm_ok(M, (int)C, (int)Ci), "bn3_bwd_fused: needs C 256, Ci 64");
+  TORCH_CHECK(lw::bn3_bwd_dgemm_ok(M, (int)C, (int)Ci),
+              "bn3_bwd_fused: needs (C, Ci) = (256, 64) or (512, 128)");
   TORCH_CHECK(bits.scalar_type() == at::kByte && bits.numel() * 8 == x.numel() &&
               bits.is_contiguous(), "bits must be a contiguous uint8 [numel/8] bitmap");
+  TORCH_CHECK(mean.numel() == C && invstd.numel() == C, "statistics must hold C floats");
+  if (dual) {
+    check_dtype(*x2, kH16, "x2");
+    TORCH_CHECK(x2->sizes() == x.sizes() && x2->is_contiguous() && x2->is_cuda(), "x2 like x");
+    check_aligned16(x2->data_ptr(), "x2");
+    TORCH_CHECK(mean2.has_value() && invstd2.has_value() && mean2->numel() == C &&
+                invstd2->numel() == C, "the shortcut BN's statistics must hold C floats");
+  }
   auto f32 = x.options().dtype(at::kFloat);
-  bool accum = false;
-  Tensor dgamma = dparam_out(dgamma_out, C, x, accum), dbeta = dparam_out(dbeta_out, C, x, accum);
-  TORCH_CHECK(!accum || ((dgamma_out.has_value() && dgamma_out->defined()) &&
-                         (dbeta_out.has_value() && dbeta_out->defined())),
-              "give both dgamma_out and dbeta_out");
-  Tensor coef = at::empty({3 * C}, f32);
-  Tensor partial = at::empty({lw::bn_reduce_blocks(M, (int)C) * 2 * C}, f32);
-  lw::BNArgs a{};
-  a.accum_dparams = accum;
-  a.coeffs_only = true;
+  bool acc1 = false, acc1b = false, acc2 = false, acc2b = false;
+  Tensor dgamma = dparam_out(dgamma_out, C, x, acc1), dbeta = dparam_out(dbeta_out, C, x, acc1b);
+  TORCH_CHECK(acc1 == acc1b, "give both dgamma_out and dbeta_out");
+  Tensor dg2 = dual ? dparam_out(dgamma2_out, C, x, acc2) : at::empty({0}, f32);
+  Tensor db2 = dual ? dparam_out(dbeta2_out, C, x, acc2b) : at::empty({0}, f32);
+  TORCH_CHECK(acc2 == acc2b, "give both dgamma2_out and dbeta2_out");
+  const int64_t nb = lw::bn_reduce_blocks(M, (int)C);
+  Tensor coef = at::empty({(dual ? 6 : 3) * C}, f32);
+  Tensor partial = at::empty({(dual ? 2 : 1) * nb * 2 * C}, f32);
+  lw::BNArgs a{}, b{};
+  for (lw::BNArgs* q : {&a, &b}) {
+    q->M = M;
+    q->C = (int)C;
+    q->bf16 = true;
+    q->training = true;
+    q->relu = true;
+    q->coeffs_only = true;
+  }
+  a.accum_dparams = acc1;
   a.x = x.data_ptr();
   a.dy = dy.data_ptr();
   a.bits = ptr<uint8_t>(bits);
-  a.M = M;
-  a.C = (int)C;
-  a.bf16 = true;
-  a.training = true;
-  a.relu = true;
   a.gamma = optr<float>(weight);
   a.mean = ptr<float>(mean);
   a.invstd = ptr<float>(invstd);
@@ -1680,13 +1674,23 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused(
   a.B = a.A + C;
   a.Cc = a.A + 2 * C;
   hipStream_t st = cur_stream();
-  lw::bn_backward(a, st);
-  Tensor da2 = at::empty({M, Ci}, x.options());
-  const int nblk = lw::bn3_bwd_dgemm_blocks(M);
-  Tensor slab = at::empty({(int64_t)nblk * C * Ci}, f32);
-  lw::bn3_bwd_dgemm(ptr<uint16_t>(dy), ptr<uint16_t>(x), ptr<uint8_t>(bits), a.A, a.B, a.Cc,
-                    ptr<uint16_t>(w3t), ptr<uint16_t>(a2), ptr<uint16_t>(da2), ptr<float>(slab),
-                    M, st);
+  Tensor dx2 = dual ? at::empty_like(x) : at::empty({0}, x.options());
+  if (dual) {
+    b.x = x2->data_ptr();
+    b.gamma = optr<float>(weight2);
+    b.mean = ptr<float>(*mean2);
+    b.invstd = ptr<float>(*invstd2);
+    b.partial = a.partial + nb * 2 * C;
+    b.dgamma = ptr<float>(dg2);
+    b.dbeta = ptr<float>(db2);
+    b.accum_dparams = acc2;
+    b.A = a.A + 3 * C;
+    b.B = a.A + 4 * C;
+    b.Cc = a.A + 5 * C;
+    lw::bn_backward_dual(a, b, st);
+  } else {
+    lw::bn_backward(a, st);
+  }
   Tensor o;
   const bool have_out = dw_out.has_value() && dw_out->defined();
   if (have_out) {
@@ -1696,20 +1700,32 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused(
                 "dw_out: contiguous [C][Ci] fp32");
     check_aligned16(o.data_ptr(), "dw_out");
   } else {
-    o = at::empty({C, Ci}, f32);
+    o = at::zeros({C, Ci}, f32);
   }
-  lw::GemmArgs g{};
-  g.partial = ptr<float>(slab);
-  g.C = o.data_ptr();
-  g.ldc = Ci;
-  g.M = (int)C;
-  g.N = (int)Ci;
-  g.out_bf16 = false;
-  g.accumulate = have_out;
-  lw::splitk_reduce(g, nblk, st);
-  if (lw::splitk_take_deferred()) splitk_keep().push_back(slab);
+  Tensor da2 = at::empty({M, Ci}, x.options());
+  const int nblk = lw::bn3_bwd_dgemm_slabs(M, (int)C, (int)Ci);
+  // one workgroup adds its dW3 into the destination itself (no slab, no reduce to defer)
+  Tensor slab = nblk > 1 ? at::empty({(int64_t)nblk * C * Ci}, f32) : o;
+  lw::bn3_bwd_dgemm(ptr<uint16_t>(dy), ptr<uint16_t>(x), ptr<uint8_t>(bits), a.A, a.B, a.Cc,
+                    ptr<uint16_t>(w3t), ptr<uint16_t>(a2), ptr<uint16_t>(da2), ptr<float>(slab),
+                    M, (int)C, (int)Ci, st, dual ? ptr<uint16_t>(*x2) : nullptr,
+                    dual ? b.A : nullptr,
+                    dual ? b.B : nullptr, dual ? b.Cc : nullptr,
+                    dual ? ptr<uint16_t>(dx2) : nullptr, nblk == 1);
+  if (nblk > 1) {
+    lw::GemmArgs g{};
+    g.partial = ptr<float>(slab);
+    g.C = o.data_ptr();
+    g.ldc = Ci;
+    g.M = (int)C;
+    g.N = (int)Ci;
+    g.out_bf16 = false;
+    g.accumulate = have_out;
+    lw::splitk_reduce(g, nblk, st);
+    if (lw::splitk_take_deferred()) splitk_keep().push_back(slab);
+  }
   launched("bn3_bwd_fused");
-  return {da2, o, dgamma, dbeta};
+  return {da2, o, dgamma, dbeta, dx2, dg2, db2};
 }
 
 // Weight gradient of the tap-reuse conv (conv3tap.hip k_conv3_tap_wgrad): dy [N, Co, H, W] and
@@ -2089,10 +2105,11 @@ LW_LIBRARY(LW_OPS_NS, m) {
       "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("stem_conv7(Tensor x, Tensor w) -> (Tensor, Tensor)");
   m.def("conv3_tap(Tensor x, Tensor w, int Co, bool want_stats) -> (Tensor, Tensor)");
-  m.def("conv3_res(Tensor x, Tensor w, bool want_stats) -> (Tensor, Tensor)");
   m.def("bn3_bwd_fused(Tensor dy, Tensor x, Tensor bits, Tensor? weight, Tensor mean, "
         "Tensor invstd, Tensor w3t, Tensor a2, Tensor(a!)? dw_out, Tensor(b!)? dgamma_out, "
-        "Tensor(c!)? dbeta_out) -> (Tensor, Tensor, Tensor, Tensor)");
+        "Tensor(c!)? dbeta_out, Tensor? x2=None, Tensor? weight2=None, Tensor? mean2=None, "
+        "Tensor? invstd2=None, Tensor(d!)? dgamma2_out=None, Tensor(e!)? dbeta2_out=None) "
+        "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("conv3_tap_wgrad(Tensor dy, Tensor x, Tensor(a!)? out, bool accumulate) -> Tensor");
   m.def(
       "bn_bwd_dual(Tensor dy, Tensor x, Tensor x2, Tensor bits, Tensor? weight, Tensor mean, "
@@ -2173,7 +2190,6 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("stem_conv7", &stem_conv7);
   m.impl("conv3_tap", &conv3_tap);
   m.impl("conv3_tap_wgrad", &conv3_tap_wgrad);
-  m.impl("conv3_res", &conv3_res);
   m.impl("bn3_bwd_fused", &bn3_bwd_fused);
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);

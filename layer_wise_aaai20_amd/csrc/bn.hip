@@ -717,6 +717,7 @@ void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st) {
     hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((p->C + 3) / 4), dim3(256), 0, st, p->partial, nb,
                        p->C, p->M, p->gamma, p->mean, p->invstd, p->dgamma, p->dbeta, p->A, p->B,
                        p->Cc, 1, (int)p->accum_dparams);
+  if (a.coeffs_only) return;
   const int64_t n8 = a.M * a.C / 8;
   hipLaunchKernelGGL(k_bn_bwd_apply_dual, dim3(apply_grid(n8, a.C, kApplyBwdGrid)), dim3(BNT), 0, st, x, x2, dy,
                      a.bits, a.A, a.B, a.Cc, b.A, b.B, b.Cc, static_cast<uint16_t*>(a.dx),

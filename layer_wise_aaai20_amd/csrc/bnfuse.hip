@@ -1,39 +1,38 @@
-// BatchNorm-backward apply fused with BOTH GEMMs that consume its output, for the ResNet-50
-// stage-1 bottleneck's BN3 (C = 256 channels of c3, 64 of a2), gfx950.
+// BatchNorm-backward apply fused with BOTH GEMMs that consume its output, for the BN3 of the
+// ResNet-50 bottlenecks of stages 1 and 2 (c3: CO = 256 / 512 channels, a2: CI = 64 / 128), gfx950.
 //
 // The per-layer path (ops/block.py) runs, after BN3's reduce + finalize:
-//   dc3 = A·(dr·bit) + B·c3 + C          k_bn_bwd_apply  reads dr, c3, bits; writes dc3 (256 ch)
+//   dc3 = A·(dr·bit) + B·c3 + C          k_bn_bwd_apply  reads dr, c3, bits; writes dc3 (CO ch)
 //   dW3 += dc3ᵀ · a2                     GEMM            reads dc3 again (+ a2)
 //   da2  = dc3 · W3                      GEMM            reads dc3 a third time, writes da2
-// i.e. five 256-channel activation streams (411 MB each at batch 256, 56x56). Here one persistent
-// kernel reads dr, c3 and the bitmap ONCE per 64-pixel tile, forms the bf16 dc3 tile in LDS (the
+// i.e. five CO-channel activation streams (411 / 205 MB each at batch 256). Here one persistent
+// kernel reads dr, c3 and the bitmap ONCE per BM-pixel tile, forms the bf16 dc3 tile in LDS (the
 // apply's exact expression and rounding) and feeds both products from that LDS image:
-//   da2 tile [64 px][64]   = dc3 tile · W3       (W3ᵀ resident in LDS, K = 256 channels)
-//   dW3 [256][64]         += dc3 tileᵀ · a2 tile (accumulated in registers across the tiles of the
-//                                                 workgroup, K = pixels; one fp32 slab per
-//                                                 workgroup, summed in fixed order by the split-K
-//                                                 reduce, gemm.hip)
-// -> two 256-channel streams instead of five (profiles/r6: 230 + 117 + 91 us per block before).
+//   da2 tile [BM px][64]   = dc3 tile · W3[:, part]  (that W3ᵀ part resident in LDS, K = CO)
+//   dW3 [CO][64 of part]  += dc3 tileᵀ · a2 tile    (accumulated in registers across the tiles of
+//                                                    the workgroup, K = pixels; one fp32 slab per
+//                                                    tile group, summed in fixed order by the
+//                                                    split-K reduce, gemm.hip)
+// A workgroup owns one 64-column part of CI (stage 2: two parts); the parts of a tile group are
+// dealt to blocks b, b + 8, ... so they share an XCD and the second reads dr / c3 from its L2.
+// Stage 1: 608.7 -> 410.4 us a block (profiles/r6/fused_bn3/).
 //
 // LDS images (bf16, 16-byte chunks XOR-swizzled by row so that every fragment read is
-// bank-conflict-free; scripts/probes check in the tests):
-//   W3ᵀ [64 ci][256 co] and dc3 [64 px][256 co]: 512-B rows, chunk c at c ^ s512(row), read by
-//     rows with ds_read_b128 (16 rows x chunks 2k, 2k+1 per 16-lane group: s512 distinct) and, for
-//     dc3, by columns with ds_read_b64_tr_b16 (the A operand dc3ᵀ of dW3);
-//   a2 [64 px][64 ci]: 128-B rows, chunk c at c ^ s128(row), read by columns (B operand of dW3);
-//   da2 staging [64 px][64 ci] for 16-byte global stores.
-// Waves (4, 256 threads, two workgroups per CU): da2 rows 16w..16w+15 of ci x 64 px (4 MFMA
-// blocks); dW3 co 64w..64w+63 x all 64 ci (16 MFMA blocks). Per tile and wave: 32 + 32 MFMAs.
+// bank-conflict-free):
+//   W3ᵀ part [64 ci][CO] and dc3 [BM px][CO]: rows of 2·CO bytes, chunk c at c ^ s512(row), read
+//     by rows with ds_read_b128 (16 rows x chunks 2k, 2k+1 per 16-lane group: distinct bank
+//     quads) and, for dc3, by columns with ds_read_b64_tr_b16 (the A operand dc3ᵀ of dW3: rows
+//     8g+q of chunks 2k, 2k+1 per 32-lane half, s512(row) >> 1 distinct);
+//   a2 part [BM px][64 ci]: 128-B rows, chunk c at c ^ s128(row), read by columns (B of dW3);
+//   da2 staging [BM px][64 ci] for 16-byte global stores.
+// Waves (4, 256 threads, one workgroup per CU): da2 ci rows 16w..16w+15 x BM px; dW3 co rows
+// CO/4·w .. +CO/4 x the part's 64 ci.
 #include "gemm_core.h"
-
-#include <cstdlib>
 
 namespace lw {
 
 namespace {
-constexpr int BF_BM = 64;                 // pixels per tile
-constexpr int BF_CO = 256, BF_CI = 64;
-constexpr int BF_LDS = 32768 + 32768 + 8192 + 8192;
+constexpr int BF_CIP = 64;                // a2 / da2 / W3ᵀ columns per workgroup (one part)
 
 __device__ __forceinline__ int s512(int r) { return ((r & 3) << 1) | (r & 8); }
 __device__ __forceinline__ int s128(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
@@ -47,125 +46,177 @@ __device__ __forceinline__ h16x8 cat8(i16x4 lo, i16x4 hi) {
   const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(h16x8, v);
 }
+
+template <int CO> struct BfGeom {
+  static constexpr int BM = CO == 256 ? 64 : 32;        // pixels per tile
+  static constexpr int CPR = CO / 8;                    // 16-byte chunks per dc3 row
+  static constexpr int RSTEP = 256 / CPR;               // rows between one thread's chunks
+  static constexpr int NROW = BM / RSTEP;               // chunks per thread per tile (8)
+  static constexpr int NA = BM * 8 / 256;               // a2 chunks per thread per tile
+  static constexpr int NCB = CO / 64;                   // dW3 16-row blocks per wave
+  static constexpr int W_BYTES = BF_CIP * CO * 2, D_BYTES = BM * CO * 2, A_BYTES = BM * 128;
+  static constexpr int LDS = W_BYTES + D_BYTES + 2 * A_BYTES;
+};
 }  // namespace
 
-template <int OCC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
+// One tile's loads (registers): dy, c3 (and the shortcut's x2) rows, the bitmap bytes, a2 rows
+template <int CO> struct BfRaw {
+  uint4 d[BfGeom<CO>::NROW], x[BfGeom<CO>::NROW], x2[BfGeom<CO>::NROW], a[BfGeom<CO>::NA];
+  uint32_t b[BfGeom<CO>::NROW];
+};
+
+// DUAL: the downsample block, whose shortcut BN (input x2 = cd) received the same dy and ReLU
+// bitmap: dx2 = A2·(dy·bit) + B2·x2 + C2 is formed in the same pass and written out (it feeds the
+// shortcut's weight and data gradients; with two parts, by the part-0 workgroup). One tile of
+// loads is in flight while a tile computes (a second register set, two tiles in flight, measured
+// 435.8 vs 420.4 us at stage 1: profiles/r6/fused_bn3/).
+// acc_out: a single tile group adds its dW3 straight into `slab` (= the destination).
+template <int CO, bool DUAL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict__ c3,
                      const uint8_t* __restrict__ bits, const float* __restrict__ A,
                      const float* __restrict__ B, const float* __restrict__ Cc,
                      const uint16_t* __restrict__ w3t, const uint16_t* __restrict__ a2,
-                     uint16_t* __restrict__ da2, float* __restrict__ slab, int64_t M, int tiles,
-                     int tpw) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[BF_LDS];
-  uint8_t* const sW = lds;                 // W3ᵀ  [64][512 B]
-  uint8_t* const sD = lds + 32768;         // dc3  [64][512 B]
-  uint8_t* const sA = lds + 65536;         // a2   [64][128 B]
-  uint8_t* const sO = lds + 73728;         // da2  [64][128 B]
+                     uint16_t* __restrict__ da2, float* __restrict__ slab,
+                     const uint16_t* __restrict__ x2, const float* __restrict__ A2,
+                     const float* __restrict__ B2, const float* __restrict__ C2,
+                     uint16_t* __restrict__ dx2, int64_t M, int CI, int tiles, int tpw,
+                     int acc_out, int xcd_pairs) {
+  using G = BfGeom<CO>;
+  constexpr int BM = G::BM, RB = CO * 2;              // dc3 / W3ᵀ row bytes
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G::LDS];
+  uint8_t* const sW = lds;                            // W3ᵀ part [64][RB]
+  uint8_t* const sD = lds + G::W_BYTES;               // dc3      [BM][RB]
+  uint8_t* const sA = sD + G::D_BYTES;                // a2 part  [BM][128 B]
+  uint8_t* const sO = sA + G::A_BYTES;                // da2      [BM][128 B]
   const int t = threadIdx.x, l = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int g = l >> 4, q = (l & 15) >> 2, p = l & 3;
-  const int u0 = (int)blockIdx.x * tpw, u1 = min(u0 + tpw, tiles);
-  const uint32_t act_bytes = (uint32_t)(M * BF_CO * 2), a2_bytes = (uint32_t)(M * BF_CI * 2);
+  // block -> (tile group, part): with a multiple of 8 groups the parts of one group are blocks 8
+  // apart (one XCD under round-robin placement: speed only), else consecutive
+  const int nparts = CI / BF_CIP;
+  const int bx = (int)blockIdx.x & 7, by = (int)blockIdx.x >> 3;
+  const int part = xcd_pairs ? by % nparts : (int)blockIdx.x % nparts;
+  const int grp = xcd_pairs ? (by / nparts) * 8 + bx : (int)blockIdx.x / nparts;
+  const int c0 = part * BF_CIP;
+  const int u0 = grp * tpw, u1 = min(u0 + tpw, tiles);
+  const bool write_dx2 = DUAL && part == 0;
+  const uint32_t act_bytes = (uint32_t)(M * CO * 2), a2_bytes = (uint32_t)(M * CI * 2);
   const __amdgpu_buffer_rsrc_t rdr = make_rsrc(dr, act_bytes), rc3 = make_rsrc(c3, act_bytes);
+  const __amdgpu_buffer_rsrc_t rx2 = make_rsrc(DUAL ? x2 : c3, act_bytes);
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(a2, a2_bytes);
 
-  // ---- W3ᵀ into LDS (once)
+  // ---- this part's W3ᵀ rows into LDS (once)
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int e = t + 256 * i, row = e >> 5, ch = e & 31;
-    const uint4 v = *reinterpret_cast<const uint4*>(w3t + row * BF_CO + ch * 8);
-    *reinterpret_cast<uint4*>(sW + row * 512 + ((ch ^ s512(row & 15)) << 4)) = v;
+  for (int i = 0; i < BF_CIP * G::CPR / 256; ++i) {
+    const int e = t + 256 * i, row = e / G::CPR, ch = e % G::CPR;
+    const uint4 v = *reinterpret_cast<const uint4*>(w3t + (int64_t)(c0 + row) * CO + ch * 8);
+    *reinterpret_cast<uint4*>(sW + row * RB + ((ch ^ s512(row & 15)) << 4)) = v;
   }
-  // ---- this thread's 8 channels of the apply: chunk column cc, rows t/32 + 8i
-  const int cc = t & 31, prow = t >> 5;
-  float ca[8], cb[8], ck[8];
+  // ---- this thread's 8 channels of the apply: chunk column cc, rows prow + RSTEP·i
+  const int cc = t % G::CPR, prow = t / G::CPR;
+  float ca[8], cb[8], ck[8], ca2[8], cb2[8], ck2[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) { ca[k] = A[cc * 8 + k]; cb[k] = B[cc * 8 + k]; ck[k] = Cc[cc * 8 + k]; }
+  for (int k = 0; k < 8; ++k) {
+    ca[k] = A[cc * 8 + k]; cb[k] = B[cc * 8 + k]; ck[k] = Cc[cc * 8 + k];
+    ca2[k] = DUAL ? A2[cc * 8 + k] : 0.f;
+    cb2[k] = DUAL ? B2[cc * 8 + k] : 0.f;
+    ck2[k] = DUAL ? C2[cc * 8 + k] : 0.f;
+  }
 
-  uint4 vd[8], vx[8], va[2];
-  uint32_t vb[8];
-  auto load_tile = [&](int u) {
-    const int64_t m0 = (int64_t)u * BF_BM;
+  auto load_tile = [&](int u, BfRaw<CO>& R) {
+    const int64_t m0 = (int64_t)u * BM;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int64_t m = m0 + prow + 8 * i;
-      const uint32_t off = m < M ? (uint32_t)((m * BF_CO + cc * 8) * 2) : OOB;
-      vd[i] = bload16(rdr, off);
-      vx[i] = bload16(rc3, off);
-      vb[i] = m < M ? (uint32_t)bits[m * (BF_CO / 8) + cc] : 0u;
+    for (int i = 0; i < G::NROW; ++i) {
+      const int64_t m = m0 + prow + G::RSTEP * i;
+      const uint32_t off = m < M ? (uint32_t)((m * CO + cc * 8) * 2) : OOB;
+      R.d[i] = bload16(rdr, off);
+      R.x[i] = bload16(rc3, off);
+      if (DUAL) R.x2[i] = bload16(rx2, off);
+      R.b[i] = m < M ? (uint32_t)bits[m * (CO / 8) + cc] : 0u;
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < G::NA; ++i) {
       const int e = t + 256 * i;
       const int64_t m = m0 + (e >> 3);
-      va[i] = bload16(ra, m < M ? (uint32_t)((m * BF_CI + (e & 7) * 8) * 2) : OOB);
+      R.a[i] = bload16(ra, m < M ? (uint32_t)((m * CI + c0 + (e & 7) * 8) * 2) : OOB);
     }
   };
 
-  f32x4 acc2[4][4];
+  f32x4 acc2[G::NCB][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < G::NCB; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (u0 < u1) load_tile(u0);
-  for (int u = u0; u < u1; ++u) {
-    // ---- phase A: dc3 = A·(dr·bit) + B·c3 + C (bf16) and a2 into their LDS images
+  // ---- phase A: dc3 = A·(dy·bit) + B·c3 + C (bf16; k_bn_bwd_apply's expression) and a2 into
+  // their LDS images (DUAL: dx2 straight to memory)
+  auto phase_a = [&](int u, const BfRaw<CO>& R) {
+    const int64_t m0 = (int64_t)u * BM;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t dw[4] = {vd[i].x, vd[i].y, vd[i].z, vd[i].w};
-      const uint32_t xw[4] = {vx[i].x, vx[i].y, vx[i].z, vx[i].w};
-      uint32_t o[4];
+    for (int i = 0; i < G::NROW; ++i) {
+      const uint32_t dw[4] = {R.d[i].x, R.d[i].y, R.d[i].z, R.d[i].w};
+      const uint32_t xw[4] = {R.x[i].x, R.x[i].y, R.x[i].z, R.x[i].w};
+      const uint32_t x2w[4] = {R.x2[i].x, R.x2[i].y, R.x2[i].z, R.x2[i].w};
+      uint32_t o[4], o2[4];
 #pragma unroll
       for (int k2 = 0; k2 < 4; ++k2) {
         float d0 = hlo(dw[k2]), d1 = hhi(dw[k2]);
-        d0 = ((vb[i] >> (2 * k2)) & 1u) ? d0 : 0.f;
-        d1 = ((vb[i] >> (2 * k2 + 1)) & 1u) ? d1 : 0.f;
-        const float o0 = ca[2 * k2] * d0 + cb[2 * k2] * hlo(xw[k2]) + ck[2 * k2];
-        const float o1 = ca[2 * k2 + 1] * d1 + cb[2 * k2 + 1] * hhi(xw[k2]) + ck[2 * k2 + 1];
-        o[k2] = (uint32_t)f2h(o0) | ((uint32_t)f2h(o1) << 16);
+        d0 = ((R.b[i] >> (2 * k2)) & 1u) ? d0 : 0.f;
+        d1 = ((R.b[i] >> (2 * k2 + 1)) & 1u) ? d1 : 0.f;
+        const float v0 = ca[2 * k2] * d0 + cb[2 * k2] * hlo(xw[k2]) + ck[2 * k2];
+        const float v1 = ca[2 * k2 + 1] * d1 + cb[2 * k2 + 1] * hhi(xw[k2]) + ck[2 * k2 + 1];
+        o[k2] = (uint32_t)f2h(v0) | ((uint32_t)f2h(v1) << 16);
+        if (DUAL) {
+          const float e0 = ca2[2 * k2] * d0 + cb2[2 * k2] * hlo(x2w[k2]) + ck2[2 * k2];
+          const float e1 = ca2[2 * k2 + 1] * d1 + cb2[2 * k2 + 1] * hhi(x2w[k2]) + ck2[2 * k2 + 1];
+          o2[k2] = (uint32_t)f2h(e0) | ((uint32_t)f2h(e1) << 16);
+        }
       }
-      const int row = prow + 8 * i;
-      *reinterpret_cast<uint4*>(sD + row * 512 + ((cc ^ s512(row & 15)) << 4)) =
+      const int row = prow + G::RSTEP * i;
+      *reinterpret_cast<uint4*>(sD + row * RB + ((cc ^ s512(row & 15)) << 4)) =
           make_uint4(o[0], o[1], o[2], o[3]);
+      if (write_dx2 && m0 + row < M)
+        *reinterpret_cast<uint4*>(dx2 + (m0 + row) * CO + cc * 8) =
+            make_uint4(o2[0], o2[1], o2[2], o2[3]);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < G::NA; ++i) {
       const int e = t + 256 * i, row = e >> 3, ch = e & 7;
-      *reinterpret_cast<uint4*>(sA + row * 128 + ((ch ^ s128(row & 15)) << 4)) = va[i];
+      *reinterpret_cast<uint4*>(sA + row * 128 + ((ch ^ s128(row & 15)) << 4)) = R.a[i];
     }
-    __syncthreads();
-    if (u + 1 < u1) load_tile(u + 1);      // in flight under this tile's MFMAs
+  };
 
-    // ---- da2 tile: D[ci 16w..][px] = W3ᵀ[ci][co] · dc3[px][co]ᵀ, K = 256 channels
-    f32x4 acc1[4];
+  // ---- phase B: both products from the LDS images, da2 staged and stored
+  auto phase_b = [&](int u) {
+    // da2 tile: D[ci 16w..][px] = W3ᵀ[ci][co] · dc3[px][co]ᵀ, K = CO channels
+    f32x4 acc1[BM / 16];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < BM / 16; ++j) acc1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int ci_r = 16 * w + (l & 15);
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
+    for (int ks = 0; ks < CO / 32; ++ks) {
       const int ch = 4 * ks + g;
-      const h16x8 fa = *reinterpret_cast<const h16x8*>(sW + ci_r * 512 + ((ch ^ s512(ci_r & 15)) << 4));
+      const h16x8 fa = *reinterpret_cast<const h16x8*>(sW + ci_r * RB + ((ch ^ s512(ci_r & 15)) << 4));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < BM / 16; ++j) {
         const int px = 16 * j + (l & 15);
-        const h16x8 fb = *reinterpret_cast<const h16x8*>(sD + px * 512 + ((ch ^ s512(px & 15)) << 4));
+        const h16x8 fb = *reinterpret_cast<const h16x8*>(sD + px * RB + ((ch ^ s512(px & 15)) << 4));
         acc1[j] = mfma16(fa, fb, acc1[j]);
       }
     }
-    // ---- dW3[co 64w..][ci] += dc3ᵀ[co][px] · a2[px][ci], K = 64 pixels (transposing reads)
+    // dW3[co CO/4·w ..][ci] += dc3ᵀ[co][px] · a2[px][ci], K = BM pixels (transposing reads)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      i16x4 ta[2][4], tb[2][4];           // [rows 8g+q / 8g+4+q][block]
+    for (int kk = 0; kk < BM / 32; ++kk) {
+      i16x4 ta[2][G::NCB], tb[2][4];     // [rows 8g+q / 8g+4+q][block]
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int px = 32 * kk + 8 * g + q + 4 * hh;
-        const uint8_t* rowD = sD + px * 512;
+        const uint8_t* rowD = sD + px * RB;
         const uint8_t* rowA = sA + px * 128;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int chd = 2 * (4 * w + i) + (p >> 1);
+        for (int i = 0; i < G::NCB; ++i) {
+          const int chd = 2 * (G::NCB * w + i) + (p >> 1);
           ta[hh][i] = tr_read(rowD + ((chd ^ s512(px & 15)) << 4) + 8 * (p & 1));
         }
 #pragma unroll
@@ -174,17 +225,19 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
           tb[hh][j] = tr_read(rowA + ((cha ^ s128(px & 15)) << 4) + 8 * (p & 1));
         }
       }
-      h16x8 fa[4], fb[4];
+      h16x8 fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { fa[i] = cat8(ta[0][i], ta[1][i]); fb[i] = cat8(tb[0][i], tb[1][i]); }
+      for (int j = 0; j < 4; ++j) fb[j] = cat8(tb[0][j], tb[1][j]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < G::NCB; ++i) {
+        const h16x8 fa = cat8(ta[0][i], ta[1][i]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc2[i][j] = mfma16(fa[i], fb[j], acc2[i][j]);
+        for (int j = 0; j < 4; ++j) acc2[i][j] = mfma16(fa, fb[j], acc2[i][j]);
+      }
     }
-    // ---- da2 tile -> staging (lane: ci 16w + 4g .. +3 of pixel 16j + (l & 15))
+    // da2 tile -> staging (lane: ci 16w + 4g .. +3 of pixel 16j + (l & 15))
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < BM / 16; ++j) {
       const int px = 16 * j + (l & 15);
       const int ch = 2 * w + (g >> 1);
       uint16_t h[4];
@@ -194,59 +247,74 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
           make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
     }
     __syncthreads();
-    const int64_t m0 = (int64_t)u * BF_BM;
+    const int64_t m0 = (int64_t)u * BM;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < G::NA; ++i) {
       const int e = t + 256 * i, row = e >> 3, ch = e & 7;
       if (m0 + row < M)
-        *reinterpret_cast<uint4*>(da2 + (m0 + row) * BF_CI + ch * 8) =
+        *reinterpret_cast<uint4*>(da2 + (m0 + row) * CI + c0 + ch * 8) =
             *reinterpret_cast<const uint4*>(sO + row * 128 + ((ch ^ s128(row & 15)) << 4));
     }
+  };
+
+  BfRaw<CO> R0;
+  if (u0 < u1) load_tile(u0, R0);
+  for (int u = u0; u < u1; ++u) {
+    phase_a(u, R0);
+    __syncthreads();
+    if (u + 1 < u1) load_tile(u + 1, R0);      // in flight under this tile's MFMAs
+    phase_b(u);
   }
-  // ---- this workgroup's dW3 slab: lane holds D[co = 64w + 16i + 4g + r][ci = 16j + (l & 15)]
-  float* sl = slab + (int64_t)blockIdx.x * BF_CO * BF_CI;
+  // ---- this group's dW3 slab (the part's columns): lane holds
+  // D[co = (NCB·w + i)·16 + 4g + r][ci = c0 + 16j + (l & 15)]
+  float* sl = slab + (int64_t)grp * CO * CI;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < G::NCB; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        sl[(64 * w + 16 * i + 4 * g + r) * BF_CI + 16 * j + (l & 15)] = acc2[i][j][r];
+      for (int r = 0; r < 4; ++r) {
+        float* d = sl + (int64_t)((G::NCB * w + i) * 16 + 4 * g + r) * CI + c0 + 16 * j + (l & 15);
+        *d = acc_out ? *d + acc2[i][j][r] : acc2[i][j][r];
+      }
 }
 
-// workgroups per CU: 1 (512 VGPRs, no spill) or 2 (256 VGPRs: 72 bytes of scratch) —
-// LWAAAI_BN3_OCC, default measured
-static int bf_occ() {
-  static const int occ = [] {
-    const char* e = std::getenv("LWAAAI_BN3_OCC");
-    return (e && e[0] == '2') ? 2 : 1;
-  }();
-  return occ;
+static int bf_tiles(int64_t M, int CO) {
+  const int bm = CO == 256 ? BfGeom<256>::BM : BfGeom<512>::BM;
+  return (int)((M + bm - 1) / bm);
 }
 
-int bn3_bwd_dgemm_blocks(int64_t M) {
-  const int64_t tiles = (M + BF_BM - 1) / BF_BM;
-  const int64_t want = bf_occ() * (int64_t)cu_count();
-  const int64_t tpw = (tiles + want - 1) / want;
-  return (int)((tiles + tpw - 1) / tpw);
+// tile groups (= dW3 slabs): a multiple of 8 (the parts of a group share an XCD), about one
+// workgroup per CU over all parts
+int bn3_bwd_dgemm_slabs(int64_t M, int C, int Ci) {
+  const int tiles = bf_tiles(M, C), nparts = Ci / BF_CIP;
+  int want = std::max(8, cu_count() / nparts / 8 * 8);
+  const int tpw = (tiles + want - 1) / want;
+  const int used = (tiles + tpw - 1) / tpw;
+  return used <= 1 ? 1 : (used + 7) / 8 * 8;
 }
 
 bool bn3_bwd_dgemm_ok(int64_t M, int C, int Ci) {
-  return C == BF_CO && Ci == BF_CI && M > 0 && M * BF_CO * 2 < (int64_t(1) << 31);
+  return ((C == 256 && Ci == 64) || (C == 512 && Ci == 128)) && M > 0 &&
+         M * C * 2 < (int64_t(1) << 31);
 }
 
 void bn3_bwd_dgemm(const uint16_t* dr, const uint16_t* c3, const uint8_t* bits, const float* A,
                    const float* B, const float* Cc, const uint16_t* w3t, const uint16_t* a2,
-                   uint16_t* da2, float* slab, int64_t M, hipStream_t st) {
-  const int64_t tiles = (M + BF_BM - 1) / BF_BM;
-  const int blocks = bn3_bwd_dgemm_blocks(M);
-  const int tpw = (int)((tiles + blocks - 1) / blocks);
-  if (bf_occ() == 2)
-    hipLaunchKernelGGL(k_bn3_bwd_dgemm<2>, dim3(blocks), dim3(256), 0, st, dr, c3, bits, A, B, Cc,
-                       w3t, a2, da2, slab, M, (int)tiles, tpw);
-  else
-    hipLaunchKernelGGL(k_bn3_bwd_dgemm<1>, dim3(blocks), dim3(256), 0, st, dr, c3, bits, A, B, Cc,
-                       w3t, a2, da2, slab, M, (int)tiles, tpw);
+                   uint16_t* da2, float* slab, int64_t M, int C, int Ci, hipStream_t st,
+                   const uint16_t* x2, const float* A2, const float* B2, const float* C2,
+                   uint16_t* dx2, bool acc_out) {
+  const int tiles = bf_tiles(M, C), nparts = Ci / BF_CIP;
+  const int groups = bn3_bwd_dgemm_slabs(M, C, Ci);
+  const int tpw = (tiles + groups - 1) / groups;
+  const int acc = (acc_out && groups == 1) ? 1 : 0;
+  const int blocks = groups * nparts, xp = groups % 8 == 0 ? 1 : 0;
+#define LW_BF(CO, DU)                                                                            \
+  hipLaunchKernelGGL((k_bn3_bwd_dgemm<CO, DU>), dim3(blocks), dim3(256), 0, st, dr, c3, bits, A, \
+                     B, Cc, w3t, a2, da2, slab, x2, A2, B2, C2, dx2, M, Ci, tiles, tpw, acc, xp)
+  if (C == 256) { if (x2) LW_BF(256, true); else LW_BF(256, false); }
+  else { if (x2) LW_BF(512, true); else LW_BF(512, false); }
+#undef LW_BF
 }
 
 }  // namespace lw

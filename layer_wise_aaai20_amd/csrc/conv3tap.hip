@@ -302,226 +302,6 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Weight-resident persistent variant for C = Co = 64 (ResNet-50 stage-1 conv2 at 56x56, the 64->64
-// convs of VGG-16 / ResNet-9): the whole [64][576] bf16 weight (72 KB) stays in LDS for the life of
-// the workgroup, one workgroup per CU walks a contiguous range of 224-pixel tiles, and the next
-// tile's 64-channel input patch is DMA'd into the other of two buffers while this tile's 18 K-steps
-// run with NO barrier between them (k_conv3_tap at C = 64 pays a weight-slice DMA + barrier per
-// K-step and a patch / weight prologue per tile: 112 us for a 56x56 forward, 3.4x the HBM floor).
-// Operand images, fragment reads, K order (chunk outer, tap inner, one 16x16x32 step each) and the
-// epilogue are k_conv3_tap's, so the output is bit-identical to it.
-//   LDS: 18 weight slices [4 k groups][64 rows][16 B] (73,728 B) + 2 patches of 8 planes (one per
-//   8-channel group; plane stride PL = a multiple of 256 B: the conflict-free read condition),
-//   PL <= 5,632 B (patches of up to 352 pixels) -> 163,840 B, the whole LDS.
-constexpr int T3R_SLICE = 64 * 64;            // bytes per K-step weight slice (64 rows x 32 k)
-constexpr int T3R_WB = 18 * T3R_SLICE;        // the resident weight
-constexpr int T3R_PLMAX = 5632;
-constexpr int T3R_LDS = T3R_WB + 2 * 8 * T3R_PLMAX;
-static_assert(T3R_LDS == 163840, "the whole LDS of a CU");
-
-__host__ __device__ inline int t3r_plane(int W) {
-  const int npix = (T3_M / W + 2) * W + 2;
-  int pl = (npix * 16 + 255) / 256 * 256;
-  return pl < 4096 ? 4096 : pl;                 // >= 32 KB per patch: the epilogue staging fits
-}
-
-template <bool STATS>
-__global__ __launch_bounds__(256) void k_conv3_res(const uint16_t* __restrict__ x,
-                                                   const uint16_t* __restrict__ w,
-                                                   uint16_t* __restrict__ y,
-                                                   float* __restrict__ stats, int NH, int H,
-                                                   int W, int tiles, int tpw, uint32_t x_bytes,
-                                                   uint32_t w_bytes) {
-  constexpr int C = 64, Co = 64, K = 9 * C, NT = 256, LDH = Co + 8;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[T3R_LDS];
-  const int PL = t3r_plane(W), PB = 8 * PL;       // plane stride, bytes per patch buffer
-  uint8_t* const pbuf = lds + T3R_WB;
-  const int R = T3_M / W, npix = (R + 2) * W + 2;
-  const int64_t NHW = (int64_t)NH * W;
-  const int u0 = (int)blockIdx.x * tpw, u1 = min(u0 + tpw, tiles);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63;
-  const int wm = wave & 1, wn = wave >> 1;
-  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, x_bytes), rw = make_rsrc(w, w_bytes);
-
-  // ---- the resident weight: slice s = (c, t) = c*9 + t, plane g, row = lane
-#pragma unroll
-  for (int j = 0; j < 18; ++j) {
-    const int I = j * 4 + wave, s = I >> 2, g = I & 3, c = s / 9, t = s - c * 9;
-    const uint32_t off = (uint32_t)((l * K + t * C + c * 32 + g * 8) * 2);
-    glds16(rw, reinterpret_cast<uint16_t*>(lds + s * T3R_SLICE + g * 1024), off);
-  }
-  // ---- patch DMA: block I = j*4 + wave of the 8*PL bytes; lane byte d = I*1024 + 16*l lands in
-  // plane G = d / PL (channels 8G..8G+7), patch pixel q = (d % PL) / 16
-  constexpr int NPJ = 8 * T3R_PLMAX / 1024 / 4;  // 11 blocks per wave at most
-  const int nbk = PB / 1024;
-  int prel[NPJ], pq[NPJ];
-#pragma unroll
-  for (int j = 0; j < NPJ; ++j) {
-    const int I = j * 4 + wave, d = I * 1024 + 16 * l;
-    const int G = d / PL, q = (d - G * PL) >> 4;
-    pq[j] = (I < nbk && q < npix) ? q : -1;
-    prel[j] = q * C * 2 + G * 16;
-  }
-  auto issue_patch = [&](int u, int buf) {
-    const int64_t P0 = (int64_t)(u * R - 1) * W - 1;
-    uint8_t* dst = pbuf + buf * PB;
-#pragma unroll
-    for (int j = 0; j < NPJ; ++j) {
-      const int I = j * 4 + wave;
-      if (I < nbk) {
-        const int64_t P = P0 + pq[j];
-        const bool ok = pq[j] >= 0 && P >= 0 && P < NHW;
-        glds16(rx, reinterpret_cast<uint16_t*>(dst + I * 1024),
-               ok ? (uint32_t)(P0 * C * 2) + (uint32_t)prel[j] : OOB);
-      }
-    }
-  };
-
-  const int g = l >> 4;
-  int wbyte[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) wbyte[j] = (g * 64 + wn * 32 + j * 16 + (l & 15)) * 16;
-  int ppix[7];
-#pragma unroll
-  for (int i = 0; i < 7; ++i) ppix[i] = (wm * 7 + i) * 16 + (l & 15);
-
-  if (u0 < u1) issue_patch(u0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int u = u0; u < u1; ++u) {
-    const int b = (u - u0) & 1;
-    if (u + 1 < u1) issue_patch(u + 1, b ^ 1);
-    const int g0 = u * R;
-    uint32_t vmask = 0;          // per block i, 4 bits: tap row 0 / row 2 / col 0 / col 2 inside
-#pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int m = ppix[i], orow = m / W, ox = m - orow * W;
-      const int yy = (g0 + orow) % H;
-      vmask |= (yy >= 1 ? 1u : 0u) << (4 * i);
-      vmask |= (yy + 1 < H ? 1u : 0u) << (4 * i + 1);
-      vmask |= (ox >= 1 ? 1u : 0u) << (4 * i + 2);
-      vmask |= (ox + 1 < W ? 1u : 0u) << (4 * i + 3);
-    }
-    const uint8_t* P = pbuf + b * PB;
-    f32x4 acc[7][2];
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const uint8_t* Pc = P + (4 * c + g) * PL;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int r = t / 3, sc = t - r * 3;
-        const uint8_t* Wt = lds + (c * 9 + t) * T3R_SLICE;
-        h16x8 fb[2], fa[7];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fb[j] = *reinterpret_cast<const h16x8*>(Wt + wbyte[j]);
-        const int toff = r * W + sc;
-#pragma unroll
-        for (int i = 0; i < 7; ++i) {
-          int pb = ppix[i];
-          asm volatile("" : "+v"(pb));
-          fa[i] = *reinterpret_cast<const h16x8*>(Pc + (pb + toff) * 16);
-          if (r != 1 || sc != 1) {
-            const uint32_t need = (r == 0 ? 1u : r == 2 ? 2u : 0u) | (sc == 0 ? 4u : sc == 2 ? 8u : 0u);
-            if (((vmask >> (4 * i)) & need) != need) fa[i] = h16x8{};
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < 7; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
-      }
-    }
-    // the next patch landed (this wave's DMAs) and every wave is done reading this one
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    uint16_t* Ch = reinterpret_cast<uint16_t*>(pbuf + b * PB);
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int m = ppix[i];
-        const int n = wn * 32 + j * 16 + 4 * g;
-        uint16_t h[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) h[q] = f2h(acc[i][j][q]);
-        *reinterpret_cast<uint2*>(Ch + m * LDH + n) =
-            make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
-      }
-    __syncthreads();
-    constexpr int CPR = Co / 8;
-    const int m_valid = min(T3_M, (NH - g0) * W);
-    const int cg = threadIdx.x % CPR;
-    float s1[8], s2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
-    const int64_t m0 = (int64_t)g0 * W;
-    for (int ch = threadIdx.x; ch < T3_M * CPR; ch += NT) {
-      const int m = ch / CPR;
-      if (m >= m_valid) break;
-      const uint4 v = *reinterpret_cast<const uint4*>(Ch + m * LDH + cg * 8);
-      *reinterpret_cast<uint4*>(y + (m0 + m) * Co + cg * 8) = v;
-      if constexpr (STATS) {
-        const uint32_t uu[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float f = k & 1 ? hhi(uu[k >> 1]) : hlo(uu[k >> 1]);
-          s1[k] += f;
-          s2[k] += f * f;
-        }
-      }
-    }
-    if constexpr (STATS) {
-      __syncthreads();
-      float* fold = reinterpret_cast<float*>(pbuf + b * PB);   // [NT][16]
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        fold[threadIdx.x * 16 + k] = s1[k];
-        fold[threadIdx.x * 16 + 8 + k] = s2[k];
-      }
-      __syncthreads();
-      constexpr int Q = NT / CPR;
-      for (int c = threadIdx.x; c < Co; c += NT) {
-        const int gq = c / 8, k = c % 8;
-        float a = 0.f, bb = 0.f;
-        for (int q = 0; q < Q; ++q) {
-          a += fold[(q * CPR + gq) * 16 + k];
-          bb += fold[(q * CPR + gq) * 16 + 8 + k];
-        }
-        stats[(int64_t)u * 2 * Co + c] = a;
-        stats[(int64_t)u * 2 * Co + Co + c] = bb;
-      }
-    }
-    __syncthreads();             // this buffer is the DMA target of tile u + 2
-  }
-}
-
-bool conv3_res_ok(int C, int Co, int H, int W) {
-  if (C != 64 || Co != 64 || W < 4 || W > 224 || T3_M % W != 0 || H < 1) return false;
-  return ((T3_M / W + 2) * W + 2) * 16 <= T3R_PLMAX;
-}
-
-void conv3_res(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
-               int W, hipStream_t st) {
-  const int NH = N * H;
-  const int tiles = conv3_tap_tiles_m(N, H, W);
-  const int cus = cu_count();
-  const int tpw = (tiles + cus - 1) / cus;
-  const int blocks = (tiles + tpw - 1) / tpw;
-  const uint32_t xb = (uint32_t)((int64_t)NH * W * 64 * 2);
-  const uint32_t wb = (uint32_t)(64 * 9 * 64 * 2);
-  if (stats)
-    hipLaunchKernelGGL((k_conv3_res<true>), dim3(blocks), dim3(256), 0, st, x, w, y, stats, NH, H,
-                       W, tiles, tpw, xb, wb);
-  else
-    hipLaunchKernelGGL((k_conv3_res<false>), dim3(blocks), dim3(256), 0, st, x, w, y, stats, NH,
-                       H, W, tiles, tpw, xb, wb);
-}
-
 bool conv3_tap_ok(int C, int Co, int H, int W) {
   if (C % 32 != 0 || C < 32 || (Co % 128 != 0 && Co != 64) || W < 4 || W > 224) return false;
   if (T3_M % W != 0) return false;

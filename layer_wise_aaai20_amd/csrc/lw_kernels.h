@@ -202,13 +202,19 @@ void bn_forward(const BNArgs& a, hipStream_t st);
 void bn_backward(const BNArgs& a, hipStream_t st);
 // two BN+ReLU backwards sharing dy and the ReLU bitmap (a bottleneck's BN3 and downsample BN)
 void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st);
-// BN3 backward apply fused with dW3 += dc3ᵀ·a2 and da2 = dc3·W3 (bnfuse.hip): C = 256, Ci = 64;
-// slab [bn3_bwd_dgemm_blocks(M)][256][64] fp32 partials of dW3 (summed by splitk_reduce)
+// BN3 backward apply fused with dW3 += dc3ᵀ·a2 and da2 = dc3·W3 (bnfuse.hip): (C, Ci) = (256, 64)
+// or (512, 128); slab [bn3_bwd_dgemm_slabs(M, C, Ci)][C][Ci] fp32 partials of dW3 (summed by
+// splitk_reduce; with a single slab and acc_out the kernel adds into slab = the destination).
+// With x2 (the downsample block: its shortcut BN's input, same dy and bitmap) also
+// dx2 = A2·(dy·bit) + B2·x2 + C2 into dx2 [M][C].
 bool bn3_bwd_dgemm_ok(int64_t M, int C, int Ci);
-int bn3_bwd_dgemm_blocks(int64_t M);
+int bn3_bwd_dgemm_slabs(int64_t M, int C, int Ci);
 void bn3_bwd_dgemm(const uint16_t* dr, const uint16_t* c3, const uint8_t* bits, const float* A,
                    const float* B, const float* Cc, const uint16_t* w3t, const uint16_t* a2,
-                   uint16_t* da2, float* slab, int64_t M, hipStream_t st);
+                   uint16_t* da2, float* slab, int64_t M, int C, int Ci, hipStream_t st,
+                   const uint16_t* x2 = nullptr, const float* A2 = nullptr,
+                   const float* B2 = nullptr, const float* C2 = nullptr, uint16_t* dx2 = nullptr,
+                   bool acc_out = false);
 
 // fused stem: BN-apply + ReLU + max-pool (bn.hip), bf16 NHWC
 struct StemArgs {
@@ -354,10 +360,6 @@ bool conv3_tap_ok(int C, int Co, int H, int W);
 int conv3_tap_tiles_m(int N, int H, int W);
 void conv3_tap(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
                int W, int C, int Co, hipStream_t st);
-// the weight-resident persistent form for C = Co = 64 (same operands, bit-identical output)
-bool conv3_res_ok(int C, int Co, int H, int W);
-void conv3_res(const uint16_t* x, const uint16_t* w, uint16_t* y, float* stats, int N, int H,
-               int W, hipStream_t st);
 // its weight gradient: fp32 dW [Co][3][3][C] (= out, accumulated when `accumulate`), `part` a
 // [splits][Co][9][C] fp32 workspace (splits: conv3_tap_wgrad_splits)
 int conv3_tap_wgrad_splits(int N, int H, int W, int C, int Co);

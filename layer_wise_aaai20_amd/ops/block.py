@@ -65,9 +65,11 @@ CL = torch.channels_last
 # * the downsample block's BN3 and shortcut-BN backwards share dy and the ReLU bitmap: one dual
 #   reduce + one dual apply pass (csrc bn.hip k_bn_reduce DUAL / k_bn_bwd_apply_dual);
 # * weight gradients run inline (a side stream measured no gain: the step is throughput-bound).
-# * the BN3 backward of a 256-channel block (ResNet-50 stage 1, no downsample) runs its apply
-#   inside one kernel with both GEMMs that read dc3 (csrc/bnfuse.hip): dy, c3 and the bitmap are
-#   read once instead of dc3 being written and read twice (LWAAAI_FUSE_BN3=0: the three passes).
+# * the BN3 backward of a 256- or 512-channel block (ResNet-50 stages 1-2) runs its apply inside
+#   one kernel with both GEMMs that read dc3 (csrc/bnfuse.hip): dy, c3 and the bitmap are read
+#   once instead of dc3 being written and read twice; stage 1: 615.6 -> 420.6 us a block, bench
+#   11,709 -> 12,052 / 12,074 img/s on one box (profiles/r6/fused_bn3/). LWAAAI_FUSE_BN3=0: the
+#   three passes.
 FUSE_BN3 = os.environ.get("LWAAAI_FUSE_BN3", "1") != "0"
 TILES = with_mf32((1, 2, 3, 4, 5, 6))   # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
@@ -383,23 +385,32 @@ class _BottleneckFn(torch.autograd.Function):
         # the bitmap — the dx GEMM as a masked addend, the shortcut BN through its ReLU mode)
         grads = {}
         dual = None
-        if has_down:
+        fused = FUSE_BN3 and (cout, width) in ((256, 64), (512, 128)) and dr.dtype == h16()
+        if fused:
+            # BN3's apply fused into both consumers of dc3 (csrc/bnfuse.hip): da2 = dc3·W3 and
+            # dW3 = dc3ᵀ·a2 from one pass over dy, c3 and the bitmap; dc3 is never written (a
+            # downsample block's shortcut-BN gradient dcd comes out of the same pass)
+            dst3, d3 = _wgrad_target(w3, (cout, width))
+            w3t = _kc_weight(W3, cout, width, cout).view(width, cout)
+            down = ()
+            if has_down:
+                cd, gd, meand, invd = saved[22], saved[24], saved[25], saved[26]
+                od = _bn_grad_outs(gdp, bdp)
+                down = (cd, gd, meand, invd, od[0], od[1])
+            with _deferred_reduce(dr, d3):
+                da2, _, dg3, db3, dcd, dgd, dbd = lib.bn3_bwd_fused(
+                    dr, c3, bits3, g3, mean3, inv3, w3t, a2, dst3, o3[0], o3[1], *down)
+            if has_down:
+                dual = (dcd, dgd, dbd, od)
+            grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
+            grads["w3"] = _wgrad_done(w3, dst3, d3)
+        elif has_down:
             cd, gd, meand, invd = saved[22], saved[24], saved[25], saved[26]
             od = _bn_grad_outs(gdp, bdp)
             dc3, dcd, dg3, db3, dgd, dbd = lib.bn_bwd_dual(dr, c3, cd, bits3, g3, mean3, inv3, gd,
                                                            meand, invd, o3[0], o3[1], od[0],
                                                            od[1])
             dual = (dcd, dgd, dbd, od)
-        elif FUSE_BN3 and (cout, width) == (256, 64) and dr.dtype == h16():
-            # BN3's apply fused into both consumers of dc3 (csrc/bnfuse.hip): da2 = dc3·W3 and
-            # dW3 = dc3ᵀ·a2 from one pass over dy, c3 and the bitmap; dc3 is never written
-            dst3, d3 = _wgrad_target(w3, (cout, width))
-            with _deferred_reduce(dr, d3):
-                da2, _, dg3, db3 = lib.bn3_bwd_fused(dr, c3, bits3, g3, mean3, inv3,
-                                                     _kc_weight(W3, cout, width, cout).view(
-                                                         width, cout), a2, dst3, o3[0], o3[1])
-            grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
-            grads["w3"] = _wgrad_done(w3, dst3, d3)
         else:
             dc3, dg3, db3, _ = lib.bn_bwd(dr, c3, None, g3, mean3, inv3, None, True, True, False,
                                           bits3, o3[0], o3[1])

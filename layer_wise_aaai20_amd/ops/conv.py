@@ -49,15 +49,9 @@ STEM_DIRECT = 31
 # gathers it 9 times), forward and — flipped, transposed weight — data gradient. C % 32 == 0,
 # Co == 64 or Co % 128 == 0, image width dividing 224.
 CONV3_TAP = 33
-# its weight-resident persistent form for C = Co = 64 (csrc/conv3tap.hip k_conv3_res): the whole
-# 72 KB weight held in LDS, one workgroup per CU over a range of tiles, the next tile's patch DMA'd
-# under this tile's MFMAs, no barrier inside a tile. Bit-identical to CONV3_TAP.
-CONV3_RES = 34
-
-
-def _conv3_res_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
-    return (_conv3_tap_fits(c, co, R, S, sh, sw, ph, pw, H, W) and c == 64 and co == 64 and
-            ((224 // W + 2) * W + 2) * 16 <= 5632)
+# (A weight-resident persistent form for C = Co = 64 — the whole 72 KB weight in LDS, one
+# workgroup per CU, no barrier inside a tile — measured 130.6 / 121.3 us against this kernel's
+# 122.2 / 111.5 at 56x56, batch 256 (profiles/r6/conv3_res_ab.txt), and was removed in round 6.)
 
 
 def _conv3_tap_fits(c, co, R, S, sh, sw, ph, pw, H, W) -> bool:
@@ -300,9 +294,6 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
         if tile == CONV3_TAP:
             ys, sts = lib.conv3_tap(xin, op, co, bool(stats))
             return ys.permute(0, 2, 3, 1).reshape(M, co), (sts if stats else None)
-        if tile == CONV3_RES:
-            ys, sts = lib.conv3_res(xin, op, bool(stats))
-            return ys.permute(0, 2, 3, 1).reshape(M, co), (sts if stats else None)
         return lib.conv_ex(xin, op, mode, geom, co, tile, 1, True, ps, pt, stats, None, False, 0,
                            True, K, bias=bf, relu=bool(relu))
     key = ("f", tuple(xin.shape), tuple(w.shape), sh, sw, ph, pw, pro is not None, stats,
@@ -315,8 +306,6 @@ def conv_fwd(x: torch.Tensor, w: torch.Tensor, stride, padding, pro=None, stats=
     if (pro is None and bias is None and not relu and not c4 and
             _conv3_tap_fits(C, co, R, S, sh, sw, ph, pw, H, W)):
         direct = direct + (CONV3_TAP,)
-        if _conv3_res_fits(C, co, R, S, sh, sw, ph, pw, H, W):
-            direct = direct + (CONV3_RES,)
     tile = TUNER.pick(key, run, ROW_TILES + big + direct, _row_default(M, co))
     y, st = run(tile)
     return y.view(Nb, Ho, Wo, co).permute(0, 3, 1, 2), st
@@ -367,10 +356,7 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
         if layout == "tap" and (dst is not None or add is not None):
             layout, tile = "kc", 2            # the direct kernels write a fresh tensor only
         if layout == "tap":           # (the flip + transpose pack is timed with the conv)
-            if tile == CONV3_RES:
-                ys, _ = lib.conv3_res(dyc, tap_dgrad_weight(w, fresh), False)
-            else:
-                ys, _ = lib.conv3_tap(dyc, tap_dgrad_weight(w, fresh), c, False)
+            ys, _ = lib.conv3_tap(dyc, tap_dgrad_weight(w, fresh), c, False)
             return ys.permute(0, 2, 3, 1).reshape(-1, c), None
         if layout == "kc":            # (the tuner times a pack of its own with the conv)
             wk, koffs, kmax = pack_dgrad_weight_kc(w, classes, sh, sw, fresh)
@@ -391,8 +377,6 @@ def conv_dgrad(dy: torch.Tensor, w: torch.Tensor, x_hw, stride, padding, wpack=N
     if (addend is None and out is None and
             _conv3_tap_fits(co, c, R, S, sh, sw, ph, pw, Ho, Wo) and (H, W) == (Ho, Wo)):
         cands.append(("tap", CONV3_TAP))
-        if _conv3_res_fits(co, c, R, S, sh, sw, ph, pw, Ho, Wo):
-            cands.append(("tap", CONV3_RES))
     cand = TUNER.pick(key, run, cands, ("nkc", _row_default(M, c)))   # (timed on scratch outputs)
     dx, _ = run(cand, out, addend, False)
     return _nchw_rows(dx, Nb, H, W)

@@ -2,9 +2,8 @@
 """BN3 backward fused with its two GEMMs (csrc/bnfuse.hip) vs the three-pass block path at the
 ResNet-50 stage-1 shape (batch 256, 56x56: M = 802816 rows, 256 / 64 channels), µs per call.
 The three-pass arm is bn_bwd (reduce + finalize + apply) + dW3 GEMM + da2 GEMM through the
-block's tuned wrappers. usage: python scripts/bn3_fused_bench.py [--occ both]"""
+block's tuned wrappers. usage: python scripts/bn3_fused_bench.py"""
 import os
-import subprocess
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -27,11 +26,6 @@ def timeit(fn, iters=20):
 
 
 def main():
-    if "--occ" in sys.argv:
-        for occ in ("1", "2"):
-            env = dict(os.environ, LWAAAI_BN3_OCC=occ)
-            subprocess.run([sys.executable, __file__], env=env, check=True)
-        return
     lib = load()
     M, C, Ci = 802816, 256, 64
     dy = torch.randn(M, C, device="cuda").to(h16())
@@ -58,8 +52,7 @@ def main():
     def reduce_only():
         lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits, dgo, dbo)
     tf, t3, tr = timeit(fused), timeit(three), timeit(reduce_only)
-    occ = os.environ.get("LWAAAI_BN3_OCC", "1")
-    print(f"occ {occ}: fused {tf:.1f} us   three-pass {t3:.1f} us   (bn_bwd alone {tr:.1f} us)",
+    print(f"fused {tf:.1f} us   three-pass {t3:.1f} us   (bn_bwd alone {tr:.1f} us)",
           flush=True)
 
 

@@ -103,13 +103,19 @@ def test_block_direct_arena_gradients():
         assert _rel(p.grad, q.grad) < 0.15, n
 
 
-def test_fused_bn3_backward_matches_three_pass_block(monkeypatch):
-    """A 256-channel bottleneck with BN3's backward fused into its two GEMMs (csrc/bnfuse.hip)
-    gives the three-pass block's input and parameter gradients to bf16 / summation-order noise."""
+@pytest.mark.parametrize("inplanes,planes,stride,down", [(256, 64, 1, False), (64, 64, 1, True),
+                                                         (512, 128, 1, False),
+                                                         (256, 128, 2, True)])
+def test_fused_bn3_backward_matches_three_pass_block(inplanes, planes, stride, down, monkeypatch):
+    """A 256-channel bottleneck (and the downsample one) with BN3's backward fused into its two
+    GEMMs (csrc/bnfuse.hip) gives the three-pass block's input and parameter gradients to bf16 /
+    summation-order noise."""
     torch.manual_seed(3)
-    ref = _make(256, 64, 1, False).cuda().to(memory_format=CL)
-    x = torch.randn(8, 256, 28, 28, device="cuda").to(torch.bfloat16).contiguous(memory_format=CL)
-    gy = torch.randn(8, 256, 28, 28, device="cuda").contiguous(memory_format=CL)
+    ref = _make(inplanes, planes, stride, down).cuda().to(memory_format=CL)
+    x = torch.randn(8, inplanes, 28, 28, device="cuda").to(torch.bfloat16)
+    x = x.contiguous(memory_format=CL)
+    gy = torch.randn(8, 4 * planes, 28 // stride, 28 // stride, device="cuda").contiguous(
+        memory_format=CL)
     outs = {}
     for fuse in (True, False):
         monkeypatch.setattr(blk, "FUSE_BN3", fuse)

@@ -399,61 +399,6 @@ def test_conv3_tap_fwd_stats_dgrad(shape):
     _close(dx, xf.grad, 1e-2)
 
 
-# the weight-resident persistent form (k_conv3_res, C = Co = 64): 56 px (4-row tiles), tiles that
-# span images and a partial last tile (H 30 at 28 px: 8-row tiles), 32 / 14 / 7 / 4 px
-RES_SHAPES = [(3, 56), (2, 56), (3, 30), (4, 32), (5, 14), (7, 7), (9, 4), (1, 28)]
-
-
-@pytest.mark.parametrize("shape", RES_SHAPES, ids=[str(s) for s in RES_SHAPES])
-def test_conv3_res_matches_tap(shape):
-    """k_conv3_res: bit-identical to k_conv3_tap (same K order and epilogue) on the forward with
-    statistics and on the data gradient, and within bf16 rounding of fp32 F.conv2d."""
-    from layer_wise_aaai20_amd.ops._ext import load
-    N, H = shape
-    W = 28 if H == 30 else H
-    lib = load()
-    g = torch.Generator(device="cuda").manual_seed(11)
-    x = torch.randn(N, 64, H, W, device="cuda", generator=g).bfloat16().contiguous(memory_format=CL)
-    w = (torch.randn(64, 64, 3, 3, device="cuda", generator=g) / 24.0).bfloat16().contiguous(
-        memory_format=CL)
-    op, _, _ = CV.pack_fwd_weight(w)
-    y, st = lib.conv3_res(x, op, True)
-    yt, stt = lib.conv3_tap(x, op, 64, True)
-    assert torch.equal(y, yt) and torch.equal(st, stt)
-    _close(y, F.conv2d(x.float(), w.float(), padding=1), 1e-2)
-    dy = torch.randn(N, 64, H, W, device="cuda", generator=g).bfloat16().contiguous(
-        memory_format=CL)
-    wt = CV.tap_dgrad_weight(w)
-    dx, _ = lib.conv3_res(dy, wt, False)
-    dxt, _ = lib.conv3_tap(dy, wt, 64, False)
-    assert torch.equal(dx, dxt)
-    xf = x.float().requires_grad_()
-    F.conv2d(xf, w.float(), padding=1).backward(dy.float())
-    _close(dx, xf.grad, 1e-2)
-
-
-def test_conv3_res_is_a_tuner_candidate(monkeypatch):
-    """Forced through the tuner (conv_fwd / conv_dgrad) the resident kernel runs and gives the
-    tap kernel's results."""
-    x, w = _inputs(2, 64, 64, 56, 3, 5)
-    calls = []
-    orig = CV.TUNER.pick
-
-    def pick(key, run, cands, default):
-        c = [c for c in cands if c == CV.CONV3_RES or c == ("tap", CV.CONV3_RES)]
-        calls.append(bool(c))
-        return c[0] if c else orig(key, run, cands, default)
-    monkeypatch.setattr(CV.TUNER, "pick", pick)
-    y, st = CV.conv_fwd(x, w, 1, 1, stats=True)
-    _close(y, F.conv2d(x.float(), w.float(), padding=1), 1e-2)
-    dy = torch.randn_like(y.float()).bfloat16().contiguous(memory_format=CL)
-    dx = CV.conv_dgrad(dy, w, (56, 56), 1, 1)
-    xf = x.float().requires_grad_()
-    F.conv2d(xf, w.float(), padding=1).backward(dy.float())
-    _close(dx, xf.grad, 1e-2)
-    assert calls == [True, True]
-
-
 def test_conv3_tap_is_a_tuner_candidate(monkeypatch):
     """Forced through the tuner (conv_fwd / conv_dgrad), the tap kernel gives the GEMM path's
     results to bf16 rounding."""

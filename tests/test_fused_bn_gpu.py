@@ -217,31 +217,47 @@ def test_bn_stats_from_rows_one_launch(M, C, R, monkeypatch):
     assert torch.isfinite(rm).all() and not torch.equal(rm, torch.zeros_like(rm))
 
 
-@pytest.mark.parametrize("M", [4096, 3000, 802816 // 16])
-def test_bn3_bwd_fused_matches_three_passes(M):
+@pytest.mark.parametrize("dual", [False, True])
+@pytest.mark.parametrize("M,C,Ci", [(4096, 256, 64), (3000, 256, 64), (802816 // 16, 256, 64),
+                                    (4096, 512, 128), (1000, 512, 128), (200704 // 8, 512, 128)])
+def test_bn3_bwd_fused_matches_three_passes(M, C, Ci, dual):
     """bn3_bwd_fused (csrc/bnfuse.hip: BN3's apply inside one kernel with da2 = dc3·W3 and
-    dW3 = dc3ᵀ·a2) vs bn_bwd + fp32 products of its dc3: dgamma/dbeta bit-identical (the same
-    reduce + finalize), da2 within bf16 rounding, dW3 within fp32 summation-order noise, and the
-    weight gradient accumulated into a given view. M = 3000 ends in a partial 64-row tile."""
+    dW3 = dc3ᵀ·a2) vs bn_bwd / bn_bwd_dual + fp32 products of their dc3: dgamma/dbeta
+    bit-identical (the same reduce + finalize), the shortcut BN's dx2 (dual) within one bf16 ulp,
+    da2 within bf16 rounding, dW3 within fp32 summation-order noise, the weight gradient
+    accumulated into a given view. M = 3000 / 1000 end in a partial tile; 4096 / 1000 run one
+    tile group (the result added straight into the destination)."""
     from layer_wise_aaai20_amd.ops._ext import h16, load
     lib = load()
-    C, Ci = 256, 64
-    g = torch.Generator(device="cuda").manual_seed(M)
-    dy = torch.randn(M, C, device="cuda", generator=g).to(h16())
-    x = torch.randn(M, C, device="cuda", generator=g).to(h16())
-    a2 = torch.randn(M, Ci, device="cuda", generator=g).to(h16())
+    g = torch.Generator(device="cuda").manual_seed(M + C + dual)
+    mk = lambda *s: torch.randn(*s, device="cuda", generator=g).to(h16())  # noqa: E731
+    dy, x, x2, a2 = mk(M, C), mk(M, C), mk(M, C), mk(M, Ci)
     w3 = (torch.randn(C, Ci, device="cuda", generator=g) / 16).to(h16())
+    w3t = w3.t().contiguous()
     bits = torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device="cuda", generator=g)
-    gam = torch.rand(C, device="cuda", generator=g) + 0.5
-    mean = torch.randn(C, device="cuda", generator=g) * 0.1
-    inv = torch.rand(C, device="cuda", generator=g) + 0.5
-    dgo, dbo = torch.randn(C, device="cuda", generator=g), torch.randn(C, device="cuda", generator=g)
-    rdg, rdb = dgo.clone(), dbo.clone()
-    dc3, _, _, _ = lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits, rdg, rdb)
+    st = [(torch.rand(C, device="cuda", generator=g) + 0.5,
+           torch.randn(C, device="cuda", generator=g) * 0.1,
+           torch.rand(C, device="cuda", generator=g) + 0.5) for _ in range(2)]
+    (gam, mean, inv), (gam2, mean2, inv2) = st
+    outs = [torch.randn(C, device="cuda", generator=g) for _ in range(4)]
+    ref = [o.clone() for o in outs]
+    if dual:
+        dc3, rdx2, _, _, _, _ = lib.bn_bwd_dual(dy, x, x2, bits, gam, mean, inv, gam2, mean2, inv2,
+                                                *ref)
+    else:
+        dc3, _, _, _ = lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits,
+                                  ref[0], ref[1])
     dw = torch.full((C, Ci), 0.25, device="cuda")
-    da2, dwr, dg, db = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3.t().contiguous(), a2, dw,
-                                         dgo, dbo)
-    assert torch.equal(dg, rdg) and torch.equal(db, rdb)
+    down = (x2, gam2, mean2, inv2, outs[2], outs[3]) if dual else ()
+    da2, dwr, dg, db, dx2, dg2, db2 = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, dw,
+                                                        outs[0], outs[1], *down)
+    assert torch.equal(dg, ref[0]) and torch.equal(db, ref[1])
+    if dual:
+        assert torch.equal(dg2, ref[2]) and torch.equal(db2, ref[3])
+        ulp = (rdx2.float().abs() * 2.0 ** -7).clamp_min(1e-30)
+        assert bool(((dx2.float() - rdx2.float()).abs() <= ulp).all())
+    else:
+        assert dx2.numel() == 0
     assert dwr.data_ptr() == dw.data_ptr()
     ref_da2 = dc3.float() @ w3.float()
     err = (da2.float() - ref_da2).abs().max().item()
@@ -250,6 +266,6 @@ def test_bn3_bwd_fused_matches_three_passes(M):
     err = ((dw - 0.25) - ref_dw).abs().max().item()
     assert err <= 1e-4 * ref_dw.abs().max().item() + 1e-3, err
     # without a destination: a fresh [C, Ci] result
-    _, dw2, _, _ = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3.t().contiguous(), a2, None,
-                                     None, None)
+    _, dw2, _, _, _, _, _ = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, None, None,
+                                              None, *((x2, gam2, mean2, inv2) if dual else ()))
     torch.testing.assert_close(dw2, dw - 0.25, rtol=1e-5, atol=1e-4)

@@ -67,9 +67,9 @@ CL = torch.channels_last
 # * weight gradients run inline (a side stream measured no gain: the step is throughput-bound).
 # * the BN3 backward of a 256- or 512-channel block (ResNet-50 stages 1-2) runs its apply inside
 #   one kernel with both GEMMs that read dc3 (csrc/bnfuse.hip): dy, c3 and the bitmap are read
-#   once instead of dc3 being written and read twice; stage 1: 615.6 -> 420.6 us a block, bench
-#   11,709 -> 12,052 / 12,074 img/s on one box (profiles/r6/fused_bn3/). LWAAAI_FUSE_BN3=0: the
-#   three passes.
+#   once instead of dc3 being written and read twice; 604.2 -> 417.1 us a stage-1 block, 327.4 ->
+#   272.2 us a stage-2 block, bench 11,738 -> 12,173 img/s on one box (profiles/r6/fused_bn3/).
+#   LWAAAI_FUSE_BN3=0: the three passes.
 FUSE_BN3 = os.environ.get("LWAAAI_FUSE_BN3", "1") != "0"
 TILES = with_mf32((1, 2, 3, 4, 5, 6))   # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256

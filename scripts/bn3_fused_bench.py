@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """BN3 backward fused with its two GEMMs (csrc/bnfuse.hip) vs the three-pass block path at the
-ResNet-50 stage-1 shape (batch 256, 56x56: M = 802816 rows, 256 / 64 channels), µs per call.
+ResNet-50 stage-1 / stage-2 shapes (batch 256: M = 802816 rows, 256 / 64 channels; M = 200704,
+512 / 128), µs per call.
 The three-pass arm is bn_bwd (reduce + finalize + apply) + dW3 GEMM + da2 GEMM through the
 block's tuned wrappers. usage: python scripts/bn3_fused_bench.py"""
 import os
@@ -27,33 +28,34 @@ def timeit(fn, iters=20):
 
 def main():
     lib = load()
-    M, C, Ci = 802816, 256, 64
-    dy = torch.randn(M, C, device="cuda").to(h16())
-    x = torch.randn(M, C, device="cuda").to(h16())
-    a2 = torch.randn(M, Ci, device="cuda").to(h16())
-    w3 = (torch.randn(C, Ci, device="cuda") / 16).to(h16())
-    w3t = w3.t().contiguous()
-    bits = torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device="cuda")
-    gam, mean, inv = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * .1, \
-        torch.rand(C, device="cuda") + 0.5
-    dgo, dbo = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
-    dw = torch.zeros(C, Ci, device="cuda")
+    for M, C, Ci in ((802816, 256, 64), (200704, 512, 128)):
+        dy = torch.randn(M, C, device="cuda").to(h16())
+        x = torch.randn(M, C, device="cuda").to(h16())
+        a2 = torch.randn(M, Ci, device="cuda").to(h16())
+        w3 = (torch.randn(C, Ci, device="cuda") / 16).to(h16())
+        w3t = w3.t().contiguous()
+        bits = torch.randint(0, 256, (M * C // 8,), dtype=torch.uint8, device="cuda")
+        gam, mean, inv = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * .1, \
+            torch.rand(C, device="cuda") + 0.5
+        dgo, dbo = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+        dw = torch.zeros(C, Ci, device="cuda")
 
-    def fused():
-        lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, dw, dgo, dbo)
+        def fused():
+            lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, dw, dgo, dbo)
 
-    def three():
-        dc3, _, _, _ = lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits,
-                                  dgo, dbo)
-        blk.gemm(dc3, C, False, a2, Ci, False, C, Ci, M, out_bf16=False, out=dw,
-                 accumulate=True, split_k=True)
-        blk.gemm_dgrad(dc3, C, w3, M, Ci, C)
+        def three():
+            dc3, _, _, _ = lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits,
+                                      dgo, dbo)
+            blk.gemm(dc3, C, False, a2, Ci, False, C, Ci, M, out_bf16=False, out=dw,
+                     accumulate=True, split_k=True)
+            blk.gemm_dgrad(dc3, C, w3, M, Ci, C)
 
-    def reduce_only():
-        lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits, dgo, dbo)
-    tf, t3, tr = timeit(fused), timeit(three), timeit(reduce_only)
-    print(f"fused {tf:.1f} us   three-pass {t3:.1f} us   (bn_bwd alone {tr:.1f} us)",
-          flush=True)
+        def reduce_only():
+            lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits, dgo, dbo)
+        tf, t3, tr = timeit(fused), timeit(three), timeit(reduce_only)
+        print(f"M {M} C {C} Ci {Ci}: fused {tf:.1f} us   three-pass {t3:.1f} us   "
+              f"(bn_bwd alone {tr:.1f} us)", flush=True)
+        del dy, x, a2, bits
 
 
 if __name__ == "__main__":

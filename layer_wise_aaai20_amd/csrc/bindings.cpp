@@ -1728,6 +1728,97 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused
   return {da2, o, dgamma, dbeta, dx2, dg2, db2};
 }
 
+// A bottleneck's BN1 backward (no downsample; bf16, training, ReLU mask from c1 through the
+// forward affine scale_shift) fused with the GEMMs consuming dc1 (bnfuse.hip k_bn1_bwd_dgemm):
+// reduce + finalize as bn_bwd, then dx = dc1·W1 + dy·bit3 ([M, Cin] bf16: the block's input
+// gradient, its shortcut term masked by the block output's ReLU bitmap bits3) and dW1 = dc1ᵀ·x
+// into dw_out (accumulated; [Wd][Cin]) or a fresh tensor. w1t = W1ᵀ [Cin][Wd].
+// Returns (dx, dW1, dgamma, dbeta); dc1 is never written.
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn1_bwd_fused(
+    Tensor da1, Tensor c1, Tensor scale_shift, c10::optional<Tensor> weight, Tensor mean,
+    Tensor invstd, Tensor w1t, Tensor x, Tensor dy, Tensor bits3, c10::optional<Tensor> dw_out,
+    c10::optional<Tensor> dgamma_out, c10::optional<Tensor> dbeta_out) {
+  const c10::DeviceGuard guard(x.device());
+  for (const Tensor* t : {&da1, &c1, &w1t, &x, &dy}) {
+    check_dtype(*t, kH16, "bn1_bwd_fused operand");
+    TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->is_contiguous(),
+                "bn1_bwd_fused: contiguous 2-D [rows, channels] operands");
+    check_aligned16(t->data_ptr(), "bn1_bwd_fused operand");
+  }
+  const int64_t M = c1.size(0), Wd = c1.size(1), Cin = x.size(1);
+  TORCH_CHECK(da1.sizes() == c1.sizes() && x.size(0) == M && dy.sizes() == x.sizes(),
+              "da1 / x / dy rows must match c1");
+  TORCH_CHECK(w1t.size(0) == Cin && w1t.size(1) == Wd, "w1t must be W1ᵀ [Cin][Wd]");
+  TORCH_CHECK(lw::bn1_bwd_dgemm_ok(M, (int)Wd, (int)Cin),
+              "bn1_bwd_fused: needs (Wd, Cin) = (64, 256) or (128, 512)");
+  TORCH_CHECK(bits3.scalar_type() == at::kByte && bits3.numel() * 8 == dy.numel() &&
+              bits3.is_contiguous(), "bits3 must be a contiguous uint8 [numel/8] bitmap of dy");
+  check_dtype(scale_shift, at::kFloat, "scale_shift");
+  TORCH_CHECK(scale_shift.numel() == 2 * Wd && scale_shift.is_contiguous(),
+              "scale_shift must hold 2*Wd floats");
+  TORCH_CHECK(mean.numel() == Wd && invstd.numel() == Wd, "statistics must hold Wd floats");
+  auto f32 = x.options().dtype(at::kFloat);
+  bool acc1 = false, acc1b = false;
+  Tensor dgamma = dparam_out(dgamma_out, Wd, x, acc1), dbeta = dparam_out(dbeta_out, Wd, x, acc1b);
+  TORCH_CHECK(acc1 == acc1b, "give both dgamma_out and dbeta_out");
+  Tensor coef = at::empty({3 * Wd}, f32);
+  Tensor partial = at::empty({lw::bn_reduce_blocks(M, (int)Wd) * 2 * Wd}, f32);
+  lw::BNArgs a{};
+  a.M = M;
+  a.C = (int)Wd;
+  a.bf16 = true;
+  a.training = true;
+  a.relu = true;
+  a.coeffs_only = true;
+  a.accum_dparams = acc1;
+  a.x = c1.data_ptr();
+  a.dy = da1.data_ptr();
+  a.scale = ptr<float>(scale_shift);
+  a.shift = a.scale + Wd;
+  a.gamma = optr<float>(weight);
+  a.mean = ptr<float>(mean);
+  a.invstd = ptr<float>(invstd);
+  a.partial = ptr<float>(partial);
+  a.dgamma = ptr<float>(dgamma);
+  a.dbeta = ptr<float>(dbeta);
+  a.A = ptr<float>(coef);
+  a.B = a.A + Wd;
+  a.Cc = a.A + 2 * Wd;
+  hipStream_t st = cur_stream();
+  lw::bn_backward(a, st);
+  Tensor o;
+  const bool have_out = dw_out.has_value() && dw_out->defined();
+  if (have_out) {
+    o = *dw_out;
+    check_dtype(o, at::kFloat, "dw_out");
+    TORCH_CHECK(o.is_cuda() && o.numel() == Wd * Cin && o.is_contiguous(),
+                "dw_out: contiguous [Wd][Cin] fp32");
+    check_aligned16(o.data_ptr(), "dw_out");
+  } else {
+    o = at::zeros({Wd, Cin}, f32);
+  }
+  Tensor dx = at::empty({M, Cin}, x.options());
+  const int nblk = lw::bn1_bwd_dgemm_slabs(M, (int)Wd, (int)Cin);
+  Tensor slab = nblk > 1 ? at::empty({(int64_t)nblk * Wd * Cin}, f32) : o;
+  lw::bn1_bwd_dgemm(ptr<uint16_t>(da1), ptr<uint16_t>(c1), a.scale, a.shift, a.A, a.B, a.Cc,
+                    ptr<uint16_t>(w1t), ptr<uint16_t>(x), ptr<uint16_t>(dy), ptr<uint8_t>(bits3),
+                    ptr<uint16_t>(dx), ptr<float>(slab), M, (int)Wd, (int)Cin, nblk == 1, st);
+  if (nblk > 1) {
+    lw::GemmArgs g{};
+    g.partial = ptr<float>(slab);
+    g.C = o.data_ptr();
+    g.ldc = Cin;
+    g.M = (int)Wd;
+    g.N = (int)Cin;
+    g.out_bf16 = false;
+    g.accumulate = have_out;
+    lw::splitk_reduce(g, nblk, st);
+    if (lw::splitk_take_deferred()) splitk_keep().push_back(slab);
+  }
+  launched("bn1_bwd_fused");
+  return {dx, o, dgamma, dbeta};
+}
+
 // Weight gradient of the tap-reuse conv (conv3tap.hip k_conv3_tap_wgrad): dy [N, Co, H, W] and
 // x [N, C, H, W] bf16 channels_last; returns fp32 dW in [Co][3][3][C] memory order (a channels_last
 // [Co, C, 3, 3] tensor), written into / accumulated onto `out` when given.
@@ -1951,6 +2042,80 @@ std::tuple<Tensor, Tensor, Tensor> stem_pool_bwd(Tensor dp, Tensor idx, Tensor x
   return {dx, dgamma, dbeta};
 }
 
+// The stem backward with its pool/BN apply fused into the 7x7/2 conv's weight gradient
+// (stemfuse.hip): pooled-side statistics + finalize as stem_pool_bwd, then one kernel forms the
+// conv-output gradient tile by tile in LDS and accumulates dW against the 4-channel image x4
+// ([N, 4, 2H, 2W] channels_last). Returns (dW [64][7 * 8 * 4] fp32 — [co][r][s][ci], tap 7 and
+// channel 3 padding — dgamma, dbeta); the conv-output gradient is never written.
+std::tuple<Tensor, Tensor, Tensor> stem_bwd_fused(Tensor dp, Tensor idx, Tensor x,
+                                                  Tensor scale_shift, c10::optional<Tensor> weight,
+                                                  Tensor mean, Tensor invstd, int64_t k, int64_t s,
+                                                  int64_t p, c10::optional<Tensor> dgamma_out,
+                                                  c10::optional<Tensor> dbeta_out, Tensor pooled,
+                                                  Tensor x4) {
+  const c10::DeviceGuard guard(x.device());
+  lw::StemArgs a{};
+  stem_geom(x, k, s, p, a);
+  check_dtype(dp, kH16, "dp");
+  TORCH_CHECK(dp.is_contiguous(at::MemoryFormat::ChannelsLast) && dp.size(2) == a.Ho &&
+              dp.size(3) == a.Wo && dp.size(1) == a.C && dp.size(0) == a.N, "dp shape/layout");
+  TORCH_CHECK(idx.numel() == dp.numel() && idx.scalar_type() == at::kByte, "idx");
+  check_dtype(pooled, kH16, "pooled");
+  TORCH_CHECK(pooled.sizes() == dp.sizes() &&
+              pooled.is_contiguous(at::MemoryFormat::ChannelsLast), "pooled shape/layout");
+  check_dtype(x4, kH16, "x4");
+  TORCH_CHECK(x4.dim() == 4 && x4.size(0) == a.N && x4.size(1) == 4 &&
+              x4.is_contiguous(at::MemoryFormat::ChannelsLast), "x4: [N, 4, H, W] channels_last");
+  TORCH_CHECK(k == 3 && s == 2 && p == 1 &&
+              lw::stem_bwd_wgrad_ok(a.C, a.H, a.W, a.Ho, a.Wo, (int)x4.size(2), (int)x4.size(3)),
+              "stem_bwd_fused: 64 channels at 112x112 from a 224x224 image, 3x3/2/1 pool");
+  TORCH_CHECK(x4.numel() * 2 < (1LL << 31), "x4 > 2 GiB");
+  check_aligned16(x4.data_ptr(), "x4");
+  auto f32 = x.options().dtype(at::kFloat);
+  bool accum = false;
+  Tensor dgamma = dparam_out(dgamma_out, a.C, x, accum);
+  Tensor dbeta = dparam_out(dbeta_out, a.C, x, accum);
+  a.accum_dparams = accum;
+  a.coeffs_only = true;
+  a.pooled = pooled.data_ptr();
+  Tensor coef = at::empty({3 * a.C}, f32);
+  Tensor partial = at::empty({(int64_t)lw::bn_reduce_blocks((int64_t)a.N * a.H * a.W, a.C) * 2 * a.C}, f32);
+  a.x = x.data_ptr();
+  a.dp = dp.data_ptr();
+  a.idx = ptr<uint8_t>(idx);
+  a.scale = ptr<float>(scale_shift);
+  a.shift = a.scale + a.C;
+  a.gamma = optr<float>(weight);
+  a.mean = ptr<float>(mean);
+  a.invstd = ptr<float>(invstd);
+  a.partial = ptr<float>(partial);
+  a.dgamma = ptr<float>(dgamma);
+  a.dbeta = ptr<float>(dbeta);
+  a.A = ptr<float>(coef);
+  a.B = a.A + a.C;
+  a.Cc = a.A + 2 * a.C;
+  hipStream_t st = cur_stream();
+  lw::stem_pool_bwd(a, st);
+  const int nblk = lw::stem_bwd_wgrad_blocks(a.N, a.Ho);
+  Tensor slab = at::empty({(int64_t)nblk * 64 * 224}, f32);
+  Tensor o = at::empty({64, 224}, f32);
+  lw::stem_bwd_wgrad(static_cast<const uint16_t*>(a.dp), a.idx, ptr<uint16_t>(x), a.scale,
+                     a.shift, a.A, a.B, a.Cc, ptr<uint16_t>(x4), ptr<float>(slab), a.N, a.Ho,
+                     a.Wo, (int)x4.size(2), (int)x4.size(3), st);
+  lw::GemmArgs g{};
+  g.partial = ptr<float>(slab);
+  g.C = o.data_ptr();
+  g.ldc = 224;
+  g.M = 64;
+  g.N = 224;
+  g.out_bf16 = false;
+  g.accumulate = false;
+  lw::splitk_reduce(g, nblk, st);
+  if (lw::splitk_take_deferred()) splitk_keep().push_back(slab);
+  launched("stem_bwd_fused");
+  return {o, dgamma, dbeta};
+}
+
 // y = relu?(x*scale+shift [+ res | + res*rscale+rshift])
 Tensor bn_apply(Tensor x, Tensor scale_shift, c10::optional<Tensor> res,
                 c10::optional<Tensor> res_scale_shift, bool relu,
@@ -2110,6 +2275,12 @@ LW_LIBRARY(LW_OPS_NS, m) {
         "Tensor(c!)? dbeta_out, Tensor? x2=None, Tensor? weight2=None, Tensor? mean2=None, "
         "Tensor? invstd2=None, Tensor(d!)? dgamma2_out=None, Tensor(e!)? dbeta2_out=None) "
         "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+  m.def("stem_bwd_fused(Tensor dp, Tensor idx, Tensor x, Tensor scale_shift, Tensor? weight, "
+        "Tensor mean, Tensor invstd, int k, int s, int p, Tensor(a!)? dgamma_out, "
+        "Tensor(b!)? dbeta_out, Tensor pooled, Tensor x4) -> (Tensor, Tensor, Tensor)");
+  m.def("bn1_bwd_fused(Tensor da1, Tensor c1, Tensor scale_shift, Tensor? weight, Tensor mean, "
+        "Tensor invstd, Tensor w1t, Tensor x, Tensor dy, Tensor bits3, Tensor(a!)? dw_out, "
+        "Tensor(b!)? dgamma_out, Tensor(c!)? dbeta_out) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("conv3_tap_wgrad(Tensor dy, Tensor x, Tensor(a!)? out, bool accumulate) -> Tensor");
   m.def(
       "bn_bwd_dual(Tensor dy, Tensor x, Tensor x2, Tensor bits, Tensor? weight, Tensor mean, "
@@ -2191,6 +2362,8 @@ LW_LIBRARY_IMPL(LW_OPS_NS, CUDA, m) {
   m.impl("conv3_tap", &conv3_tap);
   m.impl("conv3_tap_wgrad", &conv3_tap_wgrad);
   m.impl("bn3_bwd_fused", &bn3_bwd_fused);
+  m.impl("bn1_bwd_fused", &bn1_bwd_fused);
+  m.impl("stem_bwd_fused", &stem_bwd_fused);
   m.impl("gemm", &gemm);
   m.impl("gemm_ex", &gemm_ex);
   m.impl("conv_ex", &conv_ex);

@@ -1199,6 +1199,7 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb2,
                        a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
                        (int)a.accum_dparams);
+    if (a.coeffs_only) return;
   }
   if (a.k == 3 && a.s == 2 && a.p == 1 && a.H == 2 * a.Ho && a.W == 2 * a.Wo) {
     // 2x2-block form over the output grid (same partial layout: nb blocks of the grid points)

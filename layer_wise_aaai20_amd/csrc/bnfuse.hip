@@ -47,6 +47,15 @@ __device__ __forceinline__ h16x8 cat8(i16x4 lo, i16x4 hi) {
   return __builtin_bit_cast(h16x8, v);
 }
 
+// 8 bf16 values with those whose bit of `b` is clear zeroed (the ReLU-masked addend)
+__device__ __forceinline__ uint4 mask_h16x8(uint4 a, uint32_t b) {
+  const uint32_t m0 = ((b & 1u) ? 0xffffu : 0u) | ((b & 2u) ? 0xffff0000u : 0u);
+  const uint32_t m1 = ((b & 4u) ? 0xffffu : 0u) | ((b & 8u) ? 0xffff0000u : 0u);
+  const uint32_t m2 = ((b & 16u) ? 0xffffu : 0u) | ((b & 32u) ? 0xffff0000u : 0u);
+  const uint32_t m3 = ((b & 64u) ? 0xffffu : 0u) | ((b & 128u) ? 0xffff0000u : 0u);
+  return make_uint4(a.x & m0, a.y & m1, a.z & m2, a.w & m3);
+}
+
 template <int CO> struct BfGeom {
   static constexpr int BM = CO == 256 ? 64 : 32;        // pixels per tile
   static constexpr int CPR = CO / 8;                    // 16-byte chunks per dc3 row
@@ -315,6 +324,266 @@ void bn3_bwd_dgemm(const uint16_t* dr, const uint16_t* c3, const uint8_t* bits, 
   if (C == 256) { if (x2) LW_BF(256, true); else LW_BF(256, false); }
   else { if (x2) LW_BF(512, true); else LW_BF(512, false); }
 #undef LW_BF
+}
+
+// ---------------------------------------------------------------------------------------------
+// The same fusion for BN1 of a bottleneck without a downsample branch (stages 1 and 2): after
+// BN1's reduce + finalize, the per-layer path runs
+//   dc1 = A·(da1·[c1·s+h > 0]) + B·c1 + C      k_bn_bwd_apply   reads da1, c1; writes dc1 (W ch)
+//   dW1 += dc1ᵀ · x                             GEMM             reads dc1, x (Cin ch)
+//   dx   = dc1 · W1 + dy·bit3                   GEMM             reads dc1, dy, bitmap; writes dx
+// Here dc1 is formed per 64-pixel tile in LDS and feeds both products:
+//   dx tile [64 px][Cin part] = dc1 tile · W1[:, part] + dy·bit3   (W1ᵀ part resident in LDS)
+//   dW1 [W][Cin part]        += dc1 tileᵀ · x tile                 (registers, slab per group)
+// A workgroup owns a 256-column part of Cin (stage 2: two parts, sharing an XCD as above); every
+// part forms the whole dc1 tile (W = 64 / 128 channels: the small tensors are read per part).
+// LDS (bytes): W1ᵀ part [256][2W] + dc1 [64][2W] + x [64][512] + dy·bit / dx [64][512]; rows of
+// 128 B use the s128 swizzle (row AND transposed reads conflict-free), 512-B rows s512.
+template <int WD> struct B1Geom {
+  static constexpr int BM = 64, CP = 256;               // pixels per tile, Cin columns per part
+  static constexpr int WB = WD * 2;                     // dc1 / W1ᵀ row bytes
+  static constexpr int WCPR = WD / 8;                   // 16-byte chunks per dc1 row
+  static constexpr int NW = BM * WCPR / 256;            // dc1 chunks per thread per tile
+  static constexpr int NX = BM * (CP / 8) / 256;        // x / dy chunks per thread per tile (8)
+  static constexpr int W1_BYTES = CP * WB, D_BYTES = BM * WB, X_BYTES = BM * CP * 2;
+  static constexpr int LDS = W1_BYTES + D_BYTES + 2 * X_BYTES;
+  static constexpr int NWB = WD / 16;                   // dW1 16-row blocks (all waves share)
+};
+
+template <int WD> struct B1Raw {
+  uint4 d[B1Geom<WD>::NW], c[B1Geom<WD>::NW], x[B1Geom<WD>::NX], y[B1Geom<WD>::NX];
+  uint32_t b[B1Geom<WD>::NX];
+};
+
+// swizzled byte offset of 16-byte chunk ch of row r in an image with rows of RB bytes
+template <int RB>
+__device__ __forceinline__ int swz(int r, int ch) {
+  if constexpr (RB == 128) return r * 128 + ((ch ^ s128(r & 15)) << 4);
+  else return r * RB + ((ch ^ s512(r & 15)) << 4);
+}
+
+template <int WD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+void k_bn1_bwd_dgemm(const uint16_t* __restrict__ da1, const uint16_t* __restrict__ c1,
+                     const float* __restrict__ fs, const float* __restrict__ fh,
+                     const float* __restrict__ A, const float* __restrict__ B,
+                     const float* __restrict__ Cc, const uint16_t* __restrict__ w1t,
+                     const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                     const uint8_t* __restrict__ bits, uint16_t* __restrict__ dx,
+                     float* __restrict__ slab, int64_t M, int Cin, int tiles, int tpw,
+                     int acc_out, int xcd_pairs) {
+  using G = B1Geom<WD>;
+  constexpr int BM = G::BM, CP = G::CP, WB = G::WB;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G::LDS];
+  uint8_t* const sW = lds;                            // W1ᵀ part [CP][WB]
+  uint8_t* const sD = lds + G::W1_BYTES;              // dc1      [BM][WB]
+  uint8_t* const sX = sD + G::D_BYTES;                // x part   [BM][512]
+  uint8_t* const sY = sX + G::X_BYTES;                // dy·bit -> dx [BM][512]
+  const int t = threadIdx.x, l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g = l >> 4, q = (l & 15) >> 2, p = l & 3;
+  const int nparts = Cin / CP;
+  const int bx = (int)blockIdx.x & 7, by = (int)blockIdx.x >> 3;
+  const int part = xcd_pairs ? by % nparts : (int)blockIdx.x % nparts;
+  const int grp = xcd_pairs ? (by / nparts) * 8 + bx : (int)blockIdx.x / nparts;
+  const int c0 = part * CP;
+  const int u0 = grp * tpw, u1 = min(u0 + tpw, tiles);
+  const uint32_t wbytes = (uint32_t)(M * WD * 2), cbytes = (uint32_t)(M * Cin * 2);
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(da1, wbytes), rc = make_rsrc(c1, wbytes);
+  const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, cbytes), ry = make_rsrc(dy, cbytes);
+
+  // ---- this part's W1ᵀ rows (Cin c0 .. c0 + 255, W contiguous) into LDS (once)
+#pragma unroll
+  for (int i = 0; i < CP * G::WCPR / 256; ++i) {
+    const int e = t + 256 * i, row = e / G::WCPR, ch = e % G::WCPR;
+    const uint4 v = *reinterpret_cast<const uint4*>(w1t + (int64_t)(c0 + row) * WD + ch * 8);
+    *reinterpret_cast<uint4*>(sW + swz<WB>(row, ch)) = v;
+  }
+  // ---- apply mapping: dc1 chunk column wc, rows wrow + (256 / WCPR)·i; x / dy: chunk column xc,
+  // rows xrow + 8i
+  const int wc = t % G::WCPR, wrow = t / G::WCPR;
+  const int xc = t & 31, xrow = t >> 5;
+  float ca[8], cb[8], ck[8], sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    ca[k] = A[wc * 8 + k]; cb[k] = B[wc * 8 + k]; ck[k] = Cc[wc * 8 + k];
+    sc[k] = fs[wc * 8 + k]; sh[k] = fh[wc * 8 + k];
+  }
+
+  auto load_tile = [&](int u, B1Raw<WD>& R) {
+    const int64_t m0 = (int64_t)u * BM;
+#pragma unroll
+    for (int i = 0; i < G::NW; ++i) {
+      const int64_t m = m0 + wrow + (256 / G::WCPR) * i;
+      const uint32_t off = m < M ? (uint32_t)((m * WD + wc * 8) * 2) : OOB;
+      R.d[i] = bload16(rd, off);
+      R.c[i] = bload16(rc, off);
+    }
+#pragma unroll
+    for (int i = 0; i < G::NX; ++i) {
+      const int64_t m = m0 + xrow + 8 * i;
+      const uint32_t off = m < M ? (uint32_t)((m * Cin + c0 + xc * 8) * 2) : OOB;
+      R.x[i] = bload16(rx, off);
+      R.y[i] = bload16(ry, off);
+      R.b[i] = m < M ? (uint32_t)bits[(m * Cin + c0) / 8 + xc] : 0u;
+    }
+  };
+
+  f32x4 acc2[G::NWB][4];                 // dW1 rows 16i.., Cin columns 64w + 16j ..
+#pragma unroll
+  for (int i = 0; i < G::NWB; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto phase_a = [&](const B1Raw<WD>& R) {
+#pragma unroll
+    for (int i = 0; i < G::NW; ++i) {
+      const uint32_t dw[4] = {R.d[i].x, R.d[i].y, R.d[i].z, R.d[i].w};
+      const uint32_t cw[4] = {R.c[i].x, R.c[i].y, R.c[i].z, R.c[i].w};
+      uint32_t o[4];
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) {
+        const float x0 = hlo(cw[k2]), x1 = hhi(cw[k2]);
+        float d0 = hlo(dw[k2]), d1 = hhi(dw[k2]);
+        d0 = fmaf(x0, sc[2 * k2], sh[2 * k2]) > 0.f ? d0 : 0.f;
+        d1 = fmaf(x1, sc[2 * k2 + 1], sh[2 * k2 + 1]) > 0.f ? d1 : 0.f;
+        const float v0 = ca[2 * k2] * d0 + cb[2 * k2] * x0 + ck[2 * k2];
+        const float v1 = ca[2 * k2 + 1] * d1 + cb[2 * k2 + 1] * x1 + ck[2 * k2 + 1];
+        o[k2] = (uint32_t)f2h(v0) | ((uint32_t)f2h(v1) << 16);
+      }
+      const int row = wrow + (256 / G::WCPR) * i;
+      *reinterpret_cast<uint4*>(sD + swz<WB>(row, wc)) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < G::NX; ++i) {
+      const int row = xrow + 8 * i;
+      *reinterpret_cast<uint4*>(sX + swz<512>(row, xc)) = R.x[i];
+      // the masked addend dy·bit, rounded like the GEMM epilogue's addend (bf16 in, fp32 add)
+      *reinterpret_cast<uint4*>(sY + swz<512>(row, xc)) = mask_h16x8(R.y[i], R.b[i]);
+    }
+  };
+
+  auto phase_b = [&](int u) {
+    // dW1[w][cin] += dc1ᵀ[w][px] · x[px][cin], K = 64 pixels: wave w takes Cin columns 64w..
+#pragma unroll
+    for (int kk = 0; kk < BM / 32; ++kk) {
+      i16x4 ta[2][G::NWB], tb[2][4];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int px = 32 * kk + 8 * g + q + 4 * hh;
+#pragma unroll
+        for (int i = 0; i < G::NWB; ++i)
+          ta[hh][i] = tr_read(sD + swz<WB>(px, 2 * i + (p >> 1)) + 8 * (p & 1));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          tb[hh][j] = tr_read(sX + swz<512>(px, 2 * (4 * w + j) + (p >> 1)) + 8 * (p & 1));
+      }
+      h16x8 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = cat8(tb[0][j], tb[1][j]);
+#pragma unroll
+      for (int i = 0; i < G::NWB; ++i) {
+        const h16x8 fa = cat8(ta[0][i], ta[1][i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc2[i][j] = mfma16(fa, fb[j], acc2[i][j]);
+      }
+    }
+    // dx tile: D[cin 64w + 16j ..][px] = W1ᵀ[cin][w] · dc1[px][w]ᵀ, K = W
+    f32x4 acc1[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc1[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < WD / 32; ++ks) {
+      const int ch = 4 * ks + g;
+      h16x8 fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        fb[i] = *reinterpret_cast<const h16x8*>(sD + swz<WB>(16 * i + (l & 15), ch));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const h16x8 fa = *reinterpret_cast<const h16x8*>(sW + swz<WB>(64 * w + 16 * j + (l & 15), ch));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc1[j][i] = mfma16(fa, fb[i], acc1[j][i]);
+      }
+    }
+    // epilogue: lane holds cin 64w + 16j + 4g .. +3 of pixel 16i + (l & 15); dx = round(acc)
+    // + addend (the GEMM epilogue's order: bf16(acc) then + addend, rounded again)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int px = 16 * i + (l & 15);
+        const int cin = 64 * w + 16 * j + 4 * g;
+        uint2* ptr = reinterpret_cast<uint2*>(sY + swz<512>(px, cin >> 3) + 8 * ((cin >> 2) & 1));
+        const uint2 a = *ptr;
+        const float s0 = h2f(f2h(acc1[j][i][0])) + hlo(a.x), s1 = h2f(f2h(acc1[j][i][1])) + hhi(a.x);
+        const float s2 = h2f(f2h(acc1[j][i][2])) + hlo(a.y), s3 = h2f(f2h(acc1[j][i][3])) + hhi(a.y);
+        *ptr = make_uint2((uint32_t)f2h(s0) | ((uint32_t)f2h(s1) << 16),
+                          (uint32_t)f2h(s2) | ((uint32_t)f2h(s3) << 16));
+      }
+    __syncthreads();
+    const int64_t m0 = (int64_t)u * BM;
+#pragma unroll
+    for (int i = 0; i < G::NX; ++i) {
+      const int row = xrow + 8 * i;
+      if (m0 + row < M)
+        *reinterpret_cast<uint4*>(dx + (m0 + row) * Cin + c0 + xc * 8) =
+            *reinterpret_cast<const uint4*>(sY + swz<512>(row, xc));
+    }
+  };
+
+  B1Raw<WD> R0;
+  if (u0 < u1) load_tile(u0, R0);
+  for (int u = u0; u < u1; ++u) {
+    phase_a(R0);
+    __syncthreads();
+    if (u + 1 < u1) load_tile(u + 1, R0);
+    phase_b(u);
+    __syncthreads();                     // dx staging read before the next tile overwrites it
+  }
+  // ---- slab: lane holds D[w = 16i + 4g + r][cin = c0 + 64w + 16j + (l & 15)]
+  float* sl = slab + (int64_t)grp * WD * Cin;
+#pragma unroll
+  for (int i = 0; i < G::NWB; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float* d = sl + (int64_t)(16 * i + 4 * g + r) * Cin + c0 + 64 * w + 16 * j + (l & 15);
+        *d = acc_out ? *d + acc2[i][j][r] : acc2[i][j][r];
+      }
+}
+
+bool bn1_bwd_dgemm_ok(int64_t M, int Wd, int Cin) {
+  return ((Wd == 64 && Cin == 256) || (Wd == 128 && Cin == 512)) && M > 0 &&
+         M * Cin * 2 < (int64_t(1) << 31);
+}
+
+int bn1_bwd_dgemm_slabs(int64_t M, int Wd, int Cin) {
+  const int tiles = (int)((M + 63) / 64), nparts = Cin / 256;
+  const int want = std::max(8, cu_count() / nparts / 8 * 8);
+  const int tpw = (tiles + want - 1) / want;
+  const int used = (tiles + tpw - 1) / tpw;
+  return used <= 1 ? 1 : (used + 7) / 8 * 8;
+}
+
+void bn1_bwd_dgemm(const uint16_t* da1, const uint16_t* c1, const float* fs, const float* fh,
+                   const float* A, const float* B, const float* Cc, const uint16_t* w1t,
+                   const uint16_t* x, const uint16_t* dy, const uint8_t* bits, uint16_t* dx,
+                   float* slab, int64_t M, int Wd, int Cin, bool acc_out, hipStream_t st) {
+  const int tiles = (int)((M + 63) / 64), nparts = Cin / 256;
+  const int groups = bn1_bwd_dgemm_slabs(M, Wd, Cin);
+  const int tpw = (tiles + groups - 1) / groups;
+  const int acc = (acc_out && groups == 1) ? 1 : 0;
+  const int blocks = groups * nparts, xp = groups % 8 == 0 ? 1 : 0;
+  if (Wd == 64)
+    hipLaunchKernelGGL(k_bn1_bwd_dgemm<64>, dim3(blocks), dim3(256), 0, st, da1, c1, fs, fh, A, B,
+                       Cc, w1t, x, dy, bits, dx, slab, M, Cin, tiles, tpw, acc, xp);
+  else
+    hipLaunchKernelGGL(k_bn1_bwd_dgemm<128>, dim3(blocks), dim3(256), 0, st, da1, c1, fs, fh, A,
+                       B, Cc, w1t, x, dy, bits, dx, slab, M, Cin, tiles, tpw, acc, xp);
 }
 
 }  // namespace lw

@@ -207,6 +207,15 @@ void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st);
 // splitk_reduce; with a single slab and acc_out the kernel adds into slab = the destination).
 // With x2 (the downsample block: its shortcut BN's input, same dy and bitmap) also
 // dx2 = A2·(dy·bit) + B2·x2 + C2 into dx2 [M][C].
+// BN1 backward apply fused with dW1 += dc1ᵀ·x and dx = dc1·W1 + dy·bit3 (bnfuse.hip), for a
+// bottleneck without downsample: (Wd, Cin) = (64, 256) or (128, 512); the ReLU mask from c1 via
+// the forward affine (fs, fh); w1t = W1ᵀ [Cin][Wd]; slab [bn1_bwd_dgemm_slabs][Wd][Cin]
+bool bn1_bwd_dgemm_ok(int64_t M, int Wd, int Cin);
+int bn1_bwd_dgemm_slabs(int64_t M, int Wd, int Cin);
+void bn1_bwd_dgemm(const uint16_t* da1, const uint16_t* c1, const float* fs, const float* fh,
+                   const float* A, const float* B, const float* Cc, const uint16_t* w1t,
+                   const uint16_t* x, const uint16_t* dy, const uint8_t* bits, uint16_t* dx,
+                   float* slab, int64_t M, int Wd, int Cin, bool acc_out, hipStream_t st);
 bool bn3_bwd_dgemm_ok(int64_t M, int C, int Ci);
 int bn3_bwd_dgemm_slabs(int64_t M, int C, int Ci);
 void bn3_bwd_dgemm(const uint16_t* dr, const uint16_t* c3, const uint8_t* bits, const float* A,
@@ -237,10 +246,20 @@ struct StemArgs {
   const void* pooled;     // backward: the forward's pooled map (statistics from the pooled side)
   int N, H, W, C, Ho, Wo, k, s, p;
   bool accum_dparams;
+  bool coeffs_only;       // backward: statistics + finalize only (dx formed by a fused consumer)
 };
 void stem_pool_fwd(const StemArgs& a, hipStream_t st);
 void stem_pool_bwd(const StemArgs& a, hipStream_t st);
 void relu_pool_bwd(const StemArgs& a, hipStream_t st);   // pool + ReLU backward, no BN
+// the stem's pool/BN backward apply fused with the 7x7/2 conv's weight gradient (stemfuse.hip):
+// conv output C = 64 at 112x112 from a 224x224 4-channel image, 3x3/2/1 pool; slab
+// [stem_bwd_wgrad_blocks][64][224] fp32 partials of dW [co][r][s 0..7][ci 0..3]
+bool stem_bwd_wgrad_ok(int C, int H, int W, int Ho, int Wo, int Hin, int Win);
+int stem_bwd_wgrad_blocks(int N, int Ho);
+void stem_bwd_wgrad(const uint16_t* dp, const uint8_t* idx, const uint16_t* c, const float* scale,
+                    const float* shift, const float* A, const float* B, const float* Cc,
+                    const uint16_t* x4, float* slab, int N, int Ho, int Wo, int Hin, int Win,
+                    hipStream_t st);
 // kPoolIdC ones followed by kPoolIdC zeros in device memory (current device): the identity BN
 // constants of a plain ReLU max-pool, so a pool call needs no per-call fill kernels
 constexpr int kPoolIdC = 2048;

@@ -68,9 +68,10 @@ CL = torch.channels_last
 # * the BN3 backward of a 256- or 512-channel block (ResNet-50 stages 1-2) runs its apply inside
 #   one kernel with both GEMMs that read dc3 (csrc/bnfuse.hip): dy, c3 and the bitmap are read
 #   once instead of dc3 being written and read twice; 604.2 -> 417.1 us a stage-1 block, 327.4 ->
-#   272.2 us a stage-2 block, bench 11,738 -> 12,173 img/s on one box (profiles/r6/fused_bn3/).
-#   LWAAAI_FUSE_BN3=0: the three passes.
-FUSE_BN3 = os.environ.get("LWAAAI_FUSE_BN3", "1") != "0"
+#   272.2 us a stage-2 block, bench 11,738 -> 12,173 img/s on one box (profiles/r6/fused_bn3/);
+#   likewise BN1 of a block without downsample with dW1 = dc1ᵀ·x and dx = dc1·W1 + dy·bit3.
+#   LWAAAI_FUSE_BNBWD=0: the three passes.
+FUSE_BNBWD = os.environ.get("LWAAAI_FUSE_BNBWD", "1") != "0"
 TILES = with_mf32((1, 2, 3, 4, 5, 6))   # csrc GemmTile ids (0 = heuristic)
 STREAM = (11, 12, 13)               # streaming kernel, output panel 64 / 128 / 256
 BIG = (21, 22)                      # 256x256 / 256x128 8-wave LDS-DMA kernel (csrc/gemm_big.hip)
@@ -385,7 +386,7 @@ class _BottleneckFn(torch.autograd.Function):
         # the bitmap — the dx GEMM as a masked addend, the shortcut BN through its ReLU mode)
         grads = {}
         dual = None
-        fused = FUSE_BN3 and (cout, width) in ((256, 64), (512, 128)) and dr.dtype == h16()
+        fused = FUSE_BNBWD and (cout, width) in ((256, 64), (512, 128)) and dr.dtype == h16()
         if fused:
             # BN3's apply fused into both consumers of dc3 (csrc/bnfuse.hip): da2 = dc3·W3 and
             # dW3 = dc3ᵀ·a2 from one pass over dy, c3 and the bitmap; dc3 is never written (a
@@ -449,6 +450,21 @@ class _BottleneckFn(torch.autograd.Function):
         # da1 = conv3x3ᵀ(dc2)
         da1 = _rows(conv_dgrad(dc2n, W2, (H, W), stride, padding))
         o1 = _bn_grad_outs(g1p, b1p)
+        if (FUSE_BNBWD and not has_down and (width, Cin) in ((64, 256), (128, 512)) and
+                dr.dtype == h16()):
+            # BN1's apply fused into both consumers of dc1 (csrc/bnfuse.hip): dx = dc1·W1 +
+            # dy·bit3 and dW1 = dc1ᵀ·x from one pass; dc1 is never written
+            dst1, d1 = _wgrad_target(w1, (width, Cin))
+            with _deferred_reduce(da1, d1):
+                dx, _, dg1, db1 = lib.bn1_bwd_fused(
+                    da1, c1, ss1, g1, mean1, inv1,
+                    _kc_weight(W1, width, Cin, width).view(Cin, width), _rows(x), dr, bits3,
+                    dst1, o1[0], o1[1])
+            grads["g1"], grads["b1"] = _finish_bn(g1p, b1p, dg1, db1, o1)
+            grads["w1"] = _wgrad_done(w1, dst1, d1)
+            return (_nchw(dx, N, H, W), grads["w1"], grads["g1"], grads["b1"], grads["w2"],
+                    grads["g2"], grads["b2"], grads["w3"], grads["g3"], grads["b3"], None, None,
+                    None, None)
         dc1, dg1, db1, _ = lib.bn_bwd(da1, c1, None, g1, mean1, inv1, ss1, True, True, False,
                                       None, o1[0], o1[1])
         grads["g1"], grads["b1"] = _finish_bn(g1p, b1p, dg1, db1, o1)

@@ -276,6 +276,20 @@ class _StemConvPoolFn(torch.autograd.Function):
         w, g, b = ctx.params
         dout = dout.to(h16()).contiguous(memory_format=torch.channels_last)
         outs = block._bn_grad_outs(g, b)
+        if (block.FUSE_BNBWD and not ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and
+                pooled is not None and ctx.geom == (3, 2, 1) and tuple(c.shape[1:]) ==
+                (64, 112, 112) and tuple(x.shape[2:]) == (224, 224) and
+                ctx.conv == ((2, 2), (3, 3)) and tuple(w.shape) == (64, 3, 7, 7)):
+            # the pool / BN backward apply fused into the 7x7 conv's weight gradient
+            # (csrc/stemfuse.hip): the 112x112 conv-output gradient is never written
+            from .conv import _c4_input
+            x4 = x if x.shape[1] == 4 else _c4_input(x)
+            x4 = x4.to(h16()).contiguous(memory_format=torch.channels_last)
+            dw, dg, db = load().stem_bwd_fused(dout, idx, c, ss, gamma, mean, invstd, *ctx.geom,
+                                               outs[0], outs[1], pooled, x4)
+            gg, gb = block._finish_bn(g, b, dg, db, outs)
+            dw = dw.view(64, 7, 8, 4)[:, :, :7, :3].permute(0, 3, 1, 2)
+            return None, block._finish_param(w, dw, block._direct(w)), gg, gb, None, None, None
         dc, dg, db = load().stem_pool_bwd(dout, idx, c, ss, gamma, mean, invstd, *ctx.geom,
                                           outs[0], outs[1], pooled)
         gg, gb = block._finish_bn(g, b, dg, db, outs)

@@ -58,5 +58,65 @@ def main():
         del dy, x, a2, bits
 
 
+def bn1():
+    """BN1 (no downsample) fused with dW1 / dx vs bn_bwd + the two GEMMs."""
+    lib = load()
+    for M, Wd, Cin in ((802816, 64, 256), (200704, 128, 512)):
+        da1 = torch.randn(M, Wd, device="cuda").to(h16())
+        c1 = torch.randn(M, Wd, device="cuda").to(h16())
+        x = torch.randn(M, Cin, device="cuda").to(h16())
+        dy = torch.randn(M, Cin, device="cuda").to(h16())
+        w1 = (torch.randn(Wd, Cin, device="cuda") / 16).to(h16())
+        w1t = w1.t().contiguous()
+        bits = torch.randint(0, 256, (M * Cin // 8,), dtype=torch.uint8, device="cuda")
+        gam, mean, inv = torch.rand(Wd, device="cuda") + 0.5, torch.randn(Wd, device="cuda") * .1, \
+            torch.rand(Wd, device="cuda") + 0.5
+        ss = torch.cat([gam * inv, -mean * gam * inv]).contiguous()
+        dgo, dbo = torch.zeros(Wd, device="cuda"), torch.zeros(Wd, device="cuda")
+        dw = torch.zeros(Wd, Cin, device="cuda")
+
+        def fused():
+            lib.bn1_bwd_fused(da1, c1, ss, gam, mean, inv, w1t, x, dy, bits, dw, dgo, dbo)
+
+        def three():
+            dc1, _, _, _ = lib.bn_bwd(da1, c1, None, gam, mean, inv, ss, True, True, False, None,
+                                      dgo, dbo)
+            blk.gemm(dc1, Wd, False, x, Cin, False, Wd, Cin, M, out_bf16=False, out=dw,
+                     accumulate=True, split_k=True)
+            blk.gemm_dgrad(dc1, Wd, w1, M, Cin, Wd, addend=dy, addend_bits=bits)
+
+        def reduce_only():
+            lib.bn_bwd(da1, c1, None, gam, mean, inv, ss, True, True, False, None, dgo, dbo)
+        tf, t3, tr = timeit(fused), timeit(three), timeit(reduce_only)
+        print(f"BN1 M {M} W {Wd} Cin {Cin}: fused {tf:.1f} us   three-pass {t3:.1f} us   "
+              f"(bn_bwd alone {tr:.1f} us)", flush=True)
+
+
+def stem():
+    """Stem backward: pool/BN apply fused into the 7x7/2 weight gradient vs the two passes."""
+    from layer_wise_aaai20_amd.ops import conv as CV
+    lib = load()
+    N = 256
+    x4 = torch.randn(N, 4, 224, 224, device="cuda").to(h16()).contiguous(
+        memory_format=torch.channels_last)
+    c = torch.randn(N, 64, 112, 112, device="cuda").to(h16()).contiguous(
+        memory_format=torch.channels_last)
+    gam, mean, inv = torch.rand(64, device="cuda") + 0.5, torch.randn(64, device="cuda") * .1, \
+        torch.rand(64, device="cuda") + 0.5
+    ss = torch.cat([gam * inv, -mean * gam * inv]).contiguous()
+    pooled, idx = lib.stem_pool_fwd(c, ss, 3, 2, 1)
+    dp = torch.randn_like(pooled.float()).to(h16()).contiguous(memory_format=torch.channels_last)
+
+    def fused():
+        lib.stem_bwd_fused(dp, idx, c, ss, gam, mean, inv, 3, 2, 1, None, None, pooled, x4)
+
+    def two():
+        dc, _, _ = lib.stem_pool_bwd(dp, idx, c, ss, gam, mean, inv, 3, 2, 1, None, None, pooled)
+        CV.conv_wgrad(dc, x4, (64, 3, 7, 7), 2, 3)
+    print(f"stem backward: fused {timeit(fused):.1f} us   two-pass {timeit(two):.1f} us", flush=True)
+
+
 if __name__ == "__main__":
     main()
+    bn1()
+    stem()

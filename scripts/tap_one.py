@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """One tap-reuse conv shape, run N times (for rocprofv3 counter passes).
-usage: python scripts/tap_one.py [--n 256 --c 128 --co 128 --hw 28 --pass fwd|dgrad|wgrad --iters 20]"""
+usage: python scripts/tap_one.py [--n 256 --c 128 --co 128 --hw 28 --pass fwd|dgrad|wgrad|wgrad_tuned|fwd_tuned --iters 20]"""
 import argparse
 import os
 import sys
@@ -32,6 +32,10 @@ for _ in range(a.iters):
         lib.conv3_tap(x, op, a.co, True)
     elif a.pas == "dgrad":
         lib.conv3_tap(dy, wf, a.c, False)
+    elif a.pas == "wgrad_tuned":        # the shipped tuner's pick (implicit-GEMM k_gemm)
+        CV.conv_wgrad(dy, x, tuple(w.shape), 1, 1, out=dw)
+    elif a.pas == "fwd_tuned":
+        CV.conv_fwd(x, w, 1, 1, stats=True)
     else:
         lib.conv3_tap_wgrad(dy, x, dw, True)
 torch.cuda.synchronize()

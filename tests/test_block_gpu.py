@@ -107,9 +107,9 @@ def test_block_direct_arena_gradients():
                                                          (512, 128, 1, False),
                                                          (256, 128, 2, True)])
 def test_fused_bn3_backward_matches_three_pass_block(inplanes, planes, stride, down, monkeypatch):
-    """A 256-channel bottleneck (and the downsample one) with BN3's backward fused into its two
-    GEMMs (csrc/bnfuse.hip) gives the three-pass block's input and parameter gradients to bf16 /
-    summation-order noise."""
+    """Stage-1/2 bottlenecks (with and without downsample) with BN3's — and, without downsample,
+    BN1's — backward fused into their two GEMMs (csrc/bnfuse.hip) give the three-pass block's
+    input and parameter gradients to bf16 / summation-order noise."""
     torch.manual_seed(3)
     ref = _make(inplanes, planes, stride, down).cuda().to(memory_format=CL)
     x = torch.randn(8, inplanes, 28, 28, device="cuda").to(torch.bfloat16)
@@ -118,7 +118,7 @@ def test_fused_bn3_backward_matches_three_pass_block(inplanes, planes, stride, d
         memory_format=CL)
     outs = {}
     for fuse in (True, False):
-        monkeypatch.setattr(blk, "FUSE_BN3", fuse)
+        monkeypatch.setattr(blk, "FUSE_BNBWD", fuse)
         m, y, gx = _run(copy.deepcopy(ref), x.float(), gy, True)
         outs[fuse] = (y.float(), gx.float(), [p.grad.float() for p in m.parameters()])
     assert torch.equal(outs[True][0], outs[False][0])
@@ -254,3 +254,42 @@ def test_stem_pool_backward_ill_conditioned_channels(shape, monkeypatch):
     # (dx is not compared with fp32 elementwise: bf16 ties in a 3x3 window send a pixel's
     # gradient to a different argmax than fp32 picks; test_stem_bn_relu_pool_matches_layers
     # pins dx against the unfused bf16 layers instead)
+
+
+@pytest.mark.parametrize("direct", [False, True])
+def test_fused_stem_backward_matches_two_pass(direct, monkeypatch):
+    """The stem backward with the pool / BN apply fused into the 7x7/2 weight gradient
+    (csrc/stemfuse.hip) vs the two-pass path (k_stem_pool_bwd_s2 + implicit-GEMM wgrad): same
+    forward, conv-weight and BN-parameter gradients within summation-order / bf16 noise, also
+    when the gradients go straight into arena views (CompressedDDP's direct path)."""
+    from layer_wise_aaai20_amd.ops import nn as NN
+    torch.manual_seed(5)
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda()
+    conv.weight.data = conv.weight.data.to(torch.bfloat16).float()
+    bn = torch.nn.BatchNorm2d(64).cuda()
+    bn.weight.data.uniform_(0.5, 1.5)
+    bn.bias.data.normal_(0, 0.2)
+    pool = torch.nn.MaxPool2d(3, 2, 1)
+    x = torch.randn(2, 4, 224, 224, device="cuda").to(torch.bfloat16)
+    x[:, 3] = 0
+    x = x.contiguous(memory_format=CL)
+    gy = torch.randn(2, 64, 56, 56, device="cuda").contiguous(memory_format=CL)
+    res = {}
+    for fuse in (True, False):
+        monkeypatch.setattr(blk, "FUSE_BNBWD", fuse)
+        c2, b2 = copy.deepcopy(conv), copy.deepcopy(bn)
+        calls = []
+        if direct:
+            for p in (c2.weight, b2.weight, b2.bias):
+                p.grad = torch.zeros_like(p) if p is not c2.weight else \
+                    torch.zeros_like(p).contiguous(memory_format=CL)
+                p._lw_grad_ready = lambda q: calls.append(id(q))
+        y = NN.stem_conv_bn_relu_pool(x, c2, b2, pool)
+        y.backward(gy.to(y.dtype))
+        if direct:
+            assert sorted(calls) == sorted(id(p) for p in (c2.weight, b2.weight, b2.bias))
+        res[fuse] = (y.float(), c2.weight.grad.float(), b2.weight.grad.float(),
+                     b2.bias.grad.float())
+    assert torch.equal(res[True][0], res[False][0])
+    for a, b in zip(res[True][1:], res[False][1:]):
+        assert _rel(a, b) < 1e-2

@@ -269,3 +269,38 @@ def test_bn3_bwd_fused_matches_three_passes(M, C, Ci, dual):
     _, dw2, _, _, _, _, _ = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, None, None,
                                               None, *((x2, gam2, mean2, inv2) if dual else ()))
     torch.testing.assert_close(dw2, dw - 0.25, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,Wd,Cin", [(4096, 64, 256), (3000, 64, 256), (802816 // 16, 64, 256),
+                                      (1000, 128, 512), (200704 // 8, 128, 512)])
+def test_bn1_bwd_fused_matches_three_passes(M, Wd, Cin):
+    """bn1_bwd_fused (csrc/bnfuse.hip: BN1's apply, ReLU mask from c1 through the forward affine,
+    inside one kernel with dx = dc1·W1 + dy·bit3 and dW1 = dc1ᵀ·x) vs bn_bwd + fp32 products of
+    its dc1: dgamma/dbeta bit-identical, dx within bf16 rounding of the GEMM epilogue's
+    bf16(acc) + addend, dW1 within summation-order noise, accumulated into a given view."""
+    from layer_wise_aaai20_amd.ops._ext import h16, load
+    lib = load()
+    g = torch.Generator(device="cuda").manual_seed(M + Wd)
+    mk = lambda *s: torch.randn(*s, device="cuda", generator=g).to(h16())  # noqa: E731
+    da1, c1, x, dy = mk(M, Wd), mk(M, Wd), mk(M, Cin), mk(M, Cin)
+    w1 = (torch.randn(Wd, Cin, device="cuda", generator=g) / 16).to(h16())
+    bits = torch.randint(0, 256, (M * Cin // 8,), dtype=torch.uint8, device="cuda", generator=g)
+    gam = torch.rand(Wd, device="cuda", generator=g) + 0.5
+    mean = torch.randn(Wd, device="cuda", generator=g) * 0.1
+    inv = torch.rand(Wd, device="cuda", generator=g) + 0.5
+    ss = torch.cat([gam * inv, -mean * gam * inv + 0.1]).contiguous()
+    outs = [torch.randn(Wd, device="cuda", generator=g) for _ in range(2)]
+    ref = [o.clone() for o in outs]
+    dc1, _, _, _ = lib.bn_bwd(da1, c1, None, gam, mean, inv, ss, True, True, False, None, *ref)
+    dw = torch.full((Wd, Cin), 0.25, device="cuda")
+    dx, dwr, dg, db = lib.bn1_bwd_fused(da1, c1, ss, gam, mean, inv, w1.t().contiguous(), x, dy,
+                                        bits, dw, *outs)
+    assert torch.equal(dg, ref[0]) and torch.equal(db, ref[1])
+    assert dwr.data_ptr() == dw.data_ptr()
+    mask = ((bits.view(-1, 1) >> torch.arange(8, device="cuda")) & 1).view(M, Cin).bool()
+    ref_dx = (dc1.float() @ w1.float()).to(h16()).float() + torch.where(mask, dy.float(), 0.)
+    err = (dx.float() - ref_dx).abs().max().item()
+    assert err <= 1e-2 * ref_dx.abs().max().item(), err
+    ref_dw = dc1.float().t() @ x.float()
+    err = ((dw - 0.25) - ref_dw).abs().max().item()
+    assert err <= 1e-4 * ref_dw.abs().max().item() + 1e-3, err

@@ -95,10 +95,31 @@ template <int R, int BK, bool KC> struct Tile {
   static_assert(R * BK / 8 % GT == 0, "tile must split evenly over the workgroup");
 };
 
+// M/N-contiguous tiles read by the 16x16x32 transposing fragment read (load_frag, MF = 16) are
+// stored unpadded, R elements per row, with the 16-byte chunk c of row r at c ^ mn_swz<R>(r):
+// a 32-lane half reads rows {8n .. 8n+3} of two 8-row groups at chunks 2j, 2j+1, and with the
+// padded R + 8 layout those rows' 8-byte pieces overlapped in the 64 banks two by two (the weight
+// gradients spent 42 % extra LDS cycles on conflicts: profiles/r6/pmc_conv3/). The swizzles make
+// the 32 pieces land in 32 distinct bank pairs (R = 128: 256-byte rows, cdna_hip_programming.md
+// T10 image (b); R = 64 / 256: the 128- / 512-byte-row forms checked the same way), and the
+// register-staged chunk stores stay conflict-free (8 lanes, 8 consecutive chunks of one row).
+// The 32x32x16 reads (MF = 32) keep the padded layout.
+template <int R>
+__host__ __device__ constexpr int mn_swz(int r) {
+  return R == 128 ? (((r & 3) << 2) | ((r >> 2) & 3))
+       : R == 64 ? ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2))
+       : (((r & 3) << 1) | (r & 8));
+}
+template <int R, bool KC, int MF>
+__host__ __device__ constexpr bool mn_swizzled() {
+  return !KC && MF == 16 && (R == 64 || R == 128 || R == 256);
+}
+
 // element offset of chunk c of stored row r
 template <int R, int BK, bool KC, int MF = 16>
 __device__ __forceinline__ int tile_off(int r, int c) {
   using T = Tile<R, BK, KC>;
+  if constexpr (mn_swizzled<R, KC, MF>()) return r * R + (c ^ mn_swz<R>(r & 15)) * 8;
   return r * T::LD + (T::SWZ ? (c ^ swz_key<MF>(r)) : c) * 8;
 }
 
@@ -293,8 +314,16 @@ __device__ __forceinline__ h16x8 load_frag(const uint16_t* S, int i_base, int s)
   } else {
     const int g = l >> 4, t = l & 15, q = t >> 2, p4 = t & 3;
     typedef __attribute__((address_space(3))) i16x4 lds_v4;
-    const uint16_t* p0 = S + (32 * s + 8 * g + q) * T::LD + i_base + 4 * p4;
-    const uint16_t* p1 = p0 + 4 * T::LD;
+    const uint16_t* p0;
+    const uint16_t* p1;
+    if constexpr (mn_swizzled<R, KC, MF>()) {
+      const int r0 = 32 * s + 8 * g + q, col = i_base + 4 * p4;
+      p0 = S + tile_off<R, BK, KC, MF>(r0, col >> 3) + (col & 7);
+      p1 = S + tile_off<R, BK, KC, MF>(r0 + 4, col >> 3) + (col & 7);
+    } else {
+      p0 = S + (32 * s + 8 * g + q) * T::LD + i_base + 4 * p4;
+      p1 = p0 + 4 * T::LD;
+    }
     const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0));
     const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p1));
     typedef short i16x8 __attribute__((ext_vector_type(8)));
@@ -581,15 +610,14 @@ __device__ __forceinline__ void load_tile_gather_b(const ConvGeom& cv, const Col
 }
 
 // store of a B-gather tile (row-major chunk order, see ColGather)
-template <int R, int BK>
+template <int R, int BK, int MF = 16>
 __device__ __forceinline__ void store_tile_rows(uint16_t* __restrict__ S,
                                                 const uint4 (&r)[Tile<R, BK, false>::PER_T]) {
-  using T = Tile<R, BK, false>;
   using G = ColGather<R, BK>;
   const int rr = threadIdx.x / G::TPR, c0 = (threadIdx.x % G::TPR) * G::PT;
 #pragma unroll
   for (int h = 0; h < G::PT; ++h)
-    *reinterpret_cast<uint4*>(S + rr * T::LD + (c0 + h) * 8) = r[h];
+    *reinterpret_cast<uint4*>(S + tile_off<R, BK, false, MF>(rr, c0 + h)) = r[h];
 }
 
 // LDS-DMA ring depth: bytes in flight per CU, not K-steps, hide the L2/Infinity-Cache latency
@@ -773,7 +801,7 @@ __global__ __launch_bounds__(GT) void k_gemm(const GemmK p) {
   };
   auto stage = [&](uint16_t* dst, const Regs& r) {
     store_tile<BM, BK, AKC, PRO == PRO_A, MF>(dst, r.a, r.oka, r.coA);
-    if constexpr (GB) store_tile_rows<BN, BK>(dst + TA::ELEMS, r.b);
+    if constexpr (GB) store_tile_rows<BN, BK, MF>(dst + TA::ELEMS, r.b);
     else store_tile<BN, BK, BKC, PRO == PRO_B, MF>(dst + TA::ELEMS, r.b, r.okb, coB);
   };
   auto compute = [&](const uint16_t* As) {

@@ -199,7 +199,7 @@ class GradSyncEngine:
         #          backward (the reference's hook-driven DDP, sparsified_ddp.py:403-452);
         #   "auto" (default) = "0": the measured winner with the xGMI transfer priced in. The
         #          world-8 simulation with every collective paying its modelled wire time on 16
-        #          busy workgroups (profiles/r6/sim8_wire_r50.jsonl, train/simworld.py) exposed
+        #          busy workgroups (profiles/r6/sim8_wire_r50_overlap_modes.jsonl, train/simworld.py) exposed
         #          ResNet-50 layer-wise Top-K 0.1 % by 0.22 ms inline vs 0.74 ms ("1") and 0.87 ms
         #          ("comm"); entire-model QSGD-255 on the quantised reduce-scatter wire 0.48 /
         #          0.83 / 0.41 ms; AlexNet entire-model Top-K 0.07 ms in all three. The step is

@@ -1612,14 +1612,19 @@ std::tuple<Tensor, Tensor> conv3_tap(Tensor x, Tensor w, int64_t Co, bool want_s
 // With x2 (a downsample block: the shortcut BN's input, fed by the same dy and bitmap) the dual
 // reduce runs and the same pass also writes that BN's dx2 (as bn_bwd_dual's). Returns (da2, dW3,
 // dgamma, dbeta, dx2, dgamma2, dbeta2) (the last three empty without x2); dc3 is never written.
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused(
+// With bn2_x (c2 [M][Ci], BN2's input), bn2_ss (its forward scale | shift) and bn2_mean, the
+// kernel also reduces BN2's backward sums from the da2 tiles it writes; the 8th output holds
+// them as [slabs, 2, Ci] rows for bn_bwd(..., stats_rows=) (empty otherwise).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused(
     Tensor dy, Tensor x, Tensor bits, c10::optional<Tensor> weight, Tensor mean, Tensor invstd,
     Tensor w3t, Tensor a2, c10::optional<Tensor> dw_out, c10::optional<Tensor> dgamma_out,
     c10::optional<Tensor> dbeta_out, c10::optional<Tensor> x2, c10::optional<Tensor> weight2,
     c10::optional<Tensor> mean2, c10::optional<Tensor> invstd2,
-    c10::optional<Tensor> dgamma2_out, c10::optional<Tensor> dbeta2_out) {
+    c10::optional<Tensor> dgamma2_out, c10::optional<Tensor> dbeta2_out,
+    c10::optional<Tensor> bn2_x, c10::optional<Tensor> bn2_ss, c10::optional<Tensor> bn2_mean) {
   const c10::DeviceGuard guard(x.device());
   const bool dual = x2.has_value() && x2->defined();
+  const bool s2 = bn2_x.has_value() && bn2_x->defined();
   for (const Tensor* t : {&dy, &x, &w3t, &a2}) {
     check_dtype(*t, kH16, "bn3_bwd_fused operand");
     TORCH_CHECK(t->is_cuda() && t->dim() == 2 && t->is_contiguous(),
@@ -1706,12 +1711,25 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused
   const int nblk = lw::bn3_bwd_dgemm_slabs(M, (int)C, (int)Ci);
   // one workgroup adds its dW3 into the destination itself (no slab, no reduce to defer)
   Tensor slab = nblk > 1 ? at::empty({(int64_t)nblk * C * Ci}, f32) : o;
+  Tensor st2 = at::empty({s2 ? (int64_t)nblk : 0, 2, Ci}, f32);
+  if (s2) {
+    check_dtype(*bn2_x, kH16, "bn2_x");
+    TORCH_CHECK(bn2_x->is_cuda() && bn2_x->sizes() == a2.sizes() && bn2_x->is_contiguous(),
+                "bn2_x must be BN2's input [M][Ci], like a2");
+    check_aligned16(bn2_x->data_ptr(), "bn2_x");
+    TORCH_CHECK(bn2_ss.has_value() && bn2_ss->numel() == 2 * Ci && bn2_mean.has_value() &&
+                bn2_mean->numel() == Ci, "bn2_ss must hold 2*Ci and bn2_mean Ci floats");
+    check_dtype(*bn2_ss, at::kFloat, "bn2_ss");
+    check_dtype(*bn2_mean, at::kFloat, "bn2_mean");
+  }
   lw::bn3_bwd_dgemm(ptr<uint16_t>(dy), ptr<uint16_t>(x), ptr<uint8_t>(bits), a.A, a.B, a.Cc,
                     ptr<uint16_t>(w3t), ptr<uint16_t>(a2), ptr<uint16_t>(da2), ptr<float>(slab),
                     M, (int)C, (int)Ci, st, dual ? ptr<uint16_t>(*x2) : nullptr,
                     dual ? b.A : nullptr,
                     dual ? b.B : nullptr, dual ? b.Cc : nullptr,
-                    dual ? ptr<uint16_t>(dx2) : nullptr, nblk == 1);
+                    dual ? ptr<uint16_t>(dx2) : nullptr, nblk == 1,
+                    s2 ? ptr<uint16_t>(*bn2_x) : nullptr, s2 ? ptr<float>(*bn2_ss) : nullptr,
+                    s2 ? ptr<float>(*bn2_mean) : nullptr, s2 ? ptr<float>(st2) : nullptr);
   if (nblk > 1) {
     lw::GemmArgs g{};
     g.partial = ptr<float>(slab);
@@ -1725,7 +1743,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused
     if (lw::splitk_take_deferred()) splitk_keep().push_back(slab);
   }
   launched("bn3_bwd_fused");
-  return {da2, o, dgamma, dbeta, dx2, dg2, db2};
+  return {da2, o, dgamma, dbeta, dx2, dg2, db2, st2};
 }
 
 // A bottleneck's BN1 backward (no downsample; bf16, training, ReLU mask from c1 through the
@@ -2273,8 +2291,9 @@ LW_LIBRARY(LW_OPS_NS, m) {
   m.def("bn3_bwd_fused(Tensor dy, Tensor x, Tensor bits, Tensor? weight, Tensor mean, "
         "Tensor invstd, Tensor w3t, Tensor a2, Tensor(a!)? dw_out, Tensor(b!)? dgamma_out, "
         "Tensor(c!)? dbeta_out, Tensor? x2=None, Tensor? weight2=None, Tensor? mean2=None, "
-        "Tensor? invstd2=None, Tensor(d!)? dgamma2_out=None, Tensor(e!)? dbeta2_out=None) "
-        "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+        "Tensor? invstd2=None, Tensor(d!)? dgamma2_out=None, Tensor(e!)? dbeta2_out=None, "
+        "Tensor? bn2_x=None, Tensor? bn2_ss=None, Tensor? bn2_mean=None) "
+        "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("stem_bwd_fused(Tensor dp, Tensor idx, Tensor x, Tensor scale_shift, Tensor? weight, "
         "Tensor mean, Tensor invstd, int k, int s, int p, Tensor(a!)? dgamma_out, "
         "Tensor(b!)? dbeta_out, Tensor pooled, Tensor x4) -> (Tensor, Tensor, Tensor)");

@@ -423,10 +423,10 @@ __global__ __launch_bounds__(256) void k_bn_finalize_bwd(
     const float* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ invstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
     float* __restrict__ A, float* __restrict__ B, float* __restrict__ Cc, int training,
-    int accum) {
+    int accum, int rstride) {
   double s1, s2;
   int c;
-  if (!fold_partials(partial, nblocks, C, s1, s2, c)) return;
+  if (!fold_partials(partial, nblocks, C, s1, s2, c, rstride)) return;
   const double is = invstd[c];
   const double gm = gamma ? gamma[c] : 1.0;
   if (dbeta) dbeta[c] = accum ? dbeta[c] + (float)s1 : (float)s1;
@@ -665,15 +665,24 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
   reduce_geometry(a.M, a.C, rpb, nb);
   // relu mask: recompute from x when the forward had no residual (saves reading y)
   const int rmode = !a.relu ? 0 : (a.bits ? 3 : (a.scale ? 2 : 1));
+  const float* part = a.partial;
+  int rstride = 0;
   if (a.stat_rows) {
-    // the GEMM that produced dy already reduced (Σdy', Σdy'·(x−mean)) per M-tile
-    // (gemm_core.h EPI_BSTATS): only fold its rows
+    // the kernel that produced dy already reduced (Σdy', Σdy'·(x−mean)) per tile group
+    // (bnfuse.hip S2: BN2's sums from the fused BN3 kernel): only fold its rows — in place, as
+    // the forward finalize does, up to kColsumDirectMax rows
     const int64_t R = a.stats_rows_n;
-    nb = colsum_blocks(R);
-    const int64_t rows_pb = (R + nb - 1) / nb;
-    nb = (int)((R + rows_pb - 1) / rows_pb);
-    hipLaunchKernelGGL(k_colsum, dim3(nb), dim3(256), 0, st, a.stat_rows, R, 2 * a.C, rows_pb,
-                       a.partial);
+    if (R <= kColsumDirectMax) {
+      part = a.stat_rows;
+      rstride = 2 * a.C;
+      nb = (int)R;
+    } else {
+      nb = colsum_blocks(R);
+      const int64_t rows_pb = (R + nb - 1) / nb;
+      nb = (int)((R + rows_pb - 1) / rows_pb);
+      hipLaunchKernelGGL(k_colsum, dim3(nb), dim3(256), 0, st, a.stat_rows, R, 2 * a.C, rows_pb,
+                         a.partial);
+    }
   } else {
 #define LW_RED(R)                                                                                \
   hipLaunchKernelGGL((k_bn_reduce<T, 1, R, kReduceUnroll>),                                     \
@@ -684,9 +693,9 @@ static void bn_backward_t(const BNArgs& a, hipStream_t st) {
     else LW_RED(3);
 #undef LW_RED
   }
-  hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
+  hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, part, nb,
                      a.C, a.M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
-                     (int)a.training, (int)a.accum_dparams);
+                     (int)a.training, (int)a.accum_dparams, rstride);
   if (a.coeffs_only) return;
   const dim3 grid(apply_grid(n8, a.C, kApplyBwdGrid)), block(BNT);
 #define LW_BWD(R, D)                                                                            \
@@ -716,7 +725,7 @@ void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st) {
   for (const BNArgs* p : {&a, &b})
     hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((p->C + 3) / 4), dim3(256), 0, st, p->partial, nb,
                        p->C, p->M, p->gamma, p->mean, p->invstd, p->dgamma, p->dbeta, p->A, p->B,
-                       p->Cc, 1, (int)p->accum_dparams);
+                       p->Cc, 1, (int)p->accum_dparams, 0);
   if (a.coeffs_only) return;
   const int64_t n8 = a.M * a.C / 8;
   hipLaunchKernelGGL(k_bn_bwd_apply_dual, dim3(apply_grid(n8, a.C, kApplyBwdGrid)), dim3(BNT), 0, st, x, x2, dy,
@@ -1198,7 +1207,7 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
                        a.invstd, a.partial, g, rpb2);
     hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb2,
                        a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
-                       (int)a.accum_dparams);
+                       (int)a.accum_dparams, 0);
     if (a.coeffs_only) return;
   }
   if (a.k == 3 && a.s == 2 && a.p == 1 && a.H == 2 * a.Ho && a.W == 2 * a.Wo) {
@@ -1209,7 +1218,7 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
                          (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb2);
       hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial,
                          nb2, a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc,
-                         1, (int)a.accum_dparams);
+                         1, (int)a.accum_dparams, 0);
     }
     int64_t rpa;
     int nba;
@@ -1225,7 +1234,7 @@ void stem_pool_bwd(const StemArgs& a, hipStream_t st) {
                        (const float*)nullptr, (uint16_t*)nullptr, a.partial, g, rpb);
     hipLaunchKernelGGL(k_bn_finalize_bwd, dim3((a.C + 3) / 4), dim3(256), 0, st, a.partial, nb,
                        a.C, M, a.gamma, a.mean, a.invstd, a.dgamma, a.dbeta, a.A, a.B, a.Cc, 1,
-                       (int)a.accum_dparams);
+                       (int)a.accum_dparams, 0);
   }
   int64_t rpa;
   int nba;

@@ -72,6 +72,7 @@ template <int CO> struct BfGeom {
 template <int CO> struct BfRaw {
   uint4 d[BfGeom<CO>::NROW], x[BfGeom<CO>::NROW], x2[BfGeom<CO>::NROW], a[BfGeom<CO>::NA];
   uint32_t b[BfGeom<CO>::NROW];
+  uint2 c2[BfGeom<CO>::BM / 16];          // S2: c2 at this lane's 4 da2 channels, per pixel block
 };
 
 // DUAL: the downsample block, whose shortcut BN (input x2 = cd) received the same dy and ReLU
@@ -80,7 +81,12 @@ template <int CO> struct BfRaw {
 // loads is in flight while a tile computes (a second register set, two tiles in flight, measured
 // 435.8 vs 420.4 us at stage 1: profiles/r6/fused_bn3/).
 // acc_out: a single tile group adds its dW3 straight into `slab` (= the destination).
-template <int CO, bool DUAL>
+// S2: BN2's backward reduction rides on the da2 tile: with c2 (BN2's input), its forward affine
+// ss2 (scale | shift: the ReLU mask) and mean2, each workgroup adds (Σd, Σd·(c2 − mean2)) of
+// d = da2·[c2·s + h > 0] over its pixels — k_bn_reduce RELU 2's expression on the same bf16 da2
+// values — and writes them as row `grp` of st2 [groups][2][CI] (its part's 64 columns), which
+// the BN2 finalize folds in place: the separate reduce pass over da2 and c2 is gone.
+template <int CO, bool DUAL, bool S2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict__ c3,
                      const uint8_t* __restrict__ bits, const float* __restrict__ A,
@@ -89,7 +95,9 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
                      uint16_t* __restrict__ da2, float* __restrict__ slab,
                      const uint16_t* __restrict__ x2, const float* __restrict__ A2,
                      const float* __restrict__ B2, const float* __restrict__ C2,
-                     uint16_t* __restrict__ dx2, int64_t M, int CI, int tiles, int tpw,
+                     uint16_t* __restrict__ dx2, const uint16_t* __restrict__ c2,
+                     const float* __restrict__ ss2, const float* __restrict__ mean2,
+                     float* __restrict__ st2, int64_t M, int CI, int tiles, int tpw,
                      int acc_out, int xcd_pairs) {
   using G = BfGeom<CO>;
   constexpr int BM = G::BM, RB = CO * 2;              // dc3 / W3ᵀ row bytes
@@ -114,6 +122,18 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
   const __amdgpu_buffer_rsrc_t rdr = make_rsrc(dr, act_bytes), rc3 = make_rsrc(c3, act_bytes);
   const __amdgpu_buffer_rsrc_t rx2 = make_rsrc(DUAL ? x2 : c3, act_bytes);
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(a2, a2_bytes);
+  const __amdgpu_buffer_rsrc_t rc2 = make_rsrc(S2 ? c2 : a2, a2_bytes);
+  // S2: this lane's da2 channels ci2 .. ci2 + 3 (the staging layout below) and their BN2 terms
+  const int ci2 = c0 + 16 * w + 4 * g;
+  float fs2[4], fh2[4], mu2[4], st_a[4], st_b[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    fs2[r] = S2 ? ss2[ci2 + r] : 0.f;
+    fh2[r] = S2 ? ss2[CI + ci2 + r] : 0.f;
+    mu2[r] = S2 ? mean2[ci2 + r] : 0.f;
+    st_a[r] = 0.f;
+    st_b[r] = 0.f;
+  }
 
   // ---- this part's W3ᵀ rows into LDS (once)
 #pragma unroll
@@ -149,6 +169,13 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
       const int e = t + 256 * i;
       const int64_t m = m0 + (e >> 3);
       R.a[i] = bload16(ra, m < M ? (uint32_t)((m * CI + c0 + (e & 7) * 8) * 2) : OOB);
+    }
+    if (S2) {
+#pragma unroll
+      for (int j = 0; j < BM / 16; ++j) {
+        const int64_t m = m0 + 16 * j + (l & 15);
+        R.c2[j] = bload8(rc2, m < M ? (uint32_t)((m * CI + ci2) * 2) : OOB);
+      }
     }
   };
 
@@ -197,7 +224,7 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
   };
 
   // ---- phase B: both products from the LDS images, da2 staged and stored
-  auto phase_b = [&](int u) {
+  auto phase_b = [&](int u, const uint2 (&cx)[BM / 16]) {
     // da2 tile: D[ci 16w..][px] = W3ᵀ[ci][co] · dc3[px][co]ᵀ, K = CO channels
     f32x4 acc1[BM / 16];
 #pragma unroll
@@ -252,6 +279,16 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
       uint16_t h[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[r] = f2h(acc1[j][r]);
+      if (S2 && (int64_t)u * BM + px < M) {
+        const uint32_t xw[2] = {cx[j].x, cx[j].y};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xv = (r & 1) ? hhi(xw[r >> 1]) : hlo(xw[r >> 1]);
+          const float d = fmaf(xv, fs2[r], fh2[r]) > 0.f ? h2f(h[r]) : 0.f;
+          st_a[r] += d;
+          st_b[r] += d * (xv - mu2[r]);
+        }
+      }
       *reinterpret_cast<uint2*>(sO + px * 128 + ((ch ^ s128(px & 15)) << 4) + 8 * (g & 1)) =
           make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
     }
@@ -270,9 +307,27 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
   if (u0 < u1) load_tile(u0, R0);
   for (int u = u0; u < u1; ++u) {
     phase_a(u, R0);
+    uint2 cx[BM / 16];
+#pragma unroll
+    for (int j = 0; j < BM / 16; ++j) cx[j] = R0.c2[j];
     __syncthreads();
     if (u + 1 < u1) load_tile(u + 1, R0);      // in flight under this tile's MFMAs
-    phase_b(u);
+    phase_b(u, cx);
+  }
+  if (S2) {
+    // the 16 lanes of one k group hold the same 4 channels: fixed butterfly, lane 16g writes
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        st_a[r] += __shfl_xor(st_a[r], o, 64);
+        st_b[r] += __shfl_xor(st_b[r], o, 64);
+      }
+    if ((l & 15) == 0) {
+      float* row = st2 + (int64_t)grp * 2 * CI;
+      *reinterpret_cast<float4*>(row + ci2) = make_float4(st_a[0], st_a[1], st_a[2], st_a[3]);
+      *reinterpret_cast<float4*>(row + CI + ci2) = make_float4(st_b[0], st_b[1], st_b[2], st_b[3]);
+    }
   }
   // ---- this group's dW3 slab (the part's columns): lane holds
   // D[co = (NCB·w + i)·16 + 4g + r][ci = c0 + 16j + (l & 15)]
@@ -312,17 +367,21 @@ void bn3_bwd_dgemm(const uint16_t* dr, const uint16_t* c3, const uint8_t* bits, 
                    const float* B, const float* Cc, const uint16_t* w3t, const uint16_t* a2,
                    uint16_t* da2, float* slab, int64_t M, int C, int Ci, hipStream_t st,
                    const uint16_t* x2, const float* A2, const float* B2, const float* C2,
-                   uint16_t* dx2, bool acc_out) {
+                   uint16_t* dx2, bool acc_out, const uint16_t* c2, const float* ss2,
+                   const float* mean2, float* st2) {
   const int tiles = bf_tiles(M, C), nparts = Ci / BF_CIP;
   const int groups = bn3_bwd_dgemm_slabs(M, C, Ci);
   const int tpw = (tiles + groups - 1) / groups;
   const int acc = (acc_out && groups == 1) ? 1 : 0;
   const int blocks = groups * nparts, xp = groups % 8 == 0 ? 1 : 0;
-#define LW_BF(CO, DU)                                                                            \
-  hipLaunchKernelGGL((k_bn3_bwd_dgemm<CO, DU>), dim3(blocks), dim3(256), 0, st, dr, c3, bits, A, \
-                     B, Cc, w3t, a2, da2, slab, x2, A2, B2, C2, dx2, M, Ci, tiles, tpw, acc, xp)
-  if (C == 256) { if (x2) LW_BF(256, true); else LW_BF(256, false); }
-  else { if (x2) LW_BF(512, true); else LW_BF(512, false); }
+#define LW_BF(CO, DU, S)                                                                         \
+  hipLaunchKernelGGL((k_bn3_bwd_dgemm<CO, DU, S>), dim3(blocks), dim3(256), 0, st, dr, c3, bits, \
+                     A, B, Cc, w3t, a2, da2, slab, x2, A2, B2, C2, dx2, c2, ss2, mean2, st2, M,  \
+                     Ci, tiles, tpw, acc, xp)
+#define LW_BF2(CO, DU) if (st2) LW_BF(CO, DU, true); else LW_BF(CO, DU, false)
+  if (C == 256) { if (x2) { LW_BF2(256, true); } else { LW_BF2(256, false); } }
+  else { if (x2) { LW_BF2(512, true); } else { LW_BF2(512, false); } }
+#undef LW_BF2
 #undef LW_BF
 }
 

@@ -386,6 +386,7 @@ class _BottleneckFn(torch.autograd.Function):
         # the bitmap — the dx GEMM as a masked addend, the shortcut BN through its ReLU mode)
         grads = {}
         dual = None
+        st2 = None
         fused = FUSE_BNBWD and (cout, width) in ((256, 64), (512, 128)) and dr.dtype == h16()
         if fused:
             # BN3's apply fused into both consumers of dc3 (csrc/bnfuse.hip): da2 = dc3·W3 and
@@ -398,9 +399,19 @@ class _BottleneckFn(torch.autograd.Function):
                 cd, gd, meand, invd = saved[22], saved[24], saved[25], saved[26]
                 od = _bn_grad_outs(gdp, bdp)
                 down = (cd, gd, meand, invd, od[0], od[1])
+            if not has_down:
+                down = (None,) * 6
+            # stage 1: BN2's backward sums come out of the same kernel, from the da2 tiles it
+            # writes: the bandwidth-bound kernel reads c2 (+29 us a block in the step) and BN2's
+            # reduce pass over da2 and c2 (45 us) is gone: 20.769 -> 20.704 ms of kernels a
+            # step. At stage 2 they cost the kernel more than the pass they replace (292.9 vs
+            # 271.2 us in isolation). profiles/r6/bn2_sums/
+            s2 = (c2, ss2, mean2) if cout == 256 else (None,) * 3
             with _deferred_reduce(dr, d3):
-                da2, _, dg3, db3, dcd, dgd, dbd = lib.bn3_bwd_fused(
-                    dr, c3, bits3, g3, mean3, inv3, w3t, a2, dst3, o3[0], o3[1], *down)
+                da2, _, dg3, db3, dcd, dgd, dbd, st2 = lib.bn3_bwd_fused(
+                    dr, c3, bits3, g3, mean3, inv3, w3t, a2, dst3, o3[0], o3[1], *down, *s2)
+                if s2[0] is None:
+                    st2 = None
             if has_down:
                 dual = (dcd, dgd, dbd, od)
             grads["g3"], grads["b3"] = _finish_bn(g3p, b3p, dg3, db3, o3)
@@ -427,7 +438,7 @@ class _BottleneckFn(torch.autograd.Function):
             da2, _ = gemm_dgrad(dc3, cout, W3, M2, width, cout)
         o2 = _bn_grad_outs(g2p, b2p)
         dc2, dg2, db2, _ = lib.bn_bwd(da2, c2, None, g2, mean2, inv2, ss2, True, True, False,
-                                      None, o2[0], o2[1])
+                                      None, o2[0], o2[1], st2)
         grads["g2"], grads["b2"] = _finish_bn(g2p, b2p, dg2, db2, o2)
         # conv2 (3x3) backward on the implicit GEMM: the weight gradient reads a1 and accumulates
         # fp32 straight into the arena

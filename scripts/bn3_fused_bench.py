@@ -43,6 +43,17 @@ def main():
         def fused():
             lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, dw, dgo, dbo)
 
+        c2 = torch.randn(M, Ci, device="cuda").to(h16())
+        ss2 = torch.cat([torch.rand(Ci, device="cuda") + 0.5, torch.randn(Ci, device="cuda")])
+        mean2 = torch.randn(Ci, device="cuda") * .1
+
+        def fused_s2():
+            lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, dw, dgo, dbo, *(None,) * 6,
+                              c2, ss2, mean2)
+
+        def bn2_reduce():
+            lib.bn_bwd(a2, c2, None, mean2, mean2, mean2, ss2, True, True, False, None)
+
         def three():
             dc3, _, _, _ = lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits,
                                       dgo, dbo)
@@ -53,8 +64,10 @@ def main():
         def reduce_only():
             lib.bn_bwd(dy, x, None, gam, mean, inv, None, True, True, False, bits, dgo, dbo)
         tf, t3, tr = timeit(fused), timeit(three), timeit(reduce_only)
+        ts2, tb2 = timeit(fused_s2), timeit(bn2_reduce)
         print(f"M {M} C {C} Ci {Ci}: fused {tf:.1f} us   three-pass {t3:.1f} us   "
-              f"(bn_bwd alone {tr:.1f} us)", flush=True)
+              f"(bn_bwd alone {tr:.1f} us); with BN2's sums {ts2:.1f} us vs BN2's whole "
+              f"backward {tb2:.1f} us", flush=True)
         del dy, x, a2, bits
 
 

@@ -226,7 +226,9 @@ def test_bn3_bwd_fused_matches_three_passes(M, C, Ci, dual):
     bit-identical (the same reduce + finalize), the shortcut BN's dx2 (dual) within one bf16 ulp,
     da2 within bf16 rounding, dW3 within fp32 summation-order noise, the weight gradient
     accumulated into a given view. M = 3000 / 1000 end in a partial tile; 4096 / 1000 run one
-    tile group (the result added straight into the destination)."""
+    tile group (the result added straight into the destination). BN2's backward sums, reduced
+    by the same kernel from its da2 tiles (rows per tile group), match an fp64 reduction of the
+    returned da2, and BN2's backward fed those rows matches the one running its own reduce."""
     from layer_wise_aaai20_amd.ops._ext import h16, load
     lib = load()
     g = torch.Generator(device="cuda").manual_seed(M + C + dual)
@@ -249,8 +251,28 @@ def test_bn3_bwd_fused_matches_three_passes(M, C, Ci, dual):
                                   ref[0], ref[1])
     dw = torch.full((C, Ci), 0.25, device="cuda")
     down = (x2, gam2, mean2, inv2, outs[2], outs[3]) if dual else ()
-    da2, dwr, dg, db, dx2, dg2, db2 = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, dw,
-                                                        outs[0], outs[1], *down)
+    c2 = mk(M, Ci)
+    ss2 = torch.cat([torch.rand(Ci, device="cuda", generator=g) + 0.5,
+                     torch.randn(Ci, device="cuda", generator=g) * 0.3])
+    mean2b = torch.randn(Ci, device="cuda", generator=g) * 0.1
+    down = down if dual else (None,) * 6
+    da2, dwr, dg, db, dx2, dg2, db2, st2 = lib.bn3_bwd_fused(
+        dy, x, bits, gam, mean, inv, w3t, a2, dw, outs[0], outs[1], *down, c2, ss2, mean2b)
+    # BN2's sums from the kernel vs fp64 over the da2 it wrote
+    d = da2.double() * ((c2.float() * ss2[:Ci] + ss2[Ci:]) > 0).double()
+    want = torch.stack([d.sum(0), (d * (c2.double() - mean2b.double())).sum(0)])
+    got = st2.double().sum(0)
+    tol = 1e-4 * d.abs().sum(0).max().item() + 1e-4
+    assert (got - want).abs().max().item() <= tol, ((got - want).abs().max().item(), tol)
+    inv2b = torch.rand(Ci, device="cuda", generator=g) + 0.5
+    gam2b = torch.rand(Ci, device="cuda", generator=g) + 0.5
+    r_dc2, _, r_dg2, r_db2 = lib.bn_bwd(da2, c2, None, gam2b, mean2b, inv2b, ss2, True, True,
+                                        False, None)
+    f_dc2, _, f_dg2, f_db2 = lib.bn_bwd(da2, c2, None, gam2b, mean2b, inv2b, ss2, True, True,
+                                        False, None, None, None, st2)
+    torch.testing.assert_close(f_db2, r_db2, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(f_dg2, r_dg2, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(f_dc2.float(), r_dc2.float(), rtol=2e-2, atol=2e-2)
     assert torch.equal(dg, ref[0]) and torch.equal(db, ref[1])
     if dual:
         assert torch.equal(dg2, ref[2]) and torch.equal(db2, ref[3])
@@ -266,7 +288,7 @@ def test_bn3_bwd_fused_matches_three_passes(M, C, Ci, dual):
     err = ((dw - 0.25) - ref_dw).abs().max().item()
     assert err <= 1e-4 * ref_dw.abs().max().item() + 1e-3, err
     # without a destination: a fresh [C, Ci] result
-    _, dw2, _, _, _, _, _ = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, None, None,
+    _, dw2, _, _, _, _, _, _ = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, a2, None, None,
                                               None, *((x2, gam2, mean2, inv2) if dual else ()))
     torch.testing.assert_close(dw2, dw - 0.25, rtol=1e-5, atol=1e-4)
 

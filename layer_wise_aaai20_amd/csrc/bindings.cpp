@@ -1614,14 +1614,16 @@ std::tuple<Tensor, Tensor> conv3_tap(Tensor x, Tensor w, int64_t Co, bool want_s
 // dgamma, dbeta, dx2, dgamma2, dbeta2) (the last three empty without x2); dc3 is never written.
 // With bn2_x (c2 [M][Ci], BN2's input), bn2_ss (its forward scale | shift) and bn2_mean, the
 // kernel also reduces BN2's backward sums from the da2 tiles it writes; the 8th output holds
-// them as [slabs, 2, Ci] rows for bn_bwd(..., stats_rows=) (empty otherwise).
+// them as [slabs, 2, Ci] rows for bn_bwd(..., stats_rows=) (empty otherwise). With
+// a2_from_bn2, `a2` is c2 (BN2's input) and the kernel forms a2 = relu(bn2(c2)) from bn2_ss itself.
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn3_bwd_fused(
     Tensor dy, Tensor x, Tensor bits, c10::optional<Tensor> weight, Tensor mean, Tensor invstd,
     Tensor w3t, Tensor a2, c10::optional<Tensor> dw_out, c10::optional<Tensor> dgamma_out,
     c10::optional<Tensor> dbeta_out, c10::optional<Tensor> x2, c10::optional<Tensor> weight2,
     c10::optional<Tensor> mean2, c10::optional<Tensor> invstd2,
     c10::optional<Tensor> dgamma2_out, c10::optional<Tensor> dbeta2_out,
-    c10::optional<Tensor> bn2_x, c10::optional<Tensor> bn2_ss, c10::optional<Tensor> bn2_mean) {
+    c10::optional<Tensor> bn2_x, c10::optional<Tensor> bn2_ss, c10::optional<Tensor> bn2_mean,
+    bool a2_from_bn2) {
   const c10::DeviceGuard guard(x.device());
   const bool dual = x2.has_value() && x2->defined();
   const bool s2 = bn2_x.has_value() && bn2_x->defined();
@@ -1712,12 +1714,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn3_b
   // one workgroup adds its dW3 into the destination itself (no slab, no reduce to defer)
   Tensor slab = nblk > 1 ? at::empty({(int64_t)nblk * C * Ci}, f32) : o;
   Tensor st2 = at::empty({s2 ? (int64_t)nblk : 0, 2, Ci}, f32);
+  if (a2_from_bn2) {
+    TORCH_CHECK(bn2_ss.has_value() && bn2_ss->defined() && bn2_ss->numel() == 2 * Ci,
+                "a2_from_bn2 needs bn2_ss (2*Ci floats)");
+    check_dtype(*bn2_ss, at::kFloat, "bn2_ss");
+  }
   if (s2) {
     check_dtype(*bn2_x, kH16, "bn2_x");
     TORCH_CHECK(bn2_x->is_cuda() && bn2_x->sizes() == a2.sizes() && bn2_x->is_contiguous(),
                 "bn2_x must be BN2's input [M][Ci], like a2");
     check_aligned16(bn2_x->data_ptr(), "bn2_x");
-    TORCH_CHECK(bn2_ss.has_value() && bn2_ss->numel() == 2 * Ci && bn2_mean.has_value() &&
+    TORCH_CHECK(bn2_ss.has_value() && bn2_ss->defined() && bn2_ss->numel() == 2 * Ci &&
+                bn2_mean.has_value() && bn2_mean->defined() &&
                 bn2_mean->numel() == Ci, "bn2_ss must hold 2*Ci and bn2_mean Ci floats");
     check_dtype(*bn2_ss, at::kFloat, "bn2_ss");
     check_dtype(*bn2_mean, at::kFloat, "bn2_mean");
@@ -1728,8 +1736,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> bn3_b
                     dual ? b.A : nullptr,
                     dual ? b.B : nullptr, dual ? b.Cc : nullptr,
                     dual ? ptr<uint16_t>(dx2) : nullptr, nblk == 1,
-                    s2 ? ptr<uint16_t>(*bn2_x) : nullptr, s2 ? ptr<float>(*bn2_ss) : nullptr,
-                    s2 ? ptr<float>(*bn2_mean) : nullptr, s2 ? ptr<float>(st2) : nullptr);
+                    s2 ? ptr<uint16_t>(*bn2_x) : nullptr,
+                    (s2 || a2_from_bn2) ? ptr<float>(*bn2_ss) : nullptr,
+                    s2 ? ptr<float>(*bn2_mean) : nullptr, s2 ? ptr<float>(st2) : nullptr,
+                    a2_from_bn2);
   if (nblk > 1) {
     lw::GemmArgs g{};
     g.partial = ptr<float>(slab);
@@ -2292,8 +2302,8 @@ LW_LIBRARY(LW_OPS_NS, m) {
         "Tensor invstd, Tensor w3t, Tensor a2, Tensor(a!)? dw_out, Tensor(b!)? dgamma_out, "
         "Tensor(c!)? dbeta_out, Tensor? x2=None, Tensor? weight2=None, Tensor? mean2=None, "
         "Tensor? invstd2=None, Tensor(d!)? dgamma2_out=None, Tensor(e!)? dbeta2_out=None, "
-        "Tensor? bn2_x=None, Tensor? bn2_ss=None, Tensor? bn2_mean=None) "
-        "-> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
+        "Tensor? bn2_x=None, Tensor? bn2_ss=None, Tensor? bn2_mean=None, "
+        "bool a2_from_bn2=False) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)");
   m.def("stem_bwd_fused(Tensor dp, Tensor idx, Tensor x, Tensor scale_shift, Tensor? weight, "
         "Tensor mean, Tensor invstd, int k, int s, int p, Tensor(a!)? dgamma_out, "
         "Tensor(b!)? dbeta_out, Tensor pooled, Tensor x4) -> (Tensor, Tensor, Tensor)");

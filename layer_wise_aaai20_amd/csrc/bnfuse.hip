@@ -86,7 +86,10 @@ template <int CO> struct BfRaw {
 // d = da2·[c2·s + h > 0] over its pixels — k_bn_reduce RELU 2's expression on the same bf16 da2
 // values — and writes them as row `grp` of st2 [groups][2][CI] (its part's 64 columns), which
 // the BN2 finalize folds in place: the separate reduce pass over da2 and c2 is gone.
-template <int CO, bool DUAL, bool S2>
+// A2C: `a2` is c2 itself and the kernel forms a2 = relu(c2·s + h) (bf16, k_bn_apply's expression)
+// as it stages the tile — the forward then never materialises a2 (its GEMM applies BN2 in the
+// prologue), and the tile's c2 bytes are the ones S2 reads.
+template <int CO, bool DUAL, bool S2, bool A2C>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict__ c3,
                      const uint8_t* __restrict__ bits, const float* __restrict__ A,
@@ -123,6 +126,8 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
   const __amdgpu_buffer_rsrc_t rx2 = make_rsrc(DUAL ? x2 : c3, act_bytes);
   const __amdgpu_buffer_rsrc_t ra = make_rsrc(a2, a2_bytes);
   const __amdgpu_buffer_rsrc_t rc2 = make_rsrc(S2 ? c2 : a2, a2_bytes);
+  Coef8 co2;                                           // A2C: BN2 of this thread's a2 chunk column
+  if (A2C) load_coef8(co2, ss2, ss2 + CI, c0 + (t & 7) * 8, CI);
   // S2: this lane's da2 channels ci2 .. ci2 + 3 (the staging layout below) and their BN2 terms
   const int ci2 = c0 + 16 * w + 4 * g;
   float fs2[4], fh2[4], mu2[4], st_a[4], st_b[4];
@@ -219,7 +224,10 @@ void k_bn3_bwd_dgemm(const uint16_t* __restrict__ dr, const uint16_t* __restrict
 #pragma unroll
     for (int i = 0; i < G::NA; ++i) {
       const int e = t + 256 * i, row = e >> 3, ch = e & 7;
-      *reinterpret_cast<uint4*>(sA + row * 128 + ((ch ^ s128(row & 15)) << 4)) = R.a[i];
+      uint4 v = R.a[i];
+      // (rows past M stay zero: their dc3 rows are C, not zero)
+      if (A2C) v = m0 + row < M ? affine_relu8(v, co2) : make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(sA + row * 128 + ((ch ^ s128(row & 15)) << 4)) = v;
     }
   };
 
@@ -368,17 +376,19 @@ void bn3_bwd_dgemm(const uint16_t* dr, const uint16_t* c3, const uint8_t* bits, 
                    uint16_t* da2, float* slab, int64_t M, int C, int Ci, hipStream_t st,
                    const uint16_t* x2, const float* A2, const float* B2, const float* C2,
                    uint16_t* dx2, bool acc_out, const uint16_t* c2, const float* ss2,
-                   const float* mean2, float* st2) {
+                   const float* mean2, float* st2, bool a2c) {
   const int tiles = bf_tiles(M, C), nparts = Ci / BF_CIP;
   const int groups = bn3_bwd_dgemm_slabs(M, C, Ci);
   const int tpw = (tiles + groups - 1) / groups;
   const int acc = (acc_out && groups == 1) ? 1 : 0;
   const int blocks = groups * nparts, xp = groups % 8 == 0 ? 1 : 0;
-#define LW_BF(CO, DU, S)                                                                         \
-  hipLaunchKernelGGL((k_bn3_bwd_dgemm<CO, DU, S>), dim3(blocks), dim3(256), 0, st, dr, c3, bits, \
-                     A, B, Cc, w3t, a2, da2, slab, x2, A2, B2, C2, dx2, c2, ss2, mean2, st2, M,  \
-                     Ci, tiles, tpw, acc, xp)
-#define LW_BF2(CO, DU) if (st2) LW_BF(CO, DU, true); else LW_BF(CO, DU, false)
+#define LW_BF(CO, DU, S, AC)                                                                     \
+  hipLaunchKernelGGL((k_bn3_bwd_dgemm<CO, DU, S, AC>), dim3(blocks), dim3(256), 0, st, dr, c3,  \
+                     bits, A, B, Cc, w3t, a2, da2, slab, x2, A2, B2, C2, dx2, c2, ss2, mean2,   \
+                     st2, M, Ci, tiles, tpw, acc, xp)
+#define LW_BF2(CO, DU)                                                                           \
+  if (st2) { if (a2c) LW_BF(CO, DU, true, true); else LW_BF(CO, DU, true, false); }               \
+  else { if (a2c) LW_BF(CO, DU, false, true); else LW_BF(CO, DU, false, false); }
   if (C == 256) { if (x2) { LW_BF2(256, true); } else { LW_BF2(256, false); } }
   else { if (x2) { LW_BF2(512, true); } else { LW_BF2(512, false); } }
 #undef LW_BF2

@@ -208,6 +208,7 @@ void bn_backward_dual(const BNArgs& a, const BNArgs& b, hipStream_t st);
 // With x2 (the downsample block: its shortcut BN's input, same dy and bitmap) also
 // dx2 = A2·(dy·bit) + B2·x2 + C2 into dx2 [M][C]. With st2: BN2's backward sums
 // (Σd, Σd·(c2 − mean2)), d = da2·[c2·ss2 + ss2[Ci..] > 0], one row per slab: st2 [slabs][2][Ci].
+// a2c: `a2` is c2 and the kernel forms relu(c2·ss2 + ss2[Ci..]) itself (ss2 required).
 // BN1 backward apply fused with dW1 += dc1ᵀ·x and dx = dc1·W1 + dy·bit3 (bnfuse.hip), for a
 // bottleneck without downsample: (Wd, Cin) = (64, 256) or (128, 512); the ReLU mask from c1 via
 // the forward affine (fs, fh); w1t = W1ᵀ [Cin][Wd]; slab [bn1_bwd_dgemm_slabs][Wd][Cin]
@@ -225,7 +226,7 @@ void bn3_bwd_dgemm(const uint16_t* dr, const uint16_t* c3, const uint8_t* bits, 
                    const uint16_t* x2 = nullptr, const float* A2 = nullptr,
                    const float* B2 = nullptr, const float* C2 = nullptr, uint16_t* dx2 = nullptr,
                    bool acc_out = false, const uint16_t* c2 = nullptr, const float* ss2 = nullptr,
-                   const float* mean2 = nullptr, float* st2 = nullptr);
+                   const float* mean2 = nullptr, float* st2 = nullptr, bool a2c = false);
 
 // fused stem: BN-apply + ReLU + max-pool (bn.hip), bf16 NHWC
 struct StemArgs {

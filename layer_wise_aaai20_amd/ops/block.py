@@ -57,8 +57,10 @@ from .tuning import MF32, Tuner, with_mf32
 
 CL = torch.channels_last
 # Design decisions measured in earlier rounds and fixed in round 6 (their switches removed):
-# * relu(bn1(c1)) / relu(bn2(c2)) are materialised by one apply pass each, not re-normalised in the
-#   consumers' staging prologues (a 3x3 conv redoes the affine for each of its 9 taps: 1.6x slower);
+# * relu(bn1(c1)) is materialised by one apply pass, not re-normalised in the 3x3 conv's staging
+#   (it would redo the affine for each of its 9 taps: 1.6x slower); relu(bn2(c2)) likewise at
+#   stages 3-4, while at stages 1-2 conv3 applies BN2 in its GEMM prologue and the fused BN3
+#   backward re-forms a2 from c2, so a2 is never written;
 # * the BN backward reductions run as their own pass: folding them into the epilogue of the GEMM
 #   producing dy saved 1.6 ms of BN kernels but cost 2.4 ms of GEMM (profiles/r2_bstats_ab.log;
 #   -3.3 % each part, profiles/r3s2/bstats_cross_ab.txt);
@@ -334,9 +336,20 @@ class _BottleneckFn(torch.autograd.Function):
         M2 = c2.shape[0]
         mean2, inv2, ss2 = lib.bn_stats(c2, st2, g2, b2, bn2.running_mean, bn2.running_var,
                                         _bn_momentum(bn2), bn2.eps)
-        # conv3 (1x1) on a2 = relu(bn2(c2)), BN3 statistics in the epilogue
-        a2 = lib.bn_apply(c2, ss2, None, None, True)
-        c3, st3 = gemm(a2, width, True, W3, width, True, M2, cout, width, stats=True)
+        # conv3 (1x1) on a2 = relu(bn2(c2)), BN3 statistics in the epilogue. Where BN3's backward
+        # runs fused (stages 1-2) a2 is never materialised: the GEMM applies BN2 + ReLU as it
+        # stages c2 (the apply kernel's expression, bit for bit) and the fused backward re-forms
+        # a2 from c2 the same way (12,387-12,396 -> 12,456-12,469 img/s alternating on one box,
+        # profiles/r6/a2free/)
+        fuse3 = FUSE_BNBWD and (cout, width) in ((256, 64), (512, 128)) and c2.dtype == h16()
+        if fuse3:
+            a2 = c2
+            c3, st3 = gemm(c2, width, True, W3, width, True, M2, cout, width, stats=True,
+                           pro=(ss2[:width], ss2[width:]))
+        else:
+            a2 = lib.bn_apply(c2, ss2, None, None, True)
+            c3, st3 = gemm(a2, width, True, W3, width, True, M2, cout, width, stats=True)
+        ctx.fuse3 = fuse3
         mean3, inv3, ss3 = lib.bn_stats(c3, st3, g3, b3, bn3.running_mean, bn3.running_var,
                                         _bn_momentum(bn3), bn3.eps)
         if bnd is not None:
@@ -387,7 +400,7 @@ class _BottleneckFn(torch.autograd.Function):
         grads = {}
         dual = None
         st2 = None
-        fused = FUSE_BNBWD and (cout, width) in ((256, 64), (512, 128)) and dr.dtype == h16()
+        fused = ctx.fuse3             # (decided by the forward: a2 is c2 then)
         if fused:
             # BN3's apply fused into both consumers of dc3 (csrc/bnfuse.hip): da2 = dc3·W3 and
             # dW3 = dc3ᵀ·a2 from one pass over dy, c3 and the bitmap; dc3 is never written (a
@@ -406,10 +419,11 @@ class _BottleneckFn(torch.autograd.Function):
             # reduce pass over da2 and c2 (45 us) is gone: 20.769 -> 20.704 ms of kernels a
             # step. At stage 2 they cost the kernel more than the pass they replace (292.9 vs
             # 271.2 us in isolation). profiles/r6/bn2_sums/
-            s2 = (c2, ss2, mean2) if cout == 256 else (None,) * 3
+            s2 = (c2, ss2, mean2) if cout == 256 else (None, ss2, None)
             with _deferred_reduce(dr, d3):
                 da2, _, dg3, db3, dcd, dgd, dbd, st2 = lib.bn3_bwd_fused(
-                    dr, c3, bits3, g3, mean3, inv3, w3t, a2, dst3, o3[0], o3[1], *down, *s2)
+                    dr, c3, bits3, g3, mean3, inv3, w3t, c2, dst3, o3[0], o3[1], *down, *s2,
+                    True)
                 if s2[0] is None:
                     st2 = None
             if has_down:

@@ -108,8 +108,9 @@ def test_block_direct_arena_gradients():
                                                          (256, 128, 2, True)])
 def test_fused_bn3_backward_matches_three_pass_block(inplanes, planes, stride, down, monkeypatch):
     """Stage-1/2 bottlenecks (with and without downsample) with BN3's — and, without downsample,
-    BN1's — backward fused into their two GEMMs (csrc/bnfuse.hip) give the three-pass block's
-    input and parameter gradients to bf16 / summation-order noise."""
+    BN1's — backward fused into their two GEMMs (csrc/bnfuse.hip), and a2 = relu(bn2(c2)) never
+    materialised, give the three-pass block's output, input and parameter gradients to bf16 /
+    summation-order noise."""
     torch.manual_seed(3)
     ref = _make(inplanes, planes, stride, down).cuda().to(memory_format=CL)
     x = torch.randn(8, inplanes, 28, 28, device="cuda").to(torch.bfloat16)
@@ -121,7 +122,9 @@ def test_fused_bn3_backward_matches_three_pass_block(inplanes, planes, stride, d
         monkeypatch.setattr(blk, "FUSE_BNBWD", fuse)
         m, y, gx = _run(copy.deepcopy(ref), x.float(), gy, True)
         outs[fuse] = (y.float(), gx.float(), [p.grad.float() for p in m.parameters()])
-    assert torch.equal(outs[True][0], outs[False][0])
+    # the fused path's forward never materialises a2 (conv3 applies BN2 in its GEMM prologue,
+    # possibly on another tile than the plain GEMM): the outputs agree to rounding
+    assert _rel(outs[True][0], outs[False][0]) < 1e-2
     assert _rel(outs[True][1], outs[False][1]) < 2e-2
     for a, b in zip(outs[True][2], outs[False][2]):
         assert _rel(a, b) < 2e-2

@@ -228,7 +228,9 @@ def test_bn3_bwd_fused_matches_three_passes(M, C, Ci, dual):
     accumulated into a given view. M = 3000 / 1000 end in a partial tile; 4096 / 1000 run one
     tile group (the result added straight into the destination). BN2's backward sums, reduced
     by the same kernel from its da2 tiles (rows per tile group), match an fp64 reduction of the
-    returned da2, and BN2's backward fed those rows matches the one running its own reduce."""
+    returned da2, and BN2's backward fed those rows matches the one running its own reduce.
+    With a2_from_bn2 (a2 formed in the kernel from c2, as the a2-free forward needs) every output
+    is bit-identical to the run given the materialised a2 = relu(bn2(c2))."""
     from layer_wise_aaai20_amd.ops._ext import h16, load
     lib = load()
     g = torch.Generator(device="cuda").manual_seed(M + C + dual)
@@ -255,9 +257,19 @@ def test_bn3_bwd_fused_matches_three_passes(M, C, Ci, dual):
     ss2 = torch.cat([torch.rand(Ci, device="cuda", generator=g) + 0.5,
                      torch.randn(Ci, device="cuda", generator=g) * 0.3])
     mean2b = torch.randn(Ci, device="cuda", generator=g) * 0.1
+    a2 = lib.bn_apply(c2, ss2, None, None, True)
+    # a2 formed inside the kernel from c2: the same bits as from the materialised a2
+    outs_c = [o.clone() for o in outs]
+    dw_c = torch.full((C, Ci), 0.25, device="cuda")
+    down_c = (x2, gam2, mean2, inv2, outs_c[2], outs_c[3]) if dual else (None,) * 6
+    res_c = lib.bn3_bwd_fused(dy, x, bits, gam, mean, inv, w3t, c2, dw_c, outs_c[0], outs_c[1],
+                              *down_c, c2, ss2, mean2b, True)
     down = down if dual else (None,) * 6
     da2, dwr, dg, db, dx2, dg2, db2, st2 = lib.bn3_bwd_fused(
         dy, x, bits, gam, mean, inv, w3t, a2, dw, outs[0], outs[1], *down, c2, ss2, mean2b)
+    assert torch.equal(dw_c, dw) and torch.equal(res_c[0], da2) and torch.equal(res_c[7], st2)
+    if dual:
+        assert torch.equal(res_c[4], dx2)
     # BN2's sums from the kernel vs fp64 over the da2 it wrote
     d = da2.double() * ((c2.float() * ss2[:Ci] + ss2[Ci:]) > 0).double()
     want = torch.stack([d.sum(0), (d * (c2.double() - mean2b.double())).sum(0)])

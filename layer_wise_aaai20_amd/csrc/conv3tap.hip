@@ -39,6 +39,13 @@ constexpr int T3_NWS = 3;                 // weight slices in the ring
 constexpr int T3_PLANE = T3_PATCH / 4;    // bytes per 8-channel plane of a patch buffer
 constexpr int T3_PBLK = T3_PLANE / 1024;  // 64-pixel DMA blocks per plane
 
+// LW_T3_ZSEL: a tap's out-of-image fragment lanes read a zeroed 16-byte LDS slot instead of being
+// zeroed after the read — one address select per fragment instead of four register selects (the
+// tap kernels issue 6-10 VALU per MFMA: profiles/r6/pmc_conv3/)
+#ifndef LW_T3_ZSEL
+#define LW_T3_ZSEL 1
+#endif
+
 template <int N>
 __device__ __forceinline__ void t3_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
@@ -67,7 +74,9 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
   constexpr int LDH = BN + 8;                      // bf16 staging row (epilogue)
   static_assert(T3_M * LDH * 2 <= LDS, "epilogue staging fits the ring");
   static_assert(NT * 16 * 4 <= LDS, "statistics fold fits");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS + 16];   // + the zero slot
+  if (LW_T3_ZSEL && threadIdx.x == 0)              // visible after the prologue's barrier
+    *reinterpret_cast<uint4*>(lds + LDS) = make_uint4(0u, 0u, 0u, 0u);
 
   // patch pixel q <-> flat input pixel (g0 - 1) * W - 1 + q: rows g0-1 .. g0+R plus one pixel on
   // each side, no halo columns (a tap column outside the image is masked like a tap row)
@@ -160,11 +169,17 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
       int pb = ppix[i];
       asm volatile("" : "+v"(pb));
       const int p = pb + toff;
-      fa[i] = *reinterpret_cast<const h16x8*>(P + pplane + p * 16);
       if (r != 1 || s != 1) {
         const uint32_t need = (r == 0 ? 1u : r == 2 ? 2u : 0u) | (s == 0 ? 4u : s == 2 ? 8u : 0u);
         const bool ok = ((vmask >> (4 * i)) & need) == need;
-        if (!ok) fa[i] = h16x8{};
+        if (LW_T3_ZSEL) {
+          fa[i] = *reinterpret_cast<const h16x8*>(ok ? P + pplane + p * 16 : lds + LDS);
+        } else {
+          fa[i] = *reinterpret_cast<const h16x8*>(P + pplane + p * 16);
+          if (!ok) fa[i] = h16x8{};
+        }
+      } else {
+        fa[i] = *reinterpret_cast<const h16x8*>(P + pplane + p * 16);
       }
     }
     __builtin_amdgcn_s_setprio(1);

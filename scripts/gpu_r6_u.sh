@@ -1,0 +1,13 @@
+# round 6, call u: tap-conv fragment masking by a zero-slot address select (LW_T3_ZSEL) — conv
+# tests, tap microbench and bench, A/B against a -DLW_T3_ZSEL=0 build (LWAAAI_SO) on one box
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r6u
+timeout -k 10 400 python -u -m pytest tests/test_conv_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r6u/t_conv.txt 2>&1
+timeout -k 10 300 python -u scripts/conv_tap_bench.py > gpurun_out/r6u/tap_zsel1.txt 2>&1
+LWAAAI_SO=layer_wise_aaai20_amd/_exp_zsel0.so timeout -k 10 300 python -u scripts/conv_tap_bench.py > gpurun_out/r6u/tap_zsel0.txt 2>&1
+for i in 1 2; do
+timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 >> gpurun_out/r6u/bench_zsel1.jsonl 2>> gpurun_out/r6u/bench.err
+LWAAAI_SO=layer_wise_aaai20_amd/_exp_zsel0.so timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 >> gpurun_out/r6u/bench_zsel0.jsonl 2>> gpurun_out/r6u/bench.err
+done

@@ -41,9 +41,12 @@ constexpr int T3_PBLK = T3_PLANE / 1024;  // 64-pixel DMA blocks per plane
 
 // LW_T3_ZSEL: a tap's out-of-image fragment lanes read a zeroed 16-byte LDS slot instead of being
 // zeroed after the read — one address select per fragment instead of four register selects (the
-// tap kernels issue 6-10 VALU per MFMA: profiles/r6/pmc_conv3/)
+// tap kernels issue 6-10 VALU per MFMA: profiles/r6/pmc_conv3/). 2: also each fragment address
+// is one add of the lane's hoisted byte base and the step's wave-uniform offset (kept opaque in
+// an SGPR so the 63 (block, tap) addresses are not hoisted into registers), instead of a copy of
+// the pixel index, a shift and an add.
 #ifndef LW_T3_ZSEL
-#define LW_T3_ZSEL 1
+#define LW_T3_ZSEL 2
 #endif
 
 template <int N>
@@ -147,6 +150,9 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
     vmask |= (ox + 1 < W ? 1u : 0u) << (4 * i + 3);
   }
   const int pplane = g * T3_PLANE;                 // this lane's k group: its patch plane
+  uint32_t pbyte[7];                               // ZSEL 2: byte of patch pixel ppix[i], plane g
+#pragma unroll
+  for (int i = 0; i < 7; ++i) pbyte[i] = (uint32_t)(pplane + ppix[i] * 16);
   int wbyte[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) wbyte[j] = (g * BN + wn * 32 + j * 16 + (l & 15)) * 16;
@@ -162,6 +168,21 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
 #pragma unroll
     for (int j = 0; j < 2; ++j) fb[j] = *reinterpret_cast<const h16x8*>(Wt + wbyte[j]);
     const int toff = r * W + s;
+    if constexpr (LW_T3_ZSEL >= 2) {
+      uint32_t uo = (uint32_t)(P - lds) + (uint32_t)(toff * 16);
+      asm volatile("" : "+s"(uo));
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const uint32_t a = pbyte[i] + uo;
+        if (r != 1 || s != 1) {
+          const uint32_t need = (r == 0 ? 1u : r == 2 ? 2u : 0u) | (s == 0 ? 4u : s == 2 ? 8u : 0u);
+          const bool ok = ((vmask >> (4 * i)) & need) == need;
+          fa[i] = *reinterpret_cast<const h16x8*>(lds + (ok ? a : (uint32_t)LDS));
+        } else {
+          fa[i] = *reinterpret_cast<const h16x8*>(lds + a);
+        }
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
       // opaque base: keeps the 63 (block, tap) addresses from being hoisted out of the K loop
@@ -181,6 +202,7 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
       } else {
         fa[i] = *reinterpret_cast<const h16x8*>(P + pplane + p * 16);
       }
+    }
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll

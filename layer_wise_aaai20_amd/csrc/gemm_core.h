@@ -532,6 +532,9 @@ __device__ __forceinline__ void load_tile_gather_a(const ConvGeom& cv, const Con
   }
 }
 
+#ifndef LW_BGATHER_IL
+#define LW_BGATHER_IL 1     // interleaved B-gather chunks (store_tile_rows); 0: runs of PER_T
+#endif
 // ---- B-gather (weight gradient): N-contiguous tile whose rows are output pixels and whose
 // chunks are (tap, 8 channels) — or C4: (tap pair, 4 channels) — of the input. Here a thread
 // stages PER_T chunks of ONE row (row-major chunk order instead of chunk_pos), so the pixel
@@ -563,7 +566,8 @@ __device__ __forceinline__ void col_gather_init(ColGather<R, BK>& g, const uint1
   g.nok = 0;
 #pragma unroll
   for (int h = 0; h < G::PT; ++h) {
-    const int nn = n0 + ((threadIdx.x % G::TPR) * G::PT + h) * 8;
+    const int nn = n0 + (LW_BGATHER_IL ? h * G::TPR + (int)(threadIdx.x % G::TPR)
+                                       : (int)(threadIdx.x % G::TPR) * G::PT + h) * 8;
     int t, ci;
     if (C4) { t = nn >> 2; ci = 0; }
     else { t = nn / cv.C; ci = nn - t * cv.C; }
@@ -609,15 +613,21 @@ __device__ __forceinline__ void load_tile_gather_b(const ConvGeom& cv, const Col
   }
 }
 
-// store of a B-gather tile (row-major chunk order, see ColGather)
+// store of a B-gather tile (row-major chunk order, see ColGather). A row's TPR threads take its
+// chunks interleaved (chunk h·TPR + t % TPR, not a run of PT per thread): with a run, the 8 lanes
+// of a ds_write_b128 group stored chunks PT apart, i.e. into the same 16-byte bank slots (2- to
+// 4-way conflicts); interleaved, they store 4-8 consecutive chunks of a row, and the tile's row
+// swizzle puts the next row's chunks in the other slots.
 template <int R, int BK, int MF = 16>
 __device__ __forceinline__ void store_tile_rows(uint16_t* __restrict__ S,
                                                 const uint4 (&r)[Tile<R, BK, false>::PER_T]) {
   using G = ColGather<R, BK>;
-  const int rr = threadIdx.x / G::TPR, c0 = (threadIdx.x % G::TPR) * G::PT;
+  const int rr = threadIdx.x / G::TPR, c0 = threadIdx.x % G::TPR;
 #pragma unroll
-  for (int h = 0; h < G::PT; ++h)
-    *reinterpret_cast<uint4*>(S + tile_off<R, BK, false, MF>(rr, c0 + h)) = r[h];
+  for (int h = 0; h < G::PT; ++h) {
+    const int c = LW_BGATHER_IL ? h * G::TPR + c0 : c0 * G::PT + h;
+    *reinterpret_cast<uint4*>(S + tile_off<R, BK, false, MF>(rr, c)) = r[h];
+  }
 }
 
 // LDS-DMA ring depth: bytes in flight per CU, not K-steps, hide the L2/Infinity-Cache latency

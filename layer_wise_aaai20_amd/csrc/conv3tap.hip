@@ -48,6 +48,9 @@ constexpr int T3_PBLK = T3_PLANE / 1024;  // 64-pixel DMA blocks per plane
 #ifndef LW_T3_ZSEL
 #define LW_T3_ZSEL 2
 #endif
+#ifndef LW_T3_PEN
+#define LW_T3_PEN 1      // BN = 64: masked taps by max() with per-lane penalties (see below)
+#endif
 
 template <int N>
 __device__ __forceinline__ void t3_wait_barrier() {
@@ -153,6 +156,18 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
   uint32_t pbyte[7];                               // ZSEL 2: byte of patch pixel ppix[i], plane g
 #pragma unroll
   for (int i = 0; i < 7; ++i) pbyte[i] = (uint32_t)(pplane + ppix[i] * 16);
+  // BN = 64 (registers to spare at two waves per SIMD): a masked tap's address is
+  // max(address, row penalty, column penalty) — one v_max3 — where a penalty is the zero slot's
+  // address (above every patch address) for an out-of-image tap row / column, else 0
+  constexpr bool PEN = LW_T3_ZSEL >= 2 && LW_T3_PEN && BN == 64;
+  uint32_t rpen[2][PEN ? 7 : 1], cpen[2][PEN ? 7 : 1];
+#pragma unroll
+  for (int i = 0; i < (PEN ? 7 : 1); ++i) {
+    rpen[0][i] = ((vmask >> (4 * i)) & 1u) ? 0u : (uint32_t)LDS;
+    rpen[1][i] = ((vmask >> (4 * i)) & 2u) ? 0u : (uint32_t)LDS;
+    cpen[0][i] = ((vmask >> (4 * i)) & 4u) ? 0u : (uint32_t)LDS;
+    cpen[1][i] = ((vmask >> (4 * i)) & 8u) ? 0u : (uint32_t)LDS;
+  }
   int wbyte[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) wbyte[j] = (g * BN + wn * 32 + j * 16 + (l & 15)) * 16;
@@ -174,7 +189,10 @@ void k_conv3_tap(const uint16_t* __restrict__ x,
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         const uint32_t a = pbyte[i] + uo;
-        if (r != 1 || s != 1) {
+        if (PEN && (r != 1 || s != 1)) {
+          const uint32_t rp = r == 1 ? 0u : rpen[r >> 1][i], cp = s == 1 ? 0u : cpen[s >> 1][i];
+          fa[i] = *reinterpret_cast<const h16x8*>(lds + max(max(a, rp), cp));
+        } else if (r != 1 || s != 1) {
           const uint32_t need = (r == 0 ? 1u : r == 2 ? 2u : 0u) | (s == 0 ? 4u : s == 2 ? 8u : 0u);
           const bool ok = ((vmask >> (4 * i)) & need) == need;
           fa[i] = *reinterpret_cast<const h16x8*>(lds + (ok ? a : (uint32_t)LDS));
